@@ -1,0 +1,388 @@
+/*
+ * kss.h — C ABI of the MI355X-native Filter/Score evaluator (libkss.so).
+ *
+ * This is the drop-in boundary for the scheduling-cycle hot path of
+ * kube-scheduler-simulator (reference snapshot 2025-01-31, upstream scheduler
+ * k8s.io/kubernetes v1.26.2 pinned at simulator/go.mod:56).  It replaces, for
+ * one pending pod or for a sequential batch of pods:
+ *
+ *   findNodesThatFitPod -> findNodesThatPassFilters  (HOT LOOP 1)
+ *   prioritizeNodes -> RunPreScore/RunScore/Normalize (HOT LOOPS 2-4)
+ *   selectHost                                         (mirror: scheduler/scheduler.go:323-344)
+ *   Cache.AssumePod -> NodeInfo.AddPod                 (the commit the next pod sees)
+ *
+ * and the per-call result recording the simulator performs through
+ *   wrappedPlugin.Filter/Score/NormalizeScore  simulator/scheduler/plugin/wrappedplugin.go:388-548
+ *   resultstore.Store.Add* / GetStoredResult   simulator/scheduler/plugin/resultstore/store.go:133-626
+ *
+ * Conventions:
+ *  - plain C, no exceptions cross the boundary; return 0 on success, <0 on error;
+ *  - the library owns device buffers; callers own every host pointer passed in,
+ *    and no caller pointer is retained after a call returns;
+ *  - strings are interned by the caller (the Go plugin in a real integration,
+ *    kss/compile.py here); only dense integer ids cross, except the optional
+ *    name tables used to format annotations;
+ *  - nodes are given in the scheduler's canonical order (nodeTree.list() zone
+ *    round-robin); node index == canonical index.
+ *
+ * The same structs are consumed by the CPU oracle (oracle/kss_oracle.c), which is
+ * test infrastructure only.
+ */
+#ifndef KSS_H_
+#define KSS_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define KSS_ABI_VERSION 1
+
+/* ---- error codes ------------------------------------------------------- */
+#define KSS_OK 0
+#define KSS_E_INVAL (-22)        /* malformed input / shape mismatch           */
+#define KSS_E_NOMEM (-12)        /* host or device allocation failed          */
+#define KSS_E_DEVICE (-5)        /* HIP runtime error (maps to framework.Error) */
+#define KSS_E_UNSUPPORTED (-95)  /* input outside what the device path supports */
+#define KSS_E_RANGE (-34)        /* value outside the exact-arithmetic envelope */
+#define KSS_E_NOTFOUND (-2)
+
+/* ---- resources ----------------------------------------------------------
+ * Resource vector layout (framework.Resource, ⟨k8s⟩ framework/types.go):
+ * MilliCPU, Memory, EphemeralStorage, then up to 4 scalar (extended) resources. */
+#define KSS_RES_CPU 0
+#define KSS_RES_MEMORY 1
+#define KSS_RES_EPHEMERAL 2
+#define KSS_RES_SCALAR0 3
+#define KSS_NRES 7
+#define KSS_MAX_SCALAR 4
+
+/* ---- filter plugins, in default MultiPoint order -------------------------
+ * (simulator/scheduler/config/plugin_test.go:15-36).  A node's verdict is the
+ * 1-based index of the FIRST failing filter (RunFilterPlugins stops at the first
+ * non-success status), 0 when every filter passed. */
+enum kss_filter_plugin {
+  KSS_F_PASS = 0,
+  KSS_F_NODE_UNSCHEDULABLE = 1,
+  KSS_F_NODE_NAME = 2,
+  KSS_F_TAINT_TOLERATION = 3,
+  KSS_F_NODE_AFFINITY = 4,
+  KSS_F_NODE_PORTS = 5,
+  KSS_F_NODE_RESOURCES_FIT = 6,
+  KSS_F_VOLUME_RESTRICTIONS = 7,
+  KSS_F_EBS_LIMITS = 8,
+  KSS_F_GCEPD_LIMITS = 9,
+  KSS_F_NODE_VOLUME_LIMITS = 10,
+  KSS_F_AZURE_DISK_LIMITS = 11,
+  KSS_F_VOLUME_BINDING = 12,
+  KSS_F_VOLUME_ZONE = 13,
+  KSS_F_POD_TOPOLOGY_SPREAD = 14,
+  KSS_F_INTER_POD_AFFINITY = 15,
+  KSS_NFILTER = 15,
+  KSS_F_NOT_EVALUATED = 255 /* node excluded by a PreFilterResult / PreFilter failure */
+};
+
+/* fail_detail meaning per failing plugin */
+#define KSS_FIT_TOO_MANY_PODS (1u << 0)
+#define KSS_FIT_CPU (1u << 1)
+#define KSS_FIT_MEMORY (1u << 2)
+#define KSS_FIT_EPHEMERAL (1u << 3)
+#define KSS_FIT_SCALAR0 (1u << 4) /* bit (4+s) for scalar s */
+/* TaintToleration: detail = taint-dictionary id of the first untolerated taint */
+#define KSS_PTS_CONSTRAINTS_NOT_MATCH 0
+#define KSS_PTS_MISSING_LABEL 1
+#define KSS_IPA_AFFINITY 0
+#define KSS_IPA_ANTI_AFFINITY 1
+#define KSS_IPA_EXISTING_ANTI_AFFINITY 2
+
+/* ---- score plugins, in default MultiPoint order ------------------------- */
+enum kss_score_plugin {
+  KSS_S_TAINT_TOLERATION = 0,
+  KSS_S_NODE_AFFINITY = 1,
+  KSS_S_NODE_RESOURCES_FIT = 2,
+  KSS_S_VOLUME_BINDING = 3,
+  KSS_S_POD_TOPOLOGY_SPREAD = 4,
+  KSS_S_INTER_POD_AFFINITY = 5,
+  KSS_S_BALANCED_ALLOCATION = 6,
+  KSS_S_IMAGE_LOCALITY = 7,
+  KSS_NSCORE = 8
+};
+
+/* ---- node flags --------------------------------------------------------- */
+#define KSS_NODE_UNSCHEDULABLE (1u << 0) /* node.Spec.Unschedulable */
+#define KSS_NODE_HAS_LABELS (1u << 1)    /* len(node.Labels) > 0 (IPA processExistingPod) */
+
+/* ---- label-key flags ---------------------------------------------------- */
+#define KSS_KEY_UNIQUE (1u << 0)   /* no two nodes share a value: domain == node */
+#define KSS_KEY_HOSTNAME (1u << 1) /* key == "kubernetes.io/hostname" (PTS scoring special case) */
+
+/* Maximum taint dictionary size (uint64 masks) and hard taints per node kept in order. */
+#define KSS_MAX_TAINTS 64
+#define KSS_TAINT_ORDER 8
+/* Maximum domain cardinality of a NON-unique topology key on the device path. */
+#define KSS_MAX_BINS 1024
+
+/*
+ * Cluster snapshot, struct-of-arrays, canonical node order.  All arrays are
+ * caller-owned host memory; kss_load_cluster copies them to HBM.
+ * Matrices are column-blocked [attribute][node] so that a wavefront reads 64
+ * consecutive nodes of one attribute (coalesced).
+ */
+typedef struct kss_cluster {
+  int32_t n_nodes;
+  int32_t n_scalar;       /* scalar resource columns in use (0..KSS_MAX_SCALAR) */
+  int32_t n_label_keys;   /* referenced label keys (columns of label_value)      */
+  int32_t n_label_values; /* size of the value tables                            */
+  int32_t n_classes;      /* existing-pod classes (namespace + labels)           */
+  int32_t n_terms;        /* existing-pod affinity term types                    */
+  int32_t n_taints;       /* taint dictionary size (<= KSS_MAX_TAINTS)            */
+  int32_t node_base;      /* global index of row 0 (node-axis sharding); 0 otherwise */
+
+  const int64_t* alloc;        /* [KSS_NRES][n_nodes] Allocatable            */
+  const int64_t* requested;    /* [KSS_NRES][n_nodes] Requested              */
+  const int64_t* nonzero;      /* [2][n_nodes] NonZeroRequested cpu, memory  */
+  const int32_t* allowed_pods; /* [n_nodes] Allocatable.AllowedPodNumber     */
+  const int32_t* pod_count;    /* [n_nodes] len(NodeInfo.Pods)               */
+  const uint32_t* node_flags;  /* [n_nodes] KSS_NODE_*                       */
+  const uint64_t* taint_hard;  /* [n_nodes] dict bits of NoSchedule/NoExecute taints */
+  const uint64_t* taint_soft;  /* [n_nodes] dict bits of PreferNoSchedule taints     */
+  const uint8_t* taint_order;  /* [n_nodes][KSS_TAINT_ORDER] hard-taint dict ids in node.Spec.Taints order, 0xFF pad */
+  const int32_t* label_value;  /* [n_label_keys][n_nodes] key-local value id, -1 = label absent */
+  const int32_t* key_base;     /* [n_label_keys] offset of the key's values in the value tables */
+  const int32_t* key_card;     /* [n_label_keys] number of distinct values of the key */
+  const uint32_t* key_flags;   /* [n_label_keys] KSS_KEY_* */
+  const int32_t* key_empty;    /* [n_label_keys] local id of the "" value, or key_card (virtual "missing" domain) */
+  const int64_t* value_int;    /* [n_label_values] strconv.ParseInt(value,10,64) */
+  const uint8_t* value_is_int; /* [n_label_values] 1 if ParseInt succeeded */
+  const int32_t* class_count;  /* [n_classes][n_nodes] #pods of class c on node n */
+  const int32_t* term_count;   /* [n_terms][n_nodes]   #occurrences of term type t among pods on node n */
+} kss_cluster;
+
+/* ---- pod programs --------------------------------------------------------
+ * The host compiles each pod (v1.Pod) once into a fixed record plus entries in
+ * shared pools.  All label matching is reduced to predicates over value ids. */
+
+/* label requirement ops (labels.Requirement.Matches / NodeSelectorRequirement) */
+enum kss_req_op {
+  KSS_OP_FALSE = 0,  /* never matches (e.g. parse error)                      */
+  KSS_OP_TRUE = 1,
+  KSS_OP_MASK = 2,   /* low-cardinality key: match iff bit(value id) of mask; bit 63 = absent matches */
+  KSS_OP_IN = 3,     /* value id in list (absent -> false)                    */
+  KSS_OP_NOTIN = 4,  /* value id not in list (absent -> true)                 */
+  KSS_OP_EXISTS = 5,
+  KSS_OP_DNE = 6,
+  KSS_OP_GT = 7,     /* ParseInt(value) >  ival (absent or non-int -> false)  */
+  KSS_OP_LT = 8,     /* ParseInt(value) <  ival                               */
+  KSS_OP_NAME_IN = 9,    /* matchFields metadata.name In  [value]: node index == ival */
+  KSS_OP_NAME_NOTIN = 10 /* matchFields metadata.name NotIn [value]             */
+};
+
+typedef struct kss_req {
+  int32_t key;      /* label key column (unused for NAME ops / TRUE / FALSE) */
+  int32_t op;       /* enum kss_req_op */
+  int32_t list_off; /* IN/NOTIN: offset into kss_podset.ints */
+  int32_t list_len;
+  uint64_t mask;    /* OP_MASK */
+  int64_t ival;     /* GT/LT threshold; NAME ops: global node index (-1 = no such node) */
+} kss_req;
+
+/* a node-selector term: AND of requirements [req_off, req_off+req_len) */
+typedef struct kss_term {
+  int32_t req_off;
+  int32_t req_len;
+  int32_t weight; /* preferred terms: weight; required terms: unused */
+  int32_t flags;  /* reserved */
+} kss_term;
+
+/* topology spread constraint (after filterTopologySpreadConstraints/buildDefaultConstraints) */
+#define KSS_SPREAD_POLICY_AFFINITY_HONOR (1u << 0) /* NodeAffinityPolicy == Honor (default) */
+#define KSS_SPREAD_POLICY_TAINTS_HONOR (1u << 1)   /* NodeTaintsPolicy   == Honor (default Ignore) */
+typedef struct kss_spread {
+  int32_t key;        /* topology key column */
+  int32_t max_skew;
+  int32_t self_match; /* selector matches the incoming pod's own labels (filter) */
+  int32_t flags;      /* KSS_SPREAD_* */
+  int32_t cls_off;    /* classes (in the pod's namespace) matching the selector: ints[cls_off..] */
+  int32_t cls_len;
+  int32_t min_domains; /* 1 unless MinDomainsInPodTopologySpread (off in v1.26) */
+  int32_t pad;
+} kss_spread;
+
+/* inter-pod affinity program entries */
+enum kss_ipa_kind {
+  KSS_IPA_EXISTING_ANTI = 0, /* existing pods' required anti-affinity terms matching the incoming pod (rows: term types) */
+  KSS_IPA_REQ_AFFINITY = 1,  /* one per incoming required affinity term; rows: classes matching ALL terms */
+  KSS_IPA_REQ_ANTI = 2,      /* one per incoming required anti-affinity term; rows: classes matching it */
+  KSS_IPA_SCORE_CLASS = 3,   /* incoming preferred (anti-)affinity term: coef = +/-weight; rows: classes */
+  KSS_IPA_SCORE_TERM = 4     /* existing pods' terms matched by the incoming pod: coef; rows: term types */
+};
+typedef struct kss_ipa {
+  int32_t kind;
+  int32_t key;     /* topology key column */
+  int32_t row_off; /* ints[row_off .. row_off+row_len) */
+  int32_t row_len;
+  int32_t coef;    /* score entries: weight*multiplier */
+  int32_t pad;
+} kss_ipa;
+
+/* pod flags */
+#define KSS_POD_TOL_UNSCHEDULABLE (1u << 0)  /* tolerates node.kubernetes.io/unschedulable:NoSchedule */
+#define KSS_POD_HAS_REQ_AFFINITY (1u << 1)   /* RequiredDuringScheduling node affinity present */
+#define KSS_POD_PTS_REQUIRE_ALL (1u << 2)    /* PTS scoring requireAllTopologies */
+#define KSS_POD_IPA_SELF_MATCH (1u << 3)     /* podMatchesAllAffinityTerms(required, pod) */
+#define KSS_POD_IPA_HAS_PREFERRED (1u << 4)  /* incoming pod has preferred (anti-)affinity terms */
+#define KSS_POD_PTS_SCORE_STATE (1u << 5)    /* PTS preScoreState written (always, unless error) */
+
+typedef struct kss_pod {
+  int64_t fit_request[KSS_NRES];   /* Fit PreFilter computePodResourceRequest                 */
+  int64_t score_req_nz[KSS_NRES];  /* LeastAllocated: calculatePodResourceRequest(nonZero)    */
+  int64_t score_req[KSS_NRES];     /* BalancedAllocation: calculatePodResourceRequest(useRequested) */
+  int64_t commit_req[KSS_NRES];    /* NodeInfo.AddPod Requested delta (calculateResource)     */
+  int64_t commit_nz[2];            /* NodeInfo.AddPod NonZeroRequested delta                  */
+  uint64_t tol_hard;               /* dict bits of NoSchedule/NoExecute taints tolerated      */
+  uint64_t tol_soft;               /* dict bits of PreferNoSchedule taints tolerated by
+                                      tolerations with effect "" or PreferNoSchedule          */
+  int32_t node_name;               /* spec.nodeName: -1 unset, -2 names no node, else global index */
+  uint32_t flags;                  /* KSS_POD_* */
+  int32_t sel_off, sel_len;        /* nodeSelector requirements (AND), pool reqs          */
+  int32_t aff_off, aff_len;        /* required NodeSelectorTerms (OR), pool terms         */
+  int32_t pref_off, pref_len;      /* PreferredSchedulingTerms, pool terms                */
+  int32_t spread_off;              /* pool spreads: n_hard DoNotSchedule then n_soft ScheduleAnyway */
+  int32_t n_hard, n_soft;
+  int32_t ipa_off, ipa_len;        /* pool ipa entries */
+  int32_t cls;                     /* the pod's own class (class_count row it joins on commit), -1 none */
+  int32_t own_terms_off, own_terms_len; /* term-type rows this pod adds on commit: ints[] */
+  int32_t prefilter_status;        /* 0 ok, 1 NodeAffinity "pod affinity terms conflict",
+                                      2 pod-level Error (parse error)                      */
+  int32_t names_off, names_len;    /* NodeAffinity PreFilterResult node set (ints[], global idx); len<0: all nodes */
+  int32_t pad[2];
+} kss_pod;
+
+typedef struct kss_podset {
+  int32_t n_pods;
+  int32_t n_reqs, n_terms, n_spreads, n_ipa, n_ints;
+  const kss_pod* pods;
+  const kss_req* reqs;
+  const kss_term* terms;
+  const kss_spread* spreads;
+  const kss_ipa* ipa;
+  const int32_t* ints;
+} kss_podset;
+
+/* ---- profile (KubeSchedulerConfiguration profile subset) --------------- */
+#define KSS_FIT_LEAST_ALLOCATED 0
+#define KSS_FIT_MOST_ALLOCATED 1
+typedef struct kss_profile {
+  int32_t weight[KSS_NSCORE]; /* score plugin weights as getScorePluginWeight builds them (0 -> 1) */
+  uint32_t filter_enabled;    /* bit i = filter plugin i enabled (bit 0 unused) */
+  uint32_t score_enabled;     /* bit s = score plugin s enabled */
+  int32_t fit_strategy;       /* KSS_FIT_* (NodeResourcesFitArgs.ScoringStrategy.Type) */
+  int32_t fit_n;              /* scoring resources */
+  int32_t fit_res[4];
+  int64_t fit_weight[4];
+  int32_t ba_n;               /* NodeResourcesBalancedAllocationArgs.Resources */
+  int32_t ba_res[4];
+  int32_t hard_pod_affinity_weight; /* InterPodAffinityArgs.HardPodAffinityWeight */
+  int32_t pct_nodes_to_score;       /* must be 100 */
+  int32_t system_defaulted;         /* PodTopologySpreadArgs.DefaultingType == System */
+  int32_t pad;
+} kss_profile;
+
+/* the default v1.26 profile as the simulator builds it (plugins_test.go:184-209,878-1096) */
+void kss_default_profile(kss_profile* out);
+
+/* ---- per-pod results ------------------------------------------------------
+ * Caller-allocated host arrays of length n_nodes (any may be NULL to skip). */
+typedef struct kss_pod_result {
+  uint8_t* fail_plugin;  /* [n] enum kss_filter_plugin                          */
+  uint16_t* fail_detail; /* [n]                                                 */
+  int64_t* raw;          /* [KSS_NSCORE][n] Score() results (feasible nodes)    */
+  int64_t* norm;         /* [KSS_NSCORE][n] after NormalizeScore (pre-weight)   */
+  int64_t* total;        /* [n] Σ weight·norm                                   */
+  int32_t n_feasible;
+  int32_t chosen;        /* global node index, -1 if unschedulable */
+  int64_t best_total;
+  int32_t scored;        /* 1 if prioritizeNodes ran (>= 2 feasible nodes) */
+  int32_t status;        /* 0 ok; 1 unschedulable (no feasible); 2 prefilter unschedulable; 3 error */
+} kss_pod_result;
+
+/* ---- context -------------------------------------------------------------- */
+typedef struct kss_ctx kss_ctx;
+
+typedef struct kss_config {
+  int32_t device;          /* HIP device ordinal */
+  int32_t max_pods_record; /* capacity of the on-device per-pod result record (0 = no recording) */
+  int32_t class_capacity;  /* rows reserved in class_count (>= n_classes; commits may add rows) */
+  int32_t term_capacity;   /* rows reserved in term_count */
+} kss_config;
+
+int kss_abi_version(void);
+const char* kss_last_error(void); /* thread-local message of the last failing call */
+
+kss_ctx* kss_create(const kss_config* cfg, const kss_profile* prof);
+void kss_destroy(kss_ctx* ctx);
+
+/* upload a snapshot (replaces any previous one) */
+int kss_load_cluster(kss_ctx* ctx, const kss_cluster* cl);
+/* NodeInfo-generation delta sync: overwrite rows idx[0..n) of the mutable columns */
+int kss_apply_node_delta(kss_ctx* ctx, const int32_t* idx, int32_t n, const int64_t* requested /*[n][KSS_NRES]*/,
+                         const int64_t* nonzero /*[n][2]*/, const int32_t* pod_count /*[n]*/);
+/* read back the mutable columns (requested [KSS_NRES][N], nonzero [2][N], pod_count [N]) */
+int kss_read_node_state(kss_ctx* ctx, int64_t* requested, int64_t* nonzero, int32_t* pod_count,
+                        int32_t* class_count /*[n_classes][N] or NULL*/, int32_t* term_count /*or NULL*/);
+
+/* evaluate one pod against the current snapshot (no commit): the PreFilter-time call */
+int kss_eval_pod(kss_ctx* ctx, const kss_podset* ps, int32_t pod_index, kss_pod_result* out);
+/* commit pod ps.pods[pod_index] to node (AssumePod); rollback undoes it (Unreserve/ForgetPod) */
+int kss_commit(kss_ctx* ctx, const kss_podset* ps, int32_t pod_index, int32_t node);
+int kss_rollback(kss_ctx* ctx, const kss_podset* ps, int32_t pod_index, int32_t node);
+
+/* sequential scheduling of ps.pods[0..n) entirely on the device: each pod sees the
+ * previous pods' commits.  chosen_out[i] = global node index or -1.  When
+ * record != 0 (and max_pods_record >= n) per-pod results stay in HBM for
+ * kss_fetch_record / kss_format_annotations. */
+#define KSS_SCHED_RECORD (1u << 0)
+#define KSS_SCHED_FORCE_MULTI_WG (1u << 1) /* testing: use the multi-workgroup per-pod path */
+#define KSS_SCHED_FORCE_SINGLE_WG (1u << 2)
+int kss_schedule_batch(kss_ctx* ctx, const kss_podset* ps, int32_t n, uint32_t flags, int32_t* chosen_out);
+int kss_fetch_record(kss_ctx* ctx, int32_t pod_index, kss_pod_result* out);
+
+/* many independent clusters (what-if scenarios, KEP-184): clusters[s] with podsets[s];
+ * one workgroup per scenario, no inter-scenario communication. chosen_out is [sum n_pods]. */
+int kss_schedule_scenarios(int32_t device, const kss_profile* prof, int32_t n_scen, const kss_cluster* clusters,
+                           const kss_podset* podsets, int32_t* chosen_out, double* device_ms);
+
+/* timing of the last kss_schedule_batch / kss_eval_pod device work (HIP events on the work stream) */
+int kss_last_timing(kss_ctx* ctx, double* device_ms, int32_t* launches);
+
+/* ---- annotation formatting (store.go GetStoredResult semantics) -------- */
+typedef struct kss_names {
+  const char* const* node_names;    /* [n_nodes] */
+  const char* const* taint_keys;    /* [n_taints] */
+  const char* const* taint_values;  /* [n_taints] */
+  const char* const* scalar_names;  /* [n_scalar] */
+} kss_names;
+int kss_set_names(kss_ctx* ctx, const kss_names* names);
+/* Format the 13 annotation values of one recorded pod result as
+ * "key\0value\0key\0value\0...\0\0" into buf.  *need receives the byte count
+ * required (call with cap=0 to size).  Formatting is lazy: nothing is produced
+ * in the timed scheduling path. */
+int kss_format_annotations(kss_ctx* ctx, const kss_pod_result* res, int32_t n_nodes, char* buf, size_t cap,
+                           size_t* need);
+
+/* ---- synthetic clusters (SplitMix64, seed 0x5EED0000 + config) */
+typedef struct kss_synth {
+  kss_cluster cluster;
+  kss_podset pods;
+  void* owner; /* internal */
+} kss_synth;
+/* config_id 1..5 selects the BASELINE.json recipe; n_nodes/n_pods override sizes when > 0 */
+int kss_synth_make(int32_t config_id, uint64_t seed, int32_t n_nodes, int32_t n_pods, kss_synth* out);
+void kss_synth_free(kss_synth* s);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* KSS_H_ */

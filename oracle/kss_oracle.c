@@ -1,0 +1,883 @@
+/*
+ * kss_oracle.c — CPU ORACLE (TEST INFRASTRUCTURE ONLY).
+ *
+ * Plain-C restatement, in reference operation order, of the scheduling-cycle hot
+ * path of kube-scheduler-simulator (upstream k8s.io/kubernetes v1.26.2, pinned at
+ * /root/reference/simulator/go.mod:56; the module is not vendored and cannot be
+ * fetched here, so every ⟨k8s⟩ citation below names the upstream function).
+ * It works on the same struct-of-arrays input (include/kss.h) as the HIP path and
+ * is used only by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg,
+ * as the checker.  Nothing in the product links against it.
+ *
+ * Parity status: the restatement is pinned by the reference's own known-answer
+ * vector (README.md:61-79 / simulator/docs/debuggable-scheduler.md:17-35: Fit 73,
+ * BalancedAllocation 76, TaintToleration 0->300, PodTopologySpread 0->200) and is
+ * cross-checked against the independent object-level Python restatement
+ * (oracle/k8s_oracle.py).  Everything else is "parity vs the restated spec"
+ * (the Go reference is unbuildable in this container).
+ *
+ * Selection tie-break: max TotalScore, then LOWEST canonical node index (the
+ * reference's selectHost, scheduler/scheduler.go:323-344, samples ties with
+ * math/rand; north_star fixes a deterministic rule).
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+#include "../include/kss.h"
+
+#define MAXKEYS_PER_POD 16
+
+/* ---------------------------------------------------------------------------
+ * Go's math.Log restated (src/math/log.go, FreeBSD e_log.c): used for the
+ * PodTopologySpread normalizing weight math.Log(float64(size+2)).
+ * Compiled with -ffp-contract=off so no FMA is formed (Go amd64, GOAMD64=v1).
+ * ------------------------------------------------------------------------- */
+static double go_log(double x) {
+  const double Ln2Hi = 6.93147180369123816490e-01, Ln2Lo = 1.90821492927058770002e-10;
+  const double L1 = 6.666666666666735130e-01, L2 = 3.999999999940941908e-01, L3 = 2.857142874366239149e-01,
+               L4 = 2.222219843214978396e-01, L5 = 1.818357216161805012e-01, L6 = 1.531383769920937332e-01,
+               L7 = 1.479819860511658591e-01;
+  if (x != x || x == INFINITY) return x;
+  if (x < 0) return NAN;
+  if (x == 0) return -INFINITY;
+  int ki;
+  double f1 = frexp(x, &ki);
+  if (f1 < M_SQRT2 / 2) {
+    f1 *= 2;
+    ki--;
+  }
+  double f = f1 - 1;
+  double k = (double)ki;
+  double s = f / (2 + f);
+  double s2 = s * s;
+  double s4 = s2 * s2;
+  double t1 = s2 * (L1 + s4 * (L3 + s4 * (L5 + s4 * L7)));
+  double t2 = s4 * (L2 + s4 * (L4 + s4 * L6));
+  double R = t1 + t2;
+  double hfsq = 0.5 * f * f;
+  return k * Ln2Hi - ((hfsq - (s * (hfsq + R) + k * Ln2Lo)) - f);
+}
+
+double kss_oracle_go_log(double x) { return go_log(x); }
+
+/* Go math.Round: half away from zero (src/math/floor.go Round) == C round(). */
+static int64_t go_round_to_i64(double x) { return (int64_t)round(x); }
+
+/* ---------------------------------------------------------------------------
+ * mutable oracle state: a private copy of the node columns that commits change
+ * ------------------------------------------------------------------------- */
+typedef struct {
+  kss_cluster c; /* pointers below point into owned arrays */
+  int64_t* requested;
+  int64_t* nonzero;
+  int32_t* pod_count;
+  int32_t* class_count;
+  int32_t* term_count;
+} ostate;
+
+static int ostate_init(ostate* s, const kss_cluster* cl) {
+  size_t N = (size_t)cl->n_nodes;
+  s->c = *cl;
+  s->requested = (int64_t*)malloc(sizeof(int64_t) * KSS_NRES * (N ? N : 1));
+  s->nonzero = (int64_t*)malloc(sizeof(int64_t) * 2 * (N ? N : 1));
+  s->pod_count = (int32_t*)malloc(sizeof(int32_t) * (N ? N : 1));
+  s->class_count = (int32_t*)malloc(sizeof(int32_t) * ((size_t)cl->n_classes * N + 1));
+  s->term_count = (int32_t*)malloc(sizeof(int32_t) * ((size_t)cl->n_terms * N + 1));
+  if (!s->requested || !s->nonzero || !s->pod_count || !s->class_count || !s->term_count) return -1;
+  memcpy(s->requested, cl->requested, sizeof(int64_t) * KSS_NRES * N);
+  memcpy(s->nonzero, cl->nonzero, sizeof(int64_t) * 2 * N);
+  memcpy(s->pod_count, cl->pod_count, sizeof(int32_t) * N);
+  if (cl->n_classes) memcpy(s->class_count, cl->class_count, sizeof(int32_t) * (size_t)cl->n_classes * N);
+  if (cl->n_terms) memcpy(s->term_count, cl->term_count, sizeof(int32_t) * (size_t)cl->n_terms * N);
+  s->c.requested = s->requested;
+  s->c.nonzero = s->nonzero;
+  s->c.pod_count = s->pod_count;
+  s->c.class_count = s->class_count;
+  s->c.term_count = s->term_count;
+  return 0;
+}
+
+static void ostate_free(ostate* s) {
+  free(s->requested);
+  free(s->nonzero);
+  free(s->pod_count);
+  free(s->class_count);
+  free(s->term_count);
+}
+
+#define LV(cl, key, n) ((cl)->label_value[(size_t)(key) * (size_t)(cl)->n_nodes + (size_t)(n)])
+
+/* labels.Requirement.Matches (apimachinery labels/selector.go) over interned ids,
+ * plus the metadata.name field selector (component-helpers nodeaffinity). */
+static int req_matches(const kss_cluster* cl, const kss_podset* ps, const kss_req* r, int n) {
+  int64_t gidx = (int64_t)cl->node_base + n;
+  switch (r->op) {
+    case KSS_OP_FALSE:
+      return 0;
+    case KSS_OP_TRUE:
+      return 1;
+    case KSS_OP_NAME_IN:
+      return r->ival >= 0 && gidx == r->ival;
+    case KSS_OP_NAME_NOTIN:
+      return !(r->ival >= 0 && gidx == r->ival);
+    default:
+      break;
+  }
+  int32_t v = LV(cl, r->key, n);
+  switch (r->op) {
+    case KSS_OP_MASK:
+      if (v < 0) return (int)((r->mask >> 63) & 1u);
+      return v < 63 ? (int)((r->mask >> v) & 1u) : 0;
+    case KSS_OP_IN:
+      if (v < 0) return 0;
+      for (int i = 0; i < r->list_len; i++)
+        if (ps->ints[r->list_off + i] == v) return 1;
+      return 0;
+    case KSS_OP_NOTIN:
+      if (v < 0) return 1;
+      for (int i = 0; i < r->list_len; i++)
+        if (ps->ints[r->list_off + i] == v) return 0;
+      return 1;
+    case KSS_OP_EXISTS:
+      return v >= 0;
+    case KSS_OP_DNE:
+      return v < 0;
+    case KSS_OP_GT:
+    case KSS_OP_LT: {
+      if (v < 0) return 0;
+      int32_t g = cl->key_base[r->key] + v;
+      if (!cl->value_is_int[g]) return 0;
+      return r->op == KSS_OP_GT ? cl->value_int[g] > r->ival : cl->value_int[g] < r->ival;
+    }
+    default:
+      return 0;
+  }
+}
+
+/* nodeSelectorTerm.match: AND over its requirements */
+static int term_matches(const kss_cluster* cl, const kss_podset* ps, const kss_term* t, int n) {
+  for (int i = 0; i < t->req_len; i++)
+    if (!req_matches(cl, ps, &ps->reqs[t->req_off + i], n)) return 0;
+  return 1;
+}
+
+/* nodeaffinity.RequiredNodeAffinity.Match (component-helpers):
+ * nodeSelector labels AND (OR over parsed NodeSelectorTerms). */
+static int required_node_affinity(const kss_cluster* cl, const kss_podset* ps, const kss_pod* p, int n) {
+  for (int i = 0; i < p->sel_len; i++)
+    if (!req_matches(cl, ps, &ps->reqs[p->sel_off + i], n)) return 0;
+  if (p->flags & KSS_POD_HAS_REQ_AFFINITY) {
+    for (int t = 0; t < p->aff_len; t++)
+      if (term_matches(cl, ps, &ps->terms[p->aff_off + t], n)) return 1;
+    return 0;
+  }
+  return 1;
+}
+
+/* v1helper.FindMatchingUntoleratedTaint(node.Spec.Taints, tolerations, DoNotScheduleTaintsFilterFunc) */
+static int first_untolerated_taint(const kss_cluster* cl, const kss_pod* p, int n) {
+  uint64_t untol = cl->taint_hard[n] & ~p->tol_hard;
+  if (!untol) return -1;
+  const uint8_t* ord = cl->taint_order + (size_t)n * KSS_TAINT_ORDER;
+  for (int i = 0; i < KSS_TAINT_ORDER && ord[i] != 0xFF; i++)
+    if ((untol >> ord[i]) & 1u) return ord[i];
+  return 63 - __builtin_clzll(untol); /* unreachable for well-formed input */
+}
+
+static int64_t sum_rows(const int32_t* mat, size_t N, const int32_t* rows, int len, int n) {
+  int64_t s = 0;
+  for (int i = 0; i < len; i++) s += mat[(size_t)rows[i] * N + (size_t)n];
+  return s;
+}
+
+/* per-pod PreFilter / PreScore state for PodTopologySpread and InterPodAffinity */
+typedef struct {
+  /* PTS hard: per constraint, bins = card+1 */
+  int64_t* hard_cnt[8];
+  uint8_t* hard_present[8];
+  int64_t hard_min[8];
+  /* IPA: per (entry kind, key) histograms */
+  int nkeys;
+  int keys[MAXKEYS_PER_POD];
+  int64_t* hx[MAXKEYS_PER_POD]; /* existing anti-affinity */
+  int64_t* ha[MAXKEYS_PER_POD]; /* incoming affinity */
+  int64_t* hb[MAXKEYS_PER_POD]; /* incoming anti-affinity */
+  int64_t* hs[MAXKEYS_PER_POD]; /* score topologyScore */
+  int ex_nonempty, aff_nonempty, anti_nonempty, score_nonempty;
+} podstate;
+
+static int key_slot(podstate* st, int key) {
+  for (int i = 0; i < st->nkeys; i++)
+    if (st->keys[i] == key) return i;
+  return -1;
+}
+
+static int spread_policy_ok(const kss_cluster* cl, const kss_podset* ps, const kss_pod* p, const kss_spread* sp,
+                            int n) {
+  /* topologySpreadConstraint.matchNodeInclusionPolicies (NodeInclusionPolicy beta, on in v1.26) */
+  if ((sp->flags & KSS_SPREAD_POLICY_AFFINITY_HONOR) && !required_node_affinity(cl, ps, p, n)) return 0;
+  if ((sp->flags & KSS_SPREAD_POLICY_TAINTS_HONOR) && first_untolerated_taint(cl, p, n) >= 0) return 0;
+  return 1;
+}
+
+static int has_all_keys(const kss_cluster* cl, const kss_spread* sp, int cnt, int n) {
+  for (int i = 0; i < cnt; i++)
+    if (LV(cl, sp[i].key, n) < 0) return 0;
+  return 1;
+}
+
+static void podstate_free(podstate* st) {
+  for (int i = 0; i < 8; i++) {
+    free(st->hard_cnt[i]);
+    free(st->hard_present[i]);
+  }
+  for (int i = 0; i < st->nkeys; i++) {
+    free(st->hx[i]);
+    free(st->ha[i]);
+    free(st->hb[i]);
+    free(st->hs[i]);
+  }
+}
+
+/* PodTopologySpread PreFilter (calPreFilterState) and InterPodAffinity PreFilter
+ * (getExistingAntiAffinityCounts, getIncomingAffinityAntiAffinityCounts) and
+ * InterPodAffinity PreScore (processExistingPod) — all scan every node. */
+static int podstate_build(podstate* st, const kss_cluster* cl, const kss_podset* ps, const kss_pod* p,
+                          int hard_pod_affinity_weight) {
+  memset(st, 0, sizeof(*st));
+  size_t N = (size_t)cl->n_nodes;
+  const kss_spread* hard = ps->spreads + p->spread_off;
+  if (p->n_hard > 8 || p->n_soft > 8) return KSS_E_UNSUPPORTED;
+  for (int i = 0; i < p->n_hard; i++) {
+    int bins = cl->key_card[hard[i].key] + 1;
+    st->hard_cnt[i] = (int64_t*)calloc((size_t)bins, sizeof(int64_t));
+    st->hard_present[i] = (uint8_t*)calloc((size_t)bins, 1);
+  }
+  for (size_t n = 0; n < N; n++) {
+    if (!has_all_keys(cl, hard, p->n_hard, (int)n)) continue; /* nodeLabelsMatchSpreadConstraints */
+    for (int i = 0; i < p->n_hard; i++) {
+      if (!spread_policy_ok(cl, ps, p, &hard[i], (int)n)) continue;
+      int d = LV(cl, hard[i].key, n);
+      /* countPodsMatchSelector(nodeInfo.Pods, selector, pod.Namespace) */
+      int64_t c = sum_rows(cl->class_count, N, ps->ints + hard[i].cls_off, hard[i].cls_len, (int)n);
+      st->hard_cnt[i][d] += c;
+      st->hard_present[i][d] = 1;
+    }
+  }
+  for (int i = 0; i < p->n_hard; i++) {
+    /* criticalPaths[0].MatchNum: global minimum over existing pairs, MaxInt32 if none */
+    int64_t mn = INT32_MAX;
+    int bins = cl->key_card[hard[i].key] + 1;
+    for (int d = 0; d < bins; d++)
+      if (st->hard_present[i][d] && st->hard_cnt[i][d] < mn) mn = st->hard_cnt[i][d];
+    st->hard_min[i] = mn;
+  }
+
+  /* inter-pod affinity histograms, per distinct topology key */
+  const kss_ipa* ipa = ps->ipa + p->ipa_off;
+  for (int e = 0; e < p->ipa_len; e++) {
+    if (ipa[e].kind == KSS_IPA_SCORE_TERM && hard_pod_affinity_weight == 0 && ipa[e].coef == 0) continue;
+    if (key_slot(st, ipa[e].key) < 0) {
+      if (st->nkeys >= MAXKEYS_PER_POD) return KSS_E_UNSUPPORTED;
+      int k = st->nkeys++;
+      int bins = cl->key_card[ipa[e].key] + 1;
+      st->keys[k] = ipa[e].key;
+      st->hx[k] = (int64_t*)calloc((size_t)bins, sizeof(int64_t));
+      st->ha[k] = (int64_t*)calloc((size_t)bins, sizeof(int64_t));
+      st->hb[k] = (int64_t*)calloc((size_t)bins, sizeof(int64_t));
+      st->hs[k] = (int64_t*)calloc((size_t)bins, sizeof(int64_t));
+    }
+  }
+  for (size_t n = 0; n < N; n++) {
+    int has_labels = (cl->node_flags[n] & KSS_NODE_HAS_LABELS) != 0;
+    for (int e = 0; e < p->ipa_len; e++) {
+      const kss_ipa* en = &ipa[e];
+      int d = LV(cl, en->key, n);
+      if (d < 0) continue; /* topologyToMatchedTermCount.update / scoreMap.processTerm: node lacks key */
+      int k = key_slot(st, en->key);
+      const int32_t* rows = ps->ints + en->row_off;
+      switch (en->kind) {
+        case KSS_IPA_EXISTING_ANTI: {
+          int64_t c = sum_rows(cl->term_count, N, rows, en->row_len, (int)n);
+          st->hx[k][d] += c;
+          break;
+        }
+        case KSS_IPA_REQ_AFFINITY: {
+          int64_t c = sum_rows(cl->class_count, N, rows, en->row_len, (int)n);
+          st->ha[k][d] += c;
+          break;
+        }
+        case KSS_IPA_REQ_ANTI: {
+          int64_t c = sum_rows(cl->class_count, N, rows, en->row_len, (int)n);
+          st->hb[k][d] += c;
+          break;
+        }
+        case KSS_IPA_SCORE_CLASS:
+        case KSS_IPA_SCORE_TERM: {
+          if (!has_labels) break; /* processExistingPod: len(existingPodNode.Labels) == 0 -> return */
+          const int32_t* mat = en->kind == KSS_IPA_SCORE_CLASS ? cl->class_count : cl->term_count;
+          int64_t c = sum_rows(mat, N, rows, en->row_len, (int)n);
+          if (c > 0) st->score_nonempty = 1;
+          st->hs[k][d] += c * (int64_t)en->coef;
+          break;
+        }
+      }
+    }
+  }
+  for (int k = 0; k < st->nkeys; k++) {
+    int bins = cl->key_card[st->keys[k]] + 1;
+    for (int d = 0; d < bins; d++) {
+      if (st->hx[k][d] > 0) st->ex_nonempty = 1;
+      if (st->ha[k][d] > 0) st->aff_nonempty = 1;
+      if (st->hb[k][d] > 0) st->anti_nonempty = 1;
+    }
+  }
+  return 0;
+}
+
+/* ---------------------------------------------------------------------------
+ * Filter chain for one node (RunFilterPlugins, first failure wins).
+ * Returns the failing plugin id (0 = pass) and sets *detail.
+ * ------------------------------------------------------------------------- */
+static int filter_node(const kss_profile* prof, const kss_cluster* cl, const kss_podset* ps, const kss_pod* p,
+                       const podstate* st, int n, uint16_t* detail) {
+  uint32_t en = prof->filter_enabled;
+  *detail = 0;
+  /* NodeUnschedulable.Filter */
+  if ((en >> KSS_F_NODE_UNSCHEDULABLE) & 1u) {
+    if ((cl->node_flags[n] & KSS_NODE_UNSCHEDULABLE) && !(p->flags & KSS_POD_TOL_UNSCHEDULABLE))
+      return KSS_F_NODE_UNSCHEDULABLE;
+  }
+  /* NodeName.Filter: len(pod.Spec.NodeName)==0 || == node.Name */
+  if ((en >> KSS_F_NODE_NAME) & 1u) {
+    if (p->node_name != -1 && (int64_t)p->node_name != (int64_t)cl->node_base + n) return KSS_F_NODE_NAME;
+  }
+  /* TaintToleration.Filter */
+  if ((en >> KSS_F_TAINT_TOLERATION) & 1u) {
+    int t = first_untolerated_taint(cl, p, n);
+    if (t >= 0) {
+      *detail = (uint16_t)t;
+      return KSS_F_TAINT_TOLERATION;
+    }
+  }
+  /* NodeAffinity.Filter */
+  if ((en >> KSS_F_NODE_AFFINITY) & 1u) {
+    if (!required_node_affinity(cl, ps, p, n)) return KSS_F_NODE_AFFINITY;
+  }
+  /* NodePorts: pods carry no host ports (host compile rejects them) -> pass */
+  /* NodeResourcesFit.Filter -> fitsRequest */
+  if ((en >> KSS_F_NODE_RESOURCES_FIT) & 1u) {
+    size_t N = (size_t)cl->n_nodes;
+    uint16_t bits = 0;
+    if ((int64_t)cl->pod_count[n] + 1 > (int64_t)cl->allowed_pods[n]) bits |= KSS_FIT_TOO_MANY_PODS;
+    int all_zero = 1;
+    for (int r = 0; r < 3 + cl->n_scalar; r++)
+      if (p->fit_request[r] != 0) all_zero = 0;
+    /* len(podRequest.ScalarResources)==0: a zero-valued scalar entry still counts as present; the host
+       encodes "present with zero" as-is, so treat any scalar request slot flagged by the host as present */
+    if (!all_zero) {
+      for (int r = 0; r < 3 + cl->n_scalar; r++) {
+        int64_t req = p->fit_request[r];
+        if (r >= KSS_RES_SCALAR0 && req == 0) continue; /* Skip in case request quantity is zero */
+        int64_t freev = cl->alloc[(size_t)r * N + n] - cl->requested[(size_t)r * N + n];
+        if (req > freev) bits |= (uint16_t)(1u << (r + 1));
+      }
+    }
+    if (bits) {
+      *detail = bits;
+      return KSS_F_NODE_RESOURCES_FIT;
+    }
+  }
+  /* VolumeRestrictions, EBSLimits, GCEPDLimits, NodeVolumeLimits, AzureDiskLimits, VolumeBinding,
+     VolumeZone: volume-less pods pass. */
+  /* PodTopologySpread.Filter */
+  if (((en >> KSS_F_POD_TOPOLOGY_SPREAD) & 1u) && p->n_hard > 0) {
+    const kss_spread* hard = ps->spreads + p->spread_off;
+    for (int i = 0; i < p->n_hard; i++) {
+      int d = LV(cl, hard[i].key, n);
+      if (d < 0) {
+        *detail = KSS_PTS_MISSING_LABEL;
+        return KSS_F_POD_TOPOLOGY_SPREAD;
+      }
+      int64_t match = st->hard_present[i][d] ? st->hard_cnt[i][d] : 0;
+      int64_t skew = match + (int64_t)hard[i].self_match - st->hard_min[i];
+      if (skew > (int64_t)hard[i].max_skew) {
+        *detail = KSS_PTS_CONSTRAINTS_NOT_MATCH;
+        return KSS_F_POD_TOPOLOGY_SPREAD;
+      }
+    }
+  }
+  /* InterPodAffinity.Filter */
+  if ((en >> KSS_F_INTER_POD_AFFINITY) & 1u) {
+    const kss_ipa* ipa = ps->ipa + p->ipa_off;
+    /* satisfyPodAffinity */
+    int pods_exist = 1, have_aff = 0;
+    for (int e = 0; e < p->ipa_len; e++) {
+      if (ipa[e].kind != KSS_IPA_REQ_AFFINITY) continue;
+      have_aff = 1;
+      int d = LV(cl, ipa[e].key, n);
+      if (d < 0) {
+        *detail = KSS_IPA_AFFINITY;
+        return KSS_F_INTER_POD_AFFINITY;
+      }
+      int k = key_slot((podstate*)st, ipa[e].key);
+      if (st->ha[k][d] <= 0) pods_exist = 0;
+    }
+    if (have_aff && !pods_exist) {
+      if (!(!st->aff_nonempty && (p->flags & KSS_POD_IPA_SELF_MATCH))) {
+        *detail = KSS_IPA_AFFINITY;
+        return KSS_F_INTER_POD_AFFINITY;
+      }
+    }
+    /* satisfyPodAntiAffinity */
+    if (st->anti_nonempty) {
+      for (int e = 0; e < p->ipa_len; e++) {
+        if (ipa[e].kind != KSS_IPA_REQ_ANTI) continue;
+        int d = LV(cl, ipa[e].key, n);
+        if (d < 0) continue;
+        int k = key_slot((podstate*)st, ipa[e].key);
+        if (st->hb[k][d] > 0) {
+          *detail = KSS_IPA_ANTI_AFFINITY;
+          return KSS_F_INTER_POD_AFFINITY;
+        }
+      }
+    }
+    /* satisfyExistingPodsAntiAffinity */
+    if (st->ex_nonempty) {
+      for (int e = 0; e < p->ipa_len; e++) {
+        if (ipa[e].kind != KSS_IPA_EXISTING_ANTI) continue;
+        int d = LV(cl, ipa[e].key, n);
+        if (d < 0) continue;
+        int k = key_slot((podstate*)st, ipa[e].key);
+        if (st->hx[k][d] > 0) {
+          *detail = KSS_IPA_EXISTING_ANTI_AFFINITY;
+          return KSS_F_INTER_POD_AFFINITY;
+        }
+      }
+    }
+  }
+  return KSS_F_PASS;
+}
+
+/* ---------------------------------------------------------------------------
+ * raw scores (Score extension point) for one feasible node
+ * ------------------------------------------------------------------------- */
+static int64_t least_or_most(const kss_profile* prof, int64_t requested, int64_t capacity) {
+  if (prof->fit_strategy == KSS_FIT_MOST_ALLOCATED) {
+    /* mostRequestedScore (noderesources/most_allocated.go) */
+    if (capacity == 0) return 0;
+    if (requested > capacity) requested = capacity;
+    return (requested * 100) / capacity;
+  }
+  /* leastRequestedScore (noderesources/least_allocated.go) */
+  if (capacity == 0) return 0;
+  if (requested > capacity) return 0;
+  return ((capacity - requested) * 100) / capacity;
+}
+
+/* NodeResourcesFit Score: resourceAllocationScorer.score with useRequested=false */
+static int64_t fit_score(const kss_profile* prof, const kss_cluster* cl, const kss_pod* p, int n) {
+  size_t N = (size_t)cl->n_nodes;
+  int64_t node_score = 0, weight_sum = 0;
+  for (int i = 0; i < prof->fit_n; i++) {
+    int r = prof->fit_res[i];
+    int64_t preq = p->score_req_nz[r];
+    int64_t alloc, req;
+    /* calculateResourceAllocatableRequest */
+    if (r >= KSS_RES_SCALAR0 && preq == 0) continue;
+    if (r == KSS_RES_CPU || r == KSS_RES_MEMORY) {
+      alloc = cl->alloc[(size_t)r * N + n];
+      req = cl->nonzero[(size_t)r * N + n] + preq;
+    } else {
+      alloc = cl->alloc[(size_t)r * N + n];
+      req = cl->requested[(size_t)r * N + n] + preq;
+    }
+    if (alloc == 0) continue; /* score(): only fill entries with alloc != 0; scorer skips allocable==0 */
+    node_score += least_or_most(prof, req, alloc) * prof->fit_weight[i];
+    weight_sum += prof->fit_weight[i];
+  }
+  if (weight_sum == 0) return 0;
+  return node_score / weight_sum;
+}
+
+/* NodeResourcesBalancedAllocation Score: balancedResourceScorer, useRequested=true */
+static int64_t ba_score(const kss_profile* prof, const kss_cluster* cl, const kss_pod* p, int n) {
+  size_t N = (size_t)cl->n_nodes;
+  double fr[4];
+  int nf = 0;
+  double total = 0;
+  for (int i = 0; i < prof->ba_n; i++) {
+    int r = prof->ba_res[i];
+    int64_t preq = p->score_req[r];
+    if (r >= KSS_RES_SCALAR0 && preq == 0) continue;
+    int64_t alloc = cl->alloc[(size_t)r * N + n];
+    int64_t req = cl->requested[(size_t)r * N + n] + preq;
+    if (alloc == 0) continue;
+    double f = (double)req / (double)alloc;
+    if (f > 1) f = 1;
+    total += f;
+    fr[nf++] = f;
+  }
+  double sd = 0.0;
+  if (nf == 2) {
+    sd = fabs((fr[0] - fr[1]) / 2);
+  } else if (nf > 2) {
+    double mean = total / (double)nf;
+    double sum = 0;
+    for (int i = 0; i < nf; i++) sum = sum + (fr[i] - mean) * (fr[i] - mean);
+    sd = sqrt(sum / (double)nf);
+  }
+  return (int64_t)((1 - sd) * (double)100);
+}
+
+/* TaintToleration Score: countIntolerableTaintsPreferNoSchedule */
+static int64_t tt_score(const kss_cluster* cl, const kss_pod* p, int n) {
+  return (int64_t)__builtin_popcountll(cl->taint_soft[n] & ~p->tol_soft);
+}
+
+/* NodeAffinity Score: PreferredSchedulingTerms.Score */
+static int64_t na_score(const kss_cluster* cl, const kss_podset* ps, const kss_pod* p, int n) {
+  int64_t s = 0;
+  for (int t = 0; t < p->pref_len; t++) {
+    const kss_term* term = &ps->terms[p->pref_off + t];
+    if (term_matches(cl, ps, term, n)) s += term->weight;
+  }
+  return s;
+}
+
+/* helper.DefaultNormalizeScore */
+static void default_normalize(int64_t* scores, const int32_t* idx, int nf, int reverse) {
+  int64_t mx = 0;
+  for (int i = 0; i < nf; i++)
+    if (scores[idx[i]] > mx) mx = scores[idx[i]];
+  if (mx == 0) {
+    if (reverse)
+      for (int i = 0; i < nf; i++) scores[idx[i]] = 100;
+    return;
+  }
+  for (int i = 0; i < nf; i++) {
+    int64_t s = 100 * scores[idx[i]] / mx;
+    if (reverse) s = 100 - s;
+    scores[idx[i]] = s;
+  }
+}
+
+typedef struct {
+  int threads;
+} oracle_opts;
+
+/* one scheduling cycle (schedulePod) for pod p against state s; fills out (arrays sized N) */
+static int schedule_one(const kss_profile* prof, ostate* s, const kss_podset* ps, int pi, kss_pod_result* out,
+                        int threads) {
+  const kss_cluster* cl = &s->c;
+  const kss_pod* p = &ps->pods[pi];
+  int N = cl->n_nodes;
+  uint8_t* fp = (uint8_t*)malloc((size_t)(N ? N : 1));
+  uint16_t* fd = (uint16_t*)malloc(sizeof(uint16_t) * (size_t)(N ? N : 1));
+  int64_t* raw = (int64_t*)calloc((size_t)KSS_NSCORE * (size_t)(N ? N : 1), sizeof(int64_t));
+  int64_t* norm = (int64_t*)calloc((size_t)KSS_NSCORE * (size_t)(N ? N : 1), sizeof(int64_t));
+  int64_t* total = (int64_t*)calloc((size_t)(N ? N : 1), sizeof(int64_t));
+  int32_t* feas = (int32_t*)malloc(sizeof(int32_t) * (size_t)(N ? N : 1));
+  int rc = 0;
+  podstate st;
+  memset(&st, 0, sizeof(st));
+  out->chosen = -1;
+  out->n_feasible = 0;
+  out->best_total = 0;
+  out->scored = 0;
+  out->status = 0;
+  for (int n = 0; n < N; n++) {
+    fp[n] = KSS_F_NOT_EVALUATED;
+    fd[n] = 0;
+  }
+
+  if (p->prefilter_status != 0) {
+    out->status = p->prefilter_status == 1 ? 2 : 3;
+    goto done;
+  }
+  rc = podstate_build(&st, cl, ps, p, prof->hard_pod_affinity_weight);
+  if (rc) goto done;
+
+  /* HOT LOOP 1: findNodesThatPassFilters over the (PreFilterResult-restricted) node list */
+  {
+    uint8_t* inset = NULL;
+    if (p->names_len >= 0) {
+      inset = (uint8_t*)calloc((size_t)(N ? N : 1), 1);
+      for (int i = 0; i < p->names_len; i++) {
+        int64_t g = ps->ints[p->names_off + i] - cl->node_base;
+        if (g >= 0 && g < N) inset[g] = 1;
+      }
+    }
+#pragma omp parallel for num_threads(threads) schedule(static)
+    for (int n = 0; n < N; n++) {
+      if (inset && !inset[n]) continue;
+      fp[n] = (uint8_t)filter_node(prof, cl, ps, p, &st, n, &fd[n]);
+    }
+    free(inset);
+  }
+  int nf = 0;
+  for (int n = 0; n < N; n++)
+    if (fp[n] == KSS_F_PASS) feas[nf++] = n;
+  out->n_feasible = nf;
+  if (nf == 0) {
+    out->status = 1;
+    goto done;
+  }
+  if (nf == 1) { /* "When only one node after predicate, just use it." */
+    out->chosen = cl->node_base + feas[0];
+    goto done;
+  }
+  out->scored = 1;
+
+  /* PreScore PodTopologySpread: initPreScoreState + processAllNode */
+  const kss_spread* soft = ps->spreads + p->spread_off + p->n_hard;
+  int require_all = (p->flags & KSS_POD_PTS_REQUIRE_ALL) != 0;
+  double w[8];
+  int64_t* soft_cnt[8] = {0};
+  uint8_t* soft_present[8] = {0};
+  uint8_t* ignored = (uint8_t*)calloc((size_t)(N ? N : 1), 1);
+  int nignored = 0;
+  for (int i = 0; i < nf; i++) {
+    int n = feas[i];
+    if (require_all && !has_all_keys(cl, soft, p->n_soft, n)) {
+      ignored[n] = 1;
+      nignored++;
+    }
+  }
+  for (int c = 0; c < p->n_soft; c++) {
+    int key = soft[c].key;
+    int bins = cl->key_card[key] + 1;
+    soft_cnt[c] = (int64_t*)calloc((size_t)bins, sizeof(int64_t));
+    soft_present[c] = (uint8_t*)calloc((size_t)bins, 1);
+    int size = 0;
+    if (cl->key_flags[key] & KSS_KEY_HOSTNAME) {
+      size = nf - nignored;
+    } else {
+      for (int i = 0; i < nf; i++) {
+        int n = feas[i];
+        if (ignored[n]) continue;
+        int d = LV(cl, key, n);
+        if (d < 0) d = cl->key_empty[key]; /* node.Labels[key] == "" for a missing key */
+        if (!soft_present[c][d]) {
+          soft_present[c][d] = 1;
+          size++;
+        }
+      }
+    }
+    w[c] = go_log((double)(size + 2)); /* topologyNormalizingWeight */
+  }
+  if (p->n_soft > 0) {
+    for (int n = 0; n < N; n++) {
+      if (require_all && !has_all_keys(cl, soft, p->n_soft, n)) continue;
+      for (int c = 0; c < p->n_soft; c++) {
+        int key = soft[c].key;
+        if (cl->key_flags[key] & KSS_KEY_HOSTNAME) continue; /* per-node counts computed in Score */
+        if (!spread_policy_ok(cl, ps, p, &soft[c], n)) continue;
+        int d = LV(cl, key, n);
+        if (d < 0) d = cl->key_empty[key];
+        if (!soft_present[c][d]) continue; /* pair not associated with any candidate node */
+        soft_cnt[c][d] += sum_rows(cl->class_count, (size_t)N, ps->ints + soft[c].cls_off, soft[c].cls_len, n);
+      }
+    }
+  }
+
+  /* HOT LOOP 2: RunScorePlugins raw scores */
+#pragma omp parallel for num_threads(threads) schedule(static)
+  for (int i = 0; i < nf; i++) {
+    int n = feas[i];
+    size_t NN = (size_t)N;
+    raw[KSS_S_TAINT_TOLERATION * NN + n] = tt_score(cl, p, n);
+    raw[KSS_S_NODE_AFFINITY * NN + n] = na_score(cl, ps, p, n);
+    raw[KSS_S_NODE_RESOURCES_FIT * NN + n] = fit_score(prof, cl, p, n);
+    raw[KSS_S_VOLUME_BINDING * NN + n] = 0;
+    raw[KSS_S_BALANCED_ALLOCATION * NN + n] = ba_score(prof, cl, p, n);
+    raw[KSS_S_IMAGE_LOCALITY * NN + n] = 0; /* nodes carry no Status.Images: calculatePriority(minThreshold) = 0 */
+    /* PodTopologySpread.Score */
+    int64_t pts = 0;
+    if (!ignored[n]) {
+      double sc = 0;
+      for (int c = 0; c < p->n_soft; c++) {
+        int key = soft[c].key;
+        int d = LV(cl, key, n);
+        if (d < 0) continue;
+        int64_t cnt;
+        if (cl->key_flags[key] & KSS_KEY_HOSTNAME)
+          cnt = sum_rows(cl->class_count, NN, ps->ints + soft[c].cls_off, soft[c].cls_len, n);
+        else
+          cnt = soft_cnt[c][d];
+        sc += (double)cnt * w[c] + (double)(soft[c].max_skew - 1); /* scoreForCount */
+      }
+      pts = go_round_to_i64(sc);
+    }
+    raw[KSS_S_POD_TOPOLOGY_SPREAD * NN + n] = pts;
+    /* InterPodAffinity.Score: Σ over topology keys present on the node */
+    int64_t ipa = 0;
+    for (int k = 0; k < st.nkeys; k++) {
+      int d = LV(cl, st.keys[k], n);
+      if (d >= 0) ipa += st.hs[k][d];
+    }
+    raw[KSS_S_INTER_POD_AFFINITY * NN + n] = ipa;
+  }
+  memcpy(norm, raw, sizeof(int64_t) * KSS_NSCORE * (size_t)N);
+
+  /* HOT LOOP 3: NormalizeScore per plugin over the feasible list */
+  default_normalize(norm + (size_t)KSS_S_TAINT_TOLERATION * N, feas, nf, 1);
+  default_normalize(norm + (size_t)KSS_S_NODE_AFFINITY * N, feas, nf, 0);
+  { /* PodTopologySpread.NormalizeScore */
+    int64_t* sc = norm + (size_t)KSS_S_POD_TOPOLOGY_SPREAD * N;
+    int64_t mn = INT64_MAX, mx = 0;
+    for (int i = 0; i < nf; i++) {
+      int n = feas[i];
+      if (ignored[n]) continue;
+      if (sc[n] < mn) mn = sc[n];
+      if (sc[n] > mx) mx = sc[n];
+    }
+    for (int i = 0; i < nf; i++) {
+      int n = feas[i];
+      if (ignored[n]) {
+        sc[n] = 0;
+        continue;
+      }
+      if (mx == 0) {
+        sc[n] = 100;
+        continue;
+      }
+      sc[n] = 100 * (mx + mn - sc[n]) / mx;
+    }
+  }
+  if (st.score_nonempty) { /* InterPodAffinity.NormalizeScore (skipped when topologyScore is empty) */
+    int64_t* sc = norm + (size_t)KSS_S_INTER_POD_AFFINITY * N;
+    int64_t mn = INT64_MAX, mx = INT64_MIN;
+    for (int i = 0; i < nf; i++) {
+      int n = feas[i];
+      if (sc[n] > mx) mx = sc[n];
+      if (sc[n] < mn) mn = sc[n];
+    }
+    int64_t diff = mx - mn;
+    for (int i = 0; i < nf; i++) {
+      int n = feas[i];
+      double f = 0;
+      if (diff > 0) f = (double)100 * ((double)(sc[n] - mn) / (double)diff);
+      sc[n] = (int64_t)f;
+    }
+  }
+
+  /* HOT LOOP 4: weights + TotalScore, then selectHost (deterministic tie-break) */
+  {
+    int64_t best = INT64_MIN;
+    int bi = -1;
+    for (int i = 0; i < nf; i++) {
+      int n = feas[i];
+      int64_t t = 0;
+      for (int sp = 0; sp < KSS_NSCORE; sp++) {
+        if (!((prof->score_enabled >> sp) & 1u)) continue;
+        int64_t v = norm[(size_t)sp * N + n];
+        if (v > 100 || v < 0) {
+          out->status = 3; /* "plugin returns an invalid score" -> framework Error */
+        }
+        t += v * (int64_t)prof->weight[sp];
+      }
+      total[n] = t;
+      if (t > best) {
+        best = t;
+        bi = n;
+      }
+    }
+    if (out->status == 3) {
+      bi = -1;
+    }
+    out->best_total = best;
+    out->chosen = bi >= 0 ? cl->node_base + bi : -1;
+  }
+  for (int c = 0; c < p->n_soft; c++) {
+    free(soft_cnt[c]);
+    free(soft_present[c]);
+  }
+  free(ignored);
+
+done:
+  podstate_free(&st);
+  if (out->fail_plugin) memcpy(out->fail_plugin, fp, (size_t)N);
+  if (out->fail_detail) memcpy(out->fail_detail, fd, sizeof(uint16_t) * (size_t)N);
+  if (out->raw) memcpy(out->raw, raw, sizeof(int64_t) * KSS_NSCORE * (size_t)N);
+  if (out->norm) memcpy(out->norm, norm, sizeof(int64_t) * KSS_NSCORE * (size_t)N);
+  if (out->total) memcpy(out->total, total, sizeof(int64_t) * (size_t)N);
+  free(fp);
+  free(fd);
+  free(raw);
+  free(norm);
+  free(total);
+  free(feas);
+  return rc;
+}
+
+/* Cache.AssumePod -> NodeInfo.AddPod (framework/types.go calculateResource) */
+static void commit(ostate* s, const kss_podset* ps, int pi, int node_local) {
+  const kss_pod* p = &ps->pods[pi];
+  size_t N = (size_t)s->c.n_nodes;
+  for (int r = 0; r < KSS_NRES; r++) s->requested[(size_t)r * N + node_local] += p->commit_req[r];
+  s->nonzero[node_local] += p->commit_nz[0];
+  s->nonzero[N + node_local] += p->commit_nz[1];
+  s->pod_count[node_local] += 1;
+  if (p->cls >= 0) s->class_count[(size_t)p->cls * N + node_local] += 1;
+  for (int i = 0; i < p->own_terms_len; i++) s->term_count[(size_t)ps->ints[p->own_terms_off + i] * N + node_local] += 1;
+}
+
+/* ---------------------------------------------------------------------------
+ * exported entry points (ctypes)
+ * ------------------------------------------------------------------------- */
+
+/* Evaluate pod pi against cl without committing. */
+int kss_oracle_eval_pod(const kss_profile* prof, const kss_cluster* cl, const kss_podset* ps, int pi,
+                        kss_pod_result* out, int threads) {
+  ostate s;
+  if (ostate_init(&s, cl)) return KSS_E_NOMEM;
+  int rc = schedule_one(prof, &s, ps, pi, out, threads > 0 ? threads : 1);
+  ostate_free(&s);
+  return rc;
+}
+
+/* Sequentially schedule pods [0, n): each pod sees the previous commits.
+ * results (optional) is an array of n kss_pod_result whose arrays the caller
+ * allocated (any NULL array is skipped).  Final node state is written back to
+ * the optional out_* arrays. */
+int kss_oracle_schedule(const kss_profile* prof, const kss_cluster* cl, const kss_podset* ps, int n,
+                        int32_t* chosen, kss_pod_result* results, int threads, int64_t* out_requested,
+                        int64_t* out_nonzero, int32_t* out_pod_count, int32_t* out_class_count,
+                        int32_t* out_term_count) {
+  ostate s;
+  if (ostate_init(&s, cl)) return KSS_E_NOMEM;
+  int th = threads > 0 ? threads : 1;
+  int rc = 0;
+  for (int i = 0; i < n; i++) {
+    kss_pod_result tmp;
+    memset(&tmp, 0, sizeof(tmp));
+    kss_pod_result* out = results ? &results[i] : &tmp;
+    rc = schedule_one(prof, &s, ps, i, out, th);
+    if (rc) break;
+    chosen[i] = out->chosen;
+    if (out->chosen >= 0) commit(&s, ps, i, out->chosen - cl->node_base);
+  }
+  size_t N = (size_t)cl->n_nodes;
+  if (out_requested) memcpy(out_requested, s.requested, sizeof(int64_t) * KSS_NRES * N);
+  if (out_nonzero) memcpy(out_nonzero, s.nonzero, sizeof(int64_t) * 2 * N);
+  if (out_pod_count) memcpy(out_pod_count, s.pod_count, sizeof(int32_t) * N);
+  if (out_class_count && cl->n_classes)
+    memcpy(out_class_count, s.class_count, sizeof(int32_t) * (size_t)cl->n_classes * N);
+  if (out_term_count && cl->n_terms) memcpy(out_term_count, s.term_count, sizeof(int32_t) * (size_t)cl->n_terms * N);
+  ostate_free(&s);
+  return rc;
+}
+
+int kss_oracle_max_threads(void) {
+#ifdef _OPENMP
+  return omp_get_max_threads();
+#else
+  return 1;
+#endif
+}

@@ -1,0 +1,78 @@
+"""ctypes loader for the C oracle (oracle/build/libkss_oracle.so) — test infrastructure."""
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+from kss import abi
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB = os.path.join(ROOT, "oracle", "build", "libkss_oracle.so")
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB):
+            subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "oracle")])
+        _lib = C.CDLL(LIB)
+        P = C.POINTER
+        _lib.kss_oracle_schedule.argtypes = [P(abi.Profile), P(abi.Cluster), P(abi.PodSet), C.c_int,
+                                             P(C.c_int32), P(abi.PodResult), C.c_int, P(C.c_int64), P(C.c_int64),
+                                             P(C.c_int32), P(C.c_int32), P(C.c_int32)]
+        _lib.kss_oracle_schedule.restype = C.c_int
+        _lib.kss_oracle_eval_pod.argtypes = [P(abi.Profile), P(abi.Cluster), P(abi.PodSet), C.c_int,
+                                             P(abi.PodResult), C.c_int]
+        _lib.kss_oracle_eval_pod.restype = C.c_int
+        _lib.kss_oracle_go_log.argtypes = [C.c_double]
+        _lib.kss_oracle_go_log.restype = C.c_double
+        _lib.kss_oracle_max_threads.restype = C.c_int
+    return _lib
+
+
+class Results:
+    """Per-pod result arrays (numpy) for n pods x N nodes."""
+
+    def __init__(self, n_pods, n_nodes):
+        N = max(n_nodes, 1)
+        self.fail_plugin = np.zeros((n_pods, N), dtype=np.uint8)
+        self.fail_detail = np.zeros((n_pods, N), dtype=np.uint16)
+        self.raw = np.zeros((n_pods, abi.KSS_NSCORE, N), dtype=np.int64)
+        self.norm = np.zeros((n_pods, abi.KSS_NSCORE, N), dtype=np.int64)
+        self.total = np.zeros((n_pods, N), dtype=np.int64)
+        self.structs = (abi.PodResult * max(n_pods, 1))()
+        for i in range(n_pods):
+            s = self.structs[i]
+            s.fail_plugin = self.fail_plugin[i].ctypes.data_as(C.POINTER(C.c_uint8))
+            s.fail_detail = self.fail_detail[i].ctypes.data_as(C.POINTER(C.c_uint16))
+            s.raw = self.raw[i].ctypes.data_as(C.POINTER(C.c_int64))
+            s.norm = self.norm[i].ctypes.data_as(C.POINTER(C.c_int64))
+            s.total = self.total[i].ctypes.data_as(C.POINTER(C.c_int64))
+
+    def meta(self, i):
+        s = self.structs[i]
+        return dict(n_feasible=s.n_feasible, chosen=s.chosen, best_total=s.best_total, scored=s.scored,
+                    status=s.status)
+
+
+def schedule(profile, cluster_struct, podset_struct, n_pods, n_nodes, threads=1, record=True, n_classes=0,
+             n_terms=0):
+    """Run the C oracle sequentially; returns (chosen, Results|None, final_state dict)."""
+    L = lib()
+    chosen = np.full(max(n_pods, 1), -2, dtype=np.int32)
+    res = Results(n_pods, n_nodes) if record else None
+    N = max(n_nodes, 1)
+    st = dict(requested=np.zeros((abi.KSS_NRES, N), np.int64), nonzero=np.zeros((2, N), np.int64),
+              pod_count=np.zeros(N, np.int32), class_count=np.zeros((max(n_classes, 1), N), np.int32),
+              term_count=np.zeros((max(n_terms, 1), N), np.int32))
+    P = C.POINTER
+    rc = L.kss_oracle_schedule(C.byref(profile), C.byref(cluster_struct), C.byref(podset_struct), n_pods,
+                               chosen.ctypes.data_as(P(C.c_int32)), res.structs if res else None, threads,
+                               st["requested"].ctypes.data_as(P(C.c_int64)), st["nonzero"].ctypes.data_as(P(C.c_int64)),
+                               st["pod_count"].ctypes.data_as(P(C.c_int32)),
+                               st["class_count"].ctypes.data_as(P(C.c_int32)),
+                               st["term_count"].ctypes.data_as(P(C.c_int32)))
+    assert rc == 0, f"oracle rc={rc}"
+    return chosen[:n_pods], res, st
