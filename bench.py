@@ -1,0 +1,166 @@
+#!/usr/bin/env python3
+"""Benchmark: pod x node Filter+Score evaluations/s and pods scheduled/s (BASELINE.json metric).
+
+Workload (N=1 default): BASELINE config C2 — 5,000-node synthetic cluster, 10,000 pending
+pods, default plugin profile, percentageOfNodesToScore=100, scheduled sequentially on
+one MI355X (each pod sees the previous pods' bindings).  One "step" = the whole
+10,000-pod batch from the same initial snapshot (node state is reset on the device
+before each step; pod programs and the cluster are resident in HBM before timing).
+
+Multi-GPU (torchrun, one process per GPU): every rank schedules its own independent
+C2 cluster (a what-if scenario; seed + rank) — scenario sharding, no data-path
+collective, "weak" scaling.  Control-plane barrier/max uses gloo.
+
+Prints ONE JSON line on rank 0.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "kube-scheduler-simulator_amd"))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+
+# Algorithmic bytes per (pod, node) evaluation, SURVEY §8(d) / BASELINE.md §2:
+# default profile reads 92 B of node state and writes 17 B of verdict + raw scores.
+B_EVAL = {1: 109, 2: 109, 3: 129, 4: 109, 5: 109}
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+
+
+def cpu_baseline(config, n_nodes, n_pods, seconds, threads):
+    """The CPU oracle (plain-C restatement, OpenMP over nodes) on a bounded prefix of the
+    same workload: pods are scheduled sequentially until `seconds` of wall time pass."""
+    import numpy as np
+
+    import oracle_c
+    from kss import abi, native
+
+    s = native.Synth(config, 0, n_nodes, n_pods)
+    prof = abi.default_profile()
+    n = 16
+    t_used = 0.0
+    done = 0
+    while True:
+        t0 = time.perf_counter()
+        oracle_c.schedule(prof, s.cluster, s.pods, n, n_nodes, threads=threads, record=False,
+                          n_classes=s.cluster.n_classes, n_terms=s.cluster.n_terms)
+        dt = time.perf_counter() - t0
+        t_used, done = dt, n
+        if dt >= seconds or n >= n_pods:
+            break
+        n = min(n_pods, max(n * 2, int(n * seconds / max(dt, 1e-3) * 1.1)))
+    evals = done * n_nodes
+    return {"value": evals / t_used, "unit": "pod-node evals/s", "cores": threads, "kind": "port",
+            "sample": f"first {done} of {n_pods} pods of config C{config} ({n_nodes} nodes), sequential, "
+                      f"{t_used:.1f} s wall, oracle/kss_oracle.c OpenMP over nodes",
+            "pods_per_s": done / t_used}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--config", type=int, default=2)
+    ap.add_argument("--nodes", type=int, default=0)
+    ap.add_argument("--pods", type=int, default=0)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-cpu", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist  # control plane only (barrier / max of timings)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+
+    from kss import abi, native
+    from kss.synth import DEFAULT_SIZES, SEED_BASE
+
+    cfg = args.config
+    n_nodes = args.nodes or DEFAULT_SIZES[cfg][0]
+    n_pods = args.pods or DEFAULT_SIZES[cfg][1]
+    seed = SEED_BASE + cfg + 7919 * rank  # rank 0 = the canonical C2 cluster
+    s = native.Synth(cfg, seed, n_nodes, n_pods)
+    prof = abi.default_profile()
+    ctx = native.Context(prof, device=local)
+    ctx.load(s.cluster)
+    ctx.stage(s.pods)
+    import numpy as np
+    chosen = np.zeros(n_pods, np.int32)
+
+    def step():
+        ctx.reset()
+        ctx.run_staged(n_pods, out=chosen)
+        return ctx.last_timing()[0]
+
+    for _ in range(args.warmup):
+        step()
+    if dist:
+        dist.barrier()
+    t0 = time.perf_counter()
+    kern_ms = []
+    for _ in range(args.steps):
+        kern_ms.append(step())
+    t1 = time.perf_counter()
+    if dist:
+        dist.barrier()
+    elapsed = t1 - t0
+    scheduled = int((chosen >= 0).sum())
+    if dist:
+        import torch
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        sc = torch.tensor([scheduled], dtype=torch.float64)
+        dist.all_reduce(sc, op=dist.ReduceOp.SUM)
+        scheduled_total = int(sc.item())
+    else:
+        scheduled_total = scheduled
+
+    evals = world * n_pods * n_nodes * args.steps
+    value = evals / elapsed
+    pods_per_s = scheduled_total * args.steps / elapsed
+    kern_avg_s = sum(kern_ms) / len(kern_ms) / 1e3
+    achieved = B_EVAL[cfg] * n_pods * n_nodes / kern_avg_s / 1e9
+
+    if rank == 0:
+        cpu = None
+        if not args.no_cpu and world == 1:
+            threads = min(16, os.cpu_count() or 1)
+            cpu = cpu_baseline(cfg, n_nodes, n_pods, args.cpu_seconds, threads)
+        out = {
+            "metric": "pod x node filter+score evals/sec (pods scheduled/sec in extra)",
+            "value": value,
+            "unit": "evals/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "int64/f64",
+            "data": "synthetic (SplitMix64 seed 0x5EED0000+config[+7919*rank])",
+            "config": {"workload": f"C{cfg}: {n_nodes} nodes x {n_pods} pods, default profile, sequential, pct=100",
+                       "nodes": n_nodes, "pods": n_pods, "parallelism": f"scenario x{world}"},
+            "pods_per_s": pods_per_s,
+            "pods_scheduled_per_step": scheduled,
+            "kernel_ms_per_step": kern_avg_s * 1e3,
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "kernel": "k_schedule", "bytes_per_eval": B_EVAL[cfg]},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

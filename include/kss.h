@@ -349,6 +349,15 @@ int kss_rollback(kss_ctx* ctx, const kss_podset* ps, int32_t pod_index, int32_t 
 int kss_schedule_batch(kss_ctx* ctx, const kss_podset* ps, int32_t n, uint32_t flags, int32_t* chosen_out);
 int kss_fetch_record(kss_ctx* ctx, int32_t pod_index, kss_pod_result* out);
 
+/* Resident-input variant of kss_schedule_batch: kss_stage_pods validates and copies
+ * the pod programs to HBM once; kss_run_staged schedules the first n staged pods
+ * (no host->device traffic).  kss_reset_node_state restores every mutable column
+ * (requested, nonzero, pod counts, class/term counts) to the snapshot given to
+ * kss_load_cluster, on the device (what-if replays, simulator/reset). */
+int kss_stage_pods(kss_ctx* ctx, const kss_podset* ps);
+int kss_run_staged(kss_ctx* ctx, int32_t n, uint32_t flags, int32_t* chosen_out);
+int kss_reset_node_state(kss_ctx* ctx);
+
 /* many independent clusters (what-if scenarios, KEP-184): clusters[s] with podsets[s];
  * one workgroup per scenario, no inter-scenario communication. chosen_out is [sum n_pods]. */
 int kss_schedule_scenarios(int32_t device, const kss_profile* prof, int32_t n_scen, const kss_cluster* clusters,
@@ -371,6 +380,11 @@ int kss_set_names(kss_ctx* ctx, const kss_names* names);
  * in the timed scheduling path. */
 int kss_format_annotations(kss_ctx* ctx, const kss_pod_result* res, int32_t n_nodes, char* buf, size_t cap,
                            size_t* need);
+/* Context-free variant (host only): names and profile passed explicitly. */
+int kss_format_annotations_ex(const kss_names* names, const kss_profile* prof, const kss_pod_result* res,
+                              int32_t n_nodes, int32_t n_taints, int32_t n_scalar, char* buf, size_t cap, size_t* need);
+/* sizeof() of every ABI struct, in header order; returns the count written (ABI self-check) */
+int kss_abi_sizes(int32_t* out, int32_t n);
 
 /* ---- synthetic clusters (SplitMix64, seed 0x5EED0000 + config) */
 typedef struct kss_synth {

@@ -1,0 +1,270 @@
+// kss_eval.cuh — per-(pod,node) predicates and raw scores, device side (gfx950).
+//
+// Each function restates one upstream v1.26.2 plugin step (cited) over the
+// interned struct-of-arrays of include/kss.h.  Everything here is integer or
+// IEEE double arithmetic compiled with -ffp-contract=off, so results are
+// bit-identical to the reference operation order.  One lane evaluates one node;
+// pod programs are wave-uniform (read through the scalar cache).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/kss.h"
+
+namespace kss {
+
+// Device view of a loaded cluster.  Row r of a [attr][N] matrix starts at r*N.
+struct DevCluster {
+  int32_t N;
+  int32_t n_scalar;
+  int32_t n_keys;
+  int32_t n_classes;
+  int32_t n_terms;
+  int32_t node_base;
+  int32_t class_cap;
+  int32_t term_cap;
+  const int64_t* alloc;
+  int64_t* requested;
+  int64_t* nonzero;
+  const int32_t* allowed_pods;
+  int32_t* pod_count;
+  const uint32_t* node_flags;
+  const uint64_t* taint_hard;
+  const uint64_t* taint_soft;
+  const uint8_t* taint_order;
+  const int32_t* label_value;
+  const int32_t* key_base;
+  const int32_t* key_card;
+  const uint32_t* key_flags;
+  const int32_t* key_empty;
+  const int64_t* value_int;
+  const uint8_t* value_is_int;
+  int32_t* class_count;
+  int32_t* term_count;
+  const double* log_table;  // go_log(k + 2), k in [0, N]
+};
+
+struct DevPods {
+  const kss_pod* pods;
+  const kss_req* reqs;
+  const kss_term* terms;
+  const kss_spread* spreads;
+  const kss_ipa* ipa;
+  const int32_t* ints;
+};
+
+__device__ __forceinline__ int32_t label_of(const DevCluster& c, int key, int n) {
+  return c.label_value[(size_t)key * (size_t)c.N + (size_t)n];
+}
+
+// labels.Requirement.Matches over value ids (apimachinery labels/selector.go) and the
+// metadata.name field selector (component-helpers nodeaffinity).
+__device__ __forceinline__ bool req_match(const DevCluster& c, const DevPods& P, const kss_req& r, int n) {
+  const int op = r.op;
+  const int64_t g = (int64_t)c.node_base + n;
+  if (op == KSS_OP_FALSE) return false;
+  if (op == KSS_OP_TRUE) return true;
+  if (op == KSS_OP_NAME_IN) return r.ival >= 0 && g == r.ival;
+  if (op == KSS_OP_NAME_NOTIN) return !(r.ival >= 0 && g == r.ival);
+  const int32_t v = label_of(c, r.key, n);
+  switch (op) {
+    case KSS_OP_MASK:
+      if (v < 0) return (r.mask >> 63) & 1ull;
+      return v < 63 ? ((r.mask >> v) & 1ull) : false;
+    case KSS_OP_IN: {
+      if (v < 0) return false;
+      for (int i = 0; i < r.list_len; i++)
+        if (P.ints[r.list_off + i] == v) return true;
+      return false;
+    }
+    case KSS_OP_NOTIN: {
+      if (v < 0) return true;
+      for (int i = 0; i < r.list_len; i++)
+        if (P.ints[r.list_off + i] == v) return false;
+      return true;
+    }
+    case KSS_OP_EXISTS:
+      return v >= 0;
+    case KSS_OP_DNE:
+      return v < 0;
+    case KSS_OP_GT:
+    case KSS_OP_LT: {
+      if (v < 0) return false;
+      const int32_t gi = c.key_base[r.key] + v;
+      if (!c.value_is_int[gi]) return false;
+      const int64_t x = c.value_int[gi];
+      return op == KSS_OP_GT ? x > r.ival : x < r.ival;
+    }
+    default:
+      return false;
+  }
+}
+
+__device__ __forceinline__ bool term_match(const DevCluster& c, const DevPods& P, const kss_term& t, int n) {
+  for (int i = 0; i < t.req_len; i++)
+    if (!req_match(c, P, P.reqs[t.req_off + i], n)) return false;
+  return true;
+}
+
+// nodeaffinity.RequiredNodeAffinity.Match: nodeSelector AND (OR over terms)
+__device__ __forceinline__ bool required_affinity(const DevCluster& c, const DevPods& P, const kss_pod& p, int n) {
+  for (int i = 0; i < p.sel_len; i++)
+    if (!req_match(c, P, P.reqs[p.sel_off + i], n)) return false;
+  if (p.flags & KSS_POD_HAS_REQ_AFFINITY) {
+    for (int t = 0; t < p.aff_len; t++)
+      if (term_match(c, P, P.terms[p.aff_off + t], n)) return true;
+    return false;
+  }
+  return true;
+}
+
+// v1helper.FindMatchingUntoleratedTaint(node.Spec.Taints, tolerations, DoNotScheduleTaintsFilterFunc)
+__device__ __forceinline__ int first_untolerated(const DevCluster& c, const kss_pod& p, int n) {
+  const uint64_t untol = c.taint_hard[n] & ~p.tol_hard;
+  if (!untol) return -1;
+  const uint8_t* ord = c.taint_order + (size_t)n * KSS_TAINT_ORDER;
+#pragma unroll
+  for (int i = 0; i < KSS_TAINT_ORDER; i++) {
+    const int t = ord[i];
+    if (t == 0xFF) break;
+    if ((untol >> t) & 1ull) return t;
+  }
+  return 63 - __clzll(untol);
+}
+
+__device__ __forceinline__ int64_t sum_rows(const int32_t* mat, size_t N, const int32_t* rows, int len, int n) {
+  int64_t s = 0;
+  for (int i = 0; i < len; i++) s += mat[(size_t)rows[i] * N + (size_t)n];
+  return s;
+}
+
+// First-failing filter among NodeUnschedulable, NodeName, TaintToleration,
+// NodeAffinity, (NodePorts), NodeResourcesFit — the ones that need no per-pod
+// cluster-wide state.  Returns 0 when all of them pass.
+__device__ __forceinline__ int filter_local(const DevCluster& c, const DevPods& P, const kss_pod& p,
+                                            uint32_t enabled, int n, uint16_t* detail) {
+  // NodeUnschedulable.Filter
+  if ((enabled >> KSS_F_NODE_UNSCHEDULABLE) & 1u) {
+    if ((c.node_flags[n] & KSS_NODE_UNSCHEDULABLE) && !(p.flags & KSS_POD_TOL_UNSCHEDULABLE))
+      return KSS_F_NODE_UNSCHEDULABLE;
+  }
+  // NodeName.Fits
+  if ((enabled >> KSS_F_NODE_NAME) & 1u) {
+    if (p.node_name != -1 && (int64_t)p.node_name != (int64_t)c.node_base + n) return KSS_F_NODE_NAME;
+  }
+  // TaintToleration.Filter
+  if ((enabled >> KSS_F_TAINT_TOLERATION) & 1u) {
+    const int t = first_untolerated(c, p, n);
+    if (t >= 0) {
+      *detail = (uint16_t)t;
+      return KSS_F_TAINT_TOLERATION;
+    }
+  }
+  // NodeAffinity.Filter
+  if ((enabled >> KSS_F_NODE_AFFINITY) & 1u) {
+    if (!required_affinity(c, P, p, n)) return KSS_F_NODE_AFFINITY;
+  }
+  // NodeResourcesFit.Filter -> fitsRequest
+  if ((enabled >> KSS_F_NODE_RESOURCES_FIT) & 1u) {
+    const size_t N = (size_t)c.N;
+    uint32_t bits = 0;
+    if ((int64_t)c.pod_count[n] + 1 > (int64_t)c.allowed_pods[n]) bits |= KSS_FIT_TOO_MANY_PODS;
+    const int nr = 3 + c.n_scalar;
+    bool all_zero = true;
+    for (int r = 0; r < nr; r++) all_zero &= (p.fit_request[r] == 0);
+    if (!all_zero) {
+      for (int r = 0; r < nr; r++) {
+        const int64_t req = p.fit_request[r];
+        if (r >= KSS_RES_SCALAR0 && req == 0) continue;
+        const int64_t freev = c.alloc[(size_t)r * N + n] - c.requested[(size_t)r * N + n];
+        if (req > freev) bits |= 1u << (r + 1);
+      }
+    }
+    if (bits) {
+      *detail = (uint16_t)bits;
+      return KSS_F_NODE_RESOURCES_FIT;
+    }
+  }
+  return 0;
+}
+
+// leastRequestedScore / mostRequestedScore
+__device__ __forceinline__ int64_t alloc_score(int strategy, int64_t requested, int64_t capacity) {
+  if (capacity == 0) return 0;
+  if (strategy == KSS_FIT_MOST_ALLOCATED) {
+    if (requested > capacity) requested = capacity;
+    return (requested * 100) / capacity;
+  }
+  if (requested > capacity) return 0;
+  return ((capacity - requested) * 100) / capacity;
+}
+
+// NodeResourcesFit.Score (resourceAllocationScorer.score, useRequested=false)
+__device__ __forceinline__ int64_t fit_score(const DevCluster& c, const kss_profile& prof, const kss_pod& p, int n) {
+  const size_t N = (size_t)c.N;
+  int64_t node_score = 0, weight_sum = 0;
+  for (int i = 0; i < prof.fit_n; i++) {
+    const int r = prof.fit_res[i];
+    const int64_t preq = p.score_req_nz[r];
+    if (r >= KSS_RES_SCALAR0 && preq == 0) continue;
+    const int64_t alloc = c.alloc[(size_t)r * N + n];
+    const int64_t base = (r <= KSS_RES_MEMORY) ? c.nonzero[(size_t)r * N + n] : c.requested[(size_t)r * N + n];
+    if (alloc == 0) continue;
+    node_score += alloc_score(prof.fit_strategy, base + preq, alloc) * prof.fit_weight[i];
+    weight_sum += prof.fit_weight[i];
+  }
+  if (weight_sum == 0) return 0;
+  return node_score / weight_sum;
+}
+
+// NodeResourcesBalancedAllocation.Score (balancedResourceScorer, useRequested=true)
+__device__ __forceinline__ int64_t ba_score(const DevCluster& c, const kss_profile& prof, const kss_pod& p, int n) {
+  const size_t N = (size_t)c.N;
+  double fr[4];
+  int nf = 0;
+  double total = 0.0;
+  for (int i = 0; i < prof.ba_n; i++) {
+    const int r = prof.ba_res[i];
+    const int64_t preq = p.score_req[r];
+    if (r >= KSS_RES_SCALAR0 && preq == 0) continue;
+    const int64_t alloc = c.alloc[(size_t)r * N + n];
+    const int64_t req = c.requested[(size_t)r * N + n] + preq;
+    if (alloc == 0) continue;
+    double f = (double)req / (double)alloc;
+    if (f > 1.0) f = 1.0;
+    total += f;
+    fr[nf++] = f;
+  }
+  double sd = 0.0;
+  if (nf == 2) {
+    sd = fabs((fr[0] - fr[1]) / 2.0);
+  } else if (nf > 2) {
+    const double mean = total / (double)nf;
+    double sum = 0.0;
+    for (int i = 0; i < nf; i++) {
+      const double d = fr[i] - mean;
+      const double sq = d * d;
+      sum = sum + sq;
+    }
+    sd = sqrt(sum / (double)nf);
+  }
+  const double s = (1.0 - sd) * 100.0;
+  return (int64_t)s;
+}
+
+// TaintToleration.Score: countIntolerableTaintsPreferNoSchedule
+__device__ __forceinline__ int64_t tt_score(const DevCluster& c, const kss_pod& p, int n) {
+  return (int64_t)__popcll(c.taint_soft[n] & ~p.tol_soft);
+}
+
+// NodeAffinity.Score: PreferredSchedulingTerms.Score
+__device__ __forceinline__ int64_t na_score(const DevCluster& c, const DevPods& P, const kss_pod& p, int n) {
+  int64_t s = 0;
+  for (int t = 0; t < p.pref_len; t++) {
+    const kss_term& term = P.terms[p.pref_off + t];
+    if (term_match(c, P, term, n)) s += term.weight;
+  }
+  return s;
+}
+
+}  // namespace kss

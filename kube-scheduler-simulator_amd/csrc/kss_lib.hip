@@ -1,0 +1,818 @@
+// kss_lib.hip — C ABI of libkss.so (include/kss.h): device context, snapshot upload,
+// and the launches of the gfx950 scheduling kernels.
+//
+// Kernel map:
+//   k_schedule   one workgroup per cluster; sequential pods; every phase of the
+//                scheduling cycle in the workgroup (kss_sched.cuh).  Used for the
+//                sequential batch (kss_schedule_batch), the drop-in per-pod call
+//                (kss_eval_pod, no commit) and the what-if scenario sweep
+//                (kss_schedule_scenarios, grid = #scenarios).
+//   k_commit     one lane: AssumePod / ForgetPod delta on one node row.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "kss_host.h"
+#include "kss_sched.cuh"
+
+using namespace kss;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                                        \
+  do {                                                                                       \
+    hipError_t _e = (expr);                                                                  \
+    if (_e != hipSuccess) return fail(KSS_E_DEVICE, std::string(#expr) + ": " + hipGetErrorString(_e)); \
+  } while (0)
+
+__host__ __device__ inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+// per-pod output slot layout (record format), N nodes
+struct SlotLayout {
+  size_t fail, detail, raw, norm, total, bytes;
+  __host__ __device__ explicit SlotLayout(size_t N) {
+    fail = 0;
+    detail = align_up(N, 256);
+    raw = align_up(detail + 2 * N, 256);
+    norm = raw + 8 * KSS_NSCORE * N;
+    total = norm + 8 * KSS_NSCORE * N;
+    bytes = align_up(total + 8 * N, 256);
+  }
+};
+
+// one workgroup's job
+struct DevJob {
+  DevCluster c;
+  DevPods P;
+  int32_t n_pods;
+  int32_t commit;     // apply AssumePod after each pod
+  int32_t keep_norm;  // write norm/total into the slot(s)
+  int32_t record;     // one slot per pod (else slot 0 reused)
+  uint8_t* slots;
+  size_t slot_bytes;
+  int32_t* chosen;
+  PodMeta* meta;
+};
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// kernels
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(1024) void k_schedule(const DevJob* __restrict__ jobs, kss_profile prof) {
+  __shared__ Shared sh;
+  const DevJob& job = jobs[blockIdx.x];
+  const DevCluster& c = job.c;
+  const size_t N = (size_t)c.N;
+  const SlotLayout L(N);
+  for (int pi = 0; pi < job.n_pods; pi++) {
+    uint8_t* base = job.slots + (job.record ? (size_t)pi * job.slot_bytes : 0);
+    Slot s;
+    s.fail = base + L.fail;
+    s.detail = (uint16_t*)(base + L.detail);
+    s.raw = (int64_t*)(base + L.raw);
+    s.norm = (int64_t*)(base + L.norm);
+    s.total = (int64_t*)(base + L.total);
+    PodMeta m;
+    schedule_pod(c, job.P, prof, pi, sh, s, m, job.keep_norm != 0);
+    if (threadIdx.x == 0) {
+      if (job.chosen) job.chosen[pi] = m.chosen;
+      if (job.meta) job.meta[pi] = m;
+      if (job.commit && m.chosen >= 0) commit_pod(c, job.P, job.P.pods[pi], m.chosen - c.node_base, 1);
+    }
+    __syncthreads();
+  }
+}
+
+__global__ void k_commit(DevCluster c, DevPods P, int pi, int local, int sign) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) commit_pod(c, P, P.pods[pi], local, sign);
+}
+
+// ---------------------------------------------------------------------------
+// context
+// ---------------------------------------------------------------------------
+struct DevBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  int ensure(size_t bytes) {
+    if (bytes <= cap) return 0;
+    if (p) hipFree(p);
+    p = nullptr;
+    cap = 0;
+    size_t nb = std::max(bytes, (size_t)4096);
+    if (hipMalloc(&p, nb) != hipSuccess) return fail(KSS_E_NOMEM, "hipMalloc failed");
+    cap = nb;
+    return 0;
+  }
+  void release() {
+    if (p) hipFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+};
+
+struct kss_ctx {
+  kss_config cfg{};
+  kss_profile prof{};
+  hipStream_t stream = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  std::mutex mu;  // rollback may arrive from the binding goroutine
+  // cluster
+  bool loaded = false;
+  kss_cluster host{};  // sizes only (pointers not retained)
+  DevCluster dc{};
+  DevBuf cluster_buf;
+  DevBuf pristine_buf;  // load-time copy of the mutable columns (kss_reset_node_state)
+  size_t mut_bytes[5] = {0, 0, 0, 0, 0};
+  size_t pristine_off[5] = {0, 0, 0, 0, 0};
+  // pods
+  DevBuf pod_buf;      // staged pod programs (kss_stage_pods / kss_schedule_batch)
+  DevPods dp{};
+  int staged_n = -1;   // pods staged in pod_buf (-1: none)
+  DevBuf tmp_pod_buf;  // eval / commit / rollback uploads (never clobber the staged batch)
+  DevPods tdp{};
+  // outputs
+  DevBuf slot_buf, meta_buf, chosen_buf, job_buf;
+  size_t slot_bytes = 0;
+  int recorded = 0;
+  std::vector<PodMeta> meta_host;
+  double last_ms = 0;
+  int last_launches = 0;
+  kss_host_names names;
+};
+
+namespace {
+
+// Copy a host podset into a device buffer; fills dp with device pointers.
+int upload_podset(hipStream_t st, DevBuf& buf, const kss_podset* ps, DevPods& dp) {
+  const size_t sz_pods = sizeof(kss_pod) * (size_t)std::max(ps->n_pods, 1);
+  const size_t sz_reqs = sizeof(kss_req) * (size_t)std::max(ps->n_reqs, 1);
+  const size_t sz_terms = sizeof(kss_term) * (size_t)std::max(ps->n_terms, 1);
+  const size_t sz_spr = sizeof(kss_spread) * (size_t)std::max(ps->n_spreads, 1);
+  const size_t sz_ipa = sizeof(kss_ipa) * (size_t)std::max(ps->n_ipa, 1);
+  const size_t sz_ints = sizeof(int32_t) * (size_t)std::max(ps->n_ints, 1);
+  size_t o_pods = 0, o_reqs = align_up(o_pods + sz_pods, 256), o_terms = align_up(o_reqs + sz_reqs, 256),
+         o_spr = align_up(o_terms + sz_terms, 256), o_ipa = align_up(o_spr + sz_spr, 256),
+         o_ints = align_up(o_ipa + sz_ipa, 256), total = align_up(o_ints + sz_ints, 256);
+  int rc = buf.ensure(total);
+  if (rc) return rc;
+  char* b = (char*)buf.p;
+  if (ps->n_pods) HIP_TRY(hipMemcpyAsync(b + o_pods, ps->pods, sizeof(kss_pod) * ps->n_pods, hipMemcpyHostToDevice, st));
+  if (ps->n_reqs) HIP_TRY(hipMemcpyAsync(b + o_reqs, ps->reqs, sizeof(kss_req) * ps->n_reqs, hipMemcpyHostToDevice, st));
+  if (ps->n_terms) HIP_TRY(hipMemcpyAsync(b + o_terms, ps->terms, sizeof(kss_term) * ps->n_terms, hipMemcpyHostToDevice, st));
+  if (ps->n_spreads) HIP_TRY(hipMemcpyAsync(b + o_spr, ps->spreads, sizeof(kss_spread) * ps->n_spreads, hipMemcpyHostToDevice, st));
+  if (ps->n_ipa) HIP_TRY(hipMemcpyAsync(b + o_ipa, ps->ipa, sizeof(kss_ipa) * ps->n_ipa, hipMemcpyHostToDevice, st));
+  if (ps->n_ints) HIP_TRY(hipMemcpyAsync(b + o_ints, ps->ints, sizeof(int32_t) * ps->n_ints, hipMemcpyHostToDevice, st));
+  dp.pods = (const kss_pod*)(b + o_pods);
+  dp.reqs = (const kss_req*)(b + o_reqs);
+  dp.terms = (const kss_term*)(b + o_terms);
+  dp.spreads = (const kss_spread*)(b + o_spr);
+  dp.ipa = (const kss_ipa*)(b + o_ipa);
+  dp.ints = (const int32_t*)(b + o_ints);
+  return 0;
+}
+
+// Validate podset references against the cluster shape (a malformed program must
+// never reach the kernel: out-of-range ids would fault the device).
+int validate(const kss_cluster* cl, const kss_podset* ps, int n) {
+  if (n < 0 || n > ps->n_pods) return fail(KSS_E_INVAL, "pod count out of range");
+  auto in = [](int64_t off, int64_t len, int64_t cap) { return off >= 0 && len >= 0 && off + len <= cap; };
+  for (int i = 0; i < ps->n_reqs; i++) {
+    const kss_req& r = ps->reqs[i];
+    const bool keyed = r.op >= KSS_OP_MASK && r.op <= KSS_OP_LT;
+    if (r.op < KSS_OP_FALSE || r.op > KSS_OP_NAME_NOTIN) return fail(KSS_E_INVAL, "bad requirement op");
+    if (keyed && (r.key < 0 || r.key >= cl->n_label_keys)) return fail(KSS_E_INVAL, "requirement key out of range");
+    if ((r.op == KSS_OP_IN || r.op == KSS_OP_NOTIN) && !in(r.list_off, r.list_len, ps->n_ints))
+      return fail(KSS_E_INVAL, "requirement list out of range");
+  }
+  for (int i = 0; i < ps->n_terms; i++)
+    if (!in(ps->terms[i].req_off, ps->terms[i].req_len, ps->n_reqs)) return fail(KSS_E_INVAL, "term out of range");
+  for (int i = 0; i < ps->n_spreads; i++) {
+    const kss_spread& s = ps->spreads[i];
+    if (s.key < 0 || s.key >= cl->n_label_keys) return fail(KSS_E_INVAL, "spread key out of range");
+    if (!in(s.cls_off, s.cls_len, ps->n_ints)) return fail(KSS_E_INVAL, "spread class list out of range");
+    for (int j = 0; j < s.cls_len; j++)
+      if (ps->ints[s.cls_off + j] < 0 || ps->ints[s.cls_off + j] >= cl->n_classes) return fail(KSS_E_INVAL, "class id out of range");
+    if (!(cl->key_flags[s.key] & (KSS_KEY_UNIQUE | KSS_KEY_HOSTNAME)) && cl->key_card[s.key] + 1 > KSS_MAX_BINS)
+      return fail(KSS_E_UNSUPPORTED, "non-unique topology key with more than KSS_MAX_BINS domains");
+  }
+  for (int i = 0; i < ps->n_ipa; i++) {
+    const kss_ipa& e = ps->ipa[i];
+    if (e.key < 0 || e.key >= cl->n_label_keys) return fail(KSS_E_INVAL, "ipa key out of range");
+    if (!in(e.row_off, e.row_len, ps->n_ints)) return fail(KSS_E_INVAL, "ipa rows out of range");
+    const bool terms = e.kind == KSS_IPA_EXISTING_ANTI || e.kind == KSS_IPA_SCORE_TERM;
+    const int cap = terms ? cl->n_terms : cl->n_classes;
+    for (int j = 0; j < e.row_len; j++)
+      if (ps->ints[e.row_off + j] < 0 || ps->ints[e.row_off + j] >= cap) return fail(KSS_E_INVAL, "ipa row id out of range");
+    if (!(cl->key_flags[e.key] & KSS_KEY_UNIQUE) && cl->key_card[e.key] + 1 > KSS_MAX_BINS)
+      return fail(KSS_E_UNSUPPORTED, "non-unique topology key with more than KSS_MAX_BINS domains");
+  }
+  for (int i = 0; i < n; i++) {
+    const kss_pod& p = ps->pods[i];
+    if (!in(p.sel_off, p.sel_len, ps->n_reqs) || !in(p.aff_off, p.aff_len, ps->n_terms) ||
+        !in(p.pref_off, p.pref_len, ps->n_terms) || !in(p.spread_off, (int64_t)p.n_hard + p.n_soft, ps->n_spreads) ||
+        !in(p.ipa_off, p.ipa_len, ps->n_ipa) || !in(p.own_terms_off, p.own_terms_len, ps->n_ints))
+      return fail(KSS_E_INVAL, "pod program out of range");
+    if (p.names_len >= 0 && !in(p.names_off, p.names_len, ps->n_ints)) return fail(KSS_E_INVAL, "pod names out of range");
+    if (p.cls >= cl->n_classes) return fail(KSS_E_INVAL, "pod class out of range");
+    for (int j = 0; j < p.own_terms_len; j++)
+      if (ps->ints[p.own_terms_off + j] < 0 || ps->ints[p.own_terms_off + j] >= cl->n_terms)
+        return fail(KSS_E_INVAL, "own term id out of range");
+    if (p.n_hard > MAXH || p.n_soft > MAXS) return fail(KSS_E_UNSUPPORTED, "too many spread constraints for the device path");
+  }
+  return 0;
+}
+
+struct ClusterLayout {
+  size_t o_alloc, o_req, o_nz, o_allowed, o_podc, o_flags, o_th, o_ts, o_to, o_lv, o_kb, o_kc, o_kf, o_ke, o_vi, o_vii,
+      o_cc, o_tc, o_log, total;
+  ClusterLayout(const kss_cluster* cl, int class_cap, int term_cap) {
+    const size_t N = (size_t)cl->n_nodes;
+    size_t o = 0;
+    auto take = [&](size_t bytes) {
+      size_t r = o;
+      o = align_up(o + std::max(bytes, (size_t)8), 256);
+      return r;
+    };
+    o_alloc = take(8 * KSS_NRES * N);
+    o_req = take(8 * KSS_NRES * N);
+    o_nz = take(8 * 2 * N);
+    o_allowed = take(4 * N);
+    o_podc = take(4 * N);
+    o_flags = take(4 * N);
+    o_th = take(8 * N);
+    o_ts = take(8 * N);
+    o_to = take((size_t)KSS_TAINT_ORDER * N);
+    o_lv = take(4 * (size_t)cl->n_label_keys * N);
+    o_kb = take(4 * (size_t)cl->n_label_keys);
+    o_kc = take(4 * (size_t)cl->n_label_keys);
+    o_kf = take(4 * (size_t)cl->n_label_keys);
+    o_ke = take(4 * (size_t)cl->n_label_keys);
+    o_vi = take(8 * (size_t)cl->n_label_values);
+    o_vii = take((size_t)cl->n_label_values);
+    o_cc = take(4 * (size_t)class_cap * N);
+    o_tc = take(4 * (size_t)term_cap * N);
+    o_log = take(8 * (N + 3));
+    total = o;
+  }
+};
+
+int fill_cluster(hipStream_t st, const kss_cluster* cl, int class_cap, int term_cap, char* b, const ClusterLayout& L,
+                 DevCluster& dc, std::vector<double>& logtab) {
+  const size_t N = (size_t)cl->n_nodes;
+  auto cp = [&](size_t off, const void* src, size_t bytes) -> int {
+    if (bytes && src) HIP_TRY(hipMemcpyAsync(b + off, src, bytes, hipMemcpyHostToDevice, st));
+    return 0;
+  };
+  int rc = 0;
+  rc |= cp(L.o_alloc, cl->alloc, 8 * KSS_NRES * N);
+  rc |= cp(L.o_req, cl->requested, 8 * KSS_NRES * N);
+  rc |= cp(L.o_nz, cl->nonzero, 8 * 2 * N);
+  rc |= cp(L.o_allowed, cl->allowed_pods, 4 * N);
+  rc |= cp(L.o_podc, cl->pod_count, 4 * N);
+  rc |= cp(L.o_flags, cl->node_flags, 4 * N);
+  rc |= cp(L.o_th, cl->taint_hard, 8 * N);
+  rc |= cp(L.o_ts, cl->taint_soft, 8 * N);
+  rc |= cp(L.o_to, cl->taint_order, (size_t)KSS_TAINT_ORDER * N);
+  rc |= cp(L.o_lv, cl->label_value, 4 * (size_t)cl->n_label_keys * N);
+  rc |= cp(L.o_kb, cl->key_base, 4 * (size_t)cl->n_label_keys);
+  rc |= cp(L.o_kc, cl->key_card, 4 * (size_t)cl->n_label_keys);
+  rc |= cp(L.o_kf, cl->key_flags, 4 * (size_t)cl->n_label_keys);
+  rc |= cp(L.o_ke, cl->key_empty, 4 * (size_t)cl->n_label_keys);
+  rc |= cp(L.o_vi, cl->value_int, 8 * (size_t)cl->n_label_values);
+  rc |= cp(L.o_vii, cl->value_is_int, (size_t)cl->n_label_values);
+  if (class_cap) HIP_TRY(hipMemsetAsync(b + L.o_cc, 0, 4 * (size_t)class_cap * N, st));
+  if (term_cap) HIP_TRY(hipMemsetAsync(b + L.o_tc, 0, 4 * (size_t)term_cap * N, st));
+  rc |= cp(L.o_cc, cl->class_count, 4 * (size_t)cl->n_classes * N);
+  rc |= cp(L.o_tc, cl->term_count, 4 * (size_t)cl->n_terms * N);
+  logtab.resize(N + 3);
+  for (size_t k = 0; k < N + 3; k++) logtab[k] = kss_go_log((double)(k + 2));
+  rc |= cp(L.o_log, logtab.data(), 8 * (N + 3));
+  if (rc) return rc;
+  dc.N = cl->n_nodes;
+  dc.n_scalar = cl->n_scalar;
+  dc.n_keys = cl->n_label_keys;
+  dc.n_classes = cl->n_classes;
+  dc.n_terms = cl->n_terms;
+  dc.node_base = cl->node_base;
+  dc.class_cap = class_cap;
+  dc.term_cap = term_cap;
+  dc.alloc = (const int64_t*)(b + L.o_alloc);
+  dc.requested = (int64_t*)(b + L.o_req);
+  dc.nonzero = (int64_t*)(b + L.o_nz);
+  dc.allowed_pods = (const int32_t*)(b + L.o_allowed);
+  dc.pod_count = (int32_t*)(b + L.o_podc);
+  dc.node_flags = (const uint32_t*)(b + L.o_flags);
+  dc.taint_hard = (const uint64_t*)(b + L.o_th);
+  dc.taint_soft = (const uint64_t*)(b + L.o_ts);
+  dc.taint_order = (const uint8_t*)(b + L.o_to);
+  dc.label_value = (const int32_t*)(b + L.o_lv);
+  dc.key_base = (const int32_t*)(b + L.o_kb);
+  dc.key_card = (const int32_t*)(b + L.o_kc);
+  dc.key_flags = (const uint32_t*)(b + L.o_kf);
+  dc.key_empty = (const int32_t*)(b + L.o_ke);
+  dc.value_int = (const int64_t*)(b + L.o_vi);
+  dc.value_is_int = (const uint8_t*)(b + L.o_vii);
+  dc.class_count = (int32_t*)(b + L.o_cc);
+  dc.term_count = (int32_t*)(b + L.o_tc);
+  dc.log_table = (const double*)(b + L.o_log);
+  return 0;
+}
+
+int check_cluster(const kss_cluster* cl) {
+  if (!cl || cl->n_nodes < 0) return fail(KSS_E_INVAL, "null cluster");
+  if (cl->n_scalar < 0 || cl->n_scalar > KSS_MAX_SCALAR) return fail(KSS_E_INVAL, "n_scalar out of range");
+  if (cl->n_taints < 0 || cl->n_taints > KSS_MAX_TAINTS) return fail(KSS_E_INVAL, "n_taints out of range");
+  if (cl->n_nodes > 0 && (!cl->alloc || !cl->requested || !cl->nonzero || !cl->allowed_pods || !cl->pod_count ||
+                          !cl->node_flags || !cl->taint_hard || !cl->taint_soft || !cl->taint_order))
+    return fail(KSS_E_INVAL, "missing node column");
+  for (int k = 0; k < cl->n_label_keys; k++) {
+    if (cl->key_base[k] < 0 || cl->key_base[k] + cl->key_card[k] > cl->n_label_values)
+      return fail(KSS_E_INVAL, "key value table out of range");
+    if (cl->key_empty[k] < 0 || cl->key_empty[k] > cl->key_card[k]) return fail(KSS_E_INVAL, "key_empty out of range");
+  }
+  const size_t N = (size_t)cl->n_nodes;
+  for (size_t i = 0; i < (size_t)cl->n_label_keys * N; i++) {
+    const int k = (int)(i / (N ? N : 1));
+    if (cl->label_value[i] < -1 || cl->label_value[i] >= cl->key_card[k]) return fail(KSS_E_INVAL, "label value id out of range");
+  }
+  for (size_t i = 0; i < N * KSS_TAINT_ORDER; i++)
+    if (cl->taint_order[i] != 0xFF && cl->taint_order[i] >= cl->n_taints) return fail(KSS_E_INVAL, "taint id out of range");
+  return 0;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// C ABI
+// ---------------------------------------------------------------------------
+extern "C" {
+
+int kss_abi_version(void) { return KSS_ABI_VERSION; }
+const char* kss_last_error(void) { return g_err.c_str(); }
+
+int kss_abi_sizes(int32_t* out, int32_t n) {
+  const int32_t s[] = {(int32_t)sizeof(kss_cluster), (int32_t)sizeof(kss_req),     (int32_t)sizeof(kss_term),
+                       (int32_t)sizeof(kss_spread),  (int32_t)sizeof(kss_ipa),     (int32_t)sizeof(kss_pod),
+                       (int32_t)sizeof(kss_podset),  (int32_t)sizeof(kss_profile), (int32_t)sizeof(kss_pod_result),
+                       (int32_t)sizeof(kss_config),  (int32_t)sizeof(kss_names),   (int32_t)sizeof(kss_synth)};
+  const int32_t k = (int32_t)(sizeof(s) / sizeof(s[0]));
+  for (int i = 0; i < n && i < k; i++) out[i] = s[i];
+  return k;
+}
+
+kss_ctx* kss_create(const kss_config* cfg, const kss_profile* prof) {
+  if (!cfg || !prof) {
+    fail(KSS_E_INVAL, "null config/profile");
+    return nullptr;
+  }
+  if (prof->pct_nodes_to_score != 100 && prof->pct_nodes_to_score != 0) {
+    fail(KSS_E_UNSUPPORTED, "percentageOfNodesToScore must be 100 (SURVEY 8a a1)");
+    return nullptr;
+  }
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
+    fail(KSS_E_DEVICE, "no HIP device visible");
+    return nullptr;
+  }
+  if (cfg->device < 0 || cfg->device >= ndev) {
+    fail(KSS_E_INVAL, "device ordinal out of range");
+    return nullptr;
+  }
+  kss_ctx* ctx = new kss_ctx();
+  ctx->cfg = *cfg;
+  ctx->prof = *prof;
+  if (hipSetDevice(cfg->device) != hipSuccess || hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreate(&ctx->ev0) != hipSuccess || hipEventCreate(&ctx->ev1) != hipSuccess) {
+    fail(KSS_E_DEVICE, "stream/event creation failed");
+    delete ctx;
+    return nullptr;
+  }
+  return ctx;
+}
+
+void kss_destroy(kss_ctx* ctx) {
+  if (!ctx) return;
+  hipSetDevice(ctx->cfg.device);
+  if (ctx->stream) hipStreamSynchronize(ctx->stream);
+  ctx->cluster_buf.release();
+  ctx->pristine_buf.release();
+  ctx->pod_buf.release();
+  ctx->tmp_pod_buf.release();
+  ctx->slot_buf.release();
+  ctx->meta_buf.release();
+  ctx->chosen_buf.release();
+  ctx->job_buf.release();
+  if (ctx->ev0) hipEventDestroy(ctx->ev0);
+  if (ctx->ev1) hipEventDestroy(ctx->ev1);
+  if (ctx->stream) hipStreamDestroy(ctx->stream);
+  delete ctx;
+}
+
+int kss_load_cluster(kss_ctx* ctx, const kss_cluster* cl) {
+  if (!ctx) return fail(KSS_E_INVAL, "null ctx");
+  int rc = check_cluster(cl);
+  if (rc) return rc;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  HIP_TRY(hipSetDevice(ctx->cfg.device));
+  const int class_cap = std::max(cl->n_classes, ctx->cfg.class_capacity);
+  const int term_cap = std::max(cl->n_terms, ctx->cfg.term_capacity);
+  ClusterLayout L(cl, class_cap, term_cap);
+  rc = ctx->cluster_buf.ensure(L.total);
+  if (rc) return rc;
+  std::vector<double> logtab;
+  rc = fill_cluster(ctx->stream, cl, class_cap, term_cap, (char*)ctx->cluster_buf.p, L, ctx->dc, logtab);
+  if (rc) return rc;
+  // pristine copy of the mutable columns
+  const size_t N = (size_t)cl->n_nodes;
+  const size_t mb[5] = {8 * KSS_NRES * N, 8 * 2 * N, 4 * N, 4 * (size_t)class_cap * N, 4 * (size_t)term_cap * N};
+  size_t tot = 0;
+  for (int i = 0; i < 5; i++) {
+    ctx->mut_bytes[i] = mb[i];
+    ctx->pristine_off[i] = tot;
+    tot = align_up(tot + mb[i], 256);
+  }
+  rc = ctx->pristine_buf.ensure(tot);
+  if (rc) return rc;
+  void* src[5] = {ctx->dc.requested, ctx->dc.nonzero, ctx->dc.pod_count, ctx->dc.class_count, ctx->dc.term_count};
+  for (int i = 0; i < 5; i++)
+    if (mb[i])
+      HIP_TRY(hipMemcpyAsync((char*)ctx->pristine_buf.p + ctx->pristine_off[i], src[i], mb[i], hipMemcpyDeviceToDevice,
+                             ctx->stream));
+  HIP_TRY(hipStreamSynchronize(ctx->stream));
+  ctx->host = *cl;
+  ctx->loaded = true;
+  ctx->recorded = 0;
+  ctx->staged_n = -1;
+  return 0;
+}
+
+int kss_reset_node_state(kss_ctx* ctx) {
+  if (!ctx || !ctx->loaded) return fail(KSS_E_INVAL, "no cluster loaded");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  HIP_TRY(hipSetDevice(ctx->cfg.device));
+  void* dst[5] = {ctx->dc.requested, ctx->dc.nonzero, ctx->dc.pod_count, ctx->dc.class_count, ctx->dc.term_count};
+  for (int i = 0; i < 5; i++)
+    if (ctx->mut_bytes[i])
+      HIP_TRY(hipMemcpyAsync(dst[i], (char*)ctx->pristine_buf.p + ctx->pristine_off[i], ctx->mut_bytes[i],
+                             hipMemcpyDeviceToDevice, ctx->stream));
+  HIP_TRY(hipStreamSynchronize(ctx->stream));
+  return 0;
+}
+
+int kss_apply_node_delta(kss_ctx* ctx, const int32_t* idx, int32_t n, const int64_t* requested, const int64_t* nonzero,
+                         const int32_t* pod_count) {
+  if (!ctx || !ctx->loaded) return fail(KSS_E_INVAL, "no cluster loaded");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  HIP_TRY(hipSetDevice(ctx->cfg.device));
+  const size_t N = (size_t)ctx->dc.N;
+  for (int i = 0; i < n; i++) {
+    const int r0 = idx[i];
+    if (r0 < 0 || (size_t)r0 >= N) return fail(KSS_E_INVAL, "delta row out of range");
+    for (int r = 0; r < KSS_NRES; r++)
+      HIP_TRY(hipMemcpyAsync(ctx->dc.requested + (size_t)r * N + r0, requested + (size_t)i * KSS_NRES + r, 8,
+                             hipMemcpyHostToDevice, ctx->stream));
+    for (int r = 0; r < 2; r++)
+      HIP_TRY(hipMemcpyAsync(ctx->dc.nonzero + (size_t)r * N + r0, nonzero + (size_t)i * 2 + r, 8, hipMemcpyHostToDevice,
+                             ctx->stream));
+    HIP_TRY(hipMemcpyAsync(ctx->dc.pod_count + r0, pod_count + i, 4, hipMemcpyHostToDevice, ctx->stream));
+  }
+  HIP_TRY(hipStreamSynchronize(ctx->stream));
+  return 0;
+}
+
+int kss_read_node_state(kss_ctx* ctx, int64_t* requested, int64_t* nonzero, int32_t* pod_count, int32_t* class_count,
+                        int32_t* term_count) {
+  if (!ctx || !ctx->loaded) return fail(KSS_E_INVAL, "no cluster loaded");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  HIP_TRY(hipSetDevice(ctx->cfg.device));
+  const size_t N = (size_t)ctx->dc.N;
+  if (requested) HIP_TRY(hipMemcpyAsync(requested, ctx->dc.requested, 8 * KSS_NRES * N, hipMemcpyDeviceToHost, ctx->stream));
+  if (nonzero) HIP_TRY(hipMemcpyAsync(nonzero, ctx->dc.nonzero, 8 * 2 * N, hipMemcpyDeviceToHost, ctx->stream));
+  if (pod_count) HIP_TRY(hipMemcpyAsync(pod_count, ctx->dc.pod_count, 4 * N, hipMemcpyDeviceToHost, ctx->stream));
+  if (class_count && ctx->host.n_classes)
+    HIP_TRY(hipMemcpyAsync(class_count, ctx->dc.class_count, 4 * (size_t)ctx->host.n_classes * N, hipMemcpyDeviceToHost, ctx->stream));
+  if (term_count && ctx->host.n_terms)
+    HIP_TRY(hipMemcpyAsync(term_count, ctx->dc.term_count, 4 * (size_t)ctx->host.n_terms * N, hipMemcpyDeviceToHost, ctx->stream));
+  HIP_TRY(hipStreamSynchronize(ctx->stream));
+  return 0;
+}
+
+static int block_threads(int N) {
+  if (N <= 256) return 256;
+  if (N <= 512) return 512;
+  return 1024;
+}
+
+// run k_schedule on the loaded cluster for pods [0, n); results stay on the device
+static int run_single(kss_ctx* ctx, const DevPods& dp, int n, bool commit, bool record, bool keep_norm,
+                      int32_t* chosen_out) {
+  const size_t N = (size_t)ctx->dc.N;
+  const SlotLayout SL(N);
+  const int nslots = record ? std::max(n, 1) : 1;
+  int rc = ctx->slot_buf.ensure(SL.bytes * (size_t)nslots);
+  if (rc) return rc;
+  rc = ctx->meta_buf.ensure(sizeof(PodMeta) * (size_t)std::max(n, 1));
+  if (rc) return rc;
+  rc = ctx->chosen_buf.ensure(sizeof(int32_t) * (size_t)std::max(n, 1));
+  if (rc) return rc;
+  DevJob job{};
+  job.c = ctx->dc;
+  job.P = dp;
+  job.n_pods = n;
+  job.commit = commit ? 1 : 0;
+  job.keep_norm = keep_norm ? 1 : 0;
+  job.record = record ? 1 : 0;
+  job.slots = (uint8_t*)ctx->slot_buf.p;
+  job.slot_bytes = SL.bytes;
+  job.chosen = (int32_t*)ctx->chosen_buf.p;
+  job.meta = (PodMeta*)ctx->meta_buf.p;
+  rc = ctx->job_buf.ensure(sizeof(DevJob));
+  if (rc) return rc;
+  HIP_TRY(hipMemcpyAsync(ctx->job_buf.p, &job, sizeof(DevJob), hipMemcpyHostToDevice, ctx->stream));
+  HIP_TRY(hipEventRecord(ctx->ev0, ctx->stream));
+  hipLaunchKernelGGL(k_schedule, dim3(1), dim3(block_threads((int)N)), 0, ctx->stream, (const DevJob*)ctx->job_buf.p,
+                     ctx->prof);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipEventRecord(ctx->ev1, ctx->stream));
+  HIP_TRY(hipStreamSynchronize(ctx->stream));
+  float ms = 0;
+  HIP_TRY(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
+  ctx->last_ms = ms;
+  ctx->last_launches = 1;
+  ctx->meta_host.resize((size_t)std::max(n, 1));
+  HIP_TRY(hipMemcpy(ctx->meta_host.data(), ctx->meta_buf.p, sizeof(PodMeta) * (size_t)std::max(n, 1), hipMemcpyDeviceToHost));
+  if (chosen_out && n) HIP_TRY(hipMemcpy(chosen_out, ctx->chosen_buf.p, sizeof(int32_t) * n, hipMemcpyDeviceToHost));
+  ctx->recorded = record ? n : (n > 0 ? 1 : 0);
+  return 0;
+}
+
+static int copy_slot(kss_ctx* ctx, int slot, const PodMeta& m, kss_pod_result* out) {
+  const size_t N = (size_t)ctx->dc.N;
+  const SlotLayout SL(N);
+  const char* base = (const char*)ctx->slot_buf.p + (size_t)slot * SL.bytes;
+  if (out->fail_plugin) HIP_TRY(hipMemcpy(out->fail_plugin, base + SL.fail, N, hipMemcpyDeviceToHost));
+  if (out->fail_detail) HIP_TRY(hipMemcpy(out->fail_detail, base + SL.detail, 2 * N, hipMemcpyDeviceToHost));
+  if (out->raw) HIP_TRY(hipMemcpy(out->raw, base + SL.raw, 8 * KSS_NSCORE * N, hipMemcpyDeviceToHost));
+  if (out->norm) HIP_TRY(hipMemcpy(out->norm, base + SL.norm, 8 * KSS_NSCORE * N, hipMemcpyDeviceToHost));
+  if (out->total) HIP_TRY(hipMemcpy(out->total, base + SL.total, 8 * N, hipMemcpyDeviceToHost));
+  out->n_feasible = m.n_feasible;
+  out->chosen = m.chosen;
+  out->best_total = m.best_total;
+  out->scored = m.scored;
+  out->status = m.status;
+  if (m.status == 4) return fail(KSS_E_UNSUPPORTED, "pod program exceeds the device path's per-pod limits");
+  return 0;
+}
+
+int kss_eval_pod(kss_ctx* ctx, const kss_podset* ps, int32_t pod_index, kss_pod_result* out) {
+  if (!ctx || !ctx->loaded || !ps || !out) return fail(KSS_E_INVAL, "bad arguments");
+  if (pod_index < 0 || pod_index >= ps->n_pods) return fail(KSS_E_INVAL, "pod index out of range");
+  int rc = validate(&ctx->host, ps, ps->n_pods);
+  if (rc) return rc;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  HIP_TRY(hipSetDevice(ctx->cfg.device));
+  // evaluate exactly one pod: view the podset from pod_index
+  kss_podset one = *ps;
+  one.pods = ps->pods + pod_index;
+  one.n_pods = 1;
+  rc = upload_podset(ctx->stream, ctx->tmp_pod_buf, &one, ctx->tdp);
+  if (rc) return rc;
+  rc = run_single(ctx, ctx->tdp, 1, /*commit=*/false, /*record=*/false, /*keep_norm=*/true, nullptr);
+  if (rc) return rc;
+  return copy_slot(ctx, 0, ctx->meta_host[0], out);
+}
+
+int kss_commit(kss_ctx* ctx, const kss_podset* ps, int32_t pod_index, int32_t node) {
+  if (!ctx || !ctx->loaded || !ps) return fail(KSS_E_INVAL, "bad arguments");
+  if (pod_index < 0 || pod_index >= ps->n_pods) return fail(KSS_E_INVAL, "pod index out of range");
+  const int local = node - ctx->dc.node_base;
+  if (local < 0 || local >= ctx->dc.N) return fail(KSS_E_INVAL, "node out of range");
+  int rc = validate(&ctx->host, ps, ps->n_pods);
+  if (rc) return rc;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  HIP_TRY(hipSetDevice(ctx->cfg.device));
+  rc = upload_podset(ctx->stream, ctx->tmp_pod_buf, ps, ctx->tdp);
+  if (rc) return rc;
+  hipLaunchKernelGGL(k_commit, dim3(1), dim3(64), 0, ctx->stream, ctx->dc, ctx->tdp, pod_index, local, 1);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipStreamSynchronize(ctx->stream));
+  return 0;
+}
+
+int kss_rollback(kss_ctx* ctx, const kss_podset* ps, int32_t pod_index, int32_t node) {
+  if (!ctx || !ctx->loaded || !ps) return fail(KSS_E_INVAL, "bad arguments");
+  if (pod_index < 0 || pod_index >= ps->n_pods) return fail(KSS_E_INVAL, "pod index out of range");
+  const int local = node - ctx->dc.node_base;
+  if (local < 0 || local >= ctx->dc.N) return fail(KSS_E_INVAL, "node out of range");
+  int rc = validate(&ctx->host, ps, ps->n_pods);
+  if (rc) return rc;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  HIP_TRY(hipSetDevice(ctx->cfg.device));
+  rc = upload_podset(ctx->stream, ctx->tmp_pod_buf, ps, ctx->tdp);
+  if (rc) return rc;
+  hipLaunchKernelGGL(k_commit, dim3(1), dim3(64), 0, ctx->stream, ctx->dc, ctx->tdp, pod_index, local, -1);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipStreamSynchronize(ctx->stream));
+  return 0;
+}
+
+int kss_schedule_batch(kss_ctx* ctx, const kss_podset* ps, int32_t n, uint32_t flags, int32_t* chosen_out) {
+  if (!ctx || !ctx->loaded || !ps) return fail(KSS_E_INVAL, "bad arguments");
+  int rc = validate(&ctx->host, ps, n);
+  if (rc) return rc;
+  const bool record = (flags & KSS_SCHED_RECORD) != 0;
+  if (record && n > ctx->cfg.max_pods_record) return fail(KSS_E_INVAL, "record capacity (max_pods_record) exceeded");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  HIP_TRY(hipSetDevice(ctx->cfg.device));
+  rc = upload_podset(ctx->stream, ctx->pod_buf, ps, ctx->dp);
+  if (rc) return rc;
+  ctx->staged_n = ps->n_pods;
+  rc = run_single(ctx, ctx->dp, n, /*commit=*/true, record, /*keep_norm=*/record, chosen_out);
+  if (rc) return rc;
+  for (int i = 0; i < n; i++)
+    if (ctx->meta_host[i].status == 4) return fail(KSS_E_UNSUPPORTED, "pod program exceeds the device path's per-pod limits");
+  return 0;
+}
+
+int kss_stage_pods(kss_ctx* ctx, const kss_podset* ps) {
+  if (!ctx || !ctx->loaded || !ps) return fail(KSS_E_INVAL, "bad arguments");
+  int rc = validate(&ctx->host, ps, ps->n_pods);
+  if (rc) return rc;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  HIP_TRY(hipSetDevice(ctx->cfg.device));
+  rc = upload_podset(ctx->stream, ctx->pod_buf, ps, ctx->dp);
+  if (rc) return rc;
+  HIP_TRY(hipStreamSynchronize(ctx->stream));
+  ctx->staged_n = ps->n_pods;
+  return 0;
+}
+
+int kss_run_staged(kss_ctx* ctx, int32_t n, uint32_t flags, int32_t* chosen_out) {
+  if (!ctx || !ctx->loaded) return fail(KSS_E_INVAL, "no cluster loaded");
+  if (n < 0 || n > ctx->staged_n) return fail(KSS_E_INVAL, "n exceeds the staged pods");
+  const bool record = (flags & KSS_SCHED_RECORD) != 0;
+  if (record && n > ctx->cfg.max_pods_record) return fail(KSS_E_INVAL, "record capacity (max_pods_record) exceeded");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  HIP_TRY(hipSetDevice(ctx->cfg.device));
+  int rc = run_single(ctx, ctx->dp, n, /*commit=*/true, record, /*keep_norm=*/record, chosen_out);
+  if (rc) return rc;
+  for (int i = 0; i < n; i++)
+    if (ctx->meta_host[i].status == 4) return fail(KSS_E_UNSUPPORTED, "pod program exceeds the device path's per-pod limits");
+  return 0;
+}
+
+int kss_fetch_record(kss_ctx* ctx, int32_t pod_index, kss_pod_result* out) {
+  if (!ctx || !out) return fail(KSS_E_INVAL, "bad arguments");
+  if (pod_index < 0 || pod_index >= ctx->recorded) return fail(KSS_E_NOTFOUND, "pod not recorded");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  HIP_TRY(hipSetDevice(ctx->cfg.device));
+  return copy_slot(ctx, pod_index, ctx->meta_host[pod_index], out);
+}
+
+int kss_last_timing(kss_ctx* ctx, double* device_ms, int32_t* launches) {
+  if (!ctx) return fail(KSS_E_INVAL, "null ctx");
+  if (device_ms) *device_ms = ctx->last_ms;
+  if (launches) *launches = ctx->last_launches;
+  return 0;
+}
+
+int kss_schedule_scenarios(int32_t device, const kss_profile* prof, int32_t n_scen, const kss_cluster* clusters,
+                           const kss_podset* podsets, int32_t* chosen_out, double* device_ms) {
+  if (!prof || n_scen < 0 || (n_scen && (!clusters || !podsets || !chosen_out))) return fail(KSS_E_INVAL, "bad arguments");
+  if (prof->pct_nodes_to_score != 100 && prof->pct_nodes_to_score != 0)
+    return fail(KSS_E_UNSUPPORTED, "percentageOfNodesToScore must be 100");
+  if (n_scen == 0) return 0;
+  int rc;
+  for (int s = 0; s < n_scen; s++) {
+    if ((rc = check_cluster(&clusters[s]))) return rc;
+    if ((rc = validate(&clusters[s], &podsets[s], podsets[s].n_pods))) return rc;
+  }
+  HIP_TRY(hipSetDevice(device));
+  hipStream_t st;
+  HIP_TRY(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+  // one device arena: clusters, podsets, scratch slots, chosen, jobs
+  std::vector<size_t> c_off(n_scen), p_off(n_scen), s_off(n_scen), ch_off(n_scen);
+  std::vector<ClusterLayout> layouts;
+  layouts.reserve(n_scen);
+  size_t total = 0;
+  for (int s = 0; s < n_scen; s++) {
+    layouts.emplace_back(&clusters[s], clusters[s].n_classes, clusters[s].n_terms);
+    c_off[s] = total;
+    total = align_up(total + layouts[s].total, 256);
+  }
+  std::vector<size_t> pod_bytes(n_scen);
+  for (int s = 0; s < n_scen; s++) {
+    const kss_podset& ps = podsets[s];
+    size_t b = 0;
+    b = align_up(b + sizeof(kss_pod) * std::max(ps.n_pods, 1), 256);
+    b = align_up(b + sizeof(kss_req) * std::max(ps.n_reqs, 1), 256);
+    b = align_up(b + sizeof(kss_term) * std::max(ps.n_terms, 1), 256);
+    b = align_up(b + sizeof(kss_spread) * std::max(ps.n_spreads, 1), 256);
+    b = align_up(b + sizeof(kss_ipa) * std::max(ps.n_ipa, 1), 256);
+    b = align_up(b + sizeof(int32_t) * std::max(ps.n_ints, 1), 256);
+    pod_bytes[s] = b;
+    p_off[s] = total;
+    total = align_up(total + b, 256);
+  }
+  for (int s = 0; s < n_scen; s++) {
+    s_off[s] = total;
+    total = align_up(total + SlotLayout((size_t)clusters[s].n_nodes).bytes, 256);
+  }
+  for (int s = 0; s < n_scen; s++) {
+    ch_off[s] = total;
+    total = align_up(total + sizeof(int32_t) * std::max(podsets[s].n_pods, 1), 256);
+  }
+  const size_t job_off = total;
+  total = align_up(total + sizeof(DevJob) * n_scen, 256);
+  char* arena = nullptr;
+  if (hipMalloc(&arena, total) != hipSuccess) {
+    hipStreamDestroy(st);
+    return fail(KSS_E_NOMEM, "scenario arena allocation failed");
+  }
+  std::vector<DevJob> jobs(n_scen);
+  std::vector<std::vector<double>> logtabs(n_scen);
+  rc = 0;
+  for (int s = 0; s < n_scen && !rc; s++) {
+    DevJob& j = jobs[s];
+    rc = fill_cluster(st, &clusters[s], clusters[s].n_classes, clusters[s].n_terms, arena + c_off[s], layouts[s], j.c, logtabs[s]);
+    if (rc) break;
+    DevBuf view;
+    view.p = arena + p_off[s];
+    view.cap = pod_bytes[s];
+    rc = upload_podset(st, view, &podsets[s], j.P);
+    view.p = nullptr;
+    j.n_pods = podsets[s].n_pods;
+    j.commit = 1;
+    j.keep_norm = 0;
+    j.record = 0;
+    j.slots = (uint8_t*)(arena + s_off[s]);
+    j.slot_bytes = SlotLayout((size_t)clusters[s].n_nodes).bytes;
+    j.chosen = (int32_t*)(arena + ch_off[s]);
+    j.meta = nullptr;
+    // the host-side log tables must stay alive until the copies finish
+    if (s % 256 == 255) {
+      if (hipStreamSynchronize(st) != hipSuccess) rc = fail(KSS_E_DEVICE, "upload failed");
+      for (int t = s - 255; t <= s; t++) std::vector<double>().swap(logtabs[t]);
+    }
+  }
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  if (!rc) {
+    if (hipMemcpyAsync(arena + job_off, jobs.data(), sizeof(DevJob) * n_scen, hipMemcpyHostToDevice, st) != hipSuccess ||
+        hipStreamSynchronize(st) != hipSuccess)
+      rc = fail(KSS_E_DEVICE, "job upload failed");
+  }
+  if (!rc) {
+    hipEventCreate(&e0);
+    hipEventCreate(&e1);
+    int maxN = 0;
+    for (int s = 0; s < n_scen; s++) maxN = std::max(maxN, clusters[s].n_nodes);
+    hipEventRecord(e0, st);
+    hipLaunchKernelGGL(k_schedule, dim3(n_scen), dim3(block_threads(maxN)), 0, st, (const DevJob*)(arena + job_off), *prof);
+    if (hipGetLastError() != hipSuccess) rc = fail(KSS_E_DEVICE, "k_schedule launch failed");
+    hipEventRecord(e1, st);
+    if (hipStreamSynchronize(st) != hipSuccess) rc = fail(KSS_E_DEVICE, "k_schedule failed");
+    float ms = 0;
+    hipEventElapsedTime(&ms, e0, e1);
+    if (device_ms) *device_ms = ms;
+  }
+  if (!rc) {
+    size_t o = 0;
+    for (int s = 0; s < n_scen && !rc; s++) {
+      if (podsets[s].n_pods &&
+          hipMemcpy(chosen_out + o, arena + ch_off[s], sizeof(int32_t) * podsets[s].n_pods, hipMemcpyDeviceToHost) != hipSuccess)
+        rc = fail(KSS_E_DEVICE, "chosen copy failed");
+      o += (size_t)podsets[s].n_pods;
+    }
+  }
+  if (e0) hipEventDestroy(e0);
+  if (e1) hipEventDestroy(e1);
+  hipFree(arena);
+  hipStreamDestroy(st);
+  return rc;
+}
+
+int kss_set_names(kss_ctx* ctx, const kss_names* names) {
+  if (!ctx || !names) return fail(KSS_E_INVAL, "bad arguments");
+  return kss_host_set_names(&ctx->names, names, ctx->host.n_nodes, ctx->host.n_taints, ctx->host.n_scalar);
+}
+
+int kss_format_annotations(kss_ctx* ctx, const kss_pod_result* res, int32_t n_nodes, char* buf, size_t cap, size_t* need) {
+  if (!ctx || !res || !need) return fail(KSS_E_INVAL, "bad arguments");
+  return kss_host_format(&ctx->names, &ctx->prof, res, n_nodes, buf, cap, need);
+}
+
+}  // extern "C"

@@ -363,6 +363,7 @@ class CompiledPods:
     ipa: np.ndarray
     ints: np.ndarray
     names: List[Tuple[str, str]]   # (namespace, name)
+    counts: Tuple[int, int, int, int, int] = (0, 0, 0, 0, 0)  # real pool sizes (arrays are padded to >= 1)
 
     @property
     def n(self) -> int:
@@ -371,9 +372,7 @@ class CompiledPods:
     def as_struct(self) -> abi.PodSet:
         s = abi.PodSet()
         s.n_pods = self.n
-        s.n_reqs, s.n_terms, s.n_spreads, s.n_ipa, s.n_ints = (int(self.reqs.shape[0]), int(self.terms.shape[0]),
-                                                              int(self.spreads.shape[0]), int(self.ipa.shape[0]),
-                                                              int(self.ints.shape[0]))
+        s.n_reqs, s.n_terms, s.n_spreads, s.n_ipa, s.n_ints = self.counts
         s.pods = self.pods.ctypes.data_as(abi.P(abi.Pod))
         s.reqs = self.reqs.ctypes.data_as(abi.P(abi.Req))
         s.terms = self.terms.ctypes.data_as(abi.P(abi.Term))
@@ -636,7 +635,9 @@ class Compiler:
 
         return CompiledPods(pods=recs, reqs=arr(self._reqs, abi.REQ_DTYPE), terms=arr(self._terms, abi.TERM_DTYPE),
                             spreads=arr(self._spreads, abi.SPREAD_DTYPE), ipa=arr(self._ipa, abi.IPA_DTYPE),
-                            ints=_nonempty(np.array(self._ints, dtype=np.int32)), names=names)
+                            ints=_nonempty(np.array(self._ints, dtype=np.int32)), names=names,
+                            counts=(len(self._reqs), len(self._terms), len(self._spreads), len(self._ipa),
+                                    len(self._ints)))
 
     def _list(self, vals: Sequence[int]) -> Tuple[int, int]:
         off = len(self._ints)

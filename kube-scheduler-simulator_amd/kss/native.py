@@ -1,0 +1,294 @@
+"""ctypes binding of libkss.so (include/kss.h).
+
+The HIP library is the only compute path: importing this module fails loudly if
+the shared object is missing, and every device call raises ``KssError`` with
+the library's own message on failure.  There is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from typing import Dict, List, Optional, Sequence
+
+import numpy as np
+
+from . import abi
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libkss.so")
+P = C.POINTER
+
+
+class KssError(RuntimeError):
+    def __init__(self, rc: int, msg: str):
+        super().__init__(f"libkss error {rc}: {msg}")
+        self.rc = rc
+
+
+_lib: Optional[C.CDLL] = None
+
+# (name, restype, argtypes) for every entry point declared in include/kss.h
+SIGNATURES = [
+    ("kss_abi_version", C.c_int, []),
+    ("kss_last_error", C.c_char_p, []),
+    ("kss_abi_sizes", C.c_int, [P(C.c_int32), C.c_int32]),
+    ("kss_default_profile", None, [P(abi.Profile)]),
+    ("kss_create", C.c_void_p, [P(abi.Config), P(abi.Profile)]),
+    ("kss_destroy", None, [C.c_void_p]),
+    ("kss_load_cluster", C.c_int, [C.c_void_p, P(abi.Cluster)]),
+    ("kss_apply_node_delta", C.c_int, [C.c_void_p, P(C.c_int32), C.c_int32, P(C.c_int64), P(C.c_int64), P(C.c_int32)]),
+    ("kss_read_node_state", C.c_int, [C.c_void_p, P(C.c_int64), P(C.c_int64), P(C.c_int32), P(C.c_int32), P(C.c_int32)]),
+    ("kss_eval_pod", C.c_int, [C.c_void_p, P(abi.PodSet), C.c_int32, P(abi.PodResult)]),
+    ("kss_commit", C.c_int, [C.c_void_p, P(abi.PodSet), C.c_int32, C.c_int32]),
+    ("kss_rollback", C.c_int, [C.c_void_p, P(abi.PodSet), C.c_int32, C.c_int32]),
+    ("kss_schedule_batch", C.c_int, [C.c_void_p, P(abi.PodSet), C.c_int32, C.c_uint32, P(C.c_int32)]),
+    ("kss_fetch_record", C.c_int, [C.c_void_p, C.c_int32, P(abi.PodResult)]),
+    ("kss_schedule_scenarios", C.c_int, [C.c_int32, P(abi.Profile), C.c_int32, P(abi.Cluster), P(abi.PodSet),
+                                         P(C.c_int32), P(C.c_double)]),
+    ("kss_last_timing", C.c_int, [C.c_void_p, P(C.c_double), P(C.c_int32)]),
+    ("kss_set_names", C.c_int, [C.c_void_p, P(abi.Names)]),
+    ("kss_format_annotations", C.c_int, [C.c_void_p, P(abi.PodResult), C.c_int32, C.c_char_p, C.c_size_t,
+                                         P(C.c_size_t)]),
+    ("kss_format_annotations_ex", C.c_int, [P(abi.Names), P(abi.Profile), P(abi.PodResult), C.c_int32, C.c_int32,
+                                            C.c_int32, C.c_char_p, C.c_size_t, P(C.c_size_t)]),
+    ("kss_stage_pods", C.c_int, [C.c_void_p, P(abi.PodSet)]),
+    ("kss_run_staged", C.c_int, [C.c_void_p, C.c_int32, C.c_uint32, P(C.c_int32)]),
+    ("kss_reset_node_state", C.c_int, [C.c_void_p]),
+    ("kss_synth_make", C.c_int, [C.c_int32, C.c_uint64, C.c_int32, C.c_int32, P(abi.Synth)]),
+    ("kss_synth_free", None, [P(abi.Synth)]),
+]
+
+
+def lib() -> C.CDLL:
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"libkss.so not built at {LIB_PATH} (run __graft_entry__.build()); "
+                              "there is no CPU fallback for the device path")
+        L = C.CDLL(LIB_PATH)
+        for name, res, args in SIGNATURES:
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        if L.kss_abi_version() != 1:
+            raise ImportError("libkss ABI version mismatch")
+        _lib = L
+    return _lib
+
+
+def check(rc: int):
+    if rc != 0:
+        raise KssError(rc, (lib().kss_last_error() or b"").decode())
+
+
+class PodResult:
+    """Host arrays for one pod's result (kss_pod_result)."""
+
+    def __init__(self, n_nodes: int):
+        N = max(n_nodes, 1)
+        self.n_nodes = n_nodes
+        self.fail_plugin = np.zeros(N, np.uint8)
+        self.fail_detail = np.zeros(N, np.uint16)
+        self.raw = np.zeros((abi.KSS_NSCORE, N), np.int64)
+        self.norm = np.zeros((abi.KSS_NSCORE, N), np.int64)
+        self.total = np.zeros(N, np.int64)
+        s = abi.PodResult()
+        s.fail_plugin = self.fail_plugin.ctypes.data_as(P(C.c_uint8))
+        s.fail_detail = self.fail_detail.ctypes.data_as(P(C.c_uint16))
+        s.raw = self.raw.ctypes.data_as(P(C.c_int64))
+        s.norm = self.norm.ctypes.data_as(P(C.c_int64))
+        s.total = self.total.ctypes.data_as(P(C.c_int64))
+        self.s = s
+
+    @property
+    def chosen(self):
+        return self.s.chosen
+
+    @property
+    def n_feasible(self):
+        return self.s.n_feasible
+
+    @property
+    def scored(self):
+        return self.s.scored
+
+    @property
+    def status(self):
+        return self.s.status
+
+
+def _cstrs(items: Sequence[str]):
+    arr = (C.c_char_p * max(len(items), 1))()
+    for i, s in enumerate(items):
+        arr[i] = s.encode()
+    return arr
+
+
+def make_names(node_names, taints, scalars):
+    """Build a kss_names struct; returns (struct, keepalive)."""
+    nn = _cstrs(node_names)
+    tk = _cstrs([t[0] for t in taints])
+    tv = _cstrs([t[1] for t in taints])
+    sc = _cstrs(scalars)
+    n = abi.Names(C.cast(nn, P(C.c_char_p)), C.cast(tk, P(C.c_char_p)), C.cast(tv, P(C.c_char_p)),
+                  C.cast(sc, P(C.c_char_p)))
+    return n, (nn, tk, tv, sc)
+
+
+def parse_annotations(buf: bytes) -> Dict[str, str]:
+    parts = buf.split(b"\0")
+    out = {}
+    i = 0
+    while i + 1 < len(parts) and parts[i]:
+        out[parts[i].decode()] = parts[i + 1].decode()
+        i += 2
+    return out
+
+
+def format_annotations_ex(names_struct, profile, result: PodResult, n_nodes, n_taints, n_scalar) -> Dict[str, str]:
+    L = lib()
+    need = C.c_size_t(0)
+    check(L.kss_format_annotations_ex(C.byref(names_struct), C.byref(profile), C.byref(result.s), n_nodes, n_taints,
+                                      n_scalar, None, 0, C.byref(need)))
+    buf = C.create_string_buffer(need.value)
+    check(L.kss_format_annotations_ex(C.byref(names_struct), C.byref(profile), C.byref(result.s), n_nodes, n_taints,
+                                      n_scalar, buf, need.value, C.byref(need)))
+    return parse_annotations(buf.raw[:need.value])
+
+
+class Context:
+    """One device context (kss_ctx): a loaded cluster snapshot on one GPU."""
+
+    def __init__(self, profile: Optional[abi.Profile] = None, device: int = 0, max_pods_record: int = 0,
+                 class_capacity: int = 0, term_capacity: int = 0):
+        L = lib()
+        self.profile = profile if profile is not None else abi.default_profile()
+        cfg = abi.Config(device, max_pods_record, class_capacity, term_capacity)
+        h = L.kss_create(C.byref(cfg), C.byref(self.profile))
+        if not h:
+            raise KssError(-1, (L.kss_last_error() or b"").decode())
+        self.h = C.c_void_p(h)
+        self.n_nodes = 0
+        self._keep = []
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().kss_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def load(self, cluster_struct: abi.Cluster, names=None):
+        check(lib().kss_load_cluster(self.h, C.byref(cluster_struct)))
+        self.n_nodes = cluster_struct.n_nodes
+        self.n_classes = cluster_struct.n_classes
+        self.n_terms = cluster_struct.n_terms
+        self.n_taints = cluster_struct.n_taints
+        self.n_scalar = cluster_struct.n_scalar
+        if names is not None:
+            st, keep = names
+            self._keep = keep
+            check(lib().kss_set_names(self.h, C.byref(st)))
+
+    def schedule_batch(self, podset_struct: abi.PodSet, n: int, record=False, flags=0) -> np.ndarray:
+        chosen = np.full(max(n, 1), -2, np.int32)
+        fl = flags | (abi.KSS_SCHED_RECORD if record else 0)
+        check(lib().kss_schedule_batch(self.h, C.byref(podset_struct), n, fl, chosen.ctypes.data_as(P(C.c_int32))))
+        return chosen[:n]
+
+    def stage(self, podset_struct: abi.PodSet):
+        check(lib().kss_stage_pods(self.h, C.byref(podset_struct)))
+
+    def run_staged(self, n: int, record=False, out: Optional[np.ndarray] = None) -> np.ndarray:
+        chosen = out if out is not None else np.full(max(n, 1), -2, np.int32)
+        fl = abi.KSS_SCHED_RECORD if record else 0
+        check(lib().kss_run_staged(self.h, n, fl, chosen.ctypes.data_as(P(C.c_int32))))
+        return chosen[:n]
+
+    def reset(self):
+        check(lib().kss_reset_node_state(self.h))
+
+    def eval_pod(self, podset_struct: abi.PodSet, i: int) -> PodResult:
+        r = PodResult(self.n_nodes)
+        check(lib().kss_eval_pod(self.h, C.byref(podset_struct), i, C.byref(r.s)))
+        return r
+
+    def fetch_record(self, i: int) -> PodResult:
+        r = PodResult(self.n_nodes)
+        check(lib().kss_fetch_record(self.h, i, C.byref(r.s)))
+        return r
+
+    def commit(self, podset_struct, i, node):
+        check(lib().kss_commit(self.h, C.byref(podset_struct), i, node))
+
+    def rollback(self, podset_struct, i, node):
+        check(lib().kss_rollback(self.h, C.byref(podset_struct), i, node))
+
+    def node_state(self):
+        N = max(self.n_nodes, 1)
+        st = dict(requested=np.zeros((abi.KSS_NRES, N), np.int64), nonzero=np.zeros((2, N), np.int64),
+                  pod_count=np.zeros(N, np.int32), class_count=np.zeros((max(self.n_classes, 1), N), np.int32),
+                  term_count=np.zeros((max(self.n_terms, 1), N), np.int32))
+        check(lib().kss_read_node_state(self.h, st["requested"].ctypes.data_as(P(C.c_int64)),
+                                        st["nonzero"].ctypes.data_as(P(C.c_int64)),
+                                        st["pod_count"].ctypes.data_as(P(C.c_int32)),
+                                        st["class_count"].ctypes.data_as(P(C.c_int32)),
+                                        st["term_count"].ctypes.data_as(P(C.c_int32))))
+        return st
+
+    def last_timing(self):
+        ms = C.c_double(0)
+        n = C.c_int32(0)
+        check(lib().kss_last_timing(self.h, C.byref(ms), C.byref(n)))
+        return ms.value, n.value
+
+    def format_annotations(self, result: PodResult) -> Dict[str, str]:
+        L = lib()
+        need = C.c_size_t(0)
+        check(L.kss_format_annotations(self.h, C.byref(result.s), self.n_nodes, None, 0, C.byref(need)))
+        buf = C.create_string_buffer(need.value)
+        check(L.kss_format_annotations(self.h, C.byref(result.s), self.n_nodes, buf, need.value, C.byref(need)))
+        return parse_annotations(buf.raw[:need.value])
+
+
+class Synth:
+    """A C++-generated synthetic cluster (kss_synth_make); owns its arrays until close()."""
+
+    def __init__(self, config: int, seed: int = 0, n_nodes: int = 0, n_pods: int = 0):
+        self.s = abi.Synth()
+        check(lib().kss_synth_make(config, seed, n_nodes, n_pods, C.byref(self.s)))
+        self.cluster = self.s.cluster
+        self.pods = self.s.pods
+
+    @property
+    def n_nodes(self):
+        return self.s.cluster.n_nodes
+
+    @property
+    def n_pods(self):
+        return self.s.pods.n_pods
+
+    def close(self):
+        if self.s.owner:
+            lib().kss_synth_free(C.byref(self.s))
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def schedule_scenarios(profile, clusters: List[abi.Cluster], podsets: List[abi.PodSet], device=0):
+    n = len(clusters)
+    carr = (abi.Cluster * max(n, 1))(*clusters)
+    parr = (abi.PodSet * max(n, 1))(*podsets)
+    total = sum(p.n_pods for p in podsets)
+    chosen = np.full(max(total, 1), -2, np.int32)
+    ms = C.c_double(0)
+    check(lib().kss_schedule_scenarios(device, C.byref(profile), n, carr, parr, chosen.ctypes.data_as(P(C.c_int32)),
+                                       C.byref(ms)))
+    return chosen[:total], ms.value

@@ -1,0 +1,161 @@
+"""HIP path (libkss.so on gfx950) vs the CPU oracle: bit-exact filter verdicts, every
+per-plugin raw and normalized score, totals, chosen nodes and the final node state.
+
+Sizes are ones the oracle finishes in seconds; full BASELINE sizes are covered by
+size-independent properties in test_gpu_properties.py.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import k8s_oracle
+import oracle_c
+from kss import abi, native, synth
+from kss.compile import compile_cluster
+
+pytestmark = pytest.mark.gpu
+
+GOLD = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "readme_known_answer.json")))
+
+
+def _compare_records(ctx, res, chosen_o, n_pods, n_nodes):
+    for j in range(n_pods):
+        r = ctx.fetch_record(j)
+        m = res.meta(j)
+        assert r.chosen == m["chosen"], (j, r.chosen, m["chosen"])
+        assert r.n_feasible == m["n_feasible"], j
+        assert r.scored == m["scored"], j
+        assert r.status == m["status"], j
+        np.testing.assert_array_equal(r.fail_plugin[:n_nodes], res.fail_plugin[j, :n_nodes], err_msg=f"pod {j}")
+        np.testing.assert_array_equal(r.fail_detail[:n_nodes], res.fail_detail[j, :n_nodes], err_msg=f"pod {j}")
+        if m["scored"]:
+            feas = res.fail_plugin[j, :n_nodes] == 0
+            np.testing.assert_array_equal(r.raw[:, :n_nodes][:, feas], res.raw[j][:, :n_nodes][:, feas], err_msg=f"pod {j}")
+            np.testing.assert_array_equal(r.norm[:, :n_nodes][:, feas], res.norm[j][:, :n_nodes][:, feas], err_msg=f"pod {j}")
+            np.testing.assert_array_equal(r.total[:n_nodes][feas], res.total[j, :n_nodes][feas], err_msg=f"pod {j}")
+            assert r.s.best_total == m["best_total"]
+
+
+def _state_equal(ctx, st, n_nodes, n_classes, n_terms):
+    g = ctx.node_state()
+    np.testing.assert_array_equal(g["requested"][:, :n_nodes], st["requested"][:, :n_nodes])
+    np.testing.assert_array_equal(g["nonzero"][:, :n_nodes], st["nonzero"][:, :n_nodes])
+    np.testing.assert_array_equal(g["pod_count"][:n_nodes], st["pod_count"][:n_nodes])
+    if n_classes:
+        np.testing.assert_array_equal(g["class_count"][:n_classes], st["class_count"][:n_classes])
+    if n_terms:
+        np.testing.assert_array_equal(g["term_count"][:n_terms], st["term_count"][:n_terms])
+
+
+@pytest.mark.parametrize("config,n_nodes,n_pods", [
+    (1, 100, 1000),   # C1 exactly (BASELINE configs[0])
+    (2, 700, 400),
+    (3, 300, 400),    # PTS + IPA
+    (4, 500, 300),    # zone spread
+    (5, 1000, 200),
+    (1, 3, 50),       # tiny: single-feasible and unschedulable pods
+    (3, 1500, 120),   # > 1024 nodes: several nodes per lane
+])
+def test_schedule_batch_matches_oracle(config, n_nodes, n_pods):
+    prof = abi.default_profile()
+    s = native.Synth(config, 0, n_nodes, n_pods)
+    chosen_o, res, st = oracle_c.schedule(prof, s.cluster, s.pods, n_pods, n_nodes, record=True, threads=8,
+                                          n_classes=s.cluster.n_classes, n_terms=s.cluster.n_terms)
+    ctx = native.Context(prof, max_pods_record=n_pods)
+    ctx.load(s.cluster)
+    chosen_g = ctx.schedule_batch(s.pods, n_pods, record=True)
+    np.testing.assert_array_equal(chosen_g, chosen_o)
+    _compare_records(ctx, res, chosen_o, n_pods, n_nodes)
+    _state_equal(ctx, st, n_nodes, s.cluster.n_classes, s.cluster.n_terms)
+
+
+def test_schedule_without_record_same_choices():
+    prof = abi.default_profile()
+    s = native.Synth(3, 0, 400, 300)
+    chosen_o, _, st = oracle_c.schedule(prof, s.cluster, s.pods, 300, 400, record=False, threads=8,
+                                        n_classes=s.cluster.n_classes, n_terms=s.cluster.n_terms)
+    ctx = native.Context(prof)
+    ctx.load(s.cluster)
+    np.testing.assert_array_equal(ctx.schedule_batch(s.pods, 300), chosen_o)
+    _state_equal(ctx, st, 400, s.cluster.n_classes, s.cluster.n_terms)
+
+
+def test_compiled_objects_path_and_annotations():
+    """Objects -> host compiler -> GPU; annotations formatted lazily from HBM records equal the
+    object-level oracle's store.go restatement byte for byte."""
+    nodes, bound, pods = synth.make_cluster(3, 40, 80)
+    cc, cp, _ = compile_cluster(nodes, bound, pods)
+    ctx = native.Context(abi.default_profile(), max_pods_record=cp.n)
+    ctx.load(cc.as_struct(), names=native.make_names(cc.node_names, cc.taints, cc.scalars))
+    ctx.schedule_batch(cp.as_struct(), cp.n, record=True)
+    o = k8s_oracle.Oracle(nodes, bound)
+    for j in range(cp.n):
+        want = o.annotations(o.schedule_one(pods[j]))
+        got = ctx.format_annotations(ctx.fetch_record(j))
+        assert got == want, j
+
+
+def test_readme_known_answer_on_gpu():
+    cc, cp, _ = compile_cluster(GOLD["nodes"], (), [GOLD["pod"]])
+    ctx = native.Context(abi.default_profile(), max_pods_record=1)
+    ctx.load(cc.as_struct(), names=native.make_names(cc.node_names, cc.taints, cc.scalars))
+    r = ctx.eval_pod(cp.as_struct(), 0)
+    ann = ctx.format_annotations(r)
+    for k, v in GOLD["expected"].items():
+        if isinstance(v, dict):
+            assert json.loads(ann[k]) == v, k
+        else:
+            assert ann[k] == v, k
+
+
+def test_eval_pod_commit_rollback():
+    prof = abi.default_profile()
+    s = native.Synth(3, 0, 200, 20)
+    ctx = native.Context(prof)
+    ctx.load(s.cluster)
+    before = ctx.node_state()
+    for j in range(5):
+        want = oracle_c.Results(1, 200)
+        # oracle on the current committed state: schedule pods [0, j] and compare pod j
+        ch, res, _ = oracle_c.schedule(prof, s.cluster, s.pods, j + 1, 200, threads=8,
+                                       n_classes=s.cluster.n_classes, n_terms=s.cluster.n_terms)
+        r = ctx.eval_pod(s.pods, j)
+        assert r.chosen == ch[j]
+        np.testing.assert_array_equal(r.fail_plugin[:200], res.fail_plugin[j, :200])
+        if r.chosen >= 0:
+            ctx.commit(s.pods, j, r.chosen)
+    # roll everything back -> original state
+    ch, _, _ = oracle_c.schedule(prof, s.cluster, s.pods, 5, 200, n_classes=s.cluster.n_classes,
+                                 n_terms=s.cluster.n_terms)
+    for j in range(5):
+        if ch[j] >= 0:
+            ctx.rollback(s.pods, j, int(ch[j]))
+    after = ctx.node_state()
+    for k in before:
+        np.testing.assert_array_equal(before[k], after[k])
+
+
+def test_scenarios_match_oracle_per_scenario():
+    prof = abi.default_profile()
+    syn = [native.Synth(5, 0x5EED0005 + sc, 300, 150) for sc in range(12)]
+    chosen, ms = native.schedule_scenarios(prof, [x.cluster for x in syn], [x.pods for x in syn])
+    off = 0
+    for x in syn:
+        ch, _, _ = oracle_c.schedule(prof, x.cluster, x.pods, x.n_pods, x.n_nodes, record=False, threads=8,
+                                     n_classes=x.cluster.n_classes, n_terms=x.cluster.n_terms)
+        np.testing.assert_array_equal(chosen[off:off + x.n_pods], ch)
+        off += x.n_pods
+    assert ms > 0
+
+
+def test_invalid_program_is_rejected_not_run():
+    s = native.Synth(1, 0, 50, 10)
+    ctx = native.Context(abi.default_profile())
+    ctx.load(s.cluster)
+    bad = abi.PodSet.from_buffer_copy(bytes(s.pods))
+    bad.n_ints = 0
+    bad.n_reqs = 0  # requirement offsets now out of range
+    with pytest.raises(native.KssError):
+        ctx.schedule_batch(bad, 10)
