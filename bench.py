@@ -31,32 +31,33 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 
 
 def cpu_baseline(config, n_nodes, n_pods, seconds, threads):
-    """The CPU oracle (plain-C restatement, OpenMP over nodes) on a bounded prefix of the
-    same workload: pods are scheduled sequentially until `seconds` of wall time pass."""
-    import numpy as np
-
+    """The CPU oracle (plain-C restatement, OpenMP over nodes) on the same workload: the whole
+    sequential batch is scheduled from the initial snapshot, repeated until `seconds` of wall
+    time have passed (a bounded sample; a smaller pod prefix when one batch alone is longer)."""
     import oracle_c
     from kss import abi, native
 
     s = native.Synth(config, 0, n_nodes, n_pods)
     prof = abi.default_profile()
-    n = 16
-    t_used = 0.0
-    done = 0
-    while True:
+    kw = dict(threads=threads, record=False, n_classes=s.cluster.n_classes, n_terms=s.cluster.n_terms)
+    # size the prefix so one batch takes at most ~seconds/3
+    n = min(n_pods, 64)
+    t0 = time.perf_counter()
+    oracle_c.schedule(prof, s.cluster, s.pods, n, n_nodes, **kw)
+    dt = time.perf_counter() - t0
+    n = int(min(n_pods, max(n, n * (seconds / 3) / max(dt, 1e-4))))
+    reps, t_used = 0, 0.0
+    while t_used < seconds:
         t0 = time.perf_counter()
-        oracle_c.schedule(prof, s.cluster, s.pods, n, n_nodes, threads=threads, record=False,
-                          n_classes=s.cluster.n_classes, n_terms=s.cluster.n_terms)
-        dt = time.perf_counter() - t0
-        t_used, done = dt, n
-        if dt >= seconds or n >= n_pods:
-            break
-        n = min(n_pods, max(n * 2, int(n * seconds / max(dt, 1e-3) * 1.1)))
-    evals = done * n_nodes
+        oracle_c.schedule(prof, s.cluster, s.pods, n, n_nodes, **kw)
+        t_used += time.perf_counter() - t0
+        reps += 1
+    evals = reps * n * n_nodes
     return {"value": evals / t_used, "unit": "pod-node evals/s", "cores": threads, "kind": "port",
-            "sample": f"first {done} of {n_pods} pods of config C{config} ({n_nodes} nodes), sequential, "
-                      f"{t_used:.1f} s wall, oracle/kss_oracle.c OpenMP over nodes",
-            "pods_per_s": done / t_used}
+            "sample": f"{reps} x the first {n} of {n_pods} pods of config C{config} ({n_nodes} nodes), "
+                      f"sequential from the initial snapshot, {t_used:.1f} s wall, "
+                      f"oracle/kss_oracle.c OpenMP over nodes ({threads} threads)",
+            "pods_per_s": reps * n / t_used}
 
 
 def main():
@@ -152,6 +153,7 @@ def main():
             "pods_per_s": pods_per_s,
             "pods_scheduled_per_step": scheduled,
             "kernel_ms_per_step": kern_avg_s * 1e3,
+            "geometry": ctx.last_geometry(),
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": None,
                          "kernel": "k_schedule", "bytes_per_eval": B_EVAL[cfg]},

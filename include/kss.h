@@ -365,6 +365,9 @@ int kss_schedule_scenarios(int32_t device, const kss_profile* prof, int32_t n_sc
 
 /* timing of the last kss_schedule_batch / kss_eval_pod device work (HIP events on the work stream) */
 int kss_last_timing(kss_ctx* ctx, double* device_ms, int32_t* launches);
+/* launch geometry of the last scheduling launch: out[0] shards (workgroups) per cluster,
+ * out[1] threads per workgroup, out[2] node slots per lane */
+int kss_last_geometry(kss_ctx* ctx, int32_t* out3);
 
 /* ---- annotation formatting (store.go GetStoredResult semantics) -------- */
 typedef struct kss_names {

@@ -42,7 +42,67 @@ struct DevCluster {
   int32_t* class_count;
   int32_t* term_count;
   const double* log_table;  // go_log(k + 2), k in [0, N]
+  // Shard-resident LDS copies of the hot node columns (set inside the kernel; null on
+  // the host and in kernels without a cache).  Slot i holds node nc_lo + i.
+  int64_t* nc64;    // [8][nc_cap]: alloc cpu/mem/eph, requested cpu/mem/eph, nonzero cpu/mem
+  uint64_t* nct;    // [2][nc_cap]: taint_hard, taint_soft
+  int32_t* nc32;    // [3][nc_cap]: pod_count, allowed_pods, node_flags
+  int32_t* ncl;     // [n_keys][nc_cap]: label value ids, or null (read from HBM)
+  int32_t nc_lo, nc_cap;
 };
+
+// One node's hot columns, loaded once per (pod, node) into registers.
+struct NodeRow {
+  int64_t alloc[3], req[3], nz[2];
+  uint64_t th, ts;
+  int32_t pods, allowed;
+  uint32_t flags;
+};
+
+// a[r] for a runtime r in [0, 3) without dynamic register indexing
+__device__ __forceinline__ int64_t pick3(const int64_t (&a)[3], int r) { return r == 0 ? a[0] : (r == 1 ? a[1] : a[2]); }
+
+__device__ __forceinline__ NodeRow load_row(const DevCluster& c, int n) {
+  NodeRow r;
+  if (c.nc64) {
+    const int i = n - c.nc_lo, C = c.nc_cap;
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+      r.alloc[k] = c.nc64[k * C + i];
+      r.req[k] = c.nc64[(3 + k) * C + i];
+    }
+    r.nz[0] = c.nc64[6 * C + i];
+    r.nz[1] = c.nc64[7 * C + i];
+    r.th = c.nct[i];
+    r.ts = c.nct[C + i];
+    r.pods = c.nc32[i];
+    r.allowed = c.nc32[C + i];
+    r.flags = (uint32_t)c.nc32[2 * C + i];
+  } else {
+    const size_t N = (size_t)c.N;
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+      r.alloc[k] = c.alloc[k * N + n];
+      r.req[k] = c.requested[k * N + n];
+    }
+    r.nz[0] = c.nonzero[n];
+    r.nz[1] = c.nonzero[N + n];
+    r.th = c.taint_hard[n];
+    r.ts = c.taint_soft[n];
+    r.pods = c.pod_count[n];
+    r.allowed = c.allowed_pods[n];
+    r.flags = c.node_flags[n];
+  }
+  return r;
+}
+
+__device__ __forceinline__ uint64_t taint_hard_of(const DevCluster& c, int n) {
+  return c.nct ? c.nct[n - c.nc_lo] : c.taint_hard[n];
+}
+
+__device__ __forceinline__ uint32_t node_flags_of(const DevCluster& c, int n) {
+  return c.nc32 ? (uint32_t)c.nc32[2 * c.nc_cap + (n - c.nc_lo)] : c.node_flags[n];
+}
 
 struct DevPods {
   const kss_pod* pods;
@@ -54,6 +114,7 @@ struct DevPods {
 };
 
 __device__ __forceinline__ int32_t label_of(const DevCluster& c, int key, int n) {
+  if (c.ncl) return c.ncl[key * c.nc_cap + (n - c.nc_lo)];
   return c.label_value[(size_t)key * (size_t)c.N + (size_t)n];
 }
 
@@ -119,8 +180,8 @@ __device__ __forceinline__ bool required_affinity(const DevCluster& c, const Dev
 }
 
 // v1helper.FindMatchingUntoleratedTaint(node.Spec.Taints, tolerations, DoNotScheduleTaintsFilterFunc)
-__device__ __forceinline__ int first_untolerated(const DevCluster& c, const kss_pod& p, int n) {
-  const uint64_t untol = c.taint_hard[n] & ~p.tol_hard;
+__device__ __forceinline__ int first_untolerated(const DevCluster& c, const kss_pod& p, int n, uint64_t th) {
+  const uint64_t untol = th & ~p.tol_hard;
   if (!untol) return -1;
   const uint8_t* ord = c.taint_order + (size_t)n * KSS_TAINT_ORDER;
 #pragma unroll
@@ -142,10 +203,10 @@ __device__ __forceinline__ int64_t sum_rows(const int32_t* mat, size_t N, const 
 // NodeAffinity, (NodePorts), NodeResourcesFit — the ones that need no per-pod
 // cluster-wide state.  Returns 0 when all of them pass.
 __device__ __forceinline__ int filter_local(const DevCluster& c, const DevPods& P, const kss_pod& p,
-                                            uint32_t enabled, int n, uint16_t* detail) {
+                                            uint32_t enabled, int n, const NodeRow& row, uint16_t* detail) {
   // NodeUnschedulable.Filter
   if ((enabled >> KSS_F_NODE_UNSCHEDULABLE) & 1u) {
-    if ((c.node_flags[n] & KSS_NODE_UNSCHEDULABLE) && !(p.flags & KSS_POD_TOL_UNSCHEDULABLE))
+    if ((row.flags & KSS_NODE_UNSCHEDULABLE) && !(p.flags & KSS_POD_TOL_UNSCHEDULABLE))
       return KSS_F_NODE_UNSCHEDULABLE;
   }
   // NodeName.Fits
@@ -154,7 +215,7 @@ __device__ __forceinline__ int filter_local(const DevCluster& c, const DevPods& 
   }
   // TaintToleration.Filter
   if ((enabled >> KSS_F_TAINT_TOLERATION) & 1u) {
-    const int t = first_untolerated(c, p, n);
+    const int t = first_untolerated(c, p, n, row.th);
     if (t >= 0) {
       *detail = (uint16_t)t;
       return KSS_F_TAINT_TOLERATION;
@@ -168,7 +229,7 @@ __device__ __forceinline__ int filter_local(const DevCluster& c, const DevPods& 
   if ((enabled >> KSS_F_NODE_RESOURCES_FIT) & 1u) {
     const size_t N = (size_t)c.N;
     uint32_t bits = 0;
-    if ((int64_t)c.pod_count[n] + 1 > (int64_t)c.allowed_pods[n]) bits |= KSS_FIT_TOO_MANY_PODS;
+    if ((int64_t)row.pods + 1 > (int64_t)row.allowed) bits |= KSS_FIT_TOO_MANY_PODS;
     const int nr = 3 + c.n_scalar;
     bool all_zero = true;
     for (int r = 0; r < nr; r++) all_zero &= (p.fit_request[r] == 0);
@@ -176,7 +237,8 @@ __device__ __forceinline__ int filter_local(const DevCluster& c, const DevPods& 
       for (int r = 0; r < nr; r++) {
         const int64_t req = p.fit_request[r];
         if (r >= KSS_RES_SCALAR0 && req == 0) continue;
-        const int64_t freev = c.alloc[(size_t)r * N + n] - c.requested[(size_t)r * N + n];
+        const int64_t freev = r < 3 ? pick3(row.alloc, r) - pick3(row.req, r)
+                                    : c.alloc[(size_t)r * N + n] - c.requested[(size_t)r * N + n];
         if (req > freev) bits |= 1u << (r + 1);
       }
     }
@@ -188,60 +250,101 @@ __device__ __forceinline__ int filter_local(const DevCluster& c, const DevPods& 
   return 0;
 }
 
+// Go int64 division a / b for the non-negative operands the scores produce: one f64
+// division (exact operands below 2^53, error of the rounded quotient < 1) and an exact
+// integer correction; anything else takes the integer division.
+__device__ __forceinline__ int64_t div_i64(int64_t a, int64_t b) {
+  if (a >= 0 && b > 0 && a < (1ll << 53) && b < (1ll << 53)) {
+    int64_t q = (int64_t)((double)a / (double)b);
+    const int64_t r = a - q * b;
+    if (r < 0) q--;
+    else if (r >= b) q++;
+    return q;
+  }
+  return a / b;
+}
+
 // leastRequestedScore / mostRequestedScore
 __device__ __forceinline__ int64_t alloc_score(int strategy, int64_t requested, int64_t capacity) {
   if (capacity == 0) return 0;
   if (strategy == KSS_FIT_MOST_ALLOCATED) {
     if (requested > capacity) requested = capacity;
-    return (requested * 100) / capacity;
+    return div_i64(requested * 100, capacity);
   }
   if (requested > capacity) return 0;
-  return ((capacity - requested) * 100) / capacity;
+  return div_i64((capacity - requested) * 100, capacity);
 }
 
 // NodeResourcesFit.Score (resourceAllocationScorer.score, useRequested=false)
-__device__ __forceinline__ int64_t fit_score(const DevCluster& c, const kss_profile& prof, const kss_pod& p, int n) {
+__device__ __forceinline__ int64_t fit_score(const DevCluster& c, const kss_profile& prof, const kss_pod& p, int n,
+                                             const NodeRow& row) {
   const size_t N = (size_t)c.N;
   int64_t node_score = 0, weight_sum = 0;
-  for (int i = 0; i < prof.fit_n; i++) {
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    if (i >= prof.fit_n) break;
     const int r = prof.fit_res[i];
     const int64_t preq = p.score_req_nz[r];
     if (r >= KSS_RES_SCALAR0 && preq == 0) continue;
-    const int64_t alloc = c.alloc[(size_t)r * N + n];
-    const int64_t base = (r <= KSS_RES_MEMORY) ? c.nonzero[(size_t)r * N + n] : c.requested[(size_t)r * N + n];
+    const int64_t alloc = r < 3 ? pick3(row.alloc, r) : c.alloc[(size_t)r * N + n];
+    const int64_t base = r == KSS_RES_CPU       ? row.nz[0]
+                         : r == KSS_RES_MEMORY  ? row.nz[1]
+                         : r == KSS_RES_EPHEMERAL ? row.req[2]
+                                                  : c.requested[(size_t)r * N + n];
     if (alloc == 0) continue;
     node_score += alloc_score(prof.fit_strategy, base + preq, alloc) * prof.fit_weight[i];
     weight_sum += prof.fit_weight[i];
   }
   if (weight_sum == 0) return 0;
-  return node_score / weight_sum;
+  return div_i64(node_score, weight_sum);
 }
 
 // NodeResourcesBalancedAllocation.Score (balancedResourceScorer, useRequested=true)
-__device__ __forceinline__ int64_t ba_score(const DevCluster& c, const kss_profile& prof, const kss_pod& p, int n) {
+__device__ __forceinline__ int64_t ba_score(const DevCluster& c, const kss_profile& prof, const kss_pod& p, int n,
+                                            const NodeRow& row) {
   const size_t N = (size_t)c.N;
-  double fr[4];
+  double fr[4] = {0.0, 0.0, 0.0, 0.0};
+  bool use[4] = {false, false, false, false};
   int nf = 0;
   double total = 0.0;
-  for (int i = 0; i < prof.ba_n; i++) {
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    if (i >= prof.ba_n) break;
     const int r = prof.ba_res[i];
     const int64_t preq = p.score_req[r];
     if (r >= KSS_RES_SCALAR0 && preq == 0) continue;
-    const int64_t alloc = c.alloc[(size_t)r * N + n];
-    const int64_t req = c.requested[(size_t)r * N + n] + preq;
+    const int64_t alloc = r < 3 ? pick3(row.alloc, r) : c.alloc[(size_t)r * N + n];
+    const int64_t req = (r < 3 ? pick3(row.req, r) : c.requested[(size_t)r * N + n]) + preq;
     if (alloc == 0) continue;
     double f = (double)req / (double)alloc;
     if (f > 1.0) f = 1.0;
     total += f;
-    fr[nf++] = f;
+    fr[i] = f;
+    use[i] = true;
+    nf++;
   }
   double sd = 0.0;
   if (nf == 2) {
-    sd = fabs((fr[0] - fr[1]) / 2.0);
+    // the two used fractions, in resource order
+    double a = 0.0, b = 0.0;
+    bool got = false;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      if (!use[i]) continue;
+      if (!got) {
+        a = fr[i];
+        got = true;
+      } else {
+        b = fr[i];
+      }
+    }
+    sd = fabs((a - b) / 2.0);
   } else if (nf > 2) {
     const double mean = total / (double)nf;
     double sum = 0.0;
-    for (int i = 0; i < nf; i++) {
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      if (!use[i]) continue;
       const double d = fr[i] - mean;
       const double sq = d * d;
       sum = sum + sq;
@@ -253,8 +356,8 @@ __device__ __forceinline__ int64_t ba_score(const DevCluster& c, const kss_profi
 }
 
 // TaintToleration.Score: countIntolerableTaintsPreferNoSchedule
-__device__ __forceinline__ int64_t tt_score(const DevCluster& c, const kss_pod& p, int n) {
-  return (int64_t)__popcll(c.taint_soft[n] & ~p.tol_soft);
+__device__ __forceinline__ int64_t tt_score(const NodeRow& row, const kss_pod& p) {
+  return (int64_t)__popcll(row.ts & ~p.tol_soft);
 }
 
 // NodeAffinity.Score: PreferredSchedulingTerms.Score

@@ -72,12 +72,45 @@ struct DevJob {
 // ---------------------------------------------------------------------------
 // kernels
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(1024) void k_schedule(const DevJob* __restrict__ jobs, kss_profile prof) {
-  __shared__ Shared sh;
-  const DevJob& job = jobs[blockIdx.x];
-  const DevCluster& c = job.c;
+// grid = n_jobs * W; workgroup b serves shard (b % W) of cluster (b / W); each lane
+// owns npt node slots.
+template <bool GEN>
+__global__ __launch_bounds__(KSS_MAX_THREADS) void k_schedule(const DevJob* __restrict__ jobs, kss_profile prof,
+                                                              int W, int npt, int bins_cap, int cache_keys,
+                                                              unsigned long long* gran, int* err,
+                                                              unsigned long long* stamps) {
+  extern __shared__ __attribute__((aligned(16))) long long smem[];
+  const int ji = blockIdx.x / W, w = blockIdx.x % W;
+  const DevJob job = jobs[ji];  // by value: the descriptors stay in registers for the whole launch
+  DevCluster c = job.c;
   const size_t N = (size_t)c.N;
   const SlotLayout L(N);
+  if (threadIdx.x == 0) shdr(smem).abort = 0;
+  __syncthreads();
+  Shard S;
+  const int per = (c.N + W - 1) / W;
+  S.lo = min(c.N, w * per);
+  S.hi = min(c.N, S.lo + per);
+  S.W = W;
+  S.w = w;
+  S.epoch = 0;
+  S.gran = gran ? gran + (size_t)ji * 2 * W * 2 * XW_MAX : nullptr;
+  S.err = err;
+  S.stamps = nullptr;
+  const bool want_out = job.record || job.keep_norm;
+  // shard node cache: the hot node columns stay in LDS for the whole launch
+  const int cap = npt * (int)blockDim.x;
+  if (cache_keys >= 0) {
+    long long* b = xvec(smem) + NSCAL + bins_cap + slot_arrays_bytes(cap) / 8;
+    c.nc64 = reinterpret_cast<int64_t*>(b);
+    c.nct = reinterpret_cast<uint64_t*>(b + 8 * (size_t)cap);
+    c.nc32 = reinterpret_cast<int32_t*>(b + 10 * (size_t)cap);
+    c.ncl = cache_keys > 0 && cache_keys >= c.n_keys ? c.nc32 + 3 * (size_t)cap : nullptr;
+    c.nc_lo = S.lo;
+    c.nc_cap = cap;
+    cache_fill(c, S.hi, c.ncl ? c.n_keys : 0);
+    __syncthreads();
+  }
   for (int pi = 0; pi < job.n_pods; pi++) {
     uint8_t* base = job.slots + (job.record ? (size_t)pi * job.slot_bytes : 0);
     Slot s;
@@ -87,14 +120,22 @@ __global__ __launch_bounds__(1024) void k_schedule(const DevJob* __restrict__ jo
     s.norm = (int64_t*)(base + L.norm);
     s.total = (int64_t*)(base + L.total);
     PodMeta m;
-    schedule_pod(c, job.P, prof, pi, sh, s, m, job.keep_norm != 0);
+    S.stamps = (stamps && ji == 0 && w == 0 && pi < KSS_NSTAMP_PODS) ? stamps + (size_t)pi * 8 : nullptr;
+    KSS_STAMP(S, 0);
+    if (!schedule_pod<GEN>(c, job.P, prof, pi, smem, S, bins_cap, npt, want_out ? &s : nullptr, job.keep_norm != 0, m))
+      return;  // exchange timeout: the error word is set, leave the launch
     if (threadIdx.x == 0) {
-      if (job.chosen) job.chosen[pi] = m.chosen;
-      if (job.meta) job.meta[pi] = m;
-      if (job.commit && m.chosen >= 0) commit_pod(c, job.P, job.P.pods[pi], m.chosen - c.node_base, 1);
+      if (w == 0) {
+        if (job.chosen) job.chosen[pi] = m.chosen;
+        if (job.meta) job.meta[pi] = m;
+      }
+      const int local = m.chosen - c.node_base;
+      if (job.commit && m.chosen >= 0 && local >= S.lo && local < S.hi) commit_pod(c, job.P, job.P.pods[pi], local, 1);
     }
     __syncthreads();
+    KSS_STAMP(S, 6);
   }
+  if (c.nc64 && job.commit) cache_writeback(c, S.hi);
 }
 
 __global__ void k_commit(DevCluster c, DevPods P, int pi, int local, int sign) {
@@ -122,6 +163,13 @@ struct DevBuf {
     p = nullptr;
     cap = 0;
   }
+};
+
+// Per-batch LDS / exchange sizing: the host restatement of make_plan's bin counts.
+struct PlanNeeds {
+  int bins_cap = 0;  // max over pods of histogram + presence bins
+  int xw = 0;        // max exchange payload length (values) over pods and exchanges
+  bool general = false;  // some pod carries spread / inter-pod-affinity programs
 };
 
 struct kss_ctx {
@@ -152,6 +200,18 @@ struct kss_ctx {
   double last_ms = 0;
   int last_launches = 0;
   kss_host_names names;
+  // host copies of the per-key tables (plan sizing), and the exchange buffers
+  std::vector<int32_t> key_card_h;
+  std::vector<uint32_t> key_flags_h;
+  DevBuf gran_buf, err_buf;
+  int n_cu = 0;
+  int force_w = 0;            // KSS_SHARDS env override (tuning / tests)
+  int nodes_per_shard = 256;  // KSS_NODES_PER_SHARD
+  int pref_threads = 256;     // KSS_THREADS
+  PlanNeeds staged_need;
+  int last_geom[3] = {0, 0, 0};
+  const char* stamps_file = nullptr;  // KSS_STAMPS_FILE: dump per-phase timestamps of each launch
+  DevBuf stamp_buf;
 };
 
 namespace {
@@ -395,6 +455,13 @@ kss_ctx* kss_create(const kss_config* cfg, const kss_profile* prof) {
   kss_ctx* ctx = new kss_ctx();
   ctx->cfg = *cfg;
   ctx->prof = *prof;
+  hipDeviceProp_t dp{};
+  if (hipGetDeviceProperties(&dp, cfg->device) == hipSuccess) ctx->n_cu = dp.multiProcessorCount;
+  if (ctx->n_cu <= 0) ctx->n_cu = 1;
+  if (const char* e = getenv("KSS_SHARDS")) ctx->force_w = std::max(0, atoi(e));
+  ctx->stamps_file = getenv("KSS_STAMPS_FILE");
+  if (const char* e = getenv("KSS_NODES_PER_SHARD")) ctx->nodes_per_shard = std::max(1, atoi(e));
+  if (const char* e = getenv("KSS_THREADS")) ctx->pref_threads = std::min(KSS_MAX_THREADS, std::max(64, atoi(e)));
   if (hipSetDevice(cfg->device) != hipSuccess || hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreate(&ctx->ev0) != hipSuccess || hipEventCreate(&ctx->ev1) != hipSuccess) {
     fail(KSS_E_DEVICE, "stream/event creation failed");
@@ -416,6 +483,8 @@ void kss_destroy(kss_ctx* ctx) {
   ctx->meta_buf.release();
   ctx->chosen_buf.release();
   ctx->job_buf.release();
+  ctx->gran_buf.release();
+  ctx->err_buf.release();
   if (ctx->ev0) hipEventDestroy(ctx->ev0);
   if (ctx->ev1) hipEventDestroy(ctx->ev1);
   if (ctx->stream) hipStreamDestroy(ctx->stream);
@@ -454,6 +523,8 @@ int kss_load_cluster(kss_ctx* ctx, const kss_cluster* cl) {
                              ctx->stream));
   HIP_TRY(hipStreamSynchronize(ctx->stream));
   ctx->host = *cl;
+  ctx->key_card_h.assign(cl->key_card, cl->key_card + cl->n_label_keys);
+  ctx->key_flags_h.assign(cl->key_flags, cl->key_flags + cl->n_label_keys);
   ctx->loaded = true;
   ctx->recorded = 0;
   ctx->staged_n = -1;
@@ -511,15 +582,105 @@ int kss_read_node_state(kss_ctx* ctx, int64_t* requested, int64_t* nonzero, int3
   return 0;
 }
 
-static int block_threads(int N) {
-  if (N <= 256) return 256;
-  if (N <= 512) return 512;
-  return 1024;
+static PlanNeeds plan_needs(const int32_t* key_card, const uint32_t* key_flags, const kss_podset* ps, int n) {
+  PlanNeeds r;
+  r.xw = 12;  // the filter exchange's scalars
+  for (int i = 0; i < n; i++) {
+    const kss_pod& p = ps->pods[i];
+    int bins = 0, hp = 0, sp = 0;
+    if (p.n_hard | p.n_soft | p.ipa_len) r.general = true;
+    for (int h = 0; h < p.n_hard && h < MAXH; h++) {
+      const int key = ps->spreads[p.spread_off + h].key;
+      if (!(key_flags[key] & KSS_KEY_UNIQUE)) {
+        bins += key_card[key] + 1;
+        hp += key_card[key] + 1;
+      }
+    }
+    for (int q = 0; q < p.n_soft && q < MAXS; q++) {
+      const int key = ps->spreads[p.spread_off + p.n_hard + q].key;
+      if (!(key_flags[key] & (KSS_KEY_HOSTNAME | KSS_KEY_UNIQUE))) {
+        bins += key_card[key] + 1;
+        sp += key_card[key] + 1;
+      }
+    }
+    int keys[MAXK + 1], nk = 0;
+    for (int e = 0; e < p.ipa_len; e++) {
+      const int key = ps->ipa[p.ipa_off + e].key;
+      bool seen = false;
+      for (int j = 0; j < nk; j++) seen |= keys[j] == key;
+      if (seen) continue;
+      if (nk <= MAXK) keys[nk++] = key;
+      if (!(key_flags[key] & KSS_KEY_UNIQUE)) bins += 4 * (key_card[key] + 1);
+    }
+    r.bins_cap = std::max(r.bins_cap, bins + hp + sp);
+    r.xw = std::max(r.xw, std::max(MAXH + 1 + bins + hp, 12 + sp));
+  }
+  r.bins_cap = std::min(r.bins_cap, LDS_BINS);
+  return r;
+}
+
+static size_t lds_bytes(int bins_cap, int slots) {
+  return sizeof(SharedHdr) + 8 * (size_t)(NSCAL + bins_cap) + slot_arrays_bytes(slots);
+}
+
+// Geometry for clusters of at most maxN nodes split in W shards.
+struct Geometry {
+  int W = 1, threads = 64, npt = 1;
+};
+
+static bool pick_geometry(int maxN, int W, int pref_threads, Geometry& g) {
+  g.W = W;
+  const int per = (std::max(maxN, 1) + W - 1) / W;
+  int t = std::min(KSS_MAX_THREADS, std::max(pref_threads, 64));
+  if (per < t) t = std::max(64, (per + 63) / 64 * 64);
+  int npt = (per + t - 1) / t;
+  while (npt > 4 && t < KSS_MAX_THREADS) {
+    t = std::min(KSS_MAX_THREADS, t * 2);
+    npt = (per + t - 1) / t;
+  }
+  g.threads = t;
+  g.npt = npt;
+  return npt <= KSS_MAX_NPT;
+}
+
+// Launch k_schedule over n_jobs clusters (jobs already in device memory).  W > 1 needs
+// every workgroup resident: cooperative launch (the runtime checks the grid fits).
+static int launch_schedule(hipStream_t st, const Geometry& g, int n_jobs, int bins_cap, bool need_general, int n_keys,
+                           const DevJob* jobs, const kss_profile& prof, unsigned long long* gran, int* err,
+                           unsigned long long* stamps = nullptr) {
+  const int cap = g.threads * g.npt;
+  const size_t base = lds_bytes(bins_cap, cap);
+  if (base > KSS_LDS_BUDGET) return fail(KSS_E_UNSUPPORTED, "per-workgroup LDS budget exceeded (too many nodes per shard)");
+  // node cache with every label key, without labels, or none, whatever fits
+  int cache_keys = -1;
+  if (!getenv("KSS_NO_CACHE")) {
+    if (base + node_cache_bytes(cap, n_keys) <= KSS_LDS_BUDGET) cache_keys = n_keys;
+    else if (base + node_cache_bytes(cap, 0) <= KSS_LDS_BUDGET) cache_keys = 0;
+  }
+  const size_t shmem = base + (cache_keys >= 0 ? node_cache_bytes(cap, cache_keys) : 0);
+  const bool gen = bins_cap > 0 || need_general;
+  const void* fn = gen ? (const void*)k_schedule<true> : (const void*)k_schedule<false>;
+  HIP_TRY(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shmem));
+  const dim3 grid((unsigned)(n_jobs * g.W)), block((unsigned)g.threads);
+  kss_profile pr = prof;
+  int W = g.W, npt = g.npt;
+  if (g.W > 1) {
+    void* args[] = {(void*)&jobs, (void*)&pr,   (void*)&W,   (void*)&npt,   (void*)&bins_cap,
+                    (void*)&cache_keys, (void*)&gran, (void*)&err, (void*)&stamps};
+    HIP_TRY(hipLaunchCooperativeKernel(fn, grid, block, args, (unsigned)shmem, st));
+  } else {
+    if (gen)
+      hipLaunchKernelGGL(k_schedule<true>, grid, block, shmem, st, jobs, pr, W, npt, bins_cap, cache_keys, gran, err, stamps);
+    else
+      hipLaunchKernelGGL(k_schedule<false>, grid, block, shmem, st, jobs, pr, W, npt, bins_cap, cache_keys, gran, err, stamps);
+    HIP_TRY(hipGetLastError());
+  }
+  return 0;
 }
 
 // run k_schedule on the loaded cluster for pods [0, n); results stay on the device
-static int run_single(kss_ctx* ctx, const DevPods& dp, int n, bool commit, bool record, bool keep_norm,
-                      int32_t* chosen_out) {
+static int run_single(kss_ctx* ctx, const PlanNeeds& need, const DevPods& dp, int n, bool commit, bool record,
+                      bool keep_norm, uint32_t flags, int32_t* chosen_out) {
   const size_t N = (size_t)ctx->dc.N;
   const SlotLayout SL(N);
   const int nslots = record ? std::max(n, 1) : 1;
@@ -529,6 +690,21 @@ static int run_single(kss_ctx* ctx, const DevPods& dp, int n, bool commit, bool 
   if (rc) return rc;
   rc = ctx->chosen_buf.ensure(sizeof(int32_t) * (size_t)std::max(n, 1));
   if (rc) return rc;
+  // shard count: ~nodes_per_shard nodes per workgroup, at most one workgroup per CU
+  int W = std::max(1, std::min(ctx->n_cu, (int)((N + ctx->nodes_per_shard - 1) / ctx->nodes_per_shard)));
+  if (ctx->force_w > 0) W = std::min(ctx->force_w, ctx->n_cu);
+  if (flags & KSS_SCHED_FORCE_SINGLE_WG) W = 1;
+  if (flags & KSS_SCHED_FORCE_MULTI_WG) W = std::max(W, std::min(4, ctx->n_cu));
+  W = std::max(1, std::min(W, std::max(1, (int)N)));
+  const int w_min = (int)((N + KSS_MAX_NPT * KSS_MAX_THREADS - 1) / (KSS_MAX_NPT * KSS_MAX_THREADS));
+  W = std::max(W, w_min);
+  if (W > 1 && need.xw > XW_MAX) {
+    if (w_min > 1) return fail(KSS_E_UNSUPPORTED, "topology histograms too large for a sharded cluster");
+    W = 1;  // exchange payload too large for granules: one workgroup
+  }
+  if (W > ctx->n_cu) return fail(KSS_E_UNSUPPORTED, "cluster too large for one device");
+  Geometry g;
+  if (!pick_geometry((int)N, W, ctx->pref_threads, g)) return fail(KSS_E_UNSUPPORTED, "no geometry for this cluster");
   DevJob job{};
   job.c = ctx->dc;
   job.P = dp;
@@ -542,21 +718,53 @@ static int run_single(kss_ctx* ctx, const DevPods& dp, int n, bool commit, bool 
   job.meta = (PodMeta*)ctx->meta_buf.p;
   rc = ctx->job_buf.ensure(sizeof(DevJob));
   if (rc) return rc;
+  rc = ctx->err_buf.ensure(16);
+  if (rc) return rc;
+  unsigned long long* gran = nullptr;
+  if (g.W > 1) {
+    const size_t gb = sizeof(unsigned long long) * 2 * (size_t)g.W * 2 * XW_MAX;
+    rc = ctx->gran_buf.ensure(gb);
+    if (rc) return rc;
+    gran = (unsigned long long*)ctx->gran_buf.p;
+    HIP_TRY(hipMemsetAsync(gran, 0, gb, ctx->stream));  // every polled word zeroed before every launch
+  }
+  HIP_TRY(hipMemsetAsync(ctx->err_buf.p, 0, 16, ctx->stream));
   HIP_TRY(hipMemcpyAsync(ctx->job_buf.p, &job, sizeof(DevJob), hipMemcpyHostToDevice, ctx->stream));
   HIP_TRY(hipEventRecord(ctx->ev0, ctx->stream));
-  hipLaunchKernelGGL(k_schedule, dim3(1), dim3(block_threads((int)N)), 0, ctx->stream, (const DevJob*)ctx->job_buf.p,
-                     ctx->prof);
-  HIP_TRY(hipGetLastError());
+  unsigned long long* stamps = nullptr;
+  const size_t stamp_bytes = sizeof(unsigned long long) * 8 * KSS_NSTAMP_PODS;
+  if (ctx->stamps_file) {
+    if ((rc = ctx->stamp_buf.ensure(stamp_bytes))) return rc;
+    stamps = (unsigned long long*)ctx->stamp_buf.p;
+    HIP_TRY(hipMemsetAsync(stamps, 0, stamp_bytes, ctx->stream));
+  }
+  rc = launch_schedule(ctx->stream, g, 1, std::max(need.bins_cap, 0), need.general, ctx->dc.n_keys, (const DevJob*)ctx->job_buf.p,
+                       ctx->prof, gran, (int*)ctx->err_buf.p, stamps);
+  if (rc) return rc;
   HIP_TRY(hipEventRecord(ctx->ev1, ctx->stream));
   HIP_TRY(hipStreamSynchronize(ctx->stream));
   float ms = 0;
   HIP_TRY(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
   ctx->last_ms = ms;
   ctx->last_launches = 1;
+  ctx->last_geom[0] = g.W;
+  ctx->last_geom[1] = g.threads;
+  ctx->last_geom[2] = g.npt;
+  int errw = 0;
+  HIP_TRY(hipMemcpy(&errw, ctx->err_buf.p, sizeof(int), hipMemcpyDeviceToHost));
+  if (errw) return fail(KSS_E_DEVICE, "shard exchange timed out (workgroups not co-resident?)");
   ctx->meta_host.resize((size_t)std::max(n, 1));
   HIP_TRY(hipMemcpy(ctx->meta_host.data(), ctx->meta_buf.p, sizeof(PodMeta) * (size_t)std::max(n, 1), hipMemcpyDeviceToHost));
   if (chosen_out && n) HIP_TRY(hipMemcpy(chosen_out, ctx->chosen_buf.p, sizeof(int32_t) * n, hipMemcpyDeviceToHost));
   ctx->recorded = record ? n : (n > 0 ? 1 : 0);
+  if (stamps) {
+    std::vector<unsigned long long> h(8 * KSS_NSTAMP_PODS);
+    HIP_TRY(hipMemcpy(h.data(), stamps, stamp_bytes, hipMemcpyDeviceToHost));
+    if (FILE* f = fopen(ctx->stamps_file, "ab")) {
+      fwrite(h.data(), 8, h.size(), f);
+      fclose(f);
+    }
+  }
   return 0;
 }
 
@@ -591,7 +799,8 @@ int kss_eval_pod(kss_ctx* ctx, const kss_podset* ps, int32_t pod_index, kss_pod_
   one.n_pods = 1;
   rc = upload_podset(ctx->stream, ctx->tmp_pod_buf, &one, ctx->tdp);
   if (rc) return rc;
-  rc = run_single(ctx, ctx->tdp, 1, /*commit=*/false, /*record=*/false, /*keep_norm=*/true, nullptr);
+  const PlanNeeds need = plan_needs(ctx->key_card_h.data(), ctx->key_flags_h.data(), &one, 1);
+  rc = run_single(ctx, need, ctx->tdp, 1, /*commit=*/false, /*record=*/false, /*keep_norm=*/true, 0, nullptr);
   if (rc) return rc;
   return copy_slot(ctx, 0, ctx->meta_host[0], out);
 }
@@ -641,7 +850,8 @@ int kss_schedule_batch(kss_ctx* ctx, const kss_podset* ps, int32_t n, uint32_t f
   rc = upload_podset(ctx->stream, ctx->pod_buf, ps, ctx->dp);
   if (rc) return rc;
   ctx->staged_n = ps->n_pods;
-  rc = run_single(ctx, ctx->dp, n, /*commit=*/true, record, /*keep_norm=*/record, chosen_out);
+  ctx->staged_need = plan_needs(ctx->key_card_h.data(), ctx->key_flags_h.data(), ps, ps->n_pods);
+  rc = run_single(ctx, ctx->staged_need, ctx->dp, n, /*commit=*/true, record, /*keep_norm=*/record, flags, chosen_out);
   if (rc) return rc;
   for (int i = 0; i < n; i++)
     if (ctx->meta_host[i].status == 4) return fail(KSS_E_UNSUPPORTED, "pod program exceeds the device path's per-pod limits");
@@ -658,6 +868,7 @@ int kss_stage_pods(kss_ctx* ctx, const kss_podset* ps) {
   if (rc) return rc;
   HIP_TRY(hipStreamSynchronize(ctx->stream));
   ctx->staged_n = ps->n_pods;
+  ctx->staged_need = plan_needs(ctx->key_card_h.data(), ctx->key_flags_h.data(), ps, ps->n_pods);
   return 0;
 }
 
@@ -668,7 +879,7 @@ int kss_run_staged(kss_ctx* ctx, int32_t n, uint32_t flags, int32_t* chosen_out)
   if (record && n > ctx->cfg.max_pods_record) return fail(KSS_E_INVAL, "record capacity (max_pods_record) exceeded");
   std::lock_guard<std::mutex> lk(ctx->mu);
   HIP_TRY(hipSetDevice(ctx->cfg.device));
-  int rc = run_single(ctx, ctx->dp, n, /*commit=*/true, record, /*keep_norm=*/record, chosen_out);
+  int rc = run_single(ctx, ctx->staged_need, ctx->dp, n, /*commit=*/true, record, /*keep_norm=*/record, flags, chosen_out);
   if (rc) return rc;
   for (int i = 0; i < n; i++)
     if (ctx->meta_host[i].status == 4) return fail(KSS_E_UNSUPPORTED, "pod program exceeds the device path's per-pod limits");
@@ -687,6 +898,12 @@ int kss_last_timing(kss_ctx* ctx, double* device_ms, int32_t* launches) {
   if (!ctx) return fail(KSS_E_INVAL, "null ctx");
   if (device_ms) *device_ms = ctx->last_ms;
   if (launches) *launches = ctx->last_launches;
+  return 0;
+}
+
+int kss_last_geometry(kss_ctx* ctx, int32_t* out3) {
+  if (!ctx || !out3) return fail(KSS_E_INVAL, "bad arguments");
+  for (int i = 0; i < 3; i++) out3[i] = ctx->last_geom[i];
   return 0;
 }
 
@@ -775,20 +992,36 @@ int kss_schedule_scenarios(int32_t device, const kss_profile* prof, int32_t n_sc
         hipStreamSynchronize(st) != hipSuccess)
       rc = fail(KSS_E_DEVICE, "job upload failed");
   }
+  PlanNeeds need;
+  for (int sc = 0; sc < n_scen; sc++) {
+    const PlanNeeds q = plan_needs(clusters[sc].key_card, clusters[sc].key_flags, &podsets[sc], podsets[sc].n_pods);
+    need.bins_cap = std::max(need.bins_cap, q.bins_cap);
+    need.general |= q.general;
+  }
+  int maxN = 0;
+  for (int sc = 0; sc < n_scen; sc++) maxN = std::max(maxN, clusters[sc].n_nodes);
+  int pref = 256;
+  if (const char* e = getenv("KSS_THREADS")) pref = std::min(KSS_MAX_THREADS, std::max(64, atoi(e)));
+  Geometry g;
+  if (!rc && !pick_geometry(maxN, 1, pref, g)) rc = fail(KSS_E_UNSUPPORTED, "scenario cluster too large for one workgroup");
+  int* err = nullptr;
+  if (!rc && hipMalloc(&err, 16) != hipSuccess) rc = fail(KSS_E_NOMEM, "error word allocation failed");
   if (!rc) {
+    hipMemsetAsync(err, 0, 16, st);
     hipEventCreate(&e0);
     hipEventCreate(&e1);
-    int maxN = 0;
-    for (int s = 0; s < n_scen; s++) maxN = std::max(maxN, clusters[s].n_nodes);
     hipEventRecord(e0, st);
-    hipLaunchKernelGGL(k_schedule, dim3(n_scen), dim3(block_threads(maxN)), 0, st, (const DevJob*)(arena + job_off), *prof);
-    if (hipGetLastError() != hipSuccess) rc = fail(KSS_E_DEVICE, "k_schedule launch failed");
+    int max_keys = 0;
+    for (int sc = 0; sc < n_scen; sc++) max_keys = std::max(max_keys, clusters[sc].n_label_keys);
+    rc = launch_schedule(st, g, n_scen, need.bins_cap, need.general, max_keys, (const DevJob*)(arena + job_off), *prof,
+                         nullptr, err);
     hipEventRecord(e1, st);
-    if (hipStreamSynchronize(st) != hipSuccess) rc = fail(KSS_E_DEVICE, "k_schedule failed");
+    if (hipStreamSynchronize(st) != hipSuccess && !rc) rc = fail(KSS_E_DEVICE, "k_schedule failed");
     float ms = 0;
     hipEventElapsedTime(&ms, e0, e1);
     if (device_ms) *device_ms = ms;
   }
+  if (err) hipFree(err);
   if (!rc) {
     size_t o = 0;
     for (int s = 0; s < n_scen && !rc; s++) {

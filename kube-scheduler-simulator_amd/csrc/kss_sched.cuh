@@ -1,18 +1,36 @@
-// kss_sched.cuh — the scheduling cycle for one pod over all nodes of one cluster,
-// executed by ONE workgroup (all reductions are workgroup-level: LDS + s_barrier,
-// no inter-workgroup communication, so no spin can hang the device).
+// kss_sched.cuh — the scheduling cycle for one pod over all nodes of one cluster.
 //
-// Per pod (schedulePod):
+// A cluster is served by W workgroups ("shards"); shard w owns the canonical node
+// range [lo, hi) and is the only workgroup that reads or writes those nodes'
+// mutable state, so node state never crosses workgroups.  Each lane owns NPT node
+// slots (n = lo + k*blockDim + tid) and keeps every per-node intermediate of the
+// cycle (verdict, raw scores) in registers: nothing per node goes to HBM unless the
+// caller asked for a result record.
+//
+// Per pod (schedulePod) the phases are separated by cluster
+// reductions ("exchanges"):
 //   stats   PreFilter of PodTopologySpread (calPreFilterState) and InterPodAffinity
 //           (existing / incoming (anti-)affinity counts) and InterPodAffinity PreScore
 //           topologyScore: LDS-privatised histograms over topology domains for
 //           non-unique keys; unique keys (hostname) are evaluated in place.
+//           -> exchange: histogram SUM, presence OR, unique-key minima.
 //   filter  findNodesThatPassFilters (first failing plugin wins) + raw Score of every
-//           plugin on feasible nodes; reductions: #feasible, max TT/NA, IPA min/max,
+//           plugin on feasible nodes -> exchange: #feasible, max TT/NA, IPA min/max,
 //           PTS ignored / domain presence.
-//   pts     PodTopologySpread Score (needs the feasible-domain count) + min/max.
-//   select  NormalizeScore, weights, TotalScore, selectHost (max total, lowest index).
-//   commit  Cache.AssumePod -> NodeInfo.AddPod on the chosen row.
+//   pts     PodTopologySpread Score (needs the feasible-domain count) -> exchange min/max.
+//   select  NormalizeScore, weights, TotalScore, selectHost (max total, lowest index)
+//           -> exchange: packed (total, ~index) MAX.
+//   commit  Cache.AssumePod -> NodeInfo.AddPod on the chosen row, by its owner shard.
+//
+// With W == 1 an exchange is a plain workgroup reduction (LDS + s_barrier).  With
+// W > 1 wave 0 of every shard publishes the workgroup's partials as 8-byte
+// {epoch, 32-bit half} granules with agent-scope (sc1) stores and sweeps every
+// shard's granules with agent-scope loads until all tags carry the current epoch
+// (MI355X_MICROARCH.md, "R2: the data is the flag"; no fences, no counters).  The
+// granule slots are double-buffered by epoch parity: a shard can only publish
+// epoch e+2 after every shard published e+1, i.e. after every shard finished
+// reading epoch e.  Every spin is bounded; a timeout sets an error word and the
+// workgroup leaves the kernel.
 #pragma once
 #include "kss_eval.cuh"
 
@@ -21,10 +39,17 @@ namespace kss {
 constexpr int MAXH = 4;  // hard spread constraints per pod on the device path
 constexpr int MAXS = 4;  // soft spread constraints
 constexpr int MAXK = 4;  // distinct inter-pod-affinity topology keys
-constexpr int LDS_BINS = 4096;  // int64 histogram bins per workgroup
 constexpr int MAXWAVES = 16;
-constexpr int NRED = 16;  // values per block reduction
+constexpr int NSCAL = 16;      // scalar slots at the head of the exchange vector
+constexpr int LDS_BINS = 4096; // histogram + presence values per pod (device limit)
+constexpr int XW_MAX = 256;    // exchange length allowed when W > 1 (host-checked)
+constexpr unsigned SPIN_LIMIT = 1u << 20;
+constexpr int KSS_MAX_THREADS = 512;  // workgroup size cap (2 waves per SIMD: 256 VGPRs per lane)
+constexpr int KSS_NSTAMP_PODS = 256;  // pods with diagnostic phase stamps per launch
+constexpr int KSS_MAX_NPT = 6;
+constexpr size_t KSS_LDS_BUDGET = 160 * 1024;  // LDS per workgroup (one workgroup may own a whole CU's LDS)        // node slots per lane (LDS: 40 B per slot)
 
+enum { OP_SUM = 0, OP_MAX = 1, OP_MIN = 2, OP_OR = 3 };
 enum { SOFT_HOST = 0, SOFT_DIRECT = 1, SOFT_HIST = 2 };
 
 // Per-pod plan, identical in every lane (computed from wave-uniform pod data).
@@ -39,23 +64,32 @@ struct Plan {
   int key_off[MAXK];   // 4 consecutive histograms (x, a, b, s), -1 = unique (direct)
   int key_bins[MAXK];
   int total_bins;
-  int total_pbins;
+  int hard_pbins;      // presence bins of hard constraints: [0, hard_pbins)
+  int total_pbins;     // soft presence bins: [hard_pbins, total_pbins)
   bool need_stats;
 };
 
-struct Shared {
-  long long bins[LDS_BINS];
-  unsigned int pres[LDS_BINS];
-  long long red[MAXWAVES][NRED];
+// Dynamic LDS image (Guideline 17: one 16-byte aligned dynamic region, no statics).
+struct SharedHdr {
+  long long red[MAXWAVES][NSCAL];
+  kss_pod pod;  // the current pod's record, copied once per pod
+  Plan plan;    // computed by lane 0 of the workgroup each pod, read by all
+  int plan_ok;
+  int abort;
+  int pad[2];
 };
 
-// Output slot for one pod: per-node verdicts and scores (also the record format).
+__device__ __forceinline__ SharedHdr& shdr(long long* smem) { return *reinterpret_cast<SharedHdr*>(smem); }
+// exchange vector: [0, NSCAL) scalars, then bins, then presence bins
+__device__ __forceinline__ long long* xvec(long long* smem) { return smem + sizeof(SharedHdr) / 8; }
+
+// Output slot for one pod: per-node verdicts and scores (the record format).
 struct Slot {
   uint8_t* fail;
   uint16_t* detail;
   int64_t* raw;   // [KSS_NSCORE][N]
-  int64_t* norm;  // [KSS_NSCORE][N]  (nullptr: not kept)
-  int64_t* total; // [N]              (nullptr: not kept)
+  int64_t* norm;  // [KSS_NSCORE][N]
+  int64_t* total; // [N]
 };
 
 struct PodMeta {
@@ -63,43 +97,160 @@ struct PodMeta {
   int64_t best_total;
 };
 
+// Shard geometry + exchange context of one workgroup.
+struct Shard {
+  int lo, hi;       // owned local node range
+  int W, w;         // shards per cluster, this shard
+  unsigned epoch;   // exchanges done so far in this launch (uniform over the cluster)
+  unsigned long long* gran;  // this cluster's granules: [2][W][2*XW_MAX]
+  int* err;         // launch error word (timeouts)
+  unsigned long long* stamps;  // KSS_STAMPS diagnostics: phase timestamps of this pod, or null
+};
+
+// Diagnostic phase stamps (s_memrealtime, 100 MHz), lane 0 of shard 0 only.
+#define KSS_STAMP(S, i)                                              \
+  do {                                                               \
+    if ((S).stamps && threadIdx.x == 0) (S).stamps[i] = wall_clock64(); \
+  } while (0)
+
+__device__ __forceinline__ long long op_apply(int op, long long a, long long b) {
+  if (op == OP_SUM) return a + b;
+  if (op == OP_MAX) return b > a ? b : a;
+  if (op == OP_MIN) return b < a ? b : a;
+  return a | b;
+}
+
+__device__ __forceinline__ long long op_identity(int op) {
+  if (op == OP_MAX) return INT64_MIN;
+  if (op == OP_MIN) return INT64_MAX;
+  return 0;
+}
+
 __device__ __forceinline__ long long wave_reduce(long long v, int op) {
-  // op: 0 sum, 1 max, 2 min, 3 or
 #pragma unroll
-  for (int m = 32; m >= 1; m >>= 1) {
-    long long o = __shfl_xor(v, m, 64);
-    if (op == 0) v += o;
-    else if (op == 1) v = o > v ? o : v;
-    else if (op == 2) v = o < v ? o : v;
-    else v |= o;
-  }
+  for (int m = 32; m >= 1; m >>= 1) v = op_apply(op, v, __shfl_xor(v, m, 64));
   return v;
 }
 
-// Reduce up to NRED values across the workgroup; every lane gets the results.
+// Cross-shard part of an exchange, run by wave 0 only.  Payload j maps to
+// xv[j] (j < K), then xv[NSCAL+sum_lo ...] (SUM), then xv[NSCAL+or_lo ...] (OR).
+// Publish: two {epoch, half} granules per value.  Sweep: the W*M (shard, value)
+// pairs are spread over the 64 lanes, XB pairs per lane per chunk with all loads in
+// flight at once; a chunk is re-read until every tag carries the epoch (a matched
+// granule is final: it can only change at epoch+2), then combined into the LDS
+// value with a 64-bit LDS atomic of the value's operator.
+__device__ __noinline__ void shard_exchange(long long* smem, unsigned long long* gran, int W, int wself, unsigned epoch,
+                                            int* err, int K, unsigned opbits, int sum_lo, int ns, int or_lo, int no) {
+  constexpr int XB = 8;
+  long long* xv = xvec(smem);
+  const int lane = threadIdx.x & 63;
+  const int M = K + ns + no;
+  const size_t per = 2 * (size_t)XW_MAX;
+  unsigned long long* mine = gran + ((size_t)(epoch & 1) * W + wself) * per;
+  auto slot = [&](int j) -> long long* {
+    if (j < K) return xv + j;
+    if (j < K + ns) return xv + NSCAL + sum_lo + (j - K);
+    return xv + NSCAL + or_lo + (j - K - ns);
+  };
+  auto opof = [&](int j) { return j < K ? (int)((opbits >> (2 * j)) & 3u) : (j < K + ns ? OP_SUM : OP_OR); };
+  const unsigned long long tag = (unsigned long long)epoch << 32;
+  for (int j = lane; j < M; j += 64) {
+    long long* sl = slot(j);
+    const unsigned long long v = (unsigned long long)*sl;
+    __hip_atomic_store(mine + 2 * j, tag | (v & 0xFFFFFFFFull), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(mine + 2 * j + 1, tag | (v >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *sl = op_identity(opof(j));  // the own contribution comes back through the sweep
+  }
+  const unsigned long long* base = gran + (size_t)(epoch & 1) * W * per;
+  const int Q = W * M;
+  for (int q0 = 0; q0 < Q; q0 += 64 * XB) {
+    unsigned long long lo[XB], hi[XB];
+    for (unsigned spins = 0;; ++spins) {
+      bool ok = true;
+#pragma unroll
+      for (int b = 0; b < XB; b++) {
+        const int q = q0 + b * 64 + lane;
+        lo[b] = hi[b] = tag;
+        if (q < Q) {
+          const int w = q / M, j = q - w * M;
+          const unsigned long long* g = base + (size_t)w * per + 2 * j;
+          lo[b] = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          hi[b] = __hip_atomic_load(g + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      }
+#pragma unroll
+      for (int b = 0; b < XB; b++) ok &= ((lo[b] >> 32) == epoch) & ((hi[b] >> 32) == epoch);
+      if (__all(ok)) break;
+      if (spins >= SPIN_LIMIT) {
+        if (lane == 0) {
+          shdr(smem).abort = 1;
+          __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        return;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+#pragma unroll
+    for (int b = 0; b < XB; b++) {
+      const int q = q0 + b * 64 + lane;
+      if (q < Q) {
+        const int w = q / M, j = q - w * M;
+        const long long v = (long long)((hi[b] << 32) | (lo[b] & 0xFFFFFFFFull));
+        long long* sl = slot(j);
+        switch (opof(j)) {
+          case OP_SUM: atomicAdd((unsigned long long*)sl, (unsigned long long)v); break;
+          case OP_MAX: atomicMax(sl, v); break;
+          case OP_MIN: atomicMin(sl, v); break;
+          default: atomicOr((unsigned long long*)sl, (unsigned long long)v); break;
+        }
+      }
+    }
+  }
+}
+
+// Cluster reduction of K per-thread scalars v[] (ops[]), plus (W > 1 only) the
+// cross-shard combination of the LDS bin ranges [sum_lo, sum_lo+ns) (SUM) and
+// [or_lo, or_lo+no) (OR) of the exchange vector.  local = true reduces within the
+// workgroup only (values already identical across shards).  On return v[] holds
+// the cluster-wide results in every lane; returns false if the launch aborted.
 template <int K>
-__device__ __forceinline__ void block_reduce(Shared& sh, long long (&v)[K], const int (&op)[K]) {
-  static_assert(K <= NRED, "too many values");
+__device__ __forceinline__ bool cluster_reduce(long long* smem, Shard& S, long long (&v)[K], const int (&ops)[K],
+                                               int sum_lo = 0, int ns = 0, int or_lo = 0, int no = 0,
+                                               bool local = false) {
+  static_assert(K <= NSCAL, "too many values");
+  SharedHdr& h = shdr(smem);
+  long long* xv = xvec(smem);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
 #pragma unroll
   for (int k = 0; k < K; k++) {
-    long long r = wave_reduce(v[k], op[k]);
-    if (lane == 0) sh.red[wave][k] = r;
+    const long long r = wave_reduce(v[k], ops[k]);
+    if (lane == 0) h.red[wave][k] = r;
   }
   __syncthreads();
+  if (threadIdx.x < K) {
+    const int k = threadIdx.x;
+    int op = OP_SUM;
 #pragma unroll
-  for (int k = 0; k < K; k++) {
-    long long r = sh.red[0][k];
-    for (int w = 1; w < nw; w++) {
-      long long o = sh.red[w][k];
-      if (op[k] == 0) r += o;
-      else if (op[k] == 1) r = o > r ? o : r;
-      else if (op[k] == 2) r = o < r ? o : r;
-      else r |= o;
-    }
-    v[k] = r;
+    for (int q = 0; q < K; q++)
+      if (q == k) op = ops[q];
+    long long r = h.red[0][k];
+    for (int w = 1; w < nw; w++) r = op_apply(op, r, h.red[w][k]);
+    xv[k] = r;
   }
   __syncthreads();
+  if (S.W > 1 && !local) {
+    unsigned opbits = 0;
+#pragma unroll
+    for (int k = 0; k < K; k++) opbits |= (unsigned)ops[k] << (2 * k);
+    ++S.epoch;
+    if (wave == 0) shard_exchange(smem, S.gran, S.W, S.w, S.epoch, S.err, K, opbits, sum_lo, ns, or_lo, no);
+    __syncthreads();
+    if (h.abort) return false;
+  }
+#pragma unroll
+  for (int k = 0; k < K; k++) v[k] = xv[k];
+  __syncthreads();  // xv[0..K) may be rewritten by the next reduction
+  return true;
 }
 
 __device__ __forceinline__ bool key_unique(const DevCluster& c, int key) {
@@ -107,7 +258,8 @@ __device__ __forceinline__ bool key_unique(const DevCluster& c, int key) {
 }
 
 // Returns false if the pod needs more LDS bins / slots than the device path has.
-__device__ __forceinline__ bool make_plan(const DevCluster& c, const DevPods& P, const kss_pod& p, Plan& pl) {
+__device__ __forceinline__ bool make_plan(const DevCluster& c, const DevPods& P, const kss_pod& p, Plan& pl,
+                                          int bins_cap) {
   pl.n_hard = p.n_hard;
   pl.n_soft = p.n_soft;
   pl.n_keys = 0;
@@ -128,6 +280,7 @@ __device__ __forceinline__ bool make_plan(const DevCluster& c, const DevPods& P,
       poff += c.key_card[key] + 1;
     }
   }
+  pl.hard_pbins = poff;
   for (int i = 0; i < p.n_soft; i++) {
     const int key = sp[p.n_hard + i].key;
     if (c.key_flags[key] & KSS_KEY_HOSTNAME) {
@@ -165,7 +318,7 @@ __device__ __forceinline__ bool make_plan(const DevCluster& c, const DevPods& P,
   }
   pl.total_bins = off;
   pl.total_pbins = poff;
-  return off <= LDS_BINS && poff <= LDS_BINS;
+  return off + poff <= bins_cap;
 }
 
 __device__ __forceinline__ int slot_of(const Plan& pl, int key) {
@@ -178,7 +331,7 @@ __device__ __forceinline__ int slot_of(const Plan& pl, int key) {
 __device__ __forceinline__ bool spread_policy_ok(const DevCluster& c, const DevPods& P, const kss_pod& p,
                                                  const kss_spread& s, int n) {
   if ((s.flags & KSS_SPREAD_POLICY_AFFINITY_HONOR) && !required_affinity(c, P, p, n)) return false;
-  if ((s.flags & KSS_SPREAD_POLICY_TAINTS_HONOR) && first_untolerated(c, p, n) >= 0) return false;
+  if ((s.flags & KSS_SPREAD_POLICY_TAINTS_HONOR) && first_untolerated(c, p, n, taint_hard_of(c, n)) >= 0) return false;
   return true;
 }
 
@@ -193,23 +346,26 @@ __device__ __forceinline__ int64_t spread_count(const DevCluster& c, const DevPo
 }
 
 // ---------------------------------------------------------------------------
-// stats pass for node n: accumulate LDS histograms and per-lane partials
-//   part[0..MAXH) : min count over eligible nodes for unique hard keys
-//   flags bit0 ex, bit1 aff, bit2 anti, bit3 score nonempty
+// stats pass for node n: accumulate LDS histograms (bins = xv+NSCAL, pres =
+// bins+total_bins) and per-lane partials: hard_min[] for unique hard keys;
+// flags bit0 ex, bit1 aff, bit2 anti, bit3 score nonempty
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ void stats_node(const DevCluster& c, const DevPods& P, const kss_pod& p, const Plan& pl,
-                                           Shared& sh, int n, long long* hard_min, long long& flags) {
+                                           long long* bins, long long* pres, int n, long long (&hard_min)[MAXH],
+                                           long long& flags) {
   const kss_spread* sp = P.spreads + p.spread_off;
   if (p.n_hard > 0 && has_keys(c, sp, p.n_hard, n)) {  // nodeLabelsMatchSpreadConstraints
-    for (int i = 0; i < p.n_hard; i++) {
+#pragma unroll
+    for (int i = 0; i < MAXH; i++) {
+      if (i >= p.n_hard) break;
       if (!spread_policy_ok(c, P, p, sp[i], n)) continue;
       const int64_t cnt = spread_count(c, P, sp[i], n);
       if (pl.hard_off[i] < 0) {
         hard_min[i] = cnt < hard_min[i] ? cnt : hard_min[i];
       } else {
         const int d = label_of(c, sp[i].key, n);
-        atomicAdd((unsigned long long*)&sh.bins[pl.hard_off[i] + d], (unsigned long long)cnt);
-        sh.pres[pl.hard_poff[i] + d] = 1u;  // the pair (key, value) exists
+        atomicAdd((unsigned long long*)&bins[pl.hard_off[i] + d], (unsigned long long)cnt);
+        pres[pl.hard_poff[i] + d] = 1;  // the pair (key, value) exists
       }
     }
   }
@@ -223,13 +379,13 @@ __device__ __forceinline__ void stats_node(const DevCluster& c, const DevPods& P
         int d = label_of(c, so[i].key, n);
         if (d < 0) d = c.key_empty[so[i].key];
         const int64_t cnt = spread_count(c, P, so[i], n);
-        if (cnt) atomicAdd((unsigned long long*)&sh.bins[pl.soft_off[i] + d], (unsigned long long)cnt);
+        if (cnt) atomicAdd((unsigned long long*)&bins[pl.soft_off[i] + d], (unsigned long long)cnt);
       }
     }
   }
   if (p.ipa_len > 0) {
     const kss_ipa* ip = P.ipa + p.ipa_off;
-    const bool has_labels = (c.node_flags[n] & KSS_NODE_HAS_LABELS) != 0;
+    const bool has_labels = (node_flags_of(c, n) & KSS_NODE_HAS_LABELS) != 0;
     const size_t N = (size_t)c.N;
     for (int e = 0; e < p.ipa_len; e++) {
       const kss_ipa& en = ip[e];
@@ -243,13 +399,13 @@ __device__ __forceinline__ void stats_node(const DevCluster& c, const DevPods& P
         const int32_t* mat = en.kind == KSS_IPA_SCORE_CLASS ? c.class_count : c.term_count;
         const int64_t v = sum_rows(mat, N, P.ints + en.row_off, en.row_len, n);
         if (v > 0) flags |= 8;
-        if (base >= 0 && v) atomicAdd((unsigned long long*)&sh.bins[base + 3 * nb + d], (unsigned long long)(v * en.coef));
+        if (base >= 0 && v) atomicAdd((unsigned long long*)&bins[base + 3 * nb + d], (unsigned long long)(v * en.coef));
       } else {
         const int32_t* mat = en.kind == KSS_IPA_EXISTING_ANTI ? c.term_count : c.class_count;
         const int64_t v = sum_rows(mat, N, P.ints + en.row_off, en.row_len, n);
         const int h = en.kind == KSS_IPA_EXISTING_ANTI ? 0 : (en.kind == KSS_IPA_REQ_AFFINITY ? 1 : 2);
         if (v > 0) flags |= (1ll << h);
-        if (base >= 0 && v) atomicAdd((unsigned long long*)&sh.bins[base + h * nb + d], (unsigned long long)v);
+        if (base >= 0 && v) atomicAdd((unsigned long long*)&bins[base + h * nb + d], (unsigned long long)v);
       }
     }
   }
@@ -257,8 +413,8 @@ __device__ __forceinline__ void stats_node(const DevCluster& c, const DevPods& P
 
 // value of an IPA histogram h (0 x, 1 a, 2 b) at node n's domain for key slot k
 __device__ __forceinline__ int64_t ipa_value(const DevCluster& c, const DevPods& P, const kss_pod& p, const Plan& pl,
-                                             const Shared& sh, int k, int h, int d, int n) {
-  if (pl.key_off[k] >= 0) return sh.bins[pl.key_off[k] + h * pl.key_bins[k] + d];
+                                             const long long* bins, int k, int h, int d, int n) {
+  if (pl.key_off[k] >= 0) return bins[pl.key_off[k] + h * pl.key_bins[k] + d];
   // unique key: the domain holds node n only -> recompute n's own contribution
   const int kind = h == 0 ? KSS_IPA_EXISTING_ANTI : (h == 1 ? KSS_IPA_REQ_AFFINITY : KSS_IPA_REQ_ANTI);
   const kss_ipa* ip = P.ipa + p.ipa_off;
@@ -273,14 +429,16 @@ __device__ __forceinline__ int64_t ipa_value(const DevCluster& c, const DevPods&
 
 // PodTopologySpread.Filter (hard constraints) — returns detail+1 on failure, 0 on pass
 __device__ __forceinline__ int filter_pts(const DevCluster& c, const DevPods& P, const kss_pod& p, const Plan& pl,
-                                          const Shared& sh, const long long* hard_min, int n) {
+                                          const long long* bins, const long long (&hard_min)[MAXH], int n) {
   const kss_spread* sp = P.spreads + p.spread_off;
-  for (int i = 0; i < p.n_hard; i++) {
+#pragma unroll
+  for (int i = 0; i < MAXH; i++) {
+    if (i >= p.n_hard) break;
     const int d = label_of(c, sp[i].key, n);
     if (d < 0) return 1 + KSS_PTS_MISSING_LABEL;
     int64_t match;
     if (pl.hard_off[i] >= 0) {
-      match = sh.bins[pl.hard_off[i] + d];
+      match = bins[pl.hard_off[i] + d];
     } else {
       match = (has_keys(c, sp, p.n_hard, n) && spread_policy_ok(c, P, p, sp[i], n)) ? spread_count(c, P, sp[i], n) : 0;
     }
@@ -292,7 +450,7 @@ __device__ __forceinline__ int filter_pts(const DevCluster& c, const DevPods& P,
 
 // InterPodAffinity.Filter — returns detail+1 on failure, 0 on pass.  flags: bit0 ex, bit1 aff, bit2 anti
 __device__ __forceinline__ int filter_ipa(const DevCluster& c, const DevPods& P, const kss_pod& p, const Plan& pl,
-                                          const Shared& sh, long long flags, int n) {
+                                          const long long* bins, long long flags, int n) {
   const kss_ipa* ip = P.ipa + p.ipa_off;
   // satisfyPodAffinity
   bool have = false, exist = true;
@@ -302,7 +460,7 @@ __device__ __forceinline__ int filter_ipa(const DevCluster& c, const DevPods& P,
     const int d = label_of(c, ip[e].key, n);
     if (d < 0) return 1 + KSS_IPA_AFFINITY;
     const int k = slot_of(pl, ip[e].key);
-    if (ipa_value(c, P, p, pl, sh, k, 1, d, n) <= 0) exist = false;
+    if (ipa_value(c, P, p, pl, bins, k, 1, d, n) <= 0) exist = false;
   }
   if (have && !exist && !(!(flags & 2) && (p.flags & KSS_POD_IPA_SELF_MATCH))) return 1 + KSS_IPA_AFFINITY;
   // satisfyPodAntiAffinity
@@ -312,7 +470,7 @@ __device__ __forceinline__ int filter_ipa(const DevCluster& c, const DevPods& P,
       const int d = label_of(c, ip[e].key, n);
       if (d < 0) continue;
       const int k = slot_of(pl, ip[e].key);
-      if (ipa_value(c, P, p, pl, sh, k, 2, d, n) > 0) return 1 + KSS_IPA_ANTI_AFFINITY;
+      if (ipa_value(c, P, p, pl, bins, k, 2, d, n) > 0) return 1 + KSS_IPA_ANTI_AFFINITY;
     }
   }
   // satisfyExistingPodsAntiAffinity
@@ -322,7 +480,7 @@ __device__ __forceinline__ int filter_ipa(const DevCluster& c, const DevPods& P,
       const int d = label_of(c, ip[e].key, n);
       if (d < 0) continue;
       const int k = slot_of(pl, ip[e].key);
-      if (ipa_value(c, P, p, pl, sh, k, 0, d, n) > 0) return 1 + KSS_IPA_EXISTING_ANTI_AFFINITY;
+      if (ipa_value(c, P, p, pl, bins, k, 0, d, n) > 0) return 1 + KSS_IPA_EXISTING_ANTI_AFFINITY;
     }
   }
   return 0;
@@ -330,14 +488,14 @@ __device__ __forceinline__ int filter_ipa(const DevCluster& c, const DevPods& P,
 
 // InterPodAffinity.Score: Σ topologyScore[key][node value] over keys the node has
 __device__ __forceinline__ int64_t ipa_score(const DevCluster& c, const DevPods& P, const kss_pod& p, const Plan& pl,
-                                             const Shared& sh, int n) {
+                                             const long long* bins, int n) {
   int64_t s = 0;
-  const bool has_labels = (c.node_flags[n] & KSS_NODE_HAS_LABELS) != 0;
+  const bool has_labels = (node_flags_of(c, n) & KSS_NODE_HAS_LABELS) != 0;
   for (int k = 0; k < pl.n_keys; k++) {
     const int d = label_of(c, pl.key[k], n);
     if (d < 0) continue;
     if (pl.key_off[k] >= 0) {
-      s += sh.bins[pl.key_off[k] + 3 * pl.key_bins[k] + d];
+      s += bins[pl.key_off[k] + 3 * pl.key_bins[k] + d];
     } else if (has_labels) {
       const kss_ipa* ip = P.ipa + p.ipa_off;
       for (int e = 0; e < p.ipa_len; e++) {
@@ -357,31 +515,92 @@ __device__ __forceinline__ bool in_names(const DevPods& P, const kss_pod& p, int
   return false;
 }
 
+// Per-node-slot intermediates of one pod, in LDS (slot s = k*blockDim + tid).
+struct SlotArrays {
+  long long* na;   // NodeAffinity raw
+  long long* ipa;  // InterPodAffinity raw
+  long long* pts;  // PodTopologySpread raw
+  int* fail;       // verdict | ignored << 16
+  int* tt;         // TaintToleration raw
+  int* fit;        // NodeResourcesFit raw
+  int* ba;         // BalancedAllocation raw
+};
+
+__host__ __device__ inline size_t slot_arrays_bytes(int cap) { return (size_t)cap * (3 * 8 + 4 * 4); }
+// shard node cache: 10 x 8 B + 3 x 4 B per node, plus 4 B per cached label key
+__host__ __device__ inline size_t node_cache_bytes(int cap, int n_keys) { return (size_t)cap * (10 * 8 + 3 * 4 + 4 * n_keys); }
+
+__device__ __forceinline__ SlotArrays slot_arrays(long long* smem, int bins_cap, int cap) {
+  long long* b = xvec(smem) + NSCAL + bins_cap;
+  SlotArrays a;
+  a.na = b;
+  a.ipa = b + cap;
+  a.pts = b + 2 * cap;
+  int* i = reinterpret_cast<int*>(b + 3 * cap);
+  a.fail = i;
+  a.tt = i + cap;
+  a.fit = i + 2 * cap;
+  a.ba = i + 3 * cap;
+  return a;
+}
+
 // ---------------------------------------------------------------------------
-// one scheduling cycle for pod p, executed by the whole workgroup
+// one scheduling cycle for pod pi, executed by every shard of the cluster.
+// Returns false if the launch aborted (exchange timeout).
 // ---------------------------------------------------------------------------
-__device__ void schedule_pod(const DevCluster& c, const DevPods& P, const kss_profile& prof, int pi, Shared& sh,
-                             const Slot& out, PodMeta& meta, bool keep_norm) {
-  const kss_pod& p = P.pods[pi];
-  const int N = c.N;
+// GEN = false compiles the cycle without PodTopologySpread / InterPodAffinity programs
+// (the host picks it when no pod of the batch carries one): a compact kernel whose hot
+// loop stays in the instruction cache.
+template <bool GEN>
+__device__ __forceinline__ bool schedule_pod(const DevCluster& c, const DevPods& P, const kss_profile& prof, int pi, long long* smem,
+                             Shard& S, int bins_cap, int npt, const Slot* out, bool keep_norm, PodMeta& meta) {
   const int tid = threadIdx.x, nt = blockDim.x;
-  const size_t NN = (size_t)N;
+  SharedHdr& H = shdr(smem);
+  {
+    // pod record -> LDS (one coalesced copy), plan by lane 0; one barrier
+    constexpr int PD = (int)(sizeof(kss_pod) / 4);
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(P.pods + pi);
+    uint32_t* dst = reinterpret_cast<uint32_t*>(&H.pod);
+    for (int i = tid; i < PD; i += nt) dst[i] = src[i];
+    if (tid == 0) {
+      if (GEN) {
+        H.plan_ok = make_plan(c, P, P.pods[pi], H.plan, bins_cap) ? 1 : 0;
+      } else {
+        const kss_pod& q = P.pods[pi];
+        H.plan_ok = (q.n_hard | q.n_soft | q.ipa_len) == 0 ? 1 : 0;  // the host guarantees it
+        H.plan.total_bins = H.plan.hard_pbins = H.plan.total_pbins = 0;
+        H.plan.need_stats = false;
+      }
+    }
+    __syncthreads();
+  }
+  const kss_pod& p = H.pod;
+  const size_t NN = (size_t)c.N;
+  long long* xv = xvec(smem);
+  long long* bins = xv + NSCAL;
+  const SlotArrays sa = slot_arrays(smem, bins_cap, npt * nt);
   meta.chosen = -1;
   meta.n_feasible = 0;
   meta.scored = 0;
   meta.status = 0;
   meta.best_total = 0;
 
-  Plan pl;
-  const bool plan_ok = make_plan(c, P, p, pl);
+  const Plan& pl = H.plan;
+  const bool plan_ok = H.plan_ok != 0;
+  long long* pres = bins + pl.total_bins;
+  KSS_STAMP(S, 1);
   if (p.prefilter_status != 0 || !plan_ok) {
-    for (int n = tid; n < N; n += nt) {
-      out.fail[n] = KSS_F_NOT_EVALUATED;
-      out.detail[n] = 0;
+    if (out) {
+      for (int k = 0; k < npt; k++) {
+        const int n = S.lo + k * nt + tid;
+        if (n < S.hi) {
+          out->fail[n] = KSS_F_NOT_EVALUATED;
+          out->detail[n] = 0;
+        }
+      }
     }
     meta.status = !plan_ok ? 4 : (p.prefilter_status == 1 ? 2 : 3);
-    __syncthreads();
-    return;
+    return true;
   }
 
   // ---- stats -----------------------------------------------------------
@@ -389,258 +608,368 @@ __device__ void schedule_pod(const DevCluster& c, const DevPods& P, const kss_pr
   long long flags = 0;
 #pragma unroll
   for (int i = 0; i < MAXH; i++) hard_min[i] = INT32_MAX;
-  if (pl.need_stats) {
-    for (int b = tid; b < pl.total_bins; b += nt) sh.bins[b] = 0;
-    for (int b = tid; b < pl.total_pbins; b += nt) sh.pres[b] = 0;
+  if (GEN && pl.need_stats) {
+    for (int b = tid; b < pl.total_bins + pl.total_pbins; b += nt) bins[b] = 0;
     __syncthreads();
-    for (int n = tid; n < N; n += nt) stats_node(c, P, p, pl, sh, n, hard_min, flags);
-    __syncthreads();
-    // minima over present bins of non-unique hard keys
+    for (int k = 0; k < npt; k++) {
+      const int n = S.lo + k * nt + tid;
+      if (n < S.hi) stats_node(c, P, p, pl, bins, pres, n, hard_min, flags);
+    }
+    long long v[MAXH + 1];
+    const int op[MAXH + 1] = {OP_MIN, OP_MIN, OP_MIN, OP_MIN, OP_OR};
+#pragma unroll
+    for (int i = 0; i < MAXH; i++) v[i] = hard_min[i];
+    v[MAXH] = flags;
+    // histogram SUM over every bin, hard-pair presence OR (soft presence is filled later)
+    if (!cluster_reduce(smem, S, v, op, 0, pl.total_bins, pl.total_bins, pl.hard_pbins)) return false;
+    flags = v[MAXH];
+    // minima over present bins of non-unique hard keys (bins are cluster-wide now)
     const kss_spread* sp = P.spreads + p.spread_off;
-    for (int i = 0; i < p.n_hard; i++) {
+    long long m[MAXH];
+#pragma unroll
+    for (int i = 0; i < MAXH; i++) m[i] = v[i];
+    bool any_hist = false;
+#pragma unroll
+    for (int i = 0; i < MAXH; i++) {
+      if (i >= p.n_hard) break;
       if (pl.hard_off[i] < 0) continue;
+      any_hist = true;
       const int nb = c.key_card[sp[i].key] + 1;
       for (int b = tid; b < nb; b += nt) {
         const int g = pl.hard_off[i] + b;
-        if (sh.pres[pl.hard_poff[i] + b]) hard_min[i] = sh.bins[g] < hard_min[i] ? sh.bins[g] : hard_min[i];
+        if (pres[pl.hard_poff[i] + b]) m[i] = bins[g] < m[i] ? bins[g] : m[i];
       }
     }
-    long long v[MAXH + 1];
-    int op[MAXH + 1];
-#pragma unroll
-    for (int i = 0; i < MAXH; i++) {
-      v[i] = hard_min[i];
-      op[i] = 2;
+    if (any_hist) {
+      const int opm[MAXH] = {OP_MIN, OP_MIN, OP_MIN, OP_MIN};
+      cluster_reduce(smem, S, m, opm, 0, 0, 0, 0, /*local=*/true);
     }
-    v[MAXH] = flags;
-    op[MAXH] = 3;
-    block_reduce(sh, v, op);
 #pragma unroll
-    for (int i = 0; i < MAXH; i++) hard_min[i] = v[i];
-    flags = v[MAXH];
+    for (int i = 0; i < MAXH; i++) hard_min[i] = m[i];
+    // soft presence bins start empty for the filter pass
+    for (int b = pl.hard_pbins + tid; b < pl.total_pbins; b += nt) pres[b] = 0;
+    __syncthreads();
   }
 
-  // ---- filter + raw scores ---------------------------------------------
+  // ---- filter + raw scores -------------------------------------------------
   const uint32_t en = prof.filter_enabled;
   const bool restrict_names = p.names_len >= 0;
   const kss_spread* soft = P.spreads + p.spread_off + p.n_hard;
   const bool req_all = (p.flags & KSS_POD_PTS_REQUIRE_ALL) != 0;
-  long long nf = 0, nign = 0, max_tt = 0, max_na = 0, ipa_min = INT64_MAX, ipa_max = INT64_MIN, first = INT64_MAX;
-  long long sdirect[MAXS], smissing = 0;
+  const bool has_soft = GEN && p.n_soft > 0;
+  const bool has_ipa = GEN && p.ipa_len > 0;
+  long long nf = 0, max_tt = 0, max_na = 0;
+  long long nign = 0, ipa_min = INT64_MAX, ipa_max = INT64_MIN, smissing = 0;
+  long long sdirect[MAXS];
 #pragma unroll
   for (int i = 0; i < MAXS; i++) sdirect[i] = 0;
-  for (int n = tid; n < N; n += nt) {
+  for (int k = 0; k < npt; k++) {
+    const int n = S.lo + k * nt + tid;
+    const int si = k * nt + tid;
+    if (n >= S.hi) {
+      sa.fail[si] = KSS_F_NOT_EVALUATED;
+      continue;
+    }
     uint16_t detail = 0;
-    int fail;
+    int f;
+    NodeRow row;
     if (restrict_names && !in_names(P, p, (int64_t)c.node_base + n)) {
-      fail = KSS_F_NOT_EVALUATED;
+      f = KSS_F_NOT_EVALUATED;
     } else {
-      fail = filter_local(c, P, p, en, n, &detail);
-      if (!fail && ((en >> KSS_F_POD_TOPOLOGY_SPREAD) & 1u) && p.n_hard > 0) {
-        const int r = filter_pts(c, P, p, pl, sh, hard_min, n);
+      row = load_row(c, n);
+      f = filter_local(c, P, p, en, n, row, &detail);
+      if (GEN && !f && ((en >> KSS_F_POD_TOPOLOGY_SPREAD) & 1u) && p.n_hard > 0) {
+        const int r = filter_pts(c, P, p, pl, bins, hard_min, n);
         if (r) {
-          fail = KSS_F_POD_TOPOLOGY_SPREAD;
+          f = KSS_F_POD_TOPOLOGY_SPREAD;
           detail = (uint16_t)(r - 1);
         }
       }
-      if (!fail && ((en >> KSS_F_INTER_POD_AFFINITY) & 1u) && p.ipa_len > 0) {
-        const int r = filter_ipa(c, P, p, pl, sh, flags, n);
+      if (!f && ((en >> KSS_F_INTER_POD_AFFINITY) & 1u) && has_ipa) {
+        const int r = filter_ipa(c, P, p, pl, bins, flags, n);
         if (r) {
-          fail = KSS_F_INTER_POD_AFFINITY;
+          f = KSS_F_INTER_POD_AFFINITY;
           detail = (uint16_t)(r - 1);
         }
       }
     }
-    out.fail[n] = (uint8_t)fail;
-    out.detail[n] = detail;
-    if (fail == KSS_F_PASS) {
+    if (out) {
+      out->fail[n] = (uint8_t)f;
+      out->detail[n] = detail;
+    }
+    int ign = 0;
+    if (f == KSS_F_PASS) {
       nf++;
-      first = n < first ? n : first;
-      const int64_t tt = tt_score(c, p, n);
+      const int64_t tt = tt_score(row, p);
       const int64_t na = na_score(c, P, p, n);
-      const int64_t ipa = p.ipa_len > 0 ? ipa_score(c, P, p, pl, sh, n) : 0;
-      out.raw[KSS_S_TAINT_TOLERATION * NN + n] = tt;
-      out.raw[KSS_S_NODE_AFFINITY * NN + n] = na;
-      out.raw[KSS_S_NODE_RESOURCES_FIT * NN + n] = fit_score(c, prof, p, n);
-      out.raw[KSS_S_VOLUME_BINDING * NN + n] = 0;
-      out.raw[KSS_S_INTER_POD_AFFINITY * NN + n] = ipa;
-      out.raw[KSS_S_BALANCED_ALLOCATION * NN + n] = ba_score(c, prof, p, n);
-      out.raw[KSS_S_IMAGE_LOCALITY * NN + n] = 0;
+      const int64_t fit = fit_score(c, prof, p, n, row);
+      const int64_t ba = ba_score(c, prof, p, n, row);
+      sa.tt[si] = (int)tt;
+      sa.na[si] = na;
+      sa.fit[si] = (int)fit;
+      sa.ba[si] = (int)ba;
       max_tt = tt > max_tt ? tt : max_tt;
       max_na = na > max_na ? na : max_na;
-      ipa_min = ipa < ipa_min ? ipa : ipa_min;
-      ipa_max = ipa > ipa_max ? ipa : ipa_max;
-      if (p.n_soft > 0) {
-        const bool ignored = req_all && !has_keys(c, soft, p.n_soft, n);
-        if (ignored) {
+      int64_t ipa = 0;
+      if (has_ipa) {
+        ipa = ipa_score(c, P, p, pl, bins, n);
+        ipa_min = ipa < ipa_min ? ipa : ipa_min;
+        ipa_max = ipa > ipa_max ? ipa : ipa_max;
+      }
+      sa.ipa[si] = ipa;
+      sa.pts[si] = 0;
+      if (out) {
+        out->raw[KSS_S_TAINT_TOLERATION * NN + n] = tt;
+        out->raw[KSS_S_NODE_AFFINITY * NN + n] = na;
+        out->raw[KSS_S_NODE_RESOURCES_FIT * NN + n] = fit;
+        out->raw[KSS_S_VOLUME_BINDING * NN + n] = 0;
+        out->raw[KSS_S_INTER_POD_AFFINITY * NN + n] = ipa;
+        out->raw[KSS_S_BALANCED_ALLOCATION * NN + n] = ba;
+        out->raw[KSS_S_IMAGE_LOCALITY * NN + n] = 0;
+      }
+      if (has_soft) {
+        if (req_all && !has_keys(c, soft, p.n_soft, n)) {
           nign++;
+          ign = 1;
         } else {
-          for (int i = 0; i < p.n_soft; i++) {
+#pragma unroll
+          for (int i = 0; i < MAXS; i++) {
+            if (i >= p.n_soft) break;
             int d = label_of(c, soft[i].key, n);
             if (pl.soft_mode[i] == SOFT_DIRECT) {
               if (d >= 0) sdirect[i]++;
               else smissing |= 1ll << i;
             } else if (pl.soft_mode[i] == SOFT_HIST) {
               if (d < 0) d = c.key_empty[soft[i].key];
-              sh.pres[pl.soft_poff[i] + d] = 1;
+              pres[pl.soft_poff[i] + d] = 1;
             }
           }
         }
       }
     }
+    sa.fail[si] = f | (ign << 16);
   }
-  {
-    long long v[8 + MAXS] = {nf, nign, max_tt, max_na, ipa_min, ipa_max, first, smissing};
-    int op[8 + MAXS] = {0, 0, 1, 1, 2, 1, 2, 3};
+  KSS_STAMP(S, 2);
+  if (!has_soft && !has_ipa) {
+    long long v[3] = {nf, max_tt, max_na};
+    const int op[3] = {OP_SUM, OP_MAX, OP_MAX};
+    if (!cluster_reduce(smem, S, v, op)) return false;
+    nf = v[0];
+    max_tt = v[1];
+    max_na = v[2];
+  } else {
+    long long v[7 + MAXS] = {nf, nign, max_tt, max_na, ipa_min, ipa_max, smissing};
+    const int op[7 + MAXS] = {OP_SUM, OP_SUM, OP_MAX, OP_MAX, OP_MIN, OP_MAX, OP_OR, OP_SUM, OP_SUM, OP_SUM, OP_SUM};
 #pragma unroll
-    for (int i = 0; i < MAXS; i++) {
-      v[8 + i] = sdirect[i];
-      op[8 + i] = 0;
-    }
-    block_reduce(sh, v, op);
+    for (int i = 0; i < MAXS; i++) v[7 + i] = sdirect[i];
+    // soft presence bins (filled during the pass) are OR-ed across shards
+    if (!cluster_reduce(smem, S, v, op, 0, 0, pl.total_bins + pl.hard_pbins, pl.total_pbins - pl.hard_pbins)) return false;
     nf = v[0];
     nign = v[1];
     max_tt = v[2];
     max_na = v[3];
     ipa_min = v[4];
     ipa_max = v[5];
-    first = v[6];
-    smissing = v[7];
+    smissing = v[6];
 #pragma unroll
-    for (int i = 0; i < MAXS; i++) sdirect[i] = v[8 + i];
+    for (int i = 0; i < MAXS; i++) sdirect[i] = v[7 + i];
   }
+  KSS_STAMP(S, 3);
   meta.n_feasible = (int)nf;
   if (nf == 0) {
     meta.status = 1;
-    return;
+    return true;
   }
-  if (nf == 1) {
-    meta.chosen = (int)(c.node_base + first);
-    return;
-  }
-  meta.scored = 1;
+  const bool scored = nf > 1;  // a single feasible node is selected without scoring
 
   // ---- PodTopologySpread PreScore sizes + Score ---------------------------
-  double w[MAXS];
-  long long pts_min = INT64_MAX, pts_max = 0;
-  if (p.n_soft > 0) {
+  long long pts_min = 0, pts_max = 0;
+  if (scored && has_soft) {
+    double w[MAXS];
     long long sz[MAXS];
-    int op[MAXS];
+    const int op[MAXS] = {OP_SUM, OP_SUM, OP_SUM, OP_SUM};
+#pragma unroll
+    for (int i = 0; i < MAXS; i++) sz[i] = 0;
 #pragma unroll
     for (int i = 0; i < MAXS; i++) {
-      sz[i] = 0;
-      op[i] = 0;
-    }
-    for (int i = 0; i < p.n_soft; i++) {
+      if (i >= p.n_soft) break;
       if (pl.soft_mode[i] != SOFT_HIST) continue;
       const int nb = c.key_card[soft[i].key] + 1;
-      for (int b = tid; b < nb; b += nt) sz[i] += sh.pres[pl.soft_poff[i] + b] ? 1 : 0;
+      for (int b = tid; b < nb; b += nt) sz[i] += pres[pl.soft_poff[i] + b] ? 1 : 0;
     }
-    block_reduce(sh, sz, op);
-    for (int i = 0; i < p.n_soft; i++) {
+    cluster_reduce(smem, S, sz, op, 0, 0, 0, 0, /*local=*/true);
+#pragma unroll
+    for (int i = 0; i < MAXS; i++) {
+      if (i >= p.n_soft) break;
       long long size;
       if (pl.soft_mode[i] == SOFT_HOST) size = nf - nign;
       else if (pl.soft_mode[i] == SOFT_DIRECT) size = sdirect[i] + ((smissing >> i) & 1);
       else size = sz[i];
       w[i] = c.log_table[size];  // topologyNormalizingWeight = math.Log(float64(size+2))
     }
-    for (int n = tid; n < N; n += nt) {
-      if (out.fail[n] != KSS_F_PASS) continue;
+    pts_min = INT64_MAX;
+    for (int k = 0; k < npt; k++) {
+      const int n = S.lo + k * nt + tid;
+      const int si = k * nt + tid;
+      const int fi = sa.fail[si];
+      if ((fi & 0xFFFF) != KSS_F_PASS) continue;
       int64_t raw = 0;
-      const bool ignored = req_all && !has_keys(c, soft, p.n_soft, n);
-      if (!ignored) {
+      if (!(fi >> 16)) {
         double s = 0.0;
-        for (int i = 0; i < p.n_soft; i++) {
+#pragma unroll
+        for (int i = 0; i < MAXS; i++) {
+          if (i >= p.n_soft) break;
           const int d = label_of(c, soft[i].key, n);
           if (d < 0) continue;
           int64_t cnt;
           if (pl.soft_mode[i] == SOFT_HOST) cnt = spread_count(c, P, soft[i], n);
           else if (pl.soft_mode[i] == SOFT_DIRECT) cnt = spread_policy_ok(c, P, p, soft[i], n) ? spread_count(c, P, soft[i], n) : 0;
-          else cnt = sh.bins[pl.soft_off[i] + d];
+          else cnt = bins[pl.soft_off[i] + d];
           const double a = (double)cnt * w[i];
           s = s + (a + (double)(soft[i].max_skew - 1));  // scoreForCount
         }
         raw = (int64_t)round(s);
         pts_min = raw < pts_min ? raw : pts_min;
         pts_max = raw > pts_max ? raw : pts_max;
-      } else {
-        raw = 0;
       }
-      out.raw[KSS_S_POD_TOPOLOGY_SPREAD * NN + n] = raw;
+      sa.pts[si] = raw;
+      if (out) out->raw[KSS_S_POD_TOPOLOGY_SPREAD * NN + n] = raw;
     }
     long long v[2] = {pts_min, pts_max};
-    int op2[2] = {2, 1};
-    block_reduce(sh, v, op2);
+    const int op2[2] = {OP_MIN, OP_MAX};
+    if (!cluster_reduce(smem, S, v, op2)) return false;
     pts_min = v[0];
     pts_max = v[1];
-  } else {
-    for (int n = tid; n < N; n += nt)
-      if (out.fail[n] == KSS_F_PASS) out.raw[KSS_S_POD_TOPOLOGY_SPREAD * NN + n] = 0;
-    pts_min = 0;
-    pts_max = 0;
+  } else if (out) {
+    for (int k = 0; k < npt; k++) {
+      const int n = S.lo + k * nt + tid;
+      if ((sa.fail[k * nt + tid] & 0xFFFF) == KSS_F_PASS) out->raw[KSS_S_POD_TOPOLOGY_SPREAD * NN + n] = 0;
+    }
   }
 
   // ---- NormalizeScore + weights + selectHost --------------------------------
-  const bool ipa_norm = (flags & 8) != 0;
+  const bool ipa_norm = GEN && (flags & 8) != 0;
   const int64_t ipa_diff = ipa_max - ipa_min;
-  unsigned long long best = 0;
-  for (int n = tid; n < N; n += nt) {
-    if (out.fail[n] != KSS_F_PASS) continue;
-    int64_t nm[KSS_NSCORE];
-#pragma unroll
-    for (int s = 0; s < KSS_NSCORE; s++) nm[s] = out.raw[(size_t)s * NN + n];
-    // TaintToleration: DefaultNormalizeScore(100, reverse=true)
-    if (max_tt == 0) nm[KSS_S_TAINT_TOLERATION] = 100;
-    else nm[KSS_S_TAINT_TOLERATION] = 100 - (100 * nm[KSS_S_TAINT_TOLERATION]) / max_tt;
-    // NodeAffinity: DefaultNormalizeScore(100, reverse=false)
-    if (max_na != 0) nm[KSS_S_NODE_AFFINITY] = (100 * nm[KSS_S_NODE_AFFINITY]) / max_na;
-    // PodTopologySpread.NormalizeScore
-    {
-      const bool ignored = p.n_soft > 0 && req_all && !has_keys(c, soft, p.n_soft, n);
-      int64_t& v = nm[KSS_S_POD_TOPOLOGY_SPREAD];
-      if (ignored) v = 0;
-      else if (pts_max == 0) v = 100;
-      else v = 100 * (pts_max + pts_min - v) / pts_max;
-    }
-    // InterPodAffinity.NormalizeScore (skipped when topologyScore is empty)
-    if (ipa_norm) {
-      double f = 0.0;
-      if (ipa_diff > 0) f = 100.0 * ((double)(nm[KSS_S_INTER_POD_AFFINITY] - ipa_min) / (double)ipa_diff);
-      nm[KSS_S_INTER_POD_AFFINITY] = (int64_t)f;
-    }
+  const bool rec = out && keep_norm && scored;
+  long long best = 0;
+  for (int k = 0; k < npt; k++) {
+    const int n = S.lo + k * nt + tid;
+    const int si = k * nt + tid;
+    const int fi = sa.fail[si];
+    if ((fi & 0xFFFF) != KSS_F_PASS) continue;
     int64_t total = 0;
+    if (scored) {
+      int64_t nm[KSS_NSCORE];
+      nm[KSS_S_TAINT_TOLERATION] = sa.tt[si];
+      nm[KSS_S_NODE_AFFINITY] = sa.na[si];
+      nm[KSS_S_NODE_RESOURCES_FIT] = sa.fit[si];
+      nm[KSS_S_VOLUME_BINDING] = 0;
+      nm[KSS_S_POD_TOPOLOGY_SPREAD] = sa.pts[si];
+      nm[KSS_S_INTER_POD_AFFINITY] = sa.ipa[si];
+      nm[KSS_S_BALANCED_ALLOCATION] = sa.ba[si];
+      nm[KSS_S_IMAGE_LOCALITY] = 0;
+      // TaintToleration: DefaultNormalizeScore(100, reverse=true)
+      if (max_tt == 0) nm[KSS_S_TAINT_TOLERATION] = 100;
+      else nm[KSS_S_TAINT_TOLERATION] = 100 - div_i64(100 * nm[KSS_S_TAINT_TOLERATION], max_tt);
+      // NodeAffinity: DefaultNormalizeScore(100, reverse=false)
+      if (max_na != 0) nm[KSS_S_NODE_AFFINITY] = div_i64(100 * nm[KSS_S_NODE_AFFINITY], max_na);
+      // PodTopologySpread.NormalizeScore
+      {
+        int64_t& v = nm[KSS_S_POD_TOPOLOGY_SPREAD];
+        if (has_soft && (fi >> 16)) v = 0;
+        else if (pts_max == 0) v = 100;
+        else v = div_i64(100 * (pts_max + pts_min - v), pts_max);
+      }
+      // InterPodAffinity.NormalizeScore (skipped when topologyScore is empty)
+      if (ipa_norm) {
+        double f = 0.0;
+        if (ipa_diff > 0) f = 100.0 * ((double)(nm[KSS_S_INTER_POD_AFFINITY] - ipa_min) / (double)ipa_diff);
+        nm[KSS_S_INTER_POD_AFFINITY] = (int64_t)f;
+      }
 #pragma unroll
-    for (int s = 0; s < KSS_NSCORE; s++)
-      if ((prof.score_enabled >> s) & 1u) total += nm[s] * (int64_t)prof.weight[s];
-    if (keep_norm) {
+      for (int s = 0; s < KSS_NSCORE; s++)
+        if ((prof.score_enabled >> s) & 1u) total += nm[s] * (int64_t)prof.weight[s];
+      if (rec) {
 #pragma unroll
-      for (int s = 0; s < KSS_NSCORE; s++) out.norm[(size_t)s * NN + n] = nm[s];
-      out.total[n] = total;
+        for (int s = 0; s < KSS_NSCORE; s++) out->norm[(size_t)s * NN + n] = nm[s];
+        out->total[n] = total;
+      }
     }
     const uint32_t g = (uint32_t)(c.node_base + n);
-    const unsigned long long key = ((unsigned long long)(uint32_t)total << 32) | (0xFFFFFFFFull - g);
+    // totals are >= 0 and < 2^31, so the packed key's sign bit is clear and signed max == unsigned max
+    const long long key = (long long)(((unsigned long long)(uint32_t)total << 32) | (0xFFFFFFFFull - g));
     best = key > best ? key : best;
   }
+  KSS_STAMP(S, 4);
   {
-    long long v[1] = {(long long)best};
-    int op[1] = {1};
-    // totals are >= 0 and < 2^31, so the packed key's sign bit is clear and signed max == unsigned max
-    block_reduce(sh, v, op);
-    best = (unsigned long long)v[0];
+    long long v[1] = {best};
+    const int op[1] = {OP_MAX};
+    if (!cluster_reduce(smem, S, v, op)) return false;
+    best = v[0];
   }
-  meta.chosen = (int)(0xFFFFFFFFull - (best & 0xFFFFFFFFull));
-  meta.best_total = (int64_t)(best >> 32);
+  KSS_STAMP(S, 5);
+  const unsigned long long ub = (unsigned long long)best;
+  meta.chosen = (int)(0xFFFFFFFFull - (ub & 0xFFFFFFFFull));
+  meta.scored = scored ? 1 : 0;
+  meta.best_total = scored ? (int64_t)(ub >> 32) : 0;
+  return true;
 }
 
-// Cache.AssumePod -> NodeInfo.AddPod; executed by one lane.
+// Cache.AssumePod -> NodeInfo.AddPod; executed by one lane.  With a shard cache the
+// hot columns are updated in LDS (written back to HBM when the launch ends).
 __device__ __forceinline__ void commit_pod(const DevCluster& c, const DevPods& P, const kss_pod& p, int local, int sign) {
   const size_t N = (size_t)c.N;
-  for (int r = 0; r < KSS_NRES; r++) c.requested[(size_t)r * N + local] += sign * p.commit_req[r];
-  c.nonzero[local] += sign * p.commit_nz[0];
-  c.nonzero[N + local] += sign * p.commit_nz[1];
-  c.pod_count[local] += sign;
+  if (c.nc64) {
+    const int i = local - c.nc_lo, C = c.nc_cap;
+#pragma unroll
+    for (int r = 0; r < 3; r++) c.nc64[(3 + r) * C + i] += sign * p.commit_req[r];
+    c.nc64[6 * C + i] += sign * p.commit_nz[0];
+    c.nc64[7 * C + i] += sign * p.commit_nz[1];
+    c.nc32[i] += sign;
+    for (int r = 3; r < KSS_NRES; r++) c.requested[(size_t)r * N + local] += sign * p.commit_req[r];
+  } else {
+    for (int r = 0; r < KSS_NRES; r++) c.requested[(size_t)r * N + local] += sign * p.commit_req[r];
+    c.nonzero[local] += sign * p.commit_nz[0];
+    c.nonzero[N + local] += sign * p.commit_nz[1];
+    c.pod_count[local] += sign;
+  }
   if (p.cls >= 0) c.class_count[(size_t)p.cls * N + local] += sign;
   for (int i = 0; i < p.own_terms_len; i++) c.term_count[(size_t)P.ints[p.own_terms_off + i] * N + local] += sign;
+}
+
+// Shard cache fill / write-back (all lanes of the workgroup).
+__device__ __forceinline__ void cache_fill(const DevCluster& c, int hi, int n_keys_cached) {
+  const size_t N = (size_t)c.N;
+  const int C = c.nc_cap;
+  for (int n = c.nc_lo + threadIdx.x; n < hi; n += blockDim.x) {
+    const int i = n - c.nc_lo;
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+      c.nc64[k * C + i] = c.alloc[k * N + n];
+      c.nc64[(3 + k) * C + i] = c.requested[k * N + n];
+    }
+    c.nc64[6 * C + i] = c.nonzero[n];
+    c.nc64[7 * C + i] = c.nonzero[N + n];
+    c.nct[i] = c.taint_hard[n];
+    c.nct[C + i] = c.taint_soft[n];
+    c.nc32[i] = c.pod_count[n];
+    c.nc32[C + i] = c.allowed_pods[n];
+    c.nc32[2 * C + i] = (int32_t)c.node_flags[n];
+    for (int k = 0; k < n_keys_cached; k++) c.ncl[k * C + i] = c.label_value[(size_t)k * N + n];
+  }
+}
+
+__device__ __forceinline__ void cache_writeback(const DevCluster& c, int hi) {
+  const size_t N = (size_t)c.N;
+  const int C = c.nc_cap;
+  for (int n = c.nc_lo + threadIdx.x; n < hi; n += blockDim.x) {
+    const int i = n - c.nc_lo;
+#pragma unroll
+    for (int k = 0; k < 3; k++) c.requested[k * N + n] = c.nc64[(3 + k) * C + i];
+    c.nonzero[n] = c.nc64[6 * C + i];
+    c.nonzero[N + n] = c.nc64[7 * C + i];
+    c.pod_count[n] = c.nc32[i];
+  }
 }
 
 }  // namespace kss

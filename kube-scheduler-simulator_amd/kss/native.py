@@ -45,6 +45,7 @@ SIGNATURES = [
     ("kss_schedule_scenarios", C.c_int, [C.c_int32, P(abi.Profile), C.c_int32, P(abi.Cluster), P(abi.PodSet),
                                          P(C.c_int32), P(C.c_double)]),
     ("kss_last_timing", C.c_int, [C.c_void_p, P(C.c_double), P(C.c_int32)]),
+    ("kss_last_geometry", C.c_int, [C.c_void_p, P(C.c_int32)]),
     ("kss_set_names", C.c_int, [C.c_void_p, P(abi.Names)]),
     ("kss_format_annotations", C.c_int, [C.c_void_p, P(abi.PodResult), C.c_int32, C.c_char_p, C.c_size_t,
                                          P(C.c_size_t)]),
@@ -244,6 +245,11 @@ class Context:
         n = C.c_int32(0)
         check(lib().kss_last_timing(self.h, C.byref(ms), C.byref(n)))
         return ms.value, n.value
+
+    def last_geometry(self):
+        out = (C.c_int32 * 3)()
+        check(lib().kss_last_geometry(self.h, out))
+        return {"shards": out[0], "threads": out[1], "nodes_per_lane": out[2]}
 
     def format_annotations(self, result: PodResult) -> Dict[str, str]:
         L = lib()

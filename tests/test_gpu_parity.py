@@ -49,6 +49,10 @@ def _state_equal(ctx, st, n_nodes, n_classes, n_terms):
         np.testing.assert_array_equal(g["term_count"][:n_terms], st["term_count"][:n_terms])
 
 
+MODES = {"auto": 0, "single": abi.KSS_SCHED_FORCE_SINGLE_WG, "multi": abi.KSS_SCHED_FORCE_MULTI_WG}
+
+
+@pytest.mark.parametrize("mode", ["auto", "single", "multi"])
 @pytest.mark.parametrize("config,n_nodes,n_pods", [
     (1, 100, 1000),   # C1 exactly (BASELINE configs[0])
     (2, 700, 400),
@@ -56,16 +60,23 @@ def _state_equal(ctx, st, n_nodes, n_classes, n_terms):
     (4, 500, 300),    # zone spread
     (5, 1000, 200),
     (1, 3, 50),       # tiny: single-feasible and unschedulable pods
-    (3, 1500, 120),   # > 1024 nodes: several nodes per lane
+    (3, 1500, 120),   # several nodes per lane
 ])
-def test_schedule_batch_matches_oracle(config, n_nodes, n_pods):
+def test_schedule_batch_matches_oracle(config, n_nodes, n_pods, mode):
+    """Single workgroup, forced multi-shard (granule exchanges) and the automatic geometry
+    all give the oracle's results bit for bit."""
     prof = abi.default_profile()
     s = native.Synth(config, 0, n_nodes, n_pods)
     chosen_o, res, st = oracle_c.schedule(prof, s.cluster, s.pods, n_pods, n_nodes, record=True, threads=8,
                                           n_classes=s.cluster.n_classes, n_terms=s.cluster.n_terms)
     ctx = native.Context(prof, max_pods_record=n_pods)
     ctx.load(s.cluster)
-    chosen_g = ctx.schedule_batch(s.pods, n_pods, record=True)
+    chosen_g = ctx.schedule_batch(s.pods, n_pods, record=True, flags=MODES[mode])
+    geo = ctx.last_geometry()
+    if mode == "single":
+        assert geo["shards"] == 1
+    if mode == "multi" and n_nodes >= 4:
+        assert geo["shards"] > 1
     np.testing.assert_array_equal(chosen_g, chosen_o)
     _compare_records(ctx, res, chosen_o, n_pods, n_nodes)
     _state_equal(ctx, st, n_nodes, s.cluster.n_classes, s.cluster.n_terms)
@@ -159,3 +170,24 @@ def test_invalid_program_is_rejected_not_run():
     bad.n_reqs = 0  # requirement offsets now out of range
     with pytest.raises(native.KssError):
         ctx.schedule_batch(bad, 10)
+
+
+@pytest.mark.parametrize("config,n_pods", [(2, 300), (4, 200)])
+def test_c2_scale_sharded_matches_oracle(config, n_pods):
+    """5,000 nodes (BASELINE C2 cluster) on the automatic multi-shard geometry: chosen nodes
+    and final node state equal the oracle's for the first n_pods pods."""
+    prof = abi.default_profile()
+    n_nodes = 5000
+    s = native.Synth(config, 0, n_nodes, n_pods)
+    chosen_o, _, st = oracle_c.schedule(prof, s.cluster, s.pods, n_pods, n_nodes, record=False, threads=8,
+                                        n_classes=s.cluster.n_classes, n_terms=s.cluster.n_terms)
+    ctx = native.Context(prof)
+    ctx.load(s.cluster)
+    ctx.stage(s.pods)
+    chosen_g = ctx.run_staged(n_pods)
+    assert ctx.last_geometry()["shards"] > 1
+    np.testing.assert_array_equal(chosen_g, chosen_o)
+    _state_equal(ctx, st, n_nodes, s.cluster.n_classes, s.cluster.n_terms)
+    # reset + replay gives the same placements (what-if replays)
+    ctx.reset()
+    np.testing.assert_array_equal(ctx.run_staged(n_pods), chosen_o)
