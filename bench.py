@@ -156,10 +156,11 @@ def main():
             "geometry": ctx.last_geometry(),
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                         "kernel": "k_schedule", "bytes_per_eval": B_EVAL[cfg]},
+                         "kernel": ctx.last_kernel(), "bytes_per_eval": B_EVAL[cfg]},
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)
+    ctx.close()
     if dist:
         dist.destroy_process_group()
 

@@ -346,6 +346,7 @@ int kss_rollback(kss_ctx* ctx, const kss_podset* ps, int32_t pod_index, int32_t 
 #define KSS_SCHED_RECORD (1u << 0)
 #define KSS_SCHED_FORCE_MULTI_WG (1u << 1) /* testing: use the multi-workgroup per-pod path */
 #define KSS_SCHED_FORCE_SINGLE_WG (1u << 2)
+#define KSS_SCHED_GENERAL_KERNEL (1u << 3) /* testing: never use the compact k_simple path */
 int kss_schedule_batch(kss_ctx* ctx, const kss_podset* ps, int32_t n, uint32_t flags, int32_t* chosen_out);
 int kss_fetch_record(kss_ctx* ctx, int32_t pod_index, kss_pod_result* out);
 
@@ -368,6 +369,12 @@ int kss_last_timing(kss_ctx* ctx, double* device_ms, int32_t* launches);
 /* launch geometry of the last scheduling launch: out[0] shards (workgroups) per cluster,
  * out[1] threads per workgroup, out[2] node slots per lane */
 int kss_last_geometry(kss_ctx* ctx, int32_t* out3);
+/* kernel of the last scheduling launch: 0 general (k_schedule), 1 compact (k_simple:
+ * batches without spread / inter-pod programs and without a record); <0 on error */
+int kss_last_kernel(kss_ctx* ctx);
+/* outcome of pods [first, first+n) of the last scheduling launch, recorded or not:
+ * out[5*i .. 5*i+4] = chosen, n_feasible, scored, status, best_total (kss_pod_result) */
+int kss_fetch_meta(kss_ctx* ctx, int32_t first, int32_t n, int64_t* out);
 
 /* ---- annotation formatting (store.go GetStoredResult semantics) -------- */
 typedef struct kss_names {

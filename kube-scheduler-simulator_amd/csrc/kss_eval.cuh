@@ -11,6 +11,23 @@
 
 #include "../../include/kss.h"
 
+// Debug builds (make debug -> libkss_dbg.so) check every data-dependent global index
+// and trap with the offending values; release builds compile the checks away.
+#ifdef KSS_DEBUG_BOUNDS
+#define KSS_DCHECK(cond, what, a, b)                                                                      \
+  do {                                                                                                    \
+    if (!(cond)) {                                                                                        \
+      printf("KSS_DCHECK %s a=%lld b=%lld block=%d thread=%d\n", what, (long long)(a), (long long)(b),     \
+             (int)blockIdx.x, (int)threadIdx.x);                                                          \
+      __builtin_trap();                                                                                   \
+    }                                                                                                     \
+  } while (0)
+#else
+#define KSS_DCHECK(cond, what, a, b) \
+  do {                               \
+  } while (0)
+#endif
+
 namespace kss {
 
 // Device view of a loaded cluster.  Row r of a [attr][N] matrix starts at r*N.
@@ -62,37 +79,41 @@ struct NodeRow {
 // a[r] for a runtime r in [0, 3) without dynamic register indexing
 __device__ __forceinline__ int64_t pick3(const int64_t (&a)[3], int r) { return r == 0 ? a[0] : (r == 1 ? a[1] : a[2]); }
 
-__device__ __forceinline__ NodeRow load_row(const DevCluster& c, int n) {
+__device__ __forceinline__ NodeRow row_from_hbm(const DevCluster& c, int n) {
+  KSS_DCHECK(n >= 0 && n < c.N, "row_from_hbm n", n, c.N);
   NodeRow r;
-  if (c.nc64) {
-    const int i = n - c.nc_lo, C = c.nc_cap;
+  const size_t N = (size_t)c.N;
 #pragma unroll
-    for (int k = 0; k < 3; k++) {
-      r.alloc[k] = c.nc64[k * C + i];
-      r.req[k] = c.nc64[(3 + k) * C + i];
-    }
-    r.nz[0] = c.nc64[6 * C + i];
-    r.nz[1] = c.nc64[7 * C + i];
-    r.th = c.nct[i];
-    r.ts = c.nct[C + i];
-    r.pods = c.nc32[i];
-    r.allowed = c.nc32[C + i];
-    r.flags = (uint32_t)c.nc32[2 * C + i];
-  } else {
-    const size_t N = (size_t)c.N;
-#pragma unroll
-    for (int k = 0; k < 3; k++) {
-      r.alloc[k] = c.alloc[k * N + n];
-      r.req[k] = c.requested[k * N + n];
-    }
-    r.nz[0] = c.nonzero[n];
-    r.nz[1] = c.nonzero[N + n];
-    r.th = c.taint_hard[n];
-    r.ts = c.taint_soft[n];
-    r.pods = c.pod_count[n];
-    r.allowed = c.allowed_pods[n];
-    r.flags = c.node_flags[n];
+  for (int k = 0; k < 3; k++) {
+    r.alloc[k] = c.alloc[k * N + n];
+    r.req[k] = c.requested[k * N + n];
   }
+  r.nz[0] = c.nonzero[n];
+  r.nz[1] = c.nonzero[N + n];
+  r.th = c.taint_hard[n];
+  r.ts = c.taint_soft[n];
+  r.pods = c.pod_count[n];
+  r.allowed = c.allowed_pods[n];
+  r.flags = c.node_flags[n];
+  return r;
+}
+
+__device__ __forceinline__ NodeRow load_row(const DevCluster& c, int n) {
+  if (!c.nc64) return row_from_hbm(c, n);
+  NodeRow r;
+  const int i = n - c.nc_lo, C = c.nc_cap;
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    r.alloc[k] = c.nc64[k * C + i];
+    r.req[k] = c.nc64[(3 + k) * C + i];
+  }
+  r.nz[0] = c.nc64[6 * C + i];
+  r.nz[1] = c.nc64[7 * C + i];
+  r.th = c.nct[i];
+  r.ts = c.nct[C + i];
+  r.pods = c.nc32[i];
+  r.allowed = c.nc32[C + i];
+  r.flags = (uint32_t)c.nc32[2 * C + i];
   return r;
 }
 
@@ -115,19 +136,22 @@ struct DevPods {
 
 __device__ __forceinline__ int32_t label_of(const DevCluster& c, int key, int n) {
   if (c.ncl) return c.ncl[key * c.nc_cap + (n - c.nc_lo)];
+  KSS_DCHECK(key >= 0 && key < c.n_keys && n >= 0 && n < c.N, "label_of key/n", key, n);
   return c.label_value[(size_t)key * (size_t)c.N + (size_t)n];
 }
 
 // labels.Requirement.Matches over value ids (apimachinery labels/selector.go) and the
-// metadata.name field selector (component-helpers nodeaffinity).
-__device__ __forceinline__ bool req_match(const DevCluster& c, const DevPods& P, const kss_req& r, int n) {
+// metadata.name field selector (component-helpers nodeaffinity).  g is the global node
+// index, lab(key) the node's value id for a label key (-1 absent), ints the pool of
+// IN / NOTIN value lists: the HBM path and the LDS path (kss_simple.cuh) share it.
+template <class Lab>
+__device__ __forceinline__ bool req_match_t(const DevCluster& c, const int32_t* ints, const kss_req& r, int64_t g, Lab lab) {
   const int op = r.op;
-  const int64_t g = (int64_t)c.node_base + n;
   if (op == KSS_OP_FALSE) return false;
   if (op == KSS_OP_TRUE) return true;
   if (op == KSS_OP_NAME_IN) return r.ival >= 0 && g == r.ival;
   if (op == KSS_OP_NAME_NOTIN) return !(r.ival >= 0 && g == r.ival);
-  const int32_t v = label_of(c, r.key, n);
+  const int32_t v = lab(r.key);
   switch (op) {
     case KSS_OP_MASK:
       if (v < 0) return (r.mask >> 63) & 1ull;
@@ -135,13 +159,13 @@ __device__ __forceinline__ bool req_match(const DevCluster& c, const DevPods& P,
     case KSS_OP_IN: {
       if (v < 0) return false;
       for (int i = 0; i < r.list_len; i++)
-        if (P.ints[r.list_off + i] == v) return true;
+        if (ints[r.list_off + i] == v) return true;
       return false;
     }
     case KSS_OP_NOTIN: {
       if (v < 0) return true;
       for (int i = 0; i < r.list_len; i++)
-        if (P.ints[r.list_off + i] == v) return false;
+        if (ints[r.list_off + i] == v) return false;
       return true;
     }
     case KSS_OP_EXISTS:
@@ -161,28 +185,51 @@ __device__ __forceinline__ bool req_match(const DevCluster& c, const DevPods& P,
   }
 }
 
-__device__ __forceinline__ bool term_match(const DevCluster& c, const DevPods& P, const kss_term& t, int n) {
+template <class Lab>
+__device__ __forceinline__ bool term_match_t(const DevCluster& c, const kss_req* reqs, const int32_t* ints,
+                                             const kss_term& t, int64_t g, Lab lab) {
   for (int i = 0; i < t.req_len; i++)
-    if (!req_match(c, P, P.reqs[t.req_off + i], n)) return false;
+    if (!req_match_t(c, ints, reqs[t.req_off + i], g, lab)) return false;
   return true;
 }
 
 // nodeaffinity.RequiredNodeAffinity.Match: nodeSelector AND (OR over terms)
-__device__ __forceinline__ bool required_affinity(const DevCluster& c, const DevPods& P, const kss_pod& p, int n) {
+template <class Lab>
+__device__ __forceinline__ bool required_affinity_t(const DevCluster& c, const kss_req* reqs, const kss_term* terms,
+                                                    const int32_t* ints, const kss_pod& p, int64_t g, Lab lab) {
   for (int i = 0; i < p.sel_len; i++)
-    if (!req_match(c, P, P.reqs[p.sel_off + i], n)) return false;
+    if (!req_match_t(c, ints, reqs[p.sel_off + i], g, lab)) return false;
   if (p.flags & KSS_POD_HAS_REQ_AFFINITY) {
     for (int t = 0; t < p.aff_len; t++)
-      if (term_match(c, P, P.terms[p.aff_off + t], n)) return true;
+      if (term_match_t(c, reqs, ints, terms[p.aff_off + t], g, lab)) return true;
     return false;
   }
   return true;
+}
+
+// NodeAffinity.Score: PreferredSchedulingTerms.Score
+template <class Lab>
+__device__ __forceinline__ int64_t na_score_t(const DevCluster& c, const kss_req* reqs, const kss_term* terms,
+                                              const int32_t* ints, const kss_pod& p, int64_t g, Lab lab) {
+  int64_t s = 0;
+  for (int t = 0; t < p.pref_len; t++) {
+    const kss_term& term = terms[p.pref_off + t];
+    if (term_match_t(c, reqs, ints, term, g, lab)) s += term.weight;
+  }
+  return s;
+}
+
+// the same over HBM (or shard-cache) labels and the pooled pod programs
+__device__ __forceinline__ bool required_affinity(const DevCluster& c, const DevPods& P, const kss_pod& p, int n) {
+  return required_affinity_t(c, P.reqs, P.terms, P.ints, p, (int64_t)c.node_base + n,
+                             [&](int key) { return label_of(c, key, n); });
 }
 
 // v1helper.FindMatchingUntoleratedTaint(node.Spec.Taints, tolerations, DoNotScheduleTaintsFilterFunc)
 __device__ __forceinline__ int first_untolerated(const DevCluster& c, const kss_pod& p, int n, uint64_t th) {
   const uint64_t untol = th & ~p.tol_hard;
   if (!untol) return -1;
+  KSS_DCHECK(n >= 0 && n < c.N, "first_untolerated n", n, c.N);
   const uint8_t* ord = c.taint_order + (size_t)n * KSS_TAINT_ORDER;
 #pragma unroll
   for (int i = 0; i < KSS_TAINT_ORDER; i++) {
@@ -195,7 +242,10 @@ __device__ __forceinline__ int first_untolerated(const DevCluster& c, const kss_
 
 __device__ __forceinline__ int64_t sum_rows(const int32_t* mat, size_t N, const int32_t* rows, int len, int n) {
   int64_t s = 0;
-  for (int i = 0; i < len; i++) s += mat[(size_t)rows[i] * N + (size_t)n];
+  for (int i = 0; i < len; i++) {
+    KSS_DCHECK(rows[i] >= 0 && rows[i] < 4096 && n >= 0 && (size_t)n < N, "sum_rows row/n", rows[i], n);
+    s += mat[(size_t)rows[i] * N + (size_t)n];
+  }
   return s;
 }
 
@@ -253,29 +303,34 @@ __device__ __forceinline__ int filter_local(const DevCluster& c, const DevPods& 
 // Go int64 division a / b for the non-negative operands the scores produce: one f64
 // division (exact operands below 2^53, error of the rounded quotient < 1) and an exact
 // integer correction; anything else takes the integer division.
+__device__ __forceinline__ int64_t div_f53(int64_t a, int64_t b) {
+  int64_t q = (int64_t)((double)a / (double)b);
+  const int64_t r = a - q * b;
+  return r < 0 ? q - 1 : (r >= b ? q + 1 : q);
+}
+
+// SMALL = true: the caller guarantees 0 <= a, b < 2^53 (k_simple: the host checks every
+// allocatable value and profile weight at load), so the integer fallback is not compiled.
+template <bool SMALL = false>
 __device__ __forceinline__ int64_t div_i64(int64_t a, int64_t b) {
-  if (a >= 0 && b > 0 && a < (1ll << 53) && b < (1ll << 53)) {
-    int64_t q = (int64_t)((double)a / (double)b);
-    const int64_t r = a - q * b;
-    if (r < 0) q--;
-    else if (r >= b) q++;
-    return q;
-  }
+  if (SMALL || (a >= 0 && b > 0 && a < (1ll << 53) && b < (1ll << 53))) return div_f53(a, b);
   return a / b;
 }
 
 // leastRequestedScore / mostRequestedScore
+template <bool SMALL = false>
 __device__ __forceinline__ int64_t alloc_score(int strategy, int64_t requested, int64_t capacity) {
   if (capacity == 0) return 0;
   if (strategy == KSS_FIT_MOST_ALLOCATED) {
     if (requested > capacity) requested = capacity;
-    return div_i64(requested * 100, capacity);
+    return div_i64<SMALL>(requested * 100, capacity);
   }
   if (requested > capacity) return 0;
-  return div_i64((capacity - requested) * 100, capacity);
+  return div_i64<SMALL>((capacity - requested) * 100, capacity);
 }
 
 // NodeResourcesFit.Score (resourceAllocationScorer.score, useRequested=false)
+template <bool SMALL = false>
 __device__ __forceinline__ int64_t fit_score(const DevCluster& c, const kss_profile& prof, const kss_pod& p, int n,
                                              const NodeRow& row) {
   const size_t N = (size_t)c.N;
@@ -292,11 +347,11 @@ __device__ __forceinline__ int64_t fit_score(const DevCluster& c, const kss_prof
                          : r == KSS_RES_EPHEMERAL ? row.req[2]
                                                   : c.requested[(size_t)r * N + n];
     if (alloc == 0) continue;
-    node_score += alloc_score(prof.fit_strategy, base + preq, alloc) * prof.fit_weight[i];
+    node_score += alloc_score<SMALL>(prof.fit_strategy, base + preq, alloc) * prof.fit_weight[i];
     weight_sum += prof.fit_weight[i];
   }
   if (weight_sum == 0) return 0;
-  return div_i64(node_score, weight_sum);
+  return div_i64<SMALL>(node_score, weight_sum);
 }
 
 // NodeResourcesBalancedAllocation.Score (balancedResourceScorer, useRequested=true)
@@ -360,14 +415,8 @@ __device__ __forceinline__ int64_t tt_score(const NodeRow& row, const kss_pod& p
   return (int64_t)__popcll(row.ts & ~p.tol_soft);
 }
 
-// NodeAffinity.Score: PreferredSchedulingTerms.Score
 __device__ __forceinline__ int64_t na_score(const DevCluster& c, const DevPods& P, const kss_pod& p, int n) {
-  int64_t s = 0;
-  for (int t = 0; t < p.pref_len; t++) {
-    const kss_term& term = P.terms[p.pref_off + t];
-    if (term_match(c, P, term, n)) s += term.weight;
-  }
-  return s;
+  return na_score_t(c, P.reqs, P.terms, P.ints, p, (int64_t)c.node_base + n, [&](int key) { return label_of(c, key, n); });
 }
 
 }  // namespace kss

@@ -7,6 +7,9 @@
 //                sequential batch (kss_schedule_batch), the drop-in per-pod call
 //                (kss_eval_pod, no commit) and the what-if scenario sweep
 //                (kss_schedule_scenarios, grid = #scenarios).
+//   k_simple     batches without PodTopologySpread / InterPodAffinity programs and
+//                without a result record: node rows in registers, pod programs as
+//                LDS blobs, one exchange per pod (kss_simple.cuh).
 //   k_commit     one lane: AssumePod / ForgetPod delta on one node row.
 #include <hip/hip_runtime.h>
 
@@ -20,6 +23,7 @@
 
 #include "kss_host.h"
 #include "kss_sched.cuh"
+#include "kss_simple.cuh"
 
 using namespace kss;
 
@@ -65,6 +69,8 @@ struct DevJob {
   size_t slot_bytes;
   int32_t* chosen;
   PodMeta* meta;
+  const uint8_t* blobs;  // k_simple: serialized pod programs, blob_stride bytes each
+  int32_t blob_stride;
 };
 
 }  // namespace
@@ -136,6 +142,17 @@ __global__ __launch_bounds__(KSS_MAX_THREADS) void k_schedule(const DevJob* __re
     KSS_STAMP(S, 6);
   }
   if (c.nc64 && job.commit) cache_writeback(c, S.hi);
+}
+
+// grid = n_jobs * W, as k_schedule; NPT node slots per lane, held in registers.
+template <int NPT>
+__global__ __launch_bounds__(KSS_MAX_THREADS) void k_simple(const DevJob* __restrict__ jobs, kss_profile prof, int W,
+                                                            unsigned long long* gran, int* err, unsigned long long* stamps) {
+  extern __shared__ __attribute__((aligned(16))) long long smem[];
+  const int ji = blockIdx.x / W, w = blockIdx.x % W;
+  const DevJob job = jobs[ji];
+  simple_schedule<NPT>(job.c, job.blobs, job.blob_stride, job.n_pods, job.chosen, job.meta, prof, W, w,
+                       gran ? gran + (size_t)ji * 2 * W * SX_VALS : nullptr, err, ji == 0 ? stamps : nullptr, smem);
 }
 
 __global__ void k_commit(DevCluster c, DevPods P, int pi, int local, int sign) {
@@ -212,6 +229,14 @@ struct kss_ctx {
   int last_geom[3] = {0, 0, 0};
   const char* stamps_file = nullptr;  // KSS_STAMPS_FILE: dump per-phase timestamps of each launch
   DevBuf stamp_buf;
+  // staged pod programs serialized for k_simple (blob_stride 0: some pod needs k_schedule)
+  DevBuf blob_buf;
+  std::vector<uint8_t> blob_host;
+  int blob_stride = 0;
+  bool no_simple = false;  // KSS_NO_SIMPLE: always launch k_schedule
+  int last_kernel = 0;     // 0 k_schedule, 1 k_simple
+  int meta_n = 0;          // pods with an outcome in meta_host
+  bool small_values = false;  // every allocatable cpu/mem/eph < 2^46: k_simple's divisions stay below 2^53
 };
 
 namespace {
@@ -294,6 +319,80 @@ int validate(const kss_cluster* cl, const kss_podset* ps, int n) {
     if (p.n_hard > MAXH || p.n_soft > MAXS) return fail(KSS_E_UNSUPPORTED, "too many spread constraints for the device path");
   }
   return 0;
+}
+
+// One pod program as a position-independent blob for k_simple (kss_simple.cuh): the pod
+// record, then only the requirements / terms / ints it references, every offset rebased
+// into the blob.  Writes to dst when given; returns the blob size.
+size_t serialize_pod(const kss_podset* ps, int i, uint8_t* dst) {
+  const kss_pod& src = ps->pods[i];
+  kss_pod q = src;
+  std::vector<kss_req> R;
+  std::vector<kss_term> T;
+  std::vector<int32_t> I;
+  auto add_req = [&](const kss_req& r0) {
+    kss_req r = r0;
+    if (r.op == KSS_OP_IN || r.op == KSS_OP_NOTIN) {
+      r.list_off = (int32_t)I.size();
+      I.insert(I.end(), ps->ints + r0.list_off, ps->ints + r0.list_off + r0.list_len);
+    }
+    R.push_back(r);
+  };
+  auto add_terms = [&](int off, int len) {
+    const int first = (int)T.size();
+    T.insert(T.end(), ps->terms + off, ps->terms + off + len);
+    for (int t = 0; t < len; t++) {
+      const kss_term& s0 = ps->terms[off + t];
+      T[first + t].req_off = (int32_t)R.size();
+      for (int k = 0; k < s0.req_len; k++) add_req(ps->reqs[s0.req_off + k]);
+    }
+    return first;
+  };
+  q.sel_off = 0;
+  for (int k = 0; k < src.sel_len; k++) add_req(ps->reqs[src.sel_off + k]);
+  q.aff_off = add_terms(src.aff_off, src.aff_len);
+  q.pref_off = add_terms(src.pref_off, src.pref_len);
+  if (src.names_len >= 0) {
+    q.names_off = (int32_t)I.size();
+    I.insert(I.end(), ps->ints + src.names_off, ps->ints + src.names_off + src.names_len);
+  }
+  q.own_terms_off = (int32_t)I.size();
+  I.insert(I.end(), ps->ints + src.own_terms_off, ps->ints + src.own_terms_off + src.own_terms_len);
+  q.spread_off = 0;
+  q.ipa_off = 0;
+  BlobHdr h{};
+  const size_t ro = blob_body_off(), to = ro + align_up(R.size() * sizeof(kss_req), 16),
+               io = to + align_up(T.size() * sizeof(kss_term), 16), end = io + align_up(I.size() * sizeof(int32_t), 16);
+  h.req_off = (int32_t)ro;
+  h.term_off = (int32_t)to;
+  h.ints_off = (int32_t)io;
+  h.n_reqs = (int32_t)R.size();
+  h.n_terms = (int32_t)T.size();
+  h.n_ints = (int32_t)I.size();
+  if (dst) {
+    memcpy(dst, &q, sizeof(q));
+    memcpy(dst + blob_hdr_off(), &h, sizeof(h));
+    if (!R.empty()) memcpy(dst + ro, R.data(), R.size() * sizeof(kss_req));
+    if (!T.empty()) memcpy(dst + to, T.data(), T.size() * sizeof(kss_term));
+    if (!I.empty()) memcpy(dst + io, I.data(), I.size() * sizeof(int32_t));
+  }
+  return end;
+}
+
+// Blobs of every pod of a (validated) podset at one stride; returns the stride, or 0 when
+// some pod needs k_schedule (spread / inter-pod programs, or a program over BLOB_MAX).
+int build_blobs(const kss_podset* ps, std::vector<uint8_t>& out) {
+  size_t mx = 16;
+  for (int i = 0; i < ps->n_pods; i++) {
+    const kss_pod& p = ps->pods[i];
+    if (p.n_hard | p.n_soft | p.ipa_len) return 0;
+    mx = std::max(mx, serialize_pod(ps, i, nullptr));
+  }
+  const size_t stride = align_up(mx, 64);
+  if (stride > (size_t)BLOB_MAX) return 0;
+  out.assign(stride * (size_t)std::max(ps->n_pods, 1), 0);
+  for (int i = 0; i < ps->n_pods; i++) serialize_pod(ps, i, out.data() + stride * (size_t)i);
+  return (int)stride;
 }
 
 struct ClusterLayout {
@@ -460,6 +559,7 @@ kss_ctx* kss_create(const kss_config* cfg, const kss_profile* prof) {
   if (ctx->n_cu <= 0) ctx->n_cu = 1;
   if (const char* e = getenv("KSS_SHARDS")) ctx->force_w = std::max(0, atoi(e));
   ctx->stamps_file = getenv("KSS_STAMPS_FILE");
+  ctx->no_simple = getenv("KSS_NO_SIMPLE") != nullptr;
   if (const char* e = getenv("KSS_NODES_PER_SHARD")) ctx->nodes_per_shard = std::max(1, atoi(e));
   if (const char* e = getenv("KSS_THREADS")) ctx->pref_threads = std::min(KSS_MAX_THREADS, std::max(64, atoi(e)));
   if (hipSetDevice(cfg->device) != hipSuccess || hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess ||
@@ -483,6 +583,8 @@ void kss_destroy(kss_ctx* ctx) {
   ctx->meta_buf.release();
   ctx->chosen_buf.release();
   ctx->job_buf.release();
+  ctx->blob_buf.release();
+  ctx->stamp_buf.release();
   ctx->gran_buf.release();
   ctx->err_buf.release();
   if (ctx->ev0) hipEventDestroy(ctx->ev0);
@@ -523,10 +625,17 @@ int kss_load_cluster(kss_ctx* ctx, const kss_cluster* cl) {
                              ctx->stream));
   HIP_TRY(hipStreamSynchronize(ctx->stream));
   ctx->host = *cl;
+  {
+    bool small = true;
+    for (size_t i = 0; i < 3 * N && small; i++) small = cl->alloc[i] >= 0 && cl->alloc[i] < (1ll << 46);
+    for (int i = 0; i < ctx->prof.fit_n && small; i++) small = ctx->prof.fit_weight[i] >= 0 && ctx->prof.fit_weight[i] < (1ll << 20);
+    ctx->small_values = small;
+  }
   ctx->key_card_h.assign(cl->key_card, cl->key_card + cl->n_label_keys);
   ctx->key_flags_h.assign(cl->key_flags, cl->key_flags + cl->n_label_keys);
   ctx->loaded = true;
   ctx->recorded = 0;
+  ctx->meta_n = 0;
   ctx->staged_n = -1;
   return 0;
 }
@@ -634,7 +743,12 @@ static bool pick_geometry(int maxN, int W, int pref_threads, Geometry& g) {
   int t = std::min(KSS_MAX_THREADS, std::max(pref_threads, 64));
   if (per < t) t = std::max(64, (per + 63) / 64 * 64);
   int npt = (per + t - 1) / t;
-  while (npt > 4 && t < KSS_MAX_THREADS) {
+  const char* ft = getenv("KSS_FORCE_THREADS");  // tuning / diagnosis: exact workgroup size
+  if (ft) {
+    t = std::min(KSS_MAX_THREADS, std::max(64, atoi(ft) / 64 * 64));
+    npt = (per + t - 1) / t;
+  }
+  while (!ft && npt > 4 && t < KSS_MAX_THREADS) {
     t = std::min(KSS_MAX_THREADS, t * 2);
     npt = (per + t - 1) / t;
   }
@@ -678,9 +792,32 @@ static int launch_schedule(hipStream_t st, const Geometry& g, int n_jobs, int bi
   return 0;
 }
 
-// run k_schedule on the loaded cluster for pods [0, n); results stay on the device
+// Launch k_simple (same grid and co-residency rule as k_schedule).
+static int launch_simple(hipStream_t st, const Geometry& g, int n_jobs, int stride, int n_keys, const DevJob* jobs,
+                         const kss_profile& prof, unsigned long long* gran, int* err,
+                         unsigned long long* stamps = nullptr) {
+  const int npt = g.npt <= 1 ? 1 : (g.npt <= 2 ? 2 : 4);
+  const size_t shmem = simple_lds_bytes(stride, n_keys, npt * g.threads);
+  const void* fn = npt == 1 ? (const void*)k_simple<1> : (npt == 2 ? (const void*)k_simple<2> : (const void*)k_simple<4>);
+  HIP_TRY(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shmem));
+  const dim3 grid((unsigned)(n_jobs * g.W)), block((unsigned)g.threads);
+  kss_profile pr = prof;
+  int W = g.W;
+  void* args[] = {(void*)&jobs, (void*)&pr, (void*)&W, (void*)&gran, (void*)&err, (void*)&stamps};
+  if (g.W > 1) HIP_TRY(hipLaunchCooperativeKernel(fn, grid, block, args, (unsigned)shmem, st));
+  else HIP_TRY(hipLaunchKernel(fn, grid, block, args, shmem, st));
+  return 0;
+}
+
+static bool simple_fits(const Geometry& g, int stride, int n_keys) {
+  const int npt = g.npt <= 1 ? 1 : (g.npt <= 2 ? 2 : 4);
+  return stride > 0 && stride <= 32 * g.threads && g.npt <= 4 && g.W <= 64 * SX_CHUNKS &&
+         simple_lds_bytes(stride, n_keys, npt * g.threads) <= KSS_LDS_BUDGET;
+}
+
+// run k_schedule / k_simple on the loaded cluster for pods [0, n); results stay on the device
 static int run_single(kss_ctx* ctx, const PlanNeeds& need, const DevPods& dp, int n, bool commit, bool record,
-                      bool keep_norm, uint32_t flags, int32_t* chosen_out) {
+                      bool keep_norm, uint32_t flags, int32_t* chosen_out, bool staged = false) {
   const size_t N = (size_t)ctx->dc.N;
   const SlotLayout SL(N);
   const int nslots = record ? std::max(n, 1) : 1;
@@ -716,6 +853,10 @@ static int run_single(kss_ctx* ctx, const PlanNeeds& need, const DevPods& dp, in
   job.slot_bytes = SL.bytes;
   job.chosen = (int32_t*)ctx->chosen_buf.p;
   job.meta = (PodMeta*)ctx->meta_buf.p;
+  job.blobs = staged && ctx->blob_stride ? (const uint8_t*)ctx->blob_buf.p : nullptr;
+  job.blob_stride = ctx->blob_stride;
+  const bool simple = job.blobs && commit && !record && !keep_norm && !need.general && ctx->dc.n_scalar == 0 && ctx->small_values &&
+                      !ctx->no_simple && !(flags & KSS_SCHED_GENERAL_KERNEL) && simple_fits(g, ctx->blob_stride, ctx->dc.n_keys);
   rc = ctx->job_buf.ensure(sizeof(DevJob));
   if (rc) return rc;
   rc = ctx->err_buf.ensure(16);
@@ -738,9 +879,14 @@ static int run_single(kss_ctx* ctx, const PlanNeeds& need, const DevPods& dp, in
     stamps = (unsigned long long*)ctx->stamp_buf.p;
     HIP_TRY(hipMemsetAsync(stamps, 0, stamp_bytes, ctx->stream));
   }
-  rc = launch_schedule(ctx->stream, g, 1, std::max(need.bins_cap, 0), need.general, ctx->dc.n_keys, (const DevJob*)ctx->job_buf.p,
-                       ctx->prof, gran, (int*)ctx->err_buf.p, stamps);
+  if (simple)
+    rc = launch_simple(ctx->stream, g, 1, ctx->blob_stride, ctx->dc.n_keys, (const DevJob*)ctx->job_buf.p, ctx->prof, gran,
+                       (int*)ctx->err_buf.p, stamps);
+  else
+    rc = launch_schedule(ctx->stream, g, 1, std::max(need.bins_cap, 0), need.general, ctx->dc.n_keys,
+                         (const DevJob*)ctx->job_buf.p, ctx->prof, gran, (int*)ctx->err_buf.p, stamps);
   if (rc) return rc;
+  ctx->last_kernel = simple ? 1 : 0;
   HIP_TRY(hipEventRecord(ctx->ev1, ctx->stream));
   HIP_TRY(hipStreamSynchronize(ctx->stream));
   float ms = 0;
@@ -756,7 +902,8 @@ static int run_single(kss_ctx* ctx, const PlanNeeds& need, const DevPods& dp, in
   ctx->meta_host.resize((size_t)std::max(n, 1));
   HIP_TRY(hipMemcpy(ctx->meta_host.data(), ctx->meta_buf.p, sizeof(PodMeta) * (size_t)std::max(n, 1), hipMemcpyDeviceToHost));
   if (chosen_out && n) HIP_TRY(hipMemcpy(chosen_out, ctx->chosen_buf.p, sizeof(int32_t) * n, hipMemcpyDeviceToHost));
-  ctx->recorded = record ? n : (n > 0 ? 1 : 0);
+  ctx->recorded = record ? n : (n > 0 && !simple ? 1 : 0);
+  ctx->meta_n = n;
   if (stamps) {
     std::vector<unsigned long long> h(8 * KSS_NSTAMP_PODS);
     HIP_TRY(hipMemcpy(h.data(), stamps, stamp_bytes, hipMemcpyDeviceToHost));
@@ -765,6 +912,16 @@ static int run_single(kss_ctx* ctx, const PlanNeeds& need, const DevPods& dp, in
       fclose(f);
     }
   }
+  return 0;
+}
+
+// serialize the staged podset for k_simple (host copy kept alive for the async upload)
+static int stage_blobs(kss_ctx* ctx, const kss_podset* ps) {
+  ctx->blob_stride = build_blobs(ps, ctx->blob_host);
+  if (!ctx->blob_stride) return 0;
+  int rc = ctx->blob_buf.ensure(ctx->blob_host.size());
+  if (rc) return rc;
+  HIP_TRY(hipMemcpyAsync(ctx->blob_buf.p, ctx->blob_host.data(), ctx->blob_host.size(), hipMemcpyHostToDevice, ctx->stream));
   return 0;
 }
 
@@ -849,9 +1006,11 @@ int kss_schedule_batch(kss_ctx* ctx, const kss_podset* ps, int32_t n, uint32_t f
   HIP_TRY(hipSetDevice(ctx->cfg.device));
   rc = upload_podset(ctx->stream, ctx->pod_buf, ps, ctx->dp);
   if (rc) return rc;
+  if ((rc = stage_blobs(ctx, ps))) return rc;
   ctx->staged_n = ps->n_pods;
   ctx->staged_need = plan_needs(ctx->key_card_h.data(), ctx->key_flags_h.data(), ps, ps->n_pods);
-  rc = run_single(ctx, ctx->staged_need, ctx->dp, n, /*commit=*/true, record, /*keep_norm=*/record, flags, chosen_out);
+  rc = run_single(ctx, ctx->staged_need, ctx->dp, n, /*commit=*/true, record, /*keep_norm=*/record, flags, chosen_out,
+                  /*staged=*/true);
   if (rc) return rc;
   for (int i = 0; i < n; i++)
     if (ctx->meta_host[i].status == 4) return fail(KSS_E_UNSUPPORTED, "pod program exceeds the device path's per-pod limits");
@@ -866,6 +1025,7 @@ int kss_stage_pods(kss_ctx* ctx, const kss_podset* ps) {
   HIP_TRY(hipSetDevice(ctx->cfg.device));
   rc = upload_podset(ctx->stream, ctx->pod_buf, ps, ctx->dp);
   if (rc) return rc;
+  if ((rc = stage_blobs(ctx, ps))) return rc;
   HIP_TRY(hipStreamSynchronize(ctx->stream));
   ctx->staged_n = ps->n_pods;
   ctx->staged_need = plan_needs(ctx->key_card_h.data(), ctx->key_flags_h.data(), ps, ps->n_pods);
@@ -879,7 +1039,8 @@ int kss_run_staged(kss_ctx* ctx, int32_t n, uint32_t flags, int32_t* chosen_out)
   if (record && n > ctx->cfg.max_pods_record) return fail(KSS_E_INVAL, "record capacity (max_pods_record) exceeded");
   std::lock_guard<std::mutex> lk(ctx->mu);
   HIP_TRY(hipSetDevice(ctx->cfg.device));
-  int rc = run_single(ctx, ctx->staged_need, ctx->dp, n, /*commit=*/true, record, /*keep_norm=*/record, flags, chosen_out);
+  int rc = run_single(ctx, ctx->staged_need, ctx->dp, n, /*commit=*/true, record, /*keep_norm=*/record, flags, chosen_out,
+                      /*staged=*/true);
   if (rc) return rc;
   for (int i = 0; i < n; i++)
     if (ctx->meta_host[i].status == 4) return fail(KSS_E_UNSUPPORTED, "pod program exceeds the device path's per-pod limits");
@@ -904,6 +1065,26 @@ int kss_last_timing(kss_ctx* ctx, double* device_ms, int32_t* launches) {
 int kss_last_geometry(kss_ctx* ctx, int32_t* out3) {
   if (!ctx || !out3) return fail(KSS_E_INVAL, "bad arguments");
   for (int i = 0; i < 3; i++) out3[i] = ctx->last_geom[i];
+  return 0;
+}
+
+int kss_last_kernel(kss_ctx* ctx) {
+  if (!ctx) return fail(KSS_E_INVAL, "null ctx");
+  return ctx->last_kernel;
+}
+
+int kss_fetch_meta(kss_ctx* ctx, int32_t first, int32_t n, int64_t* out) {
+  if (!ctx || (n > 0 && !out)) return fail(KSS_E_INVAL, "bad arguments");
+  if (first < 0 || n < 0 || first + n > ctx->meta_n) return fail(KSS_E_NOTFOUND, "pod outcome not available");
+  for (int i = 0; i < n; i++) {
+    const PodMeta& m = ctx->meta_host[first + i];
+    int64_t* o = out + 5 * (size_t)i;
+    o[0] = m.chosen;
+    o[1] = m.n_feasible;
+    o[2] = m.scored;
+    o[3] = m.status;
+    o[4] = m.best_total;
+  }
   return 0;
 }
 

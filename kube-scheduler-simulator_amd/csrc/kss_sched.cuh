@@ -694,6 +694,7 @@ __device__ __forceinline__ bool schedule_pod(const DevCluster& c, const DevPods&
       }
     }
     if (out) {
+      KSS_DCHECK(n >= 0 && n < c.N, "out n", n, c.N);
       out->fail[n] = (uint8_t)f;
       out->detail[n] = detail;
     }
@@ -805,6 +806,7 @@ __device__ __forceinline__ bool schedule_pod(const DevCluster& c, const DevPods&
       if (pl.soft_mode[i] == SOFT_HOST) size = nf - nign;
       else if (pl.soft_mode[i] == SOFT_DIRECT) size = sdirect[i] + ((smissing >> i) & 1);
       else size = sz[i];
+      KSS_DCHECK(size >= 0 && size <= c.N + 2, "log_table size", size, c.N);
       w[i] = c.log_table[size];  // topologyNormalizingWeight = math.Log(float64(size+2))
     }
     pts_min = INT64_MAX;
@@ -919,6 +921,7 @@ __device__ __forceinline__ bool schedule_pod(const DevCluster& c, const DevPods&
 // hot columns are updated in LDS (written back to HBM when the launch ends).
 __device__ __forceinline__ void commit_pod(const DevCluster& c, const DevPods& P, const kss_pod& p, int local, int sign) {
   const size_t N = (size_t)c.N;
+  KSS_DCHECK(local >= 0 && local < c.N && p.cls < c.class_cap, "commit local/cls", local, p.cls);
   if (c.nc64) {
     const int i = local - c.nc_lo, C = c.nc_cap;
 #pragma unroll

@@ -97,6 +97,7 @@ KSS_FIT_MOST_ALLOCATED = 1
 KSS_SCHED_RECORD = 1 << 0
 KSS_SCHED_FORCE_MULTI_WG = 1 << 1
 KSS_SCHED_FORCE_SINGLE_WG = 1 << 2
+KSS_SCHED_GENERAL_KERNEL = 1 << 3
 
 P = C.POINTER
 i32, i64, u32, u64, u8, u16 = C.c_int32, C.c_int64, C.c_uint32, C.c_uint64, C.c_uint8, C.c_uint16

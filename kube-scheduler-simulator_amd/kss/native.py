@@ -14,7 +14,9 @@ import numpy as np
 
 from . import abi
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libkss.so")
+# KSS_LIB=dbg selects the bounds-checked diagnostic build (make -C csrc debug)
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)),
+                        "libkss_dbg.so" if os.environ.get("KSS_LIB") == "dbg" else "libkss.so")
 P = C.POINTER
 
 
@@ -46,6 +48,8 @@ SIGNATURES = [
                                          P(C.c_int32), P(C.c_double)]),
     ("kss_last_timing", C.c_int, [C.c_void_p, P(C.c_double), P(C.c_int32)]),
     ("kss_last_geometry", C.c_int, [C.c_void_p, P(C.c_int32)]),
+    ("kss_last_kernel", C.c_int, [C.c_void_p]),
+    ("kss_fetch_meta", C.c_int, [C.c_void_p, C.c_int32, C.c_int32, P(C.c_int64)]),
     ("kss_set_names", C.c_int, [C.c_void_p, P(abi.Names)]),
     ("kss_format_annotations", C.c_int, [C.c_void_p, P(abi.PodResult), C.c_int32, C.c_char_p, C.c_size_t,
                                          P(C.c_size_t)]),
@@ -250,6 +254,18 @@ class Context:
         out = (C.c_int32 * 3)()
         check(lib().kss_last_geometry(self.h, out))
         return {"shards": out[0], "threads": out[1], "nodes_per_lane": out[2]}
+
+    def last_kernel(self) -> str:
+        k = lib().kss_last_kernel(self.h)
+        if k < 0:
+            check(k)
+        return "k_simple" if k == 1 else "k_schedule"
+
+    def fetch_meta(self, n: int, first: int = 0) -> np.ndarray:
+        """(n, 5) int64: chosen, n_feasible, scored, status, best_total of pods [first, first+n)."""
+        out = np.zeros((max(n, 1), 5), np.int64)
+        check(lib().kss_fetch_meta(self.h, first, n, out.ctypes.data_as(P(C.c_int64))))
+        return out[:n]
 
     def format_annotations(self, result: PodResult) -> Dict[str, str]:
         L = lib()

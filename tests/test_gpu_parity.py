@@ -82,6 +82,63 @@ def test_schedule_batch_matches_oracle(config, n_nodes, n_pods, mode):
     _state_equal(ctx, st, n_nodes, s.cluster.n_classes, s.cluster.n_terms)
 
 
+@pytest.mark.parametrize("mode", ["auto", "single", "multi"])
+@pytest.mark.parametrize("config,n_nodes,n_pods", [
+    (1, 100, 1000),   # C1 exactly
+    (2, 700, 400),
+    (5, 1000, 300),
+    (1, 3, 50),       # tiny: single-feasible and unschedulable pods
+    (2, 1500, 150),   # several nodes per lane
+    (2, 5000, 120),   # C2 cluster
+])
+def test_compact_kernel_matches_oracle(config, n_nodes, n_pods, mode):
+    """k_simple (register-resident rows, one speculative exchange per pod): chosen node,
+    per-pod outcome (feasible count, scored, status, best total) and the final node state
+    equal the oracle's."""
+    if mode == "single" and n_nodes > 2048:
+        pytest.skip("more nodes than one workgroup's register rows hold (4 x 512)")
+    prof = abi.default_profile()
+    s = native.Synth(config, 0, n_nodes, n_pods)
+    chosen_o, res, st = oracle_c.schedule(prof, s.cluster, s.pods, n_pods, n_nodes, record=True, threads=8,
+                                          n_classes=s.cluster.n_classes, n_terms=s.cluster.n_terms)
+    ctx = native.Context(prof)
+    ctx.load(s.cluster)
+    chosen_g = ctx.schedule_batch(s.pods, n_pods, flags=MODES[mode])
+    assert ctx.last_kernel() == "k_simple"
+    geo = ctx.last_geometry()
+    if mode == "single":
+        assert geo["shards"] == 1
+    if mode == "multi" and n_nodes >= 4:
+        assert geo["shards"] > 1
+    np.testing.assert_array_equal(chosen_g, chosen_o)
+    meta = ctx.fetch_meta(n_pods)
+    for j in range(n_pods):
+        m = res.meta(j)
+        got = dict(chosen=meta[j, 0], n_feasible=meta[j, 1], scored=meta[j, 2], status=meta[j, 3])
+        assert got == {k: m[k] for k in got}, (j, got, m)
+        if m["scored"]:
+            assert meta[j, 4] == m["best_total"], j
+    _state_equal(ctx, st, n_nodes, s.cluster.n_classes, s.cluster.n_terms)
+
+
+def test_compact_and_general_kernels_agree_at_c2_scale():
+    prof = abi.default_profile()
+    s = native.Synth(2, 0, 5000, 2000)
+    ctx = native.Context(prof)
+    ctx.load(s.cluster)
+    ctx.stage(s.pods)
+    a = ctx.run_staged(2000).copy()
+    assert ctx.last_kernel() == "k_simple"
+    st_a = ctx.node_state()
+    ctx.reset()
+    b = ctx.schedule_batch(s.pods, 2000, flags=abi.KSS_SCHED_GENERAL_KERNEL)
+    assert ctx.last_kernel() == "k_schedule"
+    np.testing.assert_array_equal(a, b)
+    st_b = ctx.node_state()
+    for k in st_a:
+        np.testing.assert_array_equal(st_a[k], st_b[k])
+
+
 def test_schedule_without_record_same_choices():
     prof = abi.default_profile()
     s = native.Synth(3, 0, 400, 300)
