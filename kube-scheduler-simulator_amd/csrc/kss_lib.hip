@@ -144,15 +144,18 @@ __global__ __launch_bounds__(KSS_MAX_THREADS) void k_schedule(const DevJob* __re
   if (c.nc64 && job.commit) cache_writeback(c, S.hi);
 }
 
-// grid = n_jobs * W, as k_schedule; NPT node slots per lane, held in registers.
-template <int NPT>
+// grid = n_jobs * W, as k_schedule; each shard's nodes live in LDS (cap slots).
+// DEF: the profile is the v1.26 default, folded into the code.
+template <bool DEF>
 __global__ __launch_bounds__(KSS_MAX_THREADS) void k_simple(const DevJob* __restrict__ jobs, kss_profile prof, int W,
-                                                            unsigned long long* gran, int* err, unsigned long long* stamps) {
+                                                            int cap, unsigned long long* gran, int* err,
+                                                            unsigned long long* stamps) {
   extern __shared__ __attribute__((aligned(16))) long long smem[];
   const int ji = blockIdx.x / W, w = blockIdx.x % W;
   const DevJob job = jobs[ji];
-  simple_schedule<NPT>(job.c, job.blobs, job.blob_stride, job.n_pods, job.chosen, job.meta, prof, W, w,
-                       gran ? gran + (size_t)ji * 2 * W * SX_VALS : nullptr, err, ji == 0 ? stamps : nullptr, smem);
+  const kss_profile P = DEF ? default_profile_c() : prof;
+  simple_schedule(job.c, job.blobs, job.blob_stride, job.n_pods, job.chosen, job.meta, P, W, w, cap,
+                  gran ? gran + (size_t)ji * 2 * W * SX_VALS : nullptr, err, ji == 0 ? stamps : nullptr, smem);
 }
 
 __global__ void k_commit(DevCluster c, DevPods P, int pi, int local, int sign) {
@@ -792,27 +795,41 @@ static int launch_schedule(hipStream_t st, const Geometry& g, int n_jobs, int bi
   return 0;
 }
 
+// Field-wise profile equality (padding excluded).
+static bool same_profile(const kss_profile& a, const kss_profile& b) {
+  bool eq = a.filter_enabled == b.filter_enabled && a.score_enabled == b.score_enabled &&
+            a.fit_strategy == b.fit_strategy && a.fit_n == b.fit_n && a.ba_n == b.ba_n &&
+            a.hard_pod_affinity_weight == b.hard_pod_affinity_weight && a.system_defaulted == b.system_defaulted;
+  for (int i = 0; i < KSS_NSCORE; i++) eq &= a.weight[i] == b.weight[i];
+  for (int i = 0; i < 4; i++) eq &= a.fit_res[i] == b.fit_res[i] && a.fit_weight[i] == b.fit_weight[i] && a.ba_res[i] == b.ba_res[i];
+  return eq;
+}
+
+// Node slots per shard for k_simple: every lane's share, plus one spare slot when it
+// fits (the spare slot re-evaluates the candidate node in the same pass).
+static int simple_cap(const Geometry& g) { return g.npt * g.threads; }
+
 // Launch k_simple (same grid and co-residency rule as k_schedule).
 static int launch_simple(hipStream_t st, const Geometry& g, int n_jobs, int stride, int n_keys, const DevJob* jobs,
                          const kss_profile& prof, unsigned long long* gran, int* err,
                          unsigned long long* stamps = nullptr) {
-  const int npt = g.npt <= 1 ? 1 : (g.npt <= 2 ? 2 : 4);
-  const size_t shmem = simple_lds_bytes(stride, n_keys, npt * g.threads);
-  const void* fn = npt == 1 ? (const void*)k_simple<1> : (npt == 2 ? (const void*)k_simple<2> : (const void*)k_simple<4>);
+  int cap = simple_cap(g);
+  const size_t shmem = simple_lds_bytes(stride, n_keys, cap);
+  const bool def = same_profile(prof, default_profile_c());
+  const void* fn = def ? (const void*)k_simple<true> : (const void*)k_simple<false>;
   HIP_TRY(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shmem));
   const dim3 grid((unsigned)(n_jobs * g.W)), block((unsigned)g.threads);
   kss_profile pr = prof;
   int W = g.W;
-  void* args[] = {(void*)&jobs, (void*)&pr, (void*)&W, (void*)&gran, (void*)&err, (void*)&stamps};
+  void* args[] = {(void*)&jobs, (void*)&pr, (void*)&W, (void*)&cap, (void*)&gran, (void*)&err, (void*)&stamps};
   if (g.W > 1) HIP_TRY(hipLaunchCooperativeKernel(fn, grid, block, args, (unsigned)shmem, st));
   else HIP_TRY(hipLaunchKernel(fn, grid, block, args, shmem, st));
   return 0;
 }
 
 static bool simple_fits(const Geometry& g, int stride, int n_keys) {
-  const int npt = g.npt <= 1 ? 1 : (g.npt <= 2 ? 2 : 4);
-  return stride > 0 && stride <= 32 * g.threads && g.npt <= 4 && g.W <= 64 * SX_CHUNKS &&
-         simple_lds_bytes(stride, n_keys, npt * g.threads) <= KSS_LDS_BUDGET;
+  return stride > 0 && stride <= 32 * g.threads && g.W <= 64 * SX_CHUNKS &&
+         simple_lds_bytes(stride, n_keys, simple_cap(g)) <= KSS_LDS_BUDGET;
 }
 
 // run k_schedule / k_simple on the loaded cluster for pods [0, n); results stay on the device

@@ -26,6 +26,36 @@ constexpr int BLOB_MAX = 4096;  // bytes per serialized pod program (host-checke
 constexpr int SX_VALS = 8;      // granules per shard per exchange: key lo/hi, H0 (nf, tt, na), H1 (nf, tt, na)
 constexpr int SX_CHUNKS = 1;    // shards swept 64 at a time: W <= 64
 
+// The v1.26 default profile (kss_default_profile, kss_host.cpp; plugins_test.go:184-204,
+// 878-1096) as a compile-time constant: k_simple<true> folds every weight and resource
+// choice of the scoring path into the code.
+__host__ __device__ constexpr kss_profile default_profile_c() {
+  kss_profile p{};
+  p.weight[KSS_S_TAINT_TOLERATION] = 3;
+  p.weight[KSS_S_NODE_AFFINITY] = 2;
+  p.weight[KSS_S_NODE_RESOURCES_FIT] = 1;
+  p.weight[KSS_S_VOLUME_BINDING] = 1;
+  p.weight[KSS_S_POD_TOPOLOGY_SPREAD] = 2;
+  p.weight[KSS_S_INTER_POD_AFFINITY] = 2;
+  p.weight[KSS_S_BALANCED_ALLOCATION] = 1;
+  p.weight[KSS_S_IMAGE_LOCALITY] = 1;
+  for (int i = 1; i <= KSS_NFILTER; i++) p.filter_enabled |= 1u << i;
+  p.score_enabled = (1u << KSS_NSCORE) - 1;
+  p.fit_strategy = KSS_FIT_LEAST_ALLOCATED;
+  p.fit_n = 2;
+  p.fit_res[0] = KSS_RES_CPU;
+  p.fit_res[1] = KSS_RES_MEMORY;
+  p.fit_weight[0] = 1;
+  p.fit_weight[1] = 1;
+  p.ba_n = 2;
+  p.ba_res[0] = KSS_RES_CPU;
+  p.ba_res[1] = KSS_RES_MEMORY;
+  p.hard_pod_affinity_weight = 1;
+  p.pct_nodes_to_score = 100;
+  p.system_defaulted = 1;
+  return p;
+}
+
 // Blob layout: kss_pod (every offset rebased into the blob) | BlobHdr | reqs | terms | ints.
 struct BlobHdr {
   int32_t req_off, term_off, ints_off;  // byte offsets from the blob start
@@ -101,6 +131,10 @@ struct SimpleHdr {
   int pad[3];
 };
 
+// Workgroup barrier that orders LDS only.  HIP's __syncthreads() also drains every
+// outstanding global load (vmcnt), which would put the blob prefetch on the critical path.
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
 // Workgroup reduction of K values; ONE barrier.  Parity alternates between calls, so a
 // fast wave writing the next reduction never overwrites a slot a slow wave still reads.
 template <int K>
@@ -112,7 +146,7 @@ __device__ __forceinline__ void block_red(SimpleHdr& H, int parity, long long (&
                                          : (ops[k] == OP_MAX ? wave_red<OP_MAX>(v[k]) : wave_red<OP_MIN>(v[k]));
     if (lane == 0) H.red[parity][wave][k] = r;
   }
-  __syncthreads();
+  lds_barrier();
 #pragma unroll
   for (int k = 0; k < K; k++) {
     long long a = H.red[parity][0][k];
@@ -224,7 +258,7 @@ __device__ __forceinline__ bool simple_sync(SimpleHdr& H, int& parity, long long
     const long long v[7] = {key, st[0], st[1], st[2], st[3], st[4], st[5]};
     simple_exchange(H, gran, W, w, epoch, err, v, per, node_base);
   }
-  __syncthreads();
+  lds_barrier();
   if (H.abort) return false;
 #pragma unroll
   for (int i = 0; i < 4; i++) R[i] = H.res[i];
@@ -303,7 +337,7 @@ __device__ __forceinline__ long long simple_key(const kss_profile& prof, const S
   return (long long)(((unsigned long long)(uint32_t)total << 32) | (0xFFFFFFFFull - g));
 }
 
-// NodeInfo.AddPod on a register row (requested, non-zero requested, pod count).
+// NodeInfo.AddPod on a node row (requested, non-zero requested, pod count).
 __device__ __forceinline__ void add_commit(NodeRow& r, const kss_pod& p) {
 #pragma unroll
   for (int k = 0; k < 3; k++) r.req[k] += p.commit_req[k];
@@ -312,56 +346,98 @@ __device__ __forceinline__ void add_commit(NodeRow& r, const kss_pod& p) {
   r.pods += 1;
 }
 
-// Pass A for the pod of blob B: evaluate every owned node on the current state (H0),
-// and the candidate node `cand` (cluster-local index, -1 none) once more with the
-// previous pod `q` committed on it (H1, into alt).  st = {nf0, tt0, na0, nf1, tt1, na1}.
-// The slot loop is kept rolled (slot NPT is the candidate's second evaluation), so the
-// evaluation body exists once in the kernel; register arrays are only touched through
-// constant-index select chains.
-template <int NPT>
-__device__ __forceinline__ void simple_pass_a(const DevCluster& c, const kss_profile& prof, const BlobView& B, int lo,
-                                              int hi, const NodeRow (&row)[NPT], SVal (&cur)[NPT], SVal& alt,
-                                              int cand, const kss_pod& q, const int32_t* lbl, int cap,
-                                              long long (&st)[6], unsigned long long* sp = nullptr) {
+// The shard's node state in LDS for the whole launch (slot s = node lo + s), and the
+// per-slot results of the next pod; slot `cap` of the results holds the candidate node
+// re-evaluated after the previous pod's commit (H1).
+struct SimpleShard {
+  int64_t* r64;  // [8][cap]: allocatable cpu/mem/eph, requested cpu/mem/eph, non-zero cpu/mem
+  uint64_t* rt;  // [2][cap]: NoSchedule/NoExecute taints, PreferNoSchedule taints
+  int32_t* r32;  // [3][cap]: pod count, allowed pods, node flags
+  int32_t* lbl;  // [n_keys][cap]: label value ids
+  int32_t* cv;   // [5][cap + 1]: filter verdict, TT, NA, Fit, BA
+  int cap;
+};
+
+__host__ __device__ inline size_t simple_lds_bytes(int stride, int n_keys, int cap) {
+  return sizeof(SimpleHdr) + 3 * (size_t)stride + (size_t)cap * (8 * 8 + 2 * 8 + 3 * 4 + 4 * (size_t)n_keys) +
+         20 * ((size_t)cap + 1);
+}
+
+__device__ __forceinline__ SimpleShard shard_view(uint8_t* base, int n_keys, int cap) {
+  SimpleShard L;
+  L.cap = cap;
+  L.r64 = reinterpret_cast<int64_t*>(base);
+  L.rt = reinterpret_cast<uint64_t*>(base + 64 * (size_t)cap);
+  L.r32 = reinterpret_cast<int32_t*>(base + 80 * (size_t)cap);
+  L.lbl = L.r32 + 3 * (size_t)cap;
+  L.cv = L.lbl + (size_t)n_keys * cap;
+  return L;
+}
+
+__device__ __forceinline__ NodeRow shard_row(const SimpleShard& L, int s) {
+  NodeRow r;
+  const int C = L.cap;
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    r.alloc[k] = L.r64[k * C + s];
+    r.req[k] = L.r64[(3 + k) * C + s];
+  }
+  r.nz[0] = L.r64[6 * C + s];
+  r.nz[1] = L.r64[7 * C + s];
+  r.th = L.rt[s];
+  r.ts = L.rt[C + s];
+  r.pods = L.r32[s];
+  r.allowed = L.r32[C + s];
+  r.flags = (uint32_t)L.r32[2 * C + s];
+  return r;
+}
+
+__device__ __forceinline__ SVal cv_get(const SimpleShard& L, int s) {
+  const int C1 = L.cap + 1;
+  return SVal{L.cv[s], L.cv[C1 + s], L.cv[2 * C1 + s], L.cv[3 * C1 + s], L.cv[4 * C1 + s]};
+}
+
+__device__ __forceinline__ void cv_put(const SimpleShard& L, int s, const SVal& e) {
+  const int C1 = L.cap + 1;
+  L.cv[s] = e.f;
+  L.cv[C1 + s] = e.tt;
+  L.cv[2 * C1 + s] = e.na;
+  L.cv[3 * C1 + s] = e.fit;
+  L.cv[4 * C1 + s] = e.ba;
+}
+
+// Pass A for the pod of blob B over the shard's `own` nodes on the current state (H0),
+// plus the candidate slot `cand_s` (-1 none) re-evaluated with the previous pod `q`
+// committed on it (H1), by the first slot without a node (slot `own`, which is slot
+// `cap` of lane 0 when the shard is full).  st = {nf0, tt0, na0, nf1, tt1, na1}.
+__device__ __forceinline__ void simple_pass_a(const DevCluster& c, const kss_profile& prof, const BlobView& B,
+                                              const SimpleShard& L, int lo, int own, int cand_s, const kss_pod& q,
+                                              long long (&st)[6], unsigned long long* sp) {
   const int tid = threadIdx.x, nt = blockDim.x;
   const kss_pod& p = *B.pod;
   const bool pre_ok = p.prefilter_status == 0;
   long long nf = 0, tt = 0, na = 0, nf1 = 0, tt1 = 0, na1 = 0;
-  int cj = -1;
-#pragma unroll
-  for (int j = 0; j < NPT; j++)
-    if (lo + j * nt + tid == cand) cj = j;
-#pragma unroll 1
-  for (int j = 0; j <= NPT; j++) {
-    const bool extra = j == NPT;
-    const int jj = extra ? (cj < 0 ? 0 : cj) : j;
-    const int n = lo + jj * nt + tid;
-    NodeRow r = row[0];
-#pragma unroll
-    for (int t = 1; t < NPT; t++)
-      if (t == jj) r = row[t];
+  for (int s = tid; s <= L.cap; s += nt) {
+    const bool extra = s == own && cand_s >= 0;
+    if (s >= own && !extra) continue;
+    const int ns = extra ? cand_s : s;
+    NodeRow r = shard_row(L, ns);
     if (extra) add_commit(r, q);
+    if (sp && s == 0) sp[7] = wall_clock64();
     SVal e{KSS_F_NOT_EVALUATED, 0, 0, 0, 0};
-    if (sp && tid == 0 && !extra) sp[7] = wall_clock64();
-    if (n < hi && pre_ok && (!extra || cj >= 0))
-      e = simple_eval(c, prof, B, p, n, r, lbl, cap, jj * nt + tid, (sp && tid == 0 && !extra) ? sp : nullptr);
-    const bool pass = e.f == 0;
-    if (!extra) {
-#pragma unroll
-      for (int t = 0; t < NPT; t++)
-        if (t == j) cur[t] = e;
-      if (pass) {
+    if (pre_ok) e = simple_eval(c, prof, B, p, lo + ns, r, L.lbl, L.cap, ns, (sp && s == 0) ? sp : nullptr);
+    cv_put(L, extra ? L.cap : s, e);
+    if (e.f == 0) {
+      if (!extra) {
         nf++;
         tt = e.tt > tt ? e.tt : tt;
         na = e.na > na ? e.na : na;
       }
-    } else {
-      alt = e;
-    }
-    if (pass && (extra || j != cj)) {
-      nf1++;
-      tt1 = e.tt > tt1 ? e.tt : tt1;
-      na1 = e.na > na1 ? e.na : na1;
+      if (s != cand_s) {
+        nf1++;
+        tt1 = e.tt > tt1 ? e.tt : tt1;
+        na1 = e.na > na1 ? e.na : na1;
+      }
     }
   }
   st[0] = nf;
@@ -372,35 +448,39 @@ __device__ __forceinline__ void simple_pass_a(const DevCluster& c, const kss_pro
   st[5] = na1;
 }
 
-__host__ __device__ inline size_t simple_lds_bytes(int stride, int n_keys, int cap) {
-  return sizeof(SimpleHdr) + 3 * (size_t)stride + 4 * (size_t)n_keys * (size_t)cap;
-}
-
 // The whole batch for shard w of one cluster (every pod commits).  On an exchange
 // timeout the error word is set and the shard leaves without writing node state back.
-template <int NPT>
 __device__ __forceinline__ void simple_schedule(DevCluster c, const uint8_t* __restrict__ blobs, int stride, int n_pods,
                                                 int32_t* chosen, PodMeta* meta, const kss_profile& prof, int W, int w,
-                                                unsigned long long* gran, int* err, unsigned long long* stamps,
-                                                long long* smem) {
-  const int tid = threadIdx.x, nt = blockDim.x, cap = NPT * nt;
+                                                int cap, unsigned long long* gran, int* err,
+                                                unsigned long long* stamps, long long* smem) {
+  const int tid = threadIdx.x, nt = blockDim.x;
   SimpleHdr& H = *reinterpret_cast<SimpleHdr*>(smem);
   uint8_t* ring = reinterpret_cast<uint8_t*>(smem) + sizeof(SimpleHdr);
-  int32_t* lbl = reinterpret_cast<int32_t*>(ring + 3 * (size_t)stride);
+  const SimpleShard L = shard_view(ring + 3 * (size_t)stride, c.n_keys, cap);
   const size_t N = (size_t)c.N;
   const int per = (c.N + W - 1) / W;
-  const int lo = min(c.N, w * per), hi = min(c.N, lo + per);
+  const int lo = min(c.N, w * per), hi = min(c.N, lo + per), own = hi - lo;
   if (n_pods <= 0) return;
-  // shard rows -> registers, label ids -> LDS, blobs 0 and 1 -> ring
-  NodeRow row[NPT];
+  // shard rows and label ids -> LDS, blobs 0 and 1 -> ring
+  for (int s = tid; s < own; s += nt) {
+    const int n = lo + s;
 #pragma unroll
-  for (int j = 0; j < NPT; j++) {
-    const int n = lo + j * nt + tid;
-    row[j] = n < hi ? row_from_hbm(c, n) : NodeRow{};
+    for (int k = 0; k < 3; k++) {
+      L.r64[k * cap + s] = c.alloc[k * N + n];
+      L.r64[(3 + k) * cap + s] = c.requested[k * N + n];
+    }
+    L.r64[6 * cap + s] = c.nonzero[n];
+    L.r64[7 * cap + s] = c.nonzero[N + n];
+    L.rt[s] = c.taint_hard[n];
+    L.rt[cap + s] = c.taint_soft[n];
+    L.r32[s] = c.pod_count[n];
+    L.r32[cap + s] = c.allowed_pods[n];
+    L.r32[2 * cap + s] = (int32_t)c.node_flags[n];
   }
   for (int i = tid; i < c.n_keys * cap; i += nt) {
-    const int k = i / cap, n = lo + (i - k * cap);
-    lbl[i] = n < hi ? c.label_value[(size_t)k * N + n] : -1;
+    const int k = i / cap, s = i - k * cap;
+    L.lbl[i] = s < own ? c.label_value[(size_t)k * N + lo + s] : -1;
   }
   const int nq = stride / 16;
   for (int i = tid; i < min(n_pods, 2) * nq; i += nt)
@@ -408,12 +488,8 @@ __device__ __forceinline__ void simple_schedule(DevCluster c, const uint8_t* __r
   if (tid == 0) H.abort = 0;
   __syncthreads();
 
-  SVal cur[NPT];
-  SVal alt{KSS_F_NOT_EVALUATED, 0, 0, 0, 0};
-#pragma unroll
-  for (int j = 0; j < NPT; j++) cur[j] = alt;
   long long st[6], R[4] = {0, 0, 0, 0};
-  int parity = 0;
+  int parity = 0, sub_s = -1;  // slot whose pass-B values are the H1 ones (the previous winner)
   unsigned epoch = 0;
   // k = -1 is the prologue: pass A of pod 0 and the exchange of its statistics
   for (int k = -1; k < n_pods; k++) {
@@ -422,7 +498,7 @@ __device__ __forceinline__ void simple_schedule(DevCluster c, const uint8_t* __r
     if (sp && tid == 0) sp[0] = wall_clock64();
     const BlobView Bk = blob_view(ring + (size_t)((k + 3) % 3) * stride);
     const kss_pod& pk = *Bk.pod;
-    // blob k+2 -> registers now, -> its ring slot once pod k-1's last reader is past
+    // blob k+2 -> registers now, -> its ring slot at the end of this pod
     const bool pf_on = k >= 0 && k + 2 < n_pods;
     const uint4* pf_src = reinterpret_cast<const uint4*>(blobs + (size_t)(k + 2) * stride);
     uint4 pf[2];
@@ -438,11 +514,10 @@ __device__ __forceinline__ void simple_schedule(DevCluster c, const uint8_t* __r
     long long best = 0;
     if (k >= 0) {
       if (pk.prefilter_status == 0 && nf > 0) {
-#pragma unroll
-        for (int j = 0; j < NPT; j++) {
-          if (cur[j].f != 0) continue;  // also every slot past hi (NOT_EVALUATED)
-          const int n = lo + j * nt + tid;
-          const long long key = simple_key(prof, cur[j], scored, max_tt, max_na, (uint32_t)(c.node_base + n));
+        for (int s = tid; s < own; s += nt) {
+          const SVal e = cv_get(L, s == sub_s ? cap : s);
+          if (e.f != 0) continue;
+          const long long key = simple_key(prof, e, scored, max_tt, max_na, (uint32_t)(c.node_base + lo + s));
           best = key > best ? key : best;
         }
       }
@@ -454,11 +529,11 @@ __device__ __forceinline__ void simple_schedule(DevCluster c, const uint8_t* __r
       best = b[0];
       if (sp && tid == 0) sp[2] = wall_clock64();
     }
-    const int cand = best ? (int)(0xFFFFFFFFu - (uint32_t)(unsigned long long)best) - c.node_base : -1;
+    const int cand_s = best ? (int)(0xFFFFFFFFu - (uint32_t)(unsigned long long)best) - c.node_base - lo : -1;
     // pass A: pod k+1 before pod k's commit, and on the candidate after it
     if (k + 1 < n_pods) {
       const BlobView B1 = blob_view(ring + (size_t)((k + 1) % 3) * stride);
-      simple_pass_a<NPT>(c, prof, B1, lo, hi, row, cur, alt, cand, pk, lbl, cap, st, sp);
+      simple_pass_a(c, prof, B1, L, lo, own, cand_s, pk, st, sp);
     } else {
 #pragma unroll
       for (int i = 0; i < 6; i++) st[i] = 0;
@@ -479,16 +554,18 @@ __device__ __forceinline__ void simple_schedule(DevCluster c, const uint8_t* __r
       if (chosen) chosen[k] = m.chosen;
       if (meta) meta[k] = m;
     }
-    // AssumePod by the owner lane: its row, and its pod k+1 values become the H1 ones
+    // AssumePod on the winner's shard; pass B of pod k+1 takes that slot's H1 values
+    const bool won = x >= lo && x < hi;
+    sub_s = won ? x - lo : -1;
+    if (won && tid == 0) {
+      const int s = x - lo;
 #pragma unroll
-    for (int j = 0; j < NPT; j++) {
-      const int n = lo + j * nt + tid;
-      if (n == x && n < hi) {
-        add_commit(row[j], pk);
-        if (k + 1 < n_pods) cur[j] = alt;
-        if (pk.cls >= 0) c.class_count[(size_t)pk.cls * N + n] += 1;
-        for (int i = 0; i < pk.own_terms_len; i++) c.term_count[(size_t)Bk.ints[pk.own_terms_off + i] * N + n] += 1;
-      }
+      for (int r = 0; r < 3; r++) L.r64[(3 + r) * cap + s] += pk.commit_req[r];
+      L.r64[6 * cap + s] += pk.commit_nz[0];
+      L.r64[7 * cap + s] += pk.commit_nz[1];
+      L.r32[s] += 1;
+      if (pk.cls >= 0) c.class_count[(size_t)pk.cls * N + x] += 1;
+      for (int i = 0; i < pk.own_terms_len; i++) c.term_count[(size_t)Bk.ints[pk.own_terms_off + i] * N + x] += 1;
     }
     if (pf_on) {
       uint4* dst = reinterpret_cast<uint4*>(ring + (size_t)((k + 2) % 3) * stride);
@@ -501,15 +578,14 @@ __device__ __forceinline__ void simple_schedule(DevCluster c, const uint8_t* __r
     if (sp && tid == 0) sp[6] = wall_clock64();
   }
   // node state back to HBM
+  __syncthreads();
+  for (int s = tid; s < own; s += nt) {
+    const int n = lo + s;
 #pragma unroll
-  for (int j = 0; j < NPT; j++) {
-    const int n = lo + j * nt + tid;
-    if (n >= hi) continue;
-#pragma unroll
-    for (int r = 0; r < 3; r++) c.requested[(size_t)r * N + n] = row[j].req[r];
-    c.nonzero[n] = row[j].nz[0];
-    c.nonzero[N + n] = row[j].nz[1];
-    c.pod_count[n] = row[j].pods;
+    for (int r = 0; r < 3; r++) c.requested[(size_t)r * N + n] = L.r64[(3 + r) * cap + s];
+    c.nonzero[n] = L.r64[6 * cap + s];
+    c.nonzero[N + n] = L.r64[7 * cap + s];
+    c.pod_count[n] = L.r32[s];
   }
 }
 

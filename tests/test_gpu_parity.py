@@ -95,8 +95,8 @@ def test_compact_kernel_matches_oracle(config, n_nodes, n_pods, mode):
     """k_simple (register-resident rows, one speculative exchange per pod): chosen node,
     per-pod outcome (feasible count, scored, status, best total) and the final node state
     equal the oracle's."""
-    if mode == "single" and n_nodes > 2048:
-        pytest.skip("more nodes than one workgroup's register rows hold (4 x 512)")
+    if mode == "single" and n_nodes > 1024:
+        pytest.skip("more nodes than one workgroup's LDS shard image holds")
     prof = abi.default_profile()
     s = native.Synth(config, 0, n_nodes, n_pods)
     chosen_o, res, st = oracle_c.schedule(prof, s.cluster, s.pods, n_pods, n_nodes, record=True, threads=8,
