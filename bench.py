@@ -14,9 +14,14 @@ collective, "weak" scaling.  Control-plane barrier/max uses gloo.
 Prints ONE JSON line on rank 0.
 """
 import argparse
+import csv
+import glob
 import json
 import os
+import shutil
+import subprocess
 import sys
+import tempfile
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -60,6 +65,34 @@ def cpu_baseline(config, n_nodes, n_pods, seconds, threads):
             "pods_per_s": reps * n / t_used}
 
 
+def measure_traffic(args, cfg):
+    """HBM bytes per launch of the scheduling kernel from rocprofv3 PMC counters: one child
+    process per counter (FETCH_SIZE, WRITE_SIZE), started before this process touches the
+    GPU.  FETCH_SIZE is doubled (gfx950 tallies 128-B requests at 64 B,
+    MI355X_MICROARCH.md "HBM").  Returns (bytes, detail) or (None, reason)."""
+    if not shutil.which("rocprofv3"):
+        return None, "rocprofv3 not found"
+    kb = {}
+    for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
+        d = tempfile.mkdtemp(prefix="kss_pmc_")
+        cmd = ["timeout", "-s", "KILL", "120", "rocprofv3", "--pmc", ctr, "--output-format", "csv", "-d", d, "-o", "p",
+               "--", sys.executable, os.path.abspath(__file__), "--inner", "--steps", "1", "--warmup", "0",
+               "--config", str(cfg), "--nodes", str(args.nodes), "--pods", str(args.pods)]
+        subprocess.run(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL, cwd=ROOT)
+        vals = []
+        for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+            for r in csv.DictReader(open(f)):
+                if r.get("Counter_Name") == ctr and ("k_simple" in r["Kernel_Name"] or "k_schedule" in r["Kernel_Name"]):
+                    vals.append(float(r["Counter_Value"]))
+        shutil.rmtree(d, ignore_errors=True)
+        if not vals:
+            return None, f"no {ctr} sample"
+        kb[ctr] = max(vals)
+    fetch = 2.0 * kb["FETCH_SIZE"] * 1024.0
+    write = kb["WRITE_SIZE"] * 1024.0
+    return fetch + write, {"fetch_bytes": fetch, "write_bytes": write, "fetch_size_kb_raw": kb["FETCH_SIZE"]}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -70,7 +103,11 @@ def main():
     ap.add_argument("--pods", type=int, default=0)
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-traffic", action="store_true", help="skip the rocprofv3 FETCH/WRITE_SIZE passes")
+    ap.add_argument("--inner", action="store_true", help="child run under the profiler: no CPU leg, no traffic")
     args = ap.parse_args()
+    if args.inner:
+        args.no_cpu = args.no_traffic = True
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -80,10 +117,14 @@ def main():
         import torch.distributed as dist  # control plane only (barrier / max of timings)
         dist.init_process_group("gloo", rank=rank, world_size=world)
 
+    cfg = args.config
+    traffic, traffic_detail = None, "not measured"
+    if rank == 0 and world == 1 and not args.no_traffic:
+        traffic, traffic_detail = measure_traffic(args, cfg)
+
     from kss import abi, native
     from kss.synth import DEFAULT_SIZES, SEED_BASE
 
-    cfg = args.config
     n_nodes = args.nodes or DEFAULT_SIZES[cfg][0]
     n_pods = args.pods or DEFAULT_SIZES[cfg][1]
     seed = SEED_BASE + cfg + 7919 * rank  # rank 0 = the canonical C2 cluster
@@ -155,12 +196,15 @@ def main():
             "kernel_ms_per_step": kern_avg_s * 1e3,
             "geometry": ctx.last_geometry(),
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                         "kernel": ctx.last_kernel(), "bytes_per_eval": B_EVAL[cfg]},
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "kernel": ctx.last_kernel(), "bytes_per_eval": B_EVAL[cfg],
+                         "algorithmic_bytes_per_launch": B_EVAL[cfg] * n_pods * n_nodes,
+                         "traffic_detail": traffic_detail},
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)
     ctx.close()
+    s.close()
     if dist:
         dist.destroy_process_group()
 

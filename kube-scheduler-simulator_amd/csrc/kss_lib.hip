@@ -226,7 +226,7 @@ struct kss_ctx {
   DevBuf gran_buf, err_buf;
   int n_cu = 0;
   int force_w = 0;            // KSS_SHARDS env override (tuning / tests)
-  int nodes_per_shard = 256;  // KSS_NODES_PER_SHARD
+  int nodes_per_shard = 128;  // KSS_NODES_PER_SHARD (C2 sweep: 128 > 256 > 512 nodes per shard)
   int pref_threads = 256;     // KSS_THREADS
   PlanNeeds staged_need;
   int last_geom[3] = {0, 0, 0};
@@ -760,6 +760,26 @@ static bool pick_geometry(int maxN, int W, int pref_threads, Geometry& g) {
   return npt <= KSS_MAX_NPT;
 }
 
+// Launch of a sharded (W > 1) grid whose workgroups must all be resident at once: the
+// host checks the occupancy (one workgroup per CU at this LDS / register footprint, and
+// no more workgroups than CUs) and launches plainly.  KSS_COOP_LAUNCH=1 uses the
+// cooperative launch instead (same residency, runtime-checked).
+static int launch_resident(const void* fn, dim3 grid, dim3 block, void** args, size_t shmem, hipStream_t st) {
+  static const bool coop = getenv("KSS_COOP_LAUNCH") != nullptr;
+  if (coop) {
+    if (int rc = launch_resident(fn, grid, block, args, shmem, st)) return rc;
+    return 0;
+  }
+  int dev = 0, n_cu = 0, per_cu = 0;
+  HIP_TRY(hipGetDevice(&dev));
+  HIP_TRY(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev));
+  HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, (int)(block.x * block.y * block.z), shmem));
+  if (per_cu < 1 || (long long)grid.x > (long long)per_cu * n_cu)
+    return fail(KSS_E_UNSUPPORTED, "sharded grid cannot be co-resident on this device");
+  HIP_TRY(hipLaunchKernel(fn, grid, block, args, shmem, st));
+  return 0;
+}
+
 // Launch k_schedule over n_jobs clusters (jobs already in device memory).  W > 1 needs
 // every workgroup resident: cooperative launch (the runtime checks the grid fits).
 static int launch_schedule(hipStream_t st, const Geometry& g, int n_jobs, int bins_cap, bool need_general, int n_keys,
@@ -822,7 +842,9 @@ static int launch_simple(hipStream_t st, const Geometry& g, int n_jobs, int stri
   kss_profile pr = prof;
   int W = g.W;
   void* args[] = {(void*)&jobs, (void*)&pr, (void*)&W, (void*)&cap, (void*)&gran, (void*)&err, (void*)&stamps};
-  if (g.W > 1) HIP_TRY(hipLaunchCooperativeKernel(fn, grid, block, args, (unsigned)shmem, st));
+  if (g.W > 1) {
+    if (int rc = launch_resident(fn, grid, block, args, shmem, st)) return rc;
+  }
   else HIP_TRY(hipLaunchKernel(fn, grid, block, args, shmem, st));
   return 0;
 }
