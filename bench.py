@@ -65,6 +65,25 @@ def cpu_baseline(config, n_nodes, n_pods, seconds, threads):
             "pods_per_s": reps * n / t_used}
 
 
+def rank_seed(seed_base, cfg, rank):
+    """Scenario sharding: rank r schedules its own independent cluster; rank 0 is the
+    canonical BASELINE cluster of config cfg."""
+    return seed_base + cfg + 7919 * rank
+
+
+def reduce_over_ranks(elapsed, scheduled, dist):
+    """Whole-job timing and work: the slowest rank's elapsed time (MAX) and the pods
+    scheduled by all ranks (SUM), over the control-plane (gloo) group."""
+    if dist is None:
+        return elapsed, scheduled
+    import torch
+    t = torch.tensor([elapsed], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    sc = torch.tensor([scheduled], dtype=torch.float64)
+    dist.all_reduce(sc, op=dist.ReduceOp.SUM)
+    return float(t.item()), int(sc.item())
+
+
 def measure_traffic(args, cfg):
     """HBM bytes per launch of the scheduling kernel from rocprofv3 PMC counters: one child
     process per counter (FETCH_SIZE, WRITE_SIZE), started before this process touches the
@@ -127,7 +146,7 @@ def main():
 
     n_nodes = args.nodes or DEFAULT_SIZES[cfg][0]
     n_pods = args.pods or DEFAULT_SIZES[cfg][1]
-    seed = SEED_BASE + cfg + 7919 * rank  # rank 0 = the canonical C2 cluster
+    seed = rank_seed(SEED_BASE, cfg, rank)
     s = native.Synth(cfg, seed, n_nodes, n_pods)
     prof = abi.default_profile()
     ctx = native.Context(prof, device=local)
@@ -154,16 +173,7 @@ def main():
         dist.barrier()
     elapsed = t1 - t0
     scheduled = int((chosen >= 0).sum())
-    if dist:
-        import torch
-        t = torch.tensor([elapsed], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        sc = torch.tensor([scheduled], dtype=torch.float64)
-        dist.all_reduce(sc, op=dist.ReduceOp.SUM)
-        scheduled_total = int(sc.item())
-    else:
-        scheduled_total = scheduled
+    elapsed, scheduled_total = reduce_over_ranks(elapsed, scheduled, dist)
 
     evals = world * n_pods * n_nodes * args.steps
     value = evals / elapsed
