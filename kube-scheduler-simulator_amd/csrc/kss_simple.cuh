@@ -24,7 +24,7 @@ namespace kss {
 
 constexpr int BLOB_MAX = 4096;  // bytes per serialized pod program (host-checked)
 constexpr int SX_VALS = 8;      // granules per shard per exchange: key lo/hi, H0 (nf, tt, na), H1 (nf, tt, na)
-constexpr int SX_CHUNKS = 1;    // shards swept 64 at a time: W <= 64
+constexpr int SX_CHUNKS = 2;    // shards swept 64 at a time: W <= 128
 
 // The v1.26 default profile (kss_default_profile, kss_host.cpp; plugins_test.go:184-204,
 // 878-1096) as a compile-time constant: k_simple<true> folds every weight and resource
@@ -121,6 +121,33 @@ __device__ __forceinline__ long long wave_red(long long v) {
   const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)u, 63);
   const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), 63);
   return (long long)(((unsigned long long)hi << 32) | lo);
+}
+
+// Six non-negative 32-bit statistics {nf0, tt0, na0, nf1, tt1, na1} reduced together
+// (SUM, MAX, MAX, SUM, MAX, MAX): each DPP step issues all six moves before combining,
+// so the six chains overlap instead of paying the DPP latency six times.
+template <int CTRL, int ROWS>
+__device__ __forceinline__ void dpp_stats_step(uint32_t (&v)[6]) {
+  uint32_t t[6];
+#pragma unroll
+  for (int i = 0; i < 6; i++) t[i] = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v[i], CTRL, ROWS, 0xF, false);
+  v[0] += t[0];
+  v[1] = max(v[1], t[1]);
+  v[2] = max(v[2], t[2]);
+  v[3] += t[3];
+  v[4] = max(v[4], t[4]);
+  v[5] = max(v[5], t[5]);
+}
+
+__device__ __forceinline__ void wave_red_stats(uint32_t (&v)[6]) {
+  dpp_stats_step<0xB1, 0xF>(v);
+  dpp_stats_step<0x4E, 0xF>(v);
+  dpp_stats_step<0x141, 0xF>(v);
+  dpp_stats_step<0x140, 0xF>(v);
+  dpp_stats_step<0x142, 0xA>(v);
+  dpp_stats_step<0x143, 0xC>(v);
+#pragma unroll
+  for (int i = 0; i < 6; i++) v[i] = (uint32_t)__builtin_amdgcn_readlane((int)v[i], 63);
 }
 
 // LDS image of the loop head: reduction scratch (double-buffered), exchange results.
@@ -242,8 +269,26 @@ __device__ __forceinline__ bool simple_exchange(SimpleHdr& H, unsigned long long
 __device__ __forceinline__ bool simple_sync(SimpleHdr& H, int& parity, long long key, long long (&st)[6], int W, int w,
                                             unsigned epoch, unsigned long long* gran, int* err, int per, int node_base,
                                             long long (&R)[4], unsigned long long* sp) {
-  const int ops[6] = {OP_SUM, OP_MAX, OP_MAX, OP_SUM, OP_MAX, OP_MAX};
-  block_red(H, parity, st, ops);
+  {
+    uint32_t u[6];
+#pragma unroll
+    for (int i = 0; i < 6; i++) u[i] = (uint32_t)st[i];
+    wave_red_stats(u);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    if (lane == 0) {
+#pragma unroll
+      for (int i = 0; i < 6; i++) H.red[parity][wave][i] = u[i];
+    }
+    lds_barrier();
+#pragma unroll
+    for (int i = 0; i < 6; i++) st[i] = H.red[parity][0][i];
+    for (int wv = 1; wv < nw; wv++) {
+      st[0] += H.red[parity][wv][0];
+      st[3] += H.red[parity][wv][3];
+#pragma unroll
+      for (int i : {1, 2, 4, 5}) st[i] = max(st[i], H.red[parity][wv][i]);
+    }
+  }
   parity ^= 1;
   if (sp && threadIdx.x == 0) sp[4] = wall_clock64();
   if (W == 1) {  // the winner (if any) is this shard's candidate
@@ -564,8 +609,9 @@ __device__ __forceinline__ void simple_schedule(DevCluster c, const uint8_t* __r
       L.r64[6 * cap + s] += pk.commit_nz[0];
       L.r64[7 * cap + s] += pk.commit_nz[1];
       L.r32[s] += 1;
-      if (pk.cls >= 0) c.class_count[(size_t)pk.cls * N + x] += 1;
-      for (int i = 0; i < pk.own_terms_len; i++) c.term_count[(size_t)Bk.ints[pk.own_terms_off + i] * N + x] += 1;
+      // HBM-only columns: no-return atomics, so the commit never waits on a load
+      if (pk.cls >= 0) atomicAdd(&c.class_count[(size_t)pk.cls * N + x], 1);
+      for (int i = 0; i < pk.own_terms_len; i++) atomicAdd(&c.term_count[(size_t)Bk.ints[pk.own_terms_off + i] * N + x], 1);
     }
     if (pf_on) {
       uint4* dst = reinterpret_cast<uint4*>(ring + (size_t)((k + 2) % 3) * stride);
