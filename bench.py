@@ -112,6 +112,97 @@ def measure_traffic(args, cfg):
     return fetch + write, {"fetch_bytes": fetch, "write_bytes": write, "fetch_size_kb_raw": kb["FETCH_SIZE"]}
 
 
+def run_node_axis(args):
+    """Node-axis bench line (SURVEY 8(e), C4 shape): the SAME cluster on every rank, rows
+    split into contiguous blocks, two collectives per pod (all_gather of 32 B statistics,
+    all_reduce MAX of the 8 B packed key) over RCCL when world > 1.  Pods use the default
+    profile recipe (config 2): zone PodTopologySpread is not yet on the node axis.
+    `value` = pod x node evals of the whole cluster / max-over-ranks step time (strong
+    scaling: the total work is fixed as ranks are added)."""
+    import torch
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local))
+    from kss import abi, native, nodeaxis
+    from kss.synth import SEED_BASE
+    n_nodes = args.nodes or 100000
+    n_pods = args.pods or 20000
+    s = native.Synth(2, SEED_BASE + 4, n_nodes, n_pods)
+    sch = nodeaxis.NodeAxisScheduler(s.cluster, s.pods, abi.default_profile(), device=local)
+
+    def step():
+        sch.reset()
+        out = sch.schedule()
+        torch.cuda.synchronize()
+        return out
+
+    for _ in range(args.warmup):
+        step()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        chosen = step()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if dist:
+        dist.barrier()
+    scheduled = int((chosen >= 0).sum().item())
+    if dist:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    # live roofline of the dominant kernel (k_axis_eval): 200 launches on the scheduler's stream
+    k = min(200, n_pods)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    with torch.cuda.stream(sch.stream):
+        e0.record(sch.stream)
+        for i in range(k):
+            sch.ctx.axis_eval(i, sch.stats.data_ptr(), sch.stream.cuda_stream)
+        e1.record(sch.stream)
+    e1.synchronize()
+    eval_s = e0.elapsed_time(e1) / 1e3 / k
+    rows = sch.hi - sch.lo
+    achieved = B_EVAL[2] * rows / eval_s / 1e9
+    if rank == 0:
+        out = {
+            "metric": "pod x node filter+score evals/sec (pods scheduled/sec in extra)",
+            "value": n_pods * n_nodes * args.steps / elapsed,
+            "unit": "evals/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "int64/f64",
+            "data": "synthetic (SplitMix64 seed 0x5EED0004, config-2 pod recipe)",
+            "config": {"workload": f"C4 shape: {n_nodes} nodes x {n_pods} pods, default profile, node-axis sharded, "
+                                   f"pct=100", "nodes": n_nodes, "pods": n_pods, "parallelism": f"node-axis x{world}"},
+            "pods_per_s": scheduled * args.steps / elapsed,
+            "us_per_pod": elapsed / args.steps / n_pods * 1e6,
+            "pods_scheduled_per_step": scheduled,
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": None, "kernel": "k_axis_eval",
+                         "bytes_per_eval": B_EVAL[2], "algorithmic_bytes_per_launch": B_EVAL[2] * rows,
+                         "kernel_us": eval_s * 1e6,
+                         "note": "per pod the path is latency-bound: 3 launches + 2 collectives"},
+            "cpu_baseline": None,
+        }
+        print(json.dumps(out), flush=True)
+    sch.close()
+    s.close()
+    if dist:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -124,9 +215,13 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-traffic", action="store_true", help="skip the rocprofv3 FETCH/WRITE_SIZE passes")
     ap.add_argument("--inner", action="store_true", help="child run under the profiler: no CPU leg, no traffic")
+    ap.add_argument("--node-axis", action="store_true",
+                    help="C4 shape: one cluster sharded along the node axis over the ranks (RCCL per pod)")
     args = ap.parse_args()
     if args.inner:
         args.no_cpu = args.no_traffic = True
+    if args.node_axis:
+        return run_node_axis(args)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))

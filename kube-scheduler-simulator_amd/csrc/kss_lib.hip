@@ -24,6 +24,7 @@
 #include "kss_host.h"
 #include "kss_sched.cuh"
 #include "kss_simple.cuh"
+#include "kss_axis.cuh"
 
 using namespace kss;
 
@@ -240,6 +241,8 @@ struct kss_ctx {
   int last_kernel = 0;     // 0 k_schedule, 1 k_simple
   int meta_n = 0;          // pods with an outcome in meta_host
   bool small_values = false;  // every allocatable cpu/mem/eph < 2^46: k_simple's divisions stay below 2^53
+  bool axis_meta_dirty = false;  // meta_buf holds node-axis outcomes not yet copied to meta_host
+  DevBuf axis_cv;             // node-axis sharding: [5][N] per-row verdict + raw scores of the current pod
 };
 
 namespace {
@@ -590,6 +593,7 @@ void kss_destroy(kss_ctx* ctx) {
   ctx->stamp_buf.release();
   ctx->gran_buf.release();
   ctx->err_buf.release();
+  ctx->axis_cv.release();
   if (ctx->ev0) hipEventDestroy(ctx->ev0);
   if (ctx->ev1) hipEventDestroy(ctx->ev1);
   if (ctx->stream) hipStreamDestroy(ctx->stream);
@@ -639,7 +643,112 @@ int kss_load_cluster(kss_ctx* ctx, const kss_cluster* cl) {
   ctx->loaded = true;
   ctx->recorded = 0;
   ctx->meta_n = 0;
+  ctx->axis_meta_dirty = false;
   ctx->staged_n = -1;
+  return 0;
+}
+
+int kss_load_cluster_rows(kss_ctx* ctx, const kss_cluster* cl, int32_t lo, int32_t hi) {
+  if (!ctx) return fail(KSS_E_INVAL, "null ctx");
+  int rc = check_cluster(cl);
+  if (rc) return rc;
+  if (lo < 0 || hi < lo || hi > cl->n_nodes) return fail(KSS_E_INVAL, "row range out of range");
+  const size_t N = (size_t)cl->n_nodes, M = (size_t)(hi - lo);
+  // column-blocked [attr][N] matrices: take columns [lo, hi) of every attribute row
+  auto rows64 = [&](const int64_t* src, int nrow, std::vector<int64_t>& dst) {
+    dst.resize(std::max<size_t>(nrow * M, 1));
+    for (int r = 0; r < nrow; r++) std::copy(src + r * N + lo, src + r * N + hi, dst.begin() + r * M);
+  };
+  auto rows32 = [&](const int32_t* src, int nrow, std::vector<int32_t>& dst) {
+    dst.resize(std::max<size_t>(nrow * M, 1));
+    if (src)
+      for (int r = 0; r < nrow; r++) std::copy(src + r * N + lo, src + r * N + hi, dst.begin() + r * M);
+  };
+  std::vector<int64_t> alloc, req, nz;
+  std::vector<int32_t> allowed, podc, lv, cc, tc;
+  rows64(cl->alloc, KSS_NRES, alloc);
+  rows64(cl->requested, KSS_NRES, req);
+  rows64(cl->nonzero, 2, nz);
+  rows32(cl->allowed_pods, 1, allowed);
+  rows32(cl->pod_count, 1, podc);
+  rows32(cl->label_value, cl->n_label_keys, lv);
+  rows32(cl->class_count, cl->n_classes, cc);
+  rows32(cl->term_count, cl->n_terms, tc);
+  std::vector<uint32_t> flags(cl->node_flags + lo, cl->node_flags + hi);
+  std::vector<uint64_t> th(cl->taint_hard + lo, cl->taint_hard + hi), ts(cl->taint_soft + lo, cl->taint_soft + hi);
+  std::vector<uint8_t> to(cl->taint_order + (size_t)lo * KSS_TAINT_ORDER, cl->taint_order + (size_t)hi * KSS_TAINT_ORDER);
+  kss_cluster s = *cl;
+  s.n_nodes = (int32_t)M;
+  s.node_base = cl->node_base + lo;
+  s.alloc = alloc.data();
+  s.requested = req.data();
+  s.nonzero = nz.data();
+  s.allowed_pods = allowed.data();
+  s.pod_count = podc.data();
+  s.node_flags = flags.data();
+  s.taint_hard = th.data();
+  s.taint_soft = ts.data();
+  s.taint_order = to.data();
+  s.label_value = lv.data();
+  s.class_count = cl->class_count ? cc.data() : nullptr;
+  s.term_count = cl->term_count ? tc.data() : nullptr;
+  return kss_load_cluster(ctx, &s);  // synchronous: the temporaries outlive the upload
+}
+
+static hipStream_t axis_stream(kss_ctx* ctx, void* stream) { return stream ? (hipStream_t)stream : ctx->stream; }
+
+static int axis_check(kss_ctx* ctx, int32_t pod_index) {
+  if (!ctx || !ctx->loaded) return fail(KSS_E_INVAL, "no cluster loaded");
+  if (pod_index < 0 || pod_index >= ctx->staged_n) return fail(KSS_E_INVAL, "pod index outside the staged pods");
+  if (ctx->staged_need.general)
+    return fail(KSS_E_UNSUPPORTED, "node-axis path: spread / inter-pod programs need the replicated domain histograms");
+  return ctx->axis_cv.ensure(sizeof(int32_t) * 5 * (size_t)std::max(ctx->dc.N, 1));
+}
+
+static dim3 axis_grid(kss_ctx* ctx) {
+  const int blocks = (ctx->dc.N + AXIS_THREADS - 1) / AXIS_THREADS;
+  return dim3((unsigned)std::max(1, std::min(blocks, 4 * ctx->n_cu)));
+}
+
+int kss_axis_eval(kss_ctx* ctx, int32_t pod_index, int64_t* stats_dev, void* stream) {
+  int rc = axis_check(ctx, pod_index);
+  if (rc) return rc;
+  if (!stats_dev) return fail(KSS_E_INVAL, "null stats buffer");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  HIP_TRY(hipSetDevice(ctx->cfg.device));
+  hipLaunchKernelGGL(k_axis_eval, axis_grid(ctx), dim3(AXIS_THREADS), 0, axis_stream(ctx, stream), ctx->dc, ctx->dp,
+                     ctx->prof, pod_index, (int32_t*)ctx->axis_cv.p, (long long*)stats_dev);
+  HIP_TRY(hipGetLastError());
+  return 0;
+}
+
+int kss_axis_select(kss_ctx* ctx, const int64_t* gathered_dev, int32_t world, int64_t* key_dev, void* stream) {
+  int rc = axis_check(ctx, 0);
+  if (rc) return rc;
+  if (!gathered_dev || !key_dev || world < 1) return fail(KSS_E_INVAL, "bad select arguments");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  HIP_TRY(hipSetDevice(ctx->cfg.device));
+  hipLaunchKernelGGL(k_axis_select, axis_grid(ctx), dim3(AXIS_THREADS), 0, axis_stream(ctx, stream), ctx->dc, ctx->prof,
+                     (const int32_t*)ctx->axis_cv.p, (const long long*)gathered_dev, world, (long long*)key_dev);
+  HIP_TRY(hipGetLastError());
+  return 0;
+}
+
+int kss_axis_commit(kss_ctx* ctx, int32_t pod_index, int64_t* key_dev, const int64_t* gathered_dev, int32_t world,
+                    int64_t* stats_dev, int32_t* chosen_dev, void* stream) {
+  int rc = axis_check(ctx, pod_index);
+  if (rc) return rc;
+  if (!key_dev || !gathered_dev || !stats_dev || world < 1) return fail(KSS_E_INVAL, "bad commit arguments");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  HIP_TRY(hipSetDevice(ctx->cfg.device));
+  rc = ctx->meta_buf.ensure(sizeof(PodMeta) * (size_t)std::max(ctx->staged_n, 1));
+  if (rc) return rc;
+  hipLaunchKernelGGL(k_axis_commit, dim3(1), dim3(64), 0, axis_stream(ctx, stream), ctx->dc, ctx->dp, pod_index,
+                     (long long*)key_dev, (const long long*)gathered_dev, world, (long long*)stats_dev, chosen_dev,
+                     (PodMeta*)ctx->meta_buf.p);
+  HIP_TRY(hipGetLastError());
+  ctx->meta_n = std::max(ctx->meta_n, pod_index + 1);
+  ctx->axis_meta_dirty = true;
   return 0;
 }
 
@@ -943,6 +1052,7 @@ static int run_single(kss_ctx* ctx, const PlanNeeds& need, const DevPods& dp, in
   if (chosen_out && n) HIP_TRY(hipMemcpy(chosen_out, ctx->chosen_buf.p, sizeof(int32_t) * n, hipMemcpyDeviceToHost));
   ctx->recorded = record ? n : (n > 0 && !simple ? 1 : 0);
   ctx->meta_n = n;
+  ctx->axis_meta_dirty = false;
   if (stamps) {
     std::vector<unsigned long long> h(8 * KSS_NSTAMP_PODS);
     HIP_TRY(hipMemcpy(h.data(), stamps, stamp_bytes, hipMemcpyDeviceToHost));
@@ -1115,6 +1225,13 @@ int kss_last_kernel(kss_ctx* ctx) {
 int kss_fetch_meta(kss_ctx* ctx, int32_t first, int32_t n, int64_t* out) {
   if (!ctx || (n > 0 && !out)) return fail(KSS_E_INVAL, "bad arguments");
   if (first < 0 || n < 0 || first + n > ctx->meta_n) return fail(KSS_E_NOTFOUND, "pod outcome not available");
+  if (ctx->axis_meta_dirty) {  // node-axis outcomes were written on the caller's stream
+    HIP_TRY(hipSetDevice(ctx->cfg.device));
+    HIP_TRY(hipDeviceSynchronize());
+    ctx->meta_host.resize((size_t)ctx->meta_n);
+    HIP_TRY(hipMemcpy(ctx->meta_host.data(), ctx->meta_buf.p, sizeof(PodMeta) * (size_t)ctx->meta_n, hipMemcpyDeviceToHost));
+    ctx->axis_meta_dirty = false;
+  }
   for (int i = 0; i < n; i++) {
     const PodMeta& m = ctx->meta_host[first + i];
     int64_t* o = out + 5 * (size_t)i;
