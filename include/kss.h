@@ -366,27 +366,33 @@ int kss_schedule_scenarios(int32_t device, const kss_profile* prof, int32_t n_sc
 
 /* ---- node-axis sharding ----------------------------
  * One context per GPU holds rows [lo, hi) of the cluster (node_base = lo); the pods are
- * staged on every rank (kss_stage_pods).  One pod is three launches on `stream` (a
+ * staged on every rank (kss_stage_pods).  One pod is two launches on `stream` (a
  * hipStream_t, NULL = the context's stream), never synchronising with the host; the
- * caller runs two collectives between them on the same stream:
- *   kss_axis_eval    filter + raw scores of the local rows; folds {feasible count,
- *                    max TaintToleration raw, max NodeAffinity raw, 0} into stats_dev[4]
- *   (all_gather stats_dev -> gathered_dev[world][4])
- *   kss_axis_select  NormalizeScore with the global statistics, weighted total, local
- *                    selectHost key (total << 32 | 0xFFFFFFFF - global index) max-folded
- *                    into key_dev[0]
- *   (all_reduce key_dev MAX)
- *   kss_axis_commit  owner rank applies AssumePod; chosen_dev[pod_index] = global node or
- *                    -1; stats_dev and key_dev are cleared for the next pod.
- * stats_dev / key_dev must be zero before the first pod.  Outcomes are also kept for
- * kss_fetch_meta.  Replaces, per rank, the findNodesThatPassFilters / prioritizeNodes /
- * selectHost / AssumePod sequence of scheduleOne over
- * that rank's rows; pods with spread / inter-pod programs return KSS_E_UNSUPPORTED. */
+ * caller runs two collectives between them on the same stream.  With b = i & 1:
+ *   kss_axis_eval(i)    applies the pending AssumePod of pod i-1 (prev_key_dev = key[1-b],
+ *                       prev_gathered_dev = its gathered statistics; NULL for i = 0),
+ *                       clears key_zero_dev = key[b], then filter + raw scores of the local
+ *                       rows, folding {feasible count, max TaintToleration raw, max
+ *                       NodeAffinity raw, 0} into stats_dev = stats[b]
+ *   (all_gather stats[b] -> gathered_dev[world][4]; world 1: gathered = stats[b])
+ *   kss_axis_select     NormalizeScore with the global statistics, weighted total, local
+ *                       selectHost key (total << 32 | 0xFFFFFFFF - global index) max-folded
+ *                       into key_dev = key[b]; clears stats_zero_dev = stats[1-b]
+ *   (all_reduce key[b] MAX)
+ *   kss_axis_commit     after the last pod only: its pending AssumePod.
+ * chosen_dev[i] = global node or -1.  stats[0] must be zero before pod 0.  Outcomes are
+ * also kept for kss_fetch_meta.  Replaces, per rank, the findNodesThatPassFilters /
+ * prioritizeNodes / selectHost / AssumePod sequence of scheduleOne (SURVEY 8(a) a1, a15,
+ * a17, a18) over that rank's rows; pods with spread / inter-pod programs return
+ * KSS_E_UNSUPPORTED. */
 int kss_load_cluster_rows(kss_ctx* ctx, const kss_cluster* cl, int32_t lo, int32_t hi);
-int kss_axis_eval(kss_ctx* ctx, int32_t pod_index, int64_t* stats_dev, void* stream);
-int kss_axis_select(kss_ctx* ctx, const int64_t* gathered_dev, int32_t world, int64_t* key_dev, void* stream);
-int kss_axis_commit(kss_ctx* ctx, int32_t pod_index, int64_t* key_dev, const int64_t* gathered_dev, int32_t world,
-                    int64_t* stats_dev, int32_t* chosen_dev, void* stream);
+int kss_axis_eval(kss_ctx* ctx, int32_t pod_index, int64_t* stats_dev, const int64_t* prev_key_dev,
+                  const int64_t* prev_gathered_dev, int32_t world, int64_t* key_zero_dev, int32_t* chosen_dev,
+                  void* stream);
+int kss_axis_select(kss_ctx* ctx, const int64_t* gathered_dev, int32_t world, int64_t* key_dev, int64_t* stats_zero_dev,
+                    void* stream);
+int kss_axis_commit(kss_ctx* ctx, int32_t pod_index, const int64_t* key_dev, const int64_t* gathered_dev, int32_t world,
+                    int32_t* chosen_dev, void* stream);
 
 /* timing of the last kss_schedule_batch / kss_eval_pod device work (HIP events on the work stream) */
 int kss_last_timing(kss_ctx* ctx, double* device_ms, int32_t* launches);

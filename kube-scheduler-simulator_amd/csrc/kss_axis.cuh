@@ -5,16 +5,21 @@
 // two small collectives between them that the host issues on the same stream (RCCL
 // over xGMI, no host synchronisation):
 //
-//   k_axis_eval    filter chain + the four raw scores of every local row (HBM-streamed,
-//                  one lane per row); folds {feasible count, max TT raw, max NA raw} of
-//                  the local rows into stats[0..3) with device atomics.
+//   k_axis_eval    first the pending AssumePod of the previous pod (the lane owning the
+//                  winner row applies it, then reads the row), then the filter chain + the
+//                  four raw scores of every local row (HBM-streamed, one lane per row);
+//                  folds {feasible count, max TT raw, max NA raw} of the local rows into
+//                  stats[0..3) with device atomics.
 //   -- all_gather(stats) -> gathered[world][4]
 //   k_axis_select  global statistics (Σ feasible, max, max) from gathered, NormalizeScore
 //                  + weights + the packed selectHost key (total << 32 | ~global index) of
 //                  every local feasible row; the rank's best key is max-folded into key[0].
 //   -- all_reduce(key, MAX)
-//   k_axis_commit  the owning rank applies AssumePod (commit_pod) to the winner row; every
-//                  rank writes chosen[pod] and clears stats / key for the next pod.
+//   k_axis_commit  only after the last pod of a batch: its pending AssumePod.
+//
+// Two launches per pod.  The fold buffers are double-buffered by pod parity: eval(i)
+// clears key[i & 1] (select(i) folds into it) and select(i) clears stats[(i + 1) & 1]
+// (eval(i + 1) folds into it), so no launch clears a buffer another reads.
 //
 // The per-row arithmetic is the one k_schedule / k_simple use (kss_eval.cuh, references
 // there: fit.go fitsRequest, resource_allocation.go, balanced_allocation.go,
@@ -27,6 +32,7 @@
 
 #include "kss_eval.cuh"
 #include "kss_sched.cuh"
+#include "kss_simple.cuh"
 
 namespace kss {
 
@@ -55,6 +61,15 @@ __device__ __forceinline__ long long axis_key(const kss_profile& prof, const int
   return (long long)(((unsigned long long)(uint32_t)total << 32) | (0xFFFFFFFFull - g));
 }
 
+// Copy a small record into LDS with all lanes (4-byte words); the caller synchronises.
+template <class T>
+__device__ __forceinline__ void axis_stage(T* dst, const T* src) {
+  static_assert(sizeof(T) % 4 == 0, "record not word-sized");
+  const uint32_t* s = reinterpret_cast<const uint32_t*>(src);
+  uint32_t* d = reinterpret_cast<uint32_t*>(dst);
+  for (int i = threadIdx.x; i < (int)(sizeof(T) / 4); i += blockDim.x) d[i] = s[i];
+}
+
 template <int OP>  // 0 sum, 1 max
 __device__ __forceinline__ long long axis_block_reduce(long long v, long long* red) {
 #pragma unroll
@@ -72,10 +87,65 @@ __device__ __forceinline__ long long axis_block_reduce(long long v, long long* r
   return v;  // valid in thread 0
 }
 
-__global__ __launch_bounds__(AXIS_THREADS) void k_axis_eval(DevCluster c, DevPods P, kss_profile prof, int pi,
-                                                            int32_t* __restrict__ cv, long long* __restrict__ stats) {
+__device__ __forceinline__ int axis_winner(long long K) {
+  return K ? (int)(0xFFFFFFFFu - (uint32_t)(unsigned long long)K) : -1;
+}
+
+__device__ __forceinline__ void axis_global(const long long* gathered, int world, long long& nf, long long& tt,
+                                            long long& na) {
+  nf = 0;
+  tt = 0;
+  na = 0;
+  for (int r = 0; r < world; r++) {
+    nf += gathered[r * AXIS_STATS];
+    tt = gathered[r * AXIS_STATS + 1] > tt ? gathered[r * AXIS_STATS + 1] : tt;
+    na = gathered[r * AXIS_STATS + 2] > na ? gathered[r * AXIS_STATS + 2] : na;
+  }
+}
+
+// chosen[pi] and the PodMeta of pod pi from its reduced key and gathered statistics.
+__device__ __forceinline__ void axis_record(const DevPods& P, int pi, long long K, const long long* gathered, int world,
+                                            int32_t* chosen, PodMeta* meta) {
+  long long nf, tt, na;
+  axis_global(gathered, world, nf, tt, na);
+  const int g = axis_winner(K);
+  if (chosen) chosen[pi] = g;
+  if (meta) {
+    const kss_pod& p = P.pods[pi];
+    PodMeta m;
+    m.chosen = g;
+    m.n_feasible = (int32_t)nf;
+    m.scored = (K && nf > 1) ? 1 : 0;
+    m.status = p.prefilter_status != 0 ? (p.prefilter_status == 1 ? 2 : 3) : (nf == 0 ? 1 : 0);
+    m.best_total = m.scored ? (int64_t)((unsigned long long)K >> 32) : 0;
+    meta[pi] = m;
+  }
+}
+
+// The pod record is indexed with runtime resource ids: staged in LDS, not copied per lane
+// (a by-value copy lands in scratch, 392 B per lane).  DEF: the v1.26 default profile is
+// folded into the code (no scratch); otherwise the profile is staged in LDS too.
+template <bool DEF>
+__global__ __launch_bounds__(AXIS_THREADS) void k_axis_eval(DevCluster c, DevPods P, kss_profile prof_arg, int pi,
+                                                            int32_t* __restrict__ cv, long long* __restrict__ stats,
+                                                            const long long* __restrict__ prev_key,
+                                                            const long long* __restrict__ prev_gathered, int world,
+                                                            long long* __restrict__ key_zero,
+                                                            int32_t* __restrict__ chosen, PodMeta* __restrict__ meta) {
+  // pending commit of pod pi - 1 (its key was all-reduced after the previous select)
+  const int win = prev_key ? axis_winner(prev_key[0]) - c.node_base : -1;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    if (prev_key) axis_record(P, pi - 1, prev_key[0], prev_gathered, world, chosen, meta);
+    key_zero[0] = 0;  // the buffer k_axis_select folds pod pi's key into
+  }
   __shared__ long long red[AXIS_THREADS / 64];
-  const kss_pod p = P.pods[pi];
+  __shared__ kss_pod p;
+  __shared__ kss_profile prof_lds;
+  axis_stage(&p, &P.pods[pi]);
+  if (!DEF) axis_stage(&prof_lds, &prof_arg);
+  __syncthreads();
+  constexpr kss_profile prof_def = default_profile_c();
+  const kss_profile& prof = DEF ? prof_def : prof_lds;
   const size_t N = (size_t)c.N;
   long long nf = 0, tt = 0, na = 0;
   for (int n = blockIdx.x * blockDim.x + threadIdx.x; n < c.N; n += gridDim.x * blockDim.x) {
@@ -87,6 +157,7 @@ __global__ __launch_bounds__(AXIS_THREADS) void k_axis_eval(DevCluster c, DevPod
       for (int i = 0; i < p.names_len; i++) hit |= (int64_t)P.ints[p.names_off + i] == g;
       in = hit;
     }
+    if (n == win) commit_pod(c, P, P.pods[pi - 1], n, 1);  // AssumePod, then this lane reads the row
     if (in) {
       const NodeRow row = row_from_hbm(c, n);
       uint16_t detail = 0;
@@ -117,23 +188,16 @@ __global__ __launch_bounds__(AXIS_THREADS) void k_axis_eval(DevCluster c, DevPod
   }
 }
 
-__device__ __forceinline__ void axis_global(const long long* gathered, int world, long long& nf, long long& tt,
-                                            long long& na) {
-  nf = 0;
-  tt = 0;
-  na = 0;
-  for (int r = 0; r < world; r++) {
-    nf += gathered[r * AXIS_STATS];
-    tt = gathered[r * AXIS_STATS + 1] > tt ? gathered[r * AXIS_STATS + 1] : tt;
-    na = gathered[r * AXIS_STATS + 2] > na ? gathered[r * AXIS_STATS + 2] : na;
-  }
-}
-
-__global__ __launch_bounds__(AXIS_THREADS) void k_axis_select(DevCluster c, kss_profile prof,
+__global__ __launch_bounds__(AXIS_THREADS) void k_axis_select(DevCluster c, kss_profile prof_arg,
                                                               const int32_t* __restrict__ cv,
                                                               const long long* __restrict__ gathered, int world,
-                                                              long long* __restrict__ key) {
+                                                              long long* __restrict__ key,
+                                                              long long* __restrict__ stats_zero) {
+  if (blockIdx.x == 0 && threadIdx.x < AXIS_STATS) stats_zero[threadIdx.x] = 0;  // the next pod's fold buffer
   __shared__ long long red[AXIS_THREADS / 64];
+  __shared__ kss_profile prof;
+  axis_stage(&prof, &prof_arg);
+  __syncthreads();
   long long nf, tt, na;
   axis_global(gathered, world, nf, tt, na);
   const size_t N = (size_t)c.N;
@@ -147,31 +211,15 @@ __global__ __launch_bounds__(AXIS_THREADS) void k_axis_select(DevCluster c, kss_
   if (threadIdx.x == 0 && best) atomicMax(key, best);
 }
 
-// One lane: decode the global winner, commit it on the owning rank, record the outcome,
-// clear the fold buffers for the next pod.  meta (optional) receives PodMeta of the pod.
-__global__ void k_axis_commit(DevCluster c, DevPods P, int pi, long long* key, const long long* gathered, int world,
-                              long long* stats, int32_t* chosen, PodMeta* meta) {
+// One lane: the pending commit of the last pod of a batch (k_axis_eval applies every
+// other pod's commit at the start of the next pod) and its outcome.
+__global__ void k_axis_commit(DevCluster c, DevPods P, int pi, const long long* key, const long long* gathered,
+                              int world, int32_t* chosen, PodMeta* meta) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   const long long K = key[0];
-  long long nf, tt, na;
-  axis_global(gathered, world, nf, tt, na);
-  const int g = K ? (int)(0xFFFFFFFFu - (uint32_t)(unsigned long long)K) : -1;
-  const int local = g - c.node_base;
-  if (g >= 0 && local >= 0 && local < c.N) commit_pod(c, P, P.pods[pi], local, 1);
-  if (chosen) chosen[pi] = g;
-  if (meta) {
-    const kss_pod& p = P.pods[pi];
-    PodMeta m;
-    m.chosen = g;
-    m.n_feasible = (int32_t)nf;
-    m.scored = (K && nf > 1) ? 1 : 0;
-    m.status = p.prefilter_status != 0 ? (p.prefilter_status == 1 ? 2 : 3) : (nf == 0 ? 1 : 0);
-    m.best_total = m.scored ? (int64_t)((unsigned long long)K >> 32) : 0;
-    meta[pi] = m;
-  }
-  key[0] = 0;
-#pragma unroll
-  for (int i = 0; i < AXIS_STATS; i++) stats[i] = 0;
+  const int local = axis_winner(K) - c.node_base;
+  if (K && local >= 0 && local < c.N) commit_pod(c, P, P.pods[pi], local, 1);
+  axis_record(P, pi, K, gathered, world, chosen, meta);
 }
 
 }  // namespace kss

@@ -648,6 +648,8 @@ int kss_load_cluster(kss_ctx* ctx, const kss_cluster* cl) {
   return 0;
 }
 
+static bool same_profile(const kss_profile& a, const kss_profile& b);
+
 int kss_load_cluster_rows(kss_ctx* ctx, const kss_cluster* cl, int32_t lo, int32_t hi) {
   if (!ctx) return fail(KSS_E_INVAL, "null ctx");
   int rc = check_cluster(cl);
@@ -710,41 +712,55 @@ static dim3 axis_grid(kss_ctx* ctx) {
   return dim3((unsigned)std::max(1, std::min(blocks, 4 * ctx->n_cu)));
 }
 
-int kss_axis_eval(kss_ctx* ctx, int32_t pod_index, int64_t* stats_dev, void* stream) {
+int kss_axis_eval(kss_ctx* ctx, int32_t pod_index, int64_t* stats_dev, const int64_t* prev_key_dev,
+                  const int64_t* prev_gathered_dev, int32_t world, int64_t* key_zero_dev, int32_t* chosen_dev,
+                  void* stream) {
   int rc = axis_check(ctx, pod_index);
   if (rc) return rc;
-  if (!stats_dev) return fail(KSS_E_INVAL, "null stats buffer");
+  if (!stats_dev || !key_zero_dev || world < 1) return fail(KSS_E_INVAL, "bad eval arguments");
+  if (prev_key_dev && (pod_index < 1 || !prev_gathered_dev)) return fail(KSS_E_INVAL, "pending commit without a previous pod");
   std::lock_guard<std::mutex> lk(ctx->mu);
   HIP_TRY(hipSetDevice(ctx->cfg.device));
-  hipLaunchKernelGGL(k_axis_eval, axis_grid(ctx), dim3(AXIS_THREADS), 0, axis_stream(ctx, stream), ctx->dc, ctx->dp,
-                     ctx->prof, pod_index, (int32_t*)ctx->axis_cv.p, (long long*)stats_dev);
+  rc = ctx->meta_buf.ensure(sizeof(PodMeta) * (size_t)std::max(ctx->staged_n, 1));
+  if (rc) return rc;
+  auto fn = same_profile(ctx->prof, default_profile_c()) ? k_axis_eval<true> : k_axis_eval<false>;
+  hipLaunchKernelGGL(fn, axis_grid(ctx), dim3(AXIS_THREADS), 0, axis_stream(ctx, stream), ctx->dc, ctx->dp, ctx->prof,
+                     pod_index, (int32_t*)ctx->axis_cv.p, (long long*)stats_dev, (const long long*)prev_key_dev,
+                     (const long long*)prev_gathered_dev, world, (long long*)key_zero_dev, chosen_dev,
+                     (PodMeta*)ctx->meta_buf.p);
   HIP_TRY(hipGetLastError());
+  if (prev_key_dev) {
+    ctx->meta_n = std::max(ctx->meta_n, (int)pod_index);
+    ctx->axis_meta_dirty = true;
+  }
   return 0;
 }
 
-int kss_axis_select(kss_ctx* ctx, const int64_t* gathered_dev, int32_t world, int64_t* key_dev, void* stream) {
+int kss_axis_select(kss_ctx* ctx, const int64_t* gathered_dev, int32_t world, int64_t* key_dev, int64_t* stats_zero_dev,
+                    void* stream) {
   int rc = axis_check(ctx, 0);
   if (rc) return rc;
-  if (!gathered_dev || !key_dev || world < 1) return fail(KSS_E_INVAL, "bad select arguments");
+  if (!gathered_dev || !key_dev || !stats_zero_dev || world < 1) return fail(KSS_E_INVAL, "bad select arguments");
   std::lock_guard<std::mutex> lk(ctx->mu);
   HIP_TRY(hipSetDevice(ctx->cfg.device));
   hipLaunchKernelGGL(k_axis_select, axis_grid(ctx), dim3(AXIS_THREADS), 0, axis_stream(ctx, stream), ctx->dc, ctx->prof,
-                     (const int32_t*)ctx->axis_cv.p, (const long long*)gathered_dev, world, (long long*)key_dev);
+                     (const int32_t*)ctx->axis_cv.p, (const long long*)gathered_dev, world, (long long*)key_dev,
+                     (long long*)stats_zero_dev);
   HIP_TRY(hipGetLastError());
   return 0;
 }
 
-int kss_axis_commit(kss_ctx* ctx, int32_t pod_index, int64_t* key_dev, const int64_t* gathered_dev, int32_t world,
-                    int64_t* stats_dev, int32_t* chosen_dev, void* stream) {
+int kss_axis_commit(kss_ctx* ctx, int32_t pod_index, const int64_t* key_dev, const int64_t* gathered_dev, int32_t world,
+                    int32_t* chosen_dev, void* stream) {
   int rc = axis_check(ctx, pod_index);
   if (rc) return rc;
-  if (!key_dev || !gathered_dev || !stats_dev || world < 1) return fail(KSS_E_INVAL, "bad commit arguments");
+  if (!key_dev || !gathered_dev || world < 1) return fail(KSS_E_INVAL, "bad commit arguments");
   std::lock_guard<std::mutex> lk(ctx->mu);
   HIP_TRY(hipSetDevice(ctx->cfg.device));
   rc = ctx->meta_buf.ensure(sizeof(PodMeta) * (size_t)std::max(ctx->staged_n, 1));
   if (rc) return rc;
   hipLaunchKernelGGL(k_axis_commit, dim3(1), dim3(64), 0, axis_stream(ctx, stream), ctx->dc, ctx->dp, pod_index,
-                     (long long*)key_dev, (const long long*)gathered_dev, world, (long long*)stats_dev, chosen_dev,
+                     (const long long*)key_dev, (const long long*)gathered_dev, world, chosen_dev,
                      (PodMeta*)ctx->meta_buf.p);
   HIP_TRY(hipGetLastError());
   ctx->meta_n = std::max(ctx->meta_n, pod_index + 1);

@@ -59,10 +59,10 @@ SIGNATURES = [
     ("kss_run_staged", C.c_int, [C.c_void_p, C.c_int32, C.c_uint32, P(C.c_int32)]),
     ("kss_reset_node_state", C.c_int, [C.c_void_p]),
     ("kss_load_cluster_rows", C.c_int, [C.c_void_p, P(abi.Cluster), C.c_int32, C.c_int32]),
-    ("kss_axis_eval", C.c_int, [C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p]),
-    ("kss_axis_select", C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p]),
-    ("kss_axis_commit", C.c_int, [C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p,
-                                  C.c_void_p]),
+    ("kss_axis_eval", C.c_int, [C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p,
+                                C.c_void_p, C.c_void_p]),
+    ("kss_axis_select", C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p]),
+    ("kss_axis_commit", C.c_int, [C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p]),
     ("kss_synth_make", C.c_int, [C.c_int32, C.c_uint64, C.c_int32, C.c_int32, P(abi.Synth)]),
     ("kss_synth_free", None, [P(abi.Synth)]),
 ]
@@ -213,15 +213,16 @@ class Context:
         self.n_scalar = cluster_struct.n_scalar
 
     # node-axis launches (kss.h): device pointers and a hipStream_t handle as ints
-    def axis_eval(self, i: int, stats_ptr: int, stream: int):
-        check(lib().kss_axis_eval(self.h, i, stats_ptr, stream))
+    def axis_eval(self, i: int, stats_ptr: int, prev_key_ptr: int, prev_gathered_ptr: int, world: int,
+                  key_zero_ptr: int, chosen_ptr: int, stream: int):
+        check(lib().kss_axis_eval(self.h, i, stats_ptr, prev_key_ptr or None, prev_gathered_ptr or None, world,
+                                  key_zero_ptr, chosen_ptr, stream))
 
-    def axis_select(self, gathered_ptr: int, world: int, key_ptr: int, stream: int):
-        check(lib().kss_axis_select(self.h, gathered_ptr, world, key_ptr, stream))
+    def axis_select(self, gathered_ptr: int, world: int, key_ptr: int, stats_zero_ptr: int, stream: int):
+        check(lib().kss_axis_select(self.h, gathered_ptr, world, key_ptr, stats_zero_ptr, stream))
 
-    def axis_commit(self, i: int, key_ptr: int, gathered_ptr: int, world: int, stats_ptr: int, chosen_ptr: int,
-                    stream: int):
-        check(lib().kss_axis_commit(self.h, i, key_ptr, gathered_ptr, world, stats_ptr, chosen_ptr, stream))
+    def axis_commit(self, i: int, key_ptr: int, gathered_ptr: int, world: int, chosen_ptr: int, stream: int):
+        check(lib().kss_axis_commit(self.h, i, key_ptr, gathered_ptr, world, chosen_ptr, stream))
 
     def schedule_batch(self, podset_struct: abi.PodSet, n: int, record=False, flags=0) -> np.ndarray:
         chosen = np.full(max(n, 1), -2, np.int32)

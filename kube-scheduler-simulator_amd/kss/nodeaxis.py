@@ -1,16 +1,19 @@
 """Node-axis sharding of one cluster over several GPUs.
 
 Every rank owns a contiguous canonical row range of the cluster and stages the same
-pending pods.  A pod is scheduled with three HIP launches per rank and two small
-collectives between them, all enqueued on the rank's current torch stream, so the host
-never waits on the device inside the pod loop:
+pending pods.  A pod is scheduled with two HIP launches per rank and two small
+collectives between them, all enqueued on one stream of the rank, so the host never
+waits on the device inside the pod loop:
 
-    kss_axis_eval     filter chain + raw scores of the local rows, local statistics
+    kss_axis_eval     the previous pod's pending AssumePod (owning rank), then filter
+                      chain + raw scores of the local rows, local statistics
     all_gather        {feasible count, max TaintToleration raw, max NodeAffinity raw}
     kss_axis_select   NormalizeScore with the global statistics, weighted total, local
                       packed selectHost key (total << 32 | 0xFFFFFFFF - global index)
     all_reduce MAX    the packed key: the winner and the lowest-index tie-break at once
-    kss_axis_commit   the owning rank applies AssumePod to the winner row
+
+and kss_axis_commit applies the last pod's AssumePod.  The statistics and key buffers
+are double-buffered by pod parity (include/kss.h).
 
 Under the ``nccl`` backend (RCCL over xGMI) the collectives run on device tensors;
 under ``gloo`` (CPU tests, several ranks sharing one GPU) the 32-byte statistics and the
@@ -95,10 +98,10 @@ class NodeAxisScheduler:
         self.ctx.load_rows(cluster, self.lo, self.hi)
         self.ctx.stage(podset)
         i64 = torch.int64
-        self.stats = torch.zeros(AXIS_STATS, dtype=i64, device=self.device)
-        self.gathered = self.stats if self.world == 1 else torch.zeros(self.world * AXIS_STATS, dtype=i64,
-                                                                       device=self.device)
-        self.key = torch.zeros(1, dtype=i64, device=self.device)
+        self.stats = torch.zeros(2, AXIS_STATS, dtype=i64, device=self.device)  # [pod parity]
+        self.gathered = None if self.world == 1 else torch.zeros(self.world * AXIS_STATS, dtype=i64,
+                                                                 device=self.device)
+        self.key = torch.zeros(2, 1, dtype=i64, device=self.device)
         self.chosen = torch.full((max(self.n_pods, 1),), -2, dtype=torch.int32, device=self.device)
         # a stream of our own: torch's default stream has handle 0, which the C ABI reads as
         # "the context's stream" and would not be ordered with the collectives
@@ -119,17 +122,22 @@ class NodeAxisScheduler:
             raise ValueError("n exceeds the staged pods")
         self.stream.wait_stream(torch.cuda.current_stream(self.device))
         ctx, W = self.ctx, self.world
-        sp, gp, kp, cp = self.stats.data_ptr(), self.gathered.data_ptr(), self.key.data_ptr(), self.chosen.data_ptr()
+        sp = [self.stats[b].data_ptr() for b in (0, 1)]
+        kp = [self.key[b].data_ptr() for b in (0, 1)]
+        cp = self.chosen.data_ptr()
+        gp = [self.gathered.data_ptr()] * 2 if W > 1 else sp  # world 1: the statistics are global
         with torch.cuda.stream(self.stream):
             stream = self.stream.cuda_stream
             for i in range(n):
-                ctx.axis_eval(i, sp, stream)
+                b = i & 1
+                ctx.axis_eval(i, sp[b], kp[1 - b] if i else 0, gp[1 - b] if i else 0, W, kp[b], cp, stream)
                 if W > 1:
-                    gather_stats(self.stats, self.gathered, self.group)
-                ctx.axis_select(gp, W, kp, stream)
+                    gather_stats(self.stats[b], self.gathered, self.group)
+                ctx.axis_select(gp[b], W, kp[b], sp[1 - b], stream)
                 if W > 1:
-                    reduce_key(self.key, self.group)
-                ctx.axis_commit(i, kp, gp, W, sp, cp, stream)
+                    reduce_key(self.key[b], self.group)
+            if n:
+                ctx.axis_commit(n - 1, kp[(n - 1) & 1], gp[(n - 1) & 1], W, cp, stream)
         torch.cuda.current_stream(self.device).wait_stream(self.stream)
         return self.chosen[:n]
 
