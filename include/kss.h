@@ -369,12 +369,15 @@ int kss_schedule_scenarios(int32_t device, const kss_profile* prof, int32_t n_sc
  * staged on every rank (kss_stage_pods).  One pod is two launches on `stream` (a
  * hipStream_t, NULL = the context's stream), never synchronising with the host; the
  * caller runs two collectives between them on the same stream.  With b = i & 1:
+ * Fold buffers per rank: stats = int64[KSS_AXIS_SLOTS][KSS_AXIS_STATS], key =
+ * int64[KSS_AXIS_SLOTS] (workgroup w folds into slot w % KSS_AXIS_SLOTS; readers reduce
+ * over the slots, so the key's all_reduce is an elementwise MAX).
  *   kss_axis_eval(i)    applies the pending AssumePod of pod i-1 (prev_key_dev = key[1-b],
  *                       prev_gathered_dev = its gathered statistics; NULL for i = 0),
  *                       clears key_zero_dev = key[b], then filter + raw scores of the local
  *                       rows, folding {feasible count, max TaintToleration raw, max
- *                       NodeAffinity raw, 0} into stats_dev = stats[b]
- *   (all_gather stats[b] -> gathered_dev[world][4]; world 1: gathered = stats[b])
+ *                       NodeAffinity raw, 0} into the slots of stats_dev = stats[b]
+ *   (all_gather stats[b] -> gathered_dev[world][SLOTS][4]; world 1: gathered = stats[b])
  *   kss_axis_select     NormalizeScore with the global statistics, weighted total, local
  *                       selectHost key (total << 32 | 0xFFFFFFFF - global index) max-folded
  *                       into key_dev = key[b]; clears stats_zero_dev = stats[1-b]
@@ -385,6 +388,8 @@ int kss_schedule_scenarios(int32_t device, const kss_profile* prof, int32_t n_sc
  * prioritizeNodes / selectHost / AssumePod sequence of scheduleOne (SURVEY 8(a) a1, a15,
  * a17, a18) over that rank's rows; pods with spread / inter-pod programs return
  * KSS_E_UNSUPPORTED. */
+#define KSS_AXIS_SLOTS 32
+#define KSS_AXIS_STATS 4
 int kss_load_cluster_rows(kss_ctx* ctx, const kss_cluster* cl, int32_t lo, int32_t hi);
 int kss_axis_eval(kss_ctx* ctx, int32_t pod_index, int64_t* stats_dev, const int64_t* prev_key_dev,
                   const int64_t* prev_gathered_dev, int32_t world, int64_t* key_zero_dev, int32_t* chosen_dev,

@@ -13,7 +13,7 @@
 //   -- all_gather(stats) -> gathered[world][4]
 //   k_axis_select  global statistics (Σ feasible, max, max) from gathered, NormalizeScore
 //                  + weights + the packed selectHost key (total << 32 | ~global index) of
-//                  every local feasible row; the rank's best key is max-folded into key[0].
+//                  every local feasible row; the rank's best key is max-folded into key[].
 //   -- all_reduce(key, MAX)
 //   k_axis_commit  only after the last pod of a batch: its pending AssumePod.
 //
@@ -37,7 +37,16 @@
 namespace kss {
 
 constexpr int AXIS_THREADS = 256;
-constexpr int AXIS_STATS = 4;  // int64 per rank: feasible count, max TT raw, max NA raw, (reserved)
+constexpr int AXIS_MAX_KEYS = 8;  // label key columns cached in LDS per tile (more: read from HBM)
+constexpr int AXIS_STATS = 4;  // int64 per slot: feasible count, max TT raw, max NA raw, (reserved)
+// Fold slots: block b folds into slot b % AXIS_SLOTS, so device-scope atomics on one
+// address are AXIS_SLOTS times less contended (one address for the whole grid cost
+// ~8 us per launch at 100k rows); readers reduce over the slots.  Per rank the
+// statistics are [AXIS_SLOTS][AXIS_STATS] and the key is [AXIS_SLOTS] (MAX all-reduced
+// elementwise).
+constexpr int AXIS_SLOTS = 32;
+static_assert(AXIS_SLOTS == KSS_AXIS_SLOTS && AXIS_STATS == KSS_AXIS_STATS, "kss.h fold layout");
+static_assert(AXIS_SLOTS * AXIS_STATS <= AXIS_THREADS, "one block clears a fold buffer");
 
 // per-row results of the current pod, [5][N] int32: verdict, TT, NA, Fit, BA raw
 struct AxisRows {
@@ -87,27 +96,46 @@ __device__ __forceinline__ long long axis_block_reduce(long long v, long long* r
   return v;  // valid in thread 0
 }
 
+// Wave-cooperative reductions over the fold slots: every lane loads a strided share, then
+// a butterfly; all 64 lanes of the wave must be active, and every lane gets the result.
+__device__ __forceinline__ long long axis_key_max(const long long* key) {
+  const int lane = threadIdx.x & 63;
+  long long K = lane < AXIS_SLOTS ? key[lane] : 0;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const long long u = __shfl_xor(K, o, 64);
+    K = u > K ? u : K;
+  }
+  return K;
+}
+
 __device__ __forceinline__ int axis_winner(long long K) {
   return K ? (int)(0xFFFFFFFFu - (uint32_t)(unsigned long long)K) : -1;
 }
 
 __device__ __forceinline__ void axis_global(const long long* gathered, int world, long long& nf, long long& tt,
                                             long long& na) {
+  const int lane = threadIdx.x & 63;
   nf = 0;
   tt = 0;
   na = 0;
-  for (int r = 0; r < world; r++) {
+  for (int r = lane; r < world * AXIS_SLOTS; r += 64) {
     nf += gathered[r * AXIS_STATS];
     tt = gathered[r * AXIS_STATS + 1] > tt ? gathered[r * AXIS_STATS + 1] : tt;
     na = gathered[r * AXIS_STATS + 2] > na ? gathered[r * AXIS_STATS + 2] : na;
   }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    nf += __shfl_xor(nf, o, 64);
+    const long long t = __shfl_xor(tt, o, 64), a = __shfl_xor(na, o, 64);
+    tt = t > tt ? t : tt;
+    na = a > na ? a : na;
+  }
 }
 
 // chosen[pi] and the PodMeta of pod pi from its reduced key and gathered statistics.
-__device__ __forceinline__ void axis_record(const DevPods& P, int pi, long long K, const long long* gathered, int world,
-                                            int32_t* chosen, PodMeta* meta) {
-  long long nf, tt, na;
-  axis_global(gathered, world, nf, tt, na);
+__device__ __forceinline__ void axis_record(const DevPods& P, int pi, long long K, long long nf, int32_t* chosen,
+                                            PodMeta* meta) {
   const int g = axis_winner(K);
   if (chosen) chosen[pi] = g;
   if (meta) {
@@ -131,60 +159,92 @@ __global__ __launch_bounds__(AXIS_THREADS) void k_axis_eval(DevCluster c, DevPod
                                                             const long long* __restrict__ prev_key,
                                                             const long long* __restrict__ prev_gathered, int world,
                                                             long long* __restrict__ key_zero,
-                                                            int32_t* __restrict__ chosen, PodMeta* __restrict__ meta) {
+                                                            int32_t* __restrict__ chosen, PodMeta* __restrict__ meta,
+                                                            int no_fold) {
   // pending commit of pod pi - 1 (its key was all-reduced after the previous select)
-  const int win = prev_key ? axis_winner(prev_key[0]) - c.node_base : -1;
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
-    if (prev_key) axis_record(P, pi - 1, prev_key[0], prev_gathered, world, chosen, meta);
-    key_zero[0] = 0;  // the buffer k_axis_select folds pod pi's key into
+  const long long prevK = prev_key ? axis_key_max(prev_key) : 0;
+  const int win = prev_key ? axis_winner(prevK) - c.node_base : -1;
+  if (blockIdx.x == 0) {
+    if (prev_key && threadIdx.x < 64) {
+      long long pnf, ptt, pna;
+      axis_global(prev_gathered, world, pnf, ptt, pna);
+      if (threadIdx.x == 0) axis_record(P, pi - 1, prevK, pnf, chosen, meta);
+    }
+    if (threadIdx.x < AXIS_SLOTS) key_zero[threadIdx.x] = 0;  // the buffer k_axis_select folds pod pi's key into
   }
   __shared__ long long red[AXIS_THREADS / 64];
   __shared__ kss_pod p;
   __shared__ kss_profile prof_lds;
-  axis_stage(&p, &P.pods[pi]);
-  if (!DEF) axis_stage(&prof_lds, &prof_arg);
-  __syncthreads();
+  __shared__ int32_t lbl[AXIS_MAX_KEYS * AXIS_THREADS];  // label value ids of the tile's rows
   constexpr kss_profile prof_def = default_profile_c();
   const kss_profile& prof = DEF ? prof_def : prof_lds;
   const size_t N = (size_t)c.N;
+  const bool lcache = c.n_keys <= AXIS_MAX_KEYS;
+  bool staged = false;
   long long nf = 0, tt = 0, na = 0;
-  for (int n = blockIdx.x * blockDim.x + threadIdx.x; n < c.N; n += gridDim.x * blockDim.x) {
-    int f = KSS_F_NOT_EVALUATED, rt = 0, rn = 0, rf = 0, rb = 0;
-    const int64_t g = (int64_t)c.node_base + n;
-    bool in = p.prefilter_status == 0;
-    if (in && p.names_len >= 0) {  // NodeAffinity PreFilterResult: rows outside the set are not evaluated
-      bool hit = false;
-      for (int i = 0; i < p.names_len; i++) hit |= (int64_t)P.ints[p.names_off + i] == g;
-      in = hit;
+  // one row per lane per tile; the row, its labels and the pod record are all requested
+  // before the barrier, so the launch pays one memory round trip before the arithmetic
+  for (int base = blockIdx.x * AXIS_THREADS; base < c.N; base += gridDim.x * AXIS_THREADS) {
+    const int n = base + (int)threadIdx.x;
+    const bool valid = n < c.N;
+    NodeRow row{};
+    if (valid) row = row_from_hbm(c, n);
+    if (lcache)
+      for (int k = 0; k < c.n_keys; k++) lbl[k * AXIS_THREADS + threadIdx.x] = valid ? c.label_value[k * N + n] : -1;
+    if (!staged) {
+      axis_stage(&p, &P.pods[pi]);
+      if (!DEF) axis_stage(&prof_lds, &prof_arg);
+      staged = true;
     }
-    if (n == win) commit_pod(c, P, P.pods[pi - 1], n, 1);  // AssumePod, then this lane reads the row
-    if (in) {
-      const NodeRow row = row_from_hbm(c, n);
-      uint16_t detail = 0;
-      f = filter_local(c, P, p, prof.filter_enabled, n, row, &detail);
-      if (f == 0) {
-        rt = (int)tt_score(row, p);
-        rn = (int)na_score(c, P, p, n);
-        rf = (int)fit_score(c, prof, p, n, row);
-        rb = (int)ba_score(c, prof, p, n, row);
-        nf++;
-        tt = rt > tt ? rt : tt;
-        na = rn > na ? rn : na;
+    __syncthreads();
+    DevCluster cc = c;  // label_of reads the tile's LDS copy
+    if (lcache) {
+      cc.ncl = lbl;
+      cc.nc_cap = AXIS_THREADS;
+      cc.nc_lo = base;
+    }
+    if (valid) {
+      int f = KSS_F_NOT_EVALUATED, rt = 0, rn = 0, rf = 0, rb = 0;
+      const int64_t g = (int64_t)c.node_base + n;
+      bool in = p.prefilter_status == 0;
+      if (in && p.names_len >= 0) {  // NodeAffinity PreFilterResult: rows outside the set are not evaluated
+        bool hit = false;
+        for (int i = 0; i < p.names_len; i++) hit |= (int64_t)P.ints[p.names_off + i] == g;
+        in = hit;
       }
+      if (n == win) {  // AssumePod of the previous pod, then this lane re-reads its row
+        commit_pod(c, P, P.pods[pi - 1], n, 1);
+        row = row_from_hbm(c, n);
+      }
+      if (in) {
+        uint16_t detail = 0;
+        f = filter_local(cc, P, p, prof.filter_enabled, n, row, &detail);
+        if (f == 0) {
+          rt = (int)tt_score(row, p);
+          rn = (int)na_score(cc, P, p, n);
+          rf = (int)fit_score(cc, prof, p, n, row);
+          rb = (int)ba_score(cc, prof, p, n, row);
+          nf++;
+          tt = rt > tt ? rt : tt;
+          na = rn > na ? rn : na;
+        }
+      }
+      cv[n] = f;
+      cv[N + n] = rt;
+      cv[2 * N + n] = rn;
+      cv[3 * N + n] = rf;
+      cv[4 * N + n] = rb;
     }
-    cv[n] = f;
-    cv[N + n] = rt;
-    cv[2 * N + n] = rn;
-    cv[3 * N + n] = rf;
-    cv[4 * N + n] = rb;
+    __syncthreads();  // the next tile overwrites lbl
   }
   nf = axis_block_reduce<0>(nf, red);
   tt = axis_block_reduce<1>(tt, red);
   na = axis_block_reduce<1>(na, red);
-  if (threadIdx.x == 0) {
-    if (nf) atomicAdd((unsigned long long*)&stats[0], (unsigned long long)nf);
-    if (tt) atomicMax(&stats[1], tt);
-    if (na) atomicMax(&stats[2], na);
+  if (threadIdx.x == 0 && !no_fold) {
+    long long* sl = stats + (blockIdx.x % AXIS_SLOTS) * AXIS_STATS;
+    if (nf) atomicAdd((unsigned long long*)&sl[0], (unsigned long long)nf);
+    if (tt) atomicMax(&sl[1], tt);
+    if (na) atomicMax(&sl[2], na);
   }
 }
 
@@ -193,7 +253,7 @@ __global__ __launch_bounds__(AXIS_THREADS) void k_axis_select(DevCluster c, kss_
                                                               const long long* __restrict__ gathered, int world,
                                                               long long* __restrict__ key,
                                                               long long* __restrict__ stats_zero) {
-  if (blockIdx.x == 0 && threadIdx.x < AXIS_STATS) stats_zero[threadIdx.x] = 0;  // the next pod's fold buffer
+  if (blockIdx.x == 0 && threadIdx.x < AXIS_SLOTS * AXIS_STATS) stats_zero[threadIdx.x] = 0;  // the next pod's fold buffer
   __shared__ long long red[AXIS_THREADS / 64];
   __shared__ kss_profile prof;
   axis_stage(&prof, &prof_arg);
@@ -208,18 +268,21 @@ __global__ __launch_bounds__(AXIS_THREADS) void k_axis_select(DevCluster c, kss_
     best = k > best ? k : best;
   }
   best = axis_block_reduce<1>(best, red);
-  if (threadIdx.x == 0 && best) atomicMax(key, best);
+  if (threadIdx.x == 0 && best) atomicMax(&key[blockIdx.x % AXIS_SLOTS], best);
 }
 
 // One lane: the pending commit of the last pod of a batch (k_axis_eval applies every
 // other pod's commit at the start of the next pod) and its outcome.
 __global__ void k_axis_commit(DevCluster c, DevPods P, int pi, const long long* key, const long long* gathered,
                               int world, int32_t* chosen, PodMeta* meta) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
-  const long long K = key[0];
+  if (blockIdx.x != 0) return;
+  const long long K = axis_key_max(key);  // the whole wave
+  long long nf, tt, na;
+  axis_global(gathered, world, nf, tt, na);
+  if (threadIdx.x != 0) return;
   const int local = axis_winner(K) - c.node_base;
   if (K && local >= 0 && local < c.N) commit_pod(c, P, P.pods[pi], local, 1);
-  axis_record(P, pi, K, gathered, world, chosen, meta);
+  axis_record(P, pi, K, nf, chosen, meta);
 }
 
 }  // namespace kss

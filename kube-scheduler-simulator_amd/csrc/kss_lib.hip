@@ -242,7 +242,9 @@ struct kss_ctx {
   int meta_n = 0;          // pods with an outcome in meta_host
   bool small_values = false;  // every allocatable cpu/mem/eph < 2^46: k_simple's divisions stay below 2^53
   bool axis_meta_dirty = false;  // meta_buf holds node-axis outcomes not yet copied to meta_host
-  DevBuf axis_cv;             // node-axis sharding: [5][N] per-row verdict + raw scores of the current pod
+  DevBuf axis_cv;
+  int axis_max_blocks = 0;  // KSS_AXIS_BLOCKS: cap on the node-axis grid (tuning)
+  int axis_no_fold = 0;     // KSS_AXIS_NO_FOLD: timing experiment only, statistics not folded (wrong results)             // node-axis sharding: [5][N] per-row verdict + raw scores of the current pod
 };
 
 namespace {
@@ -566,6 +568,8 @@ kss_ctx* kss_create(const kss_config* cfg, const kss_profile* prof) {
   if (const char* e = getenv("KSS_SHARDS")) ctx->force_w = std::max(0, atoi(e));
   ctx->stamps_file = getenv("KSS_STAMPS_FILE");
   ctx->no_simple = getenv("KSS_NO_SIMPLE") != nullptr;
+  if (const char* e = getenv("KSS_AXIS_BLOCKS")) ctx->axis_max_blocks = std::max(0, atoi(e));
+  ctx->axis_no_fold = getenv("KSS_AXIS_NO_FOLD") != nullptr;
   if (const char* e = getenv("KSS_NODES_PER_SHARD")) ctx->nodes_per_shard = std::max(1, atoi(e));
   if (const char* e = getenv("KSS_THREADS")) ctx->pref_threads = std::min(KSS_MAX_THREADS, std::max(64, atoi(e)));
   if (hipSetDevice(cfg->device) != hipSuccess || hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess ||
@@ -709,7 +713,7 @@ static int axis_check(kss_ctx* ctx, int32_t pod_index) {
 
 static dim3 axis_grid(kss_ctx* ctx) {
   const int blocks = (ctx->dc.N + AXIS_THREADS - 1) / AXIS_THREADS;
-  return dim3((unsigned)std::max(1, std::min(blocks, 4 * ctx->n_cu)));
+  return dim3((unsigned)std::max(1, std::min(blocks, ctx->axis_max_blocks > 0 ? ctx->axis_max_blocks : 4 * ctx->n_cu)));
 }
 
 int kss_axis_eval(kss_ctx* ctx, int32_t pod_index, int64_t* stats_dev, const int64_t* prev_key_dev,
@@ -727,7 +731,7 @@ int kss_axis_eval(kss_ctx* ctx, int32_t pod_index, int64_t* stats_dev, const int
   hipLaunchKernelGGL(fn, axis_grid(ctx), dim3(AXIS_THREADS), 0, axis_stream(ctx, stream), ctx->dc, ctx->dp, ctx->prof,
                      pod_index, (int32_t*)ctx->axis_cv.p, (long long*)stats_dev, (const long long*)prev_key_dev,
                      (const long long*)prev_gathered_dev, world, (long long*)key_zero_dev, chosen_dev,
-                     (PodMeta*)ctx->meta_buf.p);
+                     (PodMeta*)ctx->meta_buf.p, ctx->axis_no_fold);
   HIP_TRY(hipGetLastError());
   if (prev_key_dev) {
     ctx->meta_n = std::max(ctx->meta_n, (int)pod_index);

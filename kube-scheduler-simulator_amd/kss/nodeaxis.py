@@ -31,7 +31,8 @@ from typing import Optional, Tuple
 
 from . import abi, native
 
-AXIS_STATS = 4  # int64 per rank (kss_axis.cuh)
+AXIS_STATS = 4   # int64 per fold slot (KSS_AXIS_STATS)
+AXIS_SLOTS = 32  # fold slots per rank (KSS_AXIS_SLOTS): stats [SLOTS][STATS], key [SLOTS]
 NO_NODE = 0     # packed key of "no feasible node"
 
 
@@ -55,7 +56,7 @@ def unpack_key(key: int) -> Tuple[int, int]:
 
 
 def gather_stats(stats, gathered, group=None):
-    """all_gather of the per-rank statistics vector into gathered[world * AXIS_STATS]."""
+    """all_gather of the per-rank statistics vector into gathered[world * len(stats)]."""
     import torch
     import torch.distributed as dist
     if stats.device.type == "cpu" or dist.get_backend(group) != "gloo":
@@ -68,7 +69,7 @@ def gather_stats(stats, gathered, group=None):
 
 
 def reduce_key(key, group=None):
-    """all_reduce MAX of the packed selectHost key (non-negative int64)."""
+    """Elementwise all_reduce MAX of the packed selectHost key slots (non-negative int64)."""
     import torch.distributed as dist
     if key.device.type == "cpu" or dist.get_backend(group) != "gloo":
         dist.all_reduce(key, op=dist.ReduceOp.MAX, group=group)
@@ -98,10 +99,10 @@ class NodeAxisScheduler:
         self.ctx.load_rows(cluster, self.lo, self.hi)
         self.ctx.stage(podset)
         i64 = torch.int64
-        self.stats = torch.zeros(2, AXIS_STATS, dtype=i64, device=self.device)  # [pod parity]
-        self.gathered = None if self.world == 1 else torch.zeros(self.world * AXIS_STATS, dtype=i64,
+        self.stats = torch.zeros(2, AXIS_SLOTS * AXIS_STATS, dtype=i64, device=self.device)  # [pod parity]
+        self.gathered = None if self.world == 1 else torch.zeros(self.world * AXIS_SLOTS * AXIS_STATS, dtype=i64,
                                                                  device=self.device)
-        self.key = torch.zeros(2, 1, dtype=i64, device=self.device)
+        self.key = torch.zeros(2, AXIS_SLOTS, dtype=i64, device=self.device)
         self.chosen = torch.full((max(self.n_pods, 1),), -2, dtype=torch.int32, device=self.device)
         # a stream of our own: torch's default stream has handle 0, which the C ABI reads as
         # "the context's stream" and would not be ordered with the collectives

@@ -147,3 +147,22 @@ def test_nodeaxis_gloo_ranks_match_oracle(world, config, n_nodes, n_pods):
         np.testing.assert_array_equal(meta, meta_o, err_msg=f"rank {rank}")
         np.testing.assert_array_equal(req[:, :hi - lo], st_o["requested"][:, lo:hi], err_msg=f"rank {rank}")
         np.testing.assert_array_equal(podc[:hi - lo], st_o["pod_count"][lo:hi], err_msg=f"rank {rank}")
+
+
+@pytest.mark.gpu
+def test_nodeaxis_custom_profile_matches_oracle():
+    """A non-default profile (MostAllocated, changed weights) takes k_axis_eval<false>."""
+    import oracle_c
+    from kss import abi, native
+    prof = abi.default_profile()
+    prof.fit_strategy = abi.KSS_FIT_MOST_ALLOCATED
+    prof.weight[abi.KSS_S_NODE_AFFINITY] = 5
+    prof.weight[abi.KSS_S_BALANCED_ALLOCATION] = 3
+    n_nodes, n_pods = 1500, 300
+    s = native.Synth(2, 0, n_nodes, n_pods)
+    chosen_o, _, st_o = oracle_c.schedule(prof, s.cluster, s.pods, n_pods, n_nodes, record=False, threads=8)
+    sch = nodeaxis.NodeAxisScheduler(s.cluster, s.pods, prof, device=0)
+    np.testing.assert_array_equal(sch.schedule().cpu().numpy(), chosen_o)
+    st = sch.node_state()
+    np.testing.assert_array_equal(st["requested"][:, :n_nodes], st_o["requested"][:, :n_nodes])
+    sch.close()
