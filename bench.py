@@ -112,6 +112,74 @@ def measure_traffic(args, cfg):
     return fetch + write, {"fetch_bytes": fetch, "write_bytes": write, "fetch_size_kb_raw": kb["FETCH_SIZE"]}
 
 
+def run_scenarios(args):
+    """What-if scenario sweep (SURVEY 8(e) scenario axis, C5 shape): each rank schedules
+    `--scenarios` independent clusters (config-5 recipe, seed + global scenario index) in
+    one kss_schedule_scenarios launch, one workgroup per scenario, no collective.  The
+    timed figure is the launch's HIP-event time (inputs resident: the upload precedes the
+    first event); the wall time including the host->device upload is reported beside it."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    from kss import abi, native
+    from kss.synth import SEED_BASE
+    S = args.scenarios
+    n_nodes = args.nodes or 1000
+    n_pods = args.pods or 1000
+    synths = [native.Synth(5, SEED_BASE + 5 + 7919 * (rank * S + k), n_nodes, n_pods) for k in range(S)]
+    prof = abi.default_profile()
+    clusters = [x.cluster for x in synths]
+    podsets = [x.pods for x in synths]
+    for _ in range(args.warmup):
+        native.schedule_scenarios(prof, clusters, podsets, device=local)
+    if dist:
+        dist.barrier()
+    dev_ms, t0 = [], time.perf_counter()
+    for _ in range(args.steps):
+        chosen, ms = native.schedule_scenarios(prof, clusters, podsets, device=local)
+        dev_ms.append(ms)
+    wall = time.perf_counter() - t0
+    elapsed = sum(dev_ms) / 1e3
+    scheduled = int((chosen >= 0).sum())
+    elapsed, scheduled_total = reduce_over_ranks(elapsed, scheduled, dist)
+    evals = world * S * n_pods * n_nodes * args.steps
+    kern_s = sum(dev_ms) / len(dev_ms) / 1e3
+    achieved = B_EVAL[5] * S * n_pods * n_nodes / kern_s / 1e9
+    if rank == 0:
+        out = {
+            "metric": "pod x node filter+score evals/sec (pods scheduled/sec in extra)",
+            "value": evals / elapsed,
+            "unit": "evals/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "int64/f64",
+            "data": "synthetic (SplitMix64, config-5 recipe, seed per scenario)",
+            "config": {"workload": f"C5 shape: {S * world} scenarios x {n_nodes} nodes x {n_pods} pods, default "
+                                   f"profile, pct=100", "scenarios": S * world, "nodes": n_nodes, "pods": n_pods,
+                       "parallelism": f"scenario batch x{world}"},
+            "pods_per_s": scheduled_total * args.steps / elapsed,
+            "wall_ms_per_step_incl_upload": wall / args.steps * 1e3,
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": None, "kernel": "k_simple",
+                         "bytes_per_eval": B_EVAL[5], "algorithmic_bytes_per_launch": B_EVAL[5] * S * n_pods * n_nodes},
+            "cpu_baseline": None,
+        }
+        print(json.dumps(out), flush=True)
+    for x in synths:
+        x.close()
+    if dist:
+        dist.destroy_process_group()
+
+
 def run_node_axis(args):
     """Node-axis bench line (SURVEY 8(e), C4 shape): the SAME cluster on every rank, rows
     split into contiguous blocks, two collectives per pod (all_gather of 32 B statistics,
@@ -216,6 +284,8 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-traffic", action="store_true", help="skip the rocprofv3 FETCH/WRITE_SIZE passes")
     ap.add_argument("--inner", action="store_true", help="child run under the profiler: no CPU leg, no traffic")
+    ap.add_argument("--scenarios", type=int, default=0,
+                    help="C5 shape: this many independent what-if clusters per rank in one launch")
     ap.add_argument("--node-axis", action="store_true",
                     help="C4 shape: one cluster sharded along the node axis over the ranks (RCCL per pod)")
     args = ap.parse_args()
@@ -223,6 +293,8 @@ def main():
         args.no_cpu = args.no_traffic = True
     if args.node_axis:
         return run_node_axis(args)
+    if args.scenarios:
+        return run_scenarios(args)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))

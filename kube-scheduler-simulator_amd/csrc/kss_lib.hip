@@ -1312,6 +1312,29 @@ int kss_schedule_scenarios(int32_t device, const kss_profile* prof, int32_t n_sc
   }
   const size_t job_off = total;
   total = align_up(total + sizeof(DevJob) * n_scen, 256);
+  // k_simple for the whole sweep when every scenario qualifies (no spread / inter-pod
+  // programs, no scalar resources, values inside the exact f64 envelope): pod programs
+  // as blobs at one common stride, one workgroup per scenario
+  bool simple = getenv("KSS_NO_SIMPLE") == nullptr;
+  for (int i = 0; i < prof->fit_n && simple; i++) simple = prof->fit_weight[i] >= 0 && prof->fit_weight[i] < (1ll << 20);
+  size_t blob_mx = 16;
+  for (int sc = 0; sc < n_scen && simple; sc++) {
+    const kss_cluster& cl = clusters[sc];
+    simple = cl.n_scalar == 0;
+    for (size_t i = 0; i < 3 * (size_t)cl.n_nodes && simple; i++) simple = cl.alloc[i] >= 0 && cl.alloc[i] < (1ll << 46);
+    for (int i = 0; i < podsets[sc].n_pods && simple; i++) {
+      const kss_pod& q = podsets[sc].pods[i];
+      simple = !(q.n_hard | q.n_soft | q.ipa_len);
+      if (simple) blob_mx = std::max(blob_mx, serialize_pod(&podsets[sc], i, nullptr));
+    }
+  }
+  const int blob_stride = simple && align_up(blob_mx, 64) <= (size_t)BLOB_MAX ? (int)align_up(blob_mx, 64) : 0;
+  std::vector<size_t> b_off(n_scen, 0);
+  if (blob_stride)
+    for (int sc = 0; sc < n_scen; sc++) {
+      b_off[sc] = total;
+      total = align_up(total + (size_t)blob_stride * std::max(podsets[sc].n_pods, 1), 256);
+    }
   char* arena = nullptr;
   if (hipMalloc(&arena, total) != hipSuccess) {
     hipStreamDestroy(st);
@@ -1337,6 +1360,16 @@ int kss_schedule_scenarios(int32_t device, const kss_profile* prof, int32_t n_sc
     j.slot_bytes = SlotLayout((size_t)clusters[s].n_nodes).bytes;
     j.chosen = (int32_t*)(arena + ch_off[s]);
     j.meta = nullptr;
+    j.blobs = nullptr;
+    j.blob_stride = 0;
+    if (blob_stride) {
+      std::vector<uint8_t> bl((size_t)blob_stride * std::max(podsets[s].n_pods, 1), 0);
+      for (int i = 0; i < podsets[s].n_pods; i++) serialize_pod(&podsets[s], i, bl.data() + (size_t)blob_stride * i);
+      if (hipMemcpy(arena + b_off[s], bl.data(), bl.size(), hipMemcpyHostToDevice) != hipSuccess)
+        rc = fail(KSS_E_DEVICE, "blob upload failed");
+      j.blobs = (const uint8_t*)(arena + b_off[s]);
+      j.blob_stride = blob_stride;
+    }
     // the host-side log tables must stay alive until the copies finish
     if (s % 256 == 255) {
       if (hipStreamSynchronize(st) != hipSuccess) rc = fail(KSS_E_DEVICE, "upload failed");
@@ -1370,8 +1403,11 @@ int kss_schedule_scenarios(int32_t device, const kss_profile* prof, int32_t n_sc
     hipEventRecord(e0, st);
     int max_keys = 0;
     for (int sc = 0; sc < n_scen; sc++) max_keys = std::max(max_keys, clusters[sc].n_label_keys);
-    rc = launch_schedule(st, g, n_scen, need.bins_cap, need.general, max_keys, (const DevJob*)(arena + job_off), *prof,
-                         nullptr, err);
+    if (blob_stride && !need.general && simple_fits(g, blob_stride, max_keys))
+      rc = launch_simple(st, g, n_scen, blob_stride, max_keys, (const DevJob*)(arena + job_off), *prof, nullptr, err);
+    else
+      rc = launch_schedule(st, g, n_scen, need.bins_cap, need.general, max_keys, (const DevJob*)(arena + job_off), *prof,
+                           nullptr, err);
     hipEventRecord(e1, st);
     if (hipStreamSynchronize(st) != hipSuccess && !rc) rc = fail(KSS_E_DEVICE, "k_schedule failed");
     float ms = 0;

@@ -205,9 +205,16 @@ def test_eval_pod_commit_rollback():
         np.testing.assert_array_equal(before[k], after[k])
 
 
-def test_scenarios_match_oracle_per_scenario():
+@pytest.mark.parametrize("config,sizes,n_pods", [
+    (5, [300] * 12, 150),            # k_simple sweep, one workgroup per scenario
+    (5, [1000] * 8, 200),            # C5 scenario size
+    (2, [100, 700, 1000, 3], 120),   # ragged scenario sizes in one launch
+    (1, [3] * 5, 30),                # single-feasible / unschedulable pods
+    (4, [200] * 6, 100),             # zone spread programs: k_schedule sweep
+])
+def test_scenarios_match_oracle_per_scenario(config, sizes, n_pods):
     prof = abi.default_profile()
-    syn = [native.Synth(5, 0x5EED0005 + sc, 300, 150) for sc in range(12)]
+    syn = [native.Synth(config, 0x5EED0000 + config + 7919 * sc, n, n_pods) for sc, n in enumerate(sizes)]
     chosen, ms = native.schedule_scenarios(prof, [x.cluster for x in syn], [x.pods for x in syn])
     off = 0
     for x in syn:
