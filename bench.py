@@ -84,7 +84,7 @@ def reduce_over_ranks(elapsed, scheduled, dist):
     return float(t.item()), int(sc.item())
 
 
-def measure_traffic(args, cfg):
+def measure_traffic(args, cfg, mode=(), match=("k_simple", "k_schedule"), mean=False):
     """HBM bytes per launch of the scheduling kernel from rocprofv3 PMC counters: one child
     process per counter (FETCH_SIZE, WRITE_SIZE), started before this process touches the
     GPU.  FETCH_SIZE is doubled (gfx950 tallies 128-B requests at 64 B,
@@ -96,17 +96,17 @@ def measure_traffic(args, cfg):
         d = tempfile.mkdtemp(prefix="kss_pmc_")
         cmd = ["timeout", "-s", "KILL", "120", "rocprofv3", "--pmc", ctr, "--output-format", "csv", "-d", d, "-o", "p",
                "--", sys.executable, os.path.abspath(__file__), "--inner", "--steps", "1", "--warmup", "0",
-               "--config", str(cfg), "--nodes", str(args.nodes), "--pods", str(args.pods)]
+               "--config", str(cfg), "--nodes", str(args.nodes), "--pods", str(args.pods), *mode]
         subprocess.run(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL, cwd=ROOT)
         vals = []
         for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
             for r in csv.DictReader(open(f)):
-                if r.get("Counter_Name") == ctr and ("k_simple" in r["Kernel_Name"] or "k_schedule" in r["Kernel_Name"]):
+                if r.get("Counter_Name") == ctr and any(m in r["Kernel_Name"] for m in match):
                     vals.append(float(r["Counter_Value"]))
         shutil.rmtree(d, ignore_errors=True)
         if not vals:
             return None, f"no {ctr} sample"
-        kb[ctr] = max(vals)
+        kb[ctr] = sum(vals) / len(vals) if mean else max(vals)
     fetch = 2.0 * kb["FETCH_SIZE"] * 1024.0
     write = kb["WRITE_SIZE"] * 1024.0
     return fetch + write, {"fetch_bytes": fetch, "write_bytes": write, "fetch_size_kb_raw": kb["FETCH_SIZE"]}
@@ -121,6 +121,9 @@ def run_scenarios(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    traffic, traffic_detail = None, "not measured"
+    if rank == 0 and world == 1 and not args.no_traffic:  # before this process touches the GPU
+        traffic, traffic_detail = measure_traffic(args, 5, mode=("--scenarios", str(args.scenarios)))
     dist = None
     if world > 1:
         import torch.distributed as dist
@@ -169,8 +172,9 @@ def run_scenarios(args):
             "pods_per_s": scheduled_total * args.steps / elapsed,
             "wall_ms_per_step_incl_upload": wall / args.steps * 1e3,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": None, "kernel": "k_simple",
-                         "bytes_per_eval": B_EVAL[5], "algorithmic_bytes_per_launch": B_EVAL[5] * S * n_pods * n_nodes},
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": "k_simple",
+                         "bytes_per_eval": B_EVAL[5], "algorithmic_bytes_per_launch": B_EVAL[5] * S * n_pods * n_nodes,
+                         "traffic_detail": traffic_detail},
             "cpu_baseline": None,
         }
         print(json.dumps(out), flush=True)
@@ -191,6 +195,11 @@ def run_node_axis(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    traffic, traffic_detail = None, "not measured"
+    if rank == 0 and world == 1 and not args.no_traffic:  # per k_axis_eval launch, mean over a 200-pod run
+        a = argparse.Namespace(**vars(args))
+        a.pods = 200
+        traffic, traffic_detail = measure_traffic(a, 2, mode=("--node-axis",), match=("k_axis_eval",), mean=True)
     torch.cuda.set_device(local)
     dist = None
     if world > 1:
@@ -259,7 +268,8 @@ def run_node_axis(args):
             "us_per_pod": elapsed / args.steps / n_pods * 1e6,
             "pods_scheduled_per_step": scheduled,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": None, "kernel": "k_axis_eval",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_detail": traffic_detail,
+                         "kernel": "k_axis_eval",
                          "bytes_per_eval": B_EVAL[2], "algorithmic_bytes_per_launch": B_EVAL[2] * rows,
                          "kernel_us": eval_s * 1e6,
                          "note": "per pod the path is latency-bound: 2 launches + 2 collectives"},
