@@ -521,6 +521,32 @@ int check_cluster(const kss_cluster* cl) {
   return 0;
 }
 
+// Profile limits of the device path.  percentageOfNodesToScore must be 100 (SURVEY 8a
+// a1).  The selectHost key packs TotalScore into the upper 32 bits of a signed 64-bit
+// key, so Σ weight·MaxNodeScore over the enabled score plugins must stay below 2^31; the
+// reference accepts any positive int32 weight whose sum fits int64 (framework.go
+// MaxTotalScore), so larger profiles are refused here rather than mis-ranked.
+int check_profile(const kss_profile* prof) {
+  if (prof->pct_nodes_to_score != 100 && prof->pct_nodes_to_score != 0)
+    return fail(KSS_E_UNSUPPORTED, "percentageOfNodesToScore must be 100 (SURVEY 8a a1)");
+  int64_t sum = 0;
+  for (int s = 0; s < KSS_NSCORE; s++) {
+    if (!((prof->score_enabled >> s) & 1u)) continue;
+    if (prof->weight[s] < 0) return fail(KSS_E_INVAL, "negative score plugin weight");
+    sum += (int64_t)prof->weight[s] * 100;
+  }
+  if (sum >= (1ll << 31)) return fail(KSS_E_UNSUPPORTED, "sum of score weights x 100 must be below 2^31 on the device path");
+  if (prof->fit_n < 0 || prof->fit_n > 4 || prof->ba_n < 0 || prof->ba_n > 4)
+    return fail(KSS_E_INVAL, "scoring resource count out of range");
+  for (int i = 0; i < prof->fit_n; i++)
+    if (prof->fit_res[i] < 0 || prof->fit_res[i] >= KSS_NRES || prof->fit_weight[i] < 0)
+      return fail(KSS_E_INVAL, "NodeResourcesFit scoring resource out of range");
+  for (int i = 0; i < prof->ba_n; i++)
+    if (prof->ba_res[i] < 0 || prof->ba_res[i] >= KSS_NRES)
+      return fail(KSS_E_INVAL, "BalancedAllocation resource out of range");
+  return 0;
+}
+
 }  // namespace
 
 // ---------------------------------------------------------------------------
@@ -546,10 +572,7 @@ kss_ctx* kss_create(const kss_config* cfg, const kss_profile* prof) {
     fail(KSS_E_INVAL, "null config/profile");
     return nullptr;
   }
-  if (prof->pct_nodes_to_score != 100 && prof->pct_nodes_to_score != 0) {
-    fail(KSS_E_UNSUPPORTED, "percentageOfNodesToScore must be 100 (SURVEY 8a a1)");
-    return nullptr;
-  }
+  if (check_profile(prof)) return nullptr;
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
     fail(KSS_E_DEVICE, "no HIP device visible");
@@ -896,7 +919,7 @@ static bool pick_geometry(int maxN, int W, int pref_threads, Geometry& g) {
 static int launch_resident(const void* fn, dim3 grid, dim3 block, void** args, size_t shmem, hipStream_t st) {
   static const bool coop = getenv("KSS_COOP_LAUNCH") != nullptr;
   if (coop) {
-    if (int rc = launch_resident(fn, grid, block, args, shmem, st)) return rc;
+    HIP_TRY(hipLaunchCooperativeKernel(fn, grid, block, args, (unsigned)shmem, st));
     return 0;
   }
   int dev = 0, n_cu = 0, per_cu = 0;
@@ -933,7 +956,7 @@ static int launch_schedule(hipStream_t st, const Geometry& g, int n_jobs, int bi
   if (g.W > 1) {
     void* args[] = {(void*)&jobs, (void*)&pr,   (void*)&W,   (void*)&npt,   (void*)&bins_cap,
                     (void*)&cache_keys, (void*)&gran, (void*)&err, (void*)&stamps};
-    HIP_TRY(hipLaunchCooperativeKernel(fn, grid, block, args, (unsigned)shmem, st));
+    if (int rc = launch_resident(fn, grid, block, args, shmem, st)) return rc;
   } else {
     if (gen)
       hipLaunchKernelGGL(k_schedule<true>, grid, block, shmem, st, jobs, pr, W, npt, bins_cap, cache_keys, gran, err, stamps);
@@ -1172,7 +1195,10 @@ int kss_rollback(kss_ctx* ctx, const kss_podset* ps, int32_t pod_index, int32_t 
 
 int kss_schedule_batch(kss_ctx* ctx, const kss_podset* ps, int32_t n, uint32_t flags, int32_t* chosen_out) {
   if (!ctx || !ctx->loaded || !ps) return fail(KSS_E_INVAL, "bad arguments");
-  int rc = validate(&ctx->host, ps, n);
+  if (n < 0 || n > ps->n_pods) return fail(KSS_E_INVAL, "pod count out of range");
+  // every pod is staged (and may be run later by kss_run_staged / the node axis): all of
+  // them are validated, not only the first n
+  int rc = validate(&ctx->host, ps, ps->n_pods);
   if (rc) return rc;
   const bool record = (flags & KSS_SCHED_RECORD) != 0;
   if (record && n > ctx->cfg.max_pods_record) return fail(KSS_E_INVAL, "record capacity (max_pods_record) exceeded");
@@ -1272,10 +1298,9 @@ int kss_fetch_meta(kss_ctx* ctx, int32_t first, int32_t n, int64_t* out) {
 int kss_schedule_scenarios(int32_t device, const kss_profile* prof, int32_t n_scen, const kss_cluster* clusters,
                            const kss_podset* podsets, int32_t* chosen_out, double* device_ms) {
   if (!prof || n_scen < 0 || (n_scen && (!clusters || !podsets || !chosen_out))) return fail(KSS_E_INVAL, "bad arguments");
-  if (prof->pct_nodes_to_score != 100 && prof->pct_nodes_to_score != 0)
-    return fail(KSS_E_UNSUPPORTED, "percentageOfNodesToScore must be 100");
+  int rc = check_profile(prof);
+  if (rc) return rc;
   if (n_scen == 0) return 0;
-  int rc;
   for (int s = 0; s < n_scen; s++) {
     if ((rc = check_cluster(&clusters[s]))) return rc;
     if ((rc = validate(&clusters[s], &podsets[s], podsets[s].n_pods))) return rc;
@@ -1314,6 +1339,13 @@ int kss_schedule_scenarios(int32_t device, const kss_profile* prof, int32_t n_sc
   for (int s = 0; s < n_scen; s++) {
     ch_off[s] = total;
     total = align_up(total + sizeof(int32_t) * std::max(podsets[s].n_pods, 1), 256);
+  }
+  // per-pod outcomes: a pod whose program exceeds the device limits (status 4) fails the
+  // call with KSS_E_UNSUPPORTED instead of looking unschedulable
+  std::vector<size_t> m_off(n_scen);
+  for (int s = 0; s < n_scen; s++) {
+    m_off[s] = total;
+    total = align_up(total + sizeof(PodMeta) * std::max(podsets[s].n_pods, 1), 256);
   }
   const size_t job_off = total;
   total = align_up(total + sizeof(DevJob) * n_scen, 256);
@@ -1364,7 +1396,7 @@ int kss_schedule_scenarios(int32_t device, const kss_profile* prof, int32_t n_sc
     j.slots = (uint8_t*)(arena + s_off[s]);
     j.slot_bytes = SlotLayout((size_t)clusters[s].n_nodes).bytes;
     j.chosen = (int32_t*)(arena + ch_off[s]);
-    j.meta = nullptr;
+    j.meta = (PodMeta*)(arena + m_off[s]);
     j.blobs = nullptr;
     j.blob_stride = 0;
     if (blob_stride) {
@@ -1429,6 +1461,15 @@ int kss_schedule_scenarios(int32_t device, const kss_profile* prof, int32_t n_sc
           hipMemcpy(chosen_out + o, arena + ch_off[s], sizeof(int32_t) * podsets[s].n_pods, hipMemcpyDeviceToHost) != hipSuccess)
         rc = fail(KSS_E_DEVICE, "chosen copy failed");
       o += (size_t)podsets[s].n_pods;
+    }
+    std::vector<PodMeta> m;
+    for (int s = 0; s < n_scen && !rc; s++) {
+      m.resize((size_t)std::max(podsets[s].n_pods, 1));
+      if (podsets[s].n_pods &&
+          hipMemcpy(m.data(), arena + m_off[s], sizeof(PodMeta) * podsets[s].n_pods, hipMemcpyDeviceToHost) != hipSuccess)
+        rc = fail(KSS_E_DEVICE, "outcome copy failed");
+      for (int i = 0; i < podsets[s].n_pods && !rc; i++)
+        if (m[i].status == 4) rc = fail(KSS_E_UNSUPPORTED, "pod program exceeds the device path's per-pod limits");
     }
   }
   if (e0) hipEventDestroy(e0);

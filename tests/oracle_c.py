@@ -35,14 +35,16 @@ def lib():
 class Results:
     """Per-pod result arrays (numpy) for n pods x N nodes."""
 
-    def __init__(self, n_pods, n_nodes):
+    def __init__(self, n_pods, n_nodes, arrays=True):
         N = max(n_nodes, 1)
+        self.structs = (abi.PodResult * max(n_pods, 1))()
+        if not arrays:  # per-pod outcomes only (chosen, n_feasible, scored, status, best_total)
+            return
         self.fail_plugin = np.zeros((n_pods, N), dtype=np.uint8)
         self.fail_detail = np.zeros((n_pods, N), dtype=np.uint16)
         self.raw = np.zeros((n_pods, abi.KSS_NSCORE, N), dtype=np.int64)
         self.norm = np.zeros((n_pods, abi.KSS_NSCORE, N), dtype=np.int64)
         self.total = np.zeros((n_pods, N), dtype=np.int64)
-        self.structs = (abi.PodResult * max(n_pods, 1))()
         for i in range(n_pods):
             s = self.structs[i]
             s.fail_plugin = self.fail_plugin[i].ctypes.data_as(C.POINTER(C.c_uint8))
@@ -59,10 +61,11 @@ class Results:
 
 def schedule(profile, cluster_struct, podset_struct, n_pods, n_nodes, threads=1, record=True, n_classes=0,
              n_terms=0):
-    """Run the C oracle sequentially; returns (chosen, Results|None, final_state dict)."""
+    """Run the C oracle sequentially; returns (chosen, Results|None, final_state dict).
+    record=True keeps every per-node array, record="meta" only the per-pod outcomes."""
     L = lib()
     chosen = np.full(max(n_pods, 1), -2, dtype=np.int32)
-    res = Results(n_pods, n_nodes) if record else None
+    res = Results(n_pods, n_nodes, arrays=record is True) if record else None
     N = max(n_nodes, 1)
     st = dict(requested=np.zeros((abi.KSS_NRES, N), np.int64), nonzero=np.zeros((2, N), np.int64),
               pod_count=np.zeros(N, np.int32), class_count=np.zeros((max(n_classes, 1), N), np.int32),

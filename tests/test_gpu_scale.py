@@ -1,0 +1,200 @@
+"""Full-size GPU parity: the BASELINE configurations and kernel geometries the smaller
+cases in test_gpu_parity.py do not reach, compared bit-exactly with the C oracle.
+
+  * C3 (5,000 nodes, 3 zones, PodTopologySpread + InterPodAffinity) with every per-node
+    record (verdict, failure detail, raw / normalized scores, totals);
+  * the whole C2 batch the bench times (5,000 nodes x 10,000 pods on k_simple);
+  * k_simple at 100,000 nodes: 128 shards x 4 node slots per lane, i.e. both chunks of the
+    shard-granule sweep (kss_simple.cuh simple_exchange, SX_CHUNKS);
+  * C4's recipe (100,000 nodes, zone DoNotSchedule spread) on one GPU (k_schedule, 256
+    shards) and the node-axis kernels at 100,000 rows, world 1;
+  * a 64-scenario slice of the C5 sweep (1,000 nodes x 1,000 pods each).
+"""
+import os
+
+import numpy as np
+import pytest
+
+import oracle_c
+from kss import abi, native, nodeaxis
+from kss.synth import SEED_BASE
+
+pytestmark = pytest.mark.gpu
+
+THREADS = min(16, os.cpu_count() or 1)
+
+
+def _oracle(prof, s, n_pods, record=False):
+    return oracle_c.schedule(prof, s.cluster, s.pods, n_pods, s.n_nodes, record=record, threads=THREADS,
+                             n_classes=s.cluster.n_classes, n_terms=s.cluster.n_terms)
+
+
+def _meta_equal(meta, res_or_chosen, n):
+    for j in range(n):
+        m = res_or_chosen.meta(j)
+        got = dict(chosen=meta[j, 0], n_feasible=meta[j, 1], scored=meta[j, 2], status=meta[j, 3])
+        assert got == {k: m[k] for k in got}, (j, got, m)
+        if m["scored"]:
+            assert meta[j, 4] == m["best_total"], j
+
+
+def _state_equal(ctx, st, n_nodes, n_classes, n_terms):
+    g = ctx.node_state()
+    np.testing.assert_array_equal(g["requested"][:, :n_nodes], st["requested"][:, :n_nodes])
+    np.testing.assert_array_equal(g["nonzero"][:, :n_nodes], st["nonzero"][:, :n_nodes])
+    np.testing.assert_array_equal(g["pod_count"][:n_nodes], st["pod_count"][:n_nodes])
+    if n_classes:
+        np.testing.assert_array_equal(g["class_count"][:n_classes], st["class_count"][:n_classes])
+    if n_terms:
+        np.testing.assert_array_equal(g["term_count"][:n_terms], st["term_count"][:n_terms])
+
+
+def test_c3_full_cluster_with_records():
+    """BASELINE configs[2]: 5,000 nodes, 500 pods, every per-node record of every pod."""
+    prof = abi.default_profile()
+    n_nodes, n_pods = 5000, 500
+    s = native.Synth(3, 0, n_nodes, n_pods)
+    chosen_o, res, st = _oracle(prof, s, n_pods, record=True)
+    ctx = native.Context(prof, max_pods_record=n_pods)
+    ctx.load(s.cluster)
+    chosen = ctx.schedule_batch(s.pods, n_pods, record=True)
+    assert ctx.last_geometry()["shards"] > 1
+    np.testing.assert_array_equal(chosen, chosen_o)
+    for j in range(n_pods):
+        r = ctx.fetch_record(j)
+        m = res.meta(j)
+        assert (r.chosen, r.n_feasible, r.scored, r.status) == (m["chosen"], m["n_feasible"], m["scored"],
+                                                                m["status"]), j
+        np.testing.assert_array_equal(r.fail_plugin[:n_nodes], res.fail_plugin[j], err_msg=f"pod {j}")
+        np.testing.assert_array_equal(r.fail_detail[:n_nodes], res.fail_detail[j], err_msg=f"pod {j}")
+        if m["scored"]:
+            feas = res.fail_plugin[j] == 0
+            np.testing.assert_array_equal(r.raw[:, feas], res.raw[j][:, feas], err_msg=f"pod {j}")
+            np.testing.assert_array_equal(r.norm[:, feas], res.norm[j][:, feas], err_msg=f"pod {j}")
+            np.testing.assert_array_equal(r.total[feas], res.total[j][feas], err_msg=f"pod {j}")
+            assert r.s.best_total == m["best_total"], j
+    _state_equal(ctx, st, n_nodes, s.cluster.n_classes, s.cluster.n_terms)
+    ctx.close()
+
+
+def test_c3_full_batch_no_record():
+    """C3 5,000 nodes x 2,000 pods through the resident path (chosen, outcomes, final
+    state including the class / term counts that commits update)."""
+    prof = abi.default_profile()
+    n_nodes, n_pods = 5000, 2000
+    s = native.Synth(3, 0, n_nodes, n_pods)
+    chosen_o, res, st = _oracle(prof, s, n_pods, record="meta")
+    ctx = native.Context(prof)
+    ctx.load(s.cluster)
+    ctx.stage(s.pods)
+    np.testing.assert_array_equal(ctx.run_staged(n_pods), chosen_o)
+    _meta_equal(ctx.fetch_meta(n_pods), res, n_pods)
+    _state_equal(ctx, st, n_nodes, s.cluster.n_classes, s.cluster.n_terms)
+    ctx.close()
+
+
+def test_c2_full_batch_matches_oracle():
+    """BASELINE configs[1] exactly as bench.py times it: 5,000 nodes x 10,000 pods from the
+    initial snapshot, resident inputs, k_simple."""
+    prof = abi.default_profile()
+    n_nodes, n_pods = 5000, 10000
+    s = native.Synth(2, SEED_BASE + 2, n_nodes, n_pods)
+    chosen_o, res, st = _oracle(prof, s, n_pods, record="meta")
+    ctx = native.Context(prof)
+    ctx.load(s.cluster)
+    ctx.stage(s.pods)
+    for rep in range(2):  # the bench's reset + replay
+        ctx.reset()
+        chosen = ctx.run_staged(n_pods)
+        assert ctx.last_kernel() == "k_simple"
+        np.testing.assert_array_equal(chosen, chosen_o, err_msg=f"replay {rep}")
+    _meta_equal(ctx.fetch_meta(n_pods), res, n_pods)
+    _state_equal(ctx, st, n_nodes, 0, 0)
+    ctx.close()
+
+
+def test_k_simple_100k_nodes_two_sweep_chunks():
+    """100,000 nodes: 128 k_simple shards (both 64-shard chunks of the granule sweep) with
+    4 node slots per lane."""
+    prof = abi.default_profile()
+    n_nodes, n_pods = 100000, 200
+    s = native.Synth(2, SEED_BASE + 4, n_nodes, n_pods)
+    chosen_o, res, st = _oracle(prof, s, n_pods, record="meta")
+    ctx = native.Context(prof)
+    ctx.load(s.cluster)
+    ctx.stage(s.pods)
+    chosen = ctx.run_staged(n_pods)
+    geo = ctx.last_geometry()
+    assert ctx.last_kernel() == "k_simple"
+    assert geo["shards"] > 64 and geo["nodes_per_lane"] > 1, geo
+    np.testing.assert_array_equal(chosen, chosen_o)
+    _meta_equal(ctx.fetch_meta(n_pods), res, n_pods)
+    _state_equal(ctx, st, n_nodes, 0, 0)
+    ctx.close()
+
+
+@pytest.mark.parametrize("shards", [65, 100])
+def test_k_simple_forced_shards_above_one_chunk(shards, monkeypatch):
+    """KSS_SHARDS forces W > 64 on a 20,000-node cluster (second sweep chunk, ragged)."""
+    monkeypatch.setenv("KSS_SHARDS", str(shards))
+    prof = abi.default_profile()
+    n_nodes, n_pods = 20000, 300
+    s = native.Synth(2, 0, n_nodes, n_pods)
+    chosen_o, res, st = _oracle(prof, s, n_pods, record="meta")
+    ctx = native.Context(prof)
+    ctx.load(s.cluster)
+    ctx.stage(s.pods)
+    chosen = ctx.run_staged(n_pods)
+    assert ctx.last_kernel() == "k_simple"
+    assert ctx.last_geometry()["shards"] == shards
+    np.testing.assert_array_equal(chosen, chosen_o)
+    _meta_equal(ctx.fetch_meta(n_pods), res, n_pods)
+    _state_equal(ctx, st, n_nodes, 0, 0)
+    ctx.close()
+
+
+def test_c4_recipe_on_one_gpu():
+    """BASELINE configs[3]'s recipe (100,000 nodes, zone DoNotSchedule spread) on one GPU:
+    the general kernel at 256 shards, 200 pods."""
+    prof = abi.default_profile()
+    n_nodes, n_pods = 100000, 200
+    s = native.Synth(4, 0, n_nodes, n_pods)
+    chosen_o, res, st = _oracle(prof, s, n_pods, record="meta")
+    ctx = native.Context(prof)
+    ctx.load(s.cluster)
+    ctx.stage(s.pods)
+    chosen = ctx.run_staged(n_pods)
+    assert ctx.last_kernel() == "k_schedule"
+    np.testing.assert_array_equal(chosen, chosen_o)
+    _meta_equal(ctx.fetch_meta(n_pods), res, n_pods)
+    _state_equal(ctx, st, n_nodes, s.cluster.n_classes, 0)
+    ctx.close()
+
+
+def test_nodeaxis_100k_rows_world1():
+    n_nodes, n_pods = 100000, 300
+    prof = abi.default_profile()
+    s = native.Synth(2, SEED_BASE + 4, n_nodes, n_pods)
+    chosen_o, res, st = _oracle(prof, s, n_pods, record="meta")
+    sch = nodeaxis.NodeAxisScheduler(s.cluster, s.pods, prof, device=0)
+    chosen = sch.schedule().cpu().numpy()
+    np.testing.assert_array_equal(chosen, chosen_o)
+    _meta_equal(sch.meta(n_pods), res, n_pods)
+    g = sch.node_state()
+    np.testing.assert_array_equal(g["requested"][:, :n_nodes], st["requested"][:, :n_nodes])
+    np.testing.assert_array_equal(g["pod_count"][:n_nodes], st["pod_count"][:n_nodes])
+    sch.close()
+
+
+def test_c5_sweep_64_scenarios():
+    """64 scenarios of the C5 sweep (1,000 nodes x 1,000 pods each, seed per scenario) in
+    one launch, each against its own oracle run."""
+    prof = abi.default_profile()
+    syn = [native.Synth(5, SEED_BASE + 5 + 7919 * k, 1000, 1000) for k in range(64)]
+    chosen, ms = native.schedule_scenarios(prof, [x.cluster for x in syn], [x.pods for x in syn])
+    assert ms > 0
+    off = 0
+    for k, x in enumerate(syn):
+        ch, _, _ = _oracle(prof, x, x.n_pods)
+        np.testing.assert_array_equal(chosen[off:off + x.n_pods], ch, err_msg=f"scenario {k}")
+        off += x.n_pods
