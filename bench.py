@@ -35,14 +35,24 @@ B_EVAL = {1: 109, 2: 109, 3: 129, 4: 109, 5: 109}
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 
 
-def cpu_baseline(config, n_nodes, n_pods, seconds, threads):
-    """The CPU oracle (plain-C restatement, OpenMP over nodes) on the same workload: the whole
+def cpu_threads():
+    """Host threads for the CPU baseline: the process's CPU share (OMP_NUM_THREADS, which the
+    GPU box sets to its per-GPU share, else the affinity mask), with nproc stated beside it."""
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    env = os.environ.get("OMP_NUM_THREADS")
+    t = int(env) if env and env.isdigit() and int(env) > 0 else aff
+    return max(1, min(t, aff)), {"nproc": os.cpu_count(), "affinity_cpus": aff, "omp_num_threads": env}
+
+
+def cpu_baseline(config, n_nodes, n_pods, seconds, threads, seed=0):
+    """The CPU oracle (plain-C restatement, OpenMP over nodes: the reference's
+    parallelize.Until over nodes inside each pod) on the same workload: the whole
     sequential batch is scheduled from the initial snapshot, repeated until `seconds` of wall
     time have passed (a bounded sample; a smaller pod prefix when one batch alone is longer)."""
     import oracle_c
     from kss import abi, native
 
-    s = native.Synth(config, 0, n_nodes, n_pods)
+    s = native.Synth(config, seed, n_nodes, n_pods)
     prof = abi.default_profile()
     kw = dict(threads=threads, record=False, n_classes=s.cluster.n_classes, n_terms=s.cluster.n_terms)
     # size the prefix so one batch takes at most ~seconds/3
@@ -58,11 +68,45 @@ def cpu_baseline(config, n_nodes, n_pods, seconds, threads):
         t_used += time.perf_counter() - t0
         reps += 1
     evals = reps * n * n_nodes
-    return {"value": evals / t_used, "unit": "pod-node evals/s", "cores": threads, "kind": "port",
+    _, host = cpu_threads()
+    return {"value": evals / t_used, "unit": "pod-node evals/s", "cores": threads, "kind": "port", "host": host,
             "sample": f"{reps} x the first {n} of {n_pods} pods of config C{config} ({n_nodes} nodes), "
                       f"sequential from the initial snapshot, {t_used:.1f} s wall, "
                       f"oracle/kss_oracle.c OpenMP over nodes ({threads} threads)",
             "pods_per_s": reps * n / t_used}
+
+
+def cpu_baseline_scenarios(n_nodes, n_pods, seconds, threads, seed_of):
+    """C5 on the CPU: independent scenarios in parallel (one oracle call per scenario and
+    thread, single-threaded inside; ctypes releases the GIL), as many scenarios as fit in
+    about `seconds` of wall time."""
+    import concurrent.futures as cf
+
+    import oracle_c
+    from kss import abi, native
+
+    prof = abi.default_profile()
+
+    def one(k):
+        s = native.Synth(5, seed_of(k), n_nodes, n_pods)
+        oracle_c.schedule(prof, s.cluster, s.pods, n_pods, n_nodes, threads=1, record=False,
+                          n_classes=s.cluster.n_classes, n_terms=s.cluster.n_terms)
+        s.close()
+
+    t0 = time.perf_counter()
+    one(0)
+    per = time.perf_counter() - t0
+    n_scen = max(threads, int(seconds / max(per, 1e-4) * threads))
+    n_scen = (n_scen + threads - 1) // threads * threads
+    t0 = time.perf_counter()
+    with cf.ThreadPoolExecutor(max_workers=threads) as ex:
+        list(ex.map(one, range(n_scen)))
+    dt = time.perf_counter() - t0
+    _, host = cpu_threads()
+    return {"value": n_scen * n_pods * n_nodes / dt, "unit": "pod-node evals/s", "cores": threads, "kind": "port",
+            "host": host, "pods_per_s": n_scen * n_pods / dt,
+            "sample": f"{n_scen} C5 scenarios ({n_nodes} nodes x {n_pods} pods each, synthesis included), "
+                      f"{threads} scenarios in parallel, {dt:.1f} s wall, oracle/kss_oracle.c single-threaded per scenario"}
 
 
 def rank_seed(seed_base, cfg, rank):
@@ -133,25 +177,36 @@ def run_scenarios(args):
     S = args.scenarios
     n_nodes = args.nodes or 1000
     n_pods = args.pods or 1000
-    synths = [native.Synth(5, SEED_BASE + 5 + 7919 * (rank * S + k), n_nodes, n_pods) for k in range(S)]
+    seed_of = lambda k: SEED_BASE + 5 + 7919 * (rank * S + k)  # noqa: E731
+    synths = [native.Synth(5, seed_of(k), n_nodes, n_pods) for k in range(S)]
     prof = abi.default_profile()
     clusters = [x.cluster for x in synths]
     podsets = [x.pods for x in synths]
+    # stage once (pack + one upload); every step then restores the snapshots on the device
+    # and schedules all scenarios: inputs resident
+    t0 = time.perf_counter()
+    sweep = native.Sweep(prof, clusters, podsets, device=local)
+    stage_s = time.perf_counter() - t0
+    info = sweep.info()
     for _ in range(args.warmup):
-        native.schedule_scenarios(prof, clusters, podsets, device=local)
+        sweep.run()
     if dist:
         dist.barrier()
     dev_ms, t0 = [], time.perf_counter()
     for _ in range(args.steps):
-        chosen, ms = native.schedule_scenarios(prof, clusters, podsets, device=local)
+        chosen, ms = sweep.run()
         dev_ms.append(ms)
     wall = time.perf_counter() - t0
-    elapsed = sum(dev_ms) / 1e3
+    elapsed = wall
     scheduled = int((chosen >= 0).sum())
     elapsed, scheduled_total = reduce_over_ranks(elapsed, scheduled, dist)
     evals = world * S * n_pods * n_nodes * args.steps
     kern_s = sum(dev_ms) / len(dev_ms) / 1e3
     achieved = B_EVAL[5] * S * n_pods * n_nodes / kern_s / 1e9
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        threads, _ = cpu_threads()
+        cpu = cpu_baseline_scenarios(n_nodes, n_pods, args.cpu_seconds, threads, seed_of)
     if rank == 0:
         out = {
             "metric": "pod x node filter+score evals/sec (pods scheduled/sec in extra)",
@@ -170,14 +225,19 @@ def run_scenarios(args):
                                    f"profile, pct=100", "scenarios": S * world, "nodes": n_nodes, "pods": n_pods,
                        "parallelism": f"scenario batch x{world}"},
             "pods_per_s": scheduled_total * args.steps / elapsed,
-            "wall_ms_per_step_incl_upload": wall / args.steps * 1e3,
+            "device_ms_per_step": kern_s * 1e3,
+            "stage_ms_once": stage_s * 1e3,
+            "upload_bytes": info["upload_bytes"],
+            "evals_per_s_incl_stage_one_step": S * n_pods * n_nodes / (stage_s + elapsed / args.steps),
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": "k_simple",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": info["kernel"],
                          "bytes_per_eval": B_EVAL[5], "algorithmic_bytes_per_launch": B_EVAL[5] * S * n_pods * n_nodes,
-                         "traffic_detail": traffic_detail},
-            "cpu_baseline": None,
+                         "traffic_detail": traffic_detail,
+                         "note": "achieved uses device time of reset + k_static + k_simple per sweep"},
+            "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)
+    sweep.close()
     for x in synths:
         x.close()
     if dist:
@@ -333,9 +393,12 @@ def main():
     import numpy as np
     chosen = np.zeros(n_pods, np.int32)
 
+    loop_ms = []
+
     def step():
         ctx.reset()
         ctx.run_staged(n_pods, out=chosen)
+        loop_ms.append(ctx.last_loop_ms())
         return ctx.last_timing()[0]
 
     for _ in range(args.warmup):
@@ -357,13 +420,14 @@ def main():
     value = evals / elapsed
     pods_per_s = scheduled_total * args.steps / elapsed
     kern_avg_s = sum(kern_ms) / len(kern_ms) / 1e3
-    achieved = B_EVAL[cfg] * n_pods * n_nodes / kern_avg_s / 1e9
+    loop_s = sum(loop_ms[-args.steps:]) / args.steps / 1e3  # the dominant kernel (k_simple / k_schedule) alone
+    achieved = B_EVAL[cfg] * n_pods * n_nodes / loop_s / 1e9
 
     if rank == 0:
         cpu = None
         if not args.no_cpu and world == 1:
-            threads = min(16, os.cpu_count() or 1)
-            cpu = cpu_baseline(cfg, n_nodes, n_pods, args.cpu_seconds, threads)
+            threads, _ = cpu_threads()
+            cpu = cpu_baseline(cfg, n_nodes, n_pods, args.cpu_seconds, threads, seed=seed)
         out = {
             "metric": "pod x node filter+score evals/sec (pods scheduled/sec in extra)",
             "value": value,
@@ -382,6 +446,8 @@ def main():
             "pods_per_s": pods_per_s,
             "pods_scheduled_per_step": scheduled,
             "kernel_ms_per_step": kern_avg_s * 1e3,
+            "loop_kernel_ms_per_step": loop_s * 1e3,
+            "us_per_pod": elapsed / args.steps / n_pods * 1e6,
             "geometry": ctx.last_geometry(),
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,

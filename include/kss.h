@@ -360,9 +360,25 @@ int kss_run_staged(kss_ctx* ctx, int32_t n, uint32_t flags, int32_t* chosen_out)
 int kss_reset_node_state(kss_ctx* ctx);
 
 /* many independent clusters (what-if scenarios, KEP-184): clusters[s] with podsets[s];
- * one workgroup per scenario, no inter-scenario communication. chosen_out is [sum n_pods]. */
+ * one workgroup per scenario, no inter-scenario communication. chosen_out is [sum n_pods].
+ * One-shot form of kss_sweep_create + kss_sweep_run + kss_sweep_destroy. */
 int kss_schedule_scenarios(int32_t device, const kss_profile* prof, int32_t n_scen, const kss_cluster* clusters,
                            const kss_podset* podsets, int32_t* chosen_out, double* device_ms);
+
+/* Resident what-if sweep.  kss_sweep_create validates and packs every scenario's
+ * snapshot and pod programs into one host image and uploads it with one copy (NULL on
+ * error: kss_last_error).  kss_sweep_run restores every scenario's node state to its
+ * snapshot on the device and schedules all of them (chosen_out [sum n_pods]; device_ms =
+ * reset + launches, HIP events).  Replaces, per scenario, the sequential scheduleOne
+ * loop of the simulator's scheduler; the scenario axis of SURVEY 8(e).
+ * kss_sweep_info: host wall time of create (pack + upload), the kernel used (1 k_simple,
+ * 0 k_schedule) and the uploaded bytes. */
+typedef struct kss_sweep kss_sweep;
+kss_sweep* kss_sweep_create(int32_t device, const kss_profile* prof, int32_t n_scen, const kss_cluster* clusters,
+                            const kss_podset* podsets);
+int kss_sweep_run(kss_sweep* sw, int32_t* chosen_out, double* device_ms);
+int kss_sweep_info(kss_sweep* sw, double* stage_ms, int32_t* kernel, int64_t* upload_bytes);
+void kss_sweep_destroy(kss_sweep* sw);
 
 /* ---- node-axis sharding ----------------------------
  * One context per GPU holds rows [lo, hi) of the cluster (node_base = lo); the pods are
@@ -401,6 +417,9 @@ int kss_axis_commit(kss_ctx* ctx, int32_t pod_index, const int64_t* key_dev, con
 
 /* timing of the last kss_schedule_batch / kss_eval_pod device work (HIP events on the work stream) */
 int kss_last_timing(kss_ctx* ctx, double* device_ms, int32_t* launches);
+/* device time of the sequential-loop kernel alone in the last batch: the k_simple
+ * launch(es) without the k_static precompute (k_schedule batches: the whole batch) */
+int kss_last_loop_timing(kss_ctx* ctx, double* loop_ms);
 /* launch geometry of the last scheduling launch: out[0] shards (workgroups) per cluster,
  * out[1] threads per workgroup, out[2] node slots per lane */
 int kss_last_geometry(kss_ctx* ctx, int32_t* out3);

@@ -7,14 +7,20 @@
 //                sequential batch (kss_schedule_batch), the drop-in per-pod call
 //                (kss_eval_pod, no commit) and the what-if scenario sweep
 //                (kss_schedule_scenarios, grid = #scenarios).
-//   k_simple     batches without PodTopologySpread / InterPodAffinity programs and
-//                without a result record: node rows in registers, pod programs as
-//                LDS blobs, one exchange per pod (kss_simple.cuh).
+//   k_static     batches without PodTopologySpread / InterPodAffinity programs: the
+//                commit-invariant part of every (pod, node) evaluation, one lane each,
+//                packed into 32-bit static words in HBM (kss_simple.cuh).
+//   k_simple     the sequential loop of those batches (no result record): node rows
+//                in LDS, compact pod records and static words in LDS rings, only the
+//                state-dependent filter / scores per pod, one exchange per pod.
 //   k_commit     one lane: AssumePod / ForgetPod delta on one node row.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
+#include <memory>
+#include <thread>
 #include <cstdio>
 #include <cstring>
 #include <mutex>
@@ -31,9 +37,11 @@ using namespace kss;
 namespace {
 
 thread_local std::string g_err;
+thread_local int g_rc = 0;  // code of the last failure (calls that return a handle report it this way)
 
 int fail(int code, const std::string& msg) {
   g_err = msg;
+  g_rc = code;
   return code;
 }
 
@@ -70,8 +78,9 @@ struct DevJob {
   size_t slot_bytes;
   int32_t* chosen;
   PodMeta* meta;
-  const uint8_t* blobs;  // k_simple: serialized pod programs, blob_stride bytes each
-  int32_t blob_stride;
+  const SPod* spods;  // k_simple: compact pod records [n_pods]
+  uint32_t* stat;     // k_static -> k_simple: static words of the current pod chunk [chunk][N]
+  kss_profile prof;   // k_simple<false>: staged word by word into LDS (a by-value kernel argument would land in scratch)
 };
 
 }  // namespace
@@ -147,16 +156,48 @@ __global__ __launch_bounds__(KSS_MAX_THREADS) void k_schedule(const DevJob* __re
 
 // grid = n_jobs * W, as k_schedule; each shard's nodes live in LDS (cap slots).
 // DEF: the profile is the v1.26 default, folded into the code.
+// Pods [k0, min(k1, n_pods)) of every job; the job's stat buffer holds their static words.
 template <bool DEF>
 __global__ __launch_bounds__(KSS_MAX_THREADS) void k_simple(const DevJob* __restrict__ jobs, kss_profile prof, int W,
-                                                            int cap, unsigned long long* gran, int* err,
+                                                            int cap, int k0, int k1, unsigned long long* gran, int* err,
                                                             unsigned long long* stamps) {
   extern __shared__ __attribute__((aligned(16))) long long smem[];
   const int ji = blockIdx.x / W, w = blockIdx.x % W;
   const DevJob job = jobs[ji];
-  const kss_profile P = DEF ? default_profile_c() : prof;
-  simple_schedule(job.c, job.blobs, job.blob_stride, job.n_pods, job.chosen, job.meta, P, W, w, cap,
+  constexpr kss_profile def_prof = default_profile_c();
+  SimpleHdr& H = *reinterpret_cast<SimpleHdr*>(smem);
+  if (!DEF) {
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(&jobs[ji].prof);
+    uint32_t* dst = reinterpret_cast<uint32_t*>(&H.prof);
+    for (int i = threadIdx.x; i < (int)(sizeof(kss_profile) / 4); i += blockDim.x) dst[i] = src[i];
+    __syncthreads();
+  }
+  const kss_profile& P = DEF ? def_prof : H.prof;
+  simple_schedule(job.c, job.spods, job.stat, job.P.ints, k0, min(k1, job.n_pods), job.chosen, job.meta, P, W, w, cap,
                   gran ? gran + (size_t)ji * 2 * W * SX_VALS : nullptr, err, ji == 0 ? stamps : nullptr, smem);
+}
+
+// Static words of pods [k0, min(k1, n_pods)) x every node of every job.  grid: x = 256-node
+// tiles, y = groups of STATIC_PODS pods, z = job.  One lane per node walks its group.
+template <bool DEF>
+__global__ __launch_bounds__(256) void k_static(const DevJob* __restrict__ jobs, kss_profile prof_arg, int k0, int k1) {
+  const DevJob& job = jobs[blockIdx.z];
+  const int N = job.c.N;
+  const int n = (int)(blockIdx.x * 256 + threadIdx.x);
+  const int kend = min(k1, job.n_pods);
+  const int kb = k0 + (int)blockIdx.y * STATIC_PODS;
+  if (kb >= kend || n >= N) return;
+  const DevCluster c = job.c;
+  const DevPods P = job.P;
+  uint32_t* stat = job.stat;
+  const kss_profile prof = DEF ? default_profile_c() : prof_arg;
+  const uint32_t flags = c.node_flags[n];
+  const uint64_t th = c.taint_hard[n], ts = c.taint_soft[n];
+  for (int t = 0; t < STATIC_PODS; t++) {
+    const int k = kb + t;
+    if (k >= kend) break;
+    stat[(size_t)(k - k0) * N + n] = static_word(c, P, P.pods[k], prof, n, flags, th, ts);
+  }
 }
 
 __global__ void k_commit(DevCluster c, DevPods P, int pi, int local, int sign) {
@@ -233,10 +274,11 @@ struct kss_ctx {
   int last_geom[3] = {0, 0, 0};
   const char* stamps_file = nullptr;  // KSS_STAMPS_FILE: dump per-phase timestamps of each launch
   DevBuf stamp_buf;
-  // staged pod programs serialized for k_simple (blob_stride 0: some pod needs k_schedule)
-  DevBuf blob_buf;
-  std::vector<uint8_t> blob_host;
-  int blob_stride = 0;
+  // compact records of the staged pods for k_simple (spod_ok false: some pod needs
+  // k_schedule) and the static-word scratch of the current chunk
+  DevBuf spod_buf, stat_buf;
+  std::vector<SPod> spod_host;
+  bool spod_ok = false;
   bool no_simple = false;  // KSS_NO_SIMPLE: always launch k_schedule
   int last_kernel = 0;     // 0 k_schedule, 1 k_simple
   int meta_n = 0;          // pods with an outcome in meta_host
@@ -244,7 +286,9 @@ struct kss_ctx {
   bool axis_meta_dirty = false;  // meta_buf holds node-axis outcomes not yet copied to meta_host
   DevBuf axis_cv;
   int axis_max_blocks = 0;  // KSS_AXIS_BLOCKS: cap on the node-axis grid (tuning)
-  int axis_no_fold = 0;     // KSS_AXIS_NO_FOLD: timing experiment only, statistics not folded (wrong results)             // node-axis sharding: [5][N] per-row verdict + raw scores of the current pod
+  int axis_no_fold = 0;
+  std::vector<hipEvent_t> loop_ev;  // around each k_simple launch of the last batch
+  double last_loop_ms = 0;          // device time of the sequential-loop kernel(s) of the last batch     // KSS_AXIS_NO_FOLD: timing experiment only, statistics not folded (wrong results)             // node-axis sharding: [5][N] per-row verdict + raw scores of the current pod
 };
 
 namespace {
@@ -329,78 +373,35 @@ int validate(const kss_cluster* cl, const kss_podset* ps, int n) {
   return 0;
 }
 
-// One pod program as a position-independent blob for k_simple (kss_simple.cuh): the pod
-// record, then only the requirements / terms / ints it references, every offset rebased
-// into the blob.  Writes to dst when given; returns the blob size.
-size_t serialize_pod(const kss_podset* ps, int i, uint8_t* dst) {
-  const kss_pod& src = ps->pods[i];
-  kss_pod q = src;
-  std::vector<kss_req> R;
-  std::vector<kss_term> T;
-  std::vector<int32_t> I;
-  auto add_req = [&](const kss_req& r0) {
-    kss_req r = r0;
-    if (r.op == KSS_OP_IN || r.op == KSS_OP_NOTIN) {
-      r.list_off = (int32_t)I.size();
-      I.insert(I.end(), ps->ints + r0.list_off, ps->ints + r0.list_off + r0.list_len);
-    }
-    R.push_back(r);
-  };
-  auto add_terms = [&](int off, int len) {
-    const int first = (int)T.size();
-    T.insert(T.end(), ps->terms + off, ps->terms + off + len);
-    for (int t = 0; t < len; t++) {
-      const kss_term& s0 = ps->terms[off + t];
-      T[first + t].req_off = (int32_t)R.size();
-      for (int k = 0; k < s0.req_len; k++) add_req(ps->reqs[s0.req_off + k]);
-    }
-    return first;
-  };
-  q.sel_off = 0;
-  for (int k = 0; k < src.sel_len; k++) add_req(ps->reqs[src.sel_off + k]);
-  q.aff_off = add_terms(src.aff_off, src.aff_len);
-  q.pref_off = add_terms(src.pref_off, src.pref_len);
-  if (src.names_len >= 0) {
-    q.names_off = (int32_t)I.size();
-    I.insert(I.end(), ps->ints + src.names_off, ps->ints + src.names_off + src.names_len);
-  }
-  q.own_terms_off = (int32_t)I.size();
-  I.insert(I.end(), ps->ints + src.own_terms_off, ps->ints + src.own_terms_off + src.own_terms_len);
-  q.spread_off = 0;
-  q.ipa_off = 0;
-  BlobHdr h{};
-  const size_t ro = blob_body_off(), to = ro + align_up(R.size() * sizeof(kss_req), 16),
-               io = to + align_up(T.size() * sizeof(kss_term), 16), end = io + align_up(I.size() * sizeof(int32_t), 16);
-  h.req_off = (int32_t)ro;
-  h.term_off = (int32_t)to;
-  h.ints_off = (int32_t)io;
-  h.n_reqs = (int32_t)R.size();
-  h.n_terms = (int32_t)T.size();
-  h.n_ints = (int32_t)I.size();
-  if (dst) {
-    memcpy(dst, &q, sizeof(q));
-    memcpy(dst + blob_hdr_off(), &h, sizeof(h));
-    if (!R.empty()) memcpy(dst + ro, R.data(), R.size() * sizeof(kss_req));
-    if (!T.empty()) memcpy(dst + to, T.data(), T.size() * sizeof(kss_term));
-    if (!I.empty()) memcpy(dst + io, I.data(), I.size() * sizeof(int32_t));
-  }
-  return end;
-}
-
-// Blobs of every pod of a (validated) podset at one stride; returns the stride, or 0 when
-// some pod needs k_schedule (spread / inter-pod programs, or a program over BLOB_MAX).
-int build_blobs(const kss_podset* ps, std::vector<uint8_t>& out) {
-  size_t mx = 16;
+// Compact records of every pod of a (validated) podset for k_simple (kss_simple.cuh
+// SPod); false when some pod needs k_schedule: spread / inter-pod-affinity programs, or
+// preferred NodeAffinity weights whose sum does not fit the static word's 16 bits.
+bool build_spods(const kss_podset* ps, int n_scalar, std::vector<SPod>& out) {
+  out.assign((size_t)std::max(ps->n_pods, 1), SPod{});
   for (int i = 0; i < ps->n_pods; i++) {
     const kss_pod& p = ps->pods[i];
-    if (p.n_hard | p.n_soft | p.ipa_len) return 0;
-    mx = std::max(mx, serialize_pod(ps, i, nullptr));
+    if (p.n_hard | p.n_soft | p.ipa_len) return false;
+    int64_t wsum = 0;
+    for (int t = 0; t < p.pref_len; t++) wsum += std::max(0, ps->terms[p.pref_off + t].weight);
+    if (wsum > 0xFFFF) return false;
+    SPod& q = out[(size_t)i];
+    bool all_zero = true;
+    for (int r = 0; r < 3 + n_scalar; r++) all_zero &= p.fit_request[r] == 0;
+    for (int r = 0; r < 3; r++) {
+      q.fit_req[r] = p.fit_request[r];
+      q.snz[r] = p.score_req_nz[r];
+      q.sreq[r] = p.score_req[r];
+      q.creq[r] = p.commit_req[r];
+    }
+    q.cnz[0] = p.commit_nz[0];
+    q.cnz[1] = p.commit_nz[1];
+    q.flags = all_zero ? SP_ALLZERO : 0;
+    q.status = p.prefilter_status;
+    q.cls = p.cls;
+    q.own_off = p.own_terms_off;
+    q.own_len = p.own_terms_len;
   }
-  const size_t stride = align_up(mx, 64);
-  if (stride > (size_t)BLOB_MAX) return 0;
-  out.assign(stride * (size_t)std::max(ps->n_pods, 1), 0);
-  for (int i = 0; i < ps->n_pods; i++) serialize_pod(ps, i, out.data() + stride * (size_t)i);
-  return (int)stride;
+  return true;
 }
 
 struct ClusterLayout {
@@ -616,11 +617,13 @@ void kss_destroy(kss_ctx* ctx) {
   ctx->meta_buf.release();
   ctx->chosen_buf.release();
   ctx->job_buf.release();
-  ctx->blob_buf.release();
+  ctx->spod_buf.release();
+  ctx->stat_buf.release();
   ctx->stamp_buf.release();
   ctx->gran_buf.release();
   ctx->err_buf.release();
   ctx->axis_cv.release();
+  for (hipEvent_t e : ctx->loop_ev) hipEventDestroy(e);
   if (ctx->ev0) hipEventDestroy(ctx->ev0);
   if (ctx->ev1) hipEventDestroy(ctx->ev1);
   if (ctx->stream) hipStreamDestroy(ctx->stream);
@@ -977,33 +980,68 @@ static bool same_profile(const kss_profile& a, const kss_profile& b) {
   return eq;
 }
 
-// Node slots per shard for k_simple: every lane's share, plus one spare slot when it
-// fits (the spare slot re-evaluates the candidate node in the same pass).
+// Node slots per shard for k_simple: every lane's share (the first slot without a node
+// re-evaluates the candidate after the previous commit).
 static int simple_cap(const Geometry& g) { return g.npt * g.threads; }
 
-// Launch k_simple (same grid and co-residency rule as k_schedule).
-static int launch_simple(hipStream_t st, const Geometry& g, int n_jobs, int stride, int n_keys, const DevJob* jobs,
-                         const kss_profile& prof, unsigned long long* gran, int* err,
-                         unsigned long long* stamps = nullptr) {
+static bool simple_fits(const Geometry& g) {
+  return g.W <= 64 * SX_CHUNKS && g.npt <= KSS_MAX_NPT && simple_lds_bytes(simple_cap(g)) <= KSS_LDS_BUDGET;
+}
+
+// Static-word scratch bound (KSS_STATIC_BYTES): pods are processed in chunks whose words
+// fit; each chunk is one k_static launch and one k_simple launch (node state stays in HBM
+// between them).  1 GiB covers C2 (5,000 x 10,000 x 4 B = 200 MB) in one chunk.
+static size_t static_budget() {
+  const char* e = getenv("KSS_STATIC_BYTES");
+  const long long v = e ? atoll(e) : 0;
+  return v > 0 ? (size_t)v : ((size_t)1 << 30);
+}
+
+// Pods per chunk for jobs whose node counts sum to sum_nodes.
+static int static_chunk(size_t sum_nodes, int n_pods) {
+  const size_t per_pod = 4 * std::max<size_t>(sum_nodes, 1);
+  const size_t c = std::max<size_t>(1, static_budget() / per_pod);
+  return (int)std::min<size_t>(c, (size_t)std::max(n_pods, 1));
+}
+
+// k_static + k_simple over pods [0, n_pods_max) of n_jobs jobs, `chunk` pods at a time.
+// The jobs' stat pointers must hold chunk x N words each.  Every polled granule is zeroed
+// before each k_simple launch (epochs restart at 1).
+// ev (optional): 2 events per chunk recorded around each k_simple launch.
+static int launch_simple(hipStream_t st, const Geometry& g, int n_jobs, const DevJob* jobs, const kss_profile& prof,
+                         int n_pods_max, int max_nodes, int chunk, unsigned long long* gran, size_t gran_bytes, int* err,
+                         unsigned long long* stamps = nullptr, hipEvent_t* ev = nullptr) {
   int cap = simple_cap(g);
-  const size_t shmem = simple_lds_bytes(stride, n_keys, cap);
+  const size_t shmem = simple_lds_bytes(cap);
   const bool def = same_profile(prof, default_profile_c());
   const void* fn = def ? (const void*)k_simple<true> : (const void*)k_simple<false>;
   HIP_TRY(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shmem));
   const dim3 grid((unsigned)(n_jobs * g.W)), block((unsigned)g.threads);
   kss_profile pr = prof;
   int W = g.W;
-  void* args[] = {(void*)&jobs, (void*)&pr, (void*)&W, (void*)&cap, (void*)&gran, (void*)&err, (void*)&stamps};
-  if (g.W > 1) {
-    if (int rc = launch_resident(fn, grid, block, args, shmem, st)) return rc;
+  for (int k0 = 0; k0 < n_pods_max; k0 += chunk) {
+    int k1 = std::min(n_pods_max, k0 + chunk);
+    const dim3 sgrid((unsigned)((max_nodes + 255) / 256), (unsigned)((k1 - k0 + STATIC_PODS - 1) / STATIC_PODS),
+                     (unsigned)n_jobs);
+    if (def)
+      hipLaunchKernelGGL(k_static<true>, sgrid, dim3(256), 0, st, jobs, pr, k0, k1);
+    else
+      hipLaunchKernelGGL(k_static<false>, sgrid, dim3(256), 0, st, jobs, pr, k0, k1);
+    HIP_TRY(hipGetLastError());
+    if (gran && k0 > 0) HIP_TRY(hipMemsetAsync(gran, 0, gran_bytes, st));
+    unsigned long long* sp = k0 == 0 ? stamps : nullptr;
+    void* args[] = {(void*)&jobs, (void*)&pr, (void*)&W, (void*)&cap, (void*)&k0, (void*)&k1,
+                    (void*)&gran, (void*)&err, (void*)&sp};
+    const int ci = k0 / chunk;
+    if (ev) HIP_TRY(hipEventRecord(ev[2 * ci], st));
+    if (g.W > 1) {
+      if (int rc = launch_resident(fn, grid, block, args, shmem, st)) return rc;
+    } else {
+      HIP_TRY(hipLaunchKernel(fn, grid, block, args, shmem, st));
+    }
+    if (ev) HIP_TRY(hipEventRecord(ev[2 * ci + 1], st));
   }
-  else HIP_TRY(hipLaunchKernel(fn, grid, block, args, shmem, st));
   return 0;
-}
-
-static bool simple_fits(const Geometry& g, int stride, int n_keys) {
-  return stride > 0 && stride <= 32 * g.threads && g.W <= 64 * SX_CHUNKS &&
-         simple_lds_bytes(stride, n_keys, simple_cap(g)) <= KSS_LDS_BUDGET;
 }
 
 // run k_schedule / k_simple on the loaded cluster for pods [0, n); results stay on the device
@@ -1027,7 +1065,7 @@ static int run_single(kss_ctx* ctx, const PlanNeeds& need, const DevPods& dp, in
   // a k_simple-eligible batch keeps W within k_simple's exchange sweep (64 * SX_CHUNKS
   // shards): at 100k nodes, 98-128 k_simple shards beat 256 k_schedule shards (69.8k
   // against 44.2k pods/s)
-  const bool simple_ok = staged && ctx->blob_stride && commit && !record && !keep_norm && !need.general &&
+  const bool simple_ok = staged && ctx->spod_ok && commit && !record && !keep_norm && !need.general &&
                          ctx->dc.n_scalar == 0 && ctx->small_values && !ctx->no_simple && !(flags & KSS_SCHED_GENERAL_KERNEL);
   if (simple_ok && ctx->force_w <= 0) W = std::min(W, 64 * SX_CHUNKS);
   const int w_min = (int)((N + KSS_MAX_NPT * KSS_MAX_THREADS - 1) / (KSS_MAX_NPT * KSS_MAX_THREADS));
@@ -1039,6 +1077,9 @@ static int run_single(kss_ctx* ctx, const PlanNeeds& need, const DevPods& dp, in
   if (W > ctx->n_cu) return fail(KSS_E_UNSUPPORTED, "cluster too large for one device");
   Geometry g;
   if (!pick_geometry((int)N, W, ctx->pref_threads, g)) return fail(KSS_E_UNSUPPORTED, "no geometry for this cluster");
+  const bool simple = simple_ok && simple_fits(g);
+  const int chunk = simple ? static_chunk(N, n) : 0;
+  if (simple && (rc = ctx->stat_buf.ensure(sizeof(uint32_t) * (size_t)chunk * std::max<size_t>(N, 1)))) return rc;
   DevJob job{};
   job.c = ctx->dc;
   job.P = dp;
@@ -1050,16 +1091,16 @@ static int run_single(kss_ctx* ctx, const PlanNeeds& need, const DevPods& dp, in
   job.slot_bytes = SL.bytes;
   job.chosen = (int32_t*)ctx->chosen_buf.p;
   job.meta = (PodMeta*)ctx->meta_buf.p;
-  job.blobs = staged && ctx->blob_stride ? (const uint8_t*)ctx->blob_buf.p : nullptr;
-  job.blob_stride = ctx->blob_stride;
-  const bool simple = job.blobs && simple_ok && simple_fits(g, ctx->blob_stride, ctx->dc.n_keys);
+  job.spods = simple ? (const SPod*)ctx->spod_buf.p : nullptr;
+  job.stat = simple ? (uint32_t*)ctx->stat_buf.p : nullptr;
+  job.prof = ctx->prof;
   rc = ctx->job_buf.ensure(sizeof(DevJob));
   if (rc) return rc;
   rc = ctx->err_buf.ensure(16);
   if (rc) return rc;
   unsigned long long* gran = nullptr;
+  const size_t gb = sizeof(unsigned long long) * 2 * (size_t)g.W * 2 * XW_MAX;
   if (g.W > 1) {
-    const size_t gb = sizeof(unsigned long long) * 2 * (size_t)g.W * 2 * XW_MAX;
     rc = ctx->gran_buf.ensure(gb);
     if (rc) return rc;
     gran = (unsigned long long*)ctx->gran_buf.p;
@@ -1075,9 +1116,15 @@ static int run_single(kss_ctx* ctx, const PlanNeeds& need, const DevPods& dp, in
     stamps = (unsigned long long*)ctx->stamp_buf.p;
     HIP_TRY(hipMemsetAsync(stamps, 0, stamp_bytes, ctx->stream));
   }
+  const int n_chunks = simple ? (n + chunk - 1) / std::max(chunk, 1) : 0;
+  while ((int)ctx->loop_ev.size() < 2 * n_chunks) {
+    hipEvent_t e;
+    HIP_TRY(hipEventCreate(&e));
+    ctx->loop_ev.push_back(e);
+  }
   if (simple)
-    rc = launch_simple(ctx->stream, g, 1, ctx->blob_stride, ctx->dc.n_keys, (const DevJob*)ctx->job_buf.p, ctx->prof, gran,
-                       (int*)ctx->err_buf.p, stamps);
+    rc = launch_simple(ctx->stream, g, 1, (const DevJob*)ctx->job_buf.p, ctx->prof, n, (int)N, chunk, gran, gb,
+                       (int*)ctx->err_buf.p, stamps, ctx->loop_ev.data());
   else
     rc = launch_schedule(ctx->stream, g, 1, std::max(need.bins_cap, 0), need.general, ctx->dc.n_keys,
                          (const DevJob*)ctx->job_buf.p, ctx->prof, gran, (int*)ctx->err_buf.p, stamps);
@@ -1088,7 +1135,13 @@ static int run_single(kss_ctx* ctx, const PlanNeeds& need, const DevPods& dp, in
   float ms = 0;
   HIP_TRY(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
   ctx->last_ms = ms;
-  ctx->last_launches = 1;
+  ctx->last_launches = simple ? 2 * n_chunks : 1;
+  ctx->last_loop_ms = simple ? 0.0 : ms;
+  for (int i = 0; i < n_chunks; i++) {
+    float t = 0;
+    HIP_TRY(hipEventElapsedTime(&t, ctx->loop_ev[2 * i], ctx->loop_ev[2 * i + 1]));
+    ctx->last_loop_ms += t;
+  }
   ctx->last_geom[0] = g.W;
   ctx->last_geom[1] = g.threads;
   ctx->last_geom[2] = g.npt;
@@ -1112,13 +1165,14 @@ static int run_single(kss_ctx* ctx, const PlanNeeds& need, const DevPods& dp, in
   return 0;
 }
 
-// serialize the staged podset for k_simple (host copy kept alive for the async upload)
-static int stage_blobs(kss_ctx* ctx, const kss_podset* ps) {
-  ctx->blob_stride = build_blobs(ps, ctx->blob_host);
-  if (!ctx->blob_stride) return 0;
-  int rc = ctx->blob_buf.ensure(ctx->blob_host.size());
+// compact records of the staged podset for k_simple (host copy kept alive for the async upload)
+static int stage_spods(kss_ctx* ctx, const kss_podset* ps) {
+  ctx->spod_ok = build_spods(ps, ctx->dc.n_scalar, ctx->spod_host);
+  if (!ctx->spod_ok) return 0;
+  int rc = ctx->spod_buf.ensure(sizeof(SPod) * ctx->spod_host.size());
   if (rc) return rc;
-  HIP_TRY(hipMemcpyAsync(ctx->blob_buf.p, ctx->blob_host.data(), ctx->blob_host.size(), hipMemcpyHostToDevice, ctx->stream));
+  HIP_TRY(hipMemcpyAsync(ctx->spod_buf.p, ctx->spod_host.data(), sizeof(SPod) * ctx->spod_host.size(),
+                         hipMemcpyHostToDevice, ctx->stream));
   return 0;
 }
 
@@ -1206,7 +1260,7 @@ int kss_schedule_batch(kss_ctx* ctx, const kss_podset* ps, int32_t n, uint32_t f
   HIP_TRY(hipSetDevice(ctx->cfg.device));
   rc = upload_podset(ctx->stream, ctx->pod_buf, ps, ctx->dp);
   if (rc) return rc;
-  if ((rc = stage_blobs(ctx, ps))) return rc;
+  if ((rc = stage_spods(ctx, ps))) return rc;
   ctx->staged_n = ps->n_pods;
   ctx->staged_need = plan_needs(ctx->key_card_h.data(), ctx->key_flags_h.data(), ps, ps->n_pods);
   rc = run_single(ctx, ctx->staged_need, ctx->dp, n, /*commit=*/true, record, /*keep_norm=*/record, flags, chosen_out,
@@ -1225,7 +1279,7 @@ int kss_stage_pods(kss_ctx* ctx, const kss_podset* ps) {
   HIP_TRY(hipSetDevice(ctx->cfg.device));
   rc = upload_podset(ctx->stream, ctx->pod_buf, ps, ctx->dp);
   if (rc) return rc;
-  if ((rc = stage_blobs(ctx, ps))) return rc;
+  if ((rc = stage_spods(ctx, ps))) return rc;
   HIP_TRY(hipStreamSynchronize(ctx->stream));
   ctx->staged_n = ps->n_pods;
   ctx->staged_need = plan_needs(ctx->key_card_h.data(), ctx->key_flags_h.data(), ps, ps->n_pods);
@@ -1262,6 +1316,12 @@ int kss_last_timing(kss_ctx* ctx, double* device_ms, int32_t* launches) {
   return 0;
 }
 
+int kss_last_loop_timing(kss_ctx* ctx, double* loop_ms) {
+  if (!ctx || !loop_ms) return fail(KSS_E_INVAL, "bad arguments");
+  *loop_ms = ctx->last_loop_ms;
+  return 0;
+}
+
 int kss_last_geometry(kss_ctx* ctx, int32_t* out3) {
   if (!ctx || !out3) return fail(KSS_E_INVAL, "bad arguments");
   for (int i = 0; i < 3; i++) out3[i] = ctx->last_geom[i];
@@ -1295,187 +1355,319 @@ int kss_fetch_meta(kss_ctx* ctx, int32_t first, int32_t n, int64_t* out) {
   return 0;
 }
 
+// ---------------------------------------------------------------------------
+// what-if scenario sweeps (KEP-184; BASELINE C5): many independent clusters, one
+// workgroup each, no inter-scenario communication.  kss_sweep_create packs every input
+// into one host image and uploads it with ONE copy; kss_sweep_run restores the node
+// state from the uploaded pristine copy (one device copy) and schedules every scenario.
+// ---------------------------------------------------------------------------
+}  // extern "C"
+
+namespace {
+
+// Bump allocator over one host image / device arena pair (offsets 256-B aligned).  With
+// h == nullptr it only sizes.
+struct Packer {
+  char* h = nullptr;
+  char* d = nullptr;
+  size_t o = 0, last = 0;
+  template <class T>
+  T* put(const T* src, size_t count, size_t reserve = 0) {
+    const size_t n = std::max(std::max(count, reserve), (size_t)1);
+    last = o;
+    o = align_up(o + sizeof(T) * n, 256);
+    if (h) {
+      const size_t done = src ? sizeof(T) * count : 0;
+      if (done) memcpy(h + last, src, done);
+      if (sizeof(T) * n > done) memset(h + last + done, 0, sizeof(T) * n - done);
+    }
+    return reinterpret_cast<T*>(d + last);
+  }
+};
+
+// The read-only part of one scenario: cluster columns except the mutable ones, the pod
+// programs and (simple sweeps) the compact pod records.
+void pack_inputs(Packer& P, const kss_cluster* cl, const kss_podset* ps, const std::vector<SPod>* spods, DevJob& j) {
+  const size_t N = (size_t)cl->n_nodes, K = (size_t)cl->n_label_keys;
+  DevCluster& c = j.c;
+  c.N = cl->n_nodes;
+  c.n_scalar = cl->n_scalar;
+  c.n_keys = cl->n_label_keys;
+  c.n_classes = cl->n_classes;
+  c.n_terms = cl->n_terms;
+  c.node_base = cl->node_base;
+  c.class_cap = cl->n_classes;
+  c.term_cap = cl->n_terms;
+  c.alloc = P.put(cl->alloc, KSS_NRES * N);
+  c.allowed_pods = P.put(cl->allowed_pods, N);
+  c.node_flags = P.put(cl->node_flags, N);
+  c.taint_hard = P.put(cl->taint_hard, N);
+  c.taint_soft = P.put(cl->taint_soft, N);
+  c.taint_order = P.put(cl->taint_order, (size_t)KSS_TAINT_ORDER * N);
+  c.label_value = P.put(cl->label_value, K * N);
+  c.key_base = P.put(cl->key_base, K);
+  c.key_card = P.put(cl->key_card, K);
+  c.key_flags = P.put(cl->key_flags, K);
+  c.key_empty = P.put(cl->key_empty, K);
+  c.value_int = P.put(cl->value_int, (size_t)cl->n_label_values);
+  c.value_is_int = P.put(cl->value_is_int, (size_t)cl->n_label_values);
+  c.log_table = P.put<double>(nullptr, N + 3);
+  if (P.h) {
+    double* lt = reinterpret_cast<double*>(P.h + P.last);
+    for (size_t k = 0; k < N + 3; k++) lt[k] = kss_go_log((double)(k + 2));
+  }
+  c.nc64 = nullptr;
+  c.nct = nullptr;
+  c.nc32 = nullptr;
+  c.ncl = nullptr;
+  j.P.pods = P.put(ps->pods, (size_t)ps->n_pods);
+  j.P.reqs = P.put(ps->reqs, (size_t)ps->n_reqs);
+  j.P.terms = P.put(ps->terms, (size_t)ps->n_terms);
+  j.P.spreads = P.put(ps->spreads, (size_t)ps->n_spreads);
+  j.P.ipa = P.put(ps->ipa, (size_t)ps->n_ipa);
+  j.P.ints = P.put(ps->ints, (size_t)ps->n_ints);
+  j.spods = spods ? P.put(spods->data(), spods->size()) : nullptr;
+}
+
+// The mutable columns of one scenario (AssumePod targets): the host image holds the
+// snapshot (the device's pristine copy); the device pointers address the live copy.
+void pack_mutable(Packer& P, const kss_cluster* cl, DevJob& j) {
+  const size_t N = (size_t)cl->n_nodes;
+  j.c.requested = P.put(cl->requested, KSS_NRES * N);
+  j.c.nonzero = P.put(cl->nonzero, 2 * N);
+  j.c.pod_count = P.put(cl->pod_count, N);
+  j.c.class_count = P.put(cl->class_count, (size_t)cl->n_classes * N);
+  j.c.term_count = P.put(cl->term_count, (size_t)cl->n_terms * N);
+}
+
+}  // namespace
+
+struct kss_sweep {
+  int device = 0;
+  kss_profile prof{};
+  int n_scen = 0;
+  hipStream_t st = nullptr;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  char* arena = nullptr;
+  size_t up_bytes = 0;                   // [0, up_bytes): uploaded once (inputs, pristine state, jobs)
+  size_t pristine_off = 0, live_off = 0, mut_bytes = 0;
+  size_t chosen_off = 0, meta_off = 0, err_off = 0, gran_off = 0, gran_bytes = 0, stat_off = 0, jobs_off = 0;
+  std::vector<int32_t> n_pods;
+  int total_pods = 0, max_pods = 0, max_nodes = 0, max_keys = 0;
+  bool simple = false;
+  int chunk = 0;
+  Geometry g;
+  PlanNeeds need;
+  double stage_ms = 0;
+  ~kss_sweep() {
+    if (st) hipStreamSynchronize(st);
+    if (arena) hipFree(arena);
+    if (e0) hipEventDestroy(e0);
+    if (e1) hipEventDestroy(e1);
+    if (st) hipStreamDestroy(st);
+  }
+};
+
+extern "C" {
+
+kss_sweep* kss_sweep_create(int32_t device, const kss_profile* prof, int32_t n_scen, const kss_cluster* clusters,
+                            const kss_podset* podsets) {
+  if (!prof || n_scen <= 0 || !clusters || !podsets) {
+    fail(KSS_E_INVAL, "bad arguments");
+    return nullptr;
+  }
+  if (check_profile(prof)) return nullptr;
+  for (int s = 0; s < n_scen; s++)
+    if (check_cluster(&clusters[s]) || validate(&clusters[s], &podsets[s], podsets[s].n_pods)) return nullptr;
+  const auto t0 = std::chrono::steady_clock::now();
+  std::unique_ptr<kss_sweep> sw(new kss_sweep());
+  sw->device = device;
+  sw->prof = *prof;
+  sw->n_scen = n_scen;
+  sw->n_pods.resize(n_scen);
+  for (int s = 0; s < n_scen; s++) {
+    sw->n_pods[s] = podsets[s].n_pods;
+    sw->total_pods += podsets[s].n_pods;
+    sw->max_pods = std::max(sw->max_pods, podsets[s].n_pods);
+    sw->max_nodes = std::max(sw->max_nodes, clusters[s].n_nodes);
+    sw->max_keys = std::max(sw->max_keys, clusters[s].n_label_keys);
+    const PlanNeeds q = plan_needs(clusters[s].key_card, clusters[s].key_flags, &podsets[s], podsets[s].n_pods);
+    sw->need.bins_cap = std::max(sw->need.bins_cap, q.bins_cap);
+    sw->need.general |= q.general;
+  }
+  // one workgroup per scenario: at most two node slots per lane (C5, 1,000 nodes: 512
+  // threads ran the 512-scenario sweep in 16.5 ms against 23.7 ms at 256)
+  int pref = sw->max_nodes > 512 ? 512 : 256;
+  if (const char* e = getenv("KSS_THREADS")) pref = std::min(KSS_MAX_THREADS, std::max(64, atoi(e)));
+  if (!pick_geometry(sw->max_nodes, 1, pref, sw->g)) {
+    fail(KSS_E_UNSUPPORTED, "scenario cluster too large for one workgroup");
+    return nullptr;
+  }
+  // k_static + k_simple for the whole sweep when every scenario qualifies (no spread /
+  // inter-pod programs, no scalar resources, values inside the exact f64 envelope)
+  std::vector<std::vector<SPod>> spods(n_scen);
+  bool simple = getenv("KSS_NO_SIMPLE") == nullptr && !sw->need.general && simple_fits(sw->g);
+  for (int i = 0; i < prof->fit_n && simple; i++) simple = prof->fit_weight[i] >= 0 && prof->fit_weight[i] < (1ll << 20);
+  for (int s = 0; s < n_scen && simple; s++) {
+    const kss_cluster& cl = clusters[s];
+    simple = cl.n_scalar == 0;
+    for (size_t i = 0; i < 3 * (size_t)cl.n_nodes && simple; i++) simple = cl.alloc[i] >= 0 && cl.alloc[i] < (1ll << 46);
+    if (simple) simple = build_spods(&podsets[s], 0, spods[s]);
+  }
+  sw->simple = simple;
+  // layout: [inputs][pristine state][jobs] uploaded; [live state][chosen][meta][err][gran][stat]
+  std::vector<DevJob> jobs(n_scen);
+  std::vector<size_t> in_off(n_scen), mut_off(n_scen);
+  Packer dry;
+  for (int s = 0; s < n_scen; s++) {
+    in_off[s] = dry.o;
+    pack_inputs(dry, &clusters[s], &podsets[s], simple ? &spods[s] : nullptr, jobs[s]);
+  }
+  sw->pristine_off = dry.o;
+  for (int s = 0; s < n_scen; s++) {
+    mut_off[s] = dry.o;
+    pack_mutable(dry, &clusters[s], jobs[s]);
+  }
+  sw->mut_bytes = dry.o - sw->pristine_off;
+  sw->jobs_off = dry.o;
+  dry.put<DevJob>(nullptr, (size_t)n_scen);
+  sw->up_bytes = dry.o;
+  sw->live_off = dry.o;
+  dry.o = align_up(dry.o + sw->mut_bytes, 256);
+  dry.put<int32_t>(nullptr, (size_t)sw->total_pods);
+  sw->chosen_off = dry.last;
+  dry.put<PodMeta>(nullptr, (size_t)sw->total_pods);
+  sw->meta_off = dry.last;
+  dry.put<int32_t>(nullptr, 4);
+  sw->err_off = dry.last;
+  size_t sum_nodes = 0;
+  for (int s = 0; s < n_scen; s++) sum_nodes += (size_t)clusters[s].n_nodes;
+  sw->chunk = simple ? static_chunk(sum_nodes, sw->max_pods) : 0;
+  if (simple) {
+    dry.put<uint32_t>(nullptr, (size_t)sw->chunk * sum_nodes);
+    sw->stat_off = dry.last;
+  }
+  const size_t total = dry.o;
+  if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&sw->st, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreate(&sw->e0) != hipSuccess || hipEventCreate(&sw->e1) != hipSuccess) {
+    fail(KSS_E_DEVICE, "stream/event creation failed");
+    return nullptr;
+  }
+  if (hipMalloc(&sw->arena, total) != hipSuccess) {
+    sw->arena = nullptr;
+    fail(KSS_E_NOMEM, "scenario arena allocation failed");
+    return nullptr;
+  }
+  // host image of [0, up_bytes), packed by scenario in parallel, then one upload
+  std::unique_ptr<char[]> img(new (std::nothrow) char[sw->up_bytes]);
+  if (!img) {
+    fail(KSS_E_NOMEM, "host staging allocation failed");
+    return nullptr;
+  }
+  const int nth = std::max(1, std::min<int>(16, (int)std::thread::hardware_concurrency()));
+  auto work = [&](int t) {
+    for (int s = t; s < n_scen; s += nth) {
+      Packer P{img.get(), sw->arena, in_off[s]};
+      pack_inputs(P, &clusters[s], &podsets[s], simple ? &spods[s] : nullptr, jobs[s]);
+      // host bytes at the pristine position, device pointers at the live position
+      Packer M{img.get(), sw->arena + (sw->live_off - sw->pristine_off), mut_off[s]};
+      pack_mutable(M, &clusters[s], jobs[s]);
+      DevJob& j = jobs[s];
+      j.n_pods = podsets[s].n_pods;
+      j.commit = 1;
+      j.keep_norm = 0;
+      j.record = 0;
+      j.prof = *prof;
+      j.slots = nullptr;  // no per-node records in a sweep (record = keep_norm = 0)
+      j.slot_bytes = 0;
+      j.stat = nullptr;
+    }
+  };
+  std::vector<std::thread> th;
+  for (int t = 1; t < nth; t++) th.emplace_back(work, t);
+  work(0);
+  for (auto& x : th) x.join();
+  size_t o_chosen = 0, o_stat = 0;
+  for (int s = 0; s < n_scen; s++) {
+    jobs[s].chosen = reinterpret_cast<int32_t*>(sw->arena + sw->chosen_off) + o_chosen;
+    jobs[s].meta = reinterpret_cast<PodMeta*>(sw->arena + sw->meta_off) + o_chosen;
+    o_chosen += (size_t)podsets[s].n_pods;
+    if (simple) {
+      jobs[s].stat = reinterpret_cast<uint32_t*>(sw->arena + sw->stat_off) + o_stat;
+      o_stat += (size_t)sw->chunk * (size_t)clusters[s].n_nodes;
+    }
+  }
+  memcpy(img.get() + sw->jobs_off, jobs.data(), sizeof(DevJob) * n_scen);
+  if (hipMemcpy(sw->arena, img.get(), sw->up_bytes, hipMemcpyHostToDevice) != hipSuccess) {
+    fail(KSS_E_DEVICE, "sweep upload failed");
+    return nullptr;
+  }
+  sw->stage_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  return sw.release();
+}
+
+int kss_sweep_run(kss_sweep* sw, int32_t* chosen_out, double* device_ms) {
+  if (!sw || (sw->total_pods && !chosen_out)) return fail(KSS_E_INVAL, "bad arguments");
+  HIP_TRY(hipSetDevice(sw->device));
+  hipStream_t st = sw->st;
+  HIP_TRY(hipEventRecord(sw->e0, st));
+  // every run starts from the snapshot: one device copy of all scenarios' mutable columns
+  HIP_TRY(hipMemcpyAsync(sw->arena + sw->live_off, sw->arena + sw->pristine_off, sw->mut_bytes, hipMemcpyDeviceToDevice, st));
+  int* err = reinterpret_cast<int*>(sw->arena + sw->err_off);
+  HIP_TRY(hipMemsetAsync(err, 0, 16, st));
+  const DevJob* jobs = reinterpret_cast<const DevJob*>(sw->arena + sw->jobs_off);
+  int rc;
+  if (sw->simple)
+    rc = launch_simple(st, sw->g, sw->n_scen, jobs, sw->prof, sw->max_pods, sw->max_nodes, sw->chunk, nullptr, 0, err);
+  else
+    rc = launch_schedule(st, sw->g, sw->n_scen, sw->need.bins_cap, sw->need.general, sw->max_keys, jobs, sw->prof,
+                         nullptr, err);
+  if (rc) return rc;
+  HIP_TRY(hipEventRecord(sw->e1, st));
+  if (sw->total_pods)
+    HIP_TRY(hipMemcpyAsync(chosen_out, sw->arena + sw->chosen_off, sizeof(int32_t) * sw->total_pods,
+                           hipMemcpyDeviceToHost, st));
+  std::vector<PodMeta> m((size_t)std::max(sw->total_pods, 1));
+  if (sw->total_pods)
+    HIP_TRY(hipMemcpyAsync(m.data(), sw->arena + sw->meta_off, sizeof(PodMeta) * sw->total_pods, hipMemcpyDeviceToHost, st));
+  int errw = 0;
+  HIP_TRY(hipMemcpyAsync(&errw, err, sizeof(int), hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  float ms = 0;
+  HIP_TRY(hipEventElapsedTime(&ms, sw->e0, sw->e1));
+  if (device_ms) *device_ms = ms;
+  if (errw) return fail(KSS_E_DEVICE, "scenario launch aborted");
+  // a pod whose program exceeds the device limits (status 4) fails the call instead of
+  // looking unschedulable
+  for (int i = 0; i < sw->total_pods; i++)
+    if (m[i].status == 4) return fail(KSS_E_UNSUPPORTED, "pod program exceeds the device path's per-pod limits");
+  return 0;
+}
+
+int kss_sweep_info(kss_sweep* sw, double* stage_ms, int32_t* kernel, int64_t* upload_bytes) {
+  if (!sw) return fail(KSS_E_INVAL, "null sweep");
+  if (stage_ms) *stage_ms = sw->stage_ms;
+  if (kernel) *kernel = sw->simple ? 1 : 0;
+  if (upload_bytes) *upload_bytes = (int64_t)sw->up_bytes;
+  return 0;
+}
+
+void kss_sweep_destroy(kss_sweep* sw) {
+  if (!sw) return;
+  hipSetDevice(sw->device);
+  delete sw;
+}
+
 int kss_schedule_scenarios(int32_t device, const kss_profile* prof, int32_t n_scen, const kss_cluster* clusters,
                            const kss_podset* podsets, int32_t* chosen_out, double* device_ms) {
   if (!prof || n_scen < 0 || (n_scen && (!clusters || !podsets || !chosen_out))) return fail(KSS_E_INVAL, "bad arguments");
   int rc = check_profile(prof);
   if (rc) return rc;
   if (n_scen == 0) return 0;
-  for (int s = 0; s < n_scen; s++) {
-    if ((rc = check_cluster(&clusters[s]))) return rc;
-    if ((rc = validate(&clusters[s], &podsets[s], podsets[s].n_pods))) return rc;
-  }
-  HIP_TRY(hipSetDevice(device));
-  hipStream_t st;
-  HIP_TRY(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
-  // one device arena: clusters, podsets, scratch slots, chosen, jobs
-  std::vector<size_t> c_off(n_scen), p_off(n_scen), s_off(n_scen), ch_off(n_scen);
-  std::vector<ClusterLayout> layouts;
-  layouts.reserve(n_scen);
-  size_t total = 0;
-  for (int s = 0; s < n_scen; s++) {
-    layouts.emplace_back(&clusters[s], clusters[s].n_classes, clusters[s].n_terms);
-    c_off[s] = total;
-    total = align_up(total + layouts[s].total, 256);
-  }
-  std::vector<size_t> pod_bytes(n_scen);
-  for (int s = 0; s < n_scen; s++) {
-    const kss_podset& ps = podsets[s];
-    size_t b = 0;
-    b = align_up(b + sizeof(kss_pod) * std::max(ps.n_pods, 1), 256);
-    b = align_up(b + sizeof(kss_req) * std::max(ps.n_reqs, 1), 256);
-    b = align_up(b + sizeof(kss_term) * std::max(ps.n_terms, 1), 256);
-    b = align_up(b + sizeof(kss_spread) * std::max(ps.n_spreads, 1), 256);
-    b = align_up(b + sizeof(kss_ipa) * std::max(ps.n_ipa, 1), 256);
-    b = align_up(b + sizeof(int32_t) * std::max(ps.n_ints, 1), 256);
-    pod_bytes[s] = b;
-    p_off[s] = total;
-    total = align_up(total + b, 256);
-  }
-  for (int s = 0; s < n_scen; s++) {
-    s_off[s] = total;
-    total = align_up(total + SlotLayout((size_t)clusters[s].n_nodes).bytes, 256);
-  }
-  for (int s = 0; s < n_scen; s++) {
-    ch_off[s] = total;
-    total = align_up(total + sizeof(int32_t) * std::max(podsets[s].n_pods, 1), 256);
-  }
-  // per-pod outcomes: a pod whose program exceeds the device limits (status 4) fails the
-  // call with KSS_E_UNSUPPORTED instead of looking unschedulable
-  std::vector<size_t> m_off(n_scen);
-  for (int s = 0; s < n_scen; s++) {
-    m_off[s] = total;
-    total = align_up(total + sizeof(PodMeta) * std::max(podsets[s].n_pods, 1), 256);
-  }
-  const size_t job_off = total;
-  total = align_up(total + sizeof(DevJob) * n_scen, 256);
-  // k_simple for the whole sweep when every scenario qualifies (no spread / inter-pod
-  // programs, no scalar resources, values inside the exact f64 envelope): pod programs
-  // as blobs at one common stride, one workgroup per scenario
-  bool simple = getenv("KSS_NO_SIMPLE") == nullptr;
-  for (int i = 0; i < prof->fit_n && simple; i++) simple = prof->fit_weight[i] >= 0 && prof->fit_weight[i] < (1ll << 20);
-  size_t blob_mx = 16;
-  for (int sc = 0; sc < n_scen && simple; sc++) {
-    const kss_cluster& cl = clusters[sc];
-    simple = cl.n_scalar == 0;
-    for (size_t i = 0; i < 3 * (size_t)cl.n_nodes && simple; i++) simple = cl.alloc[i] >= 0 && cl.alloc[i] < (1ll << 46);
-    for (int i = 0; i < podsets[sc].n_pods && simple; i++) {
-      const kss_pod& q = podsets[sc].pods[i];
-      simple = !(q.n_hard | q.n_soft | q.ipa_len);
-      if (simple) blob_mx = std::max(blob_mx, serialize_pod(&podsets[sc], i, nullptr));
-    }
-  }
-  const int blob_stride = simple && align_up(blob_mx, 64) <= (size_t)BLOB_MAX ? (int)align_up(blob_mx, 64) : 0;
-  std::vector<size_t> b_off(n_scen, 0);
-  if (blob_stride)
-    for (int sc = 0; sc < n_scen; sc++) {
-      b_off[sc] = total;
-      total = align_up(total + (size_t)blob_stride * std::max(podsets[sc].n_pods, 1), 256);
-    }
-  char* arena = nullptr;
-  if (hipMalloc(&arena, total) != hipSuccess) {
-    hipStreamDestroy(st);
-    return fail(KSS_E_NOMEM, "scenario arena allocation failed");
-  }
-  std::vector<DevJob> jobs(n_scen);
-  std::vector<std::vector<double>> logtabs(n_scen);
-  rc = 0;
-  for (int s = 0; s < n_scen && !rc; s++) {
-    DevJob& j = jobs[s];
-    rc = fill_cluster(st, &clusters[s], clusters[s].n_classes, clusters[s].n_terms, arena + c_off[s], layouts[s], j.c, logtabs[s]);
-    if (rc) break;
-    DevBuf view;
-    view.p = arena + p_off[s];
-    view.cap = pod_bytes[s];
-    rc = upload_podset(st, view, &podsets[s], j.P);
-    view.p = nullptr;
-    j.n_pods = podsets[s].n_pods;
-    j.commit = 1;
-    j.keep_norm = 0;
-    j.record = 0;
-    j.slots = (uint8_t*)(arena + s_off[s]);
-    j.slot_bytes = SlotLayout((size_t)clusters[s].n_nodes).bytes;
-    j.chosen = (int32_t*)(arena + ch_off[s]);
-    j.meta = (PodMeta*)(arena + m_off[s]);
-    j.blobs = nullptr;
-    j.blob_stride = 0;
-    if (blob_stride) {
-      std::vector<uint8_t> bl((size_t)blob_stride * std::max(podsets[s].n_pods, 1), 0);
-      for (int i = 0; i < podsets[s].n_pods; i++) serialize_pod(&podsets[s], i, bl.data() + (size_t)blob_stride * i);
-      if (hipMemcpy(arena + b_off[s], bl.data(), bl.size(), hipMemcpyHostToDevice) != hipSuccess)
-        rc = fail(KSS_E_DEVICE, "blob upload failed");
-      j.blobs = (const uint8_t*)(arena + b_off[s]);
-      j.blob_stride = blob_stride;
-    }
-    // the host-side log tables must stay alive until the copies finish
-    if (s % 256 == 255) {
-      if (hipStreamSynchronize(st) != hipSuccess) rc = fail(KSS_E_DEVICE, "upload failed");
-      for (int t = s - 255; t <= s; t++) std::vector<double>().swap(logtabs[t]);
-    }
-  }
-  hipEvent_t e0 = nullptr, e1 = nullptr;
-  if (!rc) {
-    if (hipMemcpyAsync(arena + job_off, jobs.data(), sizeof(DevJob) * n_scen, hipMemcpyHostToDevice, st) != hipSuccess ||
-        hipStreamSynchronize(st) != hipSuccess)
-      rc = fail(KSS_E_DEVICE, "job upload failed");
-  }
-  PlanNeeds need;
-  for (int sc = 0; sc < n_scen; sc++) {
-    const PlanNeeds q = plan_needs(clusters[sc].key_card, clusters[sc].key_flags, &podsets[sc], podsets[sc].n_pods);
-    need.bins_cap = std::max(need.bins_cap, q.bins_cap);
-    need.general |= q.general;
-  }
-  int maxN = 0;
-  for (int sc = 0; sc < n_scen; sc++) maxN = std::max(maxN, clusters[sc].n_nodes);
-  // one workgroup per scenario: at most two node slots per lane (C5, 1,000 nodes: 512
-  // threads ran the 512-scenario sweep in 16.5 ms against 23.7 ms at 256)
-  int pref = maxN > 512 ? 512 : 256;
-  if (const char* e = getenv("KSS_THREADS")) pref = std::min(KSS_MAX_THREADS, std::max(64, atoi(e)));
-  Geometry g;
-  if (!rc && !pick_geometry(maxN, 1, pref, g)) rc = fail(KSS_E_UNSUPPORTED, "scenario cluster too large for one workgroup");
-  int* err = nullptr;
-  if (!rc && hipMalloc(&err, 16) != hipSuccess) rc = fail(KSS_E_NOMEM, "error word allocation failed");
-  if (!rc) {
-    hipMemsetAsync(err, 0, 16, st);
-    hipEventCreate(&e0);
-    hipEventCreate(&e1);
-    hipEventRecord(e0, st);
-    int max_keys = 0;
-    for (int sc = 0; sc < n_scen; sc++) max_keys = std::max(max_keys, clusters[sc].n_label_keys);
-    if (blob_stride && !need.general && simple_fits(g, blob_stride, max_keys))
-      rc = launch_simple(st, g, n_scen, blob_stride, max_keys, (const DevJob*)(arena + job_off), *prof, nullptr, err);
-    else
-      rc = launch_schedule(st, g, n_scen, need.bins_cap, need.general, max_keys, (const DevJob*)(arena + job_off), *prof,
-                           nullptr, err);
-    hipEventRecord(e1, st);
-    if (hipStreamSynchronize(st) != hipSuccess && !rc) rc = fail(KSS_E_DEVICE, "k_schedule failed");
-    float ms = 0;
-    hipEventElapsedTime(&ms, e0, e1);
-    if (device_ms) *device_ms = ms;
-  }
-  if (err) hipFree(err);
-  if (!rc) {
-    size_t o = 0;
-    for (int s = 0; s < n_scen && !rc; s++) {
-      if (podsets[s].n_pods &&
-          hipMemcpy(chosen_out + o, arena + ch_off[s], sizeof(int32_t) * podsets[s].n_pods, hipMemcpyDeviceToHost) != hipSuccess)
-        rc = fail(KSS_E_DEVICE, "chosen copy failed");
-      o += (size_t)podsets[s].n_pods;
-    }
-    std::vector<PodMeta> m;
-    for (int s = 0; s < n_scen && !rc; s++) {
-      m.resize((size_t)std::max(podsets[s].n_pods, 1));
-      if (podsets[s].n_pods &&
-          hipMemcpy(m.data(), arena + m_off[s], sizeof(PodMeta) * podsets[s].n_pods, hipMemcpyDeviceToHost) != hipSuccess)
-        rc = fail(KSS_E_DEVICE, "outcome copy failed");
-      for (int i = 0; i < podsets[s].n_pods && !rc; i++)
-        if (m[i].status == 4) rc = fail(KSS_E_UNSUPPORTED, "pod program exceeds the device path's per-pod limits");
-    }
-  }
-  if (e0) hipEventDestroy(e0);
-  if (e1) hipEventDestroy(e1);
-  hipFree(arena);
-  hipStreamDestroy(st);
+  kss_sweep* sw = kss_sweep_create(device, prof, n_scen, clusters, podsets);
+  if (!sw) return g_rc ? g_rc : KSS_E_INVAL;
+  rc = kss_sweep_run(sw, chosen_out, device_ms);
+  kss_sweep_destroy(sw);
   return rc;
 }
 

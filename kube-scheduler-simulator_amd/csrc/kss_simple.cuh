@@ -2,11 +2,22 @@
 // InterPodAffinity programs (the default-profile workload of BASELINE C1/C2/C5), built
 // around ONE cross-shard exchange per pod.
 //
-// Same semantics as schedule_pod<false> (kss_sched.cuh), different pipeline:
-//   * every node row of the shard lives in registers for the whole launch (lane t owns
-//     nodes lo + j*blockDim + t, j < NPT); label value ids live in LDS;
-//   * pod programs arrive as position-independent blobs (host: build_blobs) staged in a
-//     3-slot LDS ring; blob k+2 is loaded into registers while pod k is scheduled;
+// Same semantics as schedule_pod<false> (kss_sched.cuh), split in two kernels:
+//
+//   k_static  (massively parallel, one lane per (pod, node)): everything of a pod's
+//             evaluation that no commit can change — the NodeUnschedulable, NodeName,
+//             TaintToleration and NodeAffinity filters (node flags, taints and labels are
+//             not touched by AssumePod) and the raw TaintToleration and NodeAffinity
+//             scores — packed in one 32-bit "static word" per (pod, node) in HBM.
+//   k_simple  (persistent, one workgroup per shard of W): the sequential loop.  Per pod it
+//             only evaluates what the state changes: the NodeResourcesFit filter, the Fit
+//             and BalancedAllocation scores (exact reciprocal arithmetic, kss_fastmath.cuh),
+//             then NormalizeScore, the packed selectHost key and the commit.
+//
+// The persistent loop:
+//   * the shard's node rows and their Allocatable reciprocals live in LDS for the launch;
+//   * the compact pod records (SPod) and the static words of pod k+2 are loaded into
+//     registers while pod k is scheduled and stored into 3-slot LDS rings at its end;
 //   * pod k's argmax and pod k+1's normalisation statistics travel in the same exchange.
 //     Pod k+1's statistics depend on pod k's commit, which touches one node only: the
 //     winner, which is some shard's local best.  Each shard therefore evaluates pod k+1
@@ -14,17 +25,15 @@
 //     publishes both statistic sets next to its pod-k key.  Once the global winner is
 //     known, the winner's shard contributes H1 and every other shard H0, which is the
 //     statistic of pod k+1 on the committed state.
-// Per pod: one block reduction for the shard's best key, one for the six partial
-// statistics, one exchange (8 granules per shard) — instead of two block reductions and
-// two exchanges separated by a full filter pass.
 #pragma once
+#include "kss_fastmath.cuh"
 #include "kss_sched.cuh"
 
 namespace kss {
 
-constexpr int BLOB_MAX = 4096;  // bytes per serialized pod program (host-checked)
-constexpr int SX_VALS = 8;      // granules per shard per exchange: key lo/hi, H0 (nf, tt, na), H1 (nf, tt, na)
-constexpr int SX_CHUNKS = 2;    // shards swept 64 at a time: W <= 128
+constexpr int SX_VALS = 8;    // granules per shard per exchange: key lo/hi, H0 (nf, tt, na), H1 (nf, tt, na)
+constexpr int SX_CHUNKS = 2;  // shards swept 64 at a time: W <= 128
+constexpr int STATIC_PODS = 8;  // pods per k_static lane
 
 // The v1.26 default profile (kss_default_profile, kss_host.cpp; plugins_test.go:184-204,
 // 878-1096) as a compile-time constant: k_simple<true> folds every weight and resource
@@ -56,30 +65,189 @@ __host__ __device__ constexpr kss_profile default_profile_c() {
   return p;
 }
 
-// Blob layout: kss_pod (every offset rebased into the blob) | BlobHdr | reqs | terms | ints.
-struct BlobHdr {
-  int32_t req_off, term_off, ints_off;  // byte offsets from the blob start
-  int32_t n_reqs, n_terms, n_ints;
-  int32_t pad[2];
+// Compact per-pod record of the simple path (host: build_spods): only what the
+// state-dependent part of the cycle reads.
+constexpr int32_t SP_ALLZERO = 1;  // computePodResourceRequest is all zero: fitsRequest checks pods only
+struct SPod {
+  int64_t fit_req[3];  // NodeResourcesFit PreFilter request cpu / memory / ephemeral
+  int64_t snz[3];      // LeastAllocated request (non-zero defaults)
+  int64_t sreq[3];     // BalancedAllocation request
+  int64_t creq[3];     // AssumePod Requested delta
+  int64_t cnz[2];      // AssumePod NonZeroRequested delta
+  int32_t flags;       // SP_*
+  int32_t status;      // kss_pod.prefilter_status
+  int32_t cls;         // class_count row the pod joins (-1 none)
+  int32_t own_off, own_len;  // term_count rows it adds: ints[own_off .. +own_len) of the staged pool
+  int32_t pad[3];
 };
-__host__ __device__ constexpr size_t blob_hdr_off() { return (sizeof(kss_pod) + 15) / 16 * 16; }
-__host__ __device__ constexpr size_t blob_body_off() { return blob_hdr_off() + (sizeof(BlobHdr) + 15) / 16 * 16; }
+static_assert(sizeof(SPod) % 16 == 0, "SPod is copied as uint4");
 
-struct BlobView {
-  const kss_pod* pod;
-  const kss_req* reqs;
-  const kss_term* terms;
-  const int32_t* ints;
+// Static word of one (pod, node): bits 0-7 the first failing static filter (0 pass, 1-4
+// KSS_F_NODE_UNSCHEDULABLE..KSS_F_NODE_AFFINITY, 255 not evaluated: PreFilter failure
+// or outside the NodeAffinity PreFilterResult), bits 8-15 raw TaintToleration, bits
+// 16-31 raw NodeAffinity (host-checked: Σ preferred weights < 2^16).
+__device__ __forceinline__ uint32_t static_word(const DevCluster& c, const DevPods& P, const kss_pod& p,
+                                                const kss_profile& prof, int n, uint32_t flags, uint64_t th,
+                                                uint64_t ts) {
+  const int64_t g = (int64_t)c.node_base + n;
+  if (p.prefilter_status != 0) return KSS_F_NOT_EVALUATED;
+  if (p.names_len >= 0) {  // NodeAffinity PreFilterResult: nodes outside the set are not evaluated
+    bool in = false;
+    for (int i = 0; i < p.names_len; i++) in |= (int64_t)P.ints[p.names_off + i] == g;
+    if (!in) return KSS_F_NOT_EVALUATED;
+  }
+  const uint32_t en = prof.filter_enabled;
+  auto lab = [&](int key) { return label_of(c, key, n); };
+  // RunFilterPlugins order (plugin_test.go:15-36): the first four filters are static
+  if (((en >> KSS_F_NODE_UNSCHEDULABLE) & 1u) && (flags & KSS_NODE_UNSCHEDULABLE) && !(p.flags & KSS_POD_TOL_UNSCHEDULABLE))
+    return KSS_F_NODE_UNSCHEDULABLE;
+  if (((en >> KSS_F_NODE_NAME) & 1u) && p.node_name != -1 && (int64_t)p.node_name != g) return KSS_F_NODE_NAME;
+  if (((en >> KSS_F_TAINT_TOLERATION) & 1u) && (th & ~p.tol_hard)) return KSS_F_TAINT_TOLERATION;
+  if (((en >> KSS_F_NODE_AFFINITY) & 1u) && !required_affinity_t(c, P.reqs, P.terms, P.ints, p, g, lab))
+    return KSS_F_NODE_AFFINITY;
+  const uint32_t tt = (uint32_t)__popcll(ts & ~p.tol_soft);                         // TaintToleration.Score
+  const uint32_t na = (uint32_t)na_score_t(c, P.reqs, P.terms, P.ints, p, g, lab);  // NodeAffinity.Score
+  return (tt << 8) | (na << 16);
+}
+
+// One (pod, node) result of the compact path: filter verdict and raw scores.
+struct SVal {
+  int f, tt, na, fit, ba;
 };
 
-__device__ __forceinline__ BlobView blob_view(const uint8_t* b) {
-  const BlobHdr* h = reinterpret_cast<const BlobHdr*>(b + blob_hdr_off());
-  BlobView v;
-  v.pod = reinterpret_cast<const kss_pod*>(b);
-  v.reqs = reinterpret_cast<const kss_req*>(b + h->req_off);
-  v.terms = reinterpret_cast<const kss_term*>(b + h->term_off);
-  v.ints = reinterpret_cast<const int32_t*>(b + h->ints_off);
-  return v;
+// A node row as the state-dependent filter and scores read it.
+struct DynRow {
+  int64_t alloc[3], req[3], nz[2];
+  double inv[3];  // RN(1 / alloc), 0 for alloc 0
+  int32_t pods, allowed;
+};
+
+// v[r] of a three-element row for a runtime resource id r in [0, 3), as masks: a select
+// chain would be folded back into an indexed access, which puts the row in scratch.
+__device__ __forceinline__ int64_t pick3m(int r, int64_t a, int64_t b, int64_t c) {
+  return (a & -(int64_t)(r == 0)) | (b & -(int64_t)(r == 1)) | (c & -(int64_t)(r == 2));
+}
+__device__ __forceinline__ double pick3d(int r, double a, double b, double c) {
+  return __longlong_as_double(pick3m(r, __double_as_longlong(a), __double_as_longlong(b), __double_as_longlong(c)));
+}
+
+// NodeResourcesFit.Score (resourceAllocationScorer.score, useRequested=false, no scalar
+// resources on this path: calculateResourceAllocatableRequest skips them at request 0).
+__device__ __forceinline__ int32_t fit_fast(const kss_profile& prof, const SPod& q, const DynRow& r) {
+  int32_t node_score = 0, weight_sum = 0;
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    if (i >= prof.fit_n) break;
+    const int res = prof.fit_res[i];
+    if (res >= KSS_RES_SCALAR0) continue;
+    const int64_t A = pick3m(res, r.alloc[0], r.alloc[1], r.alloc[2]);
+    if (A == 0) continue;
+    const int64_t base = pick3m(res, r.nz[0], r.nz[1], r.req[2]);
+    const double inv = pick3d(res, r.inv[0], r.inv[1], r.inv[2]);
+    const int64_t preq = pick3m(res, q.snz[0], q.snz[1], q.snz[2]);
+    const int32_t w = (int32_t)prof.fit_weight[i];
+    node_score += alloc_score_fast(prof.fit_strategy, base + preq, A, inv) * w;
+    weight_sum += w;
+  }
+  if (weight_sum <= 1) return weight_sum == 0 ? 0 : node_score;
+  if (weight_sum == 2) return node_score >> 1;
+  return small_div(node_score, weight_sum, __builtin_amdgcn_rcpf((float)weight_sum));
+}
+
+// NodeResourcesBalancedAllocation.Score (balancedResourceScorer, useRequested=true); the
+// float64 operations in the reference's order, divisions correctly rounded (div_rn).
+__device__ __forceinline__ int32_t ba_fast(const kss_profile& prof, const SPod& q, const DynRow& r) {
+  double fr[4] = {0.0, 0.0, 0.0, 0.0};
+  bool use[4] = {false, false, false, false};
+  int nf = 0;
+  double total = 0.0;
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    if (i >= prof.ba_n) break;
+    const int res = prof.ba_res[i];
+    if (res >= KSS_RES_SCALAR0) continue;
+    const int64_t A = pick3m(res, r.alloc[0], r.alloc[1], r.alloc[2]);
+    if (A == 0) continue;
+    const int64_t R = pick3m(res, r.req[0], r.req[1], r.req[2]) + pick3m(res, q.sreq[0], q.sreq[1], q.sreq[2]);
+    const double inv = pick3d(res, r.inv[0], r.inv[1], r.inv[2]);
+    double f = div_rn(R, A, inv);
+    if (f > 1.0) f = 1.0;
+    total += f;
+    fr[i] = f;
+    use[i] = true;
+    nf++;
+  }
+  double sd = 0.0;
+  if (nf == 2) {
+    double a = 0.0, b = 0.0;
+    bool got = false;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      if (!use[i]) continue;
+      if (!got) {
+        a = fr[i];
+        got = true;
+      } else {
+        b = fr[i];
+      }
+    }
+    sd = fabs((a - b) / 2.0);
+  } else if (nf > 2) {
+    const double mean = total / (double)nf;
+    double sum = 0.0;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      if (!use[i]) continue;
+      const double d = fr[i] - mean;
+      const double sq = d * d;
+      sum = sum + sq;
+    }
+    sd = sqrt(sum / (double)nf);
+  }
+  return (int32_t)((1.0 - sd) * 100.0);  // in [0, 100]: int32 truncation == int64(...)
+}
+
+// The state-dependent rest of one evaluation: NodeResourcesFit.Filter (fitsRequest) and
+// the Fit / BalancedAllocation scores, after the static word's filters.
+__device__ __forceinline__ SVal dyn_eval(const kss_profile& prof, const SPod& q, uint32_t w, const DynRow& r) {
+  SVal e{(int)(w & 0xFFu), 0, 0, 0, 0};
+  if (e.f) return e;
+  if ((prof.filter_enabled >> KSS_F_NODE_RESOURCES_FIT) & 1u) {
+    bool bad = (int64_t)r.pods + 1 > (int64_t)r.allowed;
+    if (!(q.flags & SP_ALLZERO)) {
+#pragma unroll
+      for (int k = 0; k < 3; k++) bad |= q.fit_req[k] > r.alloc[k] - r.req[k];
+    }
+    if (bad) {
+      e.f = KSS_F_NODE_RESOURCES_FIT;
+      return e;
+    }
+  }
+  e.tt = (int)((w >> 8) & 0xFFu);
+  e.na = (int)(w >> 16);
+  e.fit = fit_fast(prof, q, r);
+  e.ba = ba_fast(prof, q, r);
+  return e;
+}
+
+// NormalizeScore + weights + packed selectHost key of one feasible node (the scored
+// branch of schedule_pod<false>: PodTopologySpread normalises to 100 without
+// constraints, InterPodAffinity keeps its raw 0).  rtt / rna: reciprocals of the maxima.
+__device__ __forceinline__ long long simple_key(const kss_profile& prof, const SVal& e, bool scored, int max_tt,
+                                                float rtt, int max_na, float rna, uint32_t g) {
+  int64_t total = 0;
+  if (scored) {
+    // DefaultNormalizeScore(100, reverse=true) / (100, reverse=false); quotients <= 100
+    const int32_t tt = max_tt == 0 ? 100 : 100 - small_div(100 * e.tt, max_tt, rtt);
+    const int32_t na = max_na != 0 ? small_div(100 * e.na, max_na, rna) : e.na;
+    const uint32_t se = prof.score_enabled;
+    if ((se >> KSS_S_TAINT_TOLERATION) & 1u) total += (int64_t)tt * prof.weight[KSS_S_TAINT_TOLERATION];
+    if ((se >> KSS_S_NODE_AFFINITY) & 1u) total += (int64_t)na * prof.weight[KSS_S_NODE_AFFINITY];
+    if ((se >> KSS_S_NODE_RESOURCES_FIT) & 1u) total += (int64_t)e.fit * prof.weight[KSS_S_NODE_RESOURCES_FIT];
+    if ((se >> KSS_S_POD_TOPOLOGY_SPREAD) & 1u) total += 100 * (int64_t)prof.weight[KSS_S_POD_TOPOLOGY_SPREAD];
+    if ((se >> KSS_S_BALANCED_ALLOCATION) & 1u) total += (int64_t)e.ba * prof.weight[KSS_S_BALANCED_ALLOCATION];
+  }
+  return (long long)(((unsigned long long)(uint32_t)total << 32) | (0xFFFFFFFFull - g));
 }
 
 // ---------------------------------------------------------------------------
@@ -151,15 +319,16 @@ __device__ __forceinline__ void wave_red_stats(uint32_t (&v)[6]) {
 }
 
 // LDS image of the loop head: reduction scratch (double-buffered), exchange results.
-struct SimpleHdr {
+struct alignas(16) SimpleHdr {
   long long red[2][MAXWAVES][SX_VALS];
   long long res[4];  // winner key of the previous pod; nf, max TT, max NA of the next pod
+  kss_profile prof;  // a runtime (non-default) profile: indexed by resource id, so in LDS, not scratch
   int abort;
   int pad[3];
 };
 
 // Workgroup barrier that orders LDS only.  HIP's __syncthreads() also drains every
-// outstanding global load (vmcnt), which would put the blob prefetch on the critical path.
+// outstanding global load (vmcnt), which would put the prefetches on the critical path.
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 // Workgroup reduction of K values; ONE barrier.  Parity alternates between calls, so a
@@ -239,26 +408,23 @@ __device__ __forceinline__ bool simple_exchange(SimpleHdr& H, unsigned long long
     const int g = (int)(0xFFFFFFFFu - (uint32_t)(unsigned long long)best);
     wstar = (g - node_base) / per;
   }
-  long long nf = 0, tt = 0, na = 0;
+  // {nf, tt, na} of every shard's hypothesis, reduced in one interleaved DPP pass
+  uint32_t u[6] = {0, 0, 0, 0, 0, 0};
 #pragma unroll
   for (int ch = 0; ch < SX_CHUNKS; ch++) {
     const int s = ch * 64 + lane;
     if (s >= W) continue;
     const bool h1 = s == wstar;
-    nf += (long long)(h1 ? got[ch][5] : got[ch][2]);
-    const long long t = (long long)(h1 ? got[ch][6] : got[ch][3]);
-    const long long a = (long long)(h1 ? got[ch][7] : got[ch][4]);
-    tt = t > tt ? t : tt;
-    na = a > na ? a : na;
+    u[0] += h1 ? got[ch][5] : got[ch][2];
+    u[1] = max(u[1], h1 ? got[ch][6] : got[ch][3]);
+    u[2] = max(u[2], h1 ? got[ch][7] : got[ch][4]);
   }
-  nf = wave_red<OP_SUM>(nf);
-  tt = wave_red<OP_MAX>(tt);
-  na = wave_red<OP_MAX>(na);
+  wave_red_stats(u);
   if (lane == 0) {
     H.res[0] = best;
-    H.res[1] = nf;
-    H.res[2] = tt;
-    H.res[3] = na;
+    H.res[1] = u[0];
+    H.res[2] = u[1];
+    H.res[3] = u[2];
   }
   return true;
 }
@@ -310,130 +476,49 @@ __device__ __forceinline__ bool simple_sync(SimpleHdr& H, int& parity, long long
   return true;
 }
 
-// One (pod, node) evaluation of the compact path: filter verdict and raw scores.
-struct SVal {
-  int f, tt, na, fit, ba;
-};
-
-// The filters of filter_local (kss_eval.cuh) and the four raw scores, with node labels
-// from the shard's LDS table and the pod program from its LDS blob.  The TaintToleration
-// / Fit failure details are not needed here (no record is kept on this path).
-__device__ __forceinline__ SVal simple_eval(const DevCluster& c, const kss_profile& prof, const BlobView& B,
-                                            const kss_pod& p, int n, const NodeRow& row, const int32_t* lbl, int cap,
-                                            int si, unsigned long long* sp = nullptr) {
-  SVal e{0, 0, 0, 0, 0};
-  const int64_t g = (int64_t)c.node_base + n;
-  auto lab = [&](int key) { return lbl[key * cap + si]; };
-  if (p.names_len >= 0) {  // NodeAffinity PreFilterResult: nodes outside the set are not evaluated
-    bool in = false;
-    for (int i = 0; i < p.names_len; i++) in |= (int64_t)B.ints[p.names_off + i] == g;
-    if (!in) {
-      e.f = KSS_F_NOT_EVALUATED;
-      return e;
-    }
-  }
-  const uint32_t en = prof.filter_enabled;
-  if (((en >> KSS_F_NODE_UNSCHEDULABLE) & 1u) && (row.flags & KSS_NODE_UNSCHEDULABLE) &&
-      !(p.flags & KSS_POD_TOL_UNSCHEDULABLE)) {
-    e.f = KSS_F_NODE_UNSCHEDULABLE;
-  } else if (((en >> KSS_F_NODE_NAME) & 1u) && p.node_name != -1 && (int64_t)p.node_name != g) {
-    e.f = KSS_F_NODE_NAME;
-  } else if (((en >> KSS_F_TAINT_TOLERATION) & 1u) && (row.th & ~p.tol_hard)) {
-    e.f = KSS_F_TAINT_TOLERATION;
-  } else if (((en >> KSS_F_NODE_AFFINITY) & 1u) && !required_affinity_t(c, B.reqs, B.terms, B.ints, p, g, lab)) {
-    e.f = KSS_F_NODE_AFFINITY;
-  } else if ((en >> KSS_F_NODE_RESOURCES_FIT) & 1u) {
-    bool bad = (int64_t)row.pods + 1 > (int64_t)row.allowed;
-    const bool all_zero = p.fit_request[0] == 0 && p.fit_request[1] == 0 && p.fit_request[2] == 0;
-    if (!all_zero) {
-#pragma unroll
-      for (int r = 0; r < 3; r++) bad |= p.fit_request[r] > row.alloc[r] - row.req[r];
-    }
-    if (bad) e.f = KSS_F_NODE_RESOURCES_FIT;
-  }
-  if (sp) sp[8] = wall_clock64();
-  if (e.f) return e;
-  e.tt = (int)tt_score(row, p);
-  e.na = (int)na_score_t(c, B.reqs, B.terms, B.ints, p, g, lab);
-  if (sp) sp[9] = wall_clock64();
-  e.fit = (int)fit_score<true>(c, prof, p, n, row);
-  if (sp) sp[10] = wall_clock64();
-  e.ba = (int)ba_score(c, prof, p, n, row);
-  if (sp) sp[11] = wall_clock64();
-  return e;
-}
-
-// NormalizeScore + weights + packed selectHost key of one feasible node (the scored
-// branch of schedule_pod<false>: PodTopologySpread normalises to 100 without
-// constraints, InterPodAffinity keeps its raw 0).
-__device__ __forceinline__ long long simple_key(const kss_profile& prof, const SVal& e, bool scored, long long max_tt,
-                                                long long max_na, uint32_t g) {
-  int64_t total = 0;
-  if (scored) {
-    const int64_t tt = max_tt == 0 ? 100 : 100 - div_i64<true>(100 * (int64_t)e.tt, max_tt);
-    const int64_t na = max_na != 0 ? div_i64<true>(100 * (int64_t)e.na, max_na) : (int64_t)e.na;
-    const uint32_t se = prof.score_enabled;
-    if ((se >> KSS_S_TAINT_TOLERATION) & 1u) total += tt * prof.weight[KSS_S_TAINT_TOLERATION];
-    if ((se >> KSS_S_NODE_AFFINITY) & 1u) total += na * prof.weight[KSS_S_NODE_AFFINITY];
-    if ((se >> KSS_S_NODE_RESOURCES_FIT) & 1u) total += (int64_t)e.fit * prof.weight[KSS_S_NODE_RESOURCES_FIT];
-    if ((se >> KSS_S_POD_TOPOLOGY_SPREAD) & 1u) total += 100 * (int64_t)prof.weight[KSS_S_POD_TOPOLOGY_SPREAD];
-    if ((se >> KSS_S_BALANCED_ALLOCATION) & 1u) total += (int64_t)e.ba * prof.weight[KSS_S_BALANCED_ALLOCATION];
-  }
-  return (long long)(((unsigned long long)(uint32_t)total << 32) | (0xFFFFFFFFull - g));
-}
-
-// NodeInfo.AddPod on a node row (requested, non-zero requested, pod count).
-__device__ __forceinline__ void add_commit(NodeRow& r, const kss_pod& p) {
-#pragma unroll
-  for (int k = 0; k < 3; k++) r.req[k] += p.commit_req[k];
-  r.nz[0] += p.commit_nz[0];
-  r.nz[1] += p.commit_nz[1];
-  r.pods += 1;
-}
-
-// The shard's node state in LDS for the whole launch (slot s = node lo + s), and the
-// per-slot results of the next pod; slot `cap` of the results holds the candidate node
-// re-evaluated after the previous pod's commit (H1).
+// The shard's node state in LDS for the whole launch (slot s = node lo + s), the per-slot
+// results of the next pod (slot `cap` of the results holds the candidate node
+// re-evaluated after the previous pod's commit, H1) and the static-word ring.
 struct SimpleShard {
-  int64_t* r64;  // [8][cap]: allocatable cpu/mem/eph, requested cpu/mem/eph, non-zero cpu/mem
-  uint64_t* rt;  // [2][cap]: NoSchedule/NoExecute taints, PreferNoSchedule taints
-  int32_t* r32;  // [3][cap]: pod count, allowed pods, node flags
-  int32_t* lbl;  // [n_keys][cap]: label value ids
-  int32_t* cv;   // [5][cap + 1]: filter verdict, TT, NA, Fit, BA
+  int64_t* r64;   // [8][cap]: allocatable cpu/mem/eph, requested cpu/mem/eph, non-zero cpu/mem
+  double* inv;    // [3][cap]: RN(1 / allocatable)
+  int32_t* r32;   // [2][cap]: pod count, allowed pods
+  uint32_t* st;   // [3][cap]: static words of pods k, k+1, k+2 (ring slot = pod % 3)
+  int32_t* cv;    // [5][cap + 1]: filter verdict, TT, NA, Fit, BA
+  SPod* ring;     // [3]: pod records (ring slot = pod % 3)
   int cap;
 };
 
-__host__ __device__ inline size_t simple_lds_bytes(int stride, int n_keys, int cap) {
-  return sizeof(SimpleHdr) + 3 * (size_t)stride + (size_t)cap * (8 * 8 + 2 * 8 + 3 * 4 + 4 * (size_t)n_keys) +
-         20 * ((size_t)cap + 1);
+__host__ __device__ inline size_t simple_lds_bytes(int cap) {
+  return sizeof(SimpleHdr) + 3 * sizeof(SPod) + (size_t)cap * (8 * 8 + 3 * 8 + 2 * 4 + 3 * 4) + 20 * ((size_t)cap + 1);
 }
 
-__device__ __forceinline__ SimpleShard shard_view(uint8_t* base, int n_keys, int cap) {
+__device__ __forceinline__ SimpleShard shard_view(uint8_t* base, int cap) {
   SimpleShard L;
   L.cap = cap;
-  L.r64 = reinterpret_cast<int64_t*>(base);
-  L.rt = reinterpret_cast<uint64_t*>(base + 64 * (size_t)cap);
-  L.r32 = reinterpret_cast<int32_t*>(base + 80 * (size_t)cap);
-  L.lbl = L.r32 + 3 * (size_t)cap;
-  L.cv = L.lbl + (size_t)n_keys * cap;
+  L.ring = reinterpret_cast<SPod*>(base);
+  uint8_t* b = base + 3 * sizeof(SPod);
+  L.r64 = reinterpret_cast<int64_t*>(b);
+  L.inv = reinterpret_cast<double*>(b + 64 * (size_t)cap);
+  L.r32 = reinterpret_cast<int32_t*>(b + 88 * (size_t)cap);
+  L.st = reinterpret_cast<uint32_t*>(L.r32 + 2 * (size_t)cap);
+  L.cv = reinterpret_cast<int32_t*>(L.st + 3 * (size_t)cap);
   return L;
 }
 
-__device__ __forceinline__ NodeRow shard_row(const SimpleShard& L, int s) {
-  NodeRow r;
+__device__ __forceinline__ DynRow shard_row(const SimpleShard& L, int s) {
+  DynRow r;
   const int C = L.cap;
 #pragma unroll
   for (int k = 0; k < 3; k++) {
     r.alloc[k] = L.r64[k * C + s];
     r.req[k] = L.r64[(3 + k) * C + s];
+    r.inv[k] = L.inv[k * C + s];
   }
   r.nz[0] = L.r64[6 * C + s];
   r.nz[1] = L.r64[7 * C + s];
-  r.th = L.rt[s];
-  r.ts = L.rt[C + s];
   r.pods = L.r32[s];
   r.allowed = L.r32[C + s];
-  r.flags = (uint32_t)L.r32[2 * C + s];
   return r;
 }
 
@@ -451,26 +536,31 @@ __device__ __forceinline__ void cv_put(const SimpleShard& L, int s, const SVal& 
   L.cv[4 * C1 + s] = e.ba;
 }
 
-// Pass A for the pod of blob B over the shard's `own` nodes on the current state (H0),
-// plus the candidate slot `cand_s` (-1 none) re-evaluated with the previous pod `q`
-// committed on it (H1), by the first slot without a node (slot `own`, which is slot
-// `cap` of lane 0 when the shard is full).  st = {nf0, tt0, na0, nf1, tt1, na1}.
-__device__ __forceinline__ void simple_pass_a(const DevCluster& c, const kss_profile& prof, const BlobView& B,
-                                              const SimpleShard& L, int lo, int own, int cand_s, const kss_pod& q,
-                                              long long (&st)[6], unsigned long long* sp) {
+// NodeInfo.AddPod on a node row (requested, non-zero requested, pod count).
+__device__ __forceinline__ void add_commit(DynRow& r, const SPod& p) {
+#pragma unroll
+  for (int k = 0; k < 3; k++) r.req[k] += p.creq[k];
+  r.nz[0] += p.cnz[0];
+  r.nz[1] += p.cnz[1];
+  r.pods += 1;
+}
+
+// Pass A for pod q (static words in ring slot `sl`) over the shard's `own` nodes on the
+// current state (H0), plus the candidate slot `cand_s` (-1 none) re-evaluated with the
+// previous pod `q0` committed on it (H1), by the first slot without a node (slot `own`,
+// which is slot `cap` of lane 0 when the shard is full).  st = {nf0, tt0, na0, nf1, tt1, na1}.
+__device__ __forceinline__ void simple_pass_a(const kss_profile& prof, const SPod& q, const SPod& q0, const SimpleShard& L,
+                                              int sl, int own, int cand_s, long long (&st)[6]) {
   const int tid = threadIdx.x, nt = blockDim.x;
-  const kss_pod& p = *B.pod;
-  const bool pre_ok = p.prefilter_status == 0;
+  const uint32_t* sw = L.st + (size_t)sl * L.cap;
   long long nf = 0, tt = 0, na = 0, nf1 = 0, tt1 = 0, na1 = 0;
   for (int s = tid; s <= L.cap; s += nt) {
     const bool extra = s == own && cand_s >= 0;
     if (s >= own && !extra) continue;
     const int ns = extra ? cand_s : s;
-    NodeRow r = shard_row(L, ns);
-    if (extra) add_commit(r, q);
-    if (sp && s == 0) sp[7] = wall_clock64();
-    SVal e{KSS_F_NOT_EVALUATED, 0, 0, 0, 0};
-    if (pre_ok) e = simple_eval(c, prof, B, p, lo + ns, r, L.lbl, L.cap, ns, (sp && s == 0) ? sp : nullptr);
+    DynRow r = shard_row(L, ns);
+    if (extra) add_commit(r, q0);
+    const SVal e = dyn_eval(prof, q, sw[ns], r);
     cv_put(L, extra ? L.cap : s, e);
     if (e.f == 0) {
       if (!extra) {
@@ -493,76 +583,81 @@ __device__ __forceinline__ void simple_pass_a(const DevCluster& c, const kss_pro
   st[5] = na1;
 }
 
-// The whole batch for shard w of one cluster (every pod commits).  On an exchange
-// timeout the error word is set and the shard leaves without writing node state back.
-__device__ __forceinline__ void simple_schedule(DevCluster c, const uint8_t* __restrict__ blobs, int stride, int n_pods,
-                                                int32_t* chosen, PodMeta* meta, const kss_profile& prof, int W, int w,
-                                                int cap, unsigned long long* gran, int* err,
+// Pods [k0, k1) of the batch for shard w of one cluster (every pod commits).  `stat`
+// holds the static words of those pods ([k - k0][N]).  On an exchange timeout the error
+// word is set and the shard leaves without writing node state back.
+__device__ __forceinline__ void simple_schedule(DevCluster c, const SPod* __restrict__ spods,
+                                                const uint32_t* __restrict__ stat, const int32_t* __restrict__ ints,
+                                                int k0, int k1, int32_t* chosen, PodMeta* meta, const kss_profile& prof,
+                                                int W, int w, int cap, unsigned long long* gran, int* err,
                                                 unsigned long long* stamps, long long* smem) {
   const int tid = threadIdx.x, nt = blockDim.x;
   SimpleHdr& H = *reinterpret_cast<SimpleHdr*>(smem);
-  uint8_t* ring = reinterpret_cast<uint8_t*>(smem) + sizeof(SimpleHdr);
-  const SimpleShard L = shard_view(ring + 3 * (size_t)stride, c.n_keys, cap);
+  const SimpleShard L = shard_view(reinterpret_cast<uint8_t*>(smem) + sizeof(SimpleHdr), cap);
   const size_t N = (size_t)c.N;
   const int per = (c.N + W - 1) / W;
   const int lo = min(c.N, w * per), hi = min(c.N, lo + per), own = hi - lo;
-  if (n_pods <= 0) return;
-  // shard rows and label ids -> LDS, blobs 0 and 1 -> ring
+  if (k1 <= k0) return;
+  constexpr int NQ = (int)(sizeof(SPod) / 16);
+  // shard rows, reciprocals, static words of pods k0 and k0+1, their records -> LDS
   for (int s = tid; s < own; s += nt) {
     const int n = lo + s;
 #pragma unroll
     for (int k = 0; k < 3; k++) {
-      L.r64[k * cap + s] = c.alloc[k * N + n];
+      const int64_t A = c.alloc[k * N + n];
+      L.r64[k * cap + s] = A;
       L.r64[(3 + k) * cap + s] = c.requested[k * N + n];
+      L.inv[k * cap + s] = A > 0 ? 1.0 / (double)A : 0.0;
     }
     L.r64[6 * cap + s] = c.nonzero[n];
     L.r64[7 * cap + s] = c.nonzero[N + n];
-    L.rt[s] = c.taint_hard[n];
-    L.rt[cap + s] = c.taint_soft[n];
     L.r32[s] = c.pod_count[n];
     L.r32[cap + s] = c.allowed_pods[n];
-    L.r32[2 * cap + s] = (int32_t)c.node_flags[n];
+    L.st[(k0 % 3) * cap + s] = stat[(size_t)lo + s];
+    if (k0 + 1 < k1) L.st[((k0 + 1) % 3) * cap + s] = stat[N + lo + s];
   }
-  for (int i = tid; i < c.n_keys * cap; i += nt) {
-    const int k = i / cap, s = i - k * cap;
-    L.lbl[i] = s < own ? c.label_value[(size_t)k * N + lo + s] : -1;
+  for (int i = tid; i < min(k1 - k0, 2) * NQ; i += nt) {
+    const int j = k0 + i / NQ;
+    reinterpret_cast<uint4*>(L.ring + j % 3)[i % NQ] = reinterpret_cast<const uint4*>(spods + j)[i % NQ];
   }
-  const int nq = stride / 16;
-  for (int i = tid; i < min(n_pods, 2) * nq; i += nt)
-    reinterpret_cast<uint4*>(ring)[i] = reinterpret_cast<const uint4*>(blobs)[i];
   if (tid == 0) H.abort = 0;
   __syncthreads();
 
   long long st[6], R[4] = {0, 0, 0, 0};
   int parity = 0, sub_s = -1;  // slot whose pass-B values are the H1 ones (the previous winner)
   unsigned epoch = 0;
-  // k = -1 is the prologue: pass A of pod 0 and the exchange of its statistics
-  for (int k = -1; k < n_pods; k++) {
+  const int nslot = (own + nt - 1) / nt;  // node slots per lane
+  // k = k0 - 1 is the prologue: pass A of pod k0 and the exchange of its statistics
+  for (int k = k0 - 1; k < k1; k++) {
     // diagnostic phase stamps (KSS_STAMPS_FILE), lane 0 of shard 0, first pods only
-    unsigned long long* sp = (stamps && w == 0 && k >= 0 && k < KSS_NSTAMP_PODS / 2) ? stamps + (size_t)k * 16 : nullptr;
+    unsigned long long* sp =
+        (stamps && w == 0 && k >= k0 && k - k0 < KSS_NSTAMP_PODS / 2) ? stamps + (size_t)(k - k0) * 16 : nullptr;
     if (sp && tid == 0) sp[0] = wall_clock64();
-    const BlobView Bk = blob_view(ring + (size_t)((k + 3) % 3) * stride);
-    const kss_pod& pk = *Bk.pod;
-    // blob k+2 -> registers now, -> its ring slot at the end of this pod
-    const bool pf_on = k >= 0 && k + 2 < n_pods;
-    const uint4* pf_src = reinterpret_cast<const uint4*>(blobs + (size_t)(k + 2) * stride);
-    uint4 pf[2];
+    const SPod& pk = L.ring[(k + 3) % 3];
+    // pod k+2: record and static words -> registers now, -> their ring slots at the end
+    const bool pf_on = k >= k0 && k + 2 < k1;
+    uint4 pfq = make_uint4(0, 0, 0, 0);
+    if (pf_on && tid < NQ) pfq = reinterpret_cast<const uint4*>(spods + k + 2)[tid];
+    uint32_t pfw[KSS_MAX_NPT];
 #pragma unroll
-    for (int q = 0; q < 2; q++) {
-      const int i = q * nt + tid;
-      pf[q] = make_uint4(0, 0, 0, 0);
-      if (pf_on && i < nq) pf[q] = pf_src[i];
+    for (int j = 0; j < KSS_MAX_NPT; j++) {
+      const int s = j * nt + tid;
+      pfw[j] = 0;
+      if (pf_on && j < nslot && s < own) pfw[j] = stat[(size_t)(k + 2 - k0) * N + lo + s];
     }
     // pass B: NormalizeScore, weights, shard-best selectHost key of pod k
-    const long long nf = R[1], max_tt = R[2], max_na = R[3];
+    const long long nf = R[1];
+    const int max_tt = (int)R[2], max_na = (int)R[3];
     const bool scored = nf > 1;
     long long best = 0;
-    if (k >= 0) {
-      if (pk.prefilter_status == 0 && nf > 0) {
+    if (k >= k0) {
+      if (pk.status == 0 && nf > 0) {
+        const float rtt = __builtin_amdgcn_rcpf((float)max(max_tt, 1));
+        const float rna = __builtin_amdgcn_rcpf((float)max(max_na, 1));
         for (int s = tid; s < own; s += nt) {
           const SVal e = cv_get(L, s == sub_s ? cap : s);
           if (e.f != 0) continue;
-          const long long key = simple_key(prof, e, scored, max_tt, max_na, (uint32_t)(c.node_base + lo + s));
+          const long long key = simple_key(prof, e, scored, max_tt, rtt, max_na, rna, (uint32_t)(c.node_base + lo + s));
           best = key > best ? key : best;
         }
       }
@@ -576,9 +671,8 @@ __device__ __forceinline__ void simple_schedule(DevCluster c, const uint8_t* __r
     }
     const int cand_s = best ? (int)(0xFFFFFFFFu - (uint32_t)(unsigned long long)best) - c.node_base - lo : -1;
     // pass A: pod k+1 before pod k's commit, and on the candidate after it
-    if (k + 1 < n_pods) {
-      const BlobView B1 = blob_view(ring + (size_t)((k + 1) % 3) * stride);
-      simple_pass_a(c, prof, B1, L, lo, own, cand_s, pk, st, sp);
+    if (k + 1 < k1) {
+      simple_pass_a(prof, L.ring[(k + 1) % 3], pk, L, (k + 1) % 3, own, cand_s, st);
     } else {
 #pragma unroll
       for (int i = 0; i < 6; i++) st[i] = 0;
@@ -586,39 +680,40 @@ __device__ __forceinline__ void simple_schedule(DevCluster c, const uint8_t* __r
     if (sp && tid == 0) sp[3] = wall_clock64();
     if (!simple_sync(H, parity, best, st, W, w, ++epoch, gran, err, per, c.node_base, R, sp)) return;
     if (sp && tid == 0) sp[5] = wall_clock64();
-    if (k < 0) continue;
-    const long long K = R[0];
-    const int x = K ? (int)(0xFFFFFFFFu - (uint32_t)(unsigned long long)K) - c.node_base : -1;
-    if (w == 0 && tid == 0) {
-      PodMeta m;
-      m.chosen = K ? x + c.node_base : -1;
-      m.n_feasible = (int)nf;
-      m.scored = (K && scored) ? 1 : 0;
-      m.status = pk.prefilter_status != 0 ? (pk.prefilter_status == 1 ? 2 : 3) : (nf == 0 ? 1 : 0);
-      m.best_total = m.scored ? (int64_t)((unsigned long long)K >> 32) : 0;
-      if (chosen) chosen[k] = m.chosen;
-      if (meta) meta[k] = m;
-    }
-    // AssumePod on the winner's shard; pass B of pod k+1 takes that slot's H1 values
-    const bool won = x >= lo && x < hi;
-    sub_s = won ? x - lo : -1;
-    if (won && tid == 0) {
-      const int s = x - lo;
+    if (k >= k0) {
+      const long long K = R[0];
+      const int x = K ? (int)(0xFFFFFFFFu - (uint32_t)(unsigned long long)K) - c.node_base : -1;
+      if (w == 0 && tid == 0) {
+        PodMeta m;
+        m.chosen = K ? x + c.node_base : -1;
+        m.n_feasible = (int)nf;
+        m.scored = (K && scored) ? 1 : 0;
+        m.status = pk.status != 0 ? (pk.status == 1 ? 2 : 3) : (nf == 0 ? 1 : 0);
+        m.best_total = m.scored ? (int64_t)((unsigned long long)K >> 32) : 0;
+        if (chosen) chosen[k] = m.chosen;
+        if (meta) meta[k] = m;
+      }
+      // AssumePod on the winner's shard; pass B of pod k+1 takes that slot's H1 values
+      const bool won = x >= lo && x < hi;
+      sub_s = won ? x - lo : -1;
+      if (won && tid == 0) {
+        const int s = x - lo;
 #pragma unroll
-      for (int r = 0; r < 3; r++) L.r64[(3 + r) * cap + s] += pk.commit_req[r];
-      L.r64[6 * cap + s] += pk.commit_nz[0];
-      L.r64[7 * cap + s] += pk.commit_nz[1];
-      L.r32[s] += 1;
-      // HBM-only columns: no-return atomics, so the commit never waits on a load
-      if (pk.cls >= 0) atomicAdd(&c.class_count[(size_t)pk.cls * N + x], 1);
-      for (int i = 0; i < pk.own_terms_len; i++) atomicAdd(&c.term_count[(size_t)Bk.ints[pk.own_terms_off + i] * N + x], 1);
+        for (int r = 0; r < 3; r++) L.r64[(3 + r) * cap + s] += pk.creq[r];
+        L.r64[6 * cap + s] += pk.cnz[0];
+        L.r64[7 * cap + s] += pk.cnz[1];
+        L.r32[s] += 1;
+        // HBM-only columns: no-return atomics, so the commit never waits on a load
+        if (pk.cls >= 0) atomicAdd(&c.class_count[(size_t)pk.cls * N + x], 1);
+        for (int i = 0; i < pk.own_len; i++) atomicAdd(&c.term_count[(size_t)ints[pk.own_off + i] * N + x], 1);
+      }
     }
     if (pf_on) {
-      uint4* dst = reinterpret_cast<uint4*>(ring + (size_t)((k + 2) % 3) * stride);
+      if (tid < NQ) reinterpret_cast<uint4*>(L.ring + (k + 2) % 3)[tid] = pfq;
 #pragma unroll
-      for (int q = 0; q < 2; q++) {
-        const int i = q * nt + tid;
-        if (i < nq) dst[i] = pf[q];
+      for (int j = 0; j < KSS_MAX_NPT; j++) {
+        const int s = j * nt + tid;
+        if (j < nslot && s < own) L.st[((k + 2) % 3) * cap + s] = pfw[j];
       }
     }
     if (sp && tid == 0) sp[6] = wall_clock64();

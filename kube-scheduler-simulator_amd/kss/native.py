@@ -46,7 +46,12 @@ SIGNATURES = [
     ("kss_fetch_record", C.c_int, [C.c_void_p, C.c_int32, P(abi.PodResult)]),
     ("kss_schedule_scenarios", C.c_int, [C.c_int32, P(abi.Profile), C.c_int32, P(abi.Cluster), P(abi.PodSet),
                                          P(C.c_int32), P(C.c_double)]),
+    ("kss_sweep_create", C.c_void_p, [C.c_int32, P(abi.Profile), C.c_int32, P(abi.Cluster), P(abi.PodSet)]),
+    ("kss_sweep_run", C.c_int, [C.c_void_p, P(C.c_int32), P(C.c_double)]),
+    ("kss_sweep_info", C.c_int, [C.c_void_p, P(C.c_double), P(C.c_int32), P(C.c_int64)]),
+    ("kss_sweep_destroy", None, [C.c_void_p]),
     ("kss_last_timing", C.c_int, [C.c_void_p, P(C.c_double), P(C.c_int32)]),
+    ("kss_last_loop_timing", C.c_int, [C.c_void_p, P(C.c_double)]),
     ("kss_last_geometry", C.c_int, [C.c_void_p, P(C.c_int32)]),
     ("kss_last_kernel", C.c_int, [C.c_void_p]),
     ("kss_fetch_meta", C.c_int, [C.c_void_p, C.c_int32, C.c_int32, P(C.c_int64)]),
@@ -276,6 +281,12 @@ class Context:
         check(lib().kss_last_timing(self.h, C.byref(ms), C.byref(n)))
         return ms.value, n.value
 
+    def last_loop_ms(self) -> float:
+        """Device ms of the sequential-loop kernel(s) alone in the last batch."""
+        ms = C.c_double(0)
+        check(lib().kss_last_loop_timing(self.h, C.byref(ms)))
+        return ms.value
+
     def last_geometry(self):
         out = (C.c_int32 * 3)()
         check(lib().kss_last_geometry(self.h, out))
@@ -340,3 +351,41 @@ def schedule_scenarios(profile, clusters: List[abi.Cluster], podsets: List[abi.P
     check(lib().kss_schedule_scenarios(device, C.byref(profile), n, carr, parr, chosen.ctypes.data_as(P(C.c_int32)),
                                        C.byref(ms)))
     return chosen[:total], ms.value
+
+
+class Sweep:
+    """A resident what-if sweep (kss_sweep): every scenario staged once, run many times."""
+
+    def __init__(self, profile, clusters: List[abi.Cluster], podsets: List[abi.PodSet], device=0):
+        L = lib()
+        n = len(clusters)
+        carr = (abi.Cluster * max(n, 1))(*clusters)
+        parr = (abi.PodSet * max(n, 1))(*podsets)
+        h = L.kss_sweep_create(device, C.byref(profile), n, carr, parr)
+        if not h:
+            raise KssError(-1, (L.kss_last_error() or b"").decode())
+        self.h = C.c_void_p(h)
+        self.total = sum(p.n_pods for p in podsets)
+
+    def run(self):
+        """(chosen [sum n_pods], device ms of reset + launches)."""
+        chosen = np.full(max(self.total, 1), -2, np.int32)
+        ms = C.c_double(0)
+        check(lib().kss_sweep_run(self.h, chosen.ctypes.data_as(P(C.c_int32)), C.byref(ms)))
+        return chosen[:self.total], ms.value
+
+    def info(self):
+        ms, k, b = C.c_double(0), C.c_int32(0), C.c_int64(0)
+        check(lib().kss_sweep_info(self.h, C.byref(ms), C.byref(k), C.byref(b)))
+        return {"stage_ms": ms.value, "kernel": "k_simple" if k.value == 1 else "k_schedule", "upload_bytes": b.value}
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().kss_sweep_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

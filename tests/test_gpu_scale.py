@@ -198,3 +198,65 @@ def test_c5_sweep_64_scenarios():
         ch, _, _ = _oracle(prof, x, x.n_pods)
         np.testing.assert_array_equal(chosen[off:off + x.n_pods], ch, err_msg=f"scenario {k}")
         off += x.n_pods
+
+
+def test_sweep_resident_reruns_match_oracle():
+    """kss_sweep: staged once (one upload), run twice; every run restores the snapshots on
+    the device, so both equal the oracle.  Ragged sizes in one sweep."""
+    prof = abi.default_profile()
+    syn = [native.Synth(2, SEED_BASE + 2 + 7919 * k, n, 150) for k, n in enumerate([1000, 37, 700, 1000, 3, 512])]
+    sw = native.Sweep(prof, [x.cluster for x in syn], [x.pods for x in syn])
+    assert sw.info()["kernel"] == "k_simple"
+    want = np.concatenate([_oracle(prof, x, x.n_pods)[0] for x in syn])
+    for rep in range(2):
+        chosen, ms = sw.run()
+        assert ms > 0
+        np.testing.assert_array_equal(chosen, want, err_msg=f"run {rep}")
+    sw.close()
+
+
+def _custom_profile():
+    """MostAllocated over cpu:3 / memory:2 (weight sum 5), BalancedAllocation over three
+    resources (the standard-deviation branch), non-default plugin weights."""
+    prof = abi.default_profile()
+    prof.fit_strategy = abi.KSS_FIT_MOST_ALLOCATED
+    prof.fit_weight[0], prof.fit_weight[1] = 3, 2
+    prof.ba_n = 3
+    prof.ba_res[2] = abi.KSS_RES_EPHEMERAL
+    prof.weight[abi.KSS_S_NODE_AFFINITY] = 5
+    prof.weight[abi.KSS_S_TAINT_TOLERATION] = 1
+    prof.weight[abi.KSS_S_BALANCED_ALLOCATION] = 4
+    return prof
+
+
+@pytest.mark.parametrize("n_nodes,n_pods", [(5000, 1500), (700, 400)])
+def test_k_simple_custom_profile_matches_oracle(n_nodes, n_pods):
+    prof = _custom_profile()
+    s = native.Synth(2, 0, n_nodes, n_pods)
+    chosen_o, res, st = _oracle(prof, s, n_pods, record="meta")
+    ctx = native.Context(prof)
+    ctx.load(s.cluster)
+    ctx.stage(s.pods)
+    np.testing.assert_array_equal(ctx.run_staged(n_pods), chosen_o)
+    assert ctx.last_kernel() == "k_simple"
+    _meta_equal(ctx.fetch_meta(n_pods), res, n_pods)
+    _state_equal(ctx, st, n_nodes, 0, 0)
+    ctx.close()
+
+
+def test_k_simple_small_static_chunks(monkeypatch):
+    """KSS_STATIC_BYTES forces the static words into many chunks (one k_static + one
+    k_simple launch each, node state carried in HBM): same result as one chunk."""
+    monkeypatch.setenv("KSS_STATIC_BYTES", str(4 * 3000 * 37))  # 37 pods per chunk
+    prof = abi.default_profile()
+    n_nodes, n_pods = 3000, 400
+    s = native.Synth(2, 0, n_nodes, n_pods)
+    chosen_o, res, st = _oracle(prof, s, n_pods, record="meta")
+    ctx = native.Context(prof)
+    ctx.load(s.cluster)
+    ctx.stage(s.pods)
+    np.testing.assert_array_equal(ctx.run_staged(n_pods), chosen_o)
+    assert ctx.last_timing()[1] == 2 * ((n_pods + 36) // 37)
+    _meta_equal(ctx.fetch_meta(n_pods), res, n_pods)
+    _state_equal(ctx, st, n_nodes, 0, 0)
+    ctx.close()
