@@ -177,6 +177,15 @@ __global__ __launch_bounds__(KSS_MAX_THREADS) void k_simple(const DevJob* __rest
                   gran ? gran + (size_t)ji * 2 * W * SX_VALS : nullptr, err, ji == 0 ? stamps : nullptr, smem);
 }
 
+// Class / term counts of the chosen nodes of pods [k0, min(k1, n_pods)) of every job
+// (grid: x = 256-pod tiles, y = job).
+__global__ __launch_bounds__(256) void k_counts(const DevJob* __restrict__ jobs, int k0, int k1) {
+  const DevJob& job = jobs[blockIdx.y];
+  const int k = k0 + (int)(blockIdx.x * 256 + threadIdx.x);
+  if (k >= min(k1, job.n_pods) || !job.chosen) return;
+  simple_counts(job.c, job.spods, job.P.ints, job.chosen, k);
+}
+
 // Static words of pods [k0, min(k1, n_pods)) x every node of every job.  grid: x = 256-node
 // tiles, y = groups of STATIC_PODS pods, z = job.  One lane per node walks its group.
 template <bool DEF>
@@ -985,7 +994,9 @@ static bool same_profile(const kss_profile& a, const kss_profile& b) {
 static int simple_cap(const Geometry& g) { return g.npt * g.threads; }
 
 static bool simple_fits(const Geometry& g) {
-  return g.W <= 64 * SX_CHUNKS && g.npt <= KSS_MAX_NPT && simple_lds_bytes(simple_cap(g)) <= KSS_LDS_BUDGET;
+  const int pf_n = g.threads > 64 ? g.threads - 64 : g.threads;  // prefetch lanes (kss_simple.cuh)
+  return g.W <= 64 * SX_CHUNKS && g.npt <= KSS_MAX_NPT && (simple_cap(g) + pf_n - 1) / pf_n <= PF_MAX &&
+         simple_lds_bytes(simple_cap(g)) <= KSS_LDS_BUDGET;
 }
 
 // Static-word scratch bound (KSS_STATIC_BYTES): pods are processed in chunks whose words
@@ -1041,6 +1052,9 @@ static int launch_simple(hipStream_t st, const Geometry& g, int n_jobs, const De
     }
     if (ev) HIP_TRY(hipEventRecord(ev[2 * ci + 1], st));
   }
+  hipLaunchKernelGGL(k_counts, dim3((unsigned)((n_pods_max + 255) / 256), (unsigned)n_jobs), dim3(256), 0, st, jobs, 0,
+                     n_pods_max);
+  HIP_TRY(hipGetLastError());
   return 0;
 }
 

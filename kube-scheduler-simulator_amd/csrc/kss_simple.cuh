@@ -31,9 +31,20 @@
 
 namespace kss {
 
+// Global-memory accesses of the persistent loop go through address-space-1 pointers:
+// from a generic pointer the compiler emits flat instructions, which also count in
+// lgkmcnt, so every LDS-only barrier (s_waitcnt lgkmcnt(0)) would wait for the HBM
+// prefetches and the commit's atomics.
+#define KSS_GLOBAL __attribute__((address_space(1)))
+template <class T>
+__device__ __forceinline__ KSS_GLOBAL T* gp(T* p) {
+  return (KSS_GLOBAL T*)p;
+}
+
 constexpr int SX_VALS = 8;    // granules per shard per exchange: key lo/hi, H0 (nf, tt, na), H1 (nf, tt, na)
 constexpr int SX_CHUNKS = 2;  // shards swept 64 at a time: W <= 128
 constexpr int STATIC_PODS = 8;  // pods per k_static lane
+constexpr int PF_MAX = 8;       // static words per prefetch lane (host-checked: simple_fits)
 
 // The v1.26 default profile (kss_default_profile, kss_host.cpp; plugins_test.go:184-204,
 // 878-1096) as a compile-time constant: k_simple<true> folds every weight and resource
@@ -434,7 +445,7 @@ __device__ __forceinline__ bool simple_exchange(SimpleHdr& H, unsigned long long
 // every lane.  False if the launch aborted (exchange timeout).
 __device__ __forceinline__ bool simple_sync(SimpleHdr& H, int& parity, long long key, long long (&st)[6], int W, int w,
                                             unsigned epoch, unsigned long long* gran, int* err, int per, int node_base,
-                                            long long (&R)[4], unsigned long long* sp) {
+                                            long long (&R)[4], KSS_GLOBAL unsigned long long* sp) {
   {
     uint32_t u[6];
 #pragma unroll
@@ -623,27 +634,44 @@ __device__ __forceinline__ void simple_schedule(DevCluster c, const SPod* __rest
   if (tid == 0) H.abort = 0;
   __syncthreads();
 
+  KSS_GLOBAL const uint32_t* gstat = gp(stat);
+  KSS_GLOBAL const uint4* gspod = gp(reinterpret_cast<const uint4*>(spods));
+  KSS_GLOBAL int32_t* gchosen = gp(chosen);
+  KSS_GLOBAL PodMeta* gmeta = gp(meta);
+  KSS_GLOBAL unsigned long long* gstamps = gp(stamps);
   long long st[6], R[4] = {0, 0, 0, 0};
   int parity = 0, sub_s = -1;  // slot whose pass-B values are the H1 ones (the previous winner)
   unsigned epoch = 0;
-  const int nslot = (own + nt - 1) / nt;  // node slots per lane
+  const int nwave = nt >> 6;
+  // prefetch lanes: every wave but wave 0 (readfirstlane: a wave-uniform, scalar branch)
+  const bool pf_wave = nwave == 1 || __builtin_amdgcn_readfirstlane(tid >> 6) >= 1;
+  uint4 pfq = make_uint4(0, 0, 0, 0);  // prefetched record / static words of pod k+2, live across the loop
+  uint32_t pfw[PF_MAX];
+#pragma unroll
+  for (int j = 0; j < PF_MAX; j++) pfw[j] = 0;
+  const int pf_lane = nwave == 1 ? tid : tid - 64, pf_n = nwave == 1 ? nt : nt - 64;
+  const int pf_per = (own + pf_n - 1) / pf_n;  // static words per prefetch lane (<= PF_MAX)
   // k = k0 - 1 is the prologue: pass A of pod k0 and the exchange of its statistics
   for (int k = k0 - 1; k < k1; k++) {
     // diagnostic phase stamps (KSS_STAMPS_FILE), lane 0 of shard 0, first pods only
-    unsigned long long* sp =
-        (stamps && w == 0 && k >= k0 && k - k0 < KSS_NSTAMP_PODS / 2) ? stamps + (size_t)(k - k0) * 16 : nullptr;
+    KSS_GLOBAL unsigned long long* sp =
+        (stamps && w == 0 && k >= k0 && k - k0 < KSS_NSTAMP_PODS / 2) ? gstamps + (size_t)(k - k0) * 16 : nullptr;
     if (sp && tid == 0) sp[0] = wall_clock64();
     const SPod& pk = L.ring[(k + 3) % 3];
     // pod k+2: record and static words -> registers now, -> their ring slots at the end
-    const bool pf_on = k >= k0 && k + 2 < k1;
-    uint4 pfq = make_uint4(0, 0, 0, 0);
-    if (pf_on && tid < NQ) pfq = reinterpret_cast<const uint4*>(spods + k + 2)[tid];
-    uint32_t pfw[KSS_MAX_NPT];
+    // Only the prefetch waves (all but wave 0, unless there is one wave) issue these loads:
+    // vmcnt is per wave and counts stores too, so wave 0 — which publishes granules and
+    // writes the outcomes — never waits on an HBM prefetch, and the prefetch waves never
+    // wait on a store.
+    // The branch is wave-uniform and every load inside it is unconditional (clamped
+    // indices), so the compiler's wait for these registers stays on the prefetch path.
+    const bool pf_on = pf_wave && k >= k0 && k + 2 < k1 && own > 0;
+    if (pf_on) {
+      KSS_GLOBAL const uint4& src = gspod[(size_t)(k + 2) * NQ + min(pf_lane, NQ - 1)];
+      pfq = make_uint4(src.x, src.y, src.z, src.w);
 #pragma unroll
-    for (int j = 0; j < KSS_MAX_NPT; j++) {
-      const int s = j * nt + tid;
-      pfw[j] = 0;
-      if (pf_on && j < nslot && s < own) pfw[j] = stat[(size_t)(k + 2 - k0) * N + lo + s];
+      for (int j = 0; j < PF_MAX; j++)
+        if (j < pf_per) pfw[j] = gstat[(size_t)(k + 2 - k0) * N + lo + min(j * pf_n + pf_lane, own - 1)];
     }
     // pass B: NormalizeScore, weights, shard-best selectHost key of pod k
     const long long nf = R[1];
@@ -690,8 +718,14 @@ __device__ __forceinline__ void simple_schedule(DevCluster c, const SPod* __rest
         m.scored = (K && scored) ? 1 : 0;
         m.status = pk.status != 0 ? (pk.status == 1 ? 2 : 3) : (nf == 0 ? 1 : 0);
         m.best_total = m.scored ? (int64_t)((unsigned long long)K >> 32) : 0;
-        if (chosen) chosen[k] = m.chosen;
-        if (meta) meta[k] = m;
+        if (chosen) gchosen[k] = m.chosen;
+        if (meta) {
+          gmeta[k].chosen = m.chosen;
+          gmeta[k].n_feasible = m.n_feasible;
+          gmeta[k].scored = m.scored;
+          gmeta[k].status = m.status;
+          gmeta[k].best_total = m.best_total;
+        }
       }
       // AssumePod on the winner's shard; pass B of pod k+1 takes that slot's H1 values
       const bool won = x >= lo && x < hi;
@@ -703,18 +737,15 @@ __device__ __forceinline__ void simple_schedule(DevCluster c, const SPod* __rest
         L.r64[6 * cap + s] += pk.cnz[0];
         L.r64[7 * cap + s] += pk.cnz[1];
         L.r32[s] += 1;
-        // HBM-only columns: no-return atomics, so the commit never waits on a load
-        if (pk.cls >= 0) atomicAdd(&c.class_count[(size_t)pk.cls * N + x], 1);
-        for (int i = 0; i < pk.own_len; i++) atomicAdd(&c.term_count[(size_t)ints[pk.own_off + i] * N + x], 1);
+        // the HBM-only class / term counts are applied after the launch (k_counts): nothing
+        // in this loop reads them
       }
     }
-    if (pf_on) {
-      if (tid < NQ) reinterpret_cast<uint4*>(L.ring + (k + 2) % 3)[tid] = pfq;
+    if (pf_on) {  // lanes past the end rewrite the last element with its own value
+      reinterpret_cast<uint4*>(L.ring + (k + 2) % 3)[min(pf_lane, NQ - 1)] = pfq;
 #pragma unroll
-      for (int j = 0; j < KSS_MAX_NPT; j++) {
-        const int s = j * nt + tid;
-        if (j < nslot && s < own) L.st[((k + 2) % 3) * cap + s] = pfw[j];
-      }
+      for (int j = 0; j < PF_MAX; j++)
+        if (j < pf_per) L.st[((k + 2) % 3) * cap + min(j * pf_n + pf_lane, own - 1)] = pfw[j];
     }
     if (sp && tid == 0) sp[6] = wall_clock64();
   }
@@ -728,6 +759,19 @@ __device__ __forceinline__ void simple_schedule(DevCluster c, const SPod* __rest
     c.nonzero[N + n] = L.r64[7 * cap + s];
     c.pod_count[n] = L.r32[s];
   }
+}
+
+// The class / term count part of AssumePod for pods [k0, k1) of a k_simple batch, from
+// their chosen nodes (one lane per pod; counts commute, so the order is immaterial).
+__device__ __forceinline__ void simple_counts(const DevCluster& c, const SPod* __restrict__ spods,
+                                              const int32_t* __restrict__ ints, const int32_t* __restrict__ chosen,
+                                              int k) {
+  const int x = chosen[k] - c.node_base;
+  if (x < 0 || x >= c.N) return;
+  const SPod& q = spods[k];
+  const size_t N = (size_t)c.N;
+  if (q.cls >= 0) atomicAdd(&c.class_count[(size_t)q.cls * N + x], 1);
+  for (int i = 0; i < q.own_len; i++) atomicAdd(&c.term_count[(size_t)ints[q.own_off + i] * N + x], 1);
 }
 
 }  // namespace kss
