@@ -1,8 +1,8 @@
 """HIP path (libkss.so on gfx950) vs the CPU oracle: bit-exact filter verdicts, every
 per-plugin raw and normalized score, totals, chosen nodes and the final node state.
 
-Sizes are ones the oracle finishes in seconds; full BASELINE sizes are covered by
-size-independent properties in test_gpu_properties.py.
+Sizes are ones the oracle finishes in seconds; the full BASELINE sizes are in
+test_gpu_scale.py.
 """
 import json
 import os
@@ -176,6 +176,33 @@ def test_readme_known_answer_on_gpu():
             assert json.loads(ann[k]) == v, k
         else:
             assert ann[k] == v, k
+
+
+GOLD2 = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "extender_known_answer.json")))
+
+
+def _check_ann(ann, exp):
+    from test_oracle_known_answer import check_annotations
+    check_annotations(ann, exp)
+
+
+def test_extender_doc_known_answer_on_gpu():
+    """simulator/docs/plugin-extender.md:80-109 on the device: (a) the drop-in per-pod call
+    on the snapshot with node-282x7 already holding a pod; (b) the two pods as a sequential
+    batch on the empty nodes (the first one's AssumePod happens on the device)."""
+    cc, cp, _ = compile_cluster(GOLD2["nodes"], GOLD2["bound"], [GOLD2["pod"]])
+    ctx = native.Context(abi.default_profile(), max_pods_record=2)
+    ctx.load(cc.as_struct(), names=native.make_names(cc.node_names, cc.taints, cc.scalars))
+    _check_ann(ctx.format_annotations(ctx.eval_pod(cp.as_struct(), 0)), GOLD2["expected"])
+    ctx.close()
+    first = dict(GOLD2["bound"][0], spec={k: v for k, v in GOLD2["bound"][0]["spec"].items() if k != "nodeName"})
+    cc, cp, _ = compile_cluster(GOLD2["nodes"], (), [first, GOLD2["pod"]])
+    ctx = native.Context(abi.default_profile(), max_pods_record=2)
+    ctx.load(cc.as_struct(), names=native.make_names(cc.node_names, cc.taints, cc.scalars))
+    chosen = ctx.schedule_batch(cp.as_struct(), 2, record=True)
+    assert [cc.node_names[c] for c in chosen] == ["node-282x7", "node-gp9t4"]
+    _check_ann(ctx.format_annotations(ctx.fetch_record(1)), GOLD2["expected"])
+    ctx.close()
 
 
 def test_eval_pod_commit_rollback():

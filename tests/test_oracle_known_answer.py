@@ -1,9 +1,15 @@
-"""Pin the oracles against the reference's own known-answer vector.
+"""Pin the oracles against the reference's own known-answer vectors.
 
-README.md:61-79 (also simulator/docs/debuggable-scheduler.md:17-35): two empty
-4-CPU/32Gi nodes (web/components/lib/templates/node.yaml) and a 100m/16Gi pod
-(pod.yaml).  Fixture: tests/golden/readme_known_answer.json (made by
-tests/golden/make_readme_golden.py).
+  * README.md:61-79 (also simulator/docs/debuggable-scheduler.md:17-35): two empty
+    4-CPU/32Gi nodes (web/components/lib/templates/node.yaml) and a 100m/16Gi pod
+    (pod.yaml).  Fixture: tests/golden/readme_known_answer.json
+    (tests/golden/make_readme_golden.py).
+  * simulator/docs/plugin-extender.md:80-109: the same two nodes, node-282x7 already
+    holding one template pod; pod-8ldq5 scores Fit 47 / BalancedAllocation 52 there
+    against 73 / 76 on the empty node and is bound to node-gp9t4 (no tie).  It pins the
+    AssumePod accounting, the exact-fit memory boundary (16Gi of 16Gi free passes) and a
+    non-tie selectHost.  Fixture: tests/golden/extender_known_answer.json
+    (tests/golden/make_extender_golden.py).
 """
 import json
 import os
@@ -17,6 +23,50 @@ from kss import abi
 from kss.compile import compile_cluster
 
 GOLD = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "readme_known_answer.json")))
+GOLD2 = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "extender_known_answer.json")))
+
+ANN_JSON = ("scheduler-simulator/filter-result", "scheduler-simulator/score-result",
+            "scheduler-simulator/finalscore-result", "scheduler-simulator/prefilter-result-status",
+            "scheduler-simulator/prescore-result", "scheduler-simulator/reserve-result",
+            "scheduler-simulator/prebind-result", "scheduler-simulator/bind-result")
+ANN_EMPTY = ("scheduler-simulator/permit-result", "scheduler-simulator/permit-result-timeout",
+             "scheduler-simulator/postfilter-result", "scheduler-simulator/prefilter-result")
+
+
+def check_annotations(ann, exp):
+    for key in ANN_JSON:
+        assert json.loads(ann[key]) == exp[key], key
+    for key in ANN_EMPTY:
+        assert ann[key] == exp[key] == "{}", key
+    assert ann["scheduler-simulator/selected-node"] == exp["scheduler-simulator/selected-node"]
+
+
+def test_object_oracle_matches_extender_doc_annotations():
+    o = k8s_oracle.Oracle(GOLD2["nodes"], GOLD2["bound"])
+    check_annotations(o.annotations(o.schedule_one(GOLD2["pod"])), GOLD2["expected"])
+
+
+def test_object_oracle_extender_doc_as_two_pod_sequence():
+    """The bound pod scheduled first on the empty nodes (tie -> node-282x7, the lowest
+    canonical index), then pod-8ldq5 sees its AssumePod."""
+    o = k8s_oracle.Oracle(GOLD2["nodes"])
+    first = dict(GOLD2["bound"][0], spec={k: v for k, v in GOLD2["bound"][0]["spec"].items() if k != "nodeName"})
+    r0 = o.schedule_one(first)
+    assert o.annotations(r0)["scheduler-simulator/selected-node"] == "node-282x7"
+    check_annotations(o.annotations(o.schedule_one(GOLD2["pod"])), GOLD2["expected"])
+
+
+def test_c_oracle_matches_extender_doc_scores():
+    cc, cp, _ = compile_cluster(GOLD2["nodes"], GOLD2["bound"], [GOLD2["pod"]])
+    prof = abi.default_profile()
+    chosen, res, _ = oracle_c.schedule(prof, cc.as_struct(), cp.as_struct(), 1, cc.n_nodes)
+    exp = GOLD2["expected"]
+    for n, name in enumerate(cc.node_names):
+        for s, pl in enumerate(abi.SCORE_PLUGINS):
+            assert int(res.norm[0, s, n]) * prof.weight[s] == int(exp["scheduler-simulator/finalscore-result"][name][pl])
+            assert int(res.raw[0, s, n]) == int(exp["scheduler-simulator/score-result"][name][pl])
+    assert cc.node_names[chosen[0]] == exp["scheduler-simulator/selected-node"]
+    assert (res.fail_plugin[0] == 0).all()
 
 
 def test_object_oracle_matches_readme_annotations():
