@@ -53,6 +53,34 @@ __device__ __forceinline__ double div_rn(int64_t ai, int64_t bi, double y) {
   return fma(r, y, q);
 }
 
+// The same on integers held in doubles (every value an integer below 2^53, so exact):
+// the compact kernel keeps node state and pod requests as doubles, which removes the
+// int64 <-> double conversions from the loop.
+__device__ __forceinline__ int32_t quot_small_d(double x, double A, double invA) {
+  int32_t q = (int32_t)(x * invA);
+  const double r = fma(-(double)q, A, x);  // q * A and x are integers below 2^53: exact
+  if (r < 0.0) q--;
+  else if (r >= A) q++;
+  return q;
+}
+
+__device__ __forceinline__ double div_rn_d(double a, double b, double y) {
+  double q = a * y;
+  double r = fma(-q, b, a);
+  q = fma(r, y, q);
+  r = fma(-q, b, a);
+  return fma(r, y, q);
+}
+
+__device__ __forceinline__ int32_t alloc_score_d(int strategy, double requested, double capacity, double inv) {
+  if (strategy == KSS_FIT_MOST_ALLOCATED) {
+    if (requested > capacity) requested = capacity;
+    return quot_small_d(requested * 100.0, capacity, inv);
+  }
+  if (requested > capacity) return 0;
+  return quot_small_d((capacity - requested) * 100.0, capacity, inv);
+}
+
 // leastRequestedScore / mostRequestedScore (noderesources/least_allocated.go,
 // most_allocated.go) for 0 < capacity < 2^46: quotient in [0, 100].
 __device__ __forceinline__ int32_t alloc_score_fast(int strategy, int64_t requested, int64_t capacity, double inv) {

@@ -236,6 +236,12 @@ struct DevBuf {
   }
 };
 
+// k_simple exactness bounds (f64_bounds_cluster / f64_bounds_pods / f64_exact below).
+struct F64Bounds {
+  double max_req0 = 0, max_nz0 = 0, max_creq = 0, max_cnz = 0, max_pod = 0;
+  bool neg = false;
+};
+
 // Per-batch LDS / exchange sizing: the host restatement of make_plan's bin counts.
 struct PlanNeeds {
   int bins_cap = 0;  // max over pods of histogram + presence bins
@@ -292,6 +298,7 @@ struct kss_ctx {
   int last_kernel = 0;     // 0 k_schedule, 1 k_simple
   int meta_n = 0;          // pods with an outcome in meta_host
   bool small_values = false;  // every allocatable cpu/mem/eph < 2^46: k_simple's divisions stay below 2^53
+  F64Bounds f64_cluster, f64_pods;  // k_simple exactness bounds of the loaded snapshot / staged pods
   bool axis_meta_dirty = false;  // meta_buf holds node-axis outcomes not yet copied to meta_host
   DevBuf axis_cv;
   int axis_max_blocks = 0;  // KSS_AXIS_BLOCKS: cap on the node-axis grid (tuning)
@@ -382,6 +389,47 @@ int validate(const kss_cluster* cl, const kss_podset* ps, int n) {
   return 0;
 }
 
+// k_simple holds node state and pod requests as integers in doubles (kss_simple.cuh
+// SPod): exact while every value and every sum the loop can form stays below 2^53.
+// Cluster side: the largest snapshot Requested / NonZeroRequested (cpu, memory,
+// ephemeral); pod side: the largest request of any kind.  A node's Requested grows by
+// at most n_pods commits of the largest commit delta (a bound that holds even without
+// the NodeResourcesFit filter).
+void f64_bounds_cluster(const kss_cluster* cl, F64Bounds& b) {
+  const size_t N = (size_t)cl->n_nodes;
+  for (size_t i = 0; i < 3 * N; i++) {
+    b.neg |= cl->requested[i] < 0;
+    b.max_req0 = std::max(b.max_req0, (double)cl->requested[i]);
+  }
+  for (size_t i = 0; i < 2 * N; i++) {
+    b.neg |= cl->nonzero[i] < 0;
+    b.max_nz0 = std::max(b.max_nz0, (double)cl->nonzero[i]);
+  }
+}
+void f64_bounds_pods(const kss_podset* ps, F64Bounds& b) {
+  for (int i = 0; i < ps->n_pods; i++) {
+    const kss_pod& p = ps->pods[i];
+    for (int r = 0; r < 3; r++) {
+      const int64_t v[4] = {p.fit_request[r], p.score_req_nz[r], p.score_req[r], p.commit_req[r]};
+      for (int64_t x : v) {
+        b.neg |= x < 0;
+        b.max_pod = std::max(b.max_pod, (double)x);
+      }
+      b.max_creq = std::max(b.max_creq, (double)p.commit_req[r]);
+    }
+    for (int r = 0; r < 2; r++) {
+      b.neg |= p.commit_nz[r] < 0;
+      b.max_cnz = std::max(b.max_cnz, (double)p.commit_nz[r]);
+      b.max_pod = std::max(b.max_pod, (double)p.commit_nz[r]);
+    }
+  }
+}
+bool f64_exact(const F64Bounds& c, const F64Bounds& p, int n_pods) {
+  const double lim = 4503599627370496.0;  // 2^52: sums of two such values stay below 2^53
+  return !c.neg && !p.neg && p.max_pod < lim && c.max_req0 + (double)n_pods * p.max_creq < lim &&
+         c.max_nz0 + (double)n_pods * p.max_cnz < lim;
+}
+
 // Compact records of every pod of a (validated) podset for k_simple (kss_simple.cuh
 // SPod); false when some pod needs k_schedule: spread / inter-pod-affinity programs, or
 // preferred NodeAffinity weights whose sum does not fit the static word's 16 bits.
@@ -397,13 +445,13 @@ bool build_spods(const kss_podset* ps, int n_scalar, std::vector<SPod>& out) {
     bool all_zero = true;
     for (int r = 0; r < 3 + n_scalar; r++) all_zero &= p.fit_request[r] == 0;
     for (int r = 0; r < 3; r++) {
-      q.fit_req[r] = p.fit_request[r];
-      q.snz[r] = p.score_req_nz[r];
-      q.sreq[r] = p.score_req[r];
-      q.creq[r] = p.commit_req[r];
+      q.fit_req[r] = (double)p.fit_request[r];
+      q.snz[r] = (double)p.score_req_nz[r];
+      q.sreq[r] = (double)p.score_req[r];
+      q.creq[r] = (double)p.commit_req[r];
     }
-    q.cnz[0] = p.commit_nz[0];
-    q.cnz[1] = p.commit_nz[1];
+    q.cnz[0] = (double)p.commit_nz[0];
+    q.cnz[1] = (double)p.commit_nz[1];
     q.flags = all_zero ? SP_ALLZERO : 0;
     q.status = p.prefilter_status;
     q.cls = p.cls;
@@ -676,6 +724,8 @@ int kss_load_cluster(kss_ctx* ctx, const kss_cluster* cl) {
     for (size_t i = 0; i < 3 * N && small; i++) small = cl->alloc[i] >= 0 && cl->alloc[i] < (1ll << 46);
     for (int i = 0; i < ctx->prof.fit_n && small; i++) small = ctx->prof.fit_weight[i] >= 0 && ctx->prof.fit_weight[i] < (1ll << 20);
     ctx->small_values = small;
+    ctx->f64_cluster = F64Bounds{};
+    f64_bounds_cluster(cl, ctx->f64_cluster);
   }
   ctx->key_card_h.assign(cl->key_card, cl->key_card + cl->n_label_keys);
   ctx->key_flags_h.assign(cl->key_flags, cl->key_flags + cl->n_label_keys);
@@ -1080,7 +1130,8 @@ static int run_single(kss_ctx* ctx, const PlanNeeds& need, const DevPods& dp, in
   // shards): at 100k nodes, 98-128 k_simple shards beat 256 k_schedule shards (69.8k
   // against 44.2k pods/s)
   const bool simple_ok = staged && ctx->spod_ok && commit && !record && !keep_norm && !need.general &&
-                         ctx->dc.n_scalar == 0 && ctx->small_values && !ctx->no_simple && !(flags & KSS_SCHED_GENERAL_KERNEL);
+                         ctx->dc.n_scalar == 0 && ctx->small_values && f64_exact(ctx->f64_cluster, ctx->f64_pods, n) &&
+                         !ctx->no_simple && !(flags & KSS_SCHED_GENERAL_KERNEL);
   if (simple_ok && ctx->force_w <= 0) W = std::min(W, 64 * SX_CHUNKS);
   const int w_min = (int)((N + KSS_MAX_NPT * KSS_MAX_THREADS - 1) / (KSS_MAX_NPT * KSS_MAX_THREADS));
   W = std::max(W, w_min);
@@ -1124,7 +1175,8 @@ static int run_single(kss_ctx* ctx, const PlanNeeds& need, const DevPods& dp, in
   HIP_TRY(hipMemcpyAsync(ctx->job_buf.p, &job, sizeof(DevJob), hipMemcpyHostToDevice, ctx->stream));
   HIP_TRY(hipEventRecord(ctx->ev0, ctx->stream));
   unsigned long long* stamps = nullptr;
-  const size_t stamp_bytes = sizeof(unsigned long long) * 8 * KSS_NSTAMP_PODS;
+  // k_schedule: shard 0 only; k_simple: every shard (arrival skew of the exchanges)
+  const size_t stamp_bytes = sizeof(unsigned long long) * 8 * KSS_NSTAMP_PODS * (simple ? g.W : 1);
   if (ctx->stamps_file) {
     if ((rc = ctx->stamp_buf.ensure(stamp_bytes))) return rc;
     stamps = (unsigned long long*)ctx->stamp_buf.p;
@@ -1168,9 +1220,11 @@ static int run_single(kss_ctx* ctx, const PlanNeeds& need, const DevPods& dp, in
   ctx->recorded = record ? n : (n > 0 && !simple ? 1 : 0);
   ctx->meta_n = n;
   ctx->axis_meta_dirty = false;
-  if (stamps) {
-    std::vector<unsigned long long> h(8 * KSS_NSTAMP_PODS);
-    HIP_TRY(hipMemcpy(h.data(), stamps, stamp_bytes, hipMemcpyDeviceToHost));
+  if (stamps) {  // record: {kernel (0 k_schedule, 1 k_simple), shards} then the stamps
+    std::vector<unsigned long long> h(2 + stamp_bytes / 8);
+    h[0] = simple ? 1 : 0;
+    h[1] = simple ? (unsigned long long)g.W : 1;
+    HIP_TRY(hipMemcpy(h.data() + 2, stamps, stamp_bytes, hipMemcpyDeviceToHost));
     if (FILE* f = fopen(ctx->stamps_file, "ab")) {
       fwrite(h.data(), 8, h.size(), f);
       fclose(f);
@@ -1181,6 +1235,8 @@ static int run_single(kss_ctx* ctx, const PlanNeeds& need, const DevPods& dp, in
 
 // compact records of the staged podset for k_simple (host copy kept alive for the async upload)
 static int stage_spods(kss_ctx* ctx, const kss_podset* ps) {
+  ctx->f64_pods = F64Bounds{};
+  f64_bounds_pods(ps, ctx->f64_pods);
   ctx->spod_ok = build_spods(ps, ctx->dc.n_scalar, ctx->spod_host);
   if (!ctx->spod_ok) return 0;
   int rc = ctx->spod_buf.ensure(sizeof(SPod) * ctx->spod_host.size());
@@ -1526,6 +1582,12 @@ kss_sweep* kss_sweep_create(int32_t device, const kss_profile* prof, int32_t n_s
     const kss_cluster& cl = clusters[s];
     simple = cl.n_scalar == 0;
     for (size_t i = 0; i < 3 * (size_t)cl.n_nodes && simple; i++) simple = cl.alloc[i] >= 0 && cl.alloc[i] < (1ll << 46);
+    if (simple) {
+      F64Bounds bc, bp;
+      f64_bounds_cluster(&cl, bc);
+      f64_bounds_pods(&podsets[s], bp);
+      simple = f64_exact(bc, bp, podsets[s].n_pods);
+    }
     if (simple) simple = build_spods(&podsets[s], 0, spods[s]);
   }
   sw->simple = simple;

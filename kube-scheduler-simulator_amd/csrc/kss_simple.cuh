@@ -77,14 +77,16 @@ __host__ __device__ constexpr kss_profile default_profile_c() {
 }
 
 // Compact per-pod record of the simple path (host: build_spods): only what the
-// state-dependent part of the cycle reads.
+// state-dependent part of the cycle reads.  Quantities are integers held in doubles: the
+// host admits a batch to this path only if every operand and every sum the loop can form
+// stays below 2^53 (exact_f64 in kss_lib.hip), so all arithmetic on them is exact.
 constexpr int32_t SP_ALLZERO = 1;  // computePodResourceRequest is all zero: fitsRequest checks pods only
 struct SPod {
-  int64_t fit_req[3];  // NodeResourcesFit PreFilter request cpu / memory / ephemeral
-  int64_t snz[3];      // LeastAllocated request (non-zero defaults)
-  int64_t sreq[3];     // BalancedAllocation request
-  int64_t creq[3];     // AssumePod Requested delta
-  int64_t cnz[2];      // AssumePod NonZeroRequested delta
+  double fit_req[3];  // NodeResourcesFit PreFilter request cpu / memory / ephemeral
+  double snz[3];      // LeastAllocated request (non-zero defaults)
+  double sreq[3];     // BalancedAllocation request
+  double creq[3];     // AssumePod Requested delta
+  double cnz[2];      // AssumePod NonZeroRequested delta
   int32_t flags;       // SP_*
   int32_t status;      // kss_pod.prefilter_status
   int32_t cls;         // class_count row the pod joins (-1 none)
@@ -128,7 +130,7 @@ struct SVal {
 
 // A node row as the state-dependent filter and scores read it.
 struct DynRow {
-  int64_t alloc[3], req[3], nz[2];
+  double alloc[3], req[3], nz[2];
   double inv[3];  // RN(1 / alloc), 0 for alloc 0
   int32_t pods, allowed;
 };
@@ -151,13 +153,13 @@ __device__ __forceinline__ int32_t fit_fast(const kss_profile& prof, const SPod&
     if (i >= prof.fit_n) break;
     const int res = prof.fit_res[i];
     if (res >= KSS_RES_SCALAR0) continue;
-    const int64_t A = pick3m(res, r.alloc[0], r.alloc[1], r.alloc[2]);
-    if (A == 0) continue;
-    const int64_t base = pick3m(res, r.nz[0], r.nz[1], r.req[2]);
+    const double A = pick3d(res, r.alloc[0], r.alloc[1], r.alloc[2]);
+    if (A == 0.0) continue;
+    const double base = pick3d(res, r.nz[0], r.nz[1], r.req[2]);
     const double inv = pick3d(res, r.inv[0], r.inv[1], r.inv[2]);
-    const int64_t preq = pick3m(res, q.snz[0], q.snz[1], q.snz[2]);
+    const double preq = pick3d(res, q.snz[0], q.snz[1], q.snz[2]);
     const int32_t w = (int32_t)prof.fit_weight[i];
-    node_score += alloc_score_fast(prof.fit_strategy, base + preq, A, inv) * w;
+    node_score += alloc_score_d(prof.fit_strategy, base + preq, A, inv) * w;
     weight_sum += w;
   }
   if (weight_sum <= 1) return weight_sum == 0 ? 0 : node_score;
@@ -177,11 +179,11 @@ __device__ __forceinline__ int32_t ba_fast(const kss_profile& prof, const SPod& 
     if (i >= prof.ba_n) break;
     const int res = prof.ba_res[i];
     if (res >= KSS_RES_SCALAR0) continue;
-    const int64_t A = pick3m(res, r.alloc[0], r.alloc[1], r.alloc[2]);
-    if (A == 0) continue;
-    const int64_t R = pick3m(res, r.req[0], r.req[1], r.req[2]) + pick3m(res, q.sreq[0], q.sreq[1], q.sreq[2]);
+    const double A = pick3d(res, r.alloc[0], r.alloc[1], r.alloc[2]);
+    if (A == 0.0) continue;
+    const double R = pick3d(res, r.req[0], r.req[1], r.req[2]) + pick3d(res, q.sreq[0], q.sreq[1], q.sreq[2]);
     const double inv = pick3d(res, r.inv[0], r.inv[1], r.inv[2]);
-    double f = div_rn(R, A, inv);
+    double f = div_rn_d(R, A, inv);
     if (f > 1.0) f = 1.0;
     total += f;
     fr[i] = f;
@@ -414,18 +416,15 @@ __device__ __forceinline__ bool simple_exchange(SimpleHdr& H, unsigned long long
     best = k > best ? k : best;
   }
   best = wave_red<OP_MAX>(best);
-  int wstar = -1;
-  if (best != 0) {
-    const int g = (int)(0xFFFFFFFFu - (uint32_t)(unsigned long long)best);
-    wstar = (g - node_base) / per;
-  }
+  // the winner's shard: the one whose row range [s * per, (s + 1) * per) holds it
+  const int gl = best != 0 ? (int)(0xFFFFFFFFu - (uint32_t)(unsigned long long)best) - node_base : -1;
   // {nf, tt, na} of every shard's hypothesis, reduced in one interleaved DPP pass
   uint32_t u[6] = {0, 0, 0, 0, 0, 0};
 #pragma unroll
   for (int ch = 0; ch < SX_CHUNKS; ch++) {
     const int s = ch * 64 + lane;
     if (s >= W) continue;
-    const bool h1 = s == wstar;
+    const bool h1 = gl >= s * per && gl < s * per + per;
     u[0] += h1 ? got[ch][5] : got[ch][2];
     u[1] = max(u[1], h1 ? got[ch][6] : got[ch][3]);
     u[2] = max(u[2], h1 ? got[ch][7] : got[ch][4]);
@@ -491,7 +490,7 @@ __device__ __forceinline__ bool simple_sync(SimpleHdr& H, int& parity, long long
 // results of the next pod (slot `cap` of the results holds the candidate node
 // re-evaluated after the previous pod's commit, H1) and the static-word ring.
 struct SimpleShard {
-  int64_t* r64;   // [8][cap]: allocatable cpu/mem/eph, requested cpu/mem/eph, non-zero cpu/mem
+  double* r64;    // [8][cap]: allocatable cpu/mem/eph, requested cpu/mem/eph, non-zero cpu/mem (exact integers)
   double* inv;    // [3][cap]: RN(1 / allocatable)
   int32_t* r32;   // [2][cap]: pod count, allowed pods
   uint32_t* st;   // [3][cap]: static words of pods k, k+1, k+2 (ring slot = pod % 3)
@@ -509,7 +508,7 @@ __device__ __forceinline__ SimpleShard shard_view(uint8_t* base, int cap) {
   L.cap = cap;
   L.ring = reinterpret_cast<SPod*>(base);
   uint8_t* b = base + 3 * sizeof(SPod);
-  L.r64 = reinterpret_cast<int64_t*>(b);
+  L.r64 = reinterpret_cast<double*>(b);
   L.inv = reinterpret_cast<double*>(b + 64 * (size_t)cap);
   L.r32 = reinterpret_cast<int32_t*>(b + 88 * (size_t)cap);
   L.st = reinterpret_cast<uint32_t*>(L.r32 + 2 * (size_t)cap);
@@ -616,12 +615,12 @@ __device__ __forceinline__ void simple_schedule(DevCluster c, const SPod* __rest
 #pragma unroll
     for (int k = 0; k < 3; k++) {
       const int64_t A = c.alloc[k * N + n];
-      L.r64[k * cap + s] = A;
-      L.r64[(3 + k) * cap + s] = c.requested[k * N + n];
+      L.r64[k * cap + s] = (double)A;
+      L.r64[(3 + k) * cap + s] = (double)c.requested[k * N + n];
       L.inv[k * cap + s] = A > 0 ? 1.0 / (double)A : 0.0;
     }
-    L.r64[6 * cap + s] = c.nonzero[n];
-    L.r64[7 * cap + s] = c.nonzero[N + n];
+    L.r64[6 * cap + s] = (double)c.nonzero[n];
+    L.r64[7 * cap + s] = (double)c.nonzero[N + n];
     L.r32[s] = c.pod_count[n];
     L.r32[cap + s] = c.allowed_pods[n];
     L.st[(k0 % 3) * cap + s] = stat[(size_t)lo + s];
@@ -653,9 +652,10 @@ __device__ __forceinline__ void simple_schedule(DevCluster c, const SPod* __rest
   const int pf_per = (own + pf_n - 1) / pf_n;  // static words per prefetch lane (<= PF_MAX)
   // k = k0 - 1 is the prologue: pass A of pod k0 and the exchange of its statistics
   for (int k = k0 - 1; k < k1; k++) {
-    // diagnostic phase stamps (KSS_STAMPS_FILE), lane 0 of shard 0, first pods only
-    KSS_GLOBAL unsigned long long* sp =
-        (stamps && w == 0 && k >= k0 && k - k0 < KSS_NSTAMP_PODS / 2) ? gstamps + (size_t)(k - k0) * 16 : nullptr;
+    // diagnostic phase stamps (KSS_STAMPS_FILE): lane 0 of every shard, the first pods
+    KSS_GLOBAL unsigned long long* sp = (stamps && k >= k0 && k - k0 < KSS_NSTAMP_PODS / 2)
+                                            ? gstamps + (size_t)w * 8 * KSS_NSTAMP_PODS + (size_t)(k - k0) * 16
+                                            : nullptr;
     if (sp && tid == 0) sp[0] = wall_clock64();
     const SPod& pk = L.ring[(k + 3) % 3];
     // pod k+2: record and static words -> registers now, -> their ring slots at the end
@@ -754,9 +754,9 @@ __device__ __forceinline__ void simple_schedule(DevCluster c, const SPod* __rest
   for (int s = tid; s < own; s += nt) {
     const int n = lo + s;
 #pragma unroll
-    for (int r = 0; r < 3; r++) c.requested[(size_t)r * N + n] = L.r64[(3 + r) * cap + s];
-    c.nonzero[n] = L.r64[6 * cap + s];
-    c.nonzero[N + n] = L.r64[7 * cap + s];
+    for (int r = 0; r < 3; r++) c.requested[(size_t)r * N + n] = (int64_t)L.r64[(3 + r) * cap + s];
+    c.nonzero[n] = (int64_t)L.r64[6 * cap + s];
+    c.nonzero[N + n] = (int64_t)L.r64[7 * cap + s];
     c.pod_count[n] = L.r32[s];
   }
 }

@@ -42,6 +42,14 @@ static double div_rn(int64_t ai, int64_t bi, double y) {
   return fma(r, y, q);
 }
 
+static int32_t quot_small_d(double x, double A, double invA) {
+  int32_t q = (int32_t)(x * invA);
+  const double r = fma(-(double)q, A, x);
+  if (r < 0.0) q--;
+  else if (r >= A) q++;
+  return q;
+}
+
 int main(int argc, char** argv) {
   long n = argc > 1 ? atol(argv[1]) : 1000000;
   long bad_small = 0, bad_quot = 0, bad_div = 0;
@@ -62,6 +70,7 @@ int main(int argc, char** argv) {
     int64_t R = (int64_t)(rnd() % (uint64_t)(A + 1));
     int64_t x = (i & 1) ? (A - R) * 100 : R * 100;
     if (quot_small_i64(x, A, 1.0 / (double)A) != x / A) bad_quot++;
+    if (quot_small_d((double)x, (double)A, 1.0 / (double)A) != x / A) bad_quot++;
   }
   /* div_rn: 0 <= a < 2^53, 1 <= b < 2^46 (requested / allocatable, either order of size) */
   for (long i = 0; i < n; i++) {

@@ -16,6 +16,10 @@ for step in "$@"; do
     c3)     timeout -k 10 300 python -u bench.py --config 3 --no-traffic --no-cpu > $OUT/c3.json 2> $OUT/c3.err ;;
     c5)     timeout -k 10 300 python -u bench.py --scenarios 512 --no-traffic > $OUT/c5.json 2> $OUT/c5.err ;;
     axis)   timeout -k 10 300 python -u bench.py --node-axis --no-traffic > $OUT/axis.json 2> $OUT/axis.err ;;
+    sweep)  for nps in ${SWEEP_NPS:-64 96 128 192 256}; do
+              KSS_NODES_PER_SHARD=$nps timeout -k 10 120 python -u bench.py --steps 2 --warmup 1 --no-cpu --no-traffic > $OUT/sweep_n$nps.json 2>> $OUT/sweep.err
+              python -c "import json,sys; d=json.load(open('$OUT/sweep_n$nps.json')); print('nps', $nps, d['geometry'], round(d['pods_per_s']), 'pods/s', round(d['us_per_pod'],3), 'us/pod')" >> $OUT/sweep.txt
+            done ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
   echo "step $step ok"

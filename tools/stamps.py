@@ -1,41 +1,66 @@
-"""Summarise KSS_STAMPS_FILE dumps: median per-phase durations (µs) of the first pods of each launch.
-Phases: 0 pod start, 1 plan, 2 filter pass done, 3 filter exchange done, 4 normalize pass done,
-5 argmax exchange done, 6 commit + barrier done."""
+"""Summarise KSS_STAMPS_FILE dumps (s_memrealtime, 100 MHz; one record per launch:
+{kernel, shards} then the stamps).
+
+k_schedule (shard 0, 8 stamps per pod): 0 pod start, 1 plan, 2 filter pass done, 3 filter
+exchange done, 4 normalize pass done, 5 argmax exchange done, 6 commit + barrier done.
+k_simple (every shard, 16 per pod): 0 start, 1 pass B, 2 best-key reduction, 3 pass A,
+4 statistics reduction (= publish), 5 exchange + barrier, 6 commit + ring store.  For
+k_simple the arrival skew of the exchange is reported: per pod, the spread of the
+shards' publish times, and the wait from the LAST publish to each shard's completion
+(propagation + reductions)."""
 import sys
 
 import numpy as np
 
 NAMES = ["plan", "filter", "x_filter", "normalize", "x_argmax", "commit"]
-# k_simple: 0 start, 1 pass B, 2 best-key reduction, 3 pass A, 4 statistics reduction,
-# 5 exchange + barrier, 6 commit + ring store
 NAMES_SIMPLE = ["passB", "red_best", "passA", "red_stats", "xchg", "commit"]
+NSTAMP_PODS = 256
 
 
-def summarise_simple(path):
-    """k_simple records 16 stamps per pod: 0..6 the loop phases, 7 eval start (lane 0 of
-    shard 0, first slot), 8 filters done, 9 TT+NA scores, 10 Fit score, 11 BA score."""
-    a = np.fromfile(path, dtype=np.uint64).reshape(-1, 16).astype(np.int64)
-    a = a[(a[:, 0] > 0) & (a[:, 6] > 0)]
-    d = np.diff(a[:, :7], axis=1) / 100.0
-    out = " ".join(f"{n}={m:.2f}" for n, m in zip(NAMES_SIMPLE, np.median(d, axis=0)))
-    e = a[a[:, 11] > 0]
-    if len(e):
-        sub = {"filters": (7, 8), "tt_na": (8, 9), "fit": (9, 10), "ba": (10, 11), "after_eval": (11, 3)}
-        out += " || " + " ".join(f"{k}={np.median(e[:, j] - e[:, i]) / 100.0:.2f}" for k, (i, j) in sub.items())
-    tot = (a[:, 6] - a[:, 0]) / 100.0
-    return out + f" | pod={np.median(tot):.2f} us (n={len(a)})"
+def records(path):
+    raw = np.fromfile(path, dtype=np.uint64)
+    out, i = [], 0
+    while i + 2 <= raw.size:
+        kind, w = int(raw[i]), int(raw[i + 1])
+        n = 8 * NSTAMP_PODS * (w if kind == 1 else 1)
+        out.append((kind, w, raw[i + 2:i + 2 + n].astype(np.int64)))
+        i += 2 + n
+    return out
 
 
 def summarise(path):
-    if "simple" in path:
-        return summarise_simple(path)
-    names = NAMES
-    a = np.fromfile(path, dtype=np.uint64).reshape(-1, 8)
-    a = a[(a[:, 0] > 0) & (a[:, 6] > 0)]
-    d = np.diff(a[:, :7].astype(np.int64), axis=1) / 100.0  # 100 MHz -> µs
-    tot = (a[:, 6].astype(np.int64) - a[:, 0].astype(np.int64)) / 100.0
-    med = np.median(d, axis=0)
-    return " ".join(f"{n}={m:.2f}" for n, m in zip(names, med)) + f" | pod={np.median(tot):.2f} us (n={len(a)})"
+    lines = []
+    for kind, w, a in records(path):
+        if kind == 0:
+            a = a.reshape(-1, 8)
+            a = a[(a[:, 0] > 0) & (a[:, 6] > 0)]
+            d = np.diff(a[:, :7], axis=1) / 100.0
+            tot = (a[:, 6] - a[:, 0]) / 100.0
+            lines.append("k_schedule " + " ".join(f"{n}={m:.2f}" for n, m in zip(NAMES, np.median(d, axis=0)))
+                         + f" | pod={np.median(tot):.2f} us (n={len(a)})")
+            continue
+        a = a.reshape(w, NSTAMP_PODS // 2, 16)
+        s0 = a[0]
+        ok = (s0[:, 0] > 0) & (s0[:, 6] > 0)
+        d = np.diff(s0[ok, :7], axis=1) / 100.0
+        tot = (s0[ok, 6] - s0[ok, 0]) / 100.0
+        line = (f"k_simple W={w} shard0: " + " ".join(f"{n}={m:.2f}" for n, m in zip(NAMES_SIMPLE, np.median(d, axis=0)))
+                + f" | pod={np.median(tot):.2f} us (n={ok.sum()})")
+        pub, done = a[:, :, 4], a[:, :, 5]
+        good = (pub > 0).all(axis=0) & (done > 0).all(axis=0)
+        if good.sum():
+            p, dn = pub[:, good], done[:, good]
+            last = p.max(axis=0)
+            skew = (last - p.min(axis=0)) / 100.0
+            after = (dn - last[None, :]) / 100.0
+            late = np.bincount(p.argmax(axis=0), minlength=w)
+            line += (f"\n  exchange: publish spread median {np.median(skew):.2f} us (p90 {np.percentile(skew, 90):.2f}),"
+                     f" last publish -> done median {np.median(after):.2f} us (min {np.median(after.min(axis=0)):.2f}),"
+                     f" latest shard most often {int(late.argmax())} ({late.max()}/{good.sum()} pods)")
+            pa = (a[:, :, 3] - a[:, :, 0]) / 100.0
+            line += f"\n  start -> passA done per shard: median {np.median(pa[:, good]):.2f} us, max over shards (median) {np.median(pa[:, good].max(axis=0)):.2f}"
+        lines.append(line)
+    return "\n".join(lines)
 
 
 if __name__ == "__main__":
