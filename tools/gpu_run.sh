@@ -14,6 +14,9 @@ for step in "$@"; do
     stamps) rm -f $OUT/*.bin; KSS_STAMPS_FILE=$OUT/simple_c2.bin timeout -k 10 120 python -u bench.py --steps 1 --warmup 0 --pods 2000 --no-cpu --no-traffic > /dev/null && python tools/stamps.py $OUT/*.bin > $OUT/stamps.txt ;;
     prof)   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/kt -o kt -- python -u bench.py --no-cpu --no-traffic > $OUT/kt.log 2>&1 ;;
     c3)     timeout -k 10 300 python -u bench.py --config 3 --no-traffic --no-cpu > $OUT/c3.json 2> $OUT/c3.err ;;
+    c3stamps) rm -f $OUT/general_c3.bin; KSS_STAMPS_FILE=$OUT/general_c3.bin timeout -k 10 120 python -u bench.py --config 3 --steps 1 --warmup 0 --pods 1000 --no-cpu --no-traffic > /dev/null && python tools/stamps.py $OUT/general_c3.bin > $OUT/c3_stamps.txt ;;
+    c3prof) timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/c3kt -o kt -- python -u bench.py --config 3 --pods 2000 --no-cpu --no-traffic > $OUT/c3kt.log 2>&1 ;;
+    coopprof) KSS_COOP_LAUNCH=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/coopkt -o kt -- python -u bench.py --config 3 --pods 500 --steps 1 --warmup 0 --no-cpu --no-traffic > $OUT/coopkt.log 2>&1; echo "coop rc=$?" >> $OUT/coopkt.log ;;
     c5)     timeout -k 10 300 python -u bench.py --scenarios 512 --no-traffic > $OUT/c5.json 2> $OUT/c5.err ;;
     axis)   timeout -k 10 300 python -u bench.py --node-axis --no-traffic > $OUT/axis.json 2> $OUT/axis.err ;;
     sweep)  for nps in ${SWEEP_NPS:-64 96 128 192 256}; do
