@@ -417,14 +417,15 @@ int kss_axis_commit(kss_ctx* ctx, int32_t pod_index, const int64_t* key_dev, con
 
 /* timing of the last kss_schedule_batch / kss_eval_pod device work (HIP events on the work stream) */
 int kss_last_timing(kss_ctx* ctx, double* device_ms, int32_t* launches);
-/* device time of the sequential-loop kernel alone in the last batch: the k_simple
- * launch(es) without the k_static precompute (k_schedule batches: the whole batch) */
+/* device time of the sequential-loop kernel alone in the last batch: the k_simple /
+ * k_spread launch(es) without the k_static precompute (k_schedule batches: the whole batch) */
 int kss_last_loop_timing(kss_ctx* ctx, double* loop_ms);
 /* launch geometry of the last scheduling launch: out[0] shards (workgroups) per cluster,
  * out[1] threads per workgroup, out[2] node slots per lane */
 int kss_last_geometry(kss_ctx* ctx, int32_t* out3);
 /* kernel of the last scheduling launch: 0 general (k_schedule), 1 compact (k_simple:
- * batches without spread / inter-pod programs and without a record); <0 on error */
+ * batches without spread / inter-pod programs and without a record), 2 k_spread (batches
+ * with programs, without a record); <0 on error */
 int kss_last_kernel(kss_ctx* ctx);
 /* outcome of pods [first, first+n) of the last scheduling launch, recorded or not:
  * out[5*i .. 5*i+4] = chosen, n_feasible, scored, status, best_total (kss_pod_result) */
@@ -449,6 +450,10 @@ int kss_format_annotations_ex(const kss_names* names, const kss_profile* prof, c
                               int32_t n_nodes, int32_t n_taints, int32_t n_scalar, char* buf, size_t cap, size_t* need);
 /* sizeof() of every ABI struct, in header order; returns the count written (ABI self-check) */
 int kss_abi_sizes(int32_t* out, int32_t n);
+/* Test support: y[i] = the device restatement of Go math.Log (kss_spread.cuh go_log_dev,
+ * PodTopologySpread's topologyNormalizingWeight in k_spread) at x[i], i < n, evaluated on
+ * `device`; host arrays.  Compared bitwise with the host port (kss_go_log_c) by the tests. */
+int kss_device_go_log(int32_t device, const double* x, double* y, int32_t n);
 
 /* ---- synthetic clusters (SplitMix64, seed 0x5EED0000 + config) */
 typedef struct kss_synth {

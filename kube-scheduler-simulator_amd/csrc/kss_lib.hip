@@ -13,6 +13,10 @@
 //   k_simple     the sequential loop of those batches (no result record): node rows
 //                in LDS, compact pod records and static words in LDS rings, only the
 //                state-dependent filter / scores per pod, one exchange per pod.
+//   k_spread     the sequential loop of batches WITH spread / inter-pod-affinity programs
+//                (no result record): node rows, label ids, the pod's count rows and
+//                the launch's commits in LDS, host-resolved pod programs (GPod),
+//                32-bit exchanges (kss_spread.cuh).
 //   k_commit     one lane: AssumePod / ForgetPod delta on one node row.
 #include <hip/hip_runtime.h>
 
@@ -30,6 +34,7 @@
 #include "kss_host.h"
 #include "kss_sched.cuh"
 #include "kss_simple.cuh"
+#include "kss_spread.cuh"
 #include "kss_axis.cuh"
 
 using namespace kss;
@@ -79,7 +84,8 @@ struct DevJob {
   int32_t* chosen;
   PodMeta* meta;
   const SPod* spods;  // k_simple: compact pod records [n_pods]
-  uint32_t* stat;     // k_static -> k_simple: static words of the current pod chunk [chunk][N]
+  uint32_t* stat;     // k_static -> k_simple / k_spread: static words of the current pod chunk [chunk][N]
+  const GPod* gpods;  // k_spread: host-resolved pod programs [n_pods]
   kss_profile prof;   // k_simple<false>: staged word by word into LDS (a by-value kernel argument would land in scratch)
 };
 
@@ -177,6 +183,27 @@ __global__ __launch_bounds__(KSS_MAX_THREADS) void k_simple(const DevJob* __rest
                   gran ? gran + (size_t)ji * 2 * W * SX_VALS : nullptr, err, ji == 0 ? stamps : nullptr, smem);
 }
 
+// grid = W (one cluster); each shard's nodes live in LDS (cap slots); bins_cap: histogram +
+// presence values of the exchange vector.  DEF: the v1.26 default profile, folded.
+template <bool DEF>
+__global__ __launch_bounds__(KSS_MAX_THREADS) void k_spread(const DevJob* __restrict__ jobs, int W, int cap, int bins_cap,
+                                                            int rows, int k0, int k1, unsigned long long* gran, int* err) {
+  extern __shared__ __attribute__((aligned(16))) long long smem[];
+  const int ji = blockIdx.x / W, w = blockIdx.x % W;
+  const DevJob job = jobs[ji];
+  constexpr kss_profile def_prof = default_profile_c();
+  SpreadHdr& H = *reinterpret_cast<SpreadHdr*>(smem);
+  if (!DEF) {
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(&jobs[ji].prof);
+    uint32_t* dst = reinterpret_cast<uint32_t*>(&H.prof);
+    for (int i = threadIdx.x; i < (int)(sizeof(kss_profile) / 4); i += blockDim.x) dst[i] = src[i];
+    __syncthreads();
+  }
+  const kss_profile& P = DEF ? def_prof : H.prof;
+  spread_schedule(job.c, job.gpods, job.stat, job.P.ints, k0, min(k1, job.n_pods), job.chosen, job.meta, P, W, w, cap,
+                  bins_cap, rows, gran ? gran + (size_t)ji * 2 * W * G_XW : nullptr, err, smem);
+}
+
 // Class / term counts of the chosen nodes of pods [k0, min(k1, n_pods)) of every job
 // (grid: x = 256-pod tiles, y = job).
 __global__ __launch_bounds__(256) void k_counts(const DevJob* __restrict__ jobs, int k0, int k1) {
@@ -207,6 +234,11 @@ __global__ __launch_bounds__(256) void k_static(const DevJob* __restrict__ jobs,
     if (k >= kend) break;
     stat[(size_t)(k - k0) * N + n] = static_word(c, P, P.pods[k], prof, n, flags, th, ts);
   }
+}
+
+__global__ void k_go_log(const double* x, double* y, int n) {
+  const int i = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+  if (i < n) y[i] = go_log_dev(x[i]);
 }
 
 __global__ void k_commit(DevCluster c, DevPods P, int pi, int local, int sign) {
@@ -240,6 +272,18 @@ struct DevBuf {
 struct F64Bounds {
   double max_req0 = 0, max_nz0 = 0, max_creq = 0, max_cnz = 0, max_pod = 0;
   bool neg = false;
+};
+
+// What the staged batch asks of k_spread (the host side of the GPod plans).
+struct GpodNeeds {
+  int bins_cap = 0;      // max histogram + presence bins of a pod
+  int rows = 1;          // max count rows of a pod (LDS rows of the prefetched counts)
+  int max_mult = 1;      // max commits one pod adds to one count row
+  int max_own = 0;       // max term rows one pod adds
+  int max_len = 1;       // max rows summed by one constraint / entry
+  int64_t coef_sum = 0;  // max Σ|coef| of a pod's InterPodAffinity score entries
+  int max_soft = 0;      // max ScheduleAnyway constraints of a pod with more than one
+  int64_t max_skew = 0;  // their largest maxSkew
 };
 
 // Per-batch LDS / exchange sizing: the host restatement of make_plan's bin counts.
@@ -294,8 +338,19 @@ struct kss_ctx {
   DevBuf spod_buf, stat_buf;
   std::vector<SPod> spod_host;
   bool spod_ok = false;
+  // host-resolved programs of the staged pods for k_spread (gpod_ok false: k_schedule)
+  DevBuf gpod_buf;
+  std::vector<GPod> gpod_host;
+  bool gpod_ok = false;
+  GpodNeeds gneed;
+  bool no_spread = false;     // KSS_NO_SPREAD: batches with programs always take k_schedule
+  double count_bound0 = 0;    // max(Σ class_count, Σ term_count) of the loaded snapshot
+  double count_bound = 0;     // the same, plus every commit since (spread_bounds_ok)
+  int max_allowed = 0;        // max AllowedPodNumber of the loaded snapshot
+  int staged_max_own = 0;     // max own term rows of a staged pod
+  std::vector<int32_t> key_empty_h;
   bool no_simple = false;  // KSS_NO_SIMPLE: always launch k_schedule
-  int last_kernel = 0;     // 0 k_schedule, 1 k_simple
+  int last_kernel = 0;     // 0 k_schedule, 1 k_simple, 2 k_spread
   int meta_n = 0;          // pods with an outcome in meta_host
   bool small_values = false;  // every allocatable cpu/mem/eph < 2^46: k_simple's divisions stay below 2^53
   F64Bounds f64_cluster, f64_pods;  // k_simple exactness bounds of the loaded snapshot / staged pods
@@ -430,34 +485,194 @@ bool f64_exact(const F64Bounds& c, const F64Bounds& p, int n_pods) {
          c.max_nz0 + (double)n_pods * p.max_cnz < lim;
 }
 
-// Compact records of every pod of a (validated) podset for k_simple (kss_simple.cuh
-// SPod); false when some pod needs k_schedule: spread / inter-pod-affinity programs, or
-// preferred NodeAffinity weights whose sum does not fit the static word's 16 bits.
+// Compact record of one pod (kss_simple.cuh SPod); false when the preferred NodeAffinity
+// weights do not fit the static word's 20 bits.
+bool fill_spod(const kss_podset* ps, const kss_pod& p, int n_scalar, SPod& q) {
+  int64_t wsum = 0;
+  for (int t = 0; t < p.pref_len; t++) wsum += std::max(0, ps->terms[p.pref_off + t].weight);
+  if (wsum > 0xFFFFF) return false;  // static word: 20 bits of raw NodeAffinity
+  q = SPod{};
+  bool all_zero = true;
+  for (int r = 0; r < 3 + n_scalar; r++) all_zero &= p.fit_request[r] == 0;
+  for (int r = 0; r < 3; r++) {
+    q.fit_req[r] = (double)p.fit_request[r];
+    q.snz[r] = (double)p.score_req_nz[r];
+    q.sreq[r] = (double)p.score_req[r];
+    q.creq[r] = (double)p.commit_req[r];
+  }
+  q.cnz[0] = (double)p.commit_nz[0];
+  q.cnz[1] = (double)p.commit_nz[1];
+  q.flags = all_zero ? SP_ALLZERO : 0;
+  q.status = p.prefilter_status;
+  q.cls = p.cls;
+  q.own_off = p.own_terms_off;
+  q.own_len = p.own_terms_len;
+  return true;
+}
+
+// Compact records of every pod of a (validated) podset for k_simple; false when some pod
+// needs another kernel (spread / inter-pod-affinity programs, or fill_spod refuses it).
 bool build_spods(const kss_podset* ps, int n_scalar, std::vector<SPod>& out) {
   out.assign((size_t)std::max(ps->n_pods, 1), SPod{});
   for (int i = 0; i < ps->n_pods; i++) {
     const kss_pod& p = ps->pods[i];
     if (p.n_hard | p.n_soft | p.ipa_len) return false;
-    int64_t wsum = 0;
-    for (int t = 0; t < p.pref_len; t++) wsum += std::max(0, ps->terms[p.pref_off + t].weight);
-    if (wsum > 0xFFFF) return false;
-    SPod& q = out[(size_t)i];
-    bool all_zero = true;
-    for (int r = 0; r < 3 + n_scalar; r++) all_zero &= p.fit_request[r] == 0;
-    for (int r = 0; r < 3; r++) {
-      q.fit_req[r] = (double)p.fit_request[r];
-      q.snz[r] = (double)p.score_req_nz[r];
-      q.sreq[r] = (double)p.score_req[r];
-      q.creq[r] = (double)p.commit_req[r];
-    }
-    q.cnz[0] = (double)p.commit_nz[0];
-    q.cnz[1] = (double)p.commit_nz[1];
-    q.flags = all_zero ? SP_ALLZERO : 0;
-    q.status = p.prefilter_status;
-    q.cls = p.cls;
-    q.own_off = p.own_terms_off;
-    q.own_len = p.own_terms_len;
+    if (!fill_spod(ps, p, n_scalar, out[(size_t)i])) return false;
   }
+  return true;
+}
+
+// Host-resolved programs (kss_spread.cuh GPod) of every pod of a validated podset: the
+// restatement of make_plan (kss_sched.cuh) plus the table of count rows each constraint and
+// entry sums.  False when some pod exceeds the record's fixed tables or an exchange's
+// payload (the batch then runs on k_schedule).
+bool build_gpods(const kss_podset* ps, int n_scalar, int n_classes, const int32_t* key_card, const uint32_t* key_flags,
+                 const int32_t* key_empty, std::vector<GPod>& out, GpodNeeds& need) {
+  out.assign((size_t)std::max(ps->n_pods, 1), GPod{});
+  need = GpodNeeds{};
+  for (int i = 0; i < ps->n_pods; i++) {
+    const kss_pod& p = ps->pods[i];
+    GPod& g = out[(size_t)i];
+    if (!fill_spod(ps, p, n_scalar, g.dyn)) return false;
+    if (p.n_hard > MAXH || p.n_soft > MAXS || p.ipa_len > G_IPA) return false;
+    g.pflags = (int32_t)p.flags;
+    g.n_hard = p.n_hard;
+    g.n_soft = p.n_soft;
+    g.n_ipa = p.ipa_len;
+    int nref = 0;
+    auto row_of = [&](bool term, int r) -> int {
+      const int32_t code = term ? ((1 << 30) | r) : r;
+      for (int j = 0; j < g.n_rows; j++)
+        if (g.row[j] == code) return j;
+      if (g.n_rows >= G_ROWS) return -1;
+      g.row[g.n_rows] = code;
+      g.rowid[g.n_rows] = term ? n_classes + r : r;
+      return g.n_rows++;
+    };
+    auto refs = [&](bool term, int off, int len, int32_t& ri_off, int32_t& ri_len) -> bool {
+      ri_off = nref;
+      ri_len = len;
+      need.max_len = std::max(need.max_len, len);
+      for (int j = 0; j < len; j++) {
+        const int x = row_of(term, ps->ints[off + j]);
+        if (x < 0 || nref >= G_RIDX) return false;
+        g.ridx[nref++] = (int16_t)x;
+      }
+      return true;
+    };
+    int off = 0, poff = 0;
+    bool stats = false;
+    const kss_spread* sp = ps->spreads + p.spread_off;
+    for (int c = 0; c < p.n_hard + p.n_soft; c++) {
+      const kss_spread& s = sp[c];
+      GSpread& d = g.sp[c];
+      d.key = s.key;
+      d.max_skew = s.max_skew;
+      d.self_match = s.self_match;
+      d.flags = s.flags;
+      if (!refs(false, s.cls_off, s.cls_len, d.ri_off, d.ri_len)) return false;
+      d.empty = key_empty[s.key];
+      d.nb = key_card[s.key] + 1;
+      d.off = d.poff = -1;
+      d.mode = SOFT_HOST;
+    }
+    for (int c = 0; c < p.n_hard; c++) {  // make_plan: hard bins first
+      GSpread& d = g.sp[c];
+      stats = true;
+      if (!(key_flags[d.key] & KSS_KEY_UNIQUE)) {
+        d.off = off;
+        d.poff = poff;
+        off += d.nb;
+        poff += d.nb;
+      }
+    }
+    g.hard_pbins = poff;
+    for (int c = p.n_hard; c < p.n_hard + p.n_soft; c++) {
+      GSpread& d = g.sp[c];
+      if (key_flags[d.key] & KSS_KEY_HOSTNAME) {
+        d.mode = SOFT_HOST;
+      } else if (key_flags[d.key] & KSS_KEY_UNIQUE) {
+        d.mode = SOFT_DIRECT;
+      } else {
+        d.mode = SOFT_HIST;
+        d.off = off;
+        d.poff = poff;
+        off += d.nb;
+        poff += d.nb;
+        stats = true;
+      }
+      if (p.n_soft > 1) {
+        need.max_soft = std::max(need.max_soft, (int)p.n_soft);
+        need.max_skew = std::max<int64_t>(need.max_skew, std::abs((int64_t)d.max_skew));
+      }
+    }
+    const kss_ipa* ip = ps->ipa + p.ipa_off;
+    int64_t csum = 0;
+    for (int e = 0; e < p.ipa_len; e++) {
+      const kss_ipa& en = ip[e];
+      GIpa& d = g.ipa[e];
+      int k = -1;
+      for (int j = 0; j < g.n_keys; j++)
+        if (g.key[j] == en.key) k = j;
+      if (k < 0) {
+        if (g.n_keys >= MAXK) return false;
+        k = g.n_keys++;
+        g.key[k] = en.key;
+        for (int h = 0; h < 4; h++) g.hoff[k][h] = -1;
+      }
+      d.kind = en.kind;
+      d.key = en.key;
+      d.coef = en.coef;
+      d.slot = k;
+      const bool term = en.kind == KSS_IPA_EXISTING_ANTI || en.kind == KSS_IPA_SCORE_TERM;
+      if (!refs(term, en.row_off, en.row_len, d.ri_off, d.ri_len)) return false;
+      if (en.kind == KSS_IPA_SCORE_CLASS || en.kind == KSS_IPA_SCORE_TERM) csum += std::abs((int64_t)en.coef);
+      stats = true;
+    }
+    for (int k = 0; k < g.n_keys; k++) {  // one histogram per (key, kind) some entry feeds
+      if (key_flags[g.key[k]] & KSS_KEY_UNIQUE) continue;
+      for (int h = 0; h < 4; h++) {
+        bool used = false;
+        for (int e = 0; e < p.ipa_len; e++) {
+          const int kind = ip[e].kind;
+          const int eh = kind == KSS_IPA_EXISTING_ANTI ? 0 : (kind == KSS_IPA_REQ_AFFINITY ? 1 : (kind == KSS_IPA_REQ_ANTI ? 2 : 3));
+          used |= g.ipa[e].slot == k && eh == h;
+        }
+        if (used) {
+          g.hoff[k][h] = off;
+          off += key_card[g.key[k]] + 1;
+        }
+      }
+    }
+    g.total_bins = off;
+    g.total_pbins = poff;
+    g.need_stats = stats ? 1 : 0;
+    if (off + poff > LDS_BINS) return false;
+    if (MAXH + 1 + off + g.hard_pbins > G_XW || 13 + (poff - g.hard_pbins) > G_XW) return false;
+    need.bins_cap = std::max(need.bins_cap, off + poff);
+    need.rows = std::max(need.rows, (int)g.n_rows);
+    need.coef_sum = std::max(need.coef_sum, csum);
+    need.max_own = std::max(need.max_own, (int)p.own_terms_len);
+    for (int j = 0; j < p.own_terms_len; j++) {  // commits of one pod to one term row
+      int m = 0;
+      for (int x = 0; x < p.own_terms_len; x++) m += ps->ints[p.own_terms_off + x] == ps->ints[p.own_terms_off + j];
+      need.max_mult = std::max(need.max_mult, m);
+    }
+  }
+  return true;
+}
+
+// k_spread keeps counts, histograms and InterPodAffinity scores in 32 bits: with `total`
+// a bound on every count row's sum over the cluster after the batch, a constraint's count
+// is below total * max_len, a score below coef_sum times that, and a multi-constraint
+// PodTopologySpread raw score below max_soft * (count * log(N + 2) + maxSkew).
+bool spread_bounds_ok(const GpodNeeds& q, double total, int N) {
+  const double cnt = total * (double)q.max_len;
+  const double lim = 2147483647.0;
+  if (cnt >= lim / 2) return false;
+  if ((double)q.coef_sum * cnt >= lim) return false;
+  if (q.max_soft > 1 && (double)q.max_soft * (cnt * std::log((double)N + 2.0) + (double)q.max_skew + 1.0) >= lim)
+    return false;
   return true;
 }
 
@@ -649,6 +864,7 @@ kss_ctx* kss_create(const kss_config* cfg, const kss_profile* prof) {
   if (const char* e = getenv("KSS_SHARDS")) ctx->force_w = std::max(0, atoi(e));
   ctx->stamps_file = getenv("KSS_STAMPS_FILE");
   ctx->no_simple = getenv("KSS_NO_SIMPLE") != nullptr;
+  ctx->no_spread = getenv("KSS_NO_SPREAD") != nullptr;
   if (const char* e = getenv("KSS_AXIS_BLOCKS")) ctx->axis_max_blocks = std::max(0, atoi(e));
   ctx->axis_no_fold = getenv("KSS_AXIS_NO_FOLD") != nullptr;
   if (const char* e = getenv("KSS_NODES_PER_SHARD")) ctx->nodes_per_shard = std::max(1, atoi(e));
@@ -729,6 +945,17 @@ int kss_load_cluster(kss_ctx* ctx, const kss_cluster* cl) {
   }
   ctx->key_card_h.assign(cl->key_card, cl->key_card + cl->n_label_keys);
   ctx->key_flags_h.assign(cl->key_flags, cl->key_flags + cl->n_label_keys);
+  ctx->key_empty_h.assign(cl->key_empty, cl->key_empty + cl->n_label_keys);
+  {
+    double sc = 0, st = 0;
+    if (cl->class_count)
+      for (size_t i = 0; i < (size_t)cl->n_classes * N; i++) sc += std::abs((double)cl->class_count[i]);
+    if (cl->term_count)
+      for (size_t i = 0; i < (size_t)cl->n_terms * N; i++) st += std::abs((double)cl->term_count[i]);
+    ctx->count_bound0 = ctx->count_bound = std::max(sc, st);
+    ctx->max_allowed = 0;
+    for (size_t i = 0; i < N; i++) ctx->max_allowed = std::max(ctx->max_allowed, cl->allowed_pods[i]);
+  }
   ctx->loaded = true;
   ctx->recorded = 0;
   ctx->meta_n = 0;
@@ -862,6 +1089,7 @@ int kss_reset_node_state(kss_ctx* ctx) {
   std::lock_guard<std::mutex> lk(ctx->mu);
   HIP_TRY(hipSetDevice(ctx->cfg.device));
   void* dst[5] = {ctx->dc.requested, ctx->dc.nonzero, ctx->dc.pod_count, ctx->dc.class_count, ctx->dc.term_count};
+  ctx->count_bound = ctx->count_bound0;
   for (int i = 0; i < 5; i++)
     if (ctx->mut_bytes[i])
       HIP_TRY(hipMemcpyAsync(dst[i], (char*)ctx->pristine_buf.p + ctx->pristine_off[i], ctx->mut_bytes[i],
@@ -1108,7 +1336,62 @@ static int launch_simple(hipStream_t st, const Geometry& g, int n_jobs, const De
   return 0;
 }
 
-// run k_schedule / k_simple on the loaded cluster for pods [0, n); results stay on the device
+static size_t spread_lds(const Geometry& g, const GpodNeeds& q, int n_keys, int n_rowids) {
+  return spread_lds_bytes(g.npt * g.threads, q.bins_cap, n_keys, n_rowids, q.rows);
+}
+
+static bool spread_fits(const Geometry& g, const GpodNeeds& q, int n_keys, int n_rowids) {
+  const int pf_n = g.threads > 64 ? g.threads - 64 : g.threads;  // prefetch lanes (kss_spread.cuh)
+  return (g.npt * g.threads + pf_n - 1) / pf_n <= G_PF && spread_lds(g, q, n_keys, n_rowids) <= KSS_LDS_BUDGET;
+}
+
+// Pods per k_spread launch: the static-word budget, and at most 255 commits of the launch
+// to one (count row, node) (the LDS commit table holds bytes) unless NodeResourcesFit's pod
+// limit already bounds them.
+static int spread_chunk(const kss_ctx* ctx, const GpodNeeds& q, size_t N, int n) {
+  int c = static_chunk(N, n);
+  const bool pod_limit = ((ctx->prof.filter_enabled >> KSS_F_NODE_RESOURCES_FIT) & 1u) != 0;
+  if (!pod_limit || (int64_t)ctx->max_allowed * q.max_mult > 255) c = std::min(c, std::max(1, 255 / q.max_mult));
+  return c;
+}
+
+// k_static + k_spread over pods [0, n_pods) of one job, `chunk` pods at a time (node state
+// and counts back in HBM between launches).  ev (optional): 2 events per chunk.
+static int launch_spread(hipStream_t st, const Geometry& g, const GpodNeeds& q, int n_keys, int n_rowids,
+                         const DevJob* jobs, const kss_profile& prof, int n_pods, int max_nodes, int chunk,
+                         unsigned long long* gran, size_t gran_bytes, int* err, hipEvent_t* ev = nullptr) {
+  int cap = g.npt * g.threads, bins_cap = q.bins_cap, rows = q.rows;
+  const size_t shmem = spread_lds(g, q, n_keys, n_rowids);
+  const bool def = same_profile(prof, default_profile_c());
+  const void* fn = def ? (const void*)k_spread<true> : (const void*)k_spread<false>;
+  HIP_TRY(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shmem));
+  const dim3 grid((unsigned)g.W), block((unsigned)g.threads);
+  kss_profile pr = prof;
+  int W = g.W;
+  for (int k0 = 0; k0 < n_pods; k0 += chunk) {
+    int k1 = std::min(n_pods, k0 + chunk);
+    const dim3 sgrid((unsigned)((max_nodes + 255) / 256), (unsigned)((k1 - k0 + STATIC_PODS - 1) / STATIC_PODS), 1u);
+    if (def)
+      hipLaunchKernelGGL(k_static<true>, sgrid, dim3(256), 0, st, jobs, pr, k0, k1);
+    else
+      hipLaunchKernelGGL(k_static<false>, sgrid, dim3(256), 0, st, jobs, pr, k0, k1);
+    HIP_TRY(hipGetLastError());
+    if (gran && k0 > 0) HIP_TRY(hipMemsetAsync(gran, 0, gran_bytes, st));
+    void* args[] = {(void*)&jobs, (void*)&W,  (void*)&cap,  (void*)&bins_cap, (void*)&rows,
+                    (void*)&k0,   (void*)&k1, (void*)&gran, (void*)&err};
+    const int ci = k0 / chunk;
+    if (ev) HIP_TRY(hipEventRecord(ev[2 * ci], st));
+    if (g.W > 1) {
+      if (int rc = launch_resident(fn, grid, block, args, shmem, st)) return rc;
+    } else {
+      HIP_TRY(hipLaunchKernel(fn, grid, block, args, shmem, st));
+    }
+    if (ev) HIP_TRY(hipEventRecord(ev[2 * ci + 1], st));
+  }
+  return 0;
+}
+
+// run k_schedule / k_simple / k_spread on the loaded cluster for pods [0, n); results stay on the device
 static int run_single(kss_ctx* ctx, const PlanNeeds& need, const DevPods& dp, int n, bool commit, bool record,
                       bool keep_norm, uint32_t flags, int32_t* chosen_out, bool staged = false) {
   const size_t N = (size_t)ctx->dc.N;
@@ -1133,9 +1416,15 @@ static int run_single(kss_ctx* ctx, const PlanNeeds& need, const DevPods& dp, in
                          ctx->dc.n_scalar == 0 && ctx->small_values && f64_exact(ctx->f64_cluster, ctx->f64_pods, n) &&
                          !ctx->no_simple && !(flags & KSS_SCHED_GENERAL_KERNEL);
   if (simple_ok && ctx->force_w <= 0) W = std::min(W, 64 * SX_CHUNKS);
+  // a batch with programs on k_spread: 32-bit counts and scores (spread_bounds_ok)
+  const double count_total = ctx->count_bound + (commit ? (double)n * (1.0 + ctx->staged_max_own) : 0.0);
+  const bool spread_ok = staged && ctx->gpod_ok && commit && !record && !keep_norm && need.general &&
+                         ctx->dc.n_scalar == 0 && ctx->small_values && f64_exact(ctx->f64_cluster, ctx->f64_pods, n) &&
+                         !ctx->no_simple && !ctx->no_spread && !(flags & KSS_SCHED_GENERAL_KERNEL) &&
+                         spread_bounds_ok(ctx->gneed, count_total, (int)N);
   const int w_min = (int)((N + KSS_MAX_NPT * KSS_MAX_THREADS - 1) / (KSS_MAX_NPT * KSS_MAX_THREADS));
   W = std::max(W, w_min);
-  if (W > 1 && need.xw > XW_MAX) {
+  if (W > 1 && need.xw > XW_MAX && !spread_ok) {
     if (w_min > 1) return fail(KSS_E_UNSUPPORTED, "topology histograms too large for a sharded cluster");
     W = 1;  // exchange payload too large for granules: one workgroup
   }
@@ -1143,8 +1432,25 @@ static int run_single(kss_ctx* ctx, const PlanNeeds& need, const DevPods& dp, in
   Geometry g;
   if (!pick_geometry((int)N, W, ctx->pref_threads, g)) return fail(KSS_E_UNSUPPORTED, "no geometry for this cluster");
   const bool simple = simple_ok && simple_fits(g);
-  const int chunk = simple ? static_chunk(N, n) : 0;
-  if (simple && (rc = ctx->stat_buf.ensure(sizeof(uint32_t) * (size_t)chunk * std::max<size_t>(N, 1)))) return rc;
+  const int n_rowids = ctx->dc.n_classes + ctx->dc.n_terms;
+  bool spread = spread_ok && spread_fits(g, ctx->gneed, ctx->dc.n_keys, n_rowids);
+  if (spread_ok && !spread && g.threads < KSS_MAX_THREADS) {  // more prefetch lanes per shard
+    Geometry g2 = g;
+    const int per = (int)((N + g.W - 1) / g.W);
+    g2.threads = KSS_MAX_THREADS;
+    g2.npt = (per + KSS_MAX_THREADS - 1) / KSS_MAX_THREADS;
+    if (spread_fits(g2, ctx->gneed, ctx->dc.n_keys, n_rowids)) {
+      g = g2;
+      spread = true;
+    }
+  }
+  if (!spread && g.W > 1 && need.xw > XW_MAX) {  // k_schedule after all: its exchange payload needs one workgroup
+    if (w_min > 1) return fail(KSS_E_UNSUPPORTED, "topology histograms too large for a sharded cluster");
+    if (!pick_geometry((int)N, 1, ctx->pref_threads, g)) return fail(KSS_E_UNSUPPORTED, "no geometry for this cluster");
+  }
+  const bool loop = simple || spread;  // k_static + a persistent loop kernel
+  const int chunk = simple ? static_chunk(N, n) : (spread ? spread_chunk(ctx, ctx->gneed, N, n) : 0);
+  if (loop && (rc = ctx->stat_buf.ensure(sizeof(uint32_t) * (size_t)chunk * std::max<size_t>(N, 1)))) return rc;
   DevJob job{};
   job.c = ctx->dc;
   job.P = dp;
@@ -1157,14 +1463,15 @@ static int run_single(kss_ctx* ctx, const PlanNeeds& need, const DevPods& dp, in
   job.chosen = (int32_t*)ctx->chosen_buf.p;
   job.meta = (PodMeta*)ctx->meta_buf.p;
   job.spods = simple ? (const SPod*)ctx->spod_buf.p : nullptr;
-  job.stat = simple ? (uint32_t*)ctx->stat_buf.p : nullptr;
+  job.stat = loop ? (uint32_t*)ctx->stat_buf.p : nullptr;
+  job.gpods = spread ? (const GPod*)ctx->gpod_buf.p : nullptr;
   job.prof = ctx->prof;
   rc = ctx->job_buf.ensure(sizeof(DevJob));
   if (rc) return rc;
   rc = ctx->err_buf.ensure(16);
   if (rc) return rc;
   unsigned long long* gran = nullptr;
-  const size_t gb = sizeof(unsigned long long) * 2 * (size_t)g.W * 2 * XW_MAX;
+  const size_t gb = sizeof(unsigned long long) * 2 * (size_t)g.W * std::max(2 * XW_MAX, G_XW);
   if (g.W > 1) {
     rc = ctx->gran_buf.ensure(gb);
     if (rc) return rc;
@@ -1177,12 +1484,12 @@ static int run_single(kss_ctx* ctx, const PlanNeeds& need, const DevPods& dp, in
   unsigned long long* stamps = nullptr;
   // k_schedule: shard 0 only; k_simple: every shard (arrival skew of the exchanges)
   const size_t stamp_bytes = sizeof(unsigned long long) * 8 * KSS_NSTAMP_PODS * (simple ? g.W : 1);
-  if (ctx->stamps_file) {
+  if (ctx->stamps_file && !spread) {
     if ((rc = ctx->stamp_buf.ensure(stamp_bytes))) return rc;
     stamps = (unsigned long long*)ctx->stamp_buf.p;
     HIP_TRY(hipMemsetAsync(stamps, 0, stamp_bytes, ctx->stream));
   }
-  const int n_chunks = simple ? (n + chunk - 1) / std::max(chunk, 1) : 0;
+  const int n_chunks = loop ? (n + chunk - 1) / std::max(chunk, 1) : 0;
   while ((int)ctx->loop_ev.size() < 2 * n_chunks) {
     hipEvent_t e;
     HIP_TRY(hipEventCreate(&e));
@@ -1191,18 +1498,21 @@ static int run_single(kss_ctx* ctx, const PlanNeeds& need, const DevPods& dp, in
   if (simple)
     rc = launch_simple(ctx->stream, g, 1, (const DevJob*)ctx->job_buf.p, ctx->prof, n, (int)N, chunk, gran, gb,
                        (int*)ctx->err_buf.p, stamps, ctx->loop_ev.data());
+  else if (spread)
+    rc = launch_spread(ctx->stream, g, ctx->gneed, ctx->dc.n_keys, n_rowids, (const DevJob*)ctx->job_buf.p, ctx->prof, n,
+                       (int)N, chunk, gran, gb, (int*)ctx->err_buf.p, ctx->loop_ev.data());
   else
     rc = launch_schedule(ctx->stream, g, 1, std::max(need.bins_cap, 0), need.general, ctx->dc.n_keys,
                          (const DevJob*)ctx->job_buf.p, ctx->prof, gran, (int*)ctx->err_buf.p, stamps);
   if (rc) return rc;
-  ctx->last_kernel = simple ? 1 : 0;
+  ctx->last_kernel = simple ? 1 : (spread ? 2 : 0);
   HIP_TRY(hipEventRecord(ctx->ev1, ctx->stream));
   HIP_TRY(hipStreamSynchronize(ctx->stream));
   float ms = 0;
   HIP_TRY(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
   ctx->last_ms = ms;
-  ctx->last_launches = simple ? 2 * n_chunks : 1;
-  ctx->last_loop_ms = simple ? 0.0 : ms;
+  ctx->last_launches = loop ? 2 * n_chunks : 1;
+  ctx->last_loop_ms = loop ? 0.0 : ms;
   for (int i = 0; i < n_chunks; i++) {
     float t = 0;
     HIP_TRY(hipEventElapsedTime(&t, ctx->loop_ev[2 * i], ctx->loop_ev[2 * i + 1]));
@@ -1214,10 +1524,11 @@ static int run_single(kss_ctx* ctx, const PlanNeeds& need, const DevPods& dp, in
   int errw = 0;
   HIP_TRY(hipMemcpy(&errw, ctx->err_buf.p, sizeof(int), hipMemcpyDeviceToHost));
   if (errw) return fail(KSS_E_DEVICE, "shard exchange timed out (workgroups not co-resident?)");
+  if (commit) ctx->count_bound = count_total;
   ctx->meta_host.resize((size_t)std::max(n, 1));
   HIP_TRY(hipMemcpy(ctx->meta_host.data(), ctx->meta_buf.p, sizeof(PodMeta) * (size_t)std::max(n, 1), hipMemcpyDeviceToHost));
   if (chosen_out && n) HIP_TRY(hipMemcpy(chosen_out, ctx->chosen_buf.p, sizeof(int32_t) * n, hipMemcpyDeviceToHost));
-  ctx->recorded = record ? n : (n > 0 && !simple ? 1 : 0);
+  ctx->recorded = record ? n : (n > 0 && !loop ? 1 : 0);
   ctx->meta_n = n;
   ctx->axis_meta_dirty = false;
   if (stamps) {  // record: {kernel (0 k_schedule, 1 k_simple), shards} then the stamps
@@ -1233,12 +1544,25 @@ static int run_single(kss_ctx* ctx, const PlanNeeds& need, const DevPods& dp, in
   return 0;
 }
 
-// compact records of the staged podset for k_simple (host copy kept alive for the async upload)
+// compact records (k_simple) or resolved programs (k_spread) of the staged podset (host copy
+// kept alive for the async upload)
 static int stage_spods(kss_ctx* ctx, const kss_podset* ps) {
   ctx->f64_pods = F64Bounds{};
   f64_bounds_pods(ps, ctx->f64_pods);
+  ctx->staged_max_own = 0;
+  for (int i = 0; i < ps->n_pods; i++) ctx->staged_max_own = std::max(ctx->staged_max_own, (int)ps->pods[i].own_terms_len);
   ctx->spod_ok = build_spods(ps, ctx->dc.n_scalar, ctx->spod_host);
-  if (!ctx->spod_ok) return 0;
+  ctx->gpod_ok = false;
+  if (!ctx->spod_ok) {  // programs: the resolved records of k_spread
+    ctx->gpod_ok = build_gpods(ps, ctx->dc.n_scalar, ctx->dc.n_classes, ctx->key_card_h.data(), ctx->key_flags_h.data(),
+                               ctx->key_empty_h.data(), ctx->gpod_host, ctx->gneed);
+    if (!ctx->gpod_ok) return 0;
+    int rc = ctx->gpod_buf.ensure(sizeof(GPod) * ctx->gpod_host.size());
+    if (rc) return rc;
+    HIP_TRY(hipMemcpyAsync(ctx->gpod_buf.p, ctx->gpod_host.data(), sizeof(GPod) * ctx->gpod_host.size(),
+                           hipMemcpyHostToDevice, ctx->stream));
+    return 0;
+  }
   int rc = ctx->spod_buf.ensure(sizeof(SPod) * ctx->spod_host.size());
   if (rc) return rc;
   HIP_TRY(hipMemcpyAsync(ctx->spod_buf.p, ctx->spod_host.data(), sizeof(SPod) * ctx->spod_host.size(),
@@ -1294,6 +1618,7 @@ int kss_commit(kss_ctx* ctx, const kss_podset* ps, int32_t pod_index, int32_t no
   HIP_TRY(hipSetDevice(ctx->cfg.device));
   rc = upload_podset(ctx->stream, ctx->tmp_pod_buf, ps, ctx->tdp);
   if (rc) return rc;
+  ctx->count_bound += 1.0 + (double)ps->pods[pod_index].own_terms_len;
   hipLaunchKernelGGL(k_commit, dim3(1), dim3(64), 0, ctx->stream, ctx->dc, ctx->tdp, pod_index, local, 1);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipStreamSynchronize(ctx->stream));
@@ -1758,3 +2083,17 @@ int kss_format_annotations(kss_ctx* ctx, const kss_pod_result* res, int32_t n_no
 }
 
 }  // extern "C"
+
+int kss_device_go_log(int32_t device, const double* x, double* y, int32_t n) {
+  if (!x || !y || n < 0) return fail(KSS_E_INVAL, "bad arguments");
+  if (n == 0) return 0;
+  HIP_TRY(hipSetDevice(device));
+  double* d = nullptr;
+  HIP_TRY(hipMalloc(&d, 16 * (size_t)n));
+  std::unique_ptr<double, void (*)(double*)> hold(d, [](double* p) { hipFree(p); });
+  HIP_TRY(hipMemcpy(d, x, 8 * (size_t)n, hipMemcpyHostToDevice));
+  hipLaunchKernelGGL(k_go_log, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, nullptr, d, d + n, n);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipMemcpy(y, d + n, 8 * (size_t)n, hipMemcpyDeviceToHost));
+  return 0;
+}

@@ -95,32 +95,47 @@ struct SPod {
 };
 static_assert(sizeof(SPod) % 16 == 0, "SPod is copied as uint4");
 
-// Static word of one (pod, node): bits 0-7 the first failing static filter (0 pass, 1-4
-// KSS_F_NODE_UNSCHEDULABLE..KSS_F_NODE_AFFINITY, 255 not evaluated: PreFilter failure
-// or outside the NodeAffinity PreFilterResult), bits 8-15 raw TaintToleration, bits
-// 16-31 raw NodeAffinity (host-checked: Σ preferred weights < 2^16).
+// Static word of one (pod, node):
+//   bits 0-2   the first failing static filter: 0 pass, 1-4 KSS_F_NODE_UNSCHEDULABLE ..
+//              KSS_F_NODE_AFFINITY, 7 not evaluated (PreFilter failure, or outside the
+//              NodeAffinity PreFilterResult);
+//   bit 3      the pod's required node affinity matches the node (PodTopologySpread
+//              NodeAffinityPolicy=Honor), bit 4 its NoSchedule/NoExecute taints are all
+//              tolerated (NodeTaintsPolicy=Honor) — for every node, whatever bits 0-2 say;
+//   bits 5-11  raw TaintToleration (<= 64), bits 12-31 raw NodeAffinity (host-checked:
+//              Σ preferred weights < 2^20); both 0 unless bits 0-2 are 0.
+constexpr uint32_t SW_NOT_EVALUATED = 7, SW_AFF_OK = 1u << 3, SW_TAINT_OK = 1u << 4;
+__device__ __forceinline__ int sw_code(uint32_t w) {
+  const int c = (int)(w & 7u);
+  return c == (int)SW_NOT_EVALUATED ? KSS_F_NOT_EVALUATED : c;
+}
+__device__ __forceinline__ int sw_tt(uint32_t w) { return (int)((w >> 5) & 0x7Fu); }
+__device__ __forceinline__ int sw_na(uint32_t w) { return (int)(w >> 12); }
+
 __device__ __forceinline__ uint32_t static_word(const DevCluster& c, const DevPods& P, const kss_pod& p,
                                                 const kss_profile& prof, int n, uint32_t flags, uint64_t th,
                                                 uint64_t ts) {
   const int64_t g = (int64_t)c.node_base + n;
-  if (p.prefilter_status != 0) return KSS_F_NOT_EVALUATED;
+  if (p.prefilter_status != 0) return SW_NOT_EVALUATED;
+  auto lab = [&](int key) { return label_of(c, key, n); };
+  const bool aff = required_affinity_t(c, P.reqs, P.terms, P.ints, p, g, lab);
+  const bool tol = (th & ~p.tol_hard) == 0;
+  const uint32_t pol = (aff ? SW_AFF_OK : 0u) | (tol ? SW_TAINT_OK : 0u);
   if (p.names_len >= 0) {  // NodeAffinity PreFilterResult: nodes outside the set are not evaluated
     bool in = false;
     for (int i = 0; i < p.names_len; i++) in |= (int64_t)P.ints[p.names_off + i] == g;
-    if (!in) return KSS_F_NOT_EVALUATED;
+    if (!in) return pol | SW_NOT_EVALUATED;
   }
   const uint32_t en = prof.filter_enabled;
-  auto lab = [&](int key) { return label_of(c, key, n); };
   // RunFilterPlugins order (plugin_test.go:15-36): the first four filters are static
   if (((en >> KSS_F_NODE_UNSCHEDULABLE) & 1u) && (flags & KSS_NODE_UNSCHEDULABLE) && !(p.flags & KSS_POD_TOL_UNSCHEDULABLE))
-    return KSS_F_NODE_UNSCHEDULABLE;
-  if (((en >> KSS_F_NODE_NAME) & 1u) && p.node_name != -1 && (int64_t)p.node_name != g) return KSS_F_NODE_NAME;
-  if (((en >> KSS_F_TAINT_TOLERATION) & 1u) && (th & ~p.tol_hard)) return KSS_F_TAINT_TOLERATION;
-  if (((en >> KSS_F_NODE_AFFINITY) & 1u) && !required_affinity_t(c, P.reqs, P.terms, P.ints, p, g, lab))
-    return KSS_F_NODE_AFFINITY;
+    return pol | KSS_F_NODE_UNSCHEDULABLE;
+  if (((en >> KSS_F_NODE_NAME) & 1u) && p.node_name != -1 && (int64_t)p.node_name != g) return pol | KSS_F_NODE_NAME;
+  if (((en >> KSS_F_TAINT_TOLERATION) & 1u) && !tol) return pol | KSS_F_TAINT_TOLERATION;
+  if (((en >> KSS_F_NODE_AFFINITY) & 1u) && !aff) return pol | KSS_F_NODE_AFFINITY;
   const uint32_t tt = (uint32_t)__popcll(ts & ~p.tol_soft);                         // TaintToleration.Score
   const uint32_t na = (uint32_t)na_score_t(c, P.reqs, P.terms, P.ints, p, g, lab);  // NodeAffinity.Score
-  return (tt << 8) | (na << 16);
+  return pol | (tt << 5) | (na << 12);
 }
 
 // One (pod, node) result of the compact path: filter verdict and raw scores.
@@ -223,7 +238,7 @@ __device__ __forceinline__ int32_t ba_fast(const kss_profile& prof, const SPod& 
 // The state-dependent rest of one evaluation: NodeResourcesFit.Filter (fitsRequest) and
 // the Fit / BalancedAllocation scores, after the static word's filters.
 __device__ __forceinline__ SVal dyn_eval(const kss_profile& prof, const SPod& q, uint32_t w, const DynRow& r) {
-  SVal e{(int)(w & 0xFFu), 0, 0, 0, 0};
+  SVal e{sw_code(w), 0, 0, 0, 0};
   if (e.f) return e;
   if ((prof.filter_enabled >> KSS_F_NODE_RESOURCES_FIT) & 1u) {
     bool bad = (int64_t)r.pods + 1 > (int64_t)r.allowed;
@@ -236,8 +251,8 @@ __device__ __forceinline__ SVal dyn_eval(const kss_profile& prof, const SPod& q,
       return e;
     }
   }
-  e.tt = (int)((w >> 8) & 0xFFu);
-  e.na = (int)(w >> 16);
+  e.tt = sw_tt(w);
+  e.na = sw_na(w);
   e.fit = fit_fast(prof, q, r);
   e.ba = ba_fast(prof, q, r);
   return e;

@@ -1,0 +1,941 @@
+// kss_spread.cuh — the sequential scheduling loop for staged batches WITH
+// PodTopologySpread / InterPodAffinity programs (BASELINE C3, and C4's recipe on one GPU),
+// without a per-node result record.  Same semantics as schedule_pod<true> (kss_sched.cuh),
+// organised like k_simple (kss_simple.cuh):
+//
+//   * the commit-invariant part of every (pod, node) evaluation comes from k_static's
+//     static words, which for these pods also carry the inclusion-policy bits
+//     (NodeAffinityPolicy / NodeTaintsPolicy) that the PodTopologySpread counts need;
+//   * each pod's program is resolved on the host into a fixed GPod record: the plan
+//     (histogram / presence bin offsets, key slots) and a table of the class_count /
+//     term_count rows its constraints and terms read (kss_lib.hip build_gpods);
+//   * the shard's node rows, label ids, and the count rows of the next pod live in LDS.
+//     The counts come from the snapshot (HBM, read-only during the launch) plus a
+//     per-shard table of the commits of this launch (one byte per (count row, node)),
+//     written back to HBM when the launch ends;
+//   * records, static words and count rows of the next pods are prefetched by every wave
+//     but wave 0 (wave 0 runs the exchanges and never waits on an HBM prefetch);
+//   * exchanges carry 32-bit values, one {epoch, value} granule each; a pod with a single
+//     ScheduleAnyway constraint folds the PodTopologySpread score extrema into the filter
+//     exchange (the raw score is monotone in the count), so it needs no third exchange.
+//
+// Per pod: [stats pass + exchange E1 if the pod needs cluster-wide counts] -> filter +
+// raw scores + E2 -> [PodTopologySpread score pass + E3 for > 1 soft constraint] ->
+// NormalizeScore + weights + selectHost key + E4 -> commit by the winner's shard.
+#pragma once
+#include "kss_simple.cuh"
+
+namespace kss {
+
+constexpr int G_ROWS = 8;    // distinct count rows (class_count / term_count) per pod
+constexpr int G_RIDX = 32;   // row references of a pod's constraints and entries
+constexpr int G_IPA = 8;     // inter-pod-affinity entries per pod
+constexpr int G_PF = 4;      // node words per prefetch lane (host-checked)
+constexpr int G_XW = 512;    // 32-bit values per shard per exchange (host-checked)
+constexpr int G_NS = 16;     // scalar slots of an exchange
+
+struct GSpread {
+  int32_t key, max_skew, self_match, flags;  // kss_spread
+  int32_t ri_off, ri_len;                    // its classes: ridx[ri_off .. +ri_len) (row-table indices)
+  int32_t off, poff;                         // histogram / presence bin offsets (-1: node-valued key)
+  int32_t mode;                              // soft: SOFT_HOST / SOFT_DIRECT / SOFT_HIST
+  int32_t empty;                             // key_empty: domain of a node without the key
+  int32_t nb;                                // domains of the key + 1
+  int32_t pad;
+};
+struct GIpa {
+  int32_t kind, key, ri_off, ri_len, coef, slot;
+};
+// Host-resolved program of one pod (build_gpods).  Per IPA key slot k, histogram h (0
+// existing anti-affinity, 1 required affinity, 2 required anti-affinity, 3 score) lives at
+// hoff[k][h]; -1 for a node-valued (unique) key, whose value is the node's own sum, and
+// for a histogram no entry of the pod feeds (never read).
+struct alignas(16) GPod {
+  SPod dyn;
+  int32_t pflags, n_hard, n_soft, n_ipa;
+  int32_t n_rows, n_keys, total_bins, hard_pbins;
+  int32_t total_pbins, need_stats, pad0, pad1;
+  int32_t key[MAXK];
+  int32_t hoff[MAXK][4];
+  int32_t row[G_ROWS];    // class_count row r, or term_count row r as (1 << 30) | r
+  int32_t rowid[G_ROWS];  // commit-table id: class r -> r, term r -> n_classes + r
+  int16_t ridx[G_RIDX];
+  GSpread sp[MAXH + MAXS];
+  GIpa ipa[G_IPA];
+};
+constexpr int GPOD_Q = (int)(sizeof(GPod) / 16);
+static_assert(sizeof(GPod) % 16 == 0 && GPOD_Q <= 64, "a GPod is prefetched by one wave, one uint4 per lane");
+
+// Go math.Log (src/math/log.go), the same IEEE operation sequence as the host port
+// (kss_host.cpp kss_go_log; compiled with -ffp-contract=off): PodTopologySpread's
+// topologyNormalizingWeight = math.Log(float64(size + 2)), size >= 0.
+__device__ __forceinline__ double go_log_dev(double x) {
+  const double Ln2Hi = 6.93147180369123816490e-01, Ln2Lo = 1.90821492927058770002e-10;
+  const double L1 = 6.666666666666735130e-01, L2 = 3.999999999940941908e-01, L3 = 2.857142874366239149e-01,
+               L4 = 2.222219843214978396e-01, L5 = 1.818357216161805012e-01, L6 = 1.531383769920937332e-01,
+               L7 = 1.479819860511658591e-01;
+  int ki;
+  double f1 = frexp(x, &ki);
+  if (f1 < 0.70710678118654752440 /* math.Sqrt2 / 2 */) {
+    f1 *= 2;
+    ki--;
+  }
+  const double f = f1 - 1;
+  const double k = (double)ki;
+  const double s = f / (2 + f);
+  const double s2 = s * s;
+  const double s4 = s2 * s2;
+  const double t1 = s2 * (L1 + s4 * (L3 + s4 * (L5 + s4 * L7)));
+  const double t2 = s4 * (L2 + s4 * (L4 + s4 * L6));
+  const double R = t1 + t2;
+  const double hfsq = 0.5 * f * f;
+  return k * Ln2Hi - ((hfsq - (s * (hfsq + R) + k * Ln2Lo)) - f);
+}
+
+// LDS image: header, the exchange vector, then the shard arrays.
+struct alignas(16) SpreadHdr {
+  int32_t red[MAXWAVES][G_NS];
+  long long kred[2][MAXWAVES];
+  long long kres;
+  kss_profile prof;  // a runtime (non-default) profile, staged word by word (as SimpleHdr)
+  int32_t abort;
+  int32_t pad[3];
+};
+
+struct SpreadShard {
+  int32_t* xs;     // [G_NS + bins_cap]: exchange scalars, then histogram / presence bins
+  GPod* ring;      // [3] pod programs (slot = pod % 3)
+  uint32_t* st;    // [2][cap] static words (slot = pod & 1)
+  int32_t* base;   // [2][rows][cap] snapshot counts of the pod's rows (slot = pod & 1)
+  uint8_t* delta;  // [n_rowids][cap] commits of this launch per count row and node
+  double* r64;     // [8][cap] allocatable, requested (cpu, mem, eph), non-zero requested (cpu, mem)
+  double* inv;     // [3][cap]
+  int32_t* r32;    // [3][cap] pod count, allowed pods, node flags
+  int32_t* lbl;    // [n_keys][cap] label value ids
+  int32_t* sf;     // [cap] verdict | ignored << 16
+  int32_t* stt;    // [cap] TaintToleration raw
+  int32_t* sna;    // [cap] NodeAffinity raw
+  int32_t* sfit;   // [cap]
+  int32_t* sba;    // [cap]
+  int32_t* scnt;   // [cap] single soft constraint: the node's count (-1 lacks the key)
+  long long* sipa; // [cap] InterPodAffinity raw
+  long long* spts; // [cap] PodTopologySpread raw (> 1 soft constraint)
+  int cap, n_rowids, rows;
+};
+
+// rows: count rows per pod in the batch (<= G_ROWS)
+__host__ __device__ inline size_t spread_lds_bytes(int cap, int bins_cap, int n_keys, int n_rowids, int rows) {
+  const size_t C = (size_t)cap;
+  size_t b = sizeof(SpreadHdr) + 4 * ((size_t)G_NS + (size_t)bins_cap);
+  b = (b + 15) / 16 * 16 + 3 * sizeof(GPod);
+  b += 4 * 2 * C + 4 * 2 * (size_t)rows * C + ((size_t)n_rowids * C + 15) / 16 * 16;
+  b += 8 * 8 * C + 8 * 3 * C + 4 * 3 * C + 4 * (size_t)n_keys * C;
+  b += 4 * 6 * C + 8 * 2 * C;
+  return b;
+}
+
+__device__ __forceinline__ SpreadShard spread_view(long long* smem, int cap, int bins_cap, int n_keys, int n_rowids,
+                                                   int rows) {
+  SpreadShard L;
+  const size_t C = (size_t)cap;
+  uint8_t* b = reinterpret_cast<uint8_t*>(smem) + sizeof(SpreadHdr);
+  L.xs = reinterpret_cast<int32_t*>(b);
+  size_t o = ((size_t)(G_NS + bins_cap) * 4 + sizeof(SpreadHdr) + 15) / 16 * 16 - sizeof(SpreadHdr);
+  L.ring = reinterpret_cast<GPod*>(b + o);
+  o += 3 * sizeof(GPod);
+  L.st = reinterpret_cast<uint32_t*>(b + o);
+  o += 4 * 2 * C;
+  L.base = reinterpret_cast<int32_t*>(b + o);
+  o += 4 * 2 * (size_t)rows * C;
+  L.delta = b + o;
+  o += ((size_t)n_rowids * C + 15) / 16 * 16;
+  L.r64 = reinterpret_cast<double*>(b + o);
+  o += 8 * 8 * C;
+  L.inv = reinterpret_cast<double*>(b + o);
+  o += 8 * 3 * C;
+  L.sipa = reinterpret_cast<long long*>(b + o);
+  o += 8 * C;
+  L.spts = reinterpret_cast<long long*>(b + o);
+  o += 8 * C;
+  L.r32 = reinterpret_cast<int32_t*>(b + o);
+  o += 4 * 3 * C;
+  L.lbl = reinterpret_cast<int32_t*>(b + o);
+  o += 4 * (size_t)n_keys * C;
+  L.sf = reinterpret_cast<int32_t*>(b + o);
+  L.stt = L.sf + C;
+  L.sna = L.sf + 2 * C;
+  L.sfit = L.sf + 3 * C;
+  L.sba = L.sf + 4 * C;
+  L.scnt = L.sf + 5 * C;
+  L.cap = cap;
+  L.n_rowids = n_rowids;
+  L.rows = rows;
+  return L;
+}
+
+// Count of row-table entry r at slot s: snapshot + this launch's commits.
+__device__ __forceinline__ int32_t g_count(const SpreadShard& L, const GPod& q, const int32_t* base, int r, int s) {
+  return base[r * L.cap + s] + (int32_t)L.delta[(size_t)q.rowid[r] * L.cap + s];
+}
+
+// Σ over a constraint's / entry's rows (sum_rows over class_count / term_count).
+__device__ __forceinline__ int64_t g_sum(const SpreadShard& L, const GPod& q, const int32_t* base, int off, int len,
+                                         int s) {
+  int64_t v = 0;
+  for (int i = 0; i < len; i++) v += g_count(L, q, base, q.ridx[off + i], s);
+  return v;
+}
+
+__device__ __forceinline__ bool g_policy(const GSpread& sp, uint32_t w) {
+  if ((sp.flags & KSS_SPREAD_POLICY_AFFINITY_HONOR) && !(w & SW_AFF_OK)) return false;
+  if ((sp.flags & KSS_SPREAD_POLICY_TAINTS_HONOR) && !(w & SW_TAINT_OK)) return false;
+  return true;
+}
+
+__device__ __forceinline__ bool g_has_keys(const SpreadShard& L, const GSpread* sp, int cnt, int s) {
+  for (int i = 0; i < cnt; i++)
+    if (L.lbl[sp[i].key * L.cap + s] < 0) return false;
+  return true;
+}
+
+__device__ __forceinline__ int32_t op32(int op, int32_t a, int32_t b) {
+  if (op == OP_SUM) return (int32_t)((uint32_t)a + (uint32_t)b);
+  if (op == OP_MAX) return b > a ? b : a;
+  if (op == OP_MIN) return b < a ? b : a;
+  return a | b;
+}
+__device__ __forceinline__ int32_t ident32(int op) { return op == OP_MAX ? INT32_MIN : (op == OP_MIN ? INT32_MAX : 0); }
+
+// Cross-shard part of a 32-bit exchange, wave 0 only: publish M = K + ns + no values
+// (scalars xs[0..K), SUM bins xs[G_NS + sum_lo ..), OR bins xs[G_NS + or_lo ..)) as
+// {epoch, value} granules, sweep every shard's (all loads of a round in flight), and
+// combine into the same LDS slots with LDS atomics (the own contribution comes back
+// through the sweep).
+__device__ __noinline__ bool spread_exchange(SpreadHdr& H, int32_t* xs, unsigned long long* gran, int W, int wself,
+                                             unsigned epoch, int* err, int K, unsigned opbits, int sum_lo, int ns,
+                                             int or_lo, int no) {
+  constexpr int XB = 8;
+  const int lane = threadIdx.x & 63;
+  const int M = K + ns + no;
+  auto slot = [&](int j) -> int32_t* {
+    if (j < K) return xs + j;
+    if (j < K + ns) return xs + G_NS + sum_lo + (j - K);
+    return xs + G_NS + or_lo + (j - K - ns);
+  };
+  auto opof = [&](int j) { return j < K ? (int)((opbits >> (2 * j)) & 3u) : (j < K + ns ? OP_SUM : OP_OR); };
+  const unsigned long long tag = (unsigned long long)epoch << 32;
+  unsigned long long* mine = gran + ((size_t)(epoch & 1) * W + wself) * G_XW;
+  for (int j = lane; j < M; j += 64) {
+    int32_t* sl = slot(j);
+    __hip_atomic_store(mine + j, tag | (uint32_t)*sl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *sl = ident32(opof(j));
+  }
+  const unsigned long long* base = gran + (size_t)(epoch & 1) * W * G_XW;
+  const int Q = W * M;
+  for (int q0 = 0; q0 < Q; q0 += 64 * XB) {
+    unsigned long long g[XB];
+    for (unsigned spins = 0;; ++spins) {
+      bool ok = true;
+#pragma unroll
+      for (int b = 0; b < XB; b++) {
+        const int q = q0 + b * 64 + lane;
+        g[b] = tag;
+        if (q < Q) {
+          const int w = q / M, j = q - w * M;
+          g[b] = __hip_atomic_load(base + (size_t)w * G_XW + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      }
+#pragma unroll
+      for (int b = 0; b < XB; b++) ok &= (g[b] >> 32) == epoch;
+      if (__all(ok)) break;
+      if (spins >= SPIN_LIMIT) {
+        if (lane == 0) {
+          H.abort = 1;
+          __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        return false;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+#pragma unroll
+    for (int b = 0; b < XB; b++) {
+      const int q = q0 + b * 64 + lane;
+      if (q < Q) {
+        const int j = q % M;
+        const int32_t v = (int32_t)(uint32_t)g[b];
+        int32_t* sl = slot(j);
+        switch (opof(j)) {
+          case OP_SUM: atomicAdd(sl, v); break;
+          case OP_MAX: atomicMax(sl, v); break;
+          case OP_MIN: atomicMin(sl, v); break;
+          default: atomicOr(sl, v); break;
+        }
+      }
+    }
+  }
+  return true;
+}
+
+// Cluster reduction of K int32 scalars v[] (ops[]), plus (W > 1) the cross-shard SUM of
+// bins [sum_lo, sum_lo + ns) and OR of [or_lo, or_lo + no) of xs.  local: workgroup only.
+// LDS-only barriers (the prefetch waves' HBM loads stay in flight).  False on abort.
+template <int K>
+__device__ __forceinline__ bool spread_reduce(SpreadHdr& H, int32_t* xs, int W, int w, unsigned& epoch,
+                                              unsigned long long* gran, int* err, int32_t (&v)[K],
+                                              const int (&ops)[K], int sum_lo = 0, int ns = 0, int or_lo = 0,
+                                              int no = 0, bool local = false) {
+  static_assert(K <= G_NS, "too many values");
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+#pragma unroll
+  for (int k = 0; k < K; k++) {
+    int32_t r = v[k];
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) r = op32(ops[k], r, __shfl_xor(r, m, 64));
+    if (lane == 0) H.red[wave][k] = r;
+  }
+  lds_barrier();
+  if (threadIdx.x < K) {
+    const int k = threadIdx.x;
+    int op = OP_SUM;
+#pragma unroll
+    for (int q = 0; q < K; q++)
+      if (q == k) op = ops[q];
+    int32_t r = H.red[0][k];
+    for (int x = 1; x < nw; x++) r = op32(op, r, H.red[x][k]);
+    xs[k] = r;
+  }
+  lds_barrier();
+  if (W > 1 && !local) {
+    unsigned opbits = 0;
+#pragma unroll
+    for (int k = 0; k < K; k++) opbits |= (unsigned)ops[k] << (2 * k);
+    ++epoch;
+    if (wave == 0) spread_exchange(H, xs, gran, W, w, epoch, err, K, opbits, sum_lo, ns, or_lo, no);
+    lds_barrier();
+    if (H.abort) return false;
+  }
+#pragma unroll
+  for (int k = 0; k < K; k++) v[k] = xs[k];
+  lds_barrier();  // xs[0..K) may be rewritten by the next reduction
+  return true;
+}
+
+// Cluster MAX of the packed selectHost key (two granules: lo, hi).
+__device__ __forceinline__ bool spread_argmax(SpreadHdr& H, int W, int w, unsigned& epoch, unsigned long long* gran,
+                                              int* err, int parity, long long& key) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const long long r = wave_red<OP_MAX>(key);
+  if (lane == 0) H.kred[parity][wave] = r;
+  lds_barrier();
+  long long best = H.kred[parity][0];
+  for (int x = 1; x < nw; x++) best = H.kred[parity][x] > best ? H.kred[parity][x] : best;
+  if (W == 1) {
+    key = best;
+    return true;
+  }
+  ++epoch;
+  if (wave == 0) {
+    const unsigned long long tag = (unsigned long long)epoch << 32;
+    unsigned long long* mine = gran + ((size_t)(epoch & 1) * W + w) * G_XW;
+    if (lane < 2)
+      __hip_atomic_store(mine + lane, tag | (lane ? (uint32_t)((unsigned long long)best >> 32) : (uint32_t)best),
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned long long* base = gran + (size_t)(epoch & 1) * W * G_XW;
+    long long m = 0;
+    for (int c0 = 0; c0 < W; c0 += 64) {
+      const int s = c0 + lane;
+      unsigned long long lo = tag, hi = tag;
+      for (unsigned spins = 0;; ++spins) {
+        if (s < W) {
+          lo = __hip_atomic_load(base + (size_t)s * G_XW, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          hi = __hip_atomic_load(base + (size_t)s * G_XW + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (__all(((lo >> 32) == epoch) & ((hi >> 32) == epoch))) break;
+        if (spins >= SPIN_LIMIT) {
+          if (lane == 0) {
+            H.abort = 1;
+            __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          }
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      const long long k = s < W ? (long long)(((hi & 0xFFFFFFFFull) << 32) | (lo & 0xFFFFFFFFull)) : 0;
+      m = k > m ? k : m;
+    }
+    m = wave_red<OP_MAX>(m);
+    if (lane == 0) H.kres = m;
+  }
+  lds_barrier();
+  if (H.abort) return false;
+  key = H.kres;
+  return true;
+}
+
+// filter_pts / filter_ipa / ipa_score of kss_sched.cuh over the GPod and the LDS caches.
+__device__ __forceinline__ int g_filter_pts(const SpreadShard& L, const GPod& q, const int32_t* base, const int32_t* bins,
+                                            const int32_t (&hard_min)[MAXH], int s, uint32_t w) {
+  for (int i = 0; i < q.n_hard; i++) {
+    const GSpread& sp = q.sp[i];
+    const int d = L.lbl[sp.key * L.cap + s];
+    if (d < 0) return 1 + KSS_PTS_MISSING_LABEL;
+    int64_t match;
+    if (sp.off >= 0) match = bins[sp.off + d];
+    else match = (g_has_keys(L, q.sp, q.n_hard, s) && g_policy(sp, w)) ? g_sum(L, q, base, sp.ri_off, sp.ri_len, s) : 0;
+    const int64_t skew = match + (int64_t)sp.self_match - (int64_t)hard_min[i];
+    if (skew > (int64_t)sp.max_skew) return 1 + KSS_PTS_CONSTRAINTS_NOT_MATCH;
+  }
+  return 0;
+}
+
+// histogram h of key slot k at domain d, or the node's own value for a node-valued key
+__device__ __forceinline__ int64_t g_ipa_value(const SpreadShard& L, const GPod& q, const int32_t* base,
+                                               const int32_t* bins, int k, int h, int d, int s) {
+  if (q.hoff[k][h] >= 0) return bins[q.hoff[k][h] + d];
+  const int kind = h == 0 ? KSS_IPA_EXISTING_ANTI : (h == 1 ? KSS_IPA_REQ_AFFINITY : KSS_IPA_REQ_ANTI);
+  int64_t v = 0;
+  for (int e = 0; e < q.n_ipa; e++)
+    if (q.ipa[e].kind == kind && q.ipa[e].slot == k) v += g_sum(L, q, base, q.ipa[e].ri_off, q.ipa[e].ri_len, s);
+  return v;
+}
+
+__device__ __forceinline__ int g_filter_ipa(const SpreadShard& L, const GPod& q, const int32_t* base, const int32_t* bins,
+                                            int32_t flags, int s) {
+  // satisfyPodAffinity
+  bool have = false, exist = true;
+  for (int e = 0; e < q.n_ipa; e++) {
+    const GIpa& en = q.ipa[e];
+    if (en.kind != KSS_IPA_REQ_AFFINITY) continue;
+    have = true;
+    const int d = L.lbl[en.key * L.cap + s];
+    if (d < 0) return 1 + KSS_IPA_AFFINITY;
+    if (g_ipa_value(L, q, base, bins, en.slot, 1, d, s) <= 0) exist = false;
+  }
+  if (have && !exist && !(!(flags & 2) && (q.pflags & KSS_POD_IPA_SELF_MATCH))) return 1 + KSS_IPA_AFFINITY;
+  // satisfyPodAntiAffinity
+  if (flags & 4) {
+    for (int e = 0; e < q.n_ipa; e++) {
+      const GIpa& en = q.ipa[e];
+      if (en.kind != KSS_IPA_REQ_ANTI) continue;
+      const int d = L.lbl[en.key * L.cap + s];
+      if (d < 0) continue;
+      if (g_ipa_value(L, q, base, bins, en.slot, 2, d, s) > 0) return 1 + KSS_IPA_ANTI_AFFINITY;
+    }
+  }
+  // satisfyExistingPodsAntiAffinity
+  if (flags & 1) {
+    for (int e = 0; e < q.n_ipa; e++) {
+      const GIpa& en = q.ipa[e];
+      if (en.kind != KSS_IPA_EXISTING_ANTI) continue;
+      const int d = L.lbl[en.key * L.cap + s];
+      if (d < 0) continue;
+      if (g_ipa_value(L, q, base, bins, en.slot, 0, d, s) > 0) return 1 + KSS_IPA_EXISTING_ANTI_AFFINITY;
+    }
+  }
+  return 0;
+}
+
+// InterPodAffinity.Score: Σ topologyScore[key][node value] over the keys the node has
+__device__ __forceinline__ int64_t g_ipa_score(const SpreadShard& L, const GPod& q, const int32_t* base,
+                                               const int32_t* bins, int s) {
+  int64_t v = 0;
+  const bool has_labels = (L.r32[2 * L.cap + s] & KSS_NODE_HAS_LABELS) != 0;
+  for (int k = 0; k < q.n_keys; k++) {
+    const int d = L.lbl[q.key[k] * L.cap + s];
+    if (d < 0) continue;
+    if (q.hoff[k][3] >= 0) {
+      v += bins[q.hoff[k][3] + d];
+    } else if (has_labels) {
+      for (int e = 0; e < q.n_ipa; e++) {
+        const GIpa& en = q.ipa[e];
+        if (en.slot != k || (en.kind != KSS_IPA_SCORE_CLASS && en.kind != KSS_IPA_SCORE_TERM)) continue;
+        v += (int64_t)en.coef * g_sum(L, q, base, en.ri_off, en.ri_len, s);
+      }
+    }
+  }
+  return v;
+}
+
+// The batch for shard w of one cluster, pods [k0, k1).
+__device__ __forceinline__ void spread_schedule(DevCluster c, const GPod* __restrict__ gpods,
+                                                const uint32_t* __restrict__ stat, const int32_t* __restrict__ ints,
+                                                int k0, int k1, int32_t* chosen, PodMeta* meta, const kss_profile& prof,
+                                                int W, int w, int cap, int bins_cap, int rows,
+                                                unsigned long long* gran, int* err, long long* smem) {
+  const int tid = threadIdx.x, nt = blockDim.x;
+  SpreadHdr& H = *reinterpret_cast<SpreadHdr*>(smem);
+  const int n_rowids = c.n_classes + c.n_terms;
+  const SpreadShard L = spread_view(smem, cap, bins_cap, c.n_keys, n_rowids, rows);
+  const size_t N = (size_t)c.N;
+  const int per = (c.N + W - 1) / W;
+  const int lo = min(c.N, w * per), hi = min(c.N, lo + per), own = hi - lo;
+  if (k1 <= k0) return;
+  int32_t* bins = L.xs + G_NS;
+  KSS_GLOBAL const uint32_t* gstat = gp(stat);
+  KSS_GLOBAL const uint4* gq = gp(reinterpret_cast<const uint4*>(gpods));
+  KSS_GLOBAL const int32_t* gcc = gp(c.class_count);
+  KSS_GLOBAL const int32_t* gtc = gp(c.term_count);
+  KSS_GLOBAL int32_t* gchosen = gp(chosen);
+  KSS_GLOBAL PodMeta* gmeta = gp(meta);
+  // shard state -> LDS; pod programs k0, k0+1; static words and count rows of pod k0
+  for (int s = tid; s < own; s += nt) {
+    const int n = lo + s;
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+      const int64_t A = c.alloc[k * N + n];
+      L.r64[k * cap + s] = (double)A;
+      L.r64[(3 + k) * cap + s] = (double)c.requested[k * N + n];
+      L.inv[k * cap + s] = A > 0 ? 1.0 / (double)A : 0.0;
+    }
+    L.r64[6 * cap + s] = (double)c.nonzero[n];
+    L.r64[7 * cap + s] = (double)c.nonzero[N + n];
+    L.r32[s] = c.pod_count[n];
+    L.r32[cap + s] = c.allowed_pods[n];
+    L.r32[2 * cap + s] = (int32_t)c.node_flags[n];
+    for (int k = 0; k < c.n_keys; k++) L.lbl[k * cap + s] = c.label_value[(size_t)k * N + n];
+    L.st[(k0 & 1) * cap + s] = stat[(size_t)lo + s];
+  }
+  for (int i = tid; i < n_rowids * cap; i += nt) L.delta[i] = 0;
+  for (int i = tid; i < min(k1 - k0, 2) * GPOD_Q; i += nt) {
+    const int j = k0 + i / GPOD_Q;
+    reinterpret_cast<uint4*>(L.ring + j % 3)[i % GPOD_Q] = reinterpret_cast<const uint4*>(gpods + j)[i % GPOD_Q];
+  }
+  if (tid == 0) H.abort = 0;
+  __syncthreads();
+  {
+    const GPod& q0 = L.ring[k0 % 3];
+    for (int s = tid; s < own; s += nt)
+      for (int r = 0; r < q0.n_rows; r++) {
+        const int row = q0.row[r] & 0x3FFFFFFF;
+        const bool term = (q0.row[r] >> 30) & 1;
+        L.base[((k0 & 1) * rows + r) * cap + s] = (term ? c.term_count : c.class_count)[(size_t)row * N + lo + s];
+      }
+  }
+  __syncthreads();
+
+  const int nwave = nt >> 6;
+  const bool pf_wave = nwave == 1 || __builtin_amdgcn_readfirstlane(tid >> 6) >= 1;
+  const int pf_lane = nwave == 1 ? tid : tid - 64, pf_n = nwave == 1 ? nt : nt - 64;
+  const int pf_per = (own + pf_n - 1) / pf_n;  // <= G_PF (host-checked)
+  uint4 pfq = make_uint4(0, 0, 0, 0);
+  uint32_t pfw[G_PF];
+  int32_t pfc[G_ROWS][G_PF];
+#pragma unroll
+  for (int j = 0; j < G_PF; j++) {
+    pfw[j] = 0;
+#pragma unroll
+    for (int r = 0; r < G_ROWS; r++) pfc[r][j] = 0;
+  }
+  unsigned epoch = 0;
+  int kparity = 0;
+  for (int k = k0; k < k1; k++) {
+    const GPod& q = L.ring[k % 3];
+    const uint32_t* sw = L.st + (k & 1) * cap;
+    const int32_t* base = L.base + (k & 1) * rows * cap;
+    // prefetch (every wave but wave 0): record of pod k+2, static words and count rows of pod k+1
+    const bool pf_on = pf_wave && k + 1 < k1 && own > 0;
+    int nr1 = 0;
+    if (pf_on) {
+      const GPod& q1 = L.ring[(k + 1) % 3];
+      nr1 = q1.n_rows;
+      if (k + 2 < k1) {
+        KSS_GLOBAL const uint4& src = gq[(size_t)(k + 2) * GPOD_Q + min(pf_lane, GPOD_Q - 1)];
+        pfq = make_uint4(src.x, src.y, src.z, src.w);
+      }
+#pragma unroll
+      for (int j = 0; j < G_PF; j++) {
+        if (j >= pf_per) break;
+        const int s = min(j * pf_n + pf_lane, own - 1);
+        pfw[j] = gstat[(size_t)(k + 1 - k0) * N + lo + s];
+#pragma unroll
+        for (int r = 0; r < G_ROWS; r++) {
+          if (r >= nr1) break;
+          const int rw = q1.row[r];
+          const size_t idx = (size_t)(rw & 0x3FFFFFFF) * N + lo + s;
+          pfc[r][j] = ((rw >> 30) & 1) ? gtc[idx] : gcc[idx];
+        }
+      }
+    }
+    PodMeta m;
+    m.chosen = -1;
+    m.n_feasible = 0;
+    m.scored = 0;
+    m.status = 0;
+    m.best_total = 0;
+    long long best = 0;
+    bool evaluated = q.dyn.status == 0;
+    if (!evaluated) m.status = q.dyn.status == 1 ? 2 : 3;
+    int32_t flags = 0, hard_min[MAXH];
+#pragma unroll
+    for (int i = 0; i < MAXH; i++) hard_min[i] = INT32_MAX;
+    // ---- stats: PodTopologySpread PreFilter, InterPodAffinity PreFilter / PreScore ----
+    if (evaluated && q.need_stats) {
+      for (int b = tid; b < q.total_bins + q.total_pbins; b += nt) bins[b] = 0;
+      lds_barrier();
+      for (int s = tid; s < own; s += nt) {
+        const uint32_t wd = sw[s];
+        if (q.n_hard > 0 && g_has_keys(L, q.sp, q.n_hard, s)) {
+          for (int i = 0; i < q.n_hard; i++) {
+            const GSpread& sp = q.sp[i];
+            if (!g_policy(sp, wd)) continue;
+            const int32_t cnt = (int32_t)g_sum(L, q, base, sp.ri_off, sp.ri_len, s);
+            if (sp.off < 0) {
+              hard_min[i] = cnt < hard_min[i] ? cnt : hard_min[i];
+            } else {
+              const int d = L.lbl[sp.key * cap + s];
+              atomicAdd(&bins[sp.off + d], cnt);
+              bins[q.total_bins + sp.poff + d] = 1;
+            }
+          }
+        }
+        if (q.n_soft > 0) {
+          const GSpread* so = q.sp + q.n_hard;
+          if (!(q.pflags & KSS_POD_PTS_REQUIRE_ALL) || g_has_keys(L, so, q.n_soft, s)) {
+            for (int i = 0; i < q.n_soft; i++) {
+              const GSpread& sp = so[i];
+              if (sp.mode != SOFT_HIST || !g_policy(sp, wd)) continue;
+              int d = L.lbl[sp.key * cap + s];
+              if (d < 0) d = sp.empty;
+              const int32_t cnt = (int32_t)g_sum(L, q, base, sp.ri_off, sp.ri_len, s);
+              if (cnt) atomicAdd(&bins[sp.off + d], cnt);
+            }
+          }
+        }
+        if (q.n_ipa > 0) {
+          const bool has_labels = (L.r32[2 * cap + s] & KSS_NODE_HAS_LABELS) != 0;
+          for (int e = 0; e < q.n_ipa; e++) {
+            const GIpa& en = q.ipa[e];
+            const int d = L.lbl[en.key * cap + s];
+            if (d < 0) continue;
+            if (en.kind == KSS_IPA_SCORE_CLASS || en.kind == KSS_IPA_SCORE_TERM) {
+              if (!has_labels) continue;
+              const int64_t v = g_sum(L, q, base, en.ri_off, en.ri_len, s);
+              if (v > 0) flags |= 8;
+              const int ho = q.hoff[en.slot][3];
+              if (ho >= 0 && v) atomicAdd(&bins[ho + d], (int32_t)(v * en.coef));
+            } else {
+              const int64_t v = g_sum(L, q, base, en.ri_off, en.ri_len, s);
+              const int h = en.kind == KSS_IPA_EXISTING_ANTI ? 0 : (en.kind == KSS_IPA_REQ_AFFINITY ? 1 : 2);
+              if (v > 0) flags |= 1 << h;
+              const int ho = q.hoff[en.slot][h];
+              if (ho >= 0 && v) atomicAdd(&bins[ho + d], (int32_t)v);
+            }
+          }
+        }
+      }
+      int32_t v[MAXH + 1];
+      const int op[MAXH + 1] = {OP_MIN, OP_MIN, OP_MIN, OP_MIN, OP_OR};
+#pragma unroll
+      for (int i = 0; i < MAXH; i++) v[i] = hard_min[i];
+      v[MAXH] = flags;
+      if (!spread_reduce(H, L.xs, W, w, epoch, gran, err, v, op, 0, q.total_bins, q.total_bins, q.hard_pbins)) return;
+      flags = v[MAXH];
+      // criticalPaths minimum over the present domains of histogram-valued hard keys
+      int32_t mm[MAXH];
+      bool any_hist = false;
+#pragma unroll
+      for (int i = 0; i < MAXH; i++) mm[i] = v[i];
+      for (int i = 0; i < q.n_hard; i++) {
+        const GSpread& sp = q.sp[i];
+        if (sp.off < 0) continue;
+        any_hist = true;
+        for (int b = tid; b < sp.nb; b += nt)
+          if (bins[q.total_bins + sp.poff + b]) mm[i] = min(mm[i], bins[sp.off + b]);
+      }
+      if (any_hist) {
+        const int opm[MAXH] = {OP_MIN, OP_MIN, OP_MIN, OP_MIN};
+        spread_reduce(H, L.xs, W, w, epoch, gran, err, mm, opm, 0, 0, 0, 0, /*local=*/true);
+      }
+#pragma unroll
+      for (int i = 0; i < MAXH; i++) hard_min[i] = mm[i];
+      for (int b = q.hard_pbins + tid; b < q.total_pbins; b += nt) bins[q.total_bins + b] = 0;
+      lds_barrier();
+    }
+    // ---- filter + raw scores ----
+    const bool has_soft = q.n_soft > 0, has_ipa = q.n_ipa > 0;
+    const bool one_soft = q.n_soft == 1;
+    const GSpread* soft = q.sp + q.n_hard;
+    const uint32_t en = prof.filter_enabled;
+    int32_t nf = 0, nign = 0, max_tt = 0, max_na = 0, ipa_min = INT32_MAX, ipa_max = INT32_MIN, smissing = 0;
+    int32_t sdirect[MAXS] = {0, 0, 0, 0};
+    int32_t cmin = INT32_MAX, cmax = INT32_MIN, lacks = 0;
+    if (evaluated) {
+      for (int s = tid; s < own; s += nt) {
+        const uint32_t wd = sw[s];
+        DynRow r;
+#pragma unroll
+        for (int x = 0; x < 3; x++) {
+          r.alloc[x] = L.r64[x * cap + s];
+          r.req[x] = L.r64[(3 + x) * cap + s];
+          r.inv[x] = L.inv[x * cap + s];
+        }
+        r.nz[0] = L.r64[6 * cap + s];
+        r.nz[1] = L.r64[7 * cap + s];
+        r.pods = L.r32[s];
+        r.allowed = L.r32[cap + s];
+        SVal e = dyn_eval(prof, q.dyn, wd, r);
+        if (e.f == 0 && ((en >> KSS_F_POD_TOPOLOGY_SPREAD) & 1u) && q.n_hard > 0 &&
+            g_filter_pts(L, q, base, bins, hard_min, s, wd))
+          e.f = KSS_F_POD_TOPOLOGY_SPREAD;
+        if (e.f == 0 && ((en >> KSS_F_INTER_POD_AFFINITY) & 1u) && has_ipa && g_filter_ipa(L, q, base, bins, flags, s))
+          e.f = KSS_F_INTER_POD_AFFINITY;
+        int ign = 0;
+        if (e.f == 0) {
+          nf++;
+          max_tt = e.tt > max_tt ? e.tt : max_tt;
+          max_na = e.na > max_na ? e.na : max_na;
+          int64_t ipa = 0;
+          if (has_ipa) {
+            ipa = g_ipa_score(L, q, base, bins, s);
+            ipa_min = (int32_t)min((int64_t)ipa_min, ipa);
+            ipa_max = (int32_t)max((int64_t)ipa_max, ipa);
+          }
+          L.stt[s] = e.tt;
+          L.sna[s] = e.na;
+          L.sfit[s] = e.fit;
+          L.sba[s] = e.ba;
+          L.sipa[s] = ipa;
+          if (has_soft) {
+            if ((q.pflags & KSS_POD_PTS_REQUIRE_ALL) && !g_has_keys(L, soft, q.n_soft, s)) {
+              nign++;
+              ign = 1;
+            } else {
+              for (int i = 0; i < q.n_soft; i++) {
+                const GSpread& sp = soft[i];
+                int d = L.lbl[sp.key * cap + s];
+                if (sp.mode == SOFT_DIRECT) {
+                  if (d >= 0) sdirect[i]++;
+                  else smissing |= 1 << i;
+                } else if (sp.mode == SOFT_HIST) {
+                  if (d < 0) d = sp.empty;
+                  bins[q.total_bins + sp.poff + d] = 1;
+                }
+              }
+              if (one_soft) {  // the count the node's PodTopologySpread raw score is monotone in
+                const GSpread& sp = soft[0];
+                const int d = L.lbl[sp.key * cap + s];
+                int32_t cnt = -1;
+                if (d >= 0) {
+                  if (sp.mode == SOFT_HOST) cnt = (int32_t)g_sum(L, q, base, sp.ri_off, sp.ri_len, s);
+                  else if (sp.mode == SOFT_DIRECT) cnt = g_policy(sp, wd) ? (int32_t)g_sum(L, q, base, sp.ri_off, sp.ri_len, s) : 0;
+                  else cnt = bins[sp.off + d];
+                }
+                L.scnt[s] = cnt;
+                if (cnt < 0) lacks = 1;
+                else {
+                  cmin = min(cmin, cnt);
+                  cmax = max(cmax, cnt);
+                }
+              }
+            }
+          }
+        }
+        L.sf[s] = e.f | (ign << 16);
+      }
+    }
+    if (evaluated) {
+      int32_t v[13] = {nf, nign, max_tt, max_na, ipa_min, ipa_max, smissing, sdirect[0], sdirect[1], sdirect[2],
+                       sdirect[3], cmin, cmax};
+      const int op[13] = {OP_SUM, OP_SUM, OP_MAX, OP_MAX, OP_MIN, OP_MAX, OP_OR, OP_SUM, OP_SUM, OP_SUM, OP_SUM,
+                          OP_MIN, OP_MAX};
+      // lacks rides in smissing's bit 31 (OR)
+      if (lacks) v[6] |= (int32_t)0x80000000u;
+      if (!spread_reduce(H, L.xs, W, w, epoch, gran, err, v, op, 0, 0, q.total_bins + q.hard_pbins,
+                         has_soft ? q.total_pbins - q.hard_pbins : 0))
+        return;
+      nf = v[0];
+      nign = v[1];
+      max_tt = v[2];
+      max_na = v[3];
+      ipa_min = v[4];
+      ipa_max = v[5];
+      lacks = (v[6] >> 31) & 1;
+      smissing = v[6] & 0x7FFFFFFF;
+#pragma unroll
+      for (int i = 0; i < MAXS; i++) sdirect[i] = v[7 + i];
+      cmin = v[11];
+      cmax = v[12];
+      m.n_feasible = nf;
+      if (nf == 0) {
+        m.status = 1;
+        evaluated = false;
+      }
+    }
+    if (evaluated) {
+      const bool scored = nf > 1;
+      // ---- PodTopologySpread PreScore sizes + Score ----
+      long long pts_min = 0, pts_max = 0;
+      double wts[MAXS] = {0.0, 0.0, 0.0, 0.0};
+      if (scored && has_soft) {
+        int32_t sz[MAXS] = {0, 0, 0, 0};
+        for (int i = 0; i < q.n_soft; i++) {
+          const GSpread& sp = soft[i];
+          if (sp.mode != SOFT_HIST) continue;
+          for (int b = tid; b < sp.nb; b += nt) sz[i] += bins[q.total_bins + sp.poff + b] ? 1 : 0;
+        }
+        const int ops4[MAXS] = {OP_SUM, OP_SUM, OP_SUM, OP_SUM};
+        spread_reduce(H, L.xs, W, w, epoch, gran, err, sz, ops4, 0, 0, 0, 0, /*local=*/true);
+        for (int i = 0; i < q.n_soft; i++) {
+          const GSpread& sp = soft[i];
+          long long size;
+          if (sp.mode == SOFT_HOST) size = nf - nign;
+          else if (sp.mode == SOFT_DIRECT) size = sdirect[i] + ((smissing >> i) & 1);
+          else size = sz[i];
+          wts[i] = go_log_dev((double)(size + 2));  // topologyNormalizingWeight
+        }
+        if (one_soft) {  // scoreForCount is monotone in the count
+          const double c1 = (double)(soft[0].max_skew - 1);
+          pts_min = INT64_MAX;
+          if (cmax >= 0 && cmin != INT32_MAX) {
+            pts_min = (long long)round((double)cmin * wts[0] + c1);
+            pts_max = (long long)round((double)cmax * wts[0] + c1);
+          }
+          if (lacks) {  // a scored node without the key: raw round(0) = 0
+            pts_min = pts_min < 0 ? pts_min : 0;
+            pts_max = pts_max > 0 ? pts_max : 0;
+          }
+        } else {
+          long long pmin = INT64_MAX, pmax = 0;
+          for (int s = tid; s < own; s += nt) {
+            const int fi = L.sf[s];
+            if ((fi & 0xFFFF) != KSS_F_PASS) continue;
+            long long raw = 0;
+            if (!(fi >> 16)) {
+              double sc = 0.0;
+              for (int i = 0; i < q.n_soft; i++) {
+                const GSpread& sp = soft[i];
+                const int d = L.lbl[sp.key * cap + s];
+                if (d < 0) continue;
+                int64_t cnt;
+                if (sp.mode == SOFT_HOST) cnt = g_sum(L, q, base, sp.ri_off, sp.ri_len, s);
+                else if (sp.mode == SOFT_DIRECT) cnt = g_policy(sp, sw[s]) ? g_sum(L, q, base, sp.ri_off, sp.ri_len, s) : 0;
+                else cnt = bins[sp.off + d];
+                const double a = (double)cnt * wts[i];
+                sc = sc + (a + (double)(sp.max_skew - 1));
+              }
+              raw = (long long)round(sc);
+              pmin = raw < pmin ? raw : pmin;
+              pmax = raw > pmax ? raw : pmax;
+            }
+            L.spts[s] = raw;
+          }
+          // E3 in 32 bits: raw scores are bounded by the host (counts x log(N + 2) + maxSkew)
+          int32_t v2[2] = {(int32_t)min(pmin, (long long)INT32_MAX), (int32_t)pmax};
+          const int op2[2] = {OP_MIN, OP_MAX};
+          if (!spread_reduce(H, L.xs, W, w, epoch, gran, err, v2, op2)) return;
+          pts_min = v2[0] == INT32_MAX ? INT64_MAX : v2[0];
+          pts_max = v2[1];
+        }
+      }
+      // ---- NormalizeScore + weights + selectHost ----
+      const bool ipa_norm = (flags & 8) != 0;
+      const int64_t ipa_diff = (int64_t)ipa_max - (int64_t)ipa_min;
+      const float rtt = __builtin_amdgcn_rcpf((float)max(max_tt, 1));
+      const float rna = __builtin_amdgcn_rcpf((float)max(max_na, 1));
+      for (int s = tid; s < own; s += nt) {
+        const int fi = L.sf[s];
+        if ((fi & 0xFFFF) != KSS_F_PASS) continue;
+        int64_t total = 0;
+        if (scored) {
+          int64_t nm[KSS_NSCORE];
+          nm[KSS_S_TAINT_TOLERATION] = max_tt == 0 ? 100 : 100 - small_div(100 * L.stt[s], max_tt, rtt);
+          nm[KSS_S_NODE_AFFINITY] = max_na != 0 ? small_div(100 * L.sna[s], max_na, rna) : L.sna[s];
+          nm[KSS_S_NODE_RESOURCES_FIT] = L.sfit[s];
+          nm[KSS_S_VOLUME_BINDING] = 0;
+          {
+            int64_t raw = 0;
+            if (has_soft && !(fi >> 16)) {
+              if (one_soft) {
+                const int32_t cnt = L.scnt[s];
+                raw = cnt < 0 ? 0 : (long long)round((double)cnt * wts[0] + (double)(soft[0].max_skew - 1));
+              } else {
+                raw = L.spts[s];
+              }
+            }
+            int64_t& pv = nm[KSS_S_POD_TOPOLOGY_SPREAD];
+            if (has_soft && (fi >> 16)) pv = 0;
+            else if (pts_max == 0) pv = 100;
+            else pv = div_i64(100 * (pts_max + pts_min - raw), pts_max);
+          }
+          nm[KSS_S_INTER_POD_AFFINITY] = L.sipa[s];
+          if (ipa_norm) {
+            double f = 0.0;
+            if (ipa_diff > 0) f = 100.0 * ((double)(L.sipa[s] - ipa_min) / (double)ipa_diff);
+            nm[KSS_S_INTER_POD_AFFINITY] = (int64_t)f;
+          }
+          nm[KSS_S_BALANCED_ALLOCATION] = L.sba[s];
+          nm[KSS_S_IMAGE_LOCALITY] = 0;
+#pragma unroll
+          for (int x = 0; x < KSS_NSCORE; x++)
+            if ((prof.score_enabled >> x) & 1u) total += nm[x] * (int64_t)prof.weight[x];
+        }
+        const uint32_t g = (uint32_t)(c.node_base + lo + s);
+        const long long key = (long long)(((unsigned long long)(uint32_t)total << 32) | (0xFFFFFFFFull - g));
+        best = key > best ? key : best;
+      }
+      if (!spread_argmax(H, W, w, epoch, gran, err, kparity, best)) return;
+      kparity ^= 1;
+      const unsigned long long ub = (unsigned long long)best;
+      m.chosen = best ? (int)(0xFFFFFFFFull - (ub & 0xFFFFFFFFull)) : -1;
+      m.scored = scored ? 1 : 0;
+      m.best_total = scored ? (int64_t)(ub >> 32) : 0;
+    }
+    if (w == 0 && tid == 0) {
+      if (chosen) gchosen[k] = m.chosen;
+      if (meta) {
+        gmeta[k].chosen = m.chosen;
+        gmeta[k].n_feasible = m.n_feasible;
+        gmeta[k].scored = m.scored;
+        gmeta[k].status = m.status;
+        gmeta[k].best_total = m.best_total;
+      }
+    }
+    // ---- AssumePod on the winner's shard (node row, and the commit table) ----
+    const int x = m.chosen >= 0 ? m.chosen - c.node_base : -1;
+    if (x >= lo && x < hi && tid == 0) {
+      const int s = x - lo;
+      const SPod& pk = q.dyn;
+#pragma unroll
+      for (int r = 0; r < 3; r++) L.r64[(3 + r) * cap + s] += pk.creq[r];
+      L.r64[6 * cap + s] += pk.cnz[0];
+      L.r64[7 * cap + s] += pk.cnz[1];
+      L.r32[s] += 1;
+      if (pk.cls >= 0) L.delta[(size_t)pk.cls * cap + s] += 1;
+      for (int i = 0; i < pk.own_len; i++) L.delta[(size_t)(c.n_classes + ints[pk.own_off + i]) * cap + s] += 1;
+    }
+    // ---- prefetched data of pod k+1 / k+2 -> their LDS slots ----
+    if (pf_on) {
+      if (k + 2 < k1) reinterpret_cast<uint4*>(L.ring + (k + 2) % 3)[min(pf_lane, GPOD_Q - 1)] = pfq;
+#pragma unroll
+      for (int j = 0; j < G_PF; j++) {
+        if (j >= pf_per) break;
+        const int s = min(j * pf_n + pf_lane, own - 1);
+        L.st[((k + 1) & 1) * cap + s] = pfw[j];
+#pragma unroll
+        for (int r = 0; r < G_ROWS; r++) {
+          if (r >= nr1) break;
+          L.base[(((k + 1) & 1) * rows + r) * cap + s] = pfc[r][j];
+        }
+      }
+    }
+    lds_barrier();
+  }
+  // node state and the launch's commits back to HBM
+  __syncthreads();
+  for (int s = tid; s < own; s += nt) {
+    const int n = lo + s;
+#pragma unroll
+    for (int r = 0; r < 3; r++) c.requested[(size_t)r * N + n] = (int64_t)L.r64[(3 + r) * cap + s];
+    c.nonzero[n] = (int64_t)L.r64[6 * cap + s];
+    c.nonzero[N + n] = (int64_t)L.r64[7 * cap + s];
+    c.pod_count[n] = L.r32[s];
+    for (int r = 0; r < n_rowids; r++) {
+      const int dlt = L.delta[(size_t)r * cap + s];
+      if (!dlt) continue;
+      if (r < c.n_classes) c.class_count[(size_t)r * N + n] += dlt;
+      else c.term_count[(size_t)(r - c.n_classes) * N + n] += dlt;
+    }
+  }
+}
+
+}  // namespace kss

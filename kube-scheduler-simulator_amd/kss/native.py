@@ -54,6 +54,7 @@ SIGNATURES = [
     ("kss_last_loop_timing", C.c_int, [C.c_void_p, P(C.c_double)]),
     ("kss_last_geometry", C.c_int, [C.c_void_p, P(C.c_int32)]),
     ("kss_last_kernel", C.c_int, [C.c_void_p]),
+    ("kss_device_go_log", C.c_int, [C.c_int32, C.c_void_p, C.c_void_p, C.c_int32]),
     ("kss_fetch_meta", C.c_int, [C.c_void_p, C.c_int32, C.c_int32, P(C.c_int64)]),
     ("kss_set_names", C.c_int, [C.c_void_p, P(abi.Names)]),
     ("kss_format_annotations", C.c_int, [C.c_void_p, P(abi.PodResult), C.c_int32, C.c_char_p, C.c_size_t,
@@ -296,7 +297,7 @@ class Context:
         k = lib().kss_last_kernel(self.h)
         if k < 0:
             check(k)
-        return "k_simple" if k == 1 else "k_schedule"
+        return {1: "k_simple", 2: "k_spread"}.get(k, "k_schedule")
 
     def fetch_meta(self, n: int, first: int = 0) -> np.ndarray:
         """(n, 5) int64: chosen, n_feasible, scored, status, best_total of pods [first, first+n)."""
@@ -389,3 +390,11 @@ class Sweep:
             self.close()
         except Exception:
             pass
+
+
+def device_go_log(x, device: int = 0) -> np.ndarray:
+    """Go math.Log of every x as k_spread evaluates it on the device (kss_device_go_log)."""
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    y = np.empty_like(x)
+    check(lib().kss_device_go_log(device, x.ctypes.data, y.ctypes.data, len(x)))
+    return y

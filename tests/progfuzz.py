@@ -1,0 +1,175 @@
+"""Seeded random clusters whose pending pods carry every kind of PodTopologySpread /
+InterPodAffinity program the device path supports (test infrastructure).
+
+Unlike the BASELINE generators (kss/synth.py: one zone constraint, one hostname constraint,
+one app selector), these mix per pod:
+
+  * 0-2 DoNotSchedule and 0-3 ScheduleAnyway constraints over hostname (unique key),
+    zone / rack (shared keys, some nodes without the label) and instance type, maxSkew
+    1-3, NodeAffinityPolicy / NodeTaintsPolicy Honor or Ignore, matchLabels or
+    matchExpressions selectors;
+  * required pod affinity and anti-affinity, preferred affinity and anti-affinity with
+    weights, over the same keys;
+  * bound pods carrying required anti-affinity (existing-pod filter), and required /
+    preferred (anti-)affinity terms (existing-pod scores);
+  * NoExecute / NoSchedule / PreferNoSchedule taints, tolerations, nodeSelector, required
+    and preferred node affinity, spec.nodeName, a second namespace, small pod limits.
+
+Within one pod every constraint of one kind uses a distinct topology key (several
+constraints on one key are the open v1.26 same-key case, tested separately).
+"""
+import random
+from typing import Dict, List, Tuple
+
+ZONES = ["z0", "z1", "z2", "z3"]
+RACKS = ["r%d" % i for i in range(6)]
+ITYPES = ["small", "large", "gpu"]
+K_HOST = "kubernetes.io/hostname"
+K_ZONE = "topology.kubernetes.io/zone"
+K_RACK = "example.com/rack"
+K_ITYPE = "node.kubernetes.io/instance-type"
+APPS = 6
+
+
+def _node(i: int, r: random.Random) -> dict:
+    name = "n%05d" % i
+    labels: Dict[str, str] = {}
+    if r.random() >= 0.02:
+        labels[K_HOST] = name
+        if r.random() >= 0.05:
+            labels[K_ZONE] = ZONES[r.randrange(len(ZONES))]
+        if r.random() >= 0.10:
+            labels[K_RACK] = RACKS[r.randrange(len(RACKS))]
+        labels[K_ITYPE] = ITYPES[r.randrange(len(ITYPES))]
+    taints = []
+    if r.random() < 0.10:
+        taints.append({"key": "dedicated", "value": "infra", "effect": "NoSchedule"})
+    if r.random() < 0.04:
+        taints.append({"key": "evict", "value": "yes", "effect": "NoExecute"})
+    if r.random() < 0.08:
+        taints.append({"key": "spot", "value": "true", "effect": "PreferNoSchedule"})
+    cores = r.choice([2, 4, 8, 16])
+    spec: Dict = {}
+    if taints:
+        spec["taints"] = taints
+    if r.random() < 0.02:
+        spec["unschedulable"] = True
+    return {"metadata": {"name": name, "labels": labels}, "spec": spec,
+            "status": {"allocatable": {"cpu": str(cores), "memory": "%dGi" % (cores * 4),
+                                       "ephemeral-storage": "50Gi", "pods": str(r.choice([4, 8, 16, 110]))}}}
+
+
+def _sel(r: random.Random) -> dict:
+    if r.random() < 0.7:
+        return {"matchLabels": {"app": "a%d" % r.randrange(APPS)}}
+    vals = sorted({"a%d" % r.randrange(APPS) for _ in range(2)})
+    return {"matchExpressions": [{"key": "app", "operator": "In", "values": vals}]}
+
+
+def _term(r: random.Random, keys: List[str]) -> dict:
+    return {"labelSelector": _sel(r), "topologyKey": r.choice(keys)}
+
+
+def _requests(r: random.Random) -> dict:
+    if r.random() < 0.05:
+        return {}
+    return {"cpu": "%dm" % r.choice([100, 250, 500, 1000]), "memory": "%dMi" % r.choice([128, 256, 512, 1024])}
+
+
+def _bound(i: int, k: int, node: str, r: random.Random) -> dict:
+    spec: Dict = {"nodeName": node, "containers": [{"name": "c", "resources": {"requests": _requests(r)}}]}
+    aff: Dict = {}
+    u = r.random()
+    if u < 0.15:
+        aff["podAntiAffinity"] = {"requiredDuringSchedulingIgnoredDuringExecution": [_term(r, [K_HOST, K_ZONE])]}
+    elif u < 0.30:
+        aff["podAffinity"] = {"preferredDuringSchedulingIgnoredDuringExecution": [
+            {"weight": r.randint(1, 100), "podAffinityTerm": _term(r, [K_ZONE, K_RACK, K_HOST])}]}
+    elif u < 0.38:
+        aff["podAntiAffinity"] = {"preferredDuringSchedulingIgnoredDuringExecution": [
+            {"weight": r.randint(1, 100), "podAffinityTerm": _term(r, [K_ZONE, K_RACK])}]}
+    elif u < 0.45:
+        aff["podAffinity"] = {"requiredDuringSchedulingIgnoredDuringExecution": [_term(r, [K_ZONE, K_RACK])]}
+    if aff:
+        spec["affinity"] = aff
+    ns = "default" if r.random() < 0.9 else "other"
+    return {"metadata": {"name": "b%05d-%d" % (i, k), "namespace": ns, "labels": {"app": "a%d" % r.randrange(APPS)}},
+            "spec": spec}
+
+
+def _spread(r: random.Random, key: str, hard: bool) -> dict:
+    c = {"maxSkew": r.randint(1, 3), "topologyKey": key,
+         "whenUnsatisfiable": "DoNotSchedule" if hard else "ScheduleAnyway", "labelSelector": _sel(r)}
+    if r.random() < 0.25:
+        c["nodeAffinityPolicy"] = r.choice(["Honor", "Ignore"])
+    if r.random() < 0.25:
+        c["nodeTaintsPolicy"] = r.choice(["Honor", "Ignore"])
+    return c
+
+
+def _pending(j: int, r: random.Random, node_names: List[str]) -> dict:
+    spec: Dict = {"containers": [{"name": "c", "resources": {"requests": _requests(r)}}]}
+    tols = []
+    if r.random() < 0.3:
+        tols.append({"key": "dedicated", "operator": "Exists", "effect": "NoSchedule"})
+    if r.random() < 0.2:
+        tols.append({"key": "evict", "operator": "Equal", "value": "yes", "effect": "NoExecute"})
+    if r.random() < 0.3:
+        tols.append({"key": "spot", "operator": "Exists", "effect": "PreferNoSchedule"})
+    if tols:
+        spec["tolerations"] = tols
+    if r.random() < 0.1:
+        spec["nodeSelector"] = {K_ITYPE: r.choice(ITYPES)}
+    aff: Dict = {}
+    na: Dict = {}
+    if r.random() < 0.1:
+        na["requiredDuringSchedulingIgnoredDuringExecution"] = {"nodeSelectorTerms": [{"matchExpressions": [
+            {"key": K_ZONE, "operator": "In", "values": sorted(set(r.sample(ZONES, 2)))}]}]}
+    if r.random() < 0.2:
+        na["preferredDuringSchedulingIgnoredDuringExecution"] = [
+            {"weight": r.randint(1, 100), "preference": {"matchExpressions": [
+                {"key": K_RACK, "operator": "In", "values": [r.choice(RACKS)]}]}}]
+    if na:
+        aff["nodeAffinity"] = na
+    hard = r.sample([K_ZONE, K_RACK, K_HOST], r.choice([0, 0, 1, 1, 2]))
+    soft = r.sample([K_ZONE, K_RACK, K_HOST, K_ITYPE], r.choice([0, 1, 1, 2, 3]))
+    tsc = [_spread(r, k, True) for k in hard] + [_spread(r, k, False) for k in soft]
+    r.shuffle(tsc)
+    if tsc:
+        spec["topologySpreadConstraints"] = tsc
+    pa: Dict = {}
+    pn: Dict = {}
+    if r.random() < 0.12:
+        pa["requiredDuringSchedulingIgnoredDuringExecution"] = [_term(r, [K_ZONE, K_RACK])]
+    if r.random() < 0.2:
+        pn["requiredDuringSchedulingIgnoredDuringExecution"] = [_term(r, [K_HOST, K_ZONE])]
+    if r.random() < 0.3:
+        pa["preferredDuringSchedulingIgnoredDuringExecution"] = [
+            {"weight": r.randint(1, 100), "podAffinityTerm": _term(r, [K_ZONE, K_RACK, K_HOST])}]
+    if r.random() < 0.2:
+        pn["preferredDuringSchedulingIgnoredDuringExecution"] = [
+            {"weight": r.randint(1, 100), "podAffinityTerm": _term(r, [K_ZONE, K_RACK, K_ITYPE])}]
+    if pa:
+        aff["podAffinity"] = pa
+    if pn:
+        aff["podAntiAffinity"] = pn
+    if aff:
+        spec["affinity"] = aff
+    if r.random() < 0.02:
+        spec["nodeName"] = r.choice(node_names)
+    ns = "default" if r.random() < 0.9 else "other"
+    return {"metadata": {"name": "p%05d" % j, "namespace": ns, "labels": {"app": "a%d" % r.randrange(APPS)}},
+            "spec": spec}
+
+
+def make(seed: int, n_nodes: int, n_pods: int, bound_per_node: Tuple[int, int] = (0, 3)):
+    """(nodes, bound_pods, pending_pods) for one seed."""
+    r = random.Random(seed)
+    nodes = [_node(i, r) for i in range(n_nodes)]
+    names = [n["metadata"]["name"] for n in nodes]
+    bound = []
+    for i, nm in enumerate(names):
+        for k in range(r.randint(*bound_per_node)):
+            bound.append(_bound(i, k, nm, r))
+    pods = [_pending(j, r, names) for j in range(n_pods)]
+    return nodes, bound, pods

@@ -6,8 +6,8 @@ cases in test_gpu_parity.py do not reach, compared bit-exactly with the C oracle
   * the whole C2 batch the bench times (5,000 nodes x 10,000 pods on k_simple);
   * k_simple at 100,000 nodes: 128 shards x 4 node slots per lane, i.e. both chunks of the
     shard-granule sweep (kss_simple.cuh simple_exchange, SX_CHUNKS);
-  * C4's recipe (100,000 nodes, zone DoNotSchedule spread) on one GPU (k_schedule, 256
-    shards) and the node-axis kernels at 100,000 rows, world 1;
+  * C4's recipe (100,000 nodes, zone DoNotSchedule spread) on one GPU (k_spread and
+    k_schedule, 256 shards) and the node-axis kernels at 100,000 rows, world 1;
   * a 64-scenario slice of the C5 sweep (1,000 nodes x 1,000 pods each).
 """
 import os
@@ -88,6 +88,7 @@ def test_c3_full_batch_no_record():
     ctx.load(s.cluster)
     ctx.stage(s.pods)
     np.testing.assert_array_equal(ctx.run_staged(n_pods), chosen_o)
+    assert ctx.last_kernel() == "k_spread"
     _meta_equal(ctx.fetch_meta(n_pods), res, n_pods)
     _state_equal(ctx, st, n_nodes, s.cluster.n_classes, s.cluster.n_terms)
     ctx.close()
@@ -153,9 +154,12 @@ def test_k_simple_forced_shards_above_one_chunk(shards, monkeypatch):
     ctx.close()
 
 
-def test_c4_recipe_on_one_gpu():
-    """BASELINE configs[3]'s recipe (100,000 nodes, zone DoNotSchedule spread) on one GPU:
-    the general kernel at 256 shards, 200 pods."""
+@pytest.mark.parametrize("kernel", ["k_spread", "k_schedule"])
+def test_c4_recipe_on_one_gpu(kernel, monkeypatch):
+    """BASELINE configs[3]'s recipe (100,000 nodes, zone DoNotSchedule spread) on one GPU at
+    256 shards, 200 pods: k_spread, and the general kernel (KSS_NO_SPREAD)."""
+    if kernel == "k_schedule":
+        monkeypatch.setenv("KSS_NO_SPREAD", "1")
     prof = abi.default_profile()
     n_nodes, n_pods = 100000, 200
     s = native.Synth(4, 0, n_nodes, n_pods)
@@ -164,7 +168,7 @@ def test_c4_recipe_on_one_gpu():
     ctx.load(s.cluster)
     ctx.stage(s.pods)
     chosen = ctx.run_staged(n_pods)
-    assert ctx.last_kernel() == "k_schedule"
+    assert ctx.last_kernel() == kernel
     np.testing.assert_array_equal(chosen, chosen_o)
     _meta_equal(ctx.fetch_meta(n_pods), res, n_pods)
     _state_equal(ctx, st, n_nodes, s.cluster.n_classes, 0)

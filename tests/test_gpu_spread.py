@@ -1,0 +1,165 @@
+"""k_spread (kss_spread.cuh): the sequential loop for batches with PodTopologySpread /
+InterPodAffinity programs, bit-exact against the C oracle.
+
+  * seeded program fuzz (tests/progfuzz.py: every constraint / term kind, policies,
+    unique and shared keys, missing labels) in the automatic, single-workgroup and forced
+    multi-shard geometries;
+  * several launches per batch (static-word chunks; the count rows the launches commit
+    are carried in HBM between them), a non-default profile (k_spread<false>);
+  * the device restatement of Go math.Log against the host port, bit for bit;
+  * k_spread and k_schedule agree on the same batch.
+The full-size C3 / C4 batches are in test_gpu_scale.py.
+"""
+import numpy as np
+import pytest
+
+import oracle_c
+import progfuzz
+from kss import abi, native
+from kss.compile import compile_cluster
+
+pytestmark = pytest.mark.gpu
+
+MODES = {"auto": 0, "single": abi.KSS_SCHED_FORCE_SINGLE_WG, "multi": abi.KSS_SCHED_FORCE_MULTI_WG}
+
+
+def _oracle(prof, cl, ps, n, n_nodes, n_classes, n_terms):
+    return oracle_c.schedule(prof, cl, ps, n, n_nodes, record="meta", threads=8, n_classes=n_classes, n_terms=n_terms)
+
+
+def _check(ctx, res, st, chosen, chosen_o, n, n_nodes, n_classes, n_terms):
+    np.testing.assert_array_equal(chosen, chosen_o)
+    meta = ctx.fetch_meta(n)
+    for j in range(n):
+        m = res.meta(j)
+        got = dict(chosen=meta[j, 0], n_feasible=meta[j, 1], scored=meta[j, 2], status=meta[j, 3])
+        assert got == {k: m[k] for k in got}, (j, got, m)
+        if m["scored"]:
+            assert meta[j, 4] == m["best_total"], j
+    g = ctx.node_state()
+    np.testing.assert_array_equal(g["requested"][:, :n_nodes], st["requested"][:, :n_nodes])
+    np.testing.assert_array_equal(g["nonzero"][:, :n_nodes], st["nonzero"][:, :n_nodes])
+    np.testing.assert_array_equal(g["pod_count"][:n_nodes], st["pod_count"][:n_nodes])
+    if n_classes:
+        np.testing.assert_array_equal(g["class_count"][:n_classes], st["class_count"][:n_classes])
+    if n_terms:
+        np.testing.assert_array_equal(g["term_count"][:n_terms], st["term_count"][:n_terms])
+
+
+def _fuzz(seed, n_nodes, n_pods):
+    nodes, bound, pods = progfuzz.make(seed, n_nodes, n_pods)
+    cc, cp, _ = compile_cluster(nodes, bound, pods)
+    return cc, cp
+
+
+@pytest.mark.parametrize("mode", ["auto", "single", "multi"])
+@pytest.mark.parametrize("seed,n_nodes,n_pods", [(1, 60, 200), (2, 300, 300), (3, 700, 250), (4, 5, 40),
+                                                 (5, 1000, 200)])
+def test_program_fuzz_matches_oracle(seed, n_nodes, n_pods, mode):
+    prof = abi.default_profile()
+    cc, cp = _fuzz(seed, n_nodes, n_pods)
+    ncl, nt = len(cc.classes), len(cc.terms)
+    chosen_o, res, st = _oracle(prof, cc.as_struct(), cp.as_struct(), cp.n, cc.n_nodes, ncl, nt)
+    ctx = native.Context(prof)
+    ctx.load(cc.as_struct())
+    chosen = ctx.schedule_batch(cp.as_struct(), cp.n, flags=MODES[mode])
+    # one workgroup holding hundreds of nodes' rows, counts and commit table exceeds the LDS
+    # budget: k_schedule takes the batch (parity is checked either way)
+    assert ctx.last_kernel() == "k_spread" or (mode == "single" and n_nodes > 100)
+    geo = ctx.last_geometry()
+    if mode == "single":
+        assert geo["shards"] == 1
+    if mode == "multi" and n_nodes >= 4:
+        assert geo["shards"] > 1
+    _check(ctx, res, st, chosen, chosen_o, cp.n, cc.n_nodes, ncl, nt)
+    ctx.close()
+
+
+def test_program_fuzz_many_seeds_forced_shards(monkeypatch):
+    """Twelve more seeds at 9 shards (ragged last shard)."""
+    monkeypatch.setenv("KSS_SHARDS", "9")
+    prof = abi.default_profile()
+    for seed in range(20, 32):
+        cc, cp = _fuzz(seed, 211, 150)
+        ncl, nt = len(cc.classes), len(cc.terms)
+        chosen_o, res, st = _oracle(prof, cc.as_struct(), cp.as_struct(), cp.n, cc.n_nodes, ncl, nt)
+        ctx = native.Context(prof)
+        ctx.load(cc.as_struct())
+        chosen = ctx.schedule_batch(cp.as_struct(), cp.n)
+        assert ctx.last_kernel() == "k_spread" and ctx.last_geometry()["shards"] == 9
+        _check(ctx, res, st, chosen, chosen_o, cp.n, cc.n_nodes, ncl, nt)
+        ctx.close()
+
+
+def test_k_spread_static_chunks(monkeypatch):
+    """KSS_STATIC_BYTES forces one k_static + one k_spread launch per 23 pods: the commits of
+    every launch reach HBM (node rows and count rows) before the next one reads them."""
+    s = native.Synth(3, 0, 2000, 300)
+    monkeypatch.setenv("KSS_STATIC_BYTES", str(4 * 2000 * 23))
+    prof = abi.default_profile()
+    chosen_o, res, st = _oracle(prof, s.cluster, s.pods, 300, 2000, s.cluster.n_classes, s.cluster.n_terms)
+    ctx = native.Context(prof)
+    ctx.load(s.cluster)
+    ctx.stage(s.pods)
+    chosen = ctx.run_staged(300)
+    assert ctx.last_kernel() == "k_spread"
+    assert ctx.last_timing()[1] == 2 * ((300 + 22) // 23)
+    _check(ctx, res, st, chosen, chosen_o, 300, 2000, s.cluster.n_classes, s.cluster.n_terms)
+    ctx.close()
+
+
+def test_k_spread_custom_profile():
+    """A non-default profile (k_spread<false>: profile staged in LDS): MostAllocated,
+    three BalancedAllocation resources, other plugin weights."""
+    prof = abi.default_profile()
+    prof.fit_strategy = abi.KSS_FIT_MOST_ALLOCATED
+    prof.fit_weight[0], prof.fit_weight[1] = 3, 2
+    prof.ba_n = 3
+    prof.ba_res[2] = abi.KSS_RES_EPHEMERAL
+    prof.weight[abi.KSS_S_POD_TOPOLOGY_SPREAD] = 5
+    prof.weight[abi.KSS_S_INTER_POD_AFFINITY] = 7
+    prof.weight[abi.KSS_S_TAINT_TOLERATION] = 1
+    cc, cp = _fuzz(7, 400, 250)
+    ncl, nt = len(cc.classes), len(cc.terms)
+    chosen_o, res, st = _oracle(prof, cc.as_struct(), cp.as_struct(), cp.n, cc.n_nodes, ncl, nt)
+    ctx = native.Context(prof)
+    ctx.load(cc.as_struct())
+    chosen = ctx.schedule_batch(cp.as_struct(), cp.n)
+    assert ctx.last_kernel() == "k_spread"
+    _check(ctx, res, st, chosen, chosen_o, cp.n, cc.n_nodes, ncl, nt)
+    ctx.close()
+
+
+def test_k_spread_and_k_schedule_agree(monkeypatch):
+    s = native.Synth(3, 5, 3000, 800)
+    prof = abi.default_profile()
+    ctx = native.Context(prof)
+    ctx.load(s.cluster)
+    ctx.stage(s.pods)
+    a = ctx.run_staged(800).copy()
+    assert ctx.last_kernel() == "k_spread"
+    st_a = ctx.node_state()
+    ctx.reset()
+    b = ctx.schedule_batch(s.pods, 800, flags=abi.KSS_SCHED_GENERAL_KERNEL)
+    assert ctx.last_kernel() == "k_schedule"
+    np.testing.assert_array_equal(a, b)
+    st_b = ctx.node_state()
+    for k in st_a:
+        np.testing.assert_array_equal(st_a[k], st_b[k])
+    ctx.close()
+
+
+def test_device_go_log_matches_host_port():
+    """go_log_dev (k_spread's topologyNormalizingWeight) == the host port (which builds
+    k_schedule's table and is pinned against the oracle) for every size up to 10^6 + 2."""
+    from kss.native import lib
+    import ctypes as C
+    L = lib()
+    L.kss_go_log_c.restype = C.c_double
+    L.kss_go_log_c.argtypes = [C.c_double]
+    x = np.arange(2, 1_000_003, dtype=np.float64)
+    y = native.device_go_log(x)
+    for k in list(range(0, 5000)) + list(range(5000, len(x), 997)):
+        assert y[k] == L.kss_go_log_c(x[k]), (x[k], y[k])
+    host = np.array([L.kss_go_log_c(v) for v in x[::101]])
+    np.testing.assert_array_equal(y[::101], host)

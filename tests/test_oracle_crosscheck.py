@@ -20,3 +20,12 @@ def test_spread_and_interpod_affinity(n_nodes, n_pods):
 def test_zone_spread_c4_recipe():
     nodes, bound, pods = synth.make_cluster(4, 60, 150)
     run_both(nodes, bound, pods)
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_program_fuzz(seed):
+    """Every spread / inter-pod program kind (tests/progfuzz.py), the programs k_spread's
+    GPU parity tests run, with per-node verdicts and raw / normalized scores compared."""
+    import progfuzz
+    nodes, bound, pods = progfuzz.make(1000 + seed, 70, 110)
+    run_both(nodes, bound, pods)
