@@ -450,6 +450,12 @@ int kss_format_annotations_ex(const kss_names* names, const kss_profile* prof, c
                               int32_t n_nodes, int32_t n_taints, int32_t n_scalar, char* buf, size_t cap, size_t* need);
 /* sizeof() of every ABI struct, in header order; returns the count written (ABI self-check) */
 int kss_abi_sizes(int32_t* out, int32_t n);
+/* Host only (no device): which sequential-loop kernel a staged, unrecorded batch of `ps` on
+ * `cl` can take, by its pod programs: out3[0] = 1 k_simple, 2 k_spread, 0 k_schedule only;
+ * out3[1] = the first pod that rules out k_spread (-1 none), out3[2] = the reason code
+ * (kss_plan_reason).  The launch still checks LDS geometry and value bounds. */
+int kss_plan_podset(const kss_cluster* cl, const kss_podset* ps, int32_t* out3);
+const char* kss_plan_reason(int32_t code);
 /* Test support: y[i] = the device restatement of Go math.Log (kss_spread.cuh go_log_dev,
  * PodTopologySpread's topologyNormalizingWeight in k_spread) at x[i], i < n, evaluated on
  * `device`; host arrays.  Compared bitwise with the host port (kss_go_log_c) by the tests. */

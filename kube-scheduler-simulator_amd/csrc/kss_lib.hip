@@ -86,6 +86,7 @@ struct DevJob {
   const SPod* spods;  // k_simple: compact pod records [n_pods]
   uint32_t* stat;     // k_static -> k_simple / k_spread: static words of the current pod chunk [chunk][N]
   const GPod* gpods;  // k_spread: host-resolved pod programs [n_pods]
+  const int32_t* res_rows;  // k_spread: the count rows resident in LDS (GpodNeeds::res_rows)
   kss_profile prof;   // k_simple<false>: staged word by word into LDS (a by-value kernel argument would land in scratch)
 };
 
@@ -187,7 +188,8 @@ __global__ __launch_bounds__(KSS_MAX_THREADS) void k_simple(const DevJob* __rest
 // presence values of the exchange vector.  DEF: the v1.26 default profile, folded.
 template <bool DEF>
 __global__ __launch_bounds__(KSS_MAX_THREADS) void k_spread(const DevJob* __restrict__ jobs, int W, int cap, int bins_cap,
-                                                            int rows, int k0, int k1, unsigned long long* gran, int* err) {
+                                                            int n_res, int gq, int k0, int k1, unsigned long long* gran,
+                                                            int* err) {
   extern __shared__ __attribute__((aligned(16))) long long smem[];
   const int ji = blockIdx.x / W, w = blockIdx.x % W;
   const DevJob job = jobs[ji];
@@ -200,8 +202,8 @@ __global__ __launch_bounds__(KSS_MAX_THREADS) void k_spread(const DevJob* __rest
     __syncthreads();
   }
   const kss_profile& P = DEF ? def_prof : H.prof;
-  spread_schedule(job.c, job.gpods, job.stat, job.P.ints, k0, min(k1, job.n_pods), job.chosen, job.meta, P, W, w, cap,
-                  bins_cap, rows, gran ? gran + (size_t)ji * 2 * W * G_XW : nullptr, err, smem);
+  spread_schedule(job.c, job.gpods, job.stat, job.res_rows, n_res, k0, min(k1, job.n_pods), job.chosen, job.meta, P, W, w,
+                  cap, bins_cap, gq, gran ? gran + (size_t)ji * 2 * W * G_XW : nullptr, err, smem);
 }
 
 // Class / term counts of the chosen nodes of pods [k0, min(k1, n_pods)) of every job
@@ -276,14 +278,14 @@ struct F64Bounds {
 
 // What the staged batch asks of k_spread (the host side of the GPod plans).
 struct GpodNeeds {
-  int bins_cap = 0;      // max histogram + presence bins of a pod
-  int rows = 1;          // max count rows of a pod (LDS rows of the prefetched counts)
-  int max_mult = 1;      // max commits one pod adds to one count row
-  int max_own = 0;       // max term rows one pod adds
-  int max_len = 1;       // max rows summed by one constraint / entry
-  int64_t coef_sum = 0;  // max Σ|coef| of a pod's InterPodAffinity score entries
-  int max_soft = 0;      // max ScheduleAnyway constraints of a pod with more than one
-  int64_t max_skew = 0;  // their largest maxSkew
+  int bins_cap = 0;       // max histogram + presence bins of a pod
+  int max_mult = 1;       // max commits one pod adds to one count row
+  int64_t ref_weight = 1; // max Σ|coefficient| over the references of one constraint / entry
+  int max_soft = 0;       // max ScheduleAnyway constraints of a pod with more than one
+  int64_t max_skew = 0;   // their largest maxSkew
+  std::vector<int32_t> res_rows;  // the resident count rows: class r as r, term r as n_classes + r
+  int gq = 0;             // record stride (uint4) of the batch
+  int fail_code = 0, fail_pod = -1;  // why / where build_gpods refused (GP_*)
 };
 
 // Per-batch LDS / exchange sizing: the host restatement of make_plan's bin counts.
@@ -340,13 +342,15 @@ struct kss_ctx {
   bool spod_ok = false;
   // host-resolved programs of the staged pods for k_spread (gpod_ok false: k_schedule)
   DevBuf gpod_buf;
-  std::vector<GPod> gpod_host;
+  std::vector<uint4> gpod_host;  // records, gneed.gq uint4 each
   bool gpod_ok = false;
   GpodNeeds gneed;
   bool no_spread = false;     // KSS_NO_SPREAD: batches with programs always take k_schedule
   double count_bound0 = 0;    // max(Σ class_count, Σ term_count) of the loaded snapshot
   double count_bound = 0;     // the same, plus every commit since (spread_bounds_ok)
-  int max_allowed = 0;        // max AllowedPodNumber of the loaded snapshot
+  double cell_bound0 = 0;     // max single class_count / term_count entry of the loaded snapshot
+  double cell_bound = 0;      // the same, plus every commit since
+  DevBuf res_buf;             // GpodNeeds::res_rows on the device
   int staged_max_own = 0;     // max own term rows of a staged pod
   std::vector<int32_t> key_empty_h;
   bool no_simple = false;  // KSS_NO_SIMPLE: always launch k_schedule
@@ -523,42 +527,102 @@ bool build_spods(const kss_podset* ps, int n_scalar, std::vector<SPod>& out) {
 }
 
 // Host-resolved programs (kss_spread.cuh GPod) of every pod of a validated podset: the
-// restatement of make_plan (kss_sched.cuh) plus the table of count rows each constraint and
-// entry sums.  False when some pod exceeds the record's fixed tables or an exchange's
-// payload (the batch then runs on k_schedule).
+// restatement of make_plan (kss_sched.cuh), every constraint / entry as (resident count row,
+// coefficient) references, InterPodAffinity score entries merged per topology key, and the
+// batch's resident row set (every row some pod reads).  False when some pod exceeds the
+// record's fixed tables or an exchange's payload (the batch then runs on k_schedule).
+// Why build_gpods refused a batch (kss_plan_podset): code, pod.
+enum {
+  GP_OK = 0,
+  GP_NA_WEIGHTS,
+  GP_CONSTRAINTS,
+  GP_ROWS,
+  GP_COEF,
+  GP_REFS,
+  GP_KEYS,
+  GP_BINS,
+  GP_XW,
+  GP_COMMIT,
+  GP_RECORD,
+  GP_IPA,
+  GP_NCODES
+};
+const char* const kGpReason[GP_NCODES] = {
+    "eligible",
+    "preferred NodeAffinity weights exceed the static word",
+    "more than 4 spread constraints of one kind",
+    "more than 65536 resident count rows",
+    "a merged score coefficient exceeds 16 bits",
+    "too many count-row references",
+    "more than 4 inter-pod-affinity topology keys",
+    "too many histogram bins",
+    "exchange payload too large",
+    "the commit adds to more than 8 count rows",
+    "a pod's record exceeds 2 KiB (too many references)",
+    "more than 16 inter-pod-affinity entries after merging",
+};
+
+bool gfail(GpodNeeds& need, int code, int pod) {
+  need.fail_code = code;
+  need.fail_pod = pod;
+  return false;
+}
+
 bool build_gpods(const kss_podset* ps, int n_scalar, int n_classes, const int32_t* key_card, const uint32_t* key_flags,
-                 const int32_t* key_empty, std::vector<GPod>& out, GpodNeeds& need) {
-  out.assign((size_t)std::max(ps->n_pods, 1), GPod{});
+                 const int32_t* key_empty, std::vector<uint4>& words, GpodNeeds& need) {
+  std::vector<GPod> out((size_t)std::max(ps->n_pods, 1), GPod{});
+  std::vector<std::vector<uint32_t>> refs_of((size_t)std::max(ps->n_pods, 1));
   need = GpodNeeds{};
+  std::vector<int32_t> local;  // count row -> resident index (-1 none)
+  auto res_of = [&](int rowid) -> int {
+    if ((size_t)rowid >= local.size()) local.resize((size_t)rowid + 1, -1);
+    if (local[(size_t)rowid] < 0) {
+      local[(size_t)rowid] = (int32_t)need.res_rows.size();
+      need.res_rows.push_back(rowid);
+    }
+    return local[(size_t)rowid];
+  };
   for (int i = 0; i < ps->n_pods; i++) {
     const kss_pod& p = ps->pods[i];
     GPod& g = out[(size_t)i];
-    if (!fill_spod(ps, p, n_scalar, g.dyn)) return false;
-    if (p.n_hard > MAXH || p.n_soft > MAXS || p.ipa_len > G_IPA) return false;
+    std::vector<uint32_t>& R = refs_of[(size_t)i];
+    if (!fill_spod(ps, p, n_scalar, g.dyn)) return gfail(need, GP_NA_WEIGHTS, i);
+    if (p.n_hard > MAXH || p.n_soft > MAXS) return gfail(need, GP_CONSTRAINTS, i);
     g.pflags = (int32_t)p.flags;
     g.n_hard = p.n_hard;
     g.n_soft = p.n_soft;
-    g.n_ipa = p.ipa_len;
-    int nref = 0;
-    auto row_of = [&](bool term, int r) -> int {
-      const int32_t code = term ? ((1 << 30) | r) : r;
-      for (int j = 0; j < g.n_rows; j++)
-        if (g.row[j] == code) return j;
-      if (g.n_rows >= G_ROWS) return -1;
-      g.row[g.n_rows] = code;
-      g.rowid[g.n_rows] = term ? n_classes + r : r;
-      return g.n_rows++;
-    };
-    auto refs = [&](bool term, int off, int len, int32_t& ri_off, int32_t& ri_len) -> bool {
-      ri_off = nref;
-      ri_len = len;
-      need.max_len = std::max(need.max_len, len);
-      for (int j = 0; j < len; j++) {
-        const int x = row_of(term, ps->ints[off + j]);
-        if (x < 0 || nref >= G_RIDX) return false;
-        g.ridx[nref++] = (int16_t)x;
+    // references [ri_off, +ri_len) for (rowid, coef) pairs, equal rows merged:
+    // resident row index | coefficient << 16
+    std::vector<int64_t> coef;
+    auto refs = [&](const std::vector<std::pair<int, int64_t>>& rows, int16_t& ri_off, int16_t& ri_len) -> bool {
+      const int o = (int)R.size();
+      for (const auto& rc : rows) {
+        const int l = res_of(rc.first);
+        if (l > 0xFFFF) return gfail(need, GP_ROWS, i);
+        int j = o;
+        while (j < (int)R.size() && (int)(R[(size_t)j] & 0xFFFFu) != l) j++;
+        if (j == (int)R.size()) {
+          R.push_back((uint32_t)l);
+          coef.push_back(0);
+        }
+        coef[(size_t)j] += rc.second;
+        if (coef[(size_t)j] < -32768 || coef[(size_t)j] > 32767) return gfail(need, GP_COEF, i);
       }
+      int64_t wsum = 0;
+      for (size_t j = (size_t)o; j < R.size(); j++) {
+        R[j] = (R[j] & 0xFFFFu) | ((uint32_t)(uint16_t)(int16_t)coef[j] << 16);
+        wsum += std::abs(coef[j]);
+      }
+      if (R.size() > 32767) return gfail(need, GP_REFS, i);
+      ri_off = (int16_t)o;
+      ri_len = (int16_t)(R.size() - (size_t)o);
+      need.ref_weight = std::max(need.ref_weight, wsum);
       return true;
+    };
+    auto list = [&](int off, int len, bool term) {
+      std::vector<std::pair<int, int64_t>> v;
+      for (int j = 0; j < len; j++) v.push_back({(term ? n_classes : 0) + ps->ints[off + j], 1});
+      return v;
     };
     int off = 0, poff = 0;
     bool stats = false;
@@ -566,13 +630,13 @@ bool build_gpods(const kss_podset* ps, int n_scalar, int n_classes, const int32_
     for (int c = 0; c < p.n_hard + p.n_soft; c++) {
       const kss_spread& s = sp[c];
       GSpread& d = g.sp[c];
-      d.key = s.key;
+      d.key = (int16_t)s.key;
       d.max_skew = s.max_skew;
-      d.self_match = s.self_match;
-      d.flags = s.flags;
-      if (!refs(false, s.cls_off, s.cls_len, d.ri_off, d.ri_len)) return false;
-      d.empty = key_empty[s.key];
-      d.nb = key_card[s.key] + 1;
+      d.self_match = (int16_t)s.self_match;
+      d.flags = (int16_t)s.flags;
+      if (!refs(list(s.cls_off, s.cls_len, false), d.ri_off, d.ri_len)) return gfail(need, GP_REFS, i);
+      d.empty = (int16_t)key_empty[s.key];
+      d.nb = (int16_t)(key_card[s.key] + 1);
       d.off = d.poff = -1;
       d.mode = SOFT_HOST;
     }
@@ -580,8 +644,8 @@ bool build_gpods(const kss_podset* ps, int n_scalar, int n_classes, const int32_
       GSpread& d = g.sp[c];
       stats = true;
       if (!(key_flags[d.key] & KSS_KEY_UNIQUE)) {
-        d.off = off;
-        d.poff = poff;
+        d.off = (int16_t)off;
+        d.poff = (int16_t)poff;
         off += d.nb;
         poff += d.nb;
       }
@@ -595,8 +659,8 @@ bool build_gpods(const kss_podset* ps, int n_scalar, int n_classes, const int32_
         d.mode = SOFT_DIRECT;
       } else {
         d.mode = SOFT_HIST;
-        d.off = off;
-        d.poff = poff;
+        d.off = (int16_t)off;
+        d.poff = (int16_t)poff;
         off += d.nb;
         poff += d.nb;
         stats = true;
@@ -606,72 +670,119 @@ bool build_gpods(const kss_podset* ps, int n_scalar, int n_classes, const int32_
         need.max_skew = std::max<int64_t>(need.max_skew, std::abs((int64_t)d.max_skew));
       }
     }
+    // inter-pod affinity: key slots in entry order (make_plan), score entries merged per slot
     const kss_ipa* ip = ps->ipa + p.ipa_off;
-    int64_t csum = 0;
+    std::vector<int> slot_of((size_t)std::max(p.ipa_len, 1));
     for (int e = 0; e < p.ipa_len; e++) {
-      const kss_ipa& en = ip[e];
-      GIpa& d = g.ipa[e];
       int k = -1;
       for (int j = 0; j < g.n_keys; j++)
-        if (g.key[j] == en.key) k = j;
+        if (g.key[j] == ip[e].key) k = j;
       if (k < 0) {
-        if (g.n_keys >= MAXK) return false;
+        if (g.n_keys >= MAXK) return gfail(need, GP_KEYS, i);
         k = g.n_keys++;
-        g.key[k] = en.key;
+        g.key[k] = ip[e].key;
         for (int h = 0; h < 4; h++) g.hoff[k][h] = -1;
       }
-      d.kind = en.kind;
-      d.key = en.key;
-      d.coef = en.coef;
-      d.slot = k;
-      const bool term = en.kind == KSS_IPA_EXISTING_ANTI || en.kind == KSS_IPA_SCORE_TERM;
-      if (!refs(term, en.row_off, en.row_len, d.ri_off, d.ri_len)) return false;
-      if (en.kind == KSS_IPA_SCORE_CLASS || en.kind == KSS_IPA_SCORE_TERM) csum += std::abs((int64_t)en.coef);
-      stats = true;
+      slot_of[e] = k;
     }
-    for (int k = 0; k < g.n_keys; k++) {  // one histogram per (key, kind) some entry feeds
+    bool used[MAXK][4] = {};
+    for (int e = 0; e < p.ipa_len; e++) {
+      const kss_ipa& en = ip[e];
+      stats = true;
+      if (en.kind == KSS_IPA_SCORE_CLASS || en.kind == KSS_IPA_SCORE_TERM) continue;
+      if (g.n_ipa >= G_IPA) return gfail(need, GP_IPA, i);
+      GIpa& d = g.ipa[g.n_ipa++];
+      d.kind = (int16_t)en.kind;
+      d.key = (int16_t)en.key;
+      d.slot = (int16_t)slot_of[e];
+      if (!refs(list(en.row_off, en.row_len, en.kind == KSS_IPA_EXISTING_ANTI), d.ri_off, d.ri_len)) return gfail(need, GP_REFS, i);
+      used[slot_of[e]][en.kind == KSS_IPA_EXISTING_ANTI ? 0 : (en.kind == KSS_IPA_REQ_AFFINITY ? 1 : 2)] = true;
+    }
+    for (int k = 0; k < g.n_keys; k++) {
+      std::vector<std::pair<int, int64_t>> rows;
+      for (int e = 0; e < p.ipa_len; e++) {
+        const kss_ipa& en = ip[e];
+        if (slot_of[e] != k || (en.kind != KSS_IPA_SCORE_CLASS && en.kind != KSS_IPA_SCORE_TERM)) continue;
+        for (int j = 0; j < en.row_len; j++)
+          rows.push_back({(en.kind == KSS_IPA_SCORE_TERM ? n_classes : 0) + ps->ints[en.row_off + j], (int64_t)en.coef});
+      }
+      if (rows.empty()) continue;
+      if (g.n_ipa >= G_IPA) return gfail(need, GP_IPA, i);
+      GIpa& d = g.ipa[g.n_ipa++];
+      d.kind = G_SCORE;
+      d.key = (int16_t)g.key[k];
+      d.slot = (int16_t)k;
+      if (!refs(rows, d.ri_off, d.ri_len)) return gfail(need, GP_REFS, i);
+      used[k][3] = true;
+    }
+    for (int k = 0; k < g.n_keys; k++) {  // one histogram per (shared key, kind) some entry feeds
       if (key_flags[g.key[k]] & KSS_KEY_UNIQUE) continue;
-      for (int h = 0; h < 4; h++) {
-        bool used = false;
-        for (int e = 0; e < p.ipa_len; e++) {
-          const int kind = ip[e].kind;
-          const int eh = kind == KSS_IPA_EXISTING_ANTI ? 0 : (kind == KSS_IPA_REQ_AFFINITY ? 1 : (kind == KSS_IPA_REQ_ANTI ? 2 : 3));
-          used |= g.ipa[e].slot == k && eh == h;
-        }
-        if (used) {
+      for (int h = 0; h < 4; h++)
+        if (used[k][h]) {
           g.hoff[k][h] = off;
           off += key_card[g.key[k]] + 1;
         }
-      }
     }
     g.total_bins = off;
     g.total_pbins = poff;
     g.need_stats = stats ? 1 : 0;
-    if (off + poff > LDS_BINS) return false;
-    if (MAXH + 1 + off + g.hard_pbins > G_XW || 13 + (poff - g.hard_pbins) > G_XW) return false;
+    if (off + poff > LDS_BINS || off > 32767 || poff > 32767) return gfail(need, GP_BINS, i);
+    if (MAXH + 1 + off + g.hard_pbins > G_XW || 13 + (poff - g.hard_pbins) > G_XW) return gfail(need, GP_XW, i);
     need.bins_cap = std::max(need.bins_cap, off + poff);
-    need.rows = std::max(need.rows, (int)g.n_rows);
-    need.coef_sum = std::max(need.coef_sum, csum);
-    need.max_own = std::max(need.max_own, (int)p.own_terms_len);
-    for (int j = 0; j < p.own_terms_len; j++) {  // commits of one pod to one term row
+    // AssumePod's count rows: the pod's class, its own term rows
+    if (1 + p.own_terms_len > G_CMT) return gfail(need, GP_COMMIT, i);
+    auto cmt_of = [&](int rowid) -> int32_t {
+      const int l = (size_t)rowid < local.size() ? local[(size_t)rowid] : -1;
+      return l >= 0 ? l : -1 - rowid;
+    };
+    g.n_cmt = 0;
+    if (p.cls >= 0) g.cmt[g.n_cmt++] = cmt_of(p.cls);
+    for (int j = 0; j < p.own_terms_len; j++) {
+      g.cmt[g.n_cmt++] = cmt_of(n_classes + ps->ints[p.own_terms_off + j]);
       int m = 0;
       for (int x = 0; x < p.own_terms_len; x++) m += ps->ints[p.own_terms_off + x] == ps->ints[p.own_terms_off + j];
       need.max_mult = std::max(need.max_mult, m);
     }
   }
+  // rows first read by a later pod than one committing to them: re-resolve the commits
+  size_t rmax = 0;
+  int rmax_pod = 0;
+  for (int i = 0; i < ps->n_pods; i++) {
+    GPod& g = out[(size_t)i];
+    for (int j = 0; j < g.n_cmt; j++)
+      if (g.cmt[j] < 0) {
+        const int rowid = -1 - g.cmt[j];
+        if ((size_t)rowid < local.size() && local[(size_t)rowid] >= 0) g.cmt[j] = local[(size_t)rowid];
+      }
+    if (refs_of[(size_t)i].size() > rmax) {
+      rmax = refs_of[(size_t)i].size();
+      rmax_pod = i;
+    }
+  }
+  // records: header + references, one stride of gq uint4 each
+  const size_t gq = (sizeof(GPod) + 4 * rmax + 15) / 16;
+  if (gq > (size_t)G_QMAX) return gfail(need, GP_RECORD, rmax_pod);
+  need.gq = (int)gq;
+  words.assign(gq * out.size(), uint4{0, 0, 0, 0});
+  for (size_t i = 0; i < out.size(); i++) {
+    char* rec = reinterpret_cast<char*>(words.data() + i * gq);
+    std::memcpy(rec, &out[i], sizeof(GPod));
+    if (!refs_of[i].empty()) std::memcpy(rec + sizeof(GPod), refs_of[i].data(), 4 * refs_of[i].size());
+  }
   return true;
 }
 
-// k_spread keeps counts, histograms and InterPodAffinity scores in 32 bits: with `total`
-// a bound on every count row's sum over the cluster after the batch, a constraint's count
-// is below total * max_len, a score below coef_sum times that, and a multi-constraint
-// PodTopologySpread raw score below max_soft * (count * log(N + 2) + maxSkew).
-bool spread_bounds_ok(const GpodNeeds& q, double total, int N) {
-  const double cnt = total * (double)q.max_len;
+// k_spread keeps counts, histograms and scores in 32 bits and resident counts in 16: with
+// `total` a bound on every count row's sum over the cluster after the batch and `cell` a
+// bound on every single count, a reference sum (one constraint / entry) is below
+// ref_weight * total over any node set, an InterPodAffinity score below MAXK times that,
+// and a multi-constraint PodTopologySpread raw score below
+// max_soft * (count * log(N + 2) + maxSkew).
+bool spread_bounds_ok(const GpodNeeds& q, double total, double cell, int N) {
   const double lim = 2147483647.0;
-  if (cnt >= lim / 2) return false;
-  if ((double)q.coef_sum * cnt >= lim) return false;
-  if (q.max_soft > 1 && (double)q.max_soft * (cnt * std::log((double)N + 2.0) + (double)q.max_skew + 1.0) >= lim)
+  const double ref = (double)q.ref_weight * total;
+  if (cell > 65535.0 || (double)MAXK * ref >= lim) return false;
+  if (q.max_soft > 1 && (double)q.max_soft * (ref * std::log((double)N + 2.0) + (double)q.max_skew + 1.0) >= lim)
     return false;
   return true;
 }
@@ -953,8 +1064,12 @@ int kss_load_cluster(kss_ctx* ctx, const kss_cluster* cl) {
     if (cl->term_count)
       for (size_t i = 0; i < (size_t)cl->n_terms * N; i++) st += std::abs((double)cl->term_count[i]);
     ctx->count_bound0 = ctx->count_bound = std::max(sc, st);
-    ctx->max_allowed = 0;
-    for (size_t i = 0; i < N; i++) ctx->max_allowed = std::max(ctx->max_allowed, cl->allowed_pods[i]);
+    double cm = 0;
+    if (cl->class_count)
+      for (size_t i = 0; i < (size_t)cl->n_classes * N; i++) cm = std::max(cm, std::abs((double)cl->class_count[i]));
+    if (cl->term_count)
+      for (size_t i = 0; i < (size_t)cl->n_terms * N; i++) cm = std::max(cm, std::abs((double)cl->term_count[i]));
+    ctx->cell_bound0 = ctx->cell_bound = cm;
   }
   ctx->loaded = true;
   ctx->recorded = 0;
@@ -1090,6 +1205,7 @@ int kss_reset_node_state(kss_ctx* ctx) {
   HIP_TRY(hipSetDevice(ctx->cfg.device));
   void* dst[5] = {ctx->dc.requested, ctx->dc.nonzero, ctx->dc.pod_count, ctx->dc.class_count, ctx->dc.term_count};
   ctx->count_bound = ctx->count_bound0;
+  ctx->cell_bound = ctx->cell_bound0;
   for (int i = 0; i < 5; i++)
     if (ctx->mut_bytes[i])
       HIP_TRY(hipMemcpyAsync(dst[i], (char*)ctx->pristine_buf.p + ctx->pristine_off[i], ctx->mut_bytes[i],
@@ -1336,32 +1452,22 @@ static int launch_simple(hipStream_t st, const Geometry& g, int n_jobs, const De
   return 0;
 }
 
-static size_t spread_lds(const Geometry& g, const GpodNeeds& q, int n_keys, int n_rowids) {
-  return spread_lds_bytes(g.npt * g.threads, q.bins_cap, n_keys, n_rowids, q.rows);
+static size_t spread_lds(const Geometry& g, const GpodNeeds& q, int n_keys, int n_res) {
+  return spread_lds_bytes(g.npt * g.threads, q.bins_cap, n_keys, n_res, q.gq);
 }
 
-static bool spread_fits(const Geometry& g, const GpodNeeds& q, int n_keys, int n_rowids) {
+static bool spread_fits(const Geometry& g, const GpodNeeds& q, int n_keys, int n_res) {
   const int pf_n = g.threads > 64 ? g.threads - 64 : g.threads;  // prefetch lanes (kss_spread.cuh)
-  return (g.npt * g.threads + pf_n - 1) / pf_n <= G_PF && spread_lds(g, q, n_keys, n_rowids) <= KSS_LDS_BUDGET;
-}
-
-// Pods per k_spread launch: the static-word budget, and at most 255 commits of the launch
-// to one (count row, node) (the LDS commit table holds bytes) unless NodeResourcesFit's pod
-// limit already bounds them.
-static int spread_chunk(const kss_ctx* ctx, const GpodNeeds& q, size_t N, int n) {
-  int c = static_chunk(N, n);
-  const bool pod_limit = ((ctx->prof.filter_enabled >> KSS_F_NODE_RESOURCES_FIT) & 1u) != 0;
-  if (!pod_limit || (int64_t)ctx->max_allowed * q.max_mult > 255) c = std::min(c, std::max(1, 255 / q.max_mult));
-  return c;
+  return (g.npt * g.threads + pf_n - 1) / pf_n <= G_PF && spread_lds(g, q, n_keys, n_res) <= KSS_LDS_BUDGET;
 }
 
 // k_static + k_spread over pods [0, n_pods) of one job, `chunk` pods at a time (node state
 // and counts back in HBM between launches).  ev (optional): 2 events per chunk.
-static int launch_spread(hipStream_t st, const Geometry& g, const GpodNeeds& q, int n_keys, int n_rowids,
+static int launch_spread(hipStream_t st, const Geometry& g, const GpodNeeds& q, int n_keys, int n_res,
                          const DevJob* jobs, const kss_profile& prof, int n_pods, int max_nodes, int chunk,
                          unsigned long long* gran, size_t gran_bytes, int* err, hipEvent_t* ev = nullptr) {
-  int cap = g.npt * g.threads, bins_cap = q.bins_cap, rows = q.rows;
-  const size_t shmem = spread_lds(g, q, n_keys, n_rowids);
+  int cap = g.npt * g.threads, bins_cap = q.bins_cap, nr = n_res, gq = q.gq;
+  const size_t shmem = spread_lds(g, q, n_keys, n_res);
   const bool def = same_profile(prof, default_profile_c());
   const void* fn = def ? (const void*)k_spread<true> : (const void*)k_spread<false>;
   HIP_TRY(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shmem));
@@ -1377,8 +1483,8 @@ static int launch_spread(hipStream_t st, const Geometry& g, const GpodNeeds& q, 
       hipLaunchKernelGGL(k_static<false>, sgrid, dim3(256), 0, st, jobs, pr, k0, k1);
     HIP_TRY(hipGetLastError());
     if (gran && k0 > 0) HIP_TRY(hipMemsetAsync(gran, 0, gran_bytes, st));
-    void* args[] = {(void*)&jobs, (void*)&W,  (void*)&cap,  (void*)&bins_cap, (void*)&rows,
-                    (void*)&k0,   (void*)&k1, (void*)&gran, (void*)&err};
+    void* args[] = {(void*)&jobs, (void*)&W,  (void*)&cap, (void*)&bins_cap, (void*)&nr,
+                    (void*)&gq,   (void*)&k0, (void*)&k1,  (void*)&gran,     (void*)&err};
     const int ci = k0 / chunk;
     if (ev) HIP_TRY(hipEventRecord(ev[2 * ci], st));
     if (g.W > 1) {
@@ -1418,10 +1524,19 @@ static int run_single(kss_ctx* ctx, const PlanNeeds& need, const DevPods& dp, in
   if (simple_ok && ctx->force_w <= 0) W = std::min(W, 64 * SX_CHUNKS);
   // a batch with programs on k_spread: 32-bit counts and scores (spread_bounds_ok)
   const double count_total = ctx->count_bound + (commit ? (double)n * (1.0 + ctx->staged_max_own) : 0.0);
+  const double cell_total = ctx->cell_bound + (commit ? (double)n * ctx->gneed.max_mult : 0.0);
   const bool spread_ok = staged && ctx->gpod_ok && commit && !record && !keep_norm && need.general &&
                          ctx->dc.n_scalar == 0 && ctx->small_values && f64_exact(ctx->f64_cluster, ctx->f64_pods, n) &&
                          !ctx->no_simple && !ctx->no_spread && !(flags & KSS_SCHED_GENERAL_KERNEL) &&
-                         spread_bounds_ok(ctx->gneed, count_total, (int)N);
+                         spread_bounds_ok(ctx->gneed, count_total, cell_total, (int)N);
+  if (getenv("KSS_TRACE_PATH"))  // diagnosis: why a batch with programs is (not) on k_spread
+    fprintf(stderr,
+            "kss path: staged=%d gpod_ok=%d commit=%d record=%d general=%d scalar=%d small=%d f64=%d bounds=%d "
+            "(ref_weight=%lld total=%.0f cell=%.0f) n_res=%zu bins=%d\n",
+            (int)staged, (int)ctx->gpod_ok, (int)commit, (int)record, (int)need.general, ctx->dc.n_scalar,
+            (int)ctx->small_values, (int)f64_exact(ctx->f64_cluster, ctx->f64_pods, n),
+            (int)spread_bounds_ok(ctx->gneed, count_total, cell_total, (int)N), (long long)ctx->gneed.ref_weight,
+            count_total, cell_total, ctx->gneed.res_rows.size(), ctx->gneed.bins_cap);
   const int w_min = (int)((N + KSS_MAX_NPT * KSS_MAX_THREADS - 1) / (KSS_MAX_NPT * KSS_MAX_THREADS));
   W = std::max(W, w_min);
   if (W > 1 && need.xw > XW_MAX && !spread_ok) {
@@ -1432,14 +1547,14 @@ static int run_single(kss_ctx* ctx, const PlanNeeds& need, const DevPods& dp, in
   Geometry g;
   if (!pick_geometry((int)N, W, ctx->pref_threads, g)) return fail(KSS_E_UNSUPPORTED, "no geometry for this cluster");
   const bool simple = simple_ok && simple_fits(g);
-  const int n_rowids = ctx->dc.n_classes + ctx->dc.n_terms;
-  bool spread = spread_ok && spread_fits(g, ctx->gneed, ctx->dc.n_keys, n_rowids);
+  const int n_res = (int)ctx->gneed.res_rows.size();
+  bool spread = spread_ok && spread_fits(g, ctx->gneed, ctx->dc.n_keys, n_res);
   if (spread_ok && !spread && g.threads < KSS_MAX_THREADS) {  // more prefetch lanes per shard
     Geometry g2 = g;
     const int per = (int)((N + g.W - 1) / g.W);
     g2.threads = KSS_MAX_THREADS;
     g2.npt = (per + KSS_MAX_THREADS - 1) / KSS_MAX_THREADS;
-    if (spread_fits(g2, ctx->gneed, ctx->dc.n_keys, n_rowids)) {
+    if (spread_fits(g2, ctx->gneed, ctx->dc.n_keys, n_res)) {
       g = g2;
       spread = true;
     }
@@ -1449,7 +1564,7 @@ static int run_single(kss_ctx* ctx, const PlanNeeds& need, const DevPods& dp, in
     if (!pick_geometry((int)N, 1, ctx->pref_threads, g)) return fail(KSS_E_UNSUPPORTED, "no geometry for this cluster");
   }
   const bool loop = simple || spread;  // k_static + a persistent loop kernel
-  const int chunk = simple ? static_chunk(N, n) : (spread ? spread_chunk(ctx, ctx->gneed, N, n) : 0);
+  const int chunk = loop ? static_chunk(N, n) : 0;
   if (loop && (rc = ctx->stat_buf.ensure(sizeof(uint32_t) * (size_t)chunk * std::max<size_t>(N, 1)))) return rc;
   DevJob job{};
   job.c = ctx->dc;
@@ -1465,6 +1580,7 @@ static int run_single(kss_ctx* ctx, const PlanNeeds& need, const DevPods& dp, in
   job.spods = simple ? (const SPod*)ctx->spod_buf.p : nullptr;
   job.stat = loop ? (uint32_t*)ctx->stat_buf.p : nullptr;
   job.gpods = spread ? (const GPod*)ctx->gpod_buf.p : nullptr;
+  job.res_rows = spread ? (const int32_t*)ctx->res_buf.p : nullptr;
   job.prof = ctx->prof;
   rc = ctx->job_buf.ensure(sizeof(DevJob));
   if (rc) return rc;
@@ -1499,7 +1615,7 @@ static int run_single(kss_ctx* ctx, const PlanNeeds& need, const DevPods& dp, in
     rc = launch_simple(ctx->stream, g, 1, (const DevJob*)ctx->job_buf.p, ctx->prof, n, (int)N, chunk, gran, gb,
                        (int*)ctx->err_buf.p, stamps, ctx->loop_ev.data());
   else if (spread)
-    rc = launch_spread(ctx->stream, g, ctx->gneed, ctx->dc.n_keys, n_rowids, (const DevJob*)ctx->job_buf.p, ctx->prof, n,
+    rc = launch_spread(ctx->stream, g, ctx->gneed, ctx->dc.n_keys, n_res, (const DevJob*)ctx->job_buf.p, ctx->prof, n,
                        (int)N, chunk, gran, gb, (int*)ctx->err_buf.p, ctx->loop_ev.data());
   else
     rc = launch_schedule(ctx->stream, g, 1, std::max(need.bins_cap, 0), need.general, ctx->dc.n_keys,
@@ -1524,7 +1640,10 @@ static int run_single(kss_ctx* ctx, const PlanNeeds& need, const DevPods& dp, in
   int errw = 0;
   HIP_TRY(hipMemcpy(&errw, ctx->err_buf.p, sizeof(int), hipMemcpyDeviceToHost));
   if (errw) return fail(KSS_E_DEVICE, "shard exchange timed out (workgroups not co-resident?)");
-  if (commit) ctx->count_bound = count_total;
+  if (commit) {
+    ctx->count_bound = count_total;
+    ctx->cell_bound = std::max(ctx->cell_bound, cell_total);
+  }
   ctx->meta_host.resize((size_t)std::max(n, 1));
   HIP_TRY(hipMemcpy(ctx->meta_host.data(), ctx->meta_buf.p, sizeof(PodMeta) * (size_t)std::max(n, 1), hipMemcpyDeviceToHost));
   if (chosen_out && n) HIP_TRY(hipMemcpy(chosen_out, ctx->chosen_buf.p, sizeof(int32_t) * n, hipMemcpyDeviceToHost));
@@ -1557,9 +1676,13 @@ static int stage_spods(kss_ctx* ctx, const kss_podset* ps) {
     ctx->gpod_ok = build_gpods(ps, ctx->dc.n_scalar, ctx->dc.n_classes, ctx->key_card_h.data(), ctx->key_flags_h.data(),
                                ctx->key_empty_h.data(), ctx->gpod_host, ctx->gneed);
     if (!ctx->gpod_ok) return 0;
-    int rc = ctx->gpod_buf.ensure(sizeof(GPod) * ctx->gpod_host.size());
+    int rc = ctx->gpod_buf.ensure(sizeof(uint4) * ctx->gpod_host.size());
     if (rc) return rc;
-    HIP_TRY(hipMemcpyAsync(ctx->gpod_buf.p, ctx->gpod_host.data(), sizeof(GPod) * ctx->gpod_host.size(),
+    if ((rc = ctx->res_buf.ensure(sizeof(int32_t) * std::max<size_t>(ctx->gneed.res_rows.size(), 1)))) return rc;
+    if (!ctx->gneed.res_rows.empty())
+      HIP_TRY(hipMemcpyAsync(ctx->res_buf.p, ctx->gneed.res_rows.data(), sizeof(int32_t) * ctx->gneed.res_rows.size(),
+                             hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(hipMemcpyAsync(ctx->gpod_buf.p, ctx->gpod_host.data(), sizeof(uint4) * ctx->gpod_host.size(),
                            hipMemcpyHostToDevice, ctx->stream));
     return 0;
   }
@@ -1619,6 +1742,7 @@ int kss_commit(kss_ctx* ctx, const kss_podset* ps, int32_t pod_index, int32_t no
   rc = upload_podset(ctx->stream, ctx->tmp_pod_buf, ps, ctx->tdp);
   if (rc) return rc;
   ctx->count_bound += 1.0 + (double)ps->pods[pod_index].own_terms_len;
+  ctx->cell_bound += 1.0 + (double)ps->pods[pod_index].own_terms_len;
   hipLaunchKernelGGL(k_commit, dim3(1), dim3(64), 0, ctx->stream, ctx->dc, ctx->tdp, pod_index, local, 1);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipStreamSynchronize(ctx->stream));
@@ -2097,3 +2221,29 @@ int kss_device_go_log(int32_t device, const double* x, double* y, int32_t n) {
   HIP_TRY(hipMemcpy(y, d + n, 8 * (size_t)n, hipMemcpyDeviceToHost));
   return 0;
 }
+
+int kss_plan_podset(const kss_cluster* cl, const kss_podset* ps, int32_t* out3) {
+  if (!cl || !ps || !out3) return fail(KSS_E_INVAL, "bad arguments");
+  int rc = check_cluster(cl);
+  if (rc) return rc;
+  if ((rc = validate(cl, ps, ps->n_pods))) return rc;
+  std::vector<SPod> sp;
+  out3[0] = 0;
+  out3[1] = -1;
+  out3[2] = GP_OK;
+  if (build_spods(ps, cl->n_scalar, sp)) {
+    out3[0] = 1;
+    return 0;
+  }
+  std::vector<uint4> words;
+  GpodNeeds need;
+  if (build_gpods(ps, cl->n_scalar, cl->n_classes, cl->key_card, cl->key_flags, cl->key_empty, words, need)) {
+    out3[0] = 2;
+    return 0;
+  }
+  out3[1] = need.fail_pod;
+  out3[2] = need.fail_code;
+  return 0;
+}
+
+const char* kss_plan_reason(int32_t code) { return code >= 0 && code < GP_NCODES ? kGpReason[code] : "unknown"; }

@@ -4,17 +4,19 @@
 // organised like k_simple (kss_simple.cuh):
 //
 //   * the commit-invariant part of every (pod, node) evaluation comes from k_static's
-//     static words, which for these pods also carry the inclusion-policy bits
-//     (NodeAffinityPolicy / NodeTaintsPolicy) that the PodTopologySpread counts need;
+//     static words, which also carry the inclusion-policy bits (NodeAffinityPolicy /
+//     NodeTaintsPolicy) the PodTopologySpread counts need;
 //   * each pod's program is resolved on the host into a fixed GPod record: the plan
-//     (histogram / presence bin offsets, key slots) and a table of the class_count /
-//     term_count rows its constraints and terms read (kss_lib.hip build_gpods);
-//   * the shard's node rows, label ids, and the count rows of the next pod live in LDS.
-//     The counts come from the snapshot (HBM, read-only during the launch) plus a
-//     per-shard table of the commits of this launch (one byte per (count row, node)),
-//     written back to HBM when the launch ends;
-//   * records, static words and count rows of the next pods are prefetched by every wave
-//     but wave 0 (wave 0 runs the exchanges and never waits on an HBM prefetch);
+//     (histogram / presence bin offsets, key slots), and every constraint / entry as a
+//     list of (count row, coefficient) references; InterPodAffinity score entries of one
+//     topology key are merged into one weighted list (kss_lib.hip build_gpods);
+//   * the batch's read set of class_count / term_count rows is resident in LDS for the
+//     launch as 16-bit counts (host-checked), with the shard's node rows and label ids;
+//     commits update them in place (rows outside the read set: HBM atomics) and the
+//     resident rows are written back when the launch ends;
+//   * records and static words of the next pods are prefetched by every wave but wave 0
+//     (wave 0 runs the exchanges and never waits on an HBM access); the outcome stores and
+//     HBM commits are issued by a prefetch wave too;
 //   * exchanges carry 32-bit values, one {epoch, value} granule each; a pod with a single
 //     ScheduleAnyway constraint folds the PodTopologySpread score extrema into the filter
 //     exchange (the raw score is monotone in the count), so it needs no third exchange.
@@ -27,48 +29,50 @@
 
 namespace kss {
 
-constexpr int G_ROWS = 8;    // distinct count rows (class_count / term_count) per pod
-constexpr int G_RIDX = 32;   // row references of a pod's constraints and entries
-constexpr int G_IPA = 8;     // inter-pod-affinity entries per pod
-constexpr int G_PF = 4;      // node words per prefetch lane (host-checked)
+constexpr int G_QMAX = 128;  // uint4 per record (header + references; host-checked)
+constexpr int G_IPA = 16;    // inter-pod-affinity entries per pod (score entries merged per key)
+constexpr int G_CMT = 8;     // count rows a pod's commit adds to (its class, its own term rows)
+constexpr int G_PF = 4;      // static words per prefetch lane (host-checked)
 constexpr int G_XW = 512;    // 32-bit values per shard per exchange (host-checked)
 constexpr int G_NS = 16;     // scalar slots of an exchange
+constexpr int G_SCORE = 3;   // GIpa.kind of a merged InterPodAffinity score entry (KSS_IPA_SCORE_CLASS)
 
 struct GSpread {
-  int32_t key, max_skew, self_match, flags;  // kss_spread
-  int32_t ri_off, ri_len;                    // its classes: ridx[ri_off .. +ri_len) (row-table indices)
-  int32_t off, poff;                         // histogram / presence bin offsets (-1: node-valued key)
-  int32_t mode;                              // soft: SOFT_HOST / SOFT_DIRECT / SOFT_HIST
-  int32_t empty;                             // key_empty: domain of a node without the key
-  int32_t nb;                                // domains of the key + 1
-  int32_t pad;
+  int32_t max_skew;
+  int16_t key, flags, self_match, mode;  // kss_spread; mode: SOFT_HOST / SOFT_DIRECT / SOFT_HIST
+  int16_t ri_off, ri_len;                // references ri[ri_off .. +ri_len)
+  int16_t off, poff;                     // histogram / presence bin offsets (-1: node-valued key)
+  int16_t empty;                         // key_empty: domain of a node without the key
+  int16_t nb;                            // domains of the key + 1
 };
 struct GIpa {
-  int32_t kind, key, ri_off, ri_len, coef, slot;
+  int16_t kind, key, ri_off, ri_len, slot, pad;  // kind: KSS_IPA_* (score entries: G_SCORE)
 };
-// Host-resolved program of one pod (build_gpods).  Per IPA key slot k, histogram h (0
+// Host-resolved program of one pod (build_gpods): this header, then its references as
+// uint32 (resident row index | coefficient << 16), the record padded to the batch's stride
+// of `gq` uint4 (the longest reference list decides it).  Per IPA key slot k, histogram h (0
 // existing anti-affinity, 1 required affinity, 2 required anti-affinity, 3 score) lives at
 // hoff[k][h]; -1 for a node-valued (unique) key, whose value is the node's own sum, and
 // for a histogram no entry of the pod feeds (never read).
 struct alignas(16) GPod {
   SPod dyn;
   int32_t pflags, n_hard, n_soft, n_ipa;
-  int32_t n_rows, n_keys, total_bins, hard_pbins;
-  int32_t total_pbins, need_stats, pad0, pad1;
+  int32_t n_keys, total_bins, hard_pbins, total_pbins;
+  int32_t need_stats, n_cmt, pad0, pad1;
   int32_t key[MAXK];
   int32_t hoff[MAXK][4];
-  int32_t row[G_ROWS];    // class_count row r, or term_count row r as (1 << 30) | r
-  int32_t rowid[G_ROWS];  // commit-table id: class r -> r, term r -> n_classes + r
-  int16_t ridx[G_RIDX];
+  int32_t cmt[G_CMT];   // resident row index, or -(1 + class row) / -(1 + n_classes + term row) in HBM
   GSpread sp[MAXH + MAXS];
   GIpa ipa[G_IPA];
 };
-constexpr int GPOD_Q = (int)(sizeof(GPod) / 16);
-static_assert(sizeof(GPod) % 16 == 0 && GPOD_Q <= 64, "a GPod is prefetched by one wave, one uint4 per lane");
+static_assert(sizeof(GPod) % 16 == 0 && sizeof(GPod) / 16 < G_QMAX, "record header");
+// the references of a record
+__host__ __device__ inline const uint32_t* grefs(const GPod& q) { return reinterpret_cast<const uint32_t*>(&q + 1); }
 
 // Go math.Log (src/math/log.go), the same IEEE operation sequence as the host port
-// (kss_host.cpp kss_go_log; compiled with -ffp-contract=off): PodTopologySpread's
-// topologyNormalizingWeight = math.Log(float64(size + 2)), size >= 0.
+// (kss_host.cpp kss_go_log; both compiled with -ffp-contract=off):
+// PodTopologySpread's topologyNormalizingWeight = math.Log(float64(size + 2)).
+// tests/test_gpu_spread.py checks it bit for bit against the host port.
 __device__ __forceinline__ double go_log_dev(double x) {
   const double Ln2Hi = 6.93147180369123816490e-01, Ln2Lo = 1.90821492927058770002e-10;
   const double L1 = 6.666666666666735130e-01, L2 = 3.999999999940941908e-01, L3 = 2.857142874366239149e-01,
@@ -104,12 +108,13 @@ struct alignas(16) SpreadHdr {
 
 struct SpreadShard {
   int32_t* xs;     // [G_NS + bins_cap]: exchange scalars, then histogram / presence bins
-  GPod* ring;      // [3] pod programs (slot = pod % 3)
+  uint4* ring;     // [3][gq] pod programs (slot = pod % 3)
   uint32_t* st;    // [2][cap] static words (slot = pod & 1)
-  int32_t* base;   // [2][rows][cap] snapshot counts of the pod's rows (slot = pod & 1)
-  uint8_t* delta;  // [n_rowids][cap] commits of this launch per count row and node
+  uint16_t* cnt;   // [n_res][cap] resident count rows (snapshot + this launch's commits)
   double* r64;     // [8][cap] allocatable, requested (cpu, mem, eph), non-zero requested (cpu, mem)
   double* inv;     // [3][cap]
+  long long* sipa; // [cap] InterPodAffinity raw
+  long long* spts; // [cap] PodTopologySpread raw (> 1 soft constraint)
   int32_t* r32;    // [3][cap] pod count, allowed pods, node flags
   int32_t* lbl;    // [n_keys][cap] label value ids
   int32_t* sf;     // [cap] verdict | ignored << 16
@@ -118,37 +123,31 @@ struct SpreadShard {
   int32_t* sfit;   // [cap]
   int32_t* sba;    // [cap]
   int32_t* scnt;   // [cap] single soft constraint: the node's count (-1 lacks the key)
-  long long* sipa; // [cap] InterPodAffinity raw
-  long long* spts; // [cap] PodTopologySpread raw (> 1 soft constraint)
-  int cap, n_rowids, rows;
+  int cap;
 };
 
-// rows: count rows per pod in the batch (<= G_ROWS)
-__host__ __device__ inline size_t spread_lds_bytes(int cap, int bins_cap, int n_keys, int n_rowids, int rows) {
+__host__ __device__ inline size_t spread_lds_bytes(int cap, int bins_cap, int n_keys, int n_res, int gq) {
   const size_t C = (size_t)cap;
-  size_t b = sizeof(SpreadHdr) + 4 * ((size_t)G_NS + (size_t)bins_cap);
-  b = (b + 15) / 16 * 16 + 3 * sizeof(GPod);
-  b += 4 * 2 * C + 4 * 2 * (size_t)rows * C + ((size_t)n_rowids * C + 15) / 16 * 16;
-  b += 8 * 8 * C + 8 * 3 * C + 4 * 3 * C + 4 * (size_t)n_keys * C;
-  b += 4 * 6 * C + 8 * 2 * C;
+  size_t b = (sizeof(SpreadHdr) + 4 * ((size_t)G_NS + (size_t)bins_cap) + 15) / 16 * 16;
+  b += 3 * 16 * (size_t)gq + 4 * 2 * C + ((size_t)n_res * C * 2 + 15) / 16 * 16;
+  b += 8 * 8 * C + 8 * 3 * C + 8 * 2 * C + 4 * 3 * C + 4 * (size_t)n_keys * C + 4 * 6 * C;
   return b;
 }
 
-__device__ __forceinline__ SpreadShard spread_view(long long* smem, int cap, int bins_cap, int n_keys, int n_rowids,
-                                                   int rows) {
+__device__ __forceinline__ SpreadShard spread_view(long long* smem, int cap, int bins_cap, int n_keys, int n_res,
+                                                   int gq) {
   SpreadShard L;
   const size_t C = (size_t)cap;
-  uint8_t* b = reinterpret_cast<uint8_t*>(smem) + sizeof(SpreadHdr);
-  L.xs = reinterpret_cast<int32_t*>(b);
-  size_t o = ((size_t)(G_NS + bins_cap) * 4 + sizeof(SpreadHdr) + 15) / 16 * 16 - sizeof(SpreadHdr);
-  L.ring = reinterpret_cast<GPod*>(b + o);
-  o += 3 * sizeof(GPod);
+  uint8_t* b = reinterpret_cast<uint8_t*>(smem);
+  size_t o = sizeof(SpreadHdr);
+  L.xs = reinterpret_cast<int32_t*>(b + o);
+  o = (o + 4 * ((size_t)G_NS + (size_t)bins_cap) + 15) / 16 * 16;
+  L.ring = reinterpret_cast<uint4*>(b + o);
+  o += 3 * 16 * (size_t)gq;
   L.st = reinterpret_cast<uint32_t*>(b + o);
   o += 4 * 2 * C;
-  L.base = reinterpret_cast<int32_t*>(b + o);
-  o += 4 * 2 * (size_t)rows * C;
-  L.delta = b + o;
-  o += ((size_t)n_rowids * C + 15) / 16 * 16;
+  L.cnt = reinterpret_cast<uint16_t*>(b + o);
+  o += ((size_t)n_res * C * 2 + 15) / 16 * 16;
   L.r64 = reinterpret_cast<double*>(b + o);
   o += 8 * 8 * C;
   L.inv = reinterpret_cast<double*>(b + o);
@@ -168,22 +167,28 @@ __device__ __forceinline__ SpreadShard spread_view(long long* smem, int cap, int
   L.sba = L.sf + 4 * C;
   L.scnt = L.sf + 5 * C;
   L.cap = cap;
-  L.n_rowids = n_rowids;
-  L.rows = rows;
   return L;
 }
 
-// Count of row-table entry r at slot s: snapshot + this launch's commits.
-__device__ __forceinline__ int32_t g_count(const SpreadShard& L, const GPod& q, const int32_t* base, int r, int s) {
-  return base[r * L.cap + s] + (int32_t)L.delta[(size_t)q.rowid[r] * L.cap + s];
+// Σ coefficient x count over references [off, off + len) at slot s (sum_rows of
+// class_count / term_count; a merged score entry's Σ coef_e x Σ rows_e).
+__device__ __forceinline__ int32_t g_sum(const SpreadShard& L, const GPod& q, int off, int len, int s) {
+  const uint32_t* R = grefs(q);
+  int32_t v = 0;
+  for (int i = 0; i < len; i++) {
+    const uint32_t r = R[off + i];
+    v += (int32_t)(int16_t)(r >> 16) * (int32_t)L.cnt[(int)(r & 0xFFFFu) * L.cap + s];
+  }
+  return v;
 }
 
-// Σ over a constraint's / entry's rows (sum_rows over class_count / term_count).
-__device__ __forceinline__ int64_t g_sum(const SpreadShard& L, const GPod& q, const int32_t* base, int off, int len,
-                                         int s) {
-  int64_t v = 0;
-  for (int i = 0; i < len; i++) v += g_count(L, q, base, q.ridx[off + i], s);
-  return v;
+// some referenced row counts a pod at slot s (the "topologyScore is non-empty" test of a
+// score entry: every count is >= 0, so a weighted sum can cancel but this cannot)
+__device__ __forceinline__ bool g_any(const SpreadShard& L, const GPod& q, int off, int len, int s) {
+  const uint32_t* R = grefs(q);
+  bool a = false;
+  for (int i = 0; i < len; i++) a |= L.cnt[(int)(R[off + i] & 0xFFFFu) * L.cap + s] != 0;
+  return a;
 }
 
 __device__ __forceinline__ bool g_policy(const GSpread& sp, uint32_t w) {
@@ -373,7 +378,7 @@ __device__ __forceinline__ bool spread_argmax(SpreadHdr& H, int W, int w, unsign
 }
 
 // filter_pts / filter_ipa / ipa_score of kss_sched.cuh over the GPod and the LDS caches.
-__device__ __forceinline__ int g_filter_pts(const SpreadShard& L, const GPod& q, const int32_t* base, const int32_t* bins,
+__device__ __forceinline__ int g_filter_pts(const SpreadShard& L, const GPod& q, const int32_t* bins,
                                             const int32_t (&hard_min)[MAXH], int s, uint32_t w) {
   for (int i = 0; i < q.n_hard; i++) {
     const GSpread& sp = q.sp[i];
@@ -381,7 +386,7 @@ __device__ __forceinline__ int g_filter_pts(const SpreadShard& L, const GPod& q,
     if (d < 0) return 1 + KSS_PTS_MISSING_LABEL;
     int64_t match;
     if (sp.off >= 0) match = bins[sp.off + d];
-    else match = (g_has_keys(L, q.sp, q.n_hard, s) && g_policy(sp, w)) ? g_sum(L, q, base, sp.ri_off, sp.ri_len, s) : 0;
+    else match = (g_has_keys(L, q.sp, q.n_hard, s) && g_policy(sp, w)) ? g_sum(L, q, sp.ri_off, sp.ri_len, s) : 0;
     const int64_t skew = match + (int64_t)sp.self_match - (int64_t)hard_min[i];
     if (skew > (int64_t)sp.max_skew) return 1 + KSS_PTS_CONSTRAINTS_NOT_MATCH;
   }
@@ -389,18 +394,18 @@ __device__ __forceinline__ int g_filter_pts(const SpreadShard& L, const GPod& q,
 }
 
 // histogram h of key slot k at domain d, or the node's own value for a node-valued key
-__device__ __forceinline__ int64_t g_ipa_value(const SpreadShard& L, const GPod& q, const int32_t* base,
-                                               const int32_t* bins, int k, int h, int d, int s) {
+__device__ __forceinline__ int64_t g_ipa_value(const SpreadShard& L, const GPod& q, const int32_t* bins, int k, int h,
+                                               int d, int s) {
   if (q.hoff[k][h] >= 0) return bins[q.hoff[k][h] + d];
   const int kind = h == 0 ? KSS_IPA_EXISTING_ANTI : (h == 1 ? KSS_IPA_REQ_AFFINITY : KSS_IPA_REQ_ANTI);
   int64_t v = 0;
   for (int e = 0; e < q.n_ipa; e++)
-    if (q.ipa[e].kind == kind && q.ipa[e].slot == k) v += g_sum(L, q, base, q.ipa[e].ri_off, q.ipa[e].ri_len, s);
+    if (q.ipa[e].kind == kind && q.ipa[e].slot == k) v += g_sum(L, q, q.ipa[e].ri_off, q.ipa[e].ri_len, s);
   return v;
 }
 
-__device__ __forceinline__ int g_filter_ipa(const SpreadShard& L, const GPod& q, const int32_t* base, const int32_t* bins,
-                                            int32_t flags, int s) {
+__device__ __forceinline__ int g_filter_ipa(const SpreadShard& L, const GPod& q, const int32_t* bins, int32_t flags,
+                                            int s) {
   // satisfyPodAffinity
   bool have = false, exist = true;
   for (int e = 0; e < q.n_ipa; e++) {
@@ -409,7 +414,7 @@ __device__ __forceinline__ int g_filter_ipa(const SpreadShard& L, const GPod& q,
     have = true;
     const int d = L.lbl[en.key * L.cap + s];
     if (d < 0) return 1 + KSS_IPA_AFFINITY;
-    if (g_ipa_value(L, q, base, bins, en.slot, 1, d, s) <= 0) exist = false;
+    if (g_ipa_value(L, q, bins, en.slot, 1, d, s) <= 0) exist = false;
   }
   if (have && !exist && !(!(flags & 2) && (q.pflags & KSS_POD_IPA_SELF_MATCH))) return 1 + KSS_IPA_AFFINITY;
   // satisfyPodAntiAffinity
@@ -419,7 +424,7 @@ __device__ __forceinline__ int g_filter_ipa(const SpreadShard& L, const GPod& q,
       if (en.kind != KSS_IPA_REQ_ANTI) continue;
       const int d = L.lbl[en.key * L.cap + s];
       if (d < 0) continue;
-      if (g_ipa_value(L, q, base, bins, en.slot, 2, d, s) > 0) return 1 + KSS_IPA_ANTI_AFFINITY;
+      if (g_ipa_value(L, q, bins, en.slot, 2, d, s) > 0) return 1 + KSS_IPA_ANTI_AFFINITY;
     }
   }
   // satisfyExistingPodsAntiAffinity
@@ -429,15 +434,14 @@ __device__ __forceinline__ int g_filter_ipa(const SpreadShard& L, const GPod& q,
       if (en.kind != KSS_IPA_EXISTING_ANTI) continue;
       const int d = L.lbl[en.key * L.cap + s];
       if (d < 0) continue;
-      if (g_ipa_value(L, q, base, bins, en.slot, 0, d, s) > 0) return 1 + KSS_IPA_EXISTING_ANTI_AFFINITY;
+      if (g_ipa_value(L, q, bins, en.slot, 0, d, s) > 0) return 1 + KSS_IPA_EXISTING_ANTI_AFFINITY;
     }
   }
   return 0;
 }
 
 // InterPodAffinity.Score: Σ topologyScore[key][node value] over the keys the node has
-__device__ __forceinline__ int64_t g_ipa_score(const SpreadShard& L, const GPod& q, const int32_t* base,
-                                               const int32_t* bins, int s) {
+__device__ __forceinline__ int64_t g_ipa_score(const SpreadShard& L, const GPod& q, const int32_t* bins, int s) {
   int64_t v = 0;
   const bool has_labels = (L.r32[2 * L.cap + s] & KSS_NODE_HAS_LABELS) != 0;
   for (int k = 0; k < q.n_keys; k++) {
@@ -448,36 +452,30 @@ __device__ __forceinline__ int64_t g_ipa_score(const SpreadShard& L, const GPod&
     } else if (has_labels) {
       for (int e = 0; e < q.n_ipa; e++) {
         const GIpa& en = q.ipa[e];
-        if (en.slot != k || (en.kind != KSS_IPA_SCORE_CLASS && en.kind != KSS_IPA_SCORE_TERM)) continue;
-        v += (int64_t)en.coef * g_sum(L, q, base, en.ri_off, en.ri_len, s);
+        if (en.slot == k && en.kind == G_SCORE) v += g_sum(L, q, en.ri_off, en.ri_len, s);
       }
     }
   }
   return v;
 }
 
-// The batch for shard w of one cluster, pods [k0, k1).
+// The batch for shard w of one cluster, pods [k0, k1).  res_rows: the resident count rows
+// (class r as r, term r as n_classes + r), n_res of them.
 __device__ __forceinline__ void spread_schedule(DevCluster c, const GPod* __restrict__ gpods,
-                                                const uint32_t* __restrict__ stat, const int32_t* __restrict__ ints,
-                                                int k0, int k1, int32_t* chosen, PodMeta* meta, const kss_profile& prof,
-                                                int W, int w, int cap, int bins_cap, int rows,
+                                                const uint32_t* __restrict__ stat, const int32_t* __restrict__ res_rows,
+                                                int n_res, int k0, int k1, int32_t* chosen, PodMeta* meta,
+                                                const kss_profile& prof, int W, int w, int cap, int bins_cap, int gq,
                                                 unsigned long long* gran, int* err, long long* smem) {
   const int tid = threadIdx.x, nt = blockDim.x;
   SpreadHdr& H = *reinterpret_cast<SpreadHdr*>(smem);
-  const int n_rowids = c.n_classes + c.n_terms;
-  const SpreadShard L = spread_view(smem, cap, bins_cap, c.n_keys, n_rowids, rows);
+  const SpreadShard L = spread_view(smem, cap, bins_cap, c.n_keys, n_res, gq);
   const size_t N = (size_t)c.N;
   const int per = (c.N + W - 1) / W;
   const int lo = min(c.N, w * per), hi = min(c.N, lo + per), own = hi - lo;
   if (k1 <= k0) return;
   int32_t* bins = L.xs + G_NS;
-  KSS_GLOBAL const uint32_t* gstat = gp(stat);
-  KSS_GLOBAL const uint4* gq = gp(reinterpret_cast<const uint4*>(gpods));
-  KSS_GLOBAL const int32_t* gcc = gp(c.class_count);
-  KSS_GLOBAL const int32_t* gtc = gp(c.term_count);
-  KSS_GLOBAL int32_t* gchosen = gp(chosen);
-  KSS_GLOBAL PodMeta* gmeta = gp(meta);
-  // shard state -> LDS; pod programs k0, k0+1; static words and count rows of pod k0
+  // shard state -> LDS: node rows, label ids, resident count rows, static words of pod k0,
+  // records of pods k0 and k0 + 1
   for (int s = tid; s < own; s += nt) {
     const int n = lo + s;
 #pragma unroll
@@ -495,66 +493,55 @@ __device__ __forceinline__ void spread_schedule(DevCluster c, const GPod* __rest
     for (int k = 0; k < c.n_keys; k++) L.lbl[k * cap + s] = c.label_value[(size_t)k * N + n];
     L.st[(k0 & 1) * cap + s] = stat[(size_t)lo + s];
   }
-  for (int i = tid; i < n_rowids * cap; i += nt) L.delta[i] = 0;
-  for (int i = tid; i < min(k1 - k0, 2) * GPOD_Q; i += nt) {
-    const int j = k0 + i / GPOD_Q;
-    reinterpret_cast<uint4*>(L.ring + j % 3)[i % GPOD_Q] = reinterpret_cast<const uint4*>(gpods + j)[i % GPOD_Q];
+  for (int i = tid; i < n_res * own; i += nt) {
+    const int r = i / own, s = i - r * own, row = res_rows[r];
+    const int32_t v = row < c.n_classes ? c.class_count[(size_t)row * N + lo + s]
+                                        : c.term_count[(size_t)(row - c.n_classes) * N + lo + s];
+    L.cnt[r * cap + s] = (uint16_t)v;
+  }
+  const uint4* grec = reinterpret_cast<const uint4*>(gpods);
+  for (int i = tid; i < min(k1 - k0, 2) * gq; i += nt) {
+    const int j = k0 + i / gq;
+    L.ring[(j % 3) * gq + i % gq] = grec[(size_t)j * gq + i % gq];
   }
   if (tid == 0) H.abort = 0;
   __syncthreads();
-  {
-    const GPod& q0 = L.ring[k0 % 3];
-    for (int s = tid; s < own; s += nt)
-      for (int r = 0; r < q0.n_rows; r++) {
-        const int row = q0.row[r] & 0x3FFFFFFF;
-        const bool term = (q0.row[r] >> 30) & 1;
-        L.base[((k0 & 1) * rows + r) * cap + s] = (term ? c.term_count : c.class_count)[(size_t)row * N + lo + s];
-      }
-  }
-  __syncthreads();
 
+  KSS_GLOBAL const uint32_t* gstat = gp(stat);
+  KSS_GLOBAL const uint4* ggq = gp(grec);
+  KSS_GLOBAL int32_t* gchosen = gp(chosen);
+  KSS_GLOBAL PodMeta* gmeta = gp(meta);
+  KSS_GLOBAL int32_t* gcc = gp(c.class_count);
+  KSS_GLOBAL int32_t* gtc = gp(c.term_count);
   const int nwave = nt >> 6;
   const bool pf_wave = nwave == 1 || __builtin_amdgcn_readfirstlane(tid >> 6) >= 1;
   const int pf_lane = nwave == 1 ? tid : tid - 64, pf_n = nwave == 1 ? nt : nt - 64;
   const int pf_per = (own + pf_n - 1) / pf_n;  // <= G_PF (host-checked)
-  uint4 pfq = make_uint4(0, 0, 0, 0);
+  const int out_tid = nwave == 1 ? 0 : 64;     // the lane that writes outcomes and HBM commits
+  uint4 pfq0 = make_uint4(0, 0, 0, 0), pfq1 = pfq0;  // record of pod k+2: uint4 pf_lane and pf_lane + pf_n
   uint32_t pfw[G_PF];
-  int32_t pfc[G_ROWS][G_PF];
 #pragma unroll
-  for (int j = 0; j < G_PF; j++) {
-    pfw[j] = 0;
-#pragma unroll
-    for (int r = 0; r < G_ROWS; r++) pfc[r][j] = 0;
-  }
+  for (int j = 0; j < G_PF; j++) pfw[j] = 0;
   unsigned epoch = 0;
   int kparity = 0;
   for (int k = k0; k < k1; k++) {
-    const GPod& q = L.ring[k % 3];
+    const GPod& q = *reinterpret_cast<const GPod*>(L.ring + (k % 3) * gq);
     const uint32_t* sw = L.st + (k & 1) * cap;
-    const int32_t* base = L.base + (k & 1) * rows * cap;
-    // prefetch (every wave but wave 0): record of pod k+2, static words and count rows of pod k+1
-    const bool pf_on = pf_wave && k + 1 < k1 && own > 0;
-    int nr1 = 0;
+    // prefetch (every wave but wave 0): record of pod k+2, static words of pod k+1.  The
+    // branch is wave-uniform and the loads inside it unconditional (clamped indices).  A
+    // shard without nodes still takes every record: its exchanges follow the programs.
+    const bool pf_on = pf_wave && k + 1 < k1;
     if (pf_on) {
-      const GPod& q1 = L.ring[(k + 1) % 3];
-      nr1 = q1.n_rows;
       if (k + 2 < k1) {
-        KSS_GLOBAL const uint4& src = gq[(size_t)(k + 2) * GPOD_Q + min(pf_lane, GPOD_Q - 1)];
-        pfq = make_uint4(src.x, src.y, src.z, src.w);
+        KSS_GLOBAL const uint4* src = ggq + (size_t)(k + 2) * gq;
+        KSS_GLOBAL const uint4& a = src[min(pf_lane, gq - 1)];
+        KSS_GLOBAL const uint4& b = src[min(pf_lane + pf_n, gq - 1)];
+        pfq0 = make_uint4(a.x, a.y, a.z, a.w);
+        pfq1 = make_uint4(b.x, b.y, b.z, b.w);
       }
 #pragma unroll
-      for (int j = 0; j < G_PF; j++) {
-        if (j >= pf_per) break;
-        const int s = min(j * pf_n + pf_lane, own - 1);
-        pfw[j] = gstat[(size_t)(k + 1 - k0) * N + lo + s];
-#pragma unroll
-        for (int r = 0; r < G_ROWS; r++) {
-          if (r >= nr1) break;
-          const int rw = q1.row[r];
-          const size_t idx = (size_t)(rw & 0x3FFFFFFF) * N + lo + s;
-          pfc[r][j] = ((rw >> 30) & 1) ? gtc[idx] : gcc[idx];
-        }
-      }
+      for (int j = 0; j < G_PF; j++)
+        if (j < pf_per) pfw[j] = gstat[(size_t)(k + 1 - k0) * N + lo + min(j * pf_n + pf_lane, own - 1)];
     }
     PodMeta m;
     m.chosen = -1;
@@ -574,17 +561,17 @@ __device__ __forceinline__ void spread_schedule(DevCluster c, const GPod* __rest
       lds_barrier();
       for (int s = tid; s < own; s += nt) {
         const uint32_t wd = sw[s];
-        if (q.n_hard > 0 && g_has_keys(L, q.sp, q.n_hard, s)) {
+        if (q.n_hard > 0 && g_has_keys(L, q.sp, q.n_hard, s)) {  // nodeLabelsMatchSpreadConstraints
           for (int i = 0; i < q.n_hard; i++) {
             const GSpread& sp = q.sp[i];
             if (!g_policy(sp, wd)) continue;
-            const int32_t cnt = (int32_t)g_sum(L, q, base, sp.ri_off, sp.ri_len, s);
+            const int32_t cnt = g_sum(L, q, sp.ri_off, sp.ri_len, s);
             if (sp.off < 0) {
               hard_min[i] = cnt < hard_min[i] ? cnt : hard_min[i];
             } else {
               const int d = L.lbl[sp.key * cap + s];
               atomicAdd(&bins[sp.off + d], cnt);
-              bins[q.total_bins + sp.poff + d] = 1;
+              bins[q.total_bins + sp.poff + d] = 1;  // the pair (key, value) exists
             }
           }
         }
@@ -596,7 +583,7 @@ __device__ __forceinline__ void spread_schedule(DevCluster c, const GPod* __rest
               if (sp.mode != SOFT_HIST || !g_policy(sp, wd)) continue;
               int d = L.lbl[sp.key * cap + s];
               if (d < 0) d = sp.empty;
-              const int32_t cnt = (int32_t)g_sum(L, q, base, sp.ri_off, sp.ri_len, s);
+              const int32_t cnt = g_sum(L, q, sp.ri_off, sp.ri_len, s);
               if (cnt) atomicAdd(&bins[sp.off + d], cnt);
             }
           }
@@ -607,18 +594,20 @@ __device__ __forceinline__ void spread_schedule(DevCluster c, const GPod* __rest
             const GIpa& en = q.ipa[e];
             const int d = L.lbl[en.key * cap + s];
             if (d < 0) continue;
-            if (en.kind == KSS_IPA_SCORE_CLASS || en.kind == KSS_IPA_SCORE_TERM) {
+            if (en.kind == G_SCORE) {
               if (!has_labels) continue;
-              const int64_t v = g_sum(L, q, base, en.ri_off, en.ri_len, s);
-              if (v > 0) flags |= 8;
+              if (g_any(L, q, en.ri_off, en.ri_len, s)) flags |= 8;
               const int ho = q.hoff[en.slot][3];
-              if (ho >= 0 && v) atomicAdd(&bins[ho + d], (int32_t)(v * en.coef));
+              if (ho >= 0) {
+                const int32_t v = g_sum(L, q, en.ri_off, en.ri_len, s);
+                if (v) atomicAdd(&bins[ho + d], v);
+              }
             } else {
-              const int64_t v = g_sum(L, q, base, en.ri_off, en.ri_len, s);
+              const int32_t v = g_sum(L, q, en.ri_off, en.ri_len, s);
               const int h = en.kind == KSS_IPA_EXISTING_ANTI ? 0 : (en.kind == KSS_IPA_REQ_AFFINITY ? 1 : 2);
               if (v > 0) flags |= 1 << h;
               const int ho = q.hoff[en.slot][h];
-              if (ho >= 0 && v) atomicAdd(&bins[ho + d], (int32_t)v);
+              if (ho >= 0 && v) atomicAdd(&bins[ho + d], v);
             }
           }
         }
@@ -628,9 +617,10 @@ __device__ __forceinline__ void spread_schedule(DevCluster c, const GPod* __rest
 #pragma unroll
       for (int i = 0; i < MAXH; i++) v[i] = hard_min[i];
       v[MAXH] = flags;
+      // histogram SUM over every bin, hard-pair presence OR (soft presence is filled later)
       if (!spread_reduce(H, L.xs, W, w, epoch, gran, err, v, op, 0, q.total_bins, q.total_bins, q.hard_pbins)) return;
       flags = v[MAXH];
-      // criticalPaths minimum over the present domains of histogram-valued hard keys
+      // criticalPaths: minimum over the present domains of histogram-valued hard keys
       int32_t mm[MAXH];
       bool any_hist = false;
 #pragma unroll
@@ -675,9 +665,9 @@ __device__ __forceinline__ void spread_schedule(DevCluster c, const GPod* __rest
         r.allowed = L.r32[cap + s];
         SVal e = dyn_eval(prof, q.dyn, wd, r);
         if (e.f == 0 && ((en >> KSS_F_POD_TOPOLOGY_SPREAD) & 1u) && q.n_hard > 0 &&
-            g_filter_pts(L, q, base, bins, hard_min, s, wd))
+            g_filter_pts(L, q, bins, hard_min, s, wd))
           e.f = KSS_F_POD_TOPOLOGY_SPREAD;
-        if (e.f == 0 && ((en >> KSS_F_INTER_POD_AFFINITY) & 1u) && has_ipa && g_filter_ipa(L, q, base, bins, flags, s))
+        if (e.f == 0 && ((en >> KSS_F_INTER_POD_AFFINITY) & 1u) && has_ipa && g_filter_ipa(L, q, bins, flags, s))
           e.f = KSS_F_INTER_POD_AFFINITY;
         int ign = 0;
         if (e.f == 0) {
@@ -686,7 +676,7 @@ __device__ __forceinline__ void spread_schedule(DevCluster c, const GPod* __rest
           max_na = e.na > max_na ? e.na : max_na;
           int64_t ipa = 0;
           if (has_ipa) {
-            ipa = g_ipa_score(L, q, base, bins, s);
+            ipa = g_ipa_score(L, q, bins, s);
             ipa_min = (int32_t)min((int64_t)ipa_min, ipa);
             ipa_max = (int32_t)max((int64_t)ipa_max, ipa);
           }
@@ -716,13 +706,14 @@ __device__ __forceinline__ void spread_schedule(DevCluster c, const GPod* __rest
                 const int d = L.lbl[sp.key * cap + s];
                 int32_t cnt = -1;
                 if (d >= 0) {
-                  if (sp.mode == SOFT_HOST) cnt = (int32_t)g_sum(L, q, base, sp.ri_off, sp.ri_len, s);
-                  else if (sp.mode == SOFT_DIRECT) cnt = g_policy(sp, wd) ? (int32_t)g_sum(L, q, base, sp.ri_off, sp.ri_len, s) : 0;
+                  if (sp.mode == SOFT_HOST) cnt = g_sum(L, q, sp.ri_off, sp.ri_len, s);
+                  else if (sp.mode == SOFT_DIRECT) cnt = g_policy(sp, wd) ? g_sum(L, q, sp.ri_off, sp.ri_len, s) : 0;
                   else cnt = bins[sp.off + d];
                 }
                 L.scnt[s] = cnt;
-                if (cnt < 0) lacks = 1;
-                else {
+                if (cnt < 0) {
+                  lacks = 1;
+                } else {
                   cmin = min(cmin, cnt);
                   cmax = max(cmax, cnt);
                 }
@@ -732,16 +723,13 @@ __device__ __forceinline__ void spread_schedule(DevCluster c, const GPod* __rest
         }
         L.sf[s] = e.f | (ign << 16);
       }
-    }
-    if (evaluated) {
-      int32_t v[13] = {nf, nign, max_tt, max_na, ipa_min, ipa_max, smissing, sdirect[0], sdirect[1], sdirect[2],
-                       sdirect[3], cmin, cmax};
+      // one exchange: feasible count, normalisation maxima, IPA extrema, PTS sizes / extrema
+      int32_t v[13] = {nf, nign, max_tt, max_na, ipa_min, ipa_max, smissing | (lacks << 30), sdirect[0], sdirect[1],
+                       sdirect[2], sdirect[3], cmin, cmax};
       const int op[13] = {OP_SUM, OP_SUM, OP_MAX, OP_MAX, OP_MIN, OP_MAX, OP_OR, OP_SUM, OP_SUM, OP_SUM, OP_SUM,
                           OP_MIN, OP_MAX};
-      // lacks rides in smissing's bit 31 (OR)
-      if (lacks) v[6] |= (int32_t)0x80000000u;
       if (!spread_reduce(H, L.xs, W, w, epoch, gran, err, v, op, 0, 0, q.total_bins + q.hard_pbins,
-                         has_soft ? q.total_pbins - q.hard_pbins : 0))
+                         q.total_pbins - q.hard_pbins))
         return;
       nf = v[0];
       nign = v[1];
@@ -749,8 +737,8 @@ __device__ __forceinline__ void spread_schedule(DevCluster c, const GPod* __rest
       max_na = v[3];
       ipa_min = v[4];
       ipa_max = v[5];
-      lacks = (v[6] >> 31) & 1;
-      smissing = v[6] & 0x7FFFFFFF;
+      lacks = (v[6] >> 30) & 1;
+      smissing = v[6] & 0xF;
 #pragma unroll
       for (int i = 0; i < MAXS; i++) sdirect[i] = v[7 + i];
       cmin = v[11];
@@ -762,7 +750,7 @@ __device__ __forceinline__ void spread_schedule(DevCluster c, const GPod* __rest
       }
     }
     if (evaluated) {
-      const bool scored = nf > 1;
+      const bool scored = nf > 1;  // a single feasible node is selected without scoring
       // ---- PodTopologySpread PreScore sizes + Score ----
       long long pts_min = 0, pts_max = 0;
       double wts[MAXS] = {0.0, 0.0, 0.0, 0.0};
@@ -783,14 +771,14 @@ __device__ __forceinline__ void spread_schedule(DevCluster c, const GPod* __rest
           else size = sz[i];
           wts[i] = go_log_dev((double)(size + 2));  // topologyNormalizingWeight
         }
-        if (one_soft) {  // scoreForCount is monotone in the count
+        if (one_soft) {  // scoreForCount(cnt) = round(cnt * w + maxSkew - 1) is monotone in cnt
           const double c1 = (double)(soft[0].max_skew - 1);
           pts_min = INT64_MAX;
-          if (cmax >= 0 && cmin != INT32_MAX) {
+          if (cmin != INT32_MAX) {
             pts_min = (long long)round((double)cmin * wts[0] + c1);
             pts_max = (long long)round((double)cmax * wts[0] + c1);
           }
-          if (lacks) {  // a scored node without the key: raw round(0) = 0
+          if (lacks) {  // a counted node without the key: raw round(0.0) = 0
             pts_min = pts_min < 0 ? pts_min : 0;
             pts_max = pts_max > 0 ? pts_max : 0;
           }
@@ -807,11 +795,11 @@ __device__ __forceinline__ void spread_schedule(DevCluster c, const GPod* __rest
                 const int d = L.lbl[sp.key * cap + s];
                 if (d < 0) continue;
                 int64_t cnt;
-                if (sp.mode == SOFT_HOST) cnt = g_sum(L, q, base, sp.ri_off, sp.ri_len, s);
-                else if (sp.mode == SOFT_DIRECT) cnt = g_policy(sp, sw[s]) ? g_sum(L, q, base, sp.ri_off, sp.ri_len, s) : 0;
+                if (sp.mode == SOFT_HOST) cnt = g_sum(L, q, sp.ri_off, sp.ri_len, s);
+                else if (sp.mode == SOFT_DIRECT) cnt = g_policy(sp, sw[s]) ? g_sum(L, q, sp.ri_off, sp.ri_len, s) : 0;
                 else cnt = bins[sp.off + d];
                 const double a = (double)cnt * wts[i];
-                sc = sc + (a + (double)(sp.max_skew - 1));
+                sc = sc + (a + (double)(sp.max_skew - 1));  // scoreForCount
               }
               raw = (long long)round(sc);
               pmin = raw < pmin ? raw : pmin;
@@ -819,7 +807,7 @@ __device__ __forceinline__ void spread_schedule(DevCluster c, const GPod* __rest
             }
             L.spts[s] = raw;
           }
-          // E3 in 32 bits: raw scores are bounded by the host (counts x log(N + 2) + maxSkew)
+          // 32-bit extrema: raw scores are host-bounded (spread_bounds_ok)
           int32_t v2[2] = {(int32_t)min(pmin, (long long)INT32_MAX), (int32_t)pmax};
           const int op2[2] = {OP_MIN, OP_MAX};
           if (!spread_reduce(H, L.xs, W, w, epoch, gran, err, v2, op2)) return;
@@ -838,11 +826,12 @@ __device__ __forceinline__ void spread_schedule(DevCluster c, const GPod* __rest
         int64_t total = 0;
         if (scored) {
           int64_t nm[KSS_NSCORE];
+          // DefaultNormalizeScore(100, reverse=true) / (100, reverse=false); quotients <= 100
           nm[KSS_S_TAINT_TOLERATION] = max_tt == 0 ? 100 : 100 - small_div(100 * L.stt[s], max_tt, rtt);
           nm[KSS_S_NODE_AFFINITY] = max_na != 0 ? small_div(100 * L.sna[s], max_na, rna) : L.sna[s];
           nm[KSS_S_NODE_RESOURCES_FIT] = L.sfit[s];
           nm[KSS_S_VOLUME_BINDING] = 0;
-          {
+          {  // PodTopologySpread.NormalizeScore
             int64_t raw = 0;
             if (has_soft && !(fi >> 16)) {
               if (one_soft) {
@@ -858,7 +847,7 @@ __device__ __forceinline__ void spread_schedule(DevCluster c, const GPod* __rest
             else pv = div_i64(100 * (pts_max + pts_min - raw), pts_max);
           }
           nm[KSS_S_INTER_POD_AFFINITY] = L.sipa[s];
-          if (ipa_norm) {
+          if (ipa_norm) {  // InterPodAffinity.NormalizeScore (skipped when topologyScore is empty)
             double f = 0.0;
             if (ipa_diff > 0) f = 100.0 * ((double)(L.sipa[s] - ipa_min) / (double)ipa_diff);
             nm[KSS_S_INTER_POD_AFFINITY] = (int64_t)f;
@@ -880,19 +869,30 @@ __device__ __forceinline__ void spread_schedule(DevCluster c, const GPod* __rest
       m.scored = scored ? 1 : 0;
       m.best_total = scored ? (int64_t)(ub >> 32) : 0;
     }
-    if (w == 0 && tid == 0) {
-      if (chosen) gchosen[k] = m.chosen;
-      if (meta) {
-        gmeta[k].chosen = m.chosen;
-        gmeta[k].n_feasible = m.n_feasible;
-        gmeta[k].scored = m.scored;
-        gmeta[k].status = m.status;
-        gmeta[k].best_total = m.best_total;
-      }
-    }
-    // ---- AssumePod on the winner's shard (node row, and the commit table) ----
+    // ---- outcome (shard 0) and AssumePod on the winner's shard ----
     const int x = m.chosen >= 0 ? m.chosen - c.node_base : -1;
-    if (x >= lo && x < hi && tid == 0) {
+    const bool won = x >= lo && x < hi;
+    if (tid == out_tid) {  // HBM stores off wave 0 (its vmcnt stays free for the exchanges)
+      if (w == 0) {
+        if (chosen) gchosen[k] = m.chosen;
+        if (meta) {
+          gmeta[k].chosen = m.chosen;
+          gmeta[k].n_feasible = m.n_feasible;
+          gmeta[k].scored = m.scored;
+          gmeta[k].status = m.status;
+          gmeta[k].best_total = m.best_total;
+        }
+      }
+      if (won)
+        for (int i = 0; i < q.n_cmt; i++) {
+          const int cm = q.cmt[i];
+          if (cm >= 0) continue;
+          const int row = -1 - cm;
+          KSS_GLOBAL int32_t* a = row < c.n_classes ? gcc + (size_t)row * N + x : gtc + (size_t)(row - c.n_classes) * N + x;
+          __hip_atomic_fetch_add(a, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+    if (won && tid == 0) {
       const int s = x - lo;
       const SPod& pk = q.dyn;
 #pragma unroll
@@ -900,27 +900,23 @@ __device__ __forceinline__ void spread_schedule(DevCluster c, const GPod* __rest
       L.r64[6 * cap + s] += pk.cnz[0];
       L.r64[7 * cap + s] += pk.cnz[1];
       L.r32[s] += 1;
-      if (pk.cls >= 0) L.delta[(size_t)pk.cls * cap + s] += 1;
-      for (int i = 0; i < pk.own_len; i++) L.delta[(size_t)(c.n_classes + ints[pk.own_off + i]) * cap + s] += 1;
+      for (int i = 0; i < q.n_cmt; i++)
+        if (q.cmt[i] >= 0) L.cnt[q.cmt[i] * cap + s] += 1;
     }
-    // ---- prefetched data of pod k+1 / k+2 -> their LDS slots ----
+    // ---- prefetched data of pods k+1 / k+2 -> their LDS slots ----
     if (pf_on) {
-      if (k + 2 < k1) reinterpret_cast<uint4*>(L.ring + (k + 2) % 3)[min(pf_lane, GPOD_Q - 1)] = pfq;
-#pragma unroll
-      for (int j = 0; j < G_PF; j++) {
-        if (j >= pf_per) break;
-        const int s = min(j * pf_n + pf_lane, own - 1);
-        L.st[((k + 1) & 1) * cap + s] = pfw[j];
-#pragma unroll
-        for (int r = 0; r < G_ROWS; r++) {
-          if (r >= nr1) break;
-          L.base[(((k + 1) & 1) * rows + r) * cap + s] = pfc[r][j];
-        }
+      if (k + 2 < k1) {  // lanes past the end rewrite the last uint4 with its own value
+        uint4* dst = L.ring + ((k + 2) % 3) * gq;
+        dst[min(pf_lane, gq - 1)] = pfq0;
+        dst[min(pf_lane + pf_n, gq - 1)] = pfq1;
       }
+#pragma unroll
+      for (int j = 0; j < G_PF; j++)
+        if (j < pf_per) L.st[((k + 1) & 1) * cap + min(j * pf_n + pf_lane, own - 1)] = pfw[j];
     }
     lds_barrier();
   }
-  // node state and the launch's commits back to HBM
+  // node state and the resident count rows back to HBM
   __syncthreads();
   for (int s = tid; s < own; s += nt) {
     const int n = lo + s;
@@ -929,12 +925,12 @@ __device__ __forceinline__ void spread_schedule(DevCluster c, const GPod* __rest
     c.nonzero[n] = (int64_t)L.r64[6 * cap + s];
     c.nonzero[N + n] = (int64_t)L.r64[7 * cap + s];
     c.pod_count[n] = L.r32[s];
-    for (int r = 0; r < n_rowids; r++) {
-      const int dlt = L.delta[(size_t)r * cap + s];
-      if (!dlt) continue;
-      if (r < c.n_classes) c.class_count[(size_t)r * N + n] += dlt;
-      else c.term_count[(size_t)(r - c.n_classes) * N + n] += dlt;
-    }
+  }
+  for (int i = tid; i < n_res * own; i += nt) {
+    const int r = i / own, s = i - r * own, row = res_rows[r];
+    const int32_t v = L.cnt[r * cap + s];
+    if (row < c.n_classes) c.class_count[(size_t)row * N + lo + s] = v;
+    else c.term_count[(size_t)(row - c.n_classes) * N + lo + s] = v;
   }
 }
 

@@ -55,6 +55,8 @@ SIGNATURES = [
     ("kss_last_geometry", C.c_int, [C.c_void_p, P(C.c_int32)]),
     ("kss_last_kernel", C.c_int, [C.c_void_p]),
     ("kss_device_go_log", C.c_int, [C.c_int32, C.c_void_p, C.c_void_p, C.c_int32]),
+    ("kss_plan_podset", C.c_int, [C.POINTER(abi.Cluster), C.POINTER(abi.PodSet), C.c_void_p]),
+    ("kss_plan_reason", C.c_char_p, [C.c_int32]),
     ("kss_fetch_meta", C.c_int, [C.c_void_p, C.c_int32, C.c_int32, P(C.c_int64)]),
     ("kss_set_names", C.c_int, [C.c_void_p, P(abi.Names)]),
     ("kss_format_annotations", C.c_int, [C.c_void_p, P(abi.PodResult), C.c_int32, C.c_char_p, C.c_size_t,
@@ -398,3 +400,11 @@ def device_go_log(x, device: int = 0) -> np.ndarray:
     y = np.empty_like(x)
     check(lib().kss_device_go_log(device, x.ctypes.data, y.ctypes.data, len(x)))
     return y
+
+
+def plan_podset(cluster: abi.Cluster, podset: abi.PodSet) -> dict:
+    """Host-only: the sequential-loop kernel a staged batch can take (kss_plan_podset)."""
+    out = (C.c_int32 * 3)()
+    check(lib().kss_plan_podset(C.byref(cluster), C.byref(podset), out))
+    kernel = {1: "k_simple", 2: "k_spread"}.get(out[0], "k_schedule")
+    return {"kernel": kernel, "pod": out[1], "reason": lib().kss_plan_reason(out[2]).decode()}

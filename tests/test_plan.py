@@ -1,0 +1,35 @@
+"""Host-only kernel planning (kss_plan_podset): which sequential-loop kernel a batch's pod
+programs admit, and the reason when k_spread is ruled out (no GPU needed)."""
+import pytest
+
+import progfuzz
+from kss import abi, native
+from kss.compile import compile_cluster
+
+
+@pytest.mark.parametrize("config,kernel", [(1, "k_simple"), (2, "k_simple"), (3, "k_spread"), (4, "k_spread"),
+                                           (5, "k_simple")])
+def test_baseline_configs(config, kernel):
+    s = native.Synth(config, 0, 300, 200)
+    assert native.plan_podset(s.cluster, s.pods) == {"kernel": kernel, "pod": -1, "reason": "eligible"}
+
+
+@pytest.mark.parametrize("seed,n_nodes,n_pods", [(1, 60, 200), (2, 300, 300), (3, 700, 250), (5, 1000, 200)])
+def test_program_fuzz_batches_take_k_spread(seed, n_nodes, n_pods):
+    """The batches test_gpu_spread.py runs: every one admitted by k_spread (the GPU tests
+    assert the kernel that ran)."""
+    nodes, bound, pods = progfuzz.make(seed, n_nodes, n_pods)
+    cc, cp, _ = compile_cluster(nodes, bound, pods)
+    assert native.plan_podset(cc.as_struct(), cp.as_struct())["kernel"] == "k_spread"
+
+
+def test_refusal_names_pod_and_reason():
+    """Required anti-affinity over five topology keys exceeds the four key slots of a pod
+    program: k_schedule only, with the pod and the reason named."""
+    nodes, bound, pods = progfuzz.make(9, 20, 5)
+    keys = (progfuzz.K_ZONE, progfuzz.K_RACK, progfuzz.K_HOST, progfuzz.K_ITYPE, "example.com/none")
+    pods[3]["spec"]["affinity"] = {"podAntiAffinity": {"requiredDuringSchedulingIgnoredDuringExecution": [
+        {"labelSelector": {"matchLabels": {"app": "a1"}}, "topologyKey": k} for k in keys]}}
+    cc, cp, _ = compile_cluster(nodes, bound, pods)
+    plan = native.plan_podset(cc.as_struct(), cp.as_struct())
+    assert plan == {"kernel": "k_schedule", "pod": 3, "reason": "more than 4 inter-pod-affinity topology keys"}

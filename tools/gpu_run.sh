@@ -9,7 +9,7 @@ export TMPDIR=/tmp
 for step in "$@"; do
   case $step in
     tests)  timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $OUT/pytest_gpu.log 2>&1 ;;
-    spread) timeout -k 10 600 python -u -m pytest tests/test_gpu_spread.py tests/test_gpu_scale.py -k "spread or c3 or c4" -m gpu -x -v --timeout 200 --timeout-method thread > $OUT/pytest_spread.log 2>&1 ;;
+    spread) KSS_TRACE_PATH=1 timeout -k 10 600 python -u -m pytest tests/test_gpu_spread.py tests/test_gpu_scale.py -k "spread or c3 or c4" -m gpu -x -v --timeout 200 --timeout-method thread > $OUT/pytest_spread.log 2>&1 ;;
     smoke)  timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 ;;
     bench)  timeout -k 10 600 python -u bench.py > $OUT/bench.json 2> $OUT/bench.err ;;
     stamps) rm -f $OUT/*.bin; KSS_STAMPS_FILE=$OUT/simple_c2.bin timeout -k 10 120 python -u bench.py --steps 1 --warmup 0 --pods 2000 --no-cpu --no-traffic > /dev/null && python tools/stamps.py $OUT/*.bin > $OUT/stamps.txt ;;
