@@ -189,7 +189,7 @@ __global__ __launch_bounds__(KSS_MAX_THREADS) void k_simple(const DevJob* __rest
 template <bool DEF>
 __global__ __launch_bounds__(KSS_MAX_THREADS) void k_spread(const DevJob* __restrict__ jobs, int W, int cap, int bins_cap,
                                                             int n_res, int gq, int k0, int k1, unsigned long long* gran,
-                                                            int* err) {
+                                                            int* err, unsigned long long* stamps) {
   extern __shared__ __attribute__((aligned(16))) long long smem[];
   const int ji = blockIdx.x / W, w = blockIdx.x % W;
   const DevJob job = jobs[ji];
@@ -203,7 +203,7 @@ __global__ __launch_bounds__(KSS_MAX_THREADS) void k_spread(const DevJob* __rest
   }
   const kss_profile& P = DEF ? def_prof : H.prof;
   spread_schedule(job.c, job.gpods, job.stat, job.res_rows, n_res, k0, min(k1, job.n_pods), job.chosen, job.meta, P, W, w,
-                  cap, bins_cap, gq, gran ? gran + (size_t)ji * 2 * W * G_XW : nullptr, err, smem);
+                  cap, bins_cap, gq, gran ? gran + (size_t)ji * 2 * W * G_XW : nullptr, err, stamps, smem);
 }
 
 // Class / term counts of the chosen nodes of pods [k0, min(k1, n_pods)) of every job
@@ -1465,9 +1465,12 @@ static bool spread_fits(const Geometry& g, const GpodNeeds& q, int n_keys, int n
 // and counts back in HBM between launches).  ev (optional): 2 events per chunk.
 static int launch_spread(hipStream_t st, const Geometry& g, const GpodNeeds& q, int n_keys, int n_res,
                          const DevJob* jobs, const kss_profile& prof, int n_pods, int max_nodes, int chunk,
-                         unsigned long long* gran, size_t gran_bytes, int* err, hipEvent_t* ev = nullptr) {
+                         unsigned long long* gran, size_t gran_bytes, int* err, unsigned long long* stamps = nullptr,
+                         hipEvent_t* ev = nullptr) {
   int cap = g.npt * g.threads, bins_cap = q.bins_cap, nr = n_res, gq = q.gq;
-  const size_t shmem = spread_lds(g, q, n_keys, n_res);
+  size_t shmem = spread_lds(g, q, n_keys, n_res);
+  if (stamps && shmem + G_STAMP_LDS > KSS_LDS_BUDGET) stamps = nullptr;  // diagnostics only where they fit
+  if (stamps) shmem += G_STAMP_LDS;
   const bool def = same_profile(prof, default_profile_c());
   const void* fn = def ? (const void*)k_spread<true> : (const void*)k_spread<false>;
   HIP_TRY(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shmem));
@@ -1483,8 +1486,9 @@ static int launch_spread(hipStream_t st, const Geometry& g, const GpodNeeds& q, 
       hipLaunchKernelGGL(k_static<false>, sgrid, dim3(256), 0, st, jobs, pr, k0, k1);
     HIP_TRY(hipGetLastError());
     if (gran && k0 > 0) HIP_TRY(hipMemsetAsync(gran, 0, gran_bytes, st));
-    void* args[] = {(void*)&jobs, (void*)&W,  (void*)&cap, (void*)&bins_cap, (void*)&nr,
-                    (void*)&gq,   (void*)&k0, (void*)&k1,  (void*)&gran,     (void*)&err};
+    unsigned long long* sp = k0 == 0 ? stamps : nullptr;
+    void* args[] = {(void*)&jobs, (void*)&W,  (void*)&cap, (void*)&bins_cap, (void*)&nr, (void*)&gq,
+                    (void*)&k0,   (void*)&k1, (void*)&gran, (void*)&err,     (void*)&sp};
     const int ci = k0 / chunk;
     if (ev) HIP_TRY(hipEventRecord(ev[2 * ci], st));
     if (g.W > 1) {
@@ -1599,8 +1603,8 @@ static int run_single(kss_ctx* ctx, const PlanNeeds& need, const DevPods& dp, in
   HIP_TRY(hipEventRecord(ctx->ev0, ctx->stream));
   unsigned long long* stamps = nullptr;
   // k_schedule: shard 0 only; k_simple: every shard (arrival skew of the exchanges)
-  const size_t stamp_bytes = sizeof(unsigned long long) * 8 * KSS_NSTAMP_PODS * (simple ? g.W : 1);
-  if (ctx->stamps_file && !spread) {
+  const size_t stamp_bytes = sizeof(unsigned long long) * 8 * KSS_NSTAMP_PODS * (loop ? g.W : 1);
+  if (ctx->stamps_file) {
     if ((rc = ctx->stamp_buf.ensure(stamp_bytes))) return rc;
     stamps = (unsigned long long*)ctx->stamp_buf.p;
     HIP_TRY(hipMemsetAsync(stamps, 0, stamp_bytes, ctx->stream));
@@ -1616,7 +1620,7 @@ static int run_single(kss_ctx* ctx, const PlanNeeds& need, const DevPods& dp, in
                        (int*)ctx->err_buf.p, stamps, ctx->loop_ev.data());
   else if (spread)
     rc = launch_spread(ctx->stream, g, ctx->gneed, ctx->dc.n_keys, n_res, (const DevJob*)ctx->job_buf.p, ctx->prof, n,
-                       (int)N, chunk, gran, gb, (int*)ctx->err_buf.p, ctx->loop_ev.data());
+                       (int)N, chunk, gran, gb, (int*)ctx->err_buf.p, stamps, ctx->loop_ev.data());
   else
     rc = launch_schedule(ctx->stream, g, 1, std::max(need.bins_cap, 0), need.general, ctx->dc.n_keys,
                          (const DevJob*)ctx->job_buf.p, ctx->prof, gran, (int*)ctx->err_buf.p, stamps);
@@ -1650,10 +1654,10 @@ static int run_single(kss_ctx* ctx, const PlanNeeds& need, const DevPods& dp, in
   ctx->recorded = record ? n : (n > 0 && !loop ? 1 : 0);
   ctx->meta_n = n;
   ctx->axis_meta_dirty = false;
-  if (stamps) {  // record: {kernel (0 k_schedule, 1 k_simple), shards} then the stamps
+  if (stamps) {  // record: {kernel (0 k_schedule, 1 k_simple, 2 k_spread), shards} then the stamps
     std::vector<unsigned long long> h(2 + stamp_bytes / 8);
-    h[0] = simple ? 1 : 0;
-    h[1] = simple ? (unsigned long long)g.W : 1;
+    h[0] = simple ? 1 : (spread ? 2 : 0);
+    h[1] = loop ? (unsigned long long)g.W : 1;
     HIP_TRY(hipMemcpy(h.data() + 2, stamps, stamp_bytes, hipMemcpyDeviceToHost));
     if (FILE* f = fopen(ctx->stamps_file, "ab")) {
       fwrite(h.data(), 8, h.size(), f);

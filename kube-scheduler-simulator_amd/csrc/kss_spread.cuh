@@ -36,6 +36,8 @@ constexpr int G_PF = 4;      // static words per prefetch lane (host-checked)
 constexpr int G_XW = 512;    // 32-bit values per shard per exchange (host-checked)
 constexpr int G_NS = 16;     // scalar slots of an exchange
 constexpr int G_SCORE = 3;   // GIpa.kind of a merged InterPodAffinity score entry (KSS_IPA_SCORE_CLASS)
+constexpr int G_NSTAMP = KSS_NSTAMP_PODS / 2;  // pods with diagnostic phase stamps, 16 per pod
+constexpr size_t G_STAMP_LDS = 8 * 16 * (size_t)G_NSTAMP;
 
 struct GSpread {
   int32_t max_skew;
@@ -211,6 +213,29 @@ __device__ __forceinline__ int32_t op32(int op, int32_t a, int32_t b) {
 }
 __device__ __forceinline__ int32_t ident32(int op) { return op == OP_MAX ? INT32_MIN : (op == OP_MIN ? INT32_MAX : 0); }
 
+// K 32-bit wave reductions on the DPP network, interleaved: each step issues every value's
+// move before combining any (kss_simple.cuh wave_red's sequence); lane 63 holds the results.
+template <int CTRL, int ROWS, int K>
+__device__ __forceinline__ void dpp32_step(int32_t (&v)[K], const int (&ops)[K]) {
+  int32_t t[K];
+#pragma unroll
+  for (int k = 0; k < K; k++) t[k] = __builtin_amdgcn_update_dpp(ident32(ops[k]), v[k], CTRL, ROWS, 0xF, false);
+#pragma unroll
+  for (int k = 0; k < K; k++) v[k] = op32(ops[k], v[k], t[k]);
+}
+
+template <int K>
+__device__ __forceinline__ void wave_red32(int32_t (&v)[K], const int (&ops)[K]) {
+  dpp32_step<0xB1, 0xF>(v, ops);   // quad_perm [1,0,3,2]
+  dpp32_step<0x4E, 0xF>(v, ops);   // quad_perm [2,3,0,1]
+  dpp32_step<0x141, 0xF>(v, ops);  // row_half_mirror
+  dpp32_step<0x140, 0xF>(v, ops);  // row_mirror
+  dpp32_step<0x142, 0xA>(v, ops);  // row_bcast:15 -> rows 1, 3
+  dpp32_step<0x143, 0xC>(v, ops);  // row_bcast:31 -> rows 2, 3
+#pragma unroll
+  for (int k = 0; k < K; k++) v[k] = __builtin_amdgcn_readlane(v[k], 63);
+}
+
 // Cross-shard part of a 32-bit exchange, wave 0 only: publish M = K + ns + no values
 // (scalars xs[0..K), SUM bins xs[G_NS + sum_lo ..), OR bins xs[G_NS + or_lo ..)) as
 // {epoch, value} granules, sweep every shard's (all loads of a round in flight), and
@@ -219,7 +244,7 @@ __device__ __forceinline__ int32_t ident32(int op) { return op == OP_MAX ? INT32
 __device__ __noinline__ bool spread_exchange(SpreadHdr& H, int32_t* xs, unsigned long long* gran, int W, int wself,
                                              unsigned epoch, int* err, int K, unsigned opbits, int sum_lo, int ns,
                                              int or_lo, int no) {
-  constexpr int XB = 8;
+  constexpr int XB = 16;  // (shard, value) pairs per lane per poll: W * M <= 1024 in one round
   const int lane = threadIdx.x & 63;
   const int M = K + ns + no;
   auto slot = [&](int j) -> int32_t* {
@@ -291,12 +316,13 @@ __device__ __forceinline__ bool spread_reduce(SpreadHdr& H, int32_t* xs, int W, 
                                               int no = 0, bool local = false) {
   static_assert(K <= G_NS, "too many values");
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  int32_t r[K];
 #pragma unroll
-  for (int k = 0; k < K; k++) {
-    int32_t r = v[k];
+  for (int k = 0; k < K; k++) r[k] = v[k];
+  wave_red32(r, ops);
+  if (lane == 0) {
 #pragma unroll
-    for (int m = 32; m >= 1; m >>= 1) r = op32(ops[k], r, __shfl_xor(r, m, 64));
-    if (lane == 0) H.red[wave][k] = r;
+    for (int k = 0; k < K; k++) H.red[wave][k] = r[k];
   }
   lds_barrier();
   if (threadIdx.x < K) {
@@ -465,7 +491,8 @@ __device__ __forceinline__ void spread_schedule(DevCluster c, const GPod* __rest
                                                 const uint32_t* __restrict__ stat, const int32_t* __restrict__ res_rows,
                                                 int n_res, int k0, int k1, int32_t* chosen, PodMeta* meta,
                                                 const kss_profile& prof, int W, int w, int cap, int bins_cap, int gq,
-                                                unsigned long long* gran, int* err, long long* smem) {
+                                                unsigned long long* gran, int* err, unsigned long long* stamps,
+                                                long long* smem) {
   const int tid = threadIdx.x, nt = blockDim.x;
   SpreadHdr& H = *reinterpret_cast<SpreadHdr*>(smem);
   const SpreadShard L = spread_view(smem, cap, bins_cap, c.n_keys, n_res, gq);
@@ -474,6 +501,14 @@ __device__ __forceinline__ void spread_schedule(DevCluster c, const GPod* __rest
   const int lo = min(c.N, w * per), hi = min(c.N, lo + per), own = hi - lo;
   if (k1 <= k0) return;
   int32_t* bins = L.xs + G_NS;
+  // diagnostic phase stamps (KSS_STAMPS_FILE): s_memrealtime into LDS, copied out at the end
+  // (no HBM store on the exchange wave while the loop runs)
+  unsigned long long* stl =
+      stamps ? reinterpret_cast<unsigned long long*>(reinterpret_cast<uint8_t*>(smem) +
+                                                     spread_lds_bytes(cap, bins_cap, c.n_keys, n_res, gq))
+             : nullptr;
+  if (stl)
+    for (int i = tid; i < 16 * G_NSTAMP; i += nt) stl[i] = 0;
   // shard state -> LDS: node rows, label ids, resident count rows, static words of pod k0,
   // records of pods k0 and k0 + 1
   for (int s = tid; s < own; s += nt) {
@@ -525,6 +560,11 @@ __device__ __forceinline__ void spread_schedule(DevCluster c, const GPod* __rest
   unsigned epoch = 0;
   int kparity = 0;
   for (int k = k0; k < k1; k++) {
+#define GSTAMP(i)                                                                      \
+  do {                                                                                 \
+    if (stl && tid == 0 && k - k0 < G_NSTAMP) stl[(k - k0) * 16 + (i)] = wall_clock64(); \
+  } while (0)
+    GSTAMP(0);
     const GPod& q = *reinterpret_cast<const GPod*>(L.ring + (k % 3) * gq);
     const uint32_t* sw = L.st + (k & 1) * cap;
     // prefetch (every wave but wave 0): record of pod k+2, static words of pod k+1.  The
@@ -612,6 +652,7 @@ __device__ __forceinline__ void spread_schedule(DevCluster c, const GPod* __rest
           }
         }
       }
+      GSTAMP(1);
       int32_t v[MAXH + 1];
       const int op[MAXH + 1] = {OP_MIN, OP_MIN, OP_MIN, OP_MIN, OP_OR};
 #pragma unroll
@@ -640,6 +681,7 @@ __device__ __forceinline__ void spread_schedule(DevCluster c, const GPod* __rest
       for (int i = 0; i < MAXH; i++) hard_min[i] = mm[i];
       for (int b = q.hard_pbins + tid; b < q.total_pbins; b += nt) bins[q.total_bins + b] = 0;
       lds_barrier();
+      GSTAMP(2);
     }
     // ---- filter + raw scores ----
     const bool has_soft = q.n_soft > 0, has_ipa = q.n_ipa > 0;
@@ -723,6 +765,7 @@ __device__ __forceinline__ void spread_schedule(DevCluster c, const GPod* __rest
         }
         L.sf[s] = e.f | (ign << 16);
       }
+      GSTAMP(3);
       // one exchange: feasible count, normalisation maxima, IPA extrema, PTS sizes / extrema
       int32_t v[13] = {nf, nign, max_tt, max_na, ipa_min, ipa_max, smissing | (lacks << 30), sdirect[0], sdirect[1],
                        sdirect[2], sdirect[3], cmin, cmax};
@@ -743,6 +786,7 @@ __device__ __forceinline__ void spread_schedule(DevCluster c, const GPod* __rest
       for (int i = 0; i < MAXS; i++) sdirect[i] = v[7 + i];
       cmin = v[11];
       cmax = v[12];
+      GSTAMP(4);
       m.n_feasible = nf;
       if (nf == 0) {
         m.status = 1;
@@ -807,12 +851,14 @@ __device__ __forceinline__ void spread_schedule(DevCluster c, const GPod* __rest
             }
             L.spts[s] = raw;
           }
+          GSTAMP(5);
           // 32-bit extrema: raw scores are host-bounded (spread_bounds_ok)
           int32_t v2[2] = {(int32_t)min(pmin, (long long)INT32_MAX), (int32_t)pmax};
           const int op2[2] = {OP_MIN, OP_MAX};
           if (!spread_reduce(H, L.xs, W, w, epoch, gran, err, v2, op2)) return;
           pts_min = v2[0] == INT32_MAX ? INT64_MAX : v2[0];
           pts_max = v2[1];
+          GSTAMP(6);
         }
       }
       // ---- NormalizeScore + weights + selectHost ----
@@ -862,7 +908,9 @@ __device__ __forceinline__ void spread_schedule(DevCluster c, const GPod* __rest
         const long long key = (long long)(((unsigned long long)(uint32_t)total << 32) | (0xFFFFFFFFull - g));
         best = key > best ? key : best;
       }
+      GSTAMP(7);
       if (!spread_argmax(H, W, w, epoch, gran, err, kparity, best)) return;
+      GSTAMP(8);
       kparity ^= 1;
       const unsigned long long ub = (unsigned long long)best;
       m.chosen = best ? (int)(0xFFFFFFFFull - (ub & 0xFFFFFFFFull)) : -1;
@@ -915,9 +963,13 @@ __device__ __forceinline__ void spread_schedule(DevCluster c, const GPod* __rest
         if (j < pf_per) L.st[((k + 1) & 1) * cap + min(j * pf_n + pf_lane, own - 1)] = pfw[j];
     }
     lds_barrier();
+    GSTAMP(9);
+#undef GSTAMP
   }
   // node state and the resident count rows back to HBM
   __syncthreads();
+  if (stl)
+    for (int i = tid; i < 16 * G_NSTAMP; i += nt) stamps[(size_t)w * 8 * KSS_NSTAMP_PODS + i] = stl[i];
   for (int s = tid; s < own; s += nt) {
     const int n = lo + s;
 #pragma unroll

@@ -7,7 +7,11 @@ k_simple (every shard, 16 per pod): 0 start, 1 pass B, 2 best-key reduction, 3 p
 4 statistics reduction (= publish), 5 exchange + barrier, 6 commit + ring store.  For
 k_simple the arrival skew of the exchange is reported: per pod, the spread of the
 shards' publish times, and the wait from the LAST publish to each shard's completion
-(propagation + reductions)."""
+(propagation + reductions).
+k_spread (every shard, 16 per pod): 0 start, 1 stats pass, 2 stats exchange (E1) + minima,
+3 filter pass, 4 filter exchange (E2), 5 PodTopologySpread score pass, 6 its exchange (E3),
+7 normalize pass, 8 argmax exchange (E4), 9 commit + ring store.  Phases a pod skips
+carry the previous stamp (duration 0)."""
 import sys
 
 import numpy as np
@@ -15,6 +19,7 @@ import numpy as np
 NAMES = ["plan", "filter", "x_filter", "normalize", "x_argmax", "commit"]
 NAMES_SIMPLE = ["passB", "red_best", "passA", "red_stats", "xchg", "commit"]
 NSTAMP_PODS = 256
+NAMES_SPREAD = ["stats", "x_stats", "filter", "x_filter", "pts", "x_pts", "normalize", "x_argmax", "commit"]
 
 
 def records(path):
@@ -22,7 +27,7 @@ def records(path):
     out, i = [], 0
     while i + 2 <= raw.size:
         kind, w = int(raw[i]), int(raw[i + 1])
-        n = 8 * NSTAMP_PODS * (w if kind == 1 else 1)
+        n = 8 * NSTAMP_PODS * (w if kind in (1, 2) else 1)
         out.append((kind, w, raw[i + 2:i + 2 + n].astype(np.int64)))
         i += 2 + n
     return out
@@ -40,6 +45,9 @@ def summarise(path):
                          + f" | pod={np.median(tot):.2f} us (n={len(a)})")
             continue
         a = a.reshape(w, NSTAMP_PODS // 2, 16)
+        if kind == 2:
+            lines.append(spread_summary(w, a))
+            continue
         s0 = a[0]
         ok = (s0[:, 0] > 0) & (s0[:, 6] > 0)
         d = np.diff(s0[ok, :7], axis=1) / 100.0
@@ -61,6 +69,31 @@ def summarise(path):
             line += f"\n  start -> passA done per shard: median {np.median(pa[:, good]):.2f} us, max over shards (median) {np.median(pa[:, good].max(axis=0)):.2f}"
         lines.append(line)
     return "\n".join(lines)
+
+
+def spread_summary(w, a):
+    a = a[:, :, :10].copy()
+    ok = (a[:, :, 0] > 0).all(axis=0) & (a[:, :, 9] > 0).all(axis=0)
+    a = a[:, ok, :]
+    for i in range(1, 9):  # skipped phases: duration 0
+        z = a[:, :, i] == 0
+        a[:, :, i][z] = a[:, :, i - 1][z]
+    d = np.diff(a[0], axis=1) / 100.0
+    tot = (a[0, :, 9] - a[0, :, 0]) / 100.0
+    line = (f"k_spread W={w} shard0: " + " ".join(f"{n}={m:.2f}" for n, m in zip(NAMES_SPREAD, d.mean(axis=0)))
+            + f" (means) | pod median {np.median(tot):.2f} us, mean {tot.mean():.2f} (n={ok.sum()})")
+    for name, pub, done in (("E1", 1, 2), ("E2", 3, 4), ("E4", 7, 8)):
+        p, dn = a[:, :, pub], a[:, :, done]
+        used = (dn[0] > p[0])
+        if not used.any():
+            continue
+        p, dn = p[:, used], dn[:, used]
+        last = p.max(axis=0)
+        skew = (last - p.min(axis=0)) / 100.0
+        after = (dn - last[None, :]) / 100.0
+        line += (f"\n  {name} ({used.sum()} pods): publish spread median {np.median(skew):.2f} us,"
+                 f" last publish -> done median {np.median(after):.2f} us (min over shards {np.median(after.min(axis=0)):.2f})")
+    return line
 
 
 if __name__ == "__main__":
