@@ -213,6 +213,13 @@ __device__ __forceinline__ int32_t op32(int op, int32_t a, int32_t b) {
 }
 __device__ __forceinline__ int32_t ident32(int op) { return op == OP_MAX ? INT32_MIN : (op == OP_MIN ? INT32_MAX : 0); }
 
+// op32 for an operator that differs between lanes: every operator computed, one picked by
+// selects (a per-lane `op` in op32 compiles to nested exec-mask branches)
+__device__ __forceinline__ int32_t op32_lane(int op, int32_t a, int32_t b) {
+  const int32_t s = (int32_t)((uint32_t)a + (uint32_t)b), mx = max(a, b), mn = min(a, b), o = a | b;
+  return op == OP_SUM ? s : (op == OP_MAX ? mx : (op == OP_MIN ? mn : o));
+}
+
 // K 32-bit wave reductions on the DPP network, interleaved: each step issues every value's
 // move before combining any (kss_simple.cuh wave_red's sequence); lane 63 holds the results.
 template <int CTRL, int ROWS, int K>
@@ -238,15 +245,21 @@ __device__ __forceinline__ void wave_red32(int32_t (&v)[K], const int (&ops)[K])
 
 // Cross-shard part of a 32-bit exchange, wave 0 only: publish M = K + ns + no values
 // (scalars xs[0..K), SUM bins xs[G_NS + sum_lo ..), OR bins xs[G_NS + or_lo ..)) as
-// {epoch, value} granules, sweep every shard's (all loads of a round in flight), and
-// combine into the same LDS slots with LDS atomics (the own contribution comes back
-// through the sweep).
-__device__ __noinline__ bool spread_exchange(SpreadHdr& H, int32_t* xs, unsigned long long* gran, int W, int wself,
-                                             unsigned epoch, int* err, int K, unsigned opbits, int sum_lo, int ns,
-                                             int or_lo, int no) {
-  constexpr int XB = 16;  // (shard, value) pairs per lane per poll: W * M <= 1024 in one round
-  const int lane = threadIdx.x & 63;
+// {epoch, value} granules, then sweep every shard's.  The sweep gives each value
+// T = 64 / M lanes; lane (j, t) polls value j of shards t, t + T, ... (up to XS at once, all
+// in flight), folds them in registers, and one LDS atomic per lane combines the T partials
+// (the slot holds the operator's identity since the publish; the own contribution comes
+// back through the sweep).  A matched granule is final: it can only change at epoch + 2.
+// The scalars are combined over the workgroup's waves here (H.red), by the lanes that
+// publish them.  Granules are accessed through address-space-1 pointers: flat accesses would
+// also count in lgkmcnt and make every following LDS wait on the HBM stores.
+__device__ __forceinline__ bool spread_exchange(SpreadHdr& H, int32_t* xs, unsigned long long* gran_, int W, int wself,
+                                                unsigned epoch, int* err, int K, unsigned opbits, int sum_lo, int ns,
+                                                int or_lo, int no, unsigned long long* sp) {
+  constexpr int XS = 16;  // shards polled per lane at once
+  const int lane = threadIdx.x & 63, nw = blockDim.x >> 6;
   const int M = K + ns + no;
+  KSS_GLOBAL unsigned long long* gran = gp(gran_);
   auto slot = [&](int j) -> int32_t* {
     if (j < K) return xs + j;
     if (j < K + ns) return xs + G_NS + sum_lo + (j - K);
@@ -254,52 +267,70 @@ __device__ __noinline__ bool spread_exchange(SpreadHdr& H, int32_t* xs, unsigned
   };
   auto opof = [&](int j) { return j < K ? (int)((opbits >> (2 * j)) & 3u) : (j < K + ns ? OP_SUM : OP_OR); };
   const unsigned long long tag = (unsigned long long)epoch << 32;
-  unsigned long long* mine = gran + ((size_t)(epoch & 1) * W + wself) * G_XW;
+  KSS_GLOBAL unsigned long long* mine = gran + ((size_t)(epoch & 1) * W + wself) * G_XW;
   for (int j = lane; j < M; j += 64) {
     int32_t* sl = slot(j);
-    __hip_atomic_store(mine + j, tag | (uint32_t)*sl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    *sl = ident32(opof(j));
-  }
-  const unsigned long long* base = gran + (size_t)(epoch & 1) * W * G_XW;
-  const int Q = W * M;
-  for (int q0 = 0; q0 < Q; q0 += 64 * XB) {
-    unsigned long long g[XB];
-    for (unsigned spins = 0;; ++spins) {
-      bool ok = true;
-#pragma unroll
-      for (int b = 0; b < XB; b++) {
-        const int q = q0 + b * 64 + lane;
-        g[b] = tag;
-        if (q < Q) {
-          const int w = q / M, j = q - w * M;
-          g[b] = __hip_atomic_load(base + (size_t)w * G_XW + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-      }
-#pragma unroll
-      for (int b = 0; b < XB; b++) ok &= (g[b] >> 32) == epoch;
-      if (__all(ok)) break;
-      if (spins >= SPIN_LIMIT) {
-        if (lane == 0) {
-          H.abort = 1;
-          __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        return false;
-      }
-      __builtin_amdgcn_s_sleep(1);
+    const int op = opof(j);
+    int32_t v = *sl;
+    if (j < K) {  // workgroup value of scalar j: its waves' partials
+      v = H.red[0][j];
+      for (int x = 1; x < nw; x++) v = op32_lane(op, v, H.red[x][j]);
     }
+    __hip_atomic_store(mine + j, tag | (uint32_t)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *sl = ident32(op);
+  }
+  if (sp && lane == 0) sp[2] = wall_clock64();
+  KSS_GLOBAL const unsigned long long* base = gran + (size_t)(epoch & 1) * W * G_XW;
+  for (int j0 = 0; j0 < M; j0 += 64) {
+    const int mc = min(64, M - j0);
+    const int T = 64 / mc;  // lanes per value in this chunk
+    const int t = lane / mc, j = j0 + (lane - t * mc);
+    const bool act = t < T;
+    const int op = opof(min(j, M - 1));
+    // the operator differs between lanes: fold all four, branch-free, and pick one at the end
+    int32_t a_sum = 0, a_max = INT32_MIN, a_min = INT32_MAX, a_or = 0;
+    for (int w0 = 0; w0 < W; w0 += T * XS) {
+      unsigned long long g[XS];
+      for (unsigned spins = 0;; ++spins) {
+        bool ok = true;
 #pragma unroll
-    for (int b = 0; b < XB; b++) {
-      const int q = q0 + b * 64 + lane;
-      if (q < Q) {
-        const int j = q % M;
-        const int32_t v = (int32_t)(uint32_t)g[b];
-        int32_t* sl = slot(j);
-        switch (opof(j)) {
-          case OP_SUM: atomicAdd(sl, v); break;
-          case OP_MAX: atomicMax(sl, v); break;
-          case OP_MIN: atomicMin(sl, v); break;
-          default: atomicOr(sl, v); break;
+        for (int b = 0; b < XS; b++) {
+          const int w = w0 + t + T * b;
+          g[b] = tag;
+          if (act && w < W)
+            g[b] = __hip_atomic_load(base + (size_t)w * G_XW + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
+#pragma unroll
+        for (int b = 0; b < XS; b++) ok &= (g[b] >> 32) == epoch;
+        if (__all(ok)) break;
+        if (spins >= SPIN_LIMIT) {
+          if (lane == 0) {
+            H.abort = 1;
+            __hip_atomic_store(gp(err), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          }
+          return false;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      if (sp && lane == 0) sp[3] = wall_clock64();
+#pragma unroll
+      for (int b = 0; b < XS; b++) {
+        const bool in = w0 + t + T * b < W;
+        const int32_t x = (int32_t)(uint32_t)g[b];
+        a_sum += in ? x : 0;
+        a_max = max(a_max, in ? x : INT32_MIN);
+        a_min = min(a_min, in ? x : INT32_MAX);
+        a_or |= in ? x : 0;
+      }
+    }
+    const int32_t acc = op == OP_SUM ? a_sum : (op == OP_MAX ? a_max : (op == OP_MIN ? a_min : a_or));
+    if (act) {
+      int32_t* sl = slot(j);
+      switch (op) {
+        case OP_SUM: atomicAdd(sl, acc); break;
+        case OP_MAX: atomicMax(sl, acc); break;
+        case OP_MIN: atomicMin(sl, acc); break;
+        default: atomicOr(sl, acc); break;
       }
     }
   }
@@ -313,7 +344,7 @@ template <int K>
 __device__ __forceinline__ bool spread_reduce(SpreadHdr& H, int32_t* xs, int W, int w, unsigned& epoch,
                                               unsigned long long* gran, int* err, int32_t (&v)[K],
                                               const int (&ops)[K], int sum_lo = 0, int ns = 0, int or_lo = 0,
-                                              int no = 0, bool local = false) {
+                                              int no = 0, bool local = false, unsigned long long* sp = nullptr) {
   static_assert(K <= G_NS, "too many values");
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
   int32_t r[K];
@@ -325,23 +356,28 @@ __device__ __forceinline__ bool spread_reduce(SpreadHdr& H, int32_t* xs, int W, 
     for (int k = 0; k < K; k++) H.red[wave][k] = r[k];
   }
   lds_barrier();
-  if (threadIdx.x < K) {
-    const int k = threadIdx.x;
-    int op = OP_SUM;
+  if (sp && threadIdx.x == 0) sp[0] = wall_clock64();
+  const bool xchg = W > 1 && !local;
+  if (!xchg) {
+    if (threadIdx.x < K) {
+      const int k = threadIdx.x;
+      int op = OP_SUM;
 #pragma unroll
-    for (int q = 0; q < K; q++)
-      if (q == k) op = ops[q];
-    int32_t r = H.red[0][k];
-    for (int x = 1; x < nw; x++) r = op32(op, r, H.red[x][k]);
-    xs[k] = r;
-  }
-  lds_barrier();
-  if (W > 1 && !local) {
+      for (int q = 0; q < K; q++)
+        if (q == k) op = ops[q];
+      int32_t r = H.red[0][k];
+      for (int x = 1; x < nw; x++) r = op32(op, r, H.red[x][k]);
+      xs[k] = r;
+    }
+    lds_barrier();
+  } else {
     unsigned opbits = 0;
 #pragma unroll
     for (int k = 0; k < K; k++) opbits |= (unsigned)ops[k] << (2 * k);
     ++epoch;
-    if (wave == 0) spread_exchange(H, xs, gran, W, w, epoch, err, K, opbits, sum_lo, ns, or_lo, no);
+    if (sp && threadIdx.x == 0) sp[1] = wall_clock64();
+    if (wave == 0) spread_exchange(H, xs, gran, W, w, epoch, err, K, opbits, sum_lo, ns, or_lo, no, sp);
+    if (sp && threadIdx.x == 0) sp[4] = wall_clock64();
     lds_barrier();
     if (H.abort) return false;
   }
@@ -367,11 +403,11 @@ __device__ __forceinline__ bool spread_argmax(SpreadHdr& H, int W, int w, unsign
   ++epoch;
   if (wave == 0) {
     const unsigned long long tag = (unsigned long long)epoch << 32;
-    unsigned long long* mine = gran + ((size_t)(epoch & 1) * W + w) * G_XW;
+    KSS_GLOBAL unsigned long long* mine = gp(gran) + ((size_t)(epoch & 1) * W + w) * G_XW;
     if (lane < 2)
       __hip_atomic_store(mine + lane, tag | (lane ? (uint32_t)((unsigned long long)best >> 32) : (uint32_t)best),
                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const unsigned long long* base = gran + (size_t)(epoch & 1) * W * G_XW;
+    KSS_GLOBAL const unsigned long long* base = gp(gran) + (size_t)(epoch & 1) * W * G_XW;
     long long m = 0;
     for (int c0 = 0; c0 < W; c0 += 64) {
       const int s = c0 + lane;
@@ -385,7 +421,7 @@ __device__ __forceinline__ bool spread_argmax(SpreadHdr& H, int W, int w, unsign
         if (spins >= SPIN_LIMIT) {
           if (lane == 0) {
             H.abort = 1;
-            __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(gp(err), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           }
           break;
         }
@@ -772,7 +808,8 @@ __device__ __forceinline__ void spread_schedule(DevCluster c, const GPod* __rest
       const int op[13] = {OP_SUM, OP_SUM, OP_MAX, OP_MAX, OP_MIN, OP_MAX, OP_OR, OP_SUM, OP_SUM, OP_SUM, OP_SUM,
                           OP_MIN, OP_MAX};
       if (!spread_reduce(H, L.xs, W, w, epoch, gran, err, v, op, 0, 0, q.total_bins + q.hard_pbins,
-                         q.total_pbins - q.hard_pbins))
+                         q.total_pbins - q.hard_pbins, false,
+                         stl && k - k0 < G_NSTAMP ? stl + (k - k0) * 16 + 10 : nullptr))
         return;
       nf = v[0];
       nign = v[1];

@@ -47,6 +47,8 @@ def summarise(path):
         a = a.reshape(w, NSTAMP_PODS // 2, 16)
         if kind == 2:
             lines.append(spread_summary(w, a))
+            if (a[0, :, 14] > 0).any():
+                lines.append(spread_e2_detail(w, a))
             continue
         s0 = a[0]
         ok = (s0[:, 0] > 0) & (s0[:, 6] > 0)
@@ -94,6 +96,18 @@ def spread_summary(w, a):
         line += (f"\n  {name} ({used.sum()} pods): publish spread median {np.median(skew):.2f} us,"
                  f" last publish -> done median {np.median(after):.2f} us (min over shards {np.median(after.min(axis=0)):.2f})")
     return line
+
+
+def spread_e2_detail(w, a):
+    """E2 internals (slots 10-14 of shard 0): wave reduce + barrier, combine + barrier,
+    publish, sweep done, fold + atomics (exchange return)."""
+    s = a[0]
+    ok = (s[:, 3] > 0) & (s[:, 14] > 0) & (s[:, 4] > 0)
+    s = s[ok]
+    seq = np.stack([s[:, 3], s[:, 10], s[:, 11], s[:, 12], s[:, 13], s[:, 14], s[:, 4]], axis=1)
+    d = np.diff(seq, axis=1) / 100.0
+    names = ["wave_red+bar", "combine+bar", "publish", "sweep", "fold+atomic", "bar+read"]
+    return "  E2 detail (shard 0): " + " ".join(f"{n}={m:.2f}" for n, m in zip(names, np.median(d, axis=0)))
 
 
 if __name__ == "__main__":
