@@ -640,10 +640,21 @@ bool build_gpods(const kss_podset* ps, int n_scalar, int n_classes, const int32_
       d.off = d.poff = -1;
       d.mode = SOFT_HOST;
     }
+    // groups: constraints of one kind on one topology key share the leader's bins (v1.26
+    // keys the counts by topology pair; kss_spread.cuh GSpread)
+    auto leader = [&](int c, int lo_c) {
+      for (int j = lo_c; j < c; j++)
+        if (g.sp[j].key == g.sp[c].key) return j;
+      return c;
+    };
     for (int c = 0; c < p.n_hard; c++) {  // make_plan: hard bins first
       GSpread& d = g.sp[c];
       stats = true;
-      if (!(key_flags[d.key] & KSS_KEY_UNIQUE)) {
+      d.own = (int16_t)leader(c, 0);
+      if (d.own != c) {
+        d.off = g.sp[d.own].off;
+        d.poff = g.sp[d.own].poff;
+      } else if (!(key_flags[d.key] & KSS_KEY_UNIQUE)) {
         d.off = (int16_t)off;
         d.poff = (int16_t)poff;
         off += d.nb;
@@ -653,17 +664,24 @@ bool build_gpods(const kss_podset* ps, int n_scalar, int n_classes, const int32_
     g.hard_pbins = poff;
     for (int c = p.n_hard; c < p.n_hard + p.n_soft; c++) {
       GSpread& d = g.sp[c];
-      if (key_flags[d.key] & KSS_KEY_HOSTNAME) {
+      const bool host = (key_flags[d.key] & KSS_KEY_HOSTNAME) != 0;
+      d.own = (int16_t)(host ? c : leader(c, p.n_hard));  // hostname constraints are never grouped
+      if (host) {
         d.mode = SOFT_HOST;
       } else if (key_flags[d.key] & KSS_KEY_UNIQUE) {
         d.mode = SOFT_DIRECT;
       } else {
         d.mode = SOFT_HIST;
-        d.off = (int16_t)off;
-        d.poff = (int16_t)poff;
-        off += d.nb;
-        poff += d.nb;
         stats = true;
+        if (d.own != c) {
+          d.off = g.sp[d.own].off;
+          d.poff = g.sp[d.own].poff;
+        } else {
+          d.off = (int16_t)off;
+          d.poff = (int16_t)poff;
+          off += d.nb;
+          poff += d.nb;
+        }
       }
       if (p.n_soft > 1) {
         need.max_soft = std::max(need.max_soft, (int)p.n_soft);
@@ -727,6 +745,7 @@ bool build_gpods(const kss_podset* ps, int n_scalar, int n_classes, const int32_
     g.total_pbins = poff;
     g.need_stats = stats ? 1 : 0;
     if (off + poff > LDS_BINS || off > 32767 || poff > 32767) return gfail(need, GP_BINS, i);
+    // exchanges: E1 (scalars + bins), E2 (scalars + soft presence)
     if (MAXH + 1 + off + g.hard_pbins > G_XW || 13 + (poff - g.hard_pbins) > G_XW) return gfail(need, GP_XW, i);
     need.bins_cap = std::max(need.bins_cap, off + poff);
     // AssumePod's count rows: the pod's class, its own term rows
@@ -1559,6 +1578,17 @@ static int run_single(kss_ctx* ctx, const PlanNeeds& need, const DevPods& dp, in
     g2.threads = KSS_MAX_THREADS;
     g2.npt = (per + KSS_MAX_THREADS - 1) / KSS_MAX_THREADS;
     if (spread_fits(g2, ctx->gneed, ctx->dc.n_keys, n_res)) {
+      g = g2;
+      spread = true;
+    }
+  }
+  // more shards when the resident count rows of a shard exceed its LDS (not when the caller
+  // fixed the shard count)
+  for (int W2 = g.W * 2; spread_ok && !spread && ctx->force_w <= 0 && !(flags & KSS_SCHED_FORCE_SINGLE_WG) &&
+                         W2 <= ctx->n_cu && W2 <= (int)N;
+       W2 *= 2) {
+    Geometry g2;
+    if (pick_geometry((int)N, W2, ctx->pref_threads, g2) && spread_fits(g2, ctx->gneed, ctx->dc.n_keys, n_res)) {
       g = g2;
       spread = true;
     }

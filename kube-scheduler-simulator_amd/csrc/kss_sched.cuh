@@ -53,8 +53,13 @@ enum { OP_SUM = 0, OP_MAX = 1, OP_MIN = 2, OP_OR = 3 };
 enum { SOFT_HOST = 0, SOFT_DIRECT = 1, SOFT_HIST = 2 };
 
 // Per-pod plan, identical in every lane (computed from wave-uniform pod data).
+// Constraints of one kind on one topology key form a group led by its first member (v1.26
+// keys PodTopologySpread's counts by topology pair; kss_spread.cuh GSpread): hard_own /
+// soft_own index the leader, whose bins the members share.
 struct Plan {
   int n_hard, n_soft, n_keys;
+  int hard_own[MAXH];
+  int soft_own[MAXS];  // hostname constraints lead themselves (never grouped)
   int hard_off[MAXH];  // bin offset, -1 = unique key (direct)
   int hard_poff[MAXH]; // presence offset of the pair (key, domain)
   int soft_mode[MAXS];
@@ -270,7 +275,17 @@ __device__ __forceinline__ bool make_plan(const DevCluster& c, const DevPods& P,
   for (int i = 0; i < p.n_hard; i++) {
     const int key = sp[i].key;
     pl.need_stats = true;
-    if (key_unique(c, key)) {
+    int o = i;
+    for (int j = 0; j < i; j++)
+      if (sp[j].key == key) {
+        o = j;
+        break;
+      }
+    pl.hard_own[i] = o;
+    if (o != i) {
+      pl.hard_off[i] = pl.hard_off[o];
+      pl.hard_poff[i] = pl.hard_poff[o];
+    } else if (key_unique(c, key)) {
       pl.hard_off[i] = -1;
       pl.hard_poff[i] = -1;
     } else {
@@ -283,17 +298,30 @@ __device__ __forceinline__ bool make_plan(const DevCluster& c, const DevPods& P,
   pl.hard_pbins = poff;
   for (int i = 0; i < p.n_soft; i++) {
     const int key = sp[p.n_hard + i].key;
+    int o = i;
+    if (!(c.key_flags[key] & KSS_KEY_HOSTNAME))
+      for (int j = 0; j < i; j++)
+        if (sp[p.n_hard + j].key == key) {
+          o = j;
+          break;
+        }
+    pl.soft_own[i] = o;
     if (c.key_flags[key] & KSS_KEY_HOSTNAME) {
       pl.soft_mode[i] = SOFT_HOST;
     } else if (key_unique(c, key)) {
       pl.soft_mode[i] = SOFT_DIRECT;
     } else {
       pl.soft_mode[i] = SOFT_HIST;
-      pl.soft_off[i] = off;
-      pl.soft_poff[i] = poff;
-      off += c.key_card[key] + 1;
-      poff += c.key_card[key] + 1;
       pl.need_stats = true;
+      if (o != i) {
+        pl.soft_off[i] = pl.soft_off[o];
+        pl.soft_poff[i] = pl.soft_poff[o];
+      } else {
+        pl.soft_off[i] = off;
+        pl.soft_poff[i] = poff;
+        off += c.key_card[key] + 1;
+        poff += c.key_card[key] + 1;
+      }
     }
   }
   const kss_ipa* ip = P.ipa + p.ipa_off;
@@ -355,11 +383,12 @@ __device__ __forceinline__ void stats_node(const DevCluster& c, const DevPods& P
                                            long long& flags) {
   const kss_spread* sp = P.spreads + p.spread_off;
   if (p.n_hard > 0 && has_keys(c, sp, p.n_hard, n)) {  // nodeLabelsMatchSpreadConstraints
-#pragma unroll
-    for (int i = 0; i < MAXH; i++) {
-      if (i >= p.n_hard) break;
-      if (!spread_policy_ok(c, P, p, sp[i], n)) continue;
-      const int64_t cnt = spread_count(c, P, sp[i], n);
+    for (int i = 0; i < p.n_hard; i++) {
+      if (pl.hard_own[i] != i) continue;
+      int64_t cnt = -1;  // tpCounts[pair]: the count of the group's last member admitting n
+      for (int j = i; j < p.n_hard; j++)
+        if (pl.hard_own[j] == i && spread_policy_ok(c, P, p, sp[j], n)) cnt = spread_count(c, P, sp[j], n);
+      if (cnt < 0) continue;
       if (pl.hard_off[i] < 0) {
         hard_min[i] = cnt < hard_min[i] ? cnt : hard_min[i];
       } else {
@@ -431,18 +460,18 @@ __device__ __forceinline__ int64_t ipa_value(const DevCluster& c, const DevPods&
 __device__ __forceinline__ int filter_pts(const DevCluster& c, const DevPods& P, const kss_pod& p, const Plan& pl,
                                           const long long* bins, const long long (&hard_min)[MAXH], int n) {
   const kss_spread* sp = P.spreads + p.spread_off;
-#pragma unroll
-  for (int i = 0; i < MAXH; i++) {
-    if (i >= p.n_hard) break;
+  for (int i = 0; i < p.n_hard; i++) {
     const int d = label_of(c, sp[i].key, n);
     if (d < 0) return 1 + KSS_PTS_MISSING_LABEL;
-    int64_t match;
+    const int o = pl.hard_own[i];
+    int64_t match = 0;  // TpPairToMatchNum[(key, value)]
     if (pl.hard_off[i] >= 0) {
       match = bins[pl.hard_off[i] + d];
-    } else {
-      match = (has_keys(c, sp, p.n_hard, n) && spread_policy_ok(c, P, p, sp[i], n)) ? spread_count(c, P, sp[i], n) : 0;
+    } else if (has_keys(c, sp, p.n_hard, n)) {  // a node-valued key: the node's own group count
+      for (int j = o; j < p.n_hard; j++)
+        if (pl.hard_own[j] == o && spread_policy_ok(c, P, p, sp[j], n)) match = spread_count(c, P, sp[j], n);
     }
-    const int64_t skew = match + (int64_t)sp[i].self_match - hard_min[i];
+    const int64_t skew = match + (int64_t)sp[i].self_match - hard_min[o];
     if (skew > (int64_t)sp[i].max_skew) return 1 + KSS_PTS_CONSTRAINTS_NOT_MATCH;
   }
   return 0;
@@ -632,7 +661,7 @@ __device__ __forceinline__ bool schedule_pod(const DevCluster& c, const DevPods&
 #pragma unroll
     for (int i = 0; i < MAXH; i++) {
       if (i >= p.n_hard) break;
-      if (pl.hard_off[i] < 0) continue;
+      if (pl.hard_off[i] < 0 || pl.hard_own[i] != i) continue;
       any_hist = true;
       const int nb = c.key_card[sp[i].key] + 1;
       for (int b = tid; b < nb; b += nt) {
@@ -794,7 +823,7 @@ __device__ __forceinline__ bool schedule_pod(const DevCluster& c, const DevPods&
 #pragma unroll
     for (int i = 0; i < MAXS; i++) {
       if (i >= p.n_soft) break;
-      if (pl.soft_mode[i] != SOFT_HIST) continue;
+      if (pl.soft_mode[i] != SOFT_HIST || pl.soft_own[i] != i) continue;
       const int nb = c.key_card[soft[i].key] + 1;
       for (int b = tid; b < nb; b += nt) sz[i] += pres[pl.soft_poff[i] + b] ? 1 : 0;
     }
@@ -802,8 +831,9 @@ __device__ __forceinline__ bool schedule_pod(const DevCluster& c, const DevPods&
 #pragma unroll
     for (int i = 0; i < MAXS; i++) {
       if (i >= p.n_soft) break;
-      long long size;
+      long long size;  // topoSize: a group's domains count for its leader only
       if (pl.soft_mode[i] == SOFT_HOST) size = nf - nign;
+      else if (pl.soft_own[i] != i) size = 0;
       else if (pl.soft_mode[i] == SOFT_DIRECT) size = sdirect[i] + ((smissing >> i) & 1);
       else size = sz[i];
       KSS_DCHECK(size >= 0 && size <= c.N + 2, "log_table size", size, c.N);
@@ -823,10 +853,16 @@ __device__ __forceinline__ bool schedule_pod(const DevCluster& c, const DevPods&
           if (i >= p.n_soft) break;
           const int d = label_of(c, soft[i].key, n);
           if (d < 0) continue;
-          int64_t cnt;
-          if (pl.soft_mode[i] == SOFT_HOST) cnt = spread_count(c, P, soft[i], n);
-          else if (pl.soft_mode[i] == SOFT_DIRECT) cnt = spread_policy_ok(c, P, p, soft[i], n) ? spread_count(c, P, soft[i], n) : 0;
-          else cnt = bins[pl.soft_off[i] + d];
+          int64_t cnt = 0;
+          if (pl.soft_mode[i] == SOFT_HOST) {
+            cnt = spread_count(c, P, soft[i], n);
+          } else if (pl.soft_mode[i] == SOFT_DIRECT) {  // the node's pair counter: every admitting member
+            for (int j = 0; j < p.n_soft; j++)
+              if (pl.soft_own[j] == pl.soft_own[i] && spread_policy_ok(c, P, p, soft[j], n))
+                cnt += spread_count(c, P, soft[j], n);
+          } else {
+            cnt = bins[pl.soft_off[i] + d];
+          }
           const double a = (double)cnt * w[i];
           s = s + (a + (double)(soft[i].max_skew - 1));  // scoreForCount
         }

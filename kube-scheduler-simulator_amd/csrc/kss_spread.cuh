@@ -39,6 +39,14 @@ constexpr int G_SCORE = 3;   // GIpa.kind of a merged InterPodAffinity score ent
 constexpr int G_NSTAMP = KSS_NSTAMP_PODS / 2;  // pods with diagnostic phase stamps, 16 per pod
 constexpr size_t G_STAMP_LDS = 8 * 16 * (size_t)G_NSTAMP;
 
+// One topology spread constraint.  v1.26 keys PodTopologySpread's counts by topology pair,
+// not by constraint: constraints of one kind on one key form a group led by its first member
+// (`own`), which holds the group's histogram (members share off / poff).  DoNotSchedule: per
+// node the count of the group's LAST member admitting the node (calPreFilterState's
+// tpCounts[pair] = count overwrites).  ScheduleAnyway, non-hostname keys: the pair counter
+// sums every admitting member's count, and the domain count (topoSize) belongs to the
+// leader, the others weigh log(0 + 2) (initPreScoreState).  Hostname soft constraints are
+// never grouped (their counts are per node and per constraint in Score).
 struct GSpread {
   int32_t max_skew;
   int16_t key, flags, self_match, mode;  // kss_spread; mode: SOFT_HOST / SOFT_DIRECT / SOFT_HIST
@@ -46,6 +54,8 @@ struct GSpread {
   int16_t off, poff;                     // histogram / presence bin offsets (-1: node-valued key)
   int16_t empty;                         // key_empty: domain of a node without the key
   int16_t nb;                            // domains of the key + 1
+  int16_t own;                           // the group leader's index in GPod::sp
+  int16_t pad[3];
 };
 struct GIpa {
   int16_t kind, key, ri_off, ri_len, slot, pad;  // kind: KSS_IPA_* (score entries: G_SCORE)
@@ -337,14 +347,34 @@ __device__ __forceinline__ bool spread_exchange(SpreadHdr& H, int32_t* xs, unsig
   return true;
 }
 
+// Wave 0, once the cluster bins are final: criticalPaths[0] of pod q's histogram-valued
+// DoNotSchedule groups — the minimum over the present domains, into the scalar xs[i].
+__device__ __forceinline__ void hard_minima(const GPod& q, int32_t* xs) {
+  const int lane = threadIdx.x & 63;
+  const int32_t* bins = xs + G_NS;
+  for (int i = 0; i < q.n_hard; i++) {
+    const GSpread& sp = q.sp[i];
+    if (sp.off < 0 || sp.own != i) continue;
+    int32_t m[1] = {INT32_MAX};
+    for (int b = lane; b < sp.nb; b += 64)
+      if (bins[q.total_bins + sp.poff + b]) m[0] = min(m[0], bins[sp.off + b]);
+    const int op[1] = {OP_MIN};
+    wave_red32(m, op);
+    if (lane == 0) xs[i] = min(xs[i], m[0]);
+  }
+}
+
 // Cluster reduction of K int32 scalars v[] (ops[]), plus (W > 1) the cross-shard SUM of
 // bins [sum_lo, sum_lo + ns) and OR of [or_lo, or_lo + no) of xs.  local: workgroup only.
-// LDS-only barriers (the prefetch waves' HBM loads stay in flight).  False on abort.
+// minima_q: the exchange wave then folds pod minima_q's critical-path minima into v (the
+// statistics exchange).  LDS-only barriers (the prefetch waves' HBM loads stay in flight).
+// False on abort.
 template <int K>
 __device__ __forceinline__ bool spread_reduce(SpreadHdr& H, int32_t* xs, int W, int w, unsigned& epoch,
                                               unsigned long long* gran, int* err, int32_t (&v)[K],
                                               const int (&ops)[K], int sum_lo = 0, int ns = 0, int or_lo = 0,
-                                              int no = 0, bool local = false, unsigned long long* sp = nullptr) {
+                                              int no = 0, bool local = false, unsigned long long* sp = nullptr,
+                                              const GPod* minima_q = nullptr) {
   static_assert(K <= G_NS, "too many values");
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
   int32_t r[K];
@@ -369,6 +399,7 @@ __device__ __forceinline__ bool spread_reduce(SpreadHdr& H, int32_t* xs, int W, 
       for (int x = 1; x < nw; x++) r = op32(op, r, H.red[x][k]);
       xs[k] = r;
     }
+    if (minima_q && wave == 0) hard_minima(*minima_q, xs);
     lds_barrier();
   } else {
     unsigned opbits = 0;
@@ -376,7 +407,9 @@ __device__ __forceinline__ bool spread_reduce(SpreadHdr& H, int32_t* xs, int W, 
     for (int k = 0; k < K; k++) opbits |= (unsigned)ops[k] << (2 * k);
     ++epoch;
     if (sp && threadIdx.x == 0) sp[1] = wall_clock64();
-    if (wave == 0) spread_exchange(H, xs, gran, W, w, epoch, err, K, opbits, sum_lo, ns, or_lo, no, sp);
+    if (wave == 0 && spread_exchange(H, xs, gran, W, w, epoch, err, K, opbits, sum_lo, ns, or_lo, no, sp) &&
+        minima_q)
+      hard_minima(*minima_q, xs);
     if (sp && threadIdx.x == 0) sp[4] = wall_clock64();
     lds_barrier();
     if (H.abort) return false;
@@ -439,6 +472,71 @@ __device__ __forceinline__ bool spread_argmax(SpreadHdr& H, int W, int w, unsign
   return true;
 }
 
+// The statistics of node slot s for pod q, accumulated into bins (SUM) / bins + total_bins
+// (presence) and hmin / flags: PodTopologySpread calPreFilterState over the DoNotSchedule
+// groups, the ScheduleAnyway pair counters (PreScore processAllNode), InterPodAffinity
+// PreFilter counts (flags bit0 existing anti, bit1 affinity, bit2 anti) and PreScore
+// topologyScore (bit3 non-empty).
+__device__ __forceinline__ void stats_node(const SpreadShard& L, const GPod& q, int s, uint32_t wd, int32_t* bins,
+                                           int32_t (&hmin)[MAXH], int32_t& flags) {
+  const int cap = L.cap;
+  if (q.n_hard > 0 && g_has_keys(L, q.sp, q.n_hard, s)) {  // nodeLabelsMatchSpreadConstraints
+    for (int i = 0; i < q.n_hard; i++) {
+      const GSpread& sp = q.sp[i];
+      if (sp.own != i) continue;
+      int32_t eff = -1;  // tpCounts[pair]: the count of the group's last member admitting s
+      for (int j = i; j < q.n_hard; j++) {
+        const GSpread& m = q.sp[j];
+        if (m.own == i && g_policy(m, wd)) eff = g_sum(L, q, m.ri_off, m.ri_len, s);
+      }
+      if (eff < 0) continue;
+      if (sp.off < 0) {
+        hmin[i] = min(hmin[i], eff);
+      } else {
+        const int d = L.lbl[sp.key * cap + s];
+        atomicAdd(&bins[sp.off + d], eff);
+        bins[q.total_bins + sp.poff + d] = 1;  // the pair (key, value) exists
+      }
+    }
+  }
+  if (q.n_soft > 0) {
+    const GSpread* so = q.sp + q.n_hard;
+    if (!(q.pflags & KSS_POD_PTS_REQUIRE_ALL) || g_has_keys(L, so, q.n_soft, s)) {
+      for (int i = 0; i < q.n_soft; i++) {
+        const GSpread& sp = so[i];
+        if (sp.mode != SOFT_HIST || !g_policy(sp, wd)) continue;
+        int d = L.lbl[sp.key * cap + s];
+        if (d < 0) d = sp.empty;
+        const int32_t cnt = g_sum(L, q, sp.ri_off, sp.ri_len, s);  // a group's members share the bins
+        if (cnt) atomicAdd(&bins[sp.off + d], cnt);
+      }
+    }
+  }
+  if (q.n_ipa > 0) {
+    const bool has_labels = (L.r32[2 * cap + s] & KSS_NODE_HAS_LABELS) != 0;
+    for (int e = 0; e < q.n_ipa; e++) {
+      const GIpa& en = q.ipa[e];
+      const int d = L.lbl[en.key * cap + s];
+      if (d < 0) continue;
+      if (en.kind == G_SCORE) {
+        if (!has_labels) continue;
+        if (g_any(L, q, en.ri_off, en.ri_len, s)) flags |= 8;
+        const int ho = q.hoff[en.slot][3];
+        if (ho >= 0) {
+          const int32_t v = g_sum(L, q, en.ri_off, en.ri_len, s);
+          if (v) atomicAdd(&bins[ho + d], v);
+        }
+      } else {
+        const int32_t v = g_sum(L, q, en.ri_off, en.ri_len, s);
+        const int h = en.kind == KSS_IPA_EXISTING_ANTI ? 0 : (en.kind == KSS_IPA_REQ_AFFINITY ? 1 : 2);
+        if (v > 0) flags |= 1 << h;
+        const int ho = q.hoff[en.slot][h];
+        if (ho >= 0 && v) atomicAdd(&bins[ho + d], v);
+      }
+    }
+  }
+}
+
 // filter_pts / filter_ipa / ipa_score of kss_sched.cuh over the GPod and the LDS caches.
 __device__ __forceinline__ int g_filter_pts(const SpreadShard& L, const GPod& q, const int32_t* bins,
                                             const int32_t (&hard_min)[MAXH], int s, uint32_t w) {
@@ -446,10 +544,16 @@ __device__ __forceinline__ int g_filter_pts(const SpreadShard& L, const GPod& q,
     const GSpread& sp = q.sp[i];
     const int d = L.lbl[sp.key * L.cap + s];
     if (d < 0) return 1 + KSS_PTS_MISSING_LABEL;
-    int64_t match;
-    if (sp.off >= 0) match = bins[sp.off + d];
-    else match = (g_has_keys(L, q.sp, q.n_hard, s) && g_policy(sp, w)) ? g_sum(L, q, sp.ri_off, sp.ri_len, s) : 0;
-    const int64_t skew = match + (int64_t)sp.self_match - (int64_t)hard_min[i];
+    int64_t match = 0;  // TpPairToMatchNum[(key, value)]
+    if (sp.off >= 0) {
+      match = bins[sp.off + d];
+    } else if (g_has_keys(L, q.sp, q.n_hard, s)) {  // a node-valued key: the node's own group count
+      for (int j = sp.own; j < q.n_hard; j++) {
+        const GSpread& m = q.sp[j];
+        if (m.own == sp.own && g_policy(m, w)) match = g_sum(L, q, m.ri_off, m.ri_len, s);
+      }
+    }
+    const int64_t skew = match + (int64_t)sp.self_match - (int64_t)hard_min[sp.own];
     if (skew > (int64_t)sp.max_skew) return 1 + KSS_PTS_CONSTRAINTS_NOT_MATCH;
   }
   return 0;
@@ -635,88 +739,21 @@ __device__ __forceinline__ void spread_schedule(DevCluster c, const GPod* __rest
     if (evaluated && q.need_stats) {
       for (int b = tid; b < q.total_bins + q.total_pbins; b += nt) bins[b] = 0;
       lds_barrier();
-      for (int s = tid; s < own; s += nt) {
-        const uint32_t wd = sw[s];
-        if (q.n_hard > 0 && g_has_keys(L, q.sp, q.n_hard, s)) {  // nodeLabelsMatchSpreadConstraints
-          for (int i = 0; i < q.n_hard; i++) {
-            const GSpread& sp = q.sp[i];
-            if (!g_policy(sp, wd)) continue;
-            const int32_t cnt = g_sum(L, q, sp.ri_off, sp.ri_len, s);
-            if (sp.off < 0) {
-              hard_min[i] = cnt < hard_min[i] ? cnt : hard_min[i];
-            } else {
-              const int d = L.lbl[sp.key * cap + s];
-              atomicAdd(&bins[sp.off + d], cnt);
-              bins[q.total_bins + sp.poff + d] = 1;  // the pair (key, value) exists
-            }
-          }
-        }
-        if (q.n_soft > 0) {
-          const GSpread* so = q.sp + q.n_hard;
-          if (!(q.pflags & KSS_POD_PTS_REQUIRE_ALL) || g_has_keys(L, so, q.n_soft, s)) {
-            for (int i = 0; i < q.n_soft; i++) {
-              const GSpread& sp = so[i];
-              if (sp.mode != SOFT_HIST || !g_policy(sp, wd)) continue;
-              int d = L.lbl[sp.key * cap + s];
-              if (d < 0) d = sp.empty;
-              const int32_t cnt = g_sum(L, q, sp.ri_off, sp.ri_len, s);
-              if (cnt) atomicAdd(&bins[sp.off + d], cnt);
-            }
-          }
-        }
-        if (q.n_ipa > 0) {
-          const bool has_labels = (L.r32[2 * cap + s] & KSS_NODE_HAS_LABELS) != 0;
-          for (int e = 0; e < q.n_ipa; e++) {
-            const GIpa& en = q.ipa[e];
-            const int d = L.lbl[en.key * cap + s];
-            if (d < 0) continue;
-            if (en.kind == G_SCORE) {
-              if (!has_labels) continue;
-              if (g_any(L, q, en.ri_off, en.ri_len, s)) flags |= 8;
-              const int ho = q.hoff[en.slot][3];
-              if (ho >= 0) {
-                const int32_t v = g_sum(L, q, en.ri_off, en.ri_len, s);
-                if (v) atomicAdd(&bins[ho + d], v);
-              }
-            } else {
-              const int32_t v = g_sum(L, q, en.ri_off, en.ri_len, s);
-              const int h = en.kind == KSS_IPA_EXISTING_ANTI ? 0 : (en.kind == KSS_IPA_REQ_AFFINITY ? 1 : 2);
-              if (v > 0) flags |= 1 << h;
-              const int ho = q.hoff[en.slot][h];
-              if (ho >= 0 && v) atomicAdd(&bins[ho + d], v);
-            }
-          }
-        }
-      }
+      for (int s = tid; s < own; s += nt) stats_node(L, q, s, sw[s], bins, hard_min, flags);
       GSTAMP(1);
       int32_t v[MAXH + 1];
       const int op[MAXH + 1] = {OP_MIN, OP_MIN, OP_MIN, OP_MIN, OP_OR};
 #pragma unroll
       for (int i = 0; i < MAXH; i++) v[i] = hard_min[i];
       v[MAXH] = flags;
-      // histogram SUM over every bin, hard-pair presence OR (soft presence is filled later)
-      if (!spread_reduce(H, L.xs, W, w, epoch, gran, err, v, op, 0, q.total_bins, q.total_bins, q.hard_pbins)) return;
+      // histogram SUM over every bin, hard-pair presence OR (soft presence, still zero, is
+      // filled by the filter pass), then the critical-path minima
+      if (!spread_reduce(H, L.xs, W, w, epoch, gran, err, v, op, 0, q.total_bins, q.total_bins, q.hard_pbins, false,
+                         nullptr, &q))
+        return;
+#pragma unroll
+      for (int i = 0; i < MAXH; i++) hard_min[i] = v[i];
       flags = v[MAXH];
-      // criticalPaths: minimum over the present domains of histogram-valued hard keys
-      int32_t mm[MAXH];
-      bool any_hist = false;
-#pragma unroll
-      for (int i = 0; i < MAXH; i++) mm[i] = v[i];
-      for (int i = 0; i < q.n_hard; i++) {
-        const GSpread& sp = q.sp[i];
-        if (sp.off < 0) continue;
-        any_hist = true;
-        for (int b = tid; b < sp.nb; b += nt)
-          if (bins[q.total_bins + sp.poff + b]) mm[i] = min(mm[i], bins[sp.off + b]);
-      }
-      if (any_hist) {
-        const int opm[MAXH] = {OP_MIN, OP_MIN, OP_MIN, OP_MIN};
-        spread_reduce(H, L.xs, W, w, epoch, gran, err, mm, opm, 0, 0, 0, 0, /*local=*/true);
-      }
-#pragma unroll
-      for (int i = 0; i < MAXH; i++) hard_min[i] = mm[i];
-      for (int b = q.hard_pbins + tid; b < q.total_pbins; b += nt) bins[q.total_bins + b] = 0;
-      lds_barrier();
       GSTAMP(2);
     }
     // ---- filter + raw scores ----
@@ -839,15 +876,16 @@ __device__ __forceinline__ void spread_schedule(DevCluster c, const GPod* __rest
         int32_t sz[MAXS] = {0, 0, 0, 0};
         for (int i = 0; i < q.n_soft; i++) {
           const GSpread& sp = soft[i];
-          if (sp.mode != SOFT_HIST) continue;
+          if (sp.mode != SOFT_HIST || sp.own != q.n_hard + i) continue;
           for (int b = tid; b < sp.nb; b += nt) sz[i] += bins[q.total_bins + sp.poff + b] ? 1 : 0;
         }
         const int ops4[MAXS] = {OP_SUM, OP_SUM, OP_SUM, OP_SUM};
         spread_reduce(H, L.xs, W, w, epoch, gran, err, sz, ops4, 0, 0, 0, 0, /*local=*/true);
         for (int i = 0; i < q.n_soft; i++) {
           const GSpread& sp = soft[i];
-          long long size;
+          long long size;  // topoSize: a group's domains count for its leader only
           if (sp.mode == SOFT_HOST) size = nf - nign;
+          else if (sp.own != q.n_hard + i) size = 0;
           else if (sp.mode == SOFT_DIRECT) size = sdirect[i] + ((smissing >> i) & 1);
           else size = sz[i];
           wts[i] = go_log_dev((double)(size + 2));  // topologyNormalizingWeight
@@ -875,10 +913,16 @@ __device__ __forceinline__ void spread_schedule(DevCluster c, const GPod* __rest
                 const GSpread& sp = soft[i];
                 const int d = L.lbl[sp.key * cap + s];
                 if (d < 0) continue;
-                int64_t cnt;
-                if (sp.mode == SOFT_HOST) cnt = g_sum(L, q, sp.ri_off, sp.ri_len, s);
-                else if (sp.mode == SOFT_DIRECT) cnt = g_policy(sp, sw[s]) ? g_sum(L, q, sp.ri_off, sp.ri_len, s) : 0;
-                else cnt = bins[sp.off + d];
+                int64_t cnt = 0;
+                if (sp.mode == SOFT_HOST) {
+                  cnt = g_sum(L, q, sp.ri_off, sp.ri_len, s);
+                } else if (sp.mode == SOFT_DIRECT) {  // the node's pair counter: every admitting member
+                  for (int j = 0; j < q.n_soft; j++)
+                    if (soft[j].own == sp.own && g_policy(soft[j], sw[s]))
+                      cnt += g_sum(L, q, soft[j].ri_off, soft[j].ri_len, s);
+                } else {
+                  cnt = bins[sp.off + d];
+                }
                 const double a = (double)cnt * wts[i];
                 sc = sc + (a + (double)(sp.max_skew - 1));  // scoreForCount
               }

@@ -620,11 +620,15 @@ class Oracle:
             lb = _labels(ni.node)
             if not all(c["key"] in lb for c in cons):
                 continue
+            # tpCounts[pair] = count: constraints on one key overwrite each other per node
+            tp_counts: Dict[Tuple[str, str], int] = {}
             for c in cons:
                 if not self._inclusion_ok(c, pod, ni.node):
                     continue
                 pair = (c["key"], lb[c["key"]])
-                pair_num[pair] = pair_num.get(pair, 0) + self._count_match(ni, c["sel"], _ns(pod))
+                tp_counts[pair] = self._count_match(ni, c["sel"], _ns(pod))
+            for pair, cnt in tp_counts.items():
+                pair_num[pair] = pair_num.get(pair, 0) + cnt
         mins = {}
         for (k, v), num in pair_num.items():
             mins[k] = min(mins.get(k, 2**31 - 1), num)

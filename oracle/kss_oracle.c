@@ -197,7 +197,9 @@ static int64_t sum_rows(const int32_t* mat, size_t N, const int32_t* rows, int l
 
 /* per-pod PreFilter / PreScore state for PodTopologySpread and InterPodAffinity */
 typedef struct {
-  /* PTS hard: per constraint, bins = card+1 */
+  /* PTS hard: per topology key (v1.26 keys TpPairToMatchNum by pair): the histogram and the
+     critical-path minimum live at the key's first constraint hard_own[i]; bins = card+1 */
+  int hard_own[8];
   int64_t* hard_cnt[8];
   uint8_t* hard_present[8];
   int64_t hard_min[8];
@@ -254,23 +256,38 @@ static int podstate_build(podstate* st, const kss_cluster* cl, const kss_podset*
   const kss_spread* hard = ps->spreads + p->spread_off;
   if (p->n_hard > 8 || p->n_soft > 8) return KSS_E_UNSUPPORTED;
   for (int i = 0; i < p->n_hard; i++) {
+    st->hard_own[i] = i;
+    for (int j = 0; j < i; j++)
+      if (hard[j].key == hard[i].key) {
+        st->hard_own[i] = j;
+        break;
+      }
+    if (st->hard_own[i] != i) continue;
     int bins = cl->key_card[hard[i].key] + 1;
     st->hard_cnt[i] = (int64_t*)calloc((size_t)bins, sizeof(int64_t));
     st->hard_present[i] = (uint8_t*)calloc((size_t)bins, 1);
   }
   for (size_t n = 0; n < N; n++) {
     if (!has_all_keys(cl, hard, p->n_hard, (int)n)) continue; /* nodeLabelsMatchSpreadConstraints */
+    /* tpCounts[pair] = count for each admitting constraint in order: per key, the count of the
+       key's LAST constraint that admits the node (matchNodeInclusionPolicies) */
     for (int i = 0; i < p->n_hard; i++) {
-      if (!spread_policy_ok(cl, ps, p, &hard[i], (int)n)) continue;
+      if (st->hard_own[i] != i) continue;
+      int64_t eff = -1;
+      for (int j = i; j < p->n_hard; j++) {
+        if (st->hard_own[j] != i || !spread_policy_ok(cl, ps, p, &hard[j], (int)n)) continue;
+        /* countPodsMatchSelector(nodeInfo.Pods, selector, pod.Namespace) */
+        eff = sum_rows(cl->class_count, N, ps->ints + hard[j].cls_off, hard[j].cls_len, (int)n);
+      }
+      if (eff < 0) continue;
       int d = LV(cl, hard[i].key, n);
-      /* countPodsMatchSelector(nodeInfo.Pods, selector, pod.Namespace) */
-      int64_t c = sum_rows(cl->class_count, N, ps->ints + hard[i].cls_off, hard[i].cls_len, (int)n);
-      st->hard_cnt[i][d] += c;
+      st->hard_cnt[i][d] += eff; /* TpPairToMatchNum[tp] += count */
       st->hard_present[i][d] = 1;
     }
   }
   for (int i = 0; i < p->n_hard; i++) {
-    /* criticalPaths[0].MatchNum: global minimum over existing pairs, MaxInt32 if none */
+    if (st->hard_own[i] != i) continue;
+    /* TpKeyToCriticalPaths[key] paths[0].MatchNum: minimum over the key's pairs, MaxInt32 if none */
     int64_t mn = INT32_MAX;
     int bins = cl->key_card[hard[i].key] + 1;
     for (int d = 0; d < bins; d++)
@@ -404,8 +421,9 @@ static int filter_node(const kss_profile* prof, const kss_cluster* cl, const kss
         *detail = KSS_PTS_MISSING_LABEL;
         return KSS_F_POD_TOPOLOGY_SPREAD;
       }
-      int64_t match = st->hard_present[i][d] ? st->hard_cnt[i][d] : 0;
-      int64_t skew = match + (int64_t)hard[i].self_match - st->hard_min[i];
+      const int o = st->hard_own[i];
+      int64_t match = st->hard_present[o][d] ? st->hard_cnt[o][d] : 0;
+      int64_t skew = match + (int64_t)hard[i].self_match - st->hard_min[o];
       if (skew > (int64_t)hard[i].max_skew) {
         *detail = KSS_PTS_CONSTRAINTS_NOT_MATCH;
         return KSS_F_POD_TOPOLOGY_SPREAD;
@@ -649,15 +667,26 @@ static int schedule_one(const kss_profile* prof, ostate* s, const kss_podset* ps
       nignored++;
     }
   }
+  /* TopologyPairToPodCounts is keyed by pair: constraints on one (non-hostname) key share the
+     counters of the key's first constraint sown[c], which also owns every pair in topoSize
+     (the later ones find the pair created and count 0 domains) */
+  int sown[8];
   for (int c = 0; c < p->n_soft; c++) {
     int key = soft[c].key;
-    int bins = cl->key_card[key] + 1;
-    soft_cnt[c] = (int64_t*)calloc((size_t)bins, sizeof(int64_t));
-    soft_present[c] = (uint8_t*)calloc((size_t)bins, 1);
+    sown[c] = c;
+    if (!(cl->key_flags[key] & KSS_KEY_HOSTNAME))
+      for (int j = 0; j < c; j++)
+        if (soft[j].key == key) {
+          sown[c] = j;
+          break;
+        }
     int size = 0;
     if (cl->key_flags[key] & KSS_KEY_HOSTNAME) {
       size = nf - nignored;
-    } else {
+    } else if (sown[c] == c) {
+      int bins = cl->key_card[key] + 1;
+      soft_cnt[c] = (int64_t*)calloc((size_t)bins, sizeof(int64_t));
+      soft_present[c] = (uint8_t*)calloc((size_t)bins, 1);
       for (int i = 0; i < nf; i++) {
         int n = feas[i];
         if (ignored[n]) continue;
@@ -680,8 +709,9 @@ static int schedule_one(const kss_profile* prof, ostate* s, const kss_podset* ps
         if (!spread_policy_ok(cl, ps, p, &soft[c], n)) continue;
         int d = LV(cl, key, n);
         if (d < 0) d = cl->key_empty[key];
-        if (!soft_present[c][d]) continue; /* pair not associated with any candidate node */
-        soft_cnt[c][d] += sum_rows(cl->class_count, (size_t)N, ps->ints + soft[c].cls_off, soft[c].cls_len, n);
+        int o = sown[c];
+        if (!soft_present[o][d]) continue; /* pair not associated with any candidate node */
+        soft_cnt[o][d] += sum_rows(cl->class_count, (size_t)N, ps->ints + soft[c].cls_off, soft[c].cls_len, n);
       }
     }
   }
@@ -709,7 +739,7 @@ static int schedule_one(const kss_profile* prof, ostate* s, const kss_podset* ps
         if (cl->key_flags[key] & KSS_KEY_HOSTNAME)
           cnt = sum_rows(cl->class_count, NN, ps->ints + soft[c].cls_off, soft[c].cls_len, n);
         else
-          cnt = soft_cnt[c][d];
+          cnt = soft_cnt[sown[c]][d];
         sc += (double)cnt * w[c] + (double)(soft[c].max_skew - 1); /* scoreForCount */
       }
       pts = go_round_to_i64(sc);

@@ -15,8 +15,8 @@ one app selector), these mix per pod:
   * NoExecute / NoSchedule / PreferNoSchedule taints, tolerations, nodeSelector, required
     and preferred node affinity, spec.nodeName, a second namespace, small pod limits.
 
-Within one pod every constraint of one kind uses a distinct topology key (several
-constraints on one key are the open v1.26 same-key case, tested separately).
+A quarter of the pods with constraints also carry a second constraint of the same kind on
+a key they already use (v1.26 keys the counts by topology pair: test_spread_same_key.py).
 """
 import random
 from typing import Dict, List, Tuple
@@ -133,6 +133,10 @@ def _pending(j: int, r: random.Random, node_names: List[str]) -> dict:
         aff["nodeAffinity"] = na
     hard = r.sample([K_ZONE, K_RACK, K_HOST], r.choice([0, 0, 1, 1, 2]))
     soft = r.sample([K_ZONE, K_RACK, K_HOST, K_ITYPE], r.choice([0, 1, 1, 2, 3]))
+    if hard and r.random() < 0.25:  # a second DoNotSchedule constraint on a key already used
+        hard.append(r.choice(hard))
+    if soft and len(soft) < 4 and r.random() < 0.25:
+        soft.append(r.choice(soft))
     tsc = [_spread(r, k, True) for k in hard] + [_spread(r, k, False) for k in soft]
     r.shuffle(tsc)
     if tsc:

@@ -163,3 +163,55 @@ def test_device_go_log_matches_host_port():
         assert y[k] == L.kss_go_log_c(x[k]), (x[k], y[k])
     host = np.array([L.kss_go_log_c(v) for v in x[::101]])
     np.testing.assert_array_equal(y[::101], host)
+
+
+def test_same_key_fixture_both_kernels():
+    """The hand-derived v1.26 same-topology-key case (test_spread_same_key.py) on k_spread and,
+    with every per-node record, on k_schedule."""
+    import test_spread_same_key as sk
+    cc, cp, _ = compile_cluster(*sk.fixture())
+    prof = abi.default_profile()
+    ncl, nt = len(cc.classes), len(cc.terms)
+    chosen_o, res, st = oracle_c.schedule(prof, cc.as_struct(), cp.as_struct(), cp.n, cc.n_nodes, record=True,
+                                          threads=8, n_classes=ncl, n_terms=nt)
+    ctx = native.Context(prof, max_pods_record=cp.n)
+    ctx.load(cc.as_struct())
+    chosen = ctx.schedule_batch(cp.as_struct(), cp.n)
+    assert ctx.last_kernel() == "k_spread"
+    _check(ctx, res, st, chosen, chosen_o, cp.n, cc.n_nodes, ncl, nt)
+    ctx.reset()
+    chosen = ctx.schedule_batch(cp.as_struct(), cp.n, record=True)
+    assert ctx.last_kernel() == "k_schedule"
+    np.testing.assert_array_equal(chosen, chosen_o)
+    for j in range(cp.n):
+        r = ctx.fetch_record(j)
+        np.testing.assert_array_equal(r.fail_plugin[:cc.n_nodes], res.fail_plugin[j, :cc.n_nodes])
+        feas = res.fail_plugin[j, :cc.n_nodes] == 0
+        if res.meta(j)["scored"]:
+            np.testing.assert_array_equal(r.raw[:, :cc.n_nodes][:, feas], res.raw[j][:, :cc.n_nodes][:, feas])
+    ctx.close()
+
+
+@pytest.mark.parametrize("seed", [41, 42])
+def test_program_fuzz_records_on_k_schedule(seed):
+    """k_schedule with every per-node record on fuzzed programs (including same-key groups)."""
+    prof = abi.default_profile()
+    cc, cp = _fuzz(seed, 150, 120)
+    ncl, nt = len(cc.classes), len(cc.terms)
+    chosen_o, res, st = oracle_c.schedule(prof, cc.as_struct(), cp.as_struct(), cp.n, cc.n_nodes, record=True,
+                                          threads=8, n_classes=ncl, n_terms=nt)
+    ctx = native.Context(prof, max_pods_record=cp.n)
+    ctx.load(cc.as_struct())
+    chosen = ctx.schedule_batch(cp.as_struct(), cp.n, record=True, flags=abi.KSS_SCHED_FORCE_MULTI_WG)
+    np.testing.assert_array_equal(chosen, chosen_o)
+    for j in range(cp.n):
+        r = ctx.fetch_record(j)
+        m = res.meta(j)
+        assert (r.chosen, r.n_feasible, r.status) == (m["chosen"], m["n_feasible"], m["status"]), j
+        np.testing.assert_array_equal(r.fail_plugin[:cc.n_nodes], res.fail_plugin[j, :cc.n_nodes], err_msg=f"pod {j}")
+        if m["scored"]:
+            feas = res.fail_plugin[j, :cc.n_nodes] == 0
+            np.testing.assert_array_equal(r.raw[:, :cc.n_nodes][:, feas], res.raw[j][:, :cc.n_nodes][:, feas],
+                                          err_msg=f"pod {j}")
+            np.testing.assert_array_equal(r.total[:cc.n_nodes][feas], res.total[j, :cc.n_nodes][feas])
+    ctx.close()
