@@ -342,6 +342,93 @@ def run_node_axis(args):
         dist.destroy_process_group()
 
 
+def latency_profile(cfg, n_nodes, n_pods, seed, device):
+    """roofline.latency: the per-pod chain is latency-bound, so beside the HBM fraction the line
+    carries the phase breakdown of one stamped run (KSS_STAMPS_FILE: s_memrealtime per phase,
+    the first 128 pods, outside the timed region) and the measured exchange floor (per
+    exchange, the median over pods of the fastest shard's wait from the last publish to
+    completion).  bound_us_per_pod = exchanges per pod x floor."""
+    import tempfile
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "tools"))
+    import stamps
+    from kss import abi, native
+    path = os.path.join(tempfile.mkdtemp(prefix="kss_stamps_"), "stamps.bin")
+    os.environ["KSS_STAMPS_FILE"] = path
+    try:
+        s = native.Synth(cfg, seed, n_nodes, min(n_pods, 1000))
+        ctx = native.Context(abi.default_profile(), device=device)
+        ctx.load(s.cluster)
+        ctx.stage(s.pods)
+        ctx.run_staged(s.n_pods)
+        ctx.close()
+        s.close()
+    finally:
+        del os.environ["KSS_STAMPS_FILE"]
+    out = stamps.latency_summary(path)
+    floors = out.get("exchange_floor_us", {})
+    out["bound_us_per_pod"] = round(sum(floors.values()), 3)
+    out["source"] = "KSS_STAMPS_FILE phase stamps, shard 0 (floors: all shards), first 128 pods of a 1000-pod run"
+    return out
+
+
+def run_per_pod(args):
+    """The drop-in per-pod path as the Go plugin drives it: PreFilter ->
+    kss_eval_pod (the pod's program uploaded, every per-node record copied back in one
+    transfer), Reserve -> kss_commit (AssumePod from the kernel arguments), pod after pod on
+    the C2 cluster.  Reports the host-observed microseconds per call."""
+    import numpy as np
+    from kss import abi, native
+    from kss.synth import SEED_BASE
+    n_nodes = args.nodes or 5000
+    n_pods = args.pods or 500
+    s = native.Synth(2, SEED_BASE + 2, n_nodes, n_pods)
+    ctx = native.Context(abi.default_profile())
+    ctx.load(s.cluster)
+    for j in range(min(args.warmup * 20, n_pods)):  # warm the kernels, then restore the snapshot
+        r = ctx.eval_pod(s.pods, j)
+        if r.chosen >= 0:
+            ctx.commit(s.pods, j, r.chosen)
+    ctx.reset()
+    t_eval, t_commit, chosen = [], [], []
+    t0 = time.perf_counter()
+    for j in range(n_pods):
+        a = time.perf_counter()
+        r = ctx.eval_pod(s.pods, j)
+        b = time.perf_counter()
+        if r.chosen >= 0:
+            ctx.commit(s.pods, j, r.chosen)
+        c = time.perf_counter()
+        t_eval.append(b - a)
+        t_commit.append(c - b)
+        chosen.append(r.chosen)
+    elapsed = time.perf_counter() - t0
+    ev, cm = np.array(t_eval) * 1e6, np.array(t_commit) * 1e6
+    out = {
+        "metric": "per-pod API: kss_eval_pod + kss_commit latency (pods/sec in value)",
+        "value": n_pods / elapsed,
+        "unit": "pods/s",
+        "n_gpus": 1,
+        "steps": 1,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "int64/f64",
+        "data": "synthetic (SplitMix64 seed 0x5EED0002)",
+        "config": {"workload": f"C2 cluster, per-pod API: {n_nodes} nodes, {n_pods} pods one call pair each",
+                   "nodes": n_nodes, "pods": n_pods, "parallelism": "none"},
+        "eval_us": {"median": float(np.median(ev)), "mean": float(ev.mean()), "p90": float(np.percentile(ev, 90))},
+        "commit_us": {"median": float(np.median(cm)), "mean": float(cm.mean()), "p90": float(np.percentile(cm, 90))},
+        "eval_device_ms_last": ctx.last_timing()[0],
+        "geometry": ctx.last_geometry(),
+        "pods_scheduled": int(sum(1 for c in chosen if c >= 0)),
+    }
+    print(json.dumps(out), flush=True)
+    ctx.close()
+    s.close()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -358,9 +445,13 @@ def main():
                     help="C5 shape: this many independent what-if clusters per rank in one launch")
     ap.add_argument("--node-axis", action="store_true",
                     help="C4 shape: one cluster sharded along the node axis over the ranks (RCCL per pod)")
+    ap.add_argument("--per-pod", action="store_true", help="the drop-in per-pod API: kss_eval_pod + kss_commit")
+    ap.add_argument("--no-latency", action="store_true", help="skip the stamped latency-profile run")
     args = ap.parse_args()
     if args.inner:
-        args.no_cpu = args.no_traffic = True
+        args.no_cpu = args.no_traffic = args.no_latency = True
+    if args.per_pod:
+        return run_per_pod(args)
     if args.node_axis:
         return run_node_axis(args)
     if args.scenarios:
@@ -428,6 +519,11 @@ def main():
         if not args.no_cpu and world == 1:
             threads, _ = cpu_threads()
             cpu = cpu_baseline(cfg, n_nodes, n_pods, args.cpu_seconds, threads, seed=seed)
+        latency = None
+        if not args.no_latency and world == 1:
+            latency = latency_profile(cfg, n_nodes, n_pods, seed, local)
+            latency["us_per_pod"] = elapsed / args.steps / n_pods * 1e6
+            latency["frac"] = latency["bound_us_per_pod"] / latency["us_per_pod"]
         out = {
             "metric": "pod x node filter+score evals/sec (pods scheduled/sec in extra)",
             "value": value,
@@ -453,7 +549,7 @@ def main():
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": ctx.last_kernel(), "bytes_per_eval": B_EVAL[cfg],
                          "algorithmic_bytes_per_launch": B_EVAL[cfg] * n_pods * n_nodes,
-                         "traffic_detail": traffic_detail},
+                         "traffic_detail": traffic_detail, "latency": latency},
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)

@@ -326,16 +326,26 @@ void kss_destroy(kss_ctx* ctx);
 
 /* upload a snapshot (replaces any previous one) */
 int kss_load_cluster(kss_ctx* ctx, const kss_cluster* cl);
-/* NodeInfo-generation delta sync: overwrite rows idx[0..n) of the mutable columns */
+/* NodeInfo-generation delta sync: overwrite rows idx[0..n) of the mutable columns (one
+ * packed upload) */
 int kss_apply_node_delta(kss_ctx* ctx, const int32_t* idx, int32_t n, const int64_t* requested /*[n][KSS_NRES]*/,
                          const int64_t* nonzero /*[n][2]*/, const int32_t* pod_count /*[n]*/);
+/* The class / term count side of the same sync (a pod bound or deleted outside this
+ * scheduler, a re-listed node): count[row[i]][node[i]] += value[i] (mode 0) or = value[i]
+ * (mode 1).  row r < n_classes is class_count row r, otherwise term_count row r - n_classes.
+ * Replaces: the informer's NodeInfo.AddPod / RemovePod on the scheduler cache
+ * (simulator/scheduler/scheduler.go:66-104 starts the scheduler that keeps it). */
+int kss_apply_count_delta(kss_ctx* ctx, const int32_t* node, const int32_t* row, const int32_t* value, int32_t n,
+                          int32_t mode);
 /* read back the mutable columns (requested [KSS_NRES][N], nonzero [2][N], pod_count [N]) */
 int kss_read_node_state(kss_ctx* ctx, int64_t* requested, int64_t* nonzero, int32_t* pod_count,
                         int32_t* class_count /*[n_classes][N] or NULL*/, int32_t* term_count /*or NULL*/);
 
-/* evaluate one pod against the current snapshot (no commit): the PreFilter-time call */
+/* evaluate one pod against the current snapshot (no commit): the PreFilter-time call.  Only
+ * the pod's own program is uploaded; the record comes back in one copy. */
 int kss_eval_pod(kss_ctx* ctx, const kss_podset* ps, int32_t pod_index, kss_pod_result* out);
-/* commit pod ps.pods[pod_index] to node (AssumePod); rollback undoes it (Unreserve/ForgetPod) */
+/* commit pod ps.pods[pod_index] to node (AssumePod); rollback undoes it (Unreserve/ForgetPod).
+ * The deltas travel in the kernel's arguments (no upload). */
 int kss_commit(kss_ctx* ctx, const kss_podset* ps, int32_t pod_index, int32_t node);
 int kss_rollback(kss_ctx* ctx, const kss_podset* ps, int32_t pod_index, int32_t node);
 

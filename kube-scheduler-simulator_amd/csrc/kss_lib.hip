@@ -243,8 +243,47 @@ __global__ void k_go_log(const double* x, double* y, int n) {
   if (i < n) y[i] = go_log_dev(x[i]);
 }
 
-__global__ void k_commit(DevCluster c, DevPods P, int pi, int local, int sign) {
-  if (threadIdx.x == 0 && blockIdx.x == 0) commit_pod(c, P, P.pods[pi], local, sign);
+// AssumePod / ForgetPod deltas of one pod, carried in the kernel arguments (no upload).
+struct CommitArgs {
+  int64_t req[KSS_NRES];
+  int64_t nz[2];
+  int32_t cls, n_own, local, sign;
+  int32_t own[8];
+};
+
+__global__ void k_commit(DevCluster c, CommitArgs a) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  const size_t N = (size_t)c.N;
+  for (int r = 0; r < KSS_NRES; r++) c.requested[(size_t)r * N + a.local] += a.sign * a.req[r];
+  c.nonzero[a.local] += a.sign * a.nz[0];
+  c.nonzero[N + a.local] += a.sign * a.nz[1];
+  c.pod_count[a.local] += a.sign;
+  if (a.cls >= 0) c.class_count[(size_t)a.cls * N + a.local] += a.sign;
+  for (int i = 0; i < a.n_own; i++) c.term_count[(size_t)a.own[i] * N + a.local] += a.sign;
+}
+
+// Delta sync of node rows (kss_apply_node_delta): one packed upload, one scatter.
+__global__ void k_node_delta(DevCluster c, const int32_t* idx, const int64_t* req, const int64_t* nz, const int32_t* pc,
+                             int n) {
+  const int i = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+  if (i >= n) return;
+  const size_t N = (size_t)c.N;
+  const int r0 = idx[i];
+  for (int r = 0; r < KSS_NRES; r++) c.requested[(size_t)r * N + r0] = req[(size_t)i * KSS_NRES + r];
+  c.nonzero[r0] = nz[2 * (size_t)i];
+  c.nonzero[N + r0] = nz[2 * (size_t)i + 1];
+  c.pod_count[r0] = pc[i];
+}
+
+// Class / term count sync (kss_apply_count_delta): add (mode 0) or overwrite (mode 1).
+__global__ void k_count_delta(DevCluster c, const int32_t* node, const int32_t* row, const int32_t* val, int n, int mode) {
+  const int i = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+  if (i >= n) return;
+  const size_t N = (size_t)c.N;
+  int32_t* cell = row[i] < c.n_classes ? c.class_count + (size_t)row[i] * N + node[i]
+                                       : c.term_count + (size_t)(row[i] - c.n_classes) * N + node[i];
+  if (mode) *cell = val[i];
+  else atomicAdd(cell, val[i]);
 }
 
 // ---------------------------------------------------------------------------
@@ -351,6 +390,10 @@ struct kss_ctx {
   double cell_bound0 = 0;     // max single class_count / term_count entry of the loaded snapshot
   double cell_bound = 0;      // the same, plus every commit since
   DevBuf res_buf;             // GpodNeeds::res_rows on the device
+  DevBuf delta_buf;           // kss_apply_node_delta / kss_apply_count_delta staging on the device
+  std::vector<char> stage_host;  // packed host image of a delta upload
+  void* pinned = nullptr;     // kss_eval_pod's one-copy result staging (pinned)
+  size_t pinned_cap = 0;
   int staged_max_own = 0;     // max own term rows of a staged pod
   std::vector<int32_t> key_empty_h;
   bool no_simple = false;  // KSS_NO_SIMPLE: always launch k_schedule
@@ -1026,6 +1069,10 @@ void kss_destroy(kss_ctx* ctx) {
   ctx->gran_buf.release();
   ctx->err_buf.release();
   ctx->axis_cv.release();
+  ctx->gpod_buf.release();
+  ctx->res_buf.release();
+  ctx->delta_buf.release();
+  if (ctx->pinned) hipHostFree(ctx->pinned);
   for (hipEvent_t e : ctx->loop_ev) hipEventDestroy(e);
   if (ctx->ev0) hipEventDestroy(ctx->ev0);
   if (ctx->ev1) hipEventDestroy(ctx->ev1);
@@ -1236,21 +1283,80 @@ int kss_reset_node_state(kss_ctx* ctx) {
 int kss_apply_node_delta(kss_ctx* ctx, const int32_t* idx, int32_t n, const int64_t* requested, const int64_t* nonzero,
                          const int32_t* pod_count) {
   if (!ctx || !ctx->loaded) return fail(KSS_E_INVAL, "no cluster loaded");
+  if (n < 0 || (n > 0 && (!idx || !requested || !nonzero || !pod_count))) return fail(KSS_E_INVAL, "bad arguments");
+  if (n == 0) return 0;
+  for (int i = 0; i < n; i++)
+    if (idx[i] < 0 || idx[i] >= ctx->dc.N) return fail(KSS_E_INVAL, "delta row out of range");
   std::lock_guard<std::mutex> lk(ctx->mu);
   HIP_TRY(hipSetDevice(ctx->cfg.device));
-  const size_t N = (size_t)ctx->dc.N;
-  for (int i = 0; i < n; i++) {
-    const int r0 = idx[i];
-    if (r0 < 0 || (size_t)r0 >= N) return fail(KSS_E_INVAL, "delta row out of range");
-    for (int r = 0; r < KSS_NRES; r++)
-      HIP_TRY(hipMemcpyAsync(ctx->dc.requested + (size_t)r * N + r0, requested + (size_t)i * KSS_NRES + r, 8,
-                             hipMemcpyHostToDevice, ctx->stream));
-    for (int r = 0; r < 2; r++)
-      HIP_TRY(hipMemcpyAsync(ctx->dc.nonzero + (size_t)r * N + r0, nonzero + (size_t)i * 2 + r, 8, hipMemcpyHostToDevice,
-                             ctx->stream));
-    HIP_TRY(hipMemcpyAsync(ctx->dc.pod_count + r0, pod_count + i, 4, hipMemcpyHostToDevice, ctx->stream));
-  }
+  // one packed image: rows | requested | nonzero | pod counts
+  const size_t o_req = align_up(4 * (size_t)n, 16), o_nz = o_req + 8 * KSS_NRES * (size_t)n,
+               o_pc = o_nz + 16 * (size_t)n, total = o_pc + 4 * (size_t)n;
+  ctx->stage_host.resize(total);
+  char* h = ctx->stage_host.data();
+  std::memcpy(h, idx, 4 * (size_t)n);
+  std::memcpy(h + o_req, requested, 8 * KSS_NRES * (size_t)n);
+  std::memcpy(h + o_nz, nonzero, 16 * (size_t)n);
+  std::memcpy(h + o_pc, pod_count, 4 * (size_t)n);
+  int rc = ctx->delta_buf.ensure(total);
+  if (rc) return rc;
+  char* d = (char*)ctx->delta_buf.p;
+  HIP_TRY(hipMemcpyAsync(d, h, total, hipMemcpyHostToDevice, ctx->stream));
+  hipLaunchKernelGGL(k_node_delta, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, ctx->stream, ctx->dc,
+                     (const int32_t*)d, (const int64_t*)(d + o_req), (const int64_t*)(d + o_nz),
+                     (const int32_t*)(d + o_pc), n);
+  HIP_TRY(hipGetLastError());
   HIP_TRY(hipStreamSynchronize(ctx->stream));
+  // k_simple's exactness bounds track the largest requested / non-zero values
+  for (int i = 0; i < n; i++) {
+    for (int r = 0; r < 3; r++) {
+      const int64_t v = requested[(size_t)i * KSS_NRES + r];
+      ctx->f64_cluster.neg |= v < 0;
+      ctx->f64_cluster.max_req0 = std::max(ctx->f64_cluster.max_req0, (double)v);
+    }
+    for (int r = 0; r < 2; r++) {
+      const int64_t v = nonzero[(size_t)i * 2 + r];
+      ctx->f64_cluster.neg |= v < 0;
+      ctx->f64_cluster.max_nz0 = std::max(ctx->f64_cluster.max_nz0, (double)v);
+    }
+  }
+  return 0;
+}
+
+int kss_apply_count_delta(kss_ctx* ctx, const int32_t* node, const int32_t* row, const int32_t* value, int32_t n,
+                          int32_t mode) {
+  if (!ctx || !ctx->loaded) return fail(KSS_E_INVAL, "no cluster loaded");
+  if (n < 0 || (n > 0 && (!node || !row || !value)) || (mode != 0 && mode != 1)) return fail(KSS_E_INVAL, "bad arguments");
+  if (n == 0) return 0;
+  const int nc = ctx->host.n_classes, nt = ctx->host.n_terms;
+  double add = 0, top = 0;
+  for (int i = 0; i < n; i++) {
+    if (node[i] < 0 || node[i] >= ctx->dc.N) return fail(KSS_E_INVAL, "count delta node out of range");
+    if (row[i] < 0 || row[i] >= nc + nt) return fail(KSS_E_INVAL, "count delta row out of range");
+    if (mode == 1 && value[i] < 0) return fail(KSS_E_INVAL, "negative count");
+    add += std::max(0, value[i]);
+    top = std::max(top, (double)value[i]);
+  }
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  HIP_TRY(hipSetDevice(ctx->cfg.device));
+  const size_t b = 4 * (size_t)n, total = 3 * align_up(b, 16);
+  ctx->stage_host.resize(total);
+  char* h = ctx->stage_host.data();
+  std::memcpy(h, node, b);
+  std::memcpy(h + align_up(b, 16), row, b);
+  std::memcpy(h + 2 * align_up(b, 16), value, b);
+  int rc = ctx->delta_buf.ensure(total);
+  if (rc) return rc;
+  char* d = (char*)ctx->delta_buf.p;
+  HIP_TRY(hipMemcpyAsync(d, h, total, hipMemcpyHostToDevice, ctx->stream));
+  hipLaunchKernelGGL(k_count_delta, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, ctx->stream, ctx->dc,
+                     (const int32_t*)d, (const int32_t*)(d + align_up(b, 16)),
+                     (const int32_t*)(d + 2 * align_up(b, 16)), n, mode);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipStreamSynchronize(ctx->stream));
+  // the 32-bit / 16-bit bounds of k_spread (spread_bounds_ok)
+  ctx->count_bound += add;
+  ctx->cell_bound = mode ? std::max(ctx->cell_bound, top) : ctx->cell_bound + add;
   return 0;
 }
 
@@ -1727,15 +1833,39 @@ static int stage_spods(kss_ctx* ctx, const kss_podset* ps) {
   return 0;
 }
 
+// One record slot to the caller's arrays: the span of the requested fields in one D2H copy
+// through pinned staging (the slot is contiguous: SlotLayout), then host copies.
 static int copy_slot(kss_ctx* ctx, int slot, const PodMeta& m, kss_pod_result* out) {
   const size_t N = (size_t)ctx->dc.N;
   const SlotLayout SL(N);
   const char* base = (const char*)ctx->slot_buf.p + (size_t)slot * SL.bytes;
-  if (out->fail_plugin) HIP_TRY(hipMemcpy(out->fail_plugin, base + SL.fail, N, hipMemcpyDeviceToHost));
-  if (out->fail_detail) HIP_TRY(hipMemcpy(out->fail_detail, base + SL.detail, 2 * N, hipMemcpyDeviceToHost));
-  if (out->raw) HIP_TRY(hipMemcpy(out->raw, base + SL.raw, 8 * KSS_NSCORE * N, hipMemcpyDeviceToHost));
-  if (out->norm) HIP_TRY(hipMemcpy(out->norm, base + SL.norm, 8 * KSS_NSCORE * N, hipMemcpyDeviceToHost));
-  if (out->total) HIP_TRY(hipMemcpy(out->total, base + SL.total, 8 * N, hipMemcpyDeviceToHost));
+  struct Part {
+    void* dst;
+    size_t off, bytes;
+  } parts[5] = {{out->fail_plugin, SL.fail, N},
+                {out->fail_detail, SL.detail, 2 * N},
+                {out->raw, SL.raw, 8 * KSS_NSCORE * N},
+                {out->norm, SL.norm, 8 * KSS_NSCORE * N},
+                {out->total, SL.total, 8 * N}};
+  size_t lo = SL.bytes, hi = 0;
+  for (const Part& q : parts)
+    if (q.dst && q.bytes) {
+      lo = std::min(lo, q.off);
+      hi = std::max(hi, q.off + q.bytes);
+    }
+  if (hi > lo) {
+    if (ctx->pinned_cap < hi - lo) {
+      if (ctx->pinned) HIP_TRY(hipHostFree(ctx->pinned));
+      ctx->pinned = nullptr;
+      ctx->pinned_cap = 0;
+      HIP_TRY(hipHostMalloc(&ctx->pinned, hi - lo, hipHostMallocDefault));
+      ctx->pinned_cap = hi - lo;
+    }
+    HIP_TRY(hipMemcpyAsync(ctx->pinned, base + lo, hi - lo, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    for (const Part& q : parts)
+      if (q.dst && q.bytes) std::memcpy(q.dst, (const char*)ctx->pinned + (q.off - lo), q.bytes);
+  }
   out->n_feasible = m.n_feasible;
   out->chosen = m.chosen;
   out->best_total = m.best_total;
@@ -1745,59 +1875,148 @@ static int copy_slot(kss_ctx* ctx, int slot, const PodMeta& m, kss_pod_result* o
   return 0;
 }
 
+// One pod of a podset with its own compact pools (every pool reference remapped): the
+// per-pod calls upload and validate only what that pod references.
+struct OnePod {
+  kss_pod pod{};
+  std::vector<kss_req> reqs;
+  std::vector<kss_term> terms;
+  std::vector<kss_spread> spreads;
+  std::vector<kss_ipa> ipa;
+  std::vector<int32_t> ints;
+  kss_podset ps{};
+};
+
+static int compact_pod(const kss_podset* ps, int i, OnePod& o) {
+  const kss_pod& p = ps->pods[i];
+  auto in = [](int64_t off, int64_t len, int64_t cap) { return off >= 0 && len >= 0 && off + len <= cap; };
+  if (!in(p.sel_off, p.sel_len, ps->n_reqs) || !in(p.aff_off, p.aff_len, ps->n_terms) ||
+      !in(p.pref_off, p.pref_len, ps->n_terms) || !in(p.spread_off, (int64_t)p.n_hard + p.n_soft, ps->n_spreads) ||
+      !in(p.ipa_off, p.ipa_len, ps->n_ipa) || !in(p.own_terms_off, p.own_terms_len, ps->n_ints) ||
+      (p.names_len >= 0 && !in(p.names_off, p.names_len, ps->n_ints)))
+    return fail(KSS_E_INVAL, "pod program out of range");
+  o = OnePod{};
+  o.pod = p;
+  auto list = [&](int off, int len) -> int32_t {
+    const int32_t at = (int32_t)o.ints.size();
+    if (in(off, len, ps->n_ints)) o.ints.insert(o.ints.end(), ps->ints + off, ps->ints + off + len);
+    return at;
+  };
+  auto req = [&](const kss_req& r) {
+    kss_req q = r;
+    if (r.op == KSS_OP_IN || r.op == KSS_OP_NOTIN) q.list_off = list(r.list_off, r.list_len);
+    o.reqs.push_back(q);
+  };
+  auto term = [&](const kss_term& t) -> bool {
+    if (!in(t.req_off, t.req_len, ps->n_reqs)) return false;
+    kss_term u = t;
+    u.req_off = (int32_t)o.reqs.size();
+    for (int k = 0; k < t.req_len; k++) req(ps->reqs[t.req_off + k]);
+    o.terms.push_back(u);
+    return true;
+  };
+  o.pod.sel_off = 0;
+  for (int k = 0; k < p.sel_len; k++) req(ps->reqs[p.sel_off + k]);
+  // the terms of the pod are contiguous: aff then pref; each term's requirements contiguous
+  o.pod.aff_off = 0;
+  for (int t = 0; t < p.aff_len; t++)
+    if (!term(ps->terms[p.aff_off + t])) return fail(KSS_E_INVAL, "term out of range");
+  o.pod.pref_off = (int32_t)o.terms.size();
+  for (int t = 0; t < p.pref_len; t++)
+    if (!term(ps->terms[p.pref_off + t])) return fail(KSS_E_INVAL, "term out of range");
+  o.pod.spread_off = 0;
+  for (int c = 0; c < p.n_hard + p.n_soft; c++) {
+    kss_spread sp = ps->spreads[p.spread_off + c];
+    sp.cls_off = list(sp.cls_off, sp.cls_len);
+    o.spreads.push_back(sp);
+  }
+  o.pod.ipa_off = 0;
+  for (int e = 0; e < p.ipa_len; e++) {
+    kss_ipa en = ps->ipa[p.ipa_off + e];
+    en.row_off = list(en.row_off, en.row_len);
+    o.ipa.push_back(en);
+  }
+  o.pod.own_terms_off = list(p.own_terms_off, p.own_terms_len);
+  if (p.names_len >= 0) o.pod.names_off = list(p.names_off, p.names_len);
+  if (o.reqs.empty()) o.reqs.push_back(kss_req{});
+  if (o.terms.empty()) o.terms.push_back(kss_term{});
+  if (o.spreads.empty()) o.spreads.push_back(kss_spread{});
+  if (o.ipa.empty()) o.ipa.push_back(kss_ipa{});
+  if (o.ints.empty()) o.ints.push_back(0);
+  o.ps.n_pods = 1;
+  o.ps.n_reqs = (int32_t)o.reqs.size();
+  o.ps.n_terms = (int32_t)o.terms.size();
+  o.ps.n_spreads = (int32_t)o.spreads.size();
+  o.ps.n_ipa = (int32_t)o.ipa.size();
+  o.ps.n_ints = (int32_t)o.ints.size();
+  o.ps.pods = &o.pod;
+  o.ps.reqs = o.reqs.data();
+  o.ps.terms = o.terms.data();
+  o.ps.spreads = o.spreads.data();
+  o.ps.ipa = o.ipa.data();
+  o.ps.ints = o.ints.data();
+  return 0;
+}
+
 int kss_eval_pod(kss_ctx* ctx, const kss_podset* ps, int32_t pod_index, kss_pod_result* out) {
   if (!ctx || !ctx->loaded || !ps || !out) return fail(KSS_E_INVAL, "bad arguments");
   if (pod_index < 0 || pod_index >= ps->n_pods) return fail(KSS_E_INVAL, "pod index out of range");
-  int rc = validate(&ctx->host, ps, ps->n_pods);
+  OnePod one;
+  int rc = compact_pod(ps, pod_index, one);
   if (rc) return rc;
+  if ((rc = validate(&ctx->host, &one.ps, 1))) return rc;
   std::lock_guard<std::mutex> lk(ctx->mu);
   HIP_TRY(hipSetDevice(ctx->cfg.device));
-  // evaluate exactly one pod: view the podset from pod_index
-  kss_podset one = *ps;
-  one.pods = ps->pods + pod_index;
-  one.n_pods = 1;
-  rc = upload_podset(ctx->stream, ctx->tmp_pod_buf, &one, ctx->tdp);
+  rc = upload_podset(ctx->stream, ctx->tmp_pod_buf, &one.ps, ctx->tdp);
   if (rc) return rc;
-  const PlanNeeds need = plan_needs(ctx->key_card_h.data(), ctx->key_flags_h.data(), &one, 1);
+  const PlanNeeds need = plan_needs(ctx->key_card_h.data(), ctx->key_flags_h.data(), &one.ps, 1);
   rc = run_single(ctx, need, ctx->tdp, 1, /*commit=*/false, /*record=*/false, /*keep_norm=*/true, 0, nullptr);
   if (rc) return rc;
   return copy_slot(ctx, 0, ctx->meta_host[0], out);
 }
 
-int kss_commit(kss_ctx* ctx, const kss_podset* ps, int32_t pod_index, int32_t node) {
+// AssumePod (sign 1) / ForgetPod (-1) of ps.pods[pod_index] on a node: the deltas travel in
+// the kernel's arguments.
+static int commit_one(kss_ctx* ctx, const kss_podset* ps, int32_t pod_index, int32_t node, int sign) {
   if (!ctx || !ctx->loaded || !ps) return fail(KSS_E_INVAL, "bad arguments");
   if (pod_index < 0 || pod_index >= ps->n_pods) return fail(KSS_E_INVAL, "pod index out of range");
   const int local = node - ctx->dc.node_base;
   if (local < 0 || local >= ctx->dc.N) return fail(KSS_E_INVAL, "node out of range");
-  int rc = validate(&ctx->host, ps, ps->n_pods);
-  if (rc) return rc;
+  const kss_pod& p = ps->pods[pod_index];
+  if (p.cls >= ctx->host.n_classes) return fail(KSS_E_INVAL, "pod class out of range");
+  if (p.own_terms_len < 0 || p.own_terms_off < 0 || p.own_terms_off + p.own_terms_len > ps->n_ints)
+    return fail(KSS_E_INVAL, "own terms out of range");
+  if (p.own_terms_len > 8) return fail(KSS_E_UNSUPPORTED, "more than 8 own term rows");
+  CommitArgs a{};
+  for (int r = 0; r < KSS_NRES; r++) a.req[r] = p.commit_req[r];
+  a.nz[0] = p.commit_nz[0];
+  a.nz[1] = p.commit_nz[1];
+  a.cls = p.cls;
+  a.n_own = p.own_terms_len;
+  for (int i = 0; i < p.own_terms_len; i++) {
+    a.own[i] = ps->ints[p.own_terms_off + i];
+    if (a.own[i] < 0 || a.own[i] >= ctx->host.n_terms) return fail(KSS_E_INVAL, "own term id out of range");
+  }
+  a.local = local;
+  a.sign = sign;
   std::lock_guard<std::mutex> lk(ctx->mu);
   HIP_TRY(hipSetDevice(ctx->cfg.device));
-  rc = upload_podset(ctx->stream, ctx->tmp_pod_buf, ps, ctx->tdp);
-  if (rc) return rc;
-  ctx->count_bound += 1.0 + (double)ps->pods[pod_index].own_terms_len;
-  ctx->cell_bound += 1.0 + (double)ps->pods[pod_index].own_terms_len;
-  hipLaunchKernelGGL(k_commit, dim3(1), dim3(64), 0, ctx->stream, ctx->dc, ctx->tdp, pod_index, local, 1);
+  if (sign > 0) {
+    ctx->count_bound += 1.0 + (double)p.own_terms_len;
+    ctx->cell_bound += 1.0 + (double)p.own_terms_len;
+  }
+  hipLaunchKernelGGL(k_commit, dim3(1), dim3(64), 0, ctx->stream, ctx->dc, a);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipStreamSynchronize(ctx->stream));
   return 0;
 }
 
+int kss_commit(kss_ctx* ctx, const kss_podset* ps, int32_t pod_index, int32_t node) {
+  return commit_one(ctx, ps, pod_index, node, 1);
+}
+
 int kss_rollback(kss_ctx* ctx, const kss_podset* ps, int32_t pod_index, int32_t node) {
-  if (!ctx || !ctx->loaded || !ps) return fail(KSS_E_INVAL, "bad arguments");
-  if (pod_index < 0 || pod_index >= ps->n_pods) return fail(KSS_E_INVAL, "pod index out of range");
-  const int local = node - ctx->dc.node_base;
-  if (local < 0 || local >= ctx->dc.N) return fail(KSS_E_INVAL, "node out of range");
-  int rc = validate(&ctx->host, ps, ps->n_pods);
-  if (rc) return rc;
-  std::lock_guard<std::mutex> lk(ctx->mu);
-  HIP_TRY(hipSetDevice(ctx->cfg.device));
-  rc = upload_podset(ctx->stream, ctx->tmp_pod_buf, ps, ctx->tdp);
-  if (rc) return rc;
-  hipLaunchKernelGGL(k_commit, dim3(1), dim3(64), 0, ctx->stream, ctx->dc, ctx->tdp, pod_index, local, -1);
-  HIP_TRY(hipGetLastError());
-  HIP_TRY(hipStreamSynchronize(ctx->stream));
-  return 0;
+  return commit_one(ctx, ps, pod_index, node, -1);
 }
 
 int kss_schedule_batch(kss_ctx* ctx, const kss_podset* ps, int32_t n, uint32_t flags, int32_t* chosen_out) {

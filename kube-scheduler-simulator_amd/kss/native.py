@@ -38,6 +38,7 @@ SIGNATURES = [
     ("kss_destroy", None, [C.c_void_p]),
     ("kss_load_cluster", C.c_int, [C.c_void_p, P(abi.Cluster)]),
     ("kss_apply_node_delta", C.c_int, [C.c_void_p, P(C.c_int32), C.c_int32, P(C.c_int64), P(C.c_int64), P(C.c_int32)]),
+    ("kss_apply_count_delta", C.c_int, [C.c_void_p, P(C.c_int32), P(C.c_int32), P(C.c_int32), C.c_int32, C.c_int32]),
     ("kss_read_node_state", C.c_int, [C.c_void_p, P(C.c_int64), P(C.c_int64), P(C.c_int32), P(C.c_int32), P(C.c_int32)]),
     ("kss_eval_pod", C.c_int, [C.c_void_p, P(abi.PodSet), C.c_int32, P(abi.PodResult)]),
     ("kss_commit", C.c_int, [C.c_void_p, P(abi.PodSet), C.c_int32, C.c_int32]),
@@ -265,6 +266,25 @@ class Context:
 
     def rollback(self, podset_struct, i, node):
         check(lib().kss_rollback(self.h, C.byref(podset_struct), i, node))
+
+    def apply_node_delta(self, idx, requested, nonzero, pod_count):
+        """Overwrite node rows idx (kss_apply_node_delta): requested [n][KSS_NRES], nonzero [n][2]."""
+        idx = np.ascontiguousarray(idx, np.int32)
+        req = np.ascontiguousarray(requested, np.int64).reshape(len(idx), abi.KSS_NRES)
+        nz = np.ascontiguousarray(nonzero, np.int64).reshape(len(idx), 2)
+        pc = np.ascontiguousarray(pod_count, np.int32)
+        check(lib().kss_apply_node_delta(self.h, idx.ctypes.data_as(P(C.c_int32)), len(idx),
+                                         req.ctypes.data_as(P(C.c_int64)), nz.ctypes.data_as(P(C.c_int64)),
+                                         pc.ctypes.data_as(P(C.c_int32))))
+
+    def apply_count_delta(self, node, row, value, overwrite=False):
+        """class / term counts (kss_apply_count_delta): row < n_classes is a class row, else a
+        term row (row - n_classes); add value, or overwrite with it."""
+        node = np.ascontiguousarray(node, np.int32)
+        row = np.ascontiguousarray(row, np.int32)
+        value = np.ascontiguousarray(value, np.int32)
+        check(lib().kss_apply_count_delta(self.h, node.ctypes.data_as(P(C.c_int32)), row.ctypes.data_as(P(C.c_int32)),
+                                          value.ctypes.data_as(P(C.c_int32)), len(node), 1 if overwrite else 0))
 
     def node_state(self):
         N = max(self.n_nodes, 1)

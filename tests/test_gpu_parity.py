@@ -282,3 +282,50 @@ def test_c2_scale_sharded_matches_oracle(config, n_pods):
     # reset + replay gives the same placements (what-if replays)
     ctx.reset()
     np.testing.assert_array_equal(ctx.run_staged(n_pods), chosen_o)
+
+
+def _podset_from(ps, first):
+    """View of pods [first, n) of a podset (the pools are shared)."""
+    import ctypes as C
+    v = abi.PodSet.from_buffer_copy(ps)
+    v.n_pods = ps.n_pods - first
+    v.pods = C.cast(C.addressof(ps.pods.contents) + first * C.sizeof(abi.Pod), C.POINTER(abi.Pod))
+    return v
+
+
+def test_external_binds_through_node_and_count_deltas():
+    """Pods bound outside this scheduler reach the snapshot through kss_apply_node_delta (node
+    rows) and kss_apply_count_delta (class rows added, term rows overwritten): the state then
+    equals the oracle's after those pods, and the following pods schedule as the oracle's
+    uninterrupted run does."""
+    prof = abi.default_profile()
+    n_nodes, n_pods, n0 = 300, 160, 60
+    s = native.Synth(3, 0, n_nodes, n_pods)
+    ncl, nt = s.cluster.n_classes, s.cluster.n_terms
+    chosen_all, _, _ = oracle_c.schedule(prof, s.cluster, s.pods, n_pods, n_nodes, threads=8, n_classes=ncl,
+                                         n_terms=nt)
+    _, _, st0 = oracle_c.schedule(prof, s.cluster, s.pods, n0, n_nodes, threads=8, n_classes=ncl, n_terms=nt)
+    ctx = native.Context(prof)
+    ctx.load(s.cluster)
+    orig = ctx.node_state()
+    N = n_nodes
+    moved = ((st0["requested"][:, :N] != orig["requested"][:, :N]).any(0) |
+             (st0["nonzero"][:, :N] != orig["nonzero"][:, :N]).any(0) | (st0["pod_count"][:N] != orig["pod_count"][:N]))
+    rows = np.nonzero(moved)[0]
+    assert len(rows) > 20
+    ctx.apply_node_delta(rows, st0["requested"][:, rows].T, st0["nonzero"][:, rows].T, st0["pod_count"][rows])
+    dc = st0["class_count"][:ncl, :N].astype(np.int64) - orig["class_count"][:ncl, :N]
+    r, n = np.nonzero(dc)
+    ctx.apply_count_delta(n, r, dc[r, n])
+    tdiff = st0["term_count"][:nt, :N] != orig["term_count"][:nt, :N]
+    r, n = np.nonzero(tdiff)
+    ctx.apply_count_delta(n, ncl + r, st0["term_count"][:nt, :N][r, n], overwrite=True)
+    g = ctx.node_state()
+    np.testing.assert_array_equal(g["requested"][:, :N], st0["requested"][:, :N])
+    np.testing.assert_array_equal(g["nonzero"][:, :N], st0["nonzero"][:, :N])
+    np.testing.assert_array_equal(g["pod_count"][:N], st0["pod_count"][:N])
+    np.testing.assert_array_equal(g["class_count"][:ncl], st0["class_count"][:ncl])
+    np.testing.assert_array_equal(g["term_count"][:nt], st0["term_count"][:nt])
+    chosen = ctx.schedule_batch(_podset_from(s.pods, n0), n_pods - n0)
+    np.testing.assert_array_equal(chosen, chosen_all[n0:])
+    ctx.close()

@@ -110,6 +110,43 @@ def spread_e2_detail(w, a):
     return "  E2 detail (shard 0): " + " ".join(f"{n}={m:.2f}" for n, m in zip(names, np.median(d, axis=0)))
 
 
+def latency_summary(path):
+    """The first record of a stamps dump as a dict: kernel, shards, mean per-phase us of
+    shard 0, and per exchange the median over pods of the fastest shard's wait from the last
+    publish to completion (the exchange floor: propagation + combine)."""
+    kind, w, a = records(path)[0]
+    if kind == 0:
+        a = a.reshape(-1, 8)
+        a = a[(a[:, 0] > 0) & (a[:, 6] > 0)]
+        d = np.diff(a[:, :7], axis=1) / 100.0
+        return {"kernel": "k_schedule", "shards": w, "pods": int(len(a)),
+                "phases_us": {n: float(m) for n, m in zip(NAMES, d.mean(axis=0))}}
+    a = a.reshape(w, NSTAMP_PODS // 2, 16)
+    if kind == 1:
+        names, top, pairs = NAMES_SIMPLE, 6, (("exchange", 4, 5),)
+        b = a[:, :, :7]
+        ok = (b[:, :, 0] > 0).all(axis=0) & (b[:, :, 6] > 0).all(axis=0)
+    else:
+        names, top, pairs = NAMES_SPREAD, 9, (("stats", 1, 2), ("filter", 3, 4), ("argmax", 7, 8))
+        b = a[:, :, :10].copy()
+        ok = (b[:, :, 0] > 0).all(axis=0) & (b[:, :, 9] > 0).all(axis=0)
+        for i in range(1, 9):
+            z = b[:, :, i] == 0
+            b[:, :, i][z] = b[:, :, i - 1][z]
+    b = b[:, ok, :]
+    d = np.diff(b[0, :, :top + 1], axis=1) / 100.0
+    out = {"kernel": "k_simple" if kind == 1 else "k_spread", "shards": w, "pods": int(ok.sum()),
+           "phases_us": {n: round(float(m), 3) for n, m in zip(names, d.mean(axis=0))},
+           "pod_us_shard0": round(float(((b[0, :, top] - b[0, :, 0]) / 100.0).mean()), 3), "exchange_floor_us": {}}
+    for name, pub, done in pairs:
+        p, dn = b[:, :, pub], b[:, :, done]
+        used = dn[0] > p[0]
+        if used.any():
+            last = p[:, used].max(axis=0)
+            out["exchange_floor_us"][name] = round(float(np.median((dn[:, used] - last[None, :]).min(axis=0)) / 100.0), 3)
+    return out
+
+
 if __name__ == "__main__":
     for p in sys.argv[1:]:
         print(p, summarise(p))
