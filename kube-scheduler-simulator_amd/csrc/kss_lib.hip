@@ -1938,12 +1938,7 @@ static int compact_pod(const kss_podset* ps, int i, OnePod& o) {
   }
   o.pod.own_terms_off = list(p.own_terms_off, p.own_terms_len);
   if (p.names_len >= 0) o.pod.names_off = list(p.names_off, p.names_len);
-  if (o.reqs.empty()) o.reqs.push_back(kss_req{});
-  if (o.terms.empty()) o.terms.push_back(kss_term{});
-  if (o.spreads.empty()) o.spreads.push_back(kss_spread{});
-  if (o.ipa.empty()) o.ipa.push_back(kss_ipa{});
-  if (o.ints.empty()) o.ints.push_back(0);
-  o.ps.n_pods = 1;
+  o.ps.n_pods = 1;  // empty pools stay empty (upload_podset sizes them; validate skips them)
   o.ps.n_reqs = (int32_t)o.reqs.size();
   o.ps.n_terms = (int32_t)o.terms.size();
   o.ps.n_spreads = (int32_t)o.spreads.size();
