@@ -458,6 +458,15 @@ int kss_format_annotations(kss_ctx* ctx, const kss_pod_result* res, int32_t n_no
 /* Context-free variant (host only): names and profile passed explicitly. */
 int kss_format_annotations_ex(const kss_names* names, const kss_profile* prof, const kss_pod_result* res,
                               int32_t n_nodes, int32_t n_taints, int32_t n_scalar, char* buf, size_t cap, size_t* need);
+/* The same two with the pod's NodeAffinity PreFilterResult: store.go:522-534 records
+ * PreFilterResult.NodeNames.List() under scheduler-simulator/prefilter-result; ps.pods[pod_index]
+ * (names_off/names_len) supplies the node set.  Replaces the AddPreFilterResult path of
+ * simulator/scheduler/plugin/resultstore/store.go:522 for pods with matchFields metadata.name. */
+int kss_format_pod_annotations(kss_ctx* ctx, const kss_podset* ps, int32_t pod_index, const kss_pod_result* res,
+                               int32_t n_nodes, char* buf, size_t cap, size_t* need);
+int kss_format_pod_annotations_ex(const kss_names* names, const kss_profile* prof, const kss_podset* ps,
+                                  int32_t pod_index, const kss_pod_result* res, int32_t n_nodes, int32_t n_taints,
+                                  int32_t n_scalar, char* buf, size_t cap, size_t* need);
 /* sizeof() of every ABI struct, in header order; returns the count written (ABI self-check) */
 int kss_abi_sizes(int32_t* out, int32_t n);
 /* Host only (no device): which sequential-loop kernel a staged, unrecorded batch of `ps` on

@@ -186,8 +186,24 @@ std::string fail_message(const kss_host_names* nm, int plugin, unsigned detail) 
 
 }  // namespace
 
+int kss_host_prefilter_nodes(const kss_podset* ps, int32_t i, int n_nodes, std::vector<int>* out, int* has) {
+  *has = 0;
+  out->clear();
+  if (!ps || i < 0 || i >= ps->n_pods || !ps->pods) return KSS_E_INVAL;
+  const kss_pod& p = ps->pods[i];
+  if (p.names_len < 0) return 0;
+  if (p.names_off < 0 || p.names_off + p.names_len > ps->n_ints || (p.names_len && !ps->ints)) return KSS_E_INVAL;
+  for (int k = 0; k < p.names_len; k++) {
+    const int n = ps->ints[p.names_off + k];
+    if (n < 0 || n >= n_nodes) return KSS_E_INVAL;
+    out->push_back(n);
+  }
+  *has = 1;
+  return 0;
+}
+
 int kss_host_format(const kss_host_names* nm, const kss_profile* prof, const kss_pod_result* res, int n_nodes, char* buf,
-                    size_t cap, size_t* need) {
+                    size_t cap, size_t* need, const std::vector<int>* prefilter_nodes) {
   if ((int)nm->node.size() < n_nodes) return KSS_E_INVAL;
   std::vector<int> order(n_nodes);
   std::iota(order.begin(), order.end(), 0);
@@ -196,7 +212,23 @@ int kss_host_format(const kss_host_names* nm, const kss_profile* prof, const kss
   const bool prefilter_fail = res->status == 2 || res->status == 3;
   std::vector<KV> out;
   // prefilter
-  out.push_back({"scheduler-simulator/prefilter-result", "{}"});
+  // store.go:522-534: PreFilterResult.NodeNames.List() (sorted) under the plugin's name; none on a conflict
+  if (prefilter_nodes && res->status != 2) {
+    std::vector<std::string> names;
+    for (int n : *prefilter_nodes)
+      if (n >= 0 && n < n_nodes) names.push_back(nm->node[n]);
+    std::sort(names.begin(), names.end());
+    names.erase(std::unique(names.begin(), names.end()), names.end());
+    std::string o = "{\"NodeAffinity\":[";
+    for (size_t i = 0; i < names.size(); i++) {
+      if (i) o.push_back(',');
+      json_str(o, names[i]);
+    }
+    o += "]}";
+    out.push_back({"scheduler-simulator/prefilter-result", o});
+  } else {
+    out.push_back({"scheduler-simulator/prefilter-result", "{}"});
+  }
   if (res->status == 2) {
     out.push_back({"scheduler-simulator/prefilter-result-status", json_map({{"NodeAffinity", "pod affinity terms conflict"}})});
   } else {
@@ -305,4 +337,17 @@ extern "C" int kss_format_annotations_ex(const kss_names* names, const kss_profi
   kss_host_names nm;
   kss_host_set_names(&nm, names, n_nodes, n_taints, n_scalar);
   return kss_host_format(&nm, prof, res, n_nodes, buf, cap, need);
+}
+
+extern "C" int kss_format_pod_annotations_ex(const kss_names* names, const kss_profile* prof, const kss_podset* ps,
+                                             int32_t pod_index, const kss_pod_result* res, int32_t n_nodes,
+                                             int32_t n_taints, int32_t n_scalar, char* buf, size_t cap, size_t* need) {
+  if (!names || !prof || !res || !need || n_nodes < 0) return KSS_E_INVAL;
+  std::vector<int> pf;
+  int has = 0;
+  int rc = kss_host_prefilter_nodes(ps, pod_index, n_nodes, &pf, &has);
+  if (rc) return rc;
+  kss_host_names nm;
+  kss_host_set_names(&nm, names, n_nodes, n_taints, n_scalar);
+  return kss_host_format(&nm, prof, res, n_nodes, buf, cap, need, has ? &pf : nullptr);
 }

@@ -15,5 +15,10 @@ double kss_go_log(double x);
 int kss_host_set_names(kss_host_names* dst, const kss_names* src, int n_nodes, int n_taints, int n_scalar);
 
 // resultstore.Store.GetStoredResult formatting (store.go:133-198) of one pod result.
+// prefilter_nodes: the NodeAffinity PreFilterResult node set (global indices) or null for none.
 int kss_host_format(const kss_host_names* names, const kss_profile* prof, const kss_pod_result* res, int n_nodes,
-                    char* buf, size_t cap, size_t* need);
+                    char* buf, size_t cap, size_t* need, const std::vector<int>* prefilter_nodes = nullptr);
+
+// The PreFilterResult node set of ps->pods[i] (KSS_E_INVAL on a bad index or list); *has = 0 when
+// the pod's PreFilter returned none.
+int kss_host_prefilter_nodes(const kss_podset* ps, int32_t i, int n_nodes, std::vector<int>* out, int* has);

@@ -2454,6 +2454,15 @@ int kss_format_annotations(kss_ctx* ctx, const kss_pod_result* res, int32_t n_no
   return kss_host_format(&ctx->names, &ctx->prof, res, n_nodes, buf, cap, need);
 }
 
+int kss_format_pod_annotations(kss_ctx* ctx, const kss_podset* ps, int32_t pod_index, const kss_pod_result* res,
+                               int32_t n_nodes, char* buf, size_t cap, size_t* need) {
+  if (!ctx || !res || !need) return fail(KSS_E_INVAL, "bad arguments");
+  std::vector<int> pf;
+  int has = 0;
+  if (kss_host_prefilter_nodes(ps, pod_index, n_nodes, &pf, &has)) return fail(KSS_E_INVAL, "bad pod index or node set");
+  return kss_host_format(&ctx->names, &ctx->prof, res, n_nodes, buf, cap, need, has ? &pf : nullptr);
+}
+
 }  // extern "C"
 
 int kss_device_go_log(int32_t device, const double* x, double* y, int32_t n) {

@@ -788,7 +788,11 @@ class Compiler:
                     break
                 nodenames = tn if nodenames is None else (nodenames | tn)
             if nodenames:
-                idx = sorted(self.node_index[n] for n in nodenames if n in self.node_index)
+                missing = sorted(n for n in nodenames if n not in self.node_index)
+                if missing:
+                    # findNodesThatFitPod: NodeInfos().Get(name) fails -> a scheduling error, not a FitError
+                    raise Unsupported(f"PreFilterResult names nodes absent from the snapshot: {missing[:3]}")
+                idx = sorted(self.node_index[n] for n in nodenames)
                 rec["names_off"], rec["names_len"] = self._list(idx)
         rec["aff_len"] = len(self._terms) - rec["aff_off"]
 

@@ -64,6 +64,11 @@ SIGNATURES = [
                                          P(C.c_size_t)]),
     ("kss_format_annotations_ex", C.c_int, [P(abi.Names), P(abi.Profile), P(abi.PodResult), C.c_int32, C.c_int32,
                                             C.c_int32, C.c_char_p, C.c_size_t, P(C.c_size_t)]),
+    ("kss_format_pod_annotations", C.c_int, [C.c_void_p, P(abi.PodSet), C.c_int32, P(abi.PodResult), C.c_int32,
+                                             C.c_char_p, C.c_size_t, P(C.c_size_t)]),
+    ("kss_format_pod_annotations_ex", C.c_int, [P(abi.Names), P(abi.Profile), P(abi.PodSet), C.c_int32,
+                                                P(abi.PodResult), C.c_int32, C.c_int32, C.c_int32, C.c_char_p,
+                                                C.c_size_t, P(C.c_size_t)]),
     ("kss_stage_pods", C.c_int, [C.c_void_p, P(abi.PodSet)]),
     ("kss_run_staged", C.c_int, [C.c_void_p, C.c_int32, C.c_uint32, P(C.c_int32)]),
     ("kss_reset_node_state", C.c_int, [C.c_void_p]),
@@ -163,15 +168,26 @@ def parse_annotations(buf: bytes) -> Dict[str, str]:
     return out
 
 
-def format_annotations_ex(names_struct, profile, result: PodResult, n_nodes, n_taints, n_scalar) -> Dict[str, str]:
-    L = lib()
+def _format(call) -> Dict[str, str]:
     need = C.c_size_t(0)
-    check(L.kss_format_annotations_ex(C.byref(names_struct), C.byref(profile), C.byref(result.s), n_nodes, n_taints,
-                                      n_scalar, None, 0, C.byref(need)))
+    check(call(None, 0, C.byref(need)))
     buf = C.create_string_buffer(need.value)
-    check(L.kss_format_annotations_ex(C.byref(names_struct), C.byref(profile), C.byref(result.s), n_nodes, n_taints,
-                                      n_scalar, buf, need.value, C.byref(need)))
+    check(call(buf, need.value, C.byref(need)))
     return parse_annotations(buf.raw[:need.value])
+
+
+def format_annotations_ex(names_struct, profile, result: PodResult, n_nodes, n_taints, n_scalar,
+                          podset_struct: Optional[abi.PodSet] = None, pod_index: int = -1) -> Dict[str, str]:
+    """Context-free formatting; with (podset_struct, pod_index) the pod's NodeAffinity
+    PreFilterResult is recorded too (store.go:522-534)."""
+    L = lib()
+    if podset_struct is None:
+        return _format(lambda b, c, n: L.kss_format_annotations_ex(C.byref(names_struct), C.byref(profile),
+                                                                   C.byref(result.s), n_nodes, n_taints, n_scalar,
+                                                                   b, c, n))
+    return _format(lambda b, c, n: L.kss_format_pod_annotations_ex(
+        C.byref(names_struct), C.byref(profile), C.byref(podset_struct), pod_index, C.byref(result.s), n_nodes,
+        n_taints, n_scalar, b, c, n))
 
 
 class Context:
@@ -327,13 +343,15 @@ class Context:
         check(lib().kss_fetch_meta(self.h, first, n, out.ctypes.data_as(P(C.c_int64))))
         return out[:n]
 
-    def format_annotations(self, result: PodResult) -> Dict[str, str]:
+    def format_annotations(self, result: PodResult, podset_struct: Optional[abi.PodSet] = None,
+                           pod_index: int = -1) -> Dict[str, str]:
+        """store.go GetStoredResult for one result; pass the pod's podset and index to have its
+        NodeAffinity PreFilterResult recorded (store.go:522-534)."""
         L = lib()
-        need = C.c_size_t(0)
-        check(L.kss_format_annotations(self.h, C.byref(result.s), self.n_nodes, None, 0, C.byref(need)))
-        buf = C.create_string_buffer(need.value)
-        check(L.kss_format_annotations(self.h, C.byref(result.s), self.n_nodes, buf, need.value, C.byref(need)))
-        return parse_annotations(buf.raw[:need.value])
+        if podset_struct is None:
+            return _format(lambda b, c, n: L.kss_format_annotations(self.h, C.byref(result.s), self.n_nodes, b, c, n))
+        return _format(lambda b, c, n: L.kss_format_pod_annotations(self.h, C.byref(podset_struct), pod_index,
+                                                                    C.byref(result.s), self.n_nodes, b, c, n))
 
 
 class Synth:

@@ -13,7 +13,10 @@ one app selector), these mix per pod:
   * bound pods carrying required anti-affinity (existing-pod filter), and required /
     preferred (anti-)affinity terms (existing-pod scores);
   * NoExecute / NoSchedule / PreferNoSchedule taints, tolerations, nodeSelector, required
-    and preferred node affinity, spec.nodeName, a second namespace, small pod limits.
+    and preferred node affinity, spec.nodeName, a second namespace, small pod limits;
+  * every node-affinity operator (In / NotIn / Exists / DoesNotExist / Gt / Lt), matchFields
+    metadata.name In (PreFilterResult) and NotIn, an extended resource (example.com/gpu) on
+    some nodes, ephemeral-storage requests against small disks, init-container requests.
 
 A quarter of the pods with constraints also carry a second constraint of the same kind on
 a key they already use (v1.26 keys the counts by topology pair: test_spread_same_key.py).
@@ -28,6 +31,9 @@ K_HOST = "kubernetes.io/hostname"
 K_ZONE = "topology.kubernetes.io/zone"
 K_RACK = "example.com/rack"
 K_ITYPE = "node.kubernetes.io/instance-type"
+K_TIER = "example.com/tier"
+K_ACCEL = "example.com/accelerator"
+R_GPU = "example.com/gpu"
 APPS = 6
 
 
@@ -41,6 +47,10 @@ def _node(i: int, r: random.Random) -> dict:
         if r.random() >= 0.10:
             labels[K_RACK] = RACKS[r.randrange(len(RACKS))]
         labels[K_ITYPE] = ITYPES[r.randrange(len(ITYPES))]
+        if r.random() < 0.8:
+            labels[K_TIER] = str(r.randint(0, 30))
+        if r.random() < 0.3:
+            labels[K_ACCEL] = "yes"
     taints = []
     if r.random() < 0.10:
         taints.append({"key": "dedicated", "value": "infra", "effect": "NoSchedule"})
@@ -54,9 +64,11 @@ def _node(i: int, r: random.Random) -> dict:
         spec["taints"] = taints
     if r.random() < 0.02:
         spec["unschedulable"] = True
-    return {"metadata": {"name": name, "labels": labels}, "spec": spec,
-            "status": {"allocatable": {"cpu": str(cores), "memory": "%dGi" % (cores * 4),
-                                       "ephemeral-storage": "50Gi", "pods": str(r.choice([4, 8, 16, 110]))}}}
+    alloc = {"cpu": str(cores), "memory": "%dGi" % (cores * 4),
+             "ephemeral-storage": r.choice(["50Gi", "50Gi", "1Gi"]), "pods": str(r.choice([4, 8, 16, 110]))}
+    if r.random() < 0.3:
+        alloc[R_GPU] = r.choice(["1", "2", "4"])
+    return {"metadata": {"name": name, "labels": labels}, "spec": spec, "status": {"allocatable": alloc}}
 
 
 def _sel(r: random.Random) -> dict:
@@ -73,7 +85,27 @@ def _term(r: random.Random, keys: List[str]) -> dict:
 def _requests(r: random.Random) -> dict:
     if r.random() < 0.05:
         return {}
-    return {"cpu": "%dm" % r.choice([100, 250, 500, 1000]), "memory": "%dMi" % r.choice([128, 256, 512, 1024])}
+    req = {"cpu": "%dm" % r.choice([100, 250, 500, 1000]), "memory": "%dMi" % r.choice([128, 256, 512, 1024])}
+    if r.random() < 0.1:
+        req["ephemeral-storage"] = r.choice(["256Mi", "768Mi"])
+    if r.random() < 0.1:
+        req[R_GPU] = "1"
+    return req
+
+
+def _node_expr(r: random.Random) -> dict:
+    u = r.randrange(6)
+    if u == 0:
+        return {"key": K_ZONE, "operator": "In", "values": sorted(set(r.sample(ZONES, 2)))}
+    if u == 1:
+        return {"key": K_ITYPE, "operator": "NotIn", "values": [r.choice(ITYPES)]}
+    if u == 2:
+        return {"key": K_ACCEL, "operator": r.choice(["Exists", "DoesNotExist"])}
+    if u == 3:
+        return {"key": K_TIER, "operator": r.choice(["Gt", "Lt"]), "values": [str(r.randint(5, 25))]}
+    if u == 4:
+        return {"key": K_RACK, "operator": "NotIn", "values": sorted(set(r.sample(RACKS, 3)))}
+    return {"key": K_RACK, "operator": "In", "values": [r.choice(RACKS)]}
 
 
 def _bound(i: int, k: int, node: str, r: random.Random) -> dict:
@@ -109,6 +141,8 @@ def _spread(r: random.Random, key: str, hard: bool) -> dict:
 
 def _pending(j: int, r: random.Random, node_names: List[str]) -> dict:
     spec: Dict = {"containers": [{"name": "c", "resources": {"requests": _requests(r)}}]}
+    if r.random() < 0.08:
+        spec["initContainers"] = [{"name": "i", "resources": {"requests": {"cpu": r.choice(["1", "2500m"])}}}]
     tols = []
     if r.random() < 0.3:
         tols.append({"key": "dedicated", "operator": "Exists", "effect": "NoSchedule"})
@@ -122,13 +156,24 @@ def _pending(j: int, r: random.Random, node_names: List[str]) -> dict:
         spec["nodeSelector"] = {K_ITYPE: r.choice(ITYPES)}
     aff: Dict = {}
     na: Dict = {}
-    if r.random() < 0.1:
-        na["requiredDuringSchedulingIgnoredDuringExecution"] = {"nodeSelectorTerms": [{"matchExpressions": [
-            {"key": K_ZONE, "operator": "In", "values": sorted(set(r.sample(ZONES, 2)))}]}]}
+    u = r.random()
+    if u < 0.15:
+        terms = [{"matchExpressions": [_node_expr(r) for _ in range(r.choice([1, 1, 2]))]}
+                 for _ in range(r.choice([1, 1, 2]))]
+        na["requiredDuringSchedulingIgnoredDuringExecution"] = {"nodeSelectorTerms": terms}
+    elif u < 0.18:  # PreFilterResult: one node name per term (the field selector takes one value)
+        terms = [{"matchFields": [{"key": "metadata.name", "operator": "In", "values": [r.choice(node_names)]}]}
+                 for _ in range(r.choice([1, 2, 3]))]
+        if r.random() < 0.5:
+            terms[0]["matchExpressions"] = [_node_expr(r)]
+        na["requiredDuringSchedulingIgnoredDuringExecution"] = {"nodeSelectorTerms": terms}
+    elif u < 0.20:
+        na["requiredDuringSchedulingIgnoredDuringExecution"] = {"nodeSelectorTerms": [{"matchFields": [
+            {"key": "metadata.name", "operator": "NotIn", "values": [r.choice(node_names)]}]}]}
     if r.random() < 0.2:
         na["preferredDuringSchedulingIgnoredDuringExecution"] = [
-            {"weight": r.randint(1, 100), "preference": {"matchExpressions": [
-                {"key": K_RACK, "operator": "In", "values": [r.choice(RACKS)]}]}}]
+            {"weight": r.randint(1, 100), "preference": {"matchExpressions": [_node_expr(r)]}}
+            for _ in range(r.choice([1, 1, 2]))]
     if na:
         aff["nodeAffinity"] = na
     hard = r.sample([K_ZONE, K_RACK, K_HOST], r.choice([0, 0, 1, 1, 2]))

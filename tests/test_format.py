@@ -14,7 +14,7 @@ from kss.compile import compile_cluster
 GOLD = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "readme_known_answer.json")))
 
 
-def _format_from_oracle(cc, cp, res, j, prof):
+def _format_from_oracle(cc, cp, res, j, prof, pod_aware=False):
     names, keep = native.make_names(cc.node_names, cc.taints, cc.scalars)
     r = native.PodResult(cc.n_nodes)
     r.fail_plugin[:] = res.fail_plugin[j]
@@ -24,6 +24,9 @@ def _format_from_oracle(cc, cp, res, j, prof):
     r.total[:] = res.total[j]
     m = res.meta(j)
     r.s.n_feasible, r.s.chosen, r.s.scored, r.s.status = m["n_feasible"], m["chosen"], m["scored"], m["status"]
+    if pod_aware:
+        return native.format_annotations_ex(names, prof, r, cc.n_nodes, len(cc.taints), len(cc.scalars),
+                                            cp.as_struct(), j)
     return native.format_annotations_ex(names, prof, r, cc.n_nodes, len(cc.taints), len(cc.scalars))
 
 
