@@ -234,6 +234,7 @@ typedef struct kss_ipa {
 #define KSS_POD_IPA_SELF_MATCH (1u << 3)     /* podMatchesAllAffinityTerms(required, pod) */
 #define KSS_POD_IPA_HAS_PREFERRED (1u << 4)  /* incoming pod has preferred (anti-)affinity terms */
 #define KSS_POD_PTS_SCORE_STATE (1u << 5)    /* PTS preScoreState written (always, unless error) */
+#define KSS_POD_PREEMPT_NEVER (1u << 6)      /* spec.preemptionPolicy == Never (PodEligibleToPreemptOthers) */
 
 typedef struct kss_pod {
   int64_t fit_request[KSS_NRES];   /* Fit PreFilter computePodResourceRequest                 */
@@ -257,7 +258,8 @@ typedef struct kss_pod {
   int32_t prefilter_status;        /* 0 ok, 1 NodeAffinity "pod affinity terms conflict",
                                       2 pod-level Error (parse error)                      */
   int32_t names_off, names_len;    /* NodeAffinity PreFilterResult node set (ints[], global idx); len<0: all nodes */
-  int32_t pad[2];
+  int32_t priority;                /* corev1helpers.PodPriority: spec.priority, 0 when unset (DefaultPreemption) */
+  int32_t pad;
 } kss_pod;
 
 typedef struct kss_podset {
@@ -440,6 +442,56 @@ int kss_last_kernel(kss_ctx* ctx);
 /* outcome of pods [first, first+n) of the last scheduling launch, recorded or not:
  * out[5*i .. 5*i+4] = chosen, n_feasible, scored, status, best_total (kss_pod_result) */
 int kss_fetch_meta(kss_ctx* ctx, int32_t first, int32_t n, int64_t* out);
+
+/* ---- DefaultPreemption PostFilter dry run ---------------------------------
+ * Replaces wrappedPlugin.PostFilter -> DefaultPreemption.PostFilter -> Evaluator.Preempt
+ * (simulator/scheduler/plugin/wrappedplugin.go:550-577; upstream
+ * pkg/scheduler/framework/preemption/preemption.go, v1.26.2) for a pod whose filters left no
+ * feasible node: nodesWherePreemptionMightHelp, SelectVictimsOnNode on every potential node
+ * (remove the lower-priority pods, filter, reprieve in MoreImportantPod order) and
+ * pickOneNodeForPreemption.  Nothing is evicted: the caller deletes the victims
+ * (prepareCandidate) and records the nomination (store.go:436-456 "preemption victim").
+ *
+ * The bound-pod table gives the victims' identity and order: per node, NodeInfo.Pods order
+ * (the table order of the pods on that node).  kss_commit appends the committed pod to the
+ * table (id = -1 - pod_index) and kss_rollback removes it the way NodeInfo.RemovePod does
+ * (the node's last pod takes its place). */
+#define KSS_START_UNSET INT64_MAX  /* status.startTime unset (sorts after every start time) */
+typedef struct kss_boundset {
+  int32_t n;                 /* bound pods (on nodes of the loaded cluster) */
+  int32_t n_ints;
+  const int64_t* id;         /* [n] caller ids reported for victims */
+  const int32_t* node;       /* [n] global node index */
+  const int32_t* priority;   /* [n] corev1helpers.PodPriority */
+  const int64_t* start;      /* [n] status.startTime on any monotone integer clock, KSS_START_UNSET if unset */
+  const int32_t* cls;        /* [n] the class_count row the pod counts in */
+  const int64_t* req;        /* [KSS_NRES][n] the pod's NodeInfo.Requested contribution */
+  const int32_t* terms_off;  /* [n] the term_count rows it contributes: ints[terms_off .. +terms_len) */
+  const int32_t* terms_len;  /* [n] */
+  const int32_t* ints;
+} kss_boundset;
+int kss_load_bound(kss_ctx* ctx, const kss_boundset* bs);
+
+#define KSS_PREEMPT_NOMINATED 0
+#define KSS_PREEMPT_NO_CANDIDATE 1   /* FitError: no node where evicting lower-priority pods helps */
+#define KSS_PREEMPT_NOT_ELIGIBLE 2   /* preemptionPolicy Never */
+#define KSS_PREEMPT_SCHEDULABLE 3    /* a node passes every filter: PostFilter does not run */
+typedef struct kss_preempt_result {
+  int32_t status;           /* KSS_PREEMPT_* */
+  int32_t nominated;        /* global node index, -1 */
+  int32_t n_potential;      /* nodes whose filter status is not UnschedulableAndUnresolvable */
+  int32_t n_candidates;     /* potential nodes where the pod fits after evicting some pods */
+  int32_t n_victims;        /* victims on the nominated node (the first victims_cap are written) */
+  int32_t victims_cap;
+  int64_t* victims;         /* caller-owned [victims_cap]: boundset ids, in eviction (importance) order */
+  int32_t highest_priority; /* pickOneNodeForPreemption criteria of the nominated node */
+  int32_t pad;
+  int64_t sum_priority;     /* sum of (priority + 2^31) over the victims */
+  int64_t earliest_start;   /* earliest start among the highest-priority victims */
+} kss_preempt_result;
+/* PostFilter dry run of ps.pods[pod_index] against the current snapshot (the state the
+ * pod's filters saw): call after kss_eval_pod reported it unschedulable. */
+int kss_postfilter_pod(kss_ctx* ctx, const kss_podset* ps, int32_t pod_index, kss_preempt_result* out);
 
 /* ---- annotation formatting (store.go GetStoredResult semantics) -------- */
 typedef struct kss_names {

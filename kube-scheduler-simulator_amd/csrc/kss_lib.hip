@@ -18,6 +18,8 @@
 //                the launch's commits in LDS, host-resolved pod programs (GPod),
 //                32-bit exchanges (kss_spread.cuh).
 //   k_commit     one lane: AssumePod / ForgetPod delta on one node row.
+//   k_preempt    one workgroup: the DefaultPreemption PostFilter dry run of one pod
+//                (kss_preempt.cuh).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -36,6 +38,7 @@
 #include "kss_simple.cuh"
 #include "kss_spread.cuh"
 #include "kss_axis.cuh"
+#include "kss_preempt.cuh"
 
 using namespace kss;
 
@@ -262,6 +265,12 @@ __global__ void k_commit(DevCluster c, CommitArgs a) {
   for (int i = 0; i < a.n_own; i++) c.term_count[(size_t)a.own[i] * N + a.local] += a.sign;
 }
 
+// DefaultPreemption PostFilter dry run of one pod (kss_postfilter_pod).
+__global__ __launch_bounds__(PRE_THREADS) void k_preempt(const PreemptJob* __restrict__ job) {
+  extern __shared__ __attribute__((aligned(16))) long long smem[];
+  preempt_pod(*job, smem);  // descriptors read through the scalar cache
+}
+
 // Delta sync of node rows (kss_apply_node_delta): one packed upload, one scatter.
 __global__ void k_node_delta(DevCluster c, const int32_t* idx, const int64_t* req, const int64_t* nz, const int32_t* pc,
                              int n) {
@@ -334,6 +343,21 @@ struct PlanNeeds {
   bool general = false;  // some pod carries spread / inter-pod-affinity programs
 };
 
+// One pod of the PostFilter bound table (kss_boundset row, or a pod committed since).
+struct BoundPod {
+  int64_t id;
+  int64_t start;
+  int64_t req[KSS_NRES];
+  int32_t prio, cls, tlen;
+  int32_t terms[8];
+};
+// A commit (add) or rollback (remove) applied to the loaded table, in call order.
+struct BoundOp {
+  int32_t node;  // local row
+  int32_t add;
+  BoundPod b;
+};
+
 struct kss_ctx {
   kss_config cfg{};
   kss_profile prof{};
@@ -404,9 +428,19 @@ struct kss_ctx {
   bool axis_meta_dirty = false;  // meta_buf holds node-axis outcomes not yet copied to meta_host
   DevBuf axis_cv;
   int axis_max_blocks = 0;  // KSS_AXIS_BLOCKS: cap on the node-axis grid (tuning)
-  int axis_no_fold = 0;
+  int axis_no_fold = 0;      // KSS_AXIS_NO_FOLD: timing experiment only, statistics not folded (wrong results)
   std::vector<hipEvent_t> loop_ev;  // around each k_simple launch of the last batch
-  double last_loop_ms = 0;          // device time of the sequential-loop kernel(s) of the last batch     // KSS_AXIS_NO_FOLD: timing experiment only, statistics not folded (wrong results)             // node-axis sharding: [5][N] per-row verdict + raw scores of the current pod
+  double last_loop_ms = 0;          // device time of the sequential-loop kernel(s) of the last batch
+  // PostFilter bound table: the loaded rows (table order), the commits / rollbacks since
+  // (the load or the last kss_reset_node_state), the staged pods as bound pods, and the
+  // device CSR built from them on the next dry run
+  std::vector<BoundPod> bound0;
+  std::vector<int32_t> bound0_node;  // local rows
+  std::vector<BoundOp> bound_log;
+  std::vector<BoundPod> staged_bp;
+  bool bound_dirty = true;
+  DevBuf bound_buf, pre_buf;
+  DevBound bound_dev{};
 };
 
 namespace {
@@ -1007,7 +1041,8 @@ int kss_abi_sizes(int32_t* out, int32_t n) {
   const int32_t s[] = {(int32_t)sizeof(kss_cluster), (int32_t)sizeof(kss_req),     (int32_t)sizeof(kss_term),
                        (int32_t)sizeof(kss_spread),  (int32_t)sizeof(kss_ipa),     (int32_t)sizeof(kss_pod),
                        (int32_t)sizeof(kss_podset),  (int32_t)sizeof(kss_profile), (int32_t)sizeof(kss_pod_result),
-                       (int32_t)sizeof(kss_config),  (int32_t)sizeof(kss_names),   (int32_t)sizeof(kss_synth)};
+                       (int32_t)sizeof(kss_config),  (int32_t)sizeof(kss_names),   (int32_t)sizeof(kss_synth),
+                       (int32_t)sizeof(kss_boundset), (int32_t)sizeof(kss_preempt_result)};
   const int32_t k = (int32_t)(sizeof(s) / sizeof(s[0]));
   for (int i = 0; i < n && i < k; i++) out[i] = s[i];
   return k;
@@ -1065,6 +1100,8 @@ void kss_destroy(kss_ctx* ctx) {
   ctx->job_buf.release();
   ctx->spod_buf.release();
   ctx->stat_buf.release();
+  ctx->bound_buf.release();
+  ctx->pre_buf.release();
   ctx->stamp_buf.release();
   ctx->gran_buf.release();
   ctx->err_buf.release();
@@ -1138,6 +1175,10 @@ int kss_load_cluster(kss_ctx* ctx, const kss_cluster* cl) {
     ctx->cell_bound0 = ctx->cell_bound = cm;
   }
   ctx->loaded = true;
+  ctx->bound0.clear();
+  ctx->bound0_node.clear();
+  ctx->bound_log.clear();
+  ctx->bound_dirty = true;
   ctx->recorded = 0;
   ctx->meta_n = 0;
   ctx->axis_meta_dirty = false;
@@ -1272,6 +1313,8 @@ int kss_reset_node_state(kss_ctx* ctx) {
   void* dst[5] = {ctx->dc.requested, ctx->dc.nonzero, ctx->dc.pod_count, ctx->dc.class_count, ctx->dc.term_count};
   ctx->count_bound = ctx->count_bound0;
   ctx->cell_bound = ctx->cell_bound0;
+  ctx->bound_log.clear();
+  ctx->bound_dirty = true;
   for (int i = 0; i < 5; i++)
     if (ctx->mut_bytes[i])
       HIP_TRY(hipMemcpyAsync(dst[i], (char*)ctx->pristine_buf.p + ctx->pristine_off[i], ctx->mut_bytes[i],
@@ -1970,6 +2013,35 @@ int kss_eval_pod(kss_ctx* ctx, const kss_podset* ps, int32_t pod_index, kss_pod_
   return copy_slot(ctx, 0, ctx->meta_host[0], out);
 }
 
+// A pending pod as a bound pod of the PostFilter table once committed (id -1 - index,
+// status.startTime unset: it has not started).
+static BoundPod bound_from_pod(const kss_podset* ps, int i) {
+  const kss_pod& p = ps->pods[i];
+  BoundPod b{};
+  b.id = -1 - (int64_t)i;
+  b.start = KSS_START_UNSET;
+  for (int r = 0; r < KSS_NRES; r++) b.req[r] = p.commit_req[r];
+  b.prio = p.priority;
+  b.cls = p.cls;
+  b.tlen = std::min(p.own_terms_len, 8);
+  for (int t = 0; t < b.tlen; t++) b.terms[t] = ps->ints[p.own_terms_off + t];
+  return b;
+}
+
+static void stage_bound(kss_ctx* ctx, const kss_podset* ps) {
+  ctx->staged_bp.resize(ps->n_pods);
+  for (int i = 0; i < ps->n_pods; i++) ctx->staged_bp[i] = bound_from_pod(ps, i);
+}
+
+// the batch's AssumePods, as NodeInfo.AddPod appends them
+static void log_batch_commits(kss_ctx* ctx, int n) {
+  for (int i = 0; i < n && i < (int)ctx->staged_bp.size(); i++) {
+    const int local = ctx->meta_host[i].chosen - ctx->dc.node_base;
+    if (local >= 0 && local < ctx->dc.N) ctx->bound_log.push_back(BoundOp{local, 1, ctx->staged_bp[i]});
+  }
+  ctx->bound_dirty = true;
+}
+
 // AssumePod (sign 1) / ForgetPod (-1) of ps.pods[pod_index] on a node: the deltas travel in
 // the kernel's arguments.
 static int commit_one(kss_ctx* ctx, const kss_podset* ps, int32_t pod_index, int32_t node, int sign) {
@@ -2003,6 +2075,8 @@ static int commit_one(kss_ctx* ctx, const kss_podset* ps, int32_t pod_index, int
   hipLaunchKernelGGL(k_commit, dim3(1), dim3(64), 0, ctx->stream, ctx->dc, a);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipStreamSynchronize(ctx->stream));
+  ctx->bound_log.push_back(BoundOp{local, sign > 0 ? 1 : 0, bound_from_pod(ps, pod_index)});
+  ctx->bound_dirty = true;
   return 0;
 }
 
@@ -2028,11 +2102,13 @@ int kss_schedule_batch(kss_ctx* ctx, const kss_podset* ps, int32_t n, uint32_t f
   rc = upload_podset(ctx->stream, ctx->pod_buf, ps, ctx->dp);
   if (rc) return rc;
   if ((rc = stage_spods(ctx, ps))) return rc;
+  stage_bound(ctx, ps);
   ctx->staged_n = ps->n_pods;
   ctx->staged_need = plan_needs(ctx->key_card_h.data(), ctx->key_flags_h.data(), ps, ps->n_pods);
   rc = run_single(ctx, ctx->staged_need, ctx->dp, n, /*commit=*/true, record, /*keep_norm=*/record, flags, chosen_out,
                   /*staged=*/true);
   if (rc) return rc;
+  log_batch_commits(ctx, n);
   for (int i = 0; i < n; i++)
     if (ctx->meta_host[i].status == 4) return fail(KSS_E_UNSUPPORTED, "pod program exceeds the device path's per-pod limits");
   return 0;
@@ -2047,6 +2123,7 @@ int kss_stage_pods(kss_ctx* ctx, const kss_podset* ps) {
   rc = upload_podset(ctx->stream, ctx->pod_buf, ps, ctx->dp);
   if (rc) return rc;
   if ((rc = stage_spods(ctx, ps))) return rc;
+  stage_bound(ctx, ps);
   HIP_TRY(hipStreamSynchronize(ctx->stream));
   ctx->staged_n = ps->n_pods;
   ctx->staged_need = plan_needs(ctx->key_card_h.data(), ctx->key_flags_h.data(), ps, ps->n_pods);
@@ -2063,6 +2140,7 @@ int kss_run_staged(kss_ctx* ctx, int32_t n, uint32_t flags, int32_t* chosen_out)
   int rc = run_single(ctx, ctx->staged_need, ctx->dp, n, /*commit=*/true, record, /*keep_norm=*/record, flags, chosen_out,
                       /*staged=*/true);
   if (rc) return rc;
+  log_batch_commits(ctx, n);
   for (int i = 0; i < n; i++)
     if (ctx->meta_host[i].status == 4) return fail(KSS_E_UNSUPPORTED, "pod program exceeds the device path's per-pod limits");
   return 0;
@@ -2442,6 +2520,199 @@ int kss_schedule_scenarios(int32_t device, const kss_profile* prof, int32_t n_sc
   rc = kss_sweep_run(sw, chosen_out, device_ms);
   kss_sweep_destroy(sw);
   return rc;
+}
+
+int kss_load_bound(kss_ctx* ctx, const kss_boundset* bs) {
+  if (!ctx || !ctx->loaded || !bs || bs->n < 0 || bs->n_ints < 0) return fail(KSS_E_INVAL, "bad arguments");
+  if (bs->n && (!bs->id || !bs->node || !bs->priority || !bs->start || !bs->cls || !bs->req || !bs->terms_off ||
+                !bs->terms_len))
+    return fail(KSS_E_INVAL, "null boundset array");
+  std::vector<BoundPod> rows;
+  std::vector<int32_t> nodes;
+  for (int i = 0; i < bs->n; i++) {
+    const int local = bs->node[i] - ctx->dc.node_base;
+    if (local < 0 || local >= ctx->dc.N) continue;  // another shard's node
+    if (bs->cls[i] < -1 || bs->cls[i] >= ctx->host.n_classes) return fail(KSS_E_INVAL, "bound pod class out of range");
+    if (bs->terms_len[i] < 0 || bs->terms_off[i] < 0 || bs->terms_off[i] + bs->terms_len[i] > bs->n_ints ||
+        (bs->terms_len[i] && !bs->ints))
+      return fail(KSS_E_INVAL, "bound pod terms out of range");
+    if (bs->terms_len[i] > 8) return fail(KSS_E_UNSUPPORTED, "a bound pod with more than 8 affinity term rows");
+    BoundPod b{};
+    b.id = bs->id[i];
+    b.start = bs->start[i];
+    for (int r = 0; r < KSS_NRES; r++) b.req[r] = bs->req[(size_t)r * bs->n + i];
+    b.prio = bs->priority[i];
+    b.cls = bs->cls[i];
+    b.tlen = bs->terms_len[i];
+    for (int t = 0; t < b.tlen; t++) {
+      b.terms[t] = bs->ints[bs->terms_off[i] + t];
+      if (b.terms[t] < 0 || b.terms[t] >= ctx->host.n_terms) return fail(KSS_E_INVAL, "bound pod term row out of range");
+    }
+    rows.push_back(b);
+    nodes.push_back(local);
+  }
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  ctx->bound0.swap(rows);
+  ctx->bound0_node.swap(nodes);
+  ctx->bound_log.clear();
+  ctx->bound_dirty = true;
+  return 0;
+}
+
+namespace {
+
+// NodeInfo.Pods of every node: the loaded rows, then the commits / rollbacks in call order
+// (RemovePod moves the node's last pod into the freed slot), as one CSR upload.
+int upload_bound(kss_ctx* ctx) {
+  const int N = ctx->dc.N;
+  std::vector<std::vector<BoundPod>> per((size_t)N);
+  for (size_t i = 0; i < ctx->bound0.size(); i++) per[ctx->bound0_node[i]].push_back(ctx->bound0[i]);
+  for (const BoundOp& op : ctx->bound_log) {
+    auto& v = per[op.node];
+    if (op.add) {
+      v.push_back(op.b);
+    } else {
+      for (size_t k = 0; k < v.size(); k++)
+        if (v[k].id == op.b.id) {
+          v[k] = v.back();
+          v.pop_back();
+          break;
+        }
+    }
+  }
+  size_t nb = 0, ni = 0;
+  for (auto& v : per) {
+    nb += v.size();
+    for (auto& b : v) ni += b.tlen;
+  }
+  const size_t NB = std::max(nb, (size_t)1);
+  size_t o_ptr = 0, o_id = align_up(4 * (N + 1), 256), o_prio = align_up(o_id + 8 * NB, 256),
+         o_start = align_up(o_prio + 4 * NB, 256), o_cls = align_up(o_start + 8 * NB, 256),
+         o_req = align_up(o_cls + 4 * NB, 256), o_toff = align_up(o_req + 8 * KSS_NRES * NB, 256),
+         o_tlen = align_up(o_toff + 4 * NB, 256), o_ints = align_up(o_tlen + 4 * NB, 256),
+         total = align_up(o_ints + 4 * std::max(ni, (size_t)1), 256);
+  std::vector<char>& h = ctx->stage_host;
+  h.assign(total, 0);
+  int32_t* ptr = (int32_t*)(h.data() + o_ptr);
+  int64_t* id = (int64_t*)(h.data() + o_id);
+  int32_t* prio = (int32_t*)(h.data() + o_prio);
+  int64_t* start = (int64_t*)(h.data() + o_start);
+  int32_t* cls = (int32_t*)(h.data() + o_cls);
+  int64_t* req = (int64_t*)(h.data() + o_req);
+  int32_t* toff = (int32_t*)(h.data() + o_toff);
+  int32_t* tlen = (int32_t*)(h.data() + o_tlen);
+  int32_t* ints = (int32_t*)(h.data() + o_ints);
+  size_t e = 0, t = 0;
+  for (int n = 0; n < N; n++) {
+    ptr[n] = (int32_t)e;
+    for (const BoundPod& b : per[n]) {
+      id[e] = b.id;
+      prio[e] = b.prio;
+      start[e] = b.start;
+      cls[e] = b.cls;
+      for (int r = 0; r < KSS_NRES; r++) req[e * KSS_NRES + r] = b.req[r];
+      toff[e] = (int32_t)t;
+      tlen[e] = b.tlen;
+      for (int k = 0; k < b.tlen; k++) ints[t++] = b.terms[k];
+      e++;
+    }
+  }
+  ptr[N] = (int32_t)e;
+  int rc = ctx->bound_buf.ensure(total);
+  if (rc) return rc;
+  char* d = (char*)ctx->bound_buf.p;
+  HIP_TRY(hipMemcpyAsync(d, h.data(), total, hipMemcpyHostToDevice, ctx->stream));
+  HIP_TRY(hipStreamSynchronize(ctx->stream));
+  DevBound& B = ctx->bound_dev;
+  B.ptr = (const int32_t*)(d + o_ptr);
+  B.id = (const int64_t*)(d + o_id);
+  B.prio = (const int32_t*)(d + o_prio);
+  B.start = (const int64_t*)(d + o_start);
+  B.cls = (const int32_t*)(d + o_cls);
+  B.req = (const int64_t*)(d + o_req);
+  B.toff = (const int32_t*)(d + o_toff);
+  B.tlen = (const int32_t*)(d + o_tlen);
+  B.ints = (const int32_t*)(d + o_ints);
+  ctx->bound_dirty = false;
+  return 0;
+}
+
+}  // namespace
+
+int kss_postfilter_pod(kss_ctx* ctx, const kss_podset* ps, int32_t pod_index, kss_preempt_result* out) {
+  if (!ctx || !ctx->loaded || !ps || !out) return fail(KSS_E_INVAL, "bad arguments");
+  if (pod_index < 0 || pod_index >= ps->n_pods) return fail(KSS_E_INVAL, "pod index out of range");
+  if (out->victims_cap < 0 || (out->victims_cap > 0 && !out->victims)) return fail(KSS_E_INVAL, "bad victims buffer");
+  out->status = KSS_PREEMPT_NO_CANDIDATE;
+  out->nominated = -1;
+  out->n_potential = out->n_candidates = out->n_victims = 0;
+  out->highest_priority = 0;
+  out->sum_priority = out->earliest_start = 0;
+  if (ps->pods[pod_index].flags & KSS_POD_PREEMPT_NEVER) {  // PodEligibleToPreemptOthers
+    out->status = KSS_PREEMPT_NOT_ELIGIBLE;
+    return 0;
+  }
+  OnePod one;
+  int rc = compact_pod(ps, pod_index, one);
+  if (rc) return rc;
+  if ((rc = validate(&ctx->host, &one.ps, 1))) return rc;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  HIP_TRY(hipSetDevice(ctx->cfg.device));
+  rc = upload_podset(ctx->stream, ctx->tmp_pod_buf, &one.ps, ctx->tdp);
+  if (rc) return rc;
+  if (ctx->bound_dirty && (rc = upload_bound(ctx))) return rc;
+  const PlanNeeds need = plan_needs(ctx->key_card_h.data(), ctx->key_flags_h.data(), &one.ps, 1);
+  const int bins_cap = std::max(need.bins_cap, 1);
+  const size_t lds = sizeof(PreHdr) + 8 * (size_t)bins_cap;
+  if (lds > KSS_LDS_BUDGET) return fail(KSS_E_UNSUPPORTED, "the pod's topology histograms exceed LDS");
+  const size_t N = (size_t)ctx->dc.N;
+  const int cap = out->victims_cap;
+  const size_t o_job = 0, o_out = align_up(sizeof(PreemptJob), 256), o_vic = o_out + sizeof(PreemptOut),
+               o_key = align_up(o_vic + 8 * (size_t)std::max(cap, 1), 256), total = o_key + 4 * 8 * std::max(N, (size_t)1);
+  if ((rc = ctx->pre_buf.ensure(total))) return rc;
+  char* d = (char*)ctx->pre_buf.p;
+  PreemptJob J{};
+  J.c = ctx->dc;
+  J.c.nc64 = nullptr;
+  J.c.nct = nullptr;
+  J.c.nc32 = nullptr;
+  J.c.ncl = nullptr;
+  J.P = ctx->tdp;
+  J.B = ctx->bound_dev;
+  J.prof = ctx->prof;
+  J.pi = 0;
+  J.bins_cap = bins_cap;
+  J.victims_cap = cap;
+  J.key = (int64_t*)(d + o_key);
+  J.victims = (int64_t*)(d + o_vic);
+  J.out = (PreemptOut*)(d + o_out);
+  HIP_TRY(hipMemcpyAsync(d + o_job, &J, sizeof(J), hipMemcpyHostToDevice, ctx->stream));
+  hipLaunchKernelGGL(k_preempt, dim3(1), dim3(PRE_THREADS), lds, ctx->stream, (const PreemptJob*)(d + o_job));
+  HIP_TRY(hipGetLastError());
+  const size_t back = sizeof(PreemptOut) + 8 * (size_t)cap;
+  if (ctx->pinned_cap < back) {
+    if (ctx->pinned) hipHostFree(ctx->pinned);
+    ctx->pinned = nullptr;
+    ctx->pinned_cap = 0;
+    HIP_TRY(hipHostMalloc(&ctx->pinned, back));
+    ctx->pinned_cap = back;
+  }
+  HIP_TRY(hipMemcpyAsync(ctx->pinned, d + o_out, back, hipMemcpyDeviceToHost, ctx->stream));
+  HIP_TRY(hipStreamSynchronize(ctx->stream));
+  PreemptOut o;
+  std::memcpy(&o, ctx->pinned, sizeof(o));
+  if (o.status < 0) return fail(KSS_E_UNSUPPORTED, "pod program exceeds the device path's per-pod limits");
+  out->status = o.status;
+  out->nominated = o.nominated;
+  out->n_potential = o.n_potential;
+  out->n_candidates = o.n_candidates;
+  out->n_victims = o.n_victims;
+  out->highest_priority = o.highest_priority;
+  out->sum_priority = o.sum_priority;
+  out->earliest_start = o.earliest_start;
+  if (o.status == KSS_PREEMPT_NOMINATED && cap > 0)
+    std::memcpy(out->victims, (char*)ctx->pinned + sizeof(PreemptOut), 8 * (size_t)std::min(cap, o.n_victims));
+  return 0;
 }
 
 int kss_set_names(kss_ctx* ctx, const kss_names* names) {

@@ -1,0 +1,472 @@
+// kss_preempt.cuh — DefaultPreemption PostFilter dry run of one pod (k_preempt).
+//
+// Restates, for a pod whose filters left no feasible node, Evaluator.Preempt of upstream
+// k8s.io/kubernetes v1.26.2 (pkg/scheduler/framework/preemption/preemption.go) with the
+// DefaultPreemption plugin (plugins/defaultpreemption/default_preemption.go), as the
+// simulator runs it through wrappedPlugin.PostFilter (simulator/scheduler/plugin/
+// wrappedplugin.go:550-577).  The object-level restatement it is tested against is
+// oracle/k8s_preemption.py.
+//
+// One workgroup per pod (the PostFilter call is a per-pod latency path; a cluster of a
+// few thousand nodes is a few node slots per lane):
+//   1. PreFilter state of PodTopologySpread / InterPodAffinity (the same LDS histograms
+//      as k_schedule, kss_sched.cuh stats_node), plus per hard-spread key the two
+//      smallest pair counts with the smallest pair's id (criticalPaths) and the
+//      affinity-count total (len(affinityCounts) == 0);
+//   2. the filter chain per node; nodesWherePreemptionMightHelp keeps the nodes whose
+//      first failure is Unschedulable (NodeResourcesFit, the spread skew, pod
+//      anti-affinity and existing pods' anti-affinity), not UnschedulableAndUnresolvable;
+//   3. SelectVictimsOnNode on each of them, by the lane that owns the node: remove every
+//      lower-priority pod (NodeInfo.RemovePod + the RemovePod extensions: the node's own
+//      pair counts move, the spread minimum becomes min(min over the other pairs, the
+//      node's pair) — criticalPaths.update keeps exactly that minimum when one pair
+//      changes), run the filters, then reprieve in MoreImportantPod order (priority
+//      descending, start time ascending, NodeInfo order on ties), keeping each pod whose
+//      return still lets the pod fit;
+//   4. pickOneNodeForPreemption as successive workgroup reductions over the candidates'
+//      (highest victim priority min, Σ(priority + 2^31) min, #victims min, earliest
+//      start of the highest-priority victims max, node index min) — the last criterion
+//      replaces the Go map order upstream leaves to chance;
+//   5. the owner lane of the nominated node re-runs its reprieve loop and writes the
+//      victims' ids in eviction order.
+// No PodDisruptionBudgets (every victim is non-violating) and no nominated pods.
+#pragma once
+#include "kss_sched.cuh"
+
+namespace kss {
+
+constexpr int PRE_THREADS = 512;
+constexpr int PRE_WAVES = PRE_THREADS / 64;
+
+// Bound pods on the device: CSR by node, NodeInfo.Pods order inside a node.
+struct DevBound {
+  const int32_t* ptr;    // [N + 1]
+  const int64_t* id;     // [nb] caller ids
+  const int32_t* prio;   // [nb]
+  const int64_t* start;  // [nb]
+  const int32_t* cls;    // [nb]
+  const int64_t* req;    // [nb][KSS_NRES]
+  const int32_t* toff;   // [nb] into ints
+  const int32_t* tlen;   // [nb]
+  const int32_t* ints;
+};
+
+struct PreemptOut {
+  int32_t status, nominated, n_potential, n_candidates, n_victims, highest_priority;
+  int64_t sum_priority, earliest_start;
+};
+
+struct PreemptJob {
+  DevCluster c;
+  DevPods P;
+  DevBound B;
+  kss_profile prof;
+  int32_t pi;        // the preemptor's index in P
+  int32_t bins_cap;  // LDS histogram + presence bins
+  int32_t victims_cap;
+  int32_t pad;
+  int64_t* key;      // [4][N] HBM scratch: candidate keys per node
+  int64_t* victims;  // [victims_cap]
+  PreemptOut* out;
+};
+
+struct PreHdr {
+  long long red[PRE_WAVES];
+  kss_pod pod;
+  Plan plan;
+  long long m0[MAXH], id0[MAXH], m1[MAXH];  // per hard owner: smallest pair count, its pair, the next one
+  long long aff_total;
+  long long flags;
+  int plan_ok;
+  int pad[3];
+};
+
+__device__ __forceinline__ long long* pre_bins(long long* smem) { return smem + sizeof(PreHdr) / 8; }
+
+// workgroup reduction (every lane gets the result)
+__device__ __forceinline__ long long block_op(long long v, int op, long long* red) {
+  v = wave_reduce(v, op);
+  const int w = threadIdx.x >> 6;
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[w] = v;
+  __syncthreads();
+  long long r = red[0];
+  for (int i = 1; i < (int)(blockDim.x >> 6); i++) r = op_apply(op, r, red[i]);
+  return r;
+}
+
+__device__ __forceinline__ bool in_list(const int32_t* ints, int off, int len, int v) {
+  for (int i = 0; i < len; i++)
+    if (ints[off + i] == v) return true;
+  return false;
+}
+
+// tpCounts[pair] of node n for hard group owner i: the count of the group's last member
+// admitting n (calPreFilterState), -1 when no member admits n or n lacks a hard key
+__device__ __forceinline__ int64_t group_count(const DevCluster& c, const DevPods& P, const kss_pod& p, const Plan& pl,
+                                               int i, int n) {
+  const kss_spread* sp = P.spreads + p.spread_off;
+  if (!has_keys(c, sp, p.n_hard, n)) return -1;
+  int64_t cnt = -1;
+  for (int j = i; j < p.n_hard; j++)
+    if (pl.hard_own[j] == i && spread_policy_ok(c, P, p, sp[j], n)) cnt = spread_count(c, P, sp[j], n);
+  return cnt;
+}
+
+// The node-local view SelectVictimsOnNode mutates: NodeInfo.Requested / len(Pods), the
+// spread pair count of the node's pair per hard owner, the inter-pod-affinity counts of
+// the node's pairs per (key slot, x|a|b), and the affinity-count total.
+struct DryState {
+  int64_t req[KSS_NRES];
+  int64_t pods;
+  int64_t M[MAXH];
+  int64_t A[MAXK][3];
+  int64_t T;
+};
+
+// RemovePod (sign = -1) / AddPod (+1) of bound pod e on node n, with the RemovePod /
+// AddPod extensions (podtopologyspread / interpodaffinity preFilterState.updateWithPod)
+__device__ __forceinline__ void apply_pod(const PreemptJob& J, const kss_pod& p, const Plan& pl, int e, int n, int sign,
+                                          DryState& s) {
+  const DevCluster& c = J.c;
+  const DevPods& P = J.P;
+  const int nr = 3 + c.n_scalar;
+  for (int r = 0; r < nr; r++) s.req[r] += sign * J.B.req[(size_t)e * KSS_NRES + r];
+  s.pods += sign;
+  const int cls = J.B.cls[e];
+  const kss_spread* sp = P.spreads + p.spread_off;
+  for (int j = 0; j < p.n_hard; j++)  // each matching constraint moves the shared pair counter
+    if (in_list(P.ints, sp[j].cls_off, sp[j].cls_len, cls)) s.M[pl.hard_own[j]] += sign;
+  const kss_ipa* ip = P.ipa + p.ipa_off;
+  for (int q = 0; q < p.ipa_len; q++) {
+    const kss_ipa& en = ip[q];
+    if (en.kind > KSS_IPA_REQ_ANTI) continue;
+    if (label_of(c, en.key, n) < 0) continue;  // topologyToMatchedTermCount.update: node lacks the key
+    const int k = slot_of(pl, en.key);
+    if (en.kind == KSS_IPA_EXISTING_ANTI) {
+      const int t0 = J.B.toff[e], tl = J.B.tlen[e];
+      for (int t = 0; t < tl; t++)
+        if (in_list(P.ints, en.row_off, en.row_len, J.B.ints[t0 + t])) s.A[k][0] += sign;
+    } else if (in_list(P.ints, en.row_off, en.row_len, cls)) {
+      s.A[k][en.kind == KSS_IPA_REQ_AFFINITY ? 1 : 2] += sign;
+      if (en.kind == KSS_IPA_REQ_AFFINITY) s.T += sign;
+    }
+  }
+}
+
+// RunFilterPluginsWithNominatedPods on the modified node: NodeResourcesFit, PodTopologySpread,
+// InterPodAffinity (the node-level filters before them passed: the node is potential)
+__device__ __forceinline__ bool dry_fits(const PreemptJob& J, const kss_pod& p, const Plan& pl, const PreHdr& H,
+                                         const DryState& s, int n) {
+  const DevCluster& c = J.c;
+  const DevPods& P = J.P;
+  const uint32_t en = J.prof.filter_enabled;
+  const size_t N = (size_t)c.N;
+  if ((en >> KSS_F_NODE_RESOURCES_FIT) & 1u) {
+    if (s.pods + 1 > (int64_t)c.allowed_pods[n]) return false;
+    const int nr = 3 + c.n_scalar;
+    bool all_zero = true;
+    for (int r = 0; r < nr; r++) all_zero &= (p.fit_request[r] == 0);
+    if (!all_zero)
+      for (int r = 0; r < nr; r++) {
+        const int64_t q = p.fit_request[r];
+        if (r >= KSS_RES_SCALAR0 && q == 0) continue;
+        if (q > c.alloc[(size_t)r * N + n] - s.req[r]) return false;
+      }
+  }
+  if (((en >> KSS_F_POD_TOPOLOGY_SPREAD) & 1u) && p.n_hard > 0) {
+    const kss_spread* sp = P.spreads + p.spread_off;
+    for (int i = 0; i < p.n_hard; i++) {
+      const int d = label_of(c, sp[i].key, n);
+      if (d < 0) return false;
+      const int o = pl.hard_own[i];
+      const int64_t my = pl.hard_off[o] >= 0 ? (int64_t)d : (int64_t)n;
+      const int64_t others = H.id0[o] == my ? H.m1[o] : H.m0[o];
+      const int64_t mn = s.M[o] < others ? s.M[o] : others;
+      if (s.M[o] + (int64_t)sp[i].self_match - mn > (int64_t)sp[i].max_skew) return false;
+    }
+  }
+  if (((en >> KSS_F_INTER_POD_AFFINITY) & 1u) && p.ipa_len > 0) {
+    const kss_ipa* ip = P.ipa + p.ipa_off;
+    bool have = false, exist = true;
+    for (int q = 0; q < p.ipa_len; q++) {
+      if (ip[q].kind != KSS_IPA_REQ_AFFINITY) continue;
+      have = true;
+      if (label_of(c, ip[q].key, n) < 0) return false;
+      if (s.A[slot_of(pl, ip[q].key)][1] <= 0) exist = false;
+    }
+    if (have && !exist && !(s.T == 0 && (p.flags & KSS_POD_IPA_SELF_MATCH))) return false;
+    for (int q = 0; q < p.ipa_len; q++) {
+      const int kind = ip[q].kind;
+      if (kind != KSS_IPA_REQ_ANTI && kind != KSS_IPA_EXISTING_ANTI) continue;
+      if (label_of(c, ip[q].key, n) < 0) continue;
+      if (s.A[slot_of(pl, ip[q].key)][kind == KSS_IPA_REQ_ANTI ? 2 : 0] > 0) return false;
+    }
+  }
+  return true;
+}
+
+// MoreImportantPod order with NodeInfo order on ties: a before b
+__device__ __forceinline__ bool before(const DevBound& B, int a, int b) {
+  if (B.prio[a] != B.prio[b]) return B.prio[a] > B.prio[b];
+  if (B.start[a] != B.start[b]) return B.start[a] < B.start[b];
+  return a < b;
+}
+
+struct DryResult {
+  int64_t hp, sum, cnt, start;  // hp = INT64_MAX: not a candidate
+};
+
+// SelectVictimsOnNode for node n; emit: write the victims' ids (the nominated node)
+__device__ __forceinline__ DryResult select_victims(const PreemptJob& J, const kss_pod& p, const Plan& pl,
+                                                    const PreHdr& H, const long long* bins, int n, bool emit) {
+  const DevCluster& c = J.c;
+  const DevPods& P = J.P;
+  const DevBound& B = J.B;
+  DryResult res{INT64_MAX, 0, 0, 0};
+  const int e0 = B.ptr[n], e1 = B.ptr[n + 1];
+  const int prio = p.priority;
+  int nv = 0;
+  for (int e = e0; e < e1; e++) nv += B.prio[e] < prio;
+  if (nv == 0) return res;  // "No preemption victims found for incoming pod"
+  // the node's view, then every lower-priority pod removed
+  DryState s;
+  const size_t N = (size_t)c.N;
+  for (int r = 0; r < KSS_NRES; r++) s.req[r] = r < 3 + c.n_scalar ? c.requested[(size_t)r * N + n] : 0;
+  s.pods = c.pod_count[n];
+  const kss_spread* sp = P.spreads + p.spread_off;
+#pragma unroll
+  for (int i = 0; i < MAXH; i++) s.M[i] = 0;
+  for (int i = 0; i < p.n_hard; i++) {
+    if (pl.hard_own[i] != i) continue;
+    if (pl.hard_off[i] >= 0) {
+      const int d = label_of(c, sp[i].key, n);
+      s.M[i] = d >= 0 ? bins[pl.hard_off[i] + d] : 0;
+    } else {
+      const int64_t g = group_count(c, P, p, pl, i, n);
+      s.M[i] = g > 0 ? g : 0;
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < MAXK; k++)
+#pragma unroll
+    for (int h = 0; h < 3; h++) s.A[k][h] = 0;
+  for (int k = 0; k < pl.n_keys; k++) {
+    const int d = label_of(c, pl.key[k], n);
+    if (d < 0) continue;
+    for (int h = 0; h < 3; h++) s.A[k][h] = ipa_value(c, P, p, pl, bins, k, h, d, n);
+  }
+  s.T = H.aff_total;
+  for (int e = e0; e < e1; e++)
+    if (B.prio[e] < prio) apply_pod(J, p, pl, e, n, -1, s);
+  if (!dry_fits(J, p, pl, H, s, n)) return res;
+  // reprieve in importance order: the next pod is the least one after `last`
+  int last = -1, victims = 0;
+  int64_t hp = 0, sum = 0, st = 0;
+  for (int k = 0; k < nv; k++) {
+    int best = -1;
+    for (int e = e0; e < e1; e++) {
+      if (B.prio[e] >= prio) continue;
+      if (last >= 0 && !before(B, last, e)) continue;
+      if (best < 0 || before(B, e, best)) best = e;
+    }
+    last = best;
+    apply_pod(J, p, pl, best, n, 1, s);
+    if (!dry_fits(J, p, pl, H, s, n)) {
+      apply_pod(J, p, pl, best, n, -1, s);
+      if (victims == 0) {
+        hp = B.prio[best];
+        st = B.start[best];  // the earliest start among the highest-priority victims
+      }
+      if (emit && victims < J.victims_cap) J.victims[victims] = B.id[best];
+      sum += (int64_t)B.prio[best] + 2147483648ll;
+      victims++;
+    }
+  }
+  if (victims == 0) return res;  // upstream: an error status ("expected at least one victim")
+  res.hp = hp;
+  res.sum = sum;
+  res.cnt = victims;
+  res.start = st;
+  return res;
+}
+
+__device__ __forceinline__ bool resolvable(int f, int detail) {
+  if (f == KSS_F_NODE_RESOURCES_FIT || f == KSS_F_NODE_PORTS) return true;
+  if (f == KSS_F_POD_TOPOLOGY_SPREAD) return detail == KSS_PTS_CONSTRAINTS_NOT_MATCH;
+  if (f == KSS_F_INTER_POD_AFFINITY) return detail != KSS_IPA_AFFINITY;
+  return false;
+}
+
+__device__ void preempt_pod(const PreemptJob& J, long long* smem) {
+  const int tid = threadIdx.x, nt = blockDim.x;
+  PreHdr& H = *reinterpret_cast<PreHdr*>(smem);
+  const DevCluster& c = J.c;
+  const DevPods& P = J.P;
+  {
+    constexpr int PD = (int)(sizeof(kss_pod) / 4);
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(P.pods + J.pi);
+    uint32_t* dst = reinterpret_cast<uint32_t*>(&H.pod);
+    for (int i = tid; i < PD; i += nt) dst[i] = src[i];
+    if (tid == 0) H.plan_ok = make_plan(c, P, P.pods[J.pi], H.plan, J.bins_cap) ? 1 : 0;
+    __syncthreads();
+  }
+  const kss_pod& p = H.pod;
+  const Plan& pl = H.plan;
+  PreemptOut& out = *J.out;
+  if (!H.plan_ok || p.prefilter_status != 0) {
+    // a PreFilter failure gives every node UnschedulableAndUnresolvable: nothing to dry-run
+    if (tid == 0) {
+      out.status = !H.plan_ok ? -1 : KSS_PREEMPT_NO_CANDIDATE;
+      out.nominated = -1;
+      out.n_potential = out.n_candidates = out.n_victims = 0;
+    }
+    return;
+  }
+  long long* bins = pre_bins(smem);
+  long long* pres = bins + pl.total_bins;
+  const int N = c.N;
+  // ---- 1. PreFilter state --------------------------------------------------
+  long long hard_min[MAXH];
+#pragma unroll
+  for (int i = 0; i < MAXH; i++) hard_min[i] = INT32_MAX;
+  long long flags = 0, aff = 0;
+  for (int b = tid; b < pl.total_bins + pl.total_pbins; b += nt) bins[b] = 0;
+  __syncthreads();
+  const kss_ipa* ip = P.ipa + p.ipa_off;
+  if (pl.need_stats) {
+    for (int n = tid; n < N; n += nt) {
+      stats_node(c, P, p, pl, bins, pres, n, hard_min, flags);
+      for (int q = 0; q < p.ipa_len; q++)
+        if (ip[q].kind == KSS_IPA_REQ_AFFINITY && label_of(c, ip[q].key, n) >= 0)
+          aff += sum_rows(c.class_count, (size_t)N, P.ints + ip[q].row_off, ip[q].row_len, n);
+    }
+  }
+  flags = block_op(flags, OP_OR, H.red);
+  aff = block_op(aff, OP_SUM, H.red);
+  // criticalPaths per hard owner: (count << 24 | pair) minimum, then the minimum of the others
+  const kss_spread* sp = P.spreads + p.spread_off;
+  for (int i = 0; i < p.n_hard; i++) {
+    if (pl.hard_own[i] != i) continue;
+    const bool hist = pl.hard_off[i] >= 0;
+    const int span = hist ? c.key_card[sp[i].key] + 1 : N;
+    long long best = INT64_MAX;
+    for (int x = tid; x < span; x += nt) {
+      const long long v = hist ? (pres[pl.hard_poff[i] + x] ? bins[pl.hard_off[i] + x] : -1)
+                               : (long long)group_count(c, P, p, pl, i, x);
+      if (v >= 0) best = min(best, (v << 24) | x);
+    }
+    best = block_op(best, OP_MIN, H.red);
+    const long long id0 = best == INT64_MAX ? -1 : (best & 0xFFFFFF);
+    long long second = INT64_MAX;
+    for (int x = tid; x < span; x += nt) {
+      if (x == id0) continue;
+      const long long v = hist ? (pres[pl.hard_poff[i] + x] ? bins[pl.hard_off[i] + x] : -1)
+                               : (long long)group_count(c, P, p, pl, i, x);
+      if (v >= 0) second = min(second, v);
+    }
+    second = block_op(second, OP_MIN, H.red);
+    if (tid == 0) {
+      H.m0[i] = best == INT64_MAX ? INT32_MAX : (best >> 24);
+      H.id0[i] = id0;
+      H.m1[i] = second == INT64_MAX ? INT32_MAX : second;
+    }
+  }
+  if (tid == 0) {
+    H.aff_total = aff;
+    H.flags = flags;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < MAXH; i++)
+    if (i < p.n_hard) hard_min[i] = H.m0[pl.hard_own[i]];
+  // ---- 2 + 3. filters, potential nodes, SelectVictimsOnNode ------------------
+  const uint32_t en = J.prof.filter_enabled;
+  const bool restrict_names = p.names_len >= 0;
+  long long n_pot = 0, n_cand = 0, feasible = 0;
+  int64_t* K = J.key;
+  for (int n = tid; n < N; n += nt) {
+    K[n] = INT64_MAX;
+    if (restrict_names && !in_names(P, p, (int64_t)c.node_base + n)) {
+      n_pot++;  // no status in the map: potential, but NodeAffinity rejects it in the dry run
+      continue;
+    }
+    uint16_t detail = 0;
+    const NodeRow row = load_row(c, n);
+    int f = filter_local(c, P, p, en, n, row, &detail);
+    if (!f && ((en >> KSS_F_POD_TOPOLOGY_SPREAD) & 1u) && p.n_hard > 0) {
+      const int r = filter_pts(c, P, p, pl, bins, hard_min, n);
+      if (r) {
+        f = KSS_F_POD_TOPOLOGY_SPREAD;
+        detail = (uint16_t)(r - 1);
+      }
+    }
+    if (!f && ((en >> KSS_F_INTER_POD_AFFINITY) & 1u) && p.ipa_len > 0) {
+      const int r = filter_ipa(c, P, p, pl, bins, H.flags, n);
+      if (r) {
+        f = KSS_F_INTER_POD_AFFINITY;
+        detail = (uint16_t)(r - 1);
+      }
+    }
+    if (!f) {
+      feasible++;
+      continue;
+    }
+    if (!resolvable(f, detail)) continue;
+    n_pot++;
+    const DryResult d = select_victims(J, p, pl, H, bins, n, false);
+    if (d.hp == INT64_MAX) continue;
+    n_cand++;
+    K[n] = d.hp;
+    K[N + n] = d.sum;
+    K[2 * (size_t)N + n] = d.cnt;
+    K[3 * (size_t)N + n] = d.start;
+  }
+  feasible = block_op(feasible, OP_SUM, H.red);
+  n_pot = block_op(n_pot, OP_SUM, H.red);
+  n_cand = block_op(n_cand, OP_SUM, H.red);
+  if (feasible || n_cand == 0) {
+    if (tid == 0) {
+      out.status = feasible ? KSS_PREEMPT_SCHEDULABLE : KSS_PREEMPT_NO_CANDIDATE;
+      out.nominated = -1;
+      out.n_potential = (int32_t)n_pot;
+      out.n_candidates = (int32_t)n_cand;
+      out.n_victims = 0;
+    }
+    return;
+  }
+  // ---- 4. pickOneNodeForPreemption -------------------------------------------
+  long long v = INT64_MAX;
+  for (int n = tid; n < N; n += nt) v = min(v, (long long)K[n]);
+  const long long hp = block_op(v, OP_MIN, H.red);
+  v = INT64_MAX;
+  for (int n = tid; n < N; n += nt)
+    if (K[n] == hp) v = min(v, (long long)K[N + n]);
+  const long long sum = block_op(v, OP_MIN, H.red);
+  v = INT64_MAX;
+  for (int n = tid; n < N; n += nt)
+    if (K[n] == hp && K[N + n] == sum) v = min(v, (long long)K[2 * (size_t)N + n]);
+  const long long cnt = block_op(v, OP_MIN, H.red);
+  v = INT64_MIN;
+  for (int n = tid; n < N; n += nt)
+    if (K[n] == hp && K[N + n] == sum && K[2 * (size_t)N + n] == cnt) v = max(v, (long long)K[3 * (size_t)N + n]);
+  const long long st = block_op(v, OP_MAX, H.red);
+  v = INT64_MAX;
+  for (int n = tid; n < N; n += nt)
+    if (K[n] == hp && K[N + n] == sum && K[2 * (size_t)N + n] == cnt && K[3 * (size_t)N + n] == st) v = min(v, (long long)n);
+  const long long best = block_op(v, OP_MIN, H.red);
+  // ---- 5. the nominated node's victims, by its owner lane --------------------
+  if ((int)(best % nt) == tid) {
+    const DryResult d = select_victims(J, p, pl, H, bins, (int)best, true);
+    out.status = KSS_PREEMPT_NOMINATED;
+    out.nominated = (int32_t)(c.node_base + best);
+    out.n_potential = (int32_t)n_pot;
+    out.n_candidates = (int32_t)n_cand;
+    out.n_victims = (int32_t)d.cnt;
+    out.highest_priority = (int32_t)d.hp;
+    out.sum_priority = d.sum;
+    out.earliest_start = d.start;
+  }
+}
+
+}  // namespace kss

@@ -90,6 +90,13 @@ KSS_POD_PTS_REQUIRE_ALL = 1 << 2
 KSS_POD_IPA_SELF_MATCH = 1 << 3
 KSS_POD_IPA_HAS_PREFERRED = 1 << 4
 KSS_POD_PTS_SCORE_STATE = 1 << 5
+KSS_POD_PREEMPT_NEVER = 1 << 6
+
+KSS_START_UNSET = 2**63 - 1
+KSS_PREEMPT_NOMINATED = 0
+KSS_PREEMPT_NO_CANDIDATE = 1
+KSS_PREEMPT_NOT_ELIGIBLE = 2
+KSS_PREEMPT_SCHEDULABLE = 3
 
 KSS_FIT_LEAST_ALLOCATED = 0
 KSS_FIT_MOST_ALLOCATED = 1
@@ -139,7 +146,7 @@ class Pod(C.Structure):
         ("node_name", i32), ("flags", u32), ("sel_off", i32), ("sel_len", i32), ("aff_off", i32), ("aff_len", i32),
         ("pref_off", i32), ("pref_len", i32), ("spread_off", i32), ("n_hard", i32), ("n_soft", i32),
         ("ipa_off", i32), ("ipa_len", i32), ("cls", i32), ("own_terms_off", i32), ("own_terms_len", i32),
-        ("prefilter_status", i32), ("names_off", i32), ("names_len", i32), ("pad", i32 * 2),
+        ("prefilter_status", i32), ("names_off", i32), ("names_len", i32), ("priority", i32), ("pad", i32),
     ]
 
 
@@ -169,6 +176,18 @@ class Config(C.Structure):
 class Names(C.Structure):
     _fields_ = [("node_names", P(C.c_char_p)), ("taint_keys", P(C.c_char_p)), ("taint_values", P(C.c_char_p)),
                 ("scalar_names", P(C.c_char_p))]
+
+
+class Boundset(C.Structure):
+    _fields_ = [("n", i32), ("n_ints", i32), ("id", P(i64)), ("node", P(i32)), ("priority", P(i32)),
+                ("start", P(i64)), ("cls", P(i32)), ("req", P(i64)), ("terms_off", P(i32)), ("terms_len", P(i32)),
+                ("ints", P(i32))]
+
+
+class PreemptResult(C.Structure):
+    _fields_ = [("status", i32), ("nominated", i32), ("n_potential", i32), ("n_candidates", i32),
+                ("n_victims", i32), ("victims_cap", i32), ("victims", P(i64)), ("highest_priority", i32),
+                ("pad", i32), ("sum_priority", i64), ("earliest_start", i64)]
 
 
 class Synth(C.Structure):

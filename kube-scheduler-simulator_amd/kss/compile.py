@@ -84,6 +84,29 @@ def zone_key(node) -> str:
     return region + ":\x00:" + zone
 
 
+def pod_priority(p) -> int:
+    """corev1helpers.PodPriority: spec.priority (the Priority admission plugin resolves
+    priorityClassName into it), 0 when unset."""
+    v = spec(p).get("priority")
+    if v is None:
+        return 0
+    v = int(v)
+    if not -(2**31) <= v < 2**31:
+        raise CompileError(f"priority {v} out of int32 range")
+    return v
+
+
+def pod_start(p) -> int:
+    """status.startTime (RFC 3339, seconds) as Unix nanoseconds; KSS_START_UNSET when unset
+    (GetPodStartTime falls back to time.Now(): later than any recorded start)."""
+    st = (p.get("status") or {}).get("startTime")
+    if not st:
+        return abi.KSS_START_UNSET
+    from datetime import datetime, timezone
+    t = datetime.strptime(st, "%Y-%m-%dT%H:%M:%SZ").replace(tzinfo=timezone.utc)
+    return int(t.timestamp()) * 10**9
+
+
 def node_tree_order(nodes: Sequence[dict]) -> List[int]:
     """internal/cache nodeTree: zones in first-seen order, round-robin, insertion order within a zone."""
     zones: List[str] = []
@@ -327,6 +350,8 @@ class CompiledCluster:
     terms: List[Tuple[str, int, AffinityTerm]]   # (kind, weight, term)
     arrays: Dict[str, np.ndarray]
     namespaces: Dict[str, Dict[str, str]]
+    bound: Dict[str, np.ndarray] = field(default_factory=dict)     # the kss_boundset arrays
+    bound_names: List[Tuple[str, str]] = field(default_factory=list)  # (namespace, name) per bound id
     _keep: list = field(default_factory=list)
 
     @property
@@ -352,6 +377,18 @@ class CompiledCluster:
                          ("term_count", abi.i32)):
             setattr(c, name, abi.ptr(a[name], ct))
         return c
+
+    def as_boundset(self) -> abi.Boundset:
+        """The bound pods (NodeInfo.Pods order per node) for the PostFilter dry run."""
+        b = self.bound
+        s = abi.Boundset()
+        s.n = len(self.bound_names)
+        s.n_ints = int(sum(int(x) for x in b["terms_len"][:s.n]))
+        for name, ct in (("id", abi.i64), ("node", abi.i32), ("priority", abi.i32), ("start", abi.i64),
+                         ("cls", abi.i32), ("req", abi.i64), ("terms_off", abi.i32), ("terms_len", abi.i32),
+                         ("ints", abi.i32)):
+            setattr(s, name, abi.ptr(b[name], ct))
+        return s
 
 
 @dataclass
@@ -573,12 +610,25 @@ class Compiler:
         pod_count = np.zeros(N, dtype=np.int32)
         class_count = np.zeros((len(classes), N), dtype=np.int32)
         term_count = np.zeros((len(terms), N), dtype=np.int32)
+        bt = dict(id=[], node=[], priority=[], start=[], cls=[], req=[], terms_off=[], terms_len=[], ints=[])
+        bound_names = []
         for p in self.bound:
             nn = spec(p).get("nodeName")
             if nn not in self.node_index:
                 continue  # pods bound to unknown nodes are not in any NodeInfo
             i = self.node_index[nn]
             req = compute_pod_resource_request(p, scalars)
+            own = self._own_terms(p)
+            bt["id"].append(len(bound_names))
+            bt["node"].append(i)
+            bt["priority"].append(pod_priority(p))
+            bt["start"].append(pod_start(p))
+            bt["cls"].append(self.class_index[self._class_key(p)])
+            bt["req"].append(req)
+            bt["terms_off"].append(len(bt["ints"]))
+            bt["terms_len"].append(len(own))
+            bt["ints"].extend(own)
+            bound_names.append((ns_of(p), name_of(p)))
             requested[:, i] += np.array(req, dtype=np.int64)
             c0, m0 = calculate_nonzero(p)
             nonzero[0, i] += c0
@@ -595,9 +645,17 @@ class Compiler:
                       value_is_int=np.array(visint, dtype=np.uint8), class_count=class_count, term_count=term_count)
         arrays = {k: (np.zeros(1, dtype=v.dtype) if v.size == 0 else np.ascontiguousarray(v))
                   for k, v in arrays.items()}
+        nb = len(bound_names)
+        bound = dict(id=np.array(bt["id"], dtype=np.int64), node=np.array(bt["node"], dtype=np.int32),
+                     priority=np.array(bt["priority"], dtype=np.int32), start=np.array(bt["start"], dtype=np.int64),
+                     cls=np.array(bt["cls"], dtype=np.int32),
+                     req=np.ascontiguousarray(np.array(bt["req"], dtype=np.int64).reshape(nb, abi.KSS_NRES).T),
+                     terms_off=np.array(bt["terms_off"], dtype=np.int32),
+                     terms_len=np.array(bt["terms_len"], dtype=np.int32), ints=np.array(bt["ints"], dtype=np.int32))
+        bound = {k: (np.zeros(1, dtype=v.dtype) if v.size == 0 else np.ascontiguousarray(v)) for k, v in bound.items()}
         self.cc = CompiledCluster(node_names=names, order=order, scalars=scalars, label_keys=label_keys,
                                   key_values=key_values, taints=taints, classes=classes, terms=terms, arrays=arrays,
-                                  namespaces=self.namespaces)
+                                  namespaces=self.namespaces, bound=bound, bound_names=bound_names)
         self.node_labels = node_labels
         self.key_flags = key_flags
         pods = self._compile_pods(self.pending)
@@ -813,6 +871,9 @@ class Compiler:
         flags |= self._spread_flags
         self._compile_ipa(p, rec)
         flags |= self._ipa_flags
+        if (spec(p).get("preemptionPolicy") or "") == "Never":
+            flags |= abi.KSS_POD_PREEMPT_NEVER
+        rec["priority"] = pod_priority(p)
         rec["flags"] = flags
         rec["cls"] = self.class_index[self._class_key(p)]
         own = self._own_terms(p)

@@ -69,6 +69,8 @@ SIGNATURES = [
     ("kss_format_pod_annotations_ex", C.c_int, [P(abi.Names), P(abi.Profile), P(abi.PodSet), C.c_int32,
                                                 P(abi.PodResult), C.c_int32, C.c_int32, C.c_int32, C.c_char_p,
                                                 C.c_size_t, P(C.c_size_t)]),
+    ("kss_load_bound", C.c_int, [C.c_void_p, P(abi.Boundset)]),
+    ("kss_postfilter_pod", C.c_int, [C.c_void_p, P(abi.PodSet), C.c_int32, P(abi.PreemptResult)]),
     ("kss_stage_pods", C.c_int, [C.c_void_p, P(abi.PodSet)]),
     ("kss_run_staged", C.c_int, [C.c_void_p, C.c_int32, C.c_uint32, P(C.c_int32)]),
     ("kss_reset_node_state", C.c_int, [C.c_void_p]),
@@ -271,6 +273,23 @@ class Context:
         r = PodResult(self.n_nodes)
         check(lib().kss_eval_pod(self.h, C.byref(podset_struct), i, C.byref(r.s)))
         return r
+
+    def load_bound(self, boundset_struct: abi.Boundset):
+        """The bound pods the PostFilter dry run may evict (CompiledCluster.as_boundset())."""
+        check(lib().kss_load_bound(self.h, C.byref(boundset_struct)))
+
+    def postfilter_pod(self, podset_struct: abi.PodSet, i: int, victims_cap: int = 1024) -> dict:
+        """DefaultPreemption PostFilter dry run of pod i on the current snapshot: status
+        (KSS_PREEMPT_*), the nominated node (-1), the victims' bound ids in eviction order and
+        the pickOneNodeForPreemption criteria of the nominated node."""
+        vic = np.zeros(max(victims_cap, 1), np.int64)
+        r = abi.PreemptResult()
+        r.victims_cap = victims_cap
+        r.victims = vic.ctypes.data_as(P(C.c_int64))
+        check(lib().kss_postfilter_pod(self.h, C.byref(podset_struct), i, C.byref(r)))
+        return dict(status=r.status, nominated=r.nominated, n_potential=r.n_potential, n_candidates=r.n_candidates,
+                    victims=[int(v) for v in vic[:min(r.n_victims, victims_cap)]], n_victims=r.n_victims,
+                    highest_priority=r.highest_priority, sum_priority=r.sum_priority, earliest_start=r.earliest_start)
 
     def fetch_record(self, i: int) -> PodResult:
         r = PodResult(self.n_nodes)

@@ -284,6 +284,37 @@ class NodeInfo:
         self.nz_mem += m0
         self.pods.append(PodInfo(pod))
 
+    def remove_pod(self, pod):
+        """NodeInfo.RemovePod: resources back, removeFromSlice (swap with the last element)."""
+        for i, pi in enumerate(self.pods):
+            if pi.pod is pod:
+                self.pods[i] = self.pods[-1]
+                self.pods.pop()
+                break
+        else:
+            raise KeyError("pod not on node")
+        res, c0, m0 = calculate_resource(pod)
+        self.requested.milli_cpu -= res.milli_cpu
+        self.requested.memory -= res.memory
+        self.requested.ephemeral -= res.ephemeral
+        for k, v in res.scalars.items():
+            self.requested.scalars[k] = self.requested.scalars.get(k, 0) - v
+        self.nz_cpu -= c0
+        self.nz_mem -= m0
+
+    def clone(self):
+        c = NodeInfo.__new__(NodeInfo)
+        c.node = self.node
+        c.pods = list(self.pods)
+        c.requested = Resource()
+        c.requested.milli_cpu, c.requested.memory = self.requested.milli_cpu, self.requested.memory
+        c.requested.ephemeral = self.requested.ephemeral
+        c.requested.scalars = dict(self.requested.scalars)
+        c.requested.allowed_pods = self.requested.allowed_pods
+        c.nz_cpu, c.nz_mem = self.nz_cpu, self.nz_mem
+        c.allocatable = self.allocatable
+        return c
+
 
 def zone_key(node):
     lb = _labels(node)
@@ -801,6 +832,42 @@ class Oracle:
                     process(t, w, pod, nsl, node, -1)
         return topo
 
+    # ----------------------------------------------------------- runFilterPlugins
+    def filter_node(self, pod, ni: NodeInfo, pts_st, ipa_st):
+        """framework.RunFilterPlugins over one NodeInfo: (first failing plugin or None, the
+        per-plugin record up to it)."""
+        node = ni.node
+        sp = _spec(pod)
+        tols = sp.get("tolerations") or []
+        rec = {}
+        for pl in FILTERS:
+            msg = None
+            if pl == "NodeUnschedulable":
+                tol = tolerations_tolerate(tols, {"key": "node.kubernetes.io/unschedulable", "effect": "NoSchedule"})
+                if _spec(node).get("unschedulable") and not tol:
+                    msg = MSG["NodeUnschedulable"]
+            elif pl == "NodeName":
+                nn = sp.get("nodeName") or ""
+                if nn and nn != _name(node):
+                    msg = MSG["NodeName"]
+            elif pl == "TaintToleration":
+                t = find_untolerated(_spec(node).get("taints"), tols, _do_not_schedule)
+                if t is not None:
+                    msg = "node(s) had untolerated taint {%s: %s}" % (t.get("key", ""), t.get("value") or "")
+            elif pl == "NodeAffinity":
+                if not required_node_affinity_match(pod, node):
+                    msg = MSG["NodeAffinity"]
+            elif pl == "NodeResourcesFit":
+                msg = self.fit_filter(pod, ni)
+            elif pl == "PodTopologySpread":
+                msg = self.pts_filter(pts_st, pod, node)
+            elif pl == "InterPodAffinity":
+                msg = self.ipa_filter(ipa_st, pod, node)
+            rec[pl] = "passed" if msg is None else msg
+            if msg is not None:
+                return pl, rec
+        return None, rec
+
     # ----------------------------------------------------------- schedulePod
     def schedule_one(self, pod, commit=True):
         ann_filter: Dict[str, Dict[str, str]] = {}
@@ -840,41 +907,14 @@ class Oracle:
             res["prefilter_result"]["NodeAffinity"] = sorted(node_subset)
         pts_st = self.pts_prefilter(pod)
         ipa_st = self.ipa_prefilter(pod)
+        res["_pts_st"], res["_ipa_st"] = pts_st, ipa_st  # the cycle state PostFilter sees
         feasible = []
         tols = sp.get("tolerations") or []
         for i, ni in enumerate(self.infos):
             node = ni.node
             if node_subset is not None and _name(node) not in node_subset:
                 continue
-            rec = {}
-            failed = None
-            for pl in FILTERS:
-                msg = None
-                if pl == "NodeUnschedulable":
-                    tol = tolerations_tolerate(tols, {"key": "node.kubernetes.io/unschedulable", "effect": "NoSchedule"})
-                    if _spec(node).get("unschedulable") and not tol:
-                        msg = MSG["NodeUnschedulable"]
-                elif pl == "NodeName":
-                    nn = sp.get("nodeName") or ""
-                    if nn and nn != _name(node):
-                        msg = MSG["NodeName"]
-                elif pl == "TaintToleration":
-                    t = find_untolerated(_spec(node).get("taints"), tols, _do_not_schedule)
-                    if t is not None:
-                        msg = "node(s) had untolerated taint {%s: %s}" % (t.get("key", ""), t.get("value") or "")
-                elif pl == "NodeAffinity":
-                    if not required_node_affinity_match(pod, node):
-                        msg = MSG["NodeAffinity"]
-                elif pl == "NodeResourcesFit":
-                    msg = self.fit_filter(pod, ni)
-                elif pl == "PodTopologySpread":
-                    msg = self.pts_filter(pts_st, pod, node)
-                elif pl == "InterPodAffinity":
-                    msg = self.ipa_filter(ipa_st, pod, node)
-                rec[pl] = "passed" if msg is None else msg
-                if msg is not None:
-                    failed = pl
-                    break
+            failed, rec = self.filter_node(pod, ni, pts_st, ipa_st)
             ann_filter[_name(node)] = rec
             res["fail"][i] = failed
             if failed is None:
@@ -967,17 +1007,20 @@ class Oracle:
         return res
 
     # ----------------------------------------------------------- annotations
-    def annotations(self, res) -> Dict[str, str]:
-        """store.GetStoredResult for a pod scheduled by the default profile (bind assumed successful)."""
+    def annotations(self, res, nominated: Optional[int] = None) -> Dict[str, str]:
+        """store.GetStoredResult for a pod scheduled by the default profile (bind assumed successful).
+        `nominated`: the node DefaultPreemption nominated (k8s_preemption.preempt), if any."""
         sel = self.nodes[res["selected"]] if res["selected"] is not None else None
         post = {}
         if sel is None:
             # FitError -> RunPostFilterPlugins: DefaultPreemption (wrapped) records every node of the
-            # NodeToStatusMap with no nomination (equal priorities: no victims) -> {} per node.
+            # NodeToStatusMap, the nominated one with PostFilterNominatedMessage (store.go:436-456).
             if res["status"] == "prefilter":
                 post = {_name(n): {} for n in self.nodes}
             else:
                 post = {nm: {} for nm in res["filter"]}
+            if nominated is not None:
+                post[_name(self.nodes[nominated])] = {"DefaultPreemption": "preemption victim"}
         out = {
             "scheduler-simulator/prefilter-result": go_json(res["prefilter_result"]),
             "scheduler-simulator/prefilter-result-status": go_json(res["prefilter_status"]),

@@ -1,0 +1,74 @@
+"""DefaultPreemption PostFilter dry run: the object-level restatement
+(oracle/k8s_preemption.py) against hand-derived expectations (tests/preempt_fixtures.py),
+the annotation it produces, and the compiled bound-pod table the device path uses."""
+import json
+
+import numpy as np
+import pytest
+
+import k8s_oracle as ko
+import k8s_preemption as kp
+import preempt_fixtures as pf
+from kss import abi
+from kss.compile import compile_cluster
+
+
+def test_oracle_matches_hand_derived():
+    nodes, bound, pods, expect = pf.fixture()
+    o = ko.Oracle(nodes, bound)
+    for p, (status, node, victims) in zip(pods, expect):
+        r = o.schedule_one(p)
+        pre = kp.preempt(o, p, r)
+        got_node = ko._name(o.nodes[pre["nominated"]]) if pre["nominated"] is not None else None
+        assert (pre["status"], got_node, [v[1] for v in pre["victims"]]) == (status, node, victims), p["metadata"]["name"]
+
+
+def test_nominated_annotation():
+    """store.go:436-456: every node of the status map, the nominated one with
+    {"DefaultPreemption": "preemption victim"}."""
+    nodes, bound, pods, _ = pf.fixture()
+    o, out = kp.schedule_with_preemption(nodes, bound, pods[:1])
+    r, pre, ann = out[0]
+    post = json.loads(ann["scheduler-simulator/postfilter-result"])
+    assert post["a"] == {"DefaultPreemption": kp.NOMINATED_MESSAGE}
+    assert post["b"] == {} and set(post) == set(r["filter"])
+    assert ann["scheduler-simulator/selected-node"] == ""
+
+
+def test_prefilter_failure_has_no_candidate():
+    nodes, bound, pods, _ = pf.fixture()
+    p = pf.pod("conflict", 10, "100m", affinity={"nodeAffinity": {"requiredDuringSchedulingIgnoredDuringExecution": {
+        "nodeSelectorTerms": [{"matchFields": [{"key": "metadata.name", "operator": "In", "values": ["a"]},
+                                               {"key": "metadata.name", "operator": "In", "values": ["b"]}]}]}}})
+    o = ko.Oracle(nodes, bound)
+    r = o.schedule_one(p)
+    assert r["status"] == "prefilter"
+    assert kp.preempt(o, p, r)["status"] == "no_candidate"
+
+
+def test_compiled_bound_table_matches_node_state():
+    nodes, bound, pods = pf.saturated(3, 40, 20)
+    cc, cp, _ = compile_cluster(nodes, bound, pods)
+    b = cc.bound
+    n = len(cc.bound_names)
+    assert n == len(bound)
+    np.testing.assert_array_equal(np.bincount(b["node"][:n], minlength=cc.n_nodes), cc.arrays["pod_count"])
+    req = np.zeros_like(cc.arrays["requested"])
+    for i in range(n):
+        req[:, b["node"][i]] += b["req"][:, i]
+    np.testing.assert_array_equal(req, cc.arrays["requested"])
+    assert set(b["priority"][:n]) <= {0, 10, 100, 1000}
+    assert (b["start"][:n] == abi.KSS_START_UNSET).any() and (b["start"][:n] != abi.KSS_START_UNSET).any()
+    assert set(int(x) for x in cp.pods["priority"]) <= {0, 10, 100, 1000, 5000}
+    never = [bool(p["spec"].get("preemptionPolicy") == "Never") for p in pods]
+    assert [bool(f & abi.KSS_POD_PREEMPT_NEVER) for f in cp.pods["flags"]] == never
+
+
+@pytest.mark.parametrize("seed", [1, 2])
+def test_saturated_clusters_nominate(seed):
+    """The fuzz generator the GPU parity test uses reaches nominations, FitErrors and
+    not-eligible pods."""
+    nodes, bound, pods = pf.saturated(seed, 60, 40)
+    o, out = kp.schedule_with_preemption(nodes, bound, pods)
+    kinds = {pre["status"] for _, pre, _ in out if pre}
+    assert "nominated" in kinds and "no_candidate" in kinds
