@@ -622,6 +622,7 @@ enum {
   GP_COMMIT,
   GP_RECORD,
   GP_IPA,
+  GP_SCALAR,
   GP_NCODES
 };
 const char* const kGpReason[GP_NCODES] = {
@@ -637,6 +638,7 @@ const char* const kGpReason[GP_NCODES] = {
     "the commit adds to more than 8 count rows",
     "a pod's record exceeds 2 KiB (too many references)",
     "more than 16 inter-pod-affinity entries after merging",
+    "extended (scalar) resources in the cluster: k_simple / k_spread keep cpu, memory and ephemeral-storage only",
 };
 
 bool gfail(GpodNeeds& need, int code, int pod) {
@@ -2759,6 +2761,10 @@ int kss_plan_podset(const kss_cluster* cl, const kss_podset* ps, int32_t* out3) 
   out3[0] = 0;
   out3[1] = -1;
   out3[2] = GP_OK;
+  if (cl->n_scalar > 0) {  // run_single: simple_ok / spread_ok need dc.n_scalar == 0
+    out3[2] = GP_SCALAR;
+    return 0;
+  }
   if (build_spods(ps, cl->n_scalar, sp)) {
     out3[0] = 1;
     return 0;

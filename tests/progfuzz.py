@@ -37,7 +37,7 @@ R_GPU = "example.com/gpu"
 APPS = 6
 
 
-def _node(i: int, r: random.Random) -> dict:
+def _node(i: int, r: random.Random, extended: bool = True) -> dict:
     name = "n%05d" % i
     labels: Dict[str, str] = {}
     if r.random() >= 0.02:
@@ -66,7 +66,7 @@ def _node(i: int, r: random.Random) -> dict:
         spec["unschedulable"] = True
     alloc = {"cpu": str(cores), "memory": "%dGi" % (cores * 4),
              "ephemeral-storage": r.choice(["50Gi", "50Gi", "1Gi"]), "pods": str(r.choice([4, 8, 16, 110]))}
-    if r.random() < 0.3:
+    if r.random() < 0.3 and extended:
         alloc[R_GPU] = r.choice(["1", "2", "4"])
     return {"metadata": {"name": name, "labels": labels}, "spec": spec, "status": {"allocatable": alloc}}
 
@@ -82,13 +82,13 @@ def _term(r: random.Random, keys: List[str]) -> dict:
     return {"labelSelector": _sel(r), "topologyKey": r.choice(keys)}
 
 
-def _requests(r: random.Random) -> dict:
+def _requests(r: random.Random, extended: bool = True) -> dict:
     if r.random() < 0.05:
         return {}
     req = {"cpu": "%dm" % r.choice([100, 250, 500, 1000]), "memory": "%dMi" % r.choice([128, 256, 512, 1024])}
     if r.random() < 0.1:
         req["ephemeral-storage"] = r.choice(["256Mi", "768Mi"])
-    if r.random() < 0.1:
+    if r.random() < 0.1 and extended:
         req[R_GPU] = "1"
     return req
 
@@ -108,8 +108,8 @@ def _node_expr(r: random.Random) -> dict:
     return {"key": K_RACK, "operator": "In", "values": [r.choice(RACKS)]}
 
 
-def _bound(i: int, k: int, node: str, r: random.Random) -> dict:
-    spec: Dict = {"nodeName": node, "containers": [{"name": "c", "resources": {"requests": _requests(r)}}]}
+def _bound(i: int, k: int, node: str, r: random.Random, extended: bool = True) -> dict:
+    spec: Dict = {"nodeName": node, "containers": [{"name": "c", "resources": {"requests": _requests(r, extended)}}]}
     aff: Dict = {}
     u = r.random()
     if u < 0.15:
@@ -139,8 +139,8 @@ def _spread(r: random.Random, key: str, hard: bool) -> dict:
     return c
 
 
-def _pending(j: int, r: random.Random, node_names: List[str]) -> dict:
-    spec: Dict = {"containers": [{"name": "c", "resources": {"requests": _requests(r)}}]}
+def _pending(j: int, r: random.Random, node_names: List[str], extended: bool = True) -> dict:
+    spec: Dict = {"containers": [{"name": "c", "resources": {"requests": _requests(r, extended)}}]}
     if r.random() < 0.08:
         spec["initContainers"] = [{"name": "i", "resources": {"requests": {"cpu": r.choice(["1", "2500m"])}}}]
     tols = []
@@ -211,14 +211,15 @@ def _pending(j: int, r: random.Random, node_names: List[str]) -> dict:
             "spec": spec}
 
 
-def make(seed: int, n_nodes: int, n_pods: int, bound_per_node: Tuple[int, int] = (0, 3)):
-    """(nodes, bound_pods, pending_pods) for one seed."""
+def make(seed: int, n_nodes: int, n_pods: int, bound_per_node: Tuple[int, int] = (0, 3), extended: bool = True):
+    """(nodes, bound_pods, pending_pods) for one seed.  extended=False leaves the extended
+    resource out (k_simple / k_spread keep cpu, memory and ephemeral-storage only)."""
     r = random.Random(seed)
-    nodes = [_node(i, r) for i in range(n_nodes)]
+    nodes = [_node(i, r, extended) for i in range(n_nodes)]
     names = [n["metadata"]["name"] for n in nodes]
     bound = []
     for i, nm in enumerate(names):
         for k in range(r.randint(*bound_per_node)):
-            bound.append(_bound(i, k, nm, r))
-    pods = [_pending(j, r, names) for j in range(n_pods)]
+            bound.append(_bound(i, k, nm, r, extended))
+    pods = [_pending(j, r, names, extended) for j in range(n_pods)]
     return nodes, bound, pods

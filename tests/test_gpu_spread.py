@@ -46,8 +46,10 @@ def _check(ctx, res, st, chosen, chosen_o, n, n_nodes, n_classes, n_terms):
         np.testing.assert_array_equal(g["term_count"][:n_terms], st["term_count"][:n_terms])
 
 
-def _fuzz(seed, n_nodes, n_pods):
-    nodes, bound, pods = progfuzz.make(seed, n_nodes, n_pods)
+def _fuzz(seed, n_nodes, n_pods, extended=False):
+    # k_spread keeps cpu / memory / ephemeral-storage only: extended resources send a batch to
+    # k_schedule (kss_plan_podset), so the k_spread runs leave them out
+    nodes, bound, pods = progfuzz.make(seed, n_nodes, n_pods, extended=extended)
     cc, cp, _ = compile_cluster(nodes, bound, pods)
     return cc, cp
 
@@ -196,7 +198,7 @@ def test_same_key_fixture_both_kernels():
 def test_program_fuzz_records_on_k_schedule(seed):
     """k_schedule with every per-node record on fuzzed programs (including same-key groups)."""
     prof = abi.default_profile()
-    cc, cp = _fuzz(seed, 150, 120)
+    cc, cp = _fuzz(seed, 150, 120, extended=True)
     ncl, nt = len(cc.classes), len(cc.terms)
     chosen_o, res, st = oracle_c.schedule(prof, cc.as_struct(), cp.as_struct(), cp.n, cc.n_nodes, record=True,
                                           threads=8, n_classes=ncl, n_terms=nt)

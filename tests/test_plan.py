@@ -18,15 +18,23 @@ def test_baseline_configs(config, kernel):
 def test_program_fuzz_batches_take_k_spread(seed, n_nodes, n_pods):
     """The batches test_gpu_spread.py runs: every one admitted by k_spread (the GPU tests
     assert the kernel that ran)."""
-    nodes, bound, pods = progfuzz.make(seed, n_nodes, n_pods)
+    nodes, bound, pods = progfuzz.make(seed, n_nodes, n_pods, extended=False)
     cc, cp, _ = compile_cluster(nodes, bound, pods)
     assert native.plan_podset(cc.as_struct(), cp.as_struct())["kernel"] == "k_spread"
+
+
+def test_extended_resources_take_k_schedule():
+    nodes, bound, pods = progfuzz.make(1, 60, 200)
+    cc, cp, _ = compile_cluster(nodes, bound, pods)
+    assert cc.scalars == [progfuzz.R_GPU]
+    plan = native.plan_podset(cc.as_struct(), cp.as_struct())
+    assert plan["kernel"] == "k_schedule" and plan["reason"].startswith("extended (scalar) resources")
 
 
 def test_refusal_names_pod_and_reason():
     """Required anti-affinity over five topology keys exceeds the four key slots of a pod
     program: k_schedule only, with the pod and the reason named."""
-    nodes, bound, pods = progfuzz.make(9, 20, 5)
+    nodes, bound, pods = progfuzz.make(9, 20, 5, extended=False)
     keys = (progfuzz.K_ZONE, progfuzz.K_RACK, progfuzz.K_HOST, progfuzz.K_ITYPE, "example.com/none")
     pods[3]["spec"]["affinity"] = {"podAntiAffinity": {"requiredDuringSchedulingIgnoredDuringExecution": [
         {"labelSelector": {"matchLabels": {"app": "a1"}}, "topologyKey": k} for k in keys]}}
