@@ -128,7 +128,7 @@ def reduce_over_ranks(elapsed, scheduled, dist):
     return float(t.item()), int(sc.item())
 
 
-def measure_traffic(args, cfg, mode=(), match=("k_simple", "k_schedule"), mean=False):
+def measure_traffic(args, cfg, mode=(), match=("k_simple", "k_schedule", "k_spread"), mean=False):
     """HBM bytes per launch of the scheduling kernel from rocprofv3 PMC counters: one child
     process per counter (FETCH_SIZE, WRITE_SIZE), started before this process touches the
     GPU.  FETCH_SIZE is doubled (gfx950 tallies 128-B requests at 64 B,
@@ -429,6 +429,91 @@ def run_per_pod(args):
     s.close()
 
 
+def run_postfilter(args):
+    """DefaultPreemption PostFilter dry run as the simulator's cycle runs it:
+    kss_eval_pod, and for an unschedulable pod kss_postfilter_pod on the same snapshot, on a
+    saturated cluster (every node nearly full of pods of mixed priority; pending pods of
+    higher priority).  Reports dry runs per second (host-observed, one k_preempt launch each)
+    and the k_preempt device time; the CPU baseline is the object-level restatement
+    (oracle/k8s_preemption.py, one thread) on a bounded sample of the same pods."""
+    import numpy as np
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import preempt_fixtures as pf
+    from kss import abi, native
+    from kss.compile import compile_cluster
+    n_nodes = args.nodes or 5000
+    n_pods = args.pods or 200
+    t_gen = time.perf_counter()
+    nodes, bound, pods = pf.saturated(11, n_nodes, n_pods)
+    cc, cp, _ = compile_cluster(nodes, bound, pods)
+    t_gen = time.perf_counter() - t_gen
+    ps, bs = cp.as_struct(), cc.as_boundset()
+    ctx = native.Context(abi.default_profile())
+    ctx.load(cc.as_struct())
+    ctx.load_bound(bs)
+    unsched = []
+    for j in range(n_pods):  # the snapshot stays saturated: nothing is committed
+        if ctx.eval_pod(ps, j).chosen < 0:
+            unsched.append(j)
+    for j in unsched[:max(args.warmup, 1) * 3]:
+        ctx.postfilter_pod(ps, j)
+    host_us, dev_us, nominated, victims = [], [], 0, 0
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        for j in unsched:
+            a = time.perf_counter()
+            r = ctx.postfilter_pod(ps, j)
+            host_us.append((time.perf_counter() - a) * 1e6)
+            dev_us.append(ctx.last_timing()[0] * 1e3)
+            nominated += r["status"] == abi.KSS_PREEMPT_NOMINATED
+            victims += r["n_victims"]
+    elapsed = time.perf_counter() - t0
+    runs = len(host_us)
+    cpu = None
+    if not args.no_cpu and unsched:
+        import k8s_oracle as ko
+        import k8s_preemption as kp
+        o = ko.Oracle(nodes, bound)
+        done, c0 = 0, time.perf_counter()
+        for j in unsched:
+            r = o.schedule_one(pods[j], commit=False)
+            kp.preempt(o, pods[j], r)
+            done += 1
+            if time.perf_counter() - c0 > args.cpu_seconds:
+                break
+        cs = time.perf_counter() - c0
+        cpu = {"value": done / cs, "unit": "dry runs/s", "cores": 1, "kind": "port",
+               "sample": f"{done} unschedulable pods of the same saturated {n_nodes}-node cluster: "
+                         "Oracle.schedule_one (filters) + k8s_preemption.preempt, pure Python, one thread"}
+    out = {
+        "metric": "DefaultPreemption PostFilter dry runs/sec (unschedulable pods on a saturated cluster)",
+        "value": runs / elapsed,
+        "unit": "dry runs/s",
+        "n_gpus": 1,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "int64",
+        "data": "synthetic (tests/preempt_fixtures.saturated seed 11)",
+        "config": {"workload": f"PostFilter: {n_nodes} saturated nodes, {len(bound)} bound pods, "
+                               f"{len(unsched)} unschedulable of {n_pods} pending",
+                   "nodes": n_nodes, "bound_pods": len(bound), "dry_runs_per_step": len(unsched)},
+        "host_us": {"median": float(np.median(host_us)), "p90": float(np.percentile(host_us, 90))},
+        "k_preempt_us": {"median": float(np.median(dev_us)), "mean": float(np.mean(dev_us)),
+                         "max": float(np.max(dev_us))},
+        "nominated_fraction": nominated / max(runs, 1),
+        "victims_per_nomination": victims / max(nominated, 1),
+        "compile_s": t_gen,
+        "cpu_baseline": cpu,
+    }
+    print(json.dumps(out), flush=True)
+    ctx.close()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -447,11 +532,14 @@ def main():
                     help="C4 shape: one cluster sharded along the node axis over the ranks (RCCL per pod)")
     ap.add_argument("--per-pod", action="store_true", help="the drop-in per-pod API: kss_eval_pod + kss_commit")
     ap.add_argument("--no-latency", action="store_true", help="skip the stamped latency-profile run")
+    ap.add_argument("--postfilter", action="store_true", help="DefaultPreemption PostFilter dry runs (kss_postfilter_pod)")
     args = ap.parse_args()
     if args.inner:
         args.no_cpu = args.no_traffic = args.no_latency = True
     if args.per_pod:
         return run_per_pod(args)
+    if args.postfilter:
+        return run_postfilter(args)
     if args.node_axis:
         return run_node_axis(args)
     if args.scenarios:

@@ -437,7 +437,7 @@ int kss_last_loop_timing(kss_ctx* ctx, double* loop_ms);
 int kss_last_geometry(kss_ctx* ctx, int32_t* out3);
 /* kernel of the last scheduling launch: 0 general (k_schedule), 1 compact (k_simple:
  * batches without spread / inter-pod programs and without a record), 2 k_spread (batches
- * with programs, without a record); <0 on error */
+ * with programs, without a record), 3 k_preempt (kss_postfilter_pod); <0 on error */
 int kss_last_kernel(kss_ctx* ctx);
 /* outcome of pods [first, first+n) of the last scheduling launch, recorded or not:
  * out[5*i .. 5*i+4] = chosen, n_feasible, scored, status, best_total (kss_pod_result) */

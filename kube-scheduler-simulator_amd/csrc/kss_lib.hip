@@ -2689,8 +2689,10 @@ int kss_postfilter_pod(kss_ctx* ctx, const kss_podset* ps, int32_t pod_index, ks
   J.victims = (int64_t*)(d + o_vic);
   J.out = (PreemptOut*)(d + o_out);
   HIP_TRY(hipMemcpyAsync(d + o_job, &J, sizeof(J), hipMemcpyHostToDevice, ctx->stream));
+  HIP_TRY(hipEventRecord(ctx->ev0, ctx->stream));
   hipLaunchKernelGGL(k_preempt, dim3(1), dim3(PRE_THREADS), lds, ctx->stream, (const PreemptJob*)(d + o_job));
   HIP_TRY(hipGetLastError());
+  HIP_TRY(hipEventRecord(ctx->ev1, ctx->stream));
   const size_t back = sizeof(PreemptOut) + 8 * (size_t)cap;
   if (ctx->pinned_cap < back) {
     if (ctx->pinned) hipHostFree(ctx->pinned);
@@ -2701,6 +2703,11 @@ int kss_postfilter_pod(kss_ctx* ctx, const kss_podset* ps, int32_t pod_index, ks
   }
   HIP_TRY(hipMemcpyAsync(ctx->pinned, d + o_out, back, hipMemcpyDeviceToHost, ctx->stream));
   HIP_TRY(hipStreamSynchronize(ctx->stream));
+  float ms = 0;
+  HIP_TRY(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
+  ctx->last_ms = ms;
+  ctx->last_launches = 1;
+  ctx->last_kernel = 3;
   PreemptOut o;
   std::memcpy(&o, ctx->pinned, sizeof(o));
   if (o.status < 0) return fail(KSS_E_UNSUPPORTED, "pod program exceeds the device path's per-pod limits");

@@ -354,7 +354,7 @@ class Context:
         k = lib().kss_last_kernel(self.h)
         if k < 0:
             check(k)
-        return {1: "k_simple", 2: "k_spread"}.get(k, "k_schedule")
+        return {1: "k_simple", 2: "k_spread", 3: "k_preempt"}.get(k, "k_schedule")
 
     def fetch_meta(self, n: int, first: int = 0) -> np.ndarray:
         """(n, 5) int64: chosen, n_feasible, scored, status, best_total of pods [first, first+n)."""
