@@ -95,6 +95,9 @@ class NodeAxisScheduler:
         self.n_pods = podset.n_pods
         self.lo, self.hi = row_range(cluster.n_nodes, self.rank, self.world)
         self.device = torch.device("cuda", device)
+        # torch's bundled HIP runtime must open the device before libkss.so's /opt/rocm runtime
+        # does (the other order leaves torch with "No HIP GPUs are available")
+        torch.zeros(1, device=self.device)
         self.ctx = native.Context(profile, device=device)
         self.ctx.load_rows(cluster, self.lo, self.hi)
         self.ctx.stage(podset)
