@@ -265,10 +265,18 @@ __global__ void k_commit(DevCluster c, CommitArgs a) {
   for (int i = 0; i < a.n_own; i++) c.term_count[(size_t)a.own[i] * N + a.local] += a.sign;
 }
 
-// DefaultPreemption PostFilter dry run of one pod (kss_postfilter_pod).
-__global__ __launch_bounds__(PRE_THREADS) void k_preempt(const PreemptJob* __restrict__ job) {
+// DefaultPreemption PostFilter dry run of one pod (kss_postfilter_pod): three launches.
+__global__ __launch_bounds__(PRE_THREADS) void k_preempt_stats(const PreemptJob* __restrict__ job) {
   extern __shared__ __attribute__((aligned(16))) long long smem[];
-  preempt_pod(*job, smem);  // descriptors read through the scalar cache
+  preempt_stats(*job, smem);  // descriptors read through the scalar cache
+}
+__global__ __launch_bounds__(PRE_NODE_THREADS) void k_preempt_nodes(const PreemptJob* __restrict__ job) {
+  extern __shared__ __attribute__((aligned(16))) long long smem[];
+  preempt_nodes(*job, smem);
+}
+__global__ __launch_bounds__(PRE_THREADS) void k_preempt_pick(const PreemptJob* __restrict__ job) {
+  extern __shared__ __attribute__((aligned(16))) long long smem[];
+  preempt_pick(*job, smem);
 }
 
 // Delta sync of node rows (kss_apply_node_delta): one packed upload, one scatter.
@@ -2670,7 +2678,9 @@ int kss_postfilter_pod(kss_ctx* ctx, const kss_podset* ps, int32_t pod_index, ks
   const size_t N = (size_t)ctx->dc.N;
   const int cap = out->victims_cap;
   const size_t o_job = 0, o_out = align_up(sizeof(PreemptJob), 256), o_vic = o_out + sizeof(PreemptOut),
-               o_key = align_up(o_vic + 8 * (size_t)std::max(cap, 1), 256), total = o_key + 4 * 8 * std::max(N, (size_t)1);
+               o_key = align_up(o_vic + 8 * (size_t)std::max(cap, 1), 256),
+               o_g = align_up(o_key + 4 * 8 * std::max(N, (size_t)1), 256), o_bins = align_up(o_g + sizeof(PreGlobal), 256),
+               total = o_bins + 8 * (size_t)bins_cap;
   if ((rc = ctx->pre_buf.ensure(total))) return rc;
   char* d = (char*)ctx->pre_buf.p;
   PreemptJob J{};
@@ -2688,9 +2698,15 @@ int kss_postfilter_pod(kss_ctx* ctx, const kss_podset* ps, int32_t pod_index, ks
   J.key = (int64_t*)(d + o_key);
   J.victims = (int64_t*)(d + o_vic);
   J.out = (PreemptOut*)(d + o_out);
+  J.G = (PreGlobal*)(d + o_g);
+  J.gbins = (long long*)(d + o_bins);
   HIP_TRY(hipMemcpyAsync(d + o_job, &J, sizeof(J), hipMemcpyHostToDevice, ctx->stream));
   HIP_TRY(hipEventRecord(ctx->ev0, ctx->stream));
-  hipLaunchKernelGGL(k_preempt, dim3(1), dim3(PRE_THREADS), lds, ctx->stream, (const PreemptJob*)(d + o_job));
+  const PreemptJob* jd = (const PreemptJob*)(d + o_job);
+  hipLaunchKernelGGL(k_preempt_stats, dim3(1), dim3(PRE_THREADS), lds, ctx->stream, jd);
+  const unsigned nb = (unsigned)((N + PRE_NODE_THREADS - 1) / PRE_NODE_THREADS);
+  hipLaunchKernelGGL(k_preempt_nodes, dim3(std::max(nb, 1u)), dim3(PRE_NODE_THREADS), sizeof(PreHdr), ctx->stream, jd);
+  hipLaunchKernelGGL(k_preempt_pick, dim3(1), dim3(PRE_THREADS), sizeof(PreHdr), ctx->stream, jd);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipEventRecord(ctx->ev1, ctx->stream));
   const size_t back = sizeof(PreemptOut) + 8 * (size_t)cap;
@@ -2706,7 +2722,7 @@ int kss_postfilter_pod(kss_ctx* ctx, const kss_podset* ps, int32_t pod_index, ks
   float ms = 0;
   HIP_TRY(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
   ctx->last_ms = ms;
-  ctx->last_launches = 1;
+  ctx->last_launches = 3;
   ctx->last_kernel = 3;
   PreemptOut o;
   std::memcpy(&o, ctx->pinned, sizeof(o));

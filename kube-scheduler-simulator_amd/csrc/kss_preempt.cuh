@@ -7,8 +7,7 @@
 // wrappedplugin.go:550-577).  The object-level restatement it is tested against is
 // oracle/k8s_preemption.py.
 //
-// One workgroup per pod (the PostFilter call is a per-pod latency path; a cluster of a
-// few thousand nodes is a few node slots per lane):
+// Three launches per pod (the PostFilter call is a per-pod latency path):
 //   1. PreFilter state of PodTopologySpread / InterPodAffinity (the same LDS histograms
 //      as k_schedule, kss_sched.cuh stats_node), plus per hard-spread key the two
 //      smallest pair counts with the smallest pair's id (criticalPaths) and the
@@ -16,7 +15,7 @@
 //   2. the filter chain per node; nodesWherePreemptionMightHelp keeps the nodes whose
 //      first failure is Unschedulable (NodeResourcesFit, the spread skew, pod
 //      anti-affinity and existing pods' anti-affinity), not UnschedulableAndUnresolvable;
-//   3. SelectVictimsOnNode on each of them, by the lane that owns the node: remove every
+//   3. SelectVictimsOnNode on each of them, one lane per node over the grid: remove every
 //      lower-priority pod (NodeInfo.RemovePod + the RemovePod extensions: the node's own
 //      pair counts move, the spread minimum becomes min(min over the other pairs, the
 //      node's pair) — criticalPaths.update keeps exactly that minimum when one pair
@@ -27,8 +26,8 @@
 //      (highest victim priority min, Σ(priority + 2^31) min, #victims min, earliest
 //      start of the highest-priority victims max, node index min) — the last criterion
 //      replaces the Go map order upstream leaves to chance;
-//   5. the owner lane of the nominated node re-runs its reprieve loop and writes the
-//      victims' ids in eviction order.
+//   5. one lane re-runs the nominated node's reprieve loop and writes the victims' ids in
+//      eviction order.
 // No PodDisruptionBudgets (every victim is non-violating) and no nominated pods.
 #pragma once
 #include "kss_sched.cuh"
@@ -37,6 +36,7 @@ namespace kss {
 
 constexpr int PRE_THREADS = 512;
 constexpr int PRE_WAVES = PRE_THREADS / 64;
+constexpr int PRE_NODE_THREADS = 64;  // k_preempt_nodes: one lane per node, many small workgroups
 
 // Bound pods on the device: CSR by node, NodeInfo.Pods order inside a node.
 struct DevBound {
@@ -56,6 +56,14 @@ struct PreemptOut {
   int64_t sum_priority, earliest_start;
 };
 
+// PreFilter state and counters shared by the three launches (HBM)
+struct PreGlobal {
+  long long m0[MAXH], id0[MAXH], m1[MAXH];
+  long long aff_total, flags;
+  int plan_ok, prefilter;
+  int n_potential, n_candidates, feasible, pad;
+};
+
 struct PreemptJob {
   DevCluster c;
   DevPods P;
@@ -68,6 +76,8 @@ struct PreemptJob {
   int64_t* key;      // [4][N] HBM scratch: candidate keys per node
   int64_t* victims;  // [victims_cap]
   PreemptOut* out;
+  PreGlobal* G;
+  long long* gbins;  // [bins_cap] the PreFilter histograms and presence bins
 };
 
 struct PreHdr {
@@ -298,35 +308,42 @@ __device__ __forceinline__ bool resolvable(int f, int detail) {
   return false;
 }
 
-__device__ void preempt_pod(const PreemptJob& J, long long* smem) {
+// ---------------------------------------------------------------------------
+// Three launches on one stream: k_preempt_stats (one workgroup: PreFilter state into
+// HBM), k_preempt_nodes (one lane per node over the whole grid: filters, potential
+// nodes, SelectVictimsOnNode, candidate keys), k_preempt_pick (one workgroup:
+// pickOneNodeForPreemption and the nominated node's victims).
+// ---------------------------------------------------------------------------
+
+// pod record -> LDS and the plan (lane 0); false when the pod has no dry run to do
+__device__ __forceinline__ void pre_load_pod(const PreemptJob& J, PreHdr& H) {
+  const int tid = threadIdx.x, nt = blockDim.x;
+  constexpr int PD = (int)(sizeof(kss_pod) / 4);
+  const uint32_t* src = reinterpret_cast<const uint32_t*>(J.P.pods + J.pi);
+  uint32_t* dst = reinterpret_cast<uint32_t*>(&H.pod);
+  for (int i = tid; i < PD; i += nt) dst[i] = src[i];
+  if (tid == 0) H.plan_ok = make_plan(J.c, J.P, J.P.pods[J.pi], H.plan, J.bins_cap) ? 1 : 0;
+  __syncthreads();
+}
+
+__device__ void preempt_stats(const PreemptJob& J, long long* smem) {
   const int tid = threadIdx.x, nt = blockDim.x;
   PreHdr& H = *reinterpret_cast<PreHdr*>(smem);
   const DevCluster& c = J.c;
   const DevPods& P = J.P;
-  {
-    constexpr int PD = (int)(sizeof(kss_pod) / 4);
-    const uint32_t* src = reinterpret_cast<const uint32_t*>(P.pods + J.pi);
-    uint32_t* dst = reinterpret_cast<uint32_t*>(&H.pod);
-    for (int i = tid; i < PD; i += nt) dst[i] = src[i];
-    if (tid == 0) H.plan_ok = make_plan(c, P, P.pods[J.pi], H.plan, J.bins_cap) ? 1 : 0;
-    __syncthreads();
-  }
+  pre_load_pod(J, H);
   const kss_pod& p = H.pod;
   const Plan& pl = H.plan;
-  PreemptOut& out = *J.out;
-  if (!H.plan_ok || p.prefilter_status != 0) {
-    // a PreFilter failure gives every node UnschedulableAndUnresolvable: nothing to dry-run
-    if (tid == 0) {
-      out.status = !H.plan_ok ? -1 : KSS_PREEMPT_NO_CANDIDATE;
-      out.nominated = -1;
-      out.n_potential = out.n_candidates = out.n_victims = 0;
-    }
-    return;
+  PreGlobal& G = *J.G;
+  if (tid == 0) {
+    G.plan_ok = H.plan_ok;
+    G.prefilter = p.prefilter_status;
+    G.n_potential = G.n_candidates = G.feasible = 0;
   }
+  if (!H.plan_ok || p.prefilter_status != 0) return;
   long long* bins = pre_bins(smem);
   long long* pres = bins + pl.total_bins;
   const int N = c.N;
-  // ---- 1. PreFilter state --------------------------------------------------
   long long hard_min[MAXH];
 #pragma unroll
   for (int i = 0; i < MAXH; i++) hard_min[i] = INT32_MAX;
@@ -367,75 +384,134 @@ __device__ void preempt_pod(const PreemptJob& J, long long* smem) {
     }
     second = block_op(second, OP_MIN, H.red);
     if (tid == 0) {
-      H.m0[i] = best == INT64_MAX ? INT32_MAX : (best >> 24);
-      H.id0[i] = id0;
-      H.m1[i] = second == INT64_MAX ? INT32_MAX : second;
+      G.m0[i] = best == INT64_MAX ? INT32_MAX : (best >> 24);
+      G.id0[i] = id0;
+      G.m1[i] = second == INT64_MAX ? INT32_MAX : second;
     }
   }
   if (tid == 0) {
-    H.aff_total = aff;
-    H.flags = flags;
+    G.aff_total = aff;
+    G.flags = flags;
+  }
+  for (int b = tid; b < pl.total_bins + pl.total_pbins; b += nt) J.gbins[b] = bins[b];
+}
+
+__device__ void preempt_nodes(const PreemptJob& J, long long* smem) {
+  const int tid = threadIdx.x;
+  PreHdr& H = *reinterpret_cast<PreHdr*>(smem);
+  const DevCluster& c = J.c;
+  const DevPods& P = J.P;
+  const PreGlobal& G = *J.G;
+  if (!G.plan_ok || G.prefilter != 0) return;
+  pre_load_pod(J, H);
+  if (tid == 0) {
+    for (int i = 0; i < MAXH; i++) {
+      H.m0[i] = G.m0[i];
+      H.id0[i] = G.id0[i];
+      H.m1[i] = G.m1[i];
+    }
+    H.aff_total = G.aff_total;
+    H.flags = G.flags;
   }
   __syncthreads();
+  const kss_pod& p = H.pod;
+  const Plan& pl = H.plan;
+  const long long* bins = J.gbins;
+  long long hard_min[MAXH];
 #pragma unroll
-  for (int i = 0; i < MAXH; i++)
-    if (i < p.n_hard) hard_min[i] = H.m0[pl.hard_own[i]];
-  // ---- 2 + 3. filters, potential nodes, SelectVictimsOnNode ------------------
+  for (int i = 0; i < MAXH; i++) hard_min[i] = i < p.n_hard ? H.m0[pl.hard_own[i]] : INT32_MAX;
   const uint32_t en = J.prof.filter_enabled;
-  const bool restrict_names = p.names_len >= 0;
+  const int N = c.N;
+  const int n = (int)(blockIdx.x * blockDim.x) + tid;
   long long n_pot = 0, n_cand = 0, feasible = 0;
   int64_t* K = J.key;
-  for (int n = tid; n < N; n += nt) {
+  if (n < N) {
     K[n] = INT64_MAX;
-    if (restrict_names && !in_names(P, p, (int64_t)c.node_base + n)) {
-      n_pot++;  // no status in the map: potential, but NodeAffinity rejects it in the dry run
-      continue;
-    }
-    uint16_t detail = 0;
-    const NodeRow row = load_row(c, n);
-    int f = filter_local(c, P, p, en, n, row, &detail);
-    if (!f && ((en >> KSS_F_POD_TOPOLOGY_SPREAD) & 1u) && p.n_hard > 0) {
-      const int r = filter_pts(c, P, p, pl, bins, hard_min, n);
-      if (r) {
-        f = KSS_F_POD_TOPOLOGY_SPREAD;
-        detail = (uint16_t)(r - 1);
+    if (p.names_len >= 0 && !in_names(P, p, (int64_t)c.node_base + n)) {
+      n_pot = 1;  // no status in the map: potential, but NodeAffinity rejects it in the dry run
+    } else {
+      uint16_t detail = 0;
+      const NodeRow row = load_row(c, n);
+      int f = filter_local(c, P, p, en, n, row, &detail);
+      if (!f && ((en >> KSS_F_POD_TOPOLOGY_SPREAD) & 1u) && p.n_hard > 0) {
+        const int r = filter_pts(c, P, p, pl, bins, hard_min, n);
+        if (r) {
+          f = KSS_F_POD_TOPOLOGY_SPREAD;
+          detail = (uint16_t)(r - 1);
+        }
+      }
+      if (!f && ((en >> KSS_F_INTER_POD_AFFINITY) & 1u) && p.ipa_len > 0) {
+        const int r = filter_ipa(c, P, p, pl, bins, H.flags, n);
+        if (r) {
+          f = KSS_F_INTER_POD_AFFINITY;
+          detail = (uint16_t)(r - 1);
+        }
+      }
+      if (!f) {
+        feasible = 1;
+      } else if (resolvable(f, detail)) {
+        n_pot = 1;
+        const DryResult d = select_victims(J, p, pl, H, bins, n, false);
+        if (d.hp != INT64_MAX) {
+          n_cand = 1;
+          K[n] = d.hp;
+          K[N + n] = d.sum;
+          K[2 * (size_t)N + n] = d.cnt;
+          K[3 * (size_t)N + n] = d.start;
+        }
       }
     }
-    if (!f && ((en >> KSS_F_INTER_POD_AFFINITY) & 1u) && p.ipa_len > 0) {
-      const int r = filter_ipa(c, P, p, pl, bins, H.flags, n);
-      if (r) {
-        f = KSS_F_INTER_POD_AFFINITY;
-        detail = (uint16_t)(r - 1);
-      }
-    }
-    if (!f) {
-      feasible++;
-      continue;
-    }
-    if (!resolvable(f, detail)) continue;
-    n_pot++;
-    const DryResult d = select_victims(J, p, pl, H, bins, n, false);
-    if (d.hp == INT64_MAX) continue;
-    n_cand++;
-    K[n] = d.hp;
-    K[N + n] = d.sum;
-    K[2 * (size_t)N + n] = d.cnt;
-    K[3 * (size_t)N + n] = d.start;
   }
-  feasible = block_op(feasible, OP_SUM, H.red);
   n_pot = block_op(n_pot, OP_SUM, H.red);
   n_cand = block_op(n_cand, OP_SUM, H.red);
-  if (feasible || n_cand == 0) {
+  feasible = block_op(feasible, OP_SUM, H.red);
+  if (tid == 0) {
+    PreGlobal& Gw = *J.G;
+    if (n_pot) atomicAdd(&Gw.n_potential, (int)n_pot);
+    if (n_cand) atomicAdd(&Gw.n_candidates, (int)n_cand);
+    if (feasible) atomicAdd(&Gw.feasible, (int)feasible);
+  }
+}
+
+__device__ void preempt_pick(const PreemptJob& J, long long* smem) {
+  const int tid = threadIdx.x, nt = blockDim.x;
+  PreHdr& H = *reinterpret_cast<PreHdr*>(smem);
+  const DevCluster& c = J.c;
+  const PreGlobal& G = *J.G;
+  PreemptOut& out = *J.out;
+  if (!G.plan_ok || G.prefilter != 0) {
+    // a PreFilter failure gives every node UnschedulableAndUnresolvable: nothing to dry-run
     if (tid == 0) {
-      out.status = feasible ? KSS_PREEMPT_SCHEDULABLE : KSS_PREEMPT_NO_CANDIDATE;
+      out.status = !G.plan_ok ? -1 : KSS_PREEMPT_NO_CANDIDATE;
       out.nominated = -1;
-      out.n_potential = (int32_t)n_pot;
-      out.n_candidates = (int32_t)n_cand;
+      out.n_potential = out.n_candidates = out.n_victims = 0;
+    }
+    return;
+  }
+  if (G.feasible || G.n_candidates == 0) {
+    if (tid == 0) {
+      out.status = G.feasible ? KSS_PREEMPT_SCHEDULABLE : KSS_PREEMPT_NO_CANDIDATE;
+      out.nominated = -1;
+      out.n_potential = G.n_potential;
+      out.n_candidates = G.n_candidates;
       out.n_victims = 0;
     }
     return;
   }
-  // ---- 4. pickOneNodeForPreemption -------------------------------------------
+  pre_load_pod(J, H);
+  if (tid == 0) {
+    for (int i = 0; i < MAXH; i++) {
+      H.m0[i] = G.m0[i];
+      H.id0[i] = G.id0[i];
+      H.m1[i] = G.m1[i];
+    }
+    H.aff_total = G.aff_total;
+    H.flags = G.flags;
+  }
+  __syncthreads();
+  const int N = c.N;
+  const int64_t* K = J.key;
+  // pickOneNodeForPreemption as successive reductions
   long long v = INT64_MAX;
   for (int n = tid; n < N; n += nt) v = min(v, (long long)K[n]);
   const long long hp = block_op(v, OP_MIN, H.red);
@@ -455,13 +531,13 @@ __device__ void preempt_pod(const PreemptJob& J, long long* smem) {
   for (int n = tid; n < N; n += nt)
     if (K[n] == hp && K[N + n] == sum && K[2 * (size_t)N + n] == cnt && K[3 * (size_t)N + n] == st) v = min(v, (long long)n);
   const long long best = block_op(v, OP_MIN, H.red);
-  // ---- 5. the nominated node's victims, by its owner lane --------------------
-  if ((int)(best % nt) == tid) {
-    const DryResult d = select_victims(J, p, pl, H, bins, (int)best, true);
+  // the nominated node's victims, by lane 0
+  if (tid == 0) {
+    const DryResult d = select_victims(J, H.pod, H.plan, H, J.gbins, (int)best, true);
     out.status = KSS_PREEMPT_NOMINATED;
     out.nominated = (int32_t)(c.node_base + best);
-    out.n_potential = (int32_t)n_pot;
-    out.n_candidates = (int32_t)n_cand;
+    out.n_potential = G.n_potential;
+    out.n_candidates = G.n_candidates;
     out.n_victims = (int32_t)d.cnt;
     out.highest_priority = (int32_t)d.hp;
     out.sum_priority = d.sum;
