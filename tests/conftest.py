@@ -15,13 +15,12 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "slow: larger CPU cases")
 
 
-def pytest_sessionstart(session):
+def pytest_collection_modifyitems(session, config, items):
     """GPU runs: bring up torch's HIP runtime before any test loads libkss.so.  torch bundles
     its own ROCm runtime; once libkss.so's /opt/rocm runtime has opened the device first,
     torch reports "No HIP GPUs are available" (tools/torchprobe.py shows both orders), and
     the node-axis path (kss/nodeaxis.py) needs torch's device tensors."""
-    markexpr = session.config.getoption("markexpr") or ""
-    if "gpu" not in markexpr or "not gpu" in markexpr:
+    if not any(it.get_closest_marker("gpu") for it in items):
         return
     try:
         import torch
