@@ -1630,13 +1630,23 @@ static int launch_simple(hipStream_t st, const Geometry& g, int n_jobs, const De
   return 0;
 }
 
-static size_t spread_lds(const Geometry& g, const GpodNeeds& q, int n_keys, int n_res) {
-  return spread_lds_bytes(g.npt * g.threads, q.bins_cap, n_keys, n_res, q.gq);
+// k_spread's per-slot LDS arrays are strided by the largest shard's node count (rounded up
+// to 16 slots), not by threads x slots per lane: a 391-node shard of a 100k-node cluster
+// keeps 400 slots, not 512.
+static int spread_cap(const Geometry& g, size_t N) {
+  const size_t per = (N + (size_t)g.W - 1) / (size_t)g.W;
+  return (int)align_up(std::max(per, (size_t)1), 16);
 }
 
-static bool spread_fits(const Geometry& g, const GpodNeeds& q, int n_keys, int n_res) {
+static size_t spread_lds(const Geometry& g, const GpodNeeds& q, int n_keys, int n_res, size_t N) {
+  return spread_lds_bytes(spread_cap(g, N), q.bins_cap, n_keys, n_res, q.gq);
+}
+
+static bool spread_fits(const Geometry& g, const GpodNeeds& q, int n_keys, int n_res, size_t N) {
   const int pf_n = g.threads > 64 ? g.threads - 64 : g.threads;  // prefetch lanes (kss_spread.cuh)
-  return (g.npt * g.threads + pf_n - 1) / pf_n <= G_PF && spread_lds(g, q, n_keys, n_res) <= KSS_LDS_BUDGET;
+  const int per = (int)((N + (size_t)g.W - 1) / (size_t)g.W);
+  return (per + pf_n - 1) / pf_n <= G_PF && per <= g.npt * g.threads &&
+         spread_lds(g, q, n_keys, n_res, N) <= KSS_LDS_BUDGET;
 }
 
 // k_static + k_spread over pods [0, n_pods) of one job, `chunk` pods at a time (node state
@@ -1645,8 +1655,8 @@ static int launch_spread(hipStream_t st, const Geometry& g, const GpodNeeds& q, 
                          const DevJob* jobs, const kss_profile& prof, int n_pods, int max_nodes, int chunk,
                          unsigned long long* gran, size_t gran_bytes, int* err, unsigned long long* stamps = nullptr,
                          hipEvent_t* ev = nullptr) {
-  int cap = g.npt * g.threads, bins_cap = q.bins_cap, nr = n_res, gq = q.gq;
-  size_t shmem = spread_lds(g, q, n_keys, n_res);
+  int cap = spread_cap(g, (size_t)max_nodes), bins_cap = q.bins_cap, nr = n_res, gq = q.gq;
+  size_t shmem = spread_lds(g, q, n_keys, n_res, (size_t)max_nodes);
   if (stamps && shmem + G_STAMP_LDS > KSS_LDS_BUDGET) stamps = nullptr;  // diagnostics only where they fit
   if (stamps) shmem += G_STAMP_LDS;
   const bool def = same_profile(prof, default_profile_c());
@@ -1730,13 +1740,13 @@ static int run_single(kss_ctx* ctx, const PlanNeeds& need, const DevPods& dp, in
   if (!pick_geometry((int)N, W, ctx->pref_threads, g)) return fail(KSS_E_UNSUPPORTED, "no geometry for this cluster");
   const bool simple = simple_ok && simple_fits(g);
   const int n_res = (int)ctx->gneed.res_rows.size();
-  bool spread = spread_ok && spread_fits(g, ctx->gneed, ctx->dc.n_keys, n_res);
+  bool spread = spread_ok && spread_fits(g, ctx->gneed, ctx->dc.n_keys, n_res, N);
   if (spread_ok && !spread && g.threads < KSS_MAX_THREADS) {  // more prefetch lanes per shard
     Geometry g2 = g;
     const int per = (int)((N + g.W - 1) / g.W);
     g2.threads = KSS_MAX_THREADS;
     g2.npt = (per + KSS_MAX_THREADS - 1) / KSS_MAX_THREADS;
-    if (spread_fits(g2, ctx->gneed, ctx->dc.n_keys, n_res)) {
+    if (spread_fits(g2, ctx->gneed, ctx->dc.n_keys, n_res, N)) {
       g = g2;
       spread = true;
     }
@@ -1747,7 +1757,7 @@ static int run_single(kss_ctx* ctx, const PlanNeeds& need, const DevPods& dp, in
                          W2 <= ctx->n_cu && W2 <= (int)N;
        W2 *= 2) {
     Geometry g2;
-    if (pick_geometry((int)N, W2, ctx->pref_threads, g2) && spread_fits(g2, ctx->gneed, ctx->dc.n_keys, n_res)) {
+    if (pick_geometry((int)N, W2, ctx->pref_threads, g2) && spread_fits(g2, ctx->gneed, ctx->dc.n_keys, n_res, N)) {
       g = g2;
       spread = true;
     }

@@ -154,14 +154,16 @@ def test_k_simple_forced_shards_above_one_chunk(shards, monkeypatch):
     ctx.close()
 
 
-@pytest.mark.parametrize("kernel", ["k_spread", "k_schedule"])
-def test_c4_recipe_on_one_gpu(kernel, monkeypatch):
+@pytest.mark.parametrize("kernel,n_pods", [("k_spread", 200), ("k_schedule", 200), ("k_spread", 2000)])
+def test_c4_recipe_on_one_gpu(kernel, n_pods, monkeypatch):
     """BASELINE configs[3]'s recipe (100,000 nodes, zone DoNotSchedule spread) on one GPU at
-    256 shards, 200 pods: k_spread, and the general kernel (KSS_NO_SPREAD)."""
+    256 shards: k_spread, and the general kernel (KSS_NO_SPREAD).  At 2,000 pods the batch
+    reads ~100 count rows, which fit only because the LDS slots are strided by the 391-node
+    shard, not by threads x slots per lane."""
     if kernel == "k_schedule":
         monkeypatch.setenv("KSS_NO_SPREAD", "1")
     prof = abi.default_profile()
-    n_nodes, n_pods = 100000, 200
+    n_nodes = 100000
     s = native.Synth(4, 0, n_nodes, n_pods)
     chosen_o, res, st = _oracle(prof, s, n_pods, record="meta")
     ctx = native.Context(prof)
