@@ -104,7 +104,7 @@ template <bool GEN>
 __global__ __launch_bounds__(KSS_MAX_THREADS) void k_schedule(const DevJob* __restrict__ jobs, kss_profile prof,
                                                               int W, int npt, int bins_cap, int cache_keys,
                                                               unsigned long long* gran, int* err,
-                                                              unsigned long long* stamps) {
+                                                              unsigned long long* stamps, unsigned epoch0) {
   extern __shared__ __attribute__((aligned(16))) long long smem[];
   const int ji = blockIdx.x / W, w = blockIdx.x % W;
   const DevJob job = jobs[ji];  // by value: the descriptors stay in registers for the whole launch
@@ -119,7 +119,7 @@ __global__ __launch_bounds__(KSS_MAX_THREADS) void k_schedule(const DevJob* __re
   S.hi = min(c.N, S.lo + per);
   S.W = W;
   S.w = w;
-  S.epoch = 0;
+  S.epoch = epoch0;  // granule tags of earlier launches are all below epoch0 (host-tracked)
   S.gran = gran ? gran + (size_t)ji * 2 * W * 2 * XW_MAX : nullptr;
   S.err = err;
   S.stamps = nullptr;
@@ -426,6 +426,13 @@ struct kss_ctx {
   std::vector<char> stage_host;  // packed host image of a delta upload
   void* pinned = nullptr;     // kss_eval_pod's one-copy result staging (pinned)
   size_t pinned_cap = 0;
+  void* rb = nullptr;         // run_single's read-back staging (pinned): err word, meta, chosen, slot
+  size_t rb_cap = 0;
+  void* up = nullptr;         // per-pod calls: pinned image of the pod's pools + the job, one upload
+  size_t up_cap = 0;
+  // k_schedule granules are not cleared between its launches: each launch starts its epochs
+  // above every tag an earlier launch can have left (gran_epoch); 0 = clear before the next
+  unsigned gran_epoch = 0;
   int staged_max_own = 0;     // max own term rows of a staged pod
   std::vector<int32_t> key_empty_h;
   bool no_simple = false;  // KSS_NO_SIMPLE: always launch k_schedule
@@ -479,6 +486,50 @@ int upload_podset(hipStream_t st, DevBuf& buf, const kss_podset* ps, DevPods& dp
   dp.spreads = (const kss_spread*)(b + o_spr);
   dp.ipa = (const kss_ipa*)(b + o_ipa);
   dp.ints = (const int32_t*)(b + o_ints);
+  return 0;
+}
+
+// One upload for a per-pod call: the pod's pools and `extra` trailing bytes (the launch's
+// job) as one pinned image; run_single fills the job and issues the single copy.
+struct PackedUpload {
+  char* host = nullptr;  // pinned image
+  char* dev = nullptr;
+  size_t bytes = 0;
+  size_t extra_off = 0;
+};
+
+int pack_podset(DevBuf& buf, void*& pin, size_t& pin_cap, const kss_podset* ps, size_t extra, DevPods& dp,
+                PackedUpload& pu) {
+  const size_t sz[6] = {sizeof(kss_pod) * (size_t)ps->n_pods, sizeof(kss_req) * (size_t)ps->n_reqs,
+                        sizeof(kss_term) * (size_t)ps->n_terms, sizeof(kss_spread) * (size_t)ps->n_spreads,
+                        sizeof(kss_ipa) * (size_t)ps->n_ipa, sizeof(int32_t) * (size_t)ps->n_ints};
+  const void* src[6] = {ps->pods, ps->reqs, ps->terms, ps->spreads, ps->ipa, ps->ints};
+  size_t off[6], o = 0;
+  for (int i = 0; i < 6; i++) {
+    off[i] = o;
+    o = align_up(o + std::max(sz[i], (size_t)16), 64);
+  }
+  pu.extra_off = o;
+  pu.bytes = align_up(o + extra, 64);
+  int rc = buf.ensure(pu.bytes);
+  if (rc) return rc;
+  if (pin_cap < pu.bytes) {
+    if (pin) HIP_TRY(hipHostFree(pin));
+    pin = nullptr;
+    pin_cap = 0;
+    HIP_TRY(hipHostMalloc(&pin, std::max(pu.bytes, (size_t)65536), hipHostMallocDefault));
+    pin_cap = std::max(pu.bytes, (size_t)65536);
+  }
+  pu.host = (char*)pin;
+  pu.dev = (char*)buf.p;
+  for (int i = 0; i < 6; i++)
+    if (sz[i]) std::memcpy(pu.host + off[i], src[i], sz[i]);
+  dp.pods = (const kss_pod*)(pu.dev + off[0]);
+  dp.reqs = (const kss_req*)(pu.dev + off[1]);
+  dp.terms = (const kss_term*)(pu.dev + off[2]);
+  dp.spreads = (const kss_spread*)(pu.dev + off[3]);
+  dp.ipa = (const kss_ipa*)(pu.dev + off[4]);
+  dp.ints = (const int32_t*)(pu.dev + off[5]);
   return 0;
 }
 
@@ -1120,6 +1171,8 @@ void kss_destroy(kss_ctx* ctx) {
   ctx->res_buf.release();
   ctx->delta_buf.release();
   if (ctx->pinned) hipHostFree(ctx->pinned);
+  if (ctx->rb) hipHostFree(ctx->rb);
+  if (ctx->up) hipHostFree(ctx->up);
   for (hipEvent_t e : ctx->loop_ev) hipEventDestroy(e);
   if (ctx->ev0) hipEventDestroy(ctx->ev0);
   if (ctx->ev1) hipEventDestroy(ctx->ev1);
@@ -1520,7 +1573,7 @@ static int launch_resident(const void* fn, dim3 grid, dim3 block, void** args, s
 // every workgroup resident: cooperative launch (the runtime checks the grid fits).
 static int launch_schedule(hipStream_t st, const Geometry& g, int n_jobs, int bins_cap, bool need_general, int n_keys,
                            const DevJob* jobs, const kss_profile& prof, unsigned long long* gran, int* err,
-                           unsigned long long* stamps = nullptr) {
+                           unsigned long long* stamps = nullptr, unsigned epoch0 = 0) {
   const int cap = g.threads * g.npt;
   const size_t base = lds_bytes(bins_cap, cap);
   if (base > KSS_LDS_BUDGET) return fail(KSS_E_UNSUPPORTED, "per-workgroup LDS budget exceeded (too many nodes per shard)");
@@ -1539,13 +1592,15 @@ static int launch_schedule(hipStream_t st, const Geometry& g, int n_jobs, int bi
   int W = g.W, npt = g.npt;
   if (g.W > 1) {
     void* args[] = {(void*)&jobs, (void*)&pr,   (void*)&W,   (void*)&npt,   (void*)&bins_cap,
-                    (void*)&cache_keys, (void*)&gran, (void*)&err, (void*)&stamps};
+                    (void*)&cache_keys, (void*)&gran, (void*)&err, (void*)&stamps, (void*)&epoch0};
     if (int rc = launch_resident(fn, grid, block, args, shmem, st)) return rc;
   } else {
     if (gen)
-      hipLaunchKernelGGL(k_schedule<true>, grid, block, shmem, st, jobs, pr, W, npt, bins_cap, cache_keys, gran, err, stamps);
+      hipLaunchKernelGGL(k_schedule<true>, grid, block, shmem, st, jobs, pr, W, npt, bins_cap, cache_keys, gran, err, stamps,
+                         epoch0);
     else
-      hipLaunchKernelGGL(k_schedule<false>, grid, block, shmem, st, jobs, pr, W, npt, bins_cap, cache_keys, gran, err, stamps);
+      hipLaunchKernelGGL(k_schedule<false>, grid, block, shmem, st, jobs, pr, W, npt, bins_cap, cache_keys, gran, err, stamps,
+                         epoch0);
     HIP_TRY(hipGetLastError());
   }
   return 0;
@@ -1690,8 +1745,26 @@ static int launch_spread(hipStream_t st, const Geometry& g, const GpodNeeds& q, 
 }
 
 // run k_schedule / k_simple / k_spread on the loaded cluster for pods [0, n); results stay on the device
+// A device range copied back with the launch's outcome (one pinned staging, one sync).
+struct ReadBack {
+  const void* src = nullptr;
+  size_t bytes = 0;
+  const char* host = nullptr;  // set by run_single: the bytes in pinned memory until the next call
+};
+
+static int ensure_pinned(void*& p, size_t& cap, size_t need) {
+  if (cap >= need) return 0;
+  if (p) HIP_TRY(hipHostFree(p));
+  p = nullptr;
+  cap = 0;
+  HIP_TRY(hipHostMalloc(&p, std::max(need, (size_t)4096), hipHostMallocDefault));
+  cap = std::max(need, (size_t)4096);
+  return 0;
+}
+
 static int run_single(kss_ctx* ctx, const PlanNeeds& need, const DevPods& dp, int n, bool commit, bool record,
-                      bool keep_norm, uint32_t flags, int32_t* chosen_out, bool staged = false) {
+                      bool keep_norm, uint32_t flags, int32_t* chosen_out, bool staged = false, ReadBack* rbk = nullptr,
+                      const PackedUpload* pu = nullptr) {
   const size_t N = (size_t)ctx->dc.N;
   const SlotLayout SL(N);
   const int nslots = record ? std::max(n, 1) : 1;
@@ -1791,14 +1864,39 @@ static int run_single(kss_ctx* ctx, const PlanNeeds& need, const DevPods& dp, in
   if (rc) return rc;
   unsigned long long* gran = nullptr;
   const size_t gb = sizeof(unsigned long long) * 2 * (size_t)g.W * std::max(2 * XW_MAX, G_XW);
+  unsigned epoch0 = 0;
   if (g.W > 1) {
+    const void* before = ctx->gran_buf.p;
     rc = ctx->gran_buf.ensure(gb);
     if (rc) return rc;
     gran = (unsigned long long*)ctx->gran_buf.p;
-    HIP_TRY(hipMemsetAsync(gran, 0, gb, ctx->stream));  // every polled word zeroed before every launch
+    // k_schedule after k_schedule continues the epochs (a stale tag never equals a new epoch);
+    // the loop kernels restart theirs, so they, a fresh buffer, or a near-wrap clear it
+    const unsigned span = 8u * (unsigned)std::max(n, 1) + 16u;
+    const bool reuse = !loop && before == ctx->gran_buf.p && ctx->gran_epoch != 0 &&
+                       (uint64_t)ctx->gran_epoch + span < (1ull << 31);
+    if (reuse) {
+      epoch0 = ctx->gran_epoch;
+    } else {
+      HIP_TRY(hipMemsetAsync(gran, 0, gb, ctx->stream));  // every polled word zeroed
+    }
+    ctx->gran_epoch = loop ? 0 : epoch0 + span;
   }
-  HIP_TRY(hipMemsetAsync(ctx->err_buf.p, 0, 16, ctx->stream));
-  HIP_TRY(hipMemcpyAsync(ctx->job_buf.p, &job, sizeof(DevJob), hipMemcpyHostToDevice, ctx->stream));
+  int* errp = (int*)ctx->err_buf.p;
+  if (pu) {
+    errp = (int*)(pu->dev + pu->extra_off + align_up(sizeof(DevJob), 16));  // zero in the upload image
+    std::memset(pu->host + pu->extra_off + align_up(sizeof(DevJob), 16), 0, 16);
+  } else {
+    HIP_TRY(hipMemsetAsync(ctx->err_buf.p, 0, 16, ctx->stream));
+  }
+  const DevJob* jd = (const DevJob*)ctx->job_buf.p;
+  if (pu) {  // the job rides in the per-pod call's single upload
+    std::memcpy(pu->host + pu->extra_off, &job, sizeof(DevJob));
+    HIP_TRY(hipMemcpyAsync(pu->dev, pu->host, pu->bytes, hipMemcpyHostToDevice, ctx->stream));
+    jd = (const DevJob*)(pu->dev + pu->extra_off);
+  } else {
+    HIP_TRY(hipMemcpyAsync(ctx->job_buf.p, &job, sizeof(DevJob), hipMemcpyHostToDevice, ctx->stream));
+  }
   HIP_TRY(hipEventRecord(ctx->ev0, ctx->stream));
   unsigned long long* stamps = nullptr;
   // k_schedule: shard 0 only; k_simple: every shard (arrival skew of the exchanges)
@@ -1815,18 +1913,28 @@ static int run_single(kss_ctx* ctx, const PlanNeeds& need, const DevPods& dp, in
     ctx->loop_ev.push_back(e);
   }
   if (simple)
-    rc = launch_simple(ctx->stream, g, 1, (const DevJob*)ctx->job_buf.p, ctx->prof, n, (int)N, chunk, gran, gb,
-                       (int*)ctx->err_buf.p, stamps, ctx->loop_ev.data());
+    rc = launch_simple(ctx->stream, g, 1, jd, ctx->prof, n, (int)N, chunk, gran, gb,
+                       errp, stamps, ctx->loop_ev.data());
   else if (spread)
-    rc = launch_spread(ctx->stream, g, ctx->gneed, ctx->dc.n_keys, n_res, (const DevJob*)ctx->job_buf.p, ctx->prof, n,
-                       (int)N, chunk, gran, gb, (int*)ctx->err_buf.p, stamps, ctx->loop_ev.data());
+    rc = launch_spread(ctx->stream, g, ctx->gneed, ctx->dc.n_keys, n_res, jd, ctx->prof, n,
+                       (int)N, chunk, gran, gb, errp, stamps, ctx->loop_ev.data());
   else
     rc = launch_schedule(ctx->stream, g, 1, std::max(need.bins_cap, 0), need.general, ctx->dc.n_keys,
-                         (const DevJob*)ctx->job_buf.p, ctx->prof, gran, (int*)ctx->err_buf.p, stamps);
+                         jd, ctx->prof, gran, errp, stamps, epoch0);
   if (rc) return rc;
   ctx->last_kernel = simple ? 1 : (spread ? 2 : 0);
   HIP_TRY(hipEventRecord(ctx->ev1, ctx->stream));
+  // every read-back of the launch into one pinned staging, then one synchronisation
+  const size_t mb = sizeof(PodMeta) * (size_t)std::max(n, 1), cb = chosen_out && n ? sizeof(int32_t) * (size_t)n : 0;
+  const size_t o_meta = 16, o_chosen = align_up(o_meta + mb, 16), o_rb = align_up(o_chosen + cb, 16);
+  if ((rc = ensure_pinned(ctx->rb, ctx->rb_cap, o_rb + (rbk ? rbk->bytes : 0)))) return rc;
+  char* hb = (char*)ctx->rb;
+  HIP_TRY(hipMemcpyAsync(hb, errp, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+  HIP_TRY(hipMemcpyAsync(hb + o_meta, ctx->meta_buf.p, mb, hipMemcpyDeviceToHost, ctx->stream));
+  if (cb) HIP_TRY(hipMemcpyAsync(hb + o_chosen, ctx->chosen_buf.p, cb, hipMemcpyDeviceToHost, ctx->stream));
+  if (rbk && rbk->bytes) HIP_TRY(hipMemcpyAsync(hb + o_rb, rbk->src, rbk->bytes, hipMemcpyDeviceToHost, ctx->stream));
   HIP_TRY(hipStreamSynchronize(ctx->stream));
+  if (rbk) rbk->host = hb + o_rb;
   float ms = 0;
   HIP_TRY(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
   ctx->last_ms = ms;
@@ -1841,15 +1949,15 @@ static int run_single(kss_ctx* ctx, const PlanNeeds& need, const DevPods& dp, in
   ctx->last_geom[1] = g.threads;
   ctx->last_geom[2] = g.npt;
   int errw = 0;
-  HIP_TRY(hipMemcpy(&errw, ctx->err_buf.p, sizeof(int), hipMemcpyDeviceToHost));
+  std::memcpy(&errw, hb, sizeof(int));
   if (errw) return fail(KSS_E_DEVICE, "shard exchange timed out (workgroups not co-resident?)");
   if (commit) {
     ctx->count_bound = count_total;
     ctx->cell_bound = std::max(ctx->cell_bound, cell_total);
   }
   ctx->meta_host.resize((size_t)std::max(n, 1));
-  HIP_TRY(hipMemcpy(ctx->meta_host.data(), ctx->meta_buf.p, sizeof(PodMeta) * (size_t)std::max(n, 1), hipMemcpyDeviceToHost));
-  if (chosen_out && n) HIP_TRY(hipMemcpy(chosen_out, ctx->chosen_buf.p, sizeof(int32_t) * n, hipMemcpyDeviceToHost));
+  std::memcpy(ctx->meta_host.data(), hb + o_meta, mb);
+  if (cb) std::memcpy(chosen_out, hb + o_chosen, cb);
   ctx->recorded = record ? n : (n > 0 && !loop ? 1 : 0);
   ctx->meta_n = n;
   ctx->axis_meta_dirty = false;
@@ -1898,37 +2006,34 @@ static int stage_spods(kss_ctx* ctx, const kss_podset* ps) {
 
 // One record slot to the caller's arrays: the span of the requested fields in one D2H copy
 // through pinned staging (the slot is contiguous: SlotLayout), then host copies.
-static int copy_slot(kss_ctx* ctx, int slot, const PodMeta& m, kss_pod_result* out) {
-  const size_t N = (size_t)ctx->dc.N;
+// The byte range [lo, hi) of a slot that a result's requested arrays cover.
+struct SlotRange {
+  size_t lo, hi;
+};
+
+static SlotRange slot_range(size_t N, const kss_pod_result* out) {
   const SlotLayout SL(N);
-  const char* base = (const char*)ctx->slot_buf.p + (size_t)slot * SL.bytes;
-  struct Part {
-    void* dst;
-    size_t off, bytes;
-  } parts[5] = {{out->fail_plugin, SL.fail, N},
-                {out->fail_detail, SL.detail, 2 * N},
-                {out->raw, SL.raw, 8 * KSS_NSCORE * N},
-                {out->norm, SL.norm, 8 * KSS_NSCORE * N},
-                {out->total, SL.total, 8 * N}};
-  size_t lo = SL.bytes, hi = 0;
-  for (const Part& q : parts)
-    if (q.dst && q.bytes) {
-      lo = std::min(lo, q.off);
-      hi = std::max(hi, q.off + q.bytes);
+  const void* dst[5] = {out->fail_plugin, out->fail_detail, out->raw, out->norm, out->total};
+  const size_t off[5] = {SL.fail, SL.detail, SL.raw, SL.norm, SL.total};
+  const size_t bytes[5] = {N, 2 * N, 8 * KSS_NSCORE * N, 8 * KSS_NSCORE * N, 8 * N};
+  SlotRange r{SL.bytes, 0};
+  for (int i = 0; i < 5; i++)
+    if (dst[i] && bytes[i]) {
+      r.lo = std::min(r.lo, off[i]);
+      r.hi = std::max(r.hi, off[i] + bytes[i]);
     }
-  if (hi > lo) {
-    if (ctx->pinned_cap < hi - lo) {
-      if (ctx->pinned) HIP_TRY(hipHostFree(ctx->pinned));
-      ctx->pinned = nullptr;
-      ctx->pinned_cap = 0;
-      HIP_TRY(hipHostMalloc(&ctx->pinned, hi - lo, hipHostMallocDefault));
-      ctx->pinned_cap = hi - lo;
-    }
-    HIP_TRY(hipMemcpyAsync(ctx->pinned, base + lo, hi - lo, hipMemcpyDeviceToHost, ctx->stream));
-    HIP_TRY(hipStreamSynchronize(ctx->stream));
-    for (const Part& q : parts)
-      if (q.dst && q.bytes) std::memcpy(q.dst, (const char*)ctx->pinned + (q.off - lo), q.bytes);
-  }
+  return r;
+}
+
+// slot bytes [r.lo, r.hi) at `src` (host) -> the result's arrays, plus the pod's outcome
+static int scatter_slot(size_t N, const SlotRange& r, const char* src, const PodMeta& m, kss_pod_result* out) {
+  const SlotLayout SL(N);
+  void* dst[5] = {out->fail_plugin, out->fail_detail, out->raw, out->norm, out->total};
+  const size_t off[5] = {SL.fail, SL.detail, SL.raw, SL.norm, SL.total};
+  const size_t bytes[5] = {N, 2 * N, 8 * KSS_NSCORE * N, 8 * KSS_NSCORE * N, 8 * N};
+  if (r.hi > r.lo)
+    for (int i = 0; i < 5; i++)
+      if (dst[i] && bytes[i]) std::memcpy(dst[i], src + (off[i] - r.lo), bytes[i]);
   out->n_feasible = m.n_feasible;
   out->chosen = m.chosen;
   out->best_total = m.best_total;
@@ -1936,6 +2041,21 @@ static int copy_slot(kss_ctx* ctx, int slot, const PodMeta& m, kss_pod_result* o
   out->status = m.status;
   if (m.status == 4) return fail(KSS_E_UNSUPPORTED, "pod program exceeds the device path's per-pod limits");
   return 0;
+}
+
+// One recorded slot -> the caller's arrays: only the requested span, in one copy through
+// pinned staging (the slot is contiguous: SlotLayout), then host copies.
+static int copy_slot(kss_ctx* ctx, int slot, const PodMeta& m, kss_pod_result* out) {
+  const size_t N = (size_t)ctx->dc.N;
+  const SlotLayout SL(N);
+  const char* base = (const char*)ctx->slot_buf.p + (size_t)slot * SL.bytes;
+  const SlotRange r = slot_range(N, out);
+  if (r.hi > r.lo) {
+    if (int rc = ensure_pinned(ctx->pinned, ctx->pinned_cap, r.hi - r.lo)) return rc;
+    HIP_TRY(hipMemcpyAsync(ctx->pinned, base + r.lo, r.hi - r.lo, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+  }
+  return scatter_slot(N, r, (const char*)ctx->pinned, m, out);
 }
 
 // One pod of a podset with its own compact pools (every pool reference remapped): the
@@ -2025,12 +2145,20 @@ int kss_eval_pod(kss_ctx* ctx, const kss_podset* ps, int32_t pod_index, kss_pod_
   if ((rc = validate(&ctx->host, &one.ps, 1))) return rc;
   std::lock_guard<std::mutex> lk(ctx->mu);
   HIP_TRY(hipSetDevice(ctx->cfg.device));
-  rc = upload_podset(ctx->stream, ctx->tmp_pod_buf, &one.ps, ctx->tdp);
+  PackedUpload pu;
+  rc = pack_podset(ctx->tmp_pod_buf, ctx->up, ctx->up_cap, &one.ps, align_up(sizeof(DevJob), 16) + 16, ctx->tdp, pu);
   if (rc) return rc;
   const PlanNeeds need = plan_needs(ctx->key_card_h.data(), ctx->key_flags_h.data(), &one.ps, 1);
-  rc = run_single(ctx, need, ctx->tdp, 1, /*commit=*/false, /*record=*/false, /*keep_norm=*/true, 0, nullptr);
+  const size_t N = (size_t)ctx->dc.N;
+  const SlotRange r = slot_range(N, out);
+  if ((rc = ctx->slot_buf.ensure(SlotLayout(N).bytes))) return rc;
+  ReadBack rbk;
+  rbk.src = (const char*)ctx->slot_buf.p + r.lo;
+  rbk.bytes = r.hi > r.lo ? r.hi - r.lo : 0;
+  rc = run_single(ctx, need, ctx->tdp, 1, /*commit=*/false, /*record=*/false, /*keep_norm=*/true, 0, nullptr,
+                  /*staged=*/false, &rbk, &pu);
   if (rc) return rc;
-  return copy_slot(ctx, 0, ctx->meta_host[0], out);
+  return scatter_slot(N, r, rbk.host, ctx->meta_host[0], out);
 }
 
 // A pending pod as a bound pod of the PostFilter table once committed (id -1 - index,
@@ -2093,8 +2221,7 @@ static int commit_one(kss_ctx* ctx, const kss_podset* ps, int32_t pod_index, int
     ctx->cell_bound += 1.0 + (double)p.own_terms_len;
   }
   hipLaunchKernelGGL(k_commit, dim3(1), dim3(64), 0, ctx->stream, ctx->dc, a);
-  HIP_TRY(hipGetLastError());
-  HIP_TRY(hipStreamSynchronize(ctx->stream));
+  HIP_TRY(hipGetLastError());  // no synchronisation: every later call on the ctx stream is ordered after it
   ctx->bound_log.push_back(BoundOp{local, sign > 0 ? 1 : 0, bound_from_pod(ps, pod_index)});
   ctx->bound_dirty = true;
   return 0;
