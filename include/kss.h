@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define KSS_ABI_VERSION 1
+#define KSS_ABI_VERSION 2
 
 /* ---- error codes ------------------------------------------------------- */
 #define KSS_OK 0
@@ -123,6 +123,12 @@ enum kss_score_plugin {
 #define KSS_TAINT_ORDER 8
 /* Maximum domain cardinality of a NON-unique topology key on the device path. */
 #define KSS_MAX_BINS 1024
+/* Host-port dictionary size (uint64 masks): distinct (hostIP, protocol, hostPort) entries of
+ * the snapshot's NodeInfo.UsedPorts and the pending pods' container ports. */
+#define KSS_MAX_PORTS 64
+/* ImageLocality thresholds (image_locality.go: minThreshold 23 MiB, maxContainerThreshold 1000 MiB) */
+#define KSS_IMAGE_MIN_THRESHOLD (23ll * 1024 * 1024)
+#define KSS_IMAGE_MAX_CONTAINER_THRESHOLD (1000ll * 1024 * 1024)
 
 /*
  * Cluster snapshot, struct-of-arrays, canonical node order.  All arrays are
@@ -158,6 +164,15 @@ typedef struct kss_cluster {
   const uint8_t* value_is_int; /* [n_label_values] 1 if ParseInt succeeded */
   const int32_t* class_count;  /* [n_classes][n_nodes] #pods of class c on node n */
   const int32_t* term_count;   /* [n_terms][n_nodes]   #occurrences of term type t among pods on node n */
+  /* NodePorts: NodeInfo.UsedPorts as bits over the port dictionary (framework.HostPortInfo;
+   * hostIP "" -> 0.0.0.0, protocol "" -> TCP).  NULL or n_ports == 0: no host port in use. */
+  int32_t n_ports;
+  /* ImageLocality: rows of image_score, one per image name a pending pod's container
+   * references (normalizedImageName) that some node lists in Status.Images. */
+  int32_t n_images;
+  const uint64_t* port_used;   /* [n_nodes] */
+  const int64_t* image_score;  /* [n_images][n_nodes] scaledImageScore(NodeInfo.ImageStates[name], totalNumNodes),
+                                  0 where the node does not list the image */
 } kss_cluster;
 
 /* ---- pod programs --------------------------------------------------------
@@ -260,6 +275,18 @@ typedef struct kss_pod {
   int32_t names_off, names_len;    /* NodeAffinity PreFilterResult node set (ints[], global idx); len<0: all nodes */
   int32_t priority;                /* corev1helpers.PodPriority: spec.priority, 0 when unset (DefaultPreemption) */
   int32_t pad;
+  /* NodePorts (nodeports.go): port_conflict = dictionary entries any wanted container host
+   * port conflicts with (HostPortInfo.CheckConflict: same protocol and port, and either IP is
+   * 0.0.0.0 or both are equal); port_add = the pod's own entries (NodeInfo.AddPod
+   * updateUsedPorts).  Both 0 for pods without host ports. */
+  uint64_t port_conflict;
+  uint64_t port_add;
+  /* ImageLocality (image_locality.go): image_score rows of the pod's containers, one entry per
+   * container whose normalized image some node lists (ints[img_off .. +img_len)); n_containers =
+   * len(pod.Spec.Containers) for calculatePriority's maxThreshold. */
+  int32_t img_off, img_len;
+  int32_t n_containers;
+  int32_t pad2;
 } kss_pod;
 
 typedef struct kss_podset {
@@ -342,6 +369,11 @@ int kss_apply_count_delta(kss_ctx* ctx, const int32_t* node, const int32_t* row,
 /* read back the mutable columns (requested [KSS_NRES][N], nonzero [2][N], pod_count [N]) */
 int kss_read_node_state(kss_ctx* ctx, int64_t* requested, int64_t* nonzero, int32_t* pod_count,
                         int32_t* class_count /*[n_classes][N] or NULL*/, int32_t* term_count /*or NULL*/);
+/* NodeInfo.UsedPorts of every row (port dictionary bits, [N]): read back, or overwrite rows
+ * idx[0..n) (pods with host ports bound or deleted outside this context).  Replaces the
+ * informer's NodeInfo.AddPod / RemovePod updateUsedPorts on the scheduler cache. */
+int kss_read_port_state(kss_ctx* ctx, uint64_t* port_used);
+int kss_apply_port_delta(kss_ctx* ctx, const int32_t* idx, int32_t n, const uint64_t* port_used);
 
 /* evaluate one pod against the current snapshot (no commit): the PreFilter-time call.  Only
  * the pod's own program is uploaded; the record comes back in one copy. */

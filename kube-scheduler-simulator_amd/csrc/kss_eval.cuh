@@ -59,6 +59,9 @@ struct DevCluster {
   int32_t* class_count;
   int32_t* term_count;
   const double* log_table;  // go_log(k + 2), k in [0, N]
+  uint64_t* port_used;        // [N] NodeInfo.UsedPorts dictionary bits (mutable: AssumePod adds)
+  const int64_t* image_score; // [n_images][N] scaledImageScore, 0 = image absent
+  int32_t n_images;
   // Shard-resident LDS copies of the hot node columns (set inside the kernel; null on
   // the host and in kernels without a cache).  Slot i holds node nc_lo + i.
   int64_t* nc64;    // [8][nc_cap]: alloc cpu/mem/eph, requested cpu/mem/eph, nonzero cpu/mem
@@ -275,6 +278,10 @@ __device__ __forceinline__ int filter_local(const DevCluster& c, const DevPods& 
   if ((enabled >> KSS_F_NODE_AFFINITY) & 1u) {
     if (!required_affinity(c, P, p, n)) return KSS_F_NODE_AFFINITY;
   }
+  // NodePorts.Filter -> fitsPorts: HostPortInfo.CheckConflict of every wanted port
+  if ((enabled >> KSS_F_NODE_PORTS) & 1u) {
+    if (p.port_conflict && (c.port_used[n] & p.port_conflict)) return KSS_F_NODE_PORTS;
+  }
   // NodeResourcesFit.Filter -> fitsRequest
   if ((enabled >> KSS_F_NODE_RESOURCES_FIT) & 1u) {
     const size_t N = (size_t)c.N;
@@ -413,6 +420,22 @@ __device__ __forceinline__ int64_t ba_score(const DevCluster& c, const kss_profi
 // TaintToleration.Score: countIntolerableTaintsPreferNoSchedule
 __device__ __forceinline__ int64_t tt_score(const NodeRow& row, const kss_pod& p) {
   return (int64_t)__popcll(row.ts & ~p.tol_soft);
+}
+
+// ImageLocality.Score (image_locality.go): calculatePriority(sumImageScores, len(Containers));
+// the per-(image, node) scaledImageScore is host-resolved into c.image_score.
+__host__ __device__ inline int64_t image_priority(int64_t sum, int n_containers) {
+  const int64_t max_t = KSS_IMAGE_MAX_CONTAINER_THRESHOLD * (int64_t)n_containers;
+  if (sum < KSS_IMAGE_MIN_THRESHOLD) sum = KSS_IMAGE_MIN_THRESHOLD;
+  else if (sum > max_t) sum = max_t;
+  return (int64_t)100 * (sum - KSS_IMAGE_MIN_THRESHOLD) / (max_t - KSS_IMAGE_MIN_THRESHOLD);
+}
+
+__device__ __forceinline__ int64_t il_score(const DevCluster& c, const DevPods& P, const kss_pod& p, int n) {
+  if (p.img_len <= 0) return 0;
+  int64_t sum = 0;
+  for (int i = 0; i < p.img_len; i++) sum += c.image_score[(size_t)P.ints[p.img_off + i] * (size_t)c.N + (size_t)n];
+  return image_priority(sum, p.n_containers);
 }
 
 __device__ __forceinline__ int64_t na_score(const DevCluster& c, const DevPods& P, const kss_pod& p, int n) {

@@ -250,6 +250,7 @@ __global__ void k_go_log(const double* x, double* y, int n) {
 struct CommitArgs {
   int64_t req[KSS_NRES];
   int64_t nz[2];
+  uint64_t port_add;
   int32_t cls, n_own, local, sign;
   int32_t own[8];
 };
@@ -263,6 +264,7 @@ __global__ void k_commit(DevCluster c, CommitArgs a) {
   c.pod_count[a.local] += a.sign;
   if (a.cls >= 0) c.class_count[(size_t)a.cls * N + a.local] += a.sign;
   for (int i = 0; i < a.n_own; i++) c.term_count[(size_t)a.own[i] * N + a.local] += a.sign;
+  if (a.port_add) c.port_used[a.local] = a.sign > 0 ? (c.port_used[a.local] | a.port_add) : (c.port_used[a.local] & ~a.port_add);
 }
 
 // DefaultPreemption PostFilter dry run of one pod (kss_postfilter_pod): three launches.
@@ -346,6 +348,7 @@ struct GpodNeeds {
 
 // Per-batch LDS / exchange sizing: the host restatement of make_plan's bin counts.
 struct PlanNeeds {
+  bool ports_images = false;  // some pod has host ports or ImageLocality rows
   int bins_cap = 0;  // max over pods of histogram + presence bins
   int xw = 0;        // max exchange payload length (values) over pods and exchanges
   bool general = false;  // some pod carries spread / inter-pod-affinity programs
@@ -378,8 +381,8 @@ struct kss_ctx {
   DevCluster dc{};
   DevBuf cluster_buf;
   DevBuf pristine_buf;  // load-time copy of the mutable columns (kss_reset_node_state)
-  size_t mut_bytes[5] = {0, 0, 0, 0, 0};
-  size_t pristine_off[5] = {0, 0, 0, 0, 0};
+  size_t mut_bytes[6] = {0, 0, 0, 0, 0, 0};
+  size_t pristine_off[6] = {0, 0, 0, 0, 0, 0};
   // pods
   DevBuf pod_buf;      // staged pod programs (kss_stage_pods / kss_schedule_batch)
   DevPods dp{};
@@ -580,6 +583,14 @@ int validate(const kss_cluster* cl, const kss_podset* ps, int n) {
       if (ps->ints[p.own_terms_off + j] < 0 || ps->ints[p.own_terms_off + j] >= cl->n_terms)
         return fail(KSS_E_INVAL, "own term id out of range");
     if (p.n_hard > MAXH || p.n_soft > MAXS) return fail(KSS_E_UNSUPPORTED, "too many spread constraints for the device path");
+    if (cl->n_ports < KSS_MAX_PORTS && ((p.port_conflict | p.port_add) >> cl->n_ports))
+      return fail(KSS_E_INVAL, "pod port bit outside the port dictionary");
+    if (p.img_len > 0) {
+      if (!in(p.img_off, p.img_len, ps->n_ints) || p.n_containers < 1) return fail(KSS_E_INVAL, "pod image rows out of range");
+      for (int j = 0; j < p.img_len; j++)
+        if (ps->ints[p.img_off + j] < 0 || ps->ints[p.img_off + j] >= cl->n_images)
+          return fail(KSS_E_INVAL, "image row id out of range");
+    }
   }
   return 0;
 }
@@ -628,6 +639,7 @@ bool f64_exact(const F64Bounds& c, const F64Bounds& p, int n_pods) {
 // Compact record of one pod (kss_simple.cuh SPod); false when the preferred NodeAffinity
 // weights do not fit the static word's 20 bits.
 bool fill_spod(const kss_podset* ps, const kss_pod& p, int n_scalar, SPod& q) {
+  if (p.port_conflict | p.port_add || p.img_len > 0) return false;  // NodePorts / ImageLocality: k_schedule
   int64_t wsum = 0;
   for (int t = 0; t < p.pref_len; t++) wsum += std::max(0, ps->terms[p.pref_off + t].weight);
   if (wsum > 0xFFFFF) return false;  // static word: 20 bits of raw NodeAffinity
@@ -682,6 +694,7 @@ enum {
   GP_RECORD,
   GP_IPA,
   GP_SCALAR,
+  GP_PORTS_IMAGES,
   GP_NCODES
 };
 const char* const kGpReason[GP_NCODES] = {
@@ -698,6 +711,7 @@ const char* const kGpReason[GP_NCODES] = {
     "a pod's record exceeds 2 KiB (too many references)",
     "more than 16 inter-pod-affinity entries after merging",
     "extended (scalar) resources in the cluster: k_simple / k_spread keep cpu, memory and ephemeral-storage only",
+    "host ports (NodePorts) or node-cached images (ImageLocality): k_schedule only",
 };
 
 bool gfail(GpodNeeds& need, int code, int pod) {
@@ -724,6 +738,7 @@ bool build_gpods(const kss_podset* ps, int n_scalar, int n_classes, const int32_
     const kss_pod& p = ps->pods[i];
     GPod& g = out[(size_t)i];
     std::vector<uint32_t>& R = refs_of[(size_t)i];
+    if (p.port_conflict | p.port_add || p.img_len > 0) return gfail(need, GP_PORTS_IMAGES, i);
     if (!fill_spod(ps, p, n_scalar, g.dyn)) return gfail(need, GP_NA_WEIGHTS, i);
     if (p.n_hard > MAXH || p.n_soft > MAXS) return gfail(need, GP_CONSTRAINTS, i);
     g.pflags = (int32_t)p.flags;
@@ -946,7 +961,7 @@ bool spread_bounds_ok(const GpodNeeds& q, double total, double cell, int N) {
 
 struct ClusterLayout {
   size_t o_alloc, o_req, o_nz, o_allowed, o_podc, o_flags, o_th, o_ts, o_to, o_lv, o_kb, o_kc, o_kf, o_ke, o_vi, o_vii,
-      o_cc, o_tc, o_log, total;
+      o_cc, o_tc, o_log, o_pu, o_img, total;
   ClusterLayout(const kss_cluster* cl, int class_cap, int term_cap) {
     const size_t N = (size_t)cl->n_nodes;
     size_t o = 0;
@@ -974,6 +989,8 @@ struct ClusterLayout {
     o_cc = take(4 * (size_t)class_cap * N);
     o_tc = take(4 * (size_t)term_cap * N);
     o_log = take(8 * (N + 3));
+    o_pu = take(8 * N);
+    o_img = take(8 * (size_t)cl->n_images * N);
     total = o;
   }
 };
@@ -1006,6 +1023,9 @@ int fill_cluster(hipStream_t st, const kss_cluster* cl, int class_cap, int term_
   if (term_cap) HIP_TRY(hipMemsetAsync(b + L.o_tc, 0, 4 * (size_t)term_cap * N, st));
   rc |= cp(L.o_cc, cl->class_count, 4 * (size_t)cl->n_classes * N);
   rc |= cp(L.o_tc, cl->term_count, 4 * (size_t)cl->n_terms * N);
+  if (cl->port_used) rc |= cp(L.o_pu, cl->port_used, 8 * N);
+  else HIP_TRY(hipMemsetAsync(b + L.o_pu, 0, 8 * std::max<size_t>(N, 1), st));
+  rc |= cp(L.o_img, cl->image_score, 8 * (size_t)cl->n_images * N);
   logtab.resize(N + 3);
   for (size_t k = 0; k < N + 3; k++) logtab[k] = kss_go_log((double)(k + 2));
   rc |= cp(L.o_log, logtab.data(), 8 * (N + 3));
@@ -1037,6 +1057,9 @@ int fill_cluster(hipStream_t st, const kss_cluster* cl, int class_cap, int term_
   dc.class_count = (int32_t*)(b + L.o_cc);
   dc.term_count = (int32_t*)(b + L.o_tc);
   dc.log_table = (const double*)(b + L.o_log);
+  dc.port_used = (uint64_t*)(b + L.o_pu);
+  dc.image_score = (const int64_t*)(b + L.o_img);
+  dc.n_images = cl->n_images;
   return 0;
 }
 
@@ -1059,6 +1082,13 @@ int check_cluster(const kss_cluster* cl) {
   }
   for (size_t i = 0; i < N * KSS_TAINT_ORDER; i++)
     if (cl->taint_order[i] != 0xFF && cl->taint_order[i] >= cl->n_taints) return fail(KSS_E_INVAL, "taint id out of range");
+  if (cl->n_ports < 0 || cl->n_ports > KSS_MAX_PORTS) return fail(KSS_E_INVAL, "n_ports out of range");
+  if (cl->n_images < 0 || (cl->n_images > 0 && N > 0 && !cl->image_score)) return fail(KSS_E_INVAL, "missing image scores");
+  if (cl->port_used && cl->n_ports < KSS_MAX_PORTS)
+    for (size_t i = 0; i < N; i++)
+      if (cl->port_used[i] >> cl->n_ports) return fail(KSS_E_INVAL, "port bit outside the port dictionary");
+  for (size_t i = 0; i < (size_t)cl->n_images * N; i++)
+    if (cl->image_score[i] < 0) return fail(KSS_E_INVAL, "negative image score");
   return 0;
 }
 
@@ -1196,17 +1226,18 @@ int kss_load_cluster(kss_ctx* ctx, const kss_cluster* cl) {
   if (rc) return rc;
   // pristine copy of the mutable columns
   const size_t N = (size_t)cl->n_nodes;
-  const size_t mb[5] = {8 * KSS_NRES * N, 8 * 2 * N, 4 * N, 4 * (size_t)class_cap * N, 4 * (size_t)term_cap * N};
+  const size_t mb[6] = {8 * KSS_NRES * N, 8 * 2 * N, 4 * N, 4 * (size_t)class_cap * N, 4 * (size_t)term_cap * N, 8 * N};
   size_t tot = 0;
-  for (int i = 0; i < 5; i++) {
+  for (int i = 0; i < 6; i++) {
     ctx->mut_bytes[i] = mb[i];
     ctx->pristine_off[i] = tot;
     tot = align_up(tot + mb[i], 256);
   }
   rc = ctx->pristine_buf.ensure(tot);
   if (rc) return rc;
-  void* src[5] = {ctx->dc.requested, ctx->dc.nonzero, ctx->dc.pod_count, ctx->dc.class_count, ctx->dc.term_count};
-  for (int i = 0; i < 5; i++)
+  void* src[6] = {ctx->dc.requested, ctx->dc.nonzero, ctx->dc.pod_count, ctx->dc.class_count, ctx->dc.term_count,
+                  ctx->dc.port_used};
+  for (int i = 0; i < 6; i++)
     if (mb[i])
       HIP_TRY(hipMemcpyAsync((char*)ctx->pristine_buf.p + ctx->pristine_off[i], src[i], mb[i], hipMemcpyDeviceToDevice,
                              ctx->stream));
@@ -1280,6 +1311,10 @@ int kss_load_cluster_rows(kss_ctx* ctx, const kss_cluster* cl, int32_t lo, int32
   std::vector<uint32_t> flags(cl->node_flags + lo, cl->node_flags + hi);
   std::vector<uint64_t> th(cl->taint_hard + lo, cl->taint_hard + hi), ts(cl->taint_soft + lo, cl->taint_soft + hi);
   std::vector<uint8_t> to(cl->taint_order + (size_t)lo * KSS_TAINT_ORDER, cl->taint_order + (size_t)hi * KSS_TAINT_ORDER);
+  std::vector<uint64_t> pu(std::max<size_t>(M, 1), 0);
+  if (cl->port_used) std::copy(cl->port_used + lo, cl->port_used + hi, pu.begin());
+  std::vector<int64_t> img;
+  if (cl->n_images) rows64(cl->image_score, cl->n_images, img);
   kss_cluster s = *cl;
   s.n_nodes = (int32_t)M;
   s.node_base = cl->node_base + lo;
@@ -1295,6 +1330,8 @@ int kss_load_cluster_rows(kss_ctx* ctx, const kss_cluster* cl, int32_t lo, int32
   s.label_value = lv.data();
   s.class_count = cl->class_count ? cc.data() : nullptr;
   s.term_count = cl->term_count ? tc.data() : nullptr;
+  s.port_used = pu.data();
+  s.image_score = cl->n_images ? img.data() : nullptr;
   return kss_load_cluster(ctx, &s);  // synchronous: the temporaries outlive the upload
 }
 
@@ -1305,6 +1342,8 @@ static int axis_check(kss_ctx* ctx, int32_t pod_index) {
   if (pod_index < 0 || pod_index >= ctx->staged_n) return fail(KSS_E_INVAL, "pod index outside the staged pods");
   if (ctx->staged_need.general)
     return fail(KSS_E_UNSUPPORTED, "node-axis path: spread / inter-pod programs need the replicated domain histograms");
+  if (ctx->staged_need.ports_images)
+    return fail(KSS_E_UNSUPPORTED, "node-axis path: host ports / image locality are not folded into the axis key");
   return ctx->axis_cv.ensure(sizeof(int32_t) * 5 * (size_t)std::max(ctx->dc.N, 1));
 }
 
@@ -1373,12 +1412,13 @@ int kss_reset_node_state(kss_ctx* ctx) {
   if (!ctx || !ctx->loaded) return fail(KSS_E_INVAL, "no cluster loaded");
   std::lock_guard<std::mutex> lk(ctx->mu);
   HIP_TRY(hipSetDevice(ctx->cfg.device));
-  void* dst[5] = {ctx->dc.requested, ctx->dc.nonzero, ctx->dc.pod_count, ctx->dc.class_count, ctx->dc.term_count};
+  void* dst[6] = {ctx->dc.requested, ctx->dc.nonzero, ctx->dc.pod_count, ctx->dc.class_count, ctx->dc.term_count,
+                  ctx->dc.port_used};
   ctx->count_bound = ctx->count_bound0;
   ctx->cell_bound = ctx->cell_bound0;
   ctx->bound_log.clear();
   ctx->bound_dirty = true;
-  for (int i = 0; i < 5; i++)
+  for (int i = 0; i < 6; i++)
     if (ctx->mut_bytes[i])
       HIP_TRY(hipMemcpyAsync(dst[i], (char*)ctx->pristine_buf.p + ctx->pristine_off[i], ctx->mut_bytes[i],
                              hipMemcpyDeviceToDevice, ctx->stream));
@@ -1483,6 +1523,33 @@ int kss_read_node_state(kss_ctx* ctx, int64_t* requested, int64_t* nonzero, int3
   return 0;
 }
 
+int kss_read_port_state(kss_ctx* ctx, uint64_t* port_used) {
+  if (!ctx || !ctx->loaded || !port_used) return fail(KSS_E_INVAL, "bad arguments");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  HIP_TRY(hipSetDevice(ctx->cfg.device));
+  HIP_TRY(hipMemcpyAsync(port_used, ctx->dc.port_used, 8 * (size_t)ctx->dc.N, hipMemcpyDeviceToHost, ctx->stream));
+  HIP_TRY(hipStreamSynchronize(ctx->stream));
+  return 0;
+}
+
+int kss_apply_port_delta(kss_ctx* ctx, const int32_t* idx, int32_t n, const uint64_t* port_used) {
+  if (!ctx || !ctx->loaded) return fail(KSS_E_INVAL, "no cluster loaded");
+  if (n < 0 || (n > 0 && (!idx || !port_used))) return fail(KSS_E_INVAL, "bad arguments");
+  for (int i = 0; i < n; i++) {
+    if (idx[i] < 0 || idx[i] >= ctx->dc.N) return fail(KSS_E_INVAL, "port delta row out of range");
+    if (ctx->host.n_ports < KSS_MAX_PORTS && (port_used[i] >> ctx->host.n_ports))
+      return fail(KSS_E_INVAL, "port bit outside the port dictionary");
+  }
+  if (n == 0) return 0;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  HIP_TRY(hipSetDevice(ctx->cfg.device));
+  // rows are few (pods bound elsewhere): one 8-byte copy per row, ordered on the stream
+  for (int i = 0; i < n; i++)
+    HIP_TRY(hipMemcpyAsync(ctx->dc.port_used + idx[i], port_used + i, 8, hipMemcpyHostToDevice, ctx->stream));
+  HIP_TRY(hipStreamSynchronize(ctx->stream));
+  return 0;
+}
+
 static PlanNeeds plan_needs(const int32_t* key_card, const uint32_t* key_flags, const kss_podset* ps, int n) {
   PlanNeeds r;
   r.xw = 12;  // the filter exchange's scalars
@@ -1490,6 +1557,7 @@ static PlanNeeds plan_needs(const int32_t* key_card, const uint32_t* key_flags, 
     const kss_pod& p = ps->pods[i];
     int bins = 0, hp = 0, sp = 0;
     if (p.n_hard | p.n_soft | p.ipa_len) r.general = true;
+    if (p.port_conflict | p.port_add || p.img_len > 0) r.ports_images = true;
     for (int h = 0; h < p.n_hard && h < MAXH; h++) {
       const int key = ps->spreads[p.spread_off + h].key;
       if (!(key_flags[key] & KSS_KEY_UNIQUE)) {
@@ -2076,7 +2144,8 @@ static int compact_pod(const kss_podset* ps, int i, OnePod& o) {
   if (!in(p.sel_off, p.sel_len, ps->n_reqs) || !in(p.aff_off, p.aff_len, ps->n_terms) ||
       !in(p.pref_off, p.pref_len, ps->n_terms) || !in(p.spread_off, (int64_t)p.n_hard + p.n_soft, ps->n_spreads) ||
       !in(p.ipa_off, p.ipa_len, ps->n_ipa) || !in(p.own_terms_off, p.own_terms_len, ps->n_ints) ||
-      (p.names_len >= 0 && !in(p.names_off, p.names_len, ps->n_ints)))
+      (p.names_len >= 0 && !in(p.names_off, p.names_len, ps->n_ints)) ||
+      (p.img_len > 0 && !in(p.img_off, p.img_len, ps->n_ints)))
     return fail(KSS_E_INVAL, "pod program out of range");
   o = OnePod{};
   o.pod = p;
@@ -2121,6 +2190,7 @@ static int compact_pod(const kss_podset* ps, int i, OnePod& o) {
   }
   o.pod.own_terms_off = list(p.own_terms_off, p.own_terms_len);
   if (p.names_len >= 0) o.pod.names_off = list(p.names_off, p.names_len);
+  if (p.img_len > 0) o.pod.img_off = list(p.img_off, p.img_len);
   o.ps.n_pods = 1;  // empty pools stay empty (upload_podset sizes them; validate skips them)
   o.ps.n_reqs = (int32_t)o.reqs.size();
   o.ps.n_terms = (int32_t)o.terms.size();
@@ -2206,6 +2276,9 @@ static int commit_one(kss_ctx* ctx, const kss_podset* ps, int32_t pod_index, int
   for (int r = 0; r < KSS_NRES; r++) a.req[r] = p.commit_req[r];
   a.nz[0] = p.commit_nz[0];
   a.nz[1] = p.commit_nz[1];
+  a.port_add = p.port_add;
+  if (ctx->host.n_ports < KSS_MAX_PORTS && (p.port_add >> ctx->host.n_ports))
+    return fail(KSS_E_INVAL, "pod port bit outside the port dictionary");
   a.cls = p.cls;
   a.n_own = p.own_terms_len;
   for (int i = 0; i < p.own_terms_len; i++) {
@@ -2486,6 +2559,10 @@ kss_sweep* kss_sweep_create(int32_t device, const kss_profile* prof, int32_t n_s
     const PlanNeeds q = plan_needs(clusters[s].key_card, clusters[s].key_flags, &podsets[s], podsets[s].n_pods);
     sw->need.bins_cap = std::max(sw->need.bins_cap, q.bins_cap);
     sw->need.general |= q.general;
+    if (q.ports_images) {  // the sweep packs no UsedPorts / image-score columns
+      fail(KSS_E_UNSUPPORTED, "scenario sweeps: pods with host ports or ImageLocality rows take kss_schedule_batch");
+      return nullptr;
+    }
   }
   // one workgroup per scenario: at most two node slots per lane (C5, 1,000 nodes: 512
   // threads ran the 512-scenario sweep in 16.5 ms against 23.7 ms at 256)
@@ -2799,6 +2876,10 @@ int kss_postfilter_pod(kss_ctx* ctx, const kss_podset* ps, int32_t pod_index, ks
     out->status = KSS_PREEMPT_NOT_ELIGIBLE;
     return 0;
   }
+  // the victims' host ports are not in the bound-pod table: a preemptor that wants host ports
+  // (NodePorts failures are resolvable by eviction) is refused rather than mis-evaluated
+  if (ps->pods[pod_index].port_conflict)
+    return fail(KSS_E_UNSUPPORTED, "PostFilter dry run of a pod with host ports (victims' UsedPorts are not tabled)");
   OnePod one;
   int rc = compact_pod(ps, pod_index, one);
   if (rc) return rc;

@@ -727,9 +727,10 @@ __device__ __forceinline__ bool schedule_pod(const DevCluster& c, const DevPods&
       out->fail[n] = (uint8_t)f;
       out->detail[n] = detail;
     }
-    int ign = 0;
+    int ign = 0, il = 0;
     if (f == KSS_F_PASS) {
       nf++;
+      il = (int)il_score(c, P, p, n);  // ImageLocality.Score in [0, 100], carried in the fail word
       const int64_t tt = tt_score(row, p);
       const int64_t na = na_score(c, P, p, n);
       const int64_t fit = fit_score(c, prof, p, n, row);
@@ -755,7 +756,7 @@ __device__ __forceinline__ bool schedule_pod(const DevCluster& c, const DevPods&
         out->raw[KSS_S_VOLUME_BINDING * NN + n] = 0;
         out->raw[KSS_S_INTER_POD_AFFINITY * NN + n] = ipa;
         out->raw[KSS_S_BALANCED_ALLOCATION * NN + n] = ba;
-        out->raw[KSS_S_IMAGE_LOCALITY * NN + n] = 0;
+        out->raw[KSS_S_IMAGE_LOCALITY * NN + n] = il;
       }
       if (has_soft) {
         if (req_all && !has_keys(c, soft, p.n_soft, n)) {
@@ -777,7 +778,7 @@ __device__ __forceinline__ bool schedule_pod(const DevCluster& c, const DevPods&
         }
       }
     }
-    sa.fail[si] = f | (ign << 16);
+    sa.fail[si] = f | (ign << 16) | (il << 24);  // verdict | PTS-ignored bit | ImageLocality raw
   }
   KSS_STAMP(S, 2);
   if (!has_soft && !has_ipa) {
@@ -846,7 +847,7 @@ __device__ __forceinline__ bool schedule_pod(const DevCluster& c, const DevPods&
       const int fi = sa.fail[si];
       if ((fi & 0xFFFF) != KSS_F_PASS) continue;
       int64_t raw = 0;
-      if (!(fi >> 16)) {
+      if (!((fi >> 16) & 1)) {
         double s = 0.0;
 #pragma unroll
         for (int i = 0; i < MAXS; i++) {
@@ -905,7 +906,7 @@ __device__ __forceinline__ bool schedule_pod(const DevCluster& c, const DevPods&
       nm[KSS_S_POD_TOPOLOGY_SPREAD] = sa.pts[si];
       nm[KSS_S_INTER_POD_AFFINITY] = sa.ipa[si];
       nm[KSS_S_BALANCED_ALLOCATION] = sa.ba[si];
-      nm[KSS_S_IMAGE_LOCALITY] = 0;
+      nm[KSS_S_IMAGE_LOCALITY] = fi >> 24;  // no NormalizeScore
       // TaintToleration: DefaultNormalizeScore(100, reverse=true)
       if (max_tt == 0) nm[KSS_S_TAINT_TOLERATION] = 100;
       else nm[KSS_S_TAINT_TOLERATION] = 100 - div_i64(100 * nm[KSS_S_TAINT_TOLERATION], max_tt);
@@ -914,7 +915,7 @@ __device__ __forceinline__ bool schedule_pod(const DevCluster& c, const DevPods&
       // PodTopologySpread.NormalizeScore
       {
         int64_t& v = nm[KSS_S_POD_TOPOLOGY_SPREAD];
-        if (has_soft && (fi >> 16)) v = 0;
+        if (has_soft && ((fi >> 16) & 1)) v = 0;
         else if (pts_max == 0) v = 100;
         else v = div_i64(100 * (pts_max + pts_min - v), pts_max);
       }
@@ -974,6 +975,8 @@ __device__ __forceinline__ void commit_pod(const DevCluster& c, const DevPods& P
   }
   if (p.cls >= 0) c.class_count[(size_t)p.cls * N + local] += sign;
   for (int i = 0; i < p.own_terms_len; i++) c.term_count[(size_t)P.ints[p.own_terms_off + i] * N + local] += sign;
+  // NodeInfo.AddPod / RemovePod updateUsedPorts (a set: removal clears the entries)
+  if (p.port_add) c.port_used[local] = sign > 0 ? (c.port_used[local] | p.port_add) : (c.port_used[local] & ~p.port_add);
 }
 
 // Shard cache fill / write-back (all lanes of the workgroup).

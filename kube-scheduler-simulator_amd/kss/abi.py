@@ -16,6 +16,9 @@ KSS_MAX_SCALAR = 4
 KSS_MAX_TAINTS = 64
 KSS_TAINT_ORDER = 8
 KSS_MAX_BINS = 1024
+KSS_MAX_PORTS = 64
+KSS_IMAGE_MIN_THRESHOLD = 23 * 1024 * 1024
+KSS_IMAGE_MAX_CONTAINER_THRESHOLD = 1000 * 1024 * 1024
 
 # filter plugins (default MultiPoint order; simulator/scheduler/config/plugin_test.go:15-36)
 FILTER_PLUGINS = [
@@ -119,6 +122,7 @@ class Cluster(C.Structure):
         ("taint_order", P(u8)), ("label_value", P(i32)), ("key_base", P(i32)), ("key_card", P(i32)),
         ("key_flags", P(u32)), ("key_empty", P(i32)), ("value_int", P(i64)), ("value_is_int", P(u8)),
         ("class_count", P(i32)), ("term_count", P(i32)),
+        ("n_ports", i32), ("n_images", i32), ("port_used", P(u64)), ("image_score", P(i64)),
     ]
 
 
@@ -147,6 +151,8 @@ class Pod(C.Structure):
         ("pref_off", i32), ("pref_len", i32), ("spread_off", i32), ("n_hard", i32), ("n_soft", i32),
         ("ipa_off", i32), ("ipa_len", i32), ("cls", i32), ("own_terms_off", i32), ("own_terms_len", i32),
         ("prefilter_status", i32), ("names_off", i32), ("names_len", i32), ("priority", i32), ("pad", i32),
+        ("port_conflict", u64), ("port_add", u64), ("img_off", i32), ("img_len", i32), ("n_containers", i32),
+        ("pad2", i32),
     ]
 
 

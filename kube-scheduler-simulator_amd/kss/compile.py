@@ -337,6 +337,59 @@ def merge_namespaces(t: AffinityTerm, namespaces: Dict[str, Dict[str, str]]) -> 
 
 # ---------------------------------------------------------------------------
 # the compiled cluster
+def host_ports(pod) -> List[Tuple[str, str, int]]:
+    """nodeports.go getContainerPorts / NodeInfo.updateUsedPorts (v1.26: spec.containers only),
+    HostPortInfo.sanitize: hostIP "" -> 0.0.0.0, protocol "" -> TCP; hostPort <= 0 is ignored
+    (HostPortInfo.Add / CheckConflict)."""
+    out = []
+    for c in spec(pod).get("containers") or []:
+        for port in c.get("ports") or []:
+            hp = int(port.get("hostPort") or 0)
+            if hp <= 0:
+                continue
+            out.append((port.get("hostIP") or "0.0.0.0", port.get("protocol") or "TCP", hp))
+    return out
+
+
+def ports_conflict(want: Tuple[str, str, int], used: Tuple[str, str, int]) -> bool:
+    """HostPortInfo.CheckConflict of one wanted port against one used entry: the same
+    (protocol, port), and the wanted IP is 0.0.0.0 (checks every IP) or the used entry's IP
+    is 0.0.0.0 or equal."""
+    if (want[1], want[2]) != (used[1], used[2]):
+        return False
+    return want[0] == "0.0.0.0" or used[0] in ("0.0.0.0", want[0])
+
+
+def normalized_image_name(name: str) -> str:
+    """image_locality.go normalizedImageName: append ":latest" when the name has no tag."""
+    if name.rfind(":") <= name.rfind("/"):
+        name = name + ":latest"
+    return name
+
+
+def node_image_states(nodes: Sequence[dict]) -> List[Dict[str, Tuple[int, int]]]:
+    """NodeInfo.ImageStates of each node (input = cache add order) as the v1.26 scheduler
+    cache builds them (internal/cache/cache.go addNodeImageStates): the image's size is the
+    first adding node's SizeBytes, and NumNodes is copied when the node is added
+    (createImageStateSummary), i.e. the nodes listing the name among those added so far.
+    [verify] against a Go build: later releases recount NumNodes at snapshot time."""
+    size: Dict[str, int] = {}
+    seen: Dict[str, set] = {}
+    out = []
+    for n in nodes:
+        summ: Dict[str, Tuple[int, int]] = {}
+        for image in ((n.get("status") or {}).get("images") or []):
+            for nm in image.get("names") or []:
+                if nm not in size:
+                    size[nm] = int(image.get("sizeBytes") or 0)
+                    seen[nm] = set()
+                seen[nm].add(name_of(n))
+                if nm not in summ:
+                    summ[nm] = (size[nm], len(seen[nm]))
+        out.append(summ)
+    return out
+
+
 # ---------------------------------------------------------------------------
 @dataclass
 class CompiledCluster:
@@ -352,6 +405,8 @@ class CompiledCluster:
     namespaces: Dict[str, Dict[str, str]]
     bound: Dict[str, np.ndarray] = field(default_factory=dict)     # the kss_boundset arrays
     bound_names: List[Tuple[str, str]] = field(default_factory=list)  # (namespace, name) per bound id
+    ports: List[Tuple[str, str, int]] = field(default_factory=list)   # host-port dictionary (ip, protocol, port)
+    images: List[str] = field(default_factory=list)                   # image_score rows (image names)
     _keep: list = field(default_factory=list)
 
     @property
@@ -361,6 +416,10 @@ class CompiledCluster:
     def as_struct(self, node_base: int = 0) -> abi.Cluster:
         a = self.arrays
         c = abi.Cluster()
+        c.n_ports = len(self.ports)
+        c.n_images = len(self.images)
+        c.port_used = abi.ptr(a["port_used"], abi.u64)
+        c.image_score = abi.ptr(a["image_score"], abi.i64)
         c.n_nodes = self.n_nodes
         c.n_scalar = len(self.scalars)
         c.n_label_keys = len(self.label_keys)
@@ -638,11 +697,51 @@ class Compiler:
             for t in self._own_terms(p):
                 term_count[t, i] += 1
 
+        # NodePorts: the host-port dictionary over NodeInfo.UsedPorts and the pending pods' ports
+        pset = set()
+        for p in self.bound:
+            if spec(p).get("nodeName") in self.node_index:
+                pset.update(host_ports(p))
+        for p in self.pending:
+            pset.update(host_ports(p))
+        ports = sorted(pset)
+        if len(ports) > abi.KSS_MAX_PORTS:
+            raise Unsupported(f"more than {abi.KSS_MAX_PORTS} distinct host ports")
+        self.ports = ports
+        self.port_index = {e: i for i, e in enumerate(ports)}
+        port_used = np.zeros(N, dtype=np.uint64)
+        for p in self.bound:
+            nn = spec(p).get("nodeName")
+            if nn in self.node_index:
+                for e in host_ports(p):
+                    port_used[self.node_index[nn]] |= np.uint64(1) << np.uint64(self.port_index[e])
+        # ImageLocality: rows for the normalized container images of pending pods that some
+        # node lists; scaledImageScore per (row, node) with totalNumNodes = N
+        states = node_image_states(self.nodes_in)
+        canon_states = [states[i] for i in order]
+        listed = set().union(*[set(st) for st in states]) if states else set()
+        want = set()
+        for p in self.pending:
+            for c in spec(p).get("containers") or []:
+                nm = normalized_image_name(c.get("image") or "")
+                if nm in listed:
+                    want.add(nm)
+        images = sorted(want)
+        self.images = images
+        self.image_index = {nm: i for i, nm in enumerate(images)}
+        image_score = np.zeros((len(images), N), dtype=np.int64)
+        for r, nm in enumerate(images):
+            for i, st in enumerate(canon_states):
+                if nm in st:
+                    sz, num = st[nm]
+                    image_score[r, i] = int(float(sz) * (float(num) / float(N)))  # scaledImageScore
+
         arrays = dict(alloc=alloc, requested=requested, nonzero=nonzero, allowed_pods=allowed, pod_count=pod_count,
                       node_flags=flags, taint_hard=taint_hard, taint_soft=taint_soft, taint_order=taint_order,
                       label_value=label_value, key_base=key_base, key_card=key_card, key_flags=key_flags,
                       key_empty=key_empty, value_int=np.array(vint, dtype=np.int64),
-                      value_is_int=np.array(visint, dtype=np.uint8), class_count=class_count, term_count=term_count)
+                      value_is_int=np.array(visint, dtype=np.uint8), class_count=class_count, term_count=term_count,
+                      port_used=port_used, image_score=image_score)
         arrays = {k: (np.zeros(1, dtype=v.dtype) if v.size == 0 else np.ascontiguousarray(v))
                   for k, v in arrays.items()}
         nb = len(bound_names)
@@ -655,7 +754,8 @@ class Compiler:
         bound = {k: (np.zeros(1, dtype=v.dtype) if v.size == 0 else np.ascontiguousarray(v)) for k, v in bound.items()}
         self.cc = CompiledCluster(node_names=names, order=order, scalars=scalars, label_keys=label_keys,
                                   key_values=key_values, taints=taints, classes=classes, terms=terms, arrays=arrays,
-                                  namespaces=self.namespaces, bound=bound, bound_names=bound_names)
+                                  namespaces=self.namespaces, bound=bound, bound_names=bound_names, ports=ports,
+                                  images=images)
         self.node_labels = node_labels
         self.key_flags = key_flags
         pods = self._compile_pods(self.pending)
@@ -783,9 +883,21 @@ class Compiler:
         sp = spec(p)
         ns = ns_of(p)
         plabels = labels_of(p)
-        for c in (sp.get("containers") or []) + (sp.get("initContainers") or []):
-            if any(port.get("hostPort") for port in (c.get("ports") or [])):
-                raise Unsupported("pods with hostPort (NodePorts) are not supported on the device path")
+        # NodePorts PreFilter (getContainerPorts) and the pod's own UsedPorts entries
+        conflict = add = 0
+        for w in host_ports(p):
+            add |= 1 << self.port_index[w]
+            for e, j in self.port_index.items():
+                if ports_conflict(w, e):
+                    conflict |= 1 << j
+        rec["port_conflict"] = conflict
+        rec["port_add"] = add
+        # ImageLocality: one image_score row per container whose normalized image a node lists
+        conts = sp.get("containers") or []
+        rows = [self.image_index[nm] for nm in (normalized_image_name(c.get("image") or "") for c in conts)
+                if nm in self.image_index]
+        rec["n_containers"] = len(conts)
+        rec["img_off"], rec["img_len"] = self._list(rows) if rows else (0, 0)
         scal = self.scalars
         rec["fit_request"][:] = compute_pod_resource_request(p, scal)
         rec["commit_req"][:] = rec["fit_request"]

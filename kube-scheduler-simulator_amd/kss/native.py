@@ -40,6 +40,8 @@ SIGNATURES = [
     ("kss_apply_node_delta", C.c_int, [C.c_void_p, P(C.c_int32), C.c_int32, P(C.c_int64), P(C.c_int64), P(C.c_int32)]),
     ("kss_apply_count_delta", C.c_int, [C.c_void_p, P(C.c_int32), P(C.c_int32), P(C.c_int32), C.c_int32, C.c_int32]),
     ("kss_read_node_state", C.c_int, [C.c_void_p, P(C.c_int64), P(C.c_int64), P(C.c_int32), P(C.c_int32), P(C.c_int32)]),
+    ("kss_read_port_state", C.c_int, [C.c_void_p, P(C.c_uint64)]),
+    ("kss_apply_port_delta", C.c_int, [C.c_void_p, P(C.c_int32), C.c_int32, P(C.c_uint64)]),
     ("kss_eval_pod", C.c_int, [C.c_void_p, P(abi.PodSet), C.c_int32, P(abi.PodResult)]),
     ("kss_commit", C.c_int, [C.c_void_p, P(abi.PodSet), C.c_int32, C.c_int32]),
     ("kss_rollback", C.c_int, [C.c_void_p, P(abi.PodSet), C.c_int32, C.c_int32]),
@@ -95,7 +97,7 @@ def lib() -> C.CDLL:
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args
-        if L.kss_abi_version() != 1:
+        if L.kss_abi_version() != 2:
             raise ImportError("libkss ABI version mismatch")
         _lib = L
     return _lib
@@ -332,6 +334,19 @@ class Context:
                                         st["class_count"].ctypes.data_as(P(C.c_int32)),
                                         st["term_count"].ctypes.data_as(P(C.c_int32))))
         return st
+
+    def port_state(self) -> np.ndarray:
+        """NodeInfo.UsedPorts of every row as port-dictionary bits (kss_read_port_state)."""
+        out = np.zeros(max(self.n_nodes, 1), np.uint64)
+        check(lib().kss_read_port_state(self.h, out.ctypes.data_as(P(C.c_uint64))))
+        return out[:self.n_nodes]
+
+    def apply_port_delta(self, idx, used):
+        """Overwrite the UsedPorts bits of rows idx (kss_apply_port_delta)."""
+        idx = np.ascontiguousarray(idx, np.int32)
+        used = np.ascontiguousarray(used, np.uint64)
+        check(lib().kss_apply_port_delta(self.h, idx.ctypes.data_as(P(C.c_int32)), len(idx),
+                                         used.ctypes.data_as(P(C.c_uint64))))
 
     def last_timing(self):
         ms = C.c_double(0)

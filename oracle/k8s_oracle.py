@@ -261,10 +261,30 @@ class PodInfo:
                                for w in pn.get("preferredDuringSchedulingIgnoredDuringExecution") or []]
 
 
+def _container_host_ports(pod):
+    """(hostIP, protocol, hostPort) of the pod's containers' ports, HostPortInfo-sanitized
+    (framework/types.go: "" -> 0.0.0.0 / TCP; hostPort <= 0 never added nor checked)."""
+    out = []
+    for c in _spec(pod).get("containers") or []:
+        for cp in c.get("ports") or []:
+            port = int(cp.get("hostPort") or 0)
+            if port > 0:
+                out.append((cp.get("hostIP") or "0.0.0.0", cp.get("protocol") or "TCP", port))
+    return out
+
+
+def check_conflict(used, ip, protocol, port) -> bool:
+    """framework.HostPortInfo.CheckConflict over a set of (ip, protocol, port)."""
+    if ip == "0.0.0.0":
+        return any((pr, po) == (protocol, port) for _, pr, po in used)
+    return ("0.0.0.0", protocol, port) in used or (ip, protocol, port) in used
+
+
 class NodeInfo:
     def __init__(self, node):
         self.node = node
         self.pods: List[PodInfo] = []
+        self.used_ports = set()
         self.requested = Resource()
         self.nz_cpu = 0
         self.nz_mem = 0
@@ -283,6 +303,7 @@ class NodeInfo:
         self.nz_cpu += c0
         self.nz_mem += m0
         self.pods.append(PodInfo(pod))
+        self.used_ports.update(_container_host_ports(pod))  # updateUsedPorts(pod, true)
 
     def remove_pod(self, pod):
         """NodeInfo.RemovePod: resources back, removeFromSlice (swap with the last element)."""
@@ -301,6 +322,7 @@ class NodeInfo:
             self.requested.scalars[k] = self.requested.scalars.get(k, 0) - v
         self.nz_cpu -= c0
         self.nz_mem -= m0
+        self.used_ports.difference_update(_container_host_ports(pod))  # HostPortInfo.Remove
 
     def clone(self):
         c = NodeInfo.__new__(NodeInfo)
@@ -313,6 +335,8 @@ class NodeInfo:
         c.requested.allowed_pods = self.requested.allowed_pods
         c.nz_cpu, c.nz_mem = self.nz_cpu, self.nz_mem
         c.allocatable = self.allocatable
+        c.used_ports = set(self.used_ports)
+        c.image_states = getattr(self, "image_states", {})
         return c
 
 
@@ -446,6 +470,7 @@ MSG = {
     "NodeUnschedulable": "node(s) were unschedulable",
     "NodeName": "node(s) didn't match the requested node name",
     "NodeAffinity": "node(s) didn't match Pod's node affinity/selector",
+    "NodePorts": "node(s) didn't have free ports for the requested pod ports",  # nodeports.go ErrReason
     "PTS": "node(s) didn't match pod topology spread constraints",
     "PTS_LABEL": "node(s) didn't match pod topology spread constraints (missing required label)",
     "IPA_AFF": "node(s) didn't match pod affinity rules",
@@ -501,6 +526,20 @@ class Oracle:
                  ba_resources=("cpu", "memory")):
         self.nodes = node_tree_list(list(nodes))
         self.infos = [NodeInfo(n) for n in self.nodes]
+        # NodeInfo.ImageStates as the v1.26 cache builds them while nodes are added (input
+        # order): size of the first node listing the name, NumNodes counted at that node's add
+        states, size, holders = {}, {}, {}
+        for n in nodes:
+            summ = {}
+            for im in ((n.get("status") or {}).get("images") or []):
+                for nm in im.get("names") or []:
+                    if nm not in size:
+                        size[nm], holders[nm] = int(im.get("sizeBytes") or 0), set()
+                    holders[nm].add(_name(n))
+                    summ.setdefault(nm, (size[nm], len(holders[nm])))
+            states[_name(n)] = summ
+        for ni in self.infos:
+            ni.image_states = states[_name(ni.node)]
         self.by_name = {_name(n): i for i, n in enumerate(self.nodes)}
         self.namespaces = dict(namespaces or {})
         for p in bound_pods:
@@ -513,6 +552,24 @@ class Oracle:
         self.fit_strategy = fit_strategy
         self.fit_resources = list(fit_resources)
         self.ba_resources = list(ba_resources)
+
+    # ----------------------------------------------------------- ImageLocality
+    def image_locality_score(self, pod, ni) -> int:
+        """image_locality.go Score: calculatePriority(sumImageScores(...), len(Containers))."""
+        total = len(self.infos)
+        conts = _spec(pod).get("containers") or []
+        s = 0
+        for c in conts:
+            nm = c.get("image") or ""
+            if nm.rfind(":") <= nm.rfind("/"):  # normalizedImageName
+                nm += ":latest"
+            st = ni.image_states.get(nm)
+            if st is not None:
+                s += int(float(st[0]) * (float(st[1]) / float(total)))  # scaledImageScore
+        mb = 1024 * 1024
+        lo, hi = 23 * mb, 1000 * mb * len(conts)
+        s = lo if s < lo else (hi if s > hi else s)
+        return 100 * (s - lo) // (hi - lo) if hi != lo else 0
 
     # ----------------------------------------------------------- NodeResourcesFit
     def fit_filter(self, pod, ni: NodeInfo) -> Optional[str]:
@@ -857,6 +914,9 @@ class Oracle:
             elif pl == "NodeAffinity":
                 if not required_node_affinity_match(pod, node):
                     msg = MSG["NodeAffinity"]
+            elif pl == "NodePorts":
+                if any(check_conflict(ni.used_ports, *w) for w in _container_host_ports(pod)):
+                    msg = MSG["NodePorts"]
             elif pl == "NodeResourcesFit":
                 msg = self.fit_filter(pod, ni)
             elif pl == "PodTopologySpread":
@@ -956,7 +1016,7 @@ class Oracle:
             lb = _labels(node)
             raw["InterPodAffinity"][i] = sum(vals.get(lb[k], 0) for k, vals in topo.items() if k in lb)
             raw["NodeResourcesBalancedAllocation"][i] = self.ba_score(pod, ni)
-            raw["ImageLocality"][i] = 0
+            raw["ImageLocality"][i] = self.image_locality_score(pod, ni)
         norm = {pl: dict(v) for pl, v in raw.items()}
 
         def default_normalize(d, reverse):

@@ -78,6 +78,7 @@ typedef struct {
   int32_t* pod_count;
   int32_t* class_count;
   int32_t* term_count;
+  uint64_t* port_used;
 } ostate;
 
 static int ostate_init(ostate* s, const kss_cluster* cl) {
@@ -88,7 +89,9 @@ static int ostate_init(ostate* s, const kss_cluster* cl) {
   s->pod_count = (int32_t*)malloc(sizeof(int32_t) * (N ? N : 1));
   s->class_count = (int32_t*)malloc(sizeof(int32_t) * ((size_t)cl->n_classes * N + 1));
   s->term_count = (int32_t*)malloc(sizeof(int32_t) * ((size_t)cl->n_terms * N + 1));
-  if (!s->requested || !s->nonzero || !s->pod_count || !s->class_count || !s->term_count) return -1;
+  s->port_used = (uint64_t*)calloc(N ? N : 1, sizeof(uint64_t));
+  if (!s->requested || !s->nonzero || !s->pod_count || !s->class_count || !s->term_count || !s->port_used) return -1;
+  if (cl->port_used) memcpy(s->port_used, cl->port_used, sizeof(uint64_t) * N);
   memcpy(s->requested, cl->requested, sizeof(int64_t) * KSS_NRES * N);
   memcpy(s->nonzero, cl->nonzero, sizeof(int64_t) * 2 * N);
   memcpy(s->pod_count, cl->pod_count, sizeof(int32_t) * N);
@@ -99,6 +102,7 @@ static int ostate_init(ostate* s, const kss_cluster* cl) {
   s->c.pod_count = s->pod_count;
   s->c.class_count = s->class_count;
   s->c.term_count = s->term_count;
+  s->c.port_used = s->port_used;
   return 0;
 }
 
@@ -108,6 +112,7 @@ static void ostate_free(ostate* s) {
   free(s->pod_count);
   free(s->class_count);
   free(s->term_count);
+  free(s->port_used);
 }
 
 #define LV(cl, key, n) ((cl)->label_value[(size_t)(key) * (size_t)(cl)->n_nodes + (size_t)(n)])
@@ -386,7 +391,11 @@ static int filter_node(const kss_profile* prof, const kss_cluster* cl, const kss
   if ((en >> KSS_F_NODE_AFFINITY) & 1u) {
     if (!required_node_affinity(cl, ps, p, n)) return KSS_F_NODE_AFFINITY;
   }
-  /* NodePorts: pods carry no host ports (host compile rejects them) -> pass */
+  /* NodePorts.Filter -> fitsPorts: any wanted (ip, protocol, port) in conflict with
+   * NodeInfo.UsedPorts (HostPortInfo.CheckConflict; the host resolves the conflict set) */
+  if ((en >> KSS_F_NODE_PORTS) & 1u) {
+    if (p->port_conflict & cl->port_used[n]) return KSS_F_NODE_PORTS;
+  }
   /* NodeResourcesFit.Filter -> fitsRequest */
   if ((en >> KSS_F_NODE_RESOURCES_FIT) & 1u) {
     size_t N = (size_t)cl->n_nodes;
@@ -569,6 +578,19 @@ static int64_t na_score(const kss_cluster* cl, const kss_podset* ps, const kss_p
 }
 
 /* helper.DefaultNormalizeScore */
+/* ImageLocality.Score (image_locality.go): calculatePriority(sumImageScores(nodeInfo,
+ * pod.Spec.Containers, totalNumNodes), len(pod.Spec.Containers)); scaledImageScore per (image,
+ * node) is resolved on the host (the v1.26 cache's ImageStateSummary). */
+static int64_t il_score(const kss_cluster* cl, const kss_podset* ps, const kss_pod* p, int n) {
+  if (p->img_len <= 0) return 0;
+  int64_t sum = 0;
+  for (int i = 0; i < p->img_len; i++) sum += cl->image_score[(size_t)ps->ints[p->img_off + i] * (size_t)cl->n_nodes + n];
+  const int64_t max_t = KSS_IMAGE_MAX_CONTAINER_THRESHOLD * (int64_t)p->n_containers;
+  if (sum < KSS_IMAGE_MIN_THRESHOLD) sum = KSS_IMAGE_MIN_THRESHOLD;
+  else if (sum > max_t) sum = max_t;
+  return (int64_t)100 * (sum - KSS_IMAGE_MIN_THRESHOLD) / (max_t - KSS_IMAGE_MIN_THRESHOLD);
+}
+
 static void default_normalize(int64_t* scores, const int32_t* idx, int nf, int reverse) {
   int64_t mx = 0;
   for (int i = 0; i < nf; i++)
@@ -726,7 +748,7 @@ static int schedule_one(const kss_profile* prof, ostate* s, const kss_podset* ps
     raw[KSS_S_NODE_RESOURCES_FIT * NN + n] = fit_score(prof, cl, p, n);
     raw[KSS_S_VOLUME_BINDING * NN + n] = 0;
     raw[KSS_S_BALANCED_ALLOCATION * NN + n] = ba_score(prof, cl, p, n);
-    raw[KSS_S_IMAGE_LOCALITY * NN + n] = 0; /* nodes carry no Status.Images: calculatePriority(minThreshold) = 0 */
+    raw[KSS_S_IMAGE_LOCALITY * NN + n] = il_score(cl, ps, p, n);
     /* PodTopologySpread.Score */
     int64_t pts = 0;
     if (!ignored[n]) {
@@ -856,6 +878,7 @@ static void commit(ostate* s, const kss_podset* ps, int pi, int node_local) {
   s->pod_count[node_local] += 1;
   if (p->cls >= 0) s->class_count[(size_t)p->cls * N + node_local] += 1;
   for (int i = 0; i < p->own_terms_len; i++) s->term_count[(size_t)ps->ints[p->own_terms_off + i] * N + node_local] += 1;
+  s->port_used[node_local] |= p->port_add; /* NodeInfo.AddPod updateUsedPorts */
 }
 
 /* ---------------------------------------------------------------------------
@@ -879,7 +902,7 @@ int kss_oracle_eval_pod(const kss_profile* prof, const kss_cluster* cl, const ks
 int kss_oracle_schedule(const kss_profile* prof, const kss_cluster* cl, const kss_podset* ps, int n,
                         int32_t* chosen, kss_pod_result* results, int threads, int64_t* out_requested,
                         int64_t* out_nonzero, int32_t* out_pod_count, int32_t* out_class_count,
-                        int32_t* out_term_count) {
+                        int32_t* out_term_count, uint64_t* out_port_used) {
   ostate s;
   if (ostate_init(&s, cl)) return KSS_E_NOMEM;
   int th = threads > 0 ? threads : 1;
@@ -900,6 +923,7 @@ int kss_oracle_schedule(const kss_profile* prof, const kss_cluster* cl, const ks
   if (out_class_count && cl->n_classes)
     memcpy(out_class_count, s.class_count, sizeof(int32_t) * (size_t)cl->n_classes * N);
   if (out_term_count && cl->n_terms) memcpy(out_term_count, s.term_count, sizeof(int32_t) * (size_t)cl->n_terms * N);
+  if (out_port_used) memcpy(out_port_used, s.port_used, sizeof(uint64_t) * N);
   ostate_free(&s);
   return rc;
 }

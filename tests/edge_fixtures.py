@@ -34,10 +34,11 @@ M_PTS_LABEL = "node(s) didn't match pod topology spread constraints (missing req
 M_IPA_AFF = "node(s) didn't match pod affinity rules"
 M_IPA_ANTI = "node(s) didn't match pod anti-affinity rules"
 M_IPA_EXIST = "node(s) didn't satisfy existing pods anti-affinity rules"
+M_PORTS = "node(s) didn't have free ports for the requested pod ports"
 
 
 def node(name, zone=None, cpu="4", mem="8Gi", pods="110", eph="10Gi", extra=None, labels=None, taints=None,
-         unschedulable=False):
+         unschedulable=False, images=None):
     lb = {HOST: name}
     if zone is not None:
         lb[ZONE] = zone
@@ -49,7 +50,10 @@ def node(name, zone=None, cpu="4", mem="8Gi", pods="110", eph="10Gi", extra=None
         spec["taints"] = taints
     if unschedulable:
         spec["unschedulable"] = True
-    return {"metadata": {"name": name, "labels": lb}, "spec": spec, "status": {"allocatable": alloc}}
+    status = {"allocatable": alloc}
+    if images:
+        status["images"] = images
+    return {"metadata": {"name": name, "labels": lb}, "spec": spec, "status": status}
 
 
 def pod(name, requests=None, labels=None, node_name=None, init=None, annotations=None, **spec):
@@ -373,6 +377,89 @@ def fx_node_tree_order():
     return nodes, [], pods, expect
 
 
+# --------------------------------------------------------------------------------------
+# NodePorts (nodeports/node_ports.go: PreFilter getContainerPorts over spec.containers, Filter
+# fitsPorts -> framework.HostPortInfo.CheckConflict, reason ErrReason; NodeInfo.AddPod adds the
+# pod's container host ports to UsedPorts).  HostPortInfo.sanitize: hostIP "" -> 0.0.0.0,
+# protocol "" -> TCP; a wanted 0.0.0.0 port conflicts with the same protocol/port on any IP, a
+# specific IP only with 0.0.0.0 or the same IP; hostPort 0 (containerPort only) never
+# conflicts; init containers' ports are not collected in v1.26.
+# Zero-request pods on identical 4-CPU / 8Gi nodes: NodeResourcesFit is 97 / 95 / 92 with
+# 0 / 1 / 2 pods on the node (non-zero defaults 100m / 200Mi), every other score is equal.
+def _ports(*pp):
+    return [dict(zip(("hostPort", "protocol", "hostIP", "containerPort"), p)) for p in pp]
+
+
+def _cpod(name, ports, node_name=None, init_ports=None):
+    spec = {"containers": [{"name": "c", "resources": {"requests": {}}, "ports": ports}]}
+    if init_ports:
+        spec["initContainers"] = [{"name": "i", "resources": {"requests": {}}, "ports": init_ports}]
+    return pod(name, node_name=node_name, **spec)
+
+
+def fx_node_ports():
+    nodes = [node("a"), node("b"), node("c"), node("d")]
+    bound = [_cpod("web-a", _ports((8080, "", "", 80)), node_name="a"),
+             _cpod("dns-b", _ports((53, "UDP", "10.0.0.2", 53)), node_name="b"),
+             _cpod("x-c", _ports((9090, "TCP", "10.0.0.3", 9090)), node_name="c")]
+    pods = [_cpod("p-8080", _ports((8080, "TCP", "", 8080), (0, "", "", 9000))),  # 0.0.0.0:8080 vs a
+            _cpod("p-8080-again", _ports((8080, "", "", 8080))),                    # a, and d after p-8080
+            _cpod("p-udp53-any", _ports((53, "UDP", "", 53))),                      # any IP: b's 10.0.0.2
+            _cpod("p-specific", _ports((9090, "TCP", "10.0.0.3", 1), (53, "UDP", "10.0.0.2", 2))),
+            _cpod("p-tcp53", _ports((53, "TCP", "", 53)), init_ports=_ports((8080, "", "", 1)))]
+    P = ("NodePorts", M_PORTS)
+    expect = [
+        {"filter": {"a": P, "b": None, "c": None, "d": None}, "selected": "d"},          # Fit 95 95 97
+        {"filter": {"a": P, "b": None, "c": None, "d": P}, "selected": "b"},             # tie 95: b first
+        {"filter": {"a": None, "b": P, "c": None, "d": None}, "selected": "a"},          # tie 95: a first
+        # 10.0.0.3:9090 vs c (same IP); 10.0.0.2/UDP/53 vs b (same IP) and vs a's 0.0.0.0/UDP/53
+        {"filter": {"a": P, "b": P, "c": P, "d": None}, "selected": "d"},
+        # TCP 53 conflicts with no UDP entry; the init container's 8080 is not collected
+        {"filter": {"a": None, "b": None, "c": None, "d": None}, "selected": "c"},      # Fit 92 92 95 92
+    ]
+    return nodes, bound, pods, expect
+
+
+# --------------------------------------------------------------------------------------
+# ImageLocality (imagelocality/image_locality.go Score): calculatePriority(sumImageScores,
+# len(Containers)) = 100 * (clamp(sum, 23Mi, 1000Mi * #containers) - 23Mi) / (max - 23Mi)
+# (int64), sum over containers of scaledImageScore = int64(float64(size) * NumNodes/N) for
+# the node's ImageStates[normalizedImageName(image)] (":latest" appended when the name has
+# no tag after its last "/").  v1.26 cache (cache.go addNodeImageStates /
+# createImageStateSummary): the size is the first adding node's SizeBytes and NumNodes is
+# copied when the node is added (input order a, b, c, d): a app:v1 (300Mi, 1) base:latest
+# (100Mi, 1); b app:v1 (300Mi -- b's own 999Mi is ignored --, 2); c base:latest (100Mi, 2).
+MI = 1024 * 1024
+
+
+def fx_image_locality():
+    nodes = [node("a", images=[{"names": ["app:v1"], "sizeBytes": 300 * MI},
+                               {"names": ["base:latest"], "sizeBytes": 100 * MI}]),
+             node("b", images=[{"names": ["app:v1"], "sizeBytes": 999 * MI}]),
+             node("c", images=[{"names": ["base:latest"], "sizeBytes": 100 * MI}]),
+             node("d")]
+
+    def ipod(name, *images):
+        return pod(name, containers=[{"name": "c%d" % i, "image": im, "resources": {"requests": {}}}
+                                     for i, im in enumerate(images)])
+    pods = [ipod("p-app", "app:v1"),                         # a 75Mi -> 5, b 150Mi -> 12
+            ipod("p-base", "base"),                          # base:latest: a 25Mi -> 0, c 50Mi -> 2
+            ipod("p-two", "app:v1", "registry:5000/base"),   # 2 containers, max 2000Mi: a 2, b 6
+            ipod("p-app-twice", "app:v1", "app:v1")]         # a 150Mi -> 6, b 300Mi -> 14
+    # Totals differ by NodeResourcesFit + ImageLocality only.  Non-zero defaults apply per
+    # container (100m / 200Mi each), so a two-container pod requests 200m / 400Mi.
+    allpass = {n: None for n in "abcd"}
+    expect = [
+        {"filter": allpass, "selected": "b", "il": {"a": 5, "b": 12, "c": 0, "d": 0}},   # Fit 97 everywhere
+        {"filter": allpass, "selected": "c", "il": {"a": 0, "b": 0, "c": 2, "d": 0}},    # Fit 97 95 97 97
+        # Fit 95 92 92 95 (b, c: 100m + 200m): totals 97 98 92 95
+        {"filter": allpass, "selected": "b", "il": {"a": 2, "b": 6, "c": 0, "d": 0}},
+        # Fit 95 87 92 95 (b: 300m + 200m): totals 101 101 92 95, the tie goes to a
+        {"filter": allpass, "selected": "a", "il": {"a": 6, "b": 14, "c": 0, "d": 0}},
+    ]
+    return nodes, [], pods, expect
+
+
 FIXTURES = {
     "unschedulable_and_nodename": fx_unschedulable_and_nodename,
     "taints": fx_taints,
@@ -382,6 +469,8 @@ FIXTURES = {
     "system_default_spread": fx_system_default_spread,
     "interpod": fx_interpod,
     "node_tree_order": fx_node_tree_order,
+    "node_ports": fx_node_ports,
+    "image_locality": fx_image_locality,
 }
 
 
@@ -393,6 +482,10 @@ def check_expect(ann, exp, pts=None, where=""):
         assert ann["scheduler-simulator/selected-node"] == exp["selected"], where
     for k, v in (exp.get("extra") or {}).items():
         assert json.loads(ann[k]) == v, (where, k)
+    if "il" in exp:
+        sc = json.loads(ann["scheduler-simulator/score-result"])
+        for n, v in exp["il"].items():
+            assert sc[n]["ImageLocality"] == str(v), (where, n, sc[n]["ImageLocality"])
     if "pts" in exp and pts is not None:
         for n, (raw, norm) in exp["pts"].items():
             assert pts[n] == (raw, norm), (where, n, pts[n])

@@ -63,6 +63,6 @@ def test_every_filter_reason_is_covered():
                     seen.add(f[1])
     for msg in (ef.M_UNSCHED, ef.M_NAME, ef.M_AFF, ef.M_PTS, ef.M_PTS_LABEL, ef.M_IPA_AFF, ef.M_IPA_ANTI,
                 ef.M_IPA_EXIST, "Too many pods", "Insufficient cpu", "Insufficient memory",
-                "Insufficient ephemeral-storage", "Insufficient example.com/gpu"):
+                "Insufficient ephemeral-storage", "Insufficient example.com/gpu", ef.M_PORTS):
         assert msg in seen, msg
     assert any(m.startswith("node(s) had untolerated taint") for m in seen)
