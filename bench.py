@@ -31,7 +31,7 @@ sys.path.insert(0, os.path.join(ROOT, "oracle"))
 
 # Algorithmic bytes per (pod, node) evaluation, SURVEY §8(d) / BASELINE.md §2:
 # default profile reads 92 B of node state and writes 17 B of verdict + raw scores.
-B_EVAL = {1: 109, 2: 109, 3: 129, 4: 109, 5: 109}
+B_EVAL = {1: 109, 2: 109, 3: 129, 4: 129, 5: 109}
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 
 
@@ -342,6 +342,119 @@ def run_node_axis(args):
         dist.destroy_process_group()
 
 
+def run_split(args):
+    """Node axis as a split grid (kss/split.py): ONE k_spread / k_simple grid
+    whose shards are spread over the ranks' GPUs, the per-pod exchanges done by the kernels
+    themselves with xGMI peer stores into every part's inbox (no launch, collective or host
+    round trip per pod).  C4's recipe (config 4: default profile + zone DoNotSchedule spread),
+    the SAME cluster on every rank, `value` = evals of the whole cluster / max-over-ranks time
+    (strong scaling).  world 1 with --split P > 1 runs P parts on the one GPU (an emulation
+    that measures the split exchange's cost, not a speed-up)."""
+    import numpy as np
+    import torch
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    torch.zeros(1, device="cuda")  # torch's HIP runtime before libkss's
+    dist = None
+    if world > 1:
+        import torch.distributed as dist  # control plane only: the IPC handles, barriers, max of timings
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    from kss import abi, native, split
+    from kss.synth import SEED_BASE
+    cfg = args.split_recipe
+    n_nodes = args.nodes or 100000
+    n_pods = args.pods or 20000
+    parts = world if world > 1 else max(1, args.split)
+    # 256 shards in all for k_spread (~391 nodes per shard at 100k nodes); k_simple sweeps at most 128
+    wl = max(1, (256 if cfg == 4 else 128) // parts)
+    s = native.Synth(cfg, SEED_BASE + cfg, n_nodes, n_pods)
+    if world > 1:
+        runner = split.SplitRank(s.cluster, s.pods, wl, device=local)
+        ctxs = [runner.ctx]
+        run = lambda: [runner.run(n_pods)]  # noqa: E731
+    elif parts > 1:
+        runner = split.InProcessSplit(s.cluster, s.pods, parts, wl)
+        ctxs = runner.ctxs
+        run = lambda: runner.run(n_pods)  # noqa: E731
+    else:
+        c = native.Context(abi.default_profile(), device=local)
+        c.load(s.cluster)
+        c.stage(s.pods)
+        ctxs = [c]
+        run = lambda: [c.run_staged(n_pods)]  # noqa: E731
+
+    def step():
+        for c in ctxs:
+            c.reset()
+        return run()
+
+    for _ in range(args.warmup):
+        step()
+    if dist:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        outs = step()
+    elapsed = time.perf_counter() - t0
+    if dist:
+        dist.barrier()
+    chosen = outs[0]
+    scheduled = int((chosen >= 0).sum())
+    if dist:
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    loop_s = ctxs[0].last_loop_ms() / 1e3
+    rows = -(-n_nodes // parts)
+    achieved = B_EVAL[cfg] * n_pods * rows / loop_s / 1e9
+    if rank == 0:
+        cpu = None
+        if not args.no_cpu and world == 1:
+            threads, _ = cpu_threads()
+            cpu = cpu_baseline(cfg, n_nodes, n_pods, args.cpu_seconds, threads, seed=SEED_BASE + cfg)
+        out = {
+            "metric": "pod x node filter+score evals/sec (pods scheduled/sec in extra)",
+            "value": n_pods * n_nodes * args.steps / elapsed,
+            "unit": "evals/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "int64/f64",
+            "data": f"synthetic (SplitMix64 seed 0x5EED000{cfg}, config-{cfg} recipe)",
+            "config": {"workload": f"C4: {n_nodes} nodes x {n_pods} pods, "
+                                   f"{'default profile + zone PTS' if cfg == 4 else 'default profile'}, "
+                                   f"split grid {parts} part(s) x {wl} shards, pct=100",
+                       "nodes": n_nodes, "pods": n_pods, "parallelism": f"node-axis split x{parts}"
+                       + (" (one GPU)" if world == 1 and parts > 1 else "")},
+            "pods_per_s": scheduled * args.steps / elapsed,
+            "us_per_pod": elapsed / args.steps / n_pods * 1e6,
+            "pods_scheduled_per_step": scheduled,
+            "kernel": ctxs[0].last_kernel(),
+            "geometry": ctxs[0].last_geometry(),
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": None, "traffic_detail": "not measured",
+                         "kernel": ctxs[0].last_kernel(), "bytes_per_eval": B_EVAL[cfg],
+                         "algorithmic_bytes_per_launch": B_EVAL[cfg] * n_pods * rows,
+                         "loop_kernel_ms": loop_s * 1e3,
+                         "note": "latency-bound: per pod 3-4 granule exchanges across every part's shards"},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1 or parts > 1:
+        runner.close()
+    else:
+        ctxs[0].close()
+    s.close()
+    if dist:
+        dist.destroy_process_group()
+
+
 def latency_profile(cfg, n_nodes, n_pods, seed, device):
     """roofline.latency: the per-pod chain is latency-bound, so beside the HBM fraction the line
     carries the phase breakdown of one stamped run (KSS_STAMPS_FILE: s_memrealtime per phase,
@@ -530,6 +643,10 @@ def main():
                     help="C5 shape: this many independent what-if clusters per rank in one launch")
     ap.add_argument("--node-axis", action="store_true",
                     help="C4 shape: one cluster sharded along the node axis over the ranks (RCCL per pod)")
+    ap.add_argument("--split", type=int, default=0,
+                    help="C4 node axis as one split grid over the ranks' GPUs (world 1: this many parts on one GPU)")
+    ap.add_argument("--split-recipe", type=int, default=4, choices=(2, 4),
+                    help="--split pod recipe: 4 (C4: zone PTS, k_spread) or 2 (default profile, k_simple)")
     ap.add_argument("--per-pod", action="store_true", help="the drop-in per-pod API: kss_eval_pod + kss_commit")
     ap.add_argument("--no-latency", action="store_true", help="skip the stamped latency-profile run")
     ap.add_argument("--postfilter", action="store_true", help="DefaultPreemption PostFilter dry runs (kss_postfilter_pod)")
@@ -540,6 +657,8 @@ def main():
         return run_per_pod(args)
     if args.postfilter:
         return run_postfilter(args)
+    if args.split:
+        return run_split(args)
     if args.node_axis:
         return run_node_axis(args)
     if args.scenarios:

@@ -459,6 +459,30 @@ int kss_axis_select(kss_ctx* ctx, const int64_t* gathered_dev, int32_t world, in
 int kss_axis_commit(kss_ctx* ctx, int32_t pod_index, const int64_t* key_dev, const int64_t* gathered_dev, int32_t world,
                     int32_t* chosen_dev, void* stream);
 
+/* ---- split grid: the node axis as one persistent grid over several GPUs ----------
+ * Every part (one context per GPU, one process per GPU) loads the WHOLE cluster and stages
+ * the same pods; part p runs shards [p * shards_per_part, (p + 1) * shards_per_part) of the
+ * n_parts * shards_per_part shards of k_simple / k_spread, i.e. owns their node rows.  The
+ * per-pod exchanges (statistics, critical paths, the packed selectHost key) are the
+ * kernels' own granule exchanges: each granule is stored into every part's inbox (xGMI
+ * peer stores) and polled in the local inbox, so a pod costs no launch and no host round
+ * trip on any GPU.  Every part ends with the full chosen / outcome vectors; node state is
+ * current on each part for its own rows.
+ *   kss_split_config  allocates the zeroed inbox (n_parts == 1 clears the split)
+ *   kss_split_inbox   the inbox's device pointer / size / IPC handle (KSS_IPC_HANDLE_BYTES)
+ *   kss_split_peers   every part's inbox as addressable in this process (in-process parts)
+ *   kss_split_open    the same from the parts' IPC handles (one process per GPU)
+ * Then kss_run_staged on every part concurrently (all parts' grids must be resident at
+ * once).  Replaces SURVEY 8(e)'s per-pod RCCL packed-argmax all-reduce of the node axis
+ * (findNodesThatPassFilters / prioritizeNodes / selectHost per rank's rows,
+ * simulator/scheduler/scheduler.go:174-219, 232-267, 323-344). */
+#define KSS_SPLIT_MAX_PARTS 8
+#define KSS_IPC_HANDLE_BYTES 64
+int kss_split_config(kss_ctx* ctx, int32_t n_parts, int32_t part, int32_t shards_per_part);
+int kss_split_inbox(kss_ctx* ctx, void** dev_ptr, size_t* bytes, void* ipc_handle /* KSS_IPC_HANDLE_BYTES or NULL */);
+int kss_split_peers(kss_ctx* ctx, void* const* inboxes /* [n_parts] */);
+int kss_split_open(kss_ctx* ctx, const void* handles /* [n_parts][KSS_IPC_HANDLE_BYTES] */);
+
 /* timing of the last kss_schedule_batch / kss_eval_pod device work (HIP events on the work stream) */
 int kss_last_timing(kss_ctx* ctx, double* device_ms, int32_t* launches);
 /* device time of the sequential-loop kernel alone in the last batch: the k_simple /

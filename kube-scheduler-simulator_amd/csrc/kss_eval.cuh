@@ -128,6 +128,20 @@ __device__ __forceinline__ uint32_t node_flags_of(const DevCluster& c, int n) {
   return c.nc32 ? (uint32_t)c.nc32[2 * c.nc_cap + (n - c.nc_lo)] : c.node_flags[n];
 }
 
+// Split grid (node axis over several GPUs, kss_split_*): a launch runs shards
+// [w_off, w_off + wl) of the W shards of the cluster; every exchange granule is published to
+// each part's inbox (device pointers valid in this process: IPC-mapped for other GPUs) with
+// system-scope stores, and polled in the local inbox only.  n <= 1: one launch owns the grid.
+constexpr int KSS_MAX_PARTS = 8;
+struct XPeers {
+  int32_t n;
+  int32_t w_off;
+  int32_t wl;
+  int32_t pad;
+  unsigned long long* inbox[KSS_MAX_PARTS];
+};
+
+
 struct DevPods {
   const kss_pod* pods;
   const kss_req* reqs;

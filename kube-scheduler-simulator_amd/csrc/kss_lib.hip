@@ -170,9 +170,10 @@ __global__ __launch_bounds__(KSS_MAX_THREADS) void k_schedule(const DevJob* __re
 template <bool DEF>
 __global__ __launch_bounds__(KSS_MAX_THREADS) void k_simple(const DevJob* __restrict__ jobs, kss_profile prof, int W,
                                                             int cap, int k0, int k1, unsigned long long* gran, int* err,
-                                                            unsigned long long* stamps) {
+                                                            unsigned long long* stamps, XPeers X, unsigned epoch0) {
   extern __shared__ __attribute__((aligned(16))) long long smem[];
-  const int ji = blockIdx.x / W, w = blockIdx.x % W;
+  const int Wl = X.n > 1 ? X.wl : W;  // shards of this launch (a split grid runs [w_off, w_off + wl))
+  const int ji = blockIdx.x / Wl, w = X.w_off + (int)(blockIdx.x % Wl);
   const DevJob job = jobs[ji];
   constexpr kss_profile def_prof = default_profile_c();
   SimpleHdr& H = *reinterpret_cast<SimpleHdr*>(smem);
@@ -184,7 +185,7 @@ __global__ __launch_bounds__(KSS_MAX_THREADS) void k_simple(const DevJob* __rest
   }
   const kss_profile& P = DEF ? def_prof : H.prof;
   simple_schedule(job.c, job.spods, job.stat, job.P.ints, k0, min(k1, job.n_pods), job.chosen, job.meta, P, W, w, cap,
-                  gran ? gran + (size_t)ji * 2 * W * SX_VALS : nullptr, err, ji == 0 ? stamps : nullptr, smem);
+                  gran ? gran + (size_t)ji * 2 * W * SX_VALS : nullptr, X, epoch0, err, ji == 0 ? stamps : nullptr, smem);
 }
 
 // grid = W (one cluster); each shard's nodes live in LDS (cap slots); bins_cap: histogram +
@@ -192,9 +193,11 @@ __global__ __launch_bounds__(KSS_MAX_THREADS) void k_simple(const DevJob* __rest
 template <bool DEF>
 __global__ __launch_bounds__(KSS_MAX_THREADS) void k_spread(const DevJob* __restrict__ jobs, int W, int cap, int bins_cap,
                                                             int n_res, int gq, int k0, int k1, unsigned long long* gran,
-                                                            int* err, unsigned long long* stamps) {
+                                                            int* err, unsigned long long* stamps, XPeers X,
+                                                            unsigned epoch0) {
   extern __shared__ __attribute__((aligned(16))) long long smem[];
-  const int ji = blockIdx.x / W, w = blockIdx.x % W;
+  const int Wl = X.n > 1 ? X.wl : W;
+  const int ji = blockIdx.x / Wl, w = X.w_off + (int)(blockIdx.x % Wl);
   const DevJob job = jobs[ji];
   constexpr kss_profile def_prof = default_profile_c();
   SpreadHdr& H = *reinterpret_cast<SpreadHdr*>(smem);
@@ -206,7 +209,7 @@ __global__ __launch_bounds__(KSS_MAX_THREADS) void k_spread(const DevJob* __rest
   }
   const kss_profile& P = DEF ? def_prof : H.prof;
   spread_schedule(job.c, job.gpods, job.stat, job.res_rows, n_res, k0, min(k1, job.n_pods), job.chosen, job.meta, P, W, w,
-                  cap, bins_cap, gq, gran ? gran + (size_t)ji * 2 * W * G_XW : nullptr, err, stamps, smem);
+                  cap, bins_cap, gq, gran ? gran + (size_t)ji * 2 * W * G_XW : nullptr, X, epoch0, err, stamps, smem);
 }
 
 // Class / term counts of the chosen nodes of pods [k0, min(k1, n_pods)) of every job
@@ -221,13 +224,14 @@ __global__ __launch_bounds__(256) void k_counts(const DevJob* __restrict__ jobs,
 // Static words of pods [k0, min(k1, n_pods)) x every node of every job.  grid: x = 256-node
 // tiles, y = groups of STATIC_PODS pods, z = job.  One lane per node walks its group.
 template <bool DEF>
-__global__ __launch_bounds__(256) void k_static(const DevJob* __restrict__ jobs, kss_profile prof_arg, int k0, int k1) {
+__global__ __launch_bounds__(256) void k_static(const DevJob* __restrict__ jobs, kss_profile prof_arg, int k0, int k1,
+                                                int n_lo, int n_hi) {
   const DevJob& job = jobs[blockIdx.z];
   const int N = job.c.N;
-  const int n = (int)(blockIdx.x * 256 + threadIdx.x);
+  const int n = n_lo + (int)(blockIdx.x * 256 + threadIdx.x);  // rows [n_lo, min(n_hi, N)): a split grid's own rows
   const int kend = min(k1, job.n_pods);
   const int kb = k0 + (int)blockIdx.y * STATIC_PODS;
-  if (kb >= kend || n >= N) return;
+  if (kb >= kend || n >= N || n >= n_hi) return;
   const DevCluster c = job.c;
   const DevPods P = job.P;
   uint32_t* stat = job.stat;
@@ -459,6 +463,16 @@ struct kss_ctx {
   bool bound_dirty = true;
   DevBuf bound_buf, pre_buf;
   DevBound bound_dev{};
+  // split grid (kss_split_*): this context runs part split_part of split_n, split_wl shards
+  // each; split_inbox is its exchange inbox (uncached device memory, zeroed once), split_peer
+  // every part's inbox as addressable here (IPC-mapped for other processes / GPUs)
+  int split_n = 0, split_part = 0, split_wl = 0;
+  void* split_inbox = nullptr;
+  size_t split_inbox_bytes = 0;
+  unsigned long long* split_peer[KSS_MAX_PARTS] = {};
+  std::vector<void*> split_opened;  // hipIpcOpenMemHandle mappings to close
+  bool split_ready = false;
+  unsigned split_epoch = 0;
 };
 
 namespace {
@@ -1177,6 +1191,8 @@ kss_ctx* kss_create(const kss_config* cfg, const kss_profile* prof) {
   return ctx;
 }
 
+static void split_release(kss_ctx* ctx);
+
 void kss_destroy(kss_ctx* ctx) {
   if (!ctx) return;
   hipSetDevice(ctx->cfg.device);
@@ -1200,6 +1216,7 @@ void kss_destroy(kss_ctx* ctx) {
   ctx->gpod_buf.release();
   ctx->res_buf.release();
   ctx->delta_buf.release();
+  split_release(ctx);
   if (ctx->pinned) hipHostFree(ctx->pinned);
   if (ctx->rb) hipHostFree(ctx->rb);
   if (ctx->up) hipHostFree(ctx->up);
@@ -1523,6 +1540,92 @@ int kss_read_node_state(kss_ctx* ctx, int64_t* requested, int64_t* nonzero, int3
   return 0;
 }
 
+static_assert(sizeof(hipIpcMemHandle_t) == KSS_IPC_HANDLE_BYTES, "IPC handle size");
+static_assert(KSS_MAX_PARTS == KSS_SPLIT_MAX_PARTS, "kss.h split limit");
+
+static void split_release(kss_ctx* ctx) {
+  for (void* p : ctx->split_opened) hipIpcCloseMemHandle(p);
+  ctx->split_opened.clear();
+  if (ctx->split_inbox) hipFree(ctx->split_inbox);
+  ctx->split_inbox = nullptr;
+  ctx->split_inbox_bytes = 0;
+  for (auto& q : ctx->split_peer) q = nullptr;
+  ctx->split_n = ctx->split_part = ctx->split_wl = 0;
+  ctx->split_ready = false;
+  ctx->split_epoch = 0;
+}
+
+int kss_split_config(kss_ctx* ctx, int32_t n_parts, int32_t part, int32_t shards_per_part) {
+  if (!ctx) return fail(KSS_E_INVAL, "null ctx");
+  if (n_parts < 1 || n_parts > KSS_SPLIT_MAX_PARTS || part < 0 || part >= n_parts || shards_per_part < 1)
+    return fail(KSS_E_INVAL, "bad split configuration");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  HIP_TRY(hipSetDevice(ctx->cfg.device));
+  HIP_TRY(hipStreamSynchronize(ctx->stream));
+  split_release(ctx);
+  if (n_parts == 1) return 0;  // one part: the whole grid on this device, no inbox
+  const size_t W = (size_t)n_parts * (size_t)shards_per_part;
+  const size_t bytes = sizeof(unsigned long long) * 2 * W * (size_t)std::max(2 * XW_MAX, G_XW);
+  // uncached: the inbox is polled while other GPUs' stores land in it
+  if (hipExtMallocWithFlags(&ctx->split_inbox, bytes, hipDeviceMallocUncached) != hipSuccess) {
+    ctx->split_inbox = nullptr;
+    if (hipMalloc(&ctx->split_inbox, bytes) != hipSuccess) return fail(KSS_E_NOMEM, "split inbox allocation failed");
+  }
+  HIP_TRY(hipMemset(ctx->split_inbox, 0, bytes));
+  HIP_TRY(hipDeviceSynchronize());
+  ctx->split_inbox_bytes = bytes;
+  ctx->split_n = n_parts;
+  ctx->split_part = part;
+  ctx->split_wl = shards_per_part;
+  return 0;
+}
+
+int kss_split_inbox(kss_ctx* ctx, void** dev_ptr, size_t* bytes, void* ipc_handle) {
+  if (!ctx || ctx->split_n < 2) return fail(KSS_E_INVAL, "no split grid configured");
+  if (dev_ptr) *dev_ptr = ctx->split_inbox;
+  if (bytes) *bytes = ctx->split_inbox_bytes;
+  if (ipc_handle) {
+    HIP_TRY(hipSetDevice(ctx->cfg.device));
+    hipIpcMemHandle_t h;
+    HIP_TRY(hipIpcGetMemHandle(&h, ctx->split_inbox));
+    std::memcpy(ipc_handle, &h, sizeof(h));
+  }
+  return 0;
+}
+
+int kss_split_peers(kss_ctx* ctx, void* const* inboxes) {
+  if (!ctx || ctx->split_n < 2 || !inboxes) return fail(KSS_E_INVAL, "no split grid configured");
+  for (int i = 0; i < ctx->split_n; i++)
+    if (!inboxes[i]) return fail(KSS_E_INVAL, "null peer inbox");
+  if (inboxes[ctx->split_part] != ctx->split_inbox) return fail(KSS_E_INVAL, "this part's entry must be its own inbox");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  for (int i = 0; i < ctx->split_n; i++) ctx->split_peer[i] = (unsigned long long*)inboxes[i];
+  ctx->split_ready = true;
+  return 0;
+}
+
+int kss_split_open(kss_ctx* ctx, const void* handles) {
+  if (!ctx || ctx->split_n < 2 || !handles) return fail(KSS_E_INVAL, "no split grid configured");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  HIP_TRY(hipSetDevice(ctx->cfg.device));
+  for (void* p : ctx->split_opened) hipIpcCloseMemHandle(p);
+  ctx->split_opened.clear();
+  for (int i = 0; i < ctx->split_n; i++) {
+    if (i == ctx->split_part) {
+      ctx->split_peer[i] = (unsigned long long*)ctx->split_inbox;
+      continue;
+    }
+    hipIpcMemHandle_t h;
+    std::memcpy(&h, (const char*)handles + (size_t)i * KSS_IPC_HANDLE_BYTES, sizeof(h));
+    void* p = nullptr;
+    HIP_TRY(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess));
+    ctx->split_opened.push_back(p);
+    ctx->split_peer[i] = (unsigned long long*)p;
+  }
+  ctx->split_ready = true;
+  return 0;
+}
+
 int kss_read_port_state(kss_ctx* ctx, uint64_t* port_used) {
   if (!ctx || !ctx->loaded || !port_used) return fail(KSS_E_INVAL, "bad arguments");
   std::lock_guard<std::mutex> lk(ctx->mu);
@@ -1714,30 +1817,54 @@ static int static_chunk(size_t sum_nodes, int n_pods) {
 // The jobs' stat pointers must hold chunk x N words each.  Every polled granule is zeroed
 // before each k_simple launch (epochs restart at 1).
 // ev (optional): 2 events per chunk recorded around each k_simple launch.
+// Split grids (X->n > 1): this launch runs shards [w_off, w_off + wl) of g.W and k_static
+// only their rows; granules are never cleared (a peer may already publish into the inbox):
+// chunk c starts its epochs at epoch0 + c * span, above every tag an earlier chunk left.
+struct SplitRun {
+  XPeers X{};
+  unsigned epoch0 = 0;
+};
+
+static unsigned chunk_span(int pods) { return 8u * (unsigned)std::max(pods, 1) + 16u; }
+
+static void static_rows(const Geometry& g, const XPeers& X, int max_nodes, int& n_lo, int& n_hi) {
+  n_lo = 0;
+  n_hi = max_nodes;
+  if (X.n <= 1) return;
+  const int per = (max_nodes + g.W - 1) / g.W;
+  n_lo = std::min(max_nodes, X.w_off * per);
+  n_hi = std::min(max_nodes, (X.w_off + X.wl) * per);
+}
+
 static int launch_simple(hipStream_t st, const Geometry& g, int n_jobs, const DevJob* jobs, const kss_profile& prof,
                          int n_pods_max, int max_nodes, int chunk, unsigned long long* gran, size_t gran_bytes, int* err,
-                         unsigned long long* stamps = nullptr, hipEvent_t* ev = nullptr) {
+                         unsigned long long* stamps = nullptr, hipEvent_t* ev = nullptr, const SplitRun* split = nullptr) {
   int cap = simple_cap(g);
   const size_t shmem = simple_lds_bytes(cap);
   const bool def = same_profile(prof, default_profile_c());
   const void* fn = def ? (const void*)k_simple<true> : (const void*)k_simple<false>;
   HIP_TRY(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shmem));
-  const dim3 grid((unsigned)(n_jobs * g.W)), block((unsigned)g.threads);
+  XPeers X = split ? split->X : XPeers{};
+  const bool sp_grid = X.n > 1;
+  const dim3 grid((unsigned)(n_jobs * (sp_grid ? X.wl : g.W))), block((unsigned)g.threads);
   kss_profile pr = prof;
-  int W = g.W;
+  int W = g.W, n_lo = 0, n_hi = 0;
+  static_rows(g, X, max_nodes, n_lo, n_hi);
   for (int k0 = 0; k0 < n_pods_max; k0 += chunk) {
     int k1 = std::min(n_pods_max, k0 + chunk);
-    const dim3 sgrid((unsigned)((max_nodes + 255) / 256), (unsigned)((k1 - k0 + STATIC_PODS - 1) / STATIC_PODS),
+    const dim3 sgrid((unsigned)(std::max(n_hi - n_lo, 1) + 255) / 256, (unsigned)((k1 - k0 + STATIC_PODS - 1) / STATIC_PODS),
                      (unsigned)n_jobs);
     if (def)
-      hipLaunchKernelGGL(k_static<true>, sgrid, dim3(256), 0, st, jobs, pr, k0, k1);
+      hipLaunchKernelGGL(k_static<true>, sgrid, dim3(256), 0, st, jobs, pr, k0, k1, n_lo, n_hi);
     else
-      hipLaunchKernelGGL(k_static<false>, sgrid, dim3(256), 0, st, jobs, pr, k0, k1);
+      hipLaunchKernelGGL(k_static<false>, sgrid, dim3(256), 0, st, jobs, pr, k0, k1, n_lo, n_hi);
     HIP_TRY(hipGetLastError());
-    if (gran && k0 > 0) HIP_TRY(hipMemsetAsync(gran, 0, gran_bytes, st));
+    unsigned epoch0 = 0;
+    if (sp_grid) epoch0 = split->epoch0 + (unsigned)(k0 / std::max(chunk, 1)) * chunk_span(chunk);
+    else if (gran && k0 > 0) HIP_TRY(hipMemsetAsync(gran, 0, gran_bytes, st));
     unsigned long long* sp = k0 == 0 ? stamps : nullptr;
-    void* args[] = {(void*)&jobs, (void*)&pr, (void*)&W, (void*)&cap, (void*)&k0, (void*)&k1,
-                    (void*)&gran, (void*)&err, (void*)&sp};
+    void* args[] = {(void*)&jobs, (void*)&pr, (void*)&W,  (void*)&cap, (void*)&k0, (void*)&k1,
+                    (void*)&gran, (void*)&err, (void*)&sp, (void*)&X,   (void*)&epoch0};
     const int ci = k0 / chunk;
     if (ev) HIP_TRY(hipEventRecord(ev[2 * ci], st));
     if (g.W > 1) {
@@ -1777,7 +1904,7 @@ static bool spread_fits(const Geometry& g, const GpodNeeds& q, int n_keys, int n
 static int launch_spread(hipStream_t st, const Geometry& g, const GpodNeeds& q, int n_keys, int n_res,
                          const DevJob* jobs, const kss_profile& prof, int n_pods, int max_nodes, int chunk,
                          unsigned long long* gran, size_t gran_bytes, int* err, unsigned long long* stamps = nullptr,
-                         hipEvent_t* ev = nullptr) {
+                         hipEvent_t* ev = nullptr, const SplitRun* split = nullptr) {
   int cap = spread_cap(g, (size_t)max_nodes), bins_cap = q.bins_cap, nr = n_res, gq = q.gq;
   size_t shmem = spread_lds(g, q, n_keys, n_res, (size_t)max_nodes);
   if (stamps && shmem + G_STAMP_LDS > KSS_LDS_BUDGET) stamps = nullptr;  // diagnostics only where they fit
@@ -1785,21 +1912,27 @@ static int launch_spread(hipStream_t st, const Geometry& g, const GpodNeeds& q, 
   const bool def = same_profile(prof, default_profile_c());
   const void* fn = def ? (const void*)k_spread<true> : (const void*)k_spread<false>;
   HIP_TRY(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shmem));
-  const dim3 grid((unsigned)g.W), block((unsigned)g.threads);
+  XPeers X = split ? split->X : XPeers{};
+  const bool sp_grid = X.n > 1;
+  const dim3 grid((unsigned)(sp_grid ? X.wl : g.W)), block((unsigned)g.threads);
   kss_profile pr = prof;
-  int W = g.W;
+  int W = g.W, n_lo = 0, n_hi = 0;
+  static_rows(g, X, max_nodes, n_lo, n_hi);
   for (int k0 = 0; k0 < n_pods; k0 += chunk) {
     int k1 = std::min(n_pods, k0 + chunk);
-    const dim3 sgrid((unsigned)((max_nodes + 255) / 256), (unsigned)((k1 - k0 + STATIC_PODS - 1) / STATIC_PODS), 1u);
+    const dim3 sgrid((unsigned)(std::max(n_hi - n_lo, 1) + 255) / 256, (unsigned)((k1 - k0 + STATIC_PODS - 1) / STATIC_PODS), 1u);
     if (def)
-      hipLaunchKernelGGL(k_static<true>, sgrid, dim3(256), 0, st, jobs, pr, k0, k1);
+      hipLaunchKernelGGL(k_static<true>, sgrid, dim3(256), 0, st, jobs, pr, k0, k1, n_lo, n_hi);
     else
-      hipLaunchKernelGGL(k_static<false>, sgrid, dim3(256), 0, st, jobs, pr, k0, k1);
+      hipLaunchKernelGGL(k_static<false>, sgrid, dim3(256), 0, st, jobs, pr, k0, k1, n_lo, n_hi);
     HIP_TRY(hipGetLastError());
-    if (gran && k0 > 0) HIP_TRY(hipMemsetAsync(gran, 0, gran_bytes, st));
+    unsigned epoch0 = 0;
+    if (sp_grid) epoch0 = split->epoch0 + (unsigned)(k0 / std::max(chunk, 1)) * chunk_span(chunk);
+    else if (gran && k0 > 0) HIP_TRY(hipMemsetAsync(gran, 0, gran_bytes, st));
     unsigned long long* sp = k0 == 0 ? stamps : nullptr;
-    void* args[] = {(void*)&jobs, (void*)&W,  (void*)&cap, (void*)&bins_cap, (void*)&nr, (void*)&gq,
-                    (void*)&k0,   (void*)&k1, (void*)&gran, (void*)&err,     (void*)&sp};
+    void* args[] = {(void*)&jobs, (void*)&W,  (void*)&cap,  (void*)&bins_cap, (void*)&nr, (void*)&gq,
+                    (void*)&k0,   (void*)&k1, (void*)&gran, (void*)&err,      (void*)&sp, (void*)&X,
+                    (void*)&epoch0};
     const int ci = k0 / chunk;
     if (ev) HIP_TRY(hipEventRecord(ev[2 * ci], st));
     if (g.W > 1) {
@@ -1845,6 +1978,14 @@ static int run_single(kss_ctx* ctx, const PlanNeeds& need, const DevPods& dp, in
   // shard count: ~nodes_per_shard nodes per workgroup, at most one workgroup per CU
   int W = std::max(1, std::min(ctx->n_cu, (int)((N + ctx->nodes_per_shard - 1) / ctx->nodes_per_shard)));
   if (ctx->force_w > 0) W = std::min(ctx->force_w, ctx->n_cu);
+  // split grid (kss_split_config): the shard count is fixed by the parts, every part the same
+  const bool split = ctx->split_n > 1;
+  if (split) {
+    if (!staged || !commit || record || keep_norm || (flags & (KSS_SCHED_FORCE_SINGLE_WG | KSS_SCHED_FORCE_MULTI_WG)))
+      return fail(KSS_E_UNSUPPORTED, "split grids run staged, unrecorded batches (kss_run_staged)");
+    if (!ctx->split_ready) return fail(KSS_E_INVAL, "split grid: peers not set (kss_split_peers / kss_split_open)");
+    W = ctx->split_n * ctx->split_wl;
+  }
   if (flags & KSS_SCHED_FORCE_SINGLE_WG) W = 1;
   if (flags & KSS_SCHED_FORCE_MULTI_WG) W = std::max(W, std::min(4, ctx->n_cu));
   W = std::max(1, std::min(W, std::max(1, (int)N)));
@@ -1854,7 +1995,7 @@ static int run_single(kss_ctx* ctx, const PlanNeeds& need, const DevPods& dp, in
   const bool simple_ok = staged && ctx->spod_ok && commit && !record && !keep_norm && !need.general &&
                          ctx->dc.n_scalar == 0 && ctx->small_values && f64_exact(ctx->f64_cluster, ctx->f64_pods, n) &&
                          !ctx->no_simple && !(flags & KSS_SCHED_GENERAL_KERNEL);
-  if (simple_ok && ctx->force_w <= 0) W = std::min(W, 64 * SX_CHUNKS);
+  if (simple_ok && ctx->force_w <= 0 && !split) W = std::min(W, 64 * SX_CHUNKS);
   // a batch with programs on k_spread: 32-bit counts and scores (spread_bounds_ok)
   const double count_total = ctx->count_bound + (commit ? (double)n * (1.0 + ctx->staged_max_own) : 0.0);
   const double cell_total = ctx->cell_bound + (commit ? (double)n * ctx->gneed.max_mult : 0.0);
@@ -1871,17 +2012,20 @@ static int run_single(kss_ctx* ctx, const PlanNeeds& need, const DevPods& dp, in
             (int)spread_bounds_ok(ctx->gneed, count_total, cell_total, (int)N), (long long)ctx->gneed.ref_weight,
             count_total, cell_total, ctx->gneed.res_rows.size(), ctx->gneed.bins_cap);
   const int w_min = (int)((N + KSS_MAX_NPT * KSS_MAX_THREADS - 1) / (KSS_MAX_NPT * KSS_MAX_THREADS));
+  if (split && W < w_min) return fail(KSS_E_UNSUPPORTED, "split grid: too few shards for this cluster");
   W = std::max(W, w_min);
   if (W > 1 && need.xw > XW_MAX && !spread_ok) {
     if (w_min > 1) return fail(KSS_E_UNSUPPORTED, "topology histograms too large for a sharded cluster");
     W = 1;  // exchange payload too large for granules: one workgroup
   }
-  if (W > ctx->n_cu) return fail(KSS_E_UNSUPPORTED, "cluster too large for one device");
+  if (!split && W > ctx->n_cu) return fail(KSS_E_UNSUPPORTED, "cluster too large for one device");
+  if (split && ctx->split_wl > ctx->n_cu) return fail(KSS_E_UNSUPPORTED, "split grid: more shards per part than CUs");
   Geometry g;
   if (!pick_geometry((int)N, W, ctx->pref_threads, g)) return fail(KSS_E_UNSUPPORTED, "no geometry for this cluster");
   const bool simple = simple_ok && simple_fits(g);
   const int n_res = (int)ctx->gneed.res_rows.size();
   bool spread = spread_ok && spread_fits(g, ctx->gneed, ctx->dc.n_keys, n_res, N);
+  if (split && simple && g.W > 64 * SX_CHUNKS) return fail(KSS_E_UNSUPPORTED, "split grid: k_simple sweeps at most 128 shards");
   if (spread_ok && !spread && g.threads < KSS_MAX_THREADS) {  // more prefetch lanes per shard
     Geometry g2 = g;
     const int per = (int)((N + g.W - 1) / g.W);
@@ -1894,7 +2038,7 @@ static int run_single(kss_ctx* ctx, const PlanNeeds& need, const DevPods& dp, in
   }
   // more shards when the resident count rows of a shard exceed its LDS (not when the caller
   // fixed the shard count)
-  for (int W2 = g.W * 2; spread_ok && !spread && ctx->force_w <= 0 && !(flags & KSS_SCHED_FORCE_SINGLE_WG) &&
+  for (int W2 = g.W * 2; spread_ok && !spread && ctx->force_w <= 0 && !split && !(flags & KSS_SCHED_FORCE_SINGLE_WG) &&
                          W2 <= ctx->n_cu && W2 <= (int)N;
        W2 *= 2) {
     Geometry g2;
@@ -1908,6 +2052,9 @@ static int run_single(kss_ctx* ctx, const PlanNeeds& need, const DevPods& dp, in
     if (!pick_geometry((int)N, 1, ctx->pref_threads, g)) return fail(KSS_E_UNSUPPORTED, "no geometry for this cluster");
   }
   const bool loop = simple || spread;  // k_static + a persistent loop kernel
+  if (split && !loop)
+    return fail(KSS_E_UNSUPPORTED, spread_ok ? "split grid: a k_spread shard exceeds LDS (more shards per part)"
+                                             : "split grid: the batch needs k_schedule (kss_plan_podset)");
   const int chunk = loop ? static_chunk(N, n) : 0;
   if (loop && (rc = ctx->stat_buf.ensure(sizeof(uint32_t) * (size_t)chunk * std::max<size_t>(N, 1)))) return rc;
   DevJob job{};
@@ -1933,7 +2080,19 @@ static int run_single(kss_ctx* ctx, const PlanNeeds& need, const DevPods& dp, in
   unsigned long long* gran = nullptr;
   const size_t gb = sizeof(unsigned long long) * 2 * (size_t)g.W * std::max(2 * XW_MAX, G_XW);
   unsigned epoch0 = 0;
-  if (g.W > 1) {
+  SplitRun srun;
+  if (split) {  // the local inbox, never cleared: this run's epochs start above every earlier tag
+    if (gb > ctx->split_inbox_bytes) return fail(KSS_E_INVAL, "split grid: inbox smaller than the exchange buffer");
+    gran = (unsigned long long*)ctx->split_inbox;
+    srun.X.n = ctx->split_n;
+    srun.X.w_off = ctx->split_part * ctx->split_wl;
+    srun.X.wl = ctx->split_wl;
+    for (int i = 0; i < ctx->split_n; i++) srun.X.inbox[i] = ctx->split_peer[i];
+    srun.epoch0 = ctx->split_epoch;
+    const unsigned span = (unsigned)((n + chunk - 1) / std::max(chunk, 1) + 1) * chunk_span(chunk) + 16u;
+    if ((uint64_t)ctx->split_epoch + span >= (1ull << 31)) return fail(KSS_E_RANGE, "split grid: granule epochs exhausted");
+    ctx->split_epoch += span;
+  } else if (g.W > 1) {
     const void* before = ctx->gran_buf.p;
     rc = ctx->gran_buf.ensure(gb);
     if (rc) return rc;
@@ -1982,10 +2141,10 @@ static int run_single(kss_ctx* ctx, const PlanNeeds& need, const DevPods& dp, in
   }
   if (simple)
     rc = launch_simple(ctx->stream, g, 1, jd, ctx->prof, n, (int)N, chunk, gran, gb,
-                       errp, stamps, ctx->loop_ev.data());
+                       errp, stamps, ctx->loop_ev.data(), split ? &srun : nullptr);
   else if (spread)
     rc = launch_spread(ctx->stream, g, ctx->gneed, ctx->dc.n_keys, n_res, jd, ctx->prof, n,
-                       (int)N, chunk, gran, gb, errp, stamps, ctx->loop_ev.data());
+                       (int)N, chunk, gran, gb, errp, stamps, ctx->loop_ev.data(), split ? &srun : nullptr);
   else
     rc = launch_schedule(ctx->stream, g, 1, std::max(need.bins_cap, 0), need.general, ctx->dc.n_keys,
                          jd, ctx->prof, gran, errp, stamps, epoch0);

@@ -41,6 +41,16 @@ __device__ __forceinline__ KSS_GLOBAL T* gp(T* p) {
   return (KSS_GLOBAL T*)p;
 }
 
+// Publish one granule at offset `off` of the exchange buffer (the local inbox `gran`);
+// address-space-1 stores (a flat store would also count in lgkmcnt).
+__device__ __forceinline__ void xpub(const XPeers& X, unsigned long long* gran, size_t off, unsigned long long v) {
+  if (X.n <= 1) {
+    __hip_atomic_store(gp(gran) + off, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return;
+  }
+  for (int p = 0; p < X.n; p++) __hip_atomic_store(gp(X.inbox[p]) + off, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 constexpr int SX_VALS = 8;    // granules per shard per exchange: key lo/hi, H0 (nf, tt, na), H1 (nf, tt, na)
 constexpr int SX_CHUNKS = 2;  // shards swept 64 at a time: W <= 128
 constexpr int STATIC_PODS = 8;  // pods per k_static lane
@@ -383,7 +393,8 @@ __device__ __forceinline__ void block_red(SimpleHdr& H, int parity, long long (&
 // shard.  Publishes 8 granules {epoch, 32-bit value}, sweeps all W shards (64 per chunk,
 // every load of a chunk in flight at once), then: winner = max key; the winner's shard
 // (its node index / per) contributes H1, the others H0.  Results -> H.res.
-__device__ __forceinline__ bool simple_exchange(SimpleHdr& H, unsigned long long* gran, int W, int wself, unsigned epoch,
+__device__ __forceinline__ bool simple_exchange(SimpleHdr& H, unsigned long long* gran, const XPeers& X, int W, int wself,
+                                                unsigned epoch,
                                                 int* err, const long long (&v)[7], int per, int node_base) {
   const int lane = threadIdx.x & 63;
   const unsigned long long tag = (unsigned long long)epoch << 32;
@@ -393,8 +404,7 @@ __device__ __forceinline__ bool simple_exchange(SimpleHdr& H, unsigned long long
     x = lane == 1 ? (uint32_t)(key >> 32) : x;
 #pragma unroll
     for (int i = 1; i < 7; i++) x = lane == i + 1 ? (uint32_t)v[i] : x;
-    unsigned long long* mine = gran + ((size_t)(epoch & 1) * W + wself) * SX_VALS;
-    __hip_atomic_store(mine + lane, tag | x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    xpub(X, gran, ((size_t)(epoch & 1) * W + wself) * SX_VALS + lane, tag | x);
   }
   const unsigned long long* base = gran + (size_t)(epoch & 1) * W * SX_VALS;
   uint32_t got[SX_CHUNKS][SX_VALS];
@@ -458,7 +468,8 @@ __device__ __forceinline__ bool simple_exchange(SimpleHdr& H, unsigned long long
 // current pod's shard-best key, and leave {winner key, nf, max TT, max NA} in R[] of
 // every lane.  False if the launch aborted (exchange timeout).
 __device__ __forceinline__ bool simple_sync(SimpleHdr& H, int& parity, long long key, long long (&st)[6], int W, int w,
-                                            unsigned epoch, unsigned long long* gran, int* err, int per, int node_base,
+                                            unsigned epoch, unsigned long long* gran, const XPeers& X, int* err, int per,
+                                            int node_base,
                                             long long (&R)[4], KSS_GLOBAL unsigned long long* sp) {
   {
     uint32_t u[6];
@@ -492,7 +503,7 @@ __device__ __forceinline__ bool simple_sync(SimpleHdr& H, int& parity, long long
   }
   if (threadIdx.x < 64) {
     const long long v[7] = {key, st[0], st[1], st[2], st[3], st[4], st[5]};
-    simple_exchange(H, gran, W, w, epoch, err, v, per, node_base);
+    simple_exchange(H, gran, X, W, w, epoch, err, v, per, node_base);
   }
   lds_barrier();
   if (H.abort) return false;
@@ -614,8 +625,8 @@ __device__ __forceinline__ void simple_pass_a(const kss_profile& prof, const SPo
 __device__ __forceinline__ void simple_schedule(DevCluster c, const SPod* __restrict__ spods,
                                                 const uint32_t* __restrict__ stat, const int32_t* __restrict__ ints,
                                                 int k0, int k1, int32_t* chosen, PodMeta* meta, const kss_profile& prof,
-                                                int W, int w, int cap, unsigned long long* gran, int* err,
-                                                unsigned long long* stamps, long long* smem) {
+                                                int W, int w, int cap, unsigned long long* gran, const XPeers& X,
+                                                unsigned epoch0, int* err, unsigned long long* stamps, long long* smem) {
   const int tid = threadIdx.x, nt = blockDim.x;
   SimpleHdr& H = *reinterpret_cast<SimpleHdr*>(smem);
   const SimpleShard L = shard_view(reinterpret_cast<uint8_t*>(smem) + sizeof(SimpleHdr), cap);
@@ -655,7 +666,7 @@ __device__ __forceinline__ void simple_schedule(DevCluster c, const SPod* __rest
   KSS_GLOBAL unsigned long long* gstamps = gp(stamps);
   long long st[6], R[4] = {0, 0, 0, 0};
   int parity = 0, sub_s = -1;  // slot whose pass-B values are the H1 ones (the previous winner)
-  unsigned epoch = 0;
+  unsigned epoch = epoch0;  // granule tags above every tag an earlier launch left (split grids)
   const int nwave = nt >> 6;
   // prefetch lanes: every wave but wave 0 (readfirstlane: a wave-uniform, scalar branch)
   const bool pf_wave = nwave == 1 || __builtin_amdgcn_readfirstlane(tid >> 6) >= 1;
@@ -721,12 +732,12 @@ __device__ __forceinline__ void simple_schedule(DevCluster c, const SPod* __rest
       for (int i = 0; i < 6; i++) st[i] = 0;
     }
     if (sp && tid == 0) sp[3] = wall_clock64();
-    if (!simple_sync(H, parity, best, st, W, w, ++epoch, gran, err, per, c.node_base, R, sp)) return;
+    if (!simple_sync(H, parity, best, st, W, w, ++epoch, gran, X, err, per, c.node_base, R, sp)) return;
     if (sp && tid == 0) sp[5] = wall_clock64();
     if (k >= k0) {
       const long long K = R[0];
       const int x = K ? (int)(0xFFFFFFFFu - (uint32_t)(unsigned long long)K) - c.node_base : -1;
-      if (w == 0 && tid == 0) {
+      if (w == X.w_off && tid == 0) {  // every part keeps the outcomes
         PodMeta m;
         m.chosen = K ? x + c.node_base : -1;
         m.n_feasible = (int)nf;

@@ -263,7 +263,8 @@ __device__ __forceinline__ void wave_red32(int32_t (&v)[K], const int (&ops)[K])
 // The scalars are combined over the workgroup's waves here (H.red), by the lanes that
 // publish them.  Granules are accessed through address-space-1 pointers: flat accesses would
 // also count in lgkmcnt and make every following LDS wait on the HBM stores.
-__device__ __forceinline__ bool spread_exchange(SpreadHdr& H, int32_t* xs, unsigned long long* gran_, int W, int wself,
+__device__ __forceinline__ bool spread_exchange(SpreadHdr& H, int32_t* xs, unsigned long long* gran_, const XPeers& X,
+                                                int W, int wself,
                                                 unsigned epoch, int* err, int K, unsigned opbits, int sum_lo, int ns,
                                                 int or_lo, int no, unsigned long long* sp) {
   constexpr int XS = 16;  // shards polled per lane at once
@@ -277,7 +278,7 @@ __device__ __forceinline__ bool spread_exchange(SpreadHdr& H, int32_t* xs, unsig
   };
   auto opof = [&](int j) { return j < K ? (int)((opbits >> (2 * j)) & 3u) : (j < K + ns ? OP_SUM : OP_OR); };
   const unsigned long long tag = (unsigned long long)epoch << 32;
-  KSS_GLOBAL unsigned long long* mine = gran + ((size_t)(epoch & 1) * W + wself) * G_XW;
+  const size_t mine = ((size_t)(epoch & 1) * W + wself) * G_XW;
   for (int j = lane; j < M; j += 64) {
     int32_t* sl = slot(j);
     const int op = opof(j);
@@ -286,7 +287,7 @@ __device__ __forceinline__ bool spread_exchange(SpreadHdr& H, int32_t* xs, unsig
       v = H.red[0][j];
       for (int x = 1; x < nw; x++) v = op32_lane(op, v, H.red[x][j]);
     }
-    __hip_atomic_store(mine + j, tag | (uint32_t)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    xpub(X, gran_, mine + j, tag | (uint32_t)v);
     *sl = ident32(op);
   }
   if (sp && lane == 0) sp[2] = wall_clock64();
@@ -371,7 +372,7 @@ __device__ __forceinline__ void hard_minima(const GPod& q, int32_t* xs) {
 // False on abort.
 template <int K>
 __device__ __forceinline__ bool spread_reduce(SpreadHdr& H, int32_t* xs, int W, int w, unsigned& epoch,
-                                              unsigned long long* gran, int* err, int32_t (&v)[K],
+                                              unsigned long long* gran, const XPeers& X, int* err, int32_t (&v)[K],
                                               const int (&ops)[K], int sum_lo = 0, int ns = 0, int or_lo = 0,
                                               int no = 0, bool local = false, unsigned long long* sp = nullptr,
                                               const GPod* minima_q = nullptr) {
@@ -407,7 +408,7 @@ __device__ __forceinline__ bool spread_reduce(SpreadHdr& H, int32_t* xs, int W, 
     for (int k = 0; k < K; k++) opbits |= (unsigned)ops[k] << (2 * k);
     ++epoch;
     if (sp && threadIdx.x == 0) sp[1] = wall_clock64();
-    if (wave == 0 && spread_exchange(H, xs, gran, W, w, epoch, err, K, opbits, sum_lo, ns, or_lo, no, sp) &&
+    if (wave == 0 && spread_exchange(H, xs, gran, X, W, w, epoch, err, K, opbits, sum_lo, ns, or_lo, no, sp) &&
         minima_q)
       hard_minima(*minima_q, xs);
     if (sp && threadIdx.x == 0) sp[4] = wall_clock64();
@@ -422,6 +423,7 @@ __device__ __forceinline__ bool spread_reduce(SpreadHdr& H, int32_t* xs, int W, 
 
 // Cluster MAX of the packed selectHost key (two granules: lo, hi).
 __device__ __forceinline__ bool spread_argmax(SpreadHdr& H, int W, int w, unsigned& epoch, unsigned long long* gran,
+                                              const XPeers& X,
                                               int* err, int parity, long long& key) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
   const long long r = wave_red<OP_MAX>(key);
@@ -436,10 +438,9 @@ __device__ __forceinline__ bool spread_argmax(SpreadHdr& H, int W, int w, unsign
   ++epoch;
   if (wave == 0) {
     const unsigned long long tag = (unsigned long long)epoch << 32;
-    KSS_GLOBAL unsigned long long* mine = gp(gran) + ((size_t)(epoch & 1) * W + w) * G_XW;
     if (lane < 2)
-      __hip_atomic_store(mine + lane, tag | (lane ? (uint32_t)((unsigned long long)best >> 32) : (uint32_t)best),
-                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      xpub(X, gran, ((size_t)(epoch & 1) * W + w) * G_XW + lane,
+           tag | (lane ? (uint32_t)((unsigned long long)best >> 32) : (uint32_t)best));
     KSS_GLOBAL const unsigned long long* base = gp(gran) + (size_t)(epoch & 1) * W * G_XW;
     long long m = 0;
     for (int c0 = 0; c0 < W; c0 += 64) {
@@ -631,7 +632,8 @@ __device__ __forceinline__ void spread_schedule(DevCluster c, const GPod* __rest
                                                 const uint32_t* __restrict__ stat, const int32_t* __restrict__ res_rows,
                                                 int n_res, int k0, int k1, int32_t* chosen, PodMeta* meta,
                                                 const kss_profile& prof, int W, int w, int cap, int bins_cap, int gq,
-                                                unsigned long long* gran, int* err, unsigned long long* stamps,
+                                                unsigned long long* gran, const XPeers& X, unsigned epoch0, int* err,
+                                                unsigned long long* stamps,
                                                 long long* smem) {
   const int tid = threadIdx.x, nt = blockDim.x;
   SpreadHdr& H = *reinterpret_cast<SpreadHdr*>(smem);
@@ -697,7 +699,7 @@ __device__ __forceinline__ void spread_schedule(DevCluster c, const GPod* __rest
   uint32_t pfw[G_PF];
 #pragma unroll
   for (int j = 0; j < G_PF; j++) pfw[j] = 0;
-  unsigned epoch = 0;
+  unsigned epoch = epoch0;  // granule tags above every tag an earlier launch left (split grids)
   int kparity = 0;
   for (int k = k0; k < k1; k++) {
 #define GSTAMP(i)                                                                      \
@@ -748,7 +750,7 @@ __device__ __forceinline__ void spread_schedule(DevCluster c, const GPod* __rest
       v[MAXH] = flags;
       // histogram SUM over every bin, hard-pair presence OR (soft presence, still zero, is
       // filled by the filter pass), then the critical-path minima
-      if (!spread_reduce(H, L.xs, W, w, epoch, gran, err, v, op, 0, q.total_bins, q.total_bins, q.hard_pbins, false,
+      if (!spread_reduce(H, L.xs, W, w, epoch, gran, X, err, v, op, 0, q.total_bins, q.total_bins, q.hard_pbins, false,
                          nullptr, &q))
         return;
 #pragma unroll
@@ -844,7 +846,7 @@ __device__ __forceinline__ void spread_schedule(DevCluster c, const GPod* __rest
                        sdirect[2], sdirect[3], cmin, cmax};
       const int op[13] = {OP_SUM, OP_SUM, OP_MAX, OP_MAX, OP_MIN, OP_MAX, OP_OR, OP_SUM, OP_SUM, OP_SUM, OP_SUM,
                           OP_MIN, OP_MAX};
-      if (!spread_reduce(H, L.xs, W, w, epoch, gran, err, v, op, 0, 0, q.total_bins + q.hard_pbins,
+      if (!spread_reduce(H, L.xs, W, w, epoch, gran, X, err, v, op, 0, 0, q.total_bins + q.hard_pbins,
                          q.total_pbins - q.hard_pbins, false,
                          stl && k - k0 < G_NSTAMP ? stl + (k - k0) * 16 + 10 : nullptr))
         return;
@@ -880,7 +882,7 @@ __device__ __forceinline__ void spread_schedule(DevCluster c, const GPod* __rest
           for (int b = tid; b < sp.nb; b += nt) sz[i] += bins[q.total_bins + sp.poff + b] ? 1 : 0;
         }
         const int ops4[MAXS] = {OP_SUM, OP_SUM, OP_SUM, OP_SUM};
-        spread_reduce(H, L.xs, W, w, epoch, gran, err, sz, ops4, 0, 0, 0, 0, /*local=*/true);
+        spread_reduce(H, L.xs, W, w, epoch, gran, X, err, sz, ops4, 0, 0, 0, 0, /*local=*/true);
         for (int i = 0; i < q.n_soft; i++) {
           const GSpread& sp = soft[i];
           long long size;  // topoSize: a group's domains count for its leader only
@@ -936,7 +938,7 @@ __device__ __forceinline__ void spread_schedule(DevCluster c, const GPod* __rest
           // 32-bit extrema: raw scores are host-bounded (spread_bounds_ok)
           int32_t v2[2] = {(int32_t)min(pmin, (long long)INT32_MAX), (int32_t)pmax};
           const int op2[2] = {OP_MIN, OP_MAX};
-          if (!spread_reduce(H, L.xs, W, w, epoch, gran, err, v2, op2)) return;
+          if (!spread_reduce(H, L.xs, W, w, epoch, gran, X, err, v2, op2)) return;
           pts_min = v2[0] == INT32_MAX ? INT64_MAX : v2[0];
           pts_max = v2[1];
           GSTAMP(6);
@@ -990,7 +992,7 @@ __device__ __forceinline__ void spread_schedule(DevCluster c, const GPod* __rest
         best = key > best ? key : best;
       }
       GSTAMP(7);
-      if (!spread_argmax(H, W, w, epoch, gran, err, kparity, best)) return;
+      if (!spread_argmax(H, W, w, epoch, gran, X, err, kparity, best)) return;
       GSTAMP(8);
       kparity ^= 1;
       const unsigned long long ub = (unsigned long long)best;
@@ -1002,7 +1004,7 @@ __device__ __forceinline__ void spread_schedule(DevCluster c, const GPod* __rest
     const int x = m.chosen >= 0 ? m.chosen - c.node_base : -1;
     const bool won = x >= lo && x < hi;
     if (tid == out_tid) {  // HBM stores off wave 0 (its vmcnt stays free for the exchanges)
-      if (w == 0) {
+      if (w == X.w_off) {  // every part keeps the outcomes
         if (chosen) gchosen[k] = m.chosen;
         if (meta) {
           gmeta[k].chosen = m.chosen;

@@ -17,6 +17,8 @@ KSS_MAX_TAINTS = 64
 KSS_TAINT_ORDER = 8
 KSS_MAX_BINS = 1024
 KSS_MAX_PORTS = 64
+KSS_SPLIT_MAX_PARTS = 8
+KSS_IPC_HANDLE_BYTES = 64
 KSS_IMAGE_MIN_THRESHOLD = 23 * 1024 * 1024
 KSS_IMAGE_MAX_CONTAINER_THRESHOLD = 1000 * 1024 * 1024
 

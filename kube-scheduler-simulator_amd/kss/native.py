@@ -81,6 +81,10 @@ SIGNATURES = [
                                 C.c_void_p, C.c_void_p]),
     ("kss_axis_select", C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p]),
     ("kss_axis_commit", C.c_int, [C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p]),
+    ("kss_split_config", C.c_int, [C.c_void_p, C.c_int32, C.c_int32, C.c_int32]),
+    ("kss_split_inbox", C.c_int, [C.c_void_p, P(C.c_void_p), P(C.c_size_t), C.c_void_p]),
+    ("kss_split_peers", C.c_int, [C.c_void_p, P(C.c_void_p)]),
+    ("kss_split_open", C.c_int, [C.c_void_p, C.c_void_p]),
     ("kss_synth_make", C.c_int, [C.c_int32, C.c_uint64, C.c_int32, C.c_int32, P(abi.Synth)]),
     ("kss_synth_free", None, [P(abi.Synth)]),
 ]
@@ -252,6 +256,25 @@ class Context:
 
     def axis_commit(self, i: int, key_ptr: int, gathered_ptr: int, world: int, chosen_ptr: int, stream: int):
         check(lib().kss_axis_commit(self.h, i, key_ptr, gathered_ptr, world, chosen_ptr, stream))
+
+    # split grid (kss.h kss_split_*): this context runs one part of a grid spread over GPUs
+    def split_config(self, n_parts: int, part: int, shards_per_part: int):
+        check(lib().kss_split_config(self.h, n_parts, part, shards_per_part))
+
+    def split_inbox(self, with_handle: bool = False):
+        """(device pointer, bytes, IPC handle bytes or None) of this part's exchange inbox."""
+        ptr, nb = C.c_void_p(0), C.c_size_t(0)
+        h = C.create_string_buffer(abi.KSS_IPC_HANDLE_BYTES) if with_handle else None
+        check(lib().kss_split_inbox(self.h, C.byref(ptr), C.byref(nb), h))
+        return ptr.value, nb.value, (h.raw if h is not None else None)
+
+    def split_peers(self, inboxes: Sequence[int]):
+        arr = (C.c_void_p * len(inboxes))(*inboxes)
+        check(lib().kss_split_peers(self.h, arr))
+
+    def split_open(self, handles: Sequence[bytes]):
+        buf = C.create_string_buffer(b"".join(handles), abi.KSS_IPC_HANDLE_BYTES * len(handles))
+        check(lib().kss_split_open(self.h, buf))
 
     def schedule_batch(self, podset_struct: abi.PodSet, n: int, record=False, flags=0) -> np.ndarray:
         chosen = np.full(max(n, 1), -2, np.int32)

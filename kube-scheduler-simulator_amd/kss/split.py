@@ -1,0 +1,141 @@
+"""The node axis as one persistent grid over several GPUs.
+
+Every part loads the whole cluster and stages the same pods; part p runs shards
+[p * wl, (p + 1) * wl) of the n_parts * wl shards of k_simple / k_spread and so owns their
+node rows.  The per-pod exchanges the kernels already make between their shards
+(statistics, PodTopologySpread histograms and critical paths, the packed selectHost key)
+become cross-GPU by storing every granule into every part's inbox: xGMI peer stores from
+inside the running kernels, polled locally.  A pod costs no kernel launch, no collective
+call and no host round trip on any GPU -- the replacement for the per-pod RCCL packed-argmax
+all-reduce of kss/nodeaxis.py, which pays two launches and two collectives per pod.
+
+Two drivers:
+  InProcessSplit  several parts in one process (one device or several), launched from one
+                  thread each so the grids run concurrently (the tests: parts share one GPU);
+  SplitRank       one part per process / GPU (torch.distributed carries only the 64-byte
+                  IPC handles and the barriers; nothing per pod).
+
+Reference: the per-rank sequence is scheduleOne's findNodesThatPassFilters /
+prioritizeNodes / selectHost / AssumePod (simulator/scheduler/scheduler.go:174-219,
+232-267, 323-344) over the part's rows.
+"""
+from __future__ import annotations
+
+import threading
+from typing import List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from . import abi, native
+
+
+def shards_per_part(n_nodes: int, n_parts: int, nodes_per_shard: int = 391, cap: int = 256) -> int:
+    """Shards per part so that the whole grid keeps about `nodes_per_shard` nodes per shard
+    (the 1-GPU C4 geometry: 100k nodes over 256 shards), at most `cap` per part."""
+    total = max(n_parts, -(-max(n_nodes, 1) // nodes_per_shard))
+    return max(1, min(cap, -(-total // n_parts)))
+
+
+def part_rows(n_nodes: int, n_parts: int, wl: int, part: int) -> Tuple[int, int]:
+    """Canonical rows [lo, hi) a part owns: its shards' row ranges (ceil(N / W) per shard)."""
+    W = n_parts * wl
+    per = -(-n_nodes // W)
+    return min(n_nodes, part * wl * per), min(n_nodes, (part + 1) * wl * per)
+
+
+def _run_concurrently(fns):
+    out: List = [None] * len(fns)
+    errs: List = [None] * len(fns)
+
+    def go(i):
+        try:
+            out[i] = fns[i]()
+        except Exception as e:  # noqa: BLE001 - re-raised below
+            errs[i] = e
+
+    ts = [threading.Thread(target=go, args=(i,)) for i in range(len(fns))]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    for e in errs:
+        if e is not None:
+            raise e
+    return out
+
+
+class InProcessSplit:
+    """n_parts contexts in this process, each running its part of one grid."""
+
+    def __init__(self, cluster: abi.Cluster, podset: abi.PodSet, n_parts: int, wl: int,
+                 profile: Optional[abi.Profile] = None, devices: Optional[Sequence[int]] = None):
+        self.n_parts, self.wl, self.n_nodes = n_parts, wl, cluster.n_nodes
+        devices = list(devices) if devices is not None else [0] * n_parts
+        self.ctxs = []
+        for p in range(n_parts):
+            ctx = native.Context(profile, device=devices[p])
+            ctx.load(cluster)
+            ctx.stage(podset)
+            ctx.split_config(n_parts, p, wl)
+            self.ctxs.append(ctx)
+        inboxes = [c.split_inbox()[0] for c in self.ctxs]
+        for c in self.ctxs:
+            c.split_peers(inboxes)
+
+    def run(self, n: int) -> List[np.ndarray]:
+        """Schedule staged pods [0, n) on every part at once; every part's chosen vector."""
+        return _run_concurrently([lambda c=c: c.run_staged(n) for c in self.ctxs])
+
+    def reset(self):
+        for c in self.ctxs:
+            c.reset()
+
+    def node_state(self):
+        """The cluster's mutable columns assembled from the parts' own rows."""
+        out = None
+        for p, c in enumerate(self.ctxs):
+            st = c.node_state()
+            lo, hi = part_rows(self.n_nodes, self.n_parts, self.wl, p)
+            if out is None:
+                out = {k: v.copy() for k, v in st.items()}
+            for k in ("requested", "nonzero"):
+                out[k][:, lo:hi] = st[k][:, lo:hi]
+            out["pod_count"][lo:hi] = st["pod_count"][lo:hi]
+            out["class_count"][:, lo:hi] = st["class_count"][:, lo:hi]
+            out["term_count"][:, lo:hi] = st["term_count"][:, lo:hi]
+        return out
+
+    def close(self):
+        for c in self.ctxs:
+            c.close()
+
+
+class SplitRank:
+    """This process's part (rank r of world) of a grid over the ranks' GPUs."""
+
+    def __init__(self, cluster: abi.Cluster, podset: abi.PodSet, wl: int, profile: Optional[abi.Profile] = None,
+                 device: int = 0, group=None):
+        import torch
+        import torch.distributed as dist
+        self.group = group
+        self.rank, self.world = dist.get_rank(group), dist.get_world_size(group)
+        self.wl, self.n_nodes = wl, cluster.n_nodes
+        self.ctx = native.Context(profile, device=device)
+        self.ctx.load(cluster)
+        self.ctx.stage(podset)
+        self.ctx.split_config(self.world, self.rank, wl)
+        _, _, handle = self.ctx.split_inbox(with_handle=True)
+        mine = torch.frombuffer(bytearray(handle), dtype=torch.uint8)
+        allh = [torch.zeros(abi.KSS_IPC_HANDLE_BYTES, dtype=torch.uint8) for _ in range(self.world)]
+        dist.all_gather(allh, mine, group=group)  # 64 bytes per rank, once
+        self.ctx.split_open([bytes(h.numpy().tobytes()) for h in allh])
+        dist.barrier(group=group)
+
+    def run(self, n: int) -> np.ndarray:
+        return self.ctx.run_staged(n)
+
+    def rows(self) -> Tuple[int, int]:
+        return part_rows(self.n_nodes, self.world, self.wl, self.rank)
+
+    def close(self):
+        self.ctx.close()

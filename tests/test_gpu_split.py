@@ -1,0 +1,118 @@
+"""The split grid (kss_split_*, kss/split.py): the node axis as one persistent k_simple /
+k_spread grid whose parts run on different GPUs and exchange granules by peer stores.  Here
+the parts share the one GPU of the box: in one process (one thread per part) and in two
+processes (one part each, inboxes mapped through IPC handles exchanged over gloo).  Every
+part's chosen vector and outcomes, and the node state assembled from the parts' own rows,
+equal the C oracle's -- on C2's default-profile recipe (k_simple), C4's zone-spread recipe
+(k_spread, BASELINE configs[3]) and C3's spread + inter-pod recipe."""
+import os
+
+import numpy as np
+import pytest
+
+import oracle_c
+from kss import abi, native, split
+from kss.synth import SEED_BASE
+
+pytestmark = pytest.mark.gpu
+THREADS = min(16, os.cpu_count() or 1)
+
+
+def _oracle(s, n_pods):
+    return oracle_c.schedule(abi.default_profile(), s.cluster, s.pods, n_pods, s.n_nodes, record="meta",
+                             threads=THREADS, n_classes=s.cluster.n_classes, n_terms=s.cluster.n_terms)
+
+
+@pytest.mark.parametrize("config,n_nodes,n_pods,n_parts,wl,kernel", [
+    (2, 5000, 600, 2, 8, "k_simple"),
+    (4, 20000, 400, 2, 32, "k_spread"),
+    (3, 3000, 300, 3, 8, "k_spread"),
+    (4, 100000, 200, 2, 128, "k_spread"),
+])
+def test_in_process_parts_match_oracle(config, n_nodes, n_pods, n_parts, wl, kernel):
+    s = native.Synth(config, SEED_BASE + config, n_nodes, n_pods)
+    ch_o, res, st = _oracle(s, n_pods)
+    sp = split.InProcessSplit(s.cluster, s.pods, n_parts, wl)
+    for rep in range(2):  # a second run continues the epochs in the inboxes (no clearing)
+        sp.reset()
+        outs = sp.run(n_pods)
+        for p, (c, ch) in enumerate(zip(sp.ctxs, outs)):
+            assert c.last_kernel() == kernel
+            assert c.last_geometry()["shards"] == n_parts * wl
+            np.testing.assert_array_equal(ch, ch_o, err_msg=f"part {p} run {rep}")
+    meta = sp.ctxs[-1].fetch_meta(n_pods)
+    for j in range(n_pods):
+        m = res.meta(j)
+        assert (meta[j, 0], meta[j, 1], meta[j, 2], meta[j, 3]) == (m["chosen"], m["n_feasible"], m["scored"],
+                                                                    m["status"]), j
+    g = sp.node_state()
+    N = n_nodes
+    np.testing.assert_array_equal(g["requested"][:, :N], st["requested"][:, :N])
+    np.testing.assert_array_equal(g["nonzero"][:, :N], st["nonzero"][:, :N])
+    np.testing.assert_array_equal(g["pod_count"][:N], st["pod_count"][:N])
+    if s.cluster.n_classes:
+        np.testing.assert_array_equal(g["class_count"][:s.cluster.n_classes, :N], st["class_count"][:, :N])
+    sp.close()
+
+
+def test_split_refuses_what_it_cannot_run():
+    s = native.Synth(2, SEED_BASE + 2, 500, 50)
+    ctx = native.Context(abi.default_profile())
+    ctx.load(s.cluster)
+    ctx.stage(s.pods)
+    ctx.split_config(2, 0, 4)
+    with pytest.raises(native.KssError):  # peers not set
+        ctx.run_staged(10)
+    with pytest.raises(native.KssError):  # recorded batches stay on k_schedule
+        ctx.schedule_batch(s.pods, 10, record=True)
+    ctx.split_config(1, 0, 1)  # back to the whole grid on this device
+    ch_o, _, _ = _oracle(s, 50)
+    np.testing.assert_array_equal(ctx.run_staged(50), ch_o)
+    ctx.close()
+
+
+def _rank_main(rank, world, port, config, n_nodes, n_pods, wl, q):
+    import torch
+    import torch.distributed as dist
+    try:
+        torch.zeros(1, device="cuda")  # torch's HIP runtime before libkss's
+        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+        s = native.Synth(config, SEED_BASE + config, n_nodes, n_pods)
+        r = split.SplitRank(s.cluster, s.pods, wl, device=0)
+        chosen = r.run(n_pods)
+        lo, hi = r.rows()
+        st = r.ctx.node_state()
+        q.put((rank, chosen.tolist(), lo, hi, st["requested"][:, lo:hi].tolist(), r.ctx.last_kernel()))
+        dist.barrier()
+        r.close()
+        dist.destroy_process_group()
+    except Exception as e:  # noqa: BLE001 - reported to the parent
+        q.put((rank, repr(e), 0, 0, None, None))
+
+
+def test_two_processes_through_ipc_handles():
+    """One part per process (the deployment shape: one process per GPU), inboxes mapped
+    through hipIpcOpenMemHandle, the handles exchanged over gloo; both processes' grids on
+    the box's one GPU at once."""
+    import multiprocessing as mp
+    import socket
+    config, n_nodes, n_pods, wl = 4, 20000, 300, 32
+    s = native.Synth(config, SEED_BASE + config, n_nodes, n_pods)
+    ch_o, _, st = _oracle(s, n_pods)
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_rank_main, args=(r, 2, port, config, n_nodes, n_pods, wl, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    got = [q.get(timeout=240) for _ in ps]
+    for p in ps:
+        p.join(timeout=60)
+    for rank, chosen, lo, hi, req, kernel in got:
+        assert req is not None, chosen  # the child's exception
+        assert kernel == "k_spread"
+        np.testing.assert_array_equal(np.array(chosen), ch_o, err_msg=f"rank {rank}")
+        np.testing.assert_array_equal(np.array(req, dtype=np.int64).reshape(abi.KSS_NRES, hi - lo),
+                                      st["requested"][:, lo:hi], err_msg=f"rank {rank}")

@@ -3,7 +3,7 @@
 set -o pipefail
 tag=${1:-run}; shift || true
 mkdir -p gpurun_out
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread "$@" \
+timeout -k 10 900 python -u -m pytest ${PYTEST_TARGET:-tests} -m gpu -x -q --timeout 300 --timeout-method thread "$@" \
   > gpurun_out/pytest_gpu_${tag}.log 2>&1
 rc=$?
 tail -5 gpurun_out/pytest_gpu_${tag}.log
