@@ -69,6 +69,8 @@ class InProcessSplit:
 
     def __init__(self, cluster: abi.Cluster, podset: abi.PodSet, n_parts: int, wl: int,
                  profile: Optional[abi.Profile] = None, devices: Optional[Sequence[int]] = None):
+        import gc
+        gc.collect()  # contexts no longer referenced release their streams (HIP maps streams onto few HW queues)
         self.n_parts, self.wl, self.n_nodes = n_parts, wl, cluster.n_nodes
         devices = list(devices) if devices is not None else [0] * n_parts
         self.ctxs = []
@@ -125,10 +127,11 @@ class SplitRank:
         self.ctx.stage(podset)
         self.ctx.split_config(self.world, self.rank, wl)
         _, _, handle = self.ctx.split_inbox(with_handle=True)
-        mine = torch.frombuffer(bytearray(handle), dtype=torch.uint8)
-        allh = [torch.zeros(abi.KSS_IPC_HANDLE_BYTES, dtype=torch.uint8) for _ in range(self.world)]
+        dev = torch.device("cuda", device) if dist.get_backend(group) == "nccl" else torch.device("cpu")
+        mine = torch.frombuffer(bytearray(handle), dtype=torch.uint8).to(dev)
+        allh = [torch.zeros(abi.KSS_IPC_HANDLE_BYTES, dtype=torch.uint8, device=dev) for _ in range(self.world)]
         dist.all_gather(allh, mine, group=group)  # 64 bytes per rank, once
-        self.ctx.split_open([bytes(h.numpy().tobytes()) for h in allh])
+        self.ctx.split_open([bytes(h.cpu().numpy().tobytes()) for h in allh])
         dist.barrier(group=group)
 
     def run(self, n: int) -> np.ndarray:

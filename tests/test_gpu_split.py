@@ -26,7 +26,7 @@ def _oracle(s, n_pods):
 @pytest.mark.parametrize("config,n_nodes,n_pods,n_parts,wl,kernel", [
     (2, 5000, 600, 2, 8, "k_simple"),
     (4, 20000, 400, 2, 32, "k_spread"),
-    (3, 3000, 300, 3, 8, "k_spread"),
+    (3, 3000, 300, 2, 12, "k_spread"),
     (4, 100000, 200, 2, 128, "k_spread"),
 ])
 def test_in_process_parts_match_oracle(config, n_nodes, n_pods, n_parts, wl, kernel):
