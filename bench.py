@@ -478,6 +478,9 @@ def latency_profile(cfg, n_nodes, n_pods, seed, device):
     finally:
         del os.environ["KSS_STAMPS_FILE"]
     out = stamps.latency_summary(path)
+    if not out.get("pods"):  # the stamp buffer did not fit in the shard's LDS (k_spread at large shards)
+        return {"kernel": out.get("kernel"), "shards": out.get("shards"), "pods": 0, "bound_us_per_pod": None,
+                "note": "no phase stamps: the stamp buffer does not fit beside this geometry's LDS"}
     floors = out.get("exchange_floor_us", {})
     out["bound_us_per_pod"] = round(sum(floors.values()), 3)
     out["source"] = "KSS_STAMPS_FILE phase stamps, shard 0 (floors: all shards), first 128 pods of a 1000-pod run"
@@ -730,7 +733,8 @@ def main():
         if not args.no_latency and world == 1:
             latency = latency_profile(cfg, n_nodes, n_pods, seed, local)
             latency["us_per_pod"] = elapsed / args.steps / n_pods * 1e6
-            latency["frac"] = latency["bound_us_per_pod"] / latency["us_per_pod"]
+            if latency.get("bound_us_per_pod"):
+                latency["frac"] = latency["bound_us_per_pod"] / latency["us_per_pod"]
         out = {
             "metric": "pod x node filter+score evals/sec (pods scheduled/sec in extra)",
             "value": value,

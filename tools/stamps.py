@@ -134,6 +134,8 @@ def latency_summary(path):
             z = b[:, :, i] == 0
             b[:, :, i][z] = b[:, :, i - 1][z]
     b = b[:, ok, :]
+    if not ok.any():
+        return {"kernel": "k_simple" if kind == 1 else "k_spread", "shards": w, "pods": 0}
     d = np.diff(b[0, :, :top + 1], axis=1) / 100.0
     out = {"kernel": "k_simple" if kind == 1 else "k_spread", "shards": w, "pods": int(ok.sum()),
            "phases_us": {n: round(float(m), 3) for n, m in zip(names, d.mean(axis=0))},
