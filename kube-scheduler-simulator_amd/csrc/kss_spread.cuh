@@ -112,6 +112,7 @@ __device__ __forceinline__ double go_log_dev(double x) {
 struct alignas(16) SpreadHdr {
   int32_t red[MAXWAVES][G_NS];
   long long kred[2][MAXWAVES];
+  long long kx[MAXWAVES];  // multi-wave argmax sweep: each wave's maximum
   long long kres;
   kss_profile prof;  // a runtime (non-default) profile, staged word by word (as SimpleHdr)
   int32_t abort;
@@ -263,11 +264,15 @@ __device__ __forceinline__ void wave_red32(int32_t (&v)[K], const int (&ops)[K])
 // The scalars are combined over the workgroup's waves here (H.red), by the lanes that
 // publish them.  Granules are accessed through address-space-1 pointers: flat accesses would
 // also count in lgkmcnt and make every following LDS wait on the HBM stores.
+// phase bit 0: publish (wave 0), bit 1: sweep by wave gw of nsw sweeping waves (lanes of
+// every sweeping wave share the values: T = 64 nsw / M lanes per value).
+constexpr int G_XS = 16;  // shards polled per lane at once
 __device__ __forceinline__ bool spread_exchange(SpreadHdr& H, int32_t* xs, unsigned long long* gran_, const XPeers& X,
                                                 int W, int wself,
                                                 unsigned epoch, int* err, int K, unsigned opbits, int sum_lo, int ns,
-                                                int or_lo, int no, unsigned long long* sp) {
-  constexpr int XS = 16;  // shards polled per lane at once
+                                                int or_lo, int no, unsigned long long* sp, int gw = 0, int nsw = 1,
+                                                int phase = 3) {
+  constexpr int XS = G_XS;
   const int lane = threadIdx.x & 63, nw = blockDim.x >> 6;
   const int M = K + ns + no;
   KSS_GLOBAL unsigned long long* gran = gp(gran_);
@@ -279,7 +284,7 @@ __device__ __forceinline__ bool spread_exchange(SpreadHdr& H, int32_t* xs, unsig
   auto opof = [&](int j) { return j < K ? (int)((opbits >> (2 * j)) & 3u) : (j < K + ns ? OP_SUM : OP_OR); };
   const unsigned long long tag = (unsigned long long)epoch << 32;
   const size_t mine = ((size_t)(epoch & 1) * W + wself) * G_XW;
-  for (int j = lane; j < M; j += 64) {
+  for (int j = lane; (phase & 1) && j < M; j += 64) {
     int32_t* sl = slot(j);
     const int op = opof(j);
     int32_t v = *sl;
@@ -291,11 +296,13 @@ __device__ __forceinline__ bool spread_exchange(SpreadHdr& H, int32_t* xs, unsig
     *sl = ident32(op);
   }
   if (sp && lane == 0) sp[2] = wall_clock64();
+  if (!(phase & 2)) return true;
   KSS_GLOBAL const unsigned long long* base = gran + (size_t)(epoch & 1) * W * G_XW;
-  for (int j0 = 0; j0 < M; j0 += 64) {
-    const int mc = min(64, M - j0);
-    const int T = 64 / mc;  // lanes per value in this chunk
-    const int t = lane / mc, j = j0 + (lane - t * mc);
+  const int NL = 64 * nsw, gl = gw * 64 + lane;
+  for (int j0 = 0; j0 < M; j0 += NL) {
+    const int mc = min(NL, M - j0);
+    const int T = NL / mc;  // lanes per value in this chunk
+    const int t = gl / mc, j = j0 + (gl - t * mc);
     const bool act = t < T;
     const int op = opof(min(j, M - 1));
     // the operator differs between lanes: fold all four, branch-free, and pick one at the end
@@ -408,12 +415,24 @@ __device__ __forceinline__ bool spread_reduce(SpreadHdr& H, int32_t* xs, int W, 
     for (int k = 0; k < K; k++) opbits |= (unsigned)ops[k] << (2 * k);
     ++epoch;
     if (sp && threadIdx.x == 0) sp[1] = wall_clock64();
-    if (wave == 0 && spread_exchange(H, xs, gran, X, W, w, epoch, err, K, opbits, sum_lo, ns, or_lo, no, sp) &&
-        minima_q)
-      hard_minima(*minima_q, xs);
-    if (sp && threadIdx.x == 0) sp[4] = wall_clock64();
-    lds_barrier();
-    if (H.abort) return false;
+    const int M = K + ns + no;
+    if (nw == 1 || (long long)W * M <= 64LL * G_XS) {  // one polling round for one wave: wave 0 alone
+      if (wave == 0 && spread_exchange(H, xs, gran, X, W, w, epoch, err, K, opbits, sum_lo, ns, or_lo, no, sp) &&
+          minima_q)
+        hard_minima(*minima_q, xs);
+      if (sp && threadIdx.x == 0) sp[4] = wall_clock64();
+      lds_barrier();
+      if (H.abort) return false;
+    } else {  // many shards: wave 0 publishes, every wave sweeps a share (fewer polling rounds)
+      if (wave == 0) spread_exchange(H, xs, gran, X, W, w, epoch, err, K, opbits, sum_lo, ns, or_lo, no, sp, 0, 1, 1);
+      lds_barrier();  // the slots hold the operators' identities before any wave folds into them
+      spread_exchange(H, xs, gran, X, W, w, epoch, err, K, opbits, sum_lo, ns, or_lo, no, nullptr, wave, nw, 2);
+      lds_barrier();
+      if (H.abort) return false;
+      if (minima_q && wave == 0) hard_minima(*minima_q, xs);
+      if (sp && threadIdx.x == 0) sp[4] = wall_clock64();
+      lds_barrier();
+    }
   }
 #pragma unroll
   for (int k = 0; k < K; k++) v[k] = xs[k];
@@ -436,6 +455,55 @@ __device__ __forceinline__ bool spread_argmax(SpreadHdr& H, int W, int w, unsign
     return true;
   }
   ++epoch;
+  if (nw > 1 && W > 64) {  // every wave polls a share of the shards, 4 per lane in flight
+    const unsigned long long tag = (unsigned long long)epoch << 32;
+    if (wave == 0 && lane < 2)
+      xpub(X, gran, ((size_t)(epoch & 1) * W + w) * G_XW + lane,
+           tag | (lane ? (uint32_t)((unsigned long long)best >> 32) : (uint32_t)best));
+    KSS_GLOBAL const unsigned long long* base = gp(gran) + (size_t)(epoch & 1) * W * G_XW;
+    long long m = 0;
+    const int stride = 64 * nw;
+    for (int c0 = wave * 64; c0 < W; c0 += 4 * stride) {
+      unsigned long long lo[4], hi[4];
+      for (unsigned spins = 0;; ++spins) {
+        bool ok = true;
+#pragma unroll
+        for (int b = 0; b < 4; b++) {
+          const int s = c0 + lane + b * stride;
+          lo[b] = hi[b] = tag;
+          if (s < W) {
+            lo[b] = __hip_atomic_load(base + (size_t)s * G_XW, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            hi[b] = __hip_atomic_load(base + (size_t)s * G_XW + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          }
+        }
+#pragma unroll
+        for (int b = 0; b < 4; b++) ok &= ((lo[b] >> 32) == epoch) & ((hi[b] >> 32) == epoch);
+        if (__all(ok)) break;
+        if (spins >= SPIN_LIMIT) {
+          if (lane == 0) {
+            H.abort = 1;
+            __hip_atomic_store(gp(err), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          }
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+#pragma unroll
+      for (int b = 0; b < 4; b++) {
+        const int s = c0 + lane + b * stride;
+        const long long k = s < W ? (long long)(((hi[b] & 0xFFFFFFFFull) << 32) | (lo[b] & 0xFFFFFFFFull)) : 0;
+        m = k > m ? k : m;
+      }
+    }
+    m = wave_red<OP_MAX>(m);
+    if (lane == 0) H.kx[wave] = m;
+    lds_barrier();
+    if (H.abort) return false;
+    long long k = H.kx[0];
+    for (int x = 1; x < nw; x++) k = H.kx[x] > k ? H.kx[x] : k;
+    key = k;
+    return true;
+  }
   if (wave == 0) {
     const unsigned long long tag = (unsigned long long)epoch << 32;
     if (lane < 2)
