@@ -505,20 +505,31 @@ def run_per_pod(args):
         if r.chosen >= 0:
             ctx.commit(s.pods, j, r.chosen)
     ctx.reset()
-    t_eval, t_commit, chosen = [], [], []
-    t0 = time.perf_counter()
-    for j in range(n_pods):
-        a = time.perf_counter()
-        r = ctx.eval_pod(s.pods, j)
-        b = time.perf_counter()
-        if r.chosen >= 0:
-            ctx.commit(s.pods, j, r.chosen)
-        c = time.perf_counter()
-        t_eval.append(b - a)
-        t_commit.append(c - b)
-        chosen.append(r.chosen)
-    elapsed = time.perf_counter() - t0
-    ev, cm = np.array(t_eval) * 1e6, np.array(t_commit) * 1e6
+    # result buffers reused across pods, as the plugin keeps them: the full record (every
+    # per-node array, for per-plugin Filter / Score / NormalizeScore answers), or the slim one
+    # (verdicts + weighted totals, for one plugin answering Filter and Score)
+    full = native.PodResult(n_nodes)
+    slim = native.PodResult(n_nodes, fields=("fail_plugin", "fail_detail", "total"))
+
+    def loop(res):
+        t_eval, t_commit, ch = [], [], []
+        t0 = time.perf_counter()
+        for j in range(n_pods):
+            a = time.perf_counter()
+            r = ctx.eval_pod(s.pods, j, out=res)
+            b = time.perf_counter()
+            if r.chosen >= 0:
+                ctx.commit(s.pods, j, r.chosen)
+            c = time.perf_counter()
+            t_eval.append(b - a)
+            t_commit.append(c - b)
+            ch.append(r.chosen)
+        return time.perf_counter() - t0, np.array(t_eval) * 1e6, np.array(t_commit) * 1e6, ch
+
+    elapsed, ev, cm, chosen = loop(full)
+    ctx.reset()
+    elapsed_slim, ev_slim, _, chosen_slim = loop(slim)
+    assert chosen_slim == chosen
     out = {
         "metric": "per-pod API: kss_eval_pod + kss_commit latency (pods/sec in value)",
         "value": n_pods / elapsed,
@@ -535,6 +546,9 @@ def run_per_pod(args):
         "config": {"workload": f"C2 cluster, per-pod API: {n_nodes} nodes, {n_pods} pods one call pair each",
                    "nodes": n_nodes, "pods": n_pods, "parallelism": "none"},
         "eval_us": {"median": float(np.median(ev)), "mean": float(ev.mean()), "p90": float(np.percentile(ev, 90))},
+        "eval_slim_us": {"median": float(np.median(ev_slim)), "mean": float(ev_slim.mean()),
+                         "p90": float(np.percentile(ev_slim, 90)), "fields": "fail_plugin, fail_detail, total",
+                         "pods_per_s": n_pods / elapsed_slim},
         "commit_us": {"median": float(np.median(cm)), "mean": float(cm.mean()), "p90": float(np.percentile(cm, 90))},
         "eval_device_ms_last": ctx.last_timing()[0],
         "geometry": ctx.last_geometry(),

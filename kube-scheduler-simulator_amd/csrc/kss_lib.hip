@@ -65,12 +65,14 @@ __host__ __device__ inline size_t align_up(size_t x, size_t a) { return (x + a -
 struct SlotLayout {
   size_t fail, detail, raw, norm, total, bytes;
   __host__ __device__ explicit SlotLayout(size_t N) {
+    // verdicts and totals first: a caller that wants only those (one plugin answering Filter
+    // and Score) copies back the first ~11 B per node, not the ~140 B of per-plugin scores
     fail = 0;
     detail = align_up(N, 256);
-    raw = align_up(detail + 2 * N, 256);
+    total = align_up(detail + 2 * N, 256);
+    raw = align_up(total + 8 * N, 256);
     norm = raw + 8 * KSS_NSCORE * N;
-    total = norm + 8 * KSS_NSCORE * N;
-    bytes = align_up(total + 8 * N, 256);
+    bytes = align_up(norm + 8 * KSS_NSCORE * N, 256);
   }
 };
 
@@ -513,6 +515,8 @@ struct PackedUpload {
   char* dev = nullptr;
   size_t bytes = 0;
   size_t extra_off = 0;
+  size_t tail = 0;        // device bytes reserved after the image (not uploaded): the per-pod record slot
+  char* slot = nullptr;   // dev + align_up(bytes, 256) when tail > 0
 };
 
 int pack_podset(DevBuf& buf, void*& pin, size_t& pin_cap, const kss_podset* ps, size_t extra, DevPods& dp,
@@ -528,7 +532,7 @@ int pack_podset(DevBuf& buf, void*& pin, size_t& pin_cap, const kss_podset* ps, 
   }
   pu.extra_off = o;
   pu.bytes = align_up(o + extra, 64);
-  int rc = buf.ensure(pu.bytes);
+  int rc = buf.ensure(align_up(pu.bytes, 256) + pu.tail);
   if (rc) return rc;
   if (pin_cap < pu.bytes) {
     if (pin) HIP_TRY(hipHostFree(pin));
@@ -539,6 +543,7 @@ int pack_podset(DevBuf& buf, void*& pin, size_t& pin_cap, const kss_podset* ps, 
   }
   pu.host = (char*)pin;
   pu.dev = (char*)buf.p;
+  pu.slot = pu.tail ? pu.dev + align_up(pu.bytes, 256) : nullptr;
   for (int i = 0; i < 6; i++)
     if (sz[i]) std::memcpy(pu.host + off[i], src[i], sz[i]);
   dp.pods = (const kss_pod*)(pu.dev + off[0]);
@@ -2068,6 +2073,14 @@ static int run_single(kss_ctx* ctx, const PlanNeeds& need, const DevPods& dp, in
   job.slot_bytes = SL.bytes;
   job.chosen = (int32_t*)ctx->chosen_buf.p;
   job.meta = (PodMeta*)ctx->meta_buf.p;
+  // per-pod calls: error word, outcome and record slot contiguous behind the uploaded image,
+  // so the whole read-back is one copy
+  const bool one_copy = pu && pu->slot && n == 1 && !chosen_out;
+  const size_t pp_err = pu ? pu->extra_off + align_up(sizeof(DevJob), 16) : 0, pp_meta = pp_err + 64;
+  if (one_copy) {
+    job.meta = (PodMeta*)(pu->dev + pp_meta);
+    job.slots = (uint8_t*)pu->slot;
+  }
   job.spods = simple ? (const SPod*)ctx->spod_buf.p : nullptr;
   job.stat = loop ? (uint32_t*)ctx->stat_buf.p : nullptr;
   job.gpods = spread ? (const GPod*)ctx->gpod_buf.p : nullptr;
@@ -2151,6 +2164,30 @@ static int run_single(kss_ctx* ctx, const PlanNeeds& need, const DevPods& dp, in
   if (rc) return rc;
   ctx->last_kernel = simple ? 1 : (spread ? 2 : 0);
   HIP_TRY(hipEventRecord(ctx->ev1, ctx->stream));
+  if (one_copy) {  // [error word .. outcome .. record slot up to the requested span]: one copy, one sync
+    const size_t span = (size_t)(pu->slot - (pu->dev + pp_err)) + (rbk ? rbk->bytes : 0);
+    if ((rc = ensure_pinned(ctx->rb, ctx->rb_cap, span))) return rc;
+    char* hb = (char*)ctx->rb;
+    HIP_TRY(hipMemcpyAsync(hb, pu->dev + pp_err, span, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    float ms = 0;
+    HIP_TRY(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
+    ctx->last_ms = ctx->last_loop_ms = ms;
+    ctx->last_launches = 1;
+    ctx->last_geom[0] = g.W;
+    ctx->last_geom[1] = g.threads;
+    ctx->last_geom[2] = g.npt;
+    int errw = 0;
+    std::memcpy(&errw, hb, sizeof(int));
+    if (errw) return fail(KSS_E_DEVICE, "shard exchange timed out (workgroups not co-resident?)");
+    ctx->meta_host.resize(1);
+    std::memcpy(ctx->meta_host.data(), hb + (pp_meta - pp_err), sizeof(PodMeta));
+    if (rbk) rbk->host = hb + (pu->slot - (pu->dev + pp_err));
+    ctx->recorded = 0;  // the record went to the caller; kss_fetch_record has nothing to serve
+    ctx->meta_n = 1;
+    ctx->axis_meta_dirty = false;
+    return 0;
+  }
   // every read-back of the launch into one pinned staging, then one synchronisation
   const size_t mb = sizeof(PodMeta) * (size_t)std::max(n, 1), cb = chosen_out && n ? sizeof(int32_t) * (size_t)n : 0;
   const size_t o_meta = 16, o_chosen = align_up(o_meta + mb, 16), o_rb = align_up(o_chosen + cb, 16);
@@ -2374,20 +2411,21 @@ int kss_eval_pod(kss_ctx* ctx, const kss_podset* ps, int32_t pod_index, kss_pod_
   if ((rc = validate(&ctx->host, &one.ps, 1))) return rc;
   std::lock_guard<std::mutex> lk(ctx->mu);
   HIP_TRY(hipSetDevice(ctx->cfg.device));
+  const size_t N = (size_t)ctx->dc.N;
   PackedUpload pu;
-  rc = pack_podset(ctx->tmp_pod_buf, ctx->up, ctx->up_cap, &one.ps, align_up(sizeof(DevJob), 16) + 16, ctx->tdp, pu);
+  pu.tail = SlotLayout(N).bytes;  // the record slot lives right behind the image (one read-back)
+  // extra: the job, then the error word (zeroed by the upload) and the outcome (64 B further)
+  rc = pack_podset(ctx->tmp_pod_buf, ctx->up, ctx->up_cap, &one.ps, align_up(sizeof(DevJob), 16) + 64 + sizeof(PodMeta),
+                   ctx->tdp, pu);
   if (rc) return rc;
   const PlanNeeds need = plan_needs(ctx->key_card_h.data(), ctx->key_flags_h.data(), &one.ps, 1);
-  const size_t N = (size_t)ctx->dc.N;
   const SlotRange r = slot_range(N, out);
-  if ((rc = ctx->slot_buf.ensure(SlotLayout(N).bytes))) return rc;
   ReadBack rbk;
-  rbk.src = (const char*)ctx->slot_buf.p + r.lo;
-  rbk.bytes = r.hi > r.lo ? r.hi - r.lo : 0;
+  rbk.bytes = r.hi > r.lo ? r.hi : 0;  // slot bytes [0, r.hi) ride in the one copy
   rc = run_single(ctx, need, ctx->tdp, 1, /*commit=*/false, /*record=*/false, /*keep_norm=*/true, 0, nullptr,
                   /*staged=*/false, &rbk, &pu);
   if (rc) return rc;
-  return scatter_slot(N, r, rbk.host, ctx->meta_host[0], out);
+  return scatter_slot(N, r, r.hi > r.lo ? rbk.host + r.lo : nullptr, ctx->meta_host[0], out);
 }
 
 // A pending pod as a bound pod of the PostFilter table once committed (id -1 - index,

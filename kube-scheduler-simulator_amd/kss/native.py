@@ -113,9 +113,14 @@ def check(rc: int):
 
 
 class PodResult:
-    """Host arrays for one pod's result (kss_pod_result)."""
+    """Host arrays for one pod's result (kss_pod_result).  `fields` limits which per-node
+    arrays the library fills (the others are passed as NULL and not copied back): e.g.
+    ("fail_plugin", "fail_detail", "total") for a plugin that answers Filter from the
+    verdicts and Score from the weighted totals."""
 
-    def __init__(self, n_nodes: int):
+    ALL = ("fail_plugin", "fail_detail", "raw", "norm", "total")
+
+    def __init__(self, n_nodes: int, fields=ALL):
         N = max(n_nodes, 1)
         self.n_nodes = n_nodes
         self.fail_plugin = np.zeros(N, np.uint8)
@@ -129,6 +134,9 @@ class PodResult:
         s.raw = self.raw.ctypes.data_as(P(C.c_int64))
         s.norm = self.norm.ctypes.data_as(P(C.c_int64))
         s.total = self.total.ctypes.data_as(P(C.c_int64))
+        for f in self.ALL:
+            if f not in fields:
+                setattr(s, f, None)
         self.s = s
 
     @property
@@ -294,8 +302,9 @@ class Context:
     def reset(self):
         check(lib().kss_reset_node_state(self.h))
 
-    def eval_pod(self, podset_struct: abi.PodSet, i: int) -> PodResult:
-        r = PodResult(self.n_nodes)
+    def eval_pod(self, podset_struct: abi.PodSet, i: int, out: Optional[PodResult] = None) -> PodResult:
+        """kss_eval_pod into `out` (a reusable PodResult, as a plugin keeps its buffers) or a new one."""
+        r = out if out is not None else PodResult(self.n_nodes)
         check(lib().kss_eval_pod(self.h, C.byref(podset_struct), i, C.byref(r.s)))
         return r
 
