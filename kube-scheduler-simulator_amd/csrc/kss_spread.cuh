@@ -267,6 +267,9 @@ __device__ __forceinline__ void wave_red32(int32_t (&v)[K], const int (&ops)[K])
 // phase bit 0: publish (wave 0), bit 1: sweep by wave gw of nsw sweeping waves (lanes of
 // every sweeping wave share the values: T = 64 nsw / M lanes per value).
 constexpr int G_XS = 16;  // shards polled per lane at once
+#ifndef KSS_SPREAD_MW_MIN
+#define KSS_SPREAD_MW_MIN (64 * G_XS)  // W x values above which every wave sweeps a share
+#endif
 __device__ __forceinline__ bool spread_exchange(SpreadHdr& H, int32_t* xs, unsigned long long* gran_, const XPeers& X,
                                                 int W, int wself,
                                                 unsigned epoch, int* err, int K, unsigned opbits, int sum_lo, int ns,
@@ -416,7 +419,7 @@ __device__ __forceinline__ bool spread_reduce(SpreadHdr& H, int32_t* xs, int W, 
     ++epoch;
     if (sp && threadIdx.x == 0) sp[1] = wall_clock64();
     const int M = K + ns + no;
-    if (nw == 1 || (long long)W * M <= 64LL * G_XS) {  // one polling round for one wave: wave 0 alone
+    if (nw == 1 || (long long)W * M <= (long long)KSS_SPREAD_MW_MIN) {  // one polling round for one wave: wave 0 alone
       if (wave == 0 && spread_exchange(H, xs, gran, X, W, w, epoch, err, K, opbits, sum_lo, ns, or_lo, no, sp) &&
           minima_q)
         hard_minima(*minima_q, xs);

@@ -14,9 +14,11 @@ import numpy as np
 
 from . import abi
 
-# KSS_LIB=dbg selects the bounds-checked diagnostic build (make -C csrc debug)
+# KSS_LIB=dbg selects the bounds-checked diagnostic build (make -C csrc debug), KSS_LIB=<tag>
+# an experiment build (make -C csrc exp EXP=<tag> EXP_FLAGS=...)
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)),
-                        "libkss_dbg.so" if os.environ.get("KSS_LIB") == "dbg" else "libkss.so")
+                        f"libkss_{os.environ['KSS_LIB']}.so" if os.environ.get("KSS_LIB", "base") != "base"
+                        else "libkss.so")
 P = C.POINTER
 
 
