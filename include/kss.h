@@ -473,7 +473,9 @@ int kss_axis_commit(kss_ctx* ctx, int32_t pod_index, const int64_t* key_dev, con
  *   kss_split_peers   every part's inbox as addressable in this process (in-process parts)
  *   kss_split_open    the same from the parts' IPC handles (one process per GPU)
  * Then kss_run_staged on every part concurrently (all parts' grids must be resident at
- * once).  Replaces SURVEY 8(e)'s per-pod RCCL packed-argmax all-reduce of the node axis
+ * once).  A split run that fails after launching (an exchange timed out: a peer did not
+ * run, or failed) leaves the parts' granule epochs apart; that context then refuses split
+ * runs (KSS_E_INVAL) until every part is re-armed: kss_split_config, then the peers again.  Replaces SURVEY 8(e)'s per-pod RCCL packed-argmax all-reduce of the node axis
  * (findNodesThatPassFilters / prioritizeNodes / selectHost per rank's rows,
  * simulator/scheduler/scheduler.go:174-219, 232-267, 323-344). */
 #define KSS_SPLIT_MAX_PARTS 8

@@ -474,6 +474,7 @@ struct kss_ctx {
   unsigned long long* split_peer[KSS_MAX_PARTS] = {};
   std::vector<void*> split_opened;  // hipIpcOpenMemHandle mappings to close
   bool split_ready = false;
+  bool split_broken = false;  // a failed split run: refuse until re-armed (run_single)
   unsigned split_epoch = 0;
 };
 
@@ -1557,6 +1558,7 @@ static void split_release(kss_ctx* ctx) {
   for (auto& q : ctx->split_peer) q = nullptr;
   ctx->split_n = ctx->split_part = ctx->split_wl = 0;
   ctx->split_ready = false;
+  ctx->split_broken = false;
   ctx->split_epoch = 0;
 }
 
@@ -1968,9 +1970,29 @@ static int ensure_pinned(void*& p, size_t& cap, size_t need) {
   return 0;
 }
 
+static int run_single_impl(kss_ctx* ctx, const PlanNeeds& need, const DevPods& dp, int n, bool commit, bool record,
+                           bool keep_norm, uint32_t flags, int32_t* chosen_out, bool staged, ReadBack* rbk,
+                           const PackedUpload* pu);
+
+// A split run that fails once its granule epochs are assigned (an exchange timed out, or the
+// launch failed) leaves this part's epochs apart from its peers': the context then refuses
+// split runs until kss_split_config re-arms it (fresh zeroed inbox, epochs from 0) — on
+// every part, with the peers exchanged again.
 static int run_single(kss_ctx* ctx, const PlanNeeds& need, const DevPods& dp, int n, bool commit, bool record,
                       bool keep_norm, uint32_t flags, int32_t* chosen_out, bool staged = false, ReadBack* rbk = nullptr,
                       const PackedUpload* pu = nullptr) {
+  const bool split = ctx->split_n > 1;
+  if (split && ctx->split_broken)
+    return fail(KSS_E_INVAL, "split grid: an earlier run failed; re-arm every part (kss_split_config, then the peers)");
+  const unsigned e0 = ctx->split_epoch;
+  const int rc = run_single_impl(ctx, need, dp, n, commit, record, keep_norm, flags, chosen_out, staged, rbk, pu);
+  if (rc && split && ctx->split_epoch != e0) ctx->split_broken = true;
+  return rc;
+}
+
+static int run_single_impl(kss_ctx* ctx, const PlanNeeds& need, const DevPods& dp, int n, bool commit, bool record,
+                           bool keep_norm, uint32_t flags, int32_t* chosen_out, bool staged, ReadBack* rbk,
+                           const PackedUpload* pu) {
   const size_t N = (size_t)ctx->dc.N;
   const SlotLayout SL(N);
   const int nslots = record ? std::max(n, 1) : 1;

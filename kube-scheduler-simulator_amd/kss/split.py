@@ -78,8 +78,14 @@ class InProcessSplit:
             ctx = native.Context(profile, device=devices[p])
             ctx.load(cluster)
             ctx.stage(podset)
-            ctx.split_config(n_parts, p, wl)
             self.ctxs.append(ctx)
+        self.rearm()
+
+    def rearm(self):
+        """(Re)configure every part: fresh zeroed inboxes, epochs from 0, peers exchanged.  Needed
+        once at the start and after a failed run (the parts' epochs may have drifted apart)."""
+        for p, c in enumerate(self.ctxs):
+            c.split_config(self.n_parts, p, self.wl)
         inboxes = [c.split_inbox()[0] for c in self.ctxs]
         for c in self.ctxs:
             c.split_peers(inboxes)
@@ -117,22 +123,29 @@ class SplitRank:
 
     def __init__(self, cluster: abi.Cluster, podset: abi.PodSet, wl: int, profile: Optional[abi.Profile] = None,
                  device: int = 0, group=None):
-        import torch
         import torch.distributed as dist
         self.group = group
         self.rank, self.world = dist.get_rank(group), dist.get_world_size(group)
         self.wl, self.n_nodes = wl, cluster.n_nodes
+        self.device = device
         self.ctx = native.Context(profile, device=device)
         self.ctx.load(cluster)
         self.ctx.stage(podset)
-        self.ctx.split_config(self.world, self.rank, wl)
+        self.rearm()
+
+    def rearm(self):
+        """Collective over the group: a fresh inbox and epochs from 0 on every rank, IPC handles
+        exchanged.  Once at the start, and on every rank after a failed run on any rank."""
+        import torch
+        import torch.distributed as dist
+        self.ctx.split_config(self.world, self.rank, self.wl)
         _, _, handle = self.ctx.split_inbox(with_handle=True)
-        dev = torch.device("cuda", device) if dist.get_backend(group) == "nccl" else torch.device("cpu")
+        dev = torch.device("cuda", self.device) if dist.get_backend(self.group) == "nccl" else torch.device("cpu")
         mine = torch.frombuffer(bytearray(handle), dtype=torch.uint8).to(dev)
         allh = [torch.zeros(abi.KSS_IPC_HANDLE_BYTES, dtype=torch.uint8, device=dev) for _ in range(self.world)]
-        dist.all_gather(allh, mine, group=group)  # 64 bytes per rank, once
+        dist.all_gather(allh, mine, group=self.group)  # 64 bytes per rank
         self.ctx.split_open([bytes(h.cpu().numpy().tobytes()) for h in allh])
-        dist.barrier(group=group)
+        dist.barrier(group=self.group)
 
     def run(self, n: int) -> np.ndarray:
         return self.ctx.run_staged(n)

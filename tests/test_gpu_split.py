@@ -71,6 +71,23 @@ def test_split_refuses_what_it_cannot_run():
     ctx.close()
 
 
+def test_failed_run_refuses_until_rearmed():
+    """A part whose peer never runs times out in its first exchange; its epochs are then
+    apart from the peer's, so it refuses split runs until every part is re-armed."""
+    s = native.Synth(2, SEED_BASE + 2, 2000, 40)
+    ch_o, _, _ = _oracle(s, 40)
+    sp = split.InProcessSplit(s.cluster, s.pods, 2, 4)
+    with pytest.raises(native.KssError):  # part 1 never runs: part 0's exchange times out
+        sp.ctxs[0].run_staged(40)
+    with pytest.raises(native.KssError, match="re-arm"):
+        sp.ctxs[0].run_staged(40)
+    sp.rearm()
+    sp.reset()
+    for p, ch in enumerate(sp.run(40)):
+        np.testing.assert_array_equal(ch, ch_o, err_msg=f"part {p}")
+    sp.close()
+
+
 def _rank_main(rank, world, port, config, n_nodes, n_pods, wl, q):
     import torch
     import torch.distributed as dist
