@@ -511,12 +511,25 @@ def run_per_pod(args):
     full = native.PodResult(n_nodes)
     slim = native.PodResult(n_nodes, fields=("fail_plugin", "fail_detail", "total"))
 
+    # the in-place variant: kss_eval_pod_view leaves the full record in the pinned staging
+    # and hands back pointers (the Go plugin reads them through unsafe.Slice; here the
+    # ctypes call alone, no numpy views)
+    import ctypes
+    view = abi.PodView()
+    pods_ref = ctypes.byref(s.pods)
+
+    class _ViewCall:
+        def __call__(self, j):
+            native.check(native.lib().kss_eval_pod_view(ctx.h, pods_ref, j, abi.KSS_FIELD_ALL, ctypes.byref(view)))
+            return view
+
     def loop(res):
         t_eval, t_commit, ch = [], [], []
+        call = res if isinstance(res, _ViewCall) else (lambda j: ctx.eval_pod(s.pods, j, out=res))
         t0 = time.perf_counter()
         for j in range(n_pods):
             a = time.perf_counter()
-            r = ctx.eval_pod(s.pods, j, out=res)
+            r = call(j)
             b = time.perf_counter()
             if r.chosen >= 0:
                 ctx.commit(s.pods, j, r.chosen)
@@ -530,6 +543,9 @@ def run_per_pod(args):
     ctx.reset()
     elapsed_slim, ev_slim, _, chosen_slim = loop(slim)
     assert chosen_slim == chosen
+    ctx.reset()
+    elapsed_view, ev_view, _, chosen_view = loop(_ViewCall())
+    assert chosen_view == chosen
     out = {
         "metric": "per-pod API: kss_eval_pod + kss_commit latency (pods/sec in value)",
         "value": n_pods / elapsed,
@@ -549,6 +565,10 @@ def run_per_pod(args):
         "eval_slim_us": {"median": float(np.median(ev_slim)), "mean": float(ev_slim.mean()),
                          "p90": float(np.percentile(ev_slim, 90)), "fields": "fail_plugin, fail_detail, total",
                          "pods_per_s": n_pods / elapsed_slim},
+        "eval_view_us": {"median": float(np.median(ev_view)), "mean": float(ev_view.mean()),
+                         "p90": float(np.percentile(ev_view, 90)),
+                         "fields": "all, in place (kss_eval_pod_view: no copy into caller arrays)",
+                         "pods_per_s": n_pods / elapsed_view},
         "commit_us": {"median": float(np.median(cm)), "mean": float(cm.mean()), "p90": float(np.percentile(cm, 90))},
         "eval_device_ms_last": ctx.last_timing()[0],
         "geometry": ctx.last_geometry(),

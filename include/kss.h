@@ -378,6 +378,31 @@ int kss_apply_port_delta(kss_ctx* ctx, const int32_t* idx, int32_t n, const uint
 /* evaluate one pod against the current snapshot (no commit): the PreFilter-time call.  Only
  * the pod's own program is uploaded; the record comes back in one copy. */
 int kss_eval_pod(kss_ctx* ctx, const kss_podset* ps, int32_t pod_index, kss_pod_result* out);
+/* The same evaluation without the copy into caller arrays: `out` points into the context's
+ * pinned read-back staging, which the one device->host copy fills directly.  `fields`
+ * (KSS_FIELD_*) selects the arrays read back; the others are NULL.  The pointers stay valid
+ * until the next call on ctx that runs device work.  Saves the host copy of the per-node
+ * arrays (~0.7 MB for the full record at 5k nodes): the plugin reads them in place during
+ * the pod's scheduling cycle. */
+#define KSS_FIELD_FAIL (1u << 0)
+#define KSS_FIELD_DETAIL (1u << 1)
+#define KSS_FIELD_RAW (1u << 2)
+#define KSS_FIELD_NORM (1u << 3)
+#define KSS_FIELD_TOTAL (1u << 4)
+#define KSS_FIELD_ALL 0x1Fu
+typedef struct kss_pod_view {
+  const uint8_t* fail_plugin;  /* [n] */
+  const uint16_t* fail_detail; /* [n] */
+  const int64_t* raw;          /* [KSS_NSCORE][n] */
+  const int64_t* norm;         /* [KSS_NSCORE][n] */
+  const int64_t* total;        /* [n] */
+  int32_t n_feasible;
+  int32_t chosen;
+  int64_t best_total;
+  int32_t scored;
+  int32_t status;
+} kss_pod_view;
+int kss_eval_pod_view(kss_ctx* ctx, const kss_podset* ps, int32_t pod_index, uint32_t fields, kss_pod_view* out);
 /* commit pod ps.pods[pod_index] to node (AssumePod); rollback undoes it (Unreserve/ForgetPod).
  * The deltas travel in the kernel's arguments (no upload). */
 int kss_commit(kss_ctx* ctx, const kss_podset* ps, int32_t pod_index, int32_t node);

@@ -2186,6 +2186,20 @@ static int run_single_impl(kss_ctx* ctx, const PlanNeeds& need, const DevPods& d
   if (rc) return rc;
   ctx->last_kernel = simple ? 1 : (spread ? 2 : 0);
   HIP_TRY(hipEventRecord(ctx->ev1, ctx->stream));
+  // diagnostic stamps -> KSS_STAMPS_FILE, one record per launch: {kernel (0 k_schedule,
+  // 1 k_simple, 2 k_spread), shards} then the stamps
+  auto dump_stamps = [&]() -> int {
+    if (!stamps) return 0;
+    std::vector<unsigned long long> h(2 + stamp_bytes / 8);
+    h[0] = simple ? 1 : (spread ? 2 : 0);
+    h[1] = loop ? (unsigned long long)g.W : 1;
+    HIP_TRY(hipMemcpy(h.data() + 2, stamps, stamp_bytes, hipMemcpyDeviceToHost));
+    if (FILE* f = fopen(ctx->stamps_file, "ab")) {
+      fwrite(h.data(), 8, h.size(), f);
+      fclose(f);
+    }
+    return 0;
+  };
   if (one_copy) {  // [error word .. outcome .. record slot up to the requested span]: one copy, one sync
     const size_t span = (size_t)(pu->slot - (pu->dev + pp_err)) + (rbk ? rbk->bytes : 0);
     if ((rc = ensure_pinned(ctx->rb, ctx->rb_cap, span))) return rc;
@@ -2208,7 +2222,7 @@ static int run_single_impl(kss_ctx* ctx, const PlanNeeds& need, const DevPods& d
     ctx->recorded = 0;  // the record went to the caller; kss_fetch_record has nothing to serve
     ctx->meta_n = 1;
     ctx->axis_meta_dirty = false;
-    return 0;
+    return dump_stamps();
   }
   // every read-back of the launch into one pinned staging, then one synchronisation
   const size_t mb = sizeof(PodMeta) * (size_t)std::max(n, 1), cb = chosen_out && n ? sizeof(int32_t) * (size_t)n : 0;
@@ -2247,17 +2261,7 @@ static int run_single_impl(kss_ctx* ctx, const PlanNeeds& need, const DevPods& d
   ctx->recorded = record ? n : (n > 0 && !loop ? 1 : 0);
   ctx->meta_n = n;
   ctx->axis_meta_dirty = false;
-  if (stamps) {  // record: {kernel (0 k_schedule, 1 k_simple, 2 k_spread), shards} then the stamps
-    std::vector<unsigned long long> h(2 + stamp_bytes / 8);
-    h[0] = simple ? 1 : (spread ? 2 : 0);
-    h[1] = loop ? (unsigned long long)g.W : 1;
-    HIP_TRY(hipMemcpy(h.data() + 2, stamps, stamp_bytes, hipMemcpyDeviceToHost));
-    if (FILE* f = fopen(ctx->stamps_file, "ab")) {
-      fwrite(h.data(), 8, h.size(), f);
-      fclose(f);
-    }
-  }
-  return 0;
+  return dump_stamps();
 }
 
 // compact records (k_simple) or resolved programs (k_spread) of the staged podset (host copy
@@ -2297,18 +2301,24 @@ struct SlotRange {
   size_t lo, hi;
 };
 
-static SlotRange slot_range(size_t N, const kss_pod_result* out) {
+static SlotRange slot_range_fields(size_t N, uint32_t fields) {
   const SlotLayout SL(N);
-  const void* dst[5] = {out->fail_plugin, out->fail_detail, out->raw, out->norm, out->total};
+  const uint32_t bit[5] = {KSS_FIELD_FAIL, KSS_FIELD_DETAIL, KSS_FIELD_RAW, KSS_FIELD_NORM, KSS_FIELD_TOTAL};
   const size_t off[5] = {SL.fail, SL.detail, SL.raw, SL.norm, SL.total};
   const size_t bytes[5] = {N, 2 * N, 8 * KSS_NSCORE * N, 8 * KSS_NSCORE * N, 8 * N};
   SlotRange r{SL.bytes, 0};
   for (int i = 0; i < 5; i++)
-    if (dst[i] && bytes[i]) {
+    if ((fields & bit[i]) && bytes[i]) {
       r.lo = std::min(r.lo, off[i]);
       r.hi = std::max(r.hi, off[i] + bytes[i]);
     }
   return r;
+}
+
+static SlotRange slot_range(size_t N, const kss_pod_result* out) {
+  return slot_range_fields(N, (out->fail_plugin ? KSS_FIELD_FAIL : 0u) | (out->fail_detail ? KSS_FIELD_DETAIL : 0u) |
+                                  (out->raw ? KSS_FIELD_RAW : 0u) | (out->norm ? KSS_FIELD_NORM : 0u) |
+                                  (out->total ? KSS_FIELD_TOTAL : 0u));
 }
 
 // slot bytes [r.lo, r.hi) at `src` (host) -> the result's arrays, plus the pod's outcome
@@ -2424,14 +2434,16 @@ static int compact_pod(const kss_podset* ps, int i, OnePod& o) {
   return 0;
 }
 
-int kss_eval_pod(kss_ctx* ctx, const kss_podset* ps, int32_t pod_index, kss_pod_result* out) {
-  if (!ctx || !ctx->loaded || !ps || !out) return fail(KSS_E_INVAL, "bad arguments");
+// kss_eval_pod's device work: the pod's own program uploaded with the job, one launch, and
+// slot bytes [0, r.hi) read back in the same copy as the error word and the outcome
+// (rbk.host: the slot in the pinned staging).
+static int eval_pod_slot(kss_ctx* ctx, const kss_podset* ps, int32_t pod_index, const SlotRange& r, ReadBack& rbk) {
+  if (!ctx || !ctx->loaded || !ps) return fail(KSS_E_INVAL, "bad arguments");
   if (pod_index < 0 || pod_index >= ps->n_pods) return fail(KSS_E_INVAL, "pod index out of range");
   OnePod one;
   int rc = compact_pod(ps, pod_index, one);
   if (rc) return rc;
   if ((rc = validate(&ctx->host, &one.ps, 1))) return rc;
-  std::lock_guard<std::mutex> lk(ctx->mu);
   HIP_TRY(hipSetDevice(ctx->cfg.device));
   const size_t N = (size_t)ctx->dc.N;
   PackedUpload pu;
@@ -2441,13 +2453,43 @@ int kss_eval_pod(kss_ctx* ctx, const kss_podset* ps, int32_t pod_index, kss_pod_
                    ctx->tdp, pu);
   if (rc) return rc;
   const PlanNeeds need = plan_needs(ctx->key_card_h.data(), ctx->key_flags_h.data(), &one.ps, 1);
+  rbk.bytes = r.hi > r.lo ? r.hi : 0;  // slot bytes [0, r.hi) ride in the one copy
+  return run_single(ctx, need, ctx->tdp, 1, /*commit=*/false, /*record=*/false, /*keep_norm=*/true, 0, nullptr,
+                    /*staged=*/false, &rbk, &pu);
+}
+
+int kss_eval_pod(kss_ctx* ctx, const kss_podset* ps, int32_t pod_index, kss_pod_result* out) {
+  if (!ctx || !out) return fail(KSS_E_INVAL, "bad arguments");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  const size_t N = (size_t)ctx->dc.N;
   const SlotRange r = slot_range(N, out);
   ReadBack rbk;
-  rbk.bytes = r.hi > r.lo ? r.hi : 0;  // slot bytes [0, r.hi) ride in the one copy
-  rc = run_single(ctx, need, ctx->tdp, 1, /*commit=*/false, /*record=*/false, /*keep_norm=*/true, 0, nullptr,
-                  /*staged=*/false, &rbk, &pu);
-  if (rc) return rc;
+  if (int rc = eval_pod_slot(ctx, ps, pod_index, r, rbk)) return rc;
   return scatter_slot(N, r, r.hi > r.lo ? rbk.host + r.lo : nullptr, ctx->meta_host[0], out);
+}
+
+int kss_eval_pod_view(kss_ctx* ctx, const kss_podset* ps, int32_t pod_index, uint32_t fields, kss_pod_view* out) {
+  if (!ctx || !out) return fail(KSS_E_INVAL, "bad arguments");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  const size_t N = (size_t)ctx->dc.N;
+  const SlotLayout SL(N);
+  const SlotRange r = slot_range_fields(N, fields);
+  ReadBack rbk;
+  if (int rc = eval_pod_slot(ctx, ps, pod_index, r, rbk)) return rc;
+  const char* b = r.hi > r.lo ? rbk.host : nullptr;  // the slot in the pinned staging
+  out->fail_plugin = b && (fields & KSS_FIELD_FAIL) ? (const uint8_t*)(b + SL.fail) : nullptr;
+  out->fail_detail = b && (fields & KSS_FIELD_DETAIL) ? (const uint16_t*)(b + SL.detail) : nullptr;
+  out->raw = b && (fields & KSS_FIELD_RAW) ? (const int64_t*)(b + SL.raw) : nullptr;
+  out->norm = b && (fields & KSS_FIELD_NORM) ? (const int64_t*)(b + SL.norm) : nullptr;
+  out->total = b && (fields & KSS_FIELD_TOTAL) ? (const int64_t*)(b + SL.total) : nullptr;
+  const PodMeta& m = ctx->meta_host[0];
+  out->n_feasible = m.n_feasible;
+  out->chosen = m.chosen;
+  out->best_total = m.best_total;
+  out->scored = m.scored;
+  out->status = m.status;
+  if (m.status == 4) return fail(KSS_E_UNSUPPORTED, "pod program exceeds the device path's per-pod limits");
+  return 0;
 }
 
 // A pending pod as a bound pod of the PostFilter table once committed (id -1 - index,

@@ -19,6 +19,9 @@ KSS_MAX_BINS = 1024
 KSS_MAX_PORTS = 64
 KSS_SPLIT_MAX_PARTS = 8
 KSS_IPC_HANDLE_BYTES = 64
+# kss_eval_pod_view fields
+KSS_FIELD_FAIL, KSS_FIELD_DETAIL, KSS_FIELD_RAW, KSS_FIELD_NORM, KSS_FIELD_TOTAL = 1, 2, 4, 8, 16
+KSS_FIELD_ALL = 0x1F
 KSS_IMAGE_MIN_THRESHOLD = 23 * 1024 * 1024
 KSS_IMAGE_MAX_CONTAINER_THRESHOLD = 1000 * 1024 * 1024
 
@@ -172,6 +175,12 @@ class Profile(C.Structure):
 
 
 class PodResult(C.Structure):
+    _fields_ = [("fail_plugin", P(u8)), ("fail_detail", P(u16)), ("raw", P(i64)), ("norm", P(i64)),
+                ("total", P(i64)), ("n_feasible", i32), ("chosen", i32), ("best_total", i64), ("scored", i32),
+                ("status", i32)]
+
+
+class PodView(C.Structure):
     _fields_ = [("fail_plugin", P(u8)), ("fail_detail", P(u16)), ("raw", P(i64)), ("norm", P(i64)),
                 ("total", P(i64)), ("n_feasible", i32), ("chosen", i32), ("best_total", i64), ("scored", i32),
                 ("status", i32)]

@@ -45,6 +45,7 @@ SIGNATURES = [
     ("kss_read_port_state", C.c_int, [C.c_void_p, P(C.c_uint64)]),
     ("kss_apply_port_delta", C.c_int, [C.c_void_p, P(C.c_int32), C.c_int32, P(C.c_uint64)]),
     ("kss_eval_pod", C.c_int, [C.c_void_p, P(abi.PodSet), C.c_int32, P(abi.PodResult)]),
+    ("kss_eval_pod_view", C.c_int, [C.c_void_p, P(abi.PodSet), C.c_int32, C.c_uint32, P(abi.PodView)]),
     ("kss_commit", C.c_int, [C.c_void_p, P(abi.PodSet), C.c_int32, C.c_int32]),
     ("kss_rollback", C.c_int, [C.c_void_p, P(abi.PodSet), C.c_int32, C.c_int32]),
     ("kss_schedule_batch", C.c_int, [C.c_void_p, P(abi.PodSet), C.c_int32, C.c_uint32, P(C.c_int32)]),
@@ -112,6 +113,29 @@ def lib() -> C.CDLL:
 def check(rc: int):
     if rc != 0:
         raise KssError(rc, (lib().kss_last_error() or b"").decode())
+
+
+class PodView:
+    """kss_pod_view as numpy arrays aliasing the library's staging (read-only, zero-copy);
+    unrequested fields are None.  Copy what must outlive the next call on the context."""
+
+    def __init__(self, v: "abi.PodView", n_nodes: int):
+        N = n_nodes
+
+        def arr(ptr, shape):
+            if not ptr:
+                return None
+            a = np.ctypeslib.as_array(ptr, shape=shape)
+            a.flags.writeable = False
+            return a
+
+        self.fail_plugin = arr(v.fail_plugin, (N,))
+        self.fail_detail = arr(v.fail_detail, (N,))
+        self.raw = arr(v.raw, (abi.KSS_NSCORE, N))
+        self.norm = arr(v.norm, (abi.KSS_NSCORE, N))
+        self.total = arr(v.total, (N,))
+        self.n_feasible, self.chosen, self.best_total = v.n_feasible, v.chosen, v.best_total
+        self.scored, self.status = v.scored, v.status
 
 
 class PodResult:
@@ -309,6 +333,13 @@ class Context:
         r = out if out is not None else PodResult(self.n_nodes)
         check(lib().kss_eval_pod(self.h, C.byref(podset_struct), i, C.byref(r.s)))
         return r
+
+    def eval_pod_view(self, podset_struct: abi.PodSet, i: int, fields: int = abi.KSS_FIELD_ALL) -> "PodView":
+        """kss_eval_pod_view: the result's arrays as read-only numpy views of the context's
+        pinned read-back staging (no host copy); valid until the next call on this context."""
+        v = abi.PodView()
+        check(lib().kss_eval_pod_view(self.h, C.byref(podset_struct), i, fields, C.byref(v)))
+        return PodView(v, self.n_nodes)
 
     def load_bound(self, boundset_struct: abi.Boundset):
         """The bound pods the PostFilter dry run may evict (CompiledCluster.as_boundset())."""

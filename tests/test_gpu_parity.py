@@ -232,6 +232,33 @@ def test_eval_pod_commit_rollback():
         np.testing.assert_array_equal(before[k], after[k])
 
 
+def test_eval_pod_view_equals_eval_pod():
+    """kss_eval_pod_view (arrays in place in the pinned staging) returns what kss_eval_pod
+    copies out, and only the fields asked for."""
+    s = native.Synth(3, 0, 300, 12)
+    ctx = native.Context(abi.default_profile())
+    ctx.load(s.cluster)
+    N = 300
+    for j in range(12):
+        r = ctx.eval_pod(s.pods, j)
+        want = {k: getattr(r, k).copy() for k in ("fail_plugin", "fail_detail", "raw", "norm", "total")}
+        v = ctx.eval_pod_view(s.pods, j)
+        assert (v.chosen, v.n_feasible, v.scored, v.status) == (r.chosen, r.n_feasible, r.scored, r.status)
+        np.testing.assert_array_equal(v.fail_plugin, want["fail_plugin"][:N])
+        np.testing.assert_array_equal(v.fail_detail, want["fail_detail"][:N])
+        ok = want["fail_plugin"][:N] == abi.KSS_F_PASS
+        np.testing.assert_array_equal(v.raw[:, ok], want["raw"][:, :N][:, ok])
+        if r.scored:
+            np.testing.assert_array_equal(v.norm[:, ok], want["norm"][:, :N][:, ok])
+            np.testing.assert_array_equal(v.total[ok], want["total"][:N][ok])
+        slim = ctx.eval_pod_view(s.pods, j, abi.KSS_FIELD_FAIL | abi.KSS_FIELD_TOTAL)
+        assert slim.raw is None and slim.norm is None and slim.fail_detail is None
+        np.testing.assert_array_equal(slim.fail_plugin, want["fail_plugin"][:N])
+        if r.chosen >= 0:
+            ctx.commit(s.pods, j, r.chosen)
+    ctx.close()
+
+
 @pytest.mark.parametrize("config,sizes,n_pods", [
     (5, [300] * 12, 150),            # k_simple sweep, one workgroup per scenario
     (5, [1000] * 8, 200),            # C5 scenario size
