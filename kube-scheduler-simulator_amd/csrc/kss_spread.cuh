@@ -27,6 +27,8 @@
 #pragma once
 #include "kss_simple.cuh"
 
+#include <type_traits>
+
 namespace kss {
 
 constexpr int G_QMAX = 128;  // uint4 per record (header + references; host-checked)
@@ -266,7 +268,7 @@ __device__ __forceinline__ void wave_red32(int32_t (&v)[K], const int (&ops)[K])
 // also count in lgkmcnt and make every following LDS wait on the HBM stores.
 // phase bit 0: publish (wave 0), bit 1: sweep by wave gw of nsw sweeping waves (lanes of
 // every sweeping wave share the values: T = 64 nsw / M lanes per value).
-constexpr int G_XS = 16;  // shards polled per lane at once
+constexpr int G_XS = 16;  // at most this many shards polled per lane at once (4 / 8 / 16 by need)
 #ifndef KSS_SPREAD_MW_MIN
 #define KSS_SPREAD_MW_MIN (64 * G_XS)  // W x values above which every wave sweeps a share
 #endif
@@ -310,40 +312,50 @@ __device__ __forceinline__ bool spread_exchange(SpreadHdr& H, int32_t* xs, unsig
     const int op = opof(min(j, M - 1));
     // the operator differs between lanes: fold all four, branch-free, and pick one at the end
     int32_t a_sum = 0, a_max = INT32_MIN, a_min = INT32_MAX, a_or = 0;
-    for (int w0 = 0; w0 < W; w0 += T * XS) {
-      unsigned long long g[XS];
-      for (unsigned spins = 0;; ++spins) {
-        bool ok = true;
+    // loads per lane sized to the shards this lane polls (4, 8 or 16), every load issued
+    // unconditionally from a clamped address (no exec-mask region per load), the lanes and
+    // shards past the end masked in the tag test and the fold
+    auto sweep = [&](auto xs_c) -> bool {
+      constexpr int XSN = decltype(xs_c)::value;
+      const int jc = min(j, M - 1);
+      for (int w0 = 0; w0 < W; w0 += T * XSN) {
+        unsigned long long g[XSN];
+        for (unsigned spins = 0;; ++spins) {
+          bool ok = true;
 #pragma unroll
-        for (int b = 0; b < XS; b++) {
-          const int w = w0 + t + T * b;
-          g[b] = tag;
-          if (act && w < W)
-            g[b] = __hip_atomic_load(base + (size_t)w * G_XW + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-#pragma unroll
-        for (int b = 0; b < XS; b++) ok &= (g[b] >> 32) == epoch;
-        if (__all(ok)) break;
-        if (spins >= SPIN_LIMIT) {
-          if (lane == 0) {
-            H.abort = 1;
-            __hip_atomic_store(gp(err), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          for (int b = 0; b < XSN; b++) {
+            const int w = w0 + t + T * b;
+            g[b] = __hip_atomic_load(base + (size_t)min(w, W - 1) * G_XW + jc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            ok &= !(act && w < W) || (g[b] >> 32) == epoch;
           }
-          return false;
+          if (__all(ok)) break;
+          if (spins >= SPIN_LIMIT) {
+            if (lane == 0) {
+              H.abort = 1;
+              __hip_atomic_store(gp(err), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            return false;
+          }
+          __builtin_amdgcn_s_sleep(1);
         }
-        __builtin_amdgcn_s_sleep(1);
-      }
-      if (sp && lane == 0) sp[3] = wall_clock64();
+        if (sp && lane == 0) sp[3] = wall_clock64();
 #pragma unroll
-      for (int b = 0; b < XS; b++) {
-        const bool in = w0 + t + T * b < W;
-        const int32_t x = (int32_t)(uint32_t)g[b];
-        a_sum += in ? x : 0;
-        a_max = max(a_max, in ? x : INT32_MIN);
-        a_min = min(a_min, in ? x : INT32_MAX);
-        a_or |= in ? x : 0;
+        for (int b = 0; b < XSN; b++) {
+          const bool in = w0 + t + T * b < W;
+          const int32_t x = (int32_t)(uint32_t)g[b];
+          a_sum += in ? x : 0;
+          a_max = max(a_max, in ? x : INT32_MIN);
+          a_min = min(a_min, in ? x : INT32_MAX);
+          a_or |= in ? x : 0;
+        }
       }
-    }
+      return true;
+    };
+    const int need = (W + T - 1) / T;  // shards per lane
+    const bool swept = need <= 4   ? sweep(std::integral_constant<int, 4>{})
+                       : need <= 8 ? sweep(std::integral_constant<int, 8>{})
+                                   : sweep(std::integral_constant<int, XS>{});
+    if (!swept) return false;
     const int32_t acc = op == OP_SUM ? a_sum : (op == OP_MAX ? a_max : (op == OP_MIN ? a_min : a_or));
     if (act) {
       int32_t* sl = slot(j);
