@@ -451,7 +451,8 @@ __device__ __forceinline__ bool spread_reduce(SpreadHdr& H, int32_t* xs, int W, 
   }
 #pragma unroll
   for (int k = 0; k < K; k++) v[k] = xs[k];
-  lds_barrier();  // xs[0..K) may be rewritten by the next reduction
+  // no barrier here: the next reduction rewrites xs[0..K) (publish resets, or the local
+  // path's stores) only behind its own first barrier, which every wave reaches after reading
   return true;
 }
 
@@ -765,6 +766,12 @@ __device__ __forceinline__ void spread_schedule(DevCluster c, const GPod* __rest
     L.ring[(j % 3) * gq + i % gq] = grec[(size_t)j * gq + i % gq];
   }
   if (tid == 0) H.abort = 0;
+  __syncthreads();  // the first record is in the ring: zero its statistics bins
+  {
+    const GPod& q0 = *reinterpret_cast<const GPod*>(L.ring + (k0 % 3) * gq);
+    if (q0.dyn.status == 0 && q0.need_stats)
+      for (int b = tid; b < q0.total_bins + q0.total_pbins; b += nt) L.xs[G_NS + b] = 0;
+  }
   __syncthreads();
 
   KSS_GLOBAL const uint32_t* gstat = gp(stat);
@@ -822,8 +829,7 @@ __device__ __forceinline__ void spread_schedule(DevCluster c, const GPod* __rest
     for (int i = 0; i < MAXH; i++) hard_min[i] = INT32_MAX;
     // ---- stats: PodTopologySpread PreFilter, InterPodAffinity PreFilter / PreScore ----
     if (evaluated && q.need_stats) {
-      for (int b = tid; b < q.total_bins + q.total_pbins; b += nt) bins[b] = 0;
-      lds_barrier();
+      // bins zeroed at the end of the previous pod (or in the prologue), behind its barrier
       for (int s = tid; s < own; s += nt) stats_node(L, q, s, sw[s], bins, hard_min, flags);
       GSTAMP(1);
       int32_t v[MAXH + 1];
@@ -1127,6 +1133,13 @@ __device__ __forceinline__ void spread_schedule(DevCluster c, const GPod* __rest
 #pragma unroll
       for (int j = 0; j < G_PF; j++)
         if (j < pf_per) L.st[((k + 1) & 1) * cap + min(j * pf_n + pf_lane, own - 1)] = pfw[j];
+    }
+    // the statistics bins of pod k+1, zeroed ahead of the barrier that ends this pod (its
+    // passes no longer read them): its stats pass then starts without a barrier of its own
+    if (k + 1 < k1) {
+      const GPod& qn = *reinterpret_cast<const GPod*>(L.ring + ((k + 1) % 3) * gq);
+      if (qn.dyn.status == 0 && qn.need_stats)
+        for (int b = tid; b < qn.total_bins + qn.total_pbins; b += nt) bins[b] = 0;
     }
     lds_barrier();
     GSTAMP(9);
