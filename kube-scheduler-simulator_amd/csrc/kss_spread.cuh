@@ -270,7 +270,7 @@ __device__ __forceinline__ void wave_red32(int32_t (&v)[K], const int (&ops)[K])
 // every sweeping wave share the values: T = 64 nsw / M lanes per value).
 constexpr int G_XS = 16;  // at most this many shards polled per lane at once (4 / 8 / 16 by need)
 #ifndef KSS_SPREAD_MW_MIN
-#define KSS_SPREAD_MW_MIN (64 * G_XS)  // W x values above which every wave sweeps a share
+#define KSS_SPREAD_MW_MIN (64 * 4)  // W x values above which every wave sweeps a share (C3: 40 x 13)
 #endif
 __device__ __forceinline__ bool spread_exchange(SpreadHdr& H, int32_t* xs, unsigned long long* gran_, const XPeers& X,
                                                 int W, int wself,
