@@ -419,12 +419,13 @@ __device__ __forceinline__ bool simple_exchange(SimpleHdr& H, unsigned long long
     for (unsigned spins = 0;; ++spins) {
       bool ok = true;
       unsigned long long g[SX_VALS];
+      // every load issued (lanes past W read shard 0's granules), no exec-mask region per load
 #pragma unroll
       for (int i = 0; i < SX_VALS; i++)
-        g[i] = valid ? __hip_atomic_load(base + (size_t)s * SX_VALS + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : tag;
+        g[i] = __hip_atomic_load(base + (size_t)(valid ? s : 0) * SX_VALS + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #pragma unroll
       for (int i = 0; i < SX_VALS; i++) {
-        ok &= (g[i] >> 32) == epoch;
+        ok &= !valid || (g[i] >> 32) == epoch;
         got[ch][i] = valid ? (uint32_t)g[i] : 0u;
       }
       if (__all(ok)) break;
