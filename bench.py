@@ -7,11 +7,16 @@ one MI355X (each pod sees the previous pods' bindings).  One "step" = the whole
 10,000-pod batch from the same initial snapshot (node state is reset on the device
 before each step; pod programs and the cluster are resident in HBM before timing).
 
-Multi-GPU (torchrun, one process per GPU): every rank schedules its own independent
-C2 cluster (a what-if scenario; seed + rank) — scenario sharding, no data-path
-collective, "weak" scaling.  Control-plane barrier/max uses gloo.
+Multi-GPU (`--gpus N`: under torchrun, or started without it, when this process launches the
+N rank processes itself before touching any GPU; one process per GPU): every rank schedules
+its own independent C2 cluster (a what-if scenario; seed + rank) — scenario sharding, no
+data-path collective, "weak" scaling.  Control-plane barrier/max uses gloo.  Beside it, the
+same line carries `c4_split`: BASELINE config C4 (100,000 nodes x 20,000 pods, zone PTS) as ONE
+split grid over all N GPUs (kss/split.py; N = 1: the whole grid on one GPU), strong scaling —
+the north_star "pods/s at 100k nodes at 1/2/4/8 GPUs" figure.
 
-Prints ONE JSON line on rank 0.
+Prints ONE JSON line on rank 0.  Other modes: --config 1..4, --scenarios S (C5), --split P,
+--node-axis, --per-pod, --postfilter.
 """
 import argparse
 import csv
@@ -32,6 +37,9 @@ sys.path.insert(0, os.path.join(ROOT, "oracle"))
 # Algorithmic bytes per (pod, node) evaluation, SURVEY §8(d) / BASELINE.md §2:
 # default profile reads 92 B of node state and writes 17 B of verdict + raw scores.
 B_EVAL = {1: 109, 2: 109, 3: 129, 4: 129, 5: 109}
+# each config's pod recipe (SURVEY §8(d) synthetic inputs)
+RECIPE = {1: "default profile", 2: "default profile", 3: "default profile + PodTopologySpread + InterPodAffinity",
+          4: "default profile + zone PodTopologySpread (DoNotSchedule)", 5: "default profile"}
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 
 
@@ -411,7 +419,7 @@ def run_split(args):
     achieved = B_EVAL[cfg] * n_pods * rows / loop_s / 1e9
     if rank == 0:
         cpu = None
-        if not args.no_cpu and world == 1:
+        if not args.no_cpu:  # the host restatement, the same figure at every world size
             threads, _ = cpu_threads()
             cpu = cpu_baseline(cfg, n_nodes, n_pods, args.cpu_seconds, threads, seed=SEED_BASE + cfg)
         out = {
@@ -427,8 +435,7 @@ def run_split(args):
             "vs_baseline": None,
             "dtype": "int64/f64",
             "data": f"synthetic (SplitMix64 seed 0x5EED000{cfg}, config-{cfg} recipe)",
-            "config": {"workload": f"C4: {n_nodes} nodes x {n_pods} pods, "
-                                   f"{'default profile + zone PTS' if cfg == 4 else 'default profile'}, "
+            "config": {"workload": f"C4: {n_nodes} nodes x {n_pods} pods, {RECIPE[cfg]}, "
                                    f"split grid {parts} part(s) x {wl} shards, pct=100",
                        "nodes": n_nodes, "pods": n_pods, "parallelism": f"node-axis split x{parts}"
                        + (" (one GPU)" if world == 1 and parts > 1 else "")},
@@ -664,9 +671,86 @@ def run_postfilter(args):
     ctx.close()
 
 
+def visible_gpus() -> int:
+    """GPUs this process could open, counted without initialising HIP (torch.cuda.device_count
+    does not create a context on this image), so a launcher may still spawn rank processes."""
+    import torch
+    return torch.cuda.device_count()
+
+
+def free_port() -> int:
+    import socket
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def launch_ranks(n: int, argv) -> int:
+    """`bench.py --gpus N` started without torchrun: start N rank processes (torch.distributed.run,
+    one per GPU, 127.0.0.1) from this process, which never touches the GPU, and return their
+    exit code.  Fails clearly when fewer than N GPUs are visible."""
+    vis = visible_gpus()
+    if n > vis:
+        print(f"bench.py: {n} GPUs requested, {vis} visible", file=sys.stderr, flush=True)
+        return 2
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={free_port()}", os.path.abspath(__file__), *argv]
+    return subprocess.call(cmd, cwd=ROOT)
+
+
+def rank_env():
+    """(world, rank, local_rank) from torchrun's environment (1, 0, 0 without it)."""
+    return (int(os.environ.get("WORLD_SIZE", "1")), int(os.environ.get("RANK", "0")),
+            int(os.environ.get("LOCAL_RANK", "0")))
+
+
+def c4_split_leg(args, world: int, rank: int, local: int, dist) -> dict:
+    """The north_star node-axis figure beside the main line: C4 (100,000 nodes x 20,000 pods,
+    default profile + zone PTS) scheduled as ONE split grid over all `world` GPUs (world 1:
+    the unsplit grid on one GPU), strong scaling.  Each rank runs its part in a child process
+    (`bench.py --split 1`, its own gloo group for the IPC handles), so a failing cross-GPU
+    exchange is reported in the line instead of ending the bench.  Rank 0's child also times
+    the CPU restatement on a bounded C4 prefix.  Returns rank 0's result (others: {})."""
+    import torch
+    port = torch.tensor([free_port() if rank == 0 else 0], dtype=torch.int64)
+    if dist:
+        dist.broadcast(port, 0)
+    env = dict(os.environ, WORLD_SIZE=str(world), RANK=str(rank), LOCAL_RANK=str(local),
+               MASTER_ADDR="127.0.0.1", MASTER_PORT=str(int(port.item())))
+    cmd = [sys.executable, os.path.abspath(__file__), "--split", "1", "--split-recipe", "4",
+           "--steps", str(max(args.steps, 3)), "--warmup", str(max(args.warmup, 1)),
+           "--cpu-seconds", str(min(args.cpu_seconds, 8.0))]
+    if args.no_cpu:
+        cmd.append("--no-cpu")
+    t0 = time.perf_counter()
+    try:
+        r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=args.c4_timeout)
+        rc, out, err = r.returncode, r.stdout, r.stderr
+    except subprocess.TimeoutExpired as e:
+        rc, out, err = "timeout", e.stdout or "", e.stderr or ""
+        out = out if isinstance(out, str) else out.decode(errors="replace")
+        err = err if isinstance(err, str) else err.decode(errors="replace")
+    wall = time.perf_counter() - t0
+    res = {}
+    if rank == 0:
+        lines = [ln for ln in out.splitlines() if ln.startswith("{")]
+        if rc == 0 and lines:
+            res = json.loads(lines[-1])
+        else:
+            res = {"error": f"C4 split leg failed (rc {rc})", "stderr_tail": err[-600:]}
+        res["leg_wall_s"] = wall
+    ok = torch.tensor([1 if rc == 0 else 0], dtype=torch.int64)
+    if dist:
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+    if rank == 0 and not ok.item() and "error" not in res:
+        res["error"] = "a peer rank's C4 split child failed"
+    return res
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=0,
+                    help="GPUs (rank processes); without torchrun, N > 1 starts the N ranks itself")
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", type=int, default=2)
@@ -687,9 +771,18 @@ def main():
     ap.add_argument("--per-pod", action="store_true", help="the drop-in per-pod API: kss_eval_pod + kss_commit")
     ap.add_argument("--no-latency", action="store_true", help="skip the stamped latency-profile run")
     ap.add_argument("--postfilter", action="store_true", help="DefaultPreemption PostFilter dry runs (kss_postfilter_pod)")
+    ap.add_argument("--no-c4", action="store_true", help="skip the C4 split-grid leg of the main line")
+    ap.add_argument("--c4-timeout", type=float, default=420.0, help="seconds for the C4 split-grid leg")
     args = ap.parse_args()
     if args.inner:
-        args.no_cpu = args.no_traffic = args.no_latency = True
+        args.no_cpu = args.no_traffic = args.no_latency = args.no_c4 = True
+    world_env = os.environ.get("WORLD_SIZE")
+    if args.gpus > 1 and world_env is None:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    if world_env is not None and args.gpus and int(world_env) != args.gpus:
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world_env}")
+    if world_env is not None and int(os.environ.get("LOCAL_RANK", "0")) >= max(1, visible_gpus()):
+        sys.exit(f"bench.py: LOCAL_RANK {os.environ.get('LOCAL_RANK')} but {visible_gpus()} GPU(s) visible")
     if args.per_pod:
         return run_per_pod(args)
     if args.postfilter:
@@ -701,9 +794,7 @@ def main():
     if args.scenarios:
         return run_scenarios(args)
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    world, rank, local = rank_env()
     dist = None
     if world > 1:
         import torch.distributed as dist  # control plane only (barrier / max of timings)
@@ -758,6 +849,10 @@ def main():
     loop_s = sum(loop_ms[-args.steps:]) / args.steps / 1e3  # the dominant kernel (k_simple / k_schedule) alone
     achieved = B_EVAL[cfg] * n_pods * n_nodes / loop_s / 1e9
 
+    print(json.dumps({"rank": rank, "device": local, "world_size": world, "pods_scheduled": scheduled,
+                      "elapsed_s": t1 - t0}), file=sys.stderr, flush=True)
+    # the node-axis figure (C4 split grid over every rank's GPU) once the main timing is done
+    c4 = None if args.no_c4 or cfg != 2 or args.nodes or args.pods else c4_split_leg(args, world, rank, local, dist)
     if rank == 0:
         cpu = None
         if not args.no_cpu and world == 1:
@@ -782,7 +877,8 @@ def main():
             "vs_baseline": None,
             "dtype": "int64/f64",
             "data": "synthetic (SplitMix64 seed 0x5EED0000+config[+7919*rank])",
-            "config": {"workload": f"C{cfg}: {n_nodes} nodes x {n_pods} pods, default profile, sequential, pct=100",
+            "config": {"workload": f"C{cfg}: {n_nodes} nodes x {n_pods} pods, {RECIPE[cfg]}, sequential, pct=100"
+                                   + (f"; one independent cluster per GPU (seed + rank) x{world}" if world > 1 else ""),
                        "nodes": n_nodes, "pods": n_pods, "parallelism": f"scenario x{world}"},
             "pods_per_s": pods_per_s,
             "pods_scheduled_per_step": scheduled,
@@ -796,6 +892,7 @@ def main():
                          "algorithmic_bytes_per_launch": B_EVAL[cfg] * n_pods * n_nodes,
                          "traffic_detail": traffic_detail, "latency": latency},
             "cpu_baseline": cpu,
+            "c4_split": c4,
         }
         print(json.dumps(out), flush=True)
     ctx.close()

@@ -463,6 +463,10 @@ struct kss_ctx {
   std::vector<BoundOp> bound_log;
   std::vector<BoundPod> staged_bp;
   bool bound_dirty = true;
+  // a committing run failed on the device (exchange timeout): the pods it committed before the
+  // abort stay on the device rows but are not in the bound-pod log; PostFilter refuses until
+  // kss_reset_node_state / kss_load_cluster
+  bool state_unknown = false;
   DevBuf bound_buf, pre_buf;
   DevBound bound_dev{};
   // split grid (kss_split_*): this context runs part split_part of split_n, split_wl shards
@@ -476,6 +480,10 @@ struct kss_ctx {
   bool split_ready = false;
   bool split_broken = false;  // a failed split run: refuse until re-armed (run_single)
   unsigned split_epoch = 0;
+  // loop-kernel launches (chunks) run so far on this part since the last re-arm: chunk q
+  // exchanges through inbox half q & 1, so a fast part starting chunk q + 1 never overwrites
+  // a granule of chunk q that a slower peer has yet to read (every part runs the same chunks)
+  unsigned long long split_chunks = 0;
 };
 
 namespace {
@@ -1296,6 +1304,7 @@ int kss_load_cluster(kss_ctx* ctx, const kss_cluster* cl) {
   ctx->bound0_node.clear();
   ctx->bound_log.clear();
   ctx->bound_dirty = true;
+  ctx->state_unknown = false;
   ctx->recorded = 0;
   ctx->meta_n = 0;
   ctx->axis_meta_dirty = false;
@@ -1441,6 +1450,7 @@ int kss_reset_node_state(kss_ctx* ctx) {
   ctx->cell_bound = ctx->cell_bound0;
   ctx->bound_log.clear();
   ctx->bound_dirty = true;
+  ctx->state_unknown = false;
   for (int i = 0; i < 6; i++)
     if (ctx->mut_bytes[i])
       HIP_TRY(hipMemcpyAsync(dst[i], (char*)ctx->pristine_buf.p + ctx->pristine_off[i], ctx->mut_bytes[i],
@@ -1560,6 +1570,7 @@ static void split_release(kss_ctx* ctx) {
   ctx->split_ready = false;
   ctx->split_broken = false;
   ctx->split_epoch = 0;
+  ctx->split_chunks = 0;
 }
 
 int kss_split_config(kss_ctx* ctx, int32_t n_parts, int32_t part, int32_t shards_per_part) {
@@ -1572,7 +1583,8 @@ int kss_split_config(kss_ctx* ctx, int32_t n_parts, int32_t part, int32_t shards
   split_release(ctx);
   if (n_parts == 1) return 0;  // one part: the whole grid on this device, no inbox
   const size_t W = (size_t)n_parts * (size_t)shards_per_part;
-  const size_t bytes = sizeof(unsigned long long) * 2 * W * (size_t)std::max(2 * XW_MAX, G_XW);
+  // two halves (chunk parity, split_chunks), each double-buffered by epoch parity
+  const size_t bytes = 2 * sizeof(unsigned long long) * 2 * W * (size_t)std::max(2 * XW_MAX, G_XW);
   // uncached: the inbox is polled while other GPUs' stores land in it
   if (hipExtMallocWithFlags(&ctx->split_inbox, bytes, hipDeviceMallocUncached) != hipSuccess) {
     ctx->split_inbox = nullptr;
@@ -1606,6 +1618,20 @@ int kss_split_peers(kss_ctx* ctx, void* const* inboxes) {
     if (!inboxes[i]) return fail(KSS_E_INVAL, "null peer inbox");
   if (inboxes[ctx->split_part] != ctx->split_inbox) return fail(KSS_E_INVAL, "this part's entry must be its own inbox");
   std::lock_guard<std::mutex> lk(ctx->mu);
+  HIP_TRY(hipSetDevice(ctx->cfg.device));
+  // inboxes of parts on other devices of this process: this device stores into them over
+  // xGMI, which needs peer access from this device to theirs
+  for (int i = 0; i < ctx->split_n; i++) {
+    hipPointerAttribute_t a{};
+    if (hipPointerGetAttributes(&a, inboxes[i]) != hipSuccess) return fail(KSS_E_INVAL, "peer inbox is not device memory");
+    if (a.device == ctx->cfg.device) continue;
+    int can = 0;
+    HIP_TRY(hipDeviceCanAccessPeer(&can, ctx->cfg.device, a.device));
+    if (!can) return fail(KSS_E_UNSUPPORTED, "split grid: no peer access between the parts' devices");
+    const hipError_t e = hipDeviceEnablePeerAccess(a.device, 0);
+    if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) return fail(KSS_E_DEVICE, "hipDeviceEnablePeerAccess failed");
+    (void)hipGetLastError();  // clear hipErrorPeerAccessAlreadyEnabled
+  }
   for (int i = 0; i < ctx->split_n; i++) ctx->split_peer[i] = (unsigned long long*)inboxes[i];
   ctx->split_ready = true;
   return 0;
@@ -1830,7 +1856,18 @@ static int static_chunk(size_t sum_nodes, int n_pods) {
 struct SplitRun {
   XPeers X{};
   unsigned epoch0 = 0;
+  unsigned long long chunk0 = 0;  // global chunk sequence number of this run's first chunk
+  size_t half_words = 0;          // inbox half (one chunk's exchange buffer), in 8-byte words
 };
+
+// The exchange buffer and peer inboxes of chunk ci of a split run: half (chunk0 + ci) & 1.
+static void split_chunk_view(const SplitRun& sr, int ci, unsigned long long* gran, unsigned long long*& g_out,
+                             XPeers& x_out) {
+  const size_t off = (size_t)((sr.chunk0 + (unsigned long long)ci) & 1ull) * sr.half_words;
+  x_out = sr.X;
+  for (int i = 0; i < x_out.n; i++) x_out.inbox[i] = sr.X.inbox[i] + off;
+  g_out = gran + off;
+}
 
 static unsigned chunk_span(int pods) { return 8u * (unsigned)std::max(pods, 1) + 16u; }
 
@@ -1867,11 +1904,16 @@ static int launch_simple(hipStream_t st, const Geometry& g, int n_jobs, const De
       hipLaunchKernelGGL(k_static<false>, sgrid, dim3(256), 0, st, jobs, pr, k0, k1, n_lo, n_hi);
     HIP_TRY(hipGetLastError());
     unsigned epoch0 = 0;
-    if (sp_grid) epoch0 = split->epoch0 + (unsigned)(k0 / std::max(chunk, 1)) * chunk_span(chunk);
-    else if (gran && k0 > 0) HIP_TRY(hipMemsetAsync(gran, 0, gran_bytes, st));
+    unsigned long long* gc = gran;
+    if (sp_grid) {
+      epoch0 = split->epoch0 + (unsigned)(k0 / std::max(chunk, 1)) * chunk_span(chunk);
+      split_chunk_view(*split, k0 / std::max(chunk, 1), gran, gc, X);
+    } else if (gran && k0 > 0) {
+      HIP_TRY(hipMemsetAsync(gran, 0, gran_bytes, st));
+    }
     unsigned long long* sp = k0 == 0 ? stamps : nullptr;
     void* args[] = {(void*)&jobs, (void*)&pr, (void*)&W,  (void*)&cap, (void*)&k0, (void*)&k1,
-                    (void*)&gran, (void*)&err, (void*)&sp, (void*)&X,   (void*)&epoch0};
+                    (void*)&gc,   (void*)&err, (void*)&sp, (void*)&X,   (void*)&epoch0};
     const int ci = k0 / chunk;
     if (ev) HIP_TRY(hipEventRecord(ev[2 * ci], st));
     if (g.W > 1) {
@@ -1934,11 +1976,16 @@ static int launch_spread(hipStream_t st, const Geometry& g, const GpodNeeds& q, 
       hipLaunchKernelGGL(k_static<false>, sgrid, dim3(256), 0, st, jobs, pr, k0, k1, n_lo, n_hi);
     HIP_TRY(hipGetLastError());
     unsigned epoch0 = 0;
-    if (sp_grid) epoch0 = split->epoch0 + (unsigned)(k0 / std::max(chunk, 1)) * chunk_span(chunk);
-    else if (gran && k0 > 0) HIP_TRY(hipMemsetAsync(gran, 0, gran_bytes, st));
+    unsigned long long* gc = gran;
+    if (sp_grid) {
+      epoch0 = split->epoch0 + (unsigned)(k0 / std::max(chunk, 1)) * chunk_span(chunk);
+      split_chunk_view(*split, k0 / std::max(chunk, 1), gran, gc, X);
+    } else if (gran && k0 > 0) {
+      HIP_TRY(hipMemsetAsync(gran, 0, gran_bytes, st));
+    }
     unsigned long long* sp = k0 == 0 ? stamps : nullptr;
     void* args[] = {(void*)&jobs, (void*)&W,  (void*)&cap,  (void*)&bins_cap, (void*)&nr, (void*)&gq,
-                    (void*)&k0,   (void*)&k1, (void*)&gran, (void*)&err,      (void*)&sp, (void*)&X,
+                    (void*)&k0,   (void*)&k1, (void*)&gc,   (void*)&err,      (void*)&sp, (void*)&X,
                     (void*)&epoch0};
     const int ci = k0 / chunk;
     if (ev) HIP_TRY(hipEventRecord(ev[2 * ci], st));
@@ -2016,6 +2063,10 @@ static int run_single_impl(kss_ctx* ctx, const PlanNeeds& need, const DevPods& d
   if (flags & KSS_SCHED_FORCE_SINGLE_WG) W = 1;
   if (flags & KSS_SCHED_FORCE_MULTI_WG) W = std::max(W, std::min(4, ctx->n_cu));
   W = std::max(1, std::min(W, std::max(1, (int)N)));
+  // a split grid's shard count is fixed by its parts: never clamp it (a shard past W would
+  // publish into the other epoch parity's granules)
+  if (split && W != ctx->split_n * ctx->split_wl)
+    return fail(KSS_E_UNSUPPORTED, "split grid: more shards than nodes (fewer shards per part)");
   // a k_simple-eligible batch keeps W within k_simple's exchange sweep (64 * SX_CHUNKS
   // shards): at 100k nodes, 98-128 k_simple shards beat 256 k_schedule shards (69.8k
   // against 44.2k pods/s)
@@ -2117,8 +2168,11 @@ static int run_single_impl(kss_ctx* ctx, const PlanNeeds& need, const DevPods& d
   unsigned epoch0 = 0;
   SplitRun srun;
   if (split) {  // the local inbox, never cleared: this run's epochs start above every earlier tag
-    if (gb > ctx->split_inbox_bytes) return fail(KSS_E_INVAL, "split grid: inbox smaller than the exchange buffer");
+    if (2 * gb > ctx->split_inbox_bytes) return fail(KSS_E_INVAL, "split grid: inbox smaller than the exchange buffer");
     gran = (unsigned long long*)ctx->split_inbox;
+    srun.half_words = ctx->split_inbox_bytes / 2 / sizeof(unsigned long long);
+    srun.chunk0 = ctx->split_chunks;
+    ctx->split_chunks += (unsigned long long)((n + chunk - 1) / std::max(chunk, 1));
     srun.X.n = ctx->split_n;
     srun.X.w_off = ctx->split_part * ctx->split_wl;
     srun.X.wl = ctx->split_wl;
@@ -2250,6 +2304,11 @@ static int run_single_impl(kss_ctx* ctx, const PlanNeeds& need, const DevPods& d
   ctx->last_geom[2] = g.npt;
   int errw = 0;
   std::memcpy(&errw, hb, sizeof(int));
+  if (errw && commit) {  // bounds as if every pod committed (upper bounds stay safe); log unknown
+    ctx->count_bound = count_total;
+    ctx->cell_bound = std::max(ctx->cell_bound, cell_total);
+    ctx->state_unknown = true;
+  }
   if (errw) return fail(KSS_E_DEVICE, "shard exchange timed out (workgroups not co-resident?)");
   if (commit) {
     ctx->count_bound = count_total;
@@ -3128,6 +3187,8 @@ int kss_postfilter_pod(kss_ctx* ctx, const kss_podset* ps, int32_t pod_index, ks
   if (!ctx || !ctx->loaded || !ps || !out) return fail(KSS_E_INVAL, "bad arguments");
   if (pod_index < 0 || pod_index >= ps->n_pods) return fail(KSS_E_INVAL, "pod index out of range");
   if (out->victims_cap < 0 || (out->victims_cap > 0 && !out->victims)) return fail(KSS_E_INVAL, "bad victims buffer");
+  if (ctx->state_unknown)
+    return fail(KSS_E_INVAL, "node state after a failed run is unknown: kss_reset_node_state or reload first");
   out->status = KSS_PREEMPT_NO_CANDIDATE;
   out->nominated = -1;
   out->n_potential = out->n_candidates = out->n_victims = 0;

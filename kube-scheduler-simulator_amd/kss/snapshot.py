@@ -145,8 +145,41 @@ def _resource_id(name: str, scalars: Sequence[str]) -> int:
     raise Unsupported(f"scoring resource {name!r} is not a column of the compiled cluster")
 
 
+def store_weights_from_config(cfg: Optional[dict]) -> Dict[str, int]:
+    """The weights the simulator's result store applies to finalscore annotations
+    (getScorePluginWeight, plugins.go:288-303, over the configuration ConvertForSimulator
+    produced, plugins.go:173-195): the profile's Score.Enabled entries, then the MultiPoint set
+    merged with the in-tree defaults, each assignment overwriting the previous one -- so a
+    plugin listed in both takes its MultiPoint weight -- and 0 -> 1.
+
+    These can differ from the weights the framework schedules with (``profile_from_config``:
+    a plugin configured at the Score extension point keeps that weight over its MultiPoint
+    one): the simulator then records finalscores that are not the ones it selected the node
+    by.  The device schedules with the framework's weights; the formatter takes these."""
+    plugins = (((cfg or {}).get("profiles") or [{}])[0].get("plugins")) or {}
+    multi = merge_plugin_set(DEFAULT_MULTIPOINT, plugins.get("multiPoint"))
+    user_score = [(p.get("name"), int(p.get("weight") or 0)) for p in (plugins.get("score") or {}).get("enabled") or []]
+    out: Dict[str, int] = {}
+    for n, w in user_score + multi:
+        out[n] = w if w != 0 else 1
+    return out
+
+
+def store_profile_from_config(cfg: Optional[dict], scalars: Sequence[str] = ()) -> abi.Profile:
+    """``profile_from_config`` with the result store's weights (``store_weights_from_config``):
+    the profile to format annotations with (kss_format_*_ex)."""
+    prof = profile_from_config(cfg, scalars)
+    w = store_weights_from_config(cfg)
+    for s, n in enumerate(abi.SCORE_PLUGINS):
+        if prof.score_enabled & (1 << s):
+            prof.weight[s] = w.get(n, prof.weight[s])
+    return prof
+
+
 def profile_from_config(cfg: Optional[dict], scalars: Sequence[str] = ()) -> abi.Profile:
-    """kss_profile of a KubeSchedulerConfiguration's (first) profile; None -> the default."""
+    """kss_profile of a KubeSchedulerConfiguration's (first) profile; None -> the default.
+    Weights follow the framework (the Score extension point's entry wins over MultiPoint's);
+    the result store's annotation weights are ``store_weights_from_config``."""
     prof = abi.default_profile()
     if not cfg:
         return prof

@@ -33,7 +33,10 @@ def shards_per_part(n_nodes: int, n_parts: int, nodes_per_shard: int = 391, cap:
     """Shards per part so that the whole grid keeps about `nodes_per_shard` nodes per shard
     (the 1-GPU C4 geometry: 100k nodes over 256 shards), at most `cap` per part."""
     total = max(n_parts, -(-max(n_nodes, 1) // nodes_per_shard))
-    return max(1, min(cap, -(-total // n_parts)))
+    wl = max(1, min(cap, -(-total // n_parts)))
+    # every shard owns at least one node: the grid's n_parts * wl shards never exceed the
+    # cluster (the library refuses a split grid it would have to clamp)
+    return max(1, min(wl, max(n_nodes, 1) // n_parts))
 
 
 def part_rows(n_nodes: int, n_parts: int, wl: int, part: int) -> Tuple[int, int]:
@@ -64,6 +67,20 @@ def _run_concurrently(fns):
     return out
 
 
+def _check_co_resident(devices: Sequence[int], wl: int):
+    """Every part's grid must be resident at once (the shards poll each other): the parts
+    sharing one device need at most one shard per CU between them (a k_spread / k_simple
+    shard fills a CU's LDS)."""
+    import collections
+
+    import torch
+    for dev, k in collections.Counter(devices).items():
+        cus = torch.cuda.get_device_properties(dev).multi_processor_count
+        if k * wl > cus:
+            raise ValueError(f"{k} parts x {wl} shards on device {dev} exceed its {cus} CUs: "
+                             "the grids could not all be resident")
+
+
 class InProcessSplit:
     """n_parts contexts in this process, each running its part of one grid."""
 
@@ -73,6 +90,9 @@ class InProcessSplit:
         gc.collect()  # contexts no longer referenced release their streams (HIP maps streams onto few HW queues)
         self.n_parts, self.wl, self.n_nodes = n_parts, wl, cluster.n_nodes
         devices = list(devices) if devices is not None else [0] * n_parts
+        if len(devices) != n_parts:
+            raise ValueError("one device per part")
+        _check_co_resident(devices, wl)
         self.ctxs = []
         for p in range(n_parts):
             ctx = native.Context(profile, device=devices[p])

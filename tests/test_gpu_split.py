@@ -55,6 +55,66 @@ def test_in_process_parts_match_oracle(config, n_nodes, n_pods, n_parts, wl, ker
     sp.close()
 
 
+@pytest.mark.parametrize("config,n_nodes,n_pods,per_chunk,wl", [
+    (2, 3000, 240, 30, 8),   # k_simple: even chunks (the last and first epochs of adjacent chunks share a parity)
+    (2, 3000, 240, 31, 8),
+    (4, 6000, 200, 24, 16),  # k_spread: the exchange count per pod is data-dependent
+])
+def test_parts_over_many_chunks(monkeypatch, config, n_nodes, n_pods, per_chunk, wl):
+    """KSS_STATIC_BYTES forces one k_static + one loop launch per `per_chunk` pods: adjacent
+    chunks exchange through the two inbox halves, so a part that starts chunk c + 1 never
+    overwrites a granule of chunk c that its peer is still polling.  Three runs back to back
+    (the chunk sequence continues across runs)."""
+    monkeypatch.setenv("KSS_STATIC_BYTES", str(4 * n_nodes * per_chunk))
+    s = native.Synth(config, SEED_BASE + config, n_nodes, n_pods)
+    ch_o, _, st = _oracle(s, n_pods)
+    sp = split.InProcessSplit(s.cluster, s.pods, 2, wl)
+    for rep in range(3):
+        sp.reset()
+        for p, ch in enumerate(sp.run(n_pods)):
+            np.testing.assert_array_equal(ch, ch_o, err_msg=f"part {p} run {rep}")
+        assert sp.ctxs[0].last_timing()[1] == 2 * -(-n_pods // per_chunk)  # k_static + loop per chunk
+    g = sp.node_state()
+    np.testing.assert_array_equal(g["requested"][:, :n_nodes], st["requested"][:, :n_nodes])
+    sp.close()
+
+
+def test_shards_per_part_never_exceed_nodes():
+    assert split.shards_per_part(1, 2) == 1 and split.shards_per_part(3, 2) == 1
+    assert split.shards_per_part(100000, 8) == 32
+    s = native.Synth(2, SEED_BASE + 2, 6, 4)
+    ctx = native.Context(abi.default_profile())
+    ctx.load(s.cluster)
+    ctx.stage(s.pods)
+    ctx.split_config(2, 0, 4)  # 8 shards over 6 nodes
+    ctx.split_peers([ctx.split_inbox()[0]] * 2)
+    with pytest.raises(native.KssError, match="more shards than nodes"):
+        ctx.run_staged(4)
+    ctx.close()
+
+
+def _n_devices():
+    import torch
+    return torch.cuda.device_count()
+
+
+@pytest.mark.skipif(_n_devices() < 2, reason="needs 2 GPUs (the xGMI peer stores of a split grid)")
+@pytest.mark.parametrize("config,n_nodes,n_pods,wl", [(2, 5000, 400, 8), (4, 100000, 200, 128)])
+def test_two_devices_in_process(config, n_nodes, n_pods, wl):
+    """The split grid's deployment shape: parts on different GPUs, every granule stored into
+    the peer's inbox over xGMI."""
+    s = native.Synth(config, SEED_BASE + config, n_nodes, n_pods)
+    ch_o, _, st = _oracle(s, n_pods)
+    sp = split.InProcessSplit(s.cluster, s.pods, 2, wl, devices=[0, 1])
+    for rep in range(2):
+        sp.reset()
+        for p, ch in enumerate(sp.run(n_pods)):
+            np.testing.assert_array_equal(ch, ch_o, err_msg=f"part {p} run {rep}")
+    g = sp.node_state()
+    np.testing.assert_array_equal(g["requested"][:, :n_nodes], st["requested"][:, :n_nodes])
+    sp.close()
+
+
 def test_split_refuses_what_it_cannot_run():
     s = native.Synth(2, SEED_BASE + 2, 500, 50)
     ctx = native.Context(abi.default_profile())
@@ -88,14 +148,16 @@ def test_failed_run_refuses_until_rearmed():
     sp.close()
 
 
-def _rank_main(rank, world, port, config, n_nodes, n_pods, wl, q):
+def _rank_main(rank, world, port, config, n_nodes, n_pods, wl, q, device_of=None):
     import torch
     import torch.distributed as dist
     try:
+        dev = device_of(rank) if device_of else 0
+        torch.cuda.set_device(dev)
         torch.zeros(1, device="cuda")  # torch's HIP runtime before libkss's
         dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
         s = native.Synth(config, SEED_BASE + config, n_nodes, n_pods)
-        r = split.SplitRank(s.cluster, s.pods, wl, device=0)
+        r = split.SplitRank(s.cluster, s.pods, wl, device=dev)
         chosen = r.run(n_pods)
         lo, hi = r.rows()
         st = r.ctx.node_state()
@@ -107,10 +169,16 @@ def _rank_main(rank, world, port, config, n_nodes, n_pods, wl, q):
         q.put((rank, repr(e), 0, 0, None, None))
 
 
-def test_two_processes_through_ipc_handles():
+def _identity(r):
+    return r
+
+
+@pytest.mark.parametrize("two_gpus", [False, pytest.param(True, marks=pytest.mark.skipif(
+    _n_devices() < 2, reason="needs 2 GPUs"))])
+def test_two_processes_through_ipc_handles(two_gpus):
     """One part per process (the deployment shape: one process per GPU), inboxes mapped
     through hipIpcOpenMemHandle, the handles exchanged over gloo; both processes' grids on
-    the box's one GPU at once."""
+    the box's one GPU at once, or (two_gpus) rank r on GPU r, peer stores over xGMI."""
     import multiprocessing as mp
     import socket
     config, n_nodes, n_pods, wl = 4, 20000, 300, 32
@@ -121,7 +189,8 @@ def test_two_processes_through_ipc_handles():
         port = so.getsockname()[1]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    ps = [ctx.Process(target=_rank_main, args=(r, 2, port, config, n_nodes, n_pods, wl, q)) for r in range(2)]
+    ps = [ctx.Process(target=_rank_main, args=(r, 2, port, config, n_nodes, n_pods, wl, q,
+                                               _identity if two_gpus else None)) for r in range(2)]
     for p in ps:
         p.start()
     got = [q.get(timeout=240) for _ in ps]

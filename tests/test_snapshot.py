@@ -66,6 +66,25 @@ def test_config_weights_disables_and_args():
     assert p.hard_pod_affinity_weight == 4 and p.system_defaulted == 0
 
 
+def test_conflicting_weights_framework_vs_store():
+    """A plugin weighted differently at Score and MultiPoint: the framework schedules with the
+    Score entry's weight; the simulator's store (getScorePluginWeight, plugins.go:288-303:
+    Score.Enabled, then the merged MultiPoint, last assignment wins) records finalscores with
+    the MultiPoint weight -- an in-tree default when the user's MultiPoint does not list it."""
+    cfg = {"profiles": [{"plugins": {
+        "score": {"enabled": [{"name": "TaintToleration", "weight": 10}, {"name": "NodeAffinity", "weight": 9}]},
+        "multiPoint": {"enabled": [{"name": "NodeAffinity", "weight": 4}]}}}]}
+    p = snapshot.profile_from_config(cfg)
+    assert p.weight[abi.KSS_S_TAINT_TOLERATION] == 10 and p.weight[abi.KSS_S_NODE_AFFINITY] == 9
+    w = snapshot.store_weights_from_config(cfg)
+    assert w["TaintToleration"] == 3 and w["NodeAffinity"] == 4 and w["ImageLocality"] == 1
+    ps = snapshot.store_profile_from_config(cfg)
+    assert ps.weight[abi.KSS_S_TAINT_TOLERATION] == 3 and ps.weight[abi.KSS_S_NODE_AFFINITY] == 4
+    assert ps.weight[abi.KSS_S_NODE_RESOURCES_FIT] == 1 and ps.score_enabled == p.score_enabled
+    # no conflict: the two agree
+    assert snapshot.store_weights_from_config(None)["TaintToleration"] == 3
+
+
 def test_config_star_disable_and_refusals():
     cfg = {"profiles": [{"plugins": {"multiPoint": {"disabled": [{"name": "*"}],
                                                     "enabled": [{"name": "NodeResourcesFit"},
