@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define KSS_ABI_VERSION 2
+#define KSS_ABI_VERSION 3
 
 /* ---- error codes ------------------------------------------------------- */
 #define KSS_OK 0
@@ -96,6 +96,11 @@ enum kss_filter_plugin {
 #define KSS_IPA_AFFINITY 0
 #define KSS_IPA_ANTI_AFFINITY 1
 #define KSS_IPA_EXISTING_ANTI_AFFINITY 2
+/* VolumeRestrictions: "node(s) had no available disk"; EBSLimits / GCEPDLimits /
+ * NodeVolumeLimits / AzureDiskLimits: "node(s) exceed max volume count" (detail 0) */
+#define KSS_VB_NODE_CONFLICT 0 /* VolumeBinding: "node(s) had volume node affinity conflict" */
+#define KSS_VB_PV_NOT_EXIST 1  /* "node(s) unavailable due to one or more pvc(s) bound to non-existent pv(s)" */
+/* VolumeZone: detail 0 = "node(s) had no available volume zone", 1 + i = kss_names.messages[i] */
 
 /* ---- score plugins, in default MultiPoint order ------------------------- */
 enum kss_score_plugin {
@@ -113,6 +118,8 @@ enum kss_score_plugin {
 /* ---- node flags --------------------------------------------------------- */
 #define KSS_NODE_UNSCHEDULABLE (1u << 0) /* node.Spec.Unschedulable */
 #define KSS_NODE_HAS_LABELS (1u << 1)    /* len(node.Labels) > 0 (IPA processExistingPod) */
+#define KSS_NODE_VOLUME_ZONE (1u << 2)   /* the node carries a VolumeZone label (topology.kubernetes.io /
+                                            failure-domain.beta.kubernetes.io zone or region) */
 
 /* ---- label-key flags ---------------------------------------------------- */
 #define KSS_KEY_UNIQUE (1u << 0)   /* no two nodes share a value: domain == node */
@@ -173,6 +180,21 @@ typedef struct kss_cluster {
   const uint64_t* port_used;   /* [n_nodes] */
   const int64_t* image_score;  /* [n_images][n_nodes] scaledImageScore(NodeInfo.ImageStates[name], totalNumNodes),
                                   0 where the node does not list the image */
+  /* Volumes (VolumeRestrictions, the attach-limit plugins, VolumeBinding, VolumeZone).
+   * A volume row is a volume (by the limit plugins' unique name) or a disk usage (kind,
+   * identity, readOnly: VolumeRestrictions) that some pending pod's filter needs to find on a
+   * node: vol_count = how many of the node's pods use it.  A key is an attach-limit resource
+   * (attachable-volumes-aws-ebs / -gce-pd / -azure-disk, or a CSI driver's
+   * attachable-volumes-csi-<driver>) of one limit plugin: vol_attached = the distinct
+   * volumes of that key the node's pods use, vol_limit = the node's limit (-1: the plugin
+   * does not check the key on this node).  n_vol_rows == n_vol_keys == 0: no volumes. */
+  int32_t n_vol_rows;
+  int32_t n_vol_keys;
+  const int32_t* vol_count;      /* [n_vol_rows][n_nodes] (mutable: AssumePod adds) */
+  const int32_t* vol_attached;   /* [n_vol_keys][n_nodes] (mutable) */
+  const int32_t* vol_limit;      /* [n_vol_keys][n_nodes] */
+  const int32_t* vol_row_key;    /* [n_vol_rows] key the row's volume counts under, -1 (disk usage rows) */
+  const int32_t* vol_key_plugin; /* [n_vol_keys] KSS_F_EBS_LIMITS / _GCEPD_ / _NODE_VOLUME_ / _AZURE_DISK_LIMITS */
 } kss_cluster;
 
 /* ---- pod programs --------------------------------------------------------
@@ -242,6 +264,38 @@ typedef struct kss_ipa {
   int32_t pad;
 } kss_ipa;
 
+/* volume program entries, in filter order (kss_pod.vol_off / vol_len): VolumeRestrictions,
+ * then the limit plugins (grouped by key, keys in plugin order), VolumeBinding, VolumeZone, and
+ * last the AssumePod entries */
+enum kss_vol_kind {
+  KSS_VOL_CONFLICT = 0,       /* VolumeRestrictions fails where vol_count[row][n] > 0 (isVolumeConflict) */
+  KSS_VOL_LIMIT = 1,          /* a new volume under `key`: row >= 0 a shared volume, new where vol_count[row][n] == 0;
+                                 row < 0: `count` volumes no other pod uses.  Per key: fail where vol_limit >= 0 and
+                                 vol_attached + new > vol_limit (NodeVolumeLimits: only when new > 0) */
+  KSS_VOL_BIND_AFFINITY = 2,  /* VolumeBinding bound claim: its PV's required node affinity, terms [a, a + b) (OR) */
+  KSS_VOL_BIND_PV_MISSING = 3,/* VolumeBinding bound claim whose PV does not exist */
+  KSS_VOL_ZONE = 4,           /* VolumeZone on zone-labelled nodes: requirements [a, a + b) (AND) */
+  KSS_VOL_ZONE_ERROR = 5,     /* VolumeZone on zone-labelled nodes: the status message kss_names.messages[a] */
+  KSS_VOL_OWN = 6,            /* AssumePod: vol_count[row][n] += 1 (0 -> 1 also adds 1 to the row's key) */
+  KSS_VOL_OWN_PRIVATE = 7     /* AssumePod: vol_attached[key][n] += count */
+};
+typedef struct kss_vol {
+  int32_t kind;
+  int32_t key;
+  int32_t row;
+  int32_t count;
+  int32_t a;
+  int32_t b;
+} kss_vol;
+#define KSS_MAX_VOL_KEYS 64
+
+/* kss_pod.prefilter_status */
+#define KSS_PF_OK 0
+#define KSS_PF_NODE_AFFINITY_CONFLICT 1 /* NodeAffinity PreFilter: "pod affinity terms conflict" */
+#define KSS_PF_ERROR 2                  /* a PreFilter Error (pod-level) */
+#define KSS_PF_VOLUME_BINDING 3         /* VolumeBinding PreFilter UnschedulableAndUnresolvable:
+                                           kss_names.messages[prefilter_msg] */
+
 /* pod flags */
 #define KSS_POD_TOL_UNSCHEDULABLE (1u << 0)  /* tolerates node.kubernetes.io/unschedulable:NoSchedule */
 #define KSS_POD_HAS_REQ_AFFINITY (1u << 1)   /* RequiredDuringScheduling node affinity present */
@@ -270,11 +324,10 @@ typedef struct kss_pod {
   int32_t ipa_off, ipa_len;        /* pool ipa entries */
   int32_t cls;                     /* the pod's own class (class_count row it joins on commit), -1 none */
   int32_t own_terms_off, own_terms_len; /* term-type rows this pod adds on commit: ints[] */
-  int32_t prefilter_status;        /* 0 ok, 1 NodeAffinity "pod affinity terms conflict",
-                                      2 pod-level Error (parse error)                      */
+  int32_t prefilter_status;        /* KSS_PF_* */
   int32_t names_off, names_len;    /* NodeAffinity PreFilterResult node set (ints[], global idx); len<0: all nodes */
   int32_t priority;                /* corev1helpers.PodPriority: spec.priority, 0 when unset (DefaultPreemption) */
-  int32_t pad;
+  int32_t prefilter_msg;           /* KSS_PF_VOLUME_BINDING: index into kss_names.messages */
   /* NodePorts (nodeports.go): port_conflict = dictionary entries any wanted container host
    * port conflicts with (HostPortInfo.CheckConflict: same protocol and port, and either IP is
    * 0.0.0.0 or both are equal); port_add = the pod's own entries (NodeInfo.AddPod
@@ -286,6 +339,7 @@ typedef struct kss_pod {
    * len(pod.Spec.Containers) for calculatePriority's maxThreshold. */
   int32_t img_off, img_len;
   int32_t n_containers;
+  int32_t vol_off, vol_len;        /* volume program: pool vols (kss_vol), 0 entries for volume-less pods */
   int32_t pad2;
 } kss_pod;
 
@@ -298,6 +352,9 @@ typedef struct kss_podset {
   const kss_spread* spreads;
   const kss_ipa* ipa;
   const int32_t* ints;
+  int32_t n_vols;
+  int32_t pad;
+  const kss_vol* vols;
 } kss_podset;
 
 /* ---- profile (KubeSchedulerConfiguration profile subset) --------------- */
@@ -366,6 +423,15 @@ int kss_apply_node_delta(kss_ctx* ctx, const int32_t* idx, int32_t n, const int6
  * (simulator/scheduler/scheduler.go:66-104 starts the scheduler that keeps it). */
 int kss_apply_count_delta(kss_ctx* ctx, const int32_t* node, const int32_t* row, const int32_t* value, int32_t n,
                           int32_t mode);
+/* Volume state (vol_count rows, then vol_attached keys as rows n_vol_rows + k): read back, or
+ * the delta sync of pods with volumes bound or deleted outside this context:
+ * row[i] < n_vol_rows: vol_count[row][node] += value (mode 0) or = value (mode 1); otherwise
+ * vol_attached[row - n_vol_rows][node].  Replaces the informer's NodeInfo.AddPod / RemovePod
+ * (the volume plugins re-read NodeInfo.Pods' volumes on every Filter call). */
+int kss_read_volume_state(kss_ctx* ctx, int32_t* vol_count /*[n_vol_rows][N] or NULL*/,
+                          int32_t* vol_attached /*[n_vol_keys][N] or NULL*/);
+int kss_apply_volume_delta(kss_ctx* ctx, const int32_t* node, const int32_t* row, const int32_t* value, int32_t n,
+                           int32_t mode);
 /* read back the mutable columns (requested [KSS_NRES][N], nonzero [2][N], pod_count [N]) */
 int kss_read_node_state(kss_ctx* ctx, int64_t* requested, int64_t* nonzero, int32_t* pod_count,
                         int32_t* class_count /*[n_classes][N] or NULL*/, int32_t* term_count /*or NULL*/);
@@ -582,6 +648,9 @@ typedef struct kss_names {
   const char* const* taint_keys;    /* [n_taints] */
   const char* const* taint_values;  /* [n_taints] */
   const char* const* scalar_names;  /* [n_scalar] */
+  int32_t n_messages;               /* per-pod status messages (VolumeBinding PreFilter, VolumeZone errors) */
+  int32_t pad;
+  const char* const* messages;      /* [n_messages] */
 } kss_names;
 int kss_set_names(kss_ctx* ctx, const kss_names* names);
 /* Format the 13 annotation values of one recorded pod result as

@@ -144,7 +144,7 @@ __device__ __forceinline__ void axis_record(const DevPods& P, int pi, long long 
     m.chosen = g;
     m.n_feasible = (int32_t)nf;
     m.scored = (K && nf > 1) ? 1 : 0;
-    m.status = p.prefilter_status != 0 ? (p.prefilter_status == 1 ? 2 : 3) : (nf == 0 ? 1 : 0);
+    m.status = p.prefilter_status != 0 ? (p.prefilter_status == KSS_PF_ERROR ? 3 : 2) : (nf == 0 ? 1 : 0);
     m.best_total = m.scored ? (int64_t)((unsigned long long)K >> 32) : 0;
     meta[pi] = m;
   }

@@ -62,6 +62,14 @@ struct DevCluster {
   uint64_t* port_used;        // [N] NodeInfo.UsedPorts dictionary bits (mutable: AssumePod adds)
   const int64_t* image_score; // [n_images][N] scaledImageScore, 0 = image absent
   int32_t n_images;
+  // volumes (include/kss.h kss_cluster): vol_count [rows][N] and vol_attached [keys][N] are
+  // mutable (AssumePod adds), vol_limit [keys][N] static
+  int32_t n_vol_rows, n_vol_keys;
+  int32_t* vol_count;
+  int32_t* vol_attached;
+  const int32_t* vol_limit;
+  const int32_t* vol_row_key;
+  const int32_t* vol_key_plugin;
   // Shard-resident LDS copies of the hot node columns (set inside the kernel; null on
   // the host and in kernels without a cache).  Slot i holds node nc_lo + i.
   int64_t* nc64;    // [8][nc_cap]: alloc cpu/mem/eph, requested cpu/mem/eph, nonzero cpu/mem
@@ -149,6 +157,7 @@ struct DevPods {
   const kss_spread* spreads;
   const kss_ipa* ipa;
   const int32_t* ints;
+  const kss_vol* vols;
 };
 
 __device__ __forceinline__ int32_t label_of(const DevCluster& c, int key, int n) {
@@ -319,6 +328,120 @@ __device__ __forceinline__ int filter_local(const DevCluster& c, const DevPods& 
     }
   }
   return 0;
+}
+
+// The volume filters (VolumeRestrictions, EBSLimits, GCEPDLimits, NodeVolumeLimits,
+// AzureDiskLimits, VolumeBinding, VolumeZone: default MultiPoint order) over the pod's volume
+// program, whose entries the host sorted into that order (kss/volumes.py).  Returns the first
+// failing plugin (detail in *detail) or 0.  Restates, per node:
+//   volume_restrictions.go satisfyVolumeConflicts: a pod volume conflicts with a volume of a
+//     pod on the node (the host resolved isVolumeConflict into the rows each entry names);
+//   non_csi.go nonCSILimits.Filter / csi.go CSILimits.Filter: per limit key, the pod's volumes
+//     not already attached on the node (newVolumes minus attachedVolumes) on top of the
+//     node's distinct attached ones against the node's limit (CSI: only keys with a new volume);
+//   binder.go checkBoundClaims: the bound claims in order; a missing PV or a PV whose node
+//     affinity does not match the node's labels ends the walk;
+//   volume_zone.go Filter: on nodes carrying a zone label, every zone label of the pod's PVs
+//     must name the node's value, volumes in order (per-volume errors as messages).
+// One attach-limit key of the pod on node n: its plugin when the node's limit is exceeded.
+// nonCSILimits counts existing + new volumes whenever the pod has a volume of the plugin;
+// CSILimits checks only keys with a new volume.
+__device__ __forceinline__ int limit_exceeded(const DevCluster& c, int key, int n, int64_t newc, uint32_t enabled) {
+  const size_t N = (size_t)c.N;
+  const int pl = c.vol_key_plugin[key];
+  const int32_t lim = c.vol_limit[(size_t)key * N + n];
+  if (!((enabled >> pl) & 1u) || lim < 0) return 0;
+  if (pl == KSS_F_NODE_VOLUME_LIMITS && newc == 0) return 0;
+  return (int64_t)c.vol_attached[(size_t)key * N + n] + newc > (int64_t)lim ? pl : 0;
+}
+
+template <class Lab>
+__device__ __forceinline__ int filter_volumes_t(const DevCluster& c, const kss_req* reqs, const kss_term* terms,
+                                                const int32_t* ints, const kss_vol* vols, const kss_pod& p,
+                                                uint32_t enabled, int n, uint32_t node_flags, uint16_t* detail,
+                                                Lab lab) {
+  const size_t N = (size_t)c.N;
+  int cur = -1;      // the limit key of the open segment
+  int64_t newc = 0;  // its new volumes on this node
+  for (int e = 0; e < p.vol_len; e++) {
+    const kss_vol v = vols[p.vol_off + e];
+    if (v.kind != KSS_VOL_LIMIT && cur >= 0) {  // the open segment ends: check it
+      if (const int pl = limit_exceeded(c, cur, n, newc, enabled)) return pl;
+      cur = -1;
+    }
+    switch (v.kind) {
+      case KSS_VOL_CONFLICT:
+        if (((enabled >> KSS_F_VOLUME_RESTRICTIONS) & 1u) && c.vol_count[(size_t)v.row * N + n] > 0)
+          return KSS_F_VOLUME_RESTRICTIONS;
+        break;
+      case KSS_VOL_LIMIT:
+        if (v.key != cur) {
+          if (cur >= 0)  // the previous key's segment ends
+            if (const int pl = limit_exceeded(c, cur, n, newc, enabled)) return pl;
+          cur = v.key;
+          newc = 0;
+        }
+        newc += v.row >= 0 ? (c.vol_count[(size_t)v.row * N + n] == 0 ? 1 : 0) : v.count;
+        break;
+      case KSS_VOL_BIND_AFFINITY:
+        if ((enabled >> KSS_F_VOLUME_BINDING) & 1u) {
+          bool ok = false;
+          for (int t = 0; t < v.b && !ok; t++) ok = term_match_t(c, reqs, ints, terms[v.a + t], -1, lab);
+          if (!ok) {
+            *detail = KSS_VB_NODE_CONFLICT;
+            return KSS_F_VOLUME_BINDING;
+          }
+        }
+        break;
+      case KSS_VOL_BIND_PV_MISSING:
+        if ((enabled >> KSS_F_VOLUME_BINDING) & 1u) {
+          *detail = KSS_VB_PV_NOT_EXIST;
+          return KSS_F_VOLUME_BINDING;
+        }
+        break;
+      case KSS_VOL_ZONE:
+        if (((enabled >> KSS_F_VOLUME_ZONE) & 1u) && (node_flags & KSS_NODE_VOLUME_ZONE)) {
+          for (int k = 0; k < v.b; k++)
+            if (!req_match_t(c, ints, reqs[v.a + k], -1, lab)) {
+              *detail = 0;
+              return KSS_F_VOLUME_ZONE;
+            }
+        }
+        break;
+      case KSS_VOL_ZONE_ERROR:
+        if (((enabled >> KSS_F_VOLUME_ZONE) & 1u) && (node_flags & KSS_NODE_VOLUME_ZONE)) {
+          *detail = (uint16_t)(1 + v.a);
+          return KSS_F_VOLUME_ZONE;
+        }
+        break;
+      default:  // AssumePod entries close the program
+        return 0;
+    }
+  }
+  if (cur >= 0) return limit_exceeded(c, cur, n, newc, enabled);
+  return 0;
+}
+
+__device__ __forceinline__ int filter_volumes(const DevCluster& c, const DevPods& P, const kss_pod& p, uint32_t enabled,
+                                              int n, uint16_t* detail) {
+  if (p.vol_len <= 0) return 0;
+  return filter_volumes_t(c, P.reqs, P.terms, P.ints, P.vols, p, enabled, n, node_flags_of(c, n), detail,
+                          [&](int key) { return label_of(c, key, n); });
+}
+
+// AssumePod (sign 1) / ForgetPod (-1) of one KSS_VOL_OWN row on node `local`: the row's pod
+// count moves, and the row's key counts the volume once while some pod on the node uses it.
+__device__ __forceinline__ void vol_commit_row(const DevCluster& c, int row, int local, int sign) {
+  const size_t N = (size_t)c.N;
+  int32_t* cnt = c.vol_count + (size_t)row * N + local;
+  const int key = c.vol_row_key[row];
+  if (sign > 0) {
+    if (key >= 0 && *cnt == 0) c.vol_attached[(size_t)key * N + local] += 1;
+    *cnt += 1;
+  } else {
+    *cnt -= 1;
+    if (key >= 0 && *cnt == 0) c.vol_attached[(size_t)key * N + local] -= 1;
+  }
 }
 
 // Go int64 division a / b for the non-negative operands the scores produce: one f64

@@ -76,6 +76,7 @@ int kss_host_set_names(kss_host_names* dst, const kss_names* src, int n_nodes, i
   dst->taint_key.clear();
   dst->taint_value.clear();
   dst->scalar.clear();
+  dst->message.clear();
   if (src->node_names)
     for (int i = 0; i < n_nodes; i++) dst->node.emplace_back(src->node_names[i] ? src->node_names[i] : "");
   for (int i = 0; i < n_taints; i++) {
@@ -83,6 +84,7 @@ int kss_host_set_names(kss_host_names* dst, const kss_names* src, int n_nodes, i
     dst->taint_value.emplace_back(src->taint_values && src->taint_values[i] ? src->taint_values[i] : "");
   }
   for (int i = 0; i < n_scalar; i++) dst->scalar.emplace_back(src->scalar_names && src->scalar_names[i] ? src->scalar_names[i] : "");
+  for (int i = 0; i < src->n_messages; i++) dst->message.emplace_back(src->messages && src->messages[i] ? src->messages[i] : "");
   return 0;
 }
 
@@ -172,6 +174,22 @@ std::string fail_message(const kss_host_names* nm, int plugin, unsigned detail) 
       for (size_t i = 0; i < r.size(); i++) o += (i ? ", " : "") + r[i];
       return o;
     }
+    // volume plugins (v1.26 reason strings: volume_restrictions.go ErrReasonDiskConflict,
+    // nodevolumelimits ErrReasonMaxVolumeCountExceeded, volumebinding ErrReasonNodeConflict /
+    // ErrReasonPVNotExist, volume_zone.go ErrReasonConflict)
+    case KSS_F_VOLUME_RESTRICTIONS:
+      return "node(s) had no available disk";
+    case KSS_F_EBS_LIMITS:
+    case KSS_F_GCEPD_LIMITS:
+    case KSS_F_NODE_VOLUME_LIMITS:
+    case KSS_F_AZURE_DISK_LIMITS:
+      return "node(s) exceed max volume count";
+    case KSS_F_VOLUME_BINDING:
+      return detail == KSS_VB_PV_NOT_EXIST ? "node(s) unavailable due to one or more pvc(s) bound to non-existent pv(s)"
+                                           : "node(s) had volume node affinity conflict";
+    case KSS_F_VOLUME_ZONE:
+      if (detail == 0) return "node(s) had no available volume zone";
+      return detail - 1 < nm->message.size() ? nm->message[detail - 1] : std::string();
     case KSS_F_POD_TOPOLOGY_SPREAD:
       return detail == KSS_PTS_MISSING_LABEL ? "node(s) didn't match pod topology spread constraints (missing required label)"
                                              : "node(s) didn't match pod topology spread constraints";
@@ -203,17 +221,20 @@ int kss_host_prefilter_nodes(const kss_podset* ps, int32_t i, int n_nodes, std::
 }
 
 int kss_host_format(const kss_host_names* nm, const kss_profile* prof, const kss_pod_result* res, int n_nodes, char* buf,
-                    size_t cap, size_t* need, const std::vector<int>* prefilter_nodes) {
+                    size_t cap, size_t* need, const std::vector<int>* prefilter_nodes, const kss_pod* pod) {
   if ((int)nm->node.size() < n_nodes) return KSS_E_INVAL;
   std::vector<int> order(n_nodes);
   std::iota(order.begin(), order.end(), 0);
   std::sort(order.begin(), order.end(), [&](int a, int b) { return nm->node[a] < nm->node[b]; });
   const bool scheduled = res->chosen >= 0;
   const bool prefilter_fail = res->status == 2 || res->status == 3;
+  // a VolumeBinding PreFilter rejection (the pod's program says which PreFilter failed)
+  const bool vb_reject = res->status == 2 && pod && pod->prefilter_status == KSS_PF_VOLUME_BINDING;
   std::vector<KV> out;
   // prefilter
-  // store.go:522-534: PreFilterResult.NodeNames.List() (sorted) under the plugin's name; none on a conflict
-  if (prefilter_nodes && res->status != 2) {
+  // store.go:522-534: PreFilterResult.NodeNames.List() (sorted) under the plugin's name; none on a
+  // NodeAffinity conflict (a later PreFilter's rejection keeps NodeAffinity's recorded result)
+  if (prefilter_nodes && (res->status != 2 || vb_reject)) {
     std::vector<std::string> names;
     for (int n : *prefilter_nodes)
       if (n >= 0 && n < n_nodes) names.push_back(nm->node[n]);
@@ -229,7 +250,13 @@ int kss_host_format(const kss_host_names* nm, const kss_profile* prof, const kss
   } else {
     out.push_back({"scheduler-simulator/prefilter-result", "{}"});
   }
-  if (res->status == 2) {
+  if (vb_reject) {  // RunPreFilterPlugins stops at VolumeBinding: the ones before it succeeded
+    const int m = pod->prefilter_msg;
+    out.push_back({"scheduler-simulator/prefilter-result-status",
+                   json_map({{"NodeAffinity", "success"}, {"NodePorts", "success"}, {"NodeResourcesFit", "success"},
+                             {"VolumeRestrictions", "success"},
+                             {"VolumeBinding", m >= 0 && m < (int)nm->message.size() ? nm->message[m] : std::string()}})});
+  } else if (res->status == 2) {
     out.push_back({"scheduler-simulator/prefilter-result-status", json_map({{"NodeAffinity", "pod affinity terms conflict"}})});
   } else {
     out.push_back({"scheduler-simulator/prefilter-result-status",
@@ -349,5 +376,5 @@ extern "C" int kss_format_pod_annotations_ex(const kss_names* names, const kss_p
   if (rc) return rc;
   kss_host_names nm;
   kss_host_set_names(&nm, names, n_nodes, n_taints, n_scalar);
-  return kss_host_format(&nm, prof, res, n_nodes, buf, cap, need, has ? &pf : nullptr);
+  return kss_host_format(&nm, prof, res, n_nodes, buf, cap, need, has ? &pf : nullptr, &ps->pods[pod_index]);
 }

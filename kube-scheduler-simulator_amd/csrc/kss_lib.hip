@@ -259,6 +259,9 @@ struct CommitArgs {
   uint64_t port_add;
   int32_t cls, n_own, local, sign;
   int32_t own[8];
+  int32_t n_vrow, n_vpriv;   // the pod's KSS_VOL_OWN / KSS_VOL_OWN_PRIVATE entries
+  int32_t vrow[8];
+  int32_t vpriv_key[4], vpriv_cnt[4];
 };
 
 __global__ void k_commit(DevCluster c, CommitArgs a) {
@@ -271,6 +274,8 @@ __global__ void k_commit(DevCluster c, CommitArgs a) {
   if (a.cls >= 0) c.class_count[(size_t)a.cls * N + a.local] += a.sign;
   for (int i = 0; i < a.n_own; i++) c.term_count[(size_t)a.own[i] * N + a.local] += a.sign;
   if (a.port_add) c.port_used[a.local] = a.sign > 0 ? (c.port_used[a.local] | a.port_add) : (c.port_used[a.local] & ~a.port_add);
+  for (int i = 0; i < a.n_vrow; i++) vol_commit_row(c, a.vrow[i], a.local, a.sign);
+  for (int i = 0; i < a.n_vpriv; i++) c.vol_attached[(size_t)a.vpriv_key[i] * N + a.local] += a.sign * a.vpriv_cnt[i];
 }
 
 // DefaultPreemption PostFilter dry run of one pod (kss_postfilter_pod): three launches.
@@ -285,6 +290,18 @@ __global__ __launch_bounds__(PRE_NODE_THREADS) void k_preempt_nodes(const Preemp
 __global__ __launch_bounds__(PRE_THREADS) void k_preempt_pick(const PreemptJob* __restrict__ job) {
   extern __shared__ __attribute__((aligned(16))) long long smem[];
   preempt_pick(*job, smem);
+}
+
+// Volume state sync (kss_apply_volume_delta): rows < n_vol_rows are vol_count, the rest
+// vol_attached keys.  Entries are applied in order by one lane (repeated cells accumulate).
+__global__ void k_volume_delta(DevCluster c, const int32_t* node, const int32_t* row, const int32_t* val, int n, int mode) {
+  if (blockIdx.x != 0 || threadIdx.x != 0) return;
+  const size_t N = (size_t)c.N;
+  for (int i = 0; i < n; i++) {
+    int32_t* cell = row[i] < c.n_vol_rows ? c.vol_count + (size_t)row[i] * N + node[i]
+                                         : c.vol_attached + (size_t)(row[i] - c.n_vol_rows) * N + node[i];
+    *cell = mode ? val[i] : *cell + val[i];
+  }
 }
 
 // Delta sync of node rows (kss_apply_node_delta): one packed upload, one scatter.
@@ -354,7 +371,7 @@ struct GpodNeeds {
 
 // Per-batch LDS / exchange sizing: the host restatement of make_plan's bin counts.
 struct PlanNeeds {
-  bool ports_images = false;  // some pod has host ports or ImageLocality rows
+  bool ports_images = false;  // some pod has host ports, ImageLocality rows or a volume program
   int bins_cap = 0;  // max over pods of histogram + presence bins
   int xw = 0;        // max exchange payload length (values) over pods and exchanges
   bool general = false;  // some pod carries spread / inter-pod-affinity programs
@@ -387,8 +404,8 @@ struct kss_ctx {
   DevCluster dc{};
   DevBuf cluster_buf;
   DevBuf pristine_buf;  // load-time copy of the mutable columns (kss_reset_node_state)
-  size_t mut_bytes[6] = {0, 0, 0, 0, 0, 0};
-  size_t pristine_off[6] = {0, 0, 0, 0, 0, 0};
+  size_t mut_bytes[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  size_t pristine_off[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   // pods
   DevBuf pod_buf;      // staged pod programs (kss_stage_pods / kss_schedule_batch)
   DevPods dp{};
@@ -496,9 +513,11 @@ int upload_podset(hipStream_t st, DevBuf& buf, const kss_podset* ps, DevPods& dp
   const size_t sz_spr = sizeof(kss_spread) * (size_t)std::max(ps->n_spreads, 1);
   const size_t sz_ipa = sizeof(kss_ipa) * (size_t)std::max(ps->n_ipa, 1);
   const size_t sz_ints = sizeof(int32_t) * (size_t)std::max(ps->n_ints, 1);
+  const size_t sz_vols = sizeof(kss_vol) * (size_t)std::max(ps->n_vols, 1);
   size_t o_pods = 0, o_reqs = align_up(o_pods + sz_pods, 256), o_terms = align_up(o_reqs + sz_reqs, 256),
          o_spr = align_up(o_terms + sz_terms, 256), o_ipa = align_up(o_spr + sz_spr, 256),
-         o_ints = align_up(o_ipa + sz_ipa, 256), total = align_up(o_ints + sz_ints, 256);
+         o_ints = align_up(o_ipa + sz_ipa, 256), o_vols = align_up(o_ints + sz_ints, 256),
+         total = align_up(o_vols + sz_vols, 256);
   int rc = buf.ensure(total);
   if (rc) return rc;
   char* b = (char*)buf.p;
@@ -508,12 +527,14 @@ int upload_podset(hipStream_t st, DevBuf& buf, const kss_podset* ps, DevPods& dp
   if (ps->n_spreads) HIP_TRY(hipMemcpyAsync(b + o_spr, ps->spreads, sizeof(kss_spread) * ps->n_spreads, hipMemcpyHostToDevice, st));
   if (ps->n_ipa) HIP_TRY(hipMemcpyAsync(b + o_ipa, ps->ipa, sizeof(kss_ipa) * ps->n_ipa, hipMemcpyHostToDevice, st));
   if (ps->n_ints) HIP_TRY(hipMemcpyAsync(b + o_ints, ps->ints, sizeof(int32_t) * ps->n_ints, hipMemcpyHostToDevice, st));
+  if (ps->n_vols) HIP_TRY(hipMemcpyAsync(b + o_vols, ps->vols, sizeof(kss_vol) * ps->n_vols, hipMemcpyHostToDevice, st));
   dp.pods = (const kss_pod*)(b + o_pods);
   dp.reqs = (const kss_req*)(b + o_reqs);
   dp.terms = (const kss_term*)(b + o_terms);
   dp.spreads = (const kss_spread*)(b + o_spr);
   dp.ipa = (const kss_ipa*)(b + o_ipa);
   dp.ints = (const int32_t*)(b + o_ints);
+  dp.vols = (const kss_vol*)(b + o_vols);
   return 0;
 }
 
@@ -530,12 +551,13 @@ struct PackedUpload {
 
 int pack_podset(DevBuf& buf, void*& pin, size_t& pin_cap, const kss_podset* ps, size_t extra, DevPods& dp,
                 PackedUpload& pu) {
-  const size_t sz[6] = {sizeof(kss_pod) * (size_t)ps->n_pods, sizeof(kss_req) * (size_t)ps->n_reqs,
+  const size_t sz[7] = {sizeof(kss_pod) * (size_t)ps->n_pods, sizeof(kss_req) * (size_t)ps->n_reqs,
                         sizeof(kss_term) * (size_t)ps->n_terms, sizeof(kss_spread) * (size_t)ps->n_spreads,
-                        sizeof(kss_ipa) * (size_t)ps->n_ipa, sizeof(int32_t) * (size_t)ps->n_ints};
-  const void* src[6] = {ps->pods, ps->reqs, ps->terms, ps->spreads, ps->ipa, ps->ints};
-  size_t off[6], o = 0;
-  for (int i = 0; i < 6; i++) {
+                        sizeof(kss_ipa) * (size_t)ps->n_ipa, sizeof(int32_t) * (size_t)ps->n_ints,
+                        sizeof(kss_vol) * (size_t)ps->n_vols};
+  const void* src[7] = {ps->pods, ps->reqs, ps->terms, ps->spreads, ps->ipa, ps->ints, ps->vols};
+  size_t off[7], o = 0;
+  for (int i = 0; i < 7; i++) {
     off[i] = o;
     o = align_up(o + std::max(sz[i], (size_t)16), 64);
   }
@@ -553,7 +575,7 @@ int pack_podset(DevBuf& buf, void*& pin, size_t& pin_cap, const kss_podset* ps, 
   pu.host = (char*)pin;
   pu.dev = (char*)buf.p;
   pu.slot = pu.tail ? pu.dev + align_up(pu.bytes, 256) : nullptr;
-  for (int i = 0; i < 6; i++)
+  for (int i = 0; i < 7; i++)
     if (sz[i]) std::memcpy(pu.host + off[i], src[i], sz[i]);
   dp.pods = (const kss_pod*)(pu.dev + off[0]);
   dp.reqs = (const kss_req*)(pu.dev + off[1]);
@@ -561,6 +583,7 @@ int pack_podset(DevBuf& buf, void*& pin, size_t& pin_cap, const kss_podset* ps, 
   dp.spreads = (const kss_spread*)(pu.dev + off[3]);
   dp.ipa = (const kss_ipa*)(pu.dev + off[4]);
   dp.ints = (const int32_t*)(pu.dev + off[5]);
+  dp.vols = (const kss_vol*)(pu.dev + off[6]);
   return 0;
 }
 
@@ -599,8 +622,41 @@ int validate(const kss_cluster* cl, const kss_podset* ps, int n) {
     if (!(cl->key_flags[e.key] & KSS_KEY_UNIQUE) && cl->key_card[e.key] + 1 > KSS_MAX_BINS)
       return fail(KSS_E_UNSUPPORTED, "non-unique topology key with more than KSS_MAX_BINS domains");
   }
+  if (ps->n_vols < 0 || (ps->n_vols > 0 && !ps->vols)) return fail(KSS_E_INVAL, "bad volume pool");
+  for (int i = 0; i < ps->n_vols; i++) {
+    const kss_vol& v = ps->vols[i];
+    switch (v.kind) {
+      case KSS_VOL_CONFLICT:
+      case KSS_VOL_OWN:
+        if (v.row < 0 || v.row >= cl->n_vol_rows) return fail(KSS_E_INVAL, "volume row out of range");
+        break;
+      case KSS_VOL_LIMIT:
+        if (v.key < 0 || v.key >= cl->n_vol_keys || v.row >= cl->n_vol_rows || (v.row < 0 && v.count < 0))
+          return fail(KSS_E_INVAL, "volume limit entry out of range");
+        break;
+      case KSS_VOL_OWN_PRIVATE:
+        if (v.key < 0 || v.key >= cl->n_vol_keys || v.count < 0) return fail(KSS_E_INVAL, "volume key out of range");
+        break;
+      case KSS_VOL_BIND_AFFINITY:
+        if (!in(v.a, v.b, ps->n_terms)) return fail(KSS_E_INVAL, "volume node affinity terms out of range");
+        break;
+      case KSS_VOL_ZONE:
+        if (!in(v.a, v.b, ps->n_reqs)) return fail(KSS_E_INVAL, "volume zone requirements out of range");
+        break;
+      case KSS_VOL_ZONE_ERROR:
+        if (v.a < 0 || v.a > 65534) return fail(KSS_E_INVAL, "volume zone message out of range");
+        break;
+      case KSS_VOL_BIND_PV_MISSING:
+        break;
+      default:
+        return fail(KSS_E_INVAL, "bad volume entry kind");
+    }
+  }
   for (int i = 0; i < n; i++) {
     const kss_pod& p = ps->pods[i];
+    if (p.prefilter_status < KSS_PF_OK || p.prefilter_status > KSS_PF_VOLUME_BINDING)
+      return fail(KSS_E_INVAL, "bad prefilter status");
+    if (!in(p.vol_off, p.vol_len, ps->n_vols)) return fail(KSS_E_INVAL, "pod volume program out of range");
     if (!in(p.sel_off, p.sel_len, ps->n_reqs) || !in(p.aff_off, p.aff_len, ps->n_terms) ||
         !in(p.pref_off, p.pref_len, ps->n_terms) || !in(p.spread_off, (int64_t)p.n_hard + p.n_soft, ps->n_spreads) ||
         !in(p.ipa_off, p.ipa_len, ps->n_ipa) || !in(p.own_terms_off, p.own_terms_len, ps->n_ints))
@@ -667,7 +723,7 @@ bool f64_exact(const F64Bounds& c, const F64Bounds& p, int n_pods) {
 // Compact record of one pod (kss_simple.cuh SPod); false when the preferred NodeAffinity
 // weights do not fit the static word's 20 bits.
 bool fill_spod(const kss_podset* ps, const kss_pod& p, int n_scalar, SPod& q) {
-  if (p.port_conflict | p.port_add || p.img_len > 0) return false;  // NodePorts / ImageLocality: k_schedule
+  if (p.port_conflict | p.port_add || p.img_len > 0 || p.vol_len > 0) return false;  // NodePorts / ImageLocality / volumes: k_schedule
   int64_t wsum = 0;
   for (int t = 0; t < p.pref_len; t++) wsum += std::max(0, ps->terms[p.pref_off + t].weight);
   if (wsum > 0xFFFFF) return false;  // static word: 20 bits of raw NodeAffinity
@@ -739,7 +795,7 @@ const char* const kGpReason[GP_NCODES] = {
     "a pod's record exceeds 2 KiB (too many references)",
     "more than 16 inter-pod-affinity entries after merging",
     "extended (scalar) resources in the cluster: k_simple / k_spread keep cpu, memory and ephemeral-storage only",
-    "host ports (NodePorts) or node-cached images (ImageLocality): k_schedule only",
+    "host ports (NodePorts), node-cached images (ImageLocality) or volumes: k_schedule only",
 };
 
 bool gfail(GpodNeeds& need, int code, int pod) {
@@ -766,7 +822,7 @@ bool build_gpods(const kss_podset* ps, int n_scalar, int n_classes, const int32_
     const kss_pod& p = ps->pods[i];
     GPod& g = out[(size_t)i];
     std::vector<uint32_t>& R = refs_of[(size_t)i];
-    if (p.port_conflict | p.port_add || p.img_len > 0) return gfail(need, GP_PORTS_IMAGES, i);
+    if (p.port_conflict | p.port_add || p.img_len > 0 || p.vol_len > 0) return gfail(need, GP_PORTS_IMAGES, i);
     if (!fill_spod(ps, p, n_scalar, g.dyn)) return gfail(need, GP_NA_WEIGHTS, i);
     if (p.n_hard > MAXH || p.n_soft > MAXS) return gfail(need, GP_CONSTRAINTS, i);
     g.pflags = (int32_t)p.flags;
@@ -989,7 +1045,7 @@ bool spread_bounds_ok(const GpodNeeds& q, double total, double cell, int N) {
 
 struct ClusterLayout {
   size_t o_alloc, o_req, o_nz, o_allowed, o_podc, o_flags, o_th, o_ts, o_to, o_lv, o_kb, o_kc, o_kf, o_ke, o_vi, o_vii,
-      o_cc, o_tc, o_log, o_pu, o_img, total;
+      o_cc, o_tc, o_log, o_pu, o_img, o_vc, o_va, o_vl, o_vrk, o_vkp, total;
   ClusterLayout(const kss_cluster* cl, int class_cap, int term_cap) {
     const size_t N = (size_t)cl->n_nodes;
     size_t o = 0;
@@ -1019,6 +1075,11 @@ struct ClusterLayout {
     o_log = take(8 * (N + 3));
     o_pu = take(8 * N);
     o_img = take(8 * (size_t)cl->n_images * N);
+    o_vc = take(4 * (size_t)cl->n_vol_rows * N);
+    o_va = take(4 * (size_t)cl->n_vol_keys * N);
+    o_vl = take(4 * (size_t)cl->n_vol_keys * N);
+    o_vrk = take(4 * (size_t)cl->n_vol_rows);
+    o_vkp = take(4 * (size_t)cl->n_vol_keys);
     total = o;
   }
 };
@@ -1054,6 +1115,11 @@ int fill_cluster(hipStream_t st, const kss_cluster* cl, int class_cap, int term_
   if (cl->port_used) rc |= cp(L.o_pu, cl->port_used, 8 * N);
   else HIP_TRY(hipMemsetAsync(b + L.o_pu, 0, 8 * std::max<size_t>(N, 1), st));
   rc |= cp(L.o_img, cl->image_score, 8 * (size_t)cl->n_images * N);
+  rc |= cp(L.o_vc, cl->vol_count, 4 * (size_t)cl->n_vol_rows * N);
+  rc |= cp(L.o_va, cl->vol_attached, 4 * (size_t)cl->n_vol_keys * N);
+  rc |= cp(L.o_vl, cl->vol_limit, 4 * (size_t)cl->n_vol_keys * N);
+  rc |= cp(L.o_vrk, cl->vol_row_key, 4 * (size_t)cl->n_vol_rows);
+  rc |= cp(L.o_vkp, cl->vol_key_plugin, 4 * (size_t)cl->n_vol_keys);
   logtab.resize(N + 3);
   for (size_t k = 0; k < N + 3; k++) logtab[k] = kss_go_log((double)(k + 2));
   rc |= cp(L.o_log, logtab.data(), 8 * (N + 3));
@@ -1088,6 +1154,13 @@ int fill_cluster(hipStream_t st, const kss_cluster* cl, int class_cap, int term_
   dc.port_used = (uint64_t*)(b + L.o_pu);
   dc.image_score = (const int64_t*)(b + L.o_img);
   dc.n_images = cl->n_images;
+  dc.n_vol_rows = cl->n_vol_rows;
+  dc.n_vol_keys = cl->n_vol_keys;
+  dc.vol_count = (int32_t*)(b + L.o_vc);
+  dc.vol_attached = (int32_t*)(b + L.o_va);
+  dc.vol_limit = (const int32_t*)(b + L.o_vl);
+  dc.vol_row_key = (const int32_t*)(b + L.o_vrk);
+  dc.vol_key_plugin = (const int32_t*)(b + L.o_vkp);
   return 0;
 }
 
@@ -1117,6 +1190,16 @@ int check_cluster(const kss_cluster* cl) {
       if (cl->port_used[i] >> cl->n_ports) return fail(KSS_E_INVAL, "port bit outside the port dictionary");
   for (size_t i = 0; i < (size_t)cl->n_images * N; i++)
     if (cl->image_score[i] < 0) return fail(KSS_E_INVAL, "negative image score");
+  if (cl->n_vol_rows < 0 || cl->n_vol_keys < 0 || cl->n_vol_keys > KSS_MAX_VOL_KEYS)
+    return fail(KSS_E_INVAL, "volume row / key count out of range");
+  if (N > 0 && ((cl->n_vol_rows > 0 && (!cl->vol_count || !cl->vol_row_key)) ||
+                (cl->n_vol_keys > 0 && (!cl->vol_attached || !cl->vol_limit || !cl->vol_key_plugin))))
+    return fail(KSS_E_INVAL, "missing volume columns");
+  for (int r = 0; r < cl->n_vol_rows; r++)
+    if (cl->vol_row_key[r] < -1 || cl->vol_row_key[r] >= cl->n_vol_keys) return fail(KSS_E_INVAL, "volume row key out of range");
+  for (int k = 0; k < cl->n_vol_keys; k++)
+    if (cl->vol_key_plugin[k] < KSS_F_EBS_LIMITS || cl->vol_key_plugin[k] > KSS_F_AZURE_DISK_LIMITS)
+      return fail(KSS_E_INVAL, "volume key plugin out of range");
   return 0;
 }
 
@@ -1161,7 +1244,7 @@ int kss_abi_sizes(int32_t* out, int32_t n) {
                        (int32_t)sizeof(kss_spread),  (int32_t)sizeof(kss_ipa),     (int32_t)sizeof(kss_pod),
                        (int32_t)sizeof(kss_podset),  (int32_t)sizeof(kss_profile), (int32_t)sizeof(kss_pod_result),
                        (int32_t)sizeof(kss_config),  (int32_t)sizeof(kss_names),   (int32_t)sizeof(kss_synth),
-                       (int32_t)sizeof(kss_boundset), (int32_t)sizeof(kss_preempt_result)};
+                       (int32_t)sizeof(kss_boundset), (int32_t)sizeof(kss_preempt_result), (int32_t)sizeof(kss_vol)};
   const int32_t k = (int32_t)(sizeof(s) / sizeof(s[0]));
   for (int i = 0; i < n && i < k; i++) out[i] = s[i];
   return k;
@@ -1257,18 +1340,19 @@ int kss_load_cluster(kss_ctx* ctx, const kss_cluster* cl) {
   if (rc) return rc;
   // pristine copy of the mutable columns
   const size_t N = (size_t)cl->n_nodes;
-  const size_t mb[6] = {8 * KSS_NRES * N, 8 * 2 * N, 4 * N, 4 * (size_t)class_cap * N, 4 * (size_t)term_cap * N, 8 * N};
+  const size_t mb[8] = {8 * KSS_NRES * N,          8 * 2 * N, 4 * N, 4 * (size_t)class_cap * N, 4 * (size_t)term_cap * N,
+                        8 * N, 4 * (size_t)cl->n_vol_rows * N, 4 * (size_t)cl->n_vol_keys * N};
   size_t tot = 0;
-  for (int i = 0; i < 6; i++) {
+  for (int i = 0; i < 8; i++) {
     ctx->mut_bytes[i] = mb[i];
     ctx->pristine_off[i] = tot;
     tot = align_up(tot + mb[i], 256);
   }
   rc = ctx->pristine_buf.ensure(tot);
   if (rc) return rc;
-  void* src[6] = {ctx->dc.requested, ctx->dc.nonzero, ctx->dc.pod_count, ctx->dc.class_count, ctx->dc.term_count,
-                  ctx->dc.port_used};
-  for (int i = 0; i < 6; i++)
+  void* src[8] = {ctx->dc.requested,  ctx->dc.nonzero,   ctx->dc.pod_count, ctx->dc.class_count,
+                  ctx->dc.term_count, ctx->dc.port_used, ctx->dc.vol_count, ctx->dc.vol_attached};
+  for (int i = 0; i < 8; i++)
     if (mb[i])
       HIP_TRY(hipMemcpyAsync((char*)ctx->pristine_buf.p + ctx->pristine_off[i], src[i], mb[i], hipMemcpyDeviceToDevice,
                              ctx->stream));
@@ -1347,6 +1431,10 @@ int kss_load_cluster_rows(kss_ctx* ctx, const kss_cluster* cl, int32_t lo, int32
   if (cl->port_used) std::copy(cl->port_used + lo, cl->port_used + hi, pu.begin());
   std::vector<int64_t> img;
   if (cl->n_images) rows64(cl->image_score, cl->n_images, img);
+  std::vector<int32_t> vc, va, vl;
+  rows32(cl->vol_count, cl->n_vol_rows, vc);
+  rows32(cl->vol_attached, cl->n_vol_keys, va);
+  rows32(cl->vol_limit, cl->n_vol_keys, vl);
   kss_cluster s = *cl;
   s.n_nodes = (int32_t)M;
   s.node_base = cl->node_base + lo;
@@ -1364,6 +1452,9 @@ int kss_load_cluster_rows(kss_ctx* ctx, const kss_cluster* cl, int32_t lo, int32
   s.term_count = cl->term_count ? tc.data() : nullptr;
   s.port_used = pu.data();
   s.image_score = cl->n_images ? img.data() : nullptr;
+  s.vol_count = cl->n_vol_rows ? vc.data() : nullptr;
+  s.vol_attached = cl->n_vol_keys ? va.data() : nullptr;
+  s.vol_limit = cl->n_vol_keys ? vl.data() : nullptr;
   return kss_load_cluster(ctx, &s);  // synchronous: the temporaries outlive the upload
 }
 
@@ -1375,7 +1466,7 @@ static int axis_check(kss_ctx* ctx, int32_t pod_index) {
   if (ctx->staged_need.general)
     return fail(KSS_E_UNSUPPORTED, "node-axis path: spread / inter-pod programs need the replicated domain histograms");
   if (ctx->staged_need.ports_images)
-    return fail(KSS_E_UNSUPPORTED, "node-axis path: host ports / image locality are not folded into the axis key");
+    return fail(KSS_E_UNSUPPORTED, "node-axis path: host ports / image locality / volumes are not folded into the axis key");
   return ctx->axis_cv.ensure(sizeof(int32_t) * 5 * (size_t)std::max(ctx->dc.N, 1));
 }
 
@@ -1444,14 +1535,14 @@ int kss_reset_node_state(kss_ctx* ctx) {
   if (!ctx || !ctx->loaded) return fail(KSS_E_INVAL, "no cluster loaded");
   std::lock_guard<std::mutex> lk(ctx->mu);
   HIP_TRY(hipSetDevice(ctx->cfg.device));
-  void* dst[6] = {ctx->dc.requested, ctx->dc.nonzero, ctx->dc.pod_count, ctx->dc.class_count, ctx->dc.term_count,
-                  ctx->dc.port_used};
+  void* dst[8] = {ctx->dc.requested,  ctx->dc.nonzero,   ctx->dc.pod_count, ctx->dc.class_count,
+                  ctx->dc.term_count, ctx->dc.port_used, ctx->dc.vol_count, ctx->dc.vol_attached};
   ctx->count_bound = ctx->count_bound0;
   ctx->cell_bound = ctx->cell_bound0;
   ctx->bound_log.clear();
   ctx->bound_dirty = true;
   ctx->state_unknown = false;
-  for (int i = 0; i < 6; i++)
+  for (int i = 0; i < 8; i++)
     if (ctx->mut_bytes[i])
       HIP_TRY(hipMemcpyAsync(dst[i], (char*)ctx->pristine_buf.p + ctx->pristine_off[i], ctx->mut_bytes[i],
                              hipMemcpyDeviceToDevice, ctx->stream));
@@ -1686,6 +1777,49 @@ int kss_apply_port_delta(kss_ctx* ctx, const int32_t* idx, int32_t n, const uint
   return 0;
 }
 
+int kss_read_volume_state(kss_ctx* ctx, int32_t* vol_count, int32_t* vol_attached) {
+  if (!ctx || !ctx->loaded) return fail(KSS_E_INVAL, "no cluster loaded");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  HIP_TRY(hipSetDevice(ctx->cfg.device));
+  const size_t N = (size_t)ctx->dc.N;
+  if (vol_count && ctx->dc.n_vol_rows)
+    HIP_TRY(hipMemcpyAsync(vol_count, ctx->dc.vol_count, 4 * (size_t)ctx->dc.n_vol_rows * N, hipMemcpyDeviceToHost, ctx->stream));
+  if (vol_attached && ctx->dc.n_vol_keys)
+    HIP_TRY(hipMemcpyAsync(vol_attached, ctx->dc.vol_attached, 4 * (size_t)ctx->dc.n_vol_keys * N, hipMemcpyDeviceToHost,
+                           ctx->stream));
+  HIP_TRY(hipStreamSynchronize(ctx->stream));
+  return 0;
+}
+
+int kss_apply_volume_delta(kss_ctx* ctx, const int32_t* node, const int32_t* row, const int32_t* value, int32_t n,
+                           int32_t mode) {
+  if (!ctx || !ctx->loaded) return fail(KSS_E_INVAL, "no cluster loaded");
+  if (n < 0 || (n > 0 && (!node || !row || !value)) || (mode != 0 && mode != 1)) return fail(KSS_E_INVAL, "bad arguments");
+  const int R = ctx->dc.n_vol_rows, K = ctx->dc.n_vol_keys;
+  for (int i = 0; i < n; i++) {
+    if (node[i] < 0 || node[i] >= ctx->dc.N) return fail(KSS_E_INVAL, "delta node out of range");
+    if (row[i] < 0 || row[i] >= R + K) return fail(KSS_E_INVAL, "delta volume row out of range");
+  }
+  if (n == 0) return 0;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  HIP_TRY(hipSetDevice(ctx->cfg.device));
+  // one packed upload (node, row, value) and one scatter on the ctx stream
+  const size_t bytes = 12 * (size_t)n;
+  int rc = ctx->delta_buf.ensure(bytes);
+  if (rc) return rc;
+  std::vector<int32_t> h(3 * (size_t)n);
+  std::memcpy(h.data(), node, 4 * (size_t)n);
+  std::memcpy(h.data() + n, row, 4 * (size_t)n);
+  std::memcpy(h.data() + 2 * (size_t)n, value, 4 * (size_t)n);
+  HIP_TRY(hipMemcpyAsync(ctx->delta_buf.p, h.data(), bytes, hipMemcpyHostToDevice, ctx->stream));
+  const int32_t* d = (const int32_t*)ctx->delta_buf.p;
+  hipLaunchKernelGGL(k_volume_delta, dim3(1), dim3(64), 0, ctx->stream, ctx->dc, d, d + n,
+                     d + 2 * (size_t)n, n, mode);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipStreamSynchronize(ctx->stream));  // the host copy h dies here
+  return 0;
+}
+
 static PlanNeeds plan_needs(const int32_t* key_card, const uint32_t* key_flags, const kss_podset* ps, int n) {
   PlanNeeds r;
   r.xw = 12;  // the filter exchange's scalars
@@ -1693,7 +1827,7 @@ static PlanNeeds plan_needs(const int32_t* key_card, const uint32_t* key_flags, 
     const kss_pod& p = ps->pods[i];
     int bins = 0, hp = 0, sp = 0;
     if (p.n_hard | p.n_soft | p.ipa_len) r.general = true;
-    if (p.port_conflict | p.port_add || p.img_len > 0) r.ports_images = true;
+    if (p.port_conflict | p.port_add || p.img_len > 0 || p.vol_len > 0) r.ports_images = true;
     for (int h = 0; h < p.n_hard && h < MAXH; h++) {
       const int key = ps->spreads[p.spread_off + h].key;
       if (!(key_flags[key] & KSS_KEY_UNIQUE)) {
@@ -2422,6 +2556,7 @@ struct OnePod {
   std::vector<kss_spread> spreads;
   std::vector<kss_ipa> ipa;
   std::vector<int32_t> ints;
+  std::vector<kss_vol> vols;
   kss_podset ps{};
 };
 
@@ -2432,7 +2567,7 @@ static int compact_pod(const kss_podset* ps, int i, OnePod& o) {
       !in(p.pref_off, p.pref_len, ps->n_terms) || !in(p.spread_off, (int64_t)p.n_hard + p.n_soft, ps->n_spreads) ||
       !in(p.ipa_off, p.ipa_len, ps->n_ipa) || !in(p.own_terms_off, p.own_terms_len, ps->n_ints) ||
       (p.names_len >= 0 && !in(p.names_off, p.names_len, ps->n_ints)) ||
-      (p.img_len > 0 && !in(p.img_off, p.img_len, ps->n_ints)))
+      (p.img_len > 0 && !in(p.img_off, p.img_len, ps->n_ints)) || !in(p.vol_off, p.vol_len, ps->n_vols))
     return fail(KSS_E_INVAL, "pod program out of range");
   o = OnePod{};
   o.pod = p;
@@ -2478,12 +2613,33 @@ static int compact_pod(const kss_podset* ps, int i, OnePod& o) {
   o.pod.own_terms_off = list(p.own_terms_off, p.own_terms_len);
   if (p.names_len >= 0) o.pod.names_off = list(p.names_off, p.names_len);
   if (p.img_len > 0) o.pod.img_off = list(p.img_off, p.img_len);
+  // the volume program: VolumeBinding terms and VolumeZone requirements follow into the
+  // pod's own pools; rows and keys are the cluster's
+  o.pod.vol_off = 0;
+  for (int e = 0; e < p.vol_len; e++) {
+    kss_vol v = ps->vols[p.vol_off + e];
+    if (v.kind == KSS_VOL_BIND_AFFINITY) {
+      if (!in(v.a, v.b, ps->n_terms)) return fail(KSS_E_INVAL, "volume node affinity terms out of range");
+      const int32_t at = (int32_t)o.terms.size();
+      for (int t = 0; t < v.b; t++)
+        if (!term(ps->terms[v.a + t])) return fail(KSS_E_INVAL, "term out of range");
+      v.a = at;
+    } else if (v.kind == KSS_VOL_ZONE) {
+      if (!in(v.a, v.b, ps->n_reqs)) return fail(KSS_E_INVAL, "volume zone requirements out of range");
+      const int32_t at = (int32_t)o.reqs.size();
+      for (int k = 0; k < v.b; k++) req(ps->reqs[v.a + k]);
+      v.a = at;
+    }
+    o.vols.push_back(v);
+  }
   o.ps.n_pods = 1;  // empty pools stay empty (upload_podset sizes them; validate skips them)
   o.ps.n_reqs = (int32_t)o.reqs.size();
   o.ps.n_terms = (int32_t)o.terms.size();
   o.ps.n_spreads = (int32_t)o.spreads.size();
   o.ps.n_ipa = (int32_t)o.ipa.size();
   o.ps.n_ints = (int32_t)o.ints.size();
+  o.ps.n_vols = (int32_t)o.vols.size();
+  o.ps.vols = o.vols.data();
   o.ps.pods = &o.pod;
   o.ps.reqs = o.reqs.data();
   o.ps.terms = o.terms.data();
@@ -2604,6 +2760,20 @@ static int commit_one(kss_ctx* ctx, const kss_podset* ps, int32_t pod_index, int
   for (int i = 0; i < p.own_terms_len; i++) {
     a.own[i] = ps->ints[p.own_terms_off + i];
     if (a.own[i] < 0 || a.own[i] >= ctx->host.n_terms) return fail(KSS_E_INVAL, "own term id out of range");
+  }
+  if (p.vol_off < 0 || p.vol_len < 0 || p.vol_off + p.vol_len > ps->n_vols) return fail(KSS_E_INVAL, "pod volume program out of range");
+  for (int e = 0; e < p.vol_len; e++) {
+    const kss_vol& v = ps->vols[p.vol_off + e];
+    if (v.kind == KSS_VOL_OWN) {
+      if (a.n_vrow == 8) return fail(KSS_E_UNSUPPORTED, "more than 8 own volume rows");
+      if (v.row < 0 || v.row >= ctx->host.n_vol_rows) return fail(KSS_E_INVAL, "volume row out of range");
+      a.vrow[a.n_vrow++] = v.row;
+    } else if (v.kind == KSS_VOL_OWN_PRIVATE) {
+      if (a.n_vpriv == 4) return fail(KSS_E_UNSUPPORTED, "more than 4 attach-limit keys");
+      if (v.key < 0 || v.key >= ctx->host.n_vol_keys || v.count < 0) return fail(KSS_E_INVAL, "volume key out of range");
+      a.vpriv_key[a.n_vpriv] = v.key;
+      a.vpriv_cnt[a.n_vpriv++] = v.count;
+    }
   }
   a.local = local;
   a.sign = sign;
@@ -2805,6 +2975,10 @@ void pack_inputs(Packer& P, const kss_cluster* cl, const kss_podset* ps, const s
   c.nct = nullptr;
   c.nc32 = nullptr;
   c.ncl = nullptr;
+  c.n_vol_rows = c.n_vol_keys = 0;  // sweeps refuse pods with volume programs (ports_images)
+  c.vol_count = c.vol_attached = nullptr;
+  c.vol_limit = c.vol_row_key = c.vol_key_plugin = nullptr;
+  j.P.vols = nullptr;
   j.P.pods = P.put(ps->pods, (size_t)ps->n_pods);
   j.P.reqs = P.put(ps->reqs, (size_t)ps->n_reqs);
   j.P.terms = P.put(ps->terms, (size_t)ps->n_terms);
@@ -2880,7 +3054,7 @@ kss_sweep* kss_sweep_create(int32_t device, const kss_profile* prof, int32_t n_s
     sw->need.bins_cap = std::max(sw->need.bins_cap, q.bins_cap);
     sw->need.general |= q.general;
     if (q.ports_images) {  // the sweep packs no UsedPorts / image-score columns
-      fail(KSS_E_UNSUPPORTED, "scenario sweeps: pods with host ports or ImageLocality rows take kss_schedule_batch");
+      fail(KSS_E_UNSUPPORTED, "scenario sweeps: pods with host ports, ImageLocality rows or volumes take kss_schedule_batch");
       return nullptr;
     }
   }
@@ -3202,6 +3376,9 @@ int kss_postfilter_pod(kss_ctx* ctx, const kss_podset* ps, int32_t pod_index, ks
   // (NodePorts failures are resolvable by eviction) is refused rather than mis-evaluated
   if (ps->pods[pod_index].port_conflict)
     return fail(KSS_E_UNSUPPORTED, "PostFilter dry run of a pod with host ports (victims' UsedPorts are not tabled)");
+  // likewise the victims' volumes (disk conflicts and attach limits are resolvable by eviction)
+  if (ps->pods[pod_index].vol_len > 0)
+    return fail(KSS_E_UNSUPPORTED, "PostFilter dry run of a pod with volumes (victims' volumes are not tabled)");
   OnePod one;
   int rc = compact_pod(ps, pod_index, one);
   if (rc) return rc;
@@ -3296,7 +3473,7 @@ int kss_format_pod_annotations(kss_ctx* ctx, const kss_podset* ps, int32_t pod_i
   std::vector<int> pf;
   int has = 0;
   if (kss_host_prefilter_nodes(ps, pod_index, n_nodes, &pf, &has)) return fail(KSS_E_INVAL, "bad pod index or node set");
-  return kss_host_format(&ctx->names, &ctx->prof, res, n_nodes, buf, cap, need, has ? &pf : nullptr);
+  return kss_host_format(&ctx->names, &ctx->prof, res, n_nodes, buf, cap, need, has ? &pf : nullptr, &ps->pods[pod_index]);
 }
 
 }  // extern "C"

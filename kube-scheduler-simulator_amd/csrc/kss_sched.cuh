@@ -628,7 +628,7 @@ __device__ __forceinline__ bool schedule_pod(const DevCluster& c, const DevPods&
         }
       }
     }
-    meta.status = !plan_ok ? 4 : (p.prefilter_status == 1 ? 2 : 3);
+    meta.status = !plan_ok ? 4 : (p.prefilter_status == KSS_PF_ERROR ? 3 : 2);
     return true;
   }
 
@@ -707,6 +707,7 @@ __device__ __forceinline__ bool schedule_pod(const DevCluster& c, const DevPods&
     } else {
       row = load_row(c, n);
       f = filter_local(c, P, p, en, n, row, &detail);
+      if (!f) f = filter_volumes(c, P, p, en, n, &detail);
       if (GEN && !f && ((en >> KSS_F_POD_TOPOLOGY_SPREAD) & 1u) && p.n_hard > 0) {
         const int r = filter_pts(c, P, p, pl, bins, hard_min, n);
         if (r) {
@@ -977,6 +978,12 @@ __device__ __forceinline__ void commit_pod(const DevCluster& c, const DevPods& P
   for (int i = 0; i < p.own_terms_len; i++) c.term_count[(size_t)P.ints[p.own_terms_off + i] * N + local] += sign;
   // NodeInfo.AddPod / RemovePod updateUsedPorts (a set: removal clears the entries)
   if (p.port_add) c.port_used[local] = sign > 0 ? (c.port_used[local] | p.port_add) : (c.port_used[local] & ~p.port_add);
+  // the pod's volumes (NodeInfo.Pods' volumes, re-read by the volume filters upstream)
+  for (int e = 0; e < p.vol_len; e++) {
+    const kss_vol& v = P.vols[p.vol_off + e];
+    if (v.kind == KSS_VOL_OWN) vol_commit_row(c, v.row, local, sign);
+    else if (v.kind == KSS_VOL_OWN_PRIVATE) c.vol_attached[(size_t)v.key * N + local] += sign * v.count;
+  }
 }
 
 // Shard cache fill / write-back (all lanes of the workgroup).

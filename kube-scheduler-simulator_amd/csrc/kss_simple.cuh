@@ -743,7 +743,7 @@ __device__ __forceinline__ void simple_schedule(DevCluster c, const SPod* __rest
         m.chosen = K ? x + c.node_base : -1;
         m.n_feasible = (int)nf;
         m.scored = (K && scored) ? 1 : 0;
-        m.status = pk.status != 0 ? (pk.status == 1 ? 2 : 3) : (nf == 0 ? 1 : 0);
+        m.status = pk.status != 0 ? (pk.status == KSS_PF_ERROR ? 3 : 2) : (nf == 0 ? 1 : 0);
         m.best_total = m.scored ? (int64_t)((unsigned long long)K >> 32) : 0;
         if (chosen) gchosen[k] = m.chosen;
         if (meta) {

@@ -823,7 +823,7 @@ __device__ __forceinline__ void spread_schedule(DevCluster c, const GPod* __rest
     m.best_total = 0;
     long long best = 0;
     bool evaluated = q.dyn.status == 0;
-    if (!evaluated) m.status = q.dyn.status == 1 ? 2 : 3;
+    if (!evaluated) m.status = q.dyn.status == KSS_PF_ERROR ? 3 : 2;
     int32_t flags = 0, hard_min[MAXH];
 #pragma unroll
     for (int i = 0; i < MAXH; i++) hard_min[i] = INT32_MAX;

@@ -51,6 +51,13 @@ KSS_F_TAINT_TOLERATION = 3
 KSS_F_NODE_AFFINITY = 4
 KSS_F_NODE_PORTS = 5
 KSS_F_NODE_RESOURCES_FIT = 6
+KSS_F_VOLUME_RESTRICTIONS = 7
+KSS_F_EBS_LIMITS = 8
+KSS_F_GCEPD_LIMITS = 9
+KSS_F_NODE_VOLUME_LIMITS = 10
+KSS_F_AZURE_DISK_LIMITS = 11
+KSS_F_VOLUME_BINDING = 12
+KSS_F_VOLUME_ZONE = 13
 KSS_F_POD_TOPOLOGY_SPREAD = 14
 KSS_F_INTER_POD_AFFINITY = 15
 KSS_NFILTER = 15
@@ -66,6 +73,8 @@ KSS_PTS_MISSING_LABEL = 1
 KSS_IPA_AFFINITY = 0
 KSS_IPA_ANTI_AFFINITY = 1
 KSS_IPA_EXISTING_ANTI_AFFINITY = 2
+KSS_VB_NODE_CONFLICT = 0
+KSS_VB_PV_NOT_EXIST = 1
 
 SCORE_PLUGINS = [
     "TaintToleration",
@@ -83,6 +92,7 @@ KSS_NSCORE = 8
 
 KSS_NODE_UNSCHEDULABLE = 1 << 0
 KSS_NODE_HAS_LABELS = 1 << 1
+KSS_NODE_VOLUME_ZONE = 1 << 2
 KSS_KEY_UNIQUE = 1 << 0
 KSS_KEY_HOSTNAME = 1 << 1
 
@@ -91,6 +101,11 @@ KSS_KEY_HOSTNAME = 1 << 1
 KSS_SPREAD_POLICY_AFFINITY_HONOR = 1 << 0
 KSS_SPREAD_POLICY_TAINTS_HONOR = 1 << 1
 (KSS_IPA_EXISTING_ANTI, KSS_IPA_REQ_AFFINITY, KSS_IPA_REQ_ANTI, KSS_IPA_SCORE_CLASS, KSS_IPA_SCORE_TERM) = range(5)
+
+(KSS_VOL_CONFLICT, KSS_VOL_LIMIT, KSS_VOL_BIND_AFFINITY, KSS_VOL_BIND_PV_MISSING, KSS_VOL_ZONE, KSS_VOL_ZONE_ERROR,
+ KSS_VOL_OWN, KSS_VOL_OWN_PRIVATE) = range(8)
+KSS_MAX_VOL_KEYS = 64
+KSS_PF_OK, KSS_PF_NODE_AFFINITY_CONFLICT, KSS_PF_ERROR, KSS_PF_VOLUME_BINDING = range(4)
 
 KSS_POD_TOL_UNSCHEDULABLE = 1 << 0
 KSS_POD_HAS_REQ_AFFINITY = 1 << 1
@@ -128,6 +143,8 @@ class Cluster(C.Structure):
         ("key_flags", P(u32)), ("key_empty", P(i32)), ("value_int", P(i64)), ("value_is_int", P(u8)),
         ("class_count", P(i32)), ("term_count", P(i32)),
         ("n_ports", i32), ("n_images", i32), ("port_used", P(u64)), ("image_score", P(i64)),
+        ("n_vol_rows", i32), ("n_vol_keys", i32), ("vol_count", P(i32)), ("vol_attached", P(i32)),
+        ("vol_limit", P(i32)), ("vol_row_key", P(i32)), ("vol_key_plugin", P(i32)),
     ]
 
 
@@ -148,6 +165,10 @@ class Ipa(C.Structure):
     _fields_ = [("kind", i32), ("key", i32), ("row_off", i32), ("row_len", i32), ("coef", i32), ("pad", i32)]
 
 
+class Vol(C.Structure):
+    _fields_ = [("kind", i32), ("key", i32), ("row", i32), ("count", i32), ("a", i32), ("b", i32)]
+
+
 class Pod(C.Structure):
     _fields_ = [
         ("fit_request", i64 * KSS_NRES), ("score_req_nz", i64 * KSS_NRES), ("score_req", i64 * KSS_NRES),
@@ -155,16 +176,16 @@ class Pod(C.Structure):
         ("node_name", i32), ("flags", u32), ("sel_off", i32), ("sel_len", i32), ("aff_off", i32), ("aff_len", i32),
         ("pref_off", i32), ("pref_len", i32), ("spread_off", i32), ("n_hard", i32), ("n_soft", i32),
         ("ipa_off", i32), ("ipa_len", i32), ("cls", i32), ("own_terms_off", i32), ("own_terms_len", i32),
-        ("prefilter_status", i32), ("names_off", i32), ("names_len", i32), ("priority", i32), ("pad", i32),
+        ("prefilter_status", i32), ("names_off", i32), ("names_len", i32), ("priority", i32), ("prefilter_msg", i32),
         ("port_conflict", u64), ("port_add", u64), ("img_off", i32), ("img_len", i32), ("n_containers", i32),
-        ("pad2", i32),
+        ("vol_off", i32), ("vol_len", i32), ("pad2", i32),
     ]
 
 
 class PodSet(C.Structure):
     _fields_ = [("n_pods", i32), ("n_reqs", i32), ("n_terms", i32), ("n_spreads", i32), ("n_ipa", i32),
                 ("n_ints", i32), ("pods", P(Pod)), ("reqs", P(Req)), ("terms", P(Term)), ("spreads", P(Spread)),
-                ("ipa", P(Ipa)), ("ints", P(i32))]
+                ("ipa", P(Ipa)), ("ints", P(i32)), ("n_vols", i32), ("pad", i32), ("vols", P(Vol))]
 
 
 class Profile(C.Structure):
@@ -192,7 +213,7 @@ class Config(C.Structure):
 
 class Names(C.Structure):
     _fields_ = [("node_names", P(C.c_char_p)), ("taint_keys", P(C.c_char_p)), ("taint_values", P(C.c_char_p)),
-                ("scalar_names", P(C.c_char_p))]
+                ("scalar_names", P(C.c_char_p)), ("n_messages", i32), ("pad", i32), ("messages", P(C.c_char_p))]
 
 
 class Boundset(C.Structure):
@@ -216,6 +237,7 @@ REQ_DTYPE = np.dtype(Req)
 TERM_DTYPE = np.dtype(Term)
 SPREAD_DTYPE = np.dtype(Spread)
 IPA_DTYPE = np.dtype(Ipa)
+VOL_DTYPE = np.dtype(Vol)
 
 
 def ptr(arr: np.ndarray, ctype):

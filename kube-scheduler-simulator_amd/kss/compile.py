@@ -16,6 +16,8 @@ Upstream semantics restated here (k8s.io/kubernetes v1.26.2, not vendored):
   * topology spread: filterTopologySpreadConstraints / buildDefaultConstraints
   * inter-pod affinity: framework.NewPodInfo affinity terms, AffinityTerm.Matches,
     mergeAffinityTermNamespacesIfNotEmpty
+  * volumes: kss/volumes.py (VolumeRestrictions, the attach-limit plugins, VolumeBinding,
+    VolumeZone) from the snapshot's PVs, claims, StorageClasses and CSINodes
 """
 from __future__ import annotations
 
@@ -407,6 +409,8 @@ class CompiledCluster:
     bound_names: List[Tuple[str, str]] = field(default_factory=list)  # (namespace, name) per bound id
     ports: List[Tuple[str, str, int]] = field(default_factory=list)   # host-port dictionary (ip, protocol, port)
     images: List[str] = field(default_factory=list)                   # image_score rows (image names)
+    vol_rows: list = field(default_factory=list)                      # vol_count rows (volumes.VolumeCompiler.rows)
+    vol_keys: List[str] = field(default_factory=list)                 # attach-limit keys
     _keep: list = field(default_factory=list)
 
     @property
@@ -420,6 +424,10 @@ class CompiledCluster:
         c.n_images = len(self.images)
         c.port_used = abi.ptr(a["port_used"], abi.u64)
         c.image_score = abi.ptr(a["image_score"], abi.i64)
+        c.n_vol_rows = len(self.vol_rows)
+        c.n_vol_keys = len(self.vol_keys)
+        for name in ("vol_count", "vol_attached", "vol_limit", "vol_row_key", "vol_key_plugin"):
+            setattr(c, name, abi.ptr(a[name], abi.i32))
         c.n_nodes = self.n_nodes
         c.n_scalar = len(self.scalars)
         c.n_label_keys = len(self.label_keys)
@@ -460,6 +468,9 @@ class CompiledPods:
     ints: np.ndarray
     names: List[Tuple[str, str]]   # (namespace, name)
     counts: Tuple[int, int, int, int, int] = (0, 0, 0, 0, 0)  # real pool sizes (arrays are padded to >= 1)
+    vols: Optional[np.ndarray] = None   # kss_vol pool
+    n_vols: int = 0
+    messages: List[str] = field(default_factory=list)  # kss_names.messages (VolumeBinding PreFilter, VolumeZone)
 
     @property
     def n(self) -> int:
@@ -475,6 +486,10 @@ class CompiledPods:
         s.spreads = self.spreads.ctypes.data_as(abi.P(abi.Spread))
         s.ipa = self.ipa.ctypes.data_as(abi.P(abi.Ipa))
         s.ints = self.ints.ctypes.data_as(abi.P(abi.i32))
+        if self.vols is None:
+            self.vols = np.zeros(1, dtype=abi.VOL_DTYPE)
+        s.n_vols = self.n_vols
+        s.vols = self.vols.ctypes.data_as(abi.P(abi.Vol))
         return s
 
 
@@ -494,7 +509,8 @@ class Compiler:
 
     def __init__(self, nodes: Sequence[dict], bound_pods: Sequence[dict] = (), pending: Sequence[dict] = (),
                  namespaces: Optional[Dict[str, Dict[str, str]]] = None, hard_pod_affinity_weight: int = 1,
-                 system_defaulted: bool = True, device_limits: bool = True):
+                 system_defaulted: bool = True, device_limits: bool = True, storage: Optional[dict] = None):
+        """storage: {"pvs", "pvcs", "storage_classes", "csinodes"} object lists for the volume plugins."""
         self.nodes_in = list(nodes)
         self.bound = list(bound_pods)
         self.pending = list(pending)
@@ -504,6 +520,7 @@ class Compiler:
         self.hard_w = hard_pod_affinity_weight
         self.system_defaulted = system_defaulted
         self.device_limits = device_limits
+        self.storage = storage
 
     # -------------------------------------------------------------- cluster
     def compile(self) -> Tuple[CompiledCluster, CompiledPods]:
@@ -514,6 +531,13 @@ class Compiler:
             raise CompileError("duplicate node names")
         self.node_index = {nm: i for i, nm in enumerate(names)}
         N = len(nodes)
+        # volume programs (kss/volumes.py): built from the canonical node order and NodeInfo pods
+        self.vc = None
+        if self.storage or any(spec(p).get("volumes") for p in self.bound + self.pending):
+            from .volumes import VolumeCompiler
+            bound_on = [(p, self.node_index[spec(p).get("nodeName")]) for p in self.bound
+                        if spec(p).get("nodeName") in self.node_index]
+            self.vc = VolumeCompiler(self.storage, nodes, bound_on, self.pending)
 
         # scalar resources (sorted)
         sc = set()
@@ -559,6 +583,8 @@ class Compiler:
                 keys.add(t.topology_key)
             if self.system_defaulted and DEFAULT_SPREAD_SELECTOR_ANN in (meta(p).get("annotations") or {}):
                 keys.update((LABEL_HOSTNAME, LABEL_ZONE))
+        if self.vc is not None:
+            keys.update(self.vc.label_keys())
         label_keys = sorted(keys)
         self.key_index = {k: i for i, k in enumerate(label_keys)}
 
@@ -642,6 +668,8 @@ class Compiler:
                 flags[i] |= abi.KSS_NODE_UNSCHEDULABLE
             if node_labels[i]:
                 flags[i] |= abi.KSS_NODE_HAS_LABELS
+        if self.vc is not None:
+            flags |= self.vc.node_zone_flags()
 
         # classes and term types over all pods (bound + pending)
         cls_set = set()
@@ -736,12 +764,18 @@ class Compiler:
                     sz, num = st[nm]
                     image_score[r, i] = int(float(sz) * (float(num) / float(N)))  # scaledImageScore
 
+        vc = self.vc
         arrays = dict(alloc=alloc, requested=requested, nonzero=nonzero, allowed_pods=allowed, pod_count=pod_count,
                       node_flags=flags, taint_hard=taint_hard, taint_soft=taint_soft, taint_order=taint_order,
                       label_value=label_value, key_base=key_base, key_card=key_card, key_flags=key_flags,
                       key_empty=key_empty, value_int=np.array(vint, dtype=np.int64),
                       value_is_int=np.array(visint, dtype=np.uint8), class_count=class_count, term_count=term_count,
-                      port_used=port_used, image_score=image_score)
+                      port_used=port_used, image_score=image_score,
+                      vol_count=vc.vol_count if vc else np.zeros((0, N), np.int32),
+                      vol_attached=vc.vol_attached if vc else np.zeros((0, N), np.int32),
+                      vol_limit=vc.vol_limit if vc else np.zeros((0, N), np.int32),
+                      vol_row_key=vc.vol_row_key if vc else np.zeros(0, np.int32),
+                      vol_key_plugin=vc.vol_key_plugin if vc else np.zeros(0, np.int32))
         arrays = {k: (np.zeros(1, dtype=v.dtype) if v.size == 0 else np.ascontiguousarray(v))
                   for k, v in arrays.items()}
         nb = len(bound_names)
@@ -755,7 +789,7 @@ class Compiler:
         self.cc = CompiledCluster(node_names=names, order=order, scalars=scalars, label_keys=label_keys,
                                   key_values=key_values, taints=taints, classes=classes, terms=terms, arrays=arrays,
                                   namespaces=self.namespaces, bound=bound, bound_names=bound_names, ports=ports,
-                                  images=images)
+                                  images=images, vol_rows=list(vc.rows) if vc else [], vol_keys=list(vc.keys) if vc else [])
         self.node_labels = node_labels
         self.key_flags = key_flags
         pods = self._compile_pods(self.pending)
@@ -779,10 +813,12 @@ class Compiler:
         self._spreads: List[tuple] = []
         self._ipa: List[tuple] = []
         self._ints: List[int] = []
+        self._vols: List[tuple] = []
         recs = np.zeros(len(pods), dtype=abi.POD_DTYPE)
         names = []
         for i, p in enumerate(pods):
             self._compile_pod(p, recs[i])
+            self._compile_volumes(i, recs[i])
             names.append((ns_of(p), name_of(p)))
 
         def arr(rows, dt):
@@ -795,7 +831,9 @@ class Compiler:
                             spreads=arr(self._spreads, abi.SPREAD_DTYPE), ipa=arr(self._ipa, abi.IPA_DTYPE),
                             ints=_nonempty(np.array(self._ints, dtype=np.int32)), names=names,
                             counts=(len(self._reqs), len(self._terms), len(self._spreads), len(self._ipa),
-                                    len(self._ints)))
+                                    len(self._ints)),
+                            vols=arr(self._vols, abi.VOL_DTYPE), n_vols=len(self._vols),
+                            messages=list(self.vc.messages) if self.vc else [])
 
     def _list(self, vals: Sequence[int]) -> Tuple[int, int]:
         off = len(self._ints)
@@ -875,6 +913,59 @@ class Compiler:
             rows = [(0, abi.KSS_OP_FALSE, 0, 0, 0, 0)]  # a term with parse errors never matches
         self._reqs.extend(rows)
         return (off, len(rows), weight, 0)
+
+    def _pv_term(self, term: dict) -> Optional[tuple]:
+        """A PersistentVolume's required node-affinity term as CheckNodeAffinity evaluates it:
+        MatchNodeSelectorTerms against a node carrying only the labels, so matchFields never
+        constrain (nodeSelectorTerm.match skips them on empty fields); their parse errors
+        still void the term."""
+        me = term.get("matchExpressions") or []
+        mf = term.get("matchFields") or []
+        if not me and not mf:
+            return None
+        off = len(self._reqs)
+        rows = []
+        try:
+            for e in me:
+                rows.append(self._req(e.get("key", ""), e.get("operator", ""), tuple(e.get("values") or ())))
+            for e in mf:
+                self._field_req(e.get("key", ""), e.get("operator", ""), tuple(e.get("values") or ()))
+        except SelectorError:
+            rows = [(0, abi.KSS_OP_FALSE, 0, 0, 0, 0)]
+        if not rows:
+            rows = [(0, abi.KSS_OP_TRUE, 0, 0, 0, 0)]
+        self._reqs.extend(rows)
+        return (off, len(rows), 0, 0)
+
+    def _compile_volumes(self, j: int, rec):
+        """The pod's VolumeBinding PreFilter status and its volume program (kss/volumes.py)."""
+        rec["vol_off"], rec["vol_len"] = len(self._vols), 0
+        if self.vc is None:
+            return
+        msg, _ = self.vc.prefilter(j)
+        # RunPreFilterPlugins order: NodeAffinity's conflict comes first; a NodeAffinity parse
+        # error of a preferred term surfaces only at PreScore, after this PreFilter
+        if msg is not None and rec["prefilter_status"] != abi.KSS_PF_NODE_AFFINITY_CONFLICT:
+            rec["prefilter_status"] = abi.KSS_PF_VOLUME_BINDING
+            rec["prefilter_msg"] = self.vc.message(msg)
+
+        def pv_terms(terms):
+            off = len(self._terms)
+            for t in terms:
+                tt = self._pv_term(t)
+                if tt is not None:
+                    self._terms.append(tt)
+            return off, len(self._terms) - off
+
+        def zone_reqs(cons):
+            off = len(self._reqs)
+            for key, vals in cons:
+                self._reqs.append(self._req(key, "In", tuple(vals)))
+            return off, len(self._reqs) - off
+
+        prog = self.vc.program(j, pv_terms, zone_reqs)
+        self._vols.extend(prog)
+        rec["vol_len"] = len(prog)
 
     def _classes_matching(self, pred) -> List[int]:
         return [i for i, (ns, lb) in enumerate(self.classes) if pred(ns, dict(lb))]

@@ -43,6 +43,8 @@ SIGNATURES = [
     ("kss_apply_count_delta", C.c_int, [C.c_void_p, P(C.c_int32), P(C.c_int32), P(C.c_int32), C.c_int32, C.c_int32]),
     ("kss_read_node_state", C.c_int, [C.c_void_p, P(C.c_int64), P(C.c_int64), P(C.c_int32), P(C.c_int32), P(C.c_int32)]),
     ("kss_read_port_state", C.c_int, [C.c_void_p, P(C.c_uint64)]),
+    ("kss_read_volume_state", C.c_int, [C.c_void_p, P(C.c_int32), P(C.c_int32)]),
+    ("kss_apply_volume_delta", C.c_int, [C.c_void_p, P(C.c_int32), P(C.c_int32), P(C.c_int32), C.c_int32, C.c_int32]),
     ("kss_apply_port_delta", C.c_int, [C.c_void_p, P(C.c_int32), C.c_int32, P(C.c_uint64)]),
     ("kss_eval_pod", C.c_int, [C.c_void_p, P(abi.PodSet), C.c_int32, P(abi.PodResult)]),
     ("kss_eval_pod_view", C.c_int, [C.c_void_p, P(abi.PodSet), C.c_int32, C.c_uint32, P(abi.PodView)]),
@@ -104,7 +106,7 @@ def lib() -> C.CDLL:
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args
-        if L.kss_abi_version() != 2:
+        if L.kss_abi_version() != 3:
             raise ImportError("libkss ABI version mismatch")
         _lib = L
     return _lib
@@ -189,15 +191,17 @@ def _cstrs(items: Sequence[str]):
     return arr
 
 
-def make_names(node_names, taints, scalars):
-    """Build a kss_names struct; returns (struct, keepalive)."""
+def make_names(node_names, taints, scalars, messages=()):
+    """Build a kss_names struct; returns (struct, keepalive).  messages: the podset's status
+    messages (CompiledPods.messages: VolumeBinding PreFilter, VolumeZone errors)."""
     nn = _cstrs(node_names)
     tk = _cstrs([t[0] for t in taints])
     tv = _cstrs([t[1] for t in taints])
     sc = _cstrs(scalars)
+    ms = _cstrs(list(messages))
     n = abi.Names(C.cast(nn, P(C.c_char_p)), C.cast(tk, P(C.c_char_p)), C.cast(tv, P(C.c_char_p)),
-                  C.cast(sc, P(C.c_char_p)))
-    return n, (nn, tk, tv, sc)
+                  C.cast(sc, P(C.c_char_p)), len(messages), 0, C.cast(ms, P(C.c_char_p)))
+    return n, (nn, tk, tv, sc, ms)
 
 
 def parse_annotations(buf: bytes) -> Dict[str, str]:
@@ -265,6 +269,8 @@ class Context:
         self.n_terms = cluster_struct.n_terms
         self.n_taints = cluster_struct.n_taints
         self.n_scalar = cluster_struct.n_scalar
+        self.n_vol_rows = cluster_struct.n_vol_rows
+        self.n_vol_keys = cluster_struct.n_vol_keys
         if names is not None:
             st, keep = names
             self._keep = keep
@@ -412,6 +418,23 @@ class Context:
         used = np.ascontiguousarray(used, np.uint64)
         check(lib().kss_apply_port_delta(self.h, idx.ctypes.data_as(P(C.c_int32)), len(idx),
                                          used.ctypes.data_as(P(C.c_uint64))))
+
+    def volume_state(self):
+        """(vol_count [rows][N], vol_attached [keys][N]) read back (kss_read_volume_state)."""
+        N = max(self.n_nodes, 1)
+        vc = np.zeros((max(self.n_vol_rows, 1), N), np.int32)
+        va = np.zeros((max(self.n_vol_keys, 1), N), np.int32)
+        check(lib().kss_read_volume_state(self.h, vc.ctypes.data_as(P(C.c_int32)), va.ctypes.data_as(P(C.c_int32))))
+        return vc[:self.n_vol_rows, :self.n_nodes], va[:self.n_vol_keys, :self.n_nodes]
+
+    def apply_volume_delta(self, node, row, value, overwrite=False):
+        """vol_count / vol_attached sync (kss_apply_volume_delta): row r < n_vol_rows is a vol_count
+        row, r >= n_vol_rows the vol_attached key r - n_vol_rows."""
+        node = np.ascontiguousarray(node, np.int32)
+        row = np.ascontiguousarray(row, np.int32)
+        value = np.ascontiguousarray(value, np.int32)
+        check(lib().kss_apply_volume_delta(self.h, node.ctypes.data_as(P(C.c_int32)), row.ctypes.data_as(P(C.c_int32)),
+                                           value.ctypes.data_as(P(C.c_int32)), len(node), 1 if overwrite else 0))
 
     def last_timing(self):
         ms = C.c_double(0)

@@ -55,6 +55,12 @@ class Snapshot:
     pvcs: List[dict] = field(default_factory=list)
     storage_classes: List[dict] = field(default_factory=list)
 
+    def storage(self) -> dict:
+        """The volume plugins' objects for kss.compile (Compiler(storage=...)).  ResourcesForSnap
+        carries no CSINodes (snapshot.go:32-41): CSI attach limits come from allocatable only."""
+        return {"pvs": list(self.pvs), "pvcs": list(self.pvcs), "storage_classes": list(self.storage_classes),
+                "csinodes": []}
+
 
 def _resolve_priority(pod: dict, classes: Dict[str, int], default: Optional[int]) -> dict:
     spec = pod.get("spec") or {}

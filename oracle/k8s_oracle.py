@@ -523,7 +523,10 @@ class Oracle:
 
     def __init__(self, nodes, bound_pods=(), namespaces=None, weights=None, hard_pod_affinity_weight=1,
                  system_defaulted=True, fit_strategy="LeastAllocated", fit_resources=(("cpu", 1), ("memory", 1)),
-                 ba_resources=("cpu", "memory")):
+                 ba_resources=("cpu", "memory"), storage=None):
+        """storage: k8s_volumes.Storage (PVs, PVCs, StorageClasses, CSINodes) for the volume plugins."""
+        import k8s_volumes
+        self.storage = storage if storage is not None else k8s_volumes.Storage()
         self.nodes = node_tree_list(list(nodes))
         self.infos = [NodeInfo(n) for n in self.nodes]
         # NodeInfo.ImageStates as the v1.26 cache builds them while nodes are added (input
@@ -890,10 +893,11 @@ class Oracle:
         return topo
 
     # ----------------------------------------------------------- runFilterPlugins
-    def filter_node(self, pod, ni: NodeInfo, pts_st, ipa_st):
+    def filter_node(self, pod, ni: NodeInfo, pts_st, ipa_st, vb_claims=None):
         """framework.RunFilterPlugins over one NodeInfo: (first failing plugin or None, the
-        per-plugin record up to it)."""
+        per-plugin record up to it).  vb_claims: VolumeBinding's bound claims from PreFilter."""
         node = ni.node
+        st = self.storage
         sp = _spec(pod)
         tols = sp.get("tolerations") or []
         rec = {}
@@ -919,6 +923,16 @@ class Oracle:
                     msg = MSG["NodePorts"]
             elif pl == "NodeResourcesFit":
                 msg = self.fit_filter(pod, ni)
+            elif pl == "VolumeRestrictions":
+                msg = st.restrictions_filter(pod, [pi.pod for pi in ni.pods])
+            elif pl in ("EBSLimits", "GCEPDLimits", "AzureDiskLimits"):
+                msg = st.non_csi_filter(pl, pod, ni)
+            elif pl == "NodeVolumeLimits":
+                msg = st.csi_filter(pod, ni)
+            elif pl == "VolumeBinding":
+                msg = st.binding_filter(vb_claims, node, NodeSelectorTerms)
+            elif pl == "VolumeZone":
+                msg = st.zone_filter(pod, node)
             elif pl == "PodTopologySpread":
                 msg = self.pts_filter(pts_st, pod, node)
             elif pl == "InterPodAffinity":
@@ -957,14 +971,21 @@ class Oracle:
                 names |= tn
             if not conflict and names:
                 node_subset = names
+        vb_claims = None
         for pl in PREFILTERS:
             if pl == "NodeAffinity" and conflict:
                 res["prefilter_status"][pl] = "pod affinity terms conflict"
                 res["status"] = "prefilter"
                 return res
+            if pl == "NodeAffinity" and node_subset is not None:
+                res["prefilter_result"]["NodeAffinity"] = sorted(node_subset)
+            if pl == "VolumeBinding":
+                msg, vb_claims = self.storage.binding_prefilter(pod)
+                if msg is not None:
+                    res["prefilter_status"][pl] = msg
+                    res["status"] = "prefilter"
+                    return res
             res["prefilter_status"][pl] = "success"
-        if node_subset is not None:
-            res["prefilter_result"]["NodeAffinity"] = sorted(node_subset)
         pts_st = self.pts_prefilter(pod)
         ipa_st = self.ipa_prefilter(pod)
         res["_pts_st"], res["_ipa_st"] = pts_st, ipa_st  # the cycle state PostFilter sees
@@ -974,7 +995,7 @@ class Oracle:
             node = ni.node
             if node_subset is not None and _name(node) not in node_subset:
                 continue
-            failed, rec = self.filter_node(pod, ni, pts_st, ipa_st)
+            failed, rec = self.filter_node(pod, ni, pts_st, ipa_st, vb_claims)
             ann_filter[_name(node)] = rec
             res["fail"][i] = failed
             if failed is None:

@@ -79,6 +79,8 @@ typedef struct {
   int32_t* class_count;
   int32_t* term_count;
   uint64_t* port_used;
+  int32_t* vol_count;
+  int32_t* vol_attached;
 } ostate;
 
 static int ostate_init(ostate* s, const kss_cluster* cl) {
@@ -90,7 +92,13 @@ static int ostate_init(ostate* s, const kss_cluster* cl) {
   s->class_count = (int32_t*)malloc(sizeof(int32_t) * ((size_t)cl->n_classes * N + 1));
   s->term_count = (int32_t*)malloc(sizeof(int32_t) * ((size_t)cl->n_terms * N + 1));
   s->port_used = (uint64_t*)calloc(N ? N : 1, sizeof(uint64_t));
-  if (!s->requested || !s->nonzero || !s->pod_count || !s->class_count || !s->term_count || !s->port_used) return -1;
+  s->vol_count = (int32_t*)calloc((size_t)cl->n_vol_rows * N + 1, sizeof(int32_t));
+  s->vol_attached = (int32_t*)calloc((size_t)cl->n_vol_keys * N + 1, sizeof(int32_t));
+  if (!s->requested || !s->nonzero || !s->pod_count || !s->class_count || !s->term_count || !s->port_used ||
+      !s->vol_count || !s->vol_attached)
+    return -1;
+  if (cl->n_vol_rows) memcpy(s->vol_count, cl->vol_count, sizeof(int32_t) * (size_t)cl->n_vol_rows * N);
+  if (cl->n_vol_keys) memcpy(s->vol_attached, cl->vol_attached, sizeof(int32_t) * (size_t)cl->n_vol_keys * N);
   if (cl->port_used) memcpy(s->port_used, cl->port_used, sizeof(uint64_t) * N);
   memcpy(s->requested, cl->requested, sizeof(int64_t) * KSS_NRES * N);
   memcpy(s->nonzero, cl->nonzero, sizeof(int64_t) * 2 * N);
@@ -103,6 +111,8 @@ static int ostate_init(ostate* s, const kss_cluster* cl) {
   s->c.class_count = s->class_count;
   s->c.term_count = s->term_count;
   s->c.port_used = s->port_used;
+  s->c.vol_count = s->vol_count;
+  s->c.vol_attached = s->vol_attached;
   return 0;
 }
 
@@ -113,6 +123,8 @@ static void ostate_free(ostate* s) {
   free(s->class_count);
   free(s->term_count);
   free(s->port_used);
+  free(s->vol_count);
+  free(s->vol_attached);
 }
 
 #define LV(cl, key, n) ((cl)->label_value[(size_t)(key) * (size_t)(cl)->n_nodes + (size_t)(n)])
@@ -363,6 +375,90 @@ static int podstate_build(podstate* st, const kss_cluster* cl, const kss_podset*
 }
 
 /* ---------------------------------------------------------------------------
+ * Volume filters over the pod's volume program (include/kss.h kss_vol; the host resolved
+ * the objects into rows, keys and requirements, kss/volumes.py).  Restated per plugin:
+ *   VolumeRestrictions  volume_restrictions.go satisfyVolumeConflicts: some pod on the node
+ *                       uses a disk one of the pod's volumes conflicts with (isVolumeConflict);
+ *   EBSLimits / GCEPDLimits / AzureDiskLimits  non_csi.go nonCSILimits.Filter:
+ *                       len(existingVolumes) + len(newVolumes \ existingVolumes) > maxAttachLimit,
+ *                       whenever the pod has a volume of the plugin, unless migrated (limit -1);
+ *   NodeVolumeLimits    csi.go CSILimits.Filter: per limit key with new volumes,
+ *                       attachedVolumeCount + newVolumeCount > the node's limit for the key;
+ *   VolumeBinding       binder.go checkBoundClaims: bound claims in order, the first missing
+ *                       PV or PV node-affinity mismatch decides;
+ *   VolumeZone          volume_zone.go Filter: nodes without zone labels pass; otherwise every
+ *                       zone label of the pod's PVs must contain the node's value (volume order).
+ * Returns the plugin id or 0.
+ * ------------------------------------------------------------------------- */
+static int limit_check(const kss_cluster* cl, uint32_t en, int key, int n, int64_t newc) {
+  size_t N = (size_t)cl->n_nodes;
+  int pl = cl->vol_key_plugin[key];
+  int32_t lim = cl->vol_limit[(size_t)key * N + n];
+  if (!((en >> pl) & 1u) || lim < 0) return 0;
+  if (pl == KSS_F_NODE_VOLUME_LIMITS && newc == 0) return 0; /* only keys in newVolumeCount */
+  return (int64_t)cl->vol_attached[(size_t)key * N + n] + newc > (int64_t)lim ? pl : 0;
+}
+
+static int volume_filters(const kss_cluster* cl, const kss_podset* ps, const kss_pod* p, uint32_t en, int n,
+                          uint16_t* detail) {
+  size_t N = (size_t)cl->n_nodes;
+  int zone_node = (cl->node_flags[n] & KSS_NODE_VOLUME_ZONE) != 0;
+  int cur = -1, r;
+  int64_t newc = 0;
+  for (int e = 0; e < p->vol_len; e++) {
+    const kss_vol* v = &ps->vols[p->vol_off + e];
+    if (v->kind != KSS_VOL_LIMIT && cur >= 0) {
+      if ((r = limit_check(cl, en, cur, n, newc))) return r;
+      cur = -1;
+    }
+    if (v->kind == KSS_VOL_CONFLICT) {
+      if (((en >> KSS_F_VOLUME_RESTRICTIONS) & 1u) && cl->vol_count[(size_t)v->row * N + n] > 0)
+        return KSS_F_VOLUME_RESTRICTIONS;
+    } else if (v->kind == KSS_VOL_LIMIT) {
+      if (v->key != cur) {
+        if (cur >= 0 && (r = limit_check(cl, en, cur, n, newc))) return r;
+        cur = v->key;
+        newc = 0;
+      }
+      if (v->row >= 0)
+        newc += cl->vol_count[(size_t)v->row * N + n] == 0 ? 1 : 0; /* delete(newVolumes, attached) */
+      else
+        newc += v->count;
+    } else if (v->kind == KSS_VOL_BIND_AFFINITY) {
+      if ((en >> KSS_F_VOLUME_BINDING) & 1u) {
+        int ok = 0;
+        for (int t = 0; t < v->b && !ok; t++) ok = term_matches(cl, ps, &ps->terms[v->a + t], n);
+        if (!ok) {
+          *detail = KSS_VB_NODE_CONFLICT;
+          return KSS_F_VOLUME_BINDING;
+        }
+      }
+    } else if (v->kind == KSS_VOL_BIND_PV_MISSING) {
+      if ((en >> KSS_F_VOLUME_BINDING) & 1u) {
+        *detail = KSS_VB_PV_NOT_EXIST;
+        return KSS_F_VOLUME_BINDING;
+      }
+    } else if (v->kind == KSS_VOL_ZONE) {
+      if (((en >> KSS_F_VOLUME_ZONE) & 1u) && zone_node)
+        for (int k = 0; k < v->b; k++)
+          if (!req_matches(cl, ps, &ps->reqs[v->a + k], n)) {
+            *detail = 0;
+            return KSS_F_VOLUME_ZONE;
+          }
+    } else if (v->kind == KSS_VOL_ZONE_ERROR) {
+      if (((en >> KSS_F_VOLUME_ZONE) & 1u) && zone_node) {
+        *detail = (uint16_t)(1 + v->a);
+        return KSS_F_VOLUME_ZONE;
+      }
+    } else {
+      break; /* AssumePod entries */
+    }
+  }
+  if (cur >= 0) return limit_check(cl, en, cur, n, newc);
+  return 0;
+}
+
+/* ---------------------------------------------------------------------------
  * Filter chain for one node (RunFilterPlugins, first failure wins).
  * Returns the failing plugin id (0 = pass) and sets *detail.
  * ------------------------------------------------------------------------- */
@@ -421,6 +517,10 @@ static int filter_node(const kss_profile* prof, const kss_cluster* cl, const kss
   }
   /* VolumeRestrictions, EBSLimits, GCEPDLimits, NodeVolumeLimits, AzureDiskLimits, VolumeBinding,
      VolumeZone: volume-less pods pass. */
+  if (p->vol_len > 0) {
+    int r = volume_filters(cl, ps, p, en, n, detail);
+    if (r) return r;
+  }
   /* PodTopologySpread.Filter */
   if (((en >> KSS_F_POD_TOPOLOGY_SPREAD) & 1u) && p->n_hard > 0) {
     const kss_spread* hard = ps->spreads + p->spread_off;
@@ -637,7 +737,7 @@ static int schedule_one(const kss_profile* prof, ostate* s, const kss_podset* ps
   }
 
   if (p->prefilter_status != 0) {
-    out->status = p->prefilter_status == 1 ? 2 : 3;
+    out->status = p->prefilter_status == KSS_PF_ERROR ? 3 : 2;
     goto done;
   }
   rc = podstate_build(&st, cl, ps, p, prof->hard_pod_affinity_weight);
@@ -879,6 +979,18 @@ static void commit(ostate* s, const kss_podset* ps, int pi, int node_local) {
   if (p->cls >= 0) s->class_count[(size_t)p->cls * N + node_local] += 1;
   for (int i = 0; i < p->own_terms_len; i++) s->term_count[(size_t)ps->ints[p->own_terms_off + i] * N + node_local] += 1;
   s->port_used[node_local] |= p->port_add; /* NodeInfo.AddPod updateUsedPorts */
+  /* the pod's volumes join NodeInfo.Pods: a row counts the pod; its key counts the volume once */
+  for (int e = 0; e < p->vol_len; e++) {
+    const kss_vol* v = &ps->vols[p->vol_off + e];
+    if (v->kind == KSS_VOL_OWN) {
+      int key = s->c.vol_row_key[v->row];
+      int32_t* cnt = &s->vol_count[(size_t)v->row * N + node_local];
+      if (key >= 0 && *cnt == 0) s->vol_attached[(size_t)key * N + node_local] += 1;
+      *cnt += 1;
+    } else if (v->kind == KSS_VOL_OWN_PRIVATE) {
+      s->vol_attached[(size_t)v->key * N + node_local] += v->count;
+    }
+  }
 }
 
 /* ---------------------------------------------------------------------------
@@ -899,10 +1011,11 @@ int kss_oracle_eval_pod(const kss_profile* prof, const kss_cluster* cl, const ks
  * results (optional) is an array of n kss_pod_result whose arrays the caller
  * allocated (any NULL array is skipped).  Final node state is written back to
  * the optional out_* arrays. */
-int kss_oracle_schedule(const kss_profile* prof, const kss_cluster* cl, const kss_podset* ps, int n,
-                        int32_t* chosen, kss_pod_result* results, int threads, int64_t* out_requested,
-                        int64_t* out_nonzero, int32_t* out_pod_count, int32_t* out_class_count,
-                        int32_t* out_term_count, uint64_t* out_port_used) {
+int kss_oracle_schedule_v(const kss_profile* prof, const kss_cluster* cl, const kss_podset* ps, int n,
+                          int32_t* chosen, kss_pod_result* results, int threads, int64_t* out_requested,
+                          int64_t* out_nonzero, int32_t* out_pod_count, int32_t* out_class_count,
+                          int32_t* out_term_count, uint64_t* out_port_used, int32_t* out_vol_count,
+                          int32_t* out_vol_attached) {
   ostate s;
   if (ostate_init(&s, cl)) return KSS_E_NOMEM;
   int th = threads > 0 ? threads : 1;
@@ -924,8 +1037,19 @@ int kss_oracle_schedule(const kss_profile* prof, const kss_cluster* cl, const ks
     memcpy(out_class_count, s.class_count, sizeof(int32_t) * (size_t)cl->n_classes * N);
   if (out_term_count && cl->n_terms) memcpy(out_term_count, s.term_count, sizeof(int32_t) * (size_t)cl->n_terms * N);
   if (out_port_used) memcpy(out_port_used, s.port_used, sizeof(uint64_t) * N);
+  if (out_vol_count && cl->n_vol_rows) memcpy(out_vol_count, s.vol_count, sizeof(int32_t) * (size_t)cl->n_vol_rows * N);
+  if (out_vol_attached && cl->n_vol_keys)
+    memcpy(out_vol_attached, s.vol_attached, sizeof(int32_t) * (size_t)cl->n_vol_keys * N);
   ostate_free(&s);
   return rc;
+}
+
+int kss_oracle_schedule(const kss_profile* prof, const kss_cluster* cl, const kss_podset* ps, int n,
+                        int32_t* chosen, kss_pod_result* results, int threads, int64_t* out_requested,
+                        int64_t* out_nonzero, int32_t* out_pod_count, int32_t* out_class_count,
+                        int32_t* out_term_count, uint64_t* out_port_used) {
+  return kss_oracle_schedule_v(prof, cl, ps, n, chosen, results, threads, out_requested, out_nonzero, out_pod_count,
+                               out_class_count, out_term_count, out_port_used, NULL, NULL);
 }
 
 int kss_oracle_max_threads(void) {

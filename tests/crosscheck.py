@@ -9,13 +9,19 @@ from kss.compile import compile_cluster
 FILTER_CODE = {name: i for i, name in enumerate(abi.FILTER_PLUGINS) if name}
 
 
-def run_both(nodes, bound, pods, n_check=None):
-    """Schedule `pods` sequentially with both oracles and assert identical per-pod results."""
-    cc, cp, comp = compile_cluster(nodes, bound, pods)
+def run_both(nodes, bound, pods, n_check=None, storage=None):
+    """Schedule `pods` sequentially with both oracles and assert identical per-pod results.
+    storage: {"pvs", "pvcs", "storage_classes", "csinodes"} for the volume plugins."""
+    cc, cp, comp = compile_cluster(nodes, bound, pods, storage=storage)
     prof = abi.default_profile()
     chosen, res, _ = oracle_c.schedule(prof, cc.as_struct(), cp.as_struct(), cp.n, cc.n_nodes,
                                        n_classes=len(cc.classes), n_terms=len(cc.terms))
-    o = k8s_oracle.Oracle(nodes, bound)
+    st = None
+    if storage:
+        import k8s_volumes
+        st = k8s_volumes.Storage(storage.get("pvs") or (), storage.get("pvcs") or (),
+                                 storage.get("storage_classes") or (), storage.get("csinodes") or ())
+    o = k8s_oracle.Oracle(nodes, bound, storage=st)
     assert [k8s_oracle._name(n) for n in o.nodes] == cc.node_names
     n_check = len(pods) if n_check is None else n_check
     for j in range(n_check):

@@ -23,6 +23,8 @@ def lib():
                                              P(C.c_int32), P(abi.PodResult), C.c_int, P(C.c_int64), P(C.c_int64),
                                              P(C.c_int32), P(C.c_int32), P(C.c_int32), P(C.c_uint64)]
         _lib.kss_oracle_schedule.restype = C.c_int
+        _lib.kss_oracle_schedule_v.argtypes = _lib.kss_oracle_schedule.argtypes + [P(C.c_int32), P(C.c_int32)]
+        _lib.kss_oracle_schedule_v.restype = C.c_int
         _lib.kss_oracle_eval_pod.argtypes = [P(abi.Profile), P(abi.Cluster), P(abi.PodSet), C.c_int,
                                              P(abi.PodResult), C.c_int]
         _lib.kss_oracle_eval_pod.restype = C.c_int
@@ -69,14 +71,20 @@ def schedule(profile, cluster_struct, podset_struct, n_pods, n_nodes, threads=1,
     N = max(n_nodes, 1)
     st = dict(requested=np.zeros((abi.KSS_NRES, N), np.int64), nonzero=np.zeros((2, N), np.int64),
               pod_count=np.zeros(N, np.int32), class_count=np.zeros((max(n_classes, 1), N), np.int32),
-              term_count=np.zeros((max(n_terms, 1), N), np.int32), port_used=np.zeros(N, np.uint64))
+              term_count=np.zeros((max(n_terms, 1), N), np.int32), port_used=np.zeros(N, np.uint64),
+              vol_count=np.zeros((max(cluster_struct.n_vol_rows, 1), N), np.int32),
+              vol_attached=np.zeros((max(cluster_struct.n_vol_keys, 1), N), np.int32))
     P = C.POINTER
-    rc = L.kss_oracle_schedule(C.byref(profile), C.byref(cluster_struct), C.byref(podset_struct), n_pods,
+    rc = L.kss_oracle_schedule_v(C.byref(profile), C.byref(cluster_struct), C.byref(podset_struct), n_pods,
                                chosen.ctypes.data_as(P(C.c_int32)), res.structs if res else None, threads,
                                st["requested"].ctypes.data_as(P(C.c_int64)), st["nonzero"].ctypes.data_as(P(C.c_int64)),
                                st["pod_count"].ctypes.data_as(P(C.c_int32)),
                                st["class_count"].ctypes.data_as(P(C.c_int32)),
                                st["term_count"].ctypes.data_as(P(C.c_int32)),
-                               st["port_used"].ctypes.data_as(P(C.c_uint64)))
+                               st["port_used"].ctypes.data_as(P(C.c_uint64)),
+                               st["vol_count"].ctypes.data_as(P(C.c_int32)),
+                               st["vol_attached"].ctypes.data_as(P(C.c_int32)))
     assert rc == 0, f"oracle rc={rc}"
+    st["vol_count"] = st["vol_count"][:cluster_struct.n_vol_rows, :n_nodes]
+    st["vol_attached"] = st["vol_attached"][:cluster_struct.n_vol_keys, :n_nodes]
     return chosen[:n_pods], res, st

@@ -32,7 +32,7 @@ def test_struct_sizes_match_ctypes_mirror():
     out = (C.c_int32 * 16)()
     k = L.kss_abi_sizes(out, 16)
     mirror = [abi.Cluster, abi.Req, abi.Term, abi.Spread, abi.Ipa, abi.Pod, abi.PodSet, abi.Profile, abi.PodResult,
-              abi.Config, abi.Names, abi.Synth, abi.Boundset, abi.PreemptResult]
+              abi.Config, abi.Names, abi.Synth, abi.Boundset, abi.PreemptResult, abi.Vol]
     assert k == len(mirror)
     for i, t in enumerate(mirror):
         assert out[i] == C.sizeof(t), (t.__name__, out[i], C.sizeof(t))

@@ -15,7 +15,7 @@ GOLD = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "readme_
 
 
 def _format_from_oracle(cc, cp, res, j, prof, pod_aware=False):
-    names, keep = native.make_names(cc.node_names, cc.taints, cc.scalars)
+    names, keep = native.make_names(cc.node_names, cc.taints, cc.scalars, cp.messages)
     r = native.PodResult(cc.n_nodes)
     r.fail_plugin[:] = res.fail_plugin[j]
     r.fail_detail[:] = res.fail_detail[j]

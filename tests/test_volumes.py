@@ -1,0 +1,121 @@
+"""The volume plugins on CPU: both oracles (object-level oracle/k8s_volumes.py and the SoA-level
+C oracle over kss/volumes.py's compiled programs) and the lazy annotation formatter against
+the hand-derived fixtures of tests/volume_fixtures.py (disk conflicts, the in-tree and CSI
+attach limits, VolumeBinding PreFilter / Filter, VolumeZone), and against each other on
+random clusters with volumes (tests/volume_fuzz.py)."""
+import json
+
+import pytest
+
+import edge_fixtures as ef
+import k8s_oracle
+import k8s_volumes
+import volume_fixtures as vf
+from crosscheck import run_both
+from kss import abi
+from kss.compile import Unsupported, compile_cluster
+from test_format import _format_from_oracle
+
+
+def _oracle(nodes, bound, st):
+    return k8s_oracle.Oracle(nodes, bound, storage=k8s_volumes.Storage(
+        st["pvs"], st["pvcs"], st["storage_classes"], st["csinodes"]))
+
+
+@pytest.mark.parametrize("name", sorted(vf.FIXTURES))
+def test_object_oracle_matches_hand_derived(name):
+    nodes, bound, pods, expect, st = vf.FIXTURES[name]()
+    o = _oracle(nodes, bound, st)
+    for j, (p, exp) in enumerate(zip(pods, expect)):
+        ef.check_expect(o.annotations(o.schedule_one(p)), exp, where=(name, j))
+
+
+@pytest.mark.parametrize("name", sorted(vf.FIXTURES))
+def test_c_oracle_and_formatter_match_hand_derived(name):
+    nodes, bound, pods, expect, st = vf.FIXTURES[name]()
+    cc, cp, chosen, res = run_both(nodes, bound, pods, storage=st)  # the two oracles agree first
+    prof = abi.default_profile()
+    o = _oracle(nodes, bound, st)
+    for j, exp in enumerate(expect):
+        ann = _format_from_oracle(cc, cp, res, j, prof, pod_aware=True)
+        assert ann == o.annotations(o.schedule_one(pods[j])), (name, j)  # all 13 values, byte for byte
+        ef.check_expect(ann, exp, where=(name, j))
+
+
+def test_every_volume_reason_is_covered():
+    seen, pre = set(), set()
+    for fx in vf.FIXTURES.values():
+        for exp in fx()[3]:
+            seen.update(f[1] for f in exp["filter"].values() if f is not None)
+            st = (exp.get("extra") or {}).get("scheduler-simulator/prefilter-result-status")
+            if st:
+                pre.add(st["VolumeBinding"])
+    for msg in (vf.M_DISK, vf.M_MAXVOL, vf.M_VB_CONFLICT, vf.M_VB_NOPV, vf.M_ZONE):
+        assert msg in seen, msg
+    assert vf.M_UNBOUND in pre
+    plugins = {f[0] for fx in vf.FIXTURES.values() for exp in fx()[3] for f in exp["filter"].values() if f}
+    assert {"VolumeRestrictions", "EBSLimits", "GCEPDLimits", "NodeVolumeLimits", "AzureDiskLimits",
+            "VolumeBinding", "VolumeZone"} <= plugins
+
+
+def test_volume_rows_and_keys():
+    """Shared volumes get vol_count rows, private ones count on the chosen node only; the
+    attach-limit keys follow the plugin order."""
+    nodes, bound, pods, _, st = vf.fx_csi_limits()
+    cc, cp, _ = compile_cluster(nodes, bound, pods, storage=st)
+    assert cc.vol_keys == ["attachable-volumes-csi-ebs.csi.aws.com"]
+    shared = sorted(u for kind, (k, u) in cc.vol_rows if kind == "vol")
+    assert shared == ["ebs.csi.aws.com/h-1", "ebs.csi.aws.com/h-2", "ebs.csi.aws.com/h-3"]
+    a = cc.arrays
+    assert list(a["vol_attached"][0]) == [1, 1, 0]  # x's h-1 on a, y's unbound u-1 on b
+    assert list(a["vol_limit"][0]) == [1, 3, -1]
+
+
+def test_refusals():
+    nodes = [ef.node("a")]
+    wffc = {"metadata": {"name": "late"}, "provisioner": "x", "volumeBindingMode": "WaitForFirstConsumer"}
+    st = vf.storage(pvcs=[vf.pvc("u", bound=False, sc="late")], scs=[wffc])
+    with pytest.raises(Unsupported, match="WaitForFirstConsumer"):
+        compile_cluster(nodes, [], [vf.vpod("p", vf.claim("u"))], storage=st)
+    mig = [{"metadata": {"name": "a", "annotations": {"storage.alpha.kubernetes.io/migrated-plugins":
+                                                      "kubernetes.io/aws-ebs"}}, "spec": {"drivers": []}}]
+    with pytest.raises(Unsupported, match="migrated"):
+        compile_cluster(nodes, [], [vf.vpod("p", vf.ebs("v"))], storage=vf.storage(csinodes=mig))
+
+
+def test_long_csi_driver_key():
+    """GetCSIAttachLimitKey: names reaching 63 characters keep 23 characters and 16 hex of sha1."""
+    from kss.volumes import csi_attach_limit_key
+    d = "a-very-long-csi-driver-name.storage.example.com"
+    k = csi_attach_limit_key(d)
+    assert k == k8s_volumes.csi_attach_limit_key(d)
+    assert k.startswith("attachable-volumes-csi-a-very-long-csi-driver") and len(k) == 23 + 23 + 16
+    assert csi_attach_limit_key("ebs.csi.aws.com") == "attachable-volumes-csi-ebs.csi.aws.com"
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_oracles_agree_on_random_volume_clusters(seed):
+    """The object-level restatement (objects, NodeInfo.Pods re-read per filter call) and the
+    C oracle over the compiled volume rows agree on every per-node verdict, score and
+    choice, pod after pod (each AssumePod visible to the next pod)."""
+    import volume_fuzz
+    nodes, bound, pods, st = volume_fuzz.make(seed)
+    cc, cp, chosen, res = run_both(nodes, bound, pods, storage=st)
+    fails = {int(f) for f in res.fail_plugin.ravel()}
+    assert cp.n_vols > 0 and len(cc.vol_rows) > 0
+    if seed == 0:  # the generator reaches the volume plugins' failures
+        assert fails & {abi.KSS_F_VOLUME_RESTRICTIONS, abi.KSS_F_VOLUME_BINDING, abi.KSS_F_VOLUME_ZONE}
+
+
+def test_snapshot_round_trip_with_volumes():
+    """ResourcesForSnap (snapshot.go:32-41) carries pvs / pvcs / storageClasses: written, read
+    back and compiled, it schedules like the objects it came from."""
+    from kss import snapshot
+    import volume_fuzz
+    nodes, bound, pods, st = volume_fuzz.make(5)
+    snap = snapshot.Snapshot(nodes=nodes, bound=bound, pending=pods, namespaces={"default": {}},
+                             pvs=st["pvs"], pvcs=st["pvcs"], storage_classes=st["storage_classes"])
+    back = snapshot.read_snapshot(json.dumps(snapshot.write_snapshot(snap)))
+    st2 = back.storage()
+    assert st2["pvs"] == st["pvs"] and st2["pvcs"] == st["pvcs"]
+    run_both(back.nodes, back.bound, back.pending, storage=st2)
