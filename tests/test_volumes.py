@@ -119,3 +119,12 @@ def test_snapshot_round_trip_with_volumes():
     st2 = back.storage()
     assert st2["pvs"] == st["pvs"] and st2["pvcs"] == st["pvcs"]
     run_both(back.nodes, back.bound, back.pending, storage=st2)
+
+
+def test_plan_names_volumes():
+    """kss_plan_podset (host only): volume programs keep a batch on k_schedule, and say so."""
+    from kss import native
+    nodes, bound, pods, _, st = vf.fx_volume_zone()
+    cc, cp, _ = compile_cluster(nodes, bound, pods, storage=st)
+    plan = native.plan_podset(cc.as_struct(), cp.as_struct())
+    assert plan["kernel"] == "k_schedule" and "volumes" in plan["reason"], plan
