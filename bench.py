@@ -553,6 +553,40 @@ def run_per_pod(args):
     ctx.reset()
     elapsed_view, ev_view, _, chosen_view = loop(_ViewCall())
     assert chosen_view == chosen
+
+    # the persistent service grid (kss_service_*): the staged pods by index, one command per
+    # call through a pinned ring, no launch / upload / stream synchronisation per pod
+    ctx.reset()
+    ctx.stage(s.pods)
+    sview = abi.PodView()
+
+    def svc_loop(fields):
+        t_eval, t_commit, ch = [], [], []
+        t0 = time.perf_counter()
+        for j in range(n_pods):
+            a = time.perf_counter()
+            native.check(native.lib().kss_service_eval(ctx.h, j, fields, ctypes.byref(sview)))
+            b = time.perf_counter()
+            if sview.chosen >= 0:
+                native.check(native.lib().kss_service_commit(ctx.h, j, sview.chosen))
+            c = time.perf_counter()
+            t_eval.append(b - a)
+            t_commit.append(c - b)
+            ch.append(sview.chosen)
+        el = time.perf_counter() - t0
+        ctx.service_stop()
+        return el, np.array(t_eval) * 1e6, np.array(t_commit) * 1e6, ch
+
+    for j in range(min(args.warmup * 20, n_pods)):  # start the grid, warm it
+        native.check(native.lib().kss_service_eval(ctx.h, j, abi.KSS_FIELD_ALL, ctypes.byref(sview)))
+    ctx.service_stop()
+    ctx.reset()
+    elapsed_svc, ev_svc, cm_svc, chosen_svc = svc_loop(abi.KSS_FIELD_ALL)
+    assert chosen_svc == chosen, "service choices differ from kss_eval_pod's"
+    ctx.reset()
+    slim_fields = abi.KSS_FIELD_FAIL | abi.KSS_FIELD_DETAIL | abi.KSS_FIELD_TOTAL
+    elapsed_svc_slim, ev_svc_slim, _, chosen_svc_slim = svc_loop(slim_fields)
+    assert chosen_svc_slim == chosen
     out = {
         "metric": "per-pod API: kss_eval_pod + kss_commit latency (pods/sec in value)",
         "value": n_pods / elapsed,
@@ -577,6 +611,16 @@ def run_per_pod(args):
                          "fields": "all, in place (kss_eval_pod_view: no copy into caller arrays)",
                          "pods_per_s": n_pods / elapsed_view},
         "commit_us": {"median": float(np.median(cm)), "mean": float(cm.mean()), "p90": float(np.percentile(cm, 90))},
+        "service": {"api": "kss_service_eval + kss_service_commit (resident grid, pinned command ring)",
+                    "pods_per_s": n_pods / elapsed_svc,
+                    "eval_us": {"median": float(np.median(ev_svc)), "mean": float(ev_svc.mean()),
+                                "p90": float(np.percentile(ev_svc, 90)), "fields": "all, in place"},
+                    "commit_us": {"median": float(np.median(cm_svc)), "mean": float(cm_svc.mean()),
+                                  "p90": float(np.percentile(cm_svc, 90))},
+                    "slim": {"pods_per_s": n_pods / elapsed_svc_slim, "fields": "fail_plugin, fail_detail, total",
+                             "eval_us": {"median": float(np.median(ev_svc_slim)), "mean": float(ev_svc_slim.mean()),
+                                         "p90": float(np.percentile(ev_svc_slim, 90))}},
+                    "geometry": ctx.last_geometry()},
         "eval_device_ms_last": ctx.last_timing()[0],
         "geometry": ctx.last_geometry(),
         "pods_scheduled": int(sum(1 for c in chosen if c >= 0)),

@@ -469,6 +469,28 @@ typedef struct kss_pod_view {
   int32_t status;
 } kss_pod_view;
 int kss_eval_pod_view(kss_ctx* ctx, const kss_podset* ps, int32_t pod_index, uint32_t fields, kss_pod_view* out);
+/* The per-pod path as a persistent service grid: the shape wrappedPlugin.PreFilter ->
+ * evaluate, Reserve -> AssumePod, Unreserve -> ForgetPod drives
+ * (simulator/scheduler/plugin/wrappedplugin.go:491-518, 616-645) without a kernel launch, an
+ * upload or a stream synchronisation per call.  One grid stays resident on the context's
+ * device and takes commands from a ring in pinned host memory; the pods are the staged ones
+ * (kss_stage_pods: their programs already in HBM), named by index.
+ *   kss_service_eval    evaluates pod_index on the current state (filters, raw and normalised
+ *                       scores, totals, the selectHost choice): the record fields asked for
+ *                       land in a pinned host buffer and `out` points into it (valid until the
+ *                       next service call); returns when the record is complete
+ *   kss_service_commit  AssumePod of pod_index on node (queued: returns at once; the next
+ *                       evaluation sees it), kss_service_rollback its ForgetPod
+ *   kss_service_start / kss_service_stop  explicit start (the first eval / commit starts the
+ *                       grid too) and stop.  The grid leaves by itself after ~1 s without a
+ *                       command and is restarted by the next call.  Every other entry point
+ *                       that touches the context's device state stops it first.
+ * Results equal kss_eval_pod_view / kss_commit / kss_rollback on the same state. */
+int kss_service_start(kss_ctx* ctx);
+int kss_service_stop(kss_ctx* ctx);
+int kss_service_eval(kss_ctx* ctx, int32_t pod_index, uint32_t fields, kss_pod_view* out);
+int kss_service_commit(kss_ctx* ctx, int32_t pod_index, int32_t node);
+int kss_service_rollback(kss_ctx* ctx, int32_t pod_index, int32_t node);
 /* commit pod ps.pods[pod_index] to node (AssumePod); rollback undoes it (Unreserve/ForgetPod).
  * The deltas travel in the kernel's arguments (no upload). */
 int kss_commit(kss_ctx* ctx, const kss_podset* ps, int32_t pod_index, int32_t node);

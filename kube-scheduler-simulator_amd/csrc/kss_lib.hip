@@ -97,6 +97,8 @@ struct DevJob {
 
 }  // namespace
 
+#include "kss_service.cuh"
+
 // ---------------------------------------------------------------------------
 // kernels
 // ---------------------------------------------------------------------------
@@ -164,6 +166,19 @@ __global__ __launch_bounds__(KSS_MAX_THREADS) void k_schedule(const DevJob* __re
     KSS_STAMP(S, 6);
   }
   if (c.nc64 && job.commit) cache_writeback(c, S.hi);
+}
+
+// The per-pod service grid (kss_service.cuh): W shards of one cluster, commands from the
+// pinned ring starting at command `seq`.
+template <bool GEN>
+__global__ __launch_bounds__(KSS_MAX_THREADS) void k_service(const DevJob* __restrict__ jobs, kss_profile prof, int W,
+                                                             int npt, int bins_cap, int cache_keys,
+                                                             unsigned long long* gran, int* err, SvcBox* box,
+                                                             unsigned long long* relay, unsigned long long* seen,
+                                                             uint8_t* rec_host, unsigned long long seq) {
+  extern __shared__ __attribute__((aligned(16))) long long smem[];
+  const DevJob job = jobs[0];
+  service_loop<GEN>(job.c, job, prof, W, npt, bins_cap, cache_keys, gran, err, box, relay, seen, rec_host, seq, 0u, smem);
 }
 
 // grid = n_jobs * W, as k_schedule; each shard's nodes live in LDS (cap slots).
@@ -486,6 +501,21 @@ struct kss_ctx {
   bool state_unknown = false;
   DevBuf bound_buf, pre_buf;
   DevBound bound_dev{};
+  // the per-pod service grid (kss_service_*, kss_service.cuh)
+  struct Service {
+    bool running = false;          // launched and not known to have left
+    hipStream_t stream = nullptr;  // its own stream (the ctx stream stays free for the copies)
+    SvcBox* box = nullptr;         // pinned, coherent: ring, head, consumed, done flags, outcome
+    uint8_t* rec = nullptr;        // pinned, coherent: the record (SlotLayout(N)), written by the grid
+    uint8_t* rec_dev = nullptr;    // its device address
+    SvcBox* box_dev = nullptr;
+    size_t rec_bytes = 0;
+    DevBuf relay, gran, err, job;  // device relay ring + seen counters, granules, error word, DevJob
+    unsigned long long posted = 0; // commands written to the ring
+    int W = 0, threads = 0, npt = 0, bins_cap = 0, cache_keys = -1;
+    size_t shmem = 0;
+    bool gen = false;
+  } svc;
   // split grid (kss_split_*): this context runs part split_part of split_n, split_wl shards
   // each; split_inbox is its exchange inbox (uncached device memory, zeroed once), split_peer
   // every part's inbox as addressable here (IPC-mapped for other processes / GPUs)
@@ -1231,6 +1261,17 @@ int check_profile(const kss_profile* prof) {
 
 }  // namespace
 
+static int svc_stop(kss_ctx* ctx);
+static void svc_free(kss_ctx* ctx);
+
+// Entry points that use the device state themselves stop the service first.
+#define KSS_SVC_QUIESCE(ctx)                    \
+  do {                                          \
+    if ((ctx) && (ctx)->svc.running) {          \
+      if (int rc_ = svc_stop(ctx)) return rc_;  \
+    }                                           \
+  } while (0)
+
 // ---------------------------------------------------------------------------
 // C ABI
 // ---------------------------------------------------------------------------
@@ -1293,6 +1334,8 @@ static void split_release(kss_ctx* ctx);
 void kss_destroy(kss_ctx* ctx) {
   if (!ctx) return;
   hipSetDevice(ctx->cfg.device);
+  svc_stop(ctx);
+  svc_free(ctx);
   if (ctx->stream) hipStreamSynchronize(ctx->stream);
   ctx->cluster_buf.release();
   ctx->pristine_buf.release();
@@ -1325,6 +1368,7 @@ void kss_destroy(kss_ctx* ctx) {
 }
 
 int kss_load_cluster(kss_ctx* ctx, const kss_cluster* cl) {
+  KSS_SVC_QUIESCE(ctx);
   if (!ctx) return fail(KSS_E_INVAL, "null ctx");
   int rc = check_cluster(cl);
   if (rc) return rc;
@@ -1478,6 +1522,7 @@ static dim3 axis_grid(kss_ctx* ctx) {
 int kss_axis_eval(kss_ctx* ctx, int32_t pod_index, int64_t* stats_dev, const int64_t* prev_key_dev,
                   const int64_t* prev_gathered_dev, int32_t world, int64_t* key_zero_dev, int32_t* chosen_dev,
                   void* stream) {
+  KSS_SVC_QUIESCE(ctx);
   int rc = axis_check(ctx, pod_index);
   if (rc) return rc;
   if (!stats_dev || !key_zero_dev || world < 1) return fail(KSS_E_INVAL, "bad eval arguments");
@@ -1501,6 +1546,7 @@ int kss_axis_eval(kss_ctx* ctx, int32_t pod_index, int64_t* stats_dev, const int
 
 int kss_axis_select(kss_ctx* ctx, const int64_t* gathered_dev, int32_t world, int64_t* key_dev, int64_t* stats_zero_dev,
                     void* stream) {
+  KSS_SVC_QUIESCE(ctx);
   int rc = axis_check(ctx, 0);
   if (rc) return rc;
   if (!gathered_dev || !key_dev || !stats_zero_dev || world < 1) return fail(KSS_E_INVAL, "bad select arguments");
@@ -1515,6 +1561,7 @@ int kss_axis_select(kss_ctx* ctx, const int64_t* gathered_dev, int32_t world, in
 
 int kss_axis_commit(kss_ctx* ctx, int32_t pod_index, const int64_t* key_dev, const int64_t* gathered_dev, int32_t world,
                     int32_t* chosen_dev, void* stream) {
+  KSS_SVC_QUIESCE(ctx);
   int rc = axis_check(ctx, pod_index);
   if (rc) return rc;
   if (!key_dev || !gathered_dev || world < 1) return fail(KSS_E_INVAL, "bad commit arguments");
@@ -1532,6 +1579,7 @@ int kss_axis_commit(kss_ctx* ctx, int32_t pod_index, const int64_t* key_dev, con
 }
 
 int kss_reset_node_state(kss_ctx* ctx) {
+  KSS_SVC_QUIESCE(ctx);
   if (!ctx || !ctx->loaded) return fail(KSS_E_INVAL, "no cluster loaded");
   std::lock_guard<std::mutex> lk(ctx->mu);
   HIP_TRY(hipSetDevice(ctx->cfg.device));
@@ -1552,6 +1600,7 @@ int kss_reset_node_state(kss_ctx* ctx) {
 
 int kss_apply_node_delta(kss_ctx* ctx, const int32_t* idx, int32_t n, const int64_t* requested, const int64_t* nonzero,
                          const int32_t* pod_count) {
+  KSS_SVC_QUIESCE(ctx);
   if (!ctx || !ctx->loaded) return fail(KSS_E_INVAL, "no cluster loaded");
   if (n < 0 || (n > 0 && (!idx || !requested || !nonzero || !pod_count))) return fail(KSS_E_INVAL, "bad arguments");
   if (n == 0) return 0;
@@ -1595,6 +1644,7 @@ int kss_apply_node_delta(kss_ctx* ctx, const int32_t* idx, int32_t n, const int6
 
 int kss_apply_count_delta(kss_ctx* ctx, const int32_t* node, const int32_t* row, const int32_t* value, int32_t n,
                           int32_t mode) {
+  KSS_SVC_QUIESCE(ctx);
   if (!ctx || !ctx->loaded) return fail(KSS_E_INVAL, "no cluster loaded");
   if (n < 0 || (n > 0 && (!node || !row || !value)) || (mode != 0 && mode != 1)) return fail(KSS_E_INVAL, "bad arguments");
   if (n == 0) return 0;
@@ -1632,6 +1682,7 @@ int kss_apply_count_delta(kss_ctx* ctx, const int32_t* node, const int32_t* row,
 
 int kss_read_node_state(kss_ctx* ctx, int64_t* requested, int64_t* nonzero, int32_t* pod_count, int32_t* class_count,
                         int32_t* term_count) {
+  KSS_SVC_QUIESCE(ctx);
   if (!ctx || !ctx->loaded) return fail(KSS_E_INVAL, "no cluster loaded");
   std::lock_guard<std::mutex> lk(ctx->mu);
   HIP_TRY(hipSetDevice(ctx->cfg.device));
@@ -1665,6 +1716,7 @@ static void split_release(kss_ctx* ctx) {
 }
 
 int kss_split_config(kss_ctx* ctx, int32_t n_parts, int32_t part, int32_t shards_per_part) {
+  KSS_SVC_QUIESCE(ctx);
   if (!ctx) return fail(KSS_E_INVAL, "null ctx");
   if (n_parts < 1 || n_parts > KSS_SPLIT_MAX_PARTS || part < 0 || part >= n_parts || shards_per_part < 1)
     return fail(KSS_E_INVAL, "bad split configuration");
@@ -1751,6 +1803,7 @@ int kss_split_open(kss_ctx* ctx, const void* handles) {
 }
 
 int kss_read_port_state(kss_ctx* ctx, uint64_t* port_used) {
+  KSS_SVC_QUIESCE(ctx);
   if (!ctx || !ctx->loaded || !port_used) return fail(KSS_E_INVAL, "bad arguments");
   std::lock_guard<std::mutex> lk(ctx->mu);
   HIP_TRY(hipSetDevice(ctx->cfg.device));
@@ -1760,6 +1813,7 @@ int kss_read_port_state(kss_ctx* ctx, uint64_t* port_used) {
 }
 
 int kss_apply_port_delta(kss_ctx* ctx, const int32_t* idx, int32_t n, const uint64_t* port_used) {
+  KSS_SVC_QUIESCE(ctx);
   if (!ctx || !ctx->loaded) return fail(KSS_E_INVAL, "no cluster loaded");
   if (n < 0 || (n > 0 && (!idx || !port_used))) return fail(KSS_E_INVAL, "bad arguments");
   for (int i = 0; i < n; i++) {
@@ -1778,6 +1832,7 @@ int kss_apply_port_delta(kss_ctx* ctx, const int32_t* idx, int32_t n, const uint
 }
 
 int kss_read_volume_state(kss_ctx* ctx, int32_t* vol_count, int32_t* vol_attached) {
+  KSS_SVC_QUIESCE(ctx);
   if (!ctx || !ctx->loaded) return fail(KSS_E_INVAL, "no cluster loaded");
   std::lock_guard<std::mutex> lk(ctx->mu);
   HIP_TRY(hipSetDevice(ctx->cfg.device));
@@ -1793,6 +1848,7 @@ int kss_read_volume_state(kss_ctx* ctx, int32_t* vol_count, int32_t* vol_attache
 
 int kss_apply_volume_delta(kss_ctx* ctx, const int32_t* node, const int32_t* row, const int32_t* value, int32_t n,
                            int32_t mode) {
+  KSS_SVC_QUIESCE(ctx);
   if (!ctx || !ctx->loaded) return fail(KSS_E_INVAL, "no cluster loaded");
   if (n < 0 || (n > 0 && (!node || !row || !value)) || (mode != 0 && mode != 1)) return fail(KSS_E_INVAL, "bad arguments");
   const int R = ctx->dc.n_vol_rows, K = ctx->dc.n_vol_keys;
@@ -2674,6 +2730,7 @@ static int eval_pod_slot(kss_ctx* ctx, const kss_podset* ps, int32_t pod_index, 
 }
 
 int kss_eval_pod(kss_ctx* ctx, const kss_podset* ps, int32_t pod_index, kss_pod_result* out) {
+  KSS_SVC_QUIESCE(ctx);
   if (!ctx || !out) return fail(KSS_E_INVAL, "bad arguments");
   std::lock_guard<std::mutex> lk(ctx->mu);
   const size_t N = (size_t)ctx->dc.N;
@@ -2684,6 +2741,7 @@ int kss_eval_pod(kss_ctx* ctx, const kss_podset* ps, int32_t pod_index, kss_pod_
 }
 
 int kss_eval_pod_view(kss_ctx* ctx, const kss_podset* ps, int32_t pod_index, uint32_t fields, kss_pod_view* out) {
+  KSS_SVC_QUIESCE(ctx);
   if (!ctx || !out) return fail(KSS_E_INVAL, "bad arguments");
   std::lock_guard<std::mutex> lk(ctx->mu);
   const size_t N = (size_t)ctx->dc.N;
@@ -2791,14 +2849,17 @@ static int commit_one(kss_ctx* ctx, const kss_podset* ps, int32_t pod_index, int
 }
 
 int kss_commit(kss_ctx* ctx, const kss_podset* ps, int32_t pod_index, int32_t node) {
+  KSS_SVC_QUIESCE(ctx);
   return commit_one(ctx, ps, pod_index, node, 1);
 }
 
 int kss_rollback(kss_ctx* ctx, const kss_podset* ps, int32_t pod_index, int32_t node) {
+  KSS_SVC_QUIESCE(ctx);
   return commit_one(ctx, ps, pod_index, node, -1);
 }
 
 int kss_schedule_batch(kss_ctx* ctx, const kss_podset* ps, int32_t n, uint32_t flags, int32_t* chosen_out) {
+  KSS_SVC_QUIESCE(ctx);
   if (!ctx || !ctx->loaded || !ps) return fail(KSS_E_INVAL, "bad arguments");
   if (n < 0 || n > ps->n_pods) return fail(KSS_E_INVAL, "pod count out of range");
   // every pod is staged (and may be run later by kss_run_staged / the node axis): all of
@@ -2825,6 +2886,7 @@ int kss_schedule_batch(kss_ctx* ctx, const kss_podset* ps, int32_t n, uint32_t f
 }
 
 int kss_stage_pods(kss_ctx* ctx, const kss_podset* ps) {
+  KSS_SVC_QUIESCE(ctx);
   if (!ctx || !ctx->loaded || !ps) return fail(KSS_E_INVAL, "bad arguments");
   int rc = validate(&ctx->host, ps, ps->n_pods);
   if (rc) return rc;
@@ -2841,6 +2903,7 @@ int kss_stage_pods(kss_ctx* ctx, const kss_podset* ps) {
 }
 
 int kss_run_staged(kss_ctx* ctx, int32_t n, uint32_t flags, int32_t* chosen_out) {
+  KSS_SVC_QUIESCE(ctx);
   if (!ctx || !ctx->loaded) return fail(KSS_E_INVAL, "no cluster loaded");
   if (n < 0 || n > ctx->staged_n) return fail(KSS_E_INVAL, "n exceeds the staged pods");
   const bool record = (flags & KSS_SCHED_RECORD) != 0;
@@ -2856,7 +2919,262 @@ int kss_run_staged(kss_ctx* ctx, int32_t n, uint32_t flags, int32_t* chosen_out)
   return 0;
 }
 
+// ---------------------------------------------------------------------------
+// the per-pod service grid (kss_service_*): host side (kernel: kss_service.cuh)
+// ---------------------------------------------------------------------------
+static void svc_free(kss_ctx* ctx) {
+  auto& v = ctx->svc;
+  if (v.box) hipHostFree(v.box);
+  if (v.rec) hipHostFree(v.rec);
+  if (v.stream) hipStreamDestroy(v.stream);
+  v.relay.release();
+  v.gran.release();
+  v.err.release();
+  v.job.release();
+  v = kss_ctx::Service{};
+}
+
+static bool svc_alive(kss_ctx* ctx) {
+  return ctx->svc.running && hipStreamQuery(ctx->svc.stream) == hipErrorNotReady;
+}
+
+// (Re)launch the grid at the first command shard 0 has not relayed yet.
+static int svc_launch(kss_ctx* ctx) {
+  auto& v = ctx->svc;
+  const unsigned long long seq0 = __atomic_load_n(&v.box->consumed, __ATOMIC_ACQUIRE);
+  const size_t relay_bytes = sizeof(unsigned long long) * 2 * SVC_DRING;
+  HIP_TRY(hipMemsetAsync(v.relay.p, 0, relay_bytes, v.stream));
+  std::vector<unsigned long long> seen((size_t)v.W, seq0);  // the relay throttle starts from here
+  HIP_TRY(hipMemcpyAsync((char*)v.relay.p + relay_bytes, seen.data(), 8 * seen.size(), hipMemcpyHostToDevice, v.stream));
+  if (v.W > 1) HIP_TRY(hipMemsetAsync(v.gran.p, 0, v.gran.cap, v.stream));  // epochs restart at 0
+  HIP_TRY(hipMemsetAsync(v.err.p, 0, 16, v.stream));
+  v.box->err = 0;
+  const void* fn = v.gen ? (const void*)k_service<true> : (const void*)k_service<false>;
+  HIP_TRY(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)v.shmem));
+  const DevJob* jd = (const DevJob*)v.job.p;
+  kss_profile pr = ctx->prof;
+  int W = v.W, npt = v.npt, bins = v.bins_cap, ck = v.cache_keys;
+  unsigned long long* gran = (unsigned long long*)v.gran.p;
+  int* err = (int*)v.err.p;
+  SvcBox* box = v.box_dev;
+  unsigned long long* relay = (unsigned long long*)v.relay.p;
+  unsigned long long* seenp = relay + 2 * SVC_DRING;
+  uint8_t* rec = v.rec_dev;
+  unsigned long long s0 = seq0;
+  void* args[] = {(void*)&jd,   (void*)&pr,  (void*)&W,   (void*)&npt,   (void*)&bins,  (void*)&ck, (void*)&gran,
+                  (void*)&err,  (void*)&box, (void*)&relay, (void*)&seenp, (void*)&rec, (void*)&s0};
+  if (int rc = launch_resident(fn, dim3((unsigned)W), dim3((unsigned)v.threads), args, v.shmem, v.stream)) return rc;
+  v.running = true;
+  return 0;
+}
+
+// The grid with the staged pods' programs; geometry as a per-pod k_schedule launch.
+static int svc_start_locked(kss_ctx* ctx) {
+  if (!ctx->loaded) return fail(KSS_E_INVAL, "no cluster loaded");
+  if (ctx->staged_n <= 0) return fail(KSS_E_INVAL, "the service evaluates staged pods: kss_stage_pods first");
+  if (ctx->split_n > 1) return fail(KSS_E_UNSUPPORTED, "the service runs the whole cluster on one device");
+  auto& v = ctx->svc;
+  HIP_TRY(hipSetDevice(ctx->cfg.device));
+  HIP_TRY(hipStreamSynchronize(ctx->stream));  // every earlier launch / copy on the ctx stream is done
+  const size_t N = (size_t)ctx->dc.N;
+  int W = std::max(1, std::min(ctx->n_cu, (int)((N + ctx->nodes_per_shard - 1) / ctx->nodes_per_shard)));
+  if (ctx->force_w > 0) W = std::min(ctx->force_w, ctx->n_cu);
+  W = std::max(W, (int)((N + KSS_MAX_NPT * KSS_MAX_THREADS - 1) / (KSS_MAX_NPT * KSS_MAX_THREADS)));
+  W = std::min(W, std::max(1, (int)N));
+  const PlanNeeds& need = ctx->staged_need;
+  if (W > 1 && need.xw > XW_MAX) return fail(KSS_E_UNSUPPORTED, "topology histograms too large for the service grid");
+  if (W > SVC_MAX_SHARDS || W > ctx->n_cu) return fail(KSS_E_UNSUPPORTED, "cluster too large for the service grid");
+  Geometry g;
+  if (!pick_geometry((int)N, W, ctx->pref_threads, g)) return fail(KSS_E_UNSUPPORTED, "no geometry for this cluster");
+  const int bins_cap = std::max(need.bins_cap, 0);
+  const int cap = g.threads * g.npt;
+  const size_t base = lds_bytes(bins_cap, cap);
+  if (base > KSS_LDS_BUDGET) return fail(KSS_E_UNSUPPORTED, "per-workgroup LDS budget exceeded");
+  int cache_keys = -1;
+  if (base + node_cache_bytes(cap, ctx->dc.n_keys) <= KSS_LDS_BUDGET) cache_keys = ctx->dc.n_keys;
+  else if (base + node_cache_bytes(cap, 0) <= KSS_LDS_BUDGET) cache_keys = 0;
+  if (!v.stream) HIP_TRY(hipStreamCreateWithFlags(&v.stream, hipStreamNonBlocking));
+  const SlotLayout SL(N);
+  if (!v.box) {
+    HIP_TRY(hipHostMalloc((void**)&v.box, sizeof(SvcBox), hipHostMallocCoherent | hipHostMallocMapped));
+    std::memset((void*)v.box, 0, sizeof(SvcBox));
+    HIP_TRY(hipHostGetDevicePointer((void**)&v.box_dev, v.box, 0));
+    v.posted = 0;
+  }
+  if (v.rec_bytes < SL.bytes) {
+    if (v.rec) HIP_TRY(hipHostFree(v.rec));
+    v.rec = nullptr;
+    v.rec_bytes = 0;
+    HIP_TRY(hipHostMalloc((void**)&v.rec, SL.bytes, hipHostMallocCoherent | hipHostMallocMapped));
+    HIP_TRY(hipHostGetDevicePointer((void**)&v.rec_dev, v.rec, 0));
+    v.rec_bytes = SL.bytes;
+  }
+  int rc = ctx->slot_buf.ensure(SL.bytes);
+  if (!rc) rc = v.relay.ensure(sizeof(unsigned long long) * (2 * SVC_DRING + (size_t)W));
+  if (!rc) rc = v.gran.ensure(sizeof(unsigned long long) * 2 * (size_t)W * 2 * XW_MAX);
+  if (!rc) rc = v.err.ensure(16);
+  if (!rc) rc = v.job.ensure(sizeof(DevJob));
+  if (rc) return rc;
+  DevJob job{};
+  job.c = ctx->dc;
+  job.P = ctx->dp;
+  job.n_pods = ctx->staged_n;
+  job.commit = 1;
+  job.keep_norm = 1;
+  job.record = 0;
+  job.slots = (uint8_t*)ctx->slot_buf.p;
+  job.slot_bytes = SL.bytes;
+  job.prof = ctx->prof;
+  HIP_TRY(hipMemcpyAsync(v.job.p, &job, sizeof(DevJob), hipMemcpyHostToDevice, v.stream));
+  v.W = g.W;
+  v.threads = g.threads;
+  v.npt = g.npt;
+  v.bins_cap = bins_cap;
+  v.cache_keys = cache_keys;
+  v.shmem = base + (cache_keys >= 0 ? node_cache_bytes(cap, cache_keys) : 0);
+  v.gen = bins_cap > 0 || need.general;
+  ctx->last_geom[0] = g.W;
+  ctx->last_geom[1] = g.threads;
+  ctx->last_geom[2] = g.npt;
+  return svc_launch(ctx);
+}
+
+// Post one command (the ring never overruns what shard 0 has relayed).
+static int svc_post(kss_ctx* ctx, int op, int pod, int node, int fields, unsigned long long* seq_out) {
+  auto& v = ctx->svc;
+  const auto t0 = std::chrono::steady_clock::now();
+  while (v.posted - __atomic_load_n(&v.box->consumed, __ATOMIC_ACQUIRE) >= (unsigned long long)SVC_RING) {
+    if (!svc_alive(ctx)) {
+      if (int rc = svc_launch(ctx)) return rc;
+    }
+    if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(5)) return fail(KSS_E_DEVICE, "service ring full");
+  }
+  SvcCmd& c = v.box->cmd[v.posted % SVC_RING];
+  c.op = op;
+  c.pod = pod;
+  c.node = node;
+  c.fields = fields;
+  *seq_out = v.posted;
+  ++v.posted;
+  __atomic_store_n(&v.box->head, v.posted, __ATOMIC_RELEASE);
+  return 0;
+}
+
+// Stop the grid (STOP command, then the stream drains: every wait in the grid is bounded).
+static int svc_stop(kss_ctx* ctx) {
+  auto& v = ctx->svc;
+  if (!v.running) return 0;
+  unsigned long long seq = 0;
+  if (svc_alive(ctx)) {
+    if (int rc = svc_post(ctx, SVC_STOP, 0, 0, 0, &seq)) return rc;
+  }
+  HIP_TRY(hipStreamSynchronize(v.stream));
+  v.running = false;
+  const bool err = v.box->err != 0;
+  // commands posted after the grid left for good are dropped (a later start resumes after them)
+  __atomic_store_n(&v.box->consumed, v.posted, __ATOMIC_RELEASE);
+  if (err) {
+    ctx->state_unknown = true;
+    return fail(KSS_E_DEVICE, "service grid: a shard exchange timed out");
+  }
+  return 0;
+}
+
+int kss_service_start(kss_ctx* ctx) {
+  if (!ctx) return fail(KSS_E_INVAL, "null ctx");
+  KSS_SVC_QUIESCE(ctx);
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  return svc_start_locked(ctx);
+}
+
+int kss_service_stop(kss_ctx* ctx) {
+  if (!ctx) return fail(KSS_E_INVAL, "null ctx");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  return svc_stop(ctx);
+}
+
+int kss_service_eval(kss_ctx* ctx, int32_t pod_index, uint32_t fields, kss_pod_view* out) {
+  if (!ctx || !ctx->loaded || !out) return fail(KSS_E_INVAL, "bad arguments");
+  if (pod_index < 0 || pod_index >= ctx->staged_n || pod_index >= (1 << 24)) return fail(KSS_E_INVAL, "pod index outside the staged pods");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  auto& v = ctx->svc;
+  if (!v.running) {
+    if (int rc = svc_start_locked(ctx)) return rc;
+  }
+  unsigned long long seq = 0;
+  if (int rc = svc_post(ctx, SVC_EVAL, pod_index, 0, (int)(fields & KSS_FIELD_ALL), &seq)) return rc;
+  // wait for every shard's done flag; restart a grid that left idle before taking the command
+  const auto t0 = std::chrono::steady_clock::now();
+  for (unsigned spins = 0;; ++spins) {
+    bool all = true;
+    for (int w = 0; w < v.W && all; w++) all = __atomic_load_n(&v.box->done[w], __ATOMIC_ACQUIRE) > seq;
+    if (all) break;
+    if ((spins & 1023) == 1023) {
+      if (v.box->err) {
+        svc_stop(ctx);
+        ctx->state_unknown = true;
+        return fail(KSS_E_DEVICE, "service grid: a shard exchange timed out");
+      }
+      if (!svc_alive(ctx)) {
+        if (__atomic_load_n(&v.box->consumed, __ATOMIC_ACQUIRE) <= seq) {  // left idle before taking it
+          v.running = false;
+          if (int rc = svc_launch(ctx)) return rc;
+        } else {
+          v.running = false;
+          return fail(KSS_E_DEVICE, "service grid left during an evaluation");
+        }
+      }
+      if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(5)) {
+        svc_stop(ctx);
+        return fail(KSS_E_DEVICE, "service evaluation timed out");
+      }
+    }
+  }
+  const PodMeta m = v.box->meta;
+  if (m.status == 4) return fail(KSS_E_UNSUPPORTED, "pod program exceeds the device path's per-pod limits");
+  const size_t N = (size_t)ctx->dc.N;
+  const SlotLayout SL(N);
+  const uint8_t* r = v.rec;
+  out->fail_plugin = (fields & KSS_FIELD_FAIL) ? r + SL.fail : nullptr;
+  out->fail_detail = (fields & KSS_FIELD_DETAIL) ? (const uint16_t*)(r + SL.detail) : nullptr;
+  out->raw = (fields & KSS_FIELD_RAW) ? (const int64_t*)(r + SL.raw) : nullptr;
+  out->norm = (fields & KSS_FIELD_NORM) ? (const int64_t*)(r + SL.norm) : nullptr;
+  out->total = (fields & KSS_FIELD_TOTAL) ? (const int64_t*)(r + SL.total) : nullptr;
+  out->chosen = m.chosen;
+  out->n_feasible = m.n_feasible;
+  out->best_total = m.best_total;
+  out->scored = m.scored;
+  out->status = m.status;
+  return 0;
+}
+
+static int svc_commit(kss_ctx* ctx, int32_t pod_index, int32_t node, int sign) {
+  if (!ctx || !ctx->loaded) return fail(KSS_E_INVAL, "bad arguments");
+  if (pod_index < 0 || pod_index >= ctx->staged_n || pod_index >= (1 << 24)) return fail(KSS_E_INVAL, "pod index outside the staged pods");
+  const int local = node - ctx->dc.node_base;
+  if (local < 0 || local >= ctx->dc.N) return fail(KSS_E_INVAL, "node out of range");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  if (!ctx->svc.running) {
+    if (int rc = svc_start_locked(ctx)) return rc;
+  }
+  unsigned long long seq = 0;
+  if (int rc = svc_post(ctx, sign > 0 ? SVC_COMMIT : SVC_ROLLBACK, pod_index, node, 0, &seq)) return rc;
+  if (sign > 0) {  // the same host bookkeeping as kss_commit (bounds, PostFilter table)
+    const double own = pod_index < (int)ctx->staged_bp.size() ? (double)ctx->staged_bp[pod_index].tlen : 0.0;
+    ctx->count_bound += 1.0 + own;
+    ctx->cell_bound += 1.0 + own;
+  }
+  if (pod_index < (int)ctx->staged_bp.size())
+    ctx->bound_log.push_back(BoundOp{local, sign > 0 ? 1 : 0, ctx->staged_bp[pod_index]});
+  ctx->bound_dirty = true;
+  return 0;
+}
+
+int kss_service_commit(kss_ctx* ctx, int32_t pod_index, int32_t node) { return svc_commit(ctx, pod_index, node, 1); }
+int kss_service_rollback(kss_ctx* ctx, int32_t pod_index, int32_t node) { return svc_commit(ctx, pod_index, node, -1); }
+
 int kss_fetch_record(kss_ctx* ctx, int32_t pod_index, kss_pod_result* out) {
+  KSS_SVC_QUIESCE(ctx);
   if (!ctx || !out) return fail(KSS_E_INVAL, "bad arguments");
   if (pod_index < 0 || pod_index >= ctx->recorded) return fail(KSS_E_NOTFOUND, "pod not recorded");
   std::lock_guard<std::mutex> lk(ctx->mu);
@@ -3241,6 +3559,7 @@ int kss_schedule_scenarios(int32_t device, const kss_profile* prof, int32_t n_sc
 }
 
 int kss_load_bound(kss_ctx* ctx, const kss_boundset* bs) {
+  KSS_SVC_QUIESCE(ctx);
   if (!ctx || !ctx->loaded || !bs || bs->n < 0 || bs->n_ints < 0) return fail(KSS_E_INVAL, "bad arguments");
   if (bs->n && (!bs->id || !bs->node || !bs->priority || !bs->start || !bs->cls || !bs->req || !bs->terms_off ||
                 !bs->terms_len))
@@ -3358,6 +3677,7 @@ int upload_bound(kss_ctx* ctx) {
 }  // namespace
 
 int kss_postfilter_pod(kss_ctx* ctx, const kss_podset* ps, int32_t pod_index, kss_preempt_result* out) {
+  KSS_SVC_QUIESCE(ctx);
   if (!ctx || !ctx->loaded || !ps || !out) return fail(KSS_E_INVAL, "bad arguments");
   if (pod_index < 0 || pod_index >= ps->n_pods) return fail(KSS_E_INVAL, "pod index out of range");
   if (out->victims_cap < 0 || (out->victims_cap > 0 && !out->victims)) return fail(KSS_E_INVAL, "bad victims buffer");

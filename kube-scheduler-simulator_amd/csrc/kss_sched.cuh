@@ -82,6 +82,7 @@ struct SharedHdr {
   int plan_ok;
   int abort;
   int pad[2];
+  int cmd[4];   // the service grid's current command (kss_service.cuh)
 };
 
 __device__ __forceinline__ SharedHdr& shdr(long long* smem) { return *reinterpret_cast<SharedHdr*>(smem); }

@@ -1,0 +1,209 @@
+// kss_service.cuh — the per-pod drop-in path as a persistent service grid (kss_service_*).
+//
+// The Go plugin drives the evaluator one pod at a time (wrappedPlugin.PreFilter ->
+// evaluate, Reserve -> AssumePod, Unreserve -> ForgetPod: simulator/scheduler/plugin/
+// wrappedplugin.go:491-518, 616-645).  A launch per call costs a kernel dispatch, an
+// occupancy query and a stream synchronisation; here one k_schedule-shaped grid stays
+// resident and takes commands from a ring in pinned host memory instead:
+//
+//   host: writes command k into ring[k % SVC_RING], then head = k + 1 (release)
+//   shard 0: polls head (system scope), relays command k into a tagged device-memory slot
+//            (agent scope, {k+1, payload} in both words: the data is the flag) and reports
+//            consumed = k + 1 to the host
+//   every shard: polls the relay slot, runs the command:
+//     EVAL      schedule_pod (kss_sched.cuh) into the HBM record slot, then copies its own
+//               node range of the requested record fields into the pinned host record,
+//               fences at system scope and stores done[w] = k + 1
+//     COMMIT / ROLLBACK   the owning shard applies AssumePod / ForgetPod (commit_pod)
+//     STOP      leave (after writing the LDS node cache back)
+//
+// Every wait is bounded by wall time: shard 0 relays STOP after SVC_IDLE_TICKS without a
+// command (the grid drains by itself; the host restarts it on the next call from
+// `consumed`), the other shards leave after 4x that without a relay, and an exchange
+// timeout inside a pod aborts with the error word set.
+#pragma once
+#include <type_traits>
+
+#include "kss_sched.cuh"
+
+namespace kss {
+
+constexpr int SVC_RING = 1024;                                 // host command ring (entries)
+constexpr int SVC_DRING = 64;                                  // device relay ring (entries)
+constexpr int SVC_MAX_SHARDS = 256;
+constexpr unsigned long long SVC_IDLE_TICKS = 100000000ull;    // 1 s of s_memrealtime (100 MHz)
+enum { SVC_NONE = 0, SVC_EVAL = 1, SVC_COMMIT = 2, SVC_ROLLBACK = 3, SVC_STOP = 4 };
+
+struct SvcCmd {
+  int32_t op, pod, node, fields;
+};
+
+// Pinned, coherent host memory shared with the grid.
+struct SvcBox {
+  SvcCmd cmd[SVC_RING];
+  unsigned long long head;      // commands posted (host)
+  unsigned long long consumed;  // commands relayed by shard 0 (device)
+  unsigned long long done[SVC_MAX_SHARDS];  // per shard: 1 + the last EVAL finished
+  PodMeta meta;                 // outcome of the last EVAL (shard 0)
+  int32_t err;                  // an exchange timed out
+  int32_t running;              // 1 while the grid runs (shard 0)
+};
+
+__device__ __forceinline__ unsigned long long ld_sys(const unsigned long long* p) {
+  return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ void st_sys(unsigned long long* p, unsigned long long v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// Copy elements [lo, hi) of `rows` rows of ES-byte elements (row stride N) from the HBM
+// record to the pinned host record (same layout).
+template <int ES>
+__device__ __forceinline__ void svc_copy(const uint8_t* src, uint8_t* dst, size_t N, int rows, int lo, int hi) {
+  using T = typename std::conditional<ES == 8, uint64_t, typename std::conditional<ES == 2, uint16_t, uint8_t>::type>::type;
+  const T* s = reinterpret_cast<const T*>(src);
+  T* d = reinterpret_cast<T*>(dst);
+  for (int r = 0; r < rows; r++)
+    for (int i = lo + (int)threadIdx.x; i < hi; i += (int)blockDim.x) d[(size_t)r * N + i] = s[(size_t)r * N + i];
+}
+
+template <bool GEN>
+__device__ void service_loop(DevCluster c, const DevJob& job, const kss_profile& prof, int W, int npt, int bins_cap,
+                             int cache_keys, unsigned long long* gran, int* err, SvcBox* box,
+                             unsigned long long* relay, unsigned long long* seen, uint8_t* rec_host,
+                             unsigned long long seq, unsigned epoch0, long long* smem) {
+  const int w = blockIdx.x;
+  const size_t N = (size_t)c.N;
+  const SlotLayout L(N);
+  if (threadIdx.x == 0) shdr(smem).abort = 0;
+  __syncthreads();
+  Shard S;
+  const int per = (c.N + W - 1) / W;
+  S.lo = min(c.N, w * per);
+  S.hi = min(c.N, S.lo + per);
+  S.W = W;
+  S.w = w;
+  S.epoch = epoch0;
+  S.gran = gran;
+  S.err = err;
+  S.stamps = nullptr;
+  const int cap = npt * (int)blockDim.x;
+  if (cache_keys >= 0) {
+    long long* b = xvec(smem) + NSCAL + bins_cap + slot_arrays_bytes(cap) / 8;
+    c.nc64 = reinterpret_cast<int64_t*>(b);
+    c.nct = reinterpret_cast<uint64_t*>(b + 8 * (size_t)cap);
+    c.nc32 = reinterpret_cast<int32_t*>(b + 10 * (size_t)cap);
+    c.ncl = cache_keys > 0 && cache_keys >= c.n_keys ? c.nc32 + 3 * (size_t)cap : nullptr;
+    c.nc_lo = S.lo;
+    c.nc_cap = cap;
+    cache_fill(c, S.hi, c.ncl ? c.n_keys : 0);
+    __syncthreads();
+  }
+  int* cmd = shdr(smem).cmd;
+  if (w == 0 && threadIdx.x == 0) __hip_atomic_store(&box->running, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  for (;; ++seq) {
+    if (threadIdx.x == 0) {
+      int op = SVC_STOP, pod = 0, node = 0, fields = 0;
+      const unsigned long long tag = (seq + 1) << 32;
+      unsigned long long* slot = relay + 2 * (seq % SVC_DRING);
+      if (w == 0) {
+        const unsigned long long t0 = wall_clock64();
+        bool got = false;
+        for (;;) {  // the host's next command, or STOP after the idle time
+          if (ld_sys(&box->head) > seq) {
+            got = true;
+            break;
+          }
+          if (wall_clock64() - t0 > SVC_IDLE_TICKS) break;
+          __builtin_amdgcn_s_sleep(2);
+        }
+        if (got) {
+          const SvcCmd* hc = box->cmd + seq % SVC_RING;
+          op = __hip_atomic_load(&hc->op, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          pod = __hip_atomic_load(&hc->pod, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          node = __hip_atomic_load(&hc->node, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          fields = __hip_atomic_load(&hc->fields, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          if (op < SVC_EVAL || op > SVC_STOP) op = SVC_STOP;
+        }
+        // the relay slot is reused every SVC_DRING commands: every shard must have taken
+        // command seq - SVC_DRING first (bounded: a shard that left ends the wait)
+        if (seq >= (unsigned long long)SVC_DRING) {
+          const unsigned long long need = seq - SVC_DRING + 1, t1 = wall_clock64();
+          for (int q = 1; q < W; q++)
+            while (__hip_atomic_load(seen + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need &&
+                   wall_clock64() - t1 < 4 * SVC_IDLE_TICKS)
+              __builtin_amdgcn_s_sleep(1);
+        }
+        const unsigned long long w0 = tag | ((unsigned long long)(uint32_t)pod << 8) |
+                                      ((unsigned long long)(fields & 31) << 3) | (unsigned long long)(op & 7);
+        __hip_atomic_store(slot + 1, tag | (unsigned long long)(uint32_t)node, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(slot, w0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (got) st_sys(&box->consumed, seq + 1);
+      } else {
+        const unsigned long long t0 = wall_clock64();
+        for (;;) {
+          const unsigned long long a = __hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          const unsigned long long b = __hip_atomic_load(slot + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if ((a >> 32) == (seq + 1) && (b >> 32) == (seq + 1)) {
+            op = (int)(a & 7);
+            fields = (int)((a >> 3) & 31);
+            pod = (int)((a >> 8) & 0xFFFFFF);
+            node = (int)(uint32_t)b;
+            break;
+          }
+          if (wall_clock64() - t0 > 4 * SVC_IDLE_TICKS) break;  // shard 0 is gone: leave
+          __builtin_amdgcn_s_sleep(1);
+        }
+      }
+      cmd[0] = op;
+      cmd[1] = pod;
+      cmd[2] = node;
+      cmd[3] = fields;
+    }
+    __syncthreads();
+    const int op = cmd[0], pi = cmd[1], node = cmd[2], fields = cmd[3];
+    __syncthreads();  // the command words may be rewritten by the next iteration's lane 0
+    if (op == SVC_STOP) break;
+    if (op == SVC_EVAL) {
+      uint8_t* base = job.slots;
+      Slot s;
+      s.fail = base + L.fail;
+      s.detail = (uint16_t*)(base + L.detail);
+      s.raw = (int64_t*)(base + L.raw);
+      s.norm = (int64_t*)(base + L.norm);
+      s.total = (int64_t*)(base + L.total);
+      PodMeta m;
+      if (!schedule_pod<GEN>(c, job.P, prof, pi, smem, S, bins_cap, npt, &s, /*keep_norm=*/true, m)) {
+        if (threadIdx.x == 0) __hip_atomic_store(&box->err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        break;
+      }
+      // this shard's node range of the requested fields -> the pinned host record
+      if (fields & KSS_FIELD_FAIL) svc_copy<1>(base + L.fail, rec_host + L.fail, N, 1, S.lo, S.hi);
+      if (fields & KSS_FIELD_DETAIL) svc_copy<2>(base + L.detail, rec_host + L.detail, N, 1, S.lo, S.hi);
+      if (fields & KSS_FIELD_TOTAL) svc_copy<8>(base + L.total, rec_host + L.total, N, 1, S.lo, S.hi);
+      if (fields & KSS_FIELD_RAW) svc_copy<8>(base + L.raw, rec_host + L.raw, N, KSS_NSCORE, S.lo, S.hi);
+      if (fields & KSS_FIELD_NORM) svc_copy<8>(base + L.norm, rec_host + L.norm, N, KSS_NSCORE, S.lo, S.hi);
+      if (w == 0 && threadIdx.x == 0) {
+        box->meta = m;
+      }
+      __threadfence_system();  // this lane's record stores are visible to the host
+      __syncthreads();
+      if (threadIdx.x == 0) st_sys(&box->done[w], seq + 1);
+    } else if (op == SVC_COMMIT || op == SVC_ROLLBACK) {
+      const int local = node - c.node_base;
+      if (threadIdx.x == 0 && local >= S.lo && local < S.hi)
+        commit_pod(c, job.P, job.P.pods[pi], local, op == SVC_COMMIT ? 1 : -1);
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) __hip_atomic_store(seen + w, seq + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (c.nc64) {
+    __syncthreads();
+    cache_writeback(c, S.hi);
+  }
+  __threadfence_system();
+  __syncthreads();
+  if (w == 0 && threadIdx.x == 0) __hip_atomic_store(&box->running, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+}  // namespace kss

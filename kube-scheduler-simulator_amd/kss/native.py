@@ -48,6 +48,11 @@ SIGNATURES = [
     ("kss_apply_port_delta", C.c_int, [C.c_void_p, P(C.c_int32), C.c_int32, P(C.c_uint64)]),
     ("kss_eval_pod", C.c_int, [C.c_void_p, P(abi.PodSet), C.c_int32, P(abi.PodResult)]),
     ("kss_eval_pod_view", C.c_int, [C.c_void_p, P(abi.PodSet), C.c_int32, C.c_uint32, P(abi.PodView)]),
+    ("kss_service_start", C.c_int, [C.c_void_p]),
+    ("kss_service_stop", C.c_int, [C.c_void_p]),
+    ("kss_service_eval", C.c_int, [C.c_void_p, C.c_int32, C.c_uint32, P(abi.PodView)]),
+    ("kss_service_commit", C.c_int, [C.c_void_p, C.c_int32, C.c_int32]),
+    ("kss_service_rollback", C.c_int, [C.c_void_p, C.c_int32, C.c_int32]),
     ("kss_commit", C.c_int, [C.c_void_p, P(abi.PodSet), C.c_int32, C.c_int32]),
     ("kss_rollback", C.c_int, [C.c_void_p, P(abi.PodSet), C.c_int32, C.c_int32]),
     ("kss_schedule_batch", C.c_int, [C.c_void_p, P(abi.PodSet), C.c_int32, C.c_uint32, P(C.c_int32)]),
@@ -346,6 +351,26 @@ class Context:
         v = abi.PodView()
         check(lib().kss_eval_pod_view(self.h, C.byref(podset_struct), i, fields, C.byref(v)))
         return PodView(v, self.n_nodes)
+
+    # the per-pod service grid (kss_service_*): staged pods by index, no launch per call
+    def service_start(self):
+        check(lib().kss_service_start(self.h))
+
+    def service_stop(self):
+        check(lib().kss_service_stop(self.h))
+
+    def service_eval(self, i: int, fields: int = abi.KSS_FIELD_ALL, view: Optional[abi.PodView] = None) -> "PodView":
+        """kss_service_eval of staged pod i: the record as read-only views of the pinned
+        service buffer (valid until the next service call)."""
+        v = view if view is not None else abi.PodView()
+        check(lib().kss_service_eval(self.h, i, fields, C.byref(v)))
+        return PodView(v, self.n_nodes)
+
+    def service_commit(self, i: int, node: int):
+        check(lib().kss_service_commit(self.h, i, node))
+
+    def service_rollback(self, i: int, node: int):
+        check(lib().kss_service_rollback(self.h, i, node))
 
     def load_bound(self, boundset_struct: abi.Boundset):
         """The bound pods the PostFilter dry run may evict (CompiledCluster.as_boundset())."""

@@ -1,0 +1,97 @@
+"""The per-pod service grid (kss_service_*: a resident grid taking commands from a pinned host
+ring) against the launch-per-call per-pod API (kss_eval_pod_view / kss_commit): the same
+record (verdicts, details, raw / normalised scores, totals) and choice for every pod of
+default-profile, spread + inter-pod, port / image and volume workloads, commits and
+rollbacks in between, the grid restarting after its idle exit, and the other entry points
+stopping it first."""
+import time
+
+import numpy as np
+import pytest
+
+import volume_fuzz
+from kss import abi, native
+from kss.compile import compile_cluster
+from kss.synth import SEED_BASE
+
+pytestmark = pytest.mark.gpu
+
+
+def _same(a, b, N, where):
+    assert (a.chosen, a.n_feasible, a.scored, a.status, a.best_total) == \
+           (b.chosen, b.n_feasible, b.scored, b.status, b.best_total), where
+    np.testing.assert_array_equal(a.fail_plugin[:N], b.fail_plugin[:N], err_msg=str(where))
+    np.testing.assert_array_equal(a.fail_detail[:N], b.fail_detail[:N], err_msg=str(where))
+    if a.scored:
+        feas = a.fail_plugin[:N] == 0
+        np.testing.assert_array_equal(a.raw[:, :N][:, feas], b.raw[:, :N][:, feas], err_msg=str(where))
+        np.testing.assert_array_equal(a.norm[:, :N][:, feas], b.norm[:, :N][:, feas], err_msg=str(where))
+        np.testing.assert_array_equal(a.total[:N][feas], b.total[:N][feas], err_msg=str(where))
+
+
+def _copy(v):
+    out = native.PodResult.__new__(native.PodResult)
+    for k in ("fail_plugin", "fail_detail", "raw", "norm", "total"):
+        setattr(out, k, None if getattr(v, k) is None else np.array(getattr(v, k)))
+    for k in ("chosen", "n_feasible", "scored", "status", "best_total"):
+        setattr(out, k, getattr(v, k))
+    return out
+
+
+def _compare(cluster, pods, n, rollback_every=0):
+    """Service eval + commit vs eval_pod_view + commit on two contexts, pod after pod."""
+    ref = native.Context(abi.default_profile())
+    ref.load(cluster)
+    svc = native.Context(abi.default_profile())
+    svc.load(cluster)
+    svc.stage(pods)
+    N = ref.n_nodes
+    for j in range(n):
+        want = _copy(ref.eval_pod_view(pods, j))
+        got = svc.service_eval(j)
+        _same(got, want, N, j)
+        if want.chosen >= 0:
+            ref.commit(pods, j, want.chosen)
+            svc.service_commit(j, want.chosen)
+            if rollback_every and j % rollback_every == 0:
+                ref.rollback(pods, j, want.chosen)
+                svc.service_rollback(j, want.chosen)
+    svc.service_stop()
+    st_r, st_s = ref.node_state(), svc.node_state()
+    for k in ("requested", "nonzero", "pod_count"):
+        np.testing.assert_array_equal(st_s[k], st_r[k], err_msg=k)
+    ref.close()
+    svc.close()
+
+
+@pytest.mark.parametrize("config,n_nodes,n_pods", [(2, 5000, 120), (1, 100, 200), (3, 2000, 80), (4, 6000, 60)])
+def test_service_matches_per_pod_api(config, n_nodes, n_pods):
+    s = native.Synth(config, SEED_BASE + config, n_nodes, n_pods)
+    _compare(s.cluster, s.pods, n_pods, rollback_every=7)
+    s.close()
+
+
+@pytest.mark.parametrize("seed", [1, 2])
+def test_service_with_volumes(seed):
+    nodes, bound, pods, st = volume_fuzz.make(seed, n_nodes=300, n_bound=300, n_pods=60)
+    cc, cp, _ = compile_cluster(nodes, bound, pods, storage=st)
+    _compare(cc.as_struct(), cp.as_struct(), cp.n, rollback_every=5)
+
+
+def test_service_restarts_after_idle_exit_and_yields_to_other_calls():
+    s = native.Synth(2, SEED_BASE + 2, 3000, 40)
+    ctx = native.Context(abi.default_profile())
+    ctx.load(s.cluster)
+    ctx.stage(s.pods)
+    a = _copy(ctx.service_eval(0))
+    time.sleep(2.5)  # the grid leaves after ~1 s idle
+    b = ctx.service_eval(0)  # restarted transparently
+    _same(b, a, 3000, "after idle exit")
+    ctx.service_commit(0, a.chosen)
+    st = ctx.node_state()  # stops the grid first: the commit is in the state read back
+    assert st["pod_count"][a.chosen] == s.cluster.pod_count[a.chosen] + 1
+    c = ctx.eval_pod_view(s.pods, 1)  # the launch-per-call path works after the service
+    d = ctx.service_eval(1)  # and the service starts again on the same state
+    _same(d, _copy(c), 3000, "after the per-pod API")
+    ctx.close()
+    s.close()
