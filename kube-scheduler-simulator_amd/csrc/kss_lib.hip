@@ -2941,6 +2941,7 @@ static bool svc_alive(kss_ctx* ctx) {
 // (Re)launch the grid at the first command shard 0 has not relayed yet.
 static int svc_launch(kss_ctx* ctx) {
   auto& v = ctx->svc;
+  HIP_TRY(hipSetDevice(ctx->cfg.device));
   const unsigned long long seq0 = __atomic_load_n(&v.box->consumed, __ATOMIC_ACQUIRE);
   const size_t relay_bytes = sizeof(unsigned long long) * 2 * SVC_DRING;
   HIP_TRY(hipMemsetAsync(v.relay.p, 0, relay_bytes, v.stream));
