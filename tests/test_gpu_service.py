@@ -30,7 +30,8 @@ def _same(a, b, N, where):
 
 
 def _copy(v):
-    out = native.PodResult.__new__(native.PodResult)
+    import types
+    out = types.SimpleNamespace()
     for k in ("fail_plugin", "fail_detail", "raw", "norm", "total"):
         setattr(out, k, None if getattr(v, k) is None else np.array(getattr(v, k)))
     for k in ("chosen", "n_feasible", "scored", "status", "best_total"):
