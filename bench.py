@@ -583,6 +583,19 @@ def run_per_pod(args):
     ctx.reset()
     elapsed_svc, ev_svc, cm_svc, chosen_svc = svc_loop(abi.KSS_FIELD_ALL)
     assert chosen_svc == chosen, "service choices differ from kss_eval_pod's"
+    # one stamped pass (KSS_SERVICE_STAMPS): where shard 0 spends an evaluation
+    os.environ["KSS_SERVICE_STAMPS"] = "1"
+    ctx.reset()
+    phases = []
+    for j in range(min(100, n_pods)):
+        native.check(native.lib().kss_service_eval(ctx.h, j, abi.KSS_FIELD_ALL, ctypes.byref(sview)))
+        st = ctx.service_stamps()
+        phases.append([(st[1] - st[0]) / 100.0, (st[2] - st[1]) / 100.0, (st[3] - st[2]) / 100.0])
+        if sview.chosen >= 0:
+            native.check(native.lib().kss_service_commit(ctx.h, j, sview.chosen))
+    ctx.service_stop()
+    del os.environ["KSS_SERVICE_STAMPS"]
+    ph = np.median(np.array(phases), axis=0)
     ctx.reset()
     slim_fields = abi.KSS_FIELD_FAIL | abi.KSS_FIELD_DETAIL | abi.KSS_FIELD_TOTAL
     elapsed_svc_slim, ev_svc_slim, _, chosen_svc_slim = svc_loop(slim_fields)
@@ -620,6 +633,8 @@ def run_per_pod(args):
                     "slim": {"pods_per_s": n_pods / elapsed_svc_slim, "fields": "fail_plugin, fail_detail, total",
                              "eval_us": {"median": float(np.median(ev_svc_slim)), "mean": float(ev_svc_slim.mean()),
                                          "p90": float(np.percentile(ev_svc_slim, 90))}},
+                    "shard0_phases_us_median": {"relay": float(ph[0]), "pod": float(ph[1]),
+                                                "record_copy_and_fence": float(ph[2])},
                     "geometry": ctx.last_geometry()},
         "eval_device_ms_last": ctx.last_timing()[0],
         "geometry": ctx.last_geometry(),

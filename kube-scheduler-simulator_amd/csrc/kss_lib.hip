@@ -175,10 +175,11 @@ __global__ __launch_bounds__(KSS_MAX_THREADS) void k_service(const DevJob* __res
                                                              int npt, int bins_cap, int cache_keys,
                                                              unsigned long long* gran, int* err, SvcBox* box,
                                                              unsigned long long* relay, unsigned long long* seen,
-                                                             uint8_t* rec_host, unsigned long long seq) {
+                                                             uint8_t* rec_host, unsigned long long seq, int stamps) {
   extern __shared__ __attribute__((aligned(16))) long long smem[];
   const DevJob job = jobs[0];
-  service_loop<GEN>(job.c, job, prof, W, npt, bins_cap, cache_keys, gran, err, box, relay, seen, rec_host, seq, 0u, smem);
+  service_loop<GEN>(job.c, job, prof, W, npt, bins_cap, cache_keys, gran, err, box, relay, seen, rec_host, seq, 0u, stamps,
+                    smem);
 }
 
 // grid = n_jobs * W, as k_schedule; each shard's nodes live in LDS (cap slots).
@@ -2962,8 +2963,9 @@ static int svc_launch(kss_ctx* ctx) {
   unsigned long long* seenp = relay + 2 * SVC_DRING;
   uint8_t* rec = v.rec_dev;
   unsigned long long s0 = seq0;
-  void* args[] = {(void*)&jd,   (void*)&pr,  (void*)&W,   (void*)&npt,   (void*)&bins,  (void*)&ck, (void*)&gran,
-                  (void*)&err,  (void*)&box, (void*)&relay, (void*)&seenp, (void*)&rec, (void*)&s0};
+  int stamps = getenv("KSS_SERVICE_STAMPS") ? 1 : 0;
+  void* args[] = {(void*)&jd,  (void*)&pr,  (void*)&W,     (void*)&npt,   (void*)&bins, (void*)&ck, (void*)&gran,
+                  (void*)&err, (void*)&box, (void*)&relay, (void*)&seenp, (void*)&rec, (void*)&s0, (void*)&stamps};
   if (int rc = launch_resident(fn, dim3((unsigned)W), dim3((unsigned)v.threads), args, v.shmem, v.stream)) return rc;
   v.running = true;
   return 0;
@@ -3051,13 +3053,11 @@ static int svc_post(kss_ctx* ctx, int op, int pod, int node, int fields, unsigne
     if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(5)) return fail(KSS_E_DEVICE, "service ring full");
   }
   SvcCmd& c = v.box->cmd[v.posted % SVC_RING];
-  c.op = op;
-  c.pod = pod;
-  c.node = node;
-  c.fields = fields;
+  // the two tagged words: either may land first, the grid takes the entry once both carry the tag
+  __atomic_store_n(&c.w1, svc_w1(v.posted, node), __ATOMIC_RELEASE);
+  __atomic_store_n(&c.w0, svc_w0(v.posted, op, fields, pod), __ATOMIC_RELEASE);
   *seq_out = v.posted;
   ++v.posted;
-  __atomic_store_n(&v.box->head, v.posted, __ATOMIC_RELEASE);
   return 0;
 }
 
@@ -3172,6 +3172,13 @@ static int svc_commit(kss_ctx* ctx, int32_t pod_index, int32_t node, int sign) {
 }
 
 int kss_service_commit(kss_ctx* ctx, int32_t pod_index, int32_t node) { return svc_commit(ctx, pod_index, node, 1); }
+int kss_service_stamps(kss_ctx* ctx, uint64_t* out4) {
+  if (!ctx || !out4) return fail(KSS_E_INVAL, "bad arguments");
+  if (!ctx->svc.box) return fail(KSS_E_INVAL, "no service grid");
+  for (int i = 0; i < 4; i++) out4[i] = __atomic_load_n(&ctx->svc.box->stamp[i], __ATOMIC_ACQUIRE);
+  return 0;
+}
+
 int kss_service_rollback(kss_ctx* ctx, int32_t pod_index, int32_t node) { return svc_commit(ctx, pod_index, node, -1); }
 
 int kss_fetch_record(kss_ctx* ctx, int32_t pod_index, kss_pod_result* out) {

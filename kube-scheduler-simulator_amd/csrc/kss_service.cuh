@@ -6,10 +6,10 @@
 // occupancy query and a stream synchronisation; here one k_schedule-shaped grid stays
 // resident and takes commands from a ring in pinned host memory instead:
 //
-//   host: writes command k into ring[k % SVC_RING], then head = k + 1 (release)
-//   shard 0: polls head (system scope), relays command k into a tagged device-memory slot
-//            (agent scope, {k+1, payload} in both words: the data is the flag) and reports
-//            consumed = k + 1 to the host
+//   host: writes command k into ring[k % SVC_RING] as two 64-bit words, each tagged k + 1
+//         in its upper half (the data is the flag: no separate head word to read)
+//   shard 0: polls ring[k] (system scope, both words in flight), relays command k into a
+//            tagged device-memory slot (agent scope, same format) and reports consumed = k + 1
 //   every shard: polls the relay slot, runs the command:
 //     EVAL      schedule_pod (kss_sched.cuh) into the HBM record slot, then copies its own
 //               node range of the requested record fields into the pinned host record,
@@ -34,25 +34,33 @@ constexpr int SVC_MAX_SHARDS = 256;
 constexpr unsigned long long SVC_IDLE_TICKS = 100000000ull;    // 1 s of s_memrealtime (100 MHz)
 enum { SVC_NONE = 0, SVC_EVAL = 1, SVC_COMMIT = 2, SVC_ROLLBACK = 3, SVC_STOP = 4 };
 
+// A command as two tagged words: w0 = (k+1) << 32 | pod << 8 | fields << 3 | op,
+// w1 = (k+1) << 32 | node.
 struct SvcCmd {
-  int32_t op, pod, node, fields;
+  unsigned long long w0, w1;
 };
+__host__ __device__ inline unsigned long long svc_w0(unsigned long long k, int op, int fields, int pod) {
+  return ((k + 1) << 32) | ((unsigned long long)(uint32_t)pod << 8) | ((unsigned long long)(fields & 31) << 3) |
+         (unsigned long long)(op & 7);
+}
+__host__ __device__ inline unsigned long long svc_w1(unsigned long long k, int node) {
+  return ((k + 1) << 32) | (unsigned long long)(uint32_t)node;
+}
 
 // Pinned, coherent host memory shared with the grid.
 struct SvcBox {
   SvcCmd cmd[SVC_RING];
-  unsigned long long head;      // commands posted (host)
   unsigned long long consumed;  // commands relayed by shard 0 (device)
+  unsigned long long stamp[8];  // diagnostics (kss_service stamps): shard 0's clock at each phase of the last EVAL
   unsigned long long done[SVC_MAX_SHARDS];  // per shard: 1 + the last EVAL finished
   PodMeta meta;                 // outcome of the last EVAL (shard 0)
   int32_t err;                  // an exchange timed out
   int32_t running;              // 1 while the grid runs (shard 0)
 };
 
-__device__ __forceinline__ unsigned long long ld_sys(const unsigned long long* p) {
-  return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-__device__ __forceinline__ void st_sys(unsigned long long* p, unsigned long long v) {
+// Every access to the pinned box and to the relay goes through address-space-1 pointers
+// (global loads / stores: no flat address-space test on the polled words).
+__device__ __forceinline__ void st_sys(KSS_GLOBAL unsigned long long* p, unsigned long long v) {
   __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
@@ -61,17 +69,20 @@ __device__ __forceinline__ void st_sys(unsigned long long* p, unsigned long long
 template <int ES>
 __device__ __forceinline__ void svc_copy(const uint8_t* src, uint8_t* dst, size_t N, int rows, int lo, int hi) {
   using T = typename std::conditional<ES == 8, uint64_t, typename std::conditional<ES == 2, uint16_t, uint8_t>::type>::type;
-  const T* s = reinterpret_cast<const T*>(src);
-  T* d = reinterpret_cast<T*>(dst);
+  KSS_GLOBAL const T* s = gp(reinterpret_cast<const T*>(src));
+  KSS_GLOBAL T* d = gp(reinterpret_cast<T*>(dst));
   for (int r = 0; r < rows; r++)
     for (int i = lo + (int)threadIdx.x; i < hi; i += (int)blockDim.x) d[(size_t)r * N + i] = s[(size_t)r * N + i];
 }
 
 template <bool GEN>
 __device__ void service_loop(DevCluster c, const DevJob& job, const kss_profile& prof, int W, int npt, int bins_cap,
-                             int cache_keys, unsigned long long* gran, int* err, SvcBox* box,
-                             unsigned long long* relay, unsigned long long* seen, uint8_t* rec_host,
-                             unsigned long long seq, unsigned epoch0, long long* smem) {
+                             int cache_keys, unsigned long long* gran, int* err, SvcBox* box_flat,
+                             unsigned long long* relay_flat, unsigned long long* seen_flat, uint8_t* rec_host,
+                             unsigned long long seq, unsigned epoch0, int stamps, long long* smem) {
+  KSS_GLOBAL SvcBox* box = gp(box_flat);
+  KSS_GLOBAL unsigned long long* relay = gp(relay_flat);
+  KSS_GLOBAL unsigned long long* seen = gp(seen_flat);
   const int w = blockIdx.x;
   const size_t N = (size_t)c.N;
   const SlotLayout L(N);
@@ -101,28 +112,31 @@ __device__ void service_loop(DevCluster c, const DevJob& job, const kss_profile&
   }
   int* cmd = shdr(smem).cmd;
   if (w == 0 && threadIdx.x == 0) __hip_atomic_store(&box->running, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  unsigned long long st0 = 0, st1 = 0, st2 = 0;  // diagnostic clocks of shard 0's lane 0 (stamps)
   for (;; ++seq) {
     if (threadIdx.x == 0) {
       int op = SVC_STOP, pod = 0, node = 0, fields = 0;
-      const unsigned long long tag = (seq + 1) << 32;
-      unsigned long long* slot = relay + 2 * (seq % SVC_DRING);
+      KSS_GLOBAL unsigned long long* slot = relay + 2 * (seq % SVC_DRING);
       if (w == 0) {
         const unsigned long long t0 = wall_clock64();
         bool got = false;
-        for (;;) {  // the host's next command, or STOP after the idle time
-          if (ld_sys(&box->head) > seq) {
+        KSS_GLOBAL const unsigned long long* hc = &box->cmd[seq % SVC_RING].w0;
+        unsigned long long a = 0, b = 0;
+        for (;;) {  // the host's next command (both tagged words), or STOP after the idle time
+          a = __hip_atomic_load(hc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          b = __hip_atomic_load(hc + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          if ((a >> 32) == seq + 1 && (b >> 32) == seq + 1) {
             got = true;
             break;
           }
           if (wall_clock64() - t0 > SVC_IDLE_TICKS) break;
-          __builtin_amdgcn_s_sleep(2);
         }
+        st0 = wall_clock64();
         if (got) {
-          const SvcCmd* hc = box->cmd + seq % SVC_RING;
-          op = __hip_atomic_load(&hc->op, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-          pod = __hip_atomic_load(&hc->pod, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-          node = __hip_atomic_load(&hc->node, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-          fields = __hip_atomic_load(&hc->fields, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          op = (int)(a & 7);
+          fields = (int)((a >> 3) & 31);
+          pod = (int)((a >> 8) & 0xFFFFFF);
+          node = (int)(uint32_t)b;
           if (op < SVC_EVAL || op > SVC_STOP) op = SVC_STOP;
         }
         // the relay slot is reused every SVC_DRING commands: every shard must have taken
@@ -134,11 +148,10 @@ __device__ void service_loop(DevCluster c, const DevJob& job, const kss_profile&
                    wall_clock64() - t1 < 4 * SVC_IDLE_TICKS)
               __builtin_amdgcn_s_sleep(1);
         }
-        const unsigned long long w0 = tag | ((unsigned long long)(uint32_t)pod << 8) |
-                                      ((unsigned long long)(fields & 31) << 3) | (unsigned long long)(op & 7);
-        __hip_atomic_store(slot + 1, tag | (unsigned long long)(uint32_t)node, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(slot, w0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (got) st_sys(&box->consumed, seq + 1);
+        __hip_atomic_store(slot + 1, svc_w1(seq, node), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(slot, svc_w0(seq, op, fields, pod), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (got) __hip_atomic_store(&box->consumed, seq + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        st1 = wall_clock64();
       } else {
         const unsigned long long t0 = wall_clock64();
         for (;;) {
@@ -177,6 +190,7 @@ __device__ void service_loop(DevCluster c, const DevJob& job, const kss_profile&
         if (threadIdx.x == 0) __hip_atomic_store(&box->err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         break;
       }
+      if (stamps && w == 0 && threadIdx.x == 0) st2 = wall_clock64();
       // this shard's node range of the requested fields -> the pinned host record
       if (fields & KSS_FIELD_FAIL) svc_copy<1>(base + L.fail, rec_host + L.fail, N, 1, S.lo, S.hi);
       if (fields & KSS_FIELD_DETAIL) svc_copy<2>(base + L.detail, rec_host + L.detail, N, 1, S.lo, S.hi);
@@ -184,10 +198,22 @@ __device__ void service_loop(DevCluster c, const DevJob& job, const kss_profile&
       if (fields & KSS_FIELD_RAW) svc_copy<8>(base + L.raw, rec_host + L.raw, N, KSS_NSCORE, S.lo, S.hi);
       if (fields & KSS_FIELD_NORM) svc_copy<8>(base + L.norm, rec_host + L.norm, N, KSS_NSCORE, S.lo, S.hi);
       if (w == 0 && threadIdx.x == 0) {
-        box->meta = m;
+        KSS_GLOBAL int32_t* mm = reinterpret_cast<KSS_GLOBAL int32_t*>(&box->meta);
+        mm[0] = m.chosen;
+        mm[1] = m.n_feasible;
+        mm[2] = m.scored;
+        mm[3] = m.status;
+        *reinterpret_cast<KSS_GLOBAL int64_t*>(mm + 4) = m.best_total;
       }
       __threadfence_system();  // this lane's record stores are visible to the host
       __syncthreads();
+      if (stamps && w == 0 && threadIdx.x == 0) {
+        KSS_GLOBAL long long* sp = reinterpret_cast<KSS_GLOBAL long long*>(&box->stamp[0]);
+        sp[0] = (long long)st0;
+        sp[1] = (long long)st1;
+        sp[2] = (long long)st2;
+        sp[3] = wall_clock64();
+      }
       if (threadIdx.x == 0) st_sys(&box->done[w], seq + 1);
     } else if (op == SVC_COMMIT || op == SVC_ROLLBACK) {
       const int local = node - c.node_base;

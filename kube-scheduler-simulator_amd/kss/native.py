@@ -53,6 +53,7 @@ SIGNATURES = [
     ("kss_service_eval", C.c_int, [C.c_void_p, C.c_int32, C.c_uint32, P(abi.PodView)]),
     ("kss_service_commit", C.c_int, [C.c_void_p, C.c_int32, C.c_int32]),
     ("kss_service_rollback", C.c_int, [C.c_void_p, C.c_int32, C.c_int32]),
+    ("kss_service_stamps", C.c_int, [C.c_void_p, P(C.c_uint64)]),
     ("kss_commit", C.c_int, [C.c_void_p, P(abi.PodSet), C.c_int32, C.c_int32]),
     ("kss_rollback", C.c_int, [C.c_void_p, P(abi.PodSet), C.c_int32, C.c_int32]),
     ("kss_schedule_batch", C.c_int, [C.c_void_p, P(abi.PodSet), C.c_int32, C.c_uint32, P(C.c_int32)]),
@@ -371,6 +372,12 @@ class Context:
 
     def service_rollback(self, i: int, node: int):
         check(lib().kss_service_rollback(self.h, i, node))
+
+    def service_stamps(self):
+        """Shard 0's clock (100 MHz ticks) at command taken / relayed / pod done / record visible."""
+        out = (C.c_uint64 * 4)()
+        check(lib().kss_service_stamps(self.h, out))
+        return list(out)
 
     def load_bound(self, boundset_struct: abi.Boundset):
         """The bound pods the PostFilter dry run may evict (CompiledCluster.as_boundset())."""
