@@ -136,17 +136,19 @@ def reduce_over_ranks(elapsed, scheduled, dist):
     return float(t.item()), int(sc.item())
 
 
-def measure_traffic(args, cfg, mode=(), match=("k_simple", "k_schedule", "k_spread"), mean=False):
+def measure_traffic(args, cfg, mode=(), match=("k_simple", "k_schedule", "k_spread"), mean=False, timeout=120):
     """HBM bytes per launch of the scheduling kernel from rocprofv3 PMC counters: one child
     process per counter (FETCH_SIZE, WRITE_SIZE), started before this process touches the
-    GPU.  FETCH_SIZE is doubled (gfx950 tallies 128-B requests at 64 B,
-    MI355X_MICROARCH.md "HBM").  Returns (bytes, detail) or (None, reason)."""
+    GPU, running ONE step.  A step of several launches (C4: one k_spread launch per static
+    chunk) reports the mean over its launches (`launches` in the detail).  FETCH_SIZE is
+    doubled (gfx950 tallies 128-B requests at 64 B, MI355X_MICROARCH.md "HBM").  Returns
+    (bytes, detail) or (None, reason)."""
     if not shutil.which("rocprofv3"):
         return None, "rocprofv3 not found"
-    kb = {}
+    kb, launches = {}, 0
     for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
         d = tempfile.mkdtemp(prefix="kss_pmc_")
-        cmd = ["timeout", "-s", "KILL", "120", "rocprofv3", "--pmc", ctr, "--output-format", "csv", "-d", d, "-o", "p",
+        cmd = ["timeout", "-s", "KILL", str(timeout), "rocprofv3", "--pmc", ctr, "--output-format", "csv", "-d", d, "-o", "p",
                "--", sys.executable, os.path.abspath(__file__), "--inner", "--steps", "1", "--warmup", "0",
                "--config", str(cfg), "--nodes", str(args.nodes), "--pods", str(args.pods), *mode]
         subprocess.run(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL, cwd=ROOT)
@@ -158,10 +160,58 @@ def measure_traffic(args, cfg, mode=(), match=("k_simple", "k_schedule", "k_spre
         shutil.rmtree(d, ignore_errors=True)
         if not vals:
             return None, f"no {ctr} sample"
-        kb[ctr] = sum(vals) / len(vals) if mean else max(vals)
+        kb[ctr] = sum(vals) / len(vals) if mean or len(vals) > 1 else vals[0]
+        launches = len(vals)
     fetch = 2.0 * kb["FETCH_SIZE"] * 1024.0
     write = kb["WRITE_SIZE"] * 1024.0
-    return fetch + write, {"fetch_bytes": fetch, "write_bytes": write, "fetch_size_kb_raw": kb["FETCH_SIZE"]}
+    return fetch + write, {"fetch_bytes": fetch, "write_bytes": write, "fetch_size_kb_raw": kb["FETCH_SIZE"],
+                           "launches": launches, "per": "launch (mean over the launches of one step)"}
+
+
+# VALU issue peak of the chip: 256 CUs x 4 SIMDs, one wave64 VALU instruction per SIMD every
+# 2 cycles (SIMD-32, MI355X_MICROARCH.md "Wave scheduling"), 2.4 GHz max clock.
+VALU_PEAK_INSTS = 256 * 4 * 2.4e9 / 2
+SQ_GROUP = ("SQ_WAVES", "SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS", "SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES",
+            "SQ_WAIT_ANY", "SQ_ACTIVE_INST_VALU")
+
+
+def measure_sq(args, cfg, mode=(), match=("k_simple", "k_schedule", "k_spread"), timeout=120):
+    """Instruction-issue counters of the loop kernel: ONE rocprofv3 --pmc pass of eight SQ
+    counters (one pass holds at most 8 SQ_ counters) over a one-step child run started before
+    this process touches the GPU.  Counts are summed over the launches of the step.  Returns
+    ({counter: value}, detail) or (None, reason)."""
+    if not shutil.which("rocprofv3"):
+        return None, "rocprofv3 not found"
+    d = tempfile.mkdtemp(prefix="kss_sq_")
+    cmd = ["timeout", "-s", "KILL", str(timeout), "rocprofv3", "--pmc", *SQ_GROUP, "--output-format", "csv", "-d", d,
+           "-o", "p", "--", sys.executable, os.path.abspath(__file__), "--inner", "--steps", "1", "--warmup", "0",
+           "--config", str(cfg), "--nodes", str(args.nodes), "--pods", str(args.pods), *mode]
+    subprocess.run(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL, cwd=ROOT)
+    vals, disp = {}, set()
+    for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            if any(m in r["Kernel_Name"] for m in match) and r.get("Counter_Name") in SQ_GROUP:
+                vals[r["Counter_Name"]] = vals.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+                disp.add(r.get("Dispatch_Id"))
+    shutil.rmtree(d, ignore_errors=True)
+    if len(vals) < len(SQ_GROUP):
+        return None, f"SQ counters missing: {sorted(set(SQ_GROUP) - set(vals))}"
+    return vals, {"launches": len(disp), "counters": list(SQ_GROUP)}
+
+
+def valu_roofline(sq, kern_s, evals):
+    """roofline.valu: achieved VALU wave-instructions/s of the loop kernel (SQ_INSTS_VALU over
+    its HIP-event time) against the chip's issue peak, with the issue / wait split."""
+    if not sq:
+        return None
+    achieved = sq["SQ_INSTS_VALU"] / kern_s
+    wc = max(sq["SQ_WAVE_CYCLES"], 1.0)
+    return {"bound": "valu", "achieved": achieved, "peak": VALU_PEAK_INSTS, "unit": "wave64 VALU insts/s",
+            "frac": achieved / VALU_PEAK_INSTS, "valu_insts": sq["SQ_INSTS_VALU"],
+            "valu_insts_per_eval": sq["SQ_INSTS_VALU"] / evals, "salu_insts_per_eval": sq["SQ_INSTS_SALU"] / evals,
+            "lds_insts_per_eval": sq["SQ_INSTS_LDS"] / evals,
+            "wave_cycles_active_valu_frac": sq["SQ_ACTIVE_INST_VALU"] / wc, "wave_cycles_wait_frac": sq["SQ_WAIT_ANY"] / wc,
+            "counters": sq, "peak_note": "256 CUs x 4 SIMDs x 2.4 GHz / 2 cycles per wave64 VALU instruction"}
 
 
 def run_scenarios(args):
@@ -174,8 +224,11 @@ def run_scenarios(args):
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     traffic, traffic_detail = None, "not measured"
+    sq, sq_detail = None, "not measured"
     if rank == 0 and world == 1 and not args.no_traffic:  # before this process touches the GPU
         traffic, traffic_detail = measure_traffic(args, 5, mode=("--scenarios", str(args.scenarios)))
+        # k_static counted too: the sweep's device time covers reset + k_static + k_simple
+        sq, sq_detail = measure_sq(args, 5, mode=("--scenarios", str(args.scenarios)), match=("k_simple", "k_static"))
     dist = None
     if world > 1:
         import torch.distributed as dist
@@ -241,7 +294,10 @@ def run_scenarios(args):
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": info["kernel"],
                          "bytes_per_eval": B_EVAL[5], "algorithmic_bytes_per_launch": B_EVAL[5] * S * n_pods * n_nodes,
                          "traffic_detail": traffic_detail,
-                         "note": "achieved uses device time of reset + k_static + k_simple per sweep"},
+                         "note": "achieved: ALGORITHMIC bytes (109 B per evaluation, most of which never leave LDS) "
+                                 "over the device time of reset + k_static + k_simple per sweep; the binding limit "
+                                 "of this throughput-mode config is instruction issue: see valu"},
+            "valu": valu_roofline(sq, kern_s, S * n_pods * n_nodes), "valu_detail": sq_detail,
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)
@@ -861,8 +917,10 @@ def main():
 
     cfg = args.config
     traffic, traffic_detail = None, "not measured"
+    sq, sq_detail = None, "not measured"
     if rank == 0 and world == 1 and not args.no_traffic:
-        traffic, traffic_detail = measure_traffic(args, cfg)
+        traffic, traffic_detail = measure_traffic(args, cfg, timeout=300 if cfg == 4 else 120)
+        sq, sq_detail = measure_sq(args, cfg, timeout=300 if cfg == 4 else 120)
 
     from kss import abi, native
     from kss.synth import DEFAULT_SIZES, SEED_BASE
@@ -906,7 +964,11 @@ def main():
     pods_per_s = scheduled_total * args.steps / elapsed
     kern_avg_s = sum(kern_ms) / len(kern_ms) / 1e3
     loop_s = sum(loop_ms[-args.steps:]) / args.steps / 1e3  # the dominant kernel (k_simple / k_schedule) alone
-    achieved = B_EVAL[cfg] * n_pods * n_nodes / loop_s / 1e9
+    achieved = B_EVAL[cfg] * n_pods * n_nodes / loop_s / 1e9  # = per-launch bytes / mean launch time
+    # loop-kernel launches per step: one per static chunk (C4: several); from the PMC run when it
+    # ran, else from the chunk size the library reports
+    launches = traffic_detail.get("launches", 0) if isinstance(traffic_detail, dict) else 0
+    launches = launches or max(1, ctx.last_timing()[1] // 2 if ctx.last_kernel() != "k_schedule" else 1)
 
     print(json.dumps({"rank": rank, "device": local, "world_size": world, "pods_scheduled": scheduled,
                       "elapsed_s": t1 - t0}), file=sys.stderr, flush=True)
@@ -948,8 +1010,10 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": ctx.last_kernel(), "bytes_per_eval": B_EVAL[cfg],
-                         "algorithmic_bytes_per_launch": B_EVAL[cfg] * n_pods * n_nodes,
-                         "traffic_detail": traffic_detail, "latency": latency},
+                         "launches_per_step": launches,
+                         "algorithmic_bytes_per_launch": B_EVAL[cfg] * n_pods * n_nodes / launches,
+                         "traffic_detail": traffic_detail, "latency": latency,
+                         "valu": valu_roofline(sq, loop_s, n_pods * n_nodes), "valu_detail": sq_detail},
             "cpu_baseline": cpu,
             "c4_split": c4,
         }

@@ -27,11 +27,11 @@ namespace kss {
 
 // floor(x / d) for 0 <= x, 0 < d, x / d <= ~2^7 and d, x < 2^31 (the estimate's
 // error bound needs only the small quotient; x may exceed 2^24).  rd = rcp(d).
+// Branch-free: with d > 0 at most one of the two corrections applies.
 __device__ __forceinline__ int32_t small_div(int32_t x, int32_t d, float rd) {
-  int32_t q = (int32_t)((float)x * rd);
-  if ((int64_t)q * d > (int64_t)x) q--;
-  else if ((int64_t)(q + 1) * d <= (int64_t)x) q++;
-  return q;
+  const int32_t q = (int32_t)((float)x * rd);
+  const int64_t p = (int64_t)q * d;
+  return q + (p + d <= (int64_t)x ? 1 : 0) - (p > (int64_t)x ? 1 : 0);
 }
 
 // floor(x / A) for 0 <= x < 2^53, 0 < A < 2^53, x / A <= ~2^7; invA = RN(1 / (double)A).

@@ -202,7 +202,7 @@ __global__ __launch_bounds__(KSS_MAX_THREADS) void k_simple(const DevJob* __rest
     __syncthreads();
   }
   const kss_profile& P = DEF ? def_prof : H.prof;
-  simple_schedule(job.c, job.spods, job.stat, job.P.ints, k0, min(k1, job.n_pods), job.chosen, job.meta, P, W, w, cap,
+  simple_schedule<DEF>(job.c, job.spods, job.stat, job.P.ints, k0, min(k1, job.n_pods), job.chosen, job.meta, P, W, w, cap,
                   gran ? gran + (size_t)ji * 2 * W * SX_VALS : nullptr, X, epoch0, err, ji == 0 ? stamps : nullptr, smem);
 }
 
@@ -211,7 +211,7 @@ __global__ __launch_bounds__(KSS_MAX_THREADS) void k_simple(const DevJob* __rest
 template <bool DEF>
 __global__ __launch_bounds__(KSS_MAX_THREADS) void k_spread(const DevJob* __restrict__ jobs, int W, int cap, int bins_cap,
                                                             int n_res, int gq, int k0, int k1, unsigned long long* gran,
-                                                            int* err, unsigned long long* stamps, XPeers X,
+                                                            int* err, unsigned long long* stamps, int nst, XPeers X,
                                                             unsigned epoch0) {
   extern __shared__ __attribute__((aligned(16))) long long smem[];
   const int Wl = X.n > 1 ? X.wl : W;
@@ -227,7 +227,7 @@ __global__ __launch_bounds__(KSS_MAX_THREADS) void k_spread(const DevJob* __rest
   }
   const kss_profile& P = DEF ? def_prof : H.prof;
   spread_schedule(job.c, job.gpods, job.stat, job.res_rows, n_res, k0, min(k1, job.n_pods), job.chosen, job.meta, P, W, w,
-                  cap, bins_cap, gq, gran ? gran + (size_t)ji * 2 * W * G_XW : nullptr, X, epoch0, err, stamps, smem);
+                  cap, bins_cap, gq, gran ? gran + (size_t)ji * 2 * W * G_XW : nullptr, X, epoch0, err, stamps, nst, smem);
 }
 
 // Class / term counts of the chosen nodes of pods [k0, min(k1, n_pods)) of every job
@@ -2147,8 +2147,11 @@ static int launch_spread(hipStream_t st, const Geometry& g, const GpodNeeds& q, 
                          hipEvent_t* ev = nullptr, const SplitRun* split = nullptr) {
   int cap = spread_cap(g, (size_t)max_nodes), bins_cap = q.bins_cap, nr = n_res, gq = q.gq;
   size_t shmem = spread_lds(g, q, n_keys, n_res, (size_t)max_nodes);
-  if (stamps && shmem + G_STAMP_LDS > KSS_LDS_BUDGET) stamps = nullptr;  // diagnostics only where they fit
-  if (stamps) shmem += G_STAMP_LDS;
+  // diagnostic stamps in LDS: as many pods (<= G_NSTAMP, >= 8) as fit beside the shard state
+  int nst = 0;
+  if (stamps && shmem < KSS_LDS_BUDGET) nst = (int)std::min<size_t>(G_NSTAMP, (KSS_LDS_BUDGET - shmem) / (16 * 8));
+  if (nst < 8) stamps = nullptr, nst = 0;
+  shmem += (size_t)nst * 16 * 8;
   const bool def = same_profile(prof, default_profile_c());
   const void* fn = def ? (const void*)k_spread<true> : (const void*)k_spread<false>;
   HIP_TRY(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shmem));
@@ -2175,9 +2178,8 @@ static int launch_spread(hipStream_t st, const Geometry& g, const GpodNeeds& q, 
       HIP_TRY(hipMemsetAsync(gran, 0, gran_bytes, st));
     }
     unsigned long long* sp = k0 == 0 ? stamps : nullptr;
-    void* args[] = {(void*)&jobs, (void*)&W,  (void*)&cap,  (void*)&bins_cap, (void*)&nr, (void*)&gq,
-                    (void*)&k0,   (void*)&k1, (void*)&gc,   (void*)&err,      (void*)&sp, (void*)&X,
-                    (void*)&epoch0};
+    void* args[] = {(void*)&jobs, (void*)&W,  (void*)&cap, (void*)&bins_cap, (void*)&nr,  (void*)&gq, (void*)&k0,
+                    (void*)&k1,   (void*)&gc, (void*)&err, (void*)&sp,       (void*)&nst, (void*)&X,  (void*)&epoch0};
     const int ci = k0 / chunk;
     if (ev) HIP_TRY(hipEventRecord(ev[2 * ci], st));
     if (g.W > 1) {
@@ -3634,8 +3636,8 @@ int upload_bound(kss_ctx* ctx) {
   size_t o_ptr = 0, o_id = align_up(4 * (N + 1), 256), o_prio = align_up(o_id + 8 * NB, 256),
          o_start = align_up(o_prio + 4 * NB, 256), o_cls = align_up(o_start + 8 * NB, 256),
          o_req = align_up(o_cls + 4 * NB, 256), o_toff = align_up(o_req + 8 * KSS_NRES * NB, 256),
-         o_tlen = align_up(o_toff + 4 * NB, 256), o_ints = align_up(o_tlen + 4 * NB, 256),
-         total = align_up(o_ints + 4 * std::max(ni, (size_t)1), 256);
+         o_tlen = align_up(o_toff + 4 * NB, 256), o_ord = align_up(o_tlen + 4 * NB, 256),
+         o_ints = align_up(o_ord + 4 * NB, 256), total = align_up(o_ints + 4 * std::max(ni, (size_t)1), 256);
   std::vector<char>& h = ctx->stage_host;
   h.assign(total, 0);
   int32_t* ptr = (int32_t*)(h.data() + o_ptr);
@@ -3647,9 +3649,22 @@ int upload_bound(kss_ctx* ctx) {
   int32_t* toff = (int32_t*)(h.data() + o_toff);
   int32_t* tlen = (int32_t*)(h.data() + o_tlen);
   int32_t* ints = (int32_t*)(h.data() + o_ints);
+  int32_t* ord = (int32_t*)(h.data() + o_ord);
   size_t e = 0, t = 0;
+  std::vector<int32_t> perm;
   for (int n = 0; n < N; n++) {
     ptr[n] = (int32_t)e;
+    // the node's pods in MoreImportantPod order (priority descending, start ascending, NodeInfo
+    // order on ties — the preemptor does not enter it): SelectVictimsOnNode's reprieve order,
+    // and the pods below a priority form a suffix of it
+    const auto& v = per[n];
+    perm.resize(v.size());
+    for (size_t k = 0; k < v.size(); k++) perm[k] = (int32_t)k;
+    std::stable_sort(perm.begin(), perm.end(), [&](int32_t a, int32_t b) {
+      if (v[a].prio != v[b].prio) return v[a].prio > v[b].prio;
+      return v[a].start < v[b].start;
+    });
+    for (size_t k = 0; k < v.size(); k++) ord[e + k] = (int32_t)e + perm[k];
     for (const BoundPod& b : per[n]) {
       id[e] = b.id;
       prio[e] = b.prio;
@@ -3677,6 +3692,7 @@ int upload_bound(kss_ctx* ctx) {
   B.req = (const int64_t*)(d + o_req);
   B.toff = (const int32_t*)(d + o_toff);
   B.tlen = (const int32_t*)(d + o_tlen);
+  B.ord = (const int32_t*)(d + o_ord);
   B.ints = (const int32_t*)(d + o_ints);
   ctx->bound_dirty = false;
   return 0;
@@ -3724,7 +3740,7 @@ int kss_postfilter_pod(kss_ctx* ctx, const kss_podset* ps, int32_t pod_index, ks
   const int cap = out->victims_cap;
   const size_t o_job = 0, o_out = align_up(sizeof(PreemptJob), 256), o_vic = o_out + sizeof(PreemptOut),
                o_key = align_up(o_vic + 8 * (size_t)std::max(cap, 1), 256),
-               o_g = align_up(o_key + 4 * 8 * std::max(N, (size_t)1), 256), o_bins = align_up(o_g + sizeof(PreGlobal), 256),
+               o_g = align_up(o_key + 5 * 8 * std::max(N, (size_t)1), 256), o_bins = align_up(o_g + sizeof(PreGlobal), 256),
                total = o_bins + 8 * (size_t)bins_cap;
   if ((rc = ctx->pre_buf.ensure(total))) return rc;
   char* d = (char*)ctx->pre_buf.p;
@@ -3741,6 +3757,7 @@ int kss_postfilter_pod(kss_ctx* ctx, const kss_podset* ps, int32_t pod_index, ks
   J.bins_cap = bins_cap;
   J.victims_cap = cap;
   J.key = (int64_t*)(d + o_key);
+  J.n_blocks = (int32_t)std::max<size_t>((N + PRE_NODE_THREADS - 1) / PRE_NODE_THREADS, 1);
   J.victims = (int64_t*)(d + o_vic);
   J.out = (PreemptOut*)(d + o_out);
   J.G = (PreGlobal*)(d + o_g);

@@ -20,12 +20,14 @@
 //      pair counts move, the spread minimum becomes min(min over the other pairs, the
 //      node's pair) — criticalPaths.update keeps exactly that minimum when one pair
 //      changes), run the filters, then reprieve in MoreImportantPod order (priority
-//      descending, start time ascending, NodeInfo order on ties), keeping each pod whose
-//      return still lets the pod fit;
-//   4. pickOneNodeForPreemption as successive workgroup reductions over the candidates'
+//      descending, start time ascending, NodeInfo order on ties: sorted per node on the host
+//      when the bound-pod table is uploaded), keeping each pod whose return still lets the
+//      pod fit;
+//   4. pickOneNodeForPreemption as a lexicographic reduction over the candidates'
 //      (highest victim priority min, Σ(priority + 2^31) min, #victims min, earliest
 //      start of the highest-priority victims max, node index min) — the last criterion
-//      replaces the Go map order upstream leaves to chance;
+//      replaces the Go map order upstream leaves to chance — per k_preempt_nodes workgroup,
+//      then over the workgroups' tuples;
 //   5. one lane re-runs the nominated node's reprieve loop and writes the victims' ids in
 //      eviction order.
 // No PodDisruptionBudgets (every victim is non-violating) and no nominated pods.
@@ -48,6 +50,7 @@ struct DevBound {
   const int64_t* req;    // [nb][KSS_NRES]
   const int32_t* toff;   // [nb] into ints
   const int32_t* tlen;   // [nb]
+  const int32_t* ord;    // [nb] per node, its pods' indices in MoreImportantPod order (host-sorted)
   const int32_t* ints;
 };
 
@@ -72,8 +75,8 @@ struct PreemptJob {
   int32_t pi;        // the preemptor's index in P
   int32_t bins_cap;  // LDS histogram + presence bins
   int32_t victims_cap;
-  int32_t pad;
-  int64_t* key;      // [4][N] HBM scratch: candidate keys per node
+  int32_t n_blocks;  // k_preempt_nodes workgroups
+  int64_t* key;      // [5][n_blocks] HBM scratch: each workgroup's best candidate (hp, sum, cnt, start, node)
   int64_t* victims;  // [victims_cap]
   PreemptOut* out;
   PreGlobal* G;
@@ -141,27 +144,56 @@ __device__ __forceinline__ void apply_pod(const PreemptJob& J, const kss_pod& p,
   const DevCluster& c = J.c;
   const DevPods& P = J.P;
   const int nr = 3 + c.n_scalar;
-  for (int r = 0; r < nr; r++) s.req[r] += sign * J.B.req[(size_t)e * KSS_NRES + r];
+#pragma unroll
+  for (int r = 0; r < KSS_NRES; r++)
+    if (r < nr) s.req[r] += sign * J.B.req[(size_t)e * KSS_NRES + r];
   s.pods += sign;
   const int cls = J.B.cls[e];
   const kss_spread* sp = P.spreads + p.spread_off;
-  for (int j = 0; j < p.n_hard; j++)  // each matching constraint moves the shared pair counter
-    if (in_list(P.ints, sp[j].cls_off, sp[j].cls_len, cls)) s.M[pl.hard_own[j]] += sign;
+  // the DryState arrays are indexed by compile-time constants only (selects), so they stay in
+  // registers: a runtime index would put the whole state in scratch
+  for (int j = 0; j < p.n_hard; j++) {  // each matching constraint moves the shared pair counter
+    if (!in_list(P.ints, sp[j].cls_off, sp[j].cls_len, cls)) continue;
+    const int o = pl.hard_own[j];
+#pragma unroll
+    for (int x = 0; x < MAXH; x++) s.M[x] += x == o ? sign : 0;
+  }
   const kss_ipa* ip = P.ipa + p.ipa_off;
   for (int q = 0; q < p.ipa_len; q++) {
     const kss_ipa& en = ip[q];
     if (en.kind > KSS_IPA_REQ_ANTI) continue;
     if (label_of(c, en.key, n) < 0) continue;  // topologyToMatchedTermCount.update: node lacks the key
     const int k = slot_of(pl, en.key);
+    int d = 0, h = 0;
     if (en.kind == KSS_IPA_EXISTING_ANTI) {
       const int t0 = J.B.toff[e], tl = J.B.tlen[e];
-      for (int t = 0; t < tl; t++)
-        if (in_list(P.ints, en.row_off, en.row_len, J.B.ints[t0 + t])) s.A[k][0] += sign;
+      for (int t = 0; t < tl; t++) d += in_list(P.ints, en.row_off, en.row_len, J.B.ints[t0 + t]) ? sign : 0;
     } else if (in_list(P.ints, en.row_off, en.row_len, cls)) {
-      s.A[k][en.kind == KSS_IPA_REQ_AFFINITY ? 1 : 2] += sign;
+      d = sign;
+      h = en.kind == KSS_IPA_REQ_AFFINITY ? 1 : 2;
       if (en.kind == KSS_IPA_REQ_AFFINITY) s.T += sign;
     }
+#pragma unroll
+    for (int x = 0; x < MAXK; x++)
+#pragma unroll
+      for (int y = 0; y < 3; y++) s.A[x][y] += (x == k && y == h) ? d : 0;
   }
+}
+
+// s.M[o] / s.A[k][h] for runtime o, k (selects over the unrolled indices: no scratch)
+__device__ __forceinline__ int64_t dry_m(const DryState& s, int o) {
+  int64_t v = 0;
+#pragma unroll
+  for (int x = 0; x < MAXH; x++) v = x == o ? s.M[x] : v;
+  return v;
+}
+__device__ __forceinline__ int64_t dry_a(const DryState& s, int k, int h) {
+  int64_t v = 0;
+#pragma unroll
+  for (int x = 0; x < MAXK; x++)
+#pragma unroll
+    for (int y = 0; y < 3; y++) v = (x == k && y == h) ? s.A[x][y] : v;
+  return v;
 }
 
 // RunFilterPluginsWithNominatedPods on the modified node: NodeResourcesFit, PodTopologySpread,
@@ -175,14 +207,16 @@ __device__ __forceinline__ bool dry_fits(const PreemptJob& J, const kss_pod& p, 
   if ((en >> KSS_F_NODE_RESOURCES_FIT) & 1u) {
     if (s.pods + 1 > (int64_t)c.allowed_pods[n]) return false;
     const int nr = 3 + c.n_scalar;
-    bool all_zero = true;
-    for (int r = 0; r < nr; r++) all_zero &= (p.fit_request[r] == 0);
-    if (!all_zero)
-      for (int r = 0; r < nr; r++) {
-        const int64_t q = p.fit_request[r];
-        if (r >= KSS_RES_SCALAR0 && q == 0) continue;
-        if (q > c.alloc[(size_t)r * N + n] - s.req[r]) return false;
-      }
+    bool all_zero = true, bad = false;
+#pragma unroll
+    for (int r = 0; r < KSS_NRES; r++) {
+      if (r >= nr) continue;
+      const int64_t q = p.fit_request[r];
+      all_zero &= q == 0;
+      if (r >= KSS_RES_SCALAR0 && q == 0) continue;
+      bad |= q > c.alloc[(size_t)r * N + n] - s.req[r];
+    }
+    if (!all_zero && bad) return false;
   }
   if (((en >> KSS_F_POD_TOPOLOGY_SPREAD) & 1u) && p.n_hard > 0) {
     const kss_spread* sp = P.spreads + p.spread_off;
@@ -192,8 +226,9 @@ __device__ __forceinline__ bool dry_fits(const PreemptJob& J, const kss_pod& p, 
       const int o = pl.hard_own[i];
       const int64_t my = pl.hard_off[o] >= 0 ? (int64_t)d : (int64_t)n;
       const int64_t others = H.id0[o] == my ? H.m1[o] : H.m0[o];
-      const int64_t mn = s.M[o] < others ? s.M[o] : others;
-      if (s.M[o] + (int64_t)sp[i].self_match - mn > (int64_t)sp[i].max_skew) return false;
+      const int64_t mo = dry_m(s, o);
+      const int64_t mn = mo < others ? mo : others;
+      if (mo + (int64_t)sp[i].self_match - mn > (int64_t)sp[i].max_skew) return false;
     }
   }
   if (((en >> KSS_F_INTER_POD_AFFINITY) & 1u) && p.ipa_len > 0) {
@@ -203,24 +238,17 @@ __device__ __forceinline__ bool dry_fits(const PreemptJob& J, const kss_pod& p, 
       if (ip[q].kind != KSS_IPA_REQ_AFFINITY) continue;
       have = true;
       if (label_of(c, ip[q].key, n) < 0) return false;
-      if (s.A[slot_of(pl, ip[q].key)][1] <= 0) exist = false;
+      if (dry_a(s, slot_of(pl, ip[q].key), 1) <= 0) exist = false;
     }
     if (have && !exist && !(s.T == 0 && (p.flags & KSS_POD_IPA_SELF_MATCH))) return false;
     for (int q = 0; q < p.ipa_len; q++) {
       const int kind = ip[q].kind;
       if (kind != KSS_IPA_REQ_ANTI && kind != KSS_IPA_EXISTING_ANTI) continue;
       if (label_of(c, ip[q].key, n) < 0) continue;
-      if (s.A[slot_of(pl, ip[q].key)][kind == KSS_IPA_REQ_ANTI ? 2 : 0] > 0) return false;
+      if (dry_a(s, slot_of(pl, ip[q].key), kind == KSS_IPA_REQ_ANTI ? 2 : 0) > 0) return false;
     }
   }
   return true;
-}
-
-// MoreImportantPod order with NodeInfo order on ties: a before b
-__device__ __forceinline__ bool before(const DevBound& B, int a, int b) {
-  if (B.prio[a] != B.prio[b]) return B.prio[a] > B.prio[b];
-  if (B.start[a] != B.start[b]) return B.start[a] < B.start[b];
-  return a < b;
 }
 
 struct DryResult {
@@ -236,19 +264,23 @@ __device__ __forceinline__ DryResult select_victims(const PreemptJob& J, const k
   DryResult res{INT64_MAX, 0, 0, 0};
   const int e0 = B.ptr[n], e1 = B.ptr[n + 1];
   const int prio = p.priority;
-  int nv = 0;
-  for (int e = e0; e < e1; e++) nv += B.prio[e] < prio;
-  if (nv == 0) return res;  // "No preemption victims found for incoming pod"
+  // the potential victims (priority below the preemptor's) are the suffix [p0, e1) of the
+  // node's importance order, visited in reprieve order
+  int p0 = e1;
+  while (p0 > e0 && B.prio[B.ord[p0 - 1]] < prio) p0--;
+  if (p0 == e1) return res;  // "No preemption victims found for incoming pod"
   // the node's view, then every lower-priority pod removed
   DryState s;
   const size_t N = (size_t)c.N;
+#pragma unroll
   for (int r = 0; r < KSS_NRES; r++) s.req[r] = r < 3 + c.n_scalar ? c.requested[(size_t)r * N + n] : 0;
   s.pods = c.pod_count[n];
   const kss_spread* sp = P.spreads + p.spread_off;
 #pragma unroll
   for (int i = 0; i < MAXH; i++) s.M[i] = 0;
-  for (int i = 0; i < p.n_hard; i++) {
-    if (pl.hard_own[i] != i) continue;
+#pragma unroll
+  for (int i = 0; i < MAXH; i++) {
+    if (i >= p.n_hard || pl.hard_own[i] != i) continue;
     if (pl.hard_off[i] >= 0) {
       const int d = label_of(c, sp[i].key, n);
       s.M[i] = d >= 0 ? bins[pl.hard_off[i] + d] : 0;
@@ -261,26 +293,22 @@ __device__ __forceinline__ DryResult select_victims(const PreemptJob& J, const k
   for (int k = 0; k < MAXK; k++)
 #pragma unroll
     for (int h = 0; h < 3; h++) s.A[k][h] = 0;
-  for (int k = 0; k < pl.n_keys; k++) {
+#pragma unroll
+  for (int k = 0; k < MAXK; k++) {
+    if (k >= pl.n_keys) continue;
     const int d = label_of(c, pl.key[k], n);
     if (d < 0) continue;
+#pragma unroll
     for (int h = 0; h < 3; h++) s.A[k][h] = ipa_value(c, P, p, pl, bins, k, h, d, n);
   }
   s.T = H.aff_total;
-  for (int e = e0; e < e1; e++)
-    if (B.prio[e] < prio) apply_pod(J, p, pl, e, n, -1, s);
+  for (int k = p0; k < e1; k++) apply_pod(J, p, pl, B.ord[k], n, -1, s);
   if (!dry_fits(J, p, pl, H, s, n)) return res;
-  // reprieve in importance order: the next pod is the least one after `last`
-  int last = -1, victims = 0;
+  // reprieve in importance order (MoreImportantPod, NodeInfo order on ties)
+  int victims = 0;
   int64_t hp = 0, sum = 0, st = 0;
-  for (int k = 0; k < nv; k++) {
-    int best = -1;
-    for (int e = e0; e < e1; e++) {
-      if (B.prio[e] >= prio) continue;
-      if (last >= 0 && !before(B, last, e)) continue;
-      if (best < 0 || before(B, e, best)) best = e;
-    }
-    last = best;
+  for (int k = p0; k < e1; k++) {
+    const int best = B.ord[k];
     apply_pod(J, p, pl, best, n, 1, s);
     if (!dry_fits(J, p, pl, H, s, n)) {
       apply_pod(J, p, pl, best, n, -1, s);
@@ -424,9 +452,8 @@ __device__ void preempt_nodes(const PreemptJob& J, long long* smem) {
   const int N = c.N;
   const int n = (int)(blockIdx.x * blockDim.x) + tid;
   long long n_pot = 0, n_cand = 0, feasible = 0;
-  int64_t* K = J.key;
+  DryResult best{INT64_MAX, INT64_MAX, INT64_MAX, INT64_MIN};
   if (n < N) {
-    K[n] = INT64_MAX;
     if (p.names_len >= 0 && !in_names(P, p, (int64_t)c.node_base + n)) {
       n_pot = 1;  // no status in the map: potential, but NodeAffinity rejects it in the dry run
     } else {
@@ -454,10 +481,7 @@ __device__ void preempt_nodes(const PreemptJob& J, long long* smem) {
         const DryResult d = select_victims(J, p, pl, H, bins, n, false);
         if (d.hp != INT64_MAX) {
           n_cand = 1;
-          K[n] = d.hp;
-          K[N + n] = d.sum;
-          K[2 * (size_t)N + n] = d.cnt;
-          K[3 * (size_t)N + n] = d.start;
+          best = d;
         }
       }
     }
@@ -465,6 +489,29 @@ __device__ void preempt_nodes(const PreemptJob& J, long long* smem) {
   n_pot = block_op(n_pot, OP_SUM, H.red);
   n_cand = block_op(n_cand, OP_SUM, H.red);
   feasible = block_op(feasible, OP_SUM, H.red);
+  // pickOneNodeForPreemption over this workgroup's candidates (lexicographic: highest victim
+  // priority min, priority sum min, victims min, start max, node min): k_preempt_pick then
+  // reduces one tuple per workgroup instead of re-reading every node's keys
+  {
+    const long long hp = block_op(best.hp, OP_MIN, H.red);
+    bool eq = best.hp == hp;
+    const long long sum = block_op(eq ? best.sum : INT64_MAX, OP_MIN, H.red);
+    eq &= best.sum == sum;
+    const long long cnt = block_op(eq ? best.cnt : INT64_MAX, OP_MIN, H.red);
+    eq &= best.cnt == cnt;
+    const long long st = block_op(eq ? best.start : INT64_MIN, OP_MAX, H.red);
+    eq &= best.start == st;
+    const long long nn = block_op(eq && hp != INT64_MAX ? (long long)n : INT64_MAX, OP_MIN, H.red);
+    if (tid == 0) {
+      const int b = (int)blockIdx.x, nb = J.n_blocks;
+      int64_t* K = J.key;
+      K[b] = hp;
+      K[nb + b] = sum;
+      K[2 * nb + b] = cnt;
+      K[3 * nb + b] = st;
+      K[4 * nb + b] = nn;
+    }
+  }
   if (tid == 0) {
     PreGlobal& Gw = *J.G;
     if (n_pot) atomicAdd(&Gw.n_potential, (int)n_pot);
@@ -509,28 +556,25 @@ __device__ void preempt_pick(const PreemptJob& J, long long* smem) {
     H.flags = G.flags;
   }
   __syncthreads();
-  const int N = c.N;
+  const int nb = J.n_blocks;
   const int64_t* K = J.key;
-  // pickOneNodeForPreemption as successive reductions
-  long long v = INT64_MAX;
-  for (int n = tid; n < N; n += nt) v = min(v, (long long)K[n]);
-  const long long hp = block_op(v, OP_MIN, H.red);
-  v = INT64_MAX;
-  for (int n = tid; n < N; n += nt)
-    if (K[n] == hp) v = min(v, (long long)K[N + n]);
-  const long long sum = block_op(v, OP_MIN, H.red);
-  v = INT64_MAX;
-  for (int n = tid; n < N; n += nt)
-    if (K[n] == hp && K[N + n] == sum) v = min(v, (long long)K[2 * (size_t)N + n]);
-  const long long cnt = block_op(v, OP_MIN, H.red);
-  v = INT64_MIN;
-  for (int n = tid; n < N; n += nt)
-    if (K[n] == hp && K[N + n] == sum && K[2 * (size_t)N + n] == cnt) v = max(v, (long long)K[3 * (size_t)N + n]);
-  const long long st = block_op(v, OP_MAX, H.red);
-  v = INT64_MAX;
-  for (int n = tid; n < N; n += nt)
-    if (K[n] == hp && K[N + n] == sum && K[2 * (size_t)N + n] == cnt && K[3 * (size_t)N + n] == st) v = min(v, (long long)n);
-  const long long best = block_op(v, OP_MIN, H.red);
+  // pickOneNodeForPreemption over the workgroups' best tuples (each lane folds its share
+  // lexicographically, then the same successive reductions over the lanes)
+  long long hp = INT64_MAX, sum = INT64_MAX, cnt = INT64_MAX, st = INT64_MIN, nn = INT64_MAX;
+  for (int b = tid; b < nb; b += nt) {
+    const long long h = K[b], s2 = K[nb + b], c2 = K[2 * nb + b], t2 = K[3 * nb + b], n2 = K[4 * nb + b];
+    const bool better = h != hp ? h < hp : (s2 != sum ? s2 < sum : (c2 != cnt ? c2 < cnt : (t2 != st ? t2 > st : n2 < nn)));
+    if (better) hp = h, sum = s2, cnt = c2, st = t2, nn = n2;
+  }
+  const long long bhp = block_op(hp, OP_MIN, H.red);
+  bool eq = hp == bhp;
+  const long long bsum = block_op(eq ? sum : INT64_MAX, OP_MIN, H.red);
+  eq &= sum == bsum;
+  const long long bcnt = block_op(eq ? cnt : INT64_MAX, OP_MIN, H.red);
+  eq &= cnt == bcnt;
+  const long long bst = block_op(eq ? st : INT64_MIN, OP_MAX, H.red);
+  eq &= st == bst;
+  const long long best = block_op(eq ? nn : INT64_MAX, OP_MIN, H.red);
   // the nominated node's victims, by lane 0
   if (tid == 0) {
     const DryResult d = select_victims(J, H.pod, H.plan, H, J.gbins, (int)best, true);

@@ -582,35 +582,82 @@ __device__ __forceinline__ void add_commit(DynRow& r, const SPod& p) {
   r.pods += 1;
 }
 
+// leastRequestedScore for the branch-free default-profile evaluation: 0 when requested >
+// capacity; the caller masks capacity 0 (inv 0).
+__device__ __forceinline__ int32_t least_bf(double requested, double capacity, double inv) {
+  const bool over = requested > capacity;
+  const double x = (capacity - (over ? capacity : requested)) * 100.0;  // integers below 2^53: exact, >= 0
+  int32_t q = (int32_t)(x * inv);
+  const double r = fma(-(double)q, capacity, x);
+  q += (r >= capacity ? 1 : 0) - (r < 0.0 ? 1 : 0);
+  return over ? 0 : q;
+}
+
+// dyn_eval of the v1.26 default profile (NodeResourcesFit LeastAllocated over cpu / memory
+// with weights 1 / 1, BalancedAllocation over cpu / memory), branch-free: every lane
+// computes every score and selects, so the node loop carries no exec-mask regions.  The
+// scores of an infeasible node are not read (pass B skips it).
+__device__ __forceinline__ SVal dyn_eval_def(const SPod& q, uint32_t w, const DynRow& r) {
+  const int code = sw_code(w);
+  bool bad = (int64_t)r.pods + 1 > (int64_t)r.allowed;
+  const bool rq = !(q.flags & SP_ALLZERO);
+  bad |= rq & ((q.fit_req[0] > r.alloc[0] - r.req[0]) | (q.fit_req[1] > r.alloc[1] - r.req[1]) |
+               (q.fit_req[2] > r.alloc[2] - r.req[2]));
+  SVal e;
+  e.f = code ? code : (bad ? KSS_F_NODE_RESOURCES_FIT : 0);
+  e.tt = sw_tt(w);
+  e.na = sw_na(w);
+  const bool u0 = r.alloc[0] != 0.0, u1 = r.alloc[1] != 0.0;
+  // NodeResourcesFit.Score: capacity-0 resources drop out of the score and the weight sum
+  const int32_t s0 = u0 ? least_bf(r.nz[0] + q.snz[0], r.alloc[0], r.inv[0]) : 0;
+  const int32_t s1 = u1 ? least_bf(r.nz[1] + q.snz[1], r.alloc[1], r.inv[1]) : 0;
+  e.fit = (u0 && u1) ? (s0 + s1) >> 1 : s0 + s1;
+  // BalancedAllocation: two used resources give |f0 - f1| / 2, fewer a zero deviation
+  double f0 = div_rn_d(r.req[0] + q.sreq[0], r.alloc[0], r.inv[0]);
+  double f1 = div_rn_d(r.req[1] + q.sreq[1], r.alloc[1], r.inv[1]);
+  f0 = f0 > 1.0 ? 1.0 : f0;
+  f1 = f1 > 1.0 ? 1.0 : f1;
+  const double sd = (u0 && u1) ? fabs((f0 - f1) / 2.0) : 0.0;
+  e.ba = (int32_t)((1.0 - sd) * 100.0);
+  return e;
+}
+
 // Pass A for pod q (static words in ring slot `sl`) over the shard's `own` nodes on the
 // current state (H0), plus the candidate slot `cand_s` (-1 none) re-evaluated with the
 // previous pod `q0` committed on it (H1), by the first slot without a node (slot `own`,
 // which is slot `cap` of lane 0 when the shard is full).  st = {nf0, tt0, na0, nf1, tt1, na1}.
-__device__ __forceinline__ void simple_pass_a(const kss_profile& prof, const SPod& q, const SPod& q0, const SimpleShard& L,
-                                              int sl, int own, int cand_s, long long (&st)[6]) {
+// Both records are copied to registers before the node loop (its LDS stores would otherwise
+// make the compiler re-read every record field inside the loop, one LDS round trip each).
+template <bool DEF>
+__device__ __forceinline__ void simple_pass_a(const kss_profile& prof, const SPod& q_lds, const SPod& q0_lds,
+                                              const SimpleShard& L, int sl, int own, int cand_s, long long (&st)[6]) {
   const int tid = threadIdx.x, nt = blockDim.x;
   const uint32_t* sw = L.st + (size_t)sl * L.cap;
-  long long nf = 0, tt = 0, na = 0, nf1 = 0, tt1 = 0, na1 = 0;
+  const SPod q = q_lds;
+  SPod q0;
+#pragma unroll
+  for (int k = 0; k < 3; k++) q0.creq[k] = q0_lds.creq[k];
+  q0.cnz[0] = q0_lds.cnz[0];
+  q0.cnz[1] = q0_lds.cnz[1];
+  int32_t nf = 0, tt = 0, na = 0, nf1 = 0, tt1 = 0, na1 = 0;  // raw TT <= 64, NA < 2^20
   for (int s = tid; s <= L.cap; s += nt) {
     const bool extra = s == own && cand_s >= 0;
     if (s >= own && !extra) continue;
     const int ns = extra ? cand_s : s;
+    const uint32_t wd = sw[ns];
     DynRow r = shard_row(L, ns);
     if (extra) add_commit(r, q0);
-    const SVal e = dyn_eval(prof, q, sw[ns], r);
+    const SVal e = DEF ? dyn_eval_def(q, wd, r) : dyn_eval(prof, q, wd, r);
     cv_put(L, extra ? L.cap : s, e);
-    if (e.f == 0) {
-      if (!extra) {
-        nf++;
-        tt = e.tt > tt ? e.tt : tt;
-        na = e.na > na ? e.na : na;
-      }
-      if (s != cand_s) {
-        nf1++;
-        tt1 = e.tt > tt1 ? e.tt : tt1;
-        na1 = e.na > na1 ? e.na : na1;
-      }
-    }
+    // H0 counts the shard's own slots, H1 every slot but the candidate's (whose H1 value is
+    // the extra slot's); selects, no exec-mask region
+    const bool c0 = e.f == 0 && !extra, c1 = e.f == 0 && s != cand_s;
+    nf += c0 ? 1 : 0;
+    tt = max(tt, c0 ? e.tt : 0);
+    na = max(na, c0 ? e.na : 0);
+    nf1 += c1 ? 1 : 0;
+    tt1 = max(tt1, c1 ? e.tt : 0);
+    na1 = max(na1, c1 ? e.na : 0);
   }
   st[0] = nf;
   st[1] = tt;
@@ -623,6 +670,7 @@ __device__ __forceinline__ void simple_pass_a(const kss_profile& prof, const SPo
 // Pods [k0, k1) of the batch for shard w of one cluster (every pod commits).  `stat`
 // holds the static words of those pods ([k - k0][N]).  On an exchange timeout the error
 // word is set and the shard leaves without writing node state back.
+template <bool DEF>
 __device__ __forceinline__ void simple_schedule(DevCluster c, const SPod* __restrict__ spods,
                                                 const uint32_t* __restrict__ stat, const int32_t* __restrict__ ints,
                                                 int k0, int k1, int32_t* chosen, PodMeta* meta, const kss_profile& prof,
@@ -709,11 +757,12 @@ __device__ __forceinline__ void simple_schedule(DevCluster c, const SPod* __rest
       if (pk.status == 0 && nf > 0) {
         const float rtt = __builtin_amdgcn_rcpf((float)max(max_tt, 1));
         const float rna = __builtin_amdgcn_rcpf((float)max(max_na, 1));
+        // every slot's five values read at once and its key computed whatever the verdict,
+        // then selected: one LDS round trip per slot, no exec-mask region
         for (int s = tid; s < own; s += nt) {
           const SVal e = cv_get(L, s == sub_s ? cap : s);
-          if (e.f != 0) continue;
           const long long key = simple_key(prof, e, scored, max_tt, rtt, max_na, rna, (uint32_t)(c.node_base + lo + s));
-          best = key > best ? key : best;
+          best = (e.f == 0 && key > best) ? key : best;
         }
       }
       if (sp && tid == 0) sp[1] = wall_clock64();
@@ -727,7 +776,7 @@ __device__ __forceinline__ void simple_schedule(DevCluster c, const SPod* __rest
     const int cand_s = best ? (int)(0xFFFFFFFFu - (uint32_t)(unsigned long long)best) - c.node_base - lo : -1;
     // pass A: pod k+1 before pod k's commit, and on the candidate after it
     if (k + 1 < k1) {
-      simple_pass_a(prof, L.ring[(k + 1) % 3], pk, L, (k + 1) % 3, own, cand_s, st);
+      simple_pass_a<DEF>(prof, L.ring[(k + 1) % 3], pk, L, (k + 1) % 3, own, cand_s, st);
     } else {
 #pragma unroll
       for (int i = 0; i < 6; i++) st[i] = 0;

@@ -39,7 +39,6 @@ constexpr int G_XW = 512;    // 32-bit values per shard per exchange (host-check
 constexpr int G_NS = 16;     // scalar slots of an exchange
 constexpr int G_SCORE = 3;   // GIpa.kind of a merged InterPodAffinity score entry (KSS_IPA_SCORE_CLASS)
 constexpr int G_NSTAMP = KSS_NSTAMP_PODS / 2;  // pods with diagnostic phase stamps, 16 per pod
-constexpr size_t G_STAMP_LDS = 8 * 16 * (size_t)G_NSTAMP;
 
 // One topology spread constraint.  v1.26 keys PodTopologySpread's counts by topology pair,
 // not by constraint: constraints of one kind on one key form a group led by its first member
@@ -717,7 +716,7 @@ __device__ __forceinline__ void spread_schedule(DevCluster c, const GPod* __rest
                                                 int n_res, int k0, int k1, int32_t* chosen, PodMeta* meta,
                                                 const kss_profile& prof, int W, int w, int cap, int bins_cap, int gq,
                                                 unsigned long long* gran, const XPeers& X, unsigned epoch0, int* err,
-                                                unsigned long long* stamps,
+                                                unsigned long long* stamps, int nst,
                                                 long long* smem) {
   const int tid = threadIdx.x, nt = blockDim.x;
   SpreadHdr& H = *reinterpret_cast<SpreadHdr*>(smem);
@@ -734,7 +733,7 @@ __device__ __forceinline__ void spread_schedule(DevCluster c, const GPod* __rest
                                                      spread_lds_bytes(cap, bins_cap, c.n_keys, n_res, gq))
              : nullptr;
   if (stl)
-    for (int i = tid; i < 16 * G_NSTAMP; i += nt) stl[i] = 0;
+    for (int i = tid; i < 16 * nst; i += nt) stl[i] = 0;
   // shard state -> LDS: node rows, label ids, resident count rows, static words of pod k0,
   // records of pods k0 and k0 + 1
   for (int s = tid; s < own; s += nt) {
@@ -794,7 +793,7 @@ __device__ __forceinline__ void spread_schedule(DevCluster c, const GPod* __rest
   for (int k = k0; k < k1; k++) {
 #define GSTAMP(i)                                                                      \
   do {                                                                                 \
-    if (stl && tid == 0 && k - k0 < G_NSTAMP) stl[(k - k0) * 16 + (i)] = wall_clock64(); \
+    if (stl && tid == 0 && k - k0 < nst) stl[(k - k0) * 16 + (i)] = wall_clock64();      \
   } while (0)
     GSTAMP(0);
     const GPod& q = *reinterpret_cast<const GPod*>(L.ring + (k % 3) * gq);
@@ -937,7 +936,7 @@ __device__ __forceinline__ void spread_schedule(DevCluster c, const GPod* __rest
                           OP_MIN, OP_MAX};
       if (!spread_reduce(H, L.xs, W, w, epoch, gran, X, err, v, op, 0, 0, q.total_bins + q.hard_pbins,
                          q.total_pbins - q.hard_pbins, false,
-                         stl && k - k0 < G_NSTAMP ? stl + (k - k0) * 16 + 10 : nullptr))
+                         stl && k - k0 < nst ? stl + (k - k0) * 16 + 10 : nullptr))
         return;
       nf = v[0];
       nign = v[1];
@@ -1148,7 +1147,7 @@ __device__ __forceinline__ void spread_schedule(DevCluster c, const GPod* __rest
   // node state and the resident count rows back to HBM
   __syncthreads();
   if (stl)
-    for (int i = tid; i < 16 * G_NSTAMP; i += nt) stamps[(size_t)w * 8 * KSS_NSTAMP_PODS + i] = stl[i];
+    for (int i = tid; i < 16 * nst; i += nt) stamps[(size_t)w * 8 * KSS_NSTAMP_PODS + i] = stl[i];
   for (int s = tid; s < own; s += nt) {
     const int n = lo + s;
 #pragma unroll

@@ -18,11 +18,10 @@ static uint64_t rnd(void) {
   return z ^ (z >> 31);
 }
 
-static int32_t small_div(int32_t x, int32_t d, float rd) {
-  int32_t q = (int32_t)((float)x * rd);
-  if ((int64_t)q * d > (int64_t)x) q--;
-  else if ((int64_t)(q + 1) * d <= (int64_t)x) q++;
-  return q;
+static int32_t small_div(int32_t x, int32_t d, float rd) {  /* branch-free, as on the device */
+  const int32_t q = (int32_t)((float)x * rd);
+  const int64_t p = (int64_t)q * d;
+  return q + (p + d <= (int64_t)x ? 1 : 0) - (p > (int64_t)x ? 1 : 0);
 }
 
 static int32_t quot_small_i64(int64_t x, int64_t A, double invA) {
@@ -50,6 +49,16 @@ static int32_t quot_small_d(double x, double A, double invA) {
   return q;
 }
 
+/* least_bf (kss_simple.cuh): leastRequestedScore, branch-free, capacity > 0 */
+static int32_t least_bf(double requested, double capacity, double inv) {
+  const int over = requested > capacity;
+  const double x = (capacity - (over ? capacity : requested)) * 100.0;
+  int32_t q = (int32_t)(x * inv);
+  const double r = fma(-(double)q, capacity, x);
+  q += (r >= capacity ? 1 : 0) - (r < 0.0 ? 1 : 0);
+  return over ? 0 : q;
+}
+
 int main(int argc, char** argv) {
   long n = argc > 1 ? atol(argv[1]) : 1000000;
   long bad_small = 0, bad_quot = 0, bad_div = 0;
@@ -71,6 +80,10 @@ int main(int argc, char** argv) {
     int64_t x = (i & 1) ? (A - R) * 100 : R * 100;
     if (quot_small_i64(x, A, 1.0 / (double)A) != x / A) bad_quot++;
     if (quot_small_d((double)x, (double)A, 1.0 / (double)A) != x / A) bad_quot++;
+    /* requested in [0, 2A]: over-capacity requests score 0 */
+    int64_t Rq = (int64_t)(rnd() % (uint64_t)(2 * A + 1));
+    int32_t want = Rq > A ? 0 : (int32_t)((A - Rq) * 100 / A);
+    if (least_bf((double)Rq, (double)A, 1.0 / (double)A) != want) bad_quot++;
   }
   /* div_rn: 0 <= a < 2^53, 1 <= b < 2^46 (requested / allocatable, either order of size) */
   for (long i = 0; i < n; i++) {

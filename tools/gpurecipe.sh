@@ -4,7 +4,8 @@
 # runs after a failure).  Outputs go to gpurun_out/TAG_<step>.*; copy what is judged into profiles/.
 #
 # steps:
-#   tests        pytest -m gpu (whole suite; PYTEST_K narrows it with -k)
+#   tests        pytest -m gpu (whole suite; PYTEST_K narrows it with -k, PYTEST_TIMEOUT per test, default 120 s)
+#   svc          the service-grid tests alone (45 s per test)
 #   smoke        __graft_entry__.smoke()
 #   bench        the default line (C2 + c4_split leg, CPU baseline, PMC traffic, latency)
 #   gpus2        bench.py --gpus 2 (on a 1-GPU box: must refuse with "2 GPUs requested")
@@ -45,9 +46,12 @@ sq() {  # sq NAME bench-args...: one rocprofv3 --pmc pass per counter group
 
 run_step() {
   case $1 in
-    tests) timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
+    tests) timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout ${PYTEST_TIMEOUT:-120} --timeout-method thread \
              ${PYTEST_K:+-k "$PYTEST_K"} > "$O/${tag}_pytest_gpu.log" 2>&1; local rc=$?
            tail -3 "$O/${tag}_pytest_gpu.log"; return $rc ;;
+    svc)   timeout -k 10 300 python -u -m pytest tests/test_gpu_service.py -m gpu -x -v --timeout 45 --timeout-method thread \
+             > "$O/${tag}_pytest_svc.log" 2>&1; local rc=$?
+           tail -3 "$O/${tag}_pytest_svc.log"; return $rc ;;
     smoke) timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > "$O/${tag}_smoke.log" 2>&1 ;;
     bench) timeout -k 10 700 python -u bench.py > "$O/${tag}_bench.json" 2> "$O/${tag}_bench.err"; local rc=$?
            tail -c 600 "$O/${tag}_bench.json"; return $rc ;;
