@@ -706,8 +706,8 @@ def run_postfilter(args):
     kss_eval_pod, and for an unschedulable pod kss_postfilter_pod on the same snapshot, on a
     saturated cluster (every node nearly full of pods of mixed priority; pending pods of
     higher priority).  Reports dry runs per second (host-observed, one k_preempt launch each)
-    and the k_preempt device time; the CPU baseline is the object-level restatement
-    (oracle/k8s_preemption.py, one thread) on a bounded sample of the same pods."""
+    and the k_preempt device time; the CPU baseline is the plain-C restatement
+    (oracle/kss_oracle.c, OpenMP over nodes at the box's thread share) on the same pods."""
     import numpy as np
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -731,11 +731,13 @@ def run_postfilter(args):
     for j in unsched[:max(args.warmup, 1) * 3]:
         ctx.postfilter_pod(ps, j)
     host_us, dev_us, nominated, victims = [], [], 0, 0
+    nominated_of = {}
     t0 = time.perf_counter()
     for _ in range(args.steps):
         for j in unsched:
             a = time.perf_counter()
             r = ctx.postfilter_pod(ps, j)
+            nominated_of[j] = r["nominated"]
             host_us.append((time.perf_counter() - a) * 1e6)
             dev_us.append(ctx.last_timing()[0] * 1e3)
             nominated += r["status"] == abi.KSS_PREEMPT_NOMINATED
@@ -744,20 +746,28 @@ def run_postfilter(args):
     runs = len(host_us)
     cpu = None
     if not args.no_cpu and unsched:
-        import k8s_oracle as ko
-        import k8s_preemption as kp
-        o = ko.Oracle(nodes, bound)
-        done, c0 = 0, time.perf_counter()
-        for j in unsched:
-            r = o.schedule_one(pods[j], commit=False)
-            kp.preempt(o, pods[j], r)
-            done += 1
-            if time.perf_counter() - c0 > args.cpu_seconds:
-                break
+        # the plain-C restatement (oracle/kss_oracle.c kss_oracle_postfilter: the filter pass, then
+        # SelectVictimsOnNode node-parallel over OpenMP, as DryRunPreemption fans out with
+        # parallelize.Until), the same pods on the same snapshot, checked against the device's
+        # choices on the way
+        import oracle_c
+        threads, host = cpu_threads()
+        prof = abi.default_profile()
+        cl = cc.as_struct()
+        done, agree, c0 = 0, 0, time.perf_counter()
+        while time.perf_counter() - c0 < args.cpu_seconds:
+            for j in unsched:
+                r = oracle_c.postfilter(prof, cl, ps, j, bs, threads=threads)
+                agree += r["nominated"] == nominated_of[j]
+                done += 1
+                if time.perf_counter() - c0 > args.cpu_seconds:
+                    break
         cs = time.perf_counter() - c0
-        cpu = {"value": done / cs, "unit": "dry runs/s", "cores": 1, "kind": "port",
-               "sample": f"{done} unschedulable pods of the same saturated {n_nodes}-node cluster: "
-                         "Oracle.schedule_one (filters) + k8s_preemption.preempt, pure Python, one thread"}
+        cpu = {"value": done / cs, "unit": "dry runs/s", "cores": threads, "kind": "port", "host": host,
+               "sample": f"{done} dry runs of the {len(unsched)} unschedulable pods of the same saturated "
+                         f"{n_nodes}-node cluster (repeated), oracle/kss_oracle.c kss_oracle_postfilter, "
+                         f"OpenMP over nodes ({threads} threads), {cs:.1f} s wall",
+               "nominations_equal_device": agree == done}
     out = {
         "metric": "DefaultPreemption PostFilter dry runs/sec (unschedulable pods on a saturated cluster)",
         "value": runs / elapsed,

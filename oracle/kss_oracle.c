@@ -1059,3 +1059,373 @@ int kss_oracle_max_threads(void) {
   return 1;
 #endif
 }
+
+/* ===========================================================================
+ * DefaultPreemption PostFilter dry run (ORACLE / CPU BASELINE) — Evaluator.Preempt of
+ * ⟨k8s⟩ pkg/scheduler/framework/preemption/preemption.go with the DefaultPreemption plugin
+ * (plugins/defaultpreemption/default_preemption.go), as the simulator wraps it in
+ * wrappedPlugin.PostFilter (/root/reference/simulator/scheduler/plugin/wrappedplugin.go:550-577).
+ * The same restatement as oracle/k8s_preemption.py, over the struct-of-arrays snapshot and the
+ * bound-pod table (include/kss.h kss_boundset), with the same deterministic choices (DESIGN
+ * §3.4): every potential node is dry-run, unset start times sort last, sort ties keep NodeInfo
+ * order (the boundset's order of a node's pods), full ties go to the lowest node index.
+ * SelectVictimsOnNode runs node-parallel (OpenMP), the way DryRunPreemption fans out with
+ * parallelize.Until.
+ * ========================================================================= */
+
+/* The node-local view SelectVictimsOnNode mutates: NodeInfo.Requested / len(Pods), the hard
+ * spread pair count of the node's pair per hard owner, the inter-pod-affinity counts of the
+ * node's pairs per (key slot, existing anti | affinity | anti), and the affinity-count total
+ * (len(affinityCounts) == 0 <=> total 0: counts never go negative). */
+typedef struct {
+  int64_t req[KSS_NRES];
+  int64_t pods;
+  int64_t M[8];
+  int64_t A[MAXKEYS_PER_POD][3];
+  int64_t T;
+} drystate;
+
+typedef struct {
+  const kss_profile* prof;
+  const kss_cluster* cl;
+  const kss_podset* ps;
+  const kss_pod* p;
+  const podstate* st;
+  const kss_boundset* bs;
+  const int32_t* ptr;  /* [N + 1] CSR of bound pods by local node */
+  const int32_t* ord;  /* per node, its pods in MoreImportantPod order (boundset indices) */
+  int64_t m0[8], m1[8];
+  int32_t id0[8];
+  int64_t aff_total;
+} dryctx;
+
+static int in_list32(const int32_t* ints, int off, int len, int v) {
+  for (int i = 0; i < len; i++)
+    if (ints[off + i] == v) return 1;
+  return 0;
+}
+
+/* NodeInfo.RemovePod (sign -1) / AddPod (+1) of bound pod e on node n with the RemovePod /
+ * AddPod extensions: ⟨k8s⟩ podtopologyspread preFilterState.updateWithPod (each matching
+ * constraint moves the node's pair counter), interpodaffinity preFilterState.updateWithPod
+ * (topologyToMatchedTermCount.update of the node's pairs). */
+static void dry_apply(const dryctx* D, int e, int n, int sign, drystate* s) {
+  const kss_cluster* cl = D->cl;
+  const kss_podset* ps = D->ps;
+  const kss_pod* p = D->p;
+  const kss_boundset* bs = D->bs;
+  for (int r = 0; r < 3 + cl->n_scalar; r++) s->req[r] += sign * bs->req[(size_t)r * bs->n + e];
+  s->pods += sign;
+  const int cls = bs->cls[e];
+  const kss_spread* hard = ps->spreads + p->spread_off;
+  for (int j = 0; j < p->n_hard; j++)
+    if (in_list32(ps->ints, hard[j].cls_off, hard[j].cls_len, cls)) s->M[D->st->hard_own[j]] += sign;
+  const kss_ipa* ipa = ps->ipa + p->ipa_off;
+  for (int q = 0; q < p->ipa_len; q++) {
+    const kss_ipa* en = &ipa[q];
+    if (en->kind > KSS_IPA_REQ_ANTI) continue;
+    if (LV(cl, en->key, n) < 0) continue; /* the node lacks the key: no pair to update */
+    const int k = key_slot((podstate*)D->st, en->key);
+    if (en->kind == KSS_IPA_EXISTING_ANTI) {
+      for (int t = 0; t < bs->terms_len[e]; t++)
+        if (in_list32(ps->ints, en->row_off, en->row_len, bs->ints[bs->terms_off[e] + t])) s->A[k][0] += sign;
+    } else if (in_list32(ps->ints, en->row_off, en->row_len, cls)) {
+      s->A[k][en->kind == KSS_IPA_REQ_AFFINITY ? 1 : 2] += sign;
+      if (en->kind == KSS_IPA_REQ_AFFINITY) s->T += sign;
+    }
+  }
+}
+
+/* RunFilterPluginsWithNominatedPods on the modified node: NodeResourcesFit, PodTopologySpread,
+ * InterPodAffinity (the filters before them passed: the node is a potential node). */
+static int dry_fits(const dryctx* D, const drystate* s, int n) {
+  const kss_cluster* cl = D->cl;
+  const kss_podset* ps = D->ps;
+  const kss_pod* p = D->p;
+  const uint32_t en = D->prof->filter_enabled;
+  const size_t N = (size_t)cl->n_nodes;
+  if ((en >> KSS_F_NODE_RESOURCES_FIT) & 1u) {
+    if (s->pods + 1 > (int64_t)cl->allowed_pods[n]) return 0;
+    int all_zero = 1;
+    for (int r = 0; r < 3 + cl->n_scalar; r++) all_zero &= p->fit_request[r] == 0;
+    if (!all_zero)
+      for (int r = 0; r < 3 + cl->n_scalar; r++) {
+        const int64_t q = p->fit_request[r];
+        if (r >= KSS_RES_SCALAR0 && q == 0) continue;
+        if (q > cl->alloc[(size_t)r * N + n] - s->req[r]) return 0;
+      }
+  }
+  if (((en >> KSS_F_POD_TOPOLOGY_SPREAD) & 1u) && p->n_hard > 0) {
+    const kss_spread* hard = ps->spreads + p->spread_off;
+    for (int i = 0; i < p->n_hard; i++) {
+      const int d = LV(cl, hard[i].key, n);
+      if (d < 0) return 0;
+      const int o = D->st->hard_own[i];
+      /* criticalPaths after the node's pair changed: min(min over the other pairs, this pair) */
+      const int64_t others = D->id0[o] == d ? D->m1[o] : D->m0[o];
+      const int64_t mn = s->M[o] < others ? s->M[o] : others;
+      if (s->M[o] + (int64_t)hard[i].self_match - mn > (int64_t)hard[i].max_skew) return 0;
+    }
+  }
+  if (((en >> KSS_F_INTER_POD_AFFINITY) & 1u) && p->ipa_len > 0) {
+    const kss_ipa* ipa = ps->ipa + p->ipa_off;
+    int have = 0, exist = 1;
+    for (int q = 0; q < p->ipa_len; q++) {
+      if (ipa[q].kind != KSS_IPA_REQ_AFFINITY) continue;
+      have = 1;
+      if (LV(cl, ipa[q].key, n) < 0) return 0;
+      if (s->A[key_slot((podstate*)D->st, ipa[q].key)][1] <= 0) exist = 0;
+    }
+    if (have && !exist && !(s->T == 0 && (p->flags & KSS_POD_IPA_SELF_MATCH))) return 0;
+    for (int q = 0; q < p->ipa_len; q++) {
+      const int kind = ipa[q].kind;
+      if (kind != KSS_IPA_REQ_ANTI && kind != KSS_IPA_EXISTING_ANTI) continue;
+      if (LV(cl, ipa[q].key, n) < 0) continue;
+      if (s->A[key_slot((podstate*)D->st, ipa[q].key)][kind == KSS_IPA_REQ_ANTI ? 2 : 0] > 0) return 0;
+    }
+  }
+  return 1;
+}
+
+typedef struct {
+  int64_t hp, sum, cnt, start; /* hp == INT64_MAX: not a candidate */
+} dryres;
+
+/* ⟨k8s⟩ default_preemption.go SelectVictimsOnNode: remove every lower-priority pod, filter,
+ * then reprieve in MoreImportantPod order (no PodDisruptionBudgets: every pod is
+ * non-violating); victims (optional, cap) receive the boundset ids in eviction order. */
+static dryres dry_select(const dryctx* D, int n, int64_t* victims, int cap) {
+  const kss_cluster* cl = D->cl;
+  const kss_pod* p = D->p;
+  const kss_boundset* bs = D->bs;
+  const podstate* st = D->st;
+  dryres res = {INT64_MAX, 0, 0, 0};
+  const int e0 = D->ptr[n], e1 = D->ptr[n + 1];
+  int p0 = e1; /* the pods below the preemptor's priority: a suffix of the importance order */
+  while (p0 > e0 && bs->priority[D->ord[p0 - 1]] < p->priority) p0--;
+  if (p0 == e1) return res; /* "No preemption victims found for incoming pod" */
+  drystate s;
+  memset(&s, 0, sizeof(s));
+  const size_t N = (size_t)cl->n_nodes;
+  for (int r = 0; r < 3 + cl->n_scalar; r++) s.req[r] = cl->requested[(size_t)r * N + n];
+  s.pods = cl->pod_count[n];
+  const kss_spread* hard = D->ps->spreads + p->spread_off;
+  for (int i = 0; i < p->n_hard; i++) {
+    if (st->hard_own[i] != i) continue;
+    const int d = LV(cl, hard[i].key, n);
+    s.M[i] = d >= 0 ? st->hard_cnt[i][d] : 0;
+  }
+  for (int k = 0; k < st->nkeys; k++) {
+    const int d = LV(cl, st->keys[k], n);
+    if (d < 0) continue;
+    s.A[k][0] = st->hx[k][d];
+    s.A[k][1] = st->ha[k][d];
+    s.A[k][2] = st->hb[k][d];
+  }
+  s.T = D->aff_total;
+  for (int k = p0; k < e1; k++) dry_apply(D, D->ord[k], n, -1, &s);
+  if (!dry_fits(D, &s, n)) return res;
+  int nv = 0;
+  int64_t hp = 0, sum = 0, stt = 0;
+  for (int k = p0; k < e1; k++) {
+    const int e = D->ord[k];
+    dry_apply(D, e, n, 1, &s);
+    if (!dry_fits(D, &s, n)) {
+      dry_apply(D, e, n, -1, &s);
+      if (nv == 0) {
+        hp = bs->priority[e];
+        stt = bs->start[e]; /* GetEarliestPodStartTime among the highest-priority victims */
+      }
+      if (victims && nv < cap) victims[nv] = bs->id[e];
+      sum += (int64_t)bs->priority[e] + 2147483648ll;
+      nv++;
+    }
+  }
+  if (nv == 0) return res; /* upstream: an error status ("expected at least one victim") */
+  res.hp = hp;
+  res.sum = sum;
+  res.cnt = nv;
+  res.start = stt;
+  return res;
+}
+
+/* nodesWherePreemptionMightHelp: UnschedulableAndUnresolvable statuses are skipped */
+static int resolvable_status(int f, int detail) {
+  if (f == KSS_F_NODE_RESOURCES_FIT || f == KSS_F_NODE_PORTS) return 1;
+  if (f == KSS_F_POD_TOPOLOGY_SPREAD) return detail == KSS_PTS_CONSTRAINTS_NOT_MATCH;
+  if (f == KSS_F_INTER_POD_AFFINITY) return detail != KSS_IPA_AFFINITY;
+  return 0;
+}
+
+static int imp_before(const kss_boundset* bs, int a, int b) { /* MoreImportantPod, NodeInfo order on ties */
+  if (bs->priority[a] != bs->priority[b]) return bs->priority[a] > bs->priority[b];
+  if (bs->start[a] != bs->start[b]) return bs->start[a] < bs->start[b];
+  return a < b;
+}
+
+/* PostFilter dry run of ps->pods[pi] against cl and the bound pods bs (the state its filters
+ * saw).  out->victims / victims_cap as kss_postfilter_pod. */
+int kss_oracle_postfilter(const kss_profile* prof, const kss_cluster* cl, const kss_podset* ps, int pi,
+                          const kss_boundset* bs, int threads, kss_preempt_result* out) {
+  const kss_pod* p = &ps->pods[pi];
+  const int N = cl->n_nodes;
+  const int th = threads > 0 ? threads : 1;
+  out->status = KSS_PREEMPT_NO_CANDIDATE;
+  out->nominated = -1;
+  out->n_potential = out->n_candidates = out->n_victims = 0;
+  out->highest_priority = 0;
+  out->sum_priority = out->earliest_start = 0;
+  if (p->flags & KSS_POD_PREEMPT_NEVER) { /* PodEligibleToPreemptOthers */
+    out->status = KSS_PREEMPT_NOT_ELIGIBLE;
+    return 0;
+  }
+  if (p->prefilter_status != 0) return 0; /* every node UnschedulableAndUnresolvable */
+  podstate st;
+  int rc = podstate_build(&st, cl, ps, p, prof->hard_pod_affinity_weight);
+  if (rc) {
+    podstate_free(&st);
+    return rc;
+  }
+  int32_t* ptr = (int32_t*)calloc((size_t)N + 1, sizeof(int32_t));
+  int32_t* ord = (int32_t*)malloc(sizeof(int32_t) * (size_t)(bs->n > 0 ? bs->n : 1));
+  uint8_t* fp = (uint8_t*)malloc((size_t)(N ? N : 1));
+  uint16_t* fd = (uint16_t*)malloc(sizeof(uint16_t) * (size_t)(N ? N : 1));
+  dryres* dr = (dryres*)malloc(sizeof(dryres) * (size_t)(N ? N : 1));
+  uint8_t* inset = NULL;
+  if (!ptr || !ord || !fp || !fd || !dr) {
+    rc = KSS_E_NOMEM;
+    goto done;
+  }
+  /* NodeInfo.Pods per node (the boundset's order), then each node's MoreImportantPod order
+   * (insertion sort: stable, NodeInfo order on ties) */
+  for (int i = 0; i < bs->n; i++) {
+    const int n = bs->node[i] - cl->node_base;
+    if (n >= 0 && n < N) ptr[n + 1]++;
+  }
+  for (int n = 0; n < N; n++) ptr[n + 1] += ptr[n];
+  {
+    int32_t* fill = (int32_t*)malloc(sizeof(int32_t) * (size_t)(N ? N : 1));
+    for (int n = 0; n < N; n++) fill[n] = ptr[n];
+    for (int i = 0; i < bs->n; i++) {
+      const int n = bs->node[i] - cl->node_base;
+      if (n >= 0 && n < N) ord[fill[n]++] = i;
+    }
+    free(fill);
+  }
+  for (int n = 0; n < N; n++)
+    for (int a = ptr[n] + 1; a < ptr[n + 1]; a++)
+      for (int b = a; b > ptr[n] && imp_before(bs, ord[b], ord[b - 1]); b--) {
+        const int32_t t = ord[b];
+        ord[b] = ord[b - 1];
+        ord[b - 1] = t;
+      }
+  /* the pod's filter statuses (findNodesThatPassFilters over the PreFilterResult node set) */
+  if (p->names_len >= 0) {
+    inset = (uint8_t*)calloc((size_t)(N ? N : 1), 1);
+    for (int i = 0; i < p->names_len; i++) {
+      const int64_t g = ps->ints[p->names_off + i] - cl->node_base;
+      if (g >= 0 && g < N) inset[g] = 1;
+    }
+  }
+  int feasible = 0;
+#pragma omp parallel for num_threads(th) schedule(static) reduction(+ : feasible)
+  for (int n = 0; n < N; n++) {
+    fd[n] = 0;
+    if (inset && !inset[n]) {
+      fp[n] = KSS_F_NOT_EVALUATED; /* no status: potential, the dry run's NodeAffinity rejects it */
+      continue;
+    }
+    fp[n] = (uint8_t)filter_node(prof, cl, ps, p, &st, n, &fd[n]);
+    feasible += fp[n] == KSS_F_PASS;
+  }
+  if (feasible) {
+    out->status = KSS_PREEMPT_SCHEDULABLE;
+    goto done;
+  }
+  dryctx D;
+  memset(&D, 0, sizeof(D));
+  D.prof = prof;
+  D.cl = cl;
+  D.ps = ps;
+  D.p = p;
+  D.st = &st;
+  D.bs = bs;
+  D.ptr = ptr;
+  D.ord = ord;
+  /* criticalPaths per hard owner: the smallest pair count, its pair, the next smallest */
+  {
+    const kss_spread* hard = ps->spreads + p->spread_off;
+    for (int i = 0; i < p->n_hard; i++) {
+      D.m0[i] = D.m1[i] = INT32_MAX;
+      D.id0[i] = -1;
+      if (st.hard_own[i] != i) continue;
+      const int bins = cl->key_card[hard[i].key] + 1;
+      for (int d = 0; d < bins; d++) {
+        if (!st.hard_present[i][d]) continue;
+        const int64_t v = st.hard_cnt[i][d];
+        if (v < D.m0[i]) {
+          D.m1[i] = D.m0[i];
+          D.m0[i] = v;
+          D.id0[i] = d;
+        } else if (v < D.m1[i]) {
+          D.m1[i] = v;
+        }
+      }
+    }
+    for (int k = 0; k < st.nkeys; k++) {
+      const int bins = cl->key_card[st.keys[k]] + 1;
+      for (int d = 0; d < bins; d++) D.aff_total += st.ha[k][d];
+    }
+  }
+  /* DryRunPreemption: SelectVictimsOnNode on every potential node, node-parallel */
+  int n_pot = 0, n_cand = 0;
+#pragma omp parallel for num_threads(th) schedule(dynamic, 16) reduction(+ : n_pot, n_cand)
+  for (int n = 0; n < N; n++) {
+    dr[n].hp = INT64_MAX;
+    const int f = fp[n];
+    if (f != KSS_F_NOT_EVALUATED && !resolvable_status(f, fd[n])) continue;
+    n_pot++;
+    if (f == KSS_F_NOT_EVALUATED) continue;
+    dr[n] = dry_select(&D, n, NULL, 0);
+    n_cand += dr[n].hp != INT64_MAX;
+  }
+  out->n_potential = n_pot;
+  out->n_candidates = n_cand;
+  if (!n_cand) goto done;
+  /* pickOneNodeForPreemption in canonical node order: highest victim priority min, priority
+   * sum min, victims min, earliest start (of the highest-priority victims) max, then the
+   * lowest node index */
+  int best = -1;
+  for (int n = 0; n < N; n++) {
+    if (dr[n].hp == INT64_MAX) continue;
+    if (best < 0) {
+      best = n;
+      continue;
+    }
+    const dryres* a = &dr[n];
+    const dryres* b = &dr[best];
+    const int better = a->hp != b->hp ? a->hp < b->hp
+                       : a->sum != b->sum ? a->sum < b->sum
+                       : a->cnt != b->cnt ? a->cnt < b->cnt
+                                          : a->start > b->start;
+    if (better) best = n;
+  }
+  {
+    const dryres d = dry_select(&D, best, out->victims, out->victims_cap);
+    out->status = KSS_PREEMPT_NOMINATED;
+    out->nominated = cl->node_base + best;
+    out->n_victims = (int32_t)d.cnt;
+    out->highest_priority = (int32_t)d.hp;
+    out->sum_priority = d.sum;
+    out->earliest_start = d.start;
+  }
+done:
+  podstate_free(&st);
+  free(ptr);
+  free(ord);
+  free(fp);
+  free(fd);
+  free(dr);
+  free(inset);
+  return rc;
+}

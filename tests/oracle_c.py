@@ -31,7 +31,26 @@ def lib():
         _lib.kss_oracle_go_log.argtypes = [C.c_double]
         _lib.kss_oracle_go_log.restype = C.c_double
         _lib.kss_oracle_max_threads.restype = C.c_int
+        _lib.kss_oracle_postfilter.argtypes = [P(abi.Profile), P(abi.Cluster), P(abi.PodSet), C.c_int,
+                                               P(abi.Boundset), C.c_int, P(abi.PreemptResult)]
+        _lib.kss_oracle_postfilter.restype = C.c_int
     return _lib
+
+
+def postfilter(profile, cluster_struct, podset_struct, i, boundset_struct, threads=1, victims_cap=1024):
+    """kss_oracle_postfilter: the C PostFilter dry run of pod i (the same dict as
+    native.Context.postfilter_pod)."""
+    vic = np.zeros(max(victims_cap, 1), np.int64)
+    r = abi.PreemptResult()
+    r.victims_cap = victims_cap
+    r.victims = vic.ctypes.data_as(C.POINTER(C.c_int64))
+    rc = lib().kss_oracle_postfilter(C.byref(profile), C.byref(cluster_struct), C.byref(podset_struct), i,
+                                     C.byref(boundset_struct), threads, C.byref(r))
+    if rc:
+        raise RuntimeError(f"kss_oracle_postfilter: {rc}")
+    return dict(status=r.status, nominated=r.nominated, n_potential=r.n_potential, n_candidates=r.n_candidates,
+                victims=[int(v) for v in vic[:min(r.n_victims, victims_cap)]], n_victims=r.n_victims,
+                highest_priority=r.highest_priority, sum_priority=r.sum_priority, earliest_start=r.earliest_start)
 
 
 class Results:

@@ -72,3 +72,66 @@ def test_saturated_clusters_nominate(seed):
     o, out = kp.schedule_with_preemption(nodes, bound, pods)
     kinds = {pre["status"] for _, pre, _ in out if pre}
     assert "nominated" in kinds and "no_candidate" in kinds
+
+
+STATUS = {abi.KSS_PREEMPT_NOMINATED: "nominated", abi.KSS_PREEMPT_NO_CANDIDATE: "no_candidate",
+          abi.KSS_PREEMPT_NOT_ELIGIBLE: "not_eligible", abi.KSS_PREEMPT_SCHEDULABLE: "schedulable"}
+
+
+def _c_dry_runs(nodes, bound, pods, threads):
+    """The C restatement (oracle/kss_oracle.c kss_oracle_postfilter) of every pod against the
+    initial snapshot (nothing committed), as (status, nominated node, victims, criteria)."""
+    import oracle_c
+    cc, cp, _ = compile_cluster(nodes, bound, pods)
+    cl, ps, bs = cc.as_struct(), cp.as_struct(), cc.as_boundset()
+
+    def victim(v):
+        return cc.bound_names[v][1]
+
+    out = []
+    for j in range(cp.n):
+        r = oracle_c.postfilter(abi.default_profile(), cl, ps, j, bs, threads=threads)
+        nom = cc.node_names[r["nominated"]] if r["nominated"] >= 0 else None
+        out.append((STATUS[r["status"]], nom, [victim(v) for v in r["victims"]],
+                    (r["n_potential"], r["n_candidates"])))
+    return out
+
+
+def _py_dry_runs(nodes, bound, pods):
+    o = ko.Oracle(nodes, bound)
+    out = []
+    for p in pods:
+        r = o.schedule_one(p, commit=False)
+        pre = kp.preempt(o, p, r)
+        nom = ko._name(o.nodes[pre["nominated"]]) if pre["nominated"] is not None else None
+        out.append((pre["status"], nom, [v[1] for v in pre["victims"]], (pre["n_potential"], pre["n_candidates"])))
+    return out
+
+
+def test_c_postfilter_matches_hand_derived():
+    """The hand-derived fixture, one dry run per pod on the unchanged snapshot."""
+    nodes, bound, pods, _ = pf.fixture()
+    got = _c_dry_runs(nodes, bound, pods, threads=2)
+    want = _py_dry_runs(nodes, bound, pods)
+    for j, (g, w) in enumerate(zip(got, want)):
+        if w[0] == "schedulable":  # PostFilter never runs for these; a Never pod is refused first
+            assert g[0] in ("schedulable", "not_eligible"), j
+        else:
+            assert g == w, (j, pods[j]["metadata"]["name"])
+
+
+@pytest.mark.parametrize("seed,n_nodes,n_pods,threads", [(1, 60, 40, 1), (2, 60, 40, 4), (3, 200, 60, 8)])
+def test_c_postfilter_matches_object_oracle(seed, n_nodes, n_pods, threads):
+    """Saturated clusters: status, nominated node, victims in eviction order and the
+    potential / candidate counts equal the object-level restatement, at any thread count."""
+    nodes, bound, pods = pf.saturated(seed, n_nodes, n_pods)
+    got = _c_dry_runs(nodes, bound, pods, threads)
+    want = _py_dry_runs(nodes, bound, pods)
+    kinds = set()
+    for j, (g, w) in enumerate(zip(got, want)):
+        kinds.add(w[0])
+        if w[0] == "schedulable":  # PostFilter never runs for these; a Never pod is refused first
+            assert g[0] in ("schedulable", "not_eligible"), j
+        else:
+            assert g == w, j
+    assert "nominated" in kinds
