@@ -485,7 +485,11 @@ int kss_eval_pod_view(kss_ctx* ctx, const kss_podset* ps, int32_t pod_index, uin
  *                       grid too) and stop.  The grid leaves by itself after ~1 s without a
  *                       command and is restarted by the next call.  Every other entry point
  *                       that touches the context's device state stops it first.
- * Results equal kss_eval_pod_view / kss_commit / kss_rollback on the same state. */
+ * Results equal kss_eval_pod_view / kss_commit / kss_rollback on the same state.
+ * The resident grid occupies the hardware queue its stream maps to (GPU_MAX_HW_QUEUES per
+ * process): work of OTHER contexts or streams of the process that shares that queue waits for
+ * the grid to leave (kss_service_stop, or its idle exit).  Drive one context per process through
+ * the service, or stop it before using another. */
 int kss_service_start(kss_ctx* ctx);
 int kss_service_stop(kss_ctx* ctx);
 int kss_service_eval(kss_ctx* ctx, int32_t pod_index, uint32_t fields, kss_pod_view* out);

@@ -182,6 +182,9 @@ __global__ __launch_bounds__(KSS_MAX_THREADS) void k_service(const DevJob* __res
                     smem);
 }
 
+#ifndef KSS_SIMPLE_PW
+#define KSS_SIMPLE_PW 1  // experiment builds: -DKSS_SIMPLE_PW=0 keeps the two-reduction loop everywhere
+#endif
 // grid = n_jobs * W, as k_schedule; each shard's nodes live in LDS (cap slots).
 // DEF: the profile is the v1.26 default, folded into the code.
 // Pods [k0, min(k1, n_pods)) of every job; the job's stat buffer holds their static words.
@@ -202,8 +205,16 @@ __global__ __launch_bounds__(KSS_MAX_THREADS) void k_simple(const DevJob* __rest
     __syncthreads();
   }
   const kss_profile& P = DEF ? def_prof : H.prof;
-  simple_schedule<DEF>(job.c, job.spods, job.stat, job.P.ints, k0, min(k1, job.n_pods), job.chosen, job.meta, P, W, w, cap,
-                  gran ? gran + (size_t)ji * 2 * W * SX_VALS : nullptr, X, epoch0, err, ji == 0 ? stamps : nullptr, smem);
+  // per-wave mode when every shard's nodes fit PW_LANES slots per wave (one node per lane)
+  const int per = (job.c.N + W - 1) / W, nwave = (int)(blockDim.x >> 6);
+  unsigned long long* g = gran ? gran + (size_t)ji * 2 * W * SX_VALS : nullptr;
+  unsigned long long* sp = ji == 0 ? stamps : nullptr;
+  if (per <= PW_LANES * nwave && KSS_SIMPLE_PW)
+    simple_schedule<DEF, true>(job.c, job.spods, job.stat, job.P.ints, k0, min(k1, job.n_pods), job.chosen, job.meta, P, W,
+                               w, cap, g, X, epoch0, err, sp, smem);
+  else
+    simple_schedule<DEF, false>(job.c, job.spods, job.stat, job.P.ints, k0, min(k1, job.n_pods), job.chosen, job.meta, P,
+                                W, w, cap, g, X, epoch0, err, sp, smem);
 }
 
 // grid = W (one cluster); each shard's nodes live in LDS (cap slots); bins_cap: histogram +

@@ -520,26 +520,31 @@ struct SimpleShard {
   double* r64;    // [8][cap]: allocatable cpu/mem/eph, requested cpu/mem/eph, non-zero cpu/mem (exact integers)
   double* inv;    // [3][cap]: RN(1 / allocatable)
   int32_t* r32;   // [2][cap]: pod count, allowed pods
-  uint32_t* st;   // [3][cap]: static words of pods k, k+1, k+2 (ring slot = pod % 3)
-  int32_t* cv;    // [5][cap + 1]: filter verdict, TT, NA, Fit, BA
-  SPod* ring;     // [3]: pod records (ring slot = pod % 3)
+  uint32_t* st;   // [RING][cap]: static words of the pods in flight (ring slot = pod % RING)
+  int32_t* cv;    // [5][cap + CV_EXTRA]: filter verdict, TT, NA, Fit, BA (slots cap + i: H1 values)
+  SPod* ring;     // [RING]: pod records (ring slot = pod % RING)
   int cap;
 };
 
+constexpr int RING = 4;                // record / static-word ring slots
+constexpr int CV_EXTRA = MAXWAVES;     // H1 slots past the shard's nodes: one per wave (per-wave mode)
+constexpr int PW_LANES = 63;           // per-wave mode: node slots per wave (lane 63 is the wave's H1 lane)
+
 __host__ __device__ inline size_t simple_lds_bytes(int cap) {
-  return sizeof(SimpleHdr) + 3 * sizeof(SPod) + (size_t)cap * (8 * 8 + 3 * 8 + 2 * 4 + 3 * 4) + 20 * ((size_t)cap + 1);
+  return sizeof(SimpleHdr) + RING * sizeof(SPod) + (size_t)cap * (8 * 8 + 3 * 8 + 2 * 4 + RING * 4) +
+         20 * ((size_t)cap + CV_EXTRA);
 }
 
 __device__ __forceinline__ SimpleShard shard_view(uint8_t* base, int cap) {
   SimpleShard L;
   L.cap = cap;
   L.ring = reinterpret_cast<SPod*>(base);
-  uint8_t* b = base + 3 * sizeof(SPod);
+  uint8_t* b = base + RING * sizeof(SPod);
   L.r64 = reinterpret_cast<double*>(b);
   L.inv = reinterpret_cast<double*>(b + 64 * (size_t)cap);
   L.r32 = reinterpret_cast<int32_t*>(b + 88 * (size_t)cap);
   L.st = reinterpret_cast<uint32_t*>(L.r32 + 2 * (size_t)cap);
-  L.cv = reinterpret_cast<int32_t*>(L.st + 3 * (size_t)cap);
+  L.cv = reinterpret_cast<int32_t*>(L.st + RING * (size_t)cap);
   return L;
 }
 
@@ -560,12 +565,12 @@ __device__ __forceinline__ DynRow shard_row(const SimpleShard& L, int s) {
 }
 
 __device__ __forceinline__ SVal cv_get(const SimpleShard& L, int s) {
-  const int C1 = L.cap + 1;
+  const int C1 = L.cap + CV_EXTRA;
   return SVal{L.cv[s], L.cv[C1 + s], L.cv[2 * C1 + s], L.cv[3 * C1 + s], L.cv[4 * C1 + s]};
 }
 
 __device__ __forceinline__ void cv_put(const SimpleShard& L, int s, const SVal& e) {
-  const int C1 = L.cap + 1;
+  const int C1 = L.cap + CV_EXTRA;
   L.cv[s] = e.f;
   L.cv[C1 + s] = e.tt;
   L.cv[2 * C1 + s] = e.na;
@@ -667,10 +672,128 @@ __device__ __forceinline__ void simple_pass_a(const kss_profile& prof, const SPo
   st[5] = na1;
 }
 
+// Per-wave mode (every shard's nodes fit in PW_LANES slots per wave, one per lane): wave v
+// owns slots [v * pwv, v * pwv + pwv) of its shard and its lane pwv re-evaluates the WAVE's best
+// candidate of the previous pod with that pod committed (the wave's H1).  The shard then never
+// reduces its best key by itself: the waves' bests ride with the statistics, one workgroup
+// reduction per pod instead of two (simple_sync_pw).  u = the wave lane's {nf0, tt0, na0, nf1,
+// tt1, na1} (H1: the wave's slots but its candidate, plus the candidate re-evaluated).
+template <bool DEF>
+__device__ __forceinline__ void simple_pass_a_pw(const kss_profile& prof, const SPod& q_lds, const SPod& q0_lds,
+                                                 const SimpleShard& L, int sl, int own, int pwv, int cand_w,
+                                                 uint32_t (&u)[6]) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const uint32_t* sw = L.st + (size_t)sl * L.cap;
+  const SPod q = q_lds;
+  SPod q0;
+#pragma unroll
+  for (int k = 0; k < 3; k++) q0.creq[k] = q0_lds.creq[k];
+  q0.cnz[0] = q0_lds.cnz[0];
+  q0.cnz[1] = q0_lds.cnz[1];
+  const int s = wv * pwv + lane;
+  const bool extra = lane == pwv && cand_w >= 0;
+  const bool mine = lane < pwv && s < own;
+#pragma unroll
+  for (int i = 0; i < 6; i++) u[i] = 0;
+  if (mine || extra) {
+    const int ns = extra ? cand_w : s;
+    const uint32_t wd = sw[ns];
+    DynRow r = shard_row(L, ns);
+    if (extra) add_commit(r, q0);
+    const SVal e = DEF ? dyn_eval_def(q, wd, r) : dyn_eval(prof, q, wd, r);
+    cv_put(L, extra ? L.cap + wv : s, e);
+    const bool c0 = e.f == 0 && !extra, c1 = e.f == 0 && (extra || s != cand_w);
+    u[0] = c0 ? 1u : 0u;
+    u[1] = c0 ? (uint32_t)e.tt : 0u;
+    u[2] = c0 ? (uint32_t)e.na : 0u;
+    u[3] = c1 ? 1u : 0u;
+    u[4] = c1 ? (uint32_t)e.tt : 0u;
+    u[5] = c1 ? (uint32_t)e.na : 0u;
+  }
+}
+
+// AssumePod of pk on shard slot s (LDS node rows; the class / term counts follow after the
+// launch, k_counts).
+__device__ __forceinline__ void simple_commit_slot(const SimpleShard& L, const SPod& pk, int s) {
+  const int cap = L.cap;
+#pragma unroll
+  for (int r = 0; r < 3; r++) L.r64[(3 + r) * cap + s] += pk.creq[r];
+  L.r64[6 * cap + s] += pk.cnz[0];
+  L.r64[7 * cap + s] += pk.cnz[1];
+  L.r32[s] += 1;
+}
+
+// Per-wave mode's one reduction per pod: the waves' best keys and H0 / H1 statistics in one
+// LDS pass (the shard's H1 is the best wave's H1 with every other wave's H0), the cross-shard
+// exchange, and pod k's AssumePod on the winner's slot by wave 0 BEFORE the closing barrier
+// (the next pod's pass A reads that row with no barrier of its own in between).
+// R = {winner key, nf, max TT, max NA of the next pod}.  False if the launch aborted.
+__device__ __forceinline__ bool simple_sync_pw(SimpleHdr& H, int& parity, long long wbest, uint32_t (&u)[6], int W,
+                                               int w, unsigned epoch, unsigned long long* gran, const XPeers& X,
+                                               int* err, int per, int node_base, int lo, int own, const SPod& pk,
+                                               bool commit, const SimpleShard& L, long long (&R)[4],
+                                               KSS_GLOBAL unsigned long long* sp) {
+  wave_red_stats(u);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  if (lane == 0) {
+    H.red[parity][wave][0] = wbest;
+#pragma unroll
+    for (int i = 0; i < 6; i++) H.red[parity][wave][1 + i] = u[i];
+  }
+  lds_barrier();
+  long long best = 0;
+  int ws = -1;
+  for (int v = 0; v < nw; v++) {
+    const long long b = H.red[parity][v][0];
+    if (b > best) {
+      best = b;
+      ws = v;
+    }
+  }
+  long long st[6] = {0, 0, 0, 0, 0, 0};
+  for (int v = 0; v < nw; v++) {
+    const long long* h = H.red[parity][v];
+    const int o = v == ws ? 4 : 1;  // the best wave contributes its H1, the others their H0
+    st[0] += h[1];
+    st[1] = max(st[1], h[2]);
+    st[2] = max(st[2], h[3]);
+    st[3] += h[o];
+    st[4] = max(st[4], h[o + 1]);
+    st[5] = max(st[5], h[o + 2]);
+  }
+  parity ^= 1;
+  if (sp && threadIdx.x == 0) sp[4] = wall_clock64();
+  if (W == 1) {  // the winner (if any) is this shard's best
+    const bool h1 = best != 0;
+    R[0] = best;
+    R[1] = h1 ? st[3] : st[0];
+    R[2] = h1 ? st[4] : st[1];
+    R[3] = h1 ? st[5] : st[2];
+    if (commit && h1 && threadIdx.x == 0)
+      simple_commit_slot(L, pk, (int)(0xFFFFFFFFu - (uint32_t)(unsigned long long)best) - node_base - lo);
+    lds_barrier();
+    return true;
+  }
+  if (threadIdx.x < 64) {
+    const long long v[7] = {best, st[0], st[1], st[2], st[3], st[4], st[5]};
+    if (simple_exchange(H, gran, X, W, w, epoch, err, v, per, node_base) && commit && lane == 0) {
+      const long long K = H.res[0];
+      const int x = K ? (int)(0xFFFFFFFFu - (uint32_t)(unsigned long long)K) - node_base - lo : -1;
+      if (x >= 0 && x < own) simple_commit_slot(L, pk, x);
+    }
+  }
+  lds_barrier();
+  if (H.abort) return false;
+#pragma unroll
+  for (int i = 0; i < 4; i++) R[i] = H.res[i];
+  return true;
+}
+
 // Pods [k0, k1) of the batch for shard w of one cluster (every pod commits).  `stat`
 // holds the static words of those pods ([k - k0][N]).  On an exchange timeout the error
-// word is set and the shard leaves without writing node state back.
-template <bool DEF>
+// word is set and the shard leaves without writing node state back.  PW: per-wave mode
+// (simple_sync_pw; the caller checks that every shard's nodes fit it).
+template <bool DEF, bool PW>
 __device__ __forceinline__ void simple_schedule(DevCluster c, const SPod* __restrict__ spods,
                                                 const uint32_t* __restrict__ stat, const int32_t* __restrict__ ints,
                                                 int k0, int k1, int32_t* chosen, PodMeta* meta, const kss_profile& prof,
@@ -684,7 +807,11 @@ __device__ __forceinline__ void simple_schedule(DevCluster c, const SPod* __rest
   const int lo = min(c.N, w * per), hi = min(c.N, lo + per), own = hi - lo;
   if (k1 <= k0) return;
   constexpr int NQ = (int)(sizeof(SPod) / 16);
-  // shard rows, reciprocals, static words of pods k0 and k0+1, their records -> LDS
+  // prefetch distance: the record and static words of pod k + PD are loaded while pod k is
+  // scheduled.  Per-wave mode has no barrier between a pod's end and the next pod's pass A, so
+  // its prefetch stores land one pod earlier (behind two barriers) than the pass that reads them.
+  constexpr int PD = PW ? 3 : 2;
+  // shard rows, reciprocals, static words and records of pods k0 .. k0 + PD - 1 -> LDS
   for (int s = tid; s < own; s += nt) {
     const int n = lo + s;
 #pragma unroll
@@ -698,12 +825,11 @@ __device__ __forceinline__ void simple_schedule(DevCluster c, const SPod* __rest
     L.r64[7 * cap + s] = (double)c.nonzero[N + n];
     L.r32[s] = c.pod_count[n];
     L.r32[cap + s] = c.allowed_pods[n];
-    L.st[(k0 % 3) * cap + s] = stat[(size_t)lo + s];
-    if (k0 + 1 < k1) L.st[((k0 + 1) % 3) * cap + s] = stat[N + lo + s];
+    for (int d = 0; d < PD && k0 + d < k1; d++) L.st[((k0 + d) % RING) * cap + s] = stat[(size_t)d * N + lo + s];
   }
-  for (int i = tid; i < min(k1 - k0, 2) * NQ; i += nt) {
+  for (int i = tid; i < min(k1 - k0, PD) * NQ; i += nt) {
     const int j = k0 + i / NQ;
-    reinterpret_cast<uint4*>(L.ring + j % 3)[i % NQ] = reinterpret_cast<const uint4*>(spods + j)[i % NQ];
+    reinterpret_cast<uint4*>(L.ring + j % RING)[i % NQ] = reinterpret_cast<const uint4*>(spods + j)[i % NQ];
   }
   if (tid == 0) H.abort = 0;
   __syncthreads();
@@ -715,11 +841,14 @@ __device__ __forceinline__ void simple_schedule(DevCluster c, const SPod* __rest
   KSS_GLOBAL unsigned long long* gstamps = gp(stamps);
   long long st[6], R[4] = {0, 0, 0, 0};
   int parity = 0, sub_s = -1;  // slot whose pass-B values are the H1 ones (the previous winner)
+  int sub_h = cap;             // ... and the cv slot holding them
   unsigned epoch = epoch0;  // granule tags above every tag an earlier launch left (split grids)
   const int nwave = nt >> 6;
+  const int lane = tid & 63, wv = tid >> 6;
+  const int pwv = (own + nwave - 1) / nwave;  // per-wave mode: the wave's node slots (<= PW_LANES)
   // prefetch lanes: every wave but wave 0 (readfirstlane: a wave-uniform, scalar branch)
   const bool pf_wave = nwave == 1 || __builtin_amdgcn_readfirstlane(tid >> 6) >= 1;
-  uint4 pfq = make_uint4(0, 0, 0, 0);  // prefetched record / static words of pod k+2, live across the loop
+  uint4 pfq = make_uint4(0, 0, 0, 0);  // prefetched record / static words of pod k+PD, live across the loop
   uint32_t pfw[PF_MAX];
 #pragma unroll
   for (int j = 0; j < PF_MAX; j++) pfw[j] = 0;
@@ -732,57 +861,87 @@ __device__ __forceinline__ void simple_schedule(DevCluster c, const SPod* __rest
                                             ? gstamps + (size_t)w * 8 * KSS_NSTAMP_PODS + (size_t)(k - k0) * 16
                                             : nullptr;
     if (sp && tid == 0) sp[0] = wall_clock64();
-    const SPod& pk = L.ring[(k + 3) % 3];
-    // pod k+2: record and static words -> registers now, -> their ring slots at the end
+    const SPod& pk = L.ring[(k + RING) % RING];
+    // pod k+PD: record and static words -> registers now, -> their ring slots at the end
     // Only the prefetch waves (all but wave 0, unless there is one wave) issue these loads:
     // vmcnt is per wave and counts stores too, so wave 0 — which publishes granules and
     // writes the outcomes — never waits on an HBM prefetch, and the prefetch waves never
     // wait on a store.
     // The branch is wave-uniform and every load inside it is unconditional (clamped
     // indices), so the compiler's wait for these registers stays on the prefetch path.
-    const bool pf_on = pf_wave && k >= k0 && k + 2 < k1 && own > 0;
+    const bool pf_on = pf_wave && k >= k0 && k + PD < k1 && own > 0;
     if (pf_on) {
-      KSS_GLOBAL const uint4& src = gspod[(size_t)(k + 2) * NQ + min(pf_lane, NQ - 1)];
+      KSS_GLOBAL const uint4& src = gspod[(size_t)(k + PD) * NQ + min(pf_lane, NQ - 1)];
       pfq = make_uint4(src.x, src.y, src.z, src.w);
 #pragma unroll
       for (int j = 0; j < PF_MAX; j++)
-        if (j < pf_per) pfw[j] = gstat[(size_t)(k + 2 - k0) * N + lo + min(j * pf_n + pf_lane, own - 1)];
+        if (j < pf_per) pfw[j] = gstat[(size_t)(k + PD - k0) * N + lo + min(j * pf_n + pf_lane, own - 1)];
     }
     // pass B: NormalizeScore, weights, shard-best selectHost key of pod k
     const long long nf = R[1];
     const int max_tt = (int)R[2], max_na = (int)R[3];
     const bool scored = nf > 1;
     long long best = 0;
-    if (k >= k0) {
-      if (pk.status == 0 && nf > 0) {
-        const float rtt = __builtin_amdgcn_rcpf((float)max(max_tt, 1));
-        const float rna = __builtin_amdgcn_rcpf((float)max(max_na, 1));
-        // every slot's five values read at once and its key computed whatever the verdict,
-        // then selected: one LDS round trip per slot, no exec-mask region
-        for (int s = tid; s < own; s += nt) {
-          const SVal e = cv_get(L, s == sub_s ? cap : s);
-          const long long key = simple_key(prof, e, scored, max_tt, rtt, max_na, rna, (uint32_t)(c.node_base + lo + s));
-          best = (e.f == 0 && key > best) ? key : best;
-        }
+    int cand = -1;  // the candidate slot whose H1 pass A evaluates (the shard's / the wave's best)
+    const bool keys = k >= k0 && pk.status == 0 && nf > 0;
+    const float rtt = __builtin_amdgcn_rcpf((float)max(max_tt, 1));
+    const float rna = __builtin_amdgcn_rcpf((float)max(max_na, 1));
+    if constexpr (PW) {
+      // every slot's five values read at once and its key computed whatever the verdict, then
+      // selected: one LDS round trip per slot, no exec-mask region; the wave's best by DPP
+      const int s = wv * pwv + lane;
+      if (keys && lane < pwv && s < own) {
+        const SVal e = cv_get(L, s == sub_s ? sub_h : s);
+        const long long key = simple_key(prof, e, scored, max_tt, rtt, max_na, rna, (uint32_t)(c.node_base + lo + s));
+        best = e.f == 0 ? key : 0;
       }
       if (sp && tid == 0) sp[1] = wall_clock64();
-      long long b[1] = {best};
-      const int op[1] = {OP_MAX};
-      block_red(H, parity, b, op);
-      parity ^= 1;
-      best = b[0];
+      best = wave_red<OP_MAX>(best);
       if (sp && tid == 0) sp[2] = wall_clock64();
-    }
-    const int cand_s = best ? (int)(0xFFFFFFFFu - (uint32_t)(unsigned long long)best) - c.node_base - lo : -1;
-    // pass A: pod k+1 before pod k's commit, and on the candidate after it
-    if (k + 1 < k1) {
-      simple_pass_a<DEF>(prof, L.ring[(k + 1) % 3], pk, L, (k + 1) % 3, own, cand_s, st);
     } else {
-#pragma unroll
-      for (int i = 0; i < 6; i++) st[i] = 0;
+      if (k >= k0) {
+        if (keys) {
+          for (int s = tid; s < own; s += nt) {
+            const SVal e = cv_get(L, s == sub_s ? sub_h : s);
+            const long long key = simple_key(prof, e, scored, max_tt, rtt, max_na, rna, (uint32_t)(c.node_base + lo + s));
+            best = (e.f == 0 && key > best) ? key : best;
+          }
+        }
+        if (sp && tid == 0) sp[1] = wall_clock64();
+        long long b[1] = {best};
+        const int op[1] = {OP_MAX};
+        block_red(H, parity, b, op);
+        parity ^= 1;
+        best = b[0];
+        if (sp && tid == 0) sp[2] = wall_clock64();
+      }
     }
-    if (sp && tid == 0) sp[3] = wall_clock64();
-    if (!simple_sync(H, parity, best, st, W, w, ++epoch, gran, X, err, per, c.node_base, R, sp)) return;
+    cand = best ? (int)(0xFFFFFFFFu - (uint32_t)(unsigned long long)best) - c.node_base - lo : -1;
+    // pass A: pod k+1 before pod k's commit, and on the candidate after it
+    const SPod& qn = L.ring[(k + 1) % RING];
+    const int sln = (k + 1) % RING;
+    if constexpr (PW) {
+      uint32_t u[6];
+      if (k + 1 < k1) {
+        simple_pass_a_pw<DEF>(prof, qn, pk, L, sln, own, pwv, cand, u);
+      } else {
+#pragma unroll
+        for (int i = 0; i < 6; i++) u[i] = 0;
+      }
+      if (sp && tid == 0) sp[3] = wall_clock64();
+      if (!simple_sync_pw(H, parity, best, u, W, w, ++epoch, gran, X, err, per, c.node_base, lo, own, pk, k >= k0, L, R,
+                          sp))
+        return;
+    } else {
+      if (k + 1 < k1) {
+        simple_pass_a<DEF>(prof, qn, pk, L, sln, own, cand, st);
+      } else {
+#pragma unroll
+        for (int i = 0; i < 6; i++) st[i] = 0;
+      }
+      if (sp && tid == 0) sp[3] = wall_clock64();
+      if (!simple_sync(H, parity, best, st, W, w, ++epoch, gran, X, err, per, c.node_base, R, sp)) return;
+    }
     if (sp && tid == 0) sp[5] = wall_clock64();
     if (k >= k0) {
       const long long K = R[0];
@@ -803,25 +962,20 @@ __device__ __forceinline__ void simple_schedule(DevCluster c, const SPod* __rest
           gmeta[k].best_total = m.best_total;
         }
       }
-      // AssumePod on the winner's shard; pass B of pod k+1 takes that slot's H1 values
+      // AssumePod on the winner's shard (per-wave mode: done inside the sync); pass B of pod
+      // k+1 takes that slot's H1 values: cv slot cap (cap + the slot's wave in per-wave mode)
       const bool won = x >= lo && x < hi;
       sub_s = won ? x - lo : -1;
-      if (won && tid == 0) {
-        const int s = x - lo;
-#pragma unroll
-        for (int r = 0; r < 3; r++) L.r64[(3 + r) * cap + s] += pk.creq[r];
-        L.r64[6 * cap + s] += pk.cnz[0];
-        L.r64[7 * cap + s] += pk.cnz[1];
-        L.r32[s] += 1;
-        // the HBM-only class / term counts are applied after the launch (k_counts): nothing
-        // in this loop reads them
-      }
+      sub_h = PW ? cap + (won ? (x - lo) / max(pwv, 1) : 0) : cap;
+      if (!PW && won && tid == 0) simple_commit_slot(L, pk, x - lo);
+      // the HBM-only class / term counts are applied after the launch (k_counts): nothing in
+      // this loop reads them
     }
     if (pf_on) {  // lanes past the end rewrite the last element with its own value
-      reinterpret_cast<uint4*>(L.ring + (k + 2) % 3)[min(pf_lane, NQ - 1)] = pfq;
+      reinterpret_cast<uint4*>(L.ring + (k + PD) % RING)[min(pf_lane, NQ - 1)] = pfq;
 #pragma unroll
       for (int j = 0; j < PF_MAX; j++)
-        if (j < pf_per) L.st[((k + 2) % 3) * cap + min(j * pf_n + pf_lane, own - 1)] = pfw[j];
+        if (j < pf_per) L.st[((k + PD) % RING) * cap + min(j * pf_n + pf_lane, own - 1)] = pfw[j];
     }
     if (sp && tid == 0) sp[6] = wall_clock64();
   }

@@ -40,28 +40,37 @@ def _copy(v):
 
 
 def _compare(cluster, pods, n, rollback_every=0):
-    """Service eval + commit vs eval_pod_view + commit on two contexts, pod after pod."""
+    """Service eval + commit vs eval_pod_view + commit, pod after pod: the launch-per-call
+    sequence runs first, to completion, then the service sequence.  (Interleaving two contexts
+    in one process would put the reference context's launches behind the resident grid
+    whenever their streams share a hardware queue: they would wait for its idle exit.)"""
     ref = native.Context(abi.default_profile())
     ref.load(cluster)
+    N = ref.n_nodes
+    want = []
+    for j in range(n):
+        w = _copy(ref.eval_pod_view(pods, j))
+        want.append(w)
+        if w.chosen >= 0:
+            ref.commit(pods, j, w.chosen)
+            if rollback_every and j % rollback_every == 0:
+                ref.rollback(pods, j, w.chosen)
+    st_r = ref.node_state()
+    ref.close()
     svc = native.Context(abi.default_profile())
     svc.load(cluster)
     svc.stage(pods)
-    N = ref.n_nodes
     for j in range(n):
-        want = _copy(ref.eval_pod_view(pods, j))
         got = svc.service_eval(j)
-        _same(got, want, N, j)
-        if want.chosen >= 0:
-            ref.commit(pods, j, want.chosen)
-            svc.service_commit(j, want.chosen)
+        _same(got, want[j], N, j)
+        if want[j].chosen >= 0:
+            svc.service_commit(j, want[j].chosen)
             if rollback_every and j % rollback_every == 0:
-                ref.rollback(pods, j, want.chosen)
-                svc.service_rollback(j, want.chosen)
+                svc.service_rollback(j, want[j].chosen)
     svc.service_stop()
-    st_r, st_s = ref.node_state(), svc.node_state()
+    st_s = svc.node_state()
     for k in ("requested", "nonzero", "pod_count"):
         np.testing.assert_array_equal(st_s[k], st_r[k], err_msg=k)
-    ref.close()
     svc.close()
 
 

@@ -14,7 +14,7 @@
 #   split2       bench.py --split 2 (C4 as two parts on the one GPU)
 #   perpod       bench.py --per-pod
 #   postfilter   bench.py --postfilter
-#   prof_c2 prof_c3 prof_c4 prof_c5
+#   prof_c2 prof_c3 prof_c4 prof_c5 prof_pf prof_pp
 #                rocprofv3 --kernel-trace --stats of the matching inner bench run
 #   sq_c2 sq_c5  rocprofv3 --pmc SQ counter passes (one pass per group) of the inner run
 #   counters     rocprofv3 -L (the counters this box's gfx950 exposes)
@@ -69,6 +69,8 @@ run_step() {
     prof_c3) prof prof_c3 300 --config 3 --steps 3 --warmup 1 ;;
     prof_c4) prof prof_c4 400 --config 4 --steps 2 --warmup 1 ;;
     prof_c5) prof prof_c5 300 --scenarios 512 --steps 3 --warmup 1 ;;
+    prof_pf) prof prof_pf 300 --postfilter --steps 1 --warmup 1 ;;
+    prof_pp) prof prof_pp 300 --per-pod --steps 1 --warmup 1 ;;
     sq_c2) sq sq_c2 --steps 1 --warmup 0 ;;
     sq_c5) sq sq_c5 --scenarios 512 --steps 1 --warmup 0 ;;
     counters) (cd /tmp && timeout -s KILL 60 rocprofv3 -L > "$O/${tag}_counters.txt" 2>&1) ;;
