@@ -741,47 +741,38 @@ __device__ __forceinline__ bool simple_sync_pw(SimpleHdr& H, int& parity, long l
     for (int i = 0; i < 6; i++) H.red[parity][wave][1 + i] = u[i];
   }
   lds_barrier();
-  long long best = 0;
-  int ws = -1;
-  for (int v = 0; v < nw; v++) {
-    const long long b = H.red[parity][v][0];
-    if (b > best) {
-      best = b;
-      ws = v;
+  if (wave == 0) {  // wave 0 alone combines (lane v holds wave v's values) and exchanges; the others wait
+    const bool in = lane < nw;
+    const long long* h = H.red[parity][in ? lane : 0];
+    const long long b = in ? h[0] : 0;
+    const long long best = wave_red<OP_MAX>(b);
+    // the wave holding the shard's best (keys carry the node index: one wave at most)
+    const unsigned long long m = __ballot(in && best != 0 && b == best);
+    const int ws = m ? __ffsll((long long)m) - 1 : -1;
+    const int o = lane == ws ? 4 : 1;  // the best wave contributes its H1, the others their H0
+    uint32_t t[6] = {in ? (uint32_t)h[1] : 0u, in ? (uint32_t)h[2] : 0u, in ? (uint32_t)h[3] : 0u,
+                     in ? (uint32_t)h[o] : 0u, in ? (uint32_t)h[o + 1] : 0u, in ? (uint32_t)h[o + 2] : 0u};
+    wave_red_stats(t);
+    if (sp && lane == 0) sp[4] = wall_clock64();
+    if (W == 1) {  // the winner (if any) is this shard's best
+      if (lane == 0) {
+        const bool h1 = best != 0;
+        H.res[0] = best;
+        H.res[1] = h1 ? t[3] : t[0];
+        H.res[2] = h1 ? t[4] : t[1];
+        H.res[3] = h1 ? t[5] : t[2];
+        if (commit && h1) simple_commit_slot(L, pk, (int)(0xFFFFFFFFu - (uint32_t)(unsigned long long)best) - node_base - lo);
+      }
+    } else {
+      const long long v[7] = {best, t[0], t[1], t[2], t[3], t[4], t[5]};
+      if (simple_exchange(H, gran, X, W, w, epoch, err, v, per, node_base) && commit && lane == 0) {
+        const long long K = H.res[0];
+        const int x = K ? (int)(0xFFFFFFFFu - (uint32_t)(unsigned long long)K) - node_base - lo : -1;
+        if (x >= 0 && x < own) simple_commit_slot(L, pk, x);
+      }
     }
-  }
-  long long st[6] = {0, 0, 0, 0, 0, 0};
-  for (int v = 0; v < nw; v++) {
-    const long long* h = H.red[parity][v];
-    const int o = v == ws ? 4 : 1;  // the best wave contributes its H1, the others their H0
-    st[0] += h[1];
-    st[1] = max(st[1], h[2]);
-    st[2] = max(st[2], h[3]);
-    st[3] += h[o];
-    st[4] = max(st[4], h[o + 1]);
-    st[5] = max(st[5], h[o + 2]);
   }
   parity ^= 1;
-  if (sp && threadIdx.x == 0) sp[4] = wall_clock64();
-  if (W == 1) {  // the winner (if any) is this shard's best
-    const bool h1 = best != 0;
-    R[0] = best;
-    R[1] = h1 ? st[3] : st[0];
-    R[2] = h1 ? st[4] : st[1];
-    R[3] = h1 ? st[5] : st[2];
-    if (commit && h1 && threadIdx.x == 0)
-      simple_commit_slot(L, pk, (int)(0xFFFFFFFFu - (uint32_t)(unsigned long long)best) - node_base - lo);
-    lds_barrier();
-    return true;
-  }
-  if (threadIdx.x < 64) {
-    const long long v[7] = {best, st[0], st[1], st[2], st[3], st[4], st[5]};
-    if (simple_exchange(H, gran, X, W, w, epoch, err, v, per, node_base) && commit && lane == 0) {
-      const long long K = H.res[0];
-      const int x = K ? (int)(0xFFFFFFFFu - (uint32_t)(unsigned long long)K) - node_base - lo : -1;
-      if (x >= 0 && x < own) simple_commit_slot(L, pk, x);
-    }
-  }
   lds_barrier();
   if (H.abort) return false;
 #pragma unroll

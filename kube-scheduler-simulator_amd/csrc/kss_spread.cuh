@@ -929,27 +929,39 @@ __device__ __forceinline__ void spread_schedule(DevCluster c, const GPod* __rest
         L.sf[s] = e.f | (ign << 16);
       }
       GSTAMP(3);
-      // one exchange: feasible count, normalisation maxima, IPA extrema, PTS sizes / extrema
-      int32_t v[13] = {nf, nign, max_tt, max_na, ipa_min, ipa_max, smissing | (lacks << 30), sdirect[0], sdirect[1],
-                       sdirect[2], sdirect[3], cmin, cmax};
-      const int op[13] = {OP_SUM, OP_SUM, OP_MAX, OP_MAX, OP_MIN, OP_MAX, OP_OR, OP_SUM, OP_SUM, OP_SUM, OP_SUM,
-                          OP_MIN, OP_MAX};
-      if (!spread_reduce(H, L.xs, W, w, epoch, gran, X, err, v, op, 0, 0, q.total_bins + q.hard_pbins,
-                         q.total_pbins - q.hard_pbins, false,
-                         stl && k - k0 < nst ? stl + (k - k0) * 16 + 10 : nullptr))
-        return;
-      nf = v[0];
-      nign = v[1];
-      max_tt = v[2];
-      max_na = v[3];
-      ipa_min = v[4];
-      ipa_max = v[5];
-      lacks = (v[6] >> 30) & 1;
-      smissing = v[6] & 0xF;
+      // one exchange: feasible count, normalisation maxima, IPA extrema, PTS sizes / extrema.
+      // A pod without ScheduleAnyway constraints and inter-pod terms (C4's zone spread) needs
+      // only the first three: the other ten stay at their identities on every shard, so they
+      // are not exchanged (a quarter of the granules each shard sweeps).
+      unsigned long long* est = stl && k - k0 < nst ? stl + (k - k0) * 16 + 10 : nullptr;
+      if (!has_soft && !has_ipa) {
+        int32_t v[3] = {nf, max_tt, max_na};
+        const int op[3] = {OP_SUM, OP_MAX, OP_MAX};
+        if (!spread_reduce(H, L.xs, W, w, epoch, gran, X, err, v, op, 0, 0, 0, 0, false, est)) return;
+        nf = v[0];
+        max_tt = v[1];
+        max_na = v[2];
+      } else {
+        int32_t v[13] = {nf, nign, max_tt, max_na, ipa_min, ipa_max, smissing | (lacks << 30), sdirect[0], sdirect[1],
+                         sdirect[2], sdirect[3], cmin, cmax};
+        const int op[13] = {OP_SUM, OP_SUM, OP_MAX, OP_MAX, OP_MIN, OP_MAX, OP_OR, OP_SUM, OP_SUM, OP_SUM, OP_SUM,
+                            OP_MIN, OP_MAX};
+        if (!spread_reduce(H, L.xs, W, w, epoch, gran, X, err, v, op, 0, 0, q.total_bins + q.hard_pbins,
+                           q.total_pbins - q.hard_pbins, false, est))
+          return;
+        nf = v[0];
+        nign = v[1];
+        max_tt = v[2];
+        max_na = v[3];
+        ipa_min = v[4];
+        ipa_max = v[5];
+        lacks = (v[6] >> 30) & 1;
+        smissing = v[6] & 0xF;
 #pragma unroll
-      for (int i = 0; i < MAXS; i++) sdirect[i] = v[7 + i];
-      cmin = v[11];
-      cmax = v[12];
+        for (int i = 0; i < MAXS; i++) sdirect[i] = v[7 + i];
+        cmin = v[11];
+        cmax = v[12];
+      }
       GSTAMP(4);
       m.n_feasible = nf;
       if (nf == 0) {
