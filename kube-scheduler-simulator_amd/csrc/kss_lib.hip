@@ -3025,7 +3025,7 @@ static int svc_start_locked(kss_ctx* ctx) {
     HIP_TRY(hipHostGetDevicePointer((void**)&v.rec_dev, v.rec, 0));
     v.rec_bytes = SL.bytes;
   }
-  int rc = ctx->slot_buf.ensure(SL.bytes);
+  int rc = ctx->slot_buf.ensure(2 * SL.bytes);  // two record slots used in turn (kss_service.cuh)
   if (!rc) rc = v.relay.ensure(sizeof(unsigned long long) * (2 * SVC_DRING + (size_t)W));
   if (!rc) rc = v.gran.ensure(sizeof(unsigned long long) * 2 * (size_t)W * 2 * XW_MAX);
   if (!rc) rc = v.err.ensure(16);
@@ -3647,8 +3647,8 @@ int upload_bound(kss_ctx* ctx) {
   size_t o_ptr = 0, o_id = align_up(4 * (N + 1), 256), o_prio = align_up(o_id + 8 * NB, 256),
          o_start = align_up(o_prio + 4 * NB, 256), o_cls = align_up(o_start + 8 * NB, 256),
          o_req = align_up(o_cls + 4 * NB, 256), o_toff = align_up(o_req + 8 * KSS_NRES * NB, 256),
-         o_tlen = align_up(o_toff + 4 * NB, 256), o_ord = align_up(o_tlen + 4 * NB, 256),
-         o_ints = align_up(o_ord + 4 * NB, 256), total = align_up(o_ints + 4 * std::max(ni, (size_t)1), 256);
+         o_tlen = align_up(o_toff + 4 * NB, 256), o_ints = align_up(o_tlen + 4 * NB, 256),
+         total = align_up(o_ints + 4 * std::max(ni, (size_t)1), 256);
   std::vector<char>& h = ctx->stage_host;
   h.assign(total, 0);
   int32_t* ptr = (int32_t*)(h.data() + o_ptr);
@@ -3660,14 +3660,14 @@ int upload_bound(kss_ctx* ctx) {
   int32_t* toff = (int32_t*)(h.data() + o_toff);
   int32_t* tlen = (int32_t*)(h.data() + o_tlen);
   int32_t* ints = (int32_t*)(h.data() + o_ints);
-  int32_t* ord = (int32_t*)(h.data() + o_ord);
   size_t e = 0, t = 0;
   std::vector<int32_t> perm;
   for (int n = 0; n < N; n++) {
     ptr[n] = (int32_t)e;
     // the node's pods in MoreImportantPod order (priority descending, start ascending, NodeInfo
     // order on ties — the preemptor does not enter it): SelectVictimsOnNode's reprieve order,
-    // and the pods below a priority form a suffix of it
+    // and the pods below a priority form a contiguous suffix of it.  Nothing on the device
+    // needs NodeInfo order itself (the dry run's sums do not depend on it).
     const auto& v = per[n];
     perm.resize(v.size());
     for (size_t k = 0; k < v.size(); k++) perm[k] = (int32_t)k;
@@ -3675,8 +3675,8 @@ int upload_bound(kss_ctx* ctx) {
       if (v[a].prio != v[b].prio) return v[a].prio > v[b].prio;
       return v[a].start < v[b].start;
     });
-    for (size_t k = 0; k < v.size(); k++) ord[e + k] = (int32_t)e + perm[k];
-    for (const BoundPod& b : per[n]) {
+    for (const int32_t pi : perm) {
+      const BoundPod& b = v[pi];
       id[e] = b.id;
       prio[e] = b.prio;
       start[e] = b.start;
@@ -3703,7 +3703,6 @@ int upload_bound(kss_ctx* ctx) {
   B.req = (const int64_t*)(d + o_req);
   B.toff = (const int32_t*)(d + o_toff);
   B.tlen = (const int32_t*)(d + o_tlen);
-  B.ord = (const int32_t*)(d + o_ord);
   B.ints = (const int32_t*)(d + o_ints);
   ctx->bound_dirty = false;
   return 0;

@@ -40,7 +40,9 @@ constexpr int PRE_THREADS = 512;
 constexpr int PRE_WAVES = PRE_THREADS / 64;
 constexpr int PRE_NODE_THREADS = 64;  // k_preempt_nodes: one lane per node, many small workgroups
 
-// Bound pods on the device: CSR by node, NodeInfo.Pods order inside a node.
+// Bound pods on the device: CSR by node, each node's pods in MoreImportantPod order (the host
+// sorts them when it uploads the table: priority descending, start ascending, NodeInfo order
+// on ties).
 struct DevBound {
   const int32_t* ptr;    // [N + 1]
   const int64_t* id;     // [nb] caller ids
@@ -50,7 +52,6 @@ struct DevBound {
   const int64_t* req;    // [nb][KSS_NRES]
   const int32_t* toff;   // [nb] into ints
   const int32_t* tlen;   // [nb]
-  const int32_t* ord;    // [nb] per node, its pods' indices in MoreImportantPod order (host-sorted)
   const int32_t* ints;
 };
 
@@ -267,7 +268,7 @@ __device__ __forceinline__ DryResult select_victims(const PreemptJob& J, const k
   // the potential victims (priority below the preemptor's) are the suffix [p0, e1) of the
   // node's importance order, visited in reprieve order
   int p0 = e1;
-  while (p0 > e0 && B.prio[B.ord[p0 - 1]] < prio) p0--;
+  while (p0 > e0 && B.prio[p0 - 1] < prio) p0--;
   if (p0 == e1) return res;  // "No preemption victims found for incoming pod"
   // the node's view, then every lower-priority pod removed
   DryState s;
@@ -302,13 +303,13 @@ __device__ __forceinline__ DryResult select_victims(const PreemptJob& J, const k
     for (int h = 0; h < 3; h++) s.A[k][h] = ipa_value(c, P, p, pl, bins, k, h, d, n);
   }
   s.T = H.aff_total;
-  for (int k = p0; k < e1; k++) apply_pod(J, p, pl, B.ord[k], n, -1, s);
+  for (int k = p0; k < e1; k++) apply_pod(J, p, pl, k, n, -1, s);
   if (!dry_fits(J, p, pl, H, s, n)) return res;
   // reprieve in importance order (MoreImportantPod, NodeInfo order on ties)
   int victims = 0;
   int64_t hp = 0, sum = 0, st = 0;
   for (int k = p0; k < e1; k++) {
-    const int best = B.ord[k];
+    const int best = k;
     apply_pod(J, p, pl, best, n, 1, s);
     if (!dry_fits(J, p, pl, H, s, n)) {
       apply_pod(J, p, pl, best, n, -1, s);

@@ -81,7 +81,8 @@ struct SharedHdr {
   Plan plan;    // computed by lane 0 of the workgroup each pod, read by all
   int plan_ok;
   int abort;
-  int pad[2];
+  unsigned svc_dirty;  // the service grid: record rows whose shard segment changed (kss_service.cuh)
+  int pad;
   int cmd[4];   // the service grid's current command (kss_service.cuh)
 };
 

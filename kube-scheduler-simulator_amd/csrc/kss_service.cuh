@@ -71,12 +71,12 @@ __device__ __forceinline__ void st_sys(KSS_GLOBAL unsigned long long* p, unsigne
 // and element stores for the at most 15 bytes at either end.  Both buffers are 16-byte
 // aligned row blocks of the same layout (SlotLayout).
 template <int ES>
-__device__ __forceinline__ void svc_copy(const uint8_t* src, uint8_t* dst, size_t N, int rows, int lo, int hi) {
+__device__ __forceinline__ void svc_copy(const uint8_t* src, uint8_t* dst, size_t N, int r0, int rows, int lo, int hi) {
   using T = typename std::conditional<ES == 8, uint64_t, typename std::conditional<ES == 2, uint16_t, uint8_t>::type>::type;
   constexpr int V = 16 / ES;  // elements per 16-byte store
   const int tid = (int)threadIdx.x, nt = (int)blockDim.x;
-  for (int r = 0; r < rows; r++) {
-    const size_t base = (size_t)r * N;  // element offset of the row
+  for (int r = r0; r < r0 + rows; r++) {
+    const size_t base = (size_t)r * N;  // element offset of the row from the field's (16-byte aligned) start
     // elements [a, b) of the row start 16-byte aligned chunks: base + a is a multiple of V
     const size_t a0 = base + (size_t)lo, b0 = base + (size_t)hi;
     const size_t a = (a0 + V - 1) / V * V, b = b0 / V * V;
@@ -98,6 +98,54 @@ __device__ __forceinline__ void svc_copy(const uint8_t* src, uint8_t* dst, size_
       for (int i = tid; i < (int)(b0 - a0); i += nt) d[a0 + i] = s[a0 + i];
     }
   }
+}
+
+// The record as SVC_ROWS rows of one element per node: fail, detail, total, raw[KSS_NSCORE],
+// norm[KSS_NSCORE].
+constexpr int SVC_ROWS = 3 + 2 * KSS_NSCORE;
+__device__ __forceinline__ int svc_row_field(int r) {
+  return r == 0 ? KSS_FIELD_FAIL : r == 1 ? KSS_FIELD_DETAIL : r == 2 ? KSS_FIELD_TOTAL : r < 3 + KSS_NSCORE ? KSS_FIELD_RAW
+                                                                                                           : KSS_FIELD_NORM;
+}
+// record row r: its field's byte offset in a record of N nodes, the row within the field and
+// the element size
+__device__ __forceinline__ size_t svc_field(const SlotLayout& L, int r, int& fr, int& es) {
+  fr = 0;
+  if (r == 0) return es = 1, L.fail;
+  if (r == 1) return es = 2, L.detail;
+  es = 8;
+  if (r == 2) return L.total;
+  if (r < 3 + KSS_NSCORE) return fr = r - 3, L.raw;
+  return fr = r - 3 - KSS_NSCORE, L.norm;
+}
+__device__ __forceinline__ size_t svc_row_off(const SlotLayout& L, size_t N, int r, int& es) {
+  int fr = 0;
+  const size_t o = svc_field(L, r, fr, es);
+  return o + (size_t)es * (size_t)fr * N;
+}
+
+// The rows (bit r) whose elements [lo, hi) differ between two records; every lane of the
+// workgroup gets the mask (one LDS word, two barriers).
+__device__ __forceinline__ unsigned svc_changed_rows(const uint8_t* a, const uint8_t* b, const SlotLayout& L, size_t N,
+                                                     unsigned rows, int lo, int hi, unsigned& word) {
+  if (threadIdx.x == 0) word = 0;
+  __syncthreads();
+  unsigned mine = 0;
+  for (int r = 0; r < SVC_ROWS; r++) {
+    if (!((rows >> r) & 1u)) continue;
+    int es = 0;
+    const size_t o = svc_row_off(L, N, r, es);
+    bool d = false;
+    for (int i = lo + (int)threadIdx.x; i < hi; i += (int)blockDim.x) {
+      if (es == 1) d |= gp(a + o)[i] != gp(b + o)[i];
+      else if (es == 2) d |= gp(reinterpret_cast<const uint16_t*>(a + o))[i] != gp(reinterpret_cast<const uint16_t*>(b + o))[i];
+      else d |= gp(reinterpret_cast<const uint64_t*>(a + o))[i] != gp(reinterpret_cast<const uint64_t*>(b + o))[i];
+    }
+    mine |= d ? 1u << r : 0u;
+  }
+  if (mine) atomicOr(&word, mine);
+  __syncthreads();
+  return word;
 }
 
 template <bool GEN>
@@ -139,6 +187,8 @@ __device__ void service_loop(DevCluster c, const DevJob& job, const kss_profile&
   if (w == 0 && threadIdx.x == 0) __hip_atomic_store(&box->running, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   unsigned long long st0 = 0, st1 = 0, st2 = 0;  // diagnostic clocks of shard 0's lane 0 (stamps)
   unsigned long long seen_min = seq;              // shard 0: every shard has taken the commands below this
+  int parity = 0;                                 // the record slot of the next evaluation
+  unsigned host_valid = 0;  // rows (bit r) whose host segment equals the last evaluation's slot
   for (;; ++seq) {
     if (threadIdx.x == 0) {
       int op = SVC_STOP, pod = 0, node = 0, fields = 0;
@@ -210,7 +260,11 @@ __device__ void service_loop(DevCluster c, const DevJob& job, const kss_profile&
     __syncthreads();  // the command words may be rewritten by the next iteration's lane 0
     if (op == SVC_STOP) break;
     if (op == SVC_EVAL) {
-      uint8_t* base = job.slots;
+      // two HBM record slots used in turn: a row segment equal to the previous evaluation's,
+      // which the host record already holds, is not sent over PCIe again
+      uint8_t* base = job.slots + (size_t)parity * job.slot_bytes;
+      const uint8_t* prev = job.slots + (size_t)(parity ^ 1) * job.slot_bytes;
+      parity ^= 1;
       Slot s;
       s.fail = base + L.fail;
       s.detail = (uint16_t*)(base + L.detail);
@@ -223,12 +277,21 @@ __device__ void service_loop(DevCluster c, const DevJob& job, const kss_profile&
         break;
       }
       if (stamps && w == 0 && threadIdx.x == 0) st2 = wall_clock64();
-      // this shard's node range of the requested fields -> the pinned host record
-      if (fields & KSS_FIELD_FAIL) svc_copy<1>(base + L.fail, rec_host + L.fail, N, 1, S.lo, S.hi);
-      if (fields & KSS_FIELD_DETAIL) svc_copy<2>(base + L.detail, rec_host + L.detail, N, 1, S.lo, S.hi);
-      if (fields & KSS_FIELD_TOTAL) svc_copy<8>(base + L.total, rec_host + L.total, N, 1, S.lo, S.hi);
-      if (fields & KSS_FIELD_RAW) svc_copy<8>(base + L.raw, rec_host + L.raw, N, KSS_NSCORE, S.lo, S.hi);
-      if (fields & KSS_FIELD_NORM) svc_copy<8>(base + L.norm, rec_host + L.norm, N, KSS_NSCORE, S.lo, S.hi);
+      // this shard's node range of the requested rows -> the pinned host record, skipping the
+      // segments the host already holds (equal to the previous evaluation's, which it copied)
+      unsigned want = 0;
+      for (int r = 0; r < SVC_ROWS; r++) want |= (fields & svc_row_field(r)) ? 1u << r : 0u;
+      const unsigned send = (want & ~host_valid) | svc_changed_rows(base, prev, L, N, want & host_valid, S.lo, S.hi,
+                                                                    shdr(smem).svc_dirty);
+      for (int r = 0; r < SVC_ROWS; r++) {
+        if (!((send >> r) & 1u)) continue;
+        int es = 0, fr = 0;
+        const size_t o = svc_field(L, r, fr, es);
+        if (es == 1) svc_copy<1>(base + o, rec_host + o, N, fr, 1, S.lo, S.hi);
+        else if (es == 2) svc_copy<2>(base + o, rec_host + o, N, fr, 1, S.lo, S.hi);
+        else svc_copy<8>(base + o, rec_host + o, N, fr, 1, S.lo, S.hi);
+      }
+      host_valid = want;  // the host's rows not asked for now no longer mirror the newest slot
       if (w == 0 && threadIdx.x == 0) {
         KSS_GLOBAL int32_t* mm = reinterpret_cast<KSS_GLOBAL int32_t*>(&box->meta);
         mm[0] = m.chosen;

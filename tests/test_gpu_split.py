@@ -67,12 +67,19 @@ def test_parts_over_many_chunks(monkeypatch, config, n_nodes, n_pods, per_chunk,
     (the chunk sequence continues across runs)."""
     monkeypatch.setenv("KSS_STATIC_BYTES", str(4 * n_nodes * per_chunk))
     s = native.Synth(config, SEED_BASE + config, n_nodes, n_pods)
-    ch_o, _, st = _oracle(s, n_pods)
+    ch_o, res, st = _oracle(s, n_pods)
     sp = split.InProcessSplit(s.cluster, s.pods, 2, wl)
     for rep in range(3):
         sp.reset()
-        for p, ch in enumerate(sp.run(n_pods)):
-            np.testing.assert_array_equal(ch, ch_o, err_msg=f"part {p} run {rep}")
+        outs = sp.run(n_pods)
+        bad = [np.flatnonzero(np.asarray(ch) != ch_o) for ch in outs]
+        if any(len(b) for b in bad):  # what went wrong, for the record: pod, chunk position, outcomes
+            j = int(next(b for b in bad if len(b))[0])
+            meta = [c.fetch_meta(n_pods)[j].tolist() for c in sp.ctxs]
+            m = res.meta(j)
+            pytest.fail(f"run {rep}: mismatching pods per part {[b.tolist() for b in bad]}; first {j} = chunk "
+                        f"{j // per_chunk} pod {j % per_chunk}; device {[o[j] for o in outs]} meta {meta}; oracle "
+                        f"{ch_o[j]} meta {[m['chosen'], m['n_feasible'], m['scored'], m['status'], m['best_total']]}")
         assert sp.ctxs[0].last_timing()[1] == 2 * -(-n_pods // per_chunk)  # k_static + loop per chunk
     g = sp.node_state()
     np.testing.assert_array_equal(g["requested"][:, :n_nodes], st["requested"][:, :n_nodes])

@@ -16,7 +16,7 @@
 #   postfilter   bench.py --postfilter
 #   prof_c2 prof_c3 prof_c4 prof_c5 prof_pf prof_pp
 #                rocprofv3 --kernel-trace --stats of the matching inner bench run
-#   sq_c2 sq_c5  rocprofv3 --pmc SQ counter passes (one pass per group) of the inner run
+#   sq_c2 sq_c5 sq_pf  rocprofv3 --pmc SQ counter passes (one pass per group) of the inner run
 #   counters     rocprofv3 -L (the counters this box's gfx950 exposes)
 #   flake_split flake_single   tools/diag_flake.py (repeat a many-chunk run, count oracle mismatches)
 set -o pipefail
@@ -73,6 +73,7 @@ run_step() {
     prof_pp) prof prof_pp 300 --per-pod --steps 1 --warmup 1 ;;
     sq_c2) sq sq_c2 --steps 1 --warmup 0 ;;
     sq_c5) sq sq_c5 --scenarios 512 --steps 1 --warmup 0 ;;
+    sq_pf) sq sq_pf --postfilter --steps 1 --warmup 0 ;;
     counters) (cd /tmp && timeout -s KILL 60 rocprofv3 -L > "$O/${tag}_counters.txt" 2>&1) ;;
     flake_split|flake_single)  # tools/diag_flake.py: repeated split / single-context many-chunk runs vs the oracle
       timeout -k 10 240 python -u tools/diag_flake.py ${1#flake_} ${FLAKE_REPS:-8} > "$O/${tag}_$1.txt" 2>&1; local rc=$?
