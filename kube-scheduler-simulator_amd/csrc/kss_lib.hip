@@ -237,7 +237,7 @@ __global__ __launch_bounds__(KSS_MAX_THREADS) void k_spread(const DevJob* __rest
     __syncthreads();
   }
   const kss_profile& P = DEF ? def_prof : H.prof;
-  spread_schedule(job.c, job.gpods, job.stat, job.res_rows, n_res, k0, min(k1, job.n_pods), job.chosen, job.meta, P, W, w,
+  spread_schedule<DEF>(job.c, job.gpods, job.stat, job.res_rows, n_res, k0, min(k1, job.n_pods), job.chosen, job.meta, P, W, w,
                   cap, bins_cap, gq, gran ? gran + (size_t)ji * 2 * W * G_XW : nullptr, X, epoch0, err, stamps, nst, smem);
 }
 

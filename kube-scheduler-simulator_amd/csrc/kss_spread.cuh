@@ -711,6 +711,7 @@ __device__ __forceinline__ int64_t g_ipa_score(const SpreadShard& L, const GPod&
 
 // The batch for shard w of one cluster, pods [k0, k1).  res_rows: the resident count rows
 // (class r as r, term r as n_classes + r), n_res of them.
+template <bool DEF>
 __device__ __forceinline__ void spread_schedule(DevCluster c, const GPod* __restrict__ gpods,
                                                 const uint32_t* __restrict__ stat, const int32_t* __restrict__ res_rows,
                                                 int n_res, int k0, int k1, int32_t* chosen, PodMeta* meta,
@@ -855,6 +856,7 @@ __device__ __forceinline__ void spread_schedule(DevCluster c, const GPod* __rest
     int32_t sdirect[MAXS] = {0, 0, 0, 0};
     int32_t cmin = INT32_MAX, cmax = INT32_MIN, lacks = 0;
     if (evaluated) {
+      const SPod qd = q.dyn;  // in registers: the loop's LDS stores would make every field a reload
       for (int s = tid; s < own; s += nt) {
         const uint32_t wd = sw[s];
         DynRow r;
@@ -868,7 +870,7 @@ __device__ __forceinline__ void spread_schedule(DevCluster c, const GPod* __rest
         r.nz[1] = L.r64[7 * cap + s];
         r.pods = L.r32[s];
         r.allowed = L.r32[cap + s];
-        SVal e = dyn_eval(prof, q.dyn, wd, r);
+        SVal e = DEF ? dyn_eval_def(qd, wd, r) : dyn_eval(prof, qd, wd, r);
         if (e.f == 0 && ((en >> KSS_F_POD_TOPOLOGY_SPREAD) & 1u) && q.n_hard > 0 &&
             g_filter_pts(L, q, bins, hard_min, s, wd))
           e.f = KSS_F_POD_TOPOLOGY_SPREAD;
