@@ -97,6 +97,10 @@ struct Slot {
   int64_t* raw;   // [KSS_NSCORE][N]
   int64_t* norm;  // [KSS_NSCORE][N]
   int64_t* total; // [N]
+  bool canon = false;  // also write 0 to the entries the record leaves undefined (infeasible nodes'
+                       // scores, an unscored pod's normalised scores and totals): the service grid
+                       // sends only row segments that changed, so every entry must be a function
+                       // of the pod and the state
 };
 
 struct PodMeta {
@@ -729,6 +733,9 @@ __device__ __forceinline__ bool schedule_pod(const DevCluster& c, const DevPods&
       KSS_DCHECK(n >= 0 && n < c.N, "out n", n, c.N);
       out->fail[n] = (uint8_t)f;
       out->detail[n] = detail;
+      if (out->canon && f != KSS_F_PASS)
+#pragma unroll
+        for (int x = 0; x < KSS_NSCORE; x++) out->raw[(size_t)x * NN + n] = 0;
     }
     int ign = 0, il = 0;
     if (f == KSS_F_PASS) {
@@ -898,6 +905,11 @@ __device__ __forceinline__ bool schedule_pod(const DevCluster& c, const DevPods&
     const int n = S.lo + k * nt + tid;
     const int si = k * nt + tid;
     const int fi = sa.fail[si];
+    if (out && out->canon && keep_norm && n < S.hi && ((fi & 0xFFFF) != KSS_F_PASS || !scored)) {
+#pragma unroll
+      for (int x = 0; x < KSS_NSCORE; x++) out->norm[(size_t)x * NN + n] = 0;
+      out->total[n] = 0;
+    }
     if ((fi & 0xFFFF) != KSS_F_PASS) continue;
     int64_t total = 0;
     if (scored) {

@@ -266,6 +266,7 @@ __device__ void service_loop(DevCluster c, const DevJob& job, const kss_profile&
       const uint8_t* prev = job.slots + (size_t)(parity ^ 1) * job.slot_bytes;
       parity ^= 1;
       Slot s;
+      s.canon = true;
       s.fail = base + L.fail;
       s.detail = (uint16_t*)(base + L.detail);
       s.raw = (int64_t*)(base + L.raw);

@@ -724,13 +724,14 @@ __device__ __forceinline__ void simple_commit_slot(const SimpleShard& L, const S
 }
 
 // Per-wave mode's one reduction per pod: the waves' best keys and H0 / H1 statistics in one
-// LDS pass (the shard's H1 is the best wave's H1 with every other wave's H0) and the
-// cross-shard exchange.  Pod k's AssumePod is applied at the start of the next pass A by the
-// lane that owns the winner's slot.  R = {winner key, nf, max TT, max NA of the next pod}.
-// False if the launch aborted.
+// LDS pass (the shard's H1 is the best wave's H1 with every other wave's H0), the cross-shard
+// exchange, and pod k's AssumePod on the winner's slot by wave 0 BEFORE the closing barrier
+// (the next pod's pass A reads that row with no barrier of its own in between).
+// R = {winner key, nf, max TT, max NA of the next pod}.  False if the launch aborted.
 __device__ __forceinline__ bool simple_sync_pw(SimpleHdr& H, int& parity, long long wbest, uint32_t (&u)[6], int W,
                                                int w, unsigned epoch, unsigned long long* gran, const XPeers& X,
-                                               int* err, int per, int node_base, long long (&R)[4],
+                                               int* err, int per, int node_base, int lo, int own, const SPod& pk,
+                                               bool commit, const SimpleShard& L, long long (&R)[4],
                                                KSS_GLOBAL unsigned long long* sp) {
   wave_red_stats(u);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
@@ -760,10 +761,15 @@ __device__ __forceinline__ bool simple_sync_pw(SimpleHdr& H, int& parity, long l
         H.res[1] = h1 ? t[3] : t[0];
         H.res[2] = h1 ? t[4] : t[1];
         H.res[3] = h1 ? t[5] : t[2];
+        if (commit && h1) simple_commit_slot(L, pk, (int)(0xFFFFFFFFu - (uint32_t)(unsigned long long)best) - node_base - lo);
       }
     } else {
       const long long v[7] = {best, t[0], t[1], t[2], t[3], t[4], t[5]};
-      simple_exchange(H, gran, X, W, w, epoch, err, v, per, node_base);
+      if (simple_exchange(H, gran, X, W, w, epoch, err, v, per, node_base) && commit && lane == 0) {
+        const long long K = H.res[0];
+        const int x = K ? (int)(0xFFFFFFFFu - (uint32_t)(unsigned long long)K) - node_base - lo : -1;
+        if (x >= 0 && x < own) simple_commit_slot(L, pk, x);
+      }
     }
   }
   parity ^= 1;
@@ -906,12 +912,6 @@ __device__ __forceinline__ void simple_schedule(DevCluster c, const SPod* __rest
     const SPod& qn = L.ring[(k + 1) % RING];
     const int sln = (k + 1) % RING;
     if constexpr (PW) {
-      // pod k-1's AssumePod on its winner's slot, by the lane that owns the slot, ahead of its
-      // own pass-A loads (program order) and of the wave's H1 lane (the only other lane that may
-      // read the row in this pass: the same wave, and LDS keeps a wave's accesses in order), so
-      // no barrier separates it from the exchange that chose the winner
-      if (sub_s >= 0 && lane < pwv && wv * pwv + lane == sub_s) simple_commit_slot(L, L.ring[(k - 1 + RING) % RING], sub_s);
-      asm volatile("" ::: "memory");
       uint32_t u[6];
       if (k + 1 < k1) {
         simple_pass_a_pw<DEF>(prof, qn, pk, L, sln, own, pwv, cand, u);
@@ -920,7 +920,9 @@ __device__ __forceinline__ void simple_schedule(DevCluster c, const SPod* __rest
         for (int i = 0; i < 6; i++) u[i] = 0;
       }
       if (sp && tid == 0) sp[3] = wall_clock64();
-      if (!simple_sync_pw(H, parity, best, u, W, w, ++epoch, gran, X, err, per, c.node_base, R, sp)) return;
+      if (!simple_sync_pw(H, parity, best, u, W, w, ++epoch, gran, X, err, per, c.node_base, lo, own, pk, k >= k0, L, R,
+                          sp))
+        return;
     } else {
       if (k + 1 < k1) {
         simple_pass_a<DEF>(prof, qn, pk, L, sln, own, cand, st);
@@ -968,8 +970,6 @@ __device__ __forceinline__ void simple_schedule(DevCluster c, const SPod* __rest
     }
     if (sp && tid == 0) sp[6] = wall_clock64();
   }
-  // per-wave mode: the last pod's AssumePod is still pending (the next pass A would apply it)
-  if (PW && sub_s >= 0 && lane < pwv && wv * pwv + lane == sub_s) simple_commit_slot(L, L.ring[(k1 - 1) % RING], sub_s);
   // node state back to HBM
   __syncthreads();
   for (int s = tid; s < own; s += nt) {
