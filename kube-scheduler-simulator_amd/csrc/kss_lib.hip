@@ -369,6 +369,10 @@ struct DevBuf {
     size_t nb = std::max(bytes, (size_t)4096);
     if (hipMalloc(&p, nb) != hipSuccess) return fail(KSS_E_NOMEM, "hipMalloc failed");
     cap = nb;
+    // diagnostic (KSS_POISON): fresh buffers hold a byte pattern, not the zeros a new process
+    // tends to get, so a read of never-written memory shows up in a short run
+    static const bool poison = getenv("KSS_POISON") != nullptr;
+    if (poison && hipMemset(p, 0xA5, nb) != hipSuccess) return fail(KSS_E_NOMEM, "poison memset failed");
     return 0;
   }
   void release() {
@@ -513,6 +517,7 @@ struct kss_ctx {
   bool state_unknown = false;
   DevBuf bound_buf, pre_buf;
   DevBound bound_dev{};
+  size_t bound_total = 0;  // bound pods in the table
   // the per-pod service grid (kss_service_*, kss_service.cuh)
   struct Service {
     bool running = false;          // launched and not known to have left
@@ -3689,6 +3694,7 @@ int upload_bound(kss_ctx* ctx) {
     }
   }
   ptr[N] = (int32_t)e;
+  ctx->bound_total = e;
   int rc = ctx->bound_buf.ensure(total);
   if (rc) return rc;
   char* d = (char*)ctx->bound_buf.p;
@@ -3751,7 +3757,9 @@ int kss_postfilter_pod(kss_ctx* ctx, const kss_podset* ps, int32_t pod_index, ks
   const size_t o_job = 0, o_out = align_up(sizeof(PreemptJob), 256), o_vic = o_out + sizeof(PreemptOut),
                o_key = align_up(o_vic + 8 * (size_t)std::max(cap, 1), 256),
                o_g = align_up(o_key + 5 * 8 * std::max(N, (size_t)1), 256), o_bins = align_up(o_g + sizeof(PreGlobal), 256),
-               total = o_bins + 8 * (size_t)bins_cap;
+               o_top = align_up(o_bins + 8 * (size_t)bins_cap, 256),
+               o_vs = align_up(o_top + 8 * 2 * MAXH * (size_t)PRE_STATS_MAX_BLOCKS, 256),
+               total = o_vs + 8 * std::max<size_t>(ctx->bound_total, 1);
   if ((rc = ctx->pre_buf.ensure(total))) return rc;
   char* d = (char*)ctx->pre_buf.p;
   PreemptJob J{};
@@ -3772,10 +3780,15 @@ int kss_postfilter_pod(kss_ctx* ctx, const kss_podset* ps, int32_t pod_index, ks
   J.out = (PreemptOut*)(d + o_out);
   J.G = (PreGlobal*)(d + o_g);
   J.gbins = (long long*)(d + o_bins);
+  J.stop2 = (long long*)(d + o_top);
+  J.vscratch = (int64_t*)(d + o_vs);
+  // stats workgroups: about 512 nodes each (the histograms are added into the zeroed HBM bins)
+  const unsigned nsb = (unsigned)std::min<size_t>(std::max<size_t>((N + 511) / 512, 1), PRE_STATS_MAX_BLOCKS);
   HIP_TRY(hipMemcpyAsync(d + o_job, &J, sizeof(J), hipMemcpyHostToDevice, ctx->stream));
   HIP_TRY(hipEventRecord(ctx->ev0, ctx->stream));
+  HIP_TRY(hipMemsetAsync(d + o_g, 0, o_top - o_g, ctx->stream));  // PreGlobal (ticket, sums) and the bins
   const PreemptJob* jd = (const PreemptJob*)(d + o_job);
-  hipLaunchKernelGGL(k_preempt_stats, dim3(1), dim3(PRE_THREADS), lds, ctx->stream, jd);
+  hipLaunchKernelGGL(k_preempt_stats, dim3(nsb), dim3(PRE_THREADS), lds, ctx->stream, jd);
   const unsigned nb = (unsigned)((N + PRE_NODE_THREADS - 1) / PRE_NODE_THREADS);
   hipLaunchKernelGGL(k_preempt_nodes, dim3(std::max(nb, 1u)), dim3(PRE_NODE_THREADS), sizeof(PreHdr), ctx->stream, jd);
   hipLaunchKernelGGL(k_preempt_pick, dim3(1), dim3(PRE_THREADS), sizeof(PreHdr), ctx->stream, jd);

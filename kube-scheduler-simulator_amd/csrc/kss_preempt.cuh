@@ -66,7 +66,10 @@ struct PreGlobal {
   long long aff_total, flags;
   int plan_ok, prefilter;
   int n_potential, n_candidates, feasible, pad;
+  unsigned ticket;  // k_preempt_stats workgroups done (the last one finishes the criticalPaths)
+  int pad2;
 };
+constexpr int PRE_STATS_MAX_BLOCKS = 64;
 
 struct PreemptJob {
   DevCluster c;
@@ -79,6 +82,10 @@ struct PreemptJob {
   int32_t n_blocks;  // k_preempt_nodes workgroups
   int64_t* key;      // [5][n_blocks] HBM scratch: each workgroup's best candidate (hp, sum, cnt, start, node)
   int64_t* victims;  // [victims_cap]
+  int64_t* vscratch; // [bound pods]: each candidate node's victims in eviction order, at the
+                     // node's CSR offset (k_preempt_nodes; a node's victims are among its pods)
+  long long* stop2;  // [n_sblocks][MAXH][2]: per stats workgroup and node-valued hard owner, its
+                     // smallest (count << 24 | node) and the next smallest count
   PreemptOut* out;
   PreGlobal* G;
   long long* gbins;  // [bins_cap] the PreFilter histograms and presence bins
@@ -256,9 +263,10 @@ struct DryResult {
   int64_t hp, sum, cnt, start;  // hp = INT64_MAX: not a candidate
 };
 
-// SelectVictimsOnNode for node n; emit: write the victims' ids (the nominated node)
+// SelectVictimsOnNode for node n; ids (optional): the victims' ids in eviction order
 __device__ __forceinline__ DryResult select_victims(const PreemptJob& J, const kss_pod& p, const Plan& pl,
-                                                    const PreHdr& H, const long long* bins, int n, bool emit) {
+                                                    const PreHdr& H, const long long* bins, int n, int64_t* ids,
+                                                    int ids_cap) {
   const DevCluster& c = J.c;
   const DevPods& P = J.P;
   const DevBound& B = J.B;
@@ -317,7 +325,7 @@ __device__ __forceinline__ DryResult select_victims(const PreemptJob& J, const k
         hp = B.prio[best];
         st = B.start[best];  // the earliest start among the highest-priority victims
       }
-      if (emit && victims < J.victims_cap) J.victims[victims] = B.id[best];
+      if (ids && victims < ids_cap) ids[victims] = B.id[best];
       sum += (int64_t)B.prio[best] + 2147483648ll;
       victims++;
     }
@@ -338,10 +346,10 @@ __device__ __forceinline__ bool resolvable(int f, int detail) {
 }
 
 // ---------------------------------------------------------------------------
-// Three launches on one stream: k_preempt_stats (one workgroup: PreFilter state into
-// HBM), k_preempt_nodes (one lane per node over the whole grid: filters, potential
-// nodes, SelectVictimsOnNode, candidate keys), k_preempt_pick (one workgroup:
-// pickOneNodeForPreemption and the nominated node's victims).
+// Three launches on one stream: k_preempt_stats (node ranges over a few workgroups:
+// PreFilter state into HBM), k_preempt_nodes (one lane per node over the whole grid:
+// filters, potential nodes, SelectVictimsOnNode, each workgroup's best candidate),
+// k_preempt_pick (one workgroup: pickOneNodeForPreemption, the nominated node's victims).
 // ---------------------------------------------------------------------------
 
 // pod record -> LDS and the plan (lane 0); false when the pod has no dry run to do
@@ -355,6 +363,12 @@ __device__ __forceinline__ void pre_load_pod(const PreemptJob& J, PreHdr& H) {
   __syncthreads();
 }
 
+// k_preempt_stats over n_sblocks workgroups, each a contiguous node range: the PreFilter
+// histograms in LDS, added into the zeroed HBM bins (presence bins as counts: only non-zero
+// matters), flags / affinity total by atomics, and per node-valued hard owner the range's two
+// smallest counts.  The last workgroup to finish (a ticket after a release fence) reads the
+// final bins and writes criticalPaths per hard owner: its smallest pair count, that pair, the next.
+// Only the Filter's state is built (no ScheduleAnyway or InterPodAffinity score bins).
 __device__ void preempt_stats(const PreemptJob& J, long long* smem) {
   const int tid = threadIdx.x, nt = blockDim.x;
   PreHdr& H = *reinterpret_cast<PreHdr*>(smem);
@@ -364,25 +378,27 @@ __device__ void preempt_stats(const PreemptJob& J, long long* smem) {
   const kss_pod& p = H.pod;
   const Plan& pl = H.plan;
   PreGlobal& G = *J.G;
-  if (tid == 0) {
+  const int B = (int)blockIdx.x, NB = (int)gridDim.x;
+  if (B == 0 && tid == 0) {
     G.plan_ok = H.plan_ok;
     G.prefilter = p.prefilter_status;
-    G.n_potential = G.n_candidates = G.feasible = 0;
   }
-  if (!H.plan_ok || p.prefilter_status != 0) return;
+  if (!H.plan_ok || p.prefilter_status != 0) return;  // every workgroup leaves: no criticalPaths to build
   long long* bins = pre_bins(smem);
   long long* pres = bins + pl.total_bins;
   const int N = c.N;
+  const int per = (N + NB - 1) / NB, lo = min(N, B * per), hi = min(N, lo + per);
   long long hard_min[MAXH];
 #pragma unroll
   for (int i = 0; i < MAXH; i++) hard_min[i] = INT32_MAX;
   long long flags = 0, aff = 0;
-  for (int b = tid; b < pl.total_bins + pl.total_pbins; b += nt) bins[b] = 0;
+  const int nbins = pl.total_bins + pl.total_pbins;
+  for (int b = tid; b < nbins; b += nt) bins[b] = 0;
   __syncthreads();
   const kss_ipa* ip = P.ipa + p.ipa_off;
   if (pl.need_stats) {
-    for (int n = tid; n < N; n += nt) {
-      stats_node(c, P, p, pl, bins, pres, n, hard_min, flags);
+    for (int n = lo + tid; n < hi; n += nt) {
+      stats_node(c, P, p, pl, bins, pres, n, hard_min, flags, /*scoring=*/false);
       for (int q = 0; q < p.ipa_len; q++)
         if (ip[q].kind == KSS_IPA_REQ_AFFINITY && label_of(c, ip[q].key, n) >= 0)
           aff += sum_rows(c.class_count, (size_t)N, P.ints + ip[q].row_off, ip[q].row_len, n);
@@ -390,39 +406,90 @@ __device__ void preempt_stats(const PreemptJob& J, long long* smem) {
   }
   flags = block_op(flags, OP_OR, H.red);
   aff = block_op(aff, OP_SUM, H.red);
-  // criticalPaths per hard owner: (count << 24 | pair) minimum, then the minimum of the others
-  const kss_spread* sp = P.spreads + p.spread_off;
+  // this range's histograms into the cluster's
+  for (int b = tid; b < nbins; b += nt) {
+    const long long v = bins[b];
+    if (v) atomicAdd((unsigned long long*)&J.gbins[b], (unsigned long long)v);
+  }
+  if (tid == 0) {
+    if (flags) atomicOr((unsigned long long*)&G.flags, (unsigned long long)flags);
+    if (aff) atomicAdd((unsigned long long*)&G.aff_total, (unsigned long long)aff);
+  }
+  // node-valued hard owners: the range's smallest (count << 24 | node) and the next smallest count
   for (int i = 0; i < p.n_hard; i++) {
-    if (pl.hard_own[i] != i) continue;
-    const bool hist = pl.hard_off[i] >= 0;
-    const int span = hist ? c.key_card[sp[i].key] + 1 : N;
+    if (pl.hard_own[i] != i || pl.hard_off[i] >= 0) continue;
     long long best = INT64_MAX;
-    for (int x = tid; x < span; x += nt) {
-      const long long v = hist ? (pres[pl.hard_poff[i] + x] ? bins[pl.hard_off[i] + x] : -1)
-                               : (long long)group_count(c, P, p, pl, i, x);
+    for (int x = lo + tid; x < hi; x += nt) {
+      const long long v = (long long)group_count(c, P, p, pl, i, x);
       if (v >= 0) best = min(best, (v << 24) | x);
     }
     best = block_op(best, OP_MIN, H.red);
     const long long id0 = best == INT64_MAX ? -1 : (best & 0xFFFFFF);
     long long second = INT64_MAX;
-    for (int x = tid; x < span; x += nt) {
+    for (int x = lo + tid; x < hi; x += nt) {
       if (x == id0) continue;
-      const long long v = hist ? (pres[pl.hard_poff[i] + x] ? bins[pl.hard_off[i] + x] : -1)
-                               : (long long)group_count(c, P, p, pl, i, x);
+      const long long v = (long long)group_count(c, P, p, pl, i, x);
       if (v >= 0) second = min(second, v);
     }
     second = block_op(second, OP_MIN, H.red);
     if (tid == 0) {
+      J.stop2[((size_t)B * MAXH + i) * 2] = best;
+      J.stop2[((size_t)B * MAXH + i) * 2 + 1] = second;
+    }
+  }
+  // the last workgroup (ticket after a release) builds the criticalPaths from the final state
+  __threadfence();
+  __syncthreads();
+  if (tid == 0) H.plan_ok = (int)(atomicAdd(&G.ticket, 1u) == (unsigned)(NB - 1)) + 1;  // 2: last
+  __syncthreads();
+  if (H.plan_ok != 2) return;
+  __threadfence();
+  const kss_spread* sp = P.spreads + p.spread_off;
+  for (int i = 0; i < p.n_hard; i++) {
+    if (pl.hard_own[i] != i) continue;
+    long long best = INT64_MAX, second = INT64_MAX;
+    if (pl.hard_off[i] >= 0) {  // histogram key: the smallest present pair and the next
+      const int span = c.key_card[sp[i].key] + 1;
+      auto val = [&](int x) -> long long {
+        const long long pr = __hip_atomic_load(&J.gbins[pl.total_bins + pl.hard_poff[i] + x], __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT);
+        return pr ? __hip_atomic_load(&J.gbins[pl.hard_off[i] + x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : -1;
+      };
+      for (int x = tid; x < span; x += nt) {
+        const long long v = val(x);
+        if (v >= 0) best = min(best, (v << 24) | x);
+      }
+      best = block_op(best, OP_MIN, H.red);
+      const long long id0 = best == INT64_MAX ? -1 : (best & 0xFFFFFF);
+      for (int x = tid; x < span; x += nt) {
+        if (x == id0) continue;
+        const long long v = val(x);
+        if (v >= 0) second = min(second, v);
+      }
+      second = block_op(second, OP_MIN, H.red);
+    } else {  // node-valued key: merge the workgroups' two smallest
+      long long b = INT64_MAX;
+      int owner = -1;
+      for (int q = 0; q < NB; q++) {
+        const long long v = __hip_atomic_load(&J.stop2[((size_t)q * MAXH + i) * 2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (v < b) b = v, owner = q;
+      }
+      best = b;
+      for (int q = 0; q < NB; q++) {
+        const long long v = q == owner ? __hip_atomic_load(&J.stop2[((size_t)q * MAXH + i) * 2 + 1], __ATOMIC_RELAXED,
+                                                           __HIP_MEMORY_SCOPE_AGENT)
+                                       : __hip_atomic_load(&J.stop2[((size_t)q * MAXH + i) * 2], __ATOMIC_RELAXED,
+                                                           __HIP_MEMORY_SCOPE_AGENT);
+        const long long cnt = (q == owner || v == INT64_MAX) ? v : (v >> 24);
+        second = min(second, cnt);
+      }
+    }
+    if (tid == 0) {
       G.m0[i] = best == INT64_MAX ? INT32_MAX : (best >> 24);
-      G.id0[i] = id0;
+      G.id0[i] = best == INT64_MAX ? -1 : (best & 0xFFFFFF);
       G.m1[i] = second == INT64_MAX ? INT32_MAX : second;
     }
   }
-  if (tid == 0) {
-    G.aff_total = aff;
-    G.flags = flags;
-  }
-  for (int b = tid; b < pl.total_bins + pl.total_pbins; b += nt) J.gbins[b] = bins[b];
 }
 
 __device__ void preempt_nodes(const PreemptJob& J, long long* smem) {
@@ -479,7 +546,7 @@ __device__ void preempt_nodes(const PreemptJob& J, long long* smem) {
         feasible = 1;
       } else if (resolvable(f, detail)) {
         n_pot = 1;
-        const DryResult d = select_victims(J, p, pl, H, bins, n, false);
+        const DryResult d = select_victims(J, p, pl, H, bins, n, J.vscratch + J.B.ptr[n], INT32_MAX);
         if (d.hp != INT64_MAX) {
           n_cand = 1;
           best = d;
@@ -576,17 +643,19 @@ __device__ void preempt_pick(const PreemptJob& J, long long* smem) {
   const long long bst = block_op(eq ? st : INT64_MIN, OP_MAX, H.red);
   eq &= st == bst;
   const long long best = block_op(eq ? nn : INT64_MAX, OP_MIN, H.red);
-  // the nominated node's victims, by lane 0
+  // the nominated node's victims, kept by its dry run in k_preempt_nodes
+  const int nv = (int)bcnt;
+  const int64_t* vs = J.vscratch + J.B.ptr[best];
+  for (int i = tid; i < min(nv, J.victims_cap); i += nt) J.victims[i] = vs[i];
   if (tid == 0) {
-    const DryResult d = select_victims(J, H.pod, H.plan, H, J.gbins, (int)best, true);
     out.status = KSS_PREEMPT_NOMINATED;
     out.nominated = (int32_t)(c.node_base + best);
     out.n_potential = G.n_potential;
     out.n_candidates = G.n_candidates;
-    out.n_victims = (int32_t)d.cnt;
-    out.highest_priority = (int32_t)d.hp;
-    out.sum_priority = d.sum;
-    out.earliest_start = d.start;
+    out.n_victims = nv;
+    out.highest_priority = (int32_t)bhp;
+    out.sum_priority = bsum;
+    out.earliest_start = bst;
   }
 }
 

@@ -386,7 +386,7 @@ __device__ __forceinline__ int64_t spread_count(const DevCluster& c, const DevPo
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ void stats_node(const DevCluster& c, const DevPods& P, const kss_pod& p, const Plan& pl,
                                            long long* bins, long long* pres, int n, long long (&hard_min)[MAXH],
-                                           long long& flags) {
+                                           long long& flags, bool scoring = true) {
   const kss_spread* sp = P.spreads + p.spread_off;
   if (p.n_hard > 0 && has_keys(c, sp, p.n_hard, n)) {  // nodeLabelsMatchSpreadConstraints
     for (int i = 0; i < p.n_hard; i++) {
@@ -404,7 +404,7 @@ __device__ __forceinline__ void stats_node(const DevCluster& c, const DevPods& P
       }
     }
   }
-  if (p.n_soft > 0) {
+  if (scoring && p.n_soft > 0) {  // ScheduleAnyway: PreScore state (a filter-only caller skips it)
     const kss_spread* so = sp + p.n_hard;
     const bool req_all = (p.flags & KSS_POD_PTS_REQUIRE_ALL) != 0;
     if (!req_all || has_keys(c, so, p.n_soft, n)) {
@@ -430,7 +430,7 @@ __device__ __forceinline__ void stats_node(const DevCluster& c, const DevPods& P
       const int base = pl.key_off[k];
       const int nb = pl.key_bins[k];
       if (en.kind == KSS_IPA_SCORE_CLASS || en.kind == KSS_IPA_SCORE_TERM) {
-        if (!has_labels) continue;
+        if (!scoring || !has_labels) continue;
         const int32_t* mat = en.kind == KSS_IPA_SCORE_CLASS ? c.class_count : c.term_count;
         const int64_t v = sum_rows(mat, N, P.ints + en.row_off, en.row_len, n);
         if (v > 0) flags |= 8;

@@ -47,6 +47,13 @@ def main():
         bad += any(nd)
         first = [int(d[0]) if len(d) else -1 for d in diffs]
         print(f"{mode} rep {r}: mismatches per part {nd} first pod {first} ({time.perf_counter() - t0:.2f} s)", flush=True)
+        if any(nd) and bad == 1:  # the first bad run: what the device returned
+            ctxs = sp.ctxs if mode == "split" else [ctx]
+            for p, (ch, cx) in enumerate(zip(outs, ctxs)):
+                j = first[p] if first[p] >= 0 else 0
+                print(f"  part {p}: chosen[:8] {np.asarray(ch)[:8].tolist()} oracle {ch_o[:8].tolist()}; "
+                      f"meta[{j}] {cx.fetch_meta(n_pods)[j].tolist()} kernel {cx.last_kernel()} timing {cx.last_timing()}",
+                      flush=True)
     print(f"{mode}: {bad} of {reps} runs differ from the oracle", flush=True)
 
 
