@@ -615,20 +615,25 @@ def run_per_pod(args):
     ctx.reset()
     ctx.stage(s.pods)
     sview = abi.PodView()
+    cview = abi.PodCView()
 
-    def svc_loop(fields):
+    def svc_loop(fields, compact=False):
         t_eval, t_commit, ch = [], [], []
+        ev_fn = native.lib().kss_service_eval_compact if compact else native.lib().kss_service_eval
+        vp = ctypes.byref(cview if compact else sview)
+        v = cview if compact else sview
         t0 = time.perf_counter()
         for j in range(n_pods):
             a = time.perf_counter()
-            native.check(native.lib().kss_service_eval(ctx.h, j, fields, ctypes.byref(sview)))
+            native.check(ev_fn(ctx.h, j, fields, vp))
             b = time.perf_counter()
-            if sview.chosen >= 0:
-                native.check(native.lib().kss_service_commit(ctx.h, j, sview.chosen))
+            if v.chosen >= 0:
+                native.check(native.lib().kss_service_commit(ctx.h, j, v.chosen))
             c = time.perf_counter()
             t_eval.append(b - a)
             t_commit.append(c - b)
-            ch.append(sview.chosen)
+            ch.append(v.chosen)
+            assert not compact or not cview.is_wide
         el = time.perf_counter() - t0
         ctx.service_stop()
         return el, np.array(t_eval) * 1e6, np.array(t_commit) * 1e6, ch
@@ -656,6 +661,9 @@ def run_per_pod(args):
     slim_fields = abi.KSS_FIELD_FAIL | abi.KSS_FIELD_DETAIL | abi.KSS_FIELD_TOTAL
     elapsed_svc_slim, ev_svc_slim, _, chosen_svc_slim = svc_loop(slim_fields)
     assert chosen_svc_slim == chosen
+    ctx.reset()
+    elapsed_svc_c, ev_svc_c, _, chosen_svc_c = svc_loop(abi.KSS_FIELD_ALL, compact=True)
+    assert chosen_svc_c == chosen
     out = {
         "metric": "per-pod API: kss_eval_pod + kss_commit latency (pods/sec in value)",
         "value": n_pods / elapsed,
@@ -689,6 +697,10 @@ def run_per_pod(args):
                     "slim": {"pods_per_s": n_pods / elapsed_svc_slim, "fields": "fail_plugin, fail_detail, total",
                              "eval_us": {"median": float(np.median(ev_svc_slim)), "mean": float(ev_svc_slim.mean()),
                                          "p90": float(np.percentile(ev_svc_slim, 90))}},
+                    "compact": {"pods_per_s": n_pods / elapsed_svc_c,
+                                "api": "kss_service_eval_compact (every field; raw / total int32, norm uint8)",
+                                "eval_us": {"median": float(np.median(ev_svc_c)), "mean": float(ev_svc_c.mean()),
+                                            "p90": float(np.percentile(ev_svc_c, 90))}},
                     "shard0_phases_us_median": {"relay": float(ph[0]), "pod": float(ph[1]),
                                                 "record_copy_and_fence": float(ph[2])},
                     "geometry": ctx.last_geometry()},

@@ -493,6 +493,27 @@ int kss_eval_pod_view(kss_ctx* ctx, const kss_podset* ps, int32_t pod_index, uin
 int kss_service_start(kss_ctx* ctx);
 int kss_service_stop(kss_ctx* ctx);
 int kss_service_eval(kss_ctx* ctx, int32_t pod_index, uint32_t fields, kss_pod_view* out);
+/* kss_service_eval with the score rows narrowed on the device before they cross the host link
+ * (47 instead of 139 bytes per node): raw and total as int32, normalised scores (0..100) as
+ * uint8.  When some value of the pod does not fit (is_wide = 1) the pod is evaluated again
+ * into the full record and `wide` holds the kss_service_eval view instead (the narrow
+ * pointers are NULL).  Same validity as kss_service_eval. */
+typedef struct kss_pod_cview {
+  const uint8_t* fail_plugin;  /* [n] */
+  const uint16_t* fail_detail; /* [n] */
+  const int32_t* raw;          /* [KSS_NSCORE][n] */
+  const uint8_t* norm;         /* [KSS_NSCORE][n] */
+  const int32_t* total;        /* [n] */
+  int32_t n_feasible;
+  int32_t chosen;
+  int64_t best_total;
+  int32_t scored;
+  int32_t status;
+  int32_t is_wide;
+  int32_t pad;
+  kss_pod_view wide;
+} kss_pod_cview;
+int kss_service_eval_compact(kss_ctx* ctx, int32_t pod_index, uint32_t fields, kss_pod_cview* out);
 int kss_service_commit(kss_ctx* ctx, int32_t pod_index, int32_t node);
 int kss_service_rollback(kss_ctx* ctx, int32_t pod_index, int32_t node);
 /* Diagnostics (KSS_SERVICE_STAMPS set when the grid starts): shard 0's s_memrealtime (100 MHz)

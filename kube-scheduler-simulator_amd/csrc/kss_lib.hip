@@ -30,6 +30,7 @@
 #include <cstdio>
 #include <cstring>
 #include <mutex>
+#include <atomic>
 #include <string>
 #include <vector>
 
@@ -73,6 +74,21 @@ struct SlotLayout {
     raw = align_up(total + 8 * N, 256);
     norm = raw + 8 * KSS_NSCORE * N;
     bytes = align_up(norm + 8 * KSS_NSCORE * N, 256);
+  }
+};
+
+// The service grid's compact host record (kss_service_eval_compact): a slot's rows with the
+// scores narrowed, raw and total to int32 and normalised scores (0..MaxNodeScore) to uint8:
+// 47 instead of 139 bytes per node over the host link.  Fields start 256-byte aligned.
+struct CompactLayout {
+  size_t fail, detail, total, raw, norm, bytes;
+  __host__ __device__ explicit CompactLayout(size_t N) {
+    fail = 0;
+    detail = align_up(N, 256);
+    total = align_up(detail + 2 * N, 256);
+    raw = align_up(total + 4 * N, 256);
+    norm = align_up(raw + 4 * KSS_NSCORE * N, 256);
+    bytes = align_up(norm + KSS_NSCORE * N, 256);
   }
 };
 
@@ -369,10 +385,21 @@ struct DevBuf {
     size_t nb = std::max(bytes, (size_t)4096);
     if (hipMalloc(&p, nb) != hipSuccess) return fail(KSS_E_NOMEM, "hipMalloc failed");
     cap = nb;
-    // diagnostic (KSS_POISON): fresh buffers hold a byte pattern, not the zeros a new process
-    // tends to get, so a read of never-written memory shows up in a short run
-    static const bool poison = getenv("KSS_POISON") != nullptr;
-    if (poison && hipMemset(p, 0xA5, nb) != hipSuccess) return fail(KSS_E_NOMEM, "poison memset failed");
+    // diagnostic (KSS_POISON=all, or =i: only the i-th allocation of the process): fresh
+    // buffers hold a byte pattern, not the zeros a new process tends to get, so a read of
+    // never-written memory shows up in a short run
+    static const char* poison = getenv("KSS_POISON");
+    static std::atomic<int> n_alloc{0};
+    if (poison) {
+      const int i = n_alloc++;
+      const bool all = std::strcmp(poison, "all") == 0;
+      if (all || atoi(poison) == i) {
+        fprintf(stderr, "kss poison: allocation %d, %zu bytes\n", i, nb);
+        // complete before the caller's own stream touches the buffer (null-stream memset)
+        if (hipMemset(p, 0xA5, nb) != hipSuccess || hipDeviceSynchronize() != hipSuccess)
+          return fail(KSS_E_NOMEM, "poison memset failed");
+      }
+    }
     return 0;
   }
   void release() {
@@ -1302,7 +1329,8 @@ int kss_abi_sizes(int32_t* out, int32_t n) {
                        (int32_t)sizeof(kss_spread),  (int32_t)sizeof(kss_ipa),     (int32_t)sizeof(kss_pod),
                        (int32_t)sizeof(kss_podset),  (int32_t)sizeof(kss_profile), (int32_t)sizeof(kss_pod_result),
                        (int32_t)sizeof(kss_config),  (int32_t)sizeof(kss_names),   (int32_t)sizeof(kss_synth),
-                       (int32_t)sizeof(kss_boundset), (int32_t)sizeof(kss_preempt_result), (int32_t)sizeof(kss_vol)};
+                       (int32_t)sizeof(kss_boundset), (int32_t)sizeof(kss_preempt_result), (int32_t)sizeof(kss_vol),
+                       (int32_t)sizeof(kss_pod_view), (int32_t)sizeof(kss_pod_cview)};
   const int32_t k = (int32_t)(sizeof(s) / sizeof(s[0]));
   for (int i = 0; i < n && i < k; i++) out[i] = s[i];
   return k;
@@ -3022,13 +3050,14 @@ static int svc_start_locked(kss_ctx* ctx) {
     HIP_TRY(hipHostGetDevicePointer((void**)&v.box_dev, v.box, 0));
     v.posted = 0;
   }
-  if (v.rec_bytes < SL.bytes) {
+  const size_t rec_bytes = SL.bytes + CompactLayout(N).bytes;  // the full record, then the compact one
+  if (v.rec_bytes < rec_bytes) {
     if (v.rec) HIP_TRY(hipHostFree(v.rec));
     v.rec = nullptr;
     v.rec_bytes = 0;
-    HIP_TRY(hipHostMalloc((void**)&v.rec, SL.bytes, hipHostMallocCoherent | hipHostMallocMapped));
+    HIP_TRY(hipHostMalloc((void**)&v.rec, rec_bytes, hipHostMallocCoherent | hipHostMallocMapped));
     HIP_TRY(hipHostGetDevicePointer((void**)&v.rec_dev, v.rec, 0));
-    v.rec_bytes = SL.bytes;
+    v.rec_bytes = rec_bytes;
   }
   int rc = ctx->slot_buf.ensure(2 * SL.bytes);  // two record slots used in turn (kss_service.cuh)
   if (!rc) rc = v.relay.ensure(sizeof(unsigned long long) * (2 * SVC_DRING + (size_t)W));
@@ -3112,21 +3141,20 @@ int kss_service_stop(kss_ctx* ctx) {
   return svc_stop(ctx);
 }
 
-int kss_service_eval(kss_ctx* ctx, int32_t pod_index, uint32_t fields, kss_pod_view* out) {
-  if (!ctx || !ctx->loaded || !out) return fail(KSS_E_INVAL, "bad arguments");
-  if (pod_index < 0 || pod_index >= ctx->staged_n || pod_index >= (1 << 24)) return fail(KSS_E_INVAL, "pod index outside the staged pods");
-  std::lock_guard<std::mutex> lk(ctx->mu);
+// One EVAL command on the service grid and the wait for every shard's done flag (restarting
+// a grid that left idle before taking the command).  ovf: some shard's compact record value
+// did not fit its narrow type.
+static int svc_eval_wait(kss_ctx* ctx, int32_t pod_index, uint32_t fields, bool compact, bool& ovf) {
   auto& v = ctx->svc;
   if (!v.running) {
     if (int rc = svc_start_locked(ctx)) return rc;
   }
   unsigned long long seq = 0;
-  if (int rc = svc_post(ctx, SVC_EVAL, pod_index, 0, (int)(fields & KSS_FIELD_ALL), &seq)) return rc;
-  // wait for every shard's done flag; restart a grid that left idle before taking the command
+  if (int rc = svc_post(ctx, SVC_EVAL, pod_index, compact ? 1 : 0, (int)(fields & KSS_FIELD_ALL), &seq)) return rc;
   const auto t0 = std::chrono::steady_clock::now();
   for (unsigned spins = 0;; ++spins) {
     bool all = true;
-    for (int w = 0; w < v.W && all; w++) all = __atomic_load_n(&v.box->done[w], __ATOMIC_ACQUIRE) > seq;
+    for (int w = 0; w < v.W && all; w++) all = (__atomic_load_n(&v.box->done[w], __ATOMIC_ACQUIRE) & ~SVC_DONE_OVF) > seq;
     if (all) break;
     if ((spins & 1023) == 1023) {
       if (v.box->err) {
@@ -3149,16 +3177,59 @@ int kss_service_eval(kss_ctx* ctx, int32_t pod_index, uint32_t fields, kss_pod_v
       }
     }
   }
-  const PodMeta m = v.box->meta;
-  if (m.status == 4) return fail(KSS_E_UNSUPPORTED, "pod program exceeds the device path's per-pod limits");
-  const size_t N = (size_t)ctx->dc.N;
-  const SlotLayout SL(N);
-  const uint8_t* r = v.rec;
+  ovf = false;
+  for (int w = 0; w < v.W; w++) ovf |= (__atomic_load_n(&v.box->done[w], __ATOMIC_ACQUIRE) & SVC_DONE_OVF) != 0;
+  if (v.box->meta.status == 4) return fail(KSS_E_UNSUPPORTED, "pod program exceeds the device path's per-pod limits");
+  return 0;
+}
+
+static void svc_full_view(kss_ctx* ctx, uint32_t fields, kss_pod_view* out) {
+  const PodMeta m = ctx->svc.box->meta;
+  const SlotLayout SL((size_t)ctx->dc.N);
+  const uint8_t* r = ctx->svc.rec;
   out->fail_plugin = (fields & KSS_FIELD_FAIL) ? r + SL.fail : nullptr;
   out->fail_detail = (fields & KSS_FIELD_DETAIL) ? (const uint16_t*)(r + SL.detail) : nullptr;
   out->raw = (fields & KSS_FIELD_RAW) ? (const int64_t*)(r + SL.raw) : nullptr;
   out->norm = (fields & KSS_FIELD_NORM) ? (const int64_t*)(r + SL.norm) : nullptr;
   out->total = (fields & KSS_FIELD_TOTAL) ? (const int64_t*)(r + SL.total) : nullptr;
+  out->chosen = m.chosen;
+  out->n_feasible = m.n_feasible;
+  out->best_total = m.best_total;
+  out->scored = m.scored;
+  out->status = m.status;
+}
+
+int kss_service_eval(kss_ctx* ctx, int32_t pod_index, uint32_t fields, kss_pod_view* out) {
+  if (!ctx || !ctx->loaded || !out) return fail(KSS_E_INVAL, "bad arguments");
+  if (pod_index < 0 || pod_index >= ctx->staged_n || pod_index >= (1 << 24)) return fail(KSS_E_INVAL, "pod index outside the staged pods");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  bool ovf = false;
+  if (int rc = svc_eval_wait(ctx, pod_index, fields, false, ovf)) return rc;
+  svc_full_view(ctx, fields, out);
+  return 0;
+}
+
+int kss_service_eval_compact(kss_ctx* ctx, int32_t pod_index, uint32_t fields, kss_pod_cview* out) {
+  if (!ctx || !ctx->loaded || !out) return fail(KSS_E_INVAL, "bad arguments");
+  if (pod_index < 0 || pod_index >= ctx->staged_n || pod_index >= (1 << 24)) return fail(KSS_E_INVAL, "pod index outside the staged pods");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  bool ovf = false;
+  if (int rc = svc_eval_wait(ctx, pod_index, fields, true, ovf)) return rc;
+  *out = kss_pod_cview{};
+  if (ovf) {  // a score outside int32 / a normalised score above 255: the same pod, full record
+    if (int rc = svc_eval_wait(ctx, pod_index, fields, false, ovf)) return rc;
+    out->is_wide = 1;
+    svc_full_view(ctx, fields, &out->wide);
+  } else {
+    const CompactLayout CL((size_t)ctx->dc.N);
+    const uint8_t* r = ctx->svc.rec + SlotLayout((size_t)ctx->dc.N).bytes;
+    out->fail_plugin = (fields & KSS_FIELD_FAIL) ? r + CL.fail : nullptr;
+    out->fail_detail = (fields & KSS_FIELD_DETAIL) ? (const uint16_t*)(r + CL.detail) : nullptr;
+    out->raw = (fields & KSS_FIELD_RAW) ? (const int32_t*)(r + CL.raw) : nullptr;
+    out->norm = (fields & KSS_FIELD_NORM) ? r + CL.norm : nullptr;
+    out->total = (fields & KSS_FIELD_TOTAL) ? (const int32_t*)(r + CL.total) : nullptr;
+  }
+  const PodMeta m = ctx->svc.box->meta;
   out->chosen = m.chosen;
   out->n_feasible = m.n_feasible;
   out->best_total = m.best_total;
@@ -3774,6 +3845,15 @@ int kss_postfilter_pod(kss_ctx* ctx, const kss_podset* ps, int32_t pod_index, ks
   J.pi = 0;
   J.bins_cap = bins_cap;
   J.victims_cap = cap;
+  {  // the pod's bin plan, on the host: every kernel copies it instead of rebuilding it on one lane
+    DevCluster hc{};
+    hc.key_card = ctx->key_card_h.data();
+    hc.key_flags = ctx->key_flags_h.data();
+    DevPods hp{};
+    hp.spreads = one.ps.spreads;
+    hp.ipa = one.ps.ipa;
+    J.plan_ok = make_plan(hc, hp, one.ps.pods[0], J.plan, bins_cap) ? 1 : 0;
+  }
   J.key = (int64_t*)(d + o_key);
   J.n_blocks = (int32_t)std::max<size_t>((N + PRE_NODE_THREADS - 1) / PRE_NODE_THREADS, 1);
   J.victims = (int64_t*)(d + o_vic);
@@ -3782,13 +3862,13 @@ int kss_postfilter_pod(kss_ctx* ctx, const kss_podset* ps, int32_t pod_index, ks
   J.gbins = (long long*)(d + o_bins);
   J.stop2 = (long long*)(d + o_top);
   J.vscratch = (int64_t*)(d + o_vs);
-  // stats workgroups: about 512 nodes each (the histograms are added into the zeroed HBM bins)
-  const unsigned nsb = (unsigned)std::min<size_t>(std::max<size_t>((N + 511) / 512, 1), PRE_STATS_MAX_BLOCKS);
+  // stats workgroups: about 256 nodes each (the histograms are added into the zeroed HBM bins)
+  const unsigned nsb = (unsigned)std::min<size_t>(std::max<size_t>((N + 255) / 256, 1), PRE_STATS_MAX_BLOCKS);
   HIP_TRY(hipMemcpyAsync(d + o_job, &J, sizeof(J), hipMemcpyHostToDevice, ctx->stream));
   HIP_TRY(hipEventRecord(ctx->ev0, ctx->stream));
   HIP_TRY(hipMemsetAsync(d + o_g, 0, o_top - o_g, ctx->stream));  // PreGlobal (ticket, sums) and the bins
   const PreemptJob* jd = (const PreemptJob*)(d + o_job);
-  hipLaunchKernelGGL(k_preempt_stats, dim3(nsb), dim3(PRE_THREADS), lds, ctx->stream, jd);
+  hipLaunchKernelGGL(k_preempt_stats, dim3(nsb), dim3(256), lds, ctx->stream, jd);  // a lane per node of the range
   const unsigned nb = (unsigned)((N + PRE_NODE_THREADS - 1) / PRE_NODE_THREADS);
   hipLaunchKernelGGL(k_preempt_nodes, dim3(std::max(nb, 1u)), dim3(PRE_NODE_THREADS), sizeof(PreHdr), ctx->stream, jd);
   hipLaunchKernelGGL(k_preempt_pick, dim3(1), dim3(PRE_THREADS), sizeof(PreHdr), ctx->stream, jd);

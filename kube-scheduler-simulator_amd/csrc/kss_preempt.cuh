@@ -82,6 +82,8 @@ struct PreemptJob {
   int32_t n_blocks;  // k_preempt_nodes workgroups
   int64_t* key;      // [5][n_blocks] HBM scratch: each workgroup's best candidate (hp, sum, cnt, start, node)
   int64_t* victims;  // [victims_cap]
+  Plan plan;         // the pod's bin plan (make_plan on the host)
+  int32_t plan_ok;
   int64_t* vscratch; // [bound pods]: each candidate node's victims in eviction order, at the
                      // node's CSR offset (k_preempt_nodes; a node's victims are among its pods)
   long long* stop2;  // [n_sblocks][MAXH][2]: per stats workgroup and node-valued hard owner, its
@@ -275,8 +277,9 @@ __device__ __forceinline__ DryResult select_victims(const PreemptJob& J, const k
   const int prio = p.priority;
   // the potential victims (priority below the preemptor's) are the suffix [p0, e1) of the
   // node's importance order, visited in reprieve order
-  int p0 = e1;
-  while (p0 > e0 && B.prio[p0 - 1] < prio) p0--;
+  int below = 0;  // independent loads (a scan from the end would wait on each one in turn)
+  for (int k = e0; k < e1; k++) below += B.prio[k] < prio ? 1 : 0;
+  const int p0 = e1 - below;
   if (p0 == e1) return res;  // "No preemption victims found for incoming pod"
   // the node's view, then every lower-priority pod removed
   DryState s;
@@ -352,14 +355,18 @@ __device__ __forceinline__ bool resolvable(int f, int detail) {
 // k_preempt_pick (one workgroup: pickOneNodeForPreemption, the nominated node's victims).
 // ---------------------------------------------------------------------------
 
-// pod record -> LDS and the plan (lane 0); false when the pod has no dry run to do
+// pod record and its plan (built on the host, in the job) -> LDS, word-parallel
 __device__ __forceinline__ void pre_load_pod(const PreemptJob& J, PreHdr& H) {
   const int tid = threadIdx.x, nt = blockDim.x;
-  constexpr int PD = (int)(sizeof(kss_pod) / 4);
+  constexpr int PD = (int)(sizeof(kss_pod) / 4), PL = (int)(sizeof(Plan) / 4);
+  static_assert(sizeof(kss_pod) % 4 == 0 && sizeof(Plan) % 4 == 0, "word copies");
   const uint32_t* src = reinterpret_cast<const uint32_t*>(J.P.pods + J.pi);
   uint32_t* dst = reinterpret_cast<uint32_t*>(&H.pod);
   for (int i = tid; i < PD; i += nt) dst[i] = src[i];
-  if (tid == 0) H.plan_ok = make_plan(J.c, J.P, J.P.pods[J.pi], H.plan, J.bins_cap) ? 1 : 0;
+  const uint32_t* ps = reinterpret_cast<const uint32_t*>(&J.plan);
+  uint32_t* pd = reinterpret_cast<uint32_t*>(&H.plan);
+  for (int i = tid; i < PL; i += nt) pd[i] = ps[i];
+  if (tid == 0) H.plan_ok = J.plan_ok;
   __syncthreads();
 }
 

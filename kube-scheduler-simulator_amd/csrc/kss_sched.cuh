@@ -82,7 +82,7 @@ struct SharedHdr {
   int plan_ok;
   int abort;
   unsigned svc_dirty;  // the service grid: record rows whose shard segment changed (kss_service.cuh)
-  int pad;
+  unsigned svc_ovf;    // the service grid: a compact record value did not fit its narrow type
   int cmd[4];   // the service grid's current command (kss_service.cuh)
 };
 
@@ -264,12 +264,14 @@ __device__ __forceinline__ bool cluster_reduce(long long* smem, Shard& S, long l
   return true;
 }
 
-__device__ __forceinline__ bool key_unique(const DevCluster& c, int key) {
+__host__ __device__ __forceinline__ bool key_unique(const DevCluster& c, int key) {
   return (c.key_flags[key] & KSS_KEY_UNIQUE) != 0;
 }
 
-// Returns false if the pod needs more LDS bins / slots than the device path has.
-__device__ __forceinline__ bool make_plan(const DevCluster& c, const DevPods& P, const kss_pod& p, Plan& pl,
+// Returns false if the pod needs more LDS bins / slots than the device path has.  Host and
+// device: the PostFilter dry run builds it on the host (key tables and the pod's programs in
+// host memory) and ships it with the job.
+__host__ __device__ __forceinline__ bool make_plan(const DevCluster& c, const DevPods& P, const kss_pod& p, Plan& pl,
                                           int bins_cap) {
   pl.n_hard = p.n_hard;
   pl.n_soft = p.n_soft;

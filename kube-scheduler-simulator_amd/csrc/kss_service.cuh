@@ -13,7 +13,8 @@
 //   every shard: polls the relay slot, runs the command:
 //     EVAL      schedule_pod (kss_sched.cuh) into the HBM record slot, then copies its own
 //               node range of the requested record fields into the pinned host record,
-//               fences at system scope and stores done[w] = k + 1
+//               fences at system scope and stores done[w] = k + 1 (| SVC_DONE_OVF when a
+//               compact record value did not fit)
 //     COMMIT / ROLLBACK   the owning shard applies AssumePod / ForgetPod (commit_pod)
 //     STOP      leave (after writing the LDS node cache back)
 //
@@ -32,6 +33,7 @@ constexpr int SVC_RING = 1024;                                 // host command r
 constexpr int SVC_DRING = 64;                                  // device relay ring (entries)
 constexpr int SVC_MAX_SHARDS = 256;
 constexpr unsigned long long SVC_IDLE_TICKS = 100000000ull;    // 1 s of s_memrealtime (100 MHz)
+constexpr unsigned long long SVC_DONE_OVF = 1ull << 62;         // done word: a compact value overflowed
 enum { SVC_NONE = 0, SVC_EVAL = 1, SVC_COMMIT = 2, SVC_ROLLBACK = 3, SVC_STOP = 4 };
 
 // A command as two tagged words: w0 = (k+1) << 32 | pod << 8 | fields << 3 | op,
@@ -64,42 +66,6 @@ __device__ __forceinline__ void st_sys(KSS_GLOBAL unsigned long long* p, unsigne
   __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-// Copy elements [lo, hi) of `rows` rows of ES-byte elements (row stride N) from the HBM
-// record to the pinned host record (same layout).  Every row segment goes as 16-byte stores
-// over its aligned interior (each narrower store to host memory is one fabric write of its own:
-// MI355X_MICROARCH.md, 8-byte ones cost 2.7x and 2-byte ones 12.5x a 16-byte store per byte),
-// and element stores for the at most 15 bytes at either end.  Both buffers are 16-byte
-// aligned row blocks of the same layout (SlotLayout).
-template <int ES>
-__device__ __forceinline__ void svc_copy(const uint8_t* src, uint8_t* dst, size_t N, int r0, int rows, int lo, int hi) {
-  using T = typename std::conditional<ES == 8, uint64_t, typename std::conditional<ES == 2, uint16_t, uint8_t>::type>::type;
-  constexpr int V = 16 / ES;  // elements per 16-byte store
-  const int tid = (int)threadIdx.x, nt = (int)blockDim.x;
-  for (int r = r0; r < r0 + rows; r++) {
-    const size_t base = (size_t)r * N;  // element offset of the row from the field's (16-byte aligned) start
-    // elements [a, b) of the row start 16-byte aligned chunks: base + a is a multiple of V
-    const size_t a0 = base + (size_t)lo, b0 = base + (size_t)hi;
-    const size_t a = (a0 + V - 1) / V * V, b = b0 / V * V;
-    KSS_GLOBAL const T* s = gp(reinterpret_cast<const T*>(src));
-    KSS_GLOBAL T* d = gp(reinterpret_cast<T*>(dst));
-    if (a < b) {
-      KSS_GLOBAL const uint4* s4 = gp(reinterpret_cast<const uint4*>(src)) + a / V;
-      KSS_GLOBAL uint4* d4 = gp(reinterpret_cast<uint4*>(dst)) + a / V;
-      for (int i = tid; i < (int)((b - a) / V); i += nt) {
-        const uint4 x = make_uint4(s4[i].x, s4[i].y, s4[i].z, s4[i].w);
-        d4[i].x = x.x;  // member stores of one 16-byte value: the compiler merges them into one dwordx4
-        d4[i].y = x.y;
-        d4[i].z = x.z;
-        d4[i].w = x.w;
-      }
-      for (int i = tid; i < (int)(a - a0); i += nt) d[a0 + i] = s[a0 + i];  // head
-      for (int i = tid; i < (int)(b0 - b); i += nt) d[b + i] = s[b + i];    // tail
-    } else {
-      for (int i = tid; i < (int)(b0 - a0); i += nt) d[a0 + i] = s[a0 + i];
-    }
-  }
-}
-
 // The record as SVC_ROWS rows of one element per node: fail, detail, total, raw[KSS_NSCORE],
 // norm[KSS_NSCORE].
 constexpr int SVC_ROWS = 3 + 2 * KSS_NSCORE;
@@ -122,6 +88,160 @@ __device__ __forceinline__ size_t svc_row_off(const SlotLayout& L, size_t N, int
   int fr = 0;
   const size_t o = svc_field(L, r, fr, es);
   return o + (size_t)es * (size_t)fr * N;
+}
+
+// Row r of the record as one copy job: source (HBM slot, int64 score rows) and destination
+// (pinned host record, full or compact) element sizes, field byte offsets and the row's first
+// element (row r of a field starts at element fr * N).  Destination stores carry V elements:
+// 16 bytes, except the compact uint8 rows (4 bytes: V = 4, so that a store's source is at
+// most 32 bytes — two 16-byte loads — for every row).
+struct SvcRow {
+  size_t so, dof, e0;
+  int es, ed, V;
+};
+template <bool COMPACT>
+__device__ __forceinline__ SvcRow svc_row(const SlotLayout& L, const CompactLayout& CL, size_t N, int r) {
+  int fr = 0, es = 0;
+  SvcRow x;
+  x.so = svc_field(L, r, fr, es);
+  x.es = es;
+  x.e0 = (size_t)fr * N;
+  if (!COMPACT) {
+    x.dof = x.so;
+    x.ed = es;
+  } else {
+    x.dof = r == 0 ? CL.fail : r == 1 ? CL.detail : r == 2 ? CL.total : r < 3 + KSS_NSCORE ? CL.raw : CL.norm;
+    x.ed = r == 0 ? 1 : r == 1 ? 2 : r < 3 + KSS_NSCORE ? 4 : 1;
+  }
+  x.V = (COMPACT && r >= 3 + KSS_NSCORE) ? 4 : 16 / x.ed;
+  return x;
+}
+
+// One element of row x: source value (zero-extended) -> destination (narrowed when compact)
+__device__ __forceinline__ uint64_t svc_ld(const uint8_t* src, const SvcRow& x, size_t e) {
+  KSS_GLOBAL const uint8_t* p = gp(src) + x.so + e * (size_t)x.es;
+  return x.es == 1 ? *p : x.es == 2 ? *reinterpret_cast<KSS_GLOBAL const uint16_t*>(p)
+                                    : *reinterpret_cast<KSS_GLOBAL const uint64_t*>(p);
+}
+__device__ __forceinline__ void svc_st(uint8_t* dst, const SvcRow& x, size_t e, uint64_t v, bool& ovf) {
+  KSS_GLOBAL uint8_t* p = gp(dst) + x.dof + e * (size_t)x.ed;
+  if (x.ed == x.es) {  // same width: a copy
+    if (x.ed == 1) *p = (uint8_t)v;
+    else if (x.ed == 2) *reinterpret_cast<KSS_GLOBAL uint16_t*>(p) = (uint16_t)v;
+    else *reinterpret_cast<KSS_GLOBAL uint64_t*>(p) = v;
+  } else if (x.ed == 4) {
+    const int64_t s = (int64_t)v;
+    ovf |= s < INT32_MIN || s > INT32_MAX;
+    *reinterpret_cast<KSS_GLOBAL int32_t*>(p) = (int32_t)s;
+  } else {
+    const int64_t s = (int64_t)v;
+    ovf |= s < 0 || s > 255;
+    *p = (uint8_t)s;
+  }
+}
+
+// The rows in `send` of this shard's node range [lo, hi): slot -> pinned host record.  The
+// record's HBM loads are the latency here (a few hundred ns to ~1 us each), so every lane
+// first issues its loads for a batch of rows (at most one destination store per row and
+// round), then converts and stores: one load round trip per batch of 10 rows instead of one
+// per row.  Interior stores are 16-byte (4-byte for compact uint8 rows); the unaligned ends
+// of each row segment go element by element.
+template <bool COMPACT>
+__device__ __forceinline__ void svc_send(const uint8_t* slot, uint8_t* host, const SlotLayout& L,
+                                         const CompactLayout& CL, size_t N, unsigned send, int lo, int hi, bool& ovf) {
+  const int tid = (int)threadIdx.x, nt = (int)blockDim.x;
+  constexpr int RB = 10;  // rows per batch (registers: RB x 2 x 16 bytes)
+  // interior chunks of a row: at most (hi - lo) / 2 + 1 (16-byte stores of 8-byte elements)
+  const int rounds = ((hi - lo) / 2 + 1 + nt - 1) / nt;
+  for (int rb = 0; rb < SVC_ROWS; rb += RB) {
+    for (int k = 0; k < rounds; k++) {
+      uint4 v[RB][2];
+      bool have[RB];
+#pragma unroll
+      for (int q = 0; q < RB; q++) {
+        const int r = rb + q;
+        have[q] = false;
+        if (r >= SVC_ROWS || !((send >> r) & 1u)) continue;
+        const SvcRow x = svc_row<COMPACT>(L, CL, N, r);
+        const size_t a0 = x.e0 + (size_t)lo, b0 = x.e0 + (size_t)hi;
+        const size_t a = (a0 + x.V - 1) / x.V * x.V, b = b0 / x.V * x.V;
+        const size_t i = (size_t)(tid + k * nt);
+        if (a >= b || i >= (b - a) / x.V) continue;
+        have[q] = true;
+        KSS_GLOBAL const uint4* s4 = reinterpret_cast<KSS_GLOBAL const uint4*>(gp(slot) + x.so + (a + i * x.V) * x.es);
+        v[q][0] = make_uint4(s4[0].x, s4[0].y, s4[0].z, s4[0].w);
+        if (x.V * x.es > 16) v[q][1] = make_uint4(s4[1].x, s4[1].y, s4[1].z, s4[1].w);
+      }
+#pragma unroll
+      for (int q = 0; q < RB; q++) {
+        if (!have[q]) continue;
+        const int r = rb + q;
+        const SvcRow x = svc_row<COMPACT>(L, CL, N, r);
+        const size_t a0 = x.e0 + (size_t)lo;
+        const size_t a = (a0 + x.V - 1) / x.V * x.V;
+        const size_t i = (size_t)(tid + k * nt);
+        KSS_GLOBAL uint8_t* dp = gp(host) + x.dof + (a + i * x.V) * x.ed;
+        if (x.ed == x.es) {  // a 16-byte copy: member stores, merged into one dwordx4
+          KSS_GLOBAL uint4* d4 = reinterpret_cast<KSS_GLOBAL uint4*>(dp);
+          d4->x = v[q][0].x;
+          d4->y = v[q][0].y;
+          d4->z = v[q][0].z;
+          d4->w = v[q][0].w;
+        } else if (x.ed == 4) {  // 4 int64 -> 4 int32
+          const uint32_t w[8] = {v[q][0].x, v[q][0].y, v[q][0].z, v[q][0].w, v[q][1].x, v[q][1].y, v[q][1].z, v[q][1].w};
+          uint32_t o[4];
+#pragma unroll
+          for (int e = 0; e < 4; e++) {
+            const int64_t sv = (int64_t)(((uint64_t)w[2 * e + 1] << 32) | w[2 * e]);
+            ovf |= sv < INT32_MIN || sv > INT32_MAX;
+            o[e] = (uint32_t)(int32_t)sv;
+          }
+          KSS_GLOBAL uint4* d4 = reinterpret_cast<KSS_GLOBAL uint4*>(dp);
+          d4->x = o[0];
+          d4->y = o[1];
+          d4->z = o[2];
+          d4->w = o[3];
+        } else {  // 4 int64 -> 4 uint8, one 4-byte store
+          const uint32_t w[8] = {v[q][0].x, v[q][0].y, v[q][0].z, v[q][0].w, v[q][1].x, v[q][1].y, v[q][1].z, v[q][1].w};
+          uint32_t o = 0;
+#pragma unroll
+          for (int e = 0; e < 4; e++) {
+            const int64_t sv = (int64_t)(((uint64_t)w[2 * e + 1] << 32) | w[2 * e]);
+            ovf |= sv < 0 || sv > 255;
+            o |= ((uint32_t)sv & 0xFFu) << (8 * e);
+          }
+          *reinterpret_cast<KSS_GLOBAL uint32_t*>(dp) = o;
+        }
+      }
+    }
+  }
+  // the unaligned ends: at most V - 1 elements at each end of each row segment, loads first
+  for (int rb = 0; rb < SVC_ROWS; rb += RB) {
+    for (int k = 0; k < (32 + nt - 1) / nt; k++) {  // a segment has at most 31 such elements
+      uint64_t ev[RB];
+      size_t ee[RB];
+      bool have[RB];
+#pragma unroll
+      for (int q = 0; q < RB; q++) {
+        const int r = rb + q;
+        have[q] = false;
+        if (r >= SVC_ROWS || !((send >> r) & 1u)) continue;
+        const SvcRow x = svc_row<COMPACT>(L, CL, N, r);
+        const size_t a0 = x.e0 + (size_t)lo, b0 = x.e0 + (size_t)hi;
+        size_t a = (a0 + x.V - 1) / x.V * x.V, b = b0 / x.V * x.V;
+        if (a >= b) a = b = b0;  // no interior: the whole segment is a "head"
+        const int nh = (int)(a - a0), ntl = (int)(b0 - b);
+        const int i = tid + k * nt;
+        if (i >= nh + ntl) continue;
+        ee[q] = i < nh ? a0 + (size_t)i : b + (size_t)(i - nh);
+        ev[q] = svc_ld(slot, x, ee[q]);
+        have[q] = true;
+      }
+#pragma unroll
+      for (int q = 0; q < RB; q++)
+        if (have[q]) svc_st(host, svc_row<COMPACT>(L, CL, N, rb + q), ee[q], ev[q], ovf);
+    }
+  }
 }
 
 // The rows (bit r) whose elements [lo, hi) differ between two records; every lane of the
@@ -188,7 +308,10 @@ __device__ void service_loop(DevCluster c, const DevJob& job, const kss_profile&
   unsigned long long st0 = 0, st1 = 0, st2 = 0;  // diagnostic clocks of shard 0's lane 0 (stamps)
   unsigned long long seen_min = seq;              // shard 0: every shard has taken the commands below this
   int parity = 0;                                 // the record slot of the next evaluation
-  unsigned host_valid = 0;  // rows (bit r) whose host segment equals the last evaluation's slot
+  // rows (bit r) whose host segment equals the last evaluation's slot: full / compact record
+  unsigned host_valid = 0, host_valid_c = 0;
+  uint8_t* crec_host = rec_host + SlotLayout(N).bytes;  // the compact record behind the full one
+  const CompactLayout CL(N);
   for (;; ++seq) {
     if (threadIdx.x == 0) {
       int op = SVC_STOP, pod = 0, node = 0, fields = 0;
@@ -280,19 +403,20 @@ __device__ void service_loop(DevCluster c, const DevJob& job, const kss_profile&
       if (stamps && w == 0 && threadIdx.x == 0) st2 = wall_clock64();
       // this shard's node range of the requested rows -> the pinned host record, skipping the
       // segments the host already holds (equal to the previous evaluation's, which it copied)
+      // (node bit 0 of an EVAL: the compact record, scores narrowed; else the full one)
+      const bool compact = (node & 1) != 0;
       unsigned want = 0;
       for (int r = 0; r < SVC_ROWS; r++) want |= (fields & svc_row_field(r)) ? 1u << r : 0u;
-      const unsigned send = (want & ~host_valid) | svc_changed_rows(base, prev, L, N, want & host_valid, S.lo, S.hi,
-                                                                    shdr(smem).svc_dirty);
-      for (int r = 0; r < SVC_ROWS; r++) {
-        if (!((send >> r) & 1u)) continue;
-        int es = 0, fr = 0;
-        const size_t o = svc_field(L, r, fr, es);
-        if (es == 1) svc_copy<1>(base + o, rec_host + o, N, fr, 1, S.lo, S.hi);
-        else if (es == 2) svc_copy<2>(base + o, rec_host + o, N, fr, 1, S.lo, S.hi);
-        else svc_copy<8>(base + o, rec_host + o, N, fr, 1, S.lo, S.hi);
-      }
-      host_valid = want;  // the host's rows not asked for now no longer mirror the newest slot
+      unsigned& hv = compact ? host_valid_c : host_valid;
+      if (threadIdx.x == 0) shdr(smem).svc_ovf = 0;  // ordered before the copies by the barriers below
+      const unsigned send = (want & ~hv) | svc_changed_rows(base, prev, L, N, want & hv, S.lo, S.hi,
+                                                            shdr(smem).svc_dirty);
+      bool ovf = false;
+      if (compact) svc_send<true>(base, crec_host, L, CL, N, send, S.lo, S.hi, ovf);
+      else svc_send<false>(base, rec_host, L, CL, N, send, S.lo, S.hi, ovf);
+      if (ovf) atomicOr(&shdr(smem).svc_ovf, 1u);
+      hv = want;  // the host's rows not asked for now no longer mirror the newest slot
+      (compact ? host_valid : host_valid_c) = 0;  // nor does the other record
       if (w == 0 && threadIdx.x == 0) {
         KSS_GLOBAL int32_t* mm = reinterpret_cast<KSS_GLOBAL int32_t*>(&box->meta);
         mm[0] = m.chosen;
@@ -310,7 +434,7 @@ __device__ void service_loop(DevCluster c, const DevJob& job, const kss_profile&
         sp[2] = (long long)st2;
         sp[3] = wall_clock64();
       }
-      if (threadIdx.x == 0) st_sys(&box->done[w], seq + 1);
+      if (threadIdx.x == 0) st_sys(&box->done[w], (seq + 1) | (shdr(smem).svc_ovf ? SVC_DONE_OVF : 0ull));
     } else if (op == SVC_COMMIT || op == SVC_ROLLBACK) {
       const int local = node - c.node_base;
       if (threadIdx.x == 0 && local >= S.lo && local < S.hi)

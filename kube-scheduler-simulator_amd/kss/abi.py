@@ -207,6 +207,13 @@ class PodView(C.Structure):
                 ("status", i32)]
 
 
+class PodCView(C.Structure):
+    """kss_pod_cview: the compact service record (raw / total int32, norm uint8), or `wide`."""
+    _fields_ = [("fail_plugin", P(u8)), ("fail_detail", P(u16)), ("raw", P(i32)), ("norm", P(u8)),
+                ("total", P(i32)), ("n_feasible", i32), ("chosen", i32), ("best_total", i64), ("scored", i32),
+                ("status", i32), ("is_wide", i32), ("pad", i32), ("wide", PodView)]
+
+
 class Config(C.Structure):
     _fields_ = [("device", i32), ("max_pods_record", i32), ("class_capacity", i32), ("term_capacity", i32)]
 

@@ -51,6 +51,7 @@ SIGNATURES = [
     ("kss_service_start", C.c_int, [C.c_void_p]),
     ("kss_service_stop", C.c_int, [C.c_void_p]),
     ("kss_service_eval", C.c_int, [C.c_void_p, C.c_int32, C.c_uint32, P(abi.PodView)]),
+    ("kss_service_eval_compact", C.c_int, [C.c_void_p, C.c_int32, C.c_uint32, P(abi.PodCView)]),
     ("kss_service_commit", C.c_int, [C.c_void_p, C.c_int32, C.c_int32]),
     ("kss_service_rollback", C.c_int, [C.c_void_p, C.c_int32, C.c_int32]),
     ("kss_service_stamps", C.c_int, [C.c_void_p, P(C.c_uint64)]),
@@ -128,6 +129,33 @@ class PodView:
     unrequested fields are None.  Copy what must outlive the next call on the context."""
 
     def __init__(self, v: "abi.PodView", n_nodes: int):
+        N = n_nodes
+
+        def arr(ptr, shape):
+            if not ptr:
+                return None
+            a = np.ctypeslib.as_array(ptr, shape=shape)
+            a.flags.writeable = False
+            return a
+
+        self.fail_plugin = arr(v.fail_plugin, (N,))
+        self.fail_detail = arr(v.fail_detail, (N,))
+        self.raw = arr(v.raw, (abi.KSS_NSCORE, N))
+        self.norm = arr(v.norm, (abi.KSS_NSCORE, N))
+        self.total = arr(v.total, (N,))
+        self.n_feasible, self.chosen, self.best_total = v.n_feasible, v.chosen, v.best_total
+        self.scored, self.status = v.scored, v.status
+
+
+class PodCView(PodView):
+    """kss_pod_cview as read-only numpy views: raw / total int32, norm uint8 (or, when a value
+    did not fit, is_wide and the full record's int64 views)."""
+
+    def __init__(self, v: "abi.PodCView", n_nodes: int):
+        self.is_wide = bool(v.is_wide)
+        if self.is_wide:
+            super().__init__(v.wide, n_nodes)
+            return
         N = n_nodes
 
         def arr(ptr, shape):
@@ -366,6 +394,14 @@ class Context:
         v = view if view is not None else abi.PodView()
         check(lib().kss_service_eval(self.h, i, fields, C.byref(v)))
         return PodView(v, self.n_nodes)
+
+    def service_eval_compact(self, i: int, fields: int = abi.KSS_FIELD_ALL,
+                             view: Optional[abi.PodCView] = None) -> "PodCView":
+        """kss_service_eval_compact of staged pod i: the record with the scores narrowed on the
+        device (int32 raw / total, uint8 normalised), or the full record when is_wide."""
+        v = view if view is not None else abi.PodCView()
+        check(lib().kss_service_eval_compact(self.h, i, fields, C.byref(v)))
+        return PodCView(v, self.n_nodes)
 
     def service_commit(self, i: int, node: int):
         check(lib().kss_service_commit(self.h, i, node))

@@ -29,10 +29,10 @@ def test_library_exports_every_declared_symbol():
 
 def test_struct_sizes_match_ctypes_mirror():
     L = native.lib()
-    out = (C.c_int32 * 16)()
-    k = L.kss_abi_sizes(out, 16)
+    out = (C.c_int32 * 32)()
+    k = L.kss_abi_sizes(out, 32)
     mirror = [abi.Cluster, abi.Req, abi.Term, abi.Spread, abi.Ipa, abi.Pod, abi.PodSet, abi.Profile, abi.PodResult,
-              abi.Config, abi.Names, abi.Synth, abi.Boundset, abi.PreemptResult, abi.Vol]
+              abi.Config, abi.Names, abi.Synth, abi.Boundset, abi.PreemptResult, abi.Vol, abi.PodView, abi.PodCView]
     assert k == len(mirror)
     for i, t in enumerate(mirror):
         assert out[i] == C.sizeof(t), (t.__name__, out[i], C.sizeof(t))

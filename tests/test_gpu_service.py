@@ -105,3 +105,41 @@ def test_service_restarts_after_idle_exit_and_yields_to_other_calls():
     _same(d, _copy(c), 3000, "after the per-pod API")
     ctx.close()
     s.close()
+
+
+@pytest.mark.parametrize("config,n_nodes,n_pods", [(2, 5000, 40), (3, 2000, 30), (4, 6000, 24)])
+def test_service_compact_record_equals_full(config, n_nodes, n_pods):
+    """kss_service_eval_compact (scores narrowed on the device: int32 raw / total, uint8
+    normalised) against kss_service_eval on the same state, pod after pod with commits in
+    between; the two records are asked in both orders and with a field subset, so the
+    host-segment bookkeeping of each record (rows resent only when they changed) is crossed.
+    The wide fallback (a value outside the narrow types) is not reached by any in-range
+    workload: check_profile bounds the totals and the raw scores stay far below 2^31."""
+    s = native.Synth(config, SEED_BASE + config, n_nodes, n_pods)
+    svc = native.Context(abi.default_profile())
+    svc.load(s.cluster)
+    svc.stage(s.pods)
+    N = svc.n_nodes
+    sub = abi.KSS_FIELD_FAIL | abi.KSS_FIELD_TOTAL
+    for j in range(n_pods):
+        fields = sub if j % 5 == 4 else abi.KSS_FIELD_ALL
+        if j % 2:
+            c = _copy(svc.service_eval_compact(j, fields))
+            f = _copy(svc.service_eval(j, fields))
+        else:
+            f = _copy(svc.service_eval(j, fields))
+            c = _copy(svc.service_eval_compact(j, fields))
+        assert (c.chosen, c.n_feasible, c.scored, c.status, c.best_total) == \
+               (f.chosen, f.n_feasible, f.scored, f.status, f.best_total), j
+        for k in ("fail_plugin", "fail_detail", "raw", "norm", "total"):
+            a, b = getattr(c, k), getattr(f, k)
+            assert (a is None) == (b is None), (j, k)
+            if a is not None:
+                assert a.dtype == {"fail_plugin": np.uint8, "fail_detail": np.uint16, "raw": np.int32,
+                                   "norm": np.uint8, "total": np.int32}[k], (j, k, a.dtype)
+                np.testing.assert_array_equal(a[..., :N].astype(np.int64), b[..., :N].astype(np.int64),
+                                              err_msg=f"pod {j} {k}")
+        if f.chosen >= 0:
+            svc.service_commit(j, f.chosen)
+    svc.service_stop()
+    svc.close()
