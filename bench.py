@@ -651,7 +651,8 @@ def run_per_pod(args):
     for j in range(min(100, n_pods)):
         native.check(native.lib().kss_service_eval(ctx.h, j, abi.KSS_FIELD_ALL, ctypes.byref(sview)))
         st = ctx.service_stamps()
-        phases.append([(st[1] - st[0]) / 100.0, (st[2] - st[1]) / 100.0, (st[3] - st[2]) / 100.0])
+        phases.append([(st[1] - st[0]) / 100.0, (st[2] - st[1]) / 100.0, (st[3] - st[2]) / 100.0,
+                       (st[4] - st[2]) / 100.0, (st[3] - st[4]) / 100.0])
         if sview.chosen >= 0:
             native.check(native.lib().kss_service_commit(ctx.h, j, sview.chosen))
     ctx.service_stop()
@@ -702,7 +703,8 @@ def run_per_pod(args):
                                 "eval_us": {"median": float(np.median(ev_svc_c)), "mean": float(ev_svc_c.mean()),
                                             "p90": float(np.percentile(ev_svc_c, 90))}},
                     "shard0_phases_us_median": {"relay": float(ph[0]), "pod": float(ph[1]),
-                                                "record_copy_and_fence": float(ph[2])},
+                                                "record_copy_and_fence": float(ph[2]), "record_stores": float(ph[3]),
+                                                "system_fence": float(ph[4])},
                     "geometry": ctx.last_geometry()},
         "eval_device_ms_last": ctx.last_timing()[0],
         "geometry": ctx.last_geometry(),

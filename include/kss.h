@@ -517,9 +517,9 @@ int kss_service_eval_compact(kss_ctx* ctx, int32_t pod_index, uint32_t fields, k
 int kss_service_commit(kss_ctx* ctx, int32_t pod_index, int32_t node);
 int kss_service_rollback(kss_ctx* ctx, int32_t pod_index, int32_t node);
 /* Diagnostics (KSS_SERVICE_STAMPS set when the grid starts): shard 0's s_memrealtime (100 MHz)
- * in the last evaluation when it took the command, relayed it, finished the pod, and had its
- * record visible to the host. */
-int kss_service_stamps(kss_ctx* ctx, uint64_t* out4);
+ * in the last evaluation when it took the command, relayed it, finished the pod, had its
+ * record visible to the host, and had issued its record stores (before the system fence). */
+int kss_service_stamps(kss_ctx* ctx, uint64_t* out5);
 /* commit pod ps.pods[pod_index] to node (AssumePod); rollback undoes it (Unreserve/ForgetPod).
  * The deltas travel in the kernel's arguments (no upload). */
 int kss_commit(kss_ctx* ctx, const kss_podset* ps, int32_t pod_index, int32_t node);

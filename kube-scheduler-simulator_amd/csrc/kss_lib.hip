@@ -330,10 +330,6 @@ __global__ __launch_bounds__(PRE_NODE_THREADS) void k_preempt_nodes(const Preemp
   extern __shared__ __attribute__((aligned(16))) long long smem[];
   preempt_nodes(*job, smem);
 }
-__global__ __launch_bounds__(PRE_THREADS) void k_preempt_pick(const PreemptJob* __restrict__ job) {
-  extern __shared__ __attribute__((aligned(16))) long long smem[];
-  preempt_pick(*job, smem);
-}
 
 // Volume state sync (kss_apply_volume_delta): rows < n_vol_rows are vol_count, the rest
 // vol_attached keys.  Entries are applied in order by one lane (repeated cells accumulate).
@@ -3009,7 +3005,7 @@ static int svc_launch(kss_ctx* ctx) {
   unsigned long long* seenp = relay + 2 * SVC_DRING;
   uint8_t* rec = v.rec_dev;
   unsigned long long s0 = seq0;
-  int stamps = getenv("KSS_SERVICE_STAMPS") ? 1 : 0;
+  int stamps = (getenv("KSS_SERVICE_STAMPS") ? 1 : 0) | (getenv("KSS_SERVICE_NO_DIFF") ? 2 : 0);
   void* args[] = {(void*)&jd,  (void*)&pr,  (void*)&W,     (void*)&npt,   (void*)&bins, (void*)&ck, (void*)&gran,
                   (void*)&err, (void*)&box, (void*)&relay, (void*)&seenp, (void*)&rec, (void*)&s0, (void*)&stamps};
   if (int rc = launch_resident(fn, dim3((unsigned)W), dim3((unsigned)v.threads), args, v.shmem, v.stream)) return rc;
@@ -3261,10 +3257,10 @@ static int svc_commit(kss_ctx* ctx, int32_t pod_index, int32_t node, int sign) {
 }
 
 int kss_service_commit(kss_ctx* ctx, int32_t pod_index, int32_t node) { return svc_commit(ctx, pod_index, node, 1); }
-int kss_service_stamps(kss_ctx* ctx, uint64_t* out4) {
-  if (!ctx || !out4) return fail(KSS_E_INVAL, "bad arguments");
+int kss_service_stamps(kss_ctx* ctx, uint64_t* out5) {
+  if (!ctx || !out5) return fail(KSS_E_INVAL, "bad arguments");
   if (!ctx->svc.box) return fail(KSS_E_INVAL, "no service grid");
-  for (int i = 0; i < 4; i++) out4[i] = __atomic_load_n(&ctx->svc.box->stamp[i], __ATOMIC_ACQUIRE);
+  for (int i = 0; i < 5; i++) out5[i] = __atomic_load_n(&ctx->svc.box->stamp[i], __ATOMIC_ACQUIRE);
   return 0;
 }
 
@@ -3871,7 +3867,6 @@ int kss_postfilter_pod(kss_ctx* ctx, const kss_podset* ps, int32_t pod_index, ks
   hipLaunchKernelGGL(k_preempt_stats, dim3(nsb), dim3(256), lds, ctx->stream, jd);  // a lane per node of the range
   const unsigned nb = (unsigned)((N + PRE_NODE_THREADS - 1) / PRE_NODE_THREADS);
   hipLaunchKernelGGL(k_preempt_nodes, dim3(std::max(nb, 1u)), dim3(PRE_NODE_THREADS), sizeof(PreHdr), ctx->stream, jd);
-  hipLaunchKernelGGL(k_preempt_pick, dim3(1), dim3(PRE_THREADS), sizeof(PreHdr), ctx->stream, jd);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipEventRecord(ctx->ev1, ctx->stream));
   const size_t back = sizeof(PreemptOut) + 8 * (size_t)cap;
@@ -3887,7 +3882,7 @@ int kss_postfilter_pod(kss_ctx* ctx, const kss_podset* ps, int32_t pod_index, ks
   float ms = 0;
   HIP_TRY(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
   ctx->last_ms = ms;
-  ctx->last_launches = 3;
+  ctx->last_launches = 2;
   ctx->last_kernel = 3;
   PreemptOut o;
   std::memcpy(&o, ctx->pinned, sizeof(o));

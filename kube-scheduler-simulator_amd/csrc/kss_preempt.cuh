@@ -66,8 +66,8 @@ struct PreGlobal {
   long long aff_total, flags;
   int plan_ok, prefilter;
   int n_potential, n_candidates, feasible, pad;
-  unsigned ticket;  // k_preempt_stats workgroups done (the last one finishes the criticalPaths)
-  int pad2;
+  unsigned ticket;   // k_preempt_stats workgroups done (the last one finishes the criticalPaths)
+  unsigned nticket;  // k_preempt_nodes workgroups done (the last one picks the node)
 };
 constexpr int PRE_STATS_MAX_BLOCKS = 64;
 
@@ -349,10 +349,10 @@ __device__ __forceinline__ bool resolvable(int f, int detail) {
 }
 
 // ---------------------------------------------------------------------------
-// Three launches on one stream: k_preempt_stats (node ranges over a few workgroups:
+// Two launches on one stream: k_preempt_stats (node ranges over a few workgroups:
 // PreFilter state into HBM), k_preempt_nodes (one lane per node over the whole grid:
-// filters, potential nodes, SelectVictimsOnNode, each workgroup's best candidate),
-// k_preempt_pick (one workgroup: pickOneNodeForPreemption, the nominated node's victims).
+// filters, potential nodes, SelectVictimsOnNode, each workgroup's best candidate; the last
+// workgroup to finish runs pickOneNodeForPreemption and copies the nominated node's victims).
 // ---------------------------------------------------------------------------
 
 // pod record and its plan (built on the host, in the job) -> LDS, word-parallel
@@ -499,13 +499,83 @@ __device__ void preempt_stats(const PreemptJob& J, long long* smem) {
   }
 }
 
+// pickOneNodeForPreemption, by the last k_preempt_nodes workgroup (pod and plan already in
+// LDS); the other workgroups' counts and tuples through agent-scope loads (their release
+// fences wrote them back).
+__device__ __forceinline__ long long ld_agent(const long long* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ int ld_agent(const int* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+
+__device__ void preempt_pick_last(const PreemptJob& J, long long* smem) {
+  const int tid = threadIdx.x, nt = blockDim.x;
+  PreHdr& H = *reinterpret_cast<PreHdr*>(smem);
+  const DevCluster& c = J.c;
+  const PreGlobal& G = *J.G;
+  PreemptOut& out = *J.out;
+  const int feasible = ld_agent(&G.feasible), n_pot = ld_agent(&G.n_potential), n_cand = ld_agent(&G.n_candidates);
+  if (feasible || n_cand == 0) {
+    if (tid == 0) {
+      out.status = feasible ? KSS_PREEMPT_SCHEDULABLE : KSS_PREEMPT_NO_CANDIDATE;
+      out.nominated = -1;
+      out.n_potential = n_pot;
+      out.n_candidates = n_cand;
+      out.n_victims = 0;
+    }
+    return;
+  }
+  const int nb = J.n_blocks;
+  const long long* K = reinterpret_cast<const long long*>(J.key);
+  // over the workgroups' best tuples (each lane folds its share lexicographically, then the
+  // same successive reductions over the lanes)
+  long long hp = INT64_MAX, sum = INT64_MAX, cnt = INT64_MAX, st = INT64_MIN, nn = INT64_MAX;
+  for (int b = tid; b < nb; b += nt) {
+    const long long h = ld_agent(K + b), s2 = ld_agent(K + nb + b), c2 = ld_agent(K + 2 * nb + b),
+                    t2 = ld_agent(K + 3 * nb + b), n2 = ld_agent(K + 4 * nb + b);
+    const bool better = h != hp ? h < hp : (s2 != sum ? s2 < sum : (c2 != cnt ? c2 < cnt : (t2 != st ? t2 > st : n2 < nn)));
+    if (better) hp = h, sum = s2, cnt = c2, st = t2, nn = n2;
+  }
+  const long long bhp = block_op(hp, OP_MIN, H.red);
+  bool eq = hp == bhp;
+  const long long bsum = block_op(eq ? sum : INT64_MAX, OP_MIN, H.red);
+  eq &= sum == bsum;
+  const long long bcnt = block_op(eq ? cnt : INT64_MAX, OP_MIN, H.red);
+  eq &= cnt == bcnt;
+  const long long bst = block_op(eq ? st : INT64_MIN, OP_MAX, H.red);
+  eq &= st == bst;
+  const long long best = block_op(eq ? nn : INT64_MAX, OP_MIN, H.red);
+  // the nominated node's victims, kept by its dry run
+  const int nv = (int)bcnt;
+  const long long* vs = reinterpret_cast<const long long*>(J.vscratch + J.B.ptr[best]);
+  for (int i = tid; i < min(nv, J.victims_cap); i += nt) J.victims[i] = ld_agent(vs + i);
+  if (tid == 0) {
+    out.status = KSS_PREEMPT_NOMINATED;
+    out.nominated = (int32_t)(c.node_base + best);
+    out.n_potential = n_pot;
+    out.n_candidates = n_cand;
+    out.n_victims = nv;
+    out.highest_priority = (int32_t)bhp;
+    out.sum_priority = bsum;
+    out.earliest_start = bst;
+  }
+}
+
 __device__ void preempt_nodes(const PreemptJob& J, long long* smem) {
   const int tid = threadIdx.x;
   PreHdr& H = *reinterpret_cast<PreHdr*>(smem);
   const DevCluster& c = J.c;
   const DevPods& P = J.P;
   const PreGlobal& G = *J.G;
-  if (!G.plan_ok || G.prefilter != 0) return;
+  if (!G.plan_ok || G.prefilter != 0) {
+    // a PreFilter failure gives every node UnschedulableAndUnresolvable: nothing to dry-run
+    if (blockIdx.x == 0 && tid == 0) {
+      PreemptOut& out = *J.out;
+      out.status = !G.plan_ok ? -1 : KSS_PREEMPT_NO_CANDIDATE;
+      out.nominated = -1;
+      out.n_potential = out.n_candidates = out.n_victims = 0;
+    }
+    return;
+  }
   pre_load_pod(J, H);
   if (tid == 0) {
     for (int i = 0; i < MAXH; i++) {
@@ -587,83 +657,21 @@ __device__ void preempt_nodes(const PreemptJob& J, long long* smem) {
       K[4 * nb + b] = nn;
     }
   }
+  // the last workgroup to finish (a ticket after every lane's release fence: the victims'
+  // ids, the tuple and the counts) picks the node
   if (tid == 0) {
     PreGlobal& Gw = *J.G;
     if (n_pot) atomicAdd(&Gw.n_potential, (int)n_pot);
     if (n_cand) atomicAdd(&Gw.n_candidates, (int)n_cand);
     if (feasible) atomicAdd(&Gw.feasible, (int)feasible);
   }
-}
-
-__device__ void preempt_pick(const PreemptJob& J, long long* smem) {
-  const int tid = threadIdx.x, nt = blockDim.x;
-  PreHdr& H = *reinterpret_cast<PreHdr*>(smem);
-  const DevCluster& c = J.c;
-  const PreGlobal& G = *J.G;
-  PreemptOut& out = *J.out;
-  if (!G.plan_ok || G.prefilter != 0) {
-    // a PreFilter failure gives every node UnschedulableAndUnresolvable: nothing to dry-run
-    if (tid == 0) {
-      out.status = !G.plan_ok ? -1 : KSS_PREEMPT_NO_CANDIDATE;
-      out.nominated = -1;
-      out.n_potential = out.n_candidates = out.n_victims = 0;
-    }
-    return;
-  }
-  if (G.feasible || G.n_candidates == 0) {
-    if (tid == 0) {
-      out.status = G.feasible ? KSS_PREEMPT_SCHEDULABLE : KSS_PREEMPT_NO_CANDIDATE;
-      out.nominated = -1;
-      out.n_potential = G.n_potential;
-      out.n_candidates = G.n_candidates;
-      out.n_victims = 0;
-    }
-    return;
-  }
-  pre_load_pod(J, H);
-  if (tid == 0) {
-    for (int i = 0; i < MAXH; i++) {
-      H.m0[i] = G.m0[i];
-      H.id0[i] = G.id0[i];
-      H.m1[i] = G.m1[i];
-    }
-    H.aff_total = G.aff_total;
-    H.flags = G.flags;
-  }
+  __threadfence();
   __syncthreads();
-  const int nb = J.n_blocks;
-  const int64_t* K = J.key;
-  // pickOneNodeForPreemption over the workgroups' best tuples (each lane folds its share
-  // lexicographically, then the same successive reductions over the lanes)
-  long long hp = INT64_MAX, sum = INT64_MAX, cnt = INT64_MAX, st = INT64_MIN, nn = INT64_MAX;
-  for (int b = tid; b < nb; b += nt) {
-    const long long h = K[b], s2 = K[nb + b], c2 = K[2 * nb + b], t2 = K[3 * nb + b], n2 = K[4 * nb + b];
-    const bool better = h != hp ? h < hp : (s2 != sum ? s2 < sum : (c2 != cnt ? c2 < cnt : (t2 != st ? t2 > st : n2 < nn)));
-    if (better) hp = h, sum = s2, cnt = c2, st = t2, nn = n2;
-  }
-  const long long bhp = block_op(hp, OP_MIN, H.red);
-  bool eq = hp == bhp;
-  const long long bsum = block_op(eq ? sum : INT64_MAX, OP_MIN, H.red);
-  eq &= sum == bsum;
-  const long long bcnt = block_op(eq ? cnt : INT64_MAX, OP_MIN, H.red);
-  eq &= cnt == bcnt;
-  const long long bst = block_op(eq ? st : INT64_MIN, OP_MAX, H.red);
-  eq &= st == bst;
-  const long long best = block_op(eq ? nn : INT64_MAX, OP_MIN, H.red);
-  // the nominated node's victims, kept by its dry run in k_preempt_nodes
-  const int nv = (int)bcnt;
-  const int64_t* vs = J.vscratch + J.B.ptr[best];
-  for (int i = tid; i < min(nv, J.victims_cap); i += nt) J.victims[i] = vs[i];
-  if (tid == 0) {
-    out.status = KSS_PREEMPT_NOMINATED;
-    out.nominated = (int32_t)(c.node_base + best);
-    out.n_potential = G.n_potential;
-    out.n_candidates = G.n_candidates;
-    out.n_victims = nv;
-    out.highest_priority = (int32_t)bhp;
-    out.sum_priority = bsum;
-    out.earliest_start = bst;
-  }
+  if (tid == 0) H.plan_ok = (int)(atomicAdd(&J.G->nticket, 1u) == (unsigned)(gridDim.x - 1)) + 1;  // 2: last
+  __syncthreads();
+  if (H.plan_ok != 2) return;
+  __threadfence();
+  preempt_pick_last(J, smem);
 }
 
 }  // namespace kss

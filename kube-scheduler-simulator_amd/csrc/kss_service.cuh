@@ -149,10 +149,13 @@ __device__ __forceinline__ void svc_st(uint8_t* dst, const SvcRow& x, size_t e, 
 template <bool COMPACT>
 __device__ __forceinline__ void svc_send(const uint8_t* slot, uint8_t* host, const SlotLayout& L,
                                          const CompactLayout& CL, size_t N, unsigned send, int lo, int hi, bool& ovf) {
-  const int tid = (int)threadIdx.x, nt = (int)blockDim.x;
+  // rows go to the waves in turn (row r to wave r mod waves), a row's chunks to the wave's
+  // lanes: a wave's stores to host memory complete one instruction at a time, so the rows
+  // are spread over every wave of the shard rather than the lanes of one
+  const int lane = (int)threadIdx.x & 63, wave = (int)threadIdx.x >> 6, nw = (int)blockDim.x >> 6;
   constexpr int RB = 10;  // rows per batch (registers: RB x 2 x 16 bytes)
   // interior chunks of a row: at most (hi - lo) / 2 + 1 (16-byte stores of 8-byte elements)
-  const int rounds = ((hi - lo) / 2 + 1 + nt - 1) / nt;
+  const int rounds = ((hi - lo) / 2 + 1 + 63) / 64;
   for (int rb = 0; rb < SVC_ROWS; rb += RB) {
     for (int k = 0; k < rounds; k++) {
       uint4 v[RB][2];
@@ -161,11 +164,11 @@ __device__ __forceinline__ void svc_send(const uint8_t* slot, uint8_t* host, con
       for (int q = 0; q < RB; q++) {
         const int r = rb + q;
         have[q] = false;
-        if (r >= SVC_ROWS || !((send >> r) & 1u)) continue;
+        if (r >= SVC_ROWS || !((send >> r) & 1u) || r % nw != wave) continue;
         const SvcRow x = svc_row<COMPACT>(L, CL, N, r);
         const size_t a0 = x.e0 + (size_t)lo, b0 = x.e0 + (size_t)hi;
         const size_t a = (a0 + x.V - 1) / x.V * x.V, b = b0 / x.V * x.V;
-        const size_t i = (size_t)(tid + k * nt);
+        const size_t i = (size_t)(lane + k * 64);
         if (a >= b || i >= (b - a) / x.V) continue;
         have[q] = true;
         KSS_GLOBAL const uint4* s4 = reinterpret_cast<KSS_GLOBAL const uint4*>(gp(slot) + x.so + (a + i * x.V) * x.es);
@@ -179,7 +182,7 @@ __device__ __forceinline__ void svc_send(const uint8_t* slot, uint8_t* host, con
         const SvcRow x = svc_row<COMPACT>(L, CL, N, r);
         const size_t a0 = x.e0 + (size_t)lo;
         const size_t a = (a0 + x.V - 1) / x.V * x.V;
-        const size_t i = (size_t)(tid + k * nt);
+        const size_t i = (size_t)(lane + k * 64);
         KSS_GLOBAL uint8_t* dp = gp(host) + x.dof + (a + i * x.V) * x.ed;
         if (x.ed == x.es) {  // a 16-byte copy: member stores, merged into one dwordx4
           KSS_GLOBAL uint4* d4 = reinterpret_cast<KSS_GLOBAL uint4*>(dp);
@@ -217,7 +220,7 @@ __device__ __forceinline__ void svc_send(const uint8_t* slot, uint8_t* host, con
   }
   // the unaligned ends: at most V - 1 elements at each end of each row segment, loads first
   for (int rb = 0; rb < SVC_ROWS; rb += RB) {
-    for (int k = 0; k < (32 + nt - 1) / nt; k++) {  // a segment has at most 31 such elements
+    {  // a segment has at most 31 such elements: one per lane of the row's wave
       uint64_t ev[RB];
       size_t ee[RB];
       bool have[RB];
@@ -225,13 +228,13 @@ __device__ __forceinline__ void svc_send(const uint8_t* slot, uint8_t* host, con
       for (int q = 0; q < RB; q++) {
         const int r = rb + q;
         have[q] = false;
-        if (r >= SVC_ROWS || !((send >> r) & 1u)) continue;
+        if (r >= SVC_ROWS || !((send >> r) & 1u) || r % nw != wave) continue;
         const SvcRow x = svc_row<COMPACT>(L, CL, N, r);
         const size_t a0 = x.e0 + (size_t)lo, b0 = x.e0 + (size_t)hi;
         size_t a = (a0 + x.V - 1) / x.V * x.V, b = b0 / x.V * x.V;
         if (a >= b) a = b = b0;  // no interior: the whole segment is a "head"
         const int nh = (int)(a - a0), ntl = (int)(b0 - b);
-        const int i = tid + k * nt;
+        const int i = lane;
         if (i >= nh + ntl) continue;
         ee[q] = i < nh ? a0 + (size_t)i : b + (size_t)(i - nh);
         ev[q] = svc_ld(slot, x, ee[q]);
@@ -305,7 +308,7 @@ __device__ void service_loop(DevCluster c, const DevJob& job, const kss_profile&
   }
   int* cmd = shdr(smem).cmd;
   if (w == 0 && threadIdx.x == 0) __hip_atomic_store(&box->running, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  unsigned long long st0 = 0, st1 = 0, st2 = 0;  // diagnostic clocks of shard 0's lane 0 (stamps)
+  unsigned long long st0 = 0, st1 = 0, st2 = 0, st4 = 0;  // diagnostic clocks of shard 0's lane 0 (stamps)
   unsigned long long seen_min = seq;              // shard 0: every shard has taken the commands below this
   int parity = 0;                                 // the record slot of the next evaluation
   // rows (bit r) whose host segment equals the last evaluation's slot: full / compact record
@@ -400,7 +403,7 @@ __device__ void service_loop(DevCluster c, const DevJob& job, const kss_profile&
         if (threadIdx.x == 0) __hip_atomic_store(&box->err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         break;
       }
-      if (stamps && w == 0 && threadIdx.x == 0) st2 = wall_clock64();
+      if ((stamps & 1) && w == 0 && threadIdx.x == 0) st2 = wall_clock64();
       // this shard's node range of the requested rows -> the pinned host record, skipping the
       // segments the host already holds (equal to the previous evaluation's, which it copied)
       // (node bit 0 of an EVAL: the compact record, scores narrowed; else the full one)
@@ -408,13 +411,16 @@ __device__ void service_loop(DevCluster c, const DevJob& job, const kss_profile&
       unsigned want = 0;
       for (int r = 0; r < SVC_ROWS; r++) want |= (fields & svc_row_field(r)) ? 1u << r : 0u;
       unsigned& hv = compact ? host_valid_c : host_valid;
-      if (threadIdx.x == 0) shdr(smem).svc_ovf = 0;  // ordered before the copies by the barriers below
-      const unsigned send = (want & ~hv) | svc_changed_rows(base, prev, L, N, want & hv, S.lo, S.hi,
-                                                            shdr(smem).svc_dirty);
+      if (threadIdx.x == 0) shdr(smem).svc_ovf = 0;
+      __syncthreads();  // the reset before any lane's overflow report
+      const unsigned send = (stamps & 2) ? want  // experiment (KSS_SERVICE_NO_DIFF): every requested row
+                                         : (want & ~hv) | svc_changed_rows(base, prev, L, N, want & hv, S.lo, S.hi,
+                                                                           shdr(smem).svc_dirty);
       bool ovf = false;
       if (compact) svc_send<true>(base, crec_host, L, CL, N, send, S.lo, S.hi, ovf);
       else svc_send<false>(base, rec_host, L, CL, N, send, S.lo, S.hi, ovf);
       if (ovf) atomicOr(&shdr(smem).svc_ovf, 1u);
+      if ((stamps & 1) && w == 0 && threadIdx.x == 0) st4 = wall_clock64();
       hv = want;  // the host's rows not asked for now no longer mirror the newest slot
       (compact ? host_valid : host_valid_c) = 0;  // nor does the other record
       if (w == 0 && threadIdx.x == 0) {
@@ -427,14 +433,18 @@ __device__ void service_loop(DevCluster c, const DevJob& job, const kss_profile&
       }
       __threadfence_system();  // this lane's record stores are visible to the host
       __syncthreads();
-      if (stamps && w == 0 && threadIdx.x == 0) {
+      if ((stamps & 1) && w == 0 && threadIdx.x == 0) {
         KSS_GLOBAL long long* sp = reinterpret_cast<KSS_GLOBAL long long*>(&box->stamp[0]);
         sp[0] = (long long)st0;
         sp[1] = (long long)st1;
         sp[2] = (long long)st2;
         sp[3] = wall_clock64();
+        sp[4] = (long long)st4;
       }
-      if (threadIdx.x == 0) st_sys(&box->done[w], (seq + 1) | (shdr(smem).svc_ovf ? SVC_DONE_OVF : 0ull));
+      if (threadIdx.x == 0) {
+        const unsigned long long dv = (seq + 1) | (shdr(smem).svc_ovf ? SVC_DONE_OVF : 0ull);
+        st_sys(&box->done[w], dv);
+      }
     } else if (op == SVC_COMMIT || op == SVC_ROLLBACK) {
       const int local = node - c.node_base;
       if (threadIdx.x == 0 && local >= S.lo && local < S.hi)

@@ -410,8 +410,9 @@ class Context:
         check(lib().kss_service_rollback(self.h, i, node))
 
     def service_stamps(self):
-        """Shard 0's clock (100 MHz ticks) at command taken / relayed / pod done / record visible."""
-        out = (C.c_uint64 * 4)()
+        """Shard 0's clock (100 MHz ticks) at command taken / relayed / pod done / record
+        visible / record stores issued (before the system fence)."""
+        out = (C.c_uint64 * 5)()
         check(lib().kss_service_stamps(self.h, out))
         return list(out)
 
