@@ -22,6 +22,8 @@
 //                (kss_preempt.cuh).
 #include <hip/hip_runtime.h>
 
+#include <sys/mman.h>
+
 #include <algorithm>
 #include <chrono>
 #include <cmath>
@@ -550,6 +552,8 @@ struct kss_ctx {
     uint8_t* rec_dev = nullptr;    // its device address
     SvcBox* box_dev = nullptr;
     size_t rec_bytes = 0;
+    void* rec_map = nullptr;       // KSS_SVC_HUGE: the record in a registered 2 MiB-aligned mapping
+    size_t rec_map_bytes = 0;
     DevBuf relay, gran, err, job;  // device relay ring + seen counters, granules, error word, DevJob
     unsigned long long posted = 0; // commands written to the ring
     int W = 0, threads = 0, npt = 0, bins_cap = 0, cache_keys = -1;
@@ -2965,10 +2969,23 @@ int kss_run_staged(kss_ctx* ctx, int32_t n, uint32_t flags, int32_t* chosen_out)
 // ---------------------------------------------------------------------------
 // the per-pod service grid (kss_service_*): host side (kernel: kss_service.cuh)
 // ---------------------------------------------------------------------------
+static void svc_free_rec(kss_ctx::Service& v) {
+  if (v.rec && v.rec_map) {
+    hipHostUnregister(v.rec);
+    munmap(v.rec_map, v.rec_map_bytes);
+  } else if (v.rec) {
+    hipHostFree(v.rec);
+  }
+  v.rec = nullptr;
+  v.rec_map = nullptr;
+  v.rec_map_bytes = 0;
+  v.rec_bytes = 0;
+}
+
 static void svc_free(kss_ctx* ctx) {
   auto& v = ctx->svc;
   if (v.box) hipHostFree(v.box);
-  if (v.rec) hipHostFree(v.rec);
+  svc_free_rec(v);
   if (v.stream) hipStreamDestroy(v.stream);
   v.relay.release();
   v.gran.release();
@@ -3048,10 +3065,26 @@ static int svc_start_locked(kss_ctx* ctx) {
   }
   const size_t rec_bytes = SL.bytes + CompactLayout(N).bytes;  // the full record, then the compact one
   if (v.rec_bytes < rec_bytes) {
-    if (v.rec) HIP_TRY(hipHostFree(v.rec));
-    v.rec = nullptr;
-    v.rec_bytes = 0;
-    HIP_TRY(hipHostMalloc((void**)&v.rec, rec_bytes, hipHostMallocCoherent | hipHostMallocMapped));
+    svc_free_rec(v);
+    if (getenv("KSS_SVC_HUGE")) {
+      // experiment: the record in transparent huge pages (madvise), registered with the device,
+      // so that its rows do not each take their own 4 KiB translation
+      const size_t H = (size_t)2 << 20, sz = align_up(rec_bytes, H);
+      void* m = mmap(nullptr, sz + H, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+      if (m == MAP_FAILED) return fail(KSS_E_NOMEM, "record mapping failed");
+      uint8_t* a = (uint8_t*)align_up((size_t)m, H);
+      madvise(a, sz, MADV_HUGEPAGE);
+      std::memset(a, 0, sz);
+      if (hipHostRegister(a, sz, hipHostRegisterMapped) != hipSuccess) {
+        munmap(m, sz + H);
+        return fail(KSS_E_DEVICE, "record registration failed");
+      }
+      v.rec_map = m;
+      v.rec_map_bytes = sz + H;
+      v.rec = a;
+    } else {
+      HIP_TRY(hipHostMalloc((void**)&v.rec, rec_bytes, hipHostMallocCoherent | hipHostMallocMapped));
+    }
     HIP_TRY(hipHostGetDevicePointer((void**)&v.rec_dev, v.rec, 0));
     v.rec_bytes = rec_bytes;
   }
