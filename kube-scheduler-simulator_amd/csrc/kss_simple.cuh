@@ -741,26 +741,18 @@ __device__ __forceinline__ bool simple_sync_pw(SimpleHdr& H, int& parity, long l
     for (int i = 0; i < 6; i++) H.red[parity][wave][1 + i] = u[i];
   }
   lds_barrier();
-  if (wave == 0) {  // wave 0 alone combines and exchanges; the others wait
-    // every lane folds the nw (<= 4) waves' entries itself (broadcast LDS reads): no
-    // cross-lane reduction for a handful of values
-    long long best = 0;
-    int ws = -1;  // the wave holding the shard's best (keys carry the node index: one wave at most)
-    for (int x = 0; x < nw; x++) {
-      const long long b = H.red[parity][x][0];
-      if (b > best) best = b, ws = x;
-    }
-    uint32_t t[6] = {0u, 0u, 0u, 0u, 0u, 0u};
-    for (int x = 0; x < nw; x++) {
-      const long long* h = H.red[parity][x];
-      const int o = x == ws ? 4 : 1;  // the best wave contributes its H1, the others their H0
-      t[0] += (uint32_t)h[1];
-      t[1] = max(t[1], (uint32_t)h[2]);
-      t[2] = max(t[2], (uint32_t)h[3]);
-      t[3] += (uint32_t)h[o];
-      t[4] = max(t[4], (uint32_t)h[o + 1]);
-      t[5] = max(t[5], (uint32_t)h[o + 2]);
-    }
+  if (wave == 0) {  // wave 0 alone combines (lane v holds wave v's values) and exchanges; the others wait
+    const bool in = lane < nw;
+    const long long* h = H.red[parity][in ? lane : 0];
+    const long long b = in ? h[0] : 0;
+    const long long best = wave_red<OP_MAX>(b);
+    // the wave holding the shard's best (keys carry the node index: one wave at most)
+    const unsigned long long m = __ballot(in && best != 0 && b == best);
+    const int ws = m ? __ffsll((long long)m) - 1 : -1;
+    const int o = lane == ws ? 4 : 1;  // the best wave contributes its H1, the others their H0
+    uint32_t t[6] = {in ? (uint32_t)h[1] : 0u, in ? (uint32_t)h[2] : 0u, in ? (uint32_t)h[3] : 0u,
+                     in ? (uint32_t)h[o] : 0u, in ? (uint32_t)h[o + 1] : 0u, in ? (uint32_t)h[o + 2] : 0u};
+    wave_red_stats(t);
     if (sp && lane == 0) sp[4] = wall_clock64();
     if (W == 1) {  // the winner (if any) is this shard's best
       if (lane == 0) {
