@@ -111,6 +111,7 @@ struct DevJob {
   const GPod* gpods;  // k_spread: host-resolved pod programs [n_pods]
   const int32_t* res_rows;  // k_spread: the count rows resident in LDS (GpodNeeds::res_rows)
   kss_profile prof;   // k_simple<false>: staged word by word into LDS (a by-value kernel argument would land in scratch)
+  int32_t* dbg;       // KSS_SPREAD_DEBUG: k_spread's per-pod, per-shard statistics bins, local and exchanged [n][W][64]
 };
 
 }  // namespace
@@ -255,7 +256,7 @@ __global__ __launch_bounds__(KSS_MAX_THREADS) void k_spread(const DevJob* __rest
     __syncthreads();
   }
   const kss_profile& P = DEF ? def_prof : H.prof;
-  spread_schedule<DEF>(job.c, job.gpods, job.stat, job.res_rows, n_res, k0, min(k1, job.n_pods), job.chosen, job.meta, P, W, w,
+  spread_schedule<DEF>(job.dbg, job.c, job.gpods, job.stat, job.res_rows, n_res, k0, min(k1, job.n_pods), job.chosen, job.meta, P, W, w,
                   cap, bins_cap, gq, gran ? gran + (size_t)ji * 2 * W * G_XW : nullptr, X, epoch0, err, stamps, nst, smem);
 }
 
@@ -480,6 +481,8 @@ struct kss_ctx {
   std::vector<int32_t> key_card_h;
   std::vector<uint32_t> key_flags_h;
   DevBuf gran_buf, err_buf;
+  DevBuf dbg_buf;  // KSS_SPREAD_DEBUG (kss_debug_spread)
+  size_t dbg_words = 0;
   int n_cu = 0;
   int force_w = 0;            // KSS_SHARDS env override (tuning / tests)
   int nodes_per_shard = 128;  // KSS_NODES_PER_SHARD (C2 sweep: 128 > 256 > 512 nodes per shard)
@@ -1324,6 +1327,17 @@ extern "C" {
 int kss_abi_version(void) { return KSS_ABI_VERSION; }
 const char* kss_last_error(void) { return g_err.c_str(); }
 
+int kss_debug_spread(kss_ctx* ctx, int32_t* out, int64_t n_words) {
+  if (!ctx || !out || n_words < 0) return fail(KSS_E_INVAL, "bad arguments");
+  const size_t n = std::min((size_t)n_words, ctx->dbg_words);
+  if (n) {
+    HIP_TRY(hipSetDevice(ctx->cfg.device));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    HIP_TRY(hipMemcpy(out, ctx->dbg_buf.p, 4 * n, hipMemcpyDeviceToHost));
+  }
+  return (int)std::min(n, (size_t)INT32_MAX);
+}
+
 int kss_abi_sizes(int32_t* out, int32_t n) {
   const int32_t s[] = {(int32_t)sizeof(kss_cluster), (int32_t)sizeof(kss_req),     (int32_t)sizeof(kss_term),
                        (int32_t)sizeof(kss_spread),  (int32_t)sizeof(kss_ipa),     (int32_t)sizeof(kss_pod),
@@ -2164,6 +2178,10 @@ static int launch_simple(hipStream_t st, const Geometry& g, int n_jobs, const De
   return 0;
 }
 
+#ifndef KSS_SPREAD_PREF_THREADS
+#define KSS_SPREAD_PREF_THREADS 512
+#endif
+
 // k_spread's per-slot LDS arrays are strided by the largest shard's node count (rounded up
 // to 16 slots), not by threads x slots per lane: a 391-node shard of a 100k-node cluster
 // keeps 400 slots, not 512.
@@ -2340,6 +2358,15 @@ static int run_single_impl(kss_ctx* ctx, const PlanNeeds& need, const DevPods& d
   const bool simple = simple_ok && simple_fits(g);
   const int n_res = (int)ctx->gneed.res_rows.size();
   bool spread = spread_ok && spread_fits(g, ctx->gneed, ctx->dc.n_keys, n_res, N);
+  if (spread && !simple && !getenv("KSS_THREADS") && !getenv("KSS_FORCE_THREADS")) {
+    // k_spread: one node per lane where the workgroup allows it (up to KSS_SPREAD_PREF_THREADS):
+    // its per-node passes are the chain between exchanges (C4: 256 -> 512 lanes, stats +
+    // filter + normalise 4.4 -> 2.6 us per pod)
+    Geometry g2;
+    if (pick_geometry((int)N, W, KSS_SPREAD_PREF_THREADS, g2) && g2.threads > g.threads &&
+        spread_fits(g2, ctx->gneed, ctx->dc.n_keys, n_res, N))
+      g = g2;
+  }
   if (split && simple && g.W > 64 * SX_CHUNKS) return fail(KSS_E_UNSUPPORTED, "split grid: k_simple sweeps at most 128 shards");
   if (spread_ok && !spread && g.threads < KSS_MAX_THREADS) {  // more prefetch lanes per shard
     Geometry g2 = g;
@@ -2395,6 +2422,13 @@ static int run_single_impl(kss_ctx* ctx, const PlanNeeds& need, const DevPods& d
   job.stat = loop ? (uint32_t*)ctx->stat_buf.p : nullptr;
   job.gpods = spread ? (const GPod*)ctx->gpod_buf.p : nullptr;
   job.res_rows = spread ? (const int32_t*)ctx->res_buf.p : nullptr;
+  job.dbg = nullptr;
+  if (spread && getenv("KSS_SPREAD_DEBUG")) {  // diagnosis: statistics bins of every pod and shard
+    ctx->dbg_words = (size_t)n * (size_t)g.W * 64;
+    if ((rc = ctx->dbg_buf.ensure(4 * ctx->dbg_words))) return rc;
+    HIP_TRY(hipMemsetAsync(ctx->dbg_buf.p, 0, 4 * ctx->dbg_words, ctx->stream));
+    job.dbg = (int32_t*)ctx->dbg_buf.p;
+  }
   job.prof = ctx->prof;
   rc = ctx->job_buf.ensure(sizeof(DevJob));
   if (rc) return rc;

@@ -268,6 +268,9 @@ __device__ __forceinline__ void wave_red32(int32_t (&v)[K], const int (&ops)[K])
 // phase bit 0: publish (wave 0), bit 1: sweep by wave gw of nsw sweeping waves (lanes of
 // every sweeping wave share the values: T = 64 nsw / M lanes per value).
 constexpr int G_XS = 16;  // at most this many shards polled per lane at once (4 / 8 / 16 by need)
+#ifndef KSS_SPREAD_SWEEP_WAVES
+#define KSS_SPREAD_SWEEP_WAVES 4  // at most this many waves sweep one exchange (512-lane shards: half)
+#endif
 #ifndef KSS_SPREAD_MW_MIN
 #define KSS_SPREAD_MW_MIN (64 * 4)  // W x values above which every wave sweeps a share (C3: 40 x 13)
 #endif
@@ -440,7 +443,8 @@ __device__ __forceinline__ bool spread_reduce(SpreadHdr& H, int32_t* xs, int W, 
     } else {  // many shards: wave 0 publishes, every wave sweeps a share (fewer polling rounds)
       if (wave == 0) spread_exchange(H, xs, gran, X, W, w, epoch, err, K, opbits, sum_lo, ns, or_lo, no, sp, 0, 1, 1);
       lds_barrier();  // the slots hold the operators' identities before any wave folds into them
-      spread_exchange(H, xs, gran, X, W, w, epoch, err, K, opbits, sum_lo, ns, or_lo, no, nullptr, wave, nw, 2);
+      const int nsw = min(nw, KSS_SPREAD_SWEEP_WAVES);  // the sweeping waves (the rest wait)
+      if (wave < nsw) spread_exchange(H, xs, gran, X, W, w, epoch, err, K, opbits, sum_lo, ns, or_lo, no, nullptr, wave, nsw, 2);
       lds_barrier();
       if (H.abort) return false;
       if (minima_q && wave == 0) hard_minima(*minima_q, xs);
@@ -477,8 +481,9 @@ __device__ __forceinline__ bool spread_argmax(SpreadHdr& H, int W, int w, unsign
            tag | (lane ? (uint32_t)((unsigned long long)best >> 32) : (uint32_t)best));
     KSS_GLOBAL const unsigned long long* base = gp(gran) + (size_t)(epoch & 1) * W * G_XW;
     long long m = 0;
-    const int stride = 64 * nw;
-    for (int c0 = wave * 64; c0 < W; c0 += 4 * stride) {
+    const int nsw = min(nw, KSS_SPREAD_SWEEP_WAVES);  // the polling waves (the rest add 0)
+    const int stride = 64 * nsw;
+    for (int c0 = wave * 64; wave < nsw && c0 < W; c0 += 4 * stride) {
       unsigned long long lo[4], hi[4];
       for (unsigned spins = 0;; ++spins) {
         bool ok = true;
@@ -712,7 +717,7 @@ __device__ __forceinline__ int64_t g_ipa_score(const SpreadShard& L, const GPod&
 // The batch for shard w of one cluster, pods [k0, k1).  res_rows: the resident count rows
 // (class r as r, term r as n_classes + r), n_res of them.
 template <bool DEF>
-__device__ __forceinline__ void spread_schedule(DevCluster c, const GPod* __restrict__ gpods,
+__device__ __forceinline__ void spread_schedule(int32_t* dbg, DevCluster c, const GPod* __restrict__ gpods,
                                                 const uint32_t* __restrict__ stat, const int32_t* __restrict__ res_rows,
                                                 int n_res, int k0, int k1, int32_t* chosen, PodMeta* meta,
                                                 const kss_profile& prof, int W, int w, int cap, int bins_cap, int gq,
@@ -832,6 +837,11 @@ __device__ __forceinline__ void spread_schedule(DevCluster c, const GPod* __rest
       // bins zeroed at the end of the previous pod (or in the prologue), behind its barrier
       for (int s = tid; s < own; s += nt) stats_node(L, q, s, sw[s], bins, hard_min, flags);
       GSTAMP(1);
+      const int nbd = min(26, q.total_bins + q.hard_pbins);
+      if (dbg) {  // diagnosis (KSS_SPREAD_DEBUG): this shard's bins before the exchange
+        lds_barrier();
+        for (int b = tid; b < nbd; b += nt) dbg[((size_t)k * W + w) * 64 + b] = bins[b];
+      }
       int32_t v[MAXH + 1];
       const int op[MAXH + 1] = {OP_MIN, OP_MIN, OP_MIN, OP_MIN, OP_OR};
 #pragma unroll
@@ -845,6 +855,11 @@ __device__ __forceinline__ void spread_schedule(DevCluster c, const GPod* __rest
 #pragma unroll
       for (int i = 0; i < MAXH; i++) hard_min[i] = v[i];
       flags = v[MAXH];
+      if (dbg) {  // ... and the exchanged bins, minima and flags
+        for (int b = tid; b < nbd; b += nt) dbg[((size_t)k * W + w) * 64 + 32 + b] = bins[b];
+        if (tid < MAXH + 1) dbg[((size_t)k * W + w) * 64 + 58 + tid] = v[tid];
+        if (tid == 0) dbg[((size_t)k * W + w) * 64 + 63] = (int32_t)epoch;
+      }
       GSTAMP(2);
     }
     // ---- filter + raw scores ----
