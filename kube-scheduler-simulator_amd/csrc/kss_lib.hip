@@ -289,7 +289,7 @@ __global__ __launch_bounds__(256) void k_static(const DevJob* __restrict__ jobs,
   for (int t = 0; t < STATIC_PODS; t++) {
     const int k = kb + t;
     if (k >= kend) break;
-    stat[(size_t)(k - k0) * N + n] = static_word(c, P, P.pods[k], prof, n, flags, th, ts);
+    st_ag(&stat[(size_t)(k - k0) * N + n], static_word(c, P, P.pods[k], prof, n, flags, th, ts));  // sc1: read by the next launch
   }
 }
 

@@ -41,6 +41,26 @@ __device__ __forceinline__ KSS_GLOBAL T* gp(T* p) {
   return (KSS_GLOBAL T*)p;
 }
 
+// Node state and static words handed from one launch to the next (k_static -> loop kernel,
+// a chunk's write-back -> the next chunk's load, a reset copy -> the first load) go through
+// agent-scope (sc1) stores and loads: the per-XCD L2s are not coherent with each other, and a
+// line a workgroup of an earlier launch left in its XCD's L2 must not satisfy a later load on
+// that XCD.  (Observed: a split-grid run reading one stale class count at a chunk boundary.)
+// (through address-space-1 pointers: a flat access would also count in lgkmcnt, and every
+// following LDS wait would then wait on it)
+template <class T>
+__device__ __forceinline__ T ld_ag(const T* p) {
+  return __hip_atomic_load(gp(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <class T>
+__device__ __forceinline__ T ld_ag(KSS_GLOBAL const T* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <class T>
+__device__ __forceinline__ void st_ag(T* p, T v) {
+  __hip_atomic_store(gp(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // Publish one granule at offset `off` of the exchange buffer (the local inbox `gran`);
 // address-space-1 stores (a flat store would also count in lgkmcnt).
 __device__ __forceinline__ void xpub(const XPeers& X, unsigned long long* gran, size_t off, unsigned long long v) {
@@ -809,14 +829,14 @@ __device__ __forceinline__ void simple_schedule(DevCluster c, const SPod* __rest
     for (int k = 0; k < 3; k++) {
       const int64_t A = c.alloc[k * N + n];
       L.r64[k * cap + s] = (double)A;
-      L.r64[(3 + k) * cap + s] = (double)c.requested[k * N + n];
+      L.r64[(3 + k) * cap + s] = (double)ld_ag(&c.requested[k * N + n]);
       L.inv[k * cap + s] = A > 0 ? 1.0 / (double)A : 0.0;
     }
-    L.r64[6 * cap + s] = (double)c.nonzero[n];
-    L.r64[7 * cap + s] = (double)c.nonzero[N + n];
-    L.r32[s] = c.pod_count[n];
+    L.r64[6 * cap + s] = (double)ld_ag(&c.nonzero[n]);
+    L.r64[7 * cap + s] = (double)ld_ag(&c.nonzero[N + n]);
+    L.r32[s] = ld_ag(&c.pod_count[n]);
     L.r32[cap + s] = c.allowed_pods[n];
-    for (int d = 0; d < PD && k0 + d < k1; d++) L.st[((k0 + d) % RING) * cap + s] = stat[(size_t)d * N + lo + s];
+    for (int d = 0; d < PD && k0 + d < k1; d++) L.st[((k0 + d) % RING) * cap + s] = ld_ag(&stat[(size_t)d * N + lo + s]);
   }
   for (int i = tid; i < min(k1 - k0, PD) * NQ; i += nt) {
     const int j = k0 + i / NQ;
@@ -866,7 +886,7 @@ __device__ __forceinline__ void simple_schedule(DevCluster c, const SPod* __rest
       pfq = make_uint4(src.x, src.y, src.z, src.w);
 #pragma unroll
       for (int j = 0; j < PF_MAX; j++)
-        if (j < pf_per) pfw[j] = gstat[(size_t)(k + PD - k0) * N + lo + min(j * pf_n + pf_lane, own - 1)];
+        if (j < pf_per) pfw[j] = ld_ag(&gstat[(size_t)(k + PD - k0) * N + lo + min(j * pf_n + pf_lane, own - 1)]);
     }
     // pass B: NormalizeScore, weights, shard-best selectHost key of pod k
     const long long nf = R[1];
@@ -975,10 +995,10 @@ __device__ __forceinline__ void simple_schedule(DevCluster c, const SPod* __rest
   for (int s = tid; s < own; s += nt) {
     const int n = lo + s;
 #pragma unroll
-    for (int r = 0; r < 3; r++) c.requested[(size_t)r * N + n] = (int64_t)L.r64[(3 + r) * cap + s];
-    c.nonzero[n] = (int64_t)L.r64[6 * cap + s];
-    c.nonzero[N + n] = (int64_t)L.r64[7 * cap + s];
-    c.pod_count[n] = L.r32[s];
+    for (int r = 0; r < 3; r++) st_ag(&c.requested[(size_t)r * N + n], (int64_t)L.r64[(3 + r) * cap + s]);
+    st_ag(&c.nonzero[n], (int64_t)L.r64[6 * cap + s]);
+    st_ag(&c.nonzero[N + n], (int64_t)L.r64[7 * cap + s]);
+    st_ag(&c.pod_count[n], L.r32[s]);
   }
 }
 

@@ -268,6 +268,9 @@ __device__ __forceinline__ void wave_red32(int32_t (&v)[K], const int (&ops)[K])
 // phase bit 0: publish (wave 0), bit 1: sweep by wave gw of nsw sweeping waves (lanes of
 // every sweeping wave share the values: T = 64 nsw / M lanes per value).
 constexpr int G_XS = 16;  // at most this many shards polled per lane at once (4 / 8 / 16 by need)
+#ifndef KSS_SPREAD_SAFE
+#define KSS_SPREAD_SAFE 0  // experiment builds: extra barriers around the exchanges
+#endif
 #ifndef KSS_SPREAD_SWEEP_WAVES
 #define KSS_SPREAD_SWEEP_WAVES 4  // at most this many waves sweep one exchange (512-lane shards: half)
 #endif
@@ -456,6 +459,7 @@ __device__ __forceinline__ bool spread_reduce(SpreadHdr& H, int32_t* xs, int W, 
   for (int k = 0; k < K; k++) v[k] = xs[k];
   // no barrier here: the next reduction rewrites xs[0..K) (publish resets, or the local
   // path's stores) only behind its own first barrier, which every wave reaches after reading
+  if (KSS_SPREAD_SAFE) lds_barrier();  // experiment: a trailing barrier after every exchange
   return true;
 }
 
@@ -748,21 +752,21 @@ __device__ __forceinline__ void spread_schedule(int32_t* dbg, DevCluster c, cons
     for (int k = 0; k < 3; k++) {
       const int64_t A = c.alloc[k * N + n];
       L.r64[k * cap + s] = (double)A;
-      L.r64[(3 + k) * cap + s] = (double)c.requested[k * N + n];
+      L.r64[(3 + k) * cap + s] = (double)ld_ag(&c.requested[k * N + n]);
       L.inv[k * cap + s] = A > 0 ? 1.0 / (double)A : 0.0;
     }
-    L.r64[6 * cap + s] = (double)c.nonzero[n];
-    L.r64[7 * cap + s] = (double)c.nonzero[N + n];
-    L.r32[s] = c.pod_count[n];
+    L.r64[6 * cap + s] = (double)ld_ag(&c.nonzero[n]);
+    L.r64[7 * cap + s] = (double)ld_ag(&c.nonzero[N + n]);
+    L.r32[s] = ld_ag(&c.pod_count[n]);
     L.r32[cap + s] = c.allowed_pods[n];
     L.r32[2 * cap + s] = (int32_t)c.node_flags[n];
     for (int k = 0; k < c.n_keys; k++) L.lbl[k * cap + s] = c.label_value[(size_t)k * N + n];
-    L.st[(k0 & 1) * cap + s] = stat[(size_t)lo + s];
+    L.st[(k0 & 1) * cap + s] = ld_ag(&stat[(size_t)lo + s]);
   }
   for (int i = tid; i < n_res * own; i += nt) {
     const int r = i / own, s = i - r * own, row = res_rows[r];
-    const int32_t v = row < c.n_classes ? c.class_count[(size_t)row * N + lo + s]
-                                        : c.term_count[(size_t)(row - c.n_classes) * N + lo + s];
+    const int32_t v = row < c.n_classes ? ld_ag(&c.class_count[(size_t)row * N + lo + s])
+                                        : ld_ag(&c.term_count[(size_t)(row - c.n_classes) * N + lo + s]);
     L.cnt[r * cap + s] = (uint16_t)v;
   }
   const uint4* grec = reinterpret_cast<const uint4*>(gpods);
@@ -818,7 +822,7 @@ __device__ __forceinline__ void spread_schedule(int32_t* dbg, DevCluster c, cons
       }
 #pragma unroll
       for (int j = 0; j < G_PF; j++)
-        if (j < pf_per) pfw[j] = gstat[(size_t)(k + 1 - k0) * N + lo + min(j * pf_n + pf_lane, own - 1)];
+        if (j < pf_per) pfw[j] = ld_ag(&gstat[(size_t)(k + 1 - k0) * N + lo + min(j * pf_n + pf_lane, own - 1)]);
     }
     PodMeta m;
     m.chosen = -1;
@@ -833,6 +837,7 @@ __device__ __forceinline__ void spread_schedule(int32_t* dbg, DevCluster c, cons
 #pragma unroll
     for (int i = 0; i < MAXH; i++) hard_min[i] = INT32_MAX;
     // ---- stats: PodTopologySpread PreFilter, InterPodAffinity PreFilter / PreScore ----
+    if (KSS_SPREAD_SAFE) lds_barrier();
     if (evaluated && q.need_stats) {
       // bins zeroed at the end of the previous pod (or in the prologue), behind its barrier
       for (int s = tid; s < own; s += nt) stats_node(L, q, s, sw[s], bins, hard_min, flags);
@@ -1180,16 +1185,16 @@ __device__ __forceinline__ void spread_schedule(int32_t* dbg, DevCluster c, cons
   for (int s = tid; s < own; s += nt) {
     const int n = lo + s;
 #pragma unroll
-    for (int r = 0; r < 3; r++) c.requested[(size_t)r * N + n] = (int64_t)L.r64[(3 + r) * cap + s];
-    c.nonzero[n] = (int64_t)L.r64[6 * cap + s];
-    c.nonzero[N + n] = (int64_t)L.r64[7 * cap + s];
-    c.pod_count[n] = L.r32[s];
+    for (int r = 0; r < 3; r++) st_ag(&c.requested[(size_t)r * N + n], (int64_t)L.r64[(3 + r) * cap + s]);
+    st_ag(&c.nonzero[n], (int64_t)L.r64[6 * cap + s]);
+    st_ag(&c.nonzero[N + n], (int64_t)L.r64[7 * cap + s]);
+    st_ag(&c.pod_count[n], L.r32[s]);
   }
   for (int i = tid; i < n_res * own; i += nt) {
     const int r = i / own, s = i - r * own, row = res_rows[r];
     const int32_t v = L.cnt[r * cap + s];
-    if (row < c.n_classes) c.class_count[(size_t)row * N + lo + s] = v;
-    else c.term_count[(size_t)(row - c.n_classes) * N + lo + s] = v;
+    if (row < c.n_classes) st_ag(&c.class_count[(size_t)row * N + lo + s], v);
+    else st_ag(&c.term_count[(size_t)(row - c.n_classes) * N + lo + s], v);
   }
 }
 

@@ -90,6 +90,10 @@ def test_parts_over_many_chunks(monkeypatch, config, n_nodes, n_pods, per_chunk,
             m = res.meta(j)
             if len(dumps) > 1:  # KSS_SPREAD_DEBUG: which shard's statistics of pod j differ from run 0's
                 for p in range(2):
+                    own = slice(p * wl, (p + 1) * wl)
+                    dl = (dumps[0][p][:, own, :26] != dumps[-1][p][:, own, :26]).any(axis=2)  # [pod][shard]
+                    print(f"part {p}: (pod, shard) pairs whose local bins differ from run 0:",
+                          [(int(a), int(b) + p * wl) for a, b in zip(*np.nonzero(dl))][:20])
                     a, b = dumps[0][p][j], dumps[-1][p][j]
                     own = range(p * wl, (p + 1) * wl)
                     print(f"part {p} pod {j}: local bins differing (shard, bin, run0, now)",
