@@ -1117,6 +1117,11 @@ __device__ __forceinline__ void spread_schedule(int32_t* dbg, DevCluster c, cons
       if (!spread_argmax(H, W, w, epoch, gran, X, err, kparity, best)) return;
       GSTAMP(8);
       kparity ^= 1;
+      if (dbg && tid == 0) {  // diagnosis: this shard's view of the selectHost key
+        dbg[((size_t)k * W + w) * 64 + 26] = (int32_t)(uint32_t)(unsigned long long)best;
+        dbg[((size_t)k * W + w) * 64 + 27] = (int32_t)(uint32_t)((unsigned long long)best >> 32);
+        dbg[((size_t)k * W + w) * 64 + 28] = 1;
+      }
       const unsigned long long ub = (unsigned long long)best;
       m.chosen = best ? (int)(0xFFFFFFFFull - (ub & 0xFFFFFFFFull)) : -1;
       m.scored = scored ? 1 : 0;

@@ -88,6 +88,14 @@ def test_parts_over_many_chunks(monkeypatch, config, n_nodes, n_pods, per_chunk,
             j = int(next(b for b in bad if len(b))[0])
             meta = [c.fetch_meta(n_pods)[j].tolist() for c in sp.ctxs]
             m = res.meta(j)
+            if dumps:  # KSS_SPREAD_DEBUG: pods whose selectHost key some shard saw differently
+                key = np.concatenate([dumps[-1][p][:, p * wl:(p + 1) * wl, 26:29] for p in range(2)], axis=1)
+                seen = key[:, :, 2] == 1
+                dis = [int(k) for k in range(n_pods) if seen[k].any() and
+                       len({tuple(key[k, w, :2]) for w in range(2 * wl) if seen[k, w]}) > 1]
+                print("pods whose key differs between shards:", dis[:10])
+                for k in dis[:3]:
+                    print(f"  pod {k}:", [(w, int(key[k, w, 0]), int(key[k, w, 1])) for w in range(2 * wl) if seen[k, w]])
             if len(dumps) > 1:  # KSS_SPREAD_DEBUG: which shard's statistics of pod j differ from run 0's
                 for p in range(2):
                     own = slice(p * wl, (p + 1) * wl)
