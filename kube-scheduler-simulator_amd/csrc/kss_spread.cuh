@@ -843,9 +843,17 @@ __device__ __forceinline__ void spread_schedule(int32_t* dbg, DevCluster c, cons
       for (int s = tid; s < own; s += nt) stats_node(L, q, s, sw[s], bins, hard_min, flags);
       GSTAMP(1);
       const int nbd = min(26, q.total_bins + q.hard_pbins);
-      if (dbg) {  // diagnosis (KSS_SPREAD_DEBUG): this shard's bins before the exchange
+      if (dbg) {  // diagnosis (KSS_SPREAD_DEBUG): this shard's bins before the exchange, and
+        // whether the staged static words / record of this pod equal their HBM sources
         lds_barrier();
         for (int b = tid; b < nbd; b += nt) dbg[((size_t)k * W + w) * 64 + b] = bins[b];
+        int bad_w = 0, bad_r = 0;
+        for (int s2 = tid; s2 < own; s2 += nt) bad_w += sw[s2] != ld_ag(&stat[(size_t)(k - k0) * N + lo + s2]) ? 1 : 0;
+        const uint32_t* rl = reinterpret_cast<const uint32_t*>(L.ring + (k % 3) * gq);
+        const uint32_t* rg = reinterpret_cast<const uint32_t*>(grec + (size_t)k * gq);
+        for (int i = tid; i < 4 * gq; i += nt) bad_r += rl[i] != ld_ag(&rg[i]) ? 1 : 0;
+        if (bad_w) atomicAdd(&dbg[((size_t)k * W + w) * 64 + 29], bad_w);
+        if (bad_r) atomicAdd(&dbg[((size_t)k * W + w) * 64 + 30], bad_r);
       }
       int32_t v[MAXH + 1];
       const int op[MAXH + 1] = {OP_MIN, OP_MIN, OP_MIN, OP_MIN, OP_OR};

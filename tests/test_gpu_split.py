@@ -94,6 +94,9 @@ def test_parts_over_many_chunks(monkeypatch, config, n_nodes, n_pods, per_chunk,
                 dis = [int(k) for k in range(n_pods) if seen[k].any() and
                        len({tuple(key[k, w, :2]) for w in range(2 * wl) if seen[k, w]}) > 1]
                 print("pods whose key differs between shards:", dis[:10])
+                stg = np.concatenate([dumps[-1][p][:, p * wl:(p + 1) * wl, 29:31] for p in range(2)], axis=1)
+                print("(pod, shard, static words, record words) staged differently from HBM:",
+                      [(int(a), int(b), int(stg[a, b, 0]), int(stg[a, b, 1])) for a, b in zip(*np.nonzero(stg.any(axis=2)))][:12])
                 for k in dis[:3]:
                     print(f"  pod {k}:", [(w, int(key[k, w, 0]), int(key[k, w, 1])) for w in range(2 * wl) if seen[k, w]])
             if len(dumps) > 1:  # KSS_SPREAD_DEBUG: which shard's statistics of pod j differ from run 0's
