@@ -2214,6 +2214,8 @@ static int launch_spread(hipStream_t st, const Geometry& g, const GpodNeeds& q, 
   if (stamps && shmem < KSS_LDS_BUDGET) nst = (int)std::min<size_t>(G_NSTAMP, (KSS_LDS_BUDGET - shmem) / (16 * 8));
   if (nst < 8) stamps = nullptr, nst = 0;
   shmem += (size_t)nst * 16 * 8;
+  if (const char* e = getenv("KSS_SPREAD_MIN_LDS"))  // diagnosis: at most one shard per CU
+    shmem = std::max(shmem, std::min((size_t)KSS_LDS_BUDGET, (size_t)std::max(0, atoi(e))));
   const bool def = same_profile(prof, default_profile_c());
   const void* fn = def ? (const void*)k_spread<true> : (const void*)k_spread<false>;
   HIP_TRY(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shmem));
