@@ -776,7 +776,11 @@ __device__ __forceinline__ void spread_schedule(int32_t* dbg, DevCluster c, cons
   }
   if (tid == 0) H.abort = 0;
   __syncthreads();  // the first record is in the ring: zero its statistics bins
-  for (int b = tid; b < bins_cap; b += nt) L.xs[G_NS + b] = 0;
+  {
+    const GPod& q0 = *reinterpret_cast<const GPod*>(L.ring + (k0 % 3) * gq);
+    if (q0.dyn.status == 0 && q0.need_stats)
+      for (int b = tid; b < q0.total_bins + q0.total_pbins; b += nt) L.xs[G_NS + b] = 0;
+  }
   __syncthreads();
 
   KSS_GLOBAL const uint32_t* gstat = gp(stat);
@@ -1178,9 +1182,11 @@ __device__ __forceinline__ void spread_schedule(int32_t* dbg, DevCluster c, cons
     }
     // the statistics bins of pod k+1, zeroed ahead of the barrier that ends this pod (its
     // passes no longer read them): its stats pass then starts without a barrier of its own
-    // (every pod, over the whole bins capacity: not gated on the next record's fields)
-    if (k + 1 < k1)
-      for (int b = tid; b < bins_cap; b += nt) bins[b] = 0;
+    if (k + 1 < k1) {
+      const GPod& qn = *reinterpret_cast<const GPod*>(L.ring + ((k + 1) % 3) * gq);
+      if (qn.dyn.status == 0 && qn.need_stats)
+        for (int b = tid; b < qn.total_bins + qn.total_pbins; b += nt) bins[b] = 0;
+    }
     lds_barrier();
     GSTAMP(9);
 #undef GSTAMP
