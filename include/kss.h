@@ -724,11 +724,6 @@ int kss_format_pod_annotations_ex(const kss_names* names, const kss_profile* pro
                                   int32_t n_scalar, char* buf, size_t cap, size_t* need);
 /* sizeof() of every ABI struct, in header order; returns the count written (ABI self-check) */
 int kss_abi_sizes(int32_t* out, int32_t n);
-/* Diagnosis: with KSS_SPREAD_DEBUG set when the batch runs, k_spread records per pod and shard
- * 64 words — the shard's statistics bins before the exchange [0, 26), the exchanged bins
- * [32, 58), the exchanged minima and flags [58, 63), the exchange epoch [63] — into a device
- * buffer [n][shards][64]; this copies its first n_words words to `out` and returns how many. */
-int kss_debug_spread(kss_ctx* ctx, int32_t* out, int64_t n_words);
 /* Host only (no device): which sequential-loop kernel a staged, unrecorded batch of `ps` on
  * `cl` can take, by its pod programs: out3[0] = 1 k_simple, 2 k_spread, 0 k_schedule only;
  * out3[1] = the first pod that rules out k_spread (-1 none), out3[2] = the reason code

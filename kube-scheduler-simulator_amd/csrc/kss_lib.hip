@@ -111,7 +111,7 @@ struct DevJob {
   const GPod* gpods;  // k_spread: host-resolved pod programs [n_pods]
   const int32_t* res_rows;  // k_spread: the count rows resident in LDS (GpodNeeds::res_rows)
   kss_profile prof;   // k_simple<false>: staged word by word into LDS (a by-value kernel argument would land in scratch)
-  int32_t* dbg;       // KSS_SPREAD_DEBUG: k_spread's per-pod, per-shard statistics bins, local and exchanged [n][W][64]
+  GTrace trace;       // k_spread diagnostic trace (KSS_SPREAD_TRACE builds only; null otherwise)
 };
 
 }  // namespace
@@ -256,7 +256,7 @@ __global__ __launch_bounds__(KSS_MAX_THREADS) void k_spread(const DevJob* __rest
     __syncthreads();
   }
   const kss_profile& P = DEF ? def_prof : H.prof;
-  spread_schedule<DEF>(job.dbg, job.c, job.gpods, job.stat, job.res_rows, n_res, k0, min(k1, job.n_pods), job.chosen, job.meta, P, W, w,
+  spread_schedule<DEF>(job.trace, job.c, job.gpods, job.stat, job.res_rows, n_res, k0, min(k1, job.n_pods), job.chosen, job.meta, P, W, w,
                   cap, bins_cap, gq, gran ? gran + (size_t)ji * 2 * W * G_XW : nullptr, X, epoch0, err, stamps, nst, smem);
 }
 
@@ -481,8 +481,10 @@ struct kss_ctx {
   std::vector<int32_t> key_card_h;
   std::vector<uint32_t> key_flags_h;
   DevBuf gran_buf, err_buf;
-  DevBuf dbg_buf;  // KSS_SPREAD_DEBUG (kss_debug_spread)
-  size_t dbg_words = 0;
+#if KSS_SPREAD_TRACE
+  DevBuf trace_buf, trace_list_buf;  // k_spread trace of the last run (kss_trace_spread)
+  size_t trace_words = 0;
+#endif
   int n_cu = 0;
   int force_w = 0;            // KSS_SHARDS env override (tuning / tests)
   int nodes_per_shard = 128;  // KSS_NODES_PER_SHARD (C2 sweep: 128 > 256 > 512 nodes per shard)
@@ -1327,16 +1329,21 @@ extern "C" {
 int kss_abi_version(void) { return KSS_ABI_VERSION; }
 const char* kss_last_error(void) { return g_err.c_str(); }
 
-int kss_debug_spread(kss_ctx* ctx, int32_t* out, int64_t n_words) {
-  if (!ctx || !out || n_words < 0) return fail(KSS_E_INVAL, "bad arguments");
-  const size_t n = std::min((size_t)n_words, ctx->dbg_words);
-  if (n) {
-    HIP_TRY(hipSetDevice(ctx->cfg.device));
-    HIP_TRY(hipStreamSynchronize(ctx->stream));
-    HIP_TRY(hipMemcpy(out, ctx->dbg_buf.p, 4 * n, hipMemcpyDeviceToHost));
-  }
+#if KSS_SPREAD_TRACE
+// Trace builds only (not in kss.h): the last k_spread run's trace words [n][W][G_TW], its
+// count list (1 + 4 G_TLIST words) and resident rows.  Returns the words copied.
+int kss_trace_spread(kss_ctx* ctx, int32_t* words, int64_t n_words, int32_t* list, int64_t n_list, int32_t* rows,
+                     int32_t n_rows) {
+  if (!ctx || n_words < 0 || n_list < 0) return fail(KSS_E_INVAL, "bad arguments");
+  HIP_TRY(hipSetDevice(ctx->cfg.device));
+  HIP_TRY(hipStreamSynchronize(ctx->stream));
+  const size_t n = std::min((size_t)n_words, ctx->trace_words), nl = std::min((size_t)n_list, (size_t)(4 + 4 * G_TLIST));
+  if (words && n) HIP_TRY(hipMemcpy(words, ctx->trace_buf.p, 4 * n, hipMemcpyDeviceToHost));
+  if (list && nl && ctx->trace_list_buf.p) HIP_TRY(hipMemcpy(list, ctx->trace_list_buf.p, 4 * nl, hipMemcpyDeviceToHost));
+  for (int i = 0; rows && i < n_rows && i < (int)ctx->gneed.res_rows.size(); i++) rows[i] = ctx->gneed.res_rows[i];
   return (int)std::min(n, (size_t)INT32_MAX);
 }
+#endif
 
 int kss_abi_sizes(int32_t* out, int32_t n) {
   const int32_t s[] = {(int32_t)sizeof(kss_cluster), (int32_t)sizeof(kss_req),     (int32_t)sizeof(kss_term),
@@ -2424,13 +2431,18 @@ static int run_single_impl(kss_ctx* ctx, const PlanNeeds& need, const DevPods& d
   job.stat = loop ? (uint32_t*)ctx->stat_buf.p : nullptr;
   job.gpods = spread ? (const GPod*)ctx->gpod_buf.p : nullptr;
   job.res_rows = spread ? (const int32_t*)ctx->res_buf.p : nullptr;
-  job.dbg = nullptr;
-  if (spread && getenv("KSS_SPREAD_DEBUG")) {  // diagnosis: statistics bins of every pod and shard
-    ctx->dbg_words = (size_t)n * (size_t)g.W * 64;
-    if ((rc = ctx->dbg_buf.ensure(4 * ctx->dbg_words))) return rc;
-    HIP_TRY(hipMemsetAsync(ctx->dbg_buf.p, 0, 4 * ctx->dbg_words, ctx->stream));
-    job.dbg = (int32_t*)ctx->dbg_buf.p;
+  job.trace = GTrace{nullptr, nullptr};
+#if KSS_SPREAD_TRACE
+  if (spread) {  // every pod and shard, and the list of nonzero counts loaded / written back
+    ctx->trace_words = (size_t)n * (size_t)g.W * G_TW;
+    if ((rc = ctx->trace_buf.ensure(4 * ctx->trace_words))) return rc;
+    HIP_TRY(hipMemsetAsync(ctx->trace_buf.p, 0, 4 * ctx->trace_words, ctx->stream));
+    job.trace.words = (int32_t*)ctx->trace_buf.p;
+    if ((rc = ctx->trace_list_buf.ensure(4 * (4 + 4 * (size_t)G_TLIST)))) return rc;
+    HIP_TRY(hipMemsetAsync(ctx->trace_list_buf.p, 0, 16, ctx->stream));
+    job.trace.list = (int32_t*)ctx->trace_list_buf.p;
   }
+#endif
   job.prof = ctx->prof;
   rc = ctx->job_buf.ensure(sizeof(DevJob));
   if (rc) return rc;
@@ -3174,17 +3186,31 @@ static int svc_post(kss_ctx* ctx, int op, int pod, int node, int fields, unsigne
 }
 
 // Stop the grid (STOP command, then the stream drains: every wait in the grid is bounded).
+// Relaunch a grid that left after its idle timeout while commands it has not taken are in
+// the ring (a commit / rollback posted as it left): they run before anything else.
+static int svc_revive(kss_ctx* ctx) {
+  auto& v = ctx->svc;
+  if (!v.running || svc_alive(ctx)) return 0;
+  HIP_TRY(hipStreamSynchronize(v.stream));
+  if (v.box->err) return 0;  // a failed grid: svc_stop reports it
+  if (__atomic_load_n(&v.box->consumed, __ATOMIC_ACQUIRE) >= v.posted) return 0;
+  return svc_launch(ctx);
+}
+
 static int svc_stop(kss_ctx* ctx) {
   auto& v = ctx->svc;
   if (!v.running) return 0;
   unsigned long long seq = 0;
+  if (int rc = svc_revive(ctx)) return rc;  // never drop a queued commit / rollback
   if (svc_alive(ctx)) {
     if (int rc = svc_post(ctx, SVC_STOP, 0, 0, 0, &seq)) return rc;
   }
   HIP_TRY(hipStreamSynchronize(v.stream));
   v.running = false;
   const bool err = v.box->err != 0;
-  // commands posted after the grid left for good are dropped (a later start resumes after them)
+  if (!err && __atomic_load_n(&v.box->consumed, __ATOMIC_ACQUIRE) < v.posted)
+    return fail(KSS_E_DEVICE, "service grid: queued commands were not taken");
+  // after a failure the queued commands are dropped (a later start resumes after them)
   __atomic_store_n(&v.box->consumed, v.posted, __ATOMIC_RELEASE);
   if (err) {
     ctx->state_unknown = true;
@@ -3311,6 +3337,14 @@ static int svc_commit(kss_ctx* ctx, int32_t pod_index, int32_t node, int sign) {
   std::lock_guard<std::mutex> lk(ctx->mu);
   if (!ctx->svc.running) {
     if (int rc = svc_start_locked(ctx)) return rc;
+  } else if (!svc_alive(ctx)) {  // left idle: relaunch it to take the command (svc_stop also would)
+    HIP_TRY(hipStreamSynchronize(ctx->svc.stream));
+    if (ctx->svc.box->err) {
+      svc_stop(ctx);
+      ctx->state_unknown = true;
+      return fail(KSS_E_DEVICE, "service grid: a shard exchange timed out");
+    }
+    if (int rc = svc_launch(ctx)) return rc;
   }
   unsigned long long seq = 0;
   if (int rc = svc_post(ctx, sign > 0 ? SVC_COMMIT : SVC_ROLLBACK, pod_index, node, 0, &seq)) return rc;

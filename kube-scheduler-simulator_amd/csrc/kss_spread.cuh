@@ -40,6 +40,37 @@ constexpr int G_NS = 16;     // scalar slots of an exchange
 constexpr int G_SCORE = 3;   // GIpa.kind of a merged InterPodAffinity score entry (KSS_IPA_SCORE_CLASS)
 constexpr int G_NSTAMP = KSS_NSTAMP_PODS / 2;  // pods with diagnostic phase stamps, 16 per pod
 
+// Diagnostic trace, experiment builds only (make -C csrc exp EXP=trace
+// EXP_FLAGS=-DKSS_SPREAD_TRACE=1; tools/split_trace_test.py reads it): per (pod, shard)
+// G_TW words (GT_* below), and a list of every nonzero resident count a shard loads in its
+// prologue and writes back in its epilogue.  Light on purpose (no extra barrier, a few
+// stores per pod): the failure it hunts is timing-dependent.  The product build compiles
+// none of it.
+#ifndef KSS_SPREAD_TRACE
+#define KSS_SPREAD_TRACE 0
+#endif
+constexpr int G_TW = 128;
+enum : int {
+  GT_LOCAL = 0,      // [32] the shard's bins after its statistics pass
+  GT_XBINS = 32,     // [32] the bins after the statistics exchange
+  GT_MINIMA = 64,    // [5] critical-path minima and flags after the exchange
+  GT_EPOCH = 69,
+  GT_REREAD = 71,    // nodes whose first-group count differs between two reads around the pass
+  GT_BAD_ST = 72,    // staged static words that differ from HBM
+  GT_BAD_REC = 73,   // staged record words that differ from HBM (every pod, at its commit)
+  GT_BAD_LBL = 74,   // staged label ids that differ from HBM
+  GT_KEY = 75,       // [3] selectHost key lo, hi, seen
+  GT_NF = 78,
+  GT_CHOSEN = 79,
+  GT_CMT = 80,       // [8] the winner shard's commit: n_cmt, then (resident row, count before) pairs
+  GT_PRO = 88,       // nonzero bins of the first pod's range right after the prologue zeroed them
+};
+constexpr int G_TLIST = 1 << 20;  // entries of the count list: {tag, row, node, value}; tag = k0 (load) or -1 - k1 (store)
+struct GTrace {
+  int32_t* words;  // [n][W][G_TW]
+  int32_t* list;   // [0]: entries used, then G_TLIST entries of 4 words
+};
+
 // One topology spread constraint.  v1.26 keys PodTopologySpread's counts by topology pair,
 // not by constraint: constraints of one kind on one key form a group led by its first member
 // (`own`), which holds the group's histogram (members share off / poff).  DoNotSchedule: per
@@ -718,10 +749,21 @@ __device__ __forceinline__ int64_t g_ipa_score(const SpreadShard& L, const GPod&
   return v;
 }
 
+#if KSS_SPREAD_TRACE
+// trace: stats_node's count of the first hard group at slot s (-1: not counted)
+__device__ __forceinline__ int32_t trace_eff(const SpreadShard& L, const GPod& q, int s, uint32_t wd) {
+  if (q.n_hard <= 0 || !g_has_keys(L, q.sp, q.n_hard, s)) return -1;
+  int32_t eff = -1;
+  for (int j = 0; j < q.n_hard; j++)
+    if (q.sp[j].own == 0 && g_policy(q.sp[j], wd)) eff = g_sum(L, q, q.sp[j].ri_off, q.sp[j].ri_len, s);
+  return eff;
+}
+#endif
+
 // The batch for shard w of one cluster, pods [k0, k1).  res_rows: the resident count rows
 // (class r as r, term r as n_classes + r), n_res of them.
 template <bool DEF>
-__device__ __forceinline__ void spread_schedule(int32_t* dbg, DevCluster c, const GPod* __restrict__ gpods,
+__device__ __forceinline__ void spread_schedule(const GTrace& tr, DevCluster c, const GPod* __restrict__ gpods,
                                                 const uint32_t* __restrict__ stat, const int32_t* __restrict__ res_rows,
                                                 int n_res, int k0, int k1, int32_t* chosen, PodMeta* meta,
                                                 const kss_profile& prof, int W, int w, int cap, int bins_cap, int gq,
@@ -768,6 +810,18 @@ __device__ __forceinline__ void spread_schedule(int32_t* dbg, DevCluster c, cons
     const int32_t v = row < c.n_classes ? ld_ag(&c.class_count[(size_t)row * N + lo + s])
                                         : ld_ag(&c.term_count[(size_t)(row - c.n_classes) * N + lo + s]);
     L.cnt[r * cap + s] = (uint16_t)v;
+#if KSS_SPREAD_TRACE
+    if (v && tr.list) {
+      const int e = atomicAdd(tr.list, 1);
+      if (e < G_TLIST) {
+        int32_t* E = tr.list + 4 + 4 * (size_t)e;
+        E[0] = k0;
+        E[1] = row;
+        E[2] = lo + s;
+        E[3] = v;
+      }
+    }
+#endif
   }
   const uint4* grec = reinterpret_cast<const uint4*>(gpods);
   for (int i = tid; i < min(k1 - k0, 2) * gq; i += nt) {
@@ -782,6 +836,15 @@ __device__ __forceinline__ void spread_schedule(int32_t* dbg, DevCluster c, cons
       for (int b = tid; b < q0.total_bins + q0.total_pbins; b += nt) L.xs[G_NS + b] = 0;
   }
   __syncthreads();
+#if KSS_SPREAD_TRACE
+  {
+    const GPod& q0 = *reinterpret_cast<const GPod*>(L.ring + (k0 % 3) * gq);
+    int nz = 0;
+    if (q0.dyn.status == 0 && q0.need_stats)
+      for (int b = tid; b < q0.total_bins + q0.total_pbins; b += nt) nz += bins[b] != 0 ? 1 : 0;
+    if (nz) atomicAdd(&tr.words[((size_t)k0 * W + w) * G_TW + GT_PRO], nz);
+  }
+#endif
 
   KSS_GLOBAL const uint32_t* gstat = gp(stat);
   KSS_GLOBAL const uint4* ggq = gp(grec);
@@ -836,25 +899,40 @@ __device__ __forceinline__ void spread_schedule(int32_t* dbg, DevCluster c, cons
     int32_t flags = 0, hard_min[MAXH];
 #pragma unroll
     for (int i = 0; i < MAXH; i++) hard_min[i] = INT32_MAX;
+#if KSS_SPREAD_TRACE
+    int32_t* tw = tr.words + ((size_t)k * W + w) * G_TW;
+#endif
     // ---- stats: PodTopologySpread PreFilter, InterPodAffinity PreFilter / PreScore ----
     if (KSS_SPREAD_SAFE) lds_barrier();
     if (evaluated && q.need_stats) {
+#if KSS_SPREAD_TRACE
+      uint32_t th0 = 0;  // a hash of the first hard group's count per node, read before the pass
+      for (int s = tid; s < own; s += nt) th0 = th0 * 31u + (uint32_t)trace_eff(L, q, s, sw[s]) + 7u * (uint32_t)s;
+#endif
       // bins zeroed at the end of the previous pod (or in the prologue), behind its barrier
       for (int s = tid; s < own; s += nt) stats_node(L, q, s, sw[s], bins, hard_min, flags);
       GSTAMP(1);
-      const int nbd = min(26, q.total_bins + q.hard_pbins);
-      if (dbg) {  // diagnosis (KSS_SPREAD_DEBUG): this shard's bins before the exchange, and
-        // whether the staged static words / record of this pod equal their HBM sources
+#if KSS_SPREAD_TRACE
+      {  // this shard's bins before the exchange; staged inputs against their HBM sources
         lds_barrier();
-        for (int b = tid; b < nbd; b += nt) dbg[((size_t)k * W + w) * 64 + b] = bins[b];
-        int bad_w = 0, bad_r = 0;
-        for (int s2 = tid; s2 < own; s2 += nt) bad_w += sw[s2] != ld_ag(&stat[(size_t)(k - k0) * N + lo + s2]) ? 1 : 0;
+        const int nbd = min(32, q.total_bins + q.hard_pbins);
+        for (int b = tid; b < nbd; b += nt) tw[GT_LOCAL + b] = bins[b];
+        int bad_w = 0, bad_r = 0, bad_l = 0;
+        uint32_t th1 = 0;
+        for (int s2 = tid; s2 < own; s2 += nt) {
+          bad_w += sw[s2] != ld_ag(&stat[(size_t)(k - k0) * N + lo + s2]) ? 1 : 0;
+          for (int x = 0; x < c.n_keys; x++) bad_l += L.lbl[x * cap + s2] != ld_ag(&c.label_value[(size_t)x * N + lo + s2]) ? 1 : 0;
+          th1 = th1 * 31u + (uint32_t)trace_eff(L, q, s2, sw[s2]) + 7u * (uint32_t)s2;
+        }
         const uint32_t* rl = reinterpret_cast<const uint32_t*>(L.ring + (k % 3) * gq);
         const uint32_t* rg = reinterpret_cast<const uint32_t*>(grec + (size_t)k * gq);
         for (int i = tid; i < 4 * gq; i += nt) bad_r += rl[i] != ld_ag(&rg[i]) ? 1 : 0;
-        if (bad_w) atomicAdd(&dbg[((size_t)k * W + w) * 64 + 29], bad_w);
-        if (bad_r) atomicAdd(&dbg[((size_t)k * W + w) * 64 + 30], bad_r);
+        if (bad_w) atomicAdd(&tw[GT_BAD_ST], bad_w);
+        if (bad_r) atomicAdd(&tw[GT_BAD_REC], bad_r);
+        if (bad_l) atomicAdd(&tw[GT_BAD_LBL], bad_l);
+        if (th0 != th1) atomicAdd(&tw[GT_REREAD], 1);
       }
+#endif
       int32_t v[MAXH + 1];
       const int op[MAXH + 1] = {OP_MIN, OP_MIN, OP_MIN, OP_MIN, OP_OR};
 #pragma unroll
@@ -868,11 +946,14 @@ __device__ __forceinline__ void spread_schedule(int32_t* dbg, DevCluster c, cons
 #pragma unroll
       for (int i = 0; i < MAXH; i++) hard_min[i] = v[i];
       flags = v[MAXH];
-      if (dbg) {  // ... and the exchanged bins, minima and flags
-        for (int b = tid; b < nbd; b += nt) dbg[((size_t)k * W + w) * 64 + 32 + b] = bins[b];
-        if (tid < MAXH + 1) dbg[((size_t)k * W + w) * 64 + 58 + tid] = v[tid];
-        if (tid == 0) dbg[((size_t)k * W + w) * 64 + 63] = (int32_t)epoch;
+#if KSS_SPREAD_TRACE
+      {  // ... and the exchanged bins, minima and flags
+        const int nbd = min(32, q.total_bins + q.hard_pbins);
+        for (int b = tid; b < nbd; b += nt) tw[GT_XBINS + b] = bins[b];
+        if (tid < MAXH + 1) tw[GT_MINIMA + tid] = v[tid];
+        if (tid == 0) tw[GT_EPOCH] = (int32_t)epoch;
       }
+#endif
       GSTAMP(2);
     }
     // ---- filter + raw scores ----
@@ -1125,16 +1206,22 @@ __device__ __forceinline__ void spread_schedule(int32_t* dbg, DevCluster c, cons
       if (!spread_argmax(H, W, w, epoch, gran, X, err, kparity, best)) return;
       GSTAMP(8);
       kparity ^= 1;
-      if (dbg && tid == 0) {  // diagnosis: this shard's view of the selectHost key
-        dbg[((size_t)k * W + w) * 64 + 26] = (int32_t)(uint32_t)(unsigned long long)best;
-        dbg[((size_t)k * W + w) * 64 + 27] = (int32_t)(uint32_t)((unsigned long long)best >> 32);
-        dbg[((size_t)k * W + w) * 64 + 28] = 1;
+#if KSS_SPREAD_TRACE
+      if (tid == 0) {  // this shard's view of the selectHost key
+        tw[GT_KEY] = (int32_t)(uint32_t)(unsigned long long)best;
+        tw[GT_KEY + 1] = (int32_t)(uint32_t)((unsigned long long)best >> 32);
+        tw[GT_KEY + 2] = 1;
+        tw[GT_NF] = nf;
       }
+#endif
       const unsigned long long ub = (unsigned long long)best;
       m.chosen = best ? (int)(0xFFFFFFFFull - (ub & 0xFFFFFFFFull)) : -1;
       m.scored = scored ? 1 : 0;
       m.best_total = scored ? (int64_t)(ub >> 32) : 0;
     }
+#if KSS_SPREAD_TRACE
+    if (tid == 0) tw[GT_CHOSEN] = m.chosen;
+#endif
     // ---- outcome (shard 0) and AssumePod on the winner's shard ----
     const int x = m.chosen >= 0 ? m.chosen - c.node_base : -1;
     const bool won = x >= lo && x < hi;
@@ -1158,6 +1245,22 @@ __device__ __forceinline__ void spread_schedule(int32_t* dbg, DevCluster c, cons
           __hip_atomic_fetch_add(a, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
+#if KSS_SPREAD_TRACE
+    {  // this pod's staged record against HBM (every pod), and the winner's commit
+      int bad_r = 0;
+      const uint32_t* rl = reinterpret_cast<const uint32_t*>(L.ring + (k % 3) * gq);
+      const uint32_t* rg = reinterpret_cast<const uint32_t*>(grec + (size_t)k * gq);
+      for (int i = tid; i < 4 * gq; i += nt) bad_r += rl[i] != ld_ag(&rg[i]) ? 1 : 0;
+      if (bad_r) atomicAdd(&tw[GT_BAD_REC], bad_r);
+      if (won && tid == 0) {
+        tw[GT_CMT] = q.n_cmt;
+        for (int i = 0; i < q.n_cmt && i < 3; i++) {
+          tw[GT_CMT + 1 + 2 * i] = q.cmt[i];
+          tw[GT_CMT + 2 + 2 * i] = q.cmt[i] >= 0 ? (int32_t)L.cnt[q.cmt[i] * cap + (x - lo)] : -1;
+        }
+      }
+    }
+#endif
     if (won && tid == 0) {
       const int s = x - lo;
       const SPod& pk = q.dyn;
@@ -1208,6 +1311,18 @@ __device__ __forceinline__ void spread_schedule(int32_t* dbg, DevCluster c, cons
     const int32_t v = L.cnt[r * cap + s];
     if (row < c.n_classes) st_ag(&c.class_count[(size_t)row * N + lo + s], v);
     else st_ag(&c.term_count[(size_t)(row - c.n_classes) * N + lo + s], v);
+#if KSS_SPREAD_TRACE
+    if (v && tr.list) {
+      const int e = atomicAdd(tr.list, 1);
+      if (e < G_TLIST) {
+        int32_t* E = tr.list + 4 + 4 * (size_t)e;
+        E[0] = -1 - k1;
+        E[1] = row;
+        E[2] = lo + s;
+        E[3] = v;
+      }
+    }
+#endif
   }
 }
 

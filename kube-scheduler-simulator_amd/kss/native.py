@@ -52,7 +52,6 @@ SIGNATURES = [
     ("kss_service_stop", C.c_int, [C.c_void_p]),
     ("kss_service_eval", C.c_int, [C.c_void_p, C.c_int32, C.c_uint32, P(abi.PodView)]),
     ("kss_service_eval_compact", C.c_int, [C.c_void_p, C.c_int32, C.c_uint32, P(abi.PodCView)]),
-    ("kss_debug_spread", C.c_int, [C.c_void_p, P(C.c_int32), C.c_int64]),
     ("kss_service_commit", C.c_int, [C.c_void_p, C.c_int32, C.c_int32]),
     ("kss_service_rollback", C.c_int, [C.c_void_p, C.c_int32, C.c_int32]),
     ("kss_service_stamps", C.c_int, [C.c_void_p, P(C.c_uint64)]),

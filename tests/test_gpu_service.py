@@ -107,6 +107,32 @@ def test_service_restarts_after_idle_exit_and_yields_to_other_calls():
     s.close()
 
 
+def test_commit_after_idle_exit_is_applied():
+    """A commit posted after the grid left idle is not dropped: the grid is relaunched for it
+    (ADVICE r3), also when the next call stops the service right away."""
+    s = native.Synth(2, SEED_BASE + 2, 3000, 40)
+    ctx = native.Context(abi.default_profile())
+    ctx.load(s.cluster)
+    ctx.stage(s.pods)
+    a = _copy(ctx.service_eval(0))
+    time.sleep(2.5)  # the grid leaves after ~1 s idle
+    ctx.service_commit(0, a.chosen)
+    st = ctx.node_state()  # stops the service: the queued commit must be in the state
+    assert st["pod_count"][a.chosen] == s.cluster.pod_count[a.chosen] + 1
+    b = _copy(ctx.service_eval(1))
+    time.sleep(2.5)
+    ctx.service_commit(1, b.chosen)
+    time.sleep(2.5)  # the relaunched grid leaves idle again after taking the commit
+    ctx.service_rollback(1, b.chosen)
+    ctx.service_stop()
+    st2 = ctx.node_state()
+    assert st2["pod_count"][a.chosen] == s.cluster.pod_count[a.chosen] + 1
+    if b.chosen != a.chosen:
+        assert st2["pod_count"][b.chosen] == s.cluster.pod_count[b.chosen]
+    ctx.close()
+    s.close()
+
+
 @pytest.mark.parametrize("config,n_nodes,n_pods", [(2, 5000, 40), (3, 2000, 30), (4, 6000, 24)])
 def test_service_compact_record_equals_full(config, n_nodes, n_pods):
     """kss_service_eval_compact (scores narrowed on the device: int32 raw / total, uint8

@@ -18,14 +18,6 @@ pytestmark = pytest.mark.gpu
 THREADS = min(16, os.cpu_count() or 1)
 
 
-def _spread_dump(ctx, n, W):
-    """KSS_SPREAD_DEBUG: k_spread's per-pod, per-shard statistics (kss_debug_spread), [n][W][64]."""
-    import ctypes as C
-    out = np.zeros(n * W * 64, np.int32)
-    native.check(min(0, native.lib().kss_debug_spread(ctx.h, out.ctypes.data_as(C.POINTER(C.c_int32)), out.size)))
-    return out.reshape(n, W, 64)
-
-
 def _oracle(s, n_pods):
     return oracle_c.schedule(abi.default_profile(), s.cluster, s.pods, n_pods, s.n_nodes, record="meta",
                              threads=THREADS, n_classes=s.cluster.n_classes, n_terms=s.cluster.n_terms)
@@ -77,46 +69,29 @@ def test_parts_over_many_chunks(monkeypatch, config, n_nodes, n_pods, per_chunk,
     s = native.Synth(config, SEED_BASE + config, n_nodes, n_pods)
     ch_o, res, st = _oracle(s, n_pods)
     sp = split.InProcessSplit(s.cluster, s.pods, 2, wl)
-    dumps = []
+    N = n_nodes
     for rep in range(3):
         sp.reset()
         outs = sp.run(n_pods)
-        if os.environ.get("KSS_SPREAD_DEBUG") and sp.ctxs[0].last_kernel() == "k_spread":
-            dumps.append([_spread_dump(c, n_pods, 2 * wl) for c in sp.ctxs])
         bad = [np.flatnonzero(np.asarray(ch) != ch_o) for ch in outs]
         if any(len(b) for b in bad):  # what went wrong, for the record: pod, chunk position, outcomes
             j = int(next(b for b in bad if len(b))[0])
             meta = [c.fetch_meta(n_pods)[j].tolist() for c in sp.ctxs]
             m = res.meta(j)
-            if dumps:  # KSS_SPREAD_DEBUG: pods whose selectHost key some shard saw differently
-                key = np.concatenate([dumps[-1][p][:, p * wl:(p + 1) * wl, 26:29] for p in range(2)], axis=1)
-                seen = key[:, :, 2] == 1
-                dis = [int(k) for k in range(n_pods) if seen[k].any() and
-                       len({tuple(key[k, w, :2]) for w in range(2 * wl) if seen[k, w]}) > 1]
-                print("pods whose key differs between shards:", dis[:10])
-                stg = np.concatenate([dumps[-1][p][:, p * wl:(p + 1) * wl, 29:31] for p in range(2)], axis=1)
-                print("(pod, shard, static words, record words) staged differently from HBM:",
-                      [(int(a), int(b), int(stg[a, b, 0]), int(stg[a, b, 1])) for a, b in zip(*np.nonzero(stg.any(axis=2)))][:12])
-                for k in dis[:3]:
-                    print(f"  pod {k}:", [(w, int(key[k, w, 0]), int(key[k, w, 1])) for w in range(2 * wl) if seen[k, w]])
-            if len(dumps) > 1:  # KSS_SPREAD_DEBUG: which shard's statistics of pod j differ from run 0's
-                for p in range(2):
-                    own = slice(p * wl, (p + 1) * wl)
-                    dl = (dumps[0][p][:, own, :26] != dumps[-1][p][:, own, :26]).any(axis=2)  # [pod][shard]
-                    print(f"part {p}: (pod, shard) pairs whose local bins differ from run 0:",
-                          [(int(a), int(b) + p * wl) for a, b in zip(*np.nonzero(dl))][:20])
-                    a, b = dumps[0][p][j], dumps[-1][p][j]
-                    own = range(p * wl, (p + 1) * wl)
-                    print(f"part {p} pod {j}: local bins differing (shard, bin, run0, now)",
-                          [(w, i, int(a[w, i]), int(b[w, i])) for w in own for i in range(26) if a[w, i] != b[w, i]][:16])
-                    print(f"part {p} pod {j}: exchanged values differing (shard, slot, run0, now)",
-                          [(w, i, int(a[w, i]), int(b[w, i])) for w in own for i in range(32, 64) if a[w, i] != b[w, i]][:16])
             pytest.fail(f"run {rep}: mismatching pods per part {[b.tolist() for b in bad]}; first {j} = chunk "
                         f"{j // per_chunk} pod {j % per_chunk}; device {[o[j] for o in outs]} meta {meta}; oracle "
                         f"{ch_o[j]} meta {[m['chosen'], m['n_feasible'], m['scored'], m['status'], m['best_total']]}")
         assert sp.ctxs[0].last_timing()[1] == 2 * -(-n_pods // per_chunk)  # k_static + loop per chunk
-    g = sp.node_state()
-    np.testing.assert_array_equal(g["requested"][:, :n_nodes], st["requested"][:, :n_nodes])
+        # the node state every run leaves, count rows included (a wrong count need not change a choice)
+        g = sp.node_state()
+        np.testing.assert_array_equal(g["requested"][:, :N], st["requested"][:, :N], err_msg=f"run {rep}")
+        np.testing.assert_array_equal(g["pod_count"][:N], st["pod_count"][:N], err_msg=f"run {rep}")
+        if s.cluster.n_classes:
+            np.testing.assert_array_equal(g["class_count"][:s.cluster.n_classes, :N], st["class_count"][:, :N],
+                                          err_msg=f"run {rep}")
+        if s.cluster.n_terms:
+            np.testing.assert_array_equal(g["term_count"][:s.cluster.n_terms, :N], st["term_count"][:, :N],
+                                          err_msg=f"run {rep}")
     sp.close()
 
 
