@@ -240,7 +240,7 @@ __global__ __launch_bounds__(KSS_MAX_THREADS) void k_simple(const DevJob* __rest
 // presence values of the exchange vector.  DEF: the v1.26 default profile, folded.
 template <bool DEF>
 __global__ __launch_bounds__(KSS_MAX_THREADS) void k_spread(const DevJob* __restrict__ jobs, int W, int cap, int bins_cap,
-                                                            int n_res, int gq, int k0, int k1, unsigned long long* gran,
+                                                            int n_res, int gq, int gs, int k0, int k1, unsigned long long* gran,
                                                             int* err, unsigned long long* stamps, int nst, XPeers X,
                                                             unsigned epoch0) {
   extern __shared__ __attribute__((aligned(16))) long long smem[];
@@ -249,6 +249,14 @@ __global__ __launch_bounds__(KSS_MAX_THREADS) void k_spread(const DevJob* __rest
   const DevJob job = jobs[ji];
   constexpr kss_profile def_prof = default_profile_c();
   SpreadHdr& H = *reinterpret_cast<SpreadHdr*>(smem);
+#ifdef KSS_LDS_POISON  // experiment builds: the shard's LDS image filled with a pattern first
+  {
+    const size_t words = spread_lds_bytes(cap, bins_cap, job.c.n_keys, n_res, gq) / 4;
+    uint32_t* p = reinterpret_cast<uint32_t*>(smem);
+    for (size_t i = threadIdx.x; i < words; i += blockDim.x) p[i] = 0x5A5A5A5Au;
+    __syncthreads();
+  }
+#endif
   if (!DEF) {
     const uint32_t* src = reinterpret_cast<const uint32_t*>(&jobs[ji].prof);
     uint32_t* dst = reinterpret_cast<uint32_t*>(&H.prof);
@@ -257,7 +265,7 @@ __global__ __launch_bounds__(KSS_MAX_THREADS) void k_spread(const DevJob* __rest
   }
   const kss_profile& P = DEF ? def_prof : H.prof;
   spread_schedule<DEF>(job.trace, job.c, job.gpods, job.stat, job.res_rows, n_res, k0, min(k1, job.n_pods), job.chosen, job.meta, P, W, w,
-                  cap, bins_cap, gq, gran ? gran + (size_t)ji * 2 * W * G_XW : nullptr, X, epoch0, err, stamps, nst, smem);
+                  cap, bins_cap, gq, gs, gran ? gran + (size_t)ji * 2 * W * gs : nullptr, X, epoch0, err, stamps, nst, smem);
 }
 
 // Class / term counts of the chosen nodes of pods [k0, min(k1, n_pods)) of every job
@@ -267,6 +275,7 @@ __global__ __launch_bounds__(256) void k_counts(const DevJob* __restrict__ jobs,
   const int k = k0 + (int)(blockIdx.x * 256 + threadIdx.x);
   if (k >= min(k1, job.n_pods) || !job.chosen) return;
   simple_counts(job.c, job.spods, job.P.ints, job.chosen, k);
+  handoff_drain();
 }
 
 // Static words of pods [k0, min(k1, n_pods)) x every node of every job.  grid: x = 256-node
@@ -291,6 +300,7 @@ __global__ __launch_bounds__(256) void k_static(const DevJob* __restrict__ jobs,
     if (k >= kend) break;
     st_ag(&stat[(size_t)(k - k0) * N + n], static_word(c, P, P.pods[k], prof, n, flags, th, ts));  // sc1: read by the next launch
   }
+  handoff_drain();  // lanes past the rows returned: no workgroup barrier here
 }
 
 __global__ void k_go_log(const double* x, double* y, int n) {
@@ -322,6 +332,7 @@ __global__ void k_commit(DevCluster c, CommitArgs a) {
   if (a.port_add) c.port_used[a.local] = a.sign > 0 ? (c.port_used[a.local] | a.port_add) : (c.port_used[a.local] & ~a.port_add);
   for (int i = 0; i < a.n_vrow; i++) vol_commit_row(c, a.vrow[i], a.local, a.sign);
   for (int i = 0; i < a.n_vpriv; i++) c.vol_attached[(size_t)a.vpriv_key[i] * N + a.local] += a.sign * a.vpriv_cnt[i];
+  handoff_drain();
 }
 
 // DefaultPreemption PostFilter dry run of one pod (kss_postfilter_pod): three launches.
@@ -344,6 +355,7 @@ __global__ void k_volume_delta(DevCluster c, const int32_t* node, const int32_t*
                                          : c.vol_attached + (size_t)(row[i] - c.n_vol_rows) * N + node[i];
     *cell = mode ? val[i] : *cell + val[i];
   }
+  handoff_drain();
 }
 
 // Delta sync of node rows (kss_apply_node_delta): one packed upload, one scatter.
@@ -357,6 +369,7 @@ __global__ void k_node_delta(DevCluster c, const int32_t* idx, const int64_t* re
   c.nonzero[r0] = nz[2 * (size_t)i];
   c.nonzero[N + r0] = nz[2 * (size_t)i + 1];
   c.pod_count[r0] = pc[i];
+  handoff_drain();
 }
 
 // Class / term count sync (kss_apply_count_delta): add (mode 0) or overwrite (mode 1).
@@ -368,6 +381,22 @@ __global__ void k_count_delta(DevCluster c, const int32_t* node, const int32_t* 
                                        : c.term_count + (size_t)(row[i] - c.n_classes) * N + node[i];
   if (mode) *cell = val[i];
   else atomicAdd(cell, val[i]);
+  handoff_drain();
+}
+
+// kss_reset_node_state: the mutable columns back to their load-time copy, as a kernel (the
+// same hand-off path as every other writer of node state, not a copy engine): up to 8
+// (destination, source, 32-bit words) ranges, grid-stride, agent-scope stores.
+struct ResetArgs {
+  uint32_t* dst[8];
+  const uint32_t* src[8];
+  size_t n4[8];
+};
+__global__ __launch_bounds__(256) void k_reset_state(ResetArgs a) {
+  for (int r = 0; r < 8; r++)
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < a.n4[r]; i += (size_t)gridDim.x * blockDim.x)
+      st_ag(a.dst[r] + i, ld_ag(a.src[r] + i));
+  handoff_release();
 }
 
 // ---------------------------------------------------------------------------
@@ -384,21 +413,20 @@ struct DevBuf {
     size_t nb = std::max(bytes, (size_t)4096);
     if (hipMalloc(&p, nb) != hipSuccess) return fail(KSS_E_NOMEM, "hipMalloc failed");
     cap = nb;
-    // diagnostic (KSS_POISON=all, or =i: only the i-th allocation of the process): fresh
-    // buffers hold a byte pattern, not the zeros a new process tends to get, so a read of
-    // never-written memory shows up in a short run
+#ifdef KSS_EXPERIMENTS
+    // diagnostic (experiment builds, KSS_POISON=all, or =i: only the i-th allocation of the
+    // process): fresh buffers hold a byte pattern, not the zeros a new process tends to get
     static const char* poison = getenv("KSS_POISON");
     static std::atomic<int> n_alloc{0};
     if (poison) {
       const int i = n_alloc++;
       const bool all = std::strcmp(poison, "all") == 0;
       if (all || atoi(poison) == i) {
-        fprintf(stderr, "kss poison: allocation %d, %zu bytes\n", i, nb);
-        // complete before the caller's own stream touches the buffer (null-stream memset)
         if (hipMemset(p, 0xA5, nb) != hipSuccess || hipDeviceSynchronize() != hipSuccess)
           return fail(KSS_E_NOMEM, "poison memset failed");
       }
     }
+#endif
     return 0;
   }
   void release() {
@@ -423,6 +451,8 @@ struct GpodNeeds {
   int64_t max_skew = 0;   // their largest maxSkew
   std::vector<int32_t> res_rows;  // the resident count rows: class r as r, term r as n_classes + r
   int gq = 0;             // record stride (uint4) of the batch
+  int xw = 2;             // longest exchange of the batch (values per shard; the argmax's 2 at least)
+  int gs() const { return (xw + 15) / 16 * 16; }  // granule stride per shard: whole 128-byte lines
   int fail_code = 0, fail_pod = -1;  // why / where build_gpods refused (GP_*)
 };
 
@@ -460,6 +490,10 @@ struct kss_ctx {
   kss_cluster host{};  // sizes only (pointers not retained)
   DevCluster dc{};
   DevBuf cluster_buf;
+#ifdef KSS_UNCACHED_STATE
+  void* state_unc = nullptr;  // experiment: the mutable columns in uncached device memory
+  size_t state_unc_bytes = 0;
+#endif
   DevBuf pristine_buf;  // load-time copy of the mutable columns (kss_reset_node_state)
   size_t mut_bytes[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   size_t pristine_off[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -1063,6 +1097,7 @@ bool build_gpods(const kss_podset* ps, int n_scalar, int n_classes, const int32_
     if (off + poff > LDS_BINS || off > 32767 || poff > 32767) return gfail(need, GP_BINS, i);
     // exchanges: E1 (scalars + bins), E2 (scalars + soft presence)
     if (MAXH + 1 + off + g.hard_pbins > G_XW || 13 + (poff - g.hard_pbins) > G_XW) return gfail(need, GP_XW, i);
+    need.xw = std::max(need.xw, std::max(MAXH + 1 + off + g.hard_pbins, 13 + (poff - g.hard_pbins)));
     need.bins_cap = std::max(need.bins_cap, off + poff);
     // AssumePod's count rows: the pod's class, its own term rows
     if (1 + p.own_terms_len > G_CMT) return gfail(need, GP_COMMIT, i);
@@ -1448,6 +1483,32 @@ int kss_load_cluster(kss_ctx* ctx, const kss_cluster* cl) {
   std::vector<double> logtab;
   rc = fill_cluster(ctx->stream, cl, class_cap, term_cap, (char*)ctx->cluster_buf.p, L, ctx->dc, logtab);
   if (rc) return rc;
+#ifdef KSS_UNCACHED_STATE
+  {  // experiment: move the mutable columns into uncached device memory
+    const size_t N0 = (size_t)cl->n_nodes;
+    const size_t ub[8] = {8 * KSS_NRES * N0, 8 * 2 * N0, 4 * N0, 4 * (size_t)class_cap * N0, 4 * (size_t)term_cap * N0,
+                          8 * N0, 4 * (size_t)cl->n_vol_rows * N0, 4 * (size_t)cl->n_vol_keys * N0};
+    size_t tot = 0, off[8];
+    for (int i = 0; i < 8; i++) {
+      off[i] = tot;
+      tot = align_up(tot + std::max<size_t>(ub[i], 8), 256);
+    }
+    if (ctx->state_unc) hipFree(ctx->state_unc);
+    ctx->state_unc = nullptr;
+    if (hipExtMallocWithFlags(&ctx->state_unc, tot, hipDeviceMallocUncached) != hipSuccess)
+      return fail(KSS_E_NOMEM, "uncached state allocation failed");
+    ctx->state_unc_bytes = tot;
+    void** col[8] = {(void**)&ctx->dc.requested, (void**)&ctx->dc.nonzero,   (void**)&ctx->dc.pod_count,
+                     (void**)&ctx->dc.class_count, (void**)&ctx->dc.term_count, (void**)&ctx->dc.port_used,
+                     (void**)&ctx->dc.vol_count, (void**)&ctx->dc.vol_attached};
+    for (int i = 0; i < 8; i++) {
+      char* d = (char*)ctx->state_unc + off[i];
+      if (ub[i]) HIP_TRY(hipMemcpyAsync(d, *col[i], ub[i], hipMemcpyDeviceToDevice, ctx->stream));
+      *col[i] = d;
+    }
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+  }
+#endif
   // pristine copy of the mutable columns
   const size_t N = (size_t)cl->n_nodes;
   const size_t mb[8] = {8 * KSS_NRES * N,          8 * 2 * N, 4 * N, 4 * (size_t)class_cap * N, 4 * (size_t)term_cap * N,
@@ -1656,10 +1717,24 @@ int kss_reset_node_state(kss_ctx* ctx) {
   ctx->bound_log.clear();
   ctx->bound_dirty = true;
   ctx->state_unknown = false;
+  ResetArgs a{};
+  size_t most = 0;
+  for (int i = 0; i < 8; i++) {
+    a.dst[i] = (uint32_t*)dst[i];
+    a.src[i] = (const uint32_t*)((char*)ctx->pristine_buf.p + ctx->pristine_off[i]);
+    a.n4[i] = ctx->mut_bytes[i] / 4;
+    most = std::max(most, a.n4[i]);
+  }
+#ifdef KSS_NO_HANDOFF  // experiment builds: the round-3 copy-engine reset
   for (int i = 0; i < 8; i++)
-    if (ctx->mut_bytes[i])
-      HIP_TRY(hipMemcpyAsync(dst[i], (char*)ctx->pristine_buf.p + ctx->pristine_off[i], ctx->mut_bytes[i],
-                             hipMemcpyDeviceToDevice, ctx->stream));
+    if (ctx->mut_bytes[i]) HIP_TRY(hipMemcpyAsync(dst[i], a.src[i], ctx->mut_bytes[i], hipMemcpyDeviceToDevice, ctx->stream));
+  most = 0;
+#endif
+  if (most) {
+    hipLaunchKernelGGL(k_reset_state, dim3((unsigned)std::min<size_t>(1024, (most + 255) / 256)), dim3(256), 0,
+                       ctx->stream, a);
+    HIP_TRY(hipGetLastError());
+  }
   HIP_TRY(hipStreamSynchronize(ctx->stream));
   return 0;
 }
@@ -2214,15 +2289,17 @@ static int launch_spread(hipStream_t st, const Geometry& g, const GpodNeeds& q, 
                          const DevJob* jobs, const kss_profile& prof, int n_pods, int max_nodes, int chunk,
                          unsigned long long* gran, size_t gran_bytes, int* err, unsigned long long* stamps = nullptr,
                          hipEvent_t* ev = nullptr, const SplitRun* split = nullptr) {
-  int cap = spread_cap(g, (size_t)max_nodes), bins_cap = q.bins_cap, nr = n_res, gq = q.gq;
+  int cap = spread_cap(g, (size_t)max_nodes), bins_cap = q.bins_cap, nr = n_res, gq = q.gq, gs = q.gs();
   size_t shmem = spread_lds(g, q, n_keys, n_res, (size_t)max_nodes);
   // diagnostic stamps in LDS: as many pods (<= G_NSTAMP, >= 8) as fit beside the shard state
   int nst = 0;
   if (stamps && shmem < KSS_LDS_BUDGET) nst = (int)std::min<size_t>(G_NSTAMP, (KSS_LDS_BUDGET - shmem) / (16 * 8));
   if (nst < 8) stamps = nullptr, nst = 0;
   shmem += (size_t)nst * 16 * 8;
+#ifdef KSS_EXPERIMENTS
   if (const char* e = getenv("KSS_SPREAD_MIN_LDS"))  // diagnosis: at most one shard per CU
     shmem = std::max(shmem, std::min((size_t)KSS_LDS_BUDGET, (size_t)std::max(0, atoi(e))));
+#endif
   const bool def = same_profile(prof, default_profile_c());
   const void* fn = def ? (const void*)k_spread<true> : (const void*)k_spread<false>;
   HIP_TRY(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shmem));
@@ -2249,7 +2326,7 @@ static int launch_spread(hipStream_t st, const Geometry& g, const GpodNeeds& q, 
       HIP_TRY(hipMemsetAsync(gran, 0, gran_bytes, st));
     }
     unsigned long long* sp = k0 == 0 ? stamps : nullptr;
-    void* args[] = {(void*)&jobs, (void*)&W,  (void*)&cap, (void*)&bins_cap, (void*)&nr,  (void*)&gq, (void*)&k0,
+    void* args[] = {(void*)&jobs, (void*)&W,  (void*)&cap, (void*)&bins_cap, (void*)&nr,  (void*)&gq, (void*)&gs, (void*)&k0,
                     (void*)&k1,   (void*)&gc, (void*)&err, (void*)&sp,       (void*)&nst, (void*)&X,  (void*)&epoch0};
     const int ci = k0 / chunk;
     if (ev) HIP_TRY(hipEventRecord(ev[2 * ci], st));
@@ -3070,7 +3147,10 @@ static int svc_launch(kss_ctx* ctx) {
   unsigned long long* seenp = relay + 2 * SVC_DRING;
   uint8_t* rec = v.rec_dev;
   unsigned long long s0 = seq0;
-  int stamps = (getenv("KSS_SERVICE_STAMPS") ? 1 : 0) | (getenv("KSS_SERVICE_NO_DIFF") ? 2 : 0);
+  int stamps = getenv("KSS_SERVICE_STAMPS") ? 1 : 0;
+#ifdef KSS_EXPERIMENTS
+  if (getenv("KSS_SERVICE_NO_DIFF")) stamps |= 2;  // every requested row resent (no row diff)
+#endif
   void* args[] = {(void*)&jd,  (void*)&pr,  (void*)&W,     (void*)&npt,   (void*)&bins, (void*)&ck, (void*)&gran,
                   (void*)&err, (void*)&box, (void*)&relay, (void*)&seenp, (void*)&rec, (void*)&s0, (void*)&stamps};
   if (int rc = launch_resident(fn, dim3((unsigned)W), dim3((unsigned)v.threads), args, v.shmem, v.stream)) return rc;
@@ -3114,7 +3194,12 @@ static int svc_start_locked(kss_ctx* ctx) {
   const size_t rec_bytes = SL.bytes + CompactLayout(N).bytes;  // the full record, then the compact one
   if (v.rec_bytes < rec_bytes) {
     svc_free_rec(v);
-    if (getenv("KSS_SVC_HUGE")) {
+#ifdef KSS_EXPERIMENTS
+    const bool huge = getenv("KSS_SVC_HUGE") != nullptr;
+#else
+    constexpr bool huge = false;
+#endif
+    if (huge) {
       // experiment: the record in transparent huge pages (madvise), registered with the device,
       // so that its rows do not each take their own 4 KiB translation
       const size_t H = (size_t)2 << 20, sz = align_up(rec_bytes, H);

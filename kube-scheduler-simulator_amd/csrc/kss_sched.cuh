@@ -43,7 +43,17 @@ constexpr int MAXWAVES = 16;
 constexpr int NSCAL = 16;      // scalar slots at the head of the exchange vector
 constexpr int LDS_BINS = 4096; // histogram + presence values per pod (device limit)
 constexpr int XW_MAX = 256;    // exchange length allowed when W > 1 (host-checked)
-constexpr unsigned SPIN_LIMIT = 1u << 20;
+// Every exchange wait is bounded by wall time (s_memrealtime, 100 MHz), read every 64
+// polls.  The bound is far above any exchange (microseconds) and above the start-up skew
+// between the parts of a split grid, whose first launches are not aligned (code-object
+// load, IPC open, a peer process starting late): the first exchange of a launch is the
+// parts' handshake.
+constexpr long long KSS_WAIT_TICKS = 1000000000ll;  // 10 s
+__device__ __forceinline__ bool spin_expired(unsigned spins, long long& t0) {
+  if (spins == 0) t0 = (long long)__builtin_amdgcn_s_memrealtime();
+  if ((spins & 63u) != 63u) return false;
+  return (long long)__builtin_amdgcn_s_memrealtime() - t0 > KSS_WAIT_TICKS;
+}
 constexpr int KSS_MAX_THREADS = 512;  // workgroup size cap (2 waves per SIMD: 256 VGPRs per lane)
 constexpr int KSS_NSTAMP_PODS = 256;  // pods with diagnostic phase stamps per launch
 constexpr int KSS_MAX_NPT = 6;
@@ -176,6 +186,7 @@ __device__ __noinline__ void shard_exchange(long long* smem, unsigned long long*
   const int Q = W * M;
   for (int q0 = 0; q0 < Q; q0 += 64 * XB) {
     unsigned long long lo[XB], hi[XB];
+    long long t0_ = 0;
     for (unsigned spins = 0;; ++spins) {
       bool ok = true;
 #pragma unroll
@@ -192,7 +203,7 @@ __device__ __noinline__ void shard_exchange(long long* smem, unsigned long long*
 #pragma unroll
       for (int b = 0; b < XB; b++) ok &= ((lo[b] >> 32) == epoch) & ((hi[b] >> 32) == epoch);
       if (__all(ok)) break;
-      if (spins >= SPIN_LIMIT) {
+      if (spin_expired(spins, t0_)) {
         if (lane == 0) {
           shdr(smem).abort = 1;
           __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

@@ -61,6 +61,34 @@ __device__ __forceinline__ void st_ag(T* p, T v) {
   __hip_atomic_store(gp(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// The ends of a launch-to-launch hand-off of node state (a chunk's write-back -> the next
+// chunk's load, k_static -> the loop kernel, a reset / delta -> the next launch), in the
+// producer / consumer forms of MI355X_MICROARCH.md ("Valid forms"): every storing wave
+// waits for its own stores, then (after a workgroup barrier where the caller has one) an
+// agent-scope release writes the XCD's L2 back; the consumer starts with an agent-scope
+// acquire.  The kernel boundary alone did not order them under a concurrent split-grid part
+// (DESIGN §5).
+#ifndef KSS_NO_HANDOFF
+__device__ __forceinline__ void handoff_drain() {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+__device__ __forceinline__ void handoff_release() {  // whole workgroup, no thread exited
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) handoff_drain();
+}
+__device__ __forceinline__ void handoff_acquire() {
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+#else  // experiment builds: the round-3 hand-off (kernel boundaries only)
+__device__ __forceinline__ void handoff_drain() {}
+__device__ __forceinline__ void handoff_release() {}
+__device__ __forceinline__ void handoff_acquire() {}
+#endif
+
 // Publish one granule at offset `off` of the exchange buffer (the local inbox `gran`);
 // address-space-1 stores (a flat store would also count in lgkmcnt).
 __device__ __forceinline__ void xpub(const XPeers& X, unsigned long long* gran, size_t off, unsigned long long v) {
@@ -436,6 +464,7 @@ __device__ __forceinline__ bool simple_exchange(SimpleHdr& H, unsigned long long
     if (ch * 64 >= W) continue;
     const int s = ch * 64 + lane;
     const bool valid = s < W;
+    long long t0_ = 0;
     for (unsigned spins = 0;; ++spins) {
       bool ok = true;
       unsigned long long g[SX_VALS];
@@ -449,7 +478,7 @@ __device__ __forceinline__ bool simple_exchange(SimpleHdr& H, unsigned long long
         got[ch][i] = valid ? (uint32_t)g[i] : 0u;
       }
       if (__all(ok)) break;
-      if (spins >= SPIN_LIMIT) {
+      if (spin_expired(spins, t0_)) {
         if (lane == 0) {
           H.abort = 1;
           __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -823,6 +852,7 @@ __device__ __forceinline__ void simple_schedule(DevCluster c, const SPod* __rest
   // its prefetch stores land one pod earlier (behind two barriers) than the pass that reads them.
   constexpr int PD = PW ? 3 : 2;
   // shard rows, reciprocals, static words and records of pods k0 .. k0 + PD - 1 -> LDS
+  handoff_acquire();
   for (int s = tid; s < own; s += nt) {
     const int n = lo + s;
 #pragma unroll
@@ -1000,6 +1030,7 @@ __device__ __forceinline__ void simple_schedule(DevCluster c, const SPod* __rest
     st_ag(&c.nonzero[N + n], (int64_t)L.r64[7 * cap + s]);
     st_ag(&c.pod_count[n], L.r32[s]);
   }
+  handoff_release();
 }
 
 // The class / term count part of AssumePod for pods [k0, k1) of a k_simple batch, from

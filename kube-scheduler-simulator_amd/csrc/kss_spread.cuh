@@ -35,13 +35,18 @@ constexpr int G_QMAX = 128;  // uint4 per record (header + references; host-chec
 constexpr int G_IPA = 16;    // inter-pod-affinity entries per pod (score entries merged per key)
 constexpr int G_CMT = 8;     // count rows a pod's commit adds to (its class, its own term rows)
 constexpr int G_PF = 4;      // static words per prefetch lane (host-checked)
-constexpr int G_XW = 512;    // 32-bit values per shard per exchange (host-checked)
+constexpr int G_XW = 512;    // 32-bit values per shard per exchange (host-checked; the inbox is sized for it)
+// A shard's granules of one exchange sit `gs` 8-byte words after the previous shard's: the
+// batch's longest exchange rounded up to a 128-byte line (GpodNeeds::gs).  At the fixed
+// 4 KiB stride (G_XW) every shard's value j shared one page offset, so the whole grid's
+// polls and publishes went to one memory channel.
 constexpr int G_NS = 16;     // scalar slots of an exchange
 constexpr int G_SCORE = 3;   // GIpa.kind of a merged InterPodAffinity score entry (KSS_IPA_SCORE_CLASS)
 constexpr int G_NSTAMP = KSS_NSTAMP_PODS / 2;  // pods with diagnostic phase stamps, 16 per pod
 
 // Diagnostic trace, experiment builds only (make -C csrc exp EXP=trace
-// EXP_FLAGS=-DKSS_SPREAD_TRACE=1; tools/split_trace_test.py reads it): per (pod, shard)
+// EXP_FLAGS=-DKSS_SPREAD_TRACE=1, or =2 for the light form without the per-pod statistics
+// and staged-input checks; tools/split_trace_test.py reads it): per (pod, shard)
 // G_TW words (GT_* below), and a list of every nonzero resident count a shard loads in its
 // prologue and writes back in its epilogue.  Light on purpose (no extra barrier, a few
 // stores per pod): the failure it hunts is timing-dependent.  The product build compiles
@@ -309,7 +314,7 @@ constexpr int G_XS = 16;  // at most this many shards polled per lane at once (4
 #define KSS_SPREAD_MW_MIN (64 * 4)  // W x values above which every wave sweeps a share (C3: 40 x 13)
 #endif
 __device__ __forceinline__ bool spread_exchange(SpreadHdr& H, int32_t* xs, unsigned long long* gran_, const XPeers& X,
-                                                int W, int wself,
+                                                int W, int wself, int gs,
                                                 unsigned epoch, int* err, int K, unsigned opbits, int sum_lo, int ns,
                                                 int or_lo, int no, unsigned long long* sp, int gw = 0, int nsw = 1,
                                                 int phase = 3) {
@@ -324,7 +329,7 @@ __device__ __forceinline__ bool spread_exchange(SpreadHdr& H, int32_t* xs, unsig
   };
   auto opof = [&](int j) { return j < K ? (int)((opbits >> (2 * j)) & 3u) : (j < K + ns ? OP_SUM : OP_OR); };
   const unsigned long long tag = (unsigned long long)epoch << 32;
-  const size_t mine = ((size_t)(epoch & 1) * W + wself) * G_XW;
+  const size_t mine = ((size_t)(epoch & 1) * W + wself) * gs;
   for (int j = lane; (phase & 1) && j < M; j += 64) {
     int32_t* sl = slot(j);
     const int op = opof(j);
@@ -338,7 +343,7 @@ __device__ __forceinline__ bool spread_exchange(SpreadHdr& H, int32_t* xs, unsig
   }
   if (sp && lane == 0) sp[2] = wall_clock64();
   if (!(phase & 2)) return true;
-  KSS_GLOBAL const unsigned long long* base = gran + (size_t)(epoch & 1) * W * G_XW;
+  KSS_GLOBAL const unsigned long long* base = gran + (size_t)(epoch & 1) * W * gs;
   const int NL = 64 * nsw, gl = gw * 64 + lane;
   for (int j0 = 0; j0 < M; j0 += NL) {
     const int mc = min(NL, M - j0);
@@ -356,16 +361,17 @@ __device__ __forceinline__ bool spread_exchange(SpreadHdr& H, int32_t* xs, unsig
       const int jc = min(j, M - 1);
       for (int w0 = 0; w0 < W; w0 += T * XSN) {
         unsigned long long g[XSN];
+        long long t0_ = 0;
         for (unsigned spins = 0;; ++spins) {
           bool ok = true;
 #pragma unroll
           for (int b = 0; b < XSN; b++) {
             const int w = w0 + t + T * b;
-            g[b] = __hip_atomic_load(base + (size_t)min(w, W - 1) * G_XW + jc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            g[b] = __hip_atomic_load(base + (size_t)min(w, W - 1) * gs + jc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             ok &= !(act && w < W) || (g[b] >> 32) == epoch;
           }
           if (__all(ok)) break;
-          if (spins >= SPIN_LIMIT) {
+          if (spin_expired(spins, t0_)) {
             if (lane == 0) {
               H.abort = 1;
               __hip_atomic_store(gp(err), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -429,7 +435,7 @@ __device__ __forceinline__ void hard_minima(const GPod& q, int32_t* xs) {
 // statistics exchange).  LDS-only barriers (the prefetch waves' HBM loads stay in flight).
 // False on abort.
 template <int K>
-__device__ __forceinline__ bool spread_reduce(SpreadHdr& H, int32_t* xs, int W, int w, unsigned& epoch,
+__device__ __forceinline__ bool spread_reduce(SpreadHdr& H, int32_t* xs, int W, int w, int gs, unsigned& epoch,
                                               unsigned long long* gran, const XPeers& X, int* err, int32_t (&v)[K],
                                               const int (&ops)[K], int sum_lo = 0, int ns = 0, int or_lo = 0,
                                               int no = 0, bool local = false, unsigned long long* sp = nullptr,
@@ -468,17 +474,17 @@ __device__ __forceinline__ bool spread_reduce(SpreadHdr& H, int32_t* xs, int W, 
     if (sp && threadIdx.x == 0) sp[1] = wall_clock64();
     const int M = K + ns + no;
     if (nw == 1 || (long long)W * M <= (long long)KSS_SPREAD_MW_MIN) {  // one polling round for one wave: wave 0 alone
-      if (wave == 0 && spread_exchange(H, xs, gran, X, W, w, epoch, err, K, opbits, sum_lo, ns, or_lo, no, sp) &&
+      if (wave == 0 && spread_exchange(H, xs, gran, X, W, w, gs, epoch, err, K, opbits, sum_lo, ns, or_lo, no, sp) &&
           minima_q)
         hard_minima(*minima_q, xs);
       if (sp && threadIdx.x == 0) sp[4] = wall_clock64();
       lds_barrier();
       if (H.abort) return false;
     } else {  // many shards: wave 0 publishes, every wave sweeps a share (fewer polling rounds)
-      if (wave == 0) spread_exchange(H, xs, gran, X, W, w, epoch, err, K, opbits, sum_lo, ns, or_lo, no, sp, 0, 1, 1);
+      if (wave == 0) spread_exchange(H, xs, gran, X, W, w, gs, epoch, err, K, opbits, sum_lo, ns, or_lo, no, sp, 0, 1, 1);
       lds_barrier();  // the slots hold the operators' identities before any wave folds into them
       const int nsw = min(nw, KSS_SPREAD_SWEEP_WAVES);  // the sweeping waves (the rest wait)
-      if (wave < nsw) spread_exchange(H, xs, gran, X, W, w, epoch, err, K, opbits, sum_lo, ns, or_lo, no, nullptr, wave, nsw, 2);
+      if (wave < nsw) spread_exchange(H, xs, gran, X, W, w, gs, epoch, err, K, opbits, sum_lo, ns, or_lo, no, nullptr, wave, nsw, 2);
       lds_barrier();
       if (H.abort) return false;
       if (minima_q && wave == 0) hard_minima(*minima_q, xs);
@@ -495,7 +501,7 @@ __device__ __forceinline__ bool spread_reduce(SpreadHdr& H, int32_t* xs, int W, 
 }
 
 // Cluster MAX of the packed selectHost key (two granules: lo, hi).
-__device__ __forceinline__ bool spread_argmax(SpreadHdr& H, int W, int w, unsigned& epoch, unsigned long long* gran,
+__device__ __forceinline__ bool spread_argmax(SpreadHdr& H, int W, int w, int gs, unsigned& epoch, unsigned long long* gran,
                                               const XPeers& X,
                                               int* err, int parity, long long& key) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
@@ -512,14 +518,15 @@ __device__ __forceinline__ bool spread_argmax(SpreadHdr& H, int W, int w, unsign
   if (nw > 1 && W > 64) {  // every wave polls a share of the shards, 4 per lane in flight
     const unsigned long long tag = (unsigned long long)epoch << 32;
     if (wave == 0 && lane < 2)
-      xpub(X, gran, ((size_t)(epoch & 1) * W + w) * G_XW + lane,
+      xpub(X, gran, ((size_t)(epoch & 1) * W + w) * gs + lane,
            tag | (lane ? (uint32_t)((unsigned long long)best >> 32) : (uint32_t)best));
-    KSS_GLOBAL const unsigned long long* base = gp(gran) + (size_t)(epoch & 1) * W * G_XW;
+    KSS_GLOBAL const unsigned long long* base = gp(gran) + (size_t)(epoch & 1) * W * gs;
     long long m = 0;
     const int nsw = min(nw, KSS_SPREAD_SWEEP_WAVES);  // the polling waves (the rest add 0)
     const int stride = 64 * nsw;
     for (int c0 = wave * 64; wave < nsw && c0 < W; c0 += 4 * stride) {
       unsigned long long lo[4], hi[4];
+      long long t0_ = 0;
       for (unsigned spins = 0;; ++spins) {
         bool ok = true;
 #pragma unroll
@@ -527,14 +534,14 @@ __device__ __forceinline__ bool spread_argmax(SpreadHdr& H, int W, int w, unsign
           const int s = c0 + lane + b * stride;
           lo[b] = hi[b] = tag;
           if (s < W) {
-            lo[b] = __hip_atomic_load(base + (size_t)s * G_XW, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            hi[b] = __hip_atomic_load(base + (size_t)s * G_XW + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            lo[b] = __hip_atomic_load(base + (size_t)s * gs, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            hi[b] = __hip_atomic_load(base + (size_t)s * gs + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           }
         }
 #pragma unroll
         for (int b = 0; b < 4; b++) ok &= ((lo[b] >> 32) == epoch) & ((hi[b] >> 32) == epoch);
         if (__all(ok)) break;
-        if (spins >= SPIN_LIMIT) {
+        if (spin_expired(spins, t0_)) {
           if (lane == 0) {
             H.abort = 1;
             __hip_atomic_store(gp(err), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -562,20 +569,21 @@ __device__ __forceinline__ bool spread_argmax(SpreadHdr& H, int W, int w, unsign
   if (wave == 0) {
     const unsigned long long tag = (unsigned long long)epoch << 32;
     if (lane < 2)
-      xpub(X, gran, ((size_t)(epoch & 1) * W + w) * G_XW + lane,
+      xpub(X, gran, ((size_t)(epoch & 1) * W + w) * gs + lane,
            tag | (lane ? (uint32_t)((unsigned long long)best >> 32) : (uint32_t)best));
-    KSS_GLOBAL const unsigned long long* base = gp(gran) + (size_t)(epoch & 1) * W * G_XW;
+    KSS_GLOBAL const unsigned long long* base = gp(gran) + (size_t)(epoch & 1) * W * gs;
     long long m = 0;
     for (int c0 = 0; c0 < W; c0 += 64) {
       const int s = c0 + lane;
       unsigned long long lo = tag, hi = tag;
+      long long t0_ = 0;
       for (unsigned spins = 0;; ++spins) {
         if (s < W) {
-          lo = __hip_atomic_load(base + (size_t)s * G_XW, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          hi = __hip_atomic_load(base + (size_t)s * G_XW + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          lo = __hip_atomic_load(base + (size_t)s * gs, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          hi = __hip_atomic_load(base + (size_t)s * gs + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         if (__all(((lo >> 32) == epoch) & ((hi >> 32) == epoch))) break;
-        if (spins >= SPIN_LIMIT) {
+        if (spin_expired(spins, t0_)) {
           if (lane == 0) {
             H.abort = 1;
             __hip_atomic_store(gp(err), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -766,7 +774,7 @@ template <bool DEF>
 __device__ __forceinline__ void spread_schedule(const GTrace& tr, DevCluster c, const GPod* __restrict__ gpods,
                                                 const uint32_t* __restrict__ stat, const int32_t* __restrict__ res_rows,
                                                 int n_res, int k0, int k1, int32_t* chosen, PodMeta* meta,
-                                                const kss_profile& prof, int W, int w, int cap, int bins_cap, int gq,
+                                                const kss_profile& prof, int W, int w, int cap, int bins_cap, int gq, int gs,
                                                 unsigned long long* gran, const XPeers& X, unsigned epoch0, int* err,
                                                 unsigned long long* stamps, int nst,
                                                 long long* smem) {
@@ -788,6 +796,7 @@ __device__ __forceinline__ void spread_schedule(const GTrace& tr, DevCluster c, 
     for (int i = tid; i < 16 * nst; i += nt) stl[i] = 0;
   // shard state -> LDS: node rows, label ids, resident count rows, static words of pod k0,
   // records of pods k0 and k0 + 1
+  handoff_acquire();
   for (int s = tid; s < own; s += nt) {
     const int n = lo + s;
 #pragma unroll
@@ -905,14 +914,14 @@ __device__ __forceinline__ void spread_schedule(const GTrace& tr, DevCluster c, 
     // ---- stats: PodTopologySpread PreFilter, InterPodAffinity PreFilter / PreScore ----
     if (KSS_SPREAD_SAFE) lds_barrier();
     if (evaluated && q.need_stats) {
-#if KSS_SPREAD_TRACE
+#if KSS_SPREAD_TRACE == 1
       uint32_t th0 = 0;  // a hash of the first hard group's count per node, read before the pass
       for (int s = tid; s < own; s += nt) th0 = th0 * 31u + (uint32_t)trace_eff(L, q, s, sw[s]) + 7u * (uint32_t)s;
 #endif
       // bins zeroed at the end of the previous pod (or in the prologue), behind its barrier
       for (int s = tid; s < own; s += nt) stats_node(L, q, s, sw[s], bins, hard_min, flags);
       GSTAMP(1);
-#if KSS_SPREAD_TRACE
+#if KSS_SPREAD_TRACE == 1
       {  // this shard's bins before the exchange; staged inputs against their HBM sources
         lds_barrier();
         const int nbd = min(32, q.total_bins + q.hard_pbins);
@@ -940,13 +949,13 @@ __device__ __forceinline__ void spread_schedule(const GTrace& tr, DevCluster c, 
       v[MAXH] = flags;
       // histogram SUM over every bin, hard-pair presence OR (soft presence, still zero, is
       // filled by the filter pass), then the critical-path minima
-      if (!spread_reduce(H, L.xs, W, w, epoch, gran, X, err, v, op, 0, q.total_bins, q.total_bins, q.hard_pbins, false,
+      if (!spread_reduce(H, L.xs, W, w, gs, epoch, gran, X, err, v, op, 0, q.total_bins, q.total_bins, q.hard_pbins, false,
                          nullptr, &q))
         return;
 #pragma unroll
       for (int i = 0; i < MAXH; i++) hard_min[i] = v[i];
       flags = v[MAXH];
-#if KSS_SPREAD_TRACE
+#if KSS_SPREAD_TRACE == 1
       {  // ... and the exchanged bins, minima and flags
         const int nbd = min(32, q.total_bins + q.hard_pbins);
         for (int b = tid; b < nbd; b += nt) tw[GT_XBINS + b] = bins[b];
@@ -1048,7 +1057,7 @@ __device__ __forceinline__ void spread_schedule(const GTrace& tr, DevCluster c, 
       if (!has_soft && !has_ipa) {
         int32_t v[3] = {nf, max_tt, max_na};
         const int op[3] = {OP_SUM, OP_MAX, OP_MAX};
-        if (!spread_reduce(H, L.xs, W, w, epoch, gran, X, err, v, op, 0, 0, 0, 0, false, est)) return;
+        if (!spread_reduce(H, L.xs, W, w, gs, epoch, gran, X, err, v, op, 0, 0, 0, 0, false, est)) return;
         nf = v[0];
         max_tt = v[1];
         max_na = v[2];
@@ -1057,7 +1066,7 @@ __device__ __forceinline__ void spread_schedule(const GTrace& tr, DevCluster c, 
                          sdirect[2], sdirect[3], cmin, cmax};
         const int op[13] = {OP_SUM, OP_SUM, OP_MAX, OP_MAX, OP_MIN, OP_MAX, OP_OR, OP_SUM, OP_SUM, OP_SUM, OP_SUM,
                             OP_MIN, OP_MAX};
-        if (!spread_reduce(H, L.xs, W, w, epoch, gran, X, err, v, op, 0, 0, q.total_bins + q.hard_pbins,
+        if (!spread_reduce(H, L.xs, W, w, gs, epoch, gran, X, err, v, op, 0, 0, q.total_bins + q.hard_pbins,
                            q.total_pbins - q.hard_pbins, false, est))
           return;
         nf = v[0];
@@ -1093,7 +1102,7 @@ __device__ __forceinline__ void spread_schedule(const GTrace& tr, DevCluster c, 
           for (int b = tid; b < sp.nb; b += nt) sz[i] += bins[q.total_bins + sp.poff + b] ? 1 : 0;
         }
         const int ops4[MAXS] = {OP_SUM, OP_SUM, OP_SUM, OP_SUM};
-        spread_reduce(H, L.xs, W, w, epoch, gran, X, err, sz, ops4, 0, 0, 0, 0, /*local=*/true);
+        spread_reduce(H, L.xs, W, w, gs, epoch, gran, X, err, sz, ops4, 0, 0, 0, 0, /*local=*/true);
         for (int i = 0; i < q.n_soft; i++) {
           const GSpread& sp = soft[i];
           long long size;  // topoSize: a group's domains count for its leader only
@@ -1149,7 +1158,7 @@ __device__ __forceinline__ void spread_schedule(const GTrace& tr, DevCluster c, 
           // 32-bit extrema: raw scores are host-bounded (spread_bounds_ok)
           int32_t v2[2] = {(int32_t)min(pmin, (long long)INT32_MAX), (int32_t)pmax};
           const int op2[2] = {OP_MIN, OP_MAX};
-          if (!spread_reduce(H, L.xs, W, w, epoch, gran, X, err, v2, op2)) return;
+          if (!spread_reduce(H, L.xs, W, w, gs, epoch, gran, X, err, v2, op2)) return;
           pts_min = v2[0] == INT32_MAX ? INT64_MAX : v2[0];
           pts_max = v2[1];
           GSTAMP(6);
@@ -1203,7 +1212,7 @@ __device__ __forceinline__ void spread_schedule(const GTrace& tr, DevCluster c, 
         best = key > best ? key : best;
       }
       GSTAMP(7);
-      if (!spread_argmax(H, W, w, epoch, gran, X, err, kparity, best)) return;
+      if (!spread_argmax(H, W, w, gs, epoch, gran, X, err, kparity, best)) return;
       GSTAMP(8);
       kparity ^= 1;
 #if KSS_SPREAD_TRACE
@@ -1247,11 +1256,13 @@ __device__ __forceinline__ void spread_schedule(const GTrace& tr, DevCluster c, 
     }
 #if KSS_SPREAD_TRACE
     {  // this pod's staged record against HBM (every pod), and the winner's commit
+#if KSS_SPREAD_TRACE == 1
       int bad_r = 0;
       const uint32_t* rl = reinterpret_cast<const uint32_t*>(L.ring + (k % 3) * gq);
       const uint32_t* rg = reinterpret_cast<const uint32_t*>(grec + (size_t)k * gq);
       for (int i = tid; i < 4 * gq; i += nt) bad_r += rl[i] != ld_ag(&rg[i]) ? 1 : 0;
       if (bad_r) atomicAdd(&tw[GT_BAD_REC], bad_r);
+#endif
       if (won && tid == 0) {
         tw[GT_CMT] = q.n_cmt;
         for (int i = 0; i < q.n_cmt && i < 3; i++) {
@@ -1324,6 +1335,7 @@ __device__ __forceinline__ void spread_schedule(const GTrace& tr, DevCluster c, 
     }
 #endif
   }
+  handoff_release();
 }
 
 }  // namespace kss

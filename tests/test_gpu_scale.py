@@ -177,6 +177,29 @@ def test_c4_recipe_on_one_gpu(kernel, n_pods, monkeypatch):
     ctx.close()
 
 
+def test_c4_bench_shape_many_chunks(monkeypatch):
+    """The shape bench.py's C4 leg times: unsplit k_spread on BASELINE configs[3]'s recipe
+    and seed at 100,000 nodes over several k_static chunks (the bench runs 8 per step);
+    KSS_STATIC_BYTES forces 4 chunks of 1,250 pods, so node state and count rows cross three
+    launch boundaries.  Chosen nodes, per-pod outcomes and the final state with the class
+    counts against the C oracle."""
+    n_nodes, n_pods, per_chunk = 100000, 5000, 1250
+    monkeypatch.setenv("KSS_STATIC_BYTES", str(4 * n_nodes * per_chunk))
+    prof = abi.default_profile()
+    s = native.Synth(4, SEED_BASE + 4, n_nodes, n_pods)
+    chosen_o, res, st = _oracle(prof, s, n_pods, record="meta")
+    ctx = native.Context(prof)
+    ctx.load(s.cluster)
+    ctx.stage(s.pods)
+    chosen = ctx.run_staged(n_pods)
+    assert ctx.last_kernel() == "k_spread"
+    assert ctx.last_timing()[1] == 2 * (n_pods // per_chunk)  # k_static + k_spread per chunk
+    np.testing.assert_array_equal(chosen, chosen_o)
+    _meta_equal(ctx.fetch_meta(n_pods), res, n_pods)
+    _state_equal(ctx, st, n_nodes, s.cluster.n_classes, 0)
+    ctx.close()
+
+
 def test_nodeaxis_100k_rows_world1():
     n_nodes, n_pods = 100000, 300
     prof = abi.default_profile()

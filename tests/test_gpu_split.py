@@ -86,12 +86,11 @@ def test_parts_over_many_chunks(monkeypatch, config, n_nodes, n_pods, per_chunk,
         g = sp.node_state()
         np.testing.assert_array_equal(g["requested"][:, :N], st["requested"][:, :N], err_msg=f"run {rep}")
         np.testing.assert_array_equal(g["pod_count"][:N], st["pod_count"][:N], err_msg=f"run {rep}")
-        if s.cluster.n_classes:
-            np.testing.assert_array_equal(g["class_count"][:s.cluster.n_classes, :N], st["class_count"][:, :N],
-                                          err_msg=f"run {rep}")
-        if s.cluster.n_terms:
-            np.testing.assert_array_equal(g["term_count"][:s.cluster.n_terms, :N], st["term_count"][:, :N],
-                                          err_msg=f"run {rep}")
+        for key, n_rows in (("class_count", s.cluster.n_classes), ("term_count", s.cluster.n_terms)):
+            if n_rows:
+                d = np.argwhere(g[key][:n_rows, :N] != st[key][:n_rows, :N])
+                assert not len(d), (f"run {rep}: {key} differs at (row, node, device, oracle) " + str(
+                    [(int(a), int(b), int(g[key][a, b]), int(st[key][a, b])) for a, b in d[:8]]))
     sp.close()
 
 
@@ -161,6 +160,28 @@ def test_failed_run_refuses_until_rearmed():
     sp.reset()
     for p, ch in enumerate(sp.run(40)):
         np.testing.assert_array_equal(ch, ch_o, err_msg=f"part {p}")
+    sp.close()
+
+
+def test_parts_start_apart():
+    """Part 1 launches its grid 2 s after part 0 (a peer process that starts late: module
+    load, IPC open): part 0's first exchange waits for it -- every exchange wait is bounded
+    by wall time (10 s), not by a poll count -- and both parts equal the oracle, twice."""
+    import time
+    config, n_nodes, n_pods, wl = 4, 20000, 300, 32
+    s = native.Synth(config, SEED_BASE + config, n_nodes, n_pods)
+    ch_o, _, _ = _oracle(s, n_pods)
+    sp = split.InProcessSplit(s.cluster, s.pods, 2, wl)
+
+    def late(c):
+        time.sleep(2.0)
+        return c.run_staged(n_pods)
+
+    for rep, (a, b) in enumerate([(0, 1), (1, 0)]):  # each part once the late one
+        sp.reset()
+        outs = split._run_concurrently([lambda: sp.ctxs[a].run_staged(n_pods), lambda: late(sp.ctxs[b])])
+        for p, ch in zip((a, b), outs):
+            np.testing.assert_array_equal(ch, ch_o, err_msg=f"part {p} (late part {b})")
     sp.close()
 
 

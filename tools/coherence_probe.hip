@@ -28,7 +28,7 @@
     }                                                                                         \
   } while (0)
 
-constexpr int SLICE = 2048;  // int32 words per workgroup (8 KiB)
+constexpr int SLICE = 2048;
 
 __device__ __forceinline__ int xcc_id() {
   int v;
@@ -100,6 +100,67 @@ __global__ void k_noise(int* junk, int n) {
   if (i < n) junk[i] += 1;
 }
 
+// a part-1-like poller on another stream: 16 workgroups polling uncached memory with
+// system-scope loads (s_sleep(1) between polls) until `ticks` of the 100 MHz clock pass
+__global__ void k_poll(const unsigned long long* inbox, long long ticks, int* sink) {
+  const long long t0 = wall_clock64();
+  unsigned long long acc = 0;
+  while (wall_clock64() - t0 < ticks) {
+    acc += __hip_atomic_load(inbox + (threadIdx.x & 511), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __builtin_amdgcn_s_sleep(1);
+  }
+  if (acc == 12345) sink[0] = 1;
+}
+
+// writer whose every wave drains its stores (vmcnt(0)), then one agent release per workgroup
+__global__ void k_write_drain(int* buf, int tag) {
+  int* s = buf + (size_t)blockIdx.x * SLICE;
+  int acc = 0;
+  for (int i = threadIdx.x; i < SLICE; i += blockDim.x) acc += __hip_atomic_load(s + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  for (int i = threadIdx.x; i < SLICE; i += blockDim.x) __hip_atomic_store(s + i, tag + (acc & 0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+}
+
+// the split grid's exchange traffic: granules on the first line of 4 KiB blocks (G_XW = 512
+// u64 per shard), polled with agent-scope loads and stored with system-scope stores, in
+// uncached memory, by `npoll` workgroups, until `ticks` pass
+__global__ void k_gran_poll(unsigned long long* inbox, int blocks, long long ticks, int* sink) {
+  const long long t0 = wall_clock64();
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  unsigned long long acc = 0;
+  unsigned it = 0;
+  while (wall_clock64() - t0 < ticks) {
+    const int b = (lane + wave * 64 + (int)it) % blocks;
+    unsigned long long* g = inbox + (size_t)b * 512 + (lane & 15);
+    acc += __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (wave == 0 && lane < 16 && (it & 7) == 0)
+      __hip_atomic_store(inbox + (size_t)((blockIdx.x + it) % blocks) * 512 + lane, acc + it, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_SYSTEM);
+    ++it;
+    __builtin_amdgcn_s_sleep(1);
+  }
+  if (acc == 12345) sink[0] = 1;
+}
+
+// every stale word's page-offset line (0 = the first 128 B of a 4 KiB page)
+template <int LD>
+__global__ void k_read_all_lines(const int* buf, size_t n, int tag, int* stale, int* by_line) {
+  int bad = 0;
+  for (size_t i = threadIdx.x; i < n; i += blockDim.x) {
+    const int v = LD ? __hip_atomic_load(buf + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : buf[i];
+    if (v != tag) {
+      bad++;
+      atomicAdd(&by_line[(i * 4 % 4096) / 128], 1);
+    }
+  }
+  if (bad) atomicAdd(&stale[blockIdx.x], bad);
+}
+
 enum Reset { R_MEMCPY_D2D, R_MEMCPY_H2D, R_MEMSET, R_KERNEL };
 enum Alloc { A_DEFAULT, A_UNCACHED, A_FINE };
 
@@ -141,6 +202,95 @@ int main(int argc, char** argv) {
   CHECK(hipHostMalloc(&zero_pinned, bytes, hipHostMallocDefault));
   memset(zero_pinned, 0, bytes);
   CHECK(hipDeviceSynchronize());
+  // the hand-off under granule traffic on the first lines of 4 KiB blocks (mode 3)
+  if (argc > 2 && atoi(argv[2]) == 3) {
+    hipStream_t nb;
+    CHECK(hipStreamCreateWithFlags(&nb, hipStreamNonBlocking));
+    const int blocks = 64;
+    unsigned long long* inbox;
+    CHECK(hipExtMallocWithFlags((void**)&inbox, (size_t)blocks * 4096, hipDeviceMallocUncached));
+    CHECK(hipMemset(inbox, 0, (size_t)blocks * 4096));
+    int *sink, *by_line;
+    CHECK(hipMalloc(&sink, 64));
+    CHECK(hipMalloc(&by_line, 4 * 32));
+    CHECK(hipMemset(by_line, 0, 4 * 32));
+    int* buf = nullptr;
+    CHECK(hipMalloc(&buf, bytes));
+    CHECK(hipMemset(buf, 0, bytes));
+    CHECK(hipDeviceSynchronize());
+    long long bad_words = 0, bad_iters = 0, total = 0;
+    for (int it = 0; it < iters; it++) {
+      hipLaunchKernelGGL(k_gran_poll, dim3(32), dim3(512), 0, nb, inbox, blocks, 200000LL, sink);  // ~2 ms
+      for (int rep = 0; rep < 8; rep++) {
+        const int t = 8 * it + rep;
+        hipLaunchKernelGGL((k_read_all_lines<1>), dim3(G), dim3(256), 0, st, buf, n, t, stale_d, by_line);
+        hipLaunchKernelGGL((k_write<1, 1>), dim3(G), dim3(256), 0, st, buf, t + 1, xw_d);
+        CHECK(hipMemsetAsync(stale_d, 0, 4 * G, st));
+        hipLaunchKernelGGL((k_read_all_lines<1>), dim3(G), dim3(256), 0, st, buf, n, t + 1, stale_d, by_line);
+        CHECK(hipGetLastError());
+        CHECK(hipMemcpyAsync(stale.data(), stale_d, 4 * G, hipMemcpyDeviceToHost, st));
+        CHECK(hipStreamSynchronize(st));
+        long long b = 0;
+        for (int g = 0; g < G; g++) b += stale[g];
+        bad_words += b;
+        bad_iters += b != 0;
+        total++;
+      }
+      CHECK(hipStreamSynchronize(nb));
+    }
+    std::vector<int> bl(32);
+    CHECK(hipMemcpy(bl.data(), by_line, 4 * 32, hipMemcpyDeviceToHost));
+    printf("granule traffic: hand-off stale words %lld, hand-offs with stale %lld of %lld; stale by page line:", bad_words,
+           bad_iters, total);
+    for (int i = 0; i < 32; i++) printf(" %d", bl[i]);
+    printf("\n");
+    return 0;
+  }
+  // the hand-off while a second stream's persistent grid polls uncached memory (the split
+  // grid's other part): mode 0 plain end, 1 drained + released end; each with / without reset
+  if (argc > 2 && atoi(argv[2]) == 2) {
+    hipStream_t nb;
+    CHECK(hipStreamCreateWithFlags(&nb, hipStreamNonBlocking));
+    unsigned long long* inbox;
+    CHECK(hipExtMallocWithFlags((void**)&inbox, 1 << 16, hipDeviceMallocUncached));
+    CHECK(hipMemset(inbox, 0, 1 << 16));
+    int* sink;
+    CHECK(hipMalloc(&sink, 64));
+    const char* nm[] = {"poll: hand-off plain end", "poll: hand-off drained end", "poll: reset, plain end",
+                        "poll: reset, drained end"};
+    for (int mode = 0; mode < 4; mode++) {
+      int* buf = nullptr;
+      CHECK(hipMalloc(&buf, bytes));
+      CHECK(hipMemset(buf, 0, bytes));
+      CHECK(hipDeviceSynchronize());
+      long long bad_words = 0, bad_iters = 0;
+      const bool drain = mode & 1, reset = mode >= 2;
+      for (int it = 0; it < iters; it++) {
+        hipLaunchKernelGGL(k_poll, dim3(16), dim3(512), 0, nb, inbox, 100000LL, sink);  // ~1 ms
+        for (int rep = 0; rep < 4; rep++) {
+          const int t0 = reset ? 0 : 4 * it + rep, t1 = reset ? 0 : 4 * it + rep + 1;
+          hipLaunchKernelGGL((k_read_all<1, 0>), dim3(G), dim3(256), 0, st, buf, n, t0, stale_d);
+          if (drain) hipLaunchKernelGGL(k_write_drain, dim3(G), dim3(256), 0, st, buf, 4 * it + rep + 1);
+          else hipLaunchKernelGGL((k_write<1, 1>), dim3(G), dim3(256), 0, st, buf, 4 * it + rep + 1, xw_d);
+          if (reset) CHECK(hipMemcpyAsync(buf, zero_d, bytes, hipMemcpyDeviceToDevice, st));
+          CHECK(hipMemsetAsync(stale_d, 0, 4 * G, st));
+          hipLaunchKernelGGL((k_read_all<1, 0>), dim3(G), dim3(256), 0, st, buf, n, t1, stale_d);
+          CHECK(hipGetLastError());
+          CHECK(hipMemcpyAsync(stale.data(), stale_d, 4 * G, hipMemcpyDeviceToHost, st));
+          CHECK(hipStreamSynchronize(st));
+          long long b = 0;
+          for (int g = 0; g < G; g++) b += stale[g];
+          bad_words += b;
+          bad_iters += b != 0;
+        }
+        CHECK(hipStreamSynchronize(nb));
+      }
+      printf("%-34s stale words %lld, hand-offs with stale %lld of %d\n", nm[mode], bad_words, bad_iters, 4 * iters);
+      fflush(stdout);
+      CHECK(hipFree(buf));
+    }
+    return 0;
+  }
   // the hand-off (agent ld/st, d2d reset) while a second stream launches short kernels
   if (argc > 2 && atoi(argv[2]) == 1) {
     hipStream_t nb;

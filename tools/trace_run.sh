@@ -11,7 +11,8 @@ run() {  # name, env, pytest args...
   return $rc
 }
 PY="timeout -k 10 300 python -u -m pytest -m gpu -s -q --timeout 240 --timeout-method thread -p no:cacheprovider"
-run trace KSS_LIB=trace $PY tests/test_gpu_edge_fixtures.py tests/test_gpu_scale.py tools/split_trace_test.py -k 'spread or split or trace'; rc=$?
+run trace KSS_LIB=${LIB:-trace} $PY tests/test_gpu_edge_fixtures.py tests/test_gpu_scale.py tests/test_gpu_split.py::test_in_process_parts_match_oracle "tests/test_gpu_split.py::test_parts_over_many_chunks[2-3000-240-30-8]" "tests/test_gpu_split.py::test_parts_over_many_chunks[2-3000-240-31-8]" tools/split_trace_test.py -k 'spread or split or trace or in_process or many_chunks'; rc=$?
 [ $rc -le 1 ] || exit $rc
+[ -n "$NOPRODUCT" ] && exit $rc
 run product KSS_LIB=base $PY tests/test_gpu_edge_fixtures.py tests/test_gpu_scale.py tests/test_gpu_split.py -k 'spread or split'; rc=$?
 exit $rc
