@@ -632,6 +632,12 @@ int kss_last_timing(kss_ctx* ctx, double* device_ms, int32_t* launches);
 /* device time of the sequential-loop kernel alone in the last batch: the k_simple /
  * k_spread launch(es) without the k_static precompute (k_schedule batches: the whole batch) */
 int kss_last_loop_timing(kss_ctx* ctx, double* loop_ms);
+/* Node-state hand-off self-check of the last run (k_spread batches over several k_static
+ * chunks): every chunk's epilogue stores a position-mixed sum of the node state it writes back,
+ * the next chunk's prologue compares the state it loads with it and loads again while they
+ * disagree (the run fails with KSS_E_DEVICE if they never agree).  *retries = the repeated
+ * loads (0 when every hand-off was consistent at once). */
+int kss_last_handoff_retries(kss_ctx* ctx, int32_t* retries);
 /* launch geometry of the last scheduling launch: out[0] shards (workgroups) per cluster,
  * out[1] threads per workgroup, out[2] node slots per lane */
 int kss_last_geometry(kss_ctx* ctx, int32_t* out3);

@@ -242,7 +242,7 @@ template <bool DEF>
 __global__ __launch_bounds__(KSS_MAX_THREADS) void k_spread(const DevJob* __restrict__ jobs, int W, int cap, int bins_cap,
                                                             int n_res, int gq, int gs, int k0, int k1, unsigned long long* gran,
                                                             int* err, unsigned long long* stamps, int nst, XPeers X,
-                                                            unsigned epoch0) {
+                                                            unsigned epoch0, HandoffCheck hc) {
   extern __shared__ __attribute__((aligned(16))) long long smem[];
   const int Wl = X.n > 1 ? X.wl : W;
   const int ji = blockIdx.x / Wl, w = X.w_off + (int)(blockIdx.x % Wl);
@@ -265,7 +265,8 @@ __global__ __launch_bounds__(KSS_MAX_THREADS) void k_spread(const DevJob* __rest
   }
   const kss_profile& P = DEF ? def_prof : H.prof;
   spread_schedule<DEF>(job.trace, job.c, job.gpods, job.stat, job.res_rows, n_res, k0, min(k1, job.n_pods), job.chosen, job.meta, P, W, w,
-                  cap, bins_cap, gq, gs, gran ? gran + (size_t)ji * 2 * W * gs : nullptr, X, epoch0, err, stamps, nst, smem);
+                  cap, bins_cap, gq, gs, gran ? gran + (size_t)ji * 2 * W * gs : nullptr, X, epoch0, err, stamps, nst, hc,
+                  smem);
 }
 
 // Class / term counts of the chosen nodes of pods [k0, min(k1, n_pods)) of every job
@@ -515,6 +516,9 @@ struct kss_ctx {
   std::vector<int32_t> key_card_h;
   std::vector<uint32_t> key_flags_h;
   DevBuf gran_buf, err_buf;
+  DevBuf ck_buf;                    // k_spread's checked hand-off between chunks: {sum, tag} per shard
+  unsigned long long ck_seq = 0;    // the last tag a chunk wrote
+  int last_handoff_retries = 0;     // prologue loads repeated in the last run (HandoffCheck)
 #if KSS_SPREAD_TRACE
   DevBuf trace_buf, trace_list_buf;  // k_spread trace of the last run (kss_trace_spread)
   size_t trace_words = 0;
@@ -2288,7 +2292,8 @@ static bool spread_fits(const Geometry& g, const GpodNeeds& q, int n_keys, int n
 static int launch_spread(hipStream_t st, const Geometry& g, const GpodNeeds& q, int n_keys, int n_res,
                          const DevJob* jobs, const kss_profile& prof, int n_pods, int max_nodes, int chunk,
                          unsigned long long* gran, size_t gran_bytes, int* err, unsigned long long* stamps = nullptr,
-                         hipEvent_t* ev = nullptr, const SplitRun* split = nullptr) {
+                         hipEvent_t* ev = nullptr, const SplitRun* split = nullptr, unsigned long long* ck = nullptr,
+                         unsigned long long* ck_seq = nullptr) {
   int cap = spread_cap(g, (size_t)max_nodes), bins_cap = q.bins_cap, nr = n_res, gq = q.gq, gs = q.gs();
   size_t shmem = spread_lds(g, q, n_keys, n_res, (size_t)max_nodes);
   // diagnostic stamps in LDS: as many pods (<= G_NSTAMP, >= 8) as fit beside the shard state
@@ -2326,8 +2331,18 @@ static int launch_spread(hipStream_t st, const Geometry& g, const GpodNeeds& q, 
       HIP_TRY(hipMemsetAsync(gran, 0, gran_bytes, st));
     }
     unsigned long long* sp = k0 == 0 ? stamps : nullptr;
+    // the checked node-state hand-off between this call's chunks (HandoffCheck): tags increase
+    // over the context's life, the first chunk of a call checks nothing
+    HandoffCheck hc{};
+    if (ck && ck_seq && n_pods > chunk) {
+      hc.sum = ck;
+      hc.expect = k0 > 0 ? *ck_seq : 0ull;
+      hc.write = ++*ck_seq;
+      hc.retries = err + 1;
+    }
     void* args[] = {(void*)&jobs, (void*)&W,  (void*)&cap, (void*)&bins_cap, (void*)&nr,  (void*)&gq, (void*)&gs, (void*)&k0,
-                    (void*)&k1,   (void*)&gc, (void*)&err, (void*)&sp,       (void*)&nst, (void*)&X,  (void*)&epoch0};
+                    (void*)&k1,   (void*)&gc, (void*)&err, (void*)&sp,       (void*)&nst, (void*)&X,  (void*)&epoch0,
+                    (void*)&hc};
     const int ci = k0 / chunk;
     if (ev) HIP_TRY(hipEventRecord(ev[2 * ci], st));
     if (g.W > 1) {
@@ -2594,8 +2609,12 @@ static int run_single_impl(kss_ctx* ctx, const PlanNeeds& need, const DevPods& d
     rc = launch_simple(ctx->stream, g, 1, jd, ctx->prof, n, (int)N, chunk, gran, gb,
                        errp, stamps, ctx->loop_ev.data(), split ? &srun : nullptr);
   else if (spread)
+  {
+    if ((rc = ctx->ck_buf.ensure(sizeof(unsigned long long) * 2 * (size_t)g.W))) return rc;
     rc = launch_spread(ctx->stream, g, ctx->gneed, ctx->dc.n_keys, n_res, jd, ctx->prof, n,
-                       (int)N, chunk, gran, gb, errp, stamps, ctx->loop_ev.data(), split ? &srun : nullptr);
+                       (int)N, chunk, gran, gb, errp, stamps, ctx->loop_ev.data(), split ? &srun : nullptr,
+                       (unsigned long long*)ctx->ck_buf.p, &ctx->ck_seq);
+  }
   else
     rc = launch_schedule(ctx->stream, g, 1, std::max(need.bins_cap, 0), need.general, ctx->dc.n_keys,
                          jd, ctx->prof, gran, errp, stamps, epoch0);
@@ -2645,7 +2664,7 @@ static int run_single_impl(kss_ctx* ctx, const PlanNeeds& need, const DevPods& d
   const size_t o_meta = 16, o_chosen = align_up(o_meta + mb, 16), o_rb = align_up(o_chosen + cb, 16);
   if ((rc = ensure_pinned(ctx->rb, ctx->rb_cap, o_rb + (rbk ? rbk->bytes : 0)))) return rc;
   char* hb = (char*)ctx->rb;
-  HIP_TRY(hipMemcpyAsync(hb, errp, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+  HIP_TRY(hipMemcpyAsync(hb, errp, 2 * sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
   HIP_TRY(hipMemcpyAsync(hb + o_meta, ctx->meta_buf.p, mb, hipMemcpyDeviceToHost, ctx->stream));
   if (cb) HIP_TRY(hipMemcpyAsync(hb + o_chosen, ctx->chosen_buf.p, cb, hipMemcpyDeviceToHost, ctx->stream));
   if (rbk && rbk->bytes) HIP_TRY(hipMemcpyAsync(hb + o_rb, rbk->src, rbk->bytes, hipMemcpyDeviceToHost, ctx->stream));
@@ -2666,11 +2685,13 @@ static int run_single_impl(kss_ctx* ctx, const PlanNeeds& need, const DevPods& d
   ctx->last_geom[2] = g.npt;
   int errw = 0;
   std::memcpy(&errw, hb, sizeof(int));
+  std::memcpy(&ctx->last_handoff_retries, hb + sizeof(int), sizeof(int));
   if (errw && commit) {  // bounds as if every pod committed (upper bounds stay safe); log unknown
     ctx->count_bound = count_total;
     ctx->cell_bound = std::max(ctx->cell_bound, cell_total);
     ctx->state_unknown = true;
   }
+  if (errw == 2) return fail(KSS_E_DEVICE, "node state handed between chunk launches failed its check");
   if (errw) return fail(KSS_E_DEVICE, "shard exchange timed out (workgroups not co-resident?)");
   if (commit) {
     ctx->count_bound = count_total;
@@ -3467,6 +3488,12 @@ int kss_last_timing(kss_ctx* ctx, double* device_ms, int32_t* launches) {
   if (!ctx) return fail(KSS_E_INVAL, "null ctx");
   if (device_ms) *device_ms = ctx->last_ms;
   if (launches) *launches = ctx->last_launches;
+  return 0;
+}
+
+int kss_last_handoff_retries(kss_ctx* ctx, int32_t* retries) {
+  if (!ctx || !retries) return fail(KSS_E_INVAL, "bad arguments");
+  *retries = ctx->last_handoff_retries;
   return 0;
 }
 

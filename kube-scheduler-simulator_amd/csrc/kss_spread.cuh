@@ -69,6 +69,7 @@ enum : int {
   GT_CHOSEN = 79,
   GT_CMT = 80,       // [8] the winner shard's commit: n_cmt, then (resident row, count before) pairs
   GT_PRO = 88,       // nonzero bins of the first pod's range right after the prologue zeroed them
+  GT_XCC = 89,       // (first pod of a launch) the XCD the shard's workgroup runs on
 };
 constexpr int G_TLIST = 1 << 20;  // entries of the count list: {tag, row, node, value}; tag = k0 (load) or -1 - k1 (store)
 struct GTrace {
@@ -604,6 +605,65 @@ __device__ __forceinline__ bool spread_argmax(SpreadHdr& H, int W, int w, int gs
   return true;
 }
 
+// A checked hand-off of a shard's node state from one chunk launch to the next: the epilogue
+// stores, beside the state, a position-mixed sum of every word it wrote and a tag (the chunk
+// sequence number); the next chunk's prologue sums what it loaded and, while the sums
+// disagree, loads again (a bounded number of times, then the launch fails with err = 2
+// instead of scheduling on a wrong state).  hc.sum: [2 W] words {sum, tag} per shard.
+struct HandoffCheck {
+  unsigned long long* sum;  // null: no check
+  unsigned long long expect;  // tag the previous chunk wrote (0: the first chunk of the call)
+  unsigned long long write;   // tag this chunk writes
+  int* retries;               // loads repeated because the sums disagreed
+};
+__device__ __forceinline__ unsigned long long handoff_mix(unsigned long long v, size_t pos) {
+  return (v + 0x9E3779B97F4A7C15ull) * (2ull * (unsigned long long)pos + 1ull);
+}
+// Sum h over the workgroup (scratch: one slot per wave); thread 0 gets it.
+__device__ __forceinline__ unsigned long long handoff_sum(unsigned long long h, long long* scratch) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  h = (unsigned long long)wave_red<OP_SUM>((long long)h);
+  if (lane == 0) scratch[wave] = (long long)h;
+  __syncthreads();
+  unsigned long long t = 0;
+  for (int x = 0; x < nw; x++) t += (unsigned long long)scratch[x];
+  __syncthreads();
+  return t;
+}
+__device__ __forceinline__ void handoff_publish(const HandoffCheck& hc, int w, unsigned long long h, long long* scratch) {
+  const unsigned long long t = handoff_sum(h, scratch);
+  if (threadIdx.x == 0) {
+    st_ag(&hc.sum[2 * (size_t)w], t);
+    st_ag(&hc.sum[2 * (size_t)w + 1], hc.write);
+  }
+}
+// True when the loaded state matches the previous chunk's sum (or there is nothing to check).
+__device__ __forceinline__ bool handoff_verify(const HandoffCheck& hc, int w, unsigned long long h, int attempt,
+                                               long long* scratch, int* abort_flag, int* err) {
+  const unsigned long long t = handoff_sum(h, scratch);
+  if (hc.expect == 0) return true;
+  if (threadIdx.x == 0) {
+    const unsigned long long tag = ld_ag(&hc.sum[2 * (size_t)w + 1]);
+    const bool ok = tag == hc.expect && ld_ag(&hc.sum[2 * (size_t)w]) == t;
+    scratch[0] = ok ? 1 : 0;
+    if (!ok) {
+      __hip_atomic_fetch_add(hc.retries, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (attempt >= 64) {
+        *abort_flag = 1;
+        __hip_atomic_store(err, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+  }
+  __syncthreads();
+  const bool ok = scratch[0] != 0;
+  __syncthreads();
+  if (!ok && !*abort_flag) {
+    __builtin_amdgcn_s_sleep(127);
+    handoff_acquire();
+  }
+  return ok;
+}
+
 // The statistics of node slot s for pod q, accumulated into bins (SUM) / bins + total_bins
 // (presence) and hmin / flags: PodTopologySpread calPreFilterState over the DoNotSchedule
 // groups, the ScheduleAnyway pair counters (PreScore processAllNode), InterPodAffinity
@@ -776,7 +836,7 @@ __device__ __forceinline__ void spread_schedule(const GTrace& tr, DevCluster c, 
                                                 int n_res, int k0, int k1, int32_t* chosen, PodMeta* meta,
                                                 const kss_profile& prof, int W, int w, int cap, int bins_cap, int gq, int gs,
                                                 unsigned long long* gran, const XPeers& X, unsigned epoch0, int* err,
-                                                unsigned long long* stamps, int nst,
+                                                unsigned long long* stamps, int nst, const HandoffCheck& hc,
                                                 long long* smem) {
   const int tid = threadIdx.x, nt = blockDim.x;
   SpreadHdr& H = *reinterpret_cast<SpreadHdr*>(smem);
@@ -797,40 +857,61 @@ __device__ __forceinline__ void spread_schedule(const GTrace& tr, DevCluster c, 
   // shard state -> LDS: node rows, label ids, resident count rows, static words of pod k0,
   // records of pods k0 and k0 + 1
   handoff_acquire();
-  for (int s = tid; s < own; s += nt) {
+  for (int s = tid; s < own; s += nt) {  // the rows that never change
     const int n = lo + s;
 #pragma unroll
     for (int k = 0; k < 3; k++) {
       const int64_t A = c.alloc[k * N + n];
       L.r64[k * cap + s] = (double)A;
-      L.r64[(3 + k) * cap + s] = (double)ld_ag(&c.requested[k * N + n]);
       L.inv[k * cap + s] = A > 0 ? 1.0 / (double)A : 0.0;
     }
-    L.r64[6 * cap + s] = (double)ld_ag(&c.nonzero[n]);
-    L.r64[7 * cap + s] = (double)ld_ag(&c.nonzero[N + n]);
-    L.r32[s] = ld_ag(&c.pod_count[n]);
     L.r32[cap + s] = c.allowed_pods[n];
     L.r32[2 * cap + s] = (int32_t)c.node_flags[n];
     for (int k = 0; k < c.n_keys; k++) L.lbl[k * cap + s] = c.label_value[(size_t)k * N + n];
     L.st[(k0 & 1) * cap + s] = ld_ag(&stat[(size_t)lo + s]);
   }
-  for (int i = tid; i < n_res * own; i += nt) {
-    const int r = i / own, s = i - r * own, row = res_rows[r];
-    const int32_t v = row < c.n_classes ? ld_ag(&c.class_count[(size_t)row * N + lo + s])
-                                        : ld_ag(&c.term_count[(size_t)(row - c.n_classes) * N + lo + s]);
-    L.cnt[r * cap + s] = (uint16_t)v;
-#if KSS_SPREAD_TRACE
-    if (v && tr.list) {
-      const int e = atomicAdd(tr.list, 1);
-      if (e < G_TLIST) {
-        int32_t* E = tr.list + 4 + 4 * (size_t)e;
-        E[0] = k0;
-        E[1] = row;
-        E[2] = lo + s;
-        E[3] = v;
+  // node state handed over by the previous chunk: loaded, then checked against the sum its
+  // epilogue stored (HandoffCheck); loaded again until they agree, a bounded number of times
+  for (int attempt = 0;; attempt++) {
+    unsigned long long h = 0;
+    for (int s = tid; s < own; s += nt) {
+      const int n = lo + s;
+#pragma unroll
+      for (int k = 0; k < 3; k++) {
+        const int64_t R = ld_ag(&c.requested[k * N + n]);
+        L.r64[(3 + k) * cap + s] = (double)R;
+        h += handoff_mix((unsigned long long)R, (size_t)k * N + n);
       }
+      const int64_t z0 = ld_ag(&c.nonzero[n]), z1 = ld_ag(&c.nonzero[N + n]);
+      const int32_t pc = ld_ag(&c.pod_count[n]);
+      L.r64[6 * cap + s] = (double)z0;
+      L.r64[7 * cap + s] = (double)z1;
+      L.r32[s] = pc;
+      h += handoff_mix((unsigned long long)z0, 3 * N + n) + handoff_mix((unsigned long long)z1, 4 * N + n) +
+           handoff_mix((unsigned long long)(uint32_t)pc, 5 * N + n);
     }
+    for (int i = tid; i < n_res * own; i += nt) {
+      const int r = i / own, s = i - r * own, row = res_rows[r];
+      const int32_t v = row < c.n_classes ? ld_ag(&c.class_count[(size_t)row * N + lo + s])
+                                          : ld_ag(&c.term_count[(size_t)(row - c.n_classes) * N + lo + s]);
+      L.cnt[r * cap + s] = (uint16_t)v;
+      h += handoff_mix((unsigned long long)(uint32_t)v, (6 + (size_t)r) * N + lo + s);
+#if KSS_SPREAD_TRACE
+      if (v && tr.list) {
+        const int e = atomicAdd(tr.list, 1);
+        if (e < G_TLIST) {
+          int32_t* E = tr.list + 4 + 4 * (size_t)e;
+          E[0] = k0;
+          E[1] = row;
+          E[2] = lo + s;
+          E[3] = v;
+        }
+      }
 #endif
+    }
+    if (!hc.sum) break;
+    if (handoff_verify(hc, w, h, attempt, H.kx, &H.abort, err)) break;
+    if (H.abort) return;
   }
   const uint4* grec = reinterpret_cast<const uint4*>(gpods);
   for (int i = tid; i < min(k1 - k0, 2) * gq; i += nt) {
@@ -846,6 +927,11 @@ __device__ __forceinline__ void spread_schedule(const GTrace& tr, DevCluster c, 
   }
   __syncthreads();
 #if KSS_SPREAD_TRACE
+  if (tid == 0) {
+    int xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    tr.words[((size_t)k0 * W + w) * G_TW + GT_XCC] = 16 + (xcc & 0xF);
+  }
   {
     const GPod& q0 = *reinterpret_cast<const GPod*>(L.ring + (k0 % 3) * gq);
     int nz = 0;
@@ -1317,11 +1403,22 @@ __device__ __forceinline__ void spread_schedule(const GTrace& tr, DevCluster c, 
     st_ag(&c.nonzero[N + n], (int64_t)L.r64[7 * cap + s]);
     st_ag(&c.pod_count[n], L.r32[s]);
   }
+  unsigned long long h = 0;
+  if (hc.sum)
+    for (int s = tid; s < own; s += nt) {
+      const int n = lo + s;
+#pragma unroll
+      for (int k = 0; k < 3; k++) h += handoff_mix((unsigned long long)(int64_t)L.r64[(3 + k) * cap + s], (size_t)k * N + n);
+      h += handoff_mix((unsigned long long)(int64_t)L.r64[6 * cap + s], 3 * N + n) +
+           handoff_mix((unsigned long long)(int64_t)L.r64[7 * cap + s], 4 * N + n) +
+           handoff_mix((unsigned long long)(uint32_t)L.r32[s], 5 * N + n);
+    }
   for (int i = tid; i < n_res * own; i += nt) {
     const int r = i / own, s = i - r * own, row = res_rows[r];
     const int32_t v = L.cnt[r * cap + s];
     if (row < c.n_classes) st_ag(&c.class_count[(size_t)row * N + lo + s], v);
     else st_ag(&c.term_count[(size_t)(row - c.n_classes) * N + lo + s], v);
+    h += handoff_mix((unsigned long long)(uint32_t)v, (6 + (size_t)r) * N + lo + s);
 #if KSS_SPREAD_TRACE
     if (v && tr.list) {
       const int e = atomicAdd(tr.list, 1);
@@ -1335,6 +1432,7 @@ __device__ __forceinline__ void spread_schedule(const GTrace& tr, DevCluster c, 
     }
 #endif
   }
+  if (hc.sum) handoff_publish(hc, w, h, H.kx);
   handoff_release();
 }
 

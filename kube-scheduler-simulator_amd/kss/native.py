@@ -67,6 +67,7 @@ SIGNATURES = [
     ("kss_sweep_destroy", None, [C.c_void_p]),
     ("kss_last_timing", C.c_int, [C.c_void_p, P(C.c_double), P(C.c_int32)]),
     ("kss_last_loop_timing", C.c_int, [C.c_void_p, P(C.c_double)]),
+    ("kss_last_handoff_retries", C.c_int, [C.c_void_p, P(C.c_int32)]),
     ("kss_last_geometry", C.c_int, [C.c_void_p, P(C.c_int32)]),
     ("kss_last_kernel", C.c_int, [C.c_void_p]),
     ("kss_device_go_log", C.c_int, [C.c_int32, C.c_void_p, C.c_void_p, C.c_int32]),
@@ -516,6 +517,12 @@ class Context:
         ms = C.c_double(0)
         check(lib().kss_last_loop_timing(self.h, C.byref(ms)))
         return ms.value
+
+    def last_handoff_retries(self) -> int:
+        """Prologue loads of node state the last run repeated (kss_last_handoff_retries)."""
+        n = C.c_int32(0)
+        check(lib().kss_last_handoff_retries(self.h, C.byref(n)))
+        return n.value
 
     def last_geometry(self):
         out = (C.c_int32 * 3)()

@@ -11,6 +11,7 @@ import numpy as np
 import pytest
 
 import oracle_c
+import split_diag
 from kss import abi, native, split
 from kss.synth import SEED_BASE
 
@@ -70,10 +71,16 @@ def test_parts_over_many_chunks(monkeypatch, config, n_nodes, n_pods, per_chunk,
     ch_o, res, st = _oracle(s, n_pods)
     sp = split.InProcessSplit(s.cluster, s.pods, 2, wl)
     N = n_nodes
+    nc = s.cluster.n_classes
+    init_cc = np.ctypeslib.as_array(s.cluster.class_count, shape=(max(nc, 1) * N,)).reshape(max(nc, 1), N)[:nc]
     for rep in range(3):
         sp.reset()
         outs = sp.run(n_pods)
         bad = [np.flatnonzero(np.asarray(ch) != ch_o) for ch in outs]
+        g = sp.node_state()
+        if any(len(b) for b in bad) or (s.cluster.n_classes and not np.array_equal(
+                g["class_count"][:s.cluster.n_classes, :N], st["class_count"][:, :N])):
+            split_diag.report(sp, s.pods, init_cc, n_pods, wl, per_chunk, split.part_rows)  # trace builds only
         if any(len(b) for b in bad):  # what went wrong, for the record: pod, chunk position, outcomes
             j = int(next(b for b in bad if len(b))[0])
             meta = [c.fetch_meta(n_pods)[j].tolist() for c in sp.ctxs]
@@ -82,8 +89,10 @@ def test_parts_over_many_chunks(monkeypatch, config, n_nodes, n_pods, per_chunk,
                         f"{j // per_chunk} pod {j % per_chunk}; device {[o[j] for o in outs]} meta {meta}; oracle "
                         f"{ch_o[j]} meta {[m['chosen'], m['n_feasible'], m['scored'], m['status'], m['best_total']]}")
         assert sp.ctxs[0].last_timing()[1] == 2 * -(-n_pods // per_chunk)  # k_static + loop per chunk
+        retries = [c.last_handoff_retries() for c in sp.ctxs]
+        if any(retries):  # a chunk's prologue read node state that disagreed with its producer's sum
+            print(f"run {rep}: node-state hand-off reloads per part {retries}")
         # the node state every run leaves, count rows included (a wrong count need not change a choice)
-        g = sp.node_state()
         np.testing.assert_array_equal(g["requested"][:, :N], st["requested"][:, :N], err_msg=f"run {rep}")
         np.testing.assert_array_equal(g["pod_count"][:N], st["pod_count"][:N], err_msg=f"run {rep}")
         for key, n_rows in (("class_count", s.cluster.n_classes), ("term_count", s.cluster.n_terms)):
