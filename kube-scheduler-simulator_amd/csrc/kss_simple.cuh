@@ -404,6 +404,73 @@ __device__ __forceinline__ void wave_red_stats(uint32_t (&v)[6]) {
   for (int i = 0; i < 6; i++) v[i] = (uint32_t)__builtin_amdgcn_readlane((int)v[i], 63);
 }
 
+// Per-wave mode's statistics of one wave, {nf0, tt0, na0, nf1, tt1, na1}: the counts by
+// ballot, the TaintToleration maxima (7-bit raw values) as one packed 16-bit pair, so three
+// DPP chains instead of six.  Lane-uniform results.
+typedef unsigned short kss_u16x2 __attribute__((ext_vector_type(2)));
+template <int CTRL, int ROWS>
+__device__ __forceinline__ void dpp_pw_step(uint32_t& tp, uint32_t& n0, uint32_t& n1) {
+  const uint32_t a = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)tp, CTRL, ROWS, 0xF, false);
+  const uint32_t b = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)n0, CTRL, ROWS, 0xF, false);
+  const uint32_t c = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)n1, CTRL, ROWS, 0xF, false);
+  tp = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(kss_u16x2, tp),
+                                                              __builtin_bit_cast(kss_u16x2, a)));
+  n0 = max(n0, b);
+  n1 = max(n1, c);
+}
+__device__ __forceinline__ void wave_red_stats_pw(uint32_t (&v)[6]) {
+  const uint32_t nf0 = (uint32_t)__popcll(__ballot(v[0] != 0)), nf1 = (uint32_t)__popcll(__ballot(v[3] != 0));
+  uint32_t tp = v[1] | (v[4] << 16), n0 = v[2], n1 = v[5];
+  dpp_pw_step<0xB1, 0xF>(tp, n0, n1);
+  dpp_pw_step<0x4E, 0xF>(tp, n0, n1);
+  dpp_pw_step<0x141, 0xF>(tp, n0, n1);
+  dpp_pw_step<0x140, 0xF>(tp, n0, n1);
+  dpp_pw_step<0x142, 0xA>(tp, n0, n1);
+  dpp_pw_step<0x143, 0xC>(tp, n0, n1);
+  tp = (uint32_t)__builtin_amdgcn_readlane((int)tp, 63);
+  v[0] = nf0;
+  v[1] = tp & 0xFFFFu;
+  v[2] = (uint32_t)__builtin_amdgcn_readlane((int)n0, 63);
+  v[3] = nf1;
+  v[4] = tp >> 16;
+  v[5] = (uint32_t)__builtin_amdgcn_readlane((int)n1, 63);
+}
+
+// The selectHost key of a wave, reduced as 32 bits when it fits: total << kb | (2^kb - 1 -
+// local node index) keeps the order of the 64-bit key (total << 32 | ~global index) whenever
+// every total is below 2^(32 - kb) and 2^kb > N (key_bits: 0 when they do not), and
+// 0 stays "no feasible node".  One DPP max per step instead of a 64-bit compare and select.
+__device__ __forceinline__ int key_bits(const kss_profile& prof, int N) {
+  const uint32_t se = prof.score_enabled;
+  long long tmax = 0;
+  for (int p : {KSS_S_TAINT_TOLERATION, KSS_S_NODE_AFFINITY, KSS_S_NODE_RESOURCES_FIT, KSS_S_POD_TOPOLOGY_SPREAD,
+                KSS_S_BALANCED_ALLOCATION})
+    if ((se >> p) & 1u) tmax += 100ll * (long long)prof.weight[p];
+  const int kb = 32 - __clz((unsigned)max(N, 1));  // 2^kb > N
+  return tmax < (1ll << (32 - kb)) ? kb : 0;
+}
+__device__ __forceinline__ long long wave_max_key(long long key, int kb, int node_base) {
+  if (!kb) return wave_red<OP_MAX>(key);
+  const uint32_t m = (1u << kb) - 1u;
+  uint32_t k = 0;
+  if (key) {
+    const uint32_t li = (0xFFFFFFFFu - (uint32_t)(unsigned long long)key) - (uint32_t)node_base;
+    k = ((uint32_t)((unsigned long long)key >> 32) << kb) | (m - li);
+  }
+#define KSS_KSTEP(CTRL, ROWS) k = max(k, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)k, CTRL, ROWS, 0xF, false))
+  KSS_KSTEP(0xB1, 0xF);
+  KSS_KSTEP(0x4E, 0xF);
+  KSS_KSTEP(0x141, 0xF);
+  KSS_KSTEP(0x140, 0xF);
+  KSS_KSTEP(0x142, 0xA);
+  KSS_KSTEP(0x143, 0xC);
+#undef KSS_KSTEP
+  k = (uint32_t)__builtin_amdgcn_readlane((int)k, 63);
+  if (!k) return 0;
+  const uint32_t li = m - (k & m);
+  return (long long)(((unsigned long long)(k >> kb) << 32) | (0xFFFFFFFFull - ((uint32_t)node_base + li)));
+}
+
 // LDS image of the loop head: reduction scratch (double-buffered), exchange results.
 struct alignas(16) SimpleHdr {
   long long red[2][MAXWAVES][SX_VALS];
@@ -443,7 +510,7 @@ __device__ __forceinline__ void block_red(SimpleHdr& H, int parity, long long (&
 // (its node index / per) contributes H1, the others H0.  Results -> H.res.
 __device__ __forceinline__ bool simple_exchange(SimpleHdr& H, unsigned long long* gran, const XPeers& X, int W, int wself,
                                                 unsigned epoch,
-                                                int* err, const long long (&v)[7], int per, int node_base) {
+                                                int* err, const long long (&v)[7], int per, int node_base, int kb) {
   const int lane = threadIdx.x & 63;
   const unsigned long long tag = (unsigned long long)epoch << 32;
   const unsigned long long key = (unsigned long long)v[0];
@@ -490,7 +557,7 @@ __device__ __forceinline__ bool simple_exchange(SimpleHdr& H, unsigned long long
     const long long k = (long long)(((unsigned long long)got[ch][1] << 32) | got[ch][0]);
     best = k > best ? k : best;
   }
-  best = wave_red<OP_MAX>(best);
+  best = wave_max_key(best, kb, node_base);
   // the winner's shard: the one whose row range [s * per, (s + 1) * per) holds it
   const int gl = best != 0 ? (int)(0xFFFFFFFFu - (uint32_t)(unsigned long long)best) - node_base : -1;
   // {nf, tt, na} of every shard's hypothesis, reduced in one interleaved DPP pass
@@ -519,7 +586,7 @@ __device__ __forceinline__ bool simple_exchange(SimpleHdr& H, unsigned long long
 // every lane.  False if the launch aborted (exchange timeout).
 __device__ __forceinline__ bool simple_sync(SimpleHdr& H, int& parity, long long key, long long (&st)[6], int W, int w,
                                             unsigned epoch, unsigned long long* gran, const XPeers& X, int* err, int per,
-                                            int node_base,
+                                            int node_base, int kb,
                                             long long (&R)[4], KSS_GLOBAL unsigned long long* sp) {
   {
     uint32_t u[6];
@@ -553,7 +620,7 @@ __device__ __forceinline__ bool simple_sync(SimpleHdr& H, int& parity, long long
   }
   if (threadIdx.x < 64) {
     const long long v[7] = {key, st[0], st[1], st[2], st[3], st[4], st[5]};
-    simple_exchange(H, gran, X, W, w, epoch, err, v, per, node_base);
+    simple_exchange(H, gran, X, W, w, epoch, err, v, per, node_base, kb);
   }
   lds_barrier();
   if (H.abort) return false;
@@ -777,31 +844,67 @@ __device__ __forceinline__ void simple_commit_slot(const SimpleShard& L, const S
 // exchange, and pod k's AssumePod on the winner's slot by wave 0 BEFORE the closing barrier
 // (the next pod's pass A reads that row with no barrier of its own in between).
 // R = {winner key, nf, max TT, max NA of the next pod}.  False if the launch aborted.
+// `idle` runs on every wave right after the statistics barrier: the waves other than wave 0
+// wait out the exchange there (the prefetch loads are issued from it).
+template <typename Idle>
 __device__ __forceinline__ bool simple_sync_pw(SimpleHdr& H, int& parity, long long wbest, uint32_t (&u)[6], int W,
                                                int w, unsigned epoch, unsigned long long* gran, const XPeers& X,
                                                int* err, int per, int node_base, int lo, int own, const SPod& pk,
-                                               bool commit, const SimpleShard& L, long long (&R)[4],
-                                               KSS_GLOBAL unsigned long long* sp) {
-  wave_red_stats(u);
+                                               bool commit, const SimpleShard& L, int kb, long long (&R)[4],
+                                               KSS_GLOBAL unsigned long long* sp, Idle&& idle) {
+  wave_red_stats_pw(u);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  if (sp && threadIdx.x == 0) sp[7] = wall_clock64();
   if (lane == 0) {
     H.red[parity][wave][0] = wbest;
 #pragma unroll
     for (int i = 0; i < 6; i++) H.red[parity][wave][1 + i] = u[i];
   }
   lds_barrier();
-  if (wave == 0) {  // wave 0 alone combines (lane v holds wave v's values) and exchanges; the others wait
-    const bool in = lane < nw;
-    const long long* h = H.red[parity][in ? lane : 0];
-    const long long b = in ? h[0] : 0;
-    const long long best = wave_red<OP_MAX>(b);
+  if (sp && threadIdx.x == 0) sp[8] = wall_clock64();
+  idle();
+  if (wave == 0) {  // wave 0 alone combines (every lane the same few LDS words: broadcasts) and exchanges
+    // waves 0 and 1 (the usual per-wave geometry) read at once, unconditionally; waves 2.. in a loop
+    const long long* h0 = H.red[parity][0];
+    const long long* h1 = H.red[parity][nw > 1 ? 1 : 0];
+    long long a0[7], a1[7];
+#pragma unroll
+    for (int i = 0; i < 7; i++) {
+      a0[i] = h0[i];
+      a1[i] = h1[i];
+    }
+    if (nw < 2) a1[0] = 0;
     // the wave holding the shard's best (keys carry the node index: one wave at most)
-    const unsigned long long m = __ballot(in && best != 0 && b == best);
-    const int ws = m ? __ffsll((long long)m) - 1 : -1;
-    const int o = lane == ws ? 4 : 1;  // the best wave contributes its H1, the others their H0
-    uint32_t t[6] = {in ? (uint32_t)h[1] : 0u, in ? (uint32_t)h[2] : 0u, in ? (uint32_t)h[3] : 0u,
-                     in ? (uint32_t)h[o] : 0u, in ? (uint32_t)h[o + 1] : 0u, in ? (uint32_t)h[o + 2] : 0u};
-    wave_red_stats(t);
+    long long best = a0[0];
+    int ws = best ? 0 : -1;
+    if (a1[0] > best) {
+      best = a1[0];
+      ws = 1;
+    }
+    for (int v = 2; v < nw; v++) {
+      const long long b = H.red[parity][v][0];
+      ws = b > best ? v : ws;
+      best = b > best ? b : best;
+    }
+    // the best wave contributes its H1, the others their H0
+    const bool w0 = ws == 0, w1 = ws == 1;
+    uint32_t t[6];
+    t[0] = (uint32_t)a0[1] + (nw > 1 ? (uint32_t)a1[1] : 0u);
+    t[1] = max((uint32_t)a0[2], nw > 1 ? (uint32_t)a1[2] : 0u);
+    t[2] = max((uint32_t)a0[3], nw > 1 ? (uint32_t)a1[3] : 0u);
+    t[3] = (uint32_t)(w0 ? a0[4] : a0[1]) + (nw > 1 ? (uint32_t)(w1 ? a1[4] : a1[1]) : 0u);
+    t[4] = max((uint32_t)(w0 ? a0[5] : a0[2]), nw > 1 ? (uint32_t)(w1 ? a1[5] : a1[2]) : 0u);
+    t[5] = max((uint32_t)(w0 ? a0[6] : a0[3]), nw > 1 ? (uint32_t)(w1 ? a1[6] : a1[3]) : 0u);
+    for (int v = 2; v < nw; v++) {
+      const long long* h = H.red[parity][v];
+      const int o = v == ws ? 4 : 1;
+      t[0] += (uint32_t)h[1];
+      t[1] = max(t[1], (uint32_t)h[2]);
+      t[2] = max(t[2], (uint32_t)h[3]);
+      t[3] += (uint32_t)h[o];
+      t[4] = max(t[4], (uint32_t)h[o + 1]);
+      t[5] = max(t[5], (uint32_t)h[o + 2]);
+    }
     if (sp && lane == 0) sp[4] = wall_clock64();
     if (W == 1) {  // the winner (if any) is this shard's best
       if (lane == 0) {
@@ -814,7 +917,7 @@ __device__ __forceinline__ bool simple_sync_pw(SimpleHdr& H, int& parity, long l
       }
     } else {
       const long long v[7] = {best, t[0], t[1], t[2], t[3], t[4], t[5]};
-      if (simple_exchange(H, gran, X, W, w, epoch, err, v, per, node_base) && commit && lane == 0) {
+      if (simple_exchange(H, gran, X, W, w, epoch, err, v, per, node_base, kb) && commit && lane == 0) {
         const long long K = H.res[0];
         const int x = K ? (int)(0xFFFFFFFFu - (uint32_t)(unsigned long long)K) - node_base - lo : -1;
         if (x >= 0 && x < own) simple_commit_slot(L, pk, x);
@@ -887,6 +990,7 @@ __device__ __forceinline__ void simple_schedule(DevCluster c, const SPod* __rest
   const int nwave = nt >> 6;
   const int lane = tid & 63, wv = tid >> 6;
   const int pwv = (own + nwave - 1) / nwave;  // per-wave mode: the wave's node slots (<= PW_LANES)
+  const int kb = key_bits(prof, c.N);  // 32-bit key reductions when the keys fit (0: 64-bit)
   // prefetch lanes: every wave but wave 0 (readfirstlane: a wave-uniform, scalar branch)
   const bool pf_wave = nwave == 1 || __builtin_amdgcn_readfirstlane(tid >> 6) >= 1;
   uint4 pfq = make_uint4(0, 0, 0, 0);  // prefetched record / static words of pod k+PD, live across the loop
@@ -911,13 +1015,21 @@ __device__ __forceinline__ void simple_schedule(DevCluster c, const SPod* __rest
     // The branch is wave-uniform and every load inside it is unconditional (clamped
     // indices), so the compiler's wait for these registers stays on the prefetch path.
     const bool pf_on = pf_wave && k >= k0 && k + PD < k1 && own > 0;
-    if (pf_on) {
-      KSS_GLOBAL const uint4& src = gspod[(size_t)(k + PD) * NQ + min(pf_lane, NQ - 1)];
-      pfq = make_uint4(src.x, src.y, src.z, src.w);
+    auto prefetch = [&]() {
+      if (pf_on) {
+        KSS_GLOBAL const uint4& src = gspod[(size_t)(k + PD) * NQ + min(pf_lane, NQ - 1)];
+        pfq = make_uint4(src.x, src.y, src.z, src.w);
 #pragma unroll
-      for (int j = 0; j < PF_MAX; j++)
-        if (j < pf_per) pfw[j] = ld_ag(&gstat[(size_t)(k + PD - k0) * N + lo + min(j * pf_n + pf_lane, own - 1)]);
-    }
+        for (int j = 0; j < PF_MAX; j++)
+          if (j < pf_per) pfw[j] = ld_ag(&gstat[(size_t)(k + PD - k0) * N + lo + min(j * pf_n + pf_lane, own - 1)]);
+      }
+    };
+    // per-wave mode with several waves: issued while wave 0 exchanges (simple_sync_pw); a
+    // single wave issues them here (its exchange polls would otherwise wait on them)
+    if (!PW || nwave == 1) prefetch();
+    auto prefetch_idle = [&]() {
+      if (nwave > 1) prefetch();
+    };
     // pass B: NormalizeScore, weights, shard-best selectHost key of pod k
     const long long nf = R[1];
     const int max_tt = (int)R[2], max_na = (int)R[3];
@@ -937,7 +1049,7 @@ __device__ __forceinline__ void simple_schedule(DevCluster c, const SPod* __rest
         best = e.f == 0 ? key : 0;
       }
       if (sp && tid == 0) sp[1] = wall_clock64();
-      best = wave_red<OP_MAX>(best);
+      best = wave_max_key(best, kb, c.node_base);
       if (sp && tid == 0) sp[2] = wall_clock64();
     } else {
       if (k >= k0) {
@@ -970,8 +1082,8 @@ __device__ __forceinline__ void simple_schedule(DevCluster c, const SPod* __rest
         for (int i = 0; i < 6; i++) u[i] = 0;
       }
       if (sp && tid == 0) sp[3] = wall_clock64();
-      if (!simple_sync_pw(H, parity, best, u, W, w, ++epoch, gran, X, err, per, c.node_base, lo, own, pk, k >= k0, L, R,
-                          sp))
+      if (!simple_sync_pw(H, parity, best, u, W, w, ++epoch, gran, X, err, per, c.node_base, lo, own, pk, k >= k0, L, kb,
+                          R, sp, prefetch_idle))
         return;
     } else {
       if (k + 1 < k1) {
@@ -981,13 +1093,15 @@ __device__ __forceinline__ void simple_schedule(DevCluster c, const SPod* __rest
         for (int i = 0; i < 6; i++) st[i] = 0;
       }
       if (sp && tid == 0) sp[3] = wall_clock64();
-      if (!simple_sync(H, parity, best, st, W, w, ++epoch, gran, X, err, per, c.node_base, R, sp)) return;
+      if (!simple_sync(H, parity, best, st, W, w, ++epoch, gran, X, err, per, c.node_base, kb, R, sp)) return;
     }
     if (sp && tid == 0) sp[5] = wall_clock64();
     if (k >= k0) {
       const long long K = R[0];
       const int x = K ? (int)(0xFFFFFFFFu - (uint32_t)(unsigned long long)K) - c.node_base : -1;
-      if (w == X.w_off && tid == 0) {  // every part keeps the outcomes
+      // every part keeps the outcomes; their HBM stores are issued off wave 0 (behind the
+      // prefetch loads of wave 1), whose vmcnt stays free for the next exchange's polls
+      if (w == X.w_off && tid == (nwave > 1 ? 64 : 0)) {
         PodMeta m;
         m.chosen = K ? x + c.node_base : -1;
         m.n_feasible = (int)nf;

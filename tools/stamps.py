@@ -69,6 +69,12 @@ def summarise(path):
                      f" latest shard most often {int(late.argmax())} ({late.max()}/{good.sum()} pods)")
             pa = (a[:, :, 3] - a[:, :, 0]) / 100.0
             line += f"\n  start -> passA done per shard: median {np.median(pa[:, good]):.2f} us, max over shards (median) {np.median(pa[:, good].max(axis=0)):.2f}"
+        if ((s0[ok, 7] > 0) & (s0[ok, 8] > 0)).any():  # per-wave mode: statistics reduction detail
+            q = s0[ok][(s0[ok, 7] > 0) & (s0[ok, 8] > 0)]
+            seq = np.stack([q[:, 3], q[:, 7], q[:, 8], q[:, 4]], axis=1)
+            dd = np.median(np.diff(seq, axis=1) / 100.0, axis=0)
+            line += (f"\n  red_stats detail (shard 0): wave_red={dd[0]:.2f} write+barrier={dd[1]:.2f}"
+                     f" combine={dd[2]:.2f} us")
         lines.append(line)
     return "\n".join(lines)
 
