@@ -638,6 +638,15 @@ int kss_last_loop_timing(kss_ctx* ctx, double* loop_ms);
  * disagree (the run fails with KSS_E_DEVICE if they never agree).  *retries = the repeated
  * loads (0 when every hand-off was consistent at once). */
 int kss_last_handoff_retries(kss_ctx* ctx, int32_t* retries);
+/* The same hand-off's second copy and diagnosis: every epilogue also stores the node state into
+ * a shadow buffer, and odd reload attempts read the shadow; *recovered = the loads the shadow
+ * answered.  On a launch's first disagreement the prologue lists each word where the state and
+ * its shadow differ, KSS_HANDOFF_DIAG_WORDS int64 per entry: {shard | loading XCC << 32 |
+ * storing XCC << 40, array (0-2 requested, 3-4 nonzero, 5 pod count, 6 + r resident count row
+ * r), node, state by agent load, by atomic add of 0, by nontemporal load, shadow value, the
+ * chunk tag}.  Up to cap entries are copied; *n_entries = the entries listed (<= 64). */
+#define KSS_HANDOFF_DIAG_WORDS 8
+int kss_last_handoff_diag(kss_ctx* ctx, int32_t* recovered, int64_t* entries, int32_t cap, int32_t* n_entries);
 /* launch geometry of the last scheduling launch: out[0] shards (workgroups) per cluster,
  * out[1] threads per workgroup, out[2] node slots per lane */
 int kss_last_geometry(kss_ctx* ctx, int32_t* out3);

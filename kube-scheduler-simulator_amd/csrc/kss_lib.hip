@@ -519,6 +519,9 @@ struct kss_ctx {
   DevBuf ck_buf;                    // k_spread's checked hand-off between chunks: {sum, tag} per shard
   unsigned long long ck_seq = 0;    // the last tag a chunk wrote
   int last_handoff_retries = 0;     // prologue loads repeated in the last run (HandoffCheck)
+  int last_handoff_recovered = 0;   // ... of which the shadow copy answered
+  size_t ck_diag_off = 0;           // ck_buf word of the diagnosis list
+  bool last_kernel_spread = false;
 #if KSS_SPREAD_TRACE
   DevBuf trace_buf, trace_list_buf;  // k_spread trace of the last run (kss_trace_spread)
   size_t trace_words = 0;
@@ -2287,6 +2290,18 @@ static bool spread_fits(const Geometry& g, const GpodNeeds& q, int n_keys, int n
          spread_lds(g, q, n_keys, n_res, N) <= KSS_LDS_BUDGET;
 }
 
+// The checked hand-off's buffer (ck_buf), in 8-byte words: {sum, tag} per shard, the XCC of
+// each shard's last epilogue (int), the diagnosis list, the shadow copy of the node state.
+struct HandoffLayout {
+  size_t o_xcc, o_diag, o_shadow, words;
+  HandoffLayout(int W, int n_res, int N) {
+    o_xcc = 2 * (size_t)W;
+    o_diag = o_xcc + ((size_t)W + 1) / 2;
+    o_shadow = (o_diag + 1 + (size_t)HANDOFF_DIAG * HANDOFF_DIAG_W + 15) / 16 * 16;
+    words = o_shadow + (6 + (size_t)std::max(n_res, 0)) * (size_t)std::max(N, 1);
+  }
+};
+
 // k_static + k_spread over pods [0, n_pods) of one job, `chunk` pods at a time (node state
 // and counts back in HBM between launches).  ev (optional): 2 events per chunk.
 static int launch_spread(hipStream_t st, const Geometry& g, const GpodNeeds& q, int n_keys, int n_res,
@@ -2335,10 +2350,14 @@ static int launch_spread(hipStream_t st, const Geometry& g, const GpodNeeds& q, 
     // over the context's life, the first chunk of a call checks nothing
     HandoffCheck hc{};
     if (ck && ck_seq && n_pods > chunk) {
+      const HandoffLayout hl(g.W, n_res, max_nodes);
       hc.sum = ck;
       hc.expect = k0 > 0 ? *ck_seq : 0ull;
       hc.write = ++*ck_seq;
       hc.retries = err + 1;
+      hc.xcc = (int*)(ck + hl.o_xcc);
+      hc.diag = (long long*)(ck + hl.o_diag);
+      hc.shadow = (long long*)(ck + hl.o_shadow);
     }
     void* args[] = {(void*)&jobs, (void*)&W,  (void*)&cap, (void*)&bins_cap, (void*)&nr,  (void*)&gq, (void*)&gs, (void*)&k0,
                     (void*)&k1,   (void*)&gc, (void*)&err, (void*)&sp,       (void*)&nst, (void*)&X,  (void*)&epoch0,
@@ -2610,7 +2629,10 @@ static int run_single_impl(kss_ctx* ctx, const PlanNeeds& need, const DevPods& d
                        errp, stamps, ctx->loop_ev.data(), split ? &srun : nullptr);
   else if (spread)
   {
-    if ((rc = ctx->ck_buf.ensure(sizeof(unsigned long long) * 2 * (size_t)g.W))) return rc;
+    const HandoffLayout hl(g.W, n_res, (int)N);
+    if ((rc = ctx->ck_buf.ensure(sizeof(unsigned long long) * hl.words))) return rc;
+    HIP_TRY(hipMemsetAsync((unsigned long long*)ctx->ck_buf.p + hl.o_diag, 0, sizeof(unsigned long long), ctx->stream));
+    ctx->ck_diag_off = hl.o_diag;
     rc = launch_spread(ctx->stream, g, ctx->gneed, ctx->dc.n_keys, n_res, jd, ctx->prof, n,
                        (int)N, chunk, gran, gb, errp, stamps, ctx->loop_ev.data(), split ? &srun : nullptr,
                        (unsigned long long*)ctx->ck_buf.p, &ctx->ck_seq);
@@ -2664,7 +2686,7 @@ static int run_single_impl(kss_ctx* ctx, const PlanNeeds& need, const DevPods& d
   const size_t o_meta = 16, o_chosen = align_up(o_meta + mb, 16), o_rb = align_up(o_chosen + cb, 16);
   if ((rc = ensure_pinned(ctx->rb, ctx->rb_cap, o_rb + (rbk ? rbk->bytes : 0)))) return rc;
   char* hb = (char*)ctx->rb;
-  HIP_TRY(hipMemcpyAsync(hb, errp, 2 * sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+  HIP_TRY(hipMemcpyAsync(hb, errp, 3 * sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
   HIP_TRY(hipMemcpyAsync(hb + o_meta, ctx->meta_buf.p, mb, hipMemcpyDeviceToHost, ctx->stream));
   if (cb) HIP_TRY(hipMemcpyAsync(hb + o_chosen, ctx->chosen_buf.p, cb, hipMemcpyDeviceToHost, ctx->stream));
   if (rbk && rbk->bytes) HIP_TRY(hipMemcpyAsync(hb + o_rb, rbk->src, rbk->bytes, hipMemcpyDeviceToHost, ctx->stream));
@@ -2686,6 +2708,8 @@ static int run_single_impl(kss_ctx* ctx, const PlanNeeds& need, const DevPods& d
   int errw = 0;
   std::memcpy(&errw, hb, sizeof(int));
   std::memcpy(&ctx->last_handoff_retries, hb + sizeof(int), sizeof(int));
+  std::memcpy(&ctx->last_handoff_recovered, hb + 2 * sizeof(int), sizeof(int));
+  ctx->last_kernel_spread = spread;
   if (errw && commit) {  // bounds as if every pod committed (upper bounds stay safe); log unknown
     ctx->count_bound = count_total;
     ctx->cell_bound = std::max(ctx->cell_bound, cell_total);
@@ -3494,6 +3518,22 @@ int kss_last_timing(kss_ctx* ctx, double* device_ms, int32_t* launches) {
 int kss_last_handoff_retries(kss_ctx* ctx, int32_t* retries) {
   if (!ctx || !retries) return fail(KSS_E_INVAL, "bad arguments");
   *retries = ctx->last_handoff_retries;
+  return 0;
+}
+
+int kss_last_handoff_diag(kss_ctx* ctx, int32_t* recovered, int64_t* entries, int32_t cap, int32_t* n_entries) {
+  if (!ctx || !recovered || !n_entries || cap < 0 || (cap && !entries)) return fail(KSS_E_INVAL, "bad arguments");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  *recovered = ctx->last_handoff_recovered;
+  *n_entries = 0;
+  if (!ctx->last_kernel_spread || !ctx->ck_buf.p || !ctx->last_handoff_retries) return 0;
+  HIP_TRY(hipSetDevice(ctx->cfg.device));
+  std::vector<long long> h(1 + (size_t)HANDOFF_DIAG * HANDOFF_DIAG_W);
+  HIP_TRY(hipMemcpy(h.data(), (unsigned long long*)ctx->ck_buf.p + ctx->ck_diag_off, h.size() * 8, hipMemcpyDeviceToHost));
+  const int n = (int)std::min<long long>(h[0], HANDOFF_DIAG);
+  const int m = std::min(n, cap);
+  std::memcpy(entries, h.data() + 1, sizeof(int64_t) * HANDOFF_DIAG_W * (size_t)m);
+  *n_entries = n;
   return 0;
 }
 

@@ -1099,24 +1099,6 @@ __device__ __forceinline__ void simple_schedule(DevCluster c, const SPod* __rest
     if (k >= k0) {
       const long long K = R[0];
       const int x = K ? (int)(0xFFFFFFFFu - (uint32_t)(unsigned long long)K) - c.node_base : -1;
-      // every part keeps the outcomes; their HBM stores are issued off wave 0 (behind the
-      // prefetch loads of wave 1), whose vmcnt stays free for the next exchange's polls
-      if (w == X.w_off && tid == (nwave > 1 ? 64 : 0)) {
-        PodMeta m;
-        m.chosen = K ? x + c.node_base : -1;
-        m.n_feasible = (int)nf;
-        m.scored = (K && scored) ? 1 : 0;
-        m.status = pk.status != 0 ? (pk.status == KSS_PF_ERROR ? 3 : 2) : (nf == 0 ? 1 : 0);
-        m.best_total = m.scored ? (int64_t)((unsigned long long)K >> 32) : 0;
-        if (chosen) gchosen[k] = m.chosen;
-        if (meta) {
-          gmeta[k].chosen = m.chosen;
-          gmeta[k].n_feasible = m.n_feasible;
-          gmeta[k].scored = m.scored;
-          gmeta[k].status = m.status;
-          gmeta[k].best_total = m.best_total;
-        }
-      }
       // AssumePod on the winner's shard (per-wave mode: done inside the sync); pass B of pod
       // k+1 takes that slot's H1 values: cv slot cap (cap + the slot's wave in per-wave mode)
       const bool won = x >= lo && x < hi;
@@ -1131,6 +1113,27 @@ __device__ __forceinline__ void simple_schedule(DevCluster c, const SPod* __rest
 #pragma unroll
       for (int j = 0; j < PF_MAX; j++)
         if (j < pf_per) L.st[((k + PD) % RING) * cap + min(j * pf_n + pf_lane, own - 1)] = pfw[j];
+    }
+    // every part keeps the outcomes; their HBM stores are issued off wave 0 (whose vmcnt stays
+    // free for the next exchange's polls) and after the ring stores above (which wait on this
+    // wave's prefetch loads only, not on these stores)
+    if (k >= k0 && w == X.w_off && tid == (nwave > 1 ? 64 : 0)) {
+      const long long K = R[0];
+      const int x = K ? (int)(0xFFFFFFFFu - (uint32_t)(unsigned long long)K) - c.node_base : -1;
+      PodMeta m;
+      m.chosen = K ? x + c.node_base : -1;
+      m.n_feasible = (int)nf;
+      m.scored = (K && scored) ? 1 : 0;
+      m.status = pk.status != 0 ? (pk.status == KSS_PF_ERROR ? 3 : 2) : (nf == 0 ? 1 : 0);
+      m.best_total = m.scored ? (int64_t)((unsigned long long)K >> 32) : 0;
+      if (chosen) gchosen[k] = m.chosen;
+      if (meta) {
+        gmeta[k].chosen = m.chosen;
+        gmeta[k].n_feasible = m.n_feasible;
+        gmeta[k].scored = m.scored;
+        gmeta[k].status = m.status;
+        gmeta[k].best_total = m.best_total;
+      }
     }
     if (sp && tid == 0) sp[6] = wall_clock64();
   }

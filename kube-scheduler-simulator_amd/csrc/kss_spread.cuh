@@ -607,15 +607,29 @@ __device__ __forceinline__ bool spread_argmax(SpreadHdr& H, int W, int w, int gs
 
 // A checked hand-off of a shard's node state from one chunk launch to the next: the epilogue
 // stores, beside the state, a position-mixed sum of every word it wrote and a tag (the chunk
-// sequence number); the next chunk's prologue sums what it loaded and, while the sums
-// disagree, loads again (a bounded number of times, then the launch fails with err = 2
-// instead of scheduling on a wrong state).  hc.sum: [2 W] words {sum, tag} per shard.
+// sequence number), and a second copy of the state (the shadow); the next chunk's prologue sums
+// what it loaded and, while the sums disagree, loads again, alternating between the state and
+// its shadow (a bounded number of times, then the launch fails with err = 2 instead of
+// scheduling on a wrong state).  The first disagreement of a launch also lists, per differing
+// word, the state as a plain agent load, as an atomic and as a nontemporal load sees it, the
+// shadow's value and the XCCs of the storing and loading shards (kss_last_handoff_diag).
+// hc.sum: [2 W] words {sum, tag} per shard.
+constexpr int HANDOFF_DIAG = 64;   // differing words listed per run
+constexpr int HANDOFF_DIAG_W = 8;  // words per listed entry
 struct HandoffCheck {
-  unsigned long long* sum;  // null: no check
+  unsigned long long* sum;    // null: no check
   unsigned long long expect;  // tag the previous chunk wrote (0: the first chunk of the call)
   unsigned long long write;   // tag this chunk writes
-  int* retries;               // loads repeated because the sums disagreed
+  int* retries;               // [0] loads repeated because the sums disagreed, [1] loads the shadow answered
+  long long* shadow;          // [(6 + n_res) N]: requested x3, nonzero x2, pod count, resident count rows
+  int* xcc;                   // [W]: the XCC that ran each shard's last epilogue
+  long long* diag;            // [1 + HANDOFF_DIAG * HANDOFF_DIAG_W]: count, then the differing words
 };
+__device__ __forceinline__ int xcc_id() {
+  int x;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
+  return x & 0xF;
+}
 __device__ __forceinline__ unsigned long long handoff_mix(unsigned long long v, size_t pos) {
   return (v + 0x9E3779B97F4A7C15ull) * (2ull * (unsigned long long)pos + 1ull);
 }
@@ -635,6 +649,7 @@ __device__ __forceinline__ void handoff_publish(const HandoffCheck& hc, int w, u
   if (threadIdx.x == 0) {
     st_ag(&hc.sum[2 * (size_t)w], t);
     st_ag(&hc.sum[2 * (size_t)w + 1], hc.write);
+    if (hc.xcc) st_ag(&hc.xcc[w], xcc_id());
   }
 }
 // True when the loaded state matches the previous chunk's sum (or there is nothing to check).
@@ -662,6 +677,22 @@ __device__ __forceinline__ bool handoff_verify(const HandoffCheck& hc, int w, un
     handoff_acquire();
   }
   return ok;
+}
+// One differing word of the hand-off (first disagreement of a launch): array a (0-2 requested,
+// 3-4 nonzero, 5 pod count, 6 + r resident count row r), node n, and the views of it.
+__device__ __forceinline__ void handoff_note(const HandoffCheck& hc, int w, int a, int n, long long plain,
+                                             long long atomic_v, long long nt, long long shadow) {
+  const long long e = __hip_atomic_fetch_add(hc.diag, 1ll, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (e >= HANDOFF_DIAG) return;
+  long long* d = hc.diag + 1 + e * HANDOFF_DIAG_W;
+  st_ag(&d[0], (long long)w | ((long long)xcc_id() << 32) | ((long long)ld_ag(&hc.xcc[w]) << 40));
+  st_ag(&d[1], (long long)a);
+  st_ag(&d[2], (long long)n);
+  st_ag(&d[3], plain);
+  st_ag(&d[4], atomic_v);
+  st_ag(&d[5], nt);
+  st_ag(&d[6], shadow);
+  st_ag(&d[7], (long long)hc.expect);
 }
 
 // The statistics of node slot s for pod q, accumulated into bins (SUM) / bins + total_bins
@@ -871,19 +902,22 @@ __device__ __forceinline__ void spread_schedule(const GTrace& tr, DevCluster c, 
     L.st[(k0 & 1) * cap + s] = ld_ag(&stat[(size_t)lo + s]);
   }
   // node state handed over by the previous chunk: loaded, then checked against the sum its
-  // epilogue stored (HandoffCheck); loaded again until they agree, a bounded number of times
+  // epilogue stored (HandoffCheck); loaded again until they agree, a bounded number of times,
+  // odd attempts from the shadow copy
   for (int attempt = 0;; attempt++) {
+    const bool shd = hc.shadow && (attempt & 1);
     unsigned long long h = 0;
     for (int s = tid; s < own; s += nt) {
       const int n = lo + s;
 #pragma unroll
       for (int k = 0; k < 3; k++) {
-        const int64_t R = ld_ag(&c.requested[k * N + n]);
+        const int64_t R = shd ? ld_ag(&hc.shadow[k * N + n]) : ld_ag(&c.requested[k * N + n]);
         L.r64[(3 + k) * cap + s] = (double)R;
         h += handoff_mix((unsigned long long)R, (size_t)k * N + n);
       }
-      const int64_t z0 = ld_ag(&c.nonzero[n]), z1 = ld_ag(&c.nonzero[N + n]);
-      const int32_t pc = ld_ag(&c.pod_count[n]);
+      const int64_t z0 = shd ? ld_ag(&hc.shadow[3 * N + n]) : ld_ag(&c.nonzero[n]);
+      const int64_t z1 = shd ? ld_ag(&hc.shadow[4 * N + n]) : ld_ag(&c.nonzero[N + n]);
+      const int32_t pc = shd ? (int32_t)ld_ag(&hc.shadow[5 * N + n]) : ld_ag(&c.pod_count[n]);
       L.r64[6 * cap + s] = (double)z0;
       L.r64[7 * cap + s] = (double)z1;
       L.r32[s] = pc;
@@ -892,8 +926,9 @@ __device__ __forceinline__ void spread_schedule(const GTrace& tr, DevCluster c, 
     }
     for (int i = tid; i < n_res * own; i += nt) {
       const int r = i / own, s = i - r * own, row = res_rows[r];
-      const int32_t v = row < c.n_classes ? ld_ag(&c.class_count[(size_t)row * N + lo + s])
-                                          : ld_ag(&c.term_count[(size_t)(row - c.n_classes) * N + lo + s]);
+      const int32_t v = shd ? (int32_t)ld_ag(&hc.shadow[(6 + (size_t)r) * N + lo + s])
+                            : (row < c.n_classes ? ld_ag(&c.class_count[(size_t)row * N + lo + s])
+                                                 : ld_ag(&c.term_count[(size_t)(row - c.n_classes) * N + lo + s]));
       L.cnt[r * cap + s] = (uint16_t)v;
       h += handoff_mix((unsigned long long)(uint32_t)v, (6 + (size_t)r) * N + lo + s);
 #if KSS_SPREAD_TRACE
@@ -910,8 +945,41 @@ __device__ __forceinline__ void spread_schedule(const GTrace& tr, DevCluster c, 
 #endif
     }
     if (!hc.sum) break;
-    if (handoff_verify(hc, w, h, attempt, H.kx, &H.abort, err)) break;
+    if (handoff_verify(hc, w, h, attempt, H.kx, &H.abort, err)) {
+      if (shd && tid == 0) __hip_atomic_fetch_add(hc.retries + 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      break;
+    }
     if (H.abort) return;
+    if (attempt == 0 && hc.shadow && hc.diag) {  // the words where the state and its shadow differ
+      for (int s = tid; s < own; s += nt) {
+        const int n = lo + s;
+        for (int a = 0; a < 6; a++) {
+          const long long sv = ld_ag(&hc.shadow[(size_t)a * N + n]);
+          if (a < 5) {
+            int64_t* p = a < 3 ? &c.requested[(size_t)a * N + n] : &c.nonzero[(size_t)(a - 3) * N + n];
+            const long long pv = ld_ag(p);
+            if (pv != sv)
+              handoff_note(hc, w, a, n, pv, __hip_atomic_fetch_add(p, (int64_t)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                           __builtin_nontemporal_load(p), sv);
+          } else {
+            int32_t* p = &c.pod_count[n];
+            const long long pv = ld_ag(p);
+            if (pv != sv)
+              handoff_note(hc, w, a, n, pv, __hip_atomic_fetch_add(p, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                           __builtin_nontemporal_load(p), sv);
+          }
+        }
+      }
+      for (int i = tid; i < n_res * own; i += nt) {
+        const int r = i / own, s = i - r * own, row = res_rows[r];
+        int32_t* p = row < c.n_classes ? &c.class_count[(size_t)row * N + lo + s]
+                                       : &c.term_count[(size_t)(row - c.n_classes) * N + lo + s];
+        const long long sv = ld_ag(&hc.shadow[(6 + (size_t)r) * N + lo + s]), pv = ld_ag(p);
+        if (pv != sv)
+          handoff_note(hc, w, 6 + r, lo + s, pv, __hip_atomic_fetch_add(p, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                       __builtin_nontemporal_load(p), sv);
+      }
+    }
   }
   const uint4* grec = reinterpret_cast<const uint4*>(gpods);
   for (int i = tid; i < min(k1 - k0, 2) * gq; i += nt) {
@@ -1402,6 +1470,13 @@ __device__ __forceinline__ void spread_schedule(const GTrace& tr, DevCluster c, 
     st_ag(&c.nonzero[n], (int64_t)L.r64[6 * cap + s]);
     st_ag(&c.nonzero[N + n], (int64_t)L.r64[7 * cap + s]);
     st_ag(&c.pod_count[n], L.r32[s]);
+    if (hc.shadow) {
+#pragma unroll
+      for (int r = 0; r < 3; r++) st_ag(&hc.shadow[(size_t)r * N + n], (long long)L.r64[(3 + r) * cap + s]);
+      st_ag(&hc.shadow[3 * N + n], (long long)L.r64[6 * cap + s]);
+      st_ag(&hc.shadow[4 * N + n], (long long)L.r64[7 * cap + s]);
+      st_ag(&hc.shadow[5 * N + n], (long long)L.r32[s]);
+    }
   }
   unsigned long long h = 0;
   if (hc.sum)
@@ -1418,6 +1493,7 @@ __device__ __forceinline__ void spread_schedule(const GTrace& tr, DevCluster c, 
     const int32_t v = L.cnt[r * cap + s];
     if (row < c.n_classes) st_ag(&c.class_count[(size_t)row * N + lo + s], v);
     else st_ag(&c.term_count[(size_t)(row - c.n_classes) * N + lo + s], v);
+    if (hc.shadow) st_ag(&hc.shadow[(6 + (size_t)r) * N + lo + s], (long long)v);
     h += handoff_mix((unsigned long long)(uint32_t)v, (6 + (size_t)r) * N + lo + s);
 #if KSS_SPREAD_TRACE
     if (v && tr.list) {

@@ -75,7 +75,12 @@ def test_parts_over_many_chunks(monkeypatch, config, n_nodes, n_pods, per_chunk,
     init_cc = np.ctypeslib.as_array(s.cluster.class_count, shape=(max(nc, 1) * N,)).reshape(max(nc, 1), N)[:nc]
     for rep in range(3):
         sp.reset()
-        outs = sp.run(n_pods)
+        try:
+            outs = sp.run(n_pods)
+        except native.KssError:
+            _handoff_report(sp, rep, failed=True)
+            raise
+        _handoff_report(sp, rep)
         bad = [np.flatnonzero(np.asarray(ch) != ch_o) for ch in outs]
         g = sp.node_state()
         if any(len(b) for b in bad) or (s.cluster.n_classes and not np.array_equal(
@@ -89,9 +94,6 @@ def test_parts_over_many_chunks(monkeypatch, config, n_nodes, n_pods, per_chunk,
                         f"{j // per_chunk} pod {j % per_chunk}; device {[o[j] for o in outs]} meta {meta}; oracle "
                         f"{ch_o[j]} meta {[m['chosen'], m['n_feasible'], m['scored'], m['status'], m['best_total']]}")
         assert sp.ctxs[0].last_timing()[1] == 2 * -(-n_pods // per_chunk)  # k_static + loop per chunk
-        retries = [c.last_handoff_retries() for c in sp.ctxs]
-        if any(retries):  # a chunk's prologue read node state that disagreed with its producer's sum
-            print(f"run {rep}: node-state hand-off reloads per part {retries}")
         # the node state every run leaves, count rows included (a wrong count need not change a choice)
         np.testing.assert_array_equal(g["requested"][:, :N], st["requested"][:, :N], err_msg=f"run {rep}")
         np.testing.assert_array_equal(g["pod_count"][:N], st["pod_count"][:N], err_msg=f"run {rep}")
@@ -101,6 +103,26 @@ def test_parts_over_many_chunks(monkeypatch, config, n_nodes, n_pods, per_chunk,
                 assert not len(d), (f"run {rep}: {key} differs at (row, node, device, oracle) " + str(
                     [(int(a), int(b), int(g[key][a, b]), int(st[key][a, b])) for a, b in d[:8]]))
     sp.close()
+
+
+def _handoff_report(sp, rep, failed=False):
+    """The node-state hand-off check of every part after a run (k_spread chunks): reloads, loads
+    the shadow copy answered, and the words where state and shadow differed.  Printed when any
+    reload happened, and appended to $KSS_HANDOFF_LOG when set (evidence for DESIGN §5)."""
+    lines = []
+    for p, c in enumerate(sp.ctxs):
+        retries = c.last_handoff_retries()
+        if not retries:
+            continue
+        rec, entries = c.last_handoff_diag()
+        lines.append(f"run {rep} part {p}{' FAILED' if failed else ''}: reloads {retries}, shadow answered {rec}, "
+                     f"differing words {len(entries)}")
+        lines += [f"  {e}" for e in entries[:16]]
+    if lines:
+        print("\n".join(lines))
+        if os.environ.get("KSS_HANDOFF_LOG"):
+            with open(os.environ["KSS_HANDOFF_LOG"], "a") as f:
+                f.write("\n".join(lines) + "\n")
 
 
 def test_shards_per_part_never_exceed_nodes():
