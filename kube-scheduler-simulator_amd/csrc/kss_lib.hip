@@ -251,7 +251,7 @@ __global__ __launch_bounds__(KSS_MAX_THREADS) void k_spread(const DevJob* __rest
   SpreadHdr& H = *reinterpret_cast<SpreadHdr*>(smem);
 #ifdef KSS_LDS_POISON  // experiment builds: the shard's LDS image filled with a pattern first
   {
-    const size_t words = spread_lds_bytes(cap, bins_cap, job.c.n_keys, n_res, gq) / 4;
+    const size_t words = spread_lds_bytes(cap, bins_cap, job.c.n_keys, n_res, gq, job.c.n_scalar) / 4;
     uint32_t* p = reinterpret_cast<uint32_t*>(smem);
     for (size_t i = threadIdx.x; i < words; i += blockDim.x) p[i] = 0x5A5A5A5Au;
     __syncthreads();
@@ -858,6 +858,10 @@ bool fill_spod(const kss_podset* ps, const kss_pod& p, int n_scalar, SPod& q) {
   }
   q.cnz[0] = (double)p.commit_nz[0];
   q.cnz[1] = (double)p.commit_nz[1];
+  for (int s = 0; s < n_scalar; s++) {
+    q.sc_fit[s] = p.fit_request[3 + s];
+    q.sc_req[s] = p.commit_req[3 + s];
+  }
   q.flags = all_zero ? SP_ALLZERO : 0;
   q.status = p.prefilter_status;
   q.cls = p.cls;
@@ -914,7 +918,7 @@ const char* const kGpReason[GP_NCODES] = {
     "the commit adds to more than 8 count rows",
     "a pod's record exceeds 2 KiB (too many references)",
     "more than 16 inter-pod-affinity entries after merging",
-    "extended (scalar) resources in the cluster: k_simple / k_spread keep cpu, memory and ephemeral-storage only",
+    "the profile scores an extended (scalar) resource: k_simple / k_spread score cpu, memory and ephemeral-storage only",
     "host ports (NodePorts), node-cached images (ImageLocality) or volumes: k_schedule only",
 };
 
@@ -2162,10 +2166,22 @@ static bool same_profile(const kss_profile& a, const kss_profile& b) {
 // re-evaluates the candidate after the previous commit).
 static int simple_cap(const Geometry& g) { return g.npt * g.threads; }
 
-static bool simple_fits(const Geometry& g) {
+static bool simple_fits(const Geometry& g, int nsc) {
   const int pf_n = g.threads > 64 ? g.threads - 64 : g.threads;  // prefetch lanes (kss_simple.cuh)
   return g.W <= 64 * SX_CHUNKS && g.npt <= KSS_MAX_NPT && (simple_cap(g) + pf_n - 1) / pf_n <= PF_MAX &&
-         simple_lds_bytes(simple_cap(g)) <= KSS_LDS_BUDGET;
+         simple_lds_bytes(simple_cap(g), nsc) <= KSS_LDS_BUDGET;
+}
+
+// Extended (scalar) resources on k_simple / k_spread: their NodeResourcesFit filter and
+// AssumePod run in LDS; a profile that scores one (fit / BalancedAllocation resources past
+// ephemeral-storage) keeps the batch on k_schedule.
+static bool scalar_fast_ok(const kss_profile& p, int n_scalar) {
+  if (n_scalar == 0) return true;
+  for (int i = 0; i < p.fit_n && i < 4; i++)
+    if (p.fit_res[i] >= KSS_RES_SCALAR0) return false;
+  for (int i = 0; i < p.ba_n && i < 4; i++)
+    if (p.ba_res[i] >= KSS_RES_SCALAR0) return false;
+  return true;
 }
 
 // Static-word scratch bound (KSS_STATIC_BYTES): pods are processed in chunks whose words
@@ -2220,9 +2236,10 @@ static void static_rows(const Geometry& g, const XPeers& X, int max_nodes, int& 
 
 static int launch_simple(hipStream_t st, const Geometry& g, int n_jobs, const DevJob* jobs, const kss_profile& prof,
                          int n_pods_max, int max_nodes, int chunk, unsigned long long* gran, size_t gran_bytes, int* err,
-                         unsigned long long* stamps = nullptr, hipEvent_t* ev = nullptr, const SplitRun* split = nullptr) {
+                         unsigned long long* stamps = nullptr, hipEvent_t* ev = nullptr, const SplitRun* split = nullptr,
+                         int nsc = 0) {
   int cap = simple_cap(g);
-  const size_t shmem = simple_lds_bytes(cap);
+  const size_t shmem = simple_lds_bytes(cap, nsc);
   const bool def = same_profile(prof, default_profile_c());
   const void* fn = def ? (const void*)k_simple<true> : (const void*)k_simple<false>;
   HIP_TRY(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shmem));
@@ -2279,26 +2296,26 @@ static int spread_cap(const Geometry& g, size_t N) {
   return (int)align_up(std::max(per, (size_t)1), 16);
 }
 
-static size_t spread_lds(const Geometry& g, const GpodNeeds& q, int n_keys, int n_res, size_t N) {
-  return spread_lds_bytes(spread_cap(g, N), q.bins_cap, n_keys, n_res, q.gq);
+static size_t spread_lds(const Geometry& g, const GpodNeeds& q, int n_keys, int n_res, size_t N, int nsc) {
+  return spread_lds_bytes(spread_cap(g, N), q.bins_cap, n_keys, n_res, q.gq, nsc);
 }
 
-static bool spread_fits(const Geometry& g, const GpodNeeds& q, int n_keys, int n_res, size_t N) {
+static bool spread_fits(const Geometry& g, const GpodNeeds& q, int n_keys, int n_res, size_t N, int nsc) {
   const int pf_n = g.threads > 64 ? g.threads - 64 : g.threads;  // prefetch lanes (kss_spread.cuh)
   const int per = (int)((N + (size_t)g.W - 1) / (size_t)g.W);
   return (per + pf_n - 1) / pf_n <= G_PF && per <= g.npt * g.threads &&
-         spread_lds(g, q, n_keys, n_res, N) <= KSS_LDS_BUDGET;
+         spread_lds(g, q, n_keys, n_res, N, nsc) <= KSS_LDS_BUDGET;
 }
 
 // The checked hand-off's buffer (ck_buf), in 8-byte words: {sum, tag} per shard, the XCC of
 // each shard's last epilogue (int), the diagnosis list, the shadow copy of the node state.
 struct HandoffLayout {
   size_t o_xcc, o_diag, o_shadow, words;
-  HandoffLayout(int W, int n_res, int N) {
+  HandoffLayout(int W, int n_res, int N, int nsc) {
     o_xcc = 2 * (size_t)W;
     o_diag = o_xcc + ((size_t)W + 1) / 2;
     o_shadow = (o_diag + 1 + (size_t)HANDOFF_DIAG * HANDOFF_DIAG_W + 15) / 16 * 16;
-    words = o_shadow + (6 + (size_t)std::max(n_res, 0)) * (size_t)std::max(N, 1);
+    words = o_shadow + (6 + (size_t)std::max(n_res, 0) + (size_t)std::max(nsc, 0)) * (size_t)std::max(N, 1);
   }
 };
 
@@ -2308,9 +2325,9 @@ static int launch_spread(hipStream_t st, const Geometry& g, const GpodNeeds& q, 
                          const DevJob* jobs, const kss_profile& prof, int n_pods, int max_nodes, int chunk,
                          unsigned long long* gran, size_t gran_bytes, int* err, unsigned long long* stamps = nullptr,
                          hipEvent_t* ev = nullptr, const SplitRun* split = nullptr, unsigned long long* ck = nullptr,
-                         unsigned long long* ck_seq = nullptr) {
+                         unsigned long long* ck_seq = nullptr, int nsc = 0) {
   int cap = spread_cap(g, (size_t)max_nodes), bins_cap = q.bins_cap, nr = n_res, gq = q.gq, gs = q.gs();
-  size_t shmem = spread_lds(g, q, n_keys, n_res, (size_t)max_nodes);
+  size_t shmem = spread_lds(g, q, n_keys, n_res, (size_t)max_nodes, nsc);
   // diagnostic stamps in LDS: as many pods (<= G_NSTAMP, >= 8) as fit beside the shard state
   int nst = 0;
   if (stamps && shmem < KSS_LDS_BUDGET) nst = (int)std::min<size_t>(G_NSTAMP, (KSS_LDS_BUDGET - shmem) / (16 * 8));
@@ -2350,7 +2367,7 @@ static int launch_spread(hipStream_t st, const Geometry& g, const GpodNeeds& q, 
     // over the context's life, the first chunk of a call checks nothing
     HandoffCheck hc{};
     if (ck && ck_seq && n_pods > chunk) {
-      const HandoffLayout hl(g.W, n_res, max_nodes);
+      const HandoffLayout hl(g.W, n_res, max_nodes, nsc);
       hc.sum = ck;
       hc.expect = k0 > 0 ? *ck_seq : 0ull;
       hc.write = ++*ck_seq;
@@ -2446,14 +2463,14 @@ static int run_single_impl(kss_ctx* ctx, const PlanNeeds& need, const DevPods& d
   // shards): at 100k nodes, 98-128 k_simple shards beat 256 k_schedule shards (69.8k
   // against 44.2k pods/s)
   const bool simple_ok = staged && ctx->spod_ok && commit && !record && !keep_norm && !need.general &&
-                         ctx->dc.n_scalar == 0 && ctx->small_values && f64_exact(ctx->f64_cluster, ctx->f64_pods, n) &&
+                         scalar_fast_ok(ctx->prof, ctx->dc.n_scalar) && ctx->small_values && f64_exact(ctx->f64_cluster, ctx->f64_pods, n) &&
                          !ctx->no_simple && !(flags & KSS_SCHED_GENERAL_KERNEL);
   if (simple_ok && ctx->force_w <= 0 && !split) W = std::min(W, 64 * SX_CHUNKS);
   // a batch with programs on k_spread: 32-bit counts and scores (spread_bounds_ok)
   const double count_total = ctx->count_bound + (commit ? (double)n * (1.0 + ctx->staged_max_own) : 0.0);
   const double cell_total = ctx->cell_bound + (commit ? (double)n * ctx->gneed.max_mult : 0.0);
   const bool spread_ok = staged && ctx->gpod_ok && commit && !record && !keep_norm && need.general &&
-                         ctx->dc.n_scalar == 0 && ctx->small_values && f64_exact(ctx->f64_cluster, ctx->f64_pods, n) &&
+                         scalar_fast_ok(ctx->prof, ctx->dc.n_scalar) && ctx->small_values && f64_exact(ctx->f64_cluster, ctx->f64_pods, n) &&
                          !ctx->no_simple && !ctx->no_spread && !(flags & KSS_SCHED_GENERAL_KERNEL) &&
                          spread_bounds_ok(ctx->gneed, count_total, cell_total, (int)N);
   if (getenv("KSS_TRACE_PATH"))  // diagnosis: why a batch with programs is (not) on k_spread
@@ -2475,16 +2492,16 @@ static int run_single_impl(kss_ctx* ctx, const PlanNeeds& need, const DevPods& d
   if (split && ctx->split_wl > ctx->n_cu) return fail(KSS_E_UNSUPPORTED, "split grid: more shards per part than CUs");
   Geometry g;
   if (!pick_geometry((int)N, W, ctx->pref_threads, g)) return fail(KSS_E_UNSUPPORTED, "no geometry for this cluster");
-  const bool simple = simple_ok && simple_fits(g);
+  const bool simple = simple_ok && simple_fits(g, ctx->dc.n_scalar);
   const int n_res = (int)ctx->gneed.res_rows.size();
-  bool spread = spread_ok && spread_fits(g, ctx->gneed, ctx->dc.n_keys, n_res, N);
+  bool spread = spread_ok && spread_fits(g, ctx->gneed, ctx->dc.n_keys, n_res, N, ctx->dc.n_scalar);
   if (spread && !simple && !getenv("KSS_THREADS") && !getenv("KSS_FORCE_THREADS")) {
     // k_spread: one node per lane where the workgroup allows it (up to KSS_SPREAD_PREF_THREADS):
     // its per-node passes are the chain between exchanges (C4: 256 -> 512 lanes, stats +
     // filter + normalise 4.4 -> 2.6 us per pod)
     Geometry g2;
     if (pick_geometry((int)N, W, KSS_SPREAD_PREF_THREADS, g2) && g2.threads > g.threads &&
-        spread_fits(g2, ctx->gneed, ctx->dc.n_keys, n_res, N))
+        spread_fits(g2, ctx->gneed, ctx->dc.n_keys, n_res, N, ctx->dc.n_scalar))
       g = g2;
   }
   if (split && simple && g.W > 64 * SX_CHUNKS) return fail(KSS_E_UNSUPPORTED, "split grid: k_simple sweeps at most 128 shards");
@@ -2493,7 +2510,7 @@ static int run_single_impl(kss_ctx* ctx, const PlanNeeds& need, const DevPods& d
     const int per = (int)((N + g.W - 1) / g.W);
     g2.threads = KSS_MAX_THREADS;
     g2.npt = (per + KSS_MAX_THREADS - 1) / KSS_MAX_THREADS;
-    if (spread_fits(g2, ctx->gneed, ctx->dc.n_keys, n_res, N)) {
+    if (spread_fits(g2, ctx->gneed, ctx->dc.n_keys, n_res, N, ctx->dc.n_scalar)) {
       g = g2;
       spread = true;
     }
@@ -2504,7 +2521,7 @@ static int run_single_impl(kss_ctx* ctx, const PlanNeeds& need, const DevPods& d
                          W2 <= ctx->n_cu && W2 <= (int)N;
        W2 *= 2) {
     Geometry g2;
-    if (pick_geometry((int)N, W2, ctx->pref_threads, g2) && spread_fits(g2, ctx->gneed, ctx->dc.n_keys, n_res, N)) {
+    if (pick_geometry((int)N, W2, ctx->pref_threads, g2) && spread_fits(g2, ctx->gneed, ctx->dc.n_keys, n_res, N, ctx->dc.n_scalar)) {
       g = g2;
       spread = true;
     }
@@ -2626,16 +2643,16 @@ static int run_single_impl(kss_ctx* ctx, const PlanNeeds& need, const DevPods& d
   }
   if (simple)
     rc = launch_simple(ctx->stream, g, 1, jd, ctx->prof, n, (int)N, chunk, gran, gb,
-                       errp, stamps, ctx->loop_ev.data(), split ? &srun : nullptr);
+                       errp, stamps, ctx->loop_ev.data(), split ? &srun : nullptr, ctx->dc.n_scalar);
   else if (spread)
   {
-    const HandoffLayout hl(g.W, n_res, (int)N);
+    const HandoffLayout hl(g.W, n_res, (int)N, ctx->dc.n_scalar);
     if ((rc = ctx->ck_buf.ensure(sizeof(unsigned long long) * hl.words))) return rc;
     HIP_TRY(hipMemsetAsync((unsigned long long*)ctx->ck_buf.p + hl.o_diag, 0, sizeof(unsigned long long), ctx->stream));
     ctx->ck_diag_off = hl.o_diag;
     rc = launch_spread(ctx->stream, g, ctx->gneed, ctx->dc.n_keys, n_res, jd, ctx->prof, n,
                        (int)N, chunk, gran, gb, errp, stamps, ctx->loop_ev.data(), split ? &srun : nullptr,
-                       (unsigned long long*)ctx->ck_buf.p, &ctx->ck_seq);
+                       (unsigned long long*)ctx->ck_buf.p, &ctx->ck_seq, ctx->dc.n_scalar);
   }
   else
     rc = launch_schedule(ctx->stream, g, 1, std::max(need.bins_cap, 0), need.general, ctx->dc.n_keys,
@@ -3735,7 +3752,7 @@ kss_sweep* kss_sweep_create(int32_t device, const kss_profile* prof, int32_t n_s
   // k_static + k_simple for the whole sweep when every scenario qualifies (no spread /
   // inter-pod programs, no scalar resources, values inside the exact f64 envelope)
   std::vector<std::vector<SPod>> spods(n_scen);
-  bool simple = getenv("KSS_NO_SIMPLE") == nullptr && !sw->need.general && simple_fits(sw->g);
+  bool simple = getenv("KSS_NO_SIMPLE") == nullptr && !sw->need.general && simple_fits(sw->g, 0);
   for (int i = 0; i < prof->fit_n && simple; i++) simple = prof->fit_weight[i] >= 0 && prof->fit_weight[i] < (1ll << 20);
   for (int s = 0; s < n_scen && simple; s++) {
     const kss_cluster& cl = clusters[s];
@@ -4199,10 +4216,6 @@ int kss_plan_podset(const kss_cluster* cl, const kss_podset* ps, int32_t* out3) 
   out3[0] = 0;
   out3[1] = -1;
   out3[2] = GP_OK;
-  if (cl->n_scalar > 0) {  // run_single: simple_ok / spread_ok need dc.n_scalar == 0
-    out3[2] = GP_SCALAR;
-    return 0;
-  }
   if (build_spods(ps, cl->n_scalar, sp)) {
     out3[0] = 1;
     return 0;

@@ -150,6 +150,8 @@ struct SPod {
   int32_t cls;         // class_count row the pod joins (-1 none)
   int32_t own_off, own_len;  // term_count rows it adds: ints[own_off .. +own_len) of the staged pool
   int32_t pad[3];
+  int64_t sc_fit[KSS_MAX_SCALAR];  // NodeResourcesFit PreFilter request of each extended (scalar) resource
+  int64_t sc_req[KSS_MAX_SCALAR];  // AssumePod Requested delta of each scalar resource
 };
 static_assert(sizeof(SPod) % 16 == 0, "SPod is copied as uint4");
 
@@ -639,23 +641,26 @@ struct SimpleShard {
   uint32_t* st;   // [RING][cap]: static words of the pods in flight (ring slot = pod % RING)
   int32_t* cv;    // [5][cap + CV_EXTRA]: filter verdict, TT, NA, Fit, BA (slots cap + i: H1 values)
   SPod* ring;     // [RING]: pod records (ring slot = pod % RING)
-  int cap;
+  int64_t* sc;    // [2 nsc][cap]: allocatable, then requested, of each extended (scalar) resource
+  int cap, nsc;
 };
 
 constexpr int RING = 4;                // record / static-word ring slots
 constexpr int CV_EXTRA = MAXWAVES;     // H1 slots past the shard's nodes: one per wave (per-wave mode)
 constexpr int PW_LANES = 63;           // per-wave mode: node slots per wave (lane 63 is the wave's H1 lane)
 
-__host__ __device__ inline size_t simple_lds_bytes(int cap) {
-  return sizeof(SimpleHdr) + RING * sizeof(SPod) + (size_t)cap * (8 * 8 + 3 * 8 + 2 * 4 + RING * 4) +
+__host__ __device__ inline size_t simple_lds_bytes(int cap, int nsc = 0) {
+  return sizeof(SimpleHdr) + RING * sizeof(SPod) + (size_t)cap * (8 * 8 + 3 * 8 + 2 * 4 + RING * 4 + 16 * (size_t)nsc) +
          20 * ((size_t)cap + CV_EXTRA);
 }
 
-__device__ __forceinline__ SimpleShard shard_view(uint8_t* base, int cap) {
+__device__ __forceinline__ SimpleShard shard_view(uint8_t* base, int cap, int nsc) {
   SimpleShard L;
   L.cap = cap;
+  L.nsc = nsc;
   L.ring = reinterpret_cast<SPod*>(base);
-  uint8_t* b = base + RING * sizeof(SPod);
+  L.sc = reinterpret_cast<int64_t*>(base + RING * sizeof(SPod));
+  uint8_t* b = base + RING * sizeof(SPod) + 16 * (size_t)nsc * (size_t)cap;
   L.r64 = reinterpret_cast<double*>(b);
   L.inv = reinterpret_cast<double*>(b + 64 * (size_t)cap);
   L.r32 = reinterpret_cast<int32_t*>(b + 88 * (size_t)cap);
@@ -692,6 +697,22 @@ __device__ __forceinline__ void cv_put(const SimpleShard& L, int s, const SVal& 
   L.cv[2 * C1 + s] = e.na;
   L.cv[3 * C1 + s] = e.fit;
   L.cv[4 * C1 + s] = e.ba;
+}
+
+// NodeResourcesFit.Filter over the extended (scalar) resources (fitsRequest; a zero request
+// is skipped): true when some requested scalar exceeds the node's free amount.  sc: [2 nsc][cap]
+// allocatable, then requested; add: pod q0's AssumePod delta is added to the row first (H1).
+__device__ __forceinline__ bool scalar_short(const int64_t* sc, int nsc, int cap, int s, const SPod& q, bool add,
+                                             const SPod& q0) {
+  bool bad = false;
+#pragma unroll
+  for (int i = 0; i < KSS_MAX_SCALAR; i++) {
+    if (i >= nsc) break;
+    const int64_t req = q.sc_fit[i];
+    const int64_t used = sc[(size_t)(nsc + i) * cap + s] + (add ? q0.sc_req[i] : 0);
+    bad |= req != 0 && req > sc[(size_t)i * cap + s] - used;
+  }
+  return bad;
 }
 
 // NodeInfo.AddPod on a node row (requested, non-zero requested, pod count).
@@ -760,6 +781,11 @@ __device__ __forceinline__ void simple_pass_a(const kss_profile& prof, const SPo
   for (int k = 0; k < 3; k++) q0.creq[k] = q0_lds.creq[k];
   q0.cnz[0] = q0_lds.cnz[0];
   q0.cnz[1] = q0_lds.cnz[1];
+  const bool scal = L.nsc > 0 && (DEF || ((prof.filter_enabled >> KSS_F_NODE_RESOURCES_FIT) & 1u));
+  if (scal) {
+#pragma unroll
+    for (int i = 0; i < KSS_MAX_SCALAR; i++) q0.sc_req[i] = q0_lds.sc_req[i];
+  }
   int32_t nf = 0, tt = 0, na = 0, nf1 = 0, tt1 = 0, na1 = 0;  // raw TT <= 64, NA < 2^20
   for (int s = tid; s <= L.cap; s += nt) {
     const bool extra = s == own && cand_s >= 0;
@@ -768,7 +794,8 @@ __device__ __forceinline__ void simple_pass_a(const kss_profile& prof, const SPo
     const uint32_t wd = sw[ns];
     DynRow r = shard_row(L, ns);
     if (extra) add_commit(r, q0);
-    const SVal e = DEF ? dyn_eval_def(q, wd, r) : dyn_eval(prof, q, wd, r);
+    SVal e = DEF ? dyn_eval_def(q, wd, r) : dyn_eval(prof, q, wd, r);
+    if (scal && e.f == 0 && scalar_short(L.sc, L.nsc, L.cap, ns, q, extra, q0)) e.f = KSS_F_NODE_RESOURCES_FIT;
     cv_put(L, extra ? L.cap : s, e);
     // H0 counts the shard's own slots, H1 every slot but the candidate's (whose H1 value is
     // the extra slot's); selects, no exec-mask region
@@ -806,6 +833,11 @@ __device__ __forceinline__ void simple_pass_a_pw(const kss_profile& prof, const 
   for (int k = 0; k < 3; k++) q0.creq[k] = q0_lds.creq[k];
   q0.cnz[0] = q0_lds.cnz[0];
   q0.cnz[1] = q0_lds.cnz[1];
+  const bool scal = L.nsc > 0 && (DEF || ((prof.filter_enabled >> KSS_F_NODE_RESOURCES_FIT) & 1u));
+  if (scal) {
+#pragma unroll
+    for (int i = 0; i < KSS_MAX_SCALAR; i++) q0.sc_req[i] = q0_lds.sc_req[i];
+  }
   const int s = wv * pwv + lane;
   const bool extra = lane == pwv && cand_w >= 0;
   const bool mine = lane < pwv && s < own;
@@ -816,7 +848,8 @@ __device__ __forceinline__ void simple_pass_a_pw(const kss_profile& prof, const 
     const uint32_t wd = sw[ns];
     DynRow r = shard_row(L, ns);
     if (extra) add_commit(r, q0);
-    const SVal e = DEF ? dyn_eval_def(q, wd, r) : dyn_eval(prof, q, wd, r);
+    SVal e = DEF ? dyn_eval_def(q, wd, r) : dyn_eval(prof, q, wd, r);
+    if (scal && e.f == 0 && scalar_short(L.sc, L.nsc, L.cap, ns, q, extra, q0)) e.f = KSS_F_NODE_RESOURCES_FIT;
     cv_put(L, extra ? L.cap + wv : s, e);
     const bool c0 = e.f == 0 && !extra, c1 = e.f == 0 && (extra || s != cand_w);
     u[0] = c0 ? 1u : 0u;
@@ -837,6 +870,7 @@ __device__ __forceinline__ void simple_commit_slot(const SimpleShard& L, const S
   L.r64[6 * cap + s] += pk.cnz[0];
   L.r64[7 * cap + s] += pk.cnz[1];
   L.r32[s] += 1;
+  for (int i = 0; i < L.nsc; i++) L.sc[(size_t)(L.nsc + i) * cap + s] += pk.sc_req[i];
 }
 
 // Per-wave mode's one reduction per pod: the waves' best keys and H0 / H1 statistics in one
@@ -944,7 +978,7 @@ __device__ __forceinline__ void simple_schedule(DevCluster c, const SPod* __rest
                                                 unsigned epoch0, int* err, unsigned long long* stamps, long long* smem) {
   const int tid = threadIdx.x, nt = blockDim.x;
   SimpleHdr& H = *reinterpret_cast<SimpleHdr*>(smem);
-  const SimpleShard L = shard_view(reinterpret_cast<uint8_t*>(smem) + sizeof(SimpleHdr), cap);
+  const SimpleShard L = shard_view(reinterpret_cast<uint8_t*>(smem) + sizeof(SimpleHdr), cap, c.n_scalar);
   const size_t N = (size_t)c.N;
   const int per = (c.N + W - 1) / W;
   const int lo = min(c.N, w * per), hi = min(c.N, lo + per), own = hi - lo;
@@ -969,6 +1003,10 @@ __device__ __forceinline__ void simple_schedule(DevCluster c, const SPod* __rest
     L.r64[7 * cap + s] = (double)ld_ag(&c.nonzero[N + n]);
     L.r32[s] = ld_ag(&c.pod_count[n]);
     L.r32[cap + s] = c.allowed_pods[n];
+    for (int i = 0; i < L.nsc; i++) {
+      L.sc[(size_t)i * cap + s] = c.alloc[(size_t)(3 + i) * N + n];
+      L.sc[(size_t)(L.nsc + i) * cap + s] = ld_ag(&c.requested[(size_t)(3 + i) * N + n]);
+    }
     for (int d = 0; d < PD && k0 + d < k1; d++) L.st[((k0 + d) % RING) * cap + s] = ld_ag(&stat[(size_t)d * N + lo + s]);
   }
   for (int i = tid; i < min(k1 - k0, PD) * NQ; i += nt) {
@@ -1146,6 +1184,7 @@ __device__ __forceinline__ void simple_schedule(DevCluster c, const SPod* __rest
     st_ag(&c.nonzero[n], (int64_t)L.r64[6 * cap + s]);
     st_ag(&c.nonzero[N + n], (int64_t)L.r64[7 * cap + s]);
     st_ag(&c.pod_count[n], L.r32[s]);
+    for (int i = 0; i < L.nsc; i++) st_ag(&c.requested[(size_t)(3 + i) * N + n], L.sc[(size_t)(L.nsc + i) * cap + s]);
   }
   handoff_release();
 }

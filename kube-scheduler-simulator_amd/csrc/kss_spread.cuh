@@ -174,21 +174,24 @@ struct SpreadShard {
   int32_t* sfit;   // [cap]
   int32_t* sba;    // [cap]
   int32_t* scnt;   // [cap] single soft constraint: the node's count (-1 lacks the key)
-  int cap;
+  int64_t* sc;     // [2 nsc][cap] allocatable, then requested, of each extended (scalar) resource
+  int cap, nsc;
 };
 
-__host__ __device__ inline size_t spread_lds_bytes(int cap, int bins_cap, int n_keys, int n_res, int gq) {
+__host__ __device__ inline size_t spread_lds_bytes(int cap, int bins_cap, int n_keys, int n_res, int gq, int nsc = 0) {
   const size_t C = (size_t)cap;
   size_t b = (sizeof(SpreadHdr) + 4 * ((size_t)G_NS + (size_t)bins_cap) + 15) / 16 * 16;
   b += 3 * 16 * (size_t)gq + 4 * 2 * C + ((size_t)n_res * C * 2 + 15) / 16 * 16;
   b += 8 * 8 * C + 8 * 3 * C + 8 * 2 * C + 4 * 3 * C + 4 * (size_t)n_keys * C + 4 * 6 * C;
+  b += 16 * (size_t)nsc * C;
   return b;
 }
 
 __device__ __forceinline__ SpreadShard spread_view(long long* smem, int cap, int bins_cap, int n_keys, int n_res,
-                                                   int gq) {
+                                                   int gq, int nsc) {
   SpreadShard L;
   const size_t C = (size_t)cap;
+  L.nsc = nsc;
   uint8_t* b = reinterpret_cast<uint8_t*>(smem);
   size_t o = sizeof(SpreadHdr);
   L.xs = reinterpret_cast<int32_t*>(b + o);
@@ -201,6 +204,8 @@ __device__ __forceinline__ SpreadShard spread_view(long long* smem, int cap, int
   o += ((size_t)n_res * C * 2 + 15) / 16 * 16;
   L.r64 = reinterpret_cast<double*>(b + o);
   o += 8 * 8 * C;
+  L.sc = reinterpret_cast<int64_t*>(b + o);
+  o += 16 * (size_t)nsc * C;
   L.inv = reinterpret_cast<double*>(b + o);
   o += 8 * 3 * C;
   L.sipa = reinterpret_cast<long long*>(b + o);
@@ -871,7 +876,8 @@ __device__ __forceinline__ void spread_schedule(const GTrace& tr, DevCluster c, 
                                                 long long* smem) {
   const int tid = threadIdx.x, nt = blockDim.x;
   SpreadHdr& H = *reinterpret_cast<SpreadHdr*>(smem);
-  const SpreadShard L = spread_view(smem, cap, bins_cap, c.n_keys, n_res, gq);
+  const SpreadShard L = spread_view(smem, cap, bins_cap, c.n_keys, n_res, gq, c.n_scalar);
+  const int nsc = c.n_scalar;
   const size_t N = (size_t)c.N;
   const int per = (c.N + W - 1) / W;
   const int lo = min(c.N, w * per), hi = min(c.N, lo + per), own = hi - lo;
@@ -881,7 +887,7 @@ __device__ __forceinline__ void spread_schedule(const GTrace& tr, DevCluster c, 
   // (no HBM store on the exchange wave while the loop runs)
   unsigned long long* stl =
       stamps ? reinterpret_cast<unsigned long long*>(reinterpret_cast<uint8_t*>(smem) +
-                                                     spread_lds_bytes(cap, bins_cap, c.n_keys, n_res, gq))
+                                                     spread_lds_bytes(cap, bins_cap, c.n_keys, n_res, gq, c.n_scalar))
              : nullptr;
   if (stl)
     for (int i = tid; i < 16 * nst; i += nt) stl[i] = 0;
@@ -899,6 +905,7 @@ __device__ __forceinline__ void spread_schedule(const GTrace& tr, DevCluster c, 
     L.r32[cap + s] = c.allowed_pods[n];
     L.r32[2 * cap + s] = (int32_t)c.node_flags[n];
     for (int k = 0; k < c.n_keys; k++) L.lbl[k * cap + s] = c.label_value[(size_t)k * N + n];
+    for (int i = 0; i < nsc; i++) L.sc[(size_t)i * cap + s] = c.alloc[(size_t)(3 + i) * N + n];
     L.st[(k0 & 1) * cap + s] = ld_ag(&stat[(size_t)lo + s]);
   }
   // node state handed over by the previous chunk: loaded, then checked against the sum its
@@ -923,6 +930,12 @@ __device__ __forceinline__ void spread_schedule(const GTrace& tr, DevCluster c, 
       L.r32[s] = pc;
       h += handoff_mix((unsigned long long)z0, 3 * N + n) + handoff_mix((unsigned long long)z1, 4 * N + n) +
            handoff_mix((unsigned long long)(uint32_t)pc, 5 * N + n);
+      for (int i = 0; i < nsc; i++) {  // extended resources: shadow rows after the count rows
+        const size_t a = 6 + (size_t)n_res + i;
+        const int64_t v = shd ? ld_ag(&hc.shadow[a * N + n]) : ld_ag(&c.requested[(size_t)(3 + i) * N + n]);
+        L.sc[(size_t)(nsc + i) * cap + s] = v;
+        h += handoff_mix((unsigned long long)v, a * N + n);
+      }
     }
     for (int i = tid; i < n_res * own; i += nt) {
       const int r = i / own, s = i - r * own, row = res_rows[r];
@@ -1143,6 +1156,8 @@ __device__ __forceinline__ void spread_schedule(const GTrace& tr, DevCluster c, 
         r.pods = L.r32[s];
         r.allowed = L.r32[cap + s];
         SVal e = DEF ? dyn_eval_def(qd, wd, r) : dyn_eval(prof, qd, wd, r);
+        if (nsc && e.f == 0 && ((en >> KSS_F_NODE_RESOURCES_FIT) & 1u) && scalar_short(L.sc, nsc, cap, s, qd, false, qd))
+          e.f = KSS_F_NODE_RESOURCES_FIT;
         if (e.f == 0 && ((en >> KSS_F_POD_TOPOLOGY_SPREAD) & 1u) && q.n_hard > 0 &&
             g_filter_pts(L, q, bins, hard_min, s, wd))
           e.f = KSS_F_POD_TOPOLOGY_SPREAD;
@@ -1434,6 +1449,7 @@ __device__ __forceinline__ void spread_schedule(const GTrace& tr, DevCluster c, 
       L.r64[6 * cap + s] += pk.cnz[0];
       L.r64[7 * cap + s] += pk.cnz[1];
       L.r32[s] += 1;
+      for (int i = 0; i < nsc; i++) L.sc[(size_t)(nsc + i) * cap + s] += pk.sc_req[i];
       for (int i = 0; i < q.n_cmt; i++)
         if (q.cmt[i] >= 0) L.cnt[q.cmt[i] * cap + s] += 1;
     }
@@ -1477,6 +1493,11 @@ __device__ __forceinline__ void spread_schedule(const GTrace& tr, DevCluster c, 
       st_ag(&hc.shadow[4 * N + n], (long long)L.r64[7 * cap + s]);
       st_ag(&hc.shadow[5 * N + n], (long long)L.r32[s]);
     }
+    for (int i = 0; i < nsc; i++) {
+      const int64_t v = L.sc[(size_t)(nsc + i) * cap + s];
+      st_ag(&c.requested[(size_t)(3 + i) * N + n], v);
+      if (hc.shadow) st_ag(&hc.shadow[(6 + (size_t)n_res + i) * N + n], (long long)v);
+    }
   }
   unsigned long long h = 0;
   if (hc.sum)
@@ -1487,6 +1508,8 @@ __device__ __forceinline__ void spread_schedule(const GTrace& tr, DevCluster c, 
       h += handoff_mix((unsigned long long)(int64_t)L.r64[6 * cap + s], 3 * N + n) +
            handoff_mix((unsigned long long)(int64_t)L.r64[7 * cap + s], 4 * N + n) +
            handoff_mix((unsigned long long)(uint32_t)L.r32[s], 5 * N + n);
+      for (int i = 0; i < nsc; i++)
+        h += handoff_mix((unsigned long long)L.sc[(size_t)(nsc + i) * cap + s], (6 + (size_t)n_res + i) * N + n);
     }
   for (int i = tid; i < n_res * own; i += nt) {
     const int r = i / own, s = i - r * own, row = res_rows[r];

@@ -34,6 +34,8 @@ K_ITYPE = "node.kubernetes.io/instance-type"
 K_TIER = "example.com/tier"
 K_ACCEL = "example.com/accelerator"
 R_GPU = "example.com/gpu"
+# extended (scalar) resources beyond the first, used with make(..., n_extended=k)
+R_MORE = ["example.com/fpga", "hugepages-2Mi", "vendor.io/nic"]
 APPS = 6
 
 
@@ -69,6 +71,20 @@ def _node(i: int, r: random.Random, extended: bool = True) -> dict:
     if r.random() < 0.3 and extended:
         alloc[R_GPU] = r.choice(["1", "2", "4"])
     return {"metadata": {"name": name, "labels": labels}, "spec": spec, "status": {"allocatable": alloc}}
+
+
+def _more_extended(nodes, pods, bound, k: int, r: random.Random):
+    """k - 1 more extended resources: on some nodes (as allocatable), asked for by some pods."""
+    for res in R_MORE[:max(k - 1, 0)]:
+        for n in nodes:
+            if r.random() < 0.4:
+                n["status"]["allocatable"][res] = r.choice(["1", "2", "3"]) if "/" in res else r.choice(["4Mi", "8Mi"])
+        for p in pods + bound:
+            if r.random() < 0.15:
+                req = p["spec"]["containers"][0]["resources"]["requests"]
+                req[res] = "1" if "/" in res else r.choice(["2Mi", "4Mi"])
+                if r.random() < 0.1:
+                    req[res] = "0" if "/" in res else "0Mi"  # a zero request: fitsRequest skips it
 
 
 def _sel(r: random.Random) -> dict:
@@ -211,9 +227,11 @@ def _pending(j: int, r: random.Random, node_names: List[str], extended: bool = T
             "spec": spec}
 
 
-def make(seed: int, n_nodes: int, n_pods: int, bound_per_node: Tuple[int, int] = (0, 3), extended: bool = True):
+def make(seed: int, n_nodes: int, n_pods: int, bound_per_node: Tuple[int, int] = (0, 3), extended: bool = True,
+         n_extended: int = 1, programs: bool = True):
     """(nodes, bound_pods, pending_pods) for one seed.  extended=False leaves the extended
-    resource out (k_simple / k_spread keep cpu, memory and ephemeral-storage only)."""
+    resources out; n_extended (1-4) adds more of them; programs=False strips every
+    PodTopologySpread / InterPodAffinity term (pending and bound pods: a k_simple batch)."""
     r = random.Random(seed)
     nodes = [_node(i, r, extended) for i in range(n_nodes)]
     names = [n["metadata"]["name"] for n in nodes]
@@ -222,4 +240,15 @@ def make(seed: int, n_nodes: int, n_pods: int, bound_per_node: Tuple[int, int] =
         for k in range(r.randint(*bound_per_node)):
             bound.append(_bound(i, k, nm, r, extended))
     pods = [_pending(j, r, names, extended) for j in range(n_pods)]
+    if extended and n_extended > 1:
+        _more_extended(nodes, pods, bound, n_extended, r)
+    if not programs:
+        for p in pods + bound:
+            p["spec"].pop("topologySpreadConstraints", None)
+            aff = p["spec"].get("affinity")
+            if aff:
+                aff.pop("podAffinity", None)
+                aff.pop("podAntiAffinity", None)
+                if not aff:
+                    p["spec"].pop("affinity")
     return nodes, bound, pods

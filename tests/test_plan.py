@@ -23,12 +23,16 @@ def test_program_fuzz_batches_take_k_spread(seed, n_nodes, n_pods):
     assert native.plan_podset(cc.as_struct(), cp.as_struct())["kernel"] == "k_spread"
 
 
-def test_extended_resources_take_k_schedule():
-    nodes, bound, pods = progfuzz.make(1, 60, 200)
+def test_extended_resources_stay_on_the_loop_kernels():
+    """Extended (scalar) resources: k_simple / k_spread filter and commit them in LDS."""
+    nodes, bound, pods = progfuzz.make(1, 60, 200, n_extended=4)
     cc, cp, _ = compile_cluster(nodes, bound, pods)
-    assert cc.scalars == [progfuzz.R_GPU]
-    plan = native.plan_podset(cc.as_struct(), cp.as_struct())
-    assert plan["kernel"] == "k_schedule" and plan["reason"].startswith("extended (scalar) resources")
+    assert len(cc.scalars) == 4 and progfuzz.R_GPU in cc.scalars
+    assert native.plan_podset(cc.as_struct(), cp.as_struct())["kernel"] == "k_spread"
+    nodes, bound, pods = progfuzz.make(2, 60, 200, n_extended=2, programs=False)
+    cc, cp, _ = compile_cluster(nodes, bound, pods)
+    assert len(cc.scalars) == 2
+    assert native.plan_podset(cc.as_struct(), cp.as_struct())["kernel"] == "k_simple"
 
 
 def test_refusal_names_pod_and_reason():
