@@ -52,7 +52,7 @@ def cpu_threads():
     return max(1, min(t, aff)), {"nproc": os.cpu_count(), "affinity_cpus": aff, "omp_num_threads": env}
 
 
-def cpu_baseline(config, n_nodes, n_pods, seconds, threads, seed=0):
+def cpu_baseline(config, n_nodes, n_pods, seconds, threads, seed=0, curve=True):
     """The CPU oracle (plain-C restatement, OpenMP over nodes: the reference's
     parallelize.Until over nodes inside each pod) on the same workload: the whole
     sequential batch is scheduled from the initial snapshot, repeated until `seconds` of wall
@@ -77,11 +77,56 @@ def cpu_baseline(config, n_nodes, n_pods, seconds, threads, seed=0):
         reps += 1
     evals = reps * n * n_nodes
     _, host = cpu_threads()
-    return {"value": evals / t_used, "unit": "pod-node evals/s", "cores": threads, "kind": "port", "host": host,
-            "sample": f"{reps} x the first {n} of {n_pods} pods of config C{config} ({n_nodes} nodes), "
-                      f"sequential from the initial snapshot, {t_used:.1f} s wall, "
-                      f"oracle/kss_oracle.c OpenMP over nodes ({threads} threads)",
-            "pods_per_s": reps * n / t_used}
+    out = {"value": evals / t_used, "unit": "pod-node evals/s", "cores": threads, "kind": "port", "host": host,
+           "sample": f"{reps} x the first {n} of {n_pods} pods of config C{config} ({n_nodes} nodes), "
+                     f"sequential from the initial snapshot, {t_used:.1f} s wall, "
+                     f"oracle/kss_oracle.c OpenMP over nodes ({threads} threads)",
+           "pods_per_s": reps * n / t_used}
+    if curve and threads > 1:
+        out["threads_curve"] = thread_curve(prof, s, n_nodes, n, threads, out["pods_per_s"], kw)
+    return out
+
+
+def thread_curve(prof, s, n_nodes, n, threads, pods_per_s_at_threads, kw, seconds=2.0):
+    """The same oracle at 1 and threads/4 threads (short samples) beside the main figure, and
+    the figure at Parallelism = nproc PROJECTED by an Amdahl fit to the 1- and
+    `threads`-thread points: it is not measured, because a one-GPU box's CPU share is 16
+    threads (OMP_NUM_THREADS) while nproc counts the whole machine's cores."""
+    import oracle_c
+    pts = {}
+    for t in sorted({1, max(1, threads // 4)}):
+        m = max(1, n // 8)
+        k, used = 0, 0.0
+        while used < seconds:
+            t0 = time.perf_counter()
+            oracle_c.schedule(prof, s.cluster, s.pods, m, n_nodes, **dict(kw, threads=t))
+            used += time.perf_counter() - t0
+            k += 1
+        pts[t] = k * m / used
+    pts[threads] = pods_per_s_at_threads
+    s_meas = pts[threads] / pts[1]  # speedup at `threads`
+    f = max(0.0, min(1.0, (threads / s_meas - 1.0) / (threads - 1.0)))  # serial fraction
+    nproc = os.cpu_count() or threads
+    s_nproc = 1.0 / (f + (1.0 - f) / nproc)
+    return {"pods_per_s": {str(t): round(v, 2) for t, v in sorted(pts.items())}, "serial_fraction": round(f, 4),
+            "nproc": nproc, "pods_per_s_at_nproc_projected": round(pts[1] * s_nproc, 2),
+            "note": "1 and threads/4 from short samples of the same pod prefix; the nproc figure is an Amdahl "
+                    "projection from the 1- and max-thread points (not measured: a one-GPU box's CPU share is "
+                    "16 threads)"}
+
+
+def gpu_over_cpu(gpu_pods_per_s, cpu):
+    """The GPU line against the CPU restatement: at the measured thread count, and against the
+    faster nproc projection (thread_curve) when there is one."""
+    if not cpu or not cpu.get("pods_per_s"):
+        return None
+    out = {f"vs_{cpu['cores']}_threads": gpu_pods_per_s / cpu["pods_per_s"]}
+    curve = cpu.get("threads_curve") or {}
+    if curve:  # the fastest CPU figure: any measured thread count, or the nproc projection
+        best = max([cpu["pods_per_s"], curve.get("pods_per_s_at_nproc_projected", 0.0)] +
+                   list(curve.get("pods_per_s", {}).values()))
+        out["vs_fastest_cpu"] = gpu_pods_per_s / best
+    return out
 
 
 def cpu_baseline_scenarios(n_nodes, n_pods, seconds, threads, seed_of):
@@ -507,6 +552,7 @@ def run_split(args):
                          "loop_kernel_ms": loop_s * 1e3,
                          "note": "latency-bound: per pod 3-4 granule exchanges across every part's shards"},
             "cpu_baseline": cpu,
+            "gpu_over_cpu": gpu_over_cpu(scheduled * args.steps / elapsed, cpu),
         }
         print(json.dumps(out), flush=True)
     if world > 1 or parts > 1:
@@ -1039,6 +1085,7 @@ def main():
                          "traffic_detail": traffic_detail, "latency": latency,
                          "valu": valu_roofline(sq, loop_s, n_pods * n_nodes), "valu_detail": sq_detail},
             "cpu_baseline": cpu,
+            "gpu_over_cpu": gpu_over_cpu(pods_per_s, cpu),
             "c4_split": c4,
         }
         print(json.dumps(out), flush=True)
