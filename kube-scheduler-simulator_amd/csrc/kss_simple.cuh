@@ -781,11 +781,8 @@ __device__ __forceinline__ void simple_pass_a(const kss_profile& prof, const SPo
   for (int k = 0; k < 3; k++) q0.creq[k] = q0_lds.creq[k];
   q0.cnz[0] = q0_lds.cnz[0];
   q0.cnz[1] = q0_lds.cnz[1];
+  // extended resources: read from the LDS records inside the (rare) branch, not copied here
   const bool scal = L.nsc > 0 && (DEF || ((prof.filter_enabled >> KSS_F_NODE_RESOURCES_FIT) & 1u));
-  if (scal) {
-#pragma unroll
-    for (int i = 0; i < KSS_MAX_SCALAR; i++) q0.sc_req[i] = q0_lds.sc_req[i];
-  }
   int32_t nf = 0, tt = 0, na = 0, nf1 = 0, tt1 = 0, na1 = 0;  // raw TT <= 64, NA < 2^20
   for (int s = tid; s <= L.cap; s += nt) {
     const bool extra = s == own && cand_s >= 0;
@@ -795,7 +792,7 @@ __device__ __forceinline__ void simple_pass_a(const kss_profile& prof, const SPo
     DynRow r = shard_row(L, ns);
     if (extra) add_commit(r, q0);
     SVal e = DEF ? dyn_eval_def(q, wd, r) : dyn_eval(prof, q, wd, r);
-    if (scal && e.f == 0 && scalar_short(L.sc, L.nsc, L.cap, ns, q, extra, q0)) e.f = KSS_F_NODE_RESOURCES_FIT;
+    if (scal && e.f == 0 && scalar_short(L.sc, L.nsc, L.cap, ns, q_lds, extra, q0_lds)) e.f = KSS_F_NODE_RESOURCES_FIT;
     cv_put(L, extra ? L.cap : s, e);
     // H0 counts the shard's own slots, H1 every slot but the candidate's (whose H1 value is
     // the extra slot's); selects, no exec-mask region
@@ -833,11 +830,8 @@ __device__ __forceinline__ void simple_pass_a_pw(const kss_profile& prof, const 
   for (int k = 0; k < 3; k++) q0.creq[k] = q0_lds.creq[k];
   q0.cnz[0] = q0_lds.cnz[0];
   q0.cnz[1] = q0_lds.cnz[1];
+  // extended resources: read from the LDS records inside the (rare) branch, not copied here
   const bool scal = L.nsc > 0 && (DEF || ((prof.filter_enabled >> KSS_F_NODE_RESOURCES_FIT) & 1u));
-  if (scal) {
-#pragma unroll
-    for (int i = 0; i < KSS_MAX_SCALAR; i++) q0.sc_req[i] = q0_lds.sc_req[i];
-  }
   const int s = wv * pwv + lane;
   const bool extra = lane == pwv && cand_w >= 0;
   const bool mine = lane < pwv && s < own;
@@ -849,7 +843,7 @@ __device__ __forceinline__ void simple_pass_a_pw(const kss_profile& prof, const 
     DynRow r = shard_row(L, ns);
     if (extra) add_commit(r, q0);
     SVal e = DEF ? dyn_eval_def(q, wd, r) : dyn_eval(prof, q, wd, r);
-    if (scal && e.f == 0 && scalar_short(L.sc, L.nsc, L.cap, ns, q, extra, q0)) e.f = KSS_F_NODE_RESOURCES_FIT;
+    if (scal && e.f == 0 && scalar_short(L.sc, L.nsc, L.cap, ns, q_lds, extra, q0_lds)) e.f = KSS_F_NODE_RESOURCES_FIT;
     cv_put(L, extra ? L.cap + wv : s, e);
     const bool c0 = e.f == 0 && !extra, c1 = e.f == 0 && (extra || s != cand_w);
     u[0] = c0 ? 1u : 0u;
@@ -1018,10 +1012,26 @@ __device__ __forceinline__ void simple_schedule(DevCluster c, const SPod* __rest
 
   KSS_GLOBAL const uint32_t* gstat = gp(stat);
   KSS_GLOBAL const uint4* gspod = gp(reinterpret_cast<const uint4*>(spods));
-  KSS_GLOBAL int32_t* gchosen = gp(chosen);
-  KSS_GLOBAL PodMeta* gmeta = gp(meta);
   KSS_GLOBAL unsigned long long* gstamps = gp(stamps);
   long long st[6], R[4] = {0, 0, 0, 0};
+  // the outcome of pod pend_k, not yet stored (thread out_tid of shard w_off)
+  const int out_tid = (nt >> 6) > 1 ? 64 : 0;
+  const bool defer_out = PW && (nt >> 6) > 1;
+  PodMeta pend{};
+  int pend_k = -1;
+  auto store_pending = [&]() {
+    if (pend_k < 0) return;
+    if (chosen) gp(chosen)[pend_k] = pend.chosen;
+    if (meta) {
+      KSS_GLOBAL PodMeta* mm = gp(meta) + pend_k;
+      mm->chosen = pend.chosen;
+      mm->n_feasible = pend.n_feasible;
+      mm->scored = pend.scored;
+      mm->status = pend.status;
+      mm->best_total = pend.best_total;
+    }
+    pend_k = -1;
+  };
   int parity = 0, sub_s = -1;  // slot whose pass-B values are the H1 ones (the previous winner)
   int sub_h = cap;             // ... and the cv slot holding them
   unsigned epoch = epoch0;  // granule tags above every tag an earlier launch left (split grids)
@@ -1062,11 +1072,24 @@ __device__ __forceinline__ void simple_schedule(DevCluster c, const SPod* __rest
           if (j < pf_per) pfw[j] = ld_ag(&gstat[(size_t)(k + PD - k0) * N + lo + min(j * pf_n + pf_lane, own - 1)]);
       }
     };
-    // per-wave mode with several waves: issued while wave 0 exchanges (simple_sync_pw); a
-    // single wave issues them here (its exchange polls would otherwise wait on them)
-    if (!PW || nwave == 1) prefetch();
+    auto ring_store = [&]() {  // lanes past the end rewrite the last element with its own value
+      if (pf_on) {
+        reinterpret_cast<uint4*>(L.ring + (k + PD) % RING)[min(pf_lane, NQ - 1)] = pfq;
+#pragma unroll
+        for (int j = 0; j < PF_MAX; j++)
+          if (j < pf_per) L.st[((k + PD) % RING) * cap + min(j * pf_n + pf_lane, own - 1)] = pfw[j];
+      }
+    };
+    // issued here; per-wave mode with several waves stores them into the ring while wave 0
+    // exchanges (simple_sync_pw's idle hook: slot (k + PD) % RING held pod k - 1, whose last
+    // reader finished before the statistics barrier), then this pod's HBM stores follow, after
+    // every wait on a load of this wave
+    prefetch();
     auto prefetch_idle = [&]() {
-      if (nwave > 1) prefetch();
+      if (defer_out) {
+        ring_store();
+        if (tid == out_tid) store_pending();  // the previous pod's outcome
+      }
     };
     // pass B: NormalizeScore, weights, shard-best selectHost key of pod k
     const long long nf = R[1];
@@ -1146,35 +1169,25 @@ __device__ __forceinline__ void simple_schedule(DevCluster c, const SPod* __rest
       // the HBM-only class / term counts are applied after the launch (k_counts): nothing in
       // this loop reads them
     }
-    if (pf_on) {  // lanes past the end rewrite the last element with its own value
-      reinterpret_cast<uint4*>(L.ring + (k + PD) % RING)[min(pf_lane, NQ - 1)] = pfq;
-#pragma unroll
-      for (int j = 0; j < PF_MAX; j++)
-        if (j < pf_per) L.st[((k + PD) % RING) * cap + min(j * pf_n + pf_lane, own - 1)] = pfw[j];
-    }
-    // every part keeps the outcomes; their HBM stores are issued off wave 0 (whose vmcnt stays
-    // free for the next exchange's polls) and after the ring stores above (which wait on this
-    // wave's prefetch loads only, not on these stores)
-    if (k >= k0 && w == X.w_off && tid == (nwave > 1 ? 64 : 0)) {
+    if (!defer_out) ring_store();
+    // every part keeps the outcomes.  Their HBM stores are issued off wave 0 (whose vmcnt stays
+    // free for the exchange polls); with several waves in per-wave mode they are held in
+    // registers and issued while the NEXT pod's exchange runs (store_pending in the idle hook,
+    // ahead of that wave's prefetch loads), so no wait on a store lands on the pod chain
+    if (k >= k0 && w == X.w_off && tid == out_tid) {
       const long long K = R[0];
       const int x = K ? (int)(0xFFFFFFFFu - (uint32_t)(unsigned long long)K) - c.node_base : -1;
-      PodMeta m;
-      m.chosen = K ? x + c.node_base : -1;
-      m.n_feasible = (int)nf;
-      m.scored = (K && scored) ? 1 : 0;
-      m.status = pk.status != 0 ? (pk.status == KSS_PF_ERROR ? 3 : 2) : (nf == 0 ? 1 : 0);
-      m.best_total = m.scored ? (int64_t)((unsigned long long)K >> 32) : 0;
-      if (chosen) gchosen[k] = m.chosen;
-      if (meta) {
-        gmeta[k].chosen = m.chosen;
-        gmeta[k].n_feasible = m.n_feasible;
-        gmeta[k].scored = m.scored;
-        gmeta[k].status = m.status;
-        gmeta[k].best_total = m.best_total;
-      }
+      pend.chosen = K ? x + c.node_base : -1;
+      pend.n_feasible = (int)nf;
+      pend.scored = (K && scored) ? 1 : 0;
+      pend.status = pk.status != 0 ? (pk.status == KSS_PF_ERROR ? 3 : 2) : (nf == 0 ? 1 : 0);
+      pend.best_total = pend.scored ? (int64_t)((unsigned long long)K >> 32) : 0;
+      pend_k = k;
+      if (!defer_out) store_pending();
     }
     if (sp && tid == 0) sp[6] = wall_clock64();
   }
+  if (tid == out_tid) store_pending();  // the last pod's outcome
   // node state back to HBM
   __syncthreads();
   for (int s = tid; s < own; s += nt) {

@@ -1156,7 +1156,7 @@ __device__ __forceinline__ void spread_schedule(const GTrace& tr, DevCluster c, 
         r.pods = L.r32[s];
         r.allowed = L.r32[cap + s];
         SVal e = DEF ? dyn_eval_def(qd, wd, r) : dyn_eval(prof, qd, wd, r);
-        if (nsc && e.f == 0 && ((en >> KSS_F_NODE_RESOURCES_FIT) & 1u) && scalar_short(L.sc, nsc, cap, s, qd, false, qd))
+        if (nsc && e.f == 0 && ((en >> KSS_F_NODE_RESOURCES_FIT) & 1u) && scalar_short(L.sc, nsc, cap, s, q.dyn, false, q.dyn))
           e.f = KSS_F_NODE_RESOURCES_FIT;
         if (e.f == 0 && ((en >> KSS_F_POD_TOPOLOGY_SPREAD) & 1u) && q.n_hard > 0 &&
             g_filter_pts(L, q, bins, hard_min, s, wd))
