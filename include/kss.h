@@ -644,9 +644,15 @@ int kss_last_handoff_retries(kss_ctx* ctx, int32_t* retries);
  * its shadow differ, KSS_HANDOFF_DIAG_WORDS int64 per entry: {shard | loading XCC << 32 |
  * storing XCC << 40, array (0-2 requested, 3-4 nonzero, 5 pod count, 6 + r resident count row
  * r), node, state by agent load, by atomic add of 0, by nontemporal load, shadow value, the
- * chunk tag}.  Up to cap entries are copied; *n_entries = the entries listed (<= 64). */
-#define KSS_HANDOFF_DIAG_WORDS 8
+ * chunk tag, the word's device address, a 100 MHz timestamp}.  Up to cap entries are copied; *n_entries = the entries listed (<= 64). */
+#define KSS_HANDOFF_DIAG_WORDS 10
 int kss_last_handoff_diag(kss_ctx* ctx, int32_t* recovered, int64_t* entries, int32_t cap, int32_t* n_entries);
+/* Diagnosis: the device address and size of each of the context's device buffers, in a fixed
+ * order (cluster, pristine copy, pods, per-pod upload, record slot, outcomes, chosen, job,
+ * granules, error words, hand-off check, stamps, k_simple records, static words, k_spread
+ * records, resident rows, delta staging, node-axis values, bound pods, preemption scratch, the
+ * split inbox); *n = the number of entries (at most cap are written). */
+int kss_buffer_map(kss_ctx* ctx, uint64_t* base, uint64_t* bytes, int32_t cap, int32_t* n);
 /* launch geometry of the last scheduling launch: out[0] shards (workgroups) per cluster,
  * out[1] threads per workgroup, out[2] node slots per lane */
 int kss_last_geometry(kss_ctx* ctx, int32_t* out3);

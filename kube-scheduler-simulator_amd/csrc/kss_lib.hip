@@ -1468,6 +1468,7 @@ void kss_destroy(kss_ctx* ctx) {
   ctx->gpod_buf.release();
   ctx->res_buf.release();
   ctx->delta_buf.release();
+  ctx->ck_buf.release();
   split_release(ctx);
   if (ctx->pinned) hipHostFree(ctx->pinned);
   if (ctx->rb) hipHostFree(ctx->rb);
@@ -3535,6 +3536,25 @@ int kss_last_timing(kss_ctx* ctx, double* device_ms, int32_t* launches) {
 int kss_last_handoff_retries(kss_ctx* ctx, int32_t* retries) {
   if (!ctx || !retries) return fail(KSS_E_INVAL, "bad arguments");
   *retries = ctx->last_handoff_retries;
+  return 0;
+}
+
+int kss_buffer_map(kss_ctx* ctx, uint64_t* base, uint64_t* bytes, int32_t cap, int32_t* n) {
+  if (!ctx || !n || cap < 0 || (cap && (!base || !bytes))) return fail(KSS_E_INVAL, "bad arguments");
+  const DevBuf* bufs[] = {&ctx->cluster_buf, &ctx->pristine_buf, &ctx->pod_buf, &ctx->tmp_pod_buf, &ctx->slot_buf,
+                          &ctx->meta_buf,    &ctx->chosen_buf,   &ctx->job_buf, &ctx->gran_buf,    &ctx->err_buf,
+                          &ctx->ck_buf,      &ctx->stamp_buf,    &ctx->spod_buf, &ctx->stat_buf,   &ctx->gpod_buf,
+                          &ctx->res_buf,     &ctx->delta_buf,    &ctx->axis_cv, &ctx->bound_buf,   &ctx->pre_buf};
+  const int nb = (int)(sizeof(bufs) / sizeof(bufs[0]));
+  *n = nb + 1;
+  for (int i = 0; i < nb && i < cap; i++) {
+    base[i] = (uint64_t)(uintptr_t)bufs[i]->p;
+    bytes[i] = bufs[i]->cap;
+  }
+  if (nb < cap) {
+    base[nb] = (uint64_t)(uintptr_t)ctx->split_inbox;
+    bytes[nb] = ctx->split_inbox_bytes;
+  }
   return 0;
 }
 

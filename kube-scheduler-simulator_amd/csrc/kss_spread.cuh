@@ -620,7 +620,7 @@ __device__ __forceinline__ bool spread_argmax(SpreadHdr& H, int W, int w, int gs
 // shadow's value and the XCCs of the storing and loading shards (kss_last_handoff_diag).
 // hc.sum: [2 W] words {sum, tag} per shard.
 constexpr int HANDOFF_DIAG = 64;   // differing words listed per run
-constexpr int HANDOFF_DIAG_W = 8;  // words per listed entry
+constexpr int HANDOFF_DIAG_W = 10;  // words per listed entry
 struct HandoffCheck {
   unsigned long long* sum;    // null: no check
   unsigned long long expect;  // tag the previous chunk wrote (0: the first chunk of the call)
@@ -686,7 +686,7 @@ __device__ __forceinline__ bool handoff_verify(const HandoffCheck& hc, int w, un
 // One differing word of the hand-off (first disagreement of a launch): array a (0-2 requested,
 // 3-4 nonzero, 5 pod count, 6 + r resident count row r), node n, and the views of it.
 __device__ __forceinline__ void handoff_note(const HandoffCheck& hc, int w, int a, int n, long long plain,
-                                             long long atomic_v, long long nt, long long shadow) {
+                                             long long atomic_v, long long nt, long long shadow, const void* addr) {
   const long long e = __hip_atomic_fetch_add(hc.diag, 1ll, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (e >= HANDOFF_DIAG) return;
   long long* d = hc.diag + 1 + e * HANDOFF_DIAG_W;
@@ -698,6 +698,8 @@ __device__ __forceinline__ void handoff_note(const HandoffCheck& hc, int w, int 
   st_ag(&d[5], nt);
   st_ag(&d[6], shadow);
   st_ag(&d[7], (long long)hc.expect);
+  st_ag(&d[8], (long long)(uintptr_t)addr);
+  st_ag(&d[9], (long long)(unsigned)wall_clock64());
 }
 
 // The statistics of node slot s for pod q, accumulated into bins (SUM) / bins + total_bins
@@ -973,13 +975,13 @@ __device__ __forceinline__ void spread_schedule(const GTrace& tr, DevCluster c, 
             const long long pv = ld_ag(p);
             if (pv != sv)
               handoff_note(hc, w, a, n, pv, __hip_atomic_fetch_add(p, (int64_t)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
-                           __builtin_nontemporal_load(p), sv);
+                           __builtin_nontemporal_load(p), sv, p);
           } else {
             int32_t* p = &c.pod_count[n];
             const long long pv = ld_ag(p);
             if (pv != sv)
               handoff_note(hc, w, a, n, pv, __hip_atomic_fetch_add(p, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
-                           __builtin_nontemporal_load(p), sv);
+                           __builtin_nontemporal_load(p), sv, p);
           }
         }
       }
@@ -990,7 +992,7 @@ __device__ __forceinline__ void spread_schedule(const GTrace& tr, DevCluster c, 
         const long long sv = ld_ag(&hc.shadow[(6 + (size_t)r) * N + lo + s]), pv = ld_ag(p);
         if (pv != sv)
           handoff_note(hc, w, 6 + r, lo + s, pv, __hip_atomic_fetch_add(p, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
-                       __builtin_nontemporal_load(p), sv);
+                       __builtin_nontemporal_load(p), sv, p);
       }
     }
   }

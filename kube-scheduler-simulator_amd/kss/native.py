@@ -69,6 +69,7 @@ SIGNATURES = [
     ("kss_last_loop_timing", C.c_int, [C.c_void_p, P(C.c_double)]),
     ("kss_last_handoff_retries", C.c_int, [C.c_void_p, P(C.c_int32)]),
     ("kss_last_handoff_diag", C.c_int, [C.c_void_p, P(C.c_int32), P(C.c_int64), C.c_int32, P(C.c_int32)]),
+    ("kss_buffer_map", C.c_int, [C.c_void_p, P(C.c_uint64), P(C.c_uint64), C.c_int32, P(C.c_int32)]),
     ("kss_last_geometry", C.c_int, [C.c_void_p, P(C.c_int32)]),
     ("kss_last_kernel", C.c_int, [C.c_void_p]),
     ("kss_device_go_log", C.c_int, [C.c_int32, C.c_void_p, C.c_void_p, C.c_int32]),
@@ -528,15 +529,25 @@ class Context:
     def last_handoff_diag(self):
         """(shadow recoveries, [entry dicts]) of the last run (kss_last_handoff_diag)."""
         rec, n = C.c_int32(0), C.c_int32(0)
-        buf = (C.c_int64 * (64 * 8))()
+        W = 10  # KSS_HANDOFF_DIAG_WORDS
+        buf = (C.c_int64 * (64 * W))()
         check(lib().kss_last_handoff_diag(self.h, C.byref(rec), buf, 64, C.byref(n)))
         out = []
         for i in range(min(n.value, 64)):
-            e = buf[8 * i:8 * i + 8]
+            e = buf[W * i:W * i + W]
             out.append({"shard": e[0] & 0xFFFFFFFF, "xcc_load": (e[0] >> 32) & 0xFF, "xcc_store": (e[0] >> 40) & 0xFF,
                         "array": e[1], "node": e[2], "state": e[3], "atomic": e[4], "nontemporal": e[5],
-                        "shadow": e[6], "tag": e[7]})
+                        "shadow": e[6], "tag": e[7], "addr": e[8] & 0xFFFFFFFFFFFFFFFF, "t": e[9]})
         return rec.value, out
+
+    BUFFER_NAMES = ("cluster", "pristine", "pods", "tmp_pods", "slot", "meta", "chosen", "job", "gran", "err", "ck",
+                    "stamps", "spods", "stat", "gpods", "res", "delta", "axis_cv", "bound", "pre", "split_inbox")
+
+    def buffer_map(self):
+        """{name: (device base, bytes)} of the context's device buffers (kss_buffer_map)."""
+        base, size, n = (C.c_uint64 * 32)(), (C.c_uint64 * 32)(), C.c_int32(0)
+        check(lib().kss_buffer_map(self.h, base, size, 32, C.byref(n)))
+        return {nm: (base[i], size[i]) for i, nm in enumerate(self.BUFFER_NAMES[:n.value])}
 
     def last_geometry(self):
         out = (C.c_int32 * 3)()

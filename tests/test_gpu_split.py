@@ -118,7 +118,14 @@ def _handoff_report(sp, rep, failed=False):
         lines.append(f"run {rep} part {p}{' FAILED' if failed else ''}: reloads {retries}, shadow answered {rec}, "
                      f"differing words {len(entries)}")
         lines += [f"  {e}" for e in entries[:16]]
+        for e in entries[:4]:  # which buffer of which part holds the word, and its neighbours
+            for q, c2 in enumerate(sp.ctxs):
+                for nm, (b, sz) in c2.buffer_map().items():
+                    if b and b - (1 << 22) <= e["addr"] < b + sz + (1 << 22):
+                        lines.append(f"    word {e['addr']:#x}: part {q} {nm} [{b:#x}, +{sz}) offset {e['addr'] - b}")
     if lines:
+        allb = sorted((b, sz, q, nm) for q, c2 in enumerate(sp.ctxs) for nm, (b, sz) in c2.buffer_map().items() if b)
+        lines.append("  buffers: " + ", ".join(f"p{q}.{nm}@{b:#x}+{sz}" for b, sz, q, nm in allb))
         print("\n".join(lines))
         if os.environ.get("KSS_HANDOFF_LOG"):
             with open(os.environ["KSS_HANDOFF_LOG"], "a") as f:
