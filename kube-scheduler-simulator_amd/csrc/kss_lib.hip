@@ -400,6 +400,28 @@ __global__ __launch_bounds__(256) void k_reset_state(ResetArgs a) {
   handoff_release();
 }
 
+// Zero fill of device memory with agent-scope (sc1) stores, in place of the runtime's fill
+// kernel (hipMemsetAsync).  The many-chunk split-grid corruption was a class
+// count word of node state reading 0 after a chunk had stored 1 into it, in the first run
+// after the cluster upload, whose count rows a hipMemsetAsync zeroed before the host rows
+// were copied over them; no library buffer is zeroed by the runtime's fill kernel any more.
+__global__ __launch_bounds__(256) void k_zero(uint32_t* p, size_t n4) {
+  unsigned long long* q = reinterpret_cast<unsigned long long*>(p);
+  const size_t n8 = ((uintptr_t)p & 7) ? 0 : n4 / 2, stride = (size_t)gridDim.x * blockDim.x;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n8; i += stride) st_ag(q + i, 0ull);
+  for (size_t i = 2 * n8 + blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n4; i += stride) st_ag(p + i, 0u);
+  handoff_release();
+}
+// bytes: a multiple of 4 (every library buffer's element size is)
+static hipError_t dev_zero(void* p, size_t bytes, hipStream_t st) {
+  if (bytes & 3) return hipMemsetAsync(p, 0, bytes, st);  // not used by the library's buffers
+  const size_t n4 = bytes / 4;
+  if (!p || n4 == 0) return hipSuccess;
+  const unsigned grid = (unsigned)std::min<size_t>(1024, (n4 / 2 + 255) / 256 + 1);
+  hipLaunchKernelGGL(k_zero, dim3(grid), dim3(256), 0, st, (uint32_t*)p, n4);
+  return hipGetLastError();
+}
+
 // ---------------------------------------------------------------------------
 // context
 // ---------------------------------------------------------------------------
@@ -1233,12 +1255,12 @@ int fill_cluster(hipStream_t st, const kss_cluster* cl, int class_cap, int term_
   rc |= cp(L.o_ke, cl->key_empty, 4 * (size_t)cl->n_label_keys);
   rc |= cp(L.o_vi, cl->value_int, 8 * (size_t)cl->n_label_values);
   rc |= cp(L.o_vii, cl->value_is_int, (size_t)cl->n_label_values);
-  if (class_cap) HIP_TRY(hipMemsetAsync(b + L.o_cc, 0, 4 * (size_t)class_cap * N, st));
-  if (term_cap) HIP_TRY(hipMemsetAsync(b + L.o_tc, 0, 4 * (size_t)term_cap * N, st));
+  if (class_cap) HIP_TRY(dev_zero(b + L.o_cc, 4 * (size_t)class_cap * N, st));
+  if (term_cap) HIP_TRY(dev_zero(b + L.o_tc, 4 * (size_t)term_cap * N, st));
   rc |= cp(L.o_cc, cl->class_count, 4 * (size_t)cl->n_classes * N);
   rc |= cp(L.o_tc, cl->term_count, 4 * (size_t)cl->n_terms * N);
   if (cl->port_used) rc |= cp(L.o_pu, cl->port_used, 8 * N);
-  else HIP_TRY(hipMemsetAsync(b + L.o_pu, 0, 8 * std::max<size_t>(N, 1), st));
+  else HIP_TRY(dev_zero(b + L.o_pu, 8 * std::max<size_t>(N, 1), st));
   rc |= cp(L.o_img, cl->image_score, 8 * (size_t)cl->n_images * N);
   rc |= cp(L.o_vc, cl->vol_count, 4 * (size_t)cl->n_vol_rows * N);
   rc |= cp(L.o_va, cl->vol_attached, 4 * (size_t)cl->n_vol_keys * N);
@@ -1535,10 +1557,21 @@ int kss_load_cluster(kss_ctx* ctx, const kss_cluster* cl) {
   if (rc) return rc;
   void* src[8] = {ctx->dc.requested,  ctx->dc.nonzero,   ctx->dc.pod_count, ctx->dc.class_count,
                   ctx->dc.term_count, ctx->dc.port_used, ctx->dc.vol_count, ctx->dc.vol_attached};
-  for (int i = 0; i < 8; i++)
-    if (mb[i])
-      HIP_TRY(hipMemcpyAsync((char*)ctx->pristine_buf.p + ctx->pristine_off[i], src[i], mb[i], hipMemcpyDeviceToDevice,
-                             ctx->stream));
+  {  // the copy by the reset kernel (agent-scope loads and stores), not the runtime's copy path
+    ResetArgs a{};
+    size_t most = 0;
+    for (int i = 0; i < 8; i++) {
+      a.dst[i] = (uint32_t*)((char*)ctx->pristine_buf.p + ctx->pristine_off[i]);
+      a.src[i] = (const uint32_t*)src[i];
+      a.n4[i] = src[i] ? mb[i] / 4 : 0;
+      most = std::max(most, a.n4[i]);
+    }
+    if (most) {
+      hipLaunchKernelGGL(k_reset_state, dim3((unsigned)std::min<size_t>(1024, (most + 255) / 256)), dim3(256), 0,
+                         ctx->stream, a);
+      HIP_TRY(hipGetLastError());
+    }
+  }
   HIP_TRY(hipStreamSynchronize(ctx->stream));
   ctx->host = *cl;
   {
@@ -1886,7 +1919,8 @@ int kss_split_config(kss_ctx* ctx, int32_t n_parts, int32_t part, int32_t shards
     ctx->split_inbox = nullptr;
     if (hipMalloc(&ctx->split_inbox, bytes) != hipSuccess) return fail(KSS_E_NOMEM, "split inbox allocation failed");
   }
-  HIP_TRY(hipMemset(ctx->split_inbox, 0, bytes));
+  HIP_TRY(dev_zero(ctx->split_inbox, bytes, ctx->stream));
+  HIP_TRY(hipStreamSynchronize(ctx->stream));
   HIP_TRY(hipDeviceSynchronize());
   ctx->split_inbox_bytes = bytes;
   ctx->split_n = n_parts;
@@ -2265,7 +2299,7 @@ static int launch_simple(hipStream_t st, const Geometry& g, int n_jobs, const De
       epoch0 = split->epoch0 + (unsigned)(k0 / std::max(chunk, 1)) * chunk_span(chunk);
       split_chunk_view(*split, k0 / std::max(chunk, 1), gran, gc, X);
     } else if (gran && k0 > 0) {
-      HIP_TRY(hipMemsetAsync(gran, 0, gran_bytes, st));
+      HIP_TRY(dev_zero(gran, gran_bytes, st));
     }
     unsigned long long* sp = k0 == 0 ? stamps : nullptr;
     void* args[] = {(void*)&jobs, (void*)&pr, (void*)&W,  (void*)&cap, (void*)&k0, (void*)&k1,
@@ -2361,7 +2395,7 @@ static int launch_spread(hipStream_t st, const Geometry& g, const GpodNeeds& q, 
       epoch0 = split->epoch0 + (unsigned)(k0 / std::max(chunk, 1)) * chunk_span(chunk);
       split_chunk_view(*split, k0 / std::max(chunk, 1), gran, gc, X);
     } else if (gran && k0 > 0) {
-      HIP_TRY(hipMemsetAsync(gran, 0, gran_bytes, st));
+      HIP_TRY(dev_zero(gran, gran_bytes, st));
     }
     unsigned long long* sp = k0 == 0 ? stamps : nullptr;
     // the checked node-state hand-off between this call's chunks (HandoffCheck): tags increase
@@ -2565,10 +2599,10 @@ static int run_single_impl(kss_ctx* ctx, const PlanNeeds& need, const DevPods& d
   if (spread) {  // every pod and shard, and the list of nonzero counts loaded / written back
     ctx->trace_words = (size_t)n * (size_t)g.W * G_TW;
     if ((rc = ctx->trace_buf.ensure(4 * ctx->trace_words))) return rc;
-    HIP_TRY(hipMemsetAsync(ctx->trace_buf.p, 0, 4 * ctx->trace_words, ctx->stream));
+    HIP_TRY(dev_zero(ctx->trace_buf.p, 4 * ctx->trace_words, ctx->stream));
     job.trace.words = (int32_t*)ctx->trace_buf.p;
     if ((rc = ctx->trace_list_buf.ensure(4 * (4 + 4 * (size_t)G_TLIST)))) return rc;
-    HIP_TRY(hipMemsetAsync(ctx->trace_list_buf.p, 0, 16, ctx->stream));
+    HIP_TRY(dev_zero(ctx->trace_list_buf.p, 16, ctx->stream));
     job.trace.list = (int32_t*)ctx->trace_list_buf.p;
   }
 #endif
@@ -2608,7 +2642,7 @@ static int run_single_impl(kss_ctx* ctx, const PlanNeeds& need, const DevPods& d
     if (reuse) {
       epoch0 = ctx->gran_epoch;
     } else {
-      HIP_TRY(hipMemsetAsync(gran, 0, gb, ctx->stream));  // every polled word zeroed
+      HIP_TRY(dev_zero(gran, gb, ctx->stream));  // every polled word zeroed
     }
     ctx->gran_epoch = loop ? 0 : epoch0 + span;
   }
@@ -2617,7 +2651,7 @@ static int run_single_impl(kss_ctx* ctx, const PlanNeeds& need, const DevPods& d
     errp = (int*)(pu->dev + pu->extra_off + align_up(sizeof(DevJob), 16));  // zero in the upload image
     std::memset(pu->host + pu->extra_off + align_up(sizeof(DevJob), 16), 0, 16);
   } else {
-    HIP_TRY(hipMemsetAsync(ctx->err_buf.p, 0, 16, ctx->stream));
+    HIP_TRY(dev_zero(ctx->err_buf.p, 16, ctx->stream));
   }
   const DevJob* jd = (const DevJob*)ctx->job_buf.p;
   if (pu) {  // the job rides in the per-pod call's single upload
@@ -2634,7 +2668,7 @@ static int run_single_impl(kss_ctx* ctx, const PlanNeeds& need, const DevPods& d
   if (ctx->stamps_file) {
     if ((rc = ctx->stamp_buf.ensure(stamp_bytes))) return rc;
     stamps = (unsigned long long*)ctx->stamp_buf.p;
-    HIP_TRY(hipMemsetAsync(stamps, 0, stamp_bytes, ctx->stream));
+    HIP_TRY(dev_zero(stamps, stamp_bytes, ctx->stream));
   }
   const int n_chunks = loop ? (n + chunk - 1) / std::max(chunk, 1) : 0;
   while ((int)ctx->loop_ev.size() < 2 * n_chunks) {
@@ -2649,7 +2683,7 @@ static int run_single_impl(kss_ctx* ctx, const PlanNeeds& need, const DevPods& d
   {
     const HandoffLayout hl(g.W, n_res, (int)N, ctx->dc.n_scalar);
     if ((rc = ctx->ck_buf.ensure(sizeof(unsigned long long) * hl.words))) return rc;
-    HIP_TRY(hipMemsetAsync((unsigned long long*)ctx->ck_buf.p + hl.o_diag, 0, sizeof(unsigned long long), ctx->stream));
+    HIP_TRY(dev_zero((unsigned long long*)ctx->ck_buf.p + hl.o_diag, sizeof(unsigned long long), ctx->stream));
     ctx->ck_diag_off = hl.o_diag;
     rc = launch_spread(ctx->stream, g, ctx->gneed, ctx->dc.n_keys, n_res, jd, ctx->prof, n,
                        (int)N, chunk, gran, gb, errp, stamps, ctx->loop_ev.data(), split ? &srun : nullptr,
@@ -3192,11 +3226,11 @@ static int svc_launch(kss_ctx* ctx) {
   HIP_TRY(hipSetDevice(ctx->cfg.device));
   const unsigned long long seq0 = __atomic_load_n(&v.box->consumed, __ATOMIC_ACQUIRE);
   const size_t relay_bytes = sizeof(unsigned long long) * 2 * SVC_DRING;
-  HIP_TRY(hipMemsetAsync(v.relay.p, 0, relay_bytes, v.stream));
+  HIP_TRY(dev_zero(v.relay.p, relay_bytes, v.stream));
   std::vector<unsigned long long> seen((size_t)v.W, seq0);  // the relay throttle starts from here
   HIP_TRY(hipMemcpyAsync((char*)v.relay.p + relay_bytes, seen.data(), 8 * seen.size(), hipMemcpyHostToDevice, v.stream));
-  if (v.W > 1) HIP_TRY(hipMemsetAsync(v.gran.p, 0, v.gran.cap, v.stream));  // epochs restart at 0
-  HIP_TRY(hipMemsetAsync(v.err.p, 0, 16, v.stream));
+  if (v.W > 1) HIP_TRY(dev_zero(v.gran.p, v.gran.cap, v.stream));  // epochs restart at 0
+  HIP_TRY(dev_zero(v.err.p, 16, v.stream));
   v.box->err = 0;
   const void* fn = v.gen ? (const void*)k_service<true> : (const void*)k_service<false>;
   HIP_TRY(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)v.shmem));
@@ -3349,11 +3383,24 @@ static int svc_stop(kss_ctx* ctx) {
   auto& v = ctx->svc;
   if (!v.running) return 0;
   unsigned long long seq = 0;
+  bool stop_queued = false;
   if (int rc = svc_revive(ctx)) return rc;  // never drop a queued commit / rollback
   if (svc_alive(ctx)) {
     if (int rc = svc_post(ctx, SVC_STOP, 0, 0, 0, &seq)) return rc;
+    stop_queued = true;
   }
   HIP_TRY(hipStreamSynchronize(v.stream));
+  // the grid may have left on its idle timeout between the check above and the STOP: it is
+  // relaunched for the commands it did not take, a STOP behind them
+  for (int again = 0; again < 4 && !v.box->err && __atomic_load_n(&v.box->consumed, __ATOMIC_ACQUIRE) < v.posted;
+       again++) {
+    if (int rc = svc_launch(ctx)) return rc;
+    if (!stop_queued) {
+      if (int rc = svc_post(ctx, SVC_STOP, 0, 0, 0, &seq)) return rc;
+      stop_queued = true;
+    }
+    HIP_TRY(hipStreamSynchronize(v.stream));
+  }
   v.running = false;
   const bool err = v.box->err != 0;
   if (!err && __atomic_load_n(&v.box->consumed, __ATOMIC_ACQUIRE) < v.posted)
@@ -3886,7 +3933,7 @@ int kss_sweep_run(kss_sweep* sw, int32_t* chosen_out, double* device_ms) {
   // every run starts from the snapshot: one device copy of all scenarios' mutable columns
   HIP_TRY(hipMemcpyAsync(sw->arena + sw->live_off, sw->arena + sw->pristine_off, sw->mut_bytes, hipMemcpyDeviceToDevice, st));
   int* err = reinterpret_cast<int*>(sw->arena + sw->err_off);
-  HIP_TRY(hipMemsetAsync(err, 0, 16, st));
+  HIP_TRY(dev_zero(err, 16, st));
   const DevJob* jobs = reinterpret_cast<const DevJob*>(sw->arena + sw->jobs_off);
   int rc;
   if (sw->simple)
@@ -4154,7 +4201,7 @@ int kss_postfilter_pod(kss_ctx* ctx, const kss_podset* ps, int32_t pod_index, ks
   const unsigned nsb = (unsigned)std::min<size_t>(std::max<size_t>((N + 255) / 256, 1), PRE_STATS_MAX_BLOCKS);
   HIP_TRY(hipMemcpyAsync(d + o_job, &J, sizeof(J), hipMemcpyHostToDevice, ctx->stream));
   HIP_TRY(hipEventRecord(ctx->ev0, ctx->stream));
-  HIP_TRY(hipMemsetAsync(d + o_g, 0, o_top - o_g, ctx->stream));  // PreGlobal (ticket, sums) and the bins
+  HIP_TRY(dev_zero(d + o_g, o_top - o_g, ctx->stream));  // PreGlobal (ticket, sums) and the bins
   const PreemptJob* jd = (const PreemptJob*)(d + o_job);
   hipLaunchKernelGGL(k_preempt_stats, dim3(nsb), dim3(256), lds, ctx->stream, jd);  // a lane per node of the range
   const unsigned nb = (unsigned)((N + PRE_NODE_THREADS - 1) / PRE_NODE_THREADS);
