@@ -59,7 +59,7 @@ NON_CSI = {
 MIGRATABLE = {"awsElasticBlockStore": "kubernetes.io/aws-ebs", "gcePersistentDisk": "kubernetes.io/gce-pd",
               "azureDisk": "kubernetes.io/azure-disk", "azureFile": "kubernetes.io/azure-file",
               "cinder": "kubernetes.io/cinder", "vsphereVolume": "kubernetes.io/vsphere-volume",
-              "portworxVolume": "kubernetes.io/portworx-volume"}
+              "portworxVolume": "kubernetes.io/portworx-volume", "rbd": "kubernetes.io/rbd"}
 ID_PREFIX = "kss-vol"  # the plugins' randomVolumeIDPrefix: only equality of ids matters
 
 

@@ -56,7 +56,7 @@ NON_CSI = {
 MIGRATABLE = {"awsElasticBlockStore": "kubernetes.io/aws-ebs", "gcePersistentDisk": "kubernetes.io/gce-pd",
               "azureDisk": "kubernetes.io/azure-disk", "azureFile": "kubernetes.io/azure-file",
               "cinder": "kubernetes.io/cinder", "vsphereVolume": "kubernetes.io/vsphere-volume",
-              "portworxVolume": "kubernetes.io/portworx-volume"}
+              "portworxVolume": "kubernetes.io/portworx-volume", "rbd": "kubernetes.io/rbd"}
 RANDOM_PREFIX = "kss"  # each plugin's randomVolumeIDPrefix: only equality of the ids matters
 
 

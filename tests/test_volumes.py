@@ -71,6 +71,35 @@ def test_volume_rows_and_keys():
     assert list(a["vol_limit"][0]) == [1, 3, -1]
 
 
+def test_intree_rbd_provisioner_is_not_a_csi_driver():
+    """csi-translation-lib (v1.26) lists the in-tree RBD plugin: with migration off, an unbound
+    claim whose StorageClass provisioner is kubernetes.io/rbd has no CSI driver
+    (getCSIDriverInfoFromSC returns ""), so it counts toward no attach-limit key, while a CSI
+    provisioner's claim does; an inline rbd volume on a node whose CSINode lists the plugin as
+    migrated is refused like the other migratable sources (parity unpinned: the translation
+    lib is not vendored under the reference)."""
+    nodes = [ef.node("a"), ef.node("b")]
+    st = vf.storage(pvs=[vf.pv("pv-1", vf.csi("ebs.csi.aws.com", "h-1"))],
+                    pvcs=[vf.pvc("u-rbd", bound=False, sc="rbd-sc"), vf.pvc("u-csi", bound=False, sc="csi-sc"),
+                          vf.pvc("c-1", "pv-1")],
+                    scs=[{"metadata": {"name": "rbd-sc"}, "provisioner": "kubernetes.io/rbd",
+                          "volumeBindingMode": "Immediate"},
+                         {"metadata": {"name": "csi-sc"}, "provisioner": "ebs.csi.aws.com",
+                          "volumeBindingMode": "Immediate"}],
+                    csinodes=[{"metadata": {"name": n}, "spec": {"drivers": [
+                        {"name": "ebs.csi.aws.com", "allocatable": {"count": 5}},
+                        {"name": "kubernetes.io/rbd", "allocatable": {"count": 5}}]}} for n in "ab"])
+    bound = [vf.vpod("x", vf.claim("u-rbd"), node_name="a"), vf.vpod("y", vf.claim("u-csi"), node_name="b")]
+    cc, cp, _ = compile_cluster(nodes, bound, [vf.vpod("p", vf.claim("c-1"))], storage=st)
+    assert cc.vol_keys == ["attachable-volumes-csi-ebs.csi.aws.com"]
+    assert list(cc.arrays["vol_attached"][0]) == [0, 1]
+    mig = [{"metadata": {"name": "a", "annotations": {"storage.alpha.kubernetes.io/migrated-plugins":
+                                                      "kubernetes.io/rbd"}}, "spec": {"drivers": []}}]
+    with pytest.raises(Unsupported, match="migrated"):
+        compile_cluster([ef.node("a")], [], [vf.vpod("p", vf.rbd(["m1"], "p", "img"))],
+                        storage=vf.storage(csinodes=mig))
+
+
 def test_refusals():
     nodes = [ef.node("a")]
     wffc = {"metadata": {"name": "late"}, "provisioner": "x", "volumeBindingMode": "WaitForFirstConsumer"}
