@@ -444,21 +444,27 @@ __device__ __forceinline__ void wave_red_stats_pw(uint32_t (&v)[6]) {
 // 0 stays "no feasible node".  One DPP max per step instead of a 64-bit compare and select.
 __device__ __forceinline__ int key_bits(const kss_profile& prof, int N) {
   const uint32_t se = prof.score_enabled;
-  long long tmax = 0;
-  for (int p : {KSS_S_TAINT_TOLERATION, KSS_S_NODE_AFFINITY, KSS_S_NODE_RESOURCES_FIT, KSS_S_POD_TOPOLOGY_SPREAD,
-                KSS_S_BALANCED_ALLOCATION})
-    if ((se >> p) & 1u) tmax += 100ll * (long long)prof.weight[p];
+  long long tmax = 0;  // every normalised score is at most MaxNodeScore (100)
+  for (int p = 0; p < KSS_NSCORE; p++)
+    if ((se >> p) & 1u) tmax += 100ll * (long long)max(prof.weight[p], 0);
   const int kb = 32 - __clz((unsigned)max(N, 1));  // 2^kb > N
   return tmax < (1ll << (32 - kb)) ? kb : 0;
 }
+__device__ __forceinline__ uint32_t key_compress(long long key, int kb, int node_base) {
+  if (!key) return 0;
+  const uint32_t m = (1u << kb) - 1u;
+  const uint32_t li = (0xFFFFFFFFu - (uint32_t)(unsigned long long)key) - (uint32_t)node_base;
+  return ((uint32_t)((unsigned long long)key >> 32) << kb) | (m - li);
+}
+__device__ __forceinline__ long long key_expand(uint32_t k, int kb, int node_base) {
+  if (!k) return 0;
+  const uint32_t m = (1u << kb) - 1u;
+  const uint32_t li = m - (k & m);
+  return (long long)(((unsigned long long)(k >> kb) << 32) | (0xFFFFFFFFull - ((uint32_t)node_base + li)));
+}
 __device__ __forceinline__ long long wave_max_key(long long key, int kb, int node_base) {
   if (!kb) return wave_red<OP_MAX>(key);
-  const uint32_t m = (1u << kb) - 1u;
-  uint32_t k = 0;
-  if (key) {
-    const uint32_t li = (0xFFFFFFFFu - (uint32_t)(unsigned long long)key) - (uint32_t)node_base;
-    k = ((uint32_t)((unsigned long long)key >> 32) << kb) | (m - li);
-  }
+  uint32_t k = key_compress(key, kb, node_base);
 #define KSS_KSTEP(CTRL, ROWS) k = max(k, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)k, CTRL, ROWS, 0xF, false))
   KSS_KSTEP(0xB1, 0xF);
   KSS_KSTEP(0x4E, 0xF);
@@ -468,9 +474,7 @@ __device__ __forceinline__ long long wave_max_key(long long key, int kb, int nod
   KSS_KSTEP(0x143, 0xC);
 #undef KSS_KSTEP
   k = (uint32_t)__builtin_amdgcn_readlane((int)k, 63);
-  if (!k) return 0;
-  const uint32_t li = m - (k & m);
-  return (long long)(((unsigned long long)(k >> kb) << 32) | (0xFFFFFFFFull - ((uint32_t)node_base + li)));
+  return key_expand(k, kb, node_base);
 }
 
 // LDS image of the loop head: reduction scratch (double-buffered), exchange results.

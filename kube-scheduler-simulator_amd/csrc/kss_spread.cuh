@@ -506,12 +506,13 @@ __device__ __forceinline__ bool spread_reduce(SpreadHdr& H, int32_t* xs, int W, 
   return true;
 }
 
-// Cluster MAX of the packed selectHost key (two granules: lo, hi).
+// Cluster MAX of the packed selectHost key: one granule {epoch, 32-bit key} per shard when the
+// key fits 32 bits (kb > 0, key_bits), else two (lo, hi).
 __device__ __forceinline__ bool spread_argmax(SpreadHdr& H, int W, int w, int gs, unsigned& epoch, unsigned long long* gran,
                                               const XPeers& X,
-                                              int* err, int parity, long long& key) {
+                                              int* err, int parity, long long& key, int kb, int node_base) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
-  const long long r = wave_red<OP_MAX>(key);
+  const long long r = wave_max_key(key, kb, node_base);
   if (lane == 0) H.kred[parity][wave] = r;
   lds_barrier();
   long long best = H.kred[parity][0];
@@ -521,11 +522,13 @@ __device__ __forceinline__ bool spread_argmax(SpreadHdr& H, int W, int w, int gs
     return true;
   }
   ++epoch;
+  const int ng = kb ? 1 : 2;  // granules per shard
+  const uint32_t kc = kb ? key_compress(best, kb, node_base) : 0u;
   if (nw > 1 && W > 64) {  // every wave polls a share of the shards, 4 per lane in flight
     const unsigned long long tag = (unsigned long long)epoch << 32;
-    if (wave == 0 && lane < 2)
+    if (wave == 0 && lane < ng)
       xpub(X, gran, ((size_t)(epoch & 1) * W + w) * gs + lane,
-           tag | (lane ? (uint32_t)((unsigned long long)best >> 32) : (uint32_t)best));
+           tag | (kb ? kc : (lane ? (uint32_t)((unsigned long long)best >> 32) : (uint32_t)best)));
     KSS_GLOBAL const unsigned long long* base = gp(gran) + (size_t)(epoch & 1) * W * gs;
     long long m = 0;
     const int nsw = min(nw, KSS_SPREAD_SWEEP_WAVES);  // the polling waves (the rest add 0)
@@ -541,7 +544,7 @@ __device__ __forceinline__ bool spread_argmax(SpreadHdr& H, int W, int w, int gs
           lo[b] = hi[b] = tag;
           if (s < W) {
             lo[b] = __hip_atomic_load(base + (size_t)s * gs, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            hi[b] = __hip_atomic_load(base + (size_t)s * gs + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (!kb) hi[b] = __hip_atomic_load(base + (size_t)s * gs + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           }
         }
 #pragma unroll
@@ -559,11 +562,24 @@ __device__ __forceinline__ bool spread_argmax(SpreadHdr& H, int W, int w, int gs
 #pragma unroll
       for (int b = 0; b < 4; b++) {
         const int s = c0 + lane + b * stride;
-        const long long k = s < W ? (long long)(((hi[b] & 0xFFFFFFFFull) << 32) | (lo[b] & 0xFFFFFFFFull)) : 0;
+        const long long k = s >= W ? 0
+                            : kb ? (long long)(uint32_t)lo[b]
+                                 : (long long)(((hi[b] & 0xFFFFFFFFull) << 32) | (lo[b] & 0xFFFFFFFFull));
         m = k > m ? k : m;
       }
     }
-    m = wave_red<OP_MAX>(m);
+    if (kb) {  // 32-bit keys: one DPP max per step, expanded once
+      uint32_t k32 = (uint32_t)m;
+      k32 = max(k32, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)k32, 0xB1, 0xF, 0xF, false));
+      k32 = max(k32, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)k32, 0x4E, 0xF, 0xF, false));
+      k32 = max(k32, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)k32, 0x141, 0xF, 0xF, false));
+      k32 = max(k32, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)k32, 0x140, 0xF, 0xF, false));
+      k32 = max(k32, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)k32, 0x142, 0xA, 0xF, false));
+      k32 = max(k32, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)k32, 0x143, 0xC, 0xF, false));
+      m = key_expand((uint32_t)__builtin_amdgcn_readlane((int)k32, 63), kb, node_base);
+    } else {
+      m = wave_red<OP_MAX>(m);
+    }
     if (lane == 0) H.kx[wave] = m;
     lds_barrier();
     if (H.abort) return false;
@@ -574,9 +590,9 @@ __device__ __forceinline__ bool spread_argmax(SpreadHdr& H, int W, int w, int gs
   }
   if (wave == 0) {
     const unsigned long long tag = (unsigned long long)epoch << 32;
-    if (lane < 2)
+    if (lane < ng)
       xpub(X, gran, ((size_t)(epoch & 1) * W + w) * gs + lane,
-           tag | (lane ? (uint32_t)((unsigned long long)best >> 32) : (uint32_t)best));
+           tag | (kb ? kc : (lane ? (uint32_t)((unsigned long long)best >> 32) : (uint32_t)best)));
     KSS_GLOBAL const unsigned long long* base = gp(gran) + (size_t)(epoch & 1) * W * gs;
     long long m = 0;
     for (int c0 = 0; c0 < W; c0 += 64) {
@@ -586,7 +602,7 @@ __device__ __forceinline__ bool spread_argmax(SpreadHdr& H, int W, int w, int gs
       for (unsigned spins = 0;; ++spins) {
         if (s < W) {
           lo = __hip_atomic_load(base + (size_t)s * gs, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          hi = __hip_atomic_load(base + (size_t)s * gs + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (!kb) hi = __hip_atomic_load(base + (size_t)s * gs + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         if (__all(((lo >> 32) == epoch) & ((hi >> 32) == epoch))) break;
         if (spin_expired(spins, t0_)) {
@@ -598,10 +614,12 @@ __device__ __forceinline__ bool spread_argmax(SpreadHdr& H, int W, int w, int gs
         }
         __builtin_amdgcn_s_sleep(1);
       }
-      const long long k = s < W ? (long long)(((hi & 0xFFFFFFFFull) << 32) | (lo & 0xFFFFFFFFull)) : 0;
+      const long long k = s >= W ? 0
+                          : kb ? key_expand((uint32_t)lo, kb, node_base)
+                               : (long long)(((hi & 0xFFFFFFFFull) << 32) | (lo & 0xFFFFFFFFull));
       m = k > m ? k : m;
     }
-    m = wave_red<OP_MAX>(m);
+    m = wave_max_key(m, kb, node_base);
     if (lane == 0) H.kres = m;
   }
   lds_barrier();
@@ -880,6 +898,7 @@ __device__ __forceinline__ void spread_schedule(const GTrace& tr, DevCluster c, 
   SpreadHdr& H = *reinterpret_cast<SpreadHdr*>(smem);
   const SpreadShard L = spread_view(smem, cap, bins_cap, c.n_keys, n_res, gq, c.n_scalar);
   const int nsc = c.n_scalar;
+  const int kb = key_bits(prof, c.N);  // 32-bit selectHost keys when they fit (0: 64-bit, two granules)
   const size_t N = (size_t)c.N;
   const int per = (c.N + W - 1) / W;
   const int lo = min(c.N, w * per), hi = min(c.N, lo + per), own = hi - lo;
@@ -1383,7 +1402,7 @@ __device__ __forceinline__ void spread_schedule(const GTrace& tr, DevCluster c, 
         best = key > best ? key : best;
       }
       GSTAMP(7);
-      if (!spread_argmax(H, W, w, gs, epoch, gran, X, err, kparity, best)) return;
+      if (!spread_argmax(H, W, w, gs, epoch, gran, X, err, kparity, best, kb, c.node_base)) return;
       GSTAMP(8);
       kparity ^= 1;
 #if KSS_SPREAD_TRACE
