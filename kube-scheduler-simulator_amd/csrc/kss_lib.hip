@@ -301,7 +301,10 @@ __global__ __launch_bounds__(256) void k_static(const DevJob* __restrict__ jobs,
     if (k >= kend) break;
     st_ag(&stat[(size_t)(k - k0) * N + n], static_word(c, P, P.pods[k], prof, n, flags, th, ts));  // sc1: read by the next launch
   }
-  handoff_drain();  // lanes past the rows returned: no workgroup barrier here
+  // every store above is agent-scope (sc1, written through): the kernel boundary orders them
+  // for the loop kernel's agent-scope loads, no L2 write-back per wave (C5: 256k workgroups,
+  // an agent release in each cost 9 ms per sweep step)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
 __global__ void k_go_log(const double* x, double* y, int n) {
