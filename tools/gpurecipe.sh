@@ -18,7 +18,6 @@
 #                rocprofv3 --kernel-trace --stats of the matching inner bench run
 #   sq_c2 sq_c5 sq_pf  rocprofv3 --pmc SQ counter passes (one pass per group) of the inner run
 #   counters     rocprofv3 -L (the counters this box's gfx950 exposes)
-#   flake_split flake_single   tools/diag_flake.py (repeat a many-chunk run, count oracle mismatches)
 set -o pipefail
 tag=$1; shift
 R=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -75,9 +74,6 @@ run_step() {
     sq_c5) sq sq_c5 --scenarios 512 --steps 1 --warmup 0 ;;
     sq_pf) sq sq_pf --postfilter --steps 1 --warmup 0 ;;
     counters) (cd /tmp && timeout -s KILL 60 rocprofv3 -L > "$O/${tag}_counters.txt" 2>&1) ;;
-    flake_split|flake_single)  # tools/diag_flake.py: repeated split / single-context many-chunk runs vs the oracle
-      timeout -k 10 240 python -u tools/diag_flake.py ${1#flake_} ${FLAKE_REPS:-8} > "$O/${tag}_$1.txt" 2>&1; local rc=$?
-      tail -2 "$O/${tag}_$1.txt"; return $rc ;;
     *) echo "unknown step $1"; return 1 ;;
   esac
 }
