@@ -279,27 +279,42 @@ __global__ __launch_bounds__(256) void k_counts(const DevJob* __restrict__ jobs,
   handoff_drain();
 }
 
-// Static words of pods [k0, min(k1, n_pods)) x every node of every job.  grid: x = 256-node
-// tiles, y = groups of STATIC_PODS pods, z = job.  One lane per node walks its group.
+// Static words of pods [k0, min(k1, n_pods)) x every node of every job.  grid: x = 512-node
+// tiles, y = groups of STATIC_PODS pods, z = job.  One lane per PAIR of adjacent nodes walks its
+// group: the pair's two words leave as one 8-byte agent-scope store where the row layout keeps
+// it aligned (N and n_lo even), two 4-byte ones otherwise.
 template <bool DEF>
 __global__ __launch_bounds__(256) void k_static(const DevJob* __restrict__ jobs, kss_profile prof_arg, int k0, int k1,
                                                 int n_lo, int n_hi) {
   const DevJob& job = jobs[blockIdx.z];
   const int N = job.c.N;
-  const int n = n_lo + (int)(blockIdx.x * 256 + threadIdx.x);  // rows [n_lo, min(n_hi, N)): a split grid's own rows
+  const int n = n_lo + 2 * (int)(blockIdx.x * 256 + threadIdx.x);  // rows [n_lo, min(n_hi, N)): a split grid's own rows
   const int kend = min(k1, job.n_pods);
   const int kb = k0 + (int)blockIdx.y * STATIC_PODS;
-  if (kb >= kend || n >= N || n >= n_hi) return;
+  const int lim = min(N, n_hi);
+  if (kb >= kend || n >= lim) return;
+  const bool two = n + 1 < lim;
+  const bool wide = two && ((N | n_lo) & 1) == 0;
   const DevCluster c = job.c;
   const DevPods P = job.P;
   uint32_t* stat = job.stat;
   const kss_profile prof = DEF ? default_profile_c() : prof_arg;
-  const uint32_t flags = c.node_flags[n];
-  const uint64_t th = c.taint_hard[n], ts = c.taint_soft[n];
+  const int n1 = two ? n + 1 : n;
+  const uint32_t f0 = c.node_flags[n], f1 = c.node_flags[n1];
+  const uint64_t th0 = c.taint_hard[n], ts0 = c.taint_soft[n], th1 = c.taint_hard[n1], ts1 = c.taint_soft[n1];
   for (int t = 0; t < STATIC_PODS; t++) {
     const int k = kb + t;
     if (k >= kend) break;
-    st_ag(&stat[(size_t)(k - k0) * N + n], static_word(c, P, P.pods[k], prof, n, flags, th, ts));  // sc1: read by the next launch
+    const kss_pod& pod = P.pods[k];
+    const uint32_t w0 = static_word(c, P, pod, prof, n, f0, th0, ts0);
+    const uint32_t w1 = static_word(c, P, pod, prof, n1, f1, th1, ts1);
+    uint32_t* dst = &stat[(size_t)(k - k0) * N + n];
+    if (wide) {
+      st_ag(reinterpret_cast<unsigned long long*>(dst), (unsigned long long)w0 | ((unsigned long long)w1 << 32));
+    } else {
+      st_ag(dst, w0);
+      if (two) st_ag(dst + 1, w1);
+    }
   }
   // every store above is agent-scope (sc1, written through): the kernel boundary orders them
   // for the loop kernel's agent-scope loads, no L2 write-back per wave (C5: 256k workgroups,
@@ -2289,7 +2304,7 @@ static int launch_simple(hipStream_t st, const Geometry& g, int n_jobs, const De
   static_rows(g, X, max_nodes, n_lo, n_hi);
   for (int k0 = 0; k0 < n_pods_max; k0 += chunk) {
     int k1 = std::min(n_pods_max, k0 + chunk);
-    const dim3 sgrid((unsigned)(std::max(n_hi - n_lo, 1) + 255) / 256, (unsigned)((k1 - k0 + STATIC_PODS - 1) / STATIC_PODS),
+    const dim3 sgrid((unsigned)(std::max(n_hi - n_lo, 1) + 511) / 512, (unsigned)((k1 - k0 + STATIC_PODS - 1) / STATIC_PODS),
                      (unsigned)n_jobs);
     if (def)
       hipLaunchKernelGGL(k_static<true>, sgrid, dim3(256), 0, st, jobs, pr, k0, k1, n_lo, n_hi);
@@ -2386,7 +2401,7 @@ static int launch_spread(hipStream_t st, const Geometry& g, const GpodNeeds& q, 
   static_rows(g, X, max_nodes, n_lo, n_hi);
   for (int k0 = 0; k0 < n_pods; k0 += chunk) {
     int k1 = std::min(n_pods, k0 + chunk);
-    const dim3 sgrid((unsigned)(std::max(n_hi - n_lo, 1) + 255) / 256, (unsigned)((k1 - k0 + STATIC_PODS - 1) / STATIC_PODS), 1u);
+    const dim3 sgrid((unsigned)(std::max(n_hi - n_lo, 1) + 511) / 512, (unsigned)((k1 - k0 + STATIC_PODS - 1) / STATIC_PODS), 1u);
     if (def)
       hipLaunchKernelGGL(k_static<true>, sgrid, dim3(256), 0, st, jobs, pr, k0, k1, n_lo, n_hi);
     else
