@@ -13,7 +13,9 @@ its own independent C2 cluster (a what-if scenario; seed + rank) — scenario sh
 data-path collective, "weak" scaling.  Control-plane barrier/max uses gloo.  Beside it, the
 same line carries `c4_split`: BASELINE config C4 (100,000 nodes x 20,000 pods, zone PTS) as ONE
 split grid over all N GPUs (kss/split.py; N = 1: the whole grid on one GPU), strong scaling —
-the north_star "pods/s at 100k nodes at 1/2/4/8 GPUs" figure.
+the north_star "pods/s at 100k nodes at 1/2/4/8 GPUs" figure — and `c5_sweep`: BASELINE config
+C5 (4,096 what-if scenarios x 1,000 nodes x 1,000 pods) spread over the N GPUs, 4,096 / N
+scenarios per GPU in one resident sweep each.
 
 Prints ONE JSON line on rank 0.  Other modes: --config 1..4, --scenarios S (C5), --split P,
 --node-axis, --per-pod, --postfilter.
@@ -494,10 +496,16 @@ def run_split(args):
         ctxs = [c]
         run = lambda: [c.run_staged(n_pods)]  # noqa: E731
 
+    handoff = {"reloads": 0, "shadow": 0, "final": 0}  # k_spread hand-off counters over every run
+
     def step():
         for c in ctxs:
             c.reset()
-        return run()
+        outs = run()
+        for c in ctxs:
+            for k, v in c.last_handoff_status().items():
+                handoff[k] += v
+        return outs
 
     for _ in range(args.warmup):
         step()
@@ -545,6 +553,9 @@ def run_split(args):
             "pods_scheduled_per_step": scheduled,
             "kernel": ctxs[0].last_kernel(),
             "geometry": ctxs[0].last_geometry(),
+            "handoff": dict(handoff, note="k_spread node-state hand-off counters summed over every run of every "
+                                          "part: prologue reloads, loads the shadow answered, last write-backs that "
+                                          "failed the final check (all 0 = every hand-off clean)"),
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": None, "traffic_detail": "not measured",
                          "kernel": ctxs[0].last_kernel(), "bytes_per_eval": B_EVAL[cfg],
@@ -896,20 +907,40 @@ def c4_split_leg(args, world: int, rank: int, local: int, dist) -> dict:
     (`bench.py --split 1`, its own gloo group for the IPC handles), so a failing cross-GPU
     exchange is reported in the line instead of ending the bench.  Rank 0's child also times
     the CPU restatement on a bounded C4 prefix.  Returns rank 0's result (others: {})."""
+    return child_leg(args, world, rank, local, dist, ["--split", "1", "--split-recipe", "4"], "C4 split",
+                     args.c4_timeout, min(args.cpu_seconds, 8.0))
+
+
+def c5_sweep_leg(args, world: int, rank: int, local: int, dist) -> dict:
+    """BASELINE configs[4] beside the main line: 4,096 independent what-if scenarios (KEP-184) x
+    1,000 nodes x 1,000 pods in all, 4,096 / world per rank in one resident sweep per GPU (no
+    data-path collective), so every world size runs the same whole job (strong scaling; at world
+    8 it is the 512-per-GPU shape BASELINE names).  Child processes as in the C4 leg."""
+    res = child_leg(args, world, rank, local, dist, ["--scenarios", str(4096 // world), "--no-traffic"], "C5 sweep",
+                    args.c4_timeout, min(args.cpu_seconds, 6.0))
+    if res and "error" not in res:
+        res["scaling"] = "strong"  # 4,096 scenarios in all at every world size
+    return res
+
+
+def child_leg(args, world: int, rank: int, local: int, dist, mode, label, timeout, cpu_seconds) -> dict:
+    """Run `bench.py <mode>` as one child process per rank (torchrun's environment passed on, a
+    fresh gloo port), after the main timing.  Returns rank 0's JSON line (others: {}), or an
+    error record when any rank's child failed."""
     import torch
     port = torch.tensor([free_port() if rank == 0 else 0], dtype=torch.int64)
     if dist:
         dist.broadcast(port, 0)
     env = dict(os.environ, WORLD_SIZE=str(world), RANK=str(rank), LOCAL_RANK=str(local),
                MASTER_ADDR="127.0.0.1", MASTER_PORT=str(int(port.item())))
-    cmd = [sys.executable, os.path.abspath(__file__), "--split", "1", "--split-recipe", "4",
+    cmd = [sys.executable, os.path.abspath(__file__), *mode,
            "--steps", str(max(args.steps, 3)), "--warmup", str(max(args.warmup, 1)),
-           "--cpu-seconds", str(min(args.cpu_seconds, 8.0))]
+           "--cpu-seconds", str(cpu_seconds)]
     if args.no_cpu:
         cmd.append("--no-cpu")
     t0 = time.perf_counter()
     try:
-        r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=args.c4_timeout)
+        r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=timeout)
         rc, out, err = r.returncode, r.stdout, r.stderr
     except subprocess.TimeoutExpired as e:
         rc, out, err = "timeout", e.stdout or "", e.stderr or ""
@@ -922,13 +953,13 @@ def c4_split_leg(args, world: int, rank: int, local: int, dist) -> dict:
         if rc == 0 and lines:
             res = json.loads(lines[-1])
         else:
-            res = {"error": f"C4 split leg failed (rc {rc})", "stderr_tail": err[-600:]}
+            res = {"error": f"{label} leg failed (rc {rc})", "stderr_tail": err[-600:]}
         res["leg_wall_s"] = wall
     ok = torch.tensor([1 if rc == 0 else 0], dtype=torch.int64)
     if dist:
         dist.all_reduce(ok, op=dist.ReduceOp.MIN)
     if rank == 0 and not ok.item() and "error" not in res:
-        res["error"] = "a peer rank's C4 split child failed"
+        res["error"] = f"a peer rank's {label} child failed"
     return res
 
 
@@ -957,10 +988,11 @@ def main():
     ap.add_argument("--no-latency", action="store_true", help="skip the stamped latency-profile run")
     ap.add_argument("--postfilter", action="store_true", help="DefaultPreemption PostFilter dry runs (kss_postfilter_pod)")
     ap.add_argument("--no-c4", action="store_true", help="skip the C4 split-grid leg of the main line")
+    ap.add_argument("--no-c5", action="store_true", help="skip the C5 scenario-sweep leg of the main line")
     ap.add_argument("--c4-timeout", type=float, default=420.0, help="seconds for the C4 split-grid leg")
     args = ap.parse_args()
     if args.inner:
-        args.no_cpu = args.no_traffic = args.no_latency = args.no_c4 = True
+        args.no_cpu = args.no_traffic = args.no_latency = args.no_c4 = args.no_c5 = True
     world_env = os.environ.get("WORLD_SIZE")
     if args.gpus > 1 and world_env is None:
         sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
@@ -1044,6 +1076,7 @@ def main():
                       "elapsed_s": t1 - t0}), file=sys.stderr, flush=True)
     # the node-axis figure (C4 split grid over every rank's GPU) once the main timing is done
     c4 = None if args.no_c4 or cfg != 2 or args.nodes or args.pods else c4_split_leg(args, world, rank, local, dist)
+    c5 = None if args.no_c5 or cfg != 2 or args.nodes or args.pods else c5_sweep_leg(args, world, rank, local, dist)
     if rank == 0:
         cpu = None
         if not args.no_cpu and world == 1:
@@ -1087,6 +1120,7 @@ def main():
             "cpu_baseline": cpu,
             "gpu_over_cpu": gpu_over_cpu(pods_per_s, cpu),
             "c4_split": c4,
+            "c5_sweep": c5,
         }
         print(json.dumps(out), flush=True)
     ctx.close()

@@ -84,6 +84,14 @@ enum kss_filter_plugin {
   KSS_F_NOT_EVALUATED = 255 /* node excluded by a PreFilterResult / PreFilter failure */
 };
 
+/* fail_detail of a node whose verdict is KSS_F_PASS: 0 = feasible (scored when >= 2 feasible
+ * nodes); KSS_PASS_NOT_KEPT = the node that ended the search: with percentageOfNodesToScore
+ * below 100, findNodesThatPassFilters stops once it finds one feasible node more than
+ * numFeasibleNodesToFind; that node's filters ran and passed (filter-result records it) but it is
+ * not in the feasible list (no Score / NormalizeScore entry).  Nodes after it in visiting order
+ * were never filtered: KSS_F_NOT_EVALUATED. */
+#define KSS_PASS_NOT_KEPT 1
+
 /* fail_detail meaning per failing plugin */
 #define KSS_FIT_TOO_MANY_PODS (1u << 0)
 #define KSS_FIT_CPU (1u << 1)
@@ -371,7 +379,13 @@ typedef struct kss_profile {
   int32_t ba_n;               /* NodeResourcesBalancedAllocationArgs.Resources */
   int32_t ba_res[4];
   int32_t hard_pod_affinity_weight; /* InterPodAffinityArgs.HardPodAffinityWeight */
-  int32_t pct_nodes_to_score;       /* must be 100 */
+  int32_t pct_nodes_to_score;       /* KubeSchedulerConfiguration.percentageOfNodesToScore, 0..100 (0 = the
+                                       adaptive default of v1.26, which the simulator's built-in scheduler
+                                       uses: simulator/scheduler/scheduler.go:162,258-275).  100 evaluates
+                                       every node (north_star / bench configuration); below 100 the
+                                       findNodesThatPassFilters window applies (numFeasibleNodesToFind from
+                                       nextStartNodeIndex, Parallelism = 1 order) and batches run on
+                                       k_schedule.  SURVEY §8a a1. */
   int32_t system_defaulted;         /* PodTopologySpreadArgs.DefaultingType == System */
   int32_t pad;
 } kss_profile;
@@ -544,6 +558,13 @@ int kss_fetch_record(kss_ctx* ctx, int32_t pod_index, kss_pod_result* out);
 int kss_stage_pods(kss_ctx* ctx, const kss_podset* ps);
 int kss_run_staged(kss_ctx* ctx, int32_t n, uint32_t flags, int32_t* chosen_out);
 int kss_reset_node_state(kss_ctx* ctx);
+/* The scheduler's nextStartNodeIndex (schedule_one.go findNodesThatPassFilters): where the next
+ * pod's node search starts, advanced by every evaluated scheduling cycle (kss_eval_pod, batches,
+ * the service) by the nodes it processed, modulo the pod's node list.  0 after kss_load_cluster and
+ * kss_reset_node_state.  Only percentageOfNodesToScore < 100 reads it.  Replaces the field of
+ * pkg/scheduler.Scheduler that simulator/scheduler/scheduler.go:155-168 creates. */
+int kss_next_start_node_index(kss_ctx* ctx, int32_t* out);
+int kss_set_next_start_node_index(kss_ctx* ctx, int32_t value);
 
 /* many independent clusters (what-if scenarios, KEP-184): clusters[s] with podsets[s];
  * one workgroup per scenario, no inter-scenario communication. chosen_out is [sum n_pods].
@@ -647,6 +668,11 @@ int kss_last_handoff_retries(kss_ctx* ctx, int32_t* retries);
  * chunk tag, the word's device address, a 100 MHz timestamp}.  Up to cap entries are copied; *n_entries = the entries listed (<= 64). */
 #define KSS_HANDOFF_DIAG_WORDS 10
 int kss_last_handoff_diag(kss_ctx* ctx, int32_t* recovered, int64_t* entries, int32_t cap, int32_t* n_entries);
+/* The hand-off counters of the last k_spread run (0 for other kernels): out3[0] prologue reloads,
+ * out3[1] loads the shadow answered, out3[2] shards whose LAST write-back failed the final check
+ * (a trailing launch re-sums every shard's node state in HBM against its epilogue's sum; a
+ * failure fails the run with KSS_E_DEVICE and is never repaired).  A clean run is {0, 0, 0}. */
+int kss_last_handoff_status(kss_ctx* ctx, int32_t* out3);
 /* Diagnosis: the device address and size of each of the context's device buffers, in a fixed
  * order (cluster, pristine copy, pods, per-pod upload, record slot, outcomes, chosen, job,
  * granules, error words, hand-off check, stamps, k_simple records, static words, k_spread
@@ -750,6 +776,10 @@ int kss_abi_sizes(int32_t* out, int32_t n);
  * out3[1] = the first pod that rules out k_spread (-1 none), out3[2] = the reason code
  * (kss_plan_reason).  The launch still checks LDS geometry and value bounds. */
 int kss_plan_podset(const kss_cluster* cl, const kss_podset* ps, int32_t* out3);
+/* The same with the profile the batch runs under (NULL: kss_plan_podset): a profile with
+ * percentageOfNodesToScore below 100, or one that scores an extended resource on a cluster that
+ * has them, also rules out both loop kernels (out3[1] = 0, out3[2] the reason). */
+int kss_plan_podset_ex(const kss_cluster* cl, const kss_podset* ps, const kss_profile* prof, int32_t* out3);
 const char* kss_plan_reason(int32_t code);
 /* Test support: y[i] = the device restatement of Go math.Log (kss_spread.cuh go_log_dev,
  * PodTopologySpread's topologyNormalizingWeight in k_spread) at x[i], i < n, evaluated on

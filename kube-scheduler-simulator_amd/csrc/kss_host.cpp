@@ -317,6 +317,7 @@ int kss_host_format(const kss_host_names* nm, const kss_profile* prof, const kss
       bool firstn = true;
       for (int n : order) {
         if (!res->fail_plugin || res->fail_plugin[n] != KSS_F_PASS) continue;
+        if (res->fail_detail && res->fail_detail[n] == KSS_PASS_NOT_KEPT) continue;  // filtered, not in the feasible list
         std::vector<KV> kv;
         for (int s = 0; s < KSS_NSCORE; s++) {
           if (!((prof->score_enabled >> s) & 1u)) continue;

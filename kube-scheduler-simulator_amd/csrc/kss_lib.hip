@@ -112,6 +112,7 @@ struct DevJob {
   const int32_t* res_rows;  // k_spread: the count rows resident in LDS (GpodNeeds::res_rows)
   kss_profile prof;   // k_simple<false>: staged word by word into LDS (a by-value kernel argument would land in scratch)
   GTrace trace;       // k_spread diagnostic trace (KSS_SPREAD_TRACE builds only; null otherwise)
+  int32_t* cursor;    // k_schedule / the service: the cluster's nextStartNodeIndex word (null: 0, not kept)
 };
 
 }  // namespace
@@ -146,6 +147,7 @@ __global__ __launch_bounds__(KSS_MAX_THREADS) void k_schedule(const DevJob* __re
   S.gran = gran ? gran + (size_t)ji * 2 * W * 2 * XW_MAX : nullptr;
   S.err = err;
   S.stamps = nullptr;
+  S.cursor = job.cursor ? *job.cursor : 0;  // written by the previous launch / the host (stream order)
   const bool want_out = job.record || job.keep_norm;
   // shard node cache: the hot node columns stay in LDS for the whole launch
   const int cap = npt * (int)blockDim.x;
@@ -184,6 +186,7 @@ __global__ __launch_bounds__(KSS_MAX_THREADS) void k_schedule(const DevJob* __re
     __syncthreads();
     KSS_STAMP(S, 6);
   }
+  if (job.cursor && w == 0 && threadIdx.x == 0) *job.cursor = S.cursor;  // every shard holds the same value
   if (c.nc64 && job.commit) cache_writeback(c, S.hi);
 }
 
@@ -279,6 +282,15 @@ __global__ __launch_bounds__(256) void k_counts(const DevJob* __restrict__ jobs,
   handoff_drain();
 }
 
+// The final check of a k_spread run's last write-back (handoff_final_check): grid = the
+// part's shards, w_off the first of them.
+__global__ __launch_bounds__(256) void k_handoff_final(const DevJob* __restrict__ jobs, int W, int w_off, int n_res,
+                                                       HandoffCheck hc, int* err) {
+  __shared__ long long scratch[4];
+  const DevJob& job = jobs[0];
+  handoff_final_check(job.c, job.res_rows, n_res, W, w_off + (int)blockIdx.x, hc, err, scratch);
+}
+
 // Static words of pods [k0, min(k1, n_pods)) x every node of every job.  grid: x = 512-node
 // tiles, y = groups of STATIC_PODS pods, z = job.  One lane per PAIR of adjacent nodes walks its
 // group: the pair's two words leave as one 8-byte agent-scope store where the row layout keeps
@@ -294,7 +306,9 @@ __global__ __launch_bounds__(256) void k_static(const DevJob* __restrict__ jobs,
   const int lim = min(N, n_hi);
   if (kb >= kend || n >= lim) return;
   const bool two = n + 1 < lim;
-  const bool wide = two && ((N | n_lo) & 1) == 0;
+  // 8-byte stores only where the pair is 8-byte aligned: the row offset (N, n_lo even) and the
+  // job's stat buffer itself (sweeps align each scenario's to 16 bytes; checked regardless)
+  const bool wide = two && ((N | n_lo) & 1) == 0 && (reinterpret_cast<uintptr_t>(job.stat) & 7) == 0;
   const DevCluster c = job.c;
   const DevPods P = job.P;
   uint32_t* stat = job.stat;
@@ -432,7 +446,7 @@ __global__ __launch_bounds__(256) void k_zero(uint32_t* p, size_t n4) {
 }
 // bytes: a multiple of 4 (every library buffer's element size is)
 static hipError_t dev_zero(void* p, size_t bytes, hipStream_t st) {
-  if (bytes & 3) return hipMemsetAsync(p, 0, bytes, st);  // not used by the library's buffers
+  if (bytes & 3) return hipErrorInvalidValue;  // every library buffer is a whole number of 32-bit words
   const size_t n4 = bytes / 4;
   if (!p || n4 == 0) return hipSuccess;
   const unsigned grid = (unsigned)std::min<size_t>(1024, (n4 / 2 + 255) / 256 + 1);
@@ -454,20 +468,6 @@ struct DevBuf {
     size_t nb = std::max(bytes, (size_t)4096);
     if (hipMalloc(&p, nb) != hipSuccess) return fail(KSS_E_NOMEM, "hipMalloc failed");
     cap = nb;
-#ifdef KSS_EXPERIMENTS
-    // diagnostic (experiment builds, KSS_POISON=all, or =i: only the i-th allocation of the
-    // process): fresh buffers hold a byte pattern, not the zeros a new process tends to get
-    static const char* poison = getenv("KSS_POISON");
-    static std::atomic<int> n_alloc{0};
-    if (poison) {
-      const int i = n_alloc++;
-      const bool all = std::strcmp(poison, "all") == 0;
-      if (all || atoi(poison) == i) {
-        if (hipMemset(p, 0xA5, nb) != hipSuccess || hipDeviceSynchronize() != hipSuccess)
-          return fail(KSS_E_NOMEM, "poison memset failed");
-      }
-    }
-#endif
     return 0;
   }
   void release() {
@@ -531,10 +531,6 @@ struct kss_ctx {
   kss_cluster host{};  // sizes only (pointers not retained)
   DevCluster dc{};
   DevBuf cluster_buf;
-#ifdef KSS_UNCACHED_STATE
-  void* state_unc = nullptr;  // experiment: the mutable columns in uncached device memory
-  size_t state_unc_bytes = 0;
-#endif
   DevBuf pristine_buf;  // load-time copy of the mutable columns (kss_reset_node_state)
   size_t mut_bytes[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   size_t pristine_off[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -556,10 +552,12 @@ struct kss_ctx {
   std::vector<int32_t> key_card_h;
   std::vector<uint32_t> key_flags_h;
   DevBuf gran_buf, err_buf;
+  DevBuf cursor_buf;  // nextStartNodeIndex (one int32), kept on the device across launches
   DevBuf ck_buf;                    // k_spread's checked hand-off between chunks: {sum, tag} per shard
   unsigned long long ck_seq = 0;    // the last tag a chunk wrote
   int last_handoff_retries = 0;     // prologue loads repeated in the last run (HandoffCheck)
   int last_handoff_recovered = 0;   // ... of which the shadow copy answered
+  int last_handoff_final = 0;       // shards whose last write-back failed the final check (the run failed)
   size_t ck_diag_off = 0;           // ck_buf word of the diagnosis list
   bool last_kernel_spread = false;
 #if KSS_SPREAD_TRACE
@@ -822,6 +820,9 @@ int validate(const kss_cluster* cl, const kss_podset* ps, int n) {
         !in(p.ipa_off, p.ipa_len, ps->n_ipa) || !in(p.own_terms_off, p.own_terms_len, ps->n_ints))
       return fail(KSS_E_INVAL, "pod program out of range");
     if (p.names_len >= 0 && !in(p.names_off, p.names_len, ps->n_ints)) return fail(KSS_E_INVAL, "pod names out of range");
+    for (int j = 0; j < p.names_len; j++)  // the PreFilterResult list in canonical order (findNodesThatPassFilters' node list)
+      if (ps->ints[p.names_off + j] < 0 || (j > 0 && ps->ints[p.names_off + j] <= ps->ints[p.names_off + j - 1]))
+        return fail(KSS_E_INVAL, "PreFilterResult node indices must be ascending and distinct");
     if (p.cls >= cl->n_classes) return fail(KSS_E_INVAL, "pod class out of range");
     for (int j = 0; j < p.own_terms_len; j++)
       if (ps->ints[p.own_terms_off + j] < 0 || ps->ints[p.own_terms_off + j] >= cl->n_terms)
@@ -943,6 +944,8 @@ enum {
   GP_IPA,
   GP_SCALAR,
   GP_PORTS_IMAGES,
+  GP_PCT,
+  GP_SCALAR_SCORED,
   GP_NCODES
 };
 const char* const kGpReason[GP_NCODES] = {
@@ -960,6 +963,8 @@ const char* const kGpReason[GP_NCODES] = {
     "more than 16 inter-pod-affinity entries after merging",
     "the profile scores an extended (scalar) resource: k_simple / k_spread score cpu, memory and ephemeral-storage only",
     "host ports (NodePorts), node-cached images (ImageLocality) or volumes: k_schedule only",
+    "percentageOfNodesToScore below 100 (numFeasibleNodesToFind / nextStartNodeIndex window): k_schedule only",
+    "the profile scores an extended (scalar) resource and the cluster has extended resources: k_schedule only",
 };
 
 bool gfail(GpodNeeds& need, int code, int pod) {
@@ -1368,14 +1373,14 @@ int check_cluster(const kss_cluster* cl) {
   return 0;
 }
 
-// Profile limits of the device path.  percentageOfNodesToScore must be 100 (SURVEY 8a
-// a1).  The selectHost key packs TotalScore into the upper 32 bits of a signed 64-bit
+// Profile limits of the device path.  percentageOfNodesToScore in [0, 100] (0: the adaptive
+// default; below 100 the batch runs on k_schedule).  The selectHost key packs TotalScore into the upper 32 bits of a signed 64-bit
 // key, so Σ weight·MaxNodeScore over the enabled score plugins must stay below 2^31; the
 // reference accepts any positive int32 weight whose sum fits int64 (framework.go
 // MaxTotalScore), so larger profiles are refused here rather than mis-ranked.
 int check_profile(const kss_profile* prof) {
-  if (prof->pct_nodes_to_score != 100 && prof->pct_nodes_to_score != 0)
-    return fail(KSS_E_UNSUPPORTED, "percentageOfNodesToScore must be 100 (SURVEY 8a a1)");
+  if (prof->pct_nodes_to_score < 0 || prof->pct_nodes_to_score > 100)  // ValidateKubeSchedulerConfiguration
+    return fail(KSS_E_INVAL, "percentageOfNodesToScore must be between 0 and 100");
   int64_t sum = 0;
   for (int s = 0; s < KSS_NSCORE; s++) {
     if (!((prof->score_enabled >> s) & 1u)) continue;
@@ -1535,32 +1540,6 @@ int kss_load_cluster(kss_ctx* ctx, const kss_cluster* cl) {
   std::vector<double> logtab;
   rc = fill_cluster(ctx->stream, cl, class_cap, term_cap, (char*)ctx->cluster_buf.p, L, ctx->dc, logtab);
   if (rc) return rc;
-#ifdef KSS_UNCACHED_STATE
-  {  // experiment: move the mutable columns into uncached device memory
-    const size_t N0 = (size_t)cl->n_nodes;
-    const size_t ub[8] = {8 * KSS_NRES * N0, 8 * 2 * N0, 4 * N0, 4 * (size_t)class_cap * N0, 4 * (size_t)term_cap * N0,
-                          8 * N0, 4 * (size_t)cl->n_vol_rows * N0, 4 * (size_t)cl->n_vol_keys * N0};
-    size_t tot = 0, off[8];
-    for (int i = 0; i < 8; i++) {
-      off[i] = tot;
-      tot = align_up(tot + std::max<size_t>(ub[i], 8), 256);
-    }
-    if (ctx->state_unc) hipFree(ctx->state_unc);
-    ctx->state_unc = nullptr;
-    if (hipExtMallocWithFlags(&ctx->state_unc, tot, hipDeviceMallocUncached) != hipSuccess)
-      return fail(KSS_E_NOMEM, "uncached state allocation failed");
-    ctx->state_unc_bytes = tot;
-    void** col[8] = {(void**)&ctx->dc.requested, (void**)&ctx->dc.nonzero,   (void**)&ctx->dc.pod_count,
-                     (void**)&ctx->dc.class_count, (void**)&ctx->dc.term_count, (void**)&ctx->dc.port_used,
-                     (void**)&ctx->dc.vol_count, (void**)&ctx->dc.vol_attached};
-    for (int i = 0; i < 8; i++) {
-      char* d = (char*)ctx->state_unc + off[i];
-      if (ub[i]) HIP_TRY(hipMemcpyAsync(d, *col[i], ub[i], hipMemcpyDeviceToDevice, ctx->stream));
-      *col[i] = d;
-    }
-    HIP_TRY(hipStreamSynchronize(ctx->stream));
-  }
-#endif
   // pristine copy of the mutable columns
   const size_t N = (size_t)cl->n_nodes;
   const size_t mb[8] = {8 * KSS_NRES * N,          8 * 2 * N, 4 * N, 4 * (size_t)class_cap * N, 4 * (size_t)term_cap * N,
@@ -1590,6 +1569,9 @@ int kss_load_cluster(kss_ctx* ctx, const kss_cluster* cl) {
       HIP_TRY(hipGetLastError());
     }
   }
+  // nextStartNodeIndex starts at 0 with a new snapshot (a new scheduler)
+  if ((rc = ctx->cursor_buf.ensure(16))) return rc;
+  HIP_TRY(dev_zero(ctx->cursor_buf.p, 16, ctx->stream));
   HIP_TRY(hipStreamSynchronize(ctx->stream));
   ctx->host = *cl;
   {
@@ -1696,6 +1678,8 @@ static hipStream_t axis_stream(kss_ctx* ctx, void* stream) { return stream ? (hi
 
 static int axis_check(kss_ctx* ctx, int32_t pod_index) {
   if (!ctx || !ctx->loaded) return fail(KSS_E_INVAL, "no cluster loaded");
+  if (ctx->prof.pct_nodes_to_score < 100)
+    return fail(KSS_E_UNSUPPORTED, "node-axis path: percentageOfNodesToScore below 100 runs on k_schedule");
   if (pod_index < 0 || pod_index >= ctx->staged_n) return fail(KSS_E_INVAL, "pod index outside the staged pods");
   if (ctx->staged_need.general)
     return fail(KSS_E_UNSUPPORTED, "node-axis path: spread / inter-pod programs need the replicated domain histograms");
@@ -1788,16 +1772,32 @@ int kss_reset_node_state(kss_ctx* ctx) {
     a.n4[i] = ctx->mut_bytes[i] / 4;
     most = std::max(most, a.n4[i]);
   }
-#ifdef KSS_NO_HANDOFF  // experiment builds: the round-3 copy-engine reset
-  for (int i = 0; i < 8; i++)
-    if (ctx->mut_bytes[i]) HIP_TRY(hipMemcpyAsync(dst[i], a.src[i], ctx->mut_bytes[i], hipMemcpyDeviceToDevice, ctx->stream));
-  most = 0;
-#endif
   if (most) {
     hipLaunchKernelGGL(k_reset_state, dim3((unsigned)std::min<size_t>(1024, (most + 255) / 256)), dim3(256), 0,
                        ctx->stream, a);
     HIP_TRY(hipGetLastError());
   }
+  HIP_TRY(dev_zero(ctx->cursor_buf.p, 16, ctx->stream));  // the simulator's reset starts a new scheduler
+  HIP_TRY(hipStreamSynchronize(ctx->stream));
+  return 0;
+}
+
+int kss_next_start_node_index(kss_ctx* ctx, int32_t* out) {
+  KSS_SVC_QUIESCE(ctx);
+  if (!ctx || !ctx->loaded || !out) return fail(KSS_E_INVAL, "bad arguments");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  HIP_TRY(hipSetDevice(ctx->cfg.device));
+  HIP_TRY(hipMemcpyAsync(out, ctx->cursor_buf.p, sizeof(int32_t), hipMemcpyDeviceToHost, ctx->stream));
+  HIP_TRY(hipStreamSynchronize(ctx->stream));
+  return 0;
+}
+
+int kss_set_next_start_node_index(kss_ctx* ctx, int32_t v) {
+  KSS_SVC_QUIESCE(ctx);
+  if (!ctx || !ctx->loaded || v < 0) return fail(KSS_E_INVAL, "bad arguments");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  HIP_TRY(hipSetDevice(ctx->cfg.device));
+  HIP_TRY(hipMemcpyAsync(ctx->cursor_buf.p, &v, sizeof(int32_t), hipMemcpyHostToDevice, ctx->stream));
   HIP_TRY(hipStreamSynchronize(ctx->stream));
   return 0;
 }
@@ -2419,7 +2419,7 @@ static int launch_spread(hipStream_t st, const Geometry& g, const GpodNeeds& q, 
     // the checked node-state hand-off between this call's chunks (HandoffCheck): tags increase
     // over the context's life, the first chunk of a call checks nothing
     HandoffCheck hc{};
-    if (ck && ck_seq && n_pods > chunk) {
+    if (ck && ck_seq) {
       const HandoffLayout hl(g.W, n_res, max_nodes, nsc);
       hc.sum = ck;
       hc.expect = k0 > 0 ? *ck_seq : 0ull;
@@ -2440,6 +2440,14 @@ static int launch_spread(hipStream_t st, const Geometry& g, const GpodNeeds& q, 
       HIP_TRY(hipLaunchKernel(fn, grid, block, args, shmem, st));
     }
     if (ev) HIP_TRY(hipEventRecord(ev[2 * ci + 1], st));
+  }
+  if (ck && ck_seq && n_pods > 0) {  // the last chunk's write-back, checked (nothing repairs it)
+    HandoffCheck hc{};
+    hc.sum = ck;
+    hc.expect = *ck_seq;
+    hc.retries = err + 1;
+    hipLaunchKernelGGL(k_handoff_final, grid, dim3(256), 0, st, jobs, W, sp_grid ? X.w_off : 0, n_res, hc, err);
+    HIP_TRY(hipGetLastError());
   }
   return 0;
 }
@@ -2515,14 +2523,18 @@ static int run_single_impl(kss_ctx* ctx, const PlanNeeds& need, const DevPods& d
   // a k_simple-eligible batch keeps W within k_simple's exchange sweep (64 * SX_CHUNKS
   // shards): at 100k nodes, 98-128 k_simple shards beat 256 k_schedule shards (69.8k
   // against 44.2k pods/s)
-  const bool simple_ok = staged && ctx->spod_ok && commit && !record && !keep_norm && !need.general &&
+  // percentageOfNodesToScore below 100: findNodesThatPassFilters' window (numFeasibleNodesToFind,
+  // nextStartNodeIndex) runs on k_schedule only; its per-shard count exchange needs W + 1 values
+  const bool window = ctx->prof.pct_nodes_to_score < 100;
+  if (window) W = std::min(W, XW_MAX - NSCAL);
+  const bool simple_ok = !window && staged && ctx->spod_ok && commit && !record && !keep_norm && !need.general &&
                          scalar_fast_ok(ctx->prof, ctx->dc.n_scalar) && ctx->small_values && f64_exact(ctx->f64_cluster, ctx->f64_pods, n) &&
                          !ctx->no_simple && !(flags & KSS_SCHED_GENERAL_KERNEL);
   if (simple_ok && ctx->force_w <= 0 && !split) W = std::min(W, 64 * SX_CHUNKS);
   // a batch with programs on k_spread: 32-bit counts and scores (spread_bounds_ok)
   const double count_total = ctx->count_bound + (commit ? (double)n * (1.0 + ctx->staged_max_own) : 0.0);
   const double cell_total = ctx->cell_bound + (commit ? (double)n * ctx->gneed.max_mult : 0.0);
-  const bool spread_ok = staged && ctx->gpod_ok && commit && !record && !keep_norm && need.general &&
+  const bool spread_ok = !window && staged && ctx->gpod_ok && commit && !record && !keep_norm && need.general &&
                          scalar_fast_ok(ctx->prof, ctx->dc.n_scalar) && ctx->small_values && f64_exact(ctx->f64_cluster, ctx->f64_pods, n) &&
                          !ctx->no_simple && !ctx->no_spread && !(flags & KSS_SCHED_GENERAL_KERNEL) &&
                          spread_bounds_ok(ctx->gneed, count_total, cell_total, (int)N);
@@ -2613,6 +2625,7 @@ static int run_single_impl(kss_ctx* ctx, const PlanNeeds& need, const DevPods& d
   job.gpods = spread ? (const GPod*)ctx->gpod_buf.p : nullptr;
   job.res_rows = spread ? (const int32_t*)ctx->res_buf.p : nullptr;
   job.trace = GTrace{nullptr, nullptr};
+  job.cursor = (int32_t*)ctx->cursor_buf.p;
 #if KSS_SPREAD_TRACE
   if (spread) {  // every pod and shard, and the list of nonzero counts loaded / written back
     ctx->trace_words = (size_t)n * (size_t)g.W * G_TW;
@@ -2707,8 +2720,8 @@ static int run_single_impl(kss_ctx* ctx, const PlanNeeds& need, const DevPods& d
                        (int)N, chunk, gran, gb, errp, stamps, ctx->loop_ev.data(), split ? &srun : nullptr,
                        (unsigned long long*)ctx->ck_buf.p, &ctx->ck_seq, ctx->dc.n_scalar);
   }
-  else
-    rc = launch_schedule(ctx->stream, g, 1, std::max(need.bins_cap, 0), need.general, ctx->dc.n_keys,
+  else  // window: the per-shard feasible counts sit behind the plan's bins
+    rc = launch_schedule(ctx->stream, g, 1, std::max(need.bins_cap, 0) + (window ? g.W : 0), need.general, ctx->dc.n_keys,
                          jd, ctx->prof, gran, errp, stamps, epoch0);
   if (rc) return rc;
   ctx->last_kernel = simple ? 1 : (spread ? 2 : 0);
@@ -2756,7 +2769,7 @@ static int run_single_impl(kss_ctx* ctx, const PlanNeeds& need, const DevPods& d
   const size_t o_meta = 16, o_chosen = align_up(o_meta + mb, 16), o_rb = align_up(o_chosen + cb, 16);
   if ((rc = ensure_pinned(ctx->rb, ctx->rb_cap, o_rb + (rbk ? rbk->bytes : 0)))) return rc;
   char* hb = (char*)ctx->rb;
-  HIP_TRY(hipMemcpyAsync(hb, errp, 3 * sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+  HIP_TRY(hipMemcpyAsync(hb, errp, 4 * sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
   HIP_TRY(hipMemcpyAsync(hb + o_meta, ctx->meta_buf.p, mb, hipMemcpyDeviceToHost, ctx->stream));
   if (cb) HIP_TRY(hipMemcpyAsync(hb + o_chosen, ctx->chosen_buf.p, cb, hipMemcpyDeviceToHost, ctx->stream));
   if (rbk && rbk->bytes) HIP_TRY(hipMemcpyAsync(hb + o_rb, rbk->src, rbk->bytes, hipMemcpyDeviceToHost, ctx->stream));
@@ -2779,13 +2792,16 @@ static int run_single_impl(kss_ctx* ctx, const PlanNeeds& need, const DevPods& d
   std::memcpy(&errw, hb, sizeof(int));
   std::memcpy(&ctx->last_handoff_retries, hb + sizeof(int), sizeof(int));
   std::memcpy(&ctx->last_handoff_recovered, hb + 2 * sizeof(int), sizeof(int));
+  std::memcpy(&ctx->last_handoff_final, hb + 3 * sizeof(int), sizeof(int));
   ctx->last_kernel_spread = spread;
   if (errw && commit) {  // bounds as if every pod committed (upper bounds stay safe); log unknown
     ctx->count_bound = count_total;
     ctx->cell_bound = std::max(ctx->cell_bound, cell_total);
     ctx->state_unknown = true;
   }
-  if (errw == 2) return fail(KSS_E_DEVICE, "node state handed between chunk launches failed its check");
+  if (errw == 2)
+    return fail(KSS_E_DEVICE, ctx->last_handoff_final ? "the last chunk's node-state write-back failed its final check"
+                                                       : "node state handed between chunk launches failed its check");
   if (errw) return fail(KSS_E_DEVICE, "shard exchange timed out (workgroups not co-resident?)");
   if (commit) {
     ctx->count_bound = count_total;
@@ -3286,12 +3302,14 @@ static int svc_start_locked(kss_ctx* ctx) {
   if (ctx->force_w > 0) W = std::min(ctx->force_w, ctx->n_cu);
   W = std::max(W, (int)((N + KSS_MAX_NPT * KSS_MAX_THREADS - 1) / (KSS_MAX_NPT * KSS_MAX_THREADS)));
   W = std::min(W, std::max(1, (int)N));
+  const bool window = ctx->prof.pct_nodes_to_score < 100;  // k_schedule's window exchange: W + 1 values
+  if (window) W = std::min(W, XW_MAX - NSCAL);
   const PlanNeeds& need = ctx->staged_need;
   if (W > 1 && need.xw > XW_MAX) return fail(KSS_E_UNSUPPORTED, "topology histograms too large for the service grid");
   if (W > SVC_MAX_SHARDS || W > ctx->n_cu) return fail(KSS_E_UNSUPPORTED, "cluster too large for the service grid");
   Geometry g;
   if (!pick_geometry((int)N, W, ctx->pref_threads, g)) return fail(KSS_E_UNSUPPORTED, "no geometry for this cluster");
-  const int bins_cap = std::max(need.bins_cap, 0);
+  const int bins_cap = std::max(need.bins_cap, 0) + (window ? g.W : 0);
   const int cap = g.threads * g.npt;
   const size_t base = lds_bytes(bins_cap, cap);
   if (base > KSS_LDS_BUDGET) return fail(KSS_E_UNSUPPORTED, "per-workgroup LDS budget exceeded");
@@ -3352,6 +3370,7 @@ static int svc_start_locked(kss_ctx* ctx) {
   job.slots = (uint8_t*)ctx->slot_buf.p;
   job.slot_bytes = SL.bytes;
   job.prof = ctx->prof;
+  job.cursor = (int32_t*)ctx->cursor_buf.p;
   HIP_TRY(hipMemcpyAsync(v.job.p, &job, sizeof(DevJob), hipMemcpyHostToDevice, v.stream));
   v.W = g.W;
   v.threads = g.threads;
@@ -3359,7 +3378,7 @@ static int svc_start_locked(kss_ctx* ctx) {
   v.bins_cap = bins_cap;
   v.cache_keys = cache_keys;
   v.shmem = base + (cache_keys >= 0 ? node_cache_bytes(cap, cache_keys) : 0);
-  v.gen = bins_cap > 0 || need.general;
+  v.gen = std::max(need.bins_cap, 0) > 0 || need.general;
   ctx->last_geom[0] = g.W;
   ctx->last_geom[1] = g.threads;
   ctx->last_geom[2] = g.npt;
@@ -3448,13 +3467,16 @@ int kss_service_stop(kss_ctx* ctx) {
 // One EVAL command on the service grid and the wait for every shard's done flag (restarting
 // a grid that left idle before taking the command).  ovf: some shard's compact record value
 // did not fit its narrow type.
-static int svc_eval_wait(kss_ctx* ctx, int32_t pod_index, uint32_t fields, bool compact, bool& ovf) {
+static int svc_eval_wait(kss_ctx* ctx, int32_t pod_index, uint32_t fields, bool compact, bool& ovf,
+                         bool repeat = false) {
   auto& v = ctx->svc;
   if (!v.running) {
     if (int rc = svc_start_locked(ctx)) return rc;
   }
   unsigned long long seq = 0;
-  if (int rc = svc_post(ctx, SVC_EVAL, pod_index, compact ? 1 : 0, (int)(fields & KSS_FIELD_ALL), &seq)) return rc;
+  // node bit 0: the compact record; bit 1: the same cycle again (nextStartNodeIndex as before the last one)
+  if (int rc = svc_post(ctx, SVC_EVAL, pod_index, (compact ? 1 : 0) | (repeat ? 2 : 0), (int)(fields & KSS_FIELD_ALL), &seq))
+    return rc;
   const auto t0 = std::chrono::steady_clock::now();
   for (unsigned spins = 0;; ++spins) {
     bool all = true;
@@ -3521,7 +3543,7 @@ int kss_service_eval_compact(kss_ctx* ctx, int32_t pod_index, uint32_t fields, k
   if (int rc = svc_eval_wait(ctx, pod_index, fields, true, ovf)) return rc;
   *out = kss_pod_cview{};
   if (ovf) {  // a score outside int32 / a normalised score above 255: the same pod, full record
-    if (int rc = svc_eval_wait(ctx, pod_index, fields, false, ovf)) return rc;
+    if (int rc = svc_eval_wait(ctx, pod_index, fields, false, ovf, /*repeat=*/true)) return rc;
     out->is_wide = 1;
     svc_full_view(ctx, fields, &out->wide);
   } else {
@@ -3604,6 +3626,13 @@ int kss_last_handoff_retries(kss_ctx* ctx, int32_t* retries) {
   return 0;
 }
 
+int kss_last_handoff_status(kss_ctx* ctx, int32_t* out3) {
+  if (!ctx || !out3) return fail(KSS_E_INVAL, "bad arguments");
+  out3[0] = ctx->last_kernel_spread ? ctx->last_handoff_retries : 0;
+  out3[1] = ctx->last_kernel_spread ? ctx->last_handoff_recovered : 0;
+  out3[2] = ctx->last_kernel_spread ? ctx->last_handoff_final : 0;
+  return 0;
+}
 int kss_buffer_map(kss_ctx* ctx, uint64_t* base, uint64_t* bytes, int32_t cap, int32_t* n) {
   if (!ctx || !n || cap < 0 || (cap && (!base || !bytes))) return fail(KSS_E_INVAL, "bad arguments");
   const DevBuf* bufs[] = {&ctx->cluster_buf, &ctx->pristine_buf, &ctx->pod_buf, &ctx->tmp_pod_buf, &ctx->slot_buf,
@@ -3779,6 +3808,7 @@ struct kss_sweep {
   size_t up_bytes = 0;                   // [0, up_bytes): uploaded once (inputs, pristine state, jobs)
   size_t pristine_off = 0, live_off = 0, mut_bytes = 0;
   size_t chosen_off = 0, meta_off = 0, err_off = 0, gran_off = 0, gran_bytes = 0, stat_off = 0, jobs_off = 0;
+  size_t cursor_off = 0;  // one nextStartNodeIndex per scenario (percentageOfNodesToScore < 100)
   std::vector<int32_t> n_pods;
   int total_pods = 0, max_pods = 0, max_nodes = 0, max_keys = 0;
   bool simple = false;
@@ -3837,7 +3867,8 @@ kss_sweep* kss_sweep_create(int32_t device, const kss_profile* prof, int32_t n_s
   // k_static + k_simple for the whole sweep when every scenario qualifies (no spread /
   // inter-pod programs, no scalar resources, values inside the exact f64 envelope)
   std::vector<std::vector<SPod>> spods(n_scen);
-  bool simple = getenv("KSS_NO_SIMPLE") == nullptr && !sw->need.general && simple_fits(sw->g, 0);
+  bool simple = getenv("KSS_NO_SIMPLE") == nullptr && !sw->need.general && simple_fits(sw->g, 0) &&
+                prof->pct_nodes_to_score >= 100;  // the window runs on k_schedule
   for (int i = 0; i < prof->fit_n && simple; i++) simple = prof->fit_weight[i] >= 0 && prof->fit_weight[i] < (1ll << 20);
   for (int s = 0; s < n_scen && simple; s++) {
     const kss_cluster& cl = clusters[s];
@@ -3877,11 +3908,13 @@ kss_sweep* kss_sweep_create(int32_t device, const kss_profile* prof, int32_t n_s
   sw->meta_off = dry.last;
   dry.put<int32_t>(nullptr, 4);
   sw->err_off = dry.last;
+  dry.put<int32_t>(nullptr, (size_t)n_scen);
+  sw->cursor_off = dry.last;
   size_t sum_nodes = 0;
   for (int s = 0; s < n_scen; s++) sum_nodes += (size_t)clusters[s].n_nodes;
   sw->chunk = simple ? static_chunk(sum_nodes, sw->max_pods) : 0;
   if (simple) {
-    dry.put<uint32_t>(nullptr, (size_t)sw->chunk * sum_nodes);
+    dry.put<uint32_t>(nullptr, (size_t)sw->chunk * sum_nodes + 4 * (size_t)n_scen);  // + 16-byte alignment per scenario
     sw->stat_off = dry.last;
   }
   const size_t total = dry.o;
@@ -3928,10 +3961,11 @@ kss_sweep* kss_sweep_create(int32_t device, const kss_profile* prof, int32_t n_s
   for (int s = 0; s < n_scen; s++) {
     jobs[s].chosen = reinterpret_cast<int32_t*>(sw->arena + sw->chosen_off) + o_chosen;
     jobs[s].meta = reinterpret_cast<PodMeta*>(sw->arena + sw->meta_off) + o_chosen;
+    jobs[s].cursor = reinterpret_cast<int32_t*>(sw->arena + sw->cursor_off) + s;
     o_chosen += (size_t)podsets[s].n_pods;
     if (simple) {
       jobs[s].stat = reinterpret_cast<uint32_t*>(sw->arena + sw->stat_off) + o_stat;
-      o_stat += (size_t)sw->chunk * (size_t)clusters[s].n_nodes;
+      o_stat += ((size_t)sw->chunk * (size_t)clusters[s].n_nodes + 3) / 4 * 4;  // 16-byte aligned per scenario
     }
   }
   memcpy(img.get() + sw->jobs_off, jobs.data(), sizeof(DevJob) * n_scen);
@@ -3948,17 +3982,29 @@ int kss_sweep_run(kss_sweep* sw, int32_t* chosen_out, double* device_ms) {
   HIP_TRY(hipSetDevice(sw->device));
   hipStream_t st = sw->st;
   HIP_TRY(hipEventRecord(sw->e0, st));
-  // every run starts from the snapshot: one device copy of all scenarios' mutable columns
-  HIP_TRY(hipMemcpyAsync(sw->arena + sw->live_off, sw->arena + sw->pristine_off, sw->mut_bytes, hipMemcpyDeviceToDevice, st));
+  // every run starts from the snapshot: all scenarios' mutable columns copied back by the reset
+  // kernel (agent-scope loads and stores, then a release: the same hand-off as every other
+  // writer of node state, not the runtime's copy engine)
+  {
+    ResetArgs a{};
+    a.dst[0] = reinterpret_cast<uint32_t*>(sw->arena + sw->live_off);
+    a.src[0] = reinterpret_cast<const uint32_t*>(sw->arena + sw->pristine_off);
+    a.n4[0] = sw->mut_bytes / 4;
+    if (a.n4[0]) {
+      hipLaunchKernelGGL(k_reset_state, dim3((unsigned)std::min<size_t>(2048, (a.n4[0] + 255) / 256)), dim3(256), 0, st, a);
+      HIP_TRY(hipGetLastError());
+    }
+  }
   int* err = reinterpret_cast<int*>(sw->arena + sw->err_off);
   HIP_TRY(dev_zero(err, 16, st));
+  HIP_TRY(dev_zero(sw->arena + sw->cursor_off, 4 * (size_t)sw->n_scen, st));  // every scenario's scheduler starts at node 0
   const DevJob* jobs = reinterpret_cast<const DevJob*>(sw->arena + sw->jobs_off);
   int rc;
   if (sw->simple)
     rc = launch_simple(st, sw->g, sw->n_scen, jobs, sw->prof, sw->max_pods, sw->max_nodes, sw->chunk, nullptr, 0, err);
   else
-    rc = launch_schedule(st, sw->g, sw->n_scen, sw->need.bins_cap, sw->need.general, sw->max_keys, jobs, sw->prof,
-                         nullptr, err);
+    rc = launch_schedule(st, sw->g, sw->n_scen, sw->need.bins_cap + (sw->prof.pct_nodes_to_score < 100 ? 1 : 0),
+                         sw->need.general, sw->max_keys, jobs, sw->prof, nullptr, err);
   if (rc) return rc;
   HIP_TRY(hipEventRecord(sw->e1, st));
   if (sw->total_pods)
@@ -4313,6 +4359,23 @@ int kss_plan_podset(const kss_cluster* cl, const kss_podset* ps, int32_t* out3) 
   }
   out3[1] = need.fail_pod;
   out3[2] = need.fail_code;
+  return 0;
+}
+
+int kss_plan_podset_ex(const kss_cluster* cl, const kss_podset* ps, const kss_profile* prof, int32_t* out3) {
+  if (!prof) return kss_plan_podset(cl, ps, out3);
+  if (int rc = check_profile(prof)) return rc;
+  if (int rc = kss_plan_podset(cl, ps, out3)) return rc;
+  if (out3[0] == 0) return 0;  // the programs already rule out both loop kernels
+  if (prof->pct_nodes_to_score < 100) {
+    out3[0] = 0;
+    out3[1] = ps->n_pods > 0 ? 0 : -1;
+    out3[2] = GP_PCT;
+  } else if (!scalar_fast_ok(*prof, cl->n_scalar)) {
+    out3[0] = 0;
+    out3[1] = ps->n_pods > 0 ? 0 : -1;
+    out3[2] = GP_SCALAR_SCORED;
+  }
   return 0;
 }
 

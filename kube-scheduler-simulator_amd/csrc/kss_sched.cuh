@@ -54,6 +54,17 @@ __device__ __forceinline__ bool spin_expired(unsigned spins, long long& t0) {
   if ((spins & 63u) != 63u) return false;
   return (long long)__builtin_amdgcn_s_memrealtime() - t0 > KSS_WAIT_TICKS;
 }
+// The launch error word only grows (atomic max): a state-check failure (2) is never
+// overwritten by the exchange timeouts (1) it causes in the shards still waiting for it.
+__device__ __forceinline__ void err_raise(int* err, int code) {
+  __hip_atomic_fetch_max(err, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// An exchange spin ends on the wall-time bound, or as soon as the launch has failed elsewhere
+// (err != 0, read every 64 polls): the peers of a shard that left do not wait out the bound.
+__device__ __forceinline__ bool spread_spin_over(unsigned spins, long long& t0, int* err) {
+  if (spin_expired(spins, t0)) return true;
+  return (spins & 63u) == 63u && __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+}
 constexpr int KSS_MAX_THREADS = 512;  // workgroup size cap (2 waves per SIMD: 256 VGPRs per lane)
 constexpr int KSS_NSTAMP_PODS = 256;  // pods with diagnostic phase stamps per launch
 constexpr int KSS_MAX_NPT = 6;
@@ -126,7 +137,22 @@ struct Shard {
   unsigned long long* gran;  // this cluster's granules: [2][W][2*XW_MAX]
   int* err;         // launch error word (timeouts)
   unsigned long long* stamps;  // KSS_STAMPS diagnostics: phase timestamps of this pod, or null
+  int cursor;       // nextStartNodeIndex of the cluster (identical in every shard; advanced per pod)
 };
+
+// numFeasibleNodesToFind (v1.26 schedule_one.go): every node when the list is short
+// (< minFeasibleNodesToFind = 100) or pct >= 100; pct <= 0 is the adaptive default
+// 50 - N/125 percent, at least minFeasibleNodesPercentageToFind = 5; at least 100 nodes.
+__host__ __device__ __forceinline__ int num_feasible_to_find(int m, int pct) {
+  if (m < 100 || pct >= 100) return m;
+  int a = pct;
+  if (a <= 0) {
+    a = 50 - m / 125;
+    if (a < 5) a = 5;
+  }
+  const int k = (int)((long long)m * a / 100);
+  return k < 100 ? 100 : k;
+}
 
 // Diagnostic phase stamps (s_memrealtime, 100 MHz), lane 0 of shard 0 only.
 #define KSS_STAMP(S, i)                                              \
@@ -206,7 +232,7 @@ __device__ __noinline__ void shard_exchange(long long* smem, unsigned long long*
       if (spin_expired(spins, t0_)) {
         if (lane == 0) {
           shdr(smem).abort = 1;
-          __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          err_raise(err, 1);
         }
         return;
       }
@@ -592,6 +618,43 @@ __device__ __forceinline__ SlotArrays slot_arrays(long long* smem, int bins_cap,
   return a;
 }
 
+// RunFilterPlugins for node n: the verdict (first failing plugin, 0 = passed) and its detail;
+// row holds the node's columns afterwards (the score pass reads them).
+template <bool GEN>
+__device__ __forceinline__ int filter_chain(const DevCluster& c, const DevPods& P, const kss_pod& p, const Plan& pl,
+                                            const long long* bins, const long long (&hard_min)[MAXH], long long flags,
+                                            uint32_t en, bool has_ipa, int n, NodeRow& row, uint16_t* detail) {
+  row = load_row(c, n);
+  int f = filter_local(c, P, p, en, n, row, detail);
+  if (!f) f = filter_volumes(c, P, p, en, n, detail);
+  if (GEN && !f && ((en >> KSS_F_POD_TOPOLOGY_SPREAD) & 1u) && p.n_hard > 0) {
+    const int r = filter_pts(c, P, p, pl, bins, hard_min, n);
+    if (r) {
+      f = KSS_F_POD_TOPOLOGY_SPREAD;
+      *detail = (uint16_t)(r - 1);
+    }
+  }
+  if (!f && ((en >> KSS_F_INTER_POD_AFFINITY) & 1u) && has_ipa) {
+    const int r = filter_ipa(c, P, p, pl, bins, flags, n);
+    if (r) {
+      f = KSS_F_INTER_POD_AFFINITY;
+      *detail = (uint16_t)(r - 1);
+    }
+  }
+  return f;
+}
+
+// Position of global node g in the pod's ascending PreFilterResult list (binary search).
+__device__ __forceinline__ int names_rank(const DevPods& P, const kss_pod& p, int64_t g) {
+  int lo = 0, hi = p.names_len;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if ((int64_t)P.ints[p.names_off + mid] < g) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
+
 // ---------------------------------------------------------------------------
 // one scheduling cycle for pod pi, executed by every shard of the cluster.
 // Returns false if the launch aborted (exchange timeout).
@@ -706,6 +769,68 @@ __device__ __forceinline__ bool schedule_pod(const DevCluster& c, const DevPods&
   const bool req_all = (p.flags & KSS_POD_PTS_REQUIRE_ALL) != 0;
   const bool has_soft = GEN && p.n_soft > 0;
   const bool has_ipa = GEN && p.ipa_len > 0;
+
+  // ---- percentageOfNodesToScore: findNodesThatPassFilters' window ------------
+  // The node list (every node, or the PreFilterResult set in canonical order) is visited from
+  // nextStartNodeIndex, one node at a time (Parallelism = 1, the deterministic form), until
+  // one feasible node more than K = numFeasibleNodesToFind has been found: that node was
+  // filtered (its record says passed) but is neither counted nor scored, and the nodes after
+  // it were never evaluated.  With Fb(n) = the feasible nodes strictly before n in visiting
+  // order: n is visited iff Fb <= K, and scored iff feasible and Fb < K.  A pre-pass counts the
+  // feasible nodes per shard (one exchange: the per-shard counts and the feasible nodes before
+  // the start node); the stopping node's shard reports the nodes processed with the selectHost
+  // exchange, and nextStartNodeIndex advances by them.
+  const int m_list = restrict_names ? p.names_len : c.N;
+  const int k_find = num_feasible_to_find(m_list, prof.pct_nodes_to_score);
+  const bool win = k_find < m_list;
+  long long w_total = 0, w_gstar = 0, w_pre = 0;
+  int nstar = 0, spos = 0;
+  if (m_list > 0 && !win) S.cursor = (int)(((long long)S.cursor + m_list) % m_list);  // every node processed
+  if (win) {
+    const int lane = tid & 63, wave = tid >> 6, nw = nt >> 6;
+    spos = (int)((long long)S.cursor % m_list);
+    nstar = restrict_names ? (int)((int64_t)P.ints[p.names_off + spos] - c.node_base) : spos;
+    long long lt = 0;  // this lane's feasible nodes before the start node
+    for (int k = 0; k < npt; k++) {
+      const int n = S.lo + k * nt + tid;
+      bool fe = false;
+      if (n < S.hi && (!restrict_names || in_names(P, p, (int64_t)c.node_base + n))) {
+        NodeRow row;
+        uint16_t d = 0;
+        fe = filter_chain<GEN>(c, P, p, pl, bins, hard_min, flags, en, has_ipa, n, row, &d) == KSS_F_PASS;
+      }
+      const unsigned long long b = __ballot(fe);
+      sa.fit[k * nt + tid] = (int)__popcll(b & ((1ull << lane) - 1ull));  // feasible lanes before this one, row k
+      if (lane == 0) H.red[wave][k] = (long long)__popcll(b);
+      lt += (fe && n < nstar) ? 1 : 0;
+    }
+    __syncthreads();
+    long long run = 0;  // shard-local exclusive prefix in canonical order: rows before k, waves before this one
+    for (int k = 0; k < npt; k++) {
+      long long row_tot = 0, before = 0;
+      for (int x = 0; x < nw; x++) {
+        row_tot += H.red[x][k];
+        before += x < wave ? H.red[x][k] : 0;
+      }
+      sa.fit[k * nt + tid] += (int)(run + before);
+      run += row_tot;
+    }
+    __syncthreads();  // H.red is the reduction scratch of the exchange below
+    const int wb = bins_cap - S.W;  // the per-shard counts, behind the plan's bins (the host reserves W)
+    for (int j = tid; j < S.W; j += nt) bins[wb + j] = j == S.w ? run : 0;
+    long long v[1] = {lt};
+    const int op[1] = {OP_SUM};
+    if (!cluster_reduce(smem, S, v, op, wb, S.W)) return false;
+    w_gstar = v[0];
+    for (int j = 0; j < S.W; j++) {
+      const long long t = bins[wb + j];
+      w_total += t;
+      w_pre += j < S.w ? t : 0;
+    }
+    if (w_total <= k_find) S.cursor = (int)(((long long)S.cursor + m_list) % m_list);  // no stop: all processed
+  }
+  long long w_proc = 0;  // nodes processed before the stopping node (its lane only)
+
   long long nf = 0, max_tt = 0, max_na = 0;
   long long nign = 0, ipa_min = INT64_MAX, ipa_max = INT64_MIN, smissing = 0;
   long long sdirect[MAXS];
@@ -724,32 +849,32 @@ __device__ __forceinline__ bool schedule_pod(const DevCluster& c, const DevPods&
     if (restrict_names && !in_names(P, p, (int64_t)c.node_base + n)) {
       f = KSS_F_NOT_EVALUATED;
     } else {
-      row = load_row(c, n);
-      f = filter_local(c, P, p, en, n, row, &detail);
-      if (!f) f = filter_volumes(c, P, p, en, n, &detail);
-      if (GEN && !f && ((en >> KSS_F_POD_TOPOLOGY_SPREAD) & 1u) && p.n_hard > 0) {
-        const int r = filter_pts(c, P, p, pl, bins, hard_min, n);
-        if (r) {
-          f = KSS_F_POD_TOPOLOGY_SPREAD;
-          detail = (uint16_t)(r - 1);
-        }
-      }
-      if (!f && ((en >> KSS_F_INTER_POD_AFFINITY) & 1u) && has_ipa) {
-        const int r = filter_ipa(c, P, p, pl, bins, flags, n);
-        if (r) {
-          f = KSS_F_INTER_POD_AFFINITY;
-          detail = (uint16_t)(r - 1);
-        }
+      f = filter_chain<GEN>(c, P, p, pl, bins, hard_min, flags, en, has_ipa, n, row, &detail);
+    }
+    bool kept = f == KSS_F_PASS;
+    if (win && f != KSS_F_NOT_EVALUATED) {
+      const long long g = w_pre + sa.fit[si];  // feasible nodes before n in canonical order
+      const long long fb = n >= nstar ? g - w_gstar : w_total - w_gstar + g;
+      if (fb > k_find) {  // the search stopped before reaching n
+        f = KSS_F_NOT_EVALUATED;
+        detail = 0;
+        kept = false;
+      } else if (kept && fb == k_find) {  // the stopping node: filtered, dropped, not scored
+        kept = false;
+        detail = KSS_PASS_NOT_KEPT;
+        w_proc = restrict_names ? ((long long)names_rank(P, p, (int64_t)c.node_base + n) - spos + m_list) % m_list
+                                : ((long long)n - nstar + m_list) % m_list;
       }
     }
     if (out) {
       KSS_DCHECK(n >= 0 && n < c.N, "out n", n, c.N);
       out->fail[n] = (uint8_t)f;
       out->detail[n] = detail;
-      if (out->canon && f != KSS_F_PASS)
+      if (out->canon && !kept)
 #pragma unroll
         for (int x = 0; x < KSS_NSCORE; x++) out->raw[(size_t)x * NN + n] = 0;
     }
+    if (!kept) f = f == KSS_F_PASS ? KSS_F_NOT_EVALUATED : f;  // the dropped node leaves the feasible list
     int ign = 0, il = 0;
     if (f == KSS_F_PASS) {
       nf++;
@@ -968,7 +1093,13 @@ __device__ __forceinline__ bool schedule_pod(const DevCluster& c, const DevPods&
     best = key > best ? key : best;
   }
   KSS_STAMP(S, 4);
-  {
+  if (win && w_total > k_find) {  // with the stopping node's processed count
+    long long v[2] = {best, w_proc};
+    const int op[2] = {OP_MAX, OP_SUM};
+    if (!cluster_reduce(smem, S, v, op)) return false;
+    best = v[0];
+    S.cursor = (int)(((long long)S.cursor + v[1]) % m_list);
+  } else {
     long long v[1] = {best};
     const int op[1] = {OP_MAX};
     if (!cluster_reduce(smem, S, v, op)) return false;

@@ -294,6 +294,8 @@ __device__ void service_loop(DevCluster c, const DevJob& job, const kss_profile&
   S.gran = gran;
   S.err = err;
   S.stamps = nullptr;
+  S.cursor = job.cursor ? *job.cursor : 0;  // nextStartNodeIndex, kept across evaluations and relaunches
+  int cursor_prev = S.cursor;               // before the last evaluation (a repeated cycle starts from it)
   const int cap = npt * (int)blockDim.x;
   if (cache_keys >= 0) {
     long long* b = xvec(smem) + NSCAL + bins_cap + slot_arrays_bytes(cap) / 8;
@@ -399,6 +401,8 @@ __device__ void service_loop(DevCluster c, const DevJob& job, const kss_profile&
       s.norm = (int64_t*)(base + L.norm);
       s.total = (int64_t*)(base + L.total);
       PodMeta m;
+      if (node & 2) S.cursor = cursor_prev;  // the same scheduling cycle again (the full record of a compact one)
+      cursor_prev = S.cursor;
       if (!schedule_pod<GEN>(c, job.P, prof, pi, smem, S, bins_cap, npt, &s, /*keep_norm=*/true, m)) {
         if (threadIdx.x == 0) __hip_atomic_store(&box->err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         break;
@@ -424,6 +428,7 @@ __device__ void service_loop(DevCluster c, const DevJob& job, const kss_profile&
       hv = want;  // the host's rows not asked for now no longer mirror the newest slot
       (compact ? host_valid : host_valid_c) = 0;  // nor does the other record
       if (w == 0 && threadIdx.x == 0) {
+        if (job.cursor) *job.cursor = S.cursor;  // read by the next launch on this context
         KSS_GLOBAL int32_t* mm = reinterpret_cast<KSS_GLOBAL int32_t*>(&box->meta);
         mm[0] = m.chosen;
         mm[1] = m.n_feasible;

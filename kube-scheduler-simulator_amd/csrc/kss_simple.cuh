@@ -68,7 +68,6 @@ __device__ __forceinline__ void st_ag(T* p, T v) {
 // agent-scope release writes the XCD's L2 back; the consumer starts with an agent-scope
 // acquire.  The kernel boundary alone did not order them under a concurrent split-grid part
 // (DESIGN §5).
-#ifndef KSS_NO_HANDOFF
 __device__ __forceinline__ void handoff_drain() {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
@@ -83,11 +82,6 @@ __device__ __forceinline__ void handoff_acquire() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
-#else  // experiment builds: the round-3 hand-off (kernel boundaries only)
-__device__ __forceinline__ void handoff_drain() {}
-__device__ __forceinline__ void handoff_release() {}
-__device__ __forceinline__ void handoff_acquire() {}
-#endif
 
 // Publish one granule at offset `off` of the exchange buffer (the local inbox `gran`);
 // address-space-1 stores (a flat store would also count in lgkmcnt).
@@ -554,7 +548,7 @@ __device__ __forceinline__ bool simple_exchange(SimpleHdr& H, unsigned long long
       if (spin_expired(spins, t0_)) {
         if (lane == 0) {
           H.abort = 1;
-          __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          err_raise(err, 1);
         }
         return false;
       }

@@ -377,10 +377,10 @@ __device__ __forceinline__ bool spread_exchange(SpreadHdr& H, int32_t* xs, unsig
             ok &= !(act && w < W) || (g[b] >> 32) == epoch;
           }
           if (__all(ok)) break;
-          if (spin_expired(spins, t0_)) {
+          if (spread_spin_over(spins, t0_, err)) {
             if (lane == 0) {
               H.abort = 1;
-              __hip_atomic_store(gp(err), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              err_raise(err, 1);
             }
             return false;
           }
@@ -550,10 +550,10 @@ __device__ __forceinline__ bool spread_argmax(SpreadHdr& H, int W, int w, int gs
 #pragma unroll
         for (int b = 0; b < 4; b++) ok &= ((lo[b] >> 32) == epoch) & ((hi[b] >> 32) == epoch);
         if (__all(ok)) break;
-        if (spin_expired(spins, t0_)) {
+        if (spread_spin_over(spins, t0_, err)) {
           if (lane == 0) {
             H.abort = 1;
-            __hip_atomic_store(gp(err), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            err_raise(err, 1);
           }
           break;
         }
@@ -605,10 +605,10 @@ __device__ __forceinline__ bool spread_argmax(SpreadHdr& H, int W, int w, int gs
           if (!kb) hi = __hip_atomic_load(base + (size_t)s * gs + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         if (__all(((lo >> 32) == epoch) & ((hi >> 32) == epoch))) break;
-        if (spin_expired(spins, t0_)) {
+        if (spread_spin_over(spins, t0_, err)) {
           if (lane == 0) {
             H.abort = 1;
-            __hip_atomic_store(gp(err), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            err_raise(err, 1);
           }
           break;
         }
@@ -643,7 +643,8 @@ struct HandoffCheck {
   unsigned long long* sum;    // null: no check
   unsigned long long expect;  // tag the previous chunk wrote (0: the first chunk of the call)
   unsigned long long write;   // tag this chunk writes
-  int* retries;               // [0] loads repeated because the sums disagreed, [1] loads the shadow answered
+  int* retries;               // [0] loads repeated because the sums disagreed, [1] loads the shadow answered,
+                              // [2] shards whose last write-back failed the final check
   long long* shadow;          // [(6 + n_res) N]: requested x3, nonzero x2, pod count, resident count rows
   int* xcc;                   // [W]: the XCC that ran each shard's last epilogue
   long long* diag;            // [1 + HANDOFF_DIAG * HANDOFF_DIAG_W]: count, then the differing words
@@ -688,7 +689,7 @@ __device__ __forceinline__ bool handoff_verify(const HandoffCheck& hc, int w, un
       __hip_atomic_fetch_add(hc.retries, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (attempt >= 64) {
         *abort_flag = 1;
-        __hip_atomic_store(err, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        err_raise(err, 2);
       }
     }
   }
@@ -701,6 +702,43 @@ __device__ __forceinline__ bool handoff_verify(const HandoffCheck& hc, int w, un
   }
   return ok;
 }
+// The last chunk's write-back, checked after the loop launch has ended (a next chunk's
+// prologue checks every other hand-off): shard w's node state in HBM summed as the prologue
+// sums it, against the sum and tag its epilogue stored.  A disagreement fails the run (err = 2)
+// and counts in retries[2]; nothing is repaired, so no corrupted write-back passes silently.
+__device__ __forceinline__ void handoff_final_check(const DevCluster& c, const int32_t* __restrict__ res_rows, int n_res,
+                                                    int W, int w, const HandoffCheck& hc, int* err, long long* scratch) {
+  const size_t N = (size_t)c.N;
+  const int per = (c.N + W - 1) / W;
+  const int lo = min(c.N, w * per), hi = min(c.N, lo + per), own = hi - lo, nsc = c.n_scalar;
+  handoff_acquire();
+  unsigned long long h = 0;
+  for (int s = threadIdx.x; s < own; s += blockDim.x) {
+    const int n = lo + s;
+#pragma unroll
+    for (int k = 0; k < 3; k++) h += handoff_mix((unsigned long long)ld_ag(&c.requested[k * N + n]), (size_t)k * N + n);
+    h += handoff_mix((unsigned long long)ld_ag(&c.nonzero[n]), 3 * N + n) +
+         handoff_mix((unsigned long long)ld_ag(&c.nonzero[N + n]), 4 * N + n) +
+         handoff_mix((unsigned long long)(uint32_t)ld_ag(&c.pod_count[n]), 5 * N + n);
+    for (int i = 0; i < nsc; i++)
+      h += handoff_mix((unsigned long long)ld_ag(&c.requested[(size_t)(3 + i) * N + n]), (6 + (size_t)n_res + i) * N + n);
+  }
+  for (int i = threadIdx.x; i < n_res * own; i += blockDim.x) {
+    const int r = i / own, s = i - r * own, row = res_rows[r];
+    const int32_t v = row < c.n_classes ? ld_ag(&c.class_count[(size_t)row * N + lo + s])
+                                        : ld_ag(&c.term_count[(size_t)(row - c.n_classes) * N + lo + s]);
+    h += handoff_mix((unsigned long long)(uint32_t)v, (6 + (size_t)r) * N + lo + s);
+  }
+  const unsigned long long t = handoff_sum(h, scratch);
+  if (threadIdx.x == 0) {
+    const bool ok = ld_ag(&hc.sum[2 * (size_t)w + 1]) == hc.expect && ld_ag(&hc.sum[2 * (size_t)w]) == t;
+    if (!ok) {
+      __hip_atomic_fetch_add(hc.retries + 2, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      err_raise(err, 2);
+    }
+  }
+}
+
 // One differing word of the hand-off (first disagreement of a launch): array a (0-2 requested,
 // 3-4 nonzero, 5 pod count, 6 + r resident count row r), node n, and the views of it.
 __device__ __forceinline__ void handoff_note(const HandoffCheck& hc, int w, int a, int n, long long plain,

@@ -62,6 +62,7 @@ KSS_F_POD_TOPOLOGY_SPREAD = 14
 KSS_F_INTER_POD_AFFINITY = 15
 KSS_NFILTER = 15
 KSS_F_NOT_EVALUATED = 255
+KSS_PASS_NOT_KEPT = 1  # fail_detail of the passing node that ended a percentageOfNodesToScore search
 
 KSS_FIT_TOO_MANY_PODS = 1 << 0
 KSS_FIT_CPU = 1 << 1

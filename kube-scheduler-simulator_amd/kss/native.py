@@ -69,12 +69,17 @@ SIGNATURES = [
     ("kss_last_loop_timing", C.c_int, [C.c_void_p, P(C.c_double)]),
     ("kss_last_handoff_retries", C.c_int, [C.c_void_p, P(C.c_int32)]),
     ("kss_last_handoff_diag", C.c_int, [C.c_void_p, P(C.c_int32), P(C.c_int64), C.c_int32, P(C.c_int32)]),
+    ("kss_last_handoff_status", C.c_int, [C.c_void_p, P(C.c_int32)]),
     ("kss_buffer_map", C.c_int, [C.c_void_p, P(C.c_uint64), P(C.c_uint64), C.c_int32, P(C.c_int32)]),
     ("kss_last_geometry", C.c_int, [C.c_void_p, P(C.c_int32)]),
     ("kss_last_kernel", C.c_int, [C.c_void_p]),
     ("kss_device_go_log", C.c_int, [C.c_int32, C.c_void_p, C.c_void_p, C.c_int32]),
     ("kss_plan_podset", C.c_int, [C.POINTER(abi.Cluster), C.POINTER(abi.PodSet), C.c_void_p]),
+    ("kss_plan_podset_ex", C.c_int, [C.POINTER(abi.Cluster), C.POINTER(abi.PodSet), C.POINTER(abi.Profile),
+                                     C.c_void_p]),
     ("kss_plan_reason", C.c_char_p, [C.c_int32]),
+    ("kss_next_start_node_index", C.c_int, [C.c_void_p, P(C.c_int32)]),
+    ("kss_set_next_start_node_index", C.c_int, [C.c_void_p, C.c_int32]),
     ("kss_fetch_meta", C.c_int, [C.c_void_p, C.c_int32, C.c_int32, P(C.c_int64)]),
     ("kss_set_names", C.c_int, [C.c_void_p, P(abi.Names)]),
     ("kss_format_annotations", C.c_int, [C.c_void_p, P(abi.PodResult), C.c_int32, C.c_char_p, C.c_size_t,
@@ -526,6 +531,22 @@ class Context:
         check(lib().kss_last_handoff_retries(self.h, C.byref(n)))
         return n.value
 
+    def next_start_node_index(self) -> int:
+        """nextStartNodeIndex (kss_next_start_node_index)."""
+        v = C.c_int32(0)
+        check(lib().kss_next_start_node_index(self.h, C.byref(v)))
+        return v.value
+
+    def set_next_start_node_index(self, v: int):
+        check(lib().kss_set_next_start_node_index(self.h, int(v)))
+
+    def last_handoff_status(self) -> Dict[str, int]:
+        """{reloads, shadow, final} of the last k_spread run (kss_last_handoff_status): all 0
+        when every hand-off between chunk launches and the last write-back were clean."""
+        out = (C.c_int32 * 3)()
+        check(lib().kss_last_handoff_status(self.h, out))
+        return {"reloads": out[0], "shadow": out[1], "final": out[2]}
+
     def last_handoff_diag(self):
         """(shadow recoveries, [entry dicts]) of the last run (kss_last_handoff_diag)."""
         rec, n = C.c_int32(0), C.c_int32(0)
@@ -663,9 +684,14 @@ def device_go_log(x, device: int = 0) -> np.ndarray:
     return y
 
 
-def plan_podset(cluster: abi.Cluster, podset: abi.PodSet) -> dict:
-    """Host-only: the sequential-loop kernel a staged batch can take (kss_plan_podset)."""
+def plan_podset(cluster: abi.Cluster, podset: abi.PodSet, profile: Optional[abi.Profile] = None) -> dict:
+    """Host-only: the sequential-loop kernel a staged batch can take (kss_plan_podset; with the
+    profile: kss_plan_podset_ex, which also sees percentageOfNodesToScore and scored extended
+    resources)."""
     out = (C.c_int32 * 3)()
-    check(lib().kss_plan_podset(C.byref(cluster), C.byref(podset), out))
+    if profile is None:
+        check(lib().kss_plan_podset(C.byref(cluster), C.byref(podset), out))
+    else:
+        check(lib().kss_plan_podset_ex(C.byref(cluster), C.byref(podset), C.byref(profile), out))
     kernel = {1: "k_simple", 2: "k_spread"}.get(out[0], "k_schedule")
     return {"kernel": kernel, "pod": out[1], "reason": lib().kss_plan_reason(out[2]).decode()}

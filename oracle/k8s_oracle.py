@@ -492,6 +492,22 @@ DEFAULT_WEIGHTS = {"TaintToleration": 3, "NodeAffinity": 2, "NodeResourcesFit": 
                    "ImageLocality": 1}
 
 
+def num_feasible_nodes_to_find(num_all_nodes: int, pct: int) -> int:
+    """Scheduler.numFeasibleNodesToFind (pkg/scheduler/schedule_one.go, v1.26.2)."""
+    min_feasible_nodes_to_find, min_feasible_nodes_percentage_to_find = 100, 5
+    if num_all_nodes < min_feasible_nodes_to_find or pct >= 100:
+        return num_all_nodes
+    adaptive = pct
+    if adaptive <= 0:
+        adaptive = 50 - num_all_nodes // 125
+        if adaptive < min_feasible_nodes_percentage_to_find:
+            adaptive = min_feasible_nodes_percentage_to_find
+    num_nodes = num_all_nodes * adaptive // 100
+    if num_nodes < min_feasible_nodes_to_find:
+        return min_feasible_nodes_to_find
+    return num_nodes
+
+
 def go_log(x: float) -> float:
     """Go math.Log (src/math/log.go)."""
     Ln2Hi, Ln2Lo = 6.93147180369123816490e-01, 1.90821492927058770002e-10
@@ -523,8 +539,10 @@ class Oracle:
 
     def __init__(self, nodes, bound_pods=(), namespaces=None, weights=None, hard_pod_affinity_weight=1,
                  system_defaulted=True, fit_strategy="LeastAllocated", fit_resources=(("cpu", 1), ("memory", 1)),
-                 ba_resources=("cpu", "memory"), storage=None):
-        """storage: k8s_volumes.Storage (PVs, PVCs, StorageClasses, CSINodes) for the volume plugins."""
+                 ba_resources=("cpu", "memory"), storage=None, percentage_of_nodes_to_score=100):
+        """storage: k8s_volumes.Storage (PVs, PVCs, StorageClasses, CSINodes) for the volume plugins.
+        percentage_of_nodes_to_score: KubeSchedulerConfiguration.percentageOfNodesToScore (0: the
+        adaptive default the simulator's built-in scheduler runs with)."""
         import k8s_volumes
         self.storage = storage if storage is not None else k8s_volumes.Storage()
         self.nodes = node_tree_list(list(nodes))
@@ -555,6 +573,8 @@ class Oracle:
         self.fit_strategy = fit_strategy
         self.fit_resources = list(fit_resources)
         self.ba_resources = list(ba_resources)
+        self.pct = percentage_of_nodes_to_score
+        self.next_start = 0  # Scheduler.nextStartNodeIndex
 
     # ----------------------------------------------------------- ImageLocality
     def image_locality_score(self, pod, ni) -> int:
@@ -991,15 +1011,33 @@ class Oracle:
         res["_pts_st"], res["_ipa_st"] = pts_st, ipa_st  # the cycle state PostFilter sees
         feasible = []
         tols = sp.get("tolerations") or []
-        for i, ni in enumerate(self.infos):
-            node = ni.node
-            if node_subset is not None and _name(node) not in node_subset:
-                continue
+        # findNodesThatPassFilters (schedule_one.go, v1.26) with Parallelism = 1: the node list (the
+        # PreFilterResult set in canonical order -- upstream ranges over a Go map here) is checked
+        # one node at a time from nextStartNodeIndex; the feasible node that makes the count exceed
+        # numFeasibleNodesToFind cancels the search and is dropped (its filters ran: it is recorded).
+        node_list = [i for i, ni in enumerate(self.infos) if node_subset is None or _name(ni.node) in node_subset]
+        m = len(node_list)
+        num_to_find = num_feasible_nodes_to_find(m, self.pct)
+        feasible_len, statuses = 0, 0
+        res["dropped"] = None
+        for j in range(m):
+            i = node_list[(self.next_start + j) % m]
+            ni = self.infos[i]
             failed, rec = self.filter_node(pod, ni, pts_st, ipa_st, vb_claims)
-            ann_filter[_name(node)] = rec
+            ann_filter[_name(ni.node)] = rec
             res["fail"][i] = failed
             if failed is None:
+                feasible_len += 1
+                if feasible_len > num_to_find:  # cancel(); atomic.AddInt32(&feasibleNodesLen, -1)
+                    feasible_len -= 1
+                    res["dropped"] = i
+                    break
                 feasible.append(i)
+            else:
+                statuses += 1  # diagnosis.NodeToStatusMap
+        if m:
+            self.next_start = (self.next_start + feasible_len + statuses) % m
+        feasible.sort()  # selectHost's deterministic tie-break is the canonical index, not the visit order
         res["n_feasible"] = len(feasible)
         if not feasible:
             res["status"] = "unschedulable"

@@ -81,11 +81,13 @@ typedef struct {
   uint64_t* port_used;
   int32_t* vol_count;
   int32_t* vol_attached;
+  int32_t cursor; /* the scheduler's nextStartNodeIndex (schedule_one.go findNodesThatPassFilters) */
 } ostate;
 
 static int ostate_init(ostate* s, const kss_cluster* cl) {
   size_t N = (size_t)cl->n_nodes;
   s->c = *cl;
+  s->cursor = 0;
   s->requested = (int64_t*)malloc(sizeof(int64_t) * KSS_NRES * (N ? N : 1));
   s->nonzero = (int64_t*)malloc(sizeof(int64_t) * 2 * (N ? N : 1));
   s->pod_count = (int32_t*)malloc(sizeof(int32_t) * (N ? N : 1));
@@ -711,6 +713,20 @@ typedef struct {
   int threads;
 } oracle_opts;
 
+/* numFeasibleNodesToFind (v1.26 pkg/scheduler/schedule_one.go): all nodes when the list is shorter
+   than minFeasibleNodesToFind (100) or percentageOfNodesToScore >= 100; pct <= 0 means the adaptive
+   50 - numAllNodes/125 percent, at least minFeasibleNodesPercentageToFind (5); at least 100 nodes. */
+static int num_feasible_to_find(int m, int pct) {
+  if (m < 100 || pct >= 100) return m;
+  int a = pct;
+  if (a <= 0) {
+    a = 50 - m / 125;
+    if (a < 5) a = 5;
+  }
+  long long k = (long long)m * a / 100;
+  return k < 100 ? 100 : (int)k;
+}
+
 /* one scheduling cycle (schedulePod) for pod p against state s; fills out (arrays sized N) */
 static int schedule_one(const kss_profile* prof, ostate* s, const kss_podset* ps, int pi, kss_pod_result* out,
                         int threads) {
@@ -758,11 +774,43 @@ static int schedule_one(const kss_profile* prof, ostate* s, const kss_podset* ps
       if (inset && !inset[n]) continue;
       fp[n] = (uint8_t)filter_node(prof, cl, ps, p, &st, n, &fd[n]);
     }
+    /* findNodesThatPassFilters with Parallelism = 1: the node list (all nodes, or the
+       PreFilterResult set in canonical order) is visited from nextStartNodeIndex until one
+       feasible node more than numFeasibleNodesToFind has been found.  That node passed every
+       filter (recorded) but is not in the feasible list; nodes after it were never filtered.
+       nextStartNodeIndex advances by the nodes processed: the feasible ones kept plus the
+       infeasible ones visited (schedule_one.go: processedNodes = feasibleNodesLen +
+       len(diagnosis.NodeToStatusMap)). */
+    int m = 0;
+    int32_t* list = (int32_t*)malloc(sizeof(int32_t) * (size_t)(N ? N : 1));
+    for (int n = 0; n < N; n++)
+      if (!inset || inset[n]) list[m++] = n;
+    if (m > 0) {
+      const int K = num_feasible_to_find(m, prof->pct_nodes_to_score);
+      const int start = (int)((int64_t)s->cursor % m);
+      int found = 0, processed = m, i = 0;
+      for (; i < m; i++) {
+        const int n = list[(start + i) % m];
+        if (fp[n] != KSS_F_PASS) continue;
+        if (++found > K) { /* the context is cancelled after this node: it is dropped */
+          fd[n] = KSS_PASS_NOT_KEPT;
+          processed = i;
+          break;
+        }
+      }
+      for (int j = i + 1; j < m; j++) { /* never visited */
+        const int n = list[(start + j) % m];
+        fp[n] = KSS_F_NOT_EVALUATED;
+        fd[n] = 0;
+      }
+      s->cursor = (int32_t)(((int64_t)s->cursor + processed) % m);
+    }
+    free(list);
     free(inset);
   }
   int nf = 0;
   for (int n = 0; n < N; n++)
-    if (fp[n] == KSS_F_PASS) feas[nf++] = n;
+    if (fp[n] == KSS_F_PASS && fd[n] != KSS_PASS_NOT_KEPT) feas[nf++] = n;
   out->n_feasible = nf;
   if (nf == 0) {
     out->status = 1;
@@ -1007,6 +1055,13 @@ int kss_oracle_eval_pod(const kss_profile* prof, const kss_cluster* cl, const ks
   return rc;
 }
 
+/* kss_oracle_schedule_v with the scheduler's nextStartNodeIndex in and out (NULL: starts at 0). */
+int kss_oracle_schedule_c(const kss_profile* prof, const kss_cluster* cl, const kss_podset* ps, int n,
+                          int32_t* chosen, kss_pod_result* results, int threads, int64_t* out_requested,
+                          int64_t* out_nonzero, int32_t* out_pod_count, int32_t* out_class_count,
+                          int32_t* out_term_count, uint64_t* out_port_used, int32_t* out_vol_count,
+                          int32_t* out_vol_attached, int32_t* cursor);
+
 /* Sequentially schedule pods [0, n): each pod sees the previous commits.
  * results (optional) is an array of n kss_pod_result whose arrays the caller
  * allocated (any NULL array is skipped).  Final node state is written back to
@@ -1016,8 +1071,18 @@ int kss_oracle_schedule_v(const kss_profile* prof, const kss_cluster* cl, const 
                           int64_t* out_nonzero, int32_t* out_pod_count, int32_t* out_class_count,
                           int32_t* out_term_count, uint64_t* out_port_used, int32_t* out_vol_count,
                           int32_t* out_vol_attached) {
+  return kss_oracle_schedule_c(prof, cl, ps, n, chosen, results, threads, out_requested, out_nonzero, out_pod_count,
+                               out_class_count, out_term_count, out_port_used, out_vol_count, out_vol_attached, NULL);
+}
+
+int kss_oracle_schedule_c(const kss_profile* prof, const kss_cluster* cl, const kss_podset* ps, int n,
+                          int32_t* chosen, kss_pod_result* results, int threads, int64_t* out_requested,
+                          int64_t* out_nonzero, int32_t* out_pod_count, int32_t* out_class_count,
+                          int32_t* out_term_count, uint64_t* out_port_used, int32_t* out_vol_count,
+                          int32_t* out_vol_attached, int32_t* cursor) {
   ostate s;
   if (ostate_init(&s, cl)) return KSS_E_NOMEM;
+  if (cursor) s.cursor = *cursor;
   int th = threads > 0 ? threads : 1;
   int rc = 0;
   for (int i = 0; i < n; i++) {
@@ -1040,6 +1105,7 @@ int kss_oracle_schedule_v(const kss_profile* prof, const kss_cluster* cl, const 
   if (out_vol_count && cl->n_vol_rows) memcpy(out_vol_count, s.vol_count, sizeof(int32_t) * (size_t)cl->n_vol_rows * N);
   if (out_vol_attached && cl->n_vol_keys)
     memcpy(out_vol_attached, s.vol_attached, sizeof(int32_t) * (size_t)cl->n_vol_keys * N);
+  if (cursor) *cursor = s.cursor;
   ostate_free(&s);
   return rc;
 }

@@ -28,3 +28,31 @@ def pytest_collection_modifyitems(session, config, items):
         return
     if torch.cuda.is_available():
         torch.zeros(1, device="cuda")
+
+
+CLEAN_HANDOFF = {"reloads": 0, "shadow": 0, "final": 0}
+
+
+@pytest.fixture(autouse=True)
+def _k_spread_handoff_clean(request, monkeypatch):
+    """Every -m gpu test: after each k_spread run (run_staged / schedule_batch, split parts
+    included) the node-state hand-off counters must be zero -- no prologue reload, no load the
+    shadow copy answered, no last write-back that failed the final check.  A repaired hand-off
+    fails the test even when the repaired results match the oracle."""
+    if request.node.get_closest_marker("gpu") is None:
+        yield
+        return
+    from kss import native
+
+    def checked(fn):
+        def run(self, *a, **k):
+            out = fn(self, *a, **k)
+            if self.last_kernel() == "k_spread":
+                st = self.last_handoff_status()
+                assert st == CLEAN_HANDOFF, f"k_spread hand-off not clean: {st} (diag {self.last_handoff_diag()})"
+            return out
+        return run
+
+    monkeypatch.setattr(native.Context, "run_staged", checked(native.Context.run_staged))
+    monkeypatch.setattr(native.Context, "schedule_batch", checked(native.Context.schedule_batch))
+    yield

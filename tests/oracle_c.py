@@ -25,6 +25,8 @@ def lib():
         _lib.kss_oracle_schedule.restype = C.c_int
         _lib.kss_oracle_schedule_v.argtypes = _lib.kss_oracle_schedule.argtypes + [P(C.c_int32), P(C.c_int32)]
         _lib.kss_oracle_schedule_v.restype = C.c_int
+        _lib.kss_oracle_schedule_c.argtypes = _lib.kss_oracle_schedule_v.argtypes + [P(C.c_int32)]
+        _lib.kss_oracle_schedule_c.restype = C.c_int
         _lib.kss_oracle_eval_pod.argtypes = [P(abi.Profile), P(abi.Cluster), P(abi.PodSet), C.c_int,
                                              P(abi.PodResult), C.c_int]
         _lib.kss_oracle_eval_pod.restype = C.c_int
@@ -81,9 +83,11 @@ class Results:
 
 
 def schedule(profile, cluster_struct, podset_struct, n_pods, n_nodes, threads=1, record=True, n_classes=0,
-             n_terms=0):
+             n_terms=0, cursor=0):
     """Run the C oracle sequentially; returns (chosen, Results|None, final_state dict).
-    record=True keeps every per-node array, record="meta" only the per-pod outcomes."""
+    record=True keeps every per-node array, record="meta" only the per-pod outcomes.
+    cursor: the scheduler's nextStartNodeIndex at the first pod; the final value is
+    final_state["next_start"]."""
     L = lib()
     chosen = np.full(max(n_pods, 1), -2, dtype=np.int32)
     res = Results(n_pods, n_nodes, arrays=record is True) if record else None
@@ -94,7 +98,8 @@ def schedule(profile, cluster_struct, podset_struct, n_pods, n_nodes, threads=1,
               vol_count=np.zeros((max(cluster_struct.n_vol_rows, 1), N), np.int32),
               vol_attached=np.zeros((max(cluster_struct.n_vol_keys, 1), N), np.int32))
     P = C.POINTER
-    rc = L.kss_oracle_schedule_v(C.byref(profile), C.byref(cluster_struct), C.byref(podset_struct), n_pods,
+    cur = C.c_int32(cursor)
+    rc = L.kss_oracle_schedule_c(C.byref(profile), C.byref(cluster_struct), C.byref(podset_struct), n_pods,
                                chosen.ctypes.data_as(P(C.c_int32)), res.structs if res else None, threads,
                                st["requested"].ctypes.data_as(P(C.c_int64)), st["nonzero"].ctypes.data_as(P(C.c_int64)),
                                st["pod_count"].ctypes.data_as(P(C.c_int32)),
@@ -102,8 +107,9 @@ def schedule(profile, cluster_struct, podset_struct, n_pods, n_nodes, threads=1,
                                st["term_count"].ctypes.data_as(P(C.c_int32)),
                                st["port_used"].ctypes.data_as(P(C.c_uint64)),
                                st["vol_count"].ctypes.data_as(P(C.c_int32)),
-                               st["vol_attached"].ctypes.data_as(P(C.c_int32)))
+                               st["vol_attached"].ctypes.data_as(P(C.c_int32)), C.byref(cur))
     assert rc == 0, f"oracle rc={rc}"
+    st["next_start"] = cur.value
     st["vol_count"] = st["vol_count"][:cluster_struct.n_vol_rows, :n_nodes]
     st["vol_attached"] = st["vol_attached"][:cluster_struct.n_vol_keys, :n_nodes]
     return chosen[:n_pods], res, st

@@ -70,3 +70,25 @@ def test_go_json_escaping():
                                "d\n ": {"NodeUnschedulable": "node(s) were unschedulable"}})
     assert got["scheduler-simulator/filter-result"] == want
     assert "\\u003c" in want and "\\u2028" in want
+
+
+@pytest.mark.parametrize("pct", [0, 30])
+def test_formatter_window_matches_object_oracle(pct):
+    """percentageOfNodesToScore below 100: filter-result lists the visited nodes (the dropped
+    one as all-passed), score-result / finalscore-result only the kept ones, and nodes past the
+    stop are absent -- the formatter over the C oracle's records equals the object oracle's
+    store.go restatement for every pod (pod-aware: the PreFilterResult sets of test_oracle_crosscheck)."""
+    from test_oracle_crosscheck import with_name_sets
+    nodes, bound, pods = synth.make_cluster(1, 220, 90)
+    pods = with_name_sets(pods, [n["metadata"]["name"] for n in nodes], every=4, size=120)
+    cc, cp, _ = compile_cluster(nodes, bound, pods)
+    prof = abi.default_profile()
+    prof.pct_nodes_to_score = pct
+    ch, res, _ = oracle_c.schedule(prof, cc.as_struct(), cp.as_struct(), cp.n, cc.n_nodes)
+    o = k8s_oracle.Oracle(nodes, bound, percentage_of_nodes_to_score=pct)
+    dropped = 0
+    for j in range(cp.n):
+        r = o.schedule_one(pods[j])
+        dropped += r["dropped"] is not None
+        assert _format_from_oracle(cc, cp, res, j, prof, pod_aware=True) == o.annotations(r), j
+    assert dropped > 0

@@ -244,6 +244,43 @@ def test_sweep_resident_reruns_match_oracle():
     sw.close()
 
 
+def test_c5_sweep_forced_chunks_three_reruns(monkeypatch):
+    """C5's shape (64 scenarios x 1,000 nodes x 1,000 pods) with KSS_STATIC_BYTES forcing four
+    k_static chunks of 300 pods: every rerun restores all scenarios' node state with the reset
+    kernel (no runtime copy) and the chunks hand node state over in HBM; three runs, each equal
+    to the oracle scenario by scenario."""
+    monkeypatch.setenv("KSS_STATIC_BYTES", str(4 * 64 * 1000 * 300))
+    prof = abi.default_profile()
+    syn = [native.Synth(5, SEED_BASE + 5 + 7919 * k, 1000, 1000) for k in range(64)]
+    sw = native.Sweep(prof, [x.cluster for x in syn], [x.pods for x in syn])
+    assert sw.info()["kernel"] == "k_simple"
+    want = [_oracle(prof, x, x.n_pods)[0] for x in syn]
+    for rep in range(3):
+        chosen, _ = sw.run()
+        off = 0
+        for k, x in enumerate(syn):
+            np.testing.assert_array_equal(chosen[off:off + x.n_pods], want[k], err_msg=f"run {rep} scenario {k}")
+            off += x.n_pods
+    sw.close()
+
+
+def test_sweep_odd_chunk_mixed_node_parity(monkeypatch):
+    """An odd chunk (37 pods) over scenarios with odd and even node counts: each scenario's
+    static words start at a 16-byte boundary, so k_static's paired 8-byte stores stay aligned
+    (ADVICE r4); 151 pods, two runs."""
+    sizes = [1001, 37, 700, 999, 3, 512, 64]
+    monkeypatch.setenv("KSS_STATIC_BYTES", str(4 * sum(sizes) * 37))
+    prof = abi.default_profile()
+    syn = [native.Synth(2, SEED_BASE + 2 + 7919 * k, n, 151) for k, n in enumerate(sizes)]
+    sw = native.Sweep(prof, [x.cluster for x in syn], [x.pods for x in syn])
+    assert sw.info()["kernel"] == "k_simple"
+    want = np.concatenate([_oracle(prof, x, x.n_pods)[0] for x in syn])
+    for rep in range(2):
+        chosen, _ = sw.run()
+        np.testing.assert_array_equal(chosen, want, err_msg=f"run {rep}")
+    sw.close()
+
+
 def _custom_profile():
     """MostAllocated over cpu:3 / memory:2 (weight sum 5), BalancedAllocation over three
     resources (the standard-deviation branch), non-default plugin weights."""

@@ -80,7 +80,6 @@ def test_parts_over_many_chunks(monkeypatch, config, n_nodes, n_pods, per_chunk,
         except native.KssError:
             _handoff_report(sp, rep, failed=True)
             raise
-        _handoff_report(sp, rep)
         bad = [np.flatnonzero(np.asarray(ch) != ch_o) for ch in outs]
         g = sp.node_state()
         if any(len(b) for b in bad) or (s.cluster.n_classes and not np.array_equal(
@@ -102,6 +101,7 @@ def test_parts_over_many_chunks(monkeypatch, config, n_nodes, n_pods, per_chunk,
                 d = np.argwhere(g[key][:n_rows, :N] != st[key][:n_rows, :N])
                 assert not len(d), (f"run {rep}: {key} differs at (row, node, device, oracle) " + str(
                     [(int(a), int(b), int(g[key][a, b]), int(st[key][a, b])) for a, b in d[:8]]))
+        _handoff_report(sp, rep)
     sp.close()
 
 
@@ -130,6 +130,8 @@ def _handoff_report(sp, rep, failed=False):
         if os.environ.get("KSS_HANDOFF_LOG"):
             with open(os.environ["KSS_HANDOFF_LOG"], "a") as f:
                 f.write("\n".join(lines) + "\n")
+    for p, c in enumerate(sp.ctxs):  # a repaired hand-off is a failure, not a footnote
+        assert c.last_handoff_status() == {"reloads": 0, "shadow": 0, "final": 0}, (p, "\n".join(lines))
 
 
 def test_shards_per_part_never_exceed_nodes():
@@ -236,12 +238,13 @@ def _rank_main(rank, world, port, config, n_nodes, n_pods, wl, q, device_of=None
         chosen = r.run(n_pods)
         lo, hi = r.rows()
         st = r.ctx.node_state()
-        q.put((rank, chosen.tolist(), lo, hi, st["requested"][:, lo:hi].tolist(), r.ctx.last_kernel()))
+        q.put((rank, chosen.tolist(), lo, hi, st["requested"][:, lo:hi].tolist(), r.ctx.last_kernel(),
+               r.ctx.last_handoff_status()))
         dist.barrier()
         r.close()
         dist.destroy_process_group()
     except Exception as e:  # noqa: BLE001 - reported to the parent
-        q.put((rank, repr(e), 0, 0, None, None))
+        q.put((rank, repr(e), 0, 0, None, None, None))
 
 
 def _identity(r):
@@ -271,9 +274,10 @@ def test_two_processes_through_ipc_handles(two_gpus):
     got = [q.get(timeout=240) for _ in ps]
     for p in ps:
         p.join(timeout=60)
-    for rank, chosen, lo, hi, req, kernel in got:
+    for rank, chosen, lo, hi, req, kernel, handoff in got:
         assert req is not None, chosen  # the child's exception
         assert kernel == "k_spread"
+        assert handoff == {"reloads": 0, "shadow": 0, "final": 0}, (rank, handoff)
         np.testing.assert_array_equal(np.array(chosen), ch_o, err_msg=f"rank {rank}")
         np.testing.assert_array_equal(np.array(req, dtype=np.int64).reshape(abi.KSS_NRES, hi - lo),
                                       st["requested"][:, lo:hi], err_msg=f"rank {rank}")

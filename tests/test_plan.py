@@ -45,3 +45,34 @@ def test_refusal_names_pod_and_reason():
     cc, cp, _ = compile_cluster(nodes, bound, pods)
     plan = native.plan_podset(cc.as_struct(), cp.as_struct())
     assert plan == {"kernel": "k_schedule", "pod": 3, "reason": "more than 4 inter-pod-affinity topology keys"}
+
+
+def test_profile_aware_plan():
+    """kss_plan_podset_ex: the profile rules out both loop kernels when percentageOfNodesToScore
+    is below 100 (the window runs on k_schedule), or when it scores an extended resource that
+    the cluster has; otherwise it answers as kss_plan_podset."""
+    s = native.Synth(2, 0, 500, 50)
+    assert native.plan_podset(s.cluster, s.pods)["kernel"] == "k_simple"
+    for pct in (0, 30, 99):
+        p = abi.default_profile()
+        p.pct_nodes_to_score = pct
+        r = native.plan_podset(s.cluster, s.pods, p)
+        assert r["kernel"] == "k_schedule" and "percentageOfNodesToScore" in r["reason"], r
+    assert native.plan_podset(s.cluster, s.pods, abi.default_profile())["kernel"] == "k_simple"
+    nodes, bound, pods = progfuzz.make(2, 60, 200, n_extended=2, programs=False)
+    cc, cp, _ = compile_cluster(nodes, bound, pods)
+    p = abi.default_profile()
+    p.fit_n = 3
+    p.fit_res[2] = abi.KSS_RES_SCALAR0
+    p.fit_weight[2] = 1
+    r = native.plan_podset(cc.as_struct(), cp.as_struct(), p)
+    assert r["kernel"] == "k_schedule" and "extended" in r["reason"], r
+    assert native.plan_podset(cc.as_struct(), cp.as_struct(), abi.default_profile())["kernel"] == "k_simple"
+
+
+def test_profile_pct_range_is_checked():
+    s = native.Synth(2, 0, 50, 5)
+    p = abi.default_profile()
+    p.pct_nodes_to_score = 101
+    with pytest.raises(native.KssError, match="percentageOfNodesToScore"):
+        native.plan_podset(s.cluster, s.pods, p)
