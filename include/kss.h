@@ -682,6 +682,11 @@ int kss_buffer_map(kss_ctx* ctx, uint64_t* base, uint64_t* bytes, int32_t cap, i
 /* launch geometry of the last scheduling launch: out[0] shards (workgroups) per cluster,
  * out[1] threads per workgroup, out[2] node slots per lane */
 int kss_last_geometry(kss_ctx* ctx, int32_t* out3);
+/* XCD-local grid of the last run: out2[0] = 1 when its k_simple shards ran on one XCD (the
+ * per-pod exchange in that XCD's L2: a cluster of at most CUs-per-XCD shards, one node per lane;
+ * KSS_XCD=0 disables it), out2[1] = the chunks that found fewer workgroups on that XCD than shards
+ * and ran again on an unrestricted grid (correctness never rests on placement). */
+int kss_last_xcd_local(kss_ctx* ctx, int32_t* out2);
 /* kernel of the last scheduling launch: 0 general (k_schedule), 1 compact (k_simple:
  * batches without spread / inter-pod programs and without a record), 2 k_spread (batches
  * with programs, without a record), 3 k_preempt (kss_postfilter_pod); <0 on error */

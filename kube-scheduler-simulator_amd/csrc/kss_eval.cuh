@@ -145,7 +145,7 @@ struct XPeers {
   int32_t n;
   int32_t w_off;
   int32_t wl;
-  int32_t pad;
+  int32_t xcd_local;  // k_simple, one part: every shard on one XCD (xcd_slot), granules published with plain stores
   unsigned long long* inbox[KSS_MAX_PARTS];
 };
 

@@ -216,10 +216,17 @@ __global__ __launch_bounds__(KSS_MAX_THREADS) void k_simple(const DevJob* __rest
                                                             unsigned long long* stamps, XPeers X, unsigned epoch0) {
   extern __shared__ __attribute__((aligned(16))) long long smem[];
   const int Wl = X.n > 1 ? X.wl : W;  // shards of this launch (a split grid runs [w_off, w_off + wl))
-  const int ji = blockIdx.x / Wl, w = X.w_off + (int)(blockIdx.x % Wl);
+  SimpleHdr& H = *reinterpret_cast<SimpleHdr*>(smem);
+  int xs = 0;
+  if (X.xcd_local) {  // one cluster, every shard on XCD 0 (xcd_slot); the other workgroups leave
+    if (threadIdx.x == 0) H.pad[0] = xcd_slot(reinterpret_cast<int*>(gran + 2 * (size_t)W * SX_VALS), W, (int)gridDim.x, err);
+    __syncthreads();
+    xs = H.pad[0];
+    if (xs < 0) return;
+  }
+  const int ji = X.xcd_local ? 0 : blockIdx.x / Wl, w = X.xcd_local ? xs : X.w_off + (int)(blockIdx.x % Wl);
   const DevJob job = jobs[ji];
   constexpr kss_profile def_prof = default_profile_c();
-  SimpleHdr& H = *reinterpret_cast<SimpleHdr*>(smem);
   if (!DEF) {
     const uint32_t* src = reinterpret_cast<const uint32_t*>(&jobs[ji].prof);
     uint32_t* dst = reinterpret_cast<uint32_t*>(&H.prof);
@@ -291,43 +298,62 @@ __global__ __launch_bounds__(256) void k_handoff_final(const DevJob* __restrict_
   handoff_final_check(job.c, job.res_rows, n_res, W, w_off + (int)blockIdx.x, hc, err, scratch);
 }
 
-// Static words of pods [k0, min(k1, n_pods)) x every node of every job.  grid: x = 512-node
-// tiles, y = groups of STATIC_PODS pods, z = job.  One lane per PAIR of adjacent nodes walks its
-// group: the pair's two words leave as one 8-byte agent-scope store where the row layout keeps
-// it aligned (N and n_lo even), two 4-byte ones otherwise.
+// Static words of pods [k0, min(k1, n_pods)) x every node of every job.  grid: x = 1024-node
+// tiles, y = groups of STATIC_PODS pods, z = job.  One lane per QUAD of adjacent nodes walks its
+// group: the quad's four words leave as one 16-byte agent-scope (sc1, write-through) store where
+// the row layout keeps it aligned (N and n_lo multiples of 4, the job's stat buffer 16-byte
+// aligned), as 8- or 4-byte agent-scope stores otherwise.  Per byte a 16-byte sc1 store costs
+// about a third of an 8-byte one (MI355X_MICROARCH.md: dwordx2 2.7x, dword ~6x the dwordx4 time).
+typedef unsigned int kss_u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void st_ag16(uint32_t* p, kss_u32x4 v) {
+  asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+}
 template <bool DEF>
 __global__ __launch_bounds__(256) void k_static(const DevJob* __restrict__ jobs, kss_profile prof_arg, int k0, int k1,
                                                 int n_lo, int n_hi) {
   const DevJob& job = jobs[blockIdx.z];
   const int N = job.c.N;
-  const int n = n_lo + 2 * (int)(blockIdx.x * 256 + threadIdx.x);  // rows [n_lo, min(n_hi, N)): a split grid's own rows
+  const int n = n_lo + 4 * (int)(blockIdx.x * 256 + threadIdx.x);  // rows [n_lo, min(n_hi, N)): a split grid's own rows
   const int kend = min(k1, job.n_pods);
   const int kb = k0 + (int)blockIdx.y * STATIC_PODS;
   const int lim = min(N, n_hi);
   if (kb >= kend || n >= lim) return;
-  const bool two = n + 1 < lim;
-  // 8-byte stores only where the pair is 8-byte aligned: the row offset (N, n_lo even) and the
-  // job's stat buffer itself (sweeps align each scenario's to 16 bytes; checked regardless)
-  const bool wide = two && ((N | n_lo) & 1) == 0 && (reinterpret_cast<uintptr_t>(job.stat) & 7) == 0;
+  const int cnt = min(4, lim - n);
+  uint32_t* stat = job.stat;
+  const uintptr_t sa = reinterpret_cast<uintptr_t>(stat);
+  const bool quad = cnt == 4 && ((N | n_lo) & 3) == 0 && (sa & 15) == 0;
+  const bool pair = ((N | n_lo) & 1) == 0 && (sa & 7) == 0;  // 8-byte pairs at even offsets
   const DevCluster c = job.c;
   const DevPods P = job.P;
-  uint32_t* stat = job.stat;
   const kss_profile prof = DEF ? default_profile_c() : prof_arg;
-  const int n1 = two ? n + 1 : n;
-  const uint32_t f0 = c.node_flags[n], f1 = c.node_flags[n1];
-  const uint64_t th0 = c.taint_hard[n], ts0 = c.taint_soft[n], th1 = c.taint_hard[n1], ts1 = c.taint_soft[n1];
+  uint32_t f[4];
+  uint64_t th[4], ts[4];
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    const int ni = n + min(i, cnt - 1);
+    f[i] = c.node_flags[ni];
+    th[i] = c.taint_hard[ni];
+    ts[i] = c.taint_soft[ni];
+  }
   for (int t = 0; t < STATIC_PODS; t++) {
     const int k = kb + t;
     if (k >= kend) break;
     const kss_pod& pod = P.pods[k];
-    const uint32_t w0 = static_word(c, P, pod, prof, n, f0, th0, ts0);
-    const uint32_t w1 = static_word(c, P, pod, prof, n1, f1, th1, ts1);
+    uint32_t w[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) w[i] = static_word(c, P, pod, prof, n + min(i, cnt - 1), f[i], th[i], ts[i]);
     uint32_t* dst = &stat[(size_t)(k - k0) * N + n];
-    if (wide) {
-      st_ag(reinterpret_cast<unsigned long long*>(dst), (unsigned long long)w0 | ((unsigned long long)w1 << 32));
+    if (quad) {
+      st_ag16(dst, kss_u32x4{w[0], w[1], w[2], w[3]});
+    } else if (pair) {
+      if (cnt >= 2) st_ag(reinterpret_cast<unsigned long long*>(dst), (unsigned long long)w[0] | ((unsigned long long)w[1] << 32));
+      else st_ag(dst, w[0]);
+      if (cnt == 4) st_ag(reinterpret_cast<unsigned long long*>(dst + 2), (unsigned long long)w[2] | ((unsigned long long)w[3] << 32));
+      else if (cnt == 3) st_ag(dst + 2, w[2]);
     } else {
-      st_ag(dst, w0);
-      if (two) st_ag(dst + 1, w1);
+#pragma unroll
+      for (int i = 0; i < 4; i++)
+        if (i < cnt) st_ag(dst + i, w[i]);
     }
   }
   // every store above is agent-scope (sc1, written through): the kernel boundary orders them
@@ -566,6 +592,9 @@ struct kss_ctx {
 #endif
   int n_cu = 0;
   int force_w = 0;            // KSS_SHARDS env override (tuning / tests)
+  bool xcd_mode = true;       // KSS_XCD=0: no XCD-local k_simple grids
+  int xcd_w = 0;              // KSS_XCD_SHARDS: shards of an XCD-local grid (tuning; default: CUs per XCD)
+  int last_xcd[2] = {0, 0};   // the last run: XCD-local grid used, chunks that fell back to an unrestricted grid
   int nodes_per_shard = 128;  // KSS_NODES_PER_SHARD (C2 sweep: 128 > 256 > 512 nodes per shard)
   int pref_threads = 256;     // KSS_THREADS
   PlanNeeds staged_need;
@@ -1470,6 +1499,8 @@ kss_ctx* kss_create(const kss_config* cfg, const kss_profile* prof) {
   if (hipGetDeviceProperties(&dp, cfg->device) == hipSuccess) ctx->n_cu = dp.multiProcessorCount;
   if (ctx->n_cu <= 0) ctx->n_cu = 1;
   if (const char* e = getenv("KSS_SHARDS")) ctx->force_w = std::max(0, atoi(e));
+  if (const char* e = getenv("KSS_XCD")) ctx->xcd_mode = atoi(e) != 0;
+  if (const char* e = getenv("KSS_XCD_SHARDS")) ctx->xcd_w = std::max(0, std::min(64, atoi(e)));
   ctx->stamps_file = getenv("KSS_STAMPS_FILE");
   ctx->no_simple = getenv("KSS_NO_SIMPLE") != nullptr;
   ctx->no_spread = getenv("KSS_NO_SPREAD") != nullptr;
@@ -2287,10 +2318,12 @@ static void static_rows(const Geometry& g, const XPeers& X, int max_nodes, int& 
   n_hi = std::min(max_nodes, (X.w_off + X.wl) * per);
 }
 
+// xcd: one job on an XCD-local grid (xcd_slot); a chunk whose launch reports the placement
+// failure (err = 3, no state touched) is synchronised on and run again unrestricted.
 static int launch_simple(hipStream_t st, const Geometry& g, int n_jobs, const DevJob* jobs, const kss_profile& prof,
                          int n_pods_max, int max_nodes, int chunk, unsigned long long* gran, size_t gran_bytes, int* err,
                          unsigned long long* stamps = nullptr, hipEvent_t* ev = nullptr, const SplitRun* split = nullptr,
-                         int nsc = 0) {
+                         int nsc = 0, bool xcd = false, int* xcd_fallbacks = nullptr) {
   int cap = simple_cap(g);
   const size_t shmem = simple_lds_bytes(cap, nsc);
   const bool def = same_profile(prof, default_profile_c());
@@ -2298,13 +2331,15 @@ static int launch_simple(hipStream_t st, const Geometry& g, int n_jobs, const De
   HIP_TRY(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shmem));
   XPeers X = split ? split->X : XPeers{};
   const bool sp_grid = X.n > 1;
+  xcd = xcd && !sp_grid && n_jobs == 1 && gran;
   const dim3 grid((unsigned)(n_jobs * (sp_grid ? X.wl : g.W))), block((unsigned)g.threads);
+  const dim3 xgrid((unsigned)(XCD_GRID_MULT * g.W));
   kss_profile pr = prof;
   int W = g.W, n_lo = 0, n_hi = 0;
   static_rows(g, X, max_nodes, n_lo, n_hi);
   for (int k0 = 0; k0 < n_pods_max; k0 += chunk) {
     int k1 = std::min(n_pods_max, k0 + chunk);
-    const dim3 sgrid((unsigned)(std::max(n_hi - n_lo, 1) + 511) / 512, (unsigned)((k1 - k0 + STATIC_PODS - 1) / STATIC_PODS),
+    const dim3 sgrid((unsigned)(std::max(n_hi - n_lo, 1) + 1023) / 1024, (unsigned)((k1 - k0 + STATIC_PODS - 1) / STATIC_PODS),
                      (unsigned)n_jobs);
     if (def)
       hipLaunchKernelGGL(k_static<true>, sgrid, dim3(256), 0, st, jobs, pr, k0, k1, n_lo, n_hi);
@@ -2324,7 +2359,21 @@ static int launch_simple(hipStream_t st, const Geometry& g, int n_jobs, const De
                     (void*)&gc,   (void*)&err, (void*)&sp, (void*)&X,   (void*)&epoch0};
     const int ci = k0 / chunk;
     if (ev) HIP_TRY(hipEventRecord(ev[2 * ci], st));
-    if (g.W > 1) {
+    if (xcd) {
+      X.xcd_local = 1;
+      if (int rc = launch_resident(fn, xgrid, block, args, shmem, st)) return rc;
+      int e = 0;
+      HIP_TRY(hipMemcpyAsync(&e, err, sizeof(int), hipMemcpyDeviceToHost, st));
+      HIP_TRY(hipStreamSynchronize(st));
+      X.xcd_local = 0;
+      if (e == 3) {  // XCD 0 did not get W workgroups: nothing ran; again, unrestricted
+        if (xcd_fallbacks) ++*xcd_fallbacks;
+        xcd = false;
+        HIP_TRY(dev_zero(err, 4, st));
+        HIP_TRY(dev_zero(gran, gran_bytes, st));
+        if (int rc = launch_resident(fn, grid, block, args, shmem, st)) return rc;
+      }
+    } else if (g.W > 1) {
       if (int rc = launch_resident(fn, grid, block, args, shmem, st)) return rc;
     } else {
       HIP_TRY(hipLaunchKernel(fn, grid, block, args, shmem, st));
@@ -2401,7 +2450,7 @@ static int launch_spread(hipStream_t st, const Geometry& g, const GpodNeeds& q, 
   static_rows(g, X, max_nodes, n_lo, n_hi);
   for (int k0 = 0; k0 < n_pods; k0 += chunk) {
     int k1 = std::min(n_pods, k0 + chunk);
-    const dim3 sgrid((unsigned)(std::max(n_hi - n_lo, 1) + 511) / 512, (unsigned)((k1 - k0 + STATIC_PODS - 1) / STATIC_PODS), 1u);
+    const dim3 sgrid((unsigned)(std::max(n_hi - n_lo, 1) + 1023) / 1024, (unsigned)((k1 - k0 + STATIC_PODS - 1) / STATIC_PODS), 1u);
     if (def)
       hipLaunchKernelGGL(k_static<true>, sgrid, dim3(256), 0, st, jobs, pr, k0, k1, n_lo, n_hi);
     else
@@ -2442,10 +2491,14 @@ static int launch_spread(hipStream_t st, const Geometry& g, const GpodNeeds& q, 
     if (ev) HIP_TRY(hipEventRecord(ev[2 * ci + 1], st));
   }
   if (ck && ck_seq && n_pods > 0) {  // the last chunk's write-back, checked (nothing repairs it)
+    const HandoffLayout hl(g.W, n_res, max_nodes, nsc);
     HandoffCheck hc{};
     hc.sum = ck;
     hc.expect = *ck_seq;
     hc.retries = err + 1;
+    hc.xcc = (int*)(ck + hl.o_xcc);
+    hc.diag = (long long*)(ck + hl.o_diag);
+    hc.shadow = (long long*)(ck + hl.o_shadow);
     hipLaunchKernelGGL(k_handoff_final, grid, dim3(256), 0, st, jobs, W, sp_grid ? X.w_off : 0, n_res, hc, err);
     HIP_TRY(hipGetLastError());
   }
@@ -2531,6 +2584,14 @@ static int run_single_impl(kss_ctx* ctx, const PlanNeeds& need, const DevPods& d
                          scalar_fast_ok(ctx->prof, ctx->dc.n_scalar) && ctx->small_values && f64_exact(ctx->f64_cluster, ctx->f64_pods, n) &&
                          !ctx->no_simple && !(flags & KSS_SCHED_GENERAL_KERNEL);
   if (simple_ok && ctx->force_w <= 0 && !split) W = std::min(W, 64 * SX_CHUNKS);
+  // XCD-local k_simple (launch_simple xcd, xcd_slot): a cluster whose shards fit one XCD's CUs
+  // at one node per lane runs every shard on XCD 0, so the per-pod exchange stays in that
+  // XCD's L2 (KSS_XCD=0: off)
+  const int xcd_cus = ctx->n_cu / XCD_GRID_MULT;
+  const bool xcd_try = simple_ok && !split && ctx->force_w <= 0 && ctx->xcd_mode && ctx->n_cu % XCD_GRID_MULT == 0 &&
+                       !(flags & (KSS_SCHED_FORCE_SINGLE_WG | KSS_SCHED_FORCE_MULTI_WG)) &&
+                       N <= (size_t)(ctx->xcd_w > 0 ? ctx->xcd_w : xcd_cus) * PW_LANES * (KSS_MAX_THREADS / 64);
+  if (xcd_try) W = std::min(W, ctx->xcd_w > 0 ? ctx->xcd_w : xcd_cus);
   // a batch with programs on k_spread: 32-bit counts and scores (spread_bounds_ok)
   const double count_total = ctx->count_bound + (commit ? (double)n * (1.0 + ctx->staged_max_own) : 0.0);
   const double cell_total = ctx->cell_bound + (commit ? (double)n * ctx->gneed.max_mult : 0.0);
@@ -2707,9 +2768,12 @@ static int run_single_impl(kss_ctx* ctx, const PlanNeeds& need, const DevPods& d
     HIP_TRY(hipEventCreate(&e));
     ctx->loop_ev.push_back(e);
   }
+  ctx->last_xcd[0] = simple && xcd_try && g.W > 1 ? 1 : 0;
+  ctx->last_xcd[1] = 0;
   if (simple)
     rc = launch_simple(ctx->stream, g, 1, jd, ctx->prof, n, (int)N, chunk, gran, gb,
-                       errp, stamps, ctx->loop_ev.data(), split ? &srun : nullptr, ctx->dc.n_scalar);
+                       errp, stamps, ctx->loop_ev.data(), split ? &srun : nullptr, ctx->dc.n_scalar, ctx->last_xcd[0] != 0,
+                       &ctx->last_xcd[1]);
   else if (spread)
   {
     const HandoffLayout hl(g.W, n_res, (int)N, ctx->dc.n_scalar);
@@ -3657,7 +3721,7 @@ int kss_last_handoff_diag(kss_ctx* ctx, int32_t* recovered, int64_t* entries, in
   std::lock_guard<std::mutex> lk(ctx->mu);
   *recovered = ctx->last_handoff_recovered;
   *n_entries = 0;
-  if (!ctx->last_kernel_spread || !ctx->ck_buf.p || !ctx->last_handoff_retries) return 0;
+  if (!ctx->last_kernel_spread || !ctx->ck_buf.p || !(ctx->last_handoff_retries || ctx->last_handoff_final)) return 0;
   HIP_TRY(hipSetDevice(ctx->cfg.device));
   std::vector<long long> h(1 + (size_t)HANDOFF_DIAG * HANDOFF_DIAG_W);
   HIP_TRY(hipMemcpy(h.data(), (unsigned long long*)ctx->ck_buf.p + ctx->ck_diag_off, h.size() * 8, hipMemcpyDeviceToHost));
@@ -3677,6 +3741,13 @@ int kss_last_loop_timing(kss_ctx* ctx, double* loop_ms) {
 int kss_last_geometry(kss_ctx* ctx, int32_t* out3) {
   if (!ctx || !out3) return fail(KSS_E_INVAL, "bad arguments");
   for (int i = 0; i < 3; i++) out3[i] = ctx->last_geom[i];
+  return 0;
+}
+
+int kss_last_xcd_local(kss_ctx* ctx, int32_t* out2) {
+  if (!ctx || !out2) return fail(KSS_E_INVAL, "bad arguments");
+  out2[0] = ctx->last_xcd[0];
+  out2[1] = ctx->last_xcd[1];
   return 0;
 }
 

@@ -83,17 +83,58 @@ __device__ __forceinline__ void handoff_acquire() {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
+__device__ __forceinline__ int xcc_id() {
+  int x;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
+  return x & 0xF;
+}
+
 // Publish one granule at offset `off` of the exchange buffer (the local inbox `gran`);
-// address-space-1 stores (a flat store would also count in lgkmcnt).
+// address-space-1 stores (a flat store would also count in lgkmcnt).  An XCD-local grid
+// (X.xcd_local: every shard runs on the same XCD, xcd_slot) publishes with a plain store (no
+// cache-policy bits): the line stays in that XCD's L2, which every shard's agent-scope
+// (L1-bypassing) poll reads -- a third of the latency of a write-through granule
+// (tools/xcd_exchange_probe.hip, 32-way rounds: 0.41 against 1.23 us).
 __device__ __forceinline__ void xpub(const XPeers& X, unsigned long long* gran, size_t off, unsigned long long v) {
   if (X.n <= 1) {
-    __hip_atomic_store(gp(gran) + off, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (X.xcd_local) asm volatile("global_store_dwordx2 %0, %1, off" ::"v"(gran + off), "v"(v) : "memory");
+    else __hip_atomic_store(gp(gran) + off, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return;
   }
   for (int p = 0; p < X.n; p++) __hip_atomic_store(gp(X.inbox[p]) + off, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 constexpr int SX_VALS = 8;    // granules per shard per exchange: key lo/hi, H0 (nf, tt, na), H1 (nf, tt, na)
+
+// An XCD-local k_simple grid (one cluster, W <= CUs per XCD): the launch has XCD_GRID_MULT x W
+// workgroups; the first W that run on XCD 0 become shards 0 .. W-1 in arrival order and every
+// other workgroup leaves at once.  Correctness never rests on where the hardware places a
+// workgroup: a shard is one that READ its XCC id as 0, so all shards share XCD 0's L2.  When
+// XCD 0 gets fewer than W of them (counted once every workgroup of the grid has started), the
+// launch fails with err = 3 before touching any state and the host runs it again unrestricted.
+// ctr: two zeroed words behind the launch's granules, [0] shards taken, [1] workgroups started.
+// Returns the shard, -1 (leave), -2 (placement failed).
+constexpr int XCD_GRID_MULT = 8;
+__device__ __forceinline__ int xcd_slot(int* ctr, int W, int grid, int* err) {
+  int slot = -1;
+  if (xcc_id() == 0) {
+    slot = atomicAdd(&ctr[0], 1);
+    if (slot >= W) slot = -1;
+  }
+  atomicAdd(&ctr[1], 1);  // after the slot: every workgroup started => every XCD-0 slot taken
+  if (slot < 0) return -1;
+  long long t0 = 0;
+  for (unsigned spins = 0;; ++spins) {
+    if (__hip_atomic_load(&ctr[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= W) return slot;
+    if (__hip_atomic_load(&ctr[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= grid &&
+        __hip_atomic_load(&ctr[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < W)
+      break;
+    if (spin_expired(spins, t0)) break;
+    __builtin_amdgcn_s_sleep(1);
+  }
+  err_raise(err, 3);
+  return -2;
+}
 constexpr int SX_CHUNKS = 2;  // shards swept 64 at a time: W <= 128
 constexpr int STATIC_PODS = 8;  // pods per k_static lane
 constexpr int PF_MAX = 8;       // static words per prefetch lane (host-checked: simple_fits)

@@ -649,11 +649,6 @@ struct HandoffCheck {
   int* xcc;                   // [W]: the XCC that ran each shard's last epilogue
   long long* diag;            // [1 + HANDOFF_DIAG * HANDOFF_DIAG_W]: count, then the differing words
 };
-__device__ __forceinline__ int xcc_id() {
-  int x;
-  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
-  return x & 0xF;
-}
 __device__ __forceinline__ unsigned long long handoff_mix(unsigned long long v, size_t pos) {
   return (v + 0x9E3779B97F4A7C15ull) * (2ull * (unsigned long long)pos + 1ull);
 }
@@ -702,6 +697,25 @@ __device__ __forceinline__ bool handoff_verify(const HandoffCheck& hc, int w, un
   }
   return ok;
 }
+// One differing word of the hand-off (first disagreement of a launch): array a (0-2 requested,
+// 3-4 nonzero, 5 pod count, 6 + r resident count row r), node n, and the views of it.
+__device__ __forceinline__ void handoff_note(const HandoffCheck& hc, int w, int a, int n, long long plain,
+                                             long long atomic_v, long long nt, long long shadow, const void* addr) {
+  const long long e = __hip_atomic_fetch_add(hc.diag, 1ll, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (e >= HANDOFF_DIAG) return;
+  long long* d = hc.diag + 1 + e * HANDOFF_DIAG_W;
+  st_ag(&d[0], (long long)w | ((long long)xcc_id() << 32) | ((long long)ld_ag(&hc.xcc[w]) << 40));
+  st_ag(&d[1], (long long)a);
+  st_ag(&d[2], (long long)n);
+  st_ag(&d[3], plain);
+  st_ag(&d[4], atomic_v);
+  st_ag(&d[5], nt);
+  st_ag(&d[6], shadow);
+  st_ag(&d[7], (long long)hc.expect);
+  st_ag(&d[8], (long long)(uintptr_t)addr);
+  st_ag(&d[9], (long long)(unsigned)wall_clock64());
+}
+
 // The last chunk's write-back, checked after the loop launch has ended (a next chunk's
 // prologue checks every other hand-off): shard w's node state in HBM summed as the prologue
 // sums it, against the sum and tag its epilogue stored.  A disagreement fails the run (err = 2)
@@ -711,6 +725,9 @@ __device__ __forceinline__ void handoff_final_check(const DevCluster& c, const i
   const size_t N = (size_t)c.N;
   const int per = (c.N + W - 1) / W;
   const int lo = min(c.N, w * per), hi = min(c.N, lo + per), own = hi - lo, nsc = c.n_scalar;
+  // a launch that failed (an exchange timeout) left without its epilogue: nothing to check, and
+  // the run already reports why it failed
+  if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return;
   handoff_acquire();
   unsigned long long h = 0;
   for (int s = threadIdx.x; s < own; s += blockDim.x) {
@@ -732,30 +749,47 @@ __device__ __forceinline__ void handoff_final_check(const DevCluster& c, const i
   const unsigned long long t = handoff_sum(h, scratch);
   if (threadIdx.x == 0) {
     const bool ok = ld_ag(&hc.sum[2 * (size_t)w + 1]) == hc.expect && ld_ag(&hc.sum[2 * (size_t)w]) == t;
+    scratch[0] = ok ? 1 : 0;
     if (!ok) {
       __hip_atomic_fetch_add(hc.retries + 2, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       err_raise(err, 2);
+      if (hc.diag)  // array -1: {stored tag, stored sum, the sum of the state, the expected tag}
+        handoff_note(hc, w, -1, lo, (long long)ld_ag(&hc.sum[2 * (size_t)w + 1]), (long long)ld_ag(&hc.sum[2 * (size_t)w]),
+                     (long long)t, (long long)hc.expect, &hc.sum[2 * (size_t)w]);
     }
   }
-}
-
-// One differing word of the hand-off (first disagreement of a launch): array a (0-2 requested,
-// 3-4 nonzero, 5 pod count, 6 + r resident count row r), node n, and the views of it.
-__device__ __forceinline__ void handoff_note(const HandoffCheck& hc, int w, int a, int n, long long plain,
-                                             long long atomic_v, long long nt, long long shadow, const void* addr) {
-  const long long e = __hip_atomic_fetch_add(hc.diag, 1ll, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if (e >= HANDOFF_DIAG) return;
-  long long* d = hc.diag + 1 + e * HANDOFF_DIAG_W;
-  st_ag(&d[0], (long long)w | ((long long)xcc_id() << 32) | ((long long)ld_ag(&hc.xcc[w]) << 40));
-  st_ag(&d[1], (long long)a);
-  st_ag(&d[2], (long long)n);
-  st_ag(&d[3], plain);
-  st_ag(&d[4], atomic_v);
-  st_ag(&d[5], nt);
-  st_ag(&d[6], shadow);
-  st_ag(&d[7], (long long)hc.expect);
-  st_ag(&d[8], (long long)(uintptr_t)addr);
-  st_ag(&d[9], (long long)(unsigned)wall_clock64());
+  __syncthreads();
+  if (scratch[0] || !hc.shadow || !hc.diag) return;
+  // the words where the state differs from the shadow the epilogue stored beside it
+  // (kss_last_handoff_diag), as the prologue's first disagreement lists them
+  for (int s = threadIdx.x; s < own; s += blockDim.x) {
+    const int n = lo + s;
+    for (int a = 0; a < 6; a++) {
+      const long long sv = ld_ag(&hc.shadow[(size_t)a * N + n]);
+      if (a < 5) {
+        int64_t* p = a < 3 ? &c.requested[(size_t)a * N + n] : &c.nonzero[(size_t)(a - 3) * N + n];
+        const long long pv = ld_ag(p);
+        if (pv != sv)
+          handoff_note(hc, w, a, n, pv, __hip_atomic_fetch_add(p, (int64_t)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                       __builtin_nontemporal_load(p), sv, p);
+      } else {
+        int32_t* p = &c.pod_count[n];
+        const long long pv = ld_ag(p);
+        if (pv != sv)
+          handoff_note(hc, w, a, n, pv, __hip_atomic_fetch_add(p, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                       __builtin_nontemporal_load(p), sv, p);
+      }
+    }
+  }
+  for (int i = threadIdx.x; i < n_res * own; i += blockDim.x) {
+    const int r = i / own, s = i - r * own, row = res_rows[r];
+    int32_t* p = row < c.n_classes ? &c.class_count[(size_t)row * N + lo + s]
+                                   : &c.term_count[(size_t)(row - c.n_classes) * N + lo + s];
+    const long long sv = ld_ag(&hc.shadow[(6 + (size_t)r) * N + lo + s]), pv = ld_ag(p);
+    if (pv != sv)
+      handoff_note(hc, w, 6 + r, lo + s, pv, __hip_atomic_fetch_add(p, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                   __builtin_nontemporal_load(p), sv, p);
+  }
 }
 
 // The statistics of node slot s for pod q, accumulated into bins (SUM) / bins + total_bins

@@ -73,6 +73,7 @@ SIGNATURES = [
     ("kss_buffer_map", C.c_int, [C.c_void_p, P(C.c_uint64), P(C.c_uint64), C.c_int32, P(C.c_int32)]),
     ("kss_last_geometry", C.c_int, [C.c_void_p, P(C.c_int32)]),
     ("kss_last_kernel", C.c_int, [C.c_void_p]),
+    ("kss_last_xcd_local", C.c_int, [C.c_void_p, P(C.c_int32)]),
     ("kss_device_go_log", C.c_int, [C.c_int32, C.c_void_p, C.c_void_p, C.c_int32]),
     ("kss_plan_podset", C.c_int, [C.POINTER(abi.Cluster), C.POINTER(abi.PodSet), C.c_void_p]),
     ("kss_plan_podset_ex", C.c_int, [C.POINTER(abi.Cluster), C.POINTER(abi.PodSet), C.POINTER(abi.Profile),
@@ -574,6 +575,12 @@ class Context:
         out = (C.c_int32 * 3)()
         check(lib().kss_last_geometry(self.h, out))
         return {"shards": out[0], "threads": out[1], "nodes_per_lane": out[2]}
+
+    def last_xcd_local(self) -> Dict[str, int]:
+        """{used, fallbacks} of the last run's XCD-local k_simple grid (kss_last_xcd_local)."""
+        out = (C.c_int32 * 2)()
+        check(lib().kss_last_xcd_local(self.h, out))
+        return {"used": out[0], "fallbacks": out[1]}
 
     def last_kernel(self) -> str:
         k = lib().kss_last_kernel(self.h)

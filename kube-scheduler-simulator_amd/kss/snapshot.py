@@ -12,7 +12,7 @@
   (plugins.go mergePluginSet, :227-283), weights with 0 -> 1 (getScorePluginWeight,
   :288-303), NodeResourcesFitArgs.scoringStrategy, NodeResourcesBalancedAllocationArgs,
   InterPodAffinityArgs.hardPodAffinityWeight, PodTopologySpreadArgs.defaultingType and
-  percentageOfNodesToScore.
+  percentageOfNodesToScore (unset: 0, the adaptive default).
 * ``sync_deltas``: the NodeInfo-generation delta sync of an updated snapshot onto a loaded
   context (kss_apply_node_delta / kss_apply_count_delta / kss_apply_port_delta) instead of a
   full reload -- the rows whose mutable columns changed.
@@ -193,9 +193,13 @@ def profile_from_config(cfg: Optional[dict], scalars: Sequence[str] = ()) -> abi
     if len(profiles) > 1:
         raise Unsupported("one scheduler profile only (plugins.go getScorePluginWeight reads profiles[0])")
     p0 = profiles[0]
-    pct = cfg.get("percentageOfNodesToScore", p0.get("percentageOfNodesToScore"))
-    if pct not in (None, 0, 100):
-        raise Unsupported("percentageOfNodesToScore must be 100 (or unset) on the device path")
+    # v1.26 has the global field only (profiles gained their own in v1.27); unset means the v1
+    # default 0, the adaptive numFeasibleNodesToFind -- what the simulator's built-in scheduler
+    # always runs with (it resets the configuration to its defaults, scheduler.go:258-275)
+    pct = cfg.get("percentageOfNodesToScore")
+    pct = 0 if pct is None else int(pct)
+    if not 0 <= pct <= 100:
+        raise Unsupported("percentageOfNodesToScore must be between 0 and 100 (ValidateKubeSchedulerConfiguration)")
     plugins = p0.get("plugins") or {}
     multi = merge_plugin_set(DEFAULT_MULTIPOINT, plugins.get("multiPoint"))
     names = [n for n, _ in multi]
@@ -245,7 +249,7 @@ def profile_from_config(cfg: Optional[dict], scalars: Sequence[str] = ()) -> abi
     if dt == "List" and pts.get("defaultConstraints"):
         raise Unsupported("PodTopologySpread List defaulting with default constraints")
     prof.system_defaulted = 1 if dt == "System" else 0
-    prof.pct_nodes_to_score = 100
+    prof.pct_nodes_to_score = pct
     return prof
 
 

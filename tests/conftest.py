@@ -3,6 +3,14 @@ import sys
 
 import pytest
 
+# Hardware queues per process (HIP's default is 4, read when the HIP runtime starts).  The
+# in-process split-grid tests run up to 4 contexts whose grids must all be resident at once,
+# each on its own stream; torch's stream (opened first, below) takes a queue too, and two
+# streams sharing a queue run their kernels one after the other -- a split grid's parts would
+# then wait on each other until the exchange bound.  8 queues keep every part on its own.
+if int(os.environ.get("GPU_MAX_HW_QUEUES") or 4) < 8:  # the GPU box exports HIP's default, 4
+    os.environ["GPU_MAX_HW_QUEUES"] = "8"
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(ROOT, "kube-scheduler-simulator_amd")
 for p in (ROOT, PKG, os.path.join(ROOT, "oracle"), os.path.join(ROOT, "tests")):

@@ -29,6 +29,8 @@ def _oracle(s, n_pods):
     (4, 20000, 400, 2, 32, "k_spread"),
     (3, 3000, 300, 2, 12, "k_spread"),
     (4, 100000, 200, 2, 128, "k_spread"),
+    (4, 100000, 300, 4, 64, "k_spread"),   # BASELINE configs[3] split 4 ways (4 contexts: GPU_MAX_HW_QUEUES = 4)
+    (2, 100000, 300, 4, 32, "k_simple"),
 ])
 def test_in_process_parts_match_oracle(config, n_nodes, n_pods, n_parts, wl, kernel):
     s = native.Synth(config, SEED_BASE + config, n_nodes, n_pods)
@@ -251,15 +253,19 @@ def _identity(r):
     return r
 
 
-@pytest.mark.parametrize("two_gpus", [False, pytest.param(True, marks=pytest.mark.skipif(
-    _n_devices() < 2, reason="needs 2 GPUs"))])
-def test_two_processes_through_ipc_handles(two_gpus):
+@pytest.mark.parametrize("world,config,n_nodes,n_pods,wl,two_gpus", [
+    (2, 4, 20000, 300, 32, False),
+    pytest.param(2, 4, 20000, 300, 32, True, marks=pytest.mark.skipif(_n_devices() < 2, reason="needs 2 GPUs")),
+    # the 8-GPU node's shape, rehearsed on one GPU: 8 processes, 32 shards each (C4: 100k nodes),
+    # every granule published into 8 inboxes
+    (8, 4, 100000, 200, 32, False),
+])
+def test_processes_through_ipc_handles(world, config, n_nodes, n_pods, wl, two_gpus):
     """One part per process (the deployment shape: one process per GPU), inboxes mapped
-    through hipIpcOpenMemHandle, the handles exchanged over gloo; both processes' grids on
+    through hipIpcOpenMemHandle, the handles exchanged over gloo; every process's grid on
     the box's one GPU at once, or (two_gpus) rank r on GPU r, peer stores over xGMI."""
     import multiprocessing as mp
     import socket
-    config, n_nodes, n_pods, wl = 4, 20000, 300, 32
     s = native.Synth(config, SEED_BASE + config, n_nodes, n_pods)
     ch_o, _, st = _oracle(s, n_pods)
     with socket.socket() as so:
@@ -267,8 +273,8 @@ def test_two_processes_through_ipc_handles(two_gpus):
         port = so.getsockname()[1]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    ps = [ctx.Process(target=_rank_main, args=(r, 2, port, config, n_nodes, n_pods, wl, q,
-                                               _identity if two_gpus else None)) for r in range(2)]
+    ps = [ctx.Process(target=_rank_main, args=(r, world, port, config, n_nodes, n_pods, wl, q,
+                                               _identity if two_gpus else None)) for r in range(world)]
     for p in ps:
         p.start()
     got = [q.get(timeout=240) for _ in ps]

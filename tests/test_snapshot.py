@@ -41,8 +41,9 @@ def test_priority_class_resolution():
 
 def test_default_config_is_the_default_profile():
     assert _same_profile(snapshot.profile_from_config(None), abi.default_profile())
-    assert _same_profile(snapshot.profile_from_config({"profiles": [{"schedulerName": "default-scheduler"}]}),
-                         abi.default_profile())
+    d = abi.default_profile()
+    d.pct_nodes_to_score = 0  # a configuration without the field: the v1 default, adaptive
+    assert _same_profile(snapshot.profile_from_config({"profiles": [{"schedulerName": "default-scheduler"}]}), d)
 
 
 def test_config_weights_disables_and_args():
@@ -93,8 +94,11 @@ def test_config_star_disable_and_refusals():
     assert p.filter_enabled == (1 << abi.KSS_F_NODE_RESOURCES_FIT) | (1 << abi.KSS_F_TAINT_TOLERATION)
     assert p.score_enabled == (1 << abi.KSS_S_NODE_RESOURCES_FIT) | (1 << abi.KSS_S_TAINT_TOLERATION)
     assert p.weight[abi.KSS_S_TAINT_TOLERATION] == 7 and p.weight[abi.KSS_S_NODE_RESOURCES_FIT] == 1
+    assert snapshot.profile_from_config({"percentageOfNodesToScore": 50, "profiles": [{}]}).pct_nodes_to_score == 50
+    assert snapshot.profile_from_config({"profiles": [{}]}).pct_nodes_to_score == 0  # the v1 default: adaptive
+    assert snapshot.profile_from_config(None).pct_nodes_to_score == 100  # no configuration: the north_star profile
     with pytest.raises(Unsupported):
-        snapshot.profile_from_config({"percentageOfNodesToScore": 50, "profiles": [{}]})
+        snapshot.profile_from_config({"percentageOfNodesToScore": 101, "profiles": [{}]})
     with pytest.raises(Unsupported):
         snapshot.profile_from_config({"profiles": [{"pluginConfig": [{"name": "NodeResourcesFit", "args": {
             "scoringStrategy": {"type": "RequestedToCapacityRatio"}}}]}]})
