@@ -255,10 +255,17 @@ __global__ __launch_bounds__(KSS_MAX_THREADS) void k_spread(const DevJob* __rest
                                                             unsigned epoch0, HandoffCheck hc) {
   extern __shared__ __attribute__((aligned(16))) long long smem[];
   const int Wl = X.n > 1 ? X.wl : W;
-  const int ji = blockIdx.x / Wl, w = X.w_off + (int)(blockIdx.x % Wl);
+  SpreadHdr& H = *reinterpret_cast<SpreadHdr*>(smem);
+  int xs = 0;
+  if (X.xcd_local) {  // one cluster, every shard on XCD 0 (xcd_slot); the other workgroups leave
+    if (threadIdx.x == 0) H.pad[0] = xcd_slot(reinterpret_cast<int*>(gran + 2 * (size_t)W * gs), W, (int)gridDim.x, err);
+    __syncthreads();
+    xs = H.pad[0];
+    if (xs < 0) return;
+  }
+  const int ji = X.xcd_local ? 0 : blockIdx.x / Wl, w = X.xcd_local ? xs : X.w_off + (int)(blockIdx.x % Wl);
   const DevJob job = jobs[ji];
   constexpr kss_profile def_prof = default_profile_c();
-  SpreadHdr& H = *reinterpret_cast<SpreadHdr*>(smem);
 #ifdef KSS_LDS_POISON  // experiment builds: the shard's LDS image filled with a pattern first
   {
     const size_t words = spread_lds_bytes(cap, bins_cap, job.c.n_keys, n_res, gq, job.c.n_scalar) / 4;
@@ -2427,7 +2434,7 @@ static int launch_spread(hipStream_t st, const Geometry& g, const GpodNeeds& q, 
                          const DevJob* jobs, const kss_profile& prof, int n_pods, int max_nodes, int chunk,
                          unsigned long long* gran, size_t gran_bytes, int* err, unsigned long long* stamps = nullptr,
                          hipEvent_t* ev = nullptr, const SplitRun* split = nullptr, unsigned long long* ck = nullptr,
-                         unsigned long long* ck_seq = nullptr, int nsc = 0) {
+                         unsigned long long* ck_seq = nullptr, int nsc = 0, bool xcd = false, int* xcd_fallbacks = nullptr) {
   int cap = spread_cap(g, (size_t)max_nodes), bins_cap = q.bins_cap, nr = n_res, gq = q.gq, gs = q.gs();
   size_t shmem = spread_lds(g, q, n_keys, n_res, (size_t)max_nodes, nsc);
   // diagnostic stamps in LDS: as many pods (<= G_NSTAMP, >= 8) as fit beside the shard state
@@ -2444,7 +2451,9 @@ static int launch_spread(hipStream_t st, const Geometry& g, const GpodNeeds& q, 
   HIP_TRY(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shmem));
   XPeers X = split ? split->X : XPeers{};
   const bool sp_grid = X.n > 1;
+  xcd = xcd && !sp_grid && gran && g.W > 1;
   const dim3 grid((unsigned)(sp_grid ? X.wl : g.W)), block((unsigned)g.threads);
+  const dim3 xgrid((unsigned)(XCD_GRID_MULT * g.W));
   kss_profile pr = prof;
   int W = g.W, n_lo = 0, n_hi = 0;
   static_rows(g, X, max_nodes, n_lo, n_hi);
@@ -2483,7 +2492,21 @@ static int launch_spread(hipStream_t st, const Geometry& g, const GpodNeeds& q, 
                     (void*)&hc};
     const int ci = k0 / chunk;
     if (ev) HIP_TRY(hipEventRecord(ev[2 * ci], st));
-    if (g.W > 1) {
+    if (xcd) {  // as launch_simple: an XCD-local grid, run again unrestricted when placement failed
+      X.xcd_local = 1;
+      if (int rc = launch_resident(fn, xgrid, block, args, shmem, st)) return rc;
+      int e = 0;
+      HIP_TRY(hipMemcpyAsync(&e, err, sizeof(int), hipMemcpyDeviceToHost, st));
+      HIP_TRY(hipStreamSynchronize(st));
+      X.xcd_local = 0;
+      if (e == 3) {
+        if (xcd_fallbacks) ++*xcd_fallbacks;
+        xcd = false;
+        HIP_TRY(dev_zero(err, 4, st));
+        HIP_TRY(dev_zero(gran, gran_bytes, st));
+        if (int rc = launch_resident(fn, grid, block, args, shmem, st)) return rc;
+      }
+    } else if (g.W > 1) {
       if (int rc = launch_resident(fn, grid, block, args, shmem, st)) return rc;
     } else {
       HIP_TRY(hipLaunchKernel(fn, grid, block, args, shmem, st));
@@ -2656,6 +2679,20 @@ static int run_single_impl(kss_ctx* ctx, const PlanNeeds& need, const DevPods& d
     if (w_min > 1) return fail(KSS_E_UNSUPPORTED, "topology histograms too large for a sharded cluster");
     if (!pick_geometry((int)N, 1, ctx->pref_threads, g)) return fail(KSS_E_UNSUPPORTED, "no geometry for this cluster");
   }
+  // XCD-local k_spread (launch_spread xcd): the shards on one XCD when they fit its CUs
+  bool xcd_spread = false;
+  if (spread && !simple && !split && ctx->force_w <= 0 && ctx->xcd_mode && ctx->n_cu % XCD_GRID_MULT == 0 &&
+      !(flags & (KSS_SCHED_FORCE_SINGLE_WG | KSS_SCHED_FORCE_MULTI_WG))) {
+    const int xw = ctx->xcd_w > 0 ? ctx->xcd_w : xcd_cus;
+    Geometry g2;
+    if (g.W > 1 && g.W <= xw) {
+      xcd_spread = true;
+    } else if (g.W > xw && pick_geometry((int)N, xw, KSS_SPREAD_PREF_THREADS, g2) &&
+               spread_fits(g2, ctx->gneed, ctx->dc.n_keys, n_res, N, ctx->dc.n_scalar)) {
+      g = g2;
+      xcd_spread = true;
+    }
+  }
   const bool loop = simple || spread;  // k_static + a persistent loop kernel
   if (split && !loop)
     return fail(KSS_E_UNSUPPORTED, spread_ok ? "split grid: a k_spread shard exceeds LDS (more shards per part)"
@@ -2768,7 +2805,7 @@ static int run_single_impl(kss_ctx* ctx, const PlanNeeds& need, const DevPods& d
     HIP_TRY(hipEventCreate(&e));
     ctx->loop_ev.push_back(e);
   }
-  ctx->last_xcd[0] = simple && xcd_try && g.W > 1 ? 1 : 0;
+  ctx->last_xcd[0] = (simple && xcd_try && g.W > 1) || xcd_spread ? 1 : 0;
   ctx->last_xcd[1] = 0;
   if (simple)
     rc = launch_simple(ctx->stream, g, 1, jd, ctx->prof, n, (int)N, chunk, gran, gb,
@@ -2782,7 +2819,7 @@ static int run_single_impl(kss_ctx* ctx, const PlanNeeds& need, const DevPods& d
     ctx->ck_diag_off = hl.o_diag;
     rc = launch_spread(ctx->stream, g, ctx->gneed, ctx->dc.n_keys, n_res, jd, ctx->prof, n,
                        (int)N, chunk, gran, gb, errp, stamps, ctx->loop_ev.data(), split ? &srun : nullptr,
-                       (unsigned long long*)ctx->ck_buf.p, &ctx->ck_seq, ctx->dc.n_scalar);
+                       (unsigned long long*)ctx->ck_buf.p, &ctx->ck_seq, ctx->dc.n_scalar, xcd_spread, &ctx->last_xcd[1]);
   }
   else  // window: the per-shard feasible counts sit behind the plan's bins
     rc = launch_schedule(ctx->stream, g, 1, std::max(need.bins_cap, 0) + (window ? g.W : 0), need.general, ctx->dc.n_keys,
