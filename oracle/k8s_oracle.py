@@ -534,6 +534,103 @@ def go_round(x: float) -> int:
     return int(math.floor(abs(x) + 0.5)) * (1 if x >= 0 else -1)
 
 
+# ----------------------------------------------------------- AddPod / RemovePod extensions
+# The PreFilter extensions both RunFilterPluginsWithNominatedPods (addNominatedPods) and
+# SelectVictimsOnNode (k8s_preemption) drive on a cloned cycle state.
+MAX_INT32 = 2**31 - 1
+
+
+def pod_priority(pod) -> int:
+    """corev1helpers.PodPriority: spec.priority (set by the Priority admission plugin), 0 if unset."""
+    p = _spec(pod).get("priority")
+    return int(p) if p is not None else 0
+
+
+class CriticalPaths:
+    """podtopologyspread criticalPaths: [2]{TopologyValue, MatchNum}, newCriticalPaths = MaxInt32."""
+
+    def __init__(self):
+        self.p = [["", MAX_INT32], ["", MAX_INT32]]
+
+    def update(self, val, num):
+        p = self.p
+        i = 0 if val == p[0][0] else (1 if val == p[1][0] else -1)
+        if i >= 0:
+            p[i][1] = num
+            if p[0][1] > p[1][1]:
+                p[0], p[1] = p[1], p[0]
+        else:
+            if num < p[0][1]:
+                p[1] = p[0]
+                p[0] = [val, num]
+            elif num < p[1][1]:
+                p[1] = [val, num]
+
+    def min(self):
+        return self.p[0][1]
+
+
+def _pts_state(st):
+    """Clone of the PodTopologySpread preFilterState with criticalPaths built as calPreFilterState
+    does (update over every pair); `mins` mirrors paths[key][0] for Oracle.pts_filter."""
+    if not st["cons"]:
+        return dict(cons=[])
+    pair_num = dict(st["pair_num"])
+    paths: Dict[str, CriticalPaths] = {}
+    for (k, v), num in pair_num.items():
+        paths.setdefault(k, CriticalPaths()).update(v, num)
+    return dict(cons=st["cons"], pair_num=pair_num, paths=paths, mins={k: cp.min() for k, cp in paths.items()})
+
+
+def _pts_update(st, victim, preemptor, node, delta):
+    """podtopologyspread preFilterState.updateWithPod (v1.26)."""
+    if not st["cons"] or _ns(victim) != _ns(preemptor):
+        return
+    lb = _labels(node)
+    if not all(c["key"] in lb for c in st["cons"]):
+        return
+    if not required_node_affinity_match(preemptor, node):
+        return
+    plabels = _labels(victim)
+    for c in st["cons"]:
+        if not c["sel"].matches(plabels):
+            continue
+        pair = (c["key"], lb[c["key"]])
+        st["pair_num"][pair] = st["pair_num"].get(pair, 0) + delta
+        st["paths"].setdefault(c["key"], CriticalPaths()).update(lb[c["key"]], st["pair_num"][pair])
+        st["mins"][c["key"]] = st["paths"][c["key"]].min()
+
+
+def _ipa_state(st):
+    return dict(pinfo=st["pinfo"], existing=dict(st["existing"]), aff=dict(st["aff"]), anti=dict(st["anti"]))
+
+
+def _tm_update(m, node, key, value):
+    """topologyToMatchedTermCount.update: delete the pair when it reaches zero."""
+    lb = _labels(node)
+    if key in lb:
+        pair = (key, lb[key])
+        m[pair] = m.get(pair, 0) + value
+        if m[pair] == 0:
+            del m[pair]
+
+
+def _ipa_update(o, st, victim_pi, preemptor, node, mult):
+    """interpodaffinity preFilterState.updateWithPod (v1.26)."""
+    pinfo = st["pinfo"]
+    nsl = o.namespaces.get(_ns(preemptor), {})
+    for t in victim_pi.required_anti:
+        if t.matches(preemptor, nsl):
+            _tm_update(st["existing"], node, t.topology_key, mult)
+    if pinfo.required_affinity and all(t.matches(victim_pi.pod, None) for t in pinfo.required_affinity):
+        for t in pinfo.required_affinity:
+            _tm_update(st["aff"], node, t.topology_key, mult)
+    for t in pinfo.required_anti:
+        if t.matches(victim_pi.pod, None):
+            _tm_update(st["anti"], node, t.topology_key, mult)
+
+
+
 class Oracle:
     """Sequential scheduler over objects; one schedule_one() per pending pod."""
 
@@ -575,6 +672,64 @@ class Oracle:
         self.ba_resources = list(ba_resources)
         self.pct = percentage_of_nodes_to_score
         self.next_start = 0  # Scheduler.nextStartNodeIndex
+        # the scheduling queue's nominator: [(pod key, pod, node index)] in AddNominatedPod order
+        self.nominated: List[Tuple[Tuple[str, str], dict, int]] = []
+
+    # ----------------------------------------------------------- nominator
+    @staticmethod
+    def _key(pod) -> Tuple[str, str]:
+        return (_ns(pod), _name(pod))  # the pod's UID in this restatement
+
+    def nominate(self, pod, i: int):
+        """PodNominator.AddNominatedPod (a pod's earlier nomination is replaced)."""
+        self.clear_nomination(pod)
+        self.nominated.append((self._key(pod), pod, i))
+
+    def clear_nomination(self, pod):
+        """PodNominator.DeleteNominatedPodIfExists."""
+        k = self._key(pod)
+        self.nominated = [e for e in self.nominated if e[0] != k]
+
+    def nomination_of(self, pod) -> Optional[int]:
+        """status.nominatedNodeName as a node index (None when the pod is not nominated)."""
+        k = self._key(pod)
+        for kk, _, i in self.nominated:
+            if kk == k:
+                return i
+        return None
+
+    def assume(self, pod, i: int):
+        """Cache.AssumePod -> NodeInfo.AddPod, then SchedulingQueue.DeleteNominatedPodIfExists
+        (schedule_one.go assume)."""
+        self.infos[i].add_pod(pod)
+        self.clear_nomination(pod)
+
+    def filter_with_nominated(self, pod, i: int, ni: "NodeInfo", pts_st, ipa_st, vb_claims=None):
+        """framework.RunFilterPluginsWithNominatedPods (v1.26 runtime/framework.go) over NodeInfo ni
+        of node i: a first pass with every nominated pod of equal or higher priority (other than
+        the pod itself) added to a clone of ni and of the cycle state (addNominatedPods: AddPodInfo
+        and RunPreFilterExtensionAddPod -- the PodTopologySpread / InterPodAffinity updateWithPod),
+        then, when it passed and some pod was added, a second pass on the unmodified ni and state.
+        The record is the simulator's per-plugin map (store.go:423 AddFilterResult overwrites): a
+        plugin the second pass never reached keeps the first pass's "passed"."""
+        prio = pod_priority(pod)
+        k = self._key(pod)
+        noms = [q for kk, q, n in self.nominated if n == i and kk != k and pod_priority(q) >= prio]
+        if not noms:
+            return self.filter_node(pod, ni, pts_st, ipa_st, vb_claims)
+        ni1 = ni.clone()
+        pts1 = _pts_state(pts_st)
+        ipa1 = _ipa_state(ipa_st)
+        for q in noms:
+            ni1.add_pod(q)
+            _pts_update(pts1, q, pod, ni.node, 1)
+            _ipa_update(self, ipa1, PodInfo(q), pod, ni.node, 1)
+        failed, rec = self.filter_node(pod, ni1, pts1, ipa1, vb_claims)
+        if failed is not None:
+            return failed, rec
+        failed2, rec2 = self.filter_node(pod, ni, pts_st, ipa_st, vb_claims)
+        rec.update(rec2)
+        return failed2, rec
 
     # ----------------------------------------------------------- ImageLocality
     def image_locality_score(self, pod, ni) -> int:
@@ -1011,6 +1166,24 @@ class Oracle:
         res["_pts_st"], res["_ipa_st"] = pts_st, ipa_st  # the cycle state PostFilter sees
         feasible = []
         tols = sp.get("tolerations") or []
+        # PreferNominatedNode (findNodesThatFitPod -> evaluateNominatedNode): a pod nominated by an
+        # earlier preemption first runs findNodesThatPassFilters on [that node] alone -- before and
+        # regardless of the PreFilterResult set; its one-node list resets nextStartNodeIndex to 0
+        # ((start + processed) % 1).  A feasible node is the answer without scoring; otherwise the
+        # node's status stays in the diagnosis (the full search overwrites it if it gets there)
+        nom = self.nomination_of(pod)
+        if nom is not None:
+            failed, rec = self.filter_with_nominated(pod, nom, self.infos[nom], pts_st, ipa_st, vb_claims)
+            ann_filter[_name(self.infos[nom].node)] = rec
+            res["fail"][nom] = failed
+            res["nominated_eval"] = nom
+            self.next_start = 0
+            if failed is None:
+                res["n_feasible"] = 1
+                res["selected"] = nom
+                if commit:
+                    self.assume(pod, nom)
+                return res
         # findNodesThatPassFilters (schedule_one.go, v1.26) with Parallelism = 1: the node list (the
         # PreFilterResult set in canonical order -- upstream ranges over a Go map here) is checked
         # one node at a time from nextStartNodeIndex; the feasible node that makes the count exceed
@@ -1023,7 +1196,7 @@ class Oracle:
         for j in range(m):
             i = node_list[(self.next_start + j) % m]
             ni = self.infos[i]
-            failed, rec = self.filter_node(pod, ni, pts_st, ipa_st, vb_claims)
+            failed, rec = self.filter_with_nominated(pod, i, ni, pts_st, ipa_st, vb_claims)
             ann_filter[_name(ni.node)] = rec
             res["fail"][i] = failed
             if failed is None:
@@ -1045,7 +1218,7 @@ class Oracle:
         if len(feasible) == 1:
             res["selected"] = feasible[0]
             if commit:
-                self.infos[feasible[0]].add_pod(pod)
+                self.assume(pod, feasible[0])
             return res
         res["scored"] = True
         for pl in PRESCORES:
@@ -1122,7 +1295,7 @@ class Oracle:
             res["finalscore"][nm] = {pl: str(norm[pl][i] * self.weights[pl]) for pl in SCORES}
         res["selected"] = bi
         if commit:
-            self.infos[bi].add_pod(pod)
+            self.assume(pod, bi)
         return res
 
     # ----------------------------------------------------------- annotations

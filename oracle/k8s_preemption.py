@@ -33,7 +33,9 @@ Deterministic where upstream is not (both documented in DESIGN.md, "PostFilter")
   * pickOneNodeForPreemption iterates a Go map (random order) and keeps the first node on a
     full tie; here candidates are visited in canonical node order.
 No PodDisruptionBudgets (the simulator's snapshot carries none: every victim is
-non-violating) and no nominated pods (RunFilterPluginsWithNominatedPods adds none).
+non-violating).  SelectVictimsOnNode filters with RunFilterPluginsWithNominatedPods
+(Oracle.filter_with_nominated): the nominator's pods of equal or higher priority on the node
+take part in the first pass; they are never victims (they are not in NodeInfo.Pods).
 """
 from __future__ import annotations
 
@@ -41,6 +43,8 @@ from datetime import datetime, timezone
 from typing import Dict, List, Optional
 
 import k8s_oracle as ko
+from k8s_oracle import (CriticalPaths, _ipa_state, _ipa_update, _pts_state, _pts_update,  # noqa: F401
+                        _tm_update, pod_priority)
 
 MAX_INT32 = 2**31 - 1
 NOMINATED_MESSAGE = "preemption victim"  # resultstore PostFilterNominatedMessage (store.go:34)
@@ -50,12 +54,6 @@ UNRESOLVABLE = {
     ("NodeUnschedulable", None), ("NodeName", None), ("TaintToleration", None), ("NodeAffinity", None),
     ("PodTopologySpread", ko.MSG["PTS_LABEL"]), ("InterPodAffinity", ko.MSG["IPA_AFF"]),
 }
-
-
-def pod_priority(pod) -> int:
-    """corev1helpers.PodPriority: spec.priority (set by the Priority admission plugin), 0 if unset."""
-    p = ko._spec(pod).get("priority")
-    return int(p) if p is not None else 0
 
 
 def pod_start_ns(pod) -> Optional[int]:
@@ -91,90 +89,6 @@ def _sorted_by_importance(pods: List) -> List:
     return out
 
 
-class CriticalPaths:
-    """podtopologyspread criticalPaths: [2]{TopologyValue, MatchNum}, newCriticalPaths = MaxInt32."""
-
-    def __init__(self):
-        self.p = [["", MAX_INT32], ["", MAX_INT32]]
-
-    def update(self, val, num):
-        p = self.p
-        i = 0 if val == p[0][0] else (1 if val == p[1][0] else -1)
-        if i >= 0:
-            p[i][1] = num
-            if p[0][1] > p[1][1]:
-                p[0], p[1] = p[1], p[0]
-        else:
-            if num < p[0][1]:
-                p[1] = p[0]
-                p[0] = [val, num]
-            elif num < p[1][1]:
-                p[1] = [val, num]
-
-    def min(self):
-        return self.p[0][1]
-
-
-def _pts_state(st):
-    """Clone of the PodTopologySpread preFilterState with criticalPaths built as calPreFilterState
-    does (update over every pair); `mins` mirrors paths[key][0] for Oracle.pts_filter."""
-    if not st["cons"]:
-        return dict(cons=[])
-    pair_num = dict(st["pair_num"])
-    paths: Dict[str, CriticalPaths] = {}
-    for (k, v), num in pair_num.items():
-        paths.setdefault(k, CriticalPaths()).update(v, num)
-    return dict(cons=st["cons"], pair_num=pair_num, paths=paths, mins={k: cp.min() for k, cp in paths.items()})
-
-
-def _pts_update(st, victim, preemptor, node, delta):
-    """podtopologyspread preFilterState.updateWithPod (v1.26)."""
-    if not st["cons"] or ko._ns(victim) != ko._ns(preemptor):
-        return
-    lb = ko._labels(node)
-    if not all(c["key"] in lb for c in st["cons"]):
-        return
-    if not ko.required_node_affinity_match(preemptor, node):
-        return
-    plabels = ko._labels(victim)
-    for c in st["cons"]:
-        if not c["sel"].matches(plabels):
-            continue
-        pair = (c["key"], lb[c["key"]])
-        st["pair_num"][pair] = st["pair_num"].get(pair, 0) + delta
-        st["paths"].setdefault(c["key"], CriticalPaths()).update(lb[c["key"]], st["pair_num"][pair])
-        st["mins"][c["key"]] = st["paths"][c["key"]].min()
-
-
-def _ipa_state(st):
-    return dict(pinfo=st["pinfo"], existing=dict(st["existing"]), aff=dict(st["aff"]), anti=dict(st["anti"]))
-
-
-def _tm_update(m, node, key, value):
-    """topologyToMatchedTermCount.update: delete the pair when it reaches zero."""
-    lb = ko._labels(node)
-    if key in lb:
-        pair = (key, lb[key])
-        m[pair] = m.get(pair, 0) + value
-        if m[pair] == 0:
-            del m[pair]
-
-
-def _ipa_update(o, st, victim_pi, preemptor, node, mult):
-    """interpodaffinity preFilterState.updateWithPod (v1.26)."""
-    pinfo = st["pinfo"]
-    nsl = o.namespaces.get(ko._ns(preemptor), {})
-    for t in victim_pi.required_anti:
-        if t.matches(preemptor, nsl):
-            _tm_update(st["existing"], node, t.topology_key, mult)
-    if pinfo.required_affinity and all(t.matches(victim_pi.pod, None) for t in pinfo.required_affinity):
-        for t in pinfo.required_affinity:
-            _tm_update(st["aff"], node, t.topology_key, mult)
-    for t in pinfo.required_anti:
-        if t.matches(victim_pi.pod, None):
-            _tm_update(st["anti"], node, t.topology_key, mult)
-
-
 def _unresolvable(plugin: str, msg: str) -> bool:
     return (plugin, None) in UNRESOLVABLE or (plugin, msg) in UNRESOLVABLE
 
@@ -193,14 +107,14 @@ def select_victims_on_node(o: ko.Oracle, pod, i: int, pts_st, ipa_st):
         ni.remove_pod(pi.pod)
         _pts_update(pts, pi.pod, pod, node, -1)
         _ipa_update(o, ipa, pi, pod, node, -1)
-    if o.filter_node(pod, ni, pts, ipa)[0] is not None:
+    if o.filter_with_nominated(pod, i, ni, pts, ipa)[0] is not None:
         return None
     victims = []
     for pi in _sorted_by_importance(potential):  # no PDBs: every pod is non-violating
         ni.add_pod(pi.pod)
         _pts_update(pts, pi.pod, pod, node, 1)
         _ipa_update(o, ipa, pi, pod, node, 1)
-        if o.filter_node(pod, ni, pts, ipa)[0] is not None:
+        if o.filter_with_nominated(pod, i, ni, pts, ipa)[0] is not None:
             ni.remove_pod(pi.pod)
             _pts_update(pts, pi.pod, pod, node, -1)
             _ipa_update(o, ipa, pi, pod, node, -1)

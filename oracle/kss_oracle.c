@@ -82,12 +82,21 @@ typedef struct {
   int32_t* vol_count;
   int32_t* vol_attached;
   int32_t cursor; /* the scheduler's nextStartNodeIndex (schedule_one.go findNodesThatPassFilters) */
+  /* the scheduling queue's nominator (PodNominator): pods of ps nominated to a node by an earlier
+     preemption; a nomination leaves when its pod is assumed (DeleteNominatedPodIfExists) */
+  int n_nom;
+  const int32_t* nom_pod;  /* [n_nom] index in ps */
+  const int32_t* nom_node; /* [n_nom] local node */
+  uint8_t* nom_active;     /* [n_nom] */
 } ostate;
 
 static int ostate_init(ostate* s, const kss_cluster* cl) {
   size_t N = (size_t)cl->n_nodes;
   s->c = *cl;
   s->cursor = 0;
+  s->n_nom = 0;
+  s->nom_pod = s->nom_node = NULL;
+  s->nom_active = NULL;
   s->requested = (int64_t*)malloc(sizeof(int64_t) * KSS_NRES * (N ? N : 1));
   s->nonzero = (int64_t*)malloc(sizeof(int64_t) * 2 * (N ? N : 1));
   s->pod_count = (int32_t*)malloc(sizeof(int32_t) * (N ? N : 1));
@@ -127,6 +136,7 @@ static void ostate_free(ostate* s) {
   free(s->port_used);
   free(s->vol_count);
   free(s->vol_attached);
+  free(s->nom_active);
 }
 
 #define LV(cl, key, n) ((cl)->label_value[(size_t)(key) * (size_t)(cl)->n_nodes + (size_t)(n)])
@@ -593,6 +603,139 @@ static int filter_node(const kss_profile* prof, const kss_cluster* cl, const kss
   return KSS_F_PASS;
 }
 
+static int in_ints(const int32_t* ints, int off, int len, int v) {
+  for (int i = 0; i < len; i++)
+    if (ints[off + i] == v) return 1;
+  return 0;
+}
+
+/* ---------------------------------------------------------------------------
+ * RunFilterPluginsWithNominatedPods (v1.26 runtime/framework.go) for node n: the first pass
+ * runs with every nominated pod of priority >= the pod's (other than the pod itself) added to
+ * the node (addNominatedPods: NodeInfo.AddPodInfo plus the AddPod PreFilter extensions --
+ * podtopologyspread / interpodaffinity preFilterState.updateWithPod on the node's pairs); when
+ * it passes, the second pass on the unmodified node decides (*added = 1).  The state is changed
+ * in place and restored, so the caller runs it serially.  Nominees carry no volumes (the
+ * device refuses them).  The PodTopologySpread minimum after the update is the minimum over
+ * the present pairs: criticalPaths.update keeps exactly that when one pair changes.
+ * ------------------------------------------------------------------------- */
+static int filter_with_nominated(const kss_profile* prof, ostate* s, const kss_podset* ps, int pi, podstate* st,
+                                 int n, uint16_t* detail, int* added) {
+  const kss_cluster* cl = &s->c;
+  const kss_pod* p = &ps->pods[pi];
+  const size_t N = (size_t)cl->n_nodes;
+  int q[64], nq = 0;
+  *added = 0;
+  for (int j = 0; j < s->n_nom && nq < 64; j++)
+    if (s->nom_active[j] && s->nom_node[j] == n && s->nom_pod[j] != pi && ps->pods[s->nom_pod[j]].priority >= p->priority)
+      q[nq++] = s->nom_pod[j];
+  if (nq == 0) return filter_node(prof, cl, ps, p, st, n, detail);
+  int64_t save_req[KSS_NRES];
+  for (int r = 0; r < KSS_NRES; r++) save_req[r] = s->requested[(size_t)r * N + n];
+  const int32_t save_pods = s->pod_count[n];
+  const uint64_t save_ports = s->port_used[n];
+  for (int k = 0; k < nq; k++) {
+    const kss_pod* a = &ps->pods[q[k]];
+    for (int r = 0; r < KSS_NRES; r++) s->requested[(size_t)r * N + n] += a->commit_req[r];
+    s->pod_count[n] += 1;
+    s->port_used[n] |= a->port_add;
+  }
+  /* podtopologyspread updateWithPod: same namespace (the selectors' class lists hold only the
+     pod's namespace), the node carries every constraint key, the pod's required node affinity
+     matches it; each matching constraint adds one to the node's pair of its key */
+  const kss_spread* hard = ps->spreads + p->spread_off;
+  int64_t save_cnt[8] = {0}, save_min[8] = {0};
+  uint8_t save_pres[8] = {0};
+  int pts_on = p->n_hard > 0 && has_all_keys(cl, hard, p->n_hard, n) && required_node_affinity(cl, ps, p, n);
+  if (pts_on) {
+    for (int i = 0; i < p->n_hard; i++) {
+      if (st->hard_own[i] != i) continue;
+      const int d = LV(cl, hard[i].key, n);
+      save_cnt[i] = st->hard_cnt[i][d];
+      save_pres[i] = st->hard_present[i][d];
+      save_min[i] = st->hard_min[i];
+      int64_t delta = 0;
+      for (int k = 0; k < nq; k++)
+        for (int j = i; j < p->n_hard; j++)
+          if (st->hard_own[j] == i) delta += in_ints(ps->ints, hard[j].cls_off, hard[j].cls_len, ps->pods[q[k]].cls);
+      if (delta == 0) continue;
+      st->hard_cnt[i][d] += delta;
+      st->hard_present[i][d] = 1;
+      int64_t mn = INT32_MAX;
+      const int bins = cl->key_card[hard[i].key] + 1;
+      for (int b = 0; b < bins; b++)
+        if (st->hard_present[i][b] && st->hard_cnt[i][b] < mn) mn = st->hard_cnt[i][b];
+      st->hard_min[i] = mn;
+    }
+  }
+  /* interpodaffinity updateWithPod on the node's pairs: the nominee's required anti-affinity
+     terms matching the pod (existing anti), the pod's required affinity terms when the nominee
+     matches all of them, the pod's required anti-affinity terms the nominee matches */
+  const kss_ipa* ipa = ps->ipa + p->ipa_off;
+  int64_t ipa_delta[64];
+  const int ne = p->ipa_len < 64 ? p->ipa_len : 64;
+  const int save_ex = st->ex_nonempty, save_aff = st->aff_nonempty, save_anti = st->anti_nonempty;
+  for (int e = 0; e < ne; e++) {
+    ipa_delta[e] = 0;
+    const kss_ipa* en = &ipa[e];
+    if (en->kind > KSS_IPA_REQ_ANTI) continue;
+    const int d = LV(cl, en->key, n);
+    if (d < 0) continue;
+    for (int k = 0; k < nq; k++) {
+      const kss_pod* a = &ps->pods[q[k]];
+      if (en->kind == KSS_IPA_EXISTING_ANTI) {
+        for (int t = 0; t < a->own_terms_len; t++)
+          ipa_delta[e] += in_ints(ps->ints, en->row_off, en->row_len, ps->ints[a->own_terms_off + t]);
+      } else {
+        ipa_delta[e] += in_ints(ps->ints, en->row_off, en->row_len, a->cls);
+      }
+    }
+    if (!ipa_delta[e]) continue;
+    const int ks = key_slot(st, en->key);
+    int64_t* h = en->kind == KSS_IPA_EXISTING_ANTI ? st->hx[ks] : (en->kind == KSS_IPA_REQ_AFFINITY ? st->ha[ks] : st->hb[ks]);
+    h[d] += ipa_delta[e];
+    if (en->kind == KSS_IPA_EXISTING_ANTI) st->ex_nonempty = 1;
+    else if (en->kind == KSS_IPA_REQ_AFFINITY) st->aff_nonempty = 1;
+    else st->anti_nonempty = 1;
+  }
+  int f = filter_node(prof, cl, ps, p, st, n, detail);
+  /* restore */
+  for (int e = 0; e < ne; e++) {
+    const kss_ipa* en = &ipa[e];
+    if (en->kind > KSS_IPA_REQ_ANTI || !ipa_delta[e]) continue;
+    const int ks = key_slot(st, en->key);
+    int64_t* h = en->kind == KSS_IPA_EXISTING_ANTI ? st->hx[ks] : (en->kind == KSS_IPA_REQ_AFFINITY ? st->ha[ks] : st->hb[ks]);
+    h[LV(cl, en->key, n)] -= ipa_delta[e];
+  }
+  st->ex_nonempty = save_ex;
+  st->aff_nonempty = save_aff;
+  st->anti_nonempty = save_anti;
+  if (pts_on) {
+    for (int i = 0; i < p->n_hard; i++) {
+      if (st->hard_own[i] != i) continue;
+      const int d = LV(cl, hard[i].key, n);
+      st->hard_cnt[i][d] = save_cnt[i];
+      st->hard_present[i][d] = save_pres[i];
+      st->hard_min[i] = save_min[i];
+    }
+  }
+  for (int r = 0; r < KSS_NRES; r++) s->requested[(size_t)r * N + n] = save_req[r];
+  s->pod_count[n] = save_pods;
+  s->port_used[n] = save_ports;
+  *added = 1;
+  if (f != KSS_F_PASS) return f;
+  /* the second pass: the unmodified node (a failure here can only be InterPodAffinity's
+     required affinity, the last filter plugin: its record is the whole story) */
+  return filter_node(prof, cl, ps, p, st, n, detail);
+}
+
+/* the node of pod pi's active nomination (status.nominatedNodeName), or -1 */
+static int nomination_of(const ostate* s, int pi) {
+  for (int j = 0; j < s->n_nom; j++)
+    if (s->nom_active[j] && s->nom_pod[j] == pi) return s->nom_node[j];
+  return -1;
+}
+
 /* ---------------------------------------------------------------------------
  * raw scores (Score extension point) for one feasible node
  * ------------------------------------------------------------------------- */
@@ -759,6 +902,24 @@ static int schedule_one(const kss_profile* prof, ostate* s, const kss_podset* ps
   rc = podstate_build(&st, cl, ps, p, prof->hard_pod_affinity_weight);
   if (rc) goto done;
 
+  /* PreferNominatedNode (findNodesThatFitPod -> evaluateNominatedNode): a nominated pod first
+     runs findNodesThatPassFilters on [its node] alone (whatever the PreFilterResult); the
+     one-node list resets nextStartNodeIndex to 0.  A feasible node is chosen without scoring;
+     otherwise its status stays in the diagnosis and its record stands. */
+  int nom_m = nomination_of(s, pi), nom_f = 0;
+  uint16_t nom_d = 0;
+  if (nom_m >= 0) {
+    int added;
+    nom_f = filter_with_nominated(prof, s, ps, pi, &st, nom_m, &nom_d, &added);
+    s->cursor = 0;
+    if (nom_f == KSS_F_PASS) {
+      fp[nom_m] = KSS_F_PASS;
+      out->n_feasible = 1;
+      out->chosen = cl->node_base + nom_m;
+      goto done;
+    }
+  }
+
   /* HOT LOOP 1: findNodesThatPassFilters over the (PreFilterResult-restricted) node list */
   {
     uint8_t* inset = NULL;
@@ -773,6 +934,20 @@ static int schedule_one(const kss_profile* prof, ostate* s, const kss_podset* ps
     for (int n = 0; n < N; n++) {
       if (inset && !inset[n]) continue;
       fp[n] = (uint8_t)filter_node(prof, cl, ps, p, &st, n, &fd[n]);
+    }
+    /* nodes holding nominated pods: RunFilterPluginsWithNominatedPods' first pass (serial: it
+       changes the state in place) -- a failure there is the node's status */
+    for (int j = 0; j < s->n_nom; j++) {
+      const int n = s->nom_node[j];
+      if (!s->nom_active[j] || n < 0 || n >= N || (inset && !inset[n])) continue;
+      int dup = 0;
+      for (int k = 0; k < j; k++) dup |= s->nom_active[k] && s->nom_node[k] == n;
+      if (dup) continue;
+      uint16_t d;
+      int added;
+      const int f = filter_with_nominated(prof, s, ps, pi, &st, n, &d, &added);
+      fp[n] = (uint8_t)f;
+      fd[n] = d;
     }
     /* findNodesThatPassFilters with Parallelism = 1: the node list (all nodes, or the
        PreFilterResult set in canonical order) is visited from nextStartNodeIndex until one
@@ -807,6 +982,10 @@ static int schedule_one(const kss_profile* prof, ostate* s, const kss_podset* ps
     }
     free(list);
     free(inset);
+    if (nom_m >= 0) { /* the nominated node's status from evaluateNominatedNode (the same if revisited) */
+      fp[nom_m] = (uint8_t)nom_f;
+      fd[nom_m] = nom_d;
+    }
   }
   int nf = 0;
   for (int n = 0; n < N; n++)
@@ -1020,6 +1199,8 @@ done:
 static void commit(ostate* s, const kss_podset* ps, int pi, int node_local) {
   const kss_pod* p = &ps->pods[pi];
   size_t N = (size_t)s->c.n_nodes;
+  for (int j = 0; j < s->n_nom; j++) /* SchedulingQueue.DeleteNominatedPodIfExists(assumed pod) */
+    if (s->nom_pod[j] == pi) s->nom_active[j] = 0;
   for (int r = 0; r < KSS_NRES; r++) s->requested[(size_t)r * N + node_local] += p->commit_req[r];
   s->nonzero[node_local] += p->commit_nz[0];
   s->nonzero[N + node_local] += p->commit_nz[1];
@@ -1075,14 +1256,47 @@ int kss_oracle_schedule_v(const kss_profile* prof, const kss_cluster* cl, const 
                                out_class_count, out_term_count, out_port_used, out_vol_count, out_vol_attached, NULL);
 }
 
+/* kss_oracle_schedule_c with the scheduling queue's nominator: pods ps.pods[nom_pod[j]] nominated
+   to global node nom_node[j] (PodNominator.AddNominatedPod order); a pod of the batch that is
+   assumed leaves it.  *nom_left (optional) receives the nominations still active per entry. */
+int kss_oracle_schedule_n(const kss_profile* prof, const kss_cluster* cl, const kss_podset* ps, int n,
+                          int32_t* chosen, kss_pod_result* results, int threads, int64_t* out_requested,
+                          int64_t* out_nonzero, int32_t* out_pod_count, int32_t* out_class_count,
+                          int32_t* out_term_count, uint64_t* out_port_used, int32_t* out_vol_count,
+                          int32_t* out_vol_attached, int32_t* cursor, const int32_t* nom_pod,
+                          const int32_t* nom_node, int32_t n_nom, uint8_t* nom_left);
+
 int kss_oracle_schedule_c(const kss_profile* prof, const kss_cluster* cl, const kss_podset* ps, int n,
                           int32_t* chosen, kss_pod_result* results, int threads, int64_t* out_requested,
                           int64_t* out_nonzero, int32_t* out_pod_count, int32_t* out_class_count,
                           int32_t* out_term_count, uint64_t* out_port_used, int32_t* out_vol_count,
                           int32_t* out_vol_attached, int32_t* cursor) {
+  return kss_oracle_schedule_n(prof, cl, ps, n, chosen, results, threads, out_requested, out_nonzero, out_pod_count,
+                               out_class_count, out_term_count, out_port_used, out_vol_count, out_vol_attached, cursor,
+                               NULL, NULL, 0, NULL);
+}
+
+int kss_oracle_schedule_n(const kss_profile* prof, const kss_cluster* cl, const kss_podset* ps, int n,
+                          int32_t* chosen, kss_pod_result* results, int threads, int64_t* out_requested,
+                          int64_t* out_nonzero, int32_t* out_pod_count, int32_t* out_class_count,
+                          int32_t* out_term_count, uint64_t* out_port_used, int32_t* out_vol_count,
+                          int32_t* out_vol_attached, int32_t* cursor, const int32_t* nom_pod,
+                          const int32_t* nom_node, int32_t n_nom, uint8_t* nom_left) {
   ostate s;
   if (ostate_init(&s, cl)) return KSS_E_NOMEM;
   if (cursor) s.cursor = *cursor;
+  int32_t* nn_local = NULL;
+  if (n_nom > 0) {
+    s.n_nom = n_nom;
+    s.nom_pod = nom_pod;
+    nn_local = (int32_t*)malloc(sizeof(int32_t) * (size_t)n_nom);
+    s.nom_active = (uint8_t*)malloc((size_t)n_nom);
+    for (int j = 0; j < n_nom; j++) {
+      nn_local[j] = nom_node[j] - cl->node_base;
+      s.nom_active[j] = nom_pod[j] >= 0 && nom_pod[j] < ps->n_pods && nn_local[j] >= 0 && nn_local[j] < cl->n_nodes;
+    }
+    s.nom_node = nn_local;
+  }
   int th = threads > 0 ? threads : 1;
   int rc = 0;
   for (int i = 0; i < n; i++) {
@@ -1106,6 +1320,9 @@ int kss_oracle_schedule_c(const kss_profile* prof, const kss_cluster* cl, const 
   if (out_vol_attached && cl->n_vol_keys)
     memcpy(out_vol_attached, s.vol_attached, sizeof(int32_t) * (size_t)cl->n_vol_keys * N);
   if (cursor) *cursor = s.cursor;
+  if (nom_left)
+    for (int j = 0; j < n_nom; j++) nom_left[j] = s.nom_active[j];
+  free(nn_local);
   ostate_free(&s);
   return rc;
 }

@@ -9,16 +9,18 @@ from kss.compile import compile_cluster
 FILTER_CODE = {name: i for i, name in enumerate(abi.FILTER_PLUGINS) if name}
 
 
-def run_both(nodes, bound, pods, n_check=None, storage=None, pct=100):
+def run_both(nodes, bound, pods, n_check=None, storage=None, pct=100, nominations=()):
     """Schedule `pods` sequentially with both oracles and assert identical per-pod results.
     storage: {"pvs", "pvcs", "storage_classes", "csinodes"} for the volume plugins.
     pct: percentageOfNodesToScore (below 100: the findNodesThatPassFilters window; the C oracle
-    filters every node and windows afterwards, the object oracle visits nodes one at a time)."""
+    filters every node and windows afterwards, the object oracle visits nodes one at a time).
+    nominations: [(index into pods, node index)] in the nominator's order (the nominated pods
+    need not be among the first n_check)."""
     cc, cp, comp = compile_cluster(nodes, bound, pods, storage=storage)
     prof = abi.default_profile()
     prof.pct_nodes_to_score = pct
     chosen, res, _ = oracle_c.schedule(prof, cc.as_struct(), cp.as_struct(), cp.n, cc.n_nodes,
-                                       n_classes=len(cc.classes), n_terms=len(cc.terms))
+                                       n_classes=len(cc.classes), n_terms=len(cc.terms), nominations=nominations)
     st = None
     if storage:
         import k8s_volumes
@@ -26,6 +28,8 @@ def run_both(nodes, bound, pods, n_check=None, storage=None, pct=100):
                                  storage.get("storage_classes") or (), storage.get("csinodes") or ())
     o = k8s_oracle.Oracle(nodes, bound, storage=st, percentage_of_nodes_to_score=pct)
     assert [k8s_oracle._name(n) for n in o.nodes] == cc.node_names
+    for a, b in nominations:
+        o.nominate(pods[a], b)
     n_check = len(pods) if n_check is None else n_check
     for j in range(n_check):
         r = o.schedule_one(pods[j])

@@ -27,6 +27,9 @@ def lib():
         _lib.kss_oracle_schedule_v.restype = C.c_int
         _lib.kss_oracle_schedule_c.argtypes = _lib.kss_oracle_schedule_v.argtypes + [P(C.c_int32)]
         _lib.kss_oracle_schedule_c.restype = C.c_int
+        _lib.kss_oracle_schedule_n.argtypes = _lib.kss_oracle_schedule_c.argtypes + [
+            P(C.c_int32), P(C.c_int32), C.c_int32, P(C.c_uint8)]
+        _lib.kss_oracle_schedule_n.restype = C.c_int
         _lib.kss_oracle_eval_pod.argtypes = [P(abi.Profile), P(abi.Cluster), P(abi.PodSet), C.c_int,
                                              P(abi.PodResult), C.c_int]
         _lib.kss_oracle_eval_pod.restype = C.c_int
@@ -83,11 +86,12 @@ class Results:
 
 
 def schedule(profile, cluster_struct, podset_struct, n_pods, n_nodes, threads=1, record=True, n_classes=0,
-             n_terms=0, cursor=0):
+             n_terms=0, cursor=0, nominations=()):
     """Run the C oracle sequentially; returns (chosen, Results|None, final_state dict).
     record=True keeps every per-node array, record="meta" only the per-pod outcomes.
     cursor: the scheduler's nextStartNodeIndex at the first pod; the final value is
-    final_state["next_start"]."""
+    final_state["next_start"].  nominations: [(pod index, global node)] in the nominator's
+    order; final_state["nominations"] lists those still active afterwards."""
     L = lib()
     chosen = np.full(max(n_pods, 1), -2, dtype=np.int32)
     res = Results(n_pods, n_nodes, arrays=record is True) if record else None
@@ -99,7 +103,11 @@ def schedule(profile, cluster_struct, podset_struct, n_pods, n_nodes, threads=1,
               vol_attached=np.zeros((max(cluster_struct.n_vol_keys, 1), N), np.int32))
     P = C.POINTER
     cur = C.c_int32(cursor)
-    rc = L.kss_oracle_schedule_c(C.byref(profile), C.byref(cluster_struct), C.byref(podset_struct), n_pods,
+    nominations = list(nominations)
+    nom_pod = np.array([a for a, _ in nominations] or [0], dtype=np.int32)
+    nom_node = np.array([b for _, b in nominations] or [0], dtype=np.int32)
+    nom_left = np.zeros(max(len(nominations), 1), dtype=np.uint8)
+    rc = L.kss_oracle_schedule_n(C.byref(profile), C.byref(cluster_struct), C.byref(podset_struct), n_pods,
                                chosen.ctypes.data_as(P(C.c_int32)), res.structs if res else None, threads,
                                st["requested"].ctypes.data_as(P(C.c_int64)), st["nonzero"].ctypes.data_as(P(C.c_int64)),
                                st["pod_count"].ctypes.data_as(P(C.c_int32)),
@@ -107,9 +115,12 @@ def schedule(profile, cluster_struct, podset_struct, n_pods, n_nodes, threads=1,
                                st["term_count"].ctypes.data_as(P(C.c_int32)),
                                st["port_used"].ctypes.data_as(P(C.c_uint64)),
                                st["vol_count"].ctypes.data_as(P(C.c_int32)),
-                               st["vol_attached"].ctypes.data_as(P(C.c_int32)), C.byref(cur))
+                               st["vol_attached"].ctypes.data_as(P(C.c_int32)), C.byref(cur),
+                               nom_pod.ctypes.data_as(P(C.c_int32)), nom_node.ctypes.data_as(P(C.c_int32)),
+                               len(nominations), nom_left.ctypes.data_as(P(C.c_uint8)))
     assert rc == 0, f"oracle rc={rc}"
     st["next_start"] = cur.value
+    st["nominations"] = [e for e, keep in zip(nominations, nom_left) if keep]
     st["vol_count"] = st["vol_count"][:cluster_struct.n_vol_rows, :n_nodes]
     st["vol_attached"] = st["vol_attached"][:cluster_struct.n_vol_keys, :n_nodes]
     return chosen[:n_pods], res, st
