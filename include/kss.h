@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define KSS_ABI_VERSION 3
+#define KSS_ABI_VERSION 4
 
 /* ---- error codes ------------------------------------------------------- */
 #define KSS_OK 0
@@ -566,6 +566,33 @@ int kss_reset_node_state(kss_ctx* ctx);
 int kss_next_start_node_index(kss_ctx* ctx, int32_t* out);
 int kss_set_next_start_node_index(kss_ctx* ctx, int32_t value);
 
+/* The scheduling queue's nominator (PodNominator), the nominations a PostFilter leaves behind:
+ * the simulator's scheduler records them when DefaultPreemption nominates a node
+ * (simulator/scheduler/plugin/wrappedplugin.go:550-577 returns the PostFilterResult whose
+ * NominatedNodeName the scheduler's handleSchedulingFailure stores).
+ *   kss_nominate          AddNominatedPod: ps.pods[pod_index] is nominated to global node `node`
+ *                         (an earlier nomination of the same pod is replaced).  The pod's identity
+ *                         is its index in the podset the caller schedules from (the staged one
+ *                         for batches, the one passed to kss_eval_pod).  At most 64 entries; pods
+ *                         with volumes are refused.
+ *   kss_clear_nomination  DeleteNominatedPodIfExists (a PostFilter that found no candidate, a
+ *                         lower-priority nomination cleared by prepareCandidate); no-op if absent
+ *   kss_nominations       the entries in AddNominatedPod order (*n = count; cap entries copied)
+ * Every scheduling cycle (kss_eval_pod, batches, kss_postfilter_pod's dry run) then filters with
+ * RunFilterPluginsWithNominatedPods: on a node holding nominees of priority >= the pod's (other
+ * than the pod itself) the filters run first with them added (their requests, pod count, host
+ * ports, and their labels / required anti-affinity terms in the PodTopologySpread and
+ * InterPodAffinity counts of the node's pairs); a failure there is the node's status, otherwise
+ * the plain pass decides.  A nominated pod first evaluates its own node (PreferNominatedNode:
+ * chosen without scoring when it passes; nextStartNodeIndex restarts at 0).  An assumed pod leaves
+ * the nominator (kss_commit, batch commits).  kss_load_cluster / kss_reset_node_state empty it.
+ * While it is non-empty batches run on k_schedule and the service grid, node axis and split
+ * grids refuse (KSS_E_UNSUPPORTED).  Replaces the nominator of the scheduler that
+ * simulator/scheduler/scheduler.go:155-168 creates (pkg/scheduler/internal/queue, v1.26). */
+int kss_nominate(kss_ctx* ctx, const kss_podset* ps, int32_t pod_index, int32_t node);
+int kss_clear_nomination(kss_ctx* ctx, int32_t pod_index);
+int kss_nominations(kss_ctx* ctx, int32_t* pods, int32_t* nodes, int32_t cap, int32_t* n);
+
 /* many independent clusters (what-if scenarios, KEP-184): clusters[s] with podsets[s];
  * one workgroup per scenario, no inter-scenario communication. chosen_out is [sum n_pods].
  * One-shot form of kss_sweep_create + kss_sweep_run + kss_sweep_destroy. */
@@ -721,8 +748,18 @@ typedef struct kss_boundset {
   const int32_t* terms_off;  /* [n] the term_count rows it contributes: ints[terms_off .. +terms_len) */
   const int32_t* terms_len;  /* [n] */
   const int32_t* ints;
+  const int64_t* nonzero;    /* [2][n] NodeInfo.NonZeroRequested cpu / memory contribution, or NULL */
+  const uint64_t* ports;     /* [n] the NodeInfo.UsedPorts bits it holds, or NULL (none) */
 } kss_boundset;
 int kss_load_bound(kss_ctx* ctx, const kss_boundset* bs);
+/* The informer's RemovePod for pods of the bound-pod table -- the victims a PostFilter named, once
+ * the caller deleted them (prepareCandidate; simulator/scheduler/plugin/wrappedplugin.go:550-577
+ * records the nomination): every id (a kss_boundset id, or -1 - i for a pod committed from
+ * ps.pods[i]) leaves the table and its node (Requested, NonZeroRequested, pod count, class and term
+ * counts, host ports).  Loaded pods need the boundset's nonzero array; pods with volumes are
+ * refused (KSS_E_UNSUPPORTED: kss_apply_volume_delta is their sync).  An id not in the table is
+ * KSS_E_INVAL and nothing is removed. */
+int kss_remove_bound(kss_ctx* ctx, const int64_t* ids, int32_t n);
 
 #define KSS_PREEMPT_NOMINATED 0
 #define KSS_PREEMPT_NO_CANDIDATE 1   /* FitError: no node where evicting lower-priority pods helps */

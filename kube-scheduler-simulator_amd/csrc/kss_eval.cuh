@@ -80,6 +80,21 @@ struct DevCluster {
 };
 
 // One node's hot columns, loaded once per (pod, node) into registers.
+// One entry of the scheduling queue's nominator (kss_nominate): a pod nominated to a node by an
+// earlier preemption, with what NodeInfo.AddPodInfo and the AddPod PreFilter extensions need.
+struct DevNom {
+  int32_t node;      // local row
+  int32_t prio;      // corev1helpers.PodPriority
+  int32_t pod;       // the pod's identity: its index in the podset
+  int32_t cls;       // class_count row (labels + namespace)
+  int32_t n_terms;   // term_count rows it contributes
+  int32_t terms[8];
+  int32_t pad;
+  uint64_t ports;    // NodeInfo.UsedPorts bits it adds
+  int64_t req[KSS_NRES];
+};
+constexpr int KSS_NOM_MAX = 64;  // entries (one 64-bit activity mask)
+
 struct NodeRow {
   int64_t alloc[3], req[3], nz[2];
   uint64_t th, ts;
@@ -278,8 +293,15 @@ __device__ __forceinline__ int64_t sum_rows(const int32_t* mat, size_t N, const 
 // First-failing filter among NodeUnschedulable, NodeName, TaintToleration,
 // NodeAffinity, (NodePorts), NodeResourcesFit — the ones that need no per-pod
 // cluster-wide state.  Returns 0 when all of them pass.
+// nom / here: the nominated pods added to the node (RunFilterPluginsWithNominatedPods' first
+// pass: NodeInfo.AddPodInfo of each entry whose bit is set) -- null for the plain pass.
 __device__ __forceinline__ int filter_local(const DevCluster& c, const DevPods& P, const kss_pod& p,
-                                            uint32_t enabled, int n, const NodeRow& row, uint16_t* detail) {
+                                            uint32_t enabled, int n, const NodeRow& row, uint16_t* detail,
+                                            const DevNom* nom = nullptr, uint64_t here = 0) {
+  const int xpods = nom ? __popcll(here) : 0;
+  uint64_t xports = 0;
+  if (nom)
+    for (uint64_t m = here; m; m &= m - 1) xports |= nom[__ffsll((unsigned long long)m) - 1].ports;
   // NodeUnschedulable.Filter
   if ((enabled >> KSS_F_NODE_UNSCHEDULABLE) & 1u) {
     if ((row.flags & KSS_NODE_UNSCHEDULABLE) && !(p.flags & KSS_POD_TOL_UNSCHEDULABLE))
@@ -303,13 +325,13 @@ __device__ __forceinline__ int filter_local(const DevCluster& c, const DevPods& 
   }
   // NodePorts.Filter -> fitsPorts: HostPortInfo.CheckConflict of every wanted port
   if ((enabled >> KSS_F_NODE_PORTS) & 1u) {
-    if (p.port_conflict && (c.port_used[n] & p.port_conflict)) return KSS_F_NODE_PORTS;
+    if (p.port_conflict && ((c.port_used[n] | xports) & p.port_conflict)) return KSS_F_NODE_PORTS;
   }
   // NodeResourcesFit.Filter -> fitsRequest
   if ((enabled >> KSS_F_NODE_RESOURCES_FIT) & 1u) {
     const size_t N = (size_t)c.N;
     uint32_t bits = 0;
-    if ((int64_t)row.pods + 1 > (int64_t)row.allowed) bits |= KSS_FIT_TOO_MANY_PODS;
+    if ((int64_t)row.pods + xpods + 1 > (int64_t)row.allowed) bits |= KSS_FIT_TOO_MANY_PODS;
     const int nr = 3 + c.n_scalar;
     bool all_zero = true;
     for (int r = 0; r < nr; r++) all_zero &= (p.fit_request[r] == 0);
@@ -317,8 +339,10 @@ __device__ __forceinline__ int filter_local(const DevCluster& c, const DevPods& 
       for (int r = 0; r < nr; r++) {
         const int64_t req = p.fit_request[r];
         if (r >= KSS_RES_SCALAR0 && req == 0) continue;
-        const int64_t freev = r < 3 ? pick3(row.alloc, r) - pick3(row.req, r)
-                                    : c.alloc[(size_t)r * N + n] - c.requested[(size_t)r * N + n];
+        int64_t freev = r < 3 ? pick3(row.alloc, r) - pick3(row.req, r)
+                              : c.alloc[(size_t)r * N + n] - c.requested[(size_t)r * N + n];
+        if (nom)
+          for (uint64_t m = here; m; m &= m - 1) freev -= nom[__ffsll((unsigned long long)m) - 1].req[r];
         if (req > freev) bits |= 1u << (r + 1);
       }
     }

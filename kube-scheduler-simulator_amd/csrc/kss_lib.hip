@@ -113,6 +113,9 @@ struct DevJob {
   kss_profile prof;   // k_simple<false>: staged word by word into LDS (a by-value kernel argument would land in scratch)
   GTrace trace;       // k_spread diagnostic trace (KSS_SPREAD_TRACE builds only; null otherwise)
   int32_t* cursor;    // k_schedule / the service: the cluster's nextStartNodeIndex word (null: 0, not kept)
+  const DevNom* nom;  // k_schedule: the nominator's entries (kss_nominate), all nominated at launch
+  int32_t n_nom;      // entries (<= KSS_NOM_MAX; 0: none)
+  int32_t pod_base;   // the identity of pod pi is pod_base + pi (its index in the caller's podset)
 };
 
 }  // namespace
@@ -162,9 +165,11 @@ __global__ __launch_bounds__(KSS_MAX_THREADS) void k_schedule(const DevJob* __re
     cache_fill(c, S.hi, c.ncl ? c.n_keys : 0);
     __syncthreads();
   }
+  NomView nv{job.nom, job.n_nom, -1, job.n_nom >= 64 ? ~0ull : ((1ull << job.n_nom) - 1ull)};
   for (int pi = 0; pi < job.n_pods; pi++) {
     uint8_t* base = job.slots + (job.record ? (size_t)pi * job.slot_bytes : 0);
     Slot s;
+    nv.pod = job.pod_base + pi;
     s.fail = base + L.fail;
     s.detail = (uint16_t*)(base + L.detail);
     s.raw = (int64_t*)(base + L.raw);
@@ -173,8 +178,12 @@ __global__ __launch_bounds__(KSS_MAX_THREADS) void k_schedule(const DevJob* __re
     PodMeta m;
     S.stamps = (stamps && ji == 0 && w == 0 && pi < KSS_NSTAMP_PODS) ? stamps + (size_t)pi * 8 : nullptr;
     KSS_STAMP(S, 0);
-    if (!schedule_pod<GEN>(c, job.P, prof, pi, smem, S, bins_cap, npt, want_out ? &s : nullptr, job.keep_norm != 0, m))
+    if (!schedule_pod<GEN>(c, job.P, prof, pi, smem, S, bins_cap, npt, want_out ? &s : nullptr, job.keep_norm != 0, m,
+                           nv))
       return;  // exchange timeout: the error word is set, leave the launch
+    if (job.commit && m.chosen >= 0)  // assume -> DeleteNominatedPodIfExists (every shard knows the choice)
+      for (int j = 0; j < nv.n; j++)
+        if (job.nom[j].pod == nv.pod) nv.active &= ~(1ull << j);
     if (threadIdx.x == 0) {
       if (w == 0) {
         if (job.chosen) job.chosen[pi] = m.chosen;
@@ -543,8 +552,12 @@ struct BoundPod {
   int64_t id;
   int64_t start;
   int64_t req[KSS_NRES];
+  int64_t nz[2];     // NonZeroRequested cpu / memory (valid when has_nz)
+  uint64_t ports;    // UsedPorts bits it holds
   int32_t prio, cls, tlen;
   int32_t terms[8];
+  int32_t has_nz;    // the loaded boundset carried nonzero (kss_remove_bound needs it)
+  int32_t has_vols;  // a committed pod with volumes (kss_remove_bound refuses it)
 };
 // A commit (add) or rollback (remove) applied to the loaded table, in call order.
 struct BoundOp {
@@ -586,6 +599,12 @@ struct kss_ctx {
   std::vector<uint32_t> key_flags_h;
   DevBuf gran_buf, err_buf;
   DevBuf cursor_buf;  // nextStartNodeIndex (one int32), kept on the device across launches
+  // the scheduling queue's nominator (kss_nominate): host mirror in AddNominatedPod order, uploaded
+  // before a launch that reads it; run_pod_base = the podset index of the launch's pod 0
+  std::vector<DevNom> nom;
+  DevBuf nom_buf;
+  bool nom_dirty = true;
+  int32_t run_pod_base = 0;
   DevBuf ck_buf;                    // k_spread's checked hand-off between chunks: {sum, tag} per shard
   unsigned long long ck_seq = 0;    // the last tag a chunk wrote
   int last_handoff_retries = 0;     // prologue loads repeated in the last run (HandoffCheck)
@@ -1642,6 +1661,8 @@ int kss_load_cluster(kss_ctx* ctx, const kss_cluster* cl) {
   ctx->bound0_node.clear();
   ctx->bound_log.clear();
   ctx->bound_dirty = true;
+  ctx->nom.clear();
+  ctx->nom_dirty = true;
   ctx->state_unknown = false;
   ctx->recorded = 0;
   ctx->meta_n = 0;
@@ -1737,6 +1758,7 @@ int kss_axis_eval(kss_ctx* ctx, int32_t pod_index, int64_t* stats_dev, const int
   KSS_SVC_QUIESCE(ctx);
   int rc = axis_check(ctx, pod_index);
   if (rc) return rc;
+  if (!ctx->nom.empty()) return fail(KSS_E_UNSUPPORTED, "the node axis does not read the nominator");
   if (!stats_dev || !key_zero_dev || world < 1) return fail(KSS_E_INVAL, "bad eval arguments");
   if (prev_key_dev && (pod_index < 1 || !prev_gathered_dev)) return fail(KSS_E_INVAL, "pending commit without a previous pod");
   std::lock_guard<std::mutex> lk(ctx->mu);
@@ -1816,6 +1838,8 @@ int kss_reset_node_state(kss_ctx* ctx) {
     HIP_TRY(hipGetLastError());
   }
   HIP_TRY(dev_zero(ctx->cursor_buf.p, 16, ctx->stream));  // the simulator's reset starts a new scheduler
+  ctx->nom.clear();  // ... with an empty scheduling queue (no nominator entries)
+  ctx->nom_dirty = true;
   HIP_TRY(hipStreamSynchronize(ctx->stream));
   return 0;
 }
@@ -1827,6 +1851,65 @@ int kss_next_start_node_index(kss_ctx* ctx, int32_t* out) {
   HIP_TRY(hipSetDevice(ctx->cfg.device));
   HIP_TRY(hipMemcpyAsync(out, ctx->cursor_buf.p, sizeof(int32_t), hipMemcpyDeviceToHost, ctx->stream));
   HIP_TRY(hipStreamSynchronize(ctx->stream));
+  return 0;
+}
+
+int kss_nominate(kss_ctx* ctx, const kss_podset* ps, int32_t pod_index, int32_t node) {
+  KSS_SVC_QUIESCE(ctx);
+  if (!ctx || !ctx->loaded || !ps) return fail(KSS_E_INVAL, "bad arguments");
+  if (pod_index < 0 || pod_index >= ps->n_pods) return fail(KSS_E_INVAL, "pod index out of range");
+  const int local = node - ctx->dc.node_base;
+  if (local < 0 || local >= ctx->dc.N) return fail(KSS_E_INVAL, "node out of range");
+  if (ctx->split_n > 1) return fail(KSS_E_UNSUPPORTED, "split grids do not read the nominator");
+  const kss_pod& p = ps->pods[pod_index];
+  if (p.vol_len > 0) return fail(KSS_E_UNSUPPORTED, "a nominated pod with volumes (the volume filters do not add nominees)");
+  if (p.cls < 0 || p.cls >= ctx->host.n_classes) return fail(KSS_E_INVAL, "pod class out of range");
+  if (p.own_terms_len < 0 || p.own_terms_off < 0 || p.own_terms_off + p.own_terms_len > ps->n_ints)
+    return fail(KSS_E_INVAL, "own terms out of range");
+  if (p.own_terms_len > 8) return fail(KSS_E_UNSUPPORTED, "a nominated pod with more than 8 own term rows");
+  if (ctx->host.n_ports < KSS_MAX_PORTS && (p.port_add >> ctx->host.n_ports))
+    return fail(KSS_E_INVAL, "pod port bit outside the port dictionary");
+  DevNom e{};
+  e.node = local;
+  e.prio = p.priority;
+  e.pod = pod_index;
+  e.cls = p.cls;
+  e.n_terms = p.own_terms_len;
+  for (int t = 0; t < p.own_terms_len; t++) {
+    e.terms[t] = ps->ints[p.own_terms_off + t];
+    if (e.terms[t] < 0 || e.terms[t] >= ctx->host.n_terms) return fail(KSS_E_INVAL, "own term id out of range");
+  }
+  e.ports = p.port_add;
+  for (int r = 0; r < KSS_NRES; r++) e.req[r] = p.commit_req[r];
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  // AddNominatedPod: an earlier nomination of the pod is replaced (it moves to the end)
+  ctx->nom.erase(std::remove_if(ctx->nom.begin(), ctx->nom.end(), [&](const DevNom& x) { return x.pod == pod_index; }),
+                 ctx->nom.end());
+  if ((int)ctx->nom.size() >= KSS_NOM_MAX) return fail(KSS_E_UNSUPPORTED, "more than 64 nominated pods");
+  ctx->nom.push_back(e);
+  ctx->nom_dirty = true;
+  return 0;
+}
+
+int kss_clear_nomination(kss_ctx* ctx, int32_t pod_index) {
+  KSS_SVC_QUIESCE(ctx);
+  if (!ctx) return fail(KSS_E_INVAL, "bad arguments");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  const size_t before = ctx->nom.size();
+  ctx->nom.erase(std::remove_if(ctx->nom.begin(), ctx->nom.end(), [&](const DevNom& x) { return x.pod == pod_index; }),
+                 ctx->nom.end());
+  if (ctx->nom.size() != before) ctx->nom_dirty = true;
+  return 0;
+}
+
+int kss_nominations(kss_ctx* ctx, int32_t* pods, int32_t* nodes, int32_t cap, int32_t* n) {
+  if (!ctx || !n || cap < 0 || (cap > 0 && (!pods || !nodes))) return fail(KSS_E_INVAL, "bad arguments");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  *n = (int32_t)ctx->nom.size();
+  for (int i = 0; i < *n && i < cap; i++) {
+    pods[i] = ctx->nom[i].pod;
+    nodes[i] = ctx->dc.node_base + ctx->nom[i].node;
+  }
   return 0;
 }
 
@@ -2603,7 +2686,11 @@ static int run_single_impl(kss_ctx* ctx, const PlanNeeds& need, const DevPods& d
   // nextStartNodeIndex) runs on k_schedule only; its per-shard count exchange needs W + 1 values
   const bool window = ctx->prof.pct_nodes_to_score < 100;
   if (window) W = std::min(W, XW_MAX - NSCAL);
-  const bool simple_ok = !window && staged && ctx->spod_ok && commit && !record && !keep_norm && !need.general &&
+  // nominated pods (kss_nominate): RunFilterPluginsWithNominatedPods and PreferNominatedNode run on
+  // k_schedule only
+  const bool nomq = !ctx->nom.empty();
+  if (nomq && split) return fail(KSS_E_UNSUPPORTED, "split grids do not read the nominator");
+  const bool simple_ok = !window && !nomq && staged && ctx->spod_ok && commit && !record && !keep_norm && !need.general &&
                          scalar_fast_ok(ctx->prof, ctx->dc.n_scalar) && ctx->small_values && f64_exact(ctx->f64_cluster, ctx->f64_pods, n) &&
                          !ctx->no_simple && !(flags & KSS_SCHED_GENERAL_KERNEL);
   if (simple_ok && ctx->force_w <= 0 && !split) W = std::min(W, 64 * SX_CHUNKS);
@@ -2618,7 +2705,7 @@ static int run_single_impl(kss_ctx* ctx, const PlanNeeds& need, const DevPods& d
   // a batch with programs on k_spread: 32-bit counts and scores (spread_bounds_ok)
   const double count_total = ctx->count_bound + (commit ? (double)n * (1.0 + ctx->staged_max_own) : 0.0);
   const double cell_total = ctx->cell_bound + (commit ? (double)n * ctx->gneed.max_mult : 0.0);
-  const bool spread_ok = !window && staged && ctx->gpod_ok && commit && !record && !keep_norm && need.general &&
+  const bool spread_ok = !window && !nomq && staged && ctx->gpod_ok && commit && !record && !keep_norm && need.general &&
                          scalar_fast_ok(ctx->prof, ctx->dc.n_scalar) && ctx->small_values && f64_exact(ctx->f64_cluster, ctx->f64_pods, n) &&
                          !ctx->no_simple && !ctx->no_spread && !(flags & KSS_SCHED_GENERAL_KERNEL) &&
                          spread_bounds_ok(ctx->gneed, count_total, cell_total, (int)N);
@@ -2724,6 +2811,17 @@ static int run_single_impl(kss_ctx* ctx, const PlanNeeds& need, const DevPods& d
   job.res_rows = spread ? (const int32_t*)ctx->res_buf.p : nullptr;
   job.trace = GTrace{nullptr, nullptr};
   job.cursor = (int32_t*)ctx->cursor_buf.p;
+  if (nomq) {
+    if (ctx->nom_dirty) {
+      if ((rc = ctx->nom_buf.ensure(sizeof(DevNom) * ctx->nom.size()))) return rc;
+      HIP_TRY(hipMemcpyAsync(ctx->nom_buf.p, ctx->nom.data(), sizeof(DevNom) * ctx->nom.size(), hipMemcpyHostToDevice,
+                             ctx->stream));
+      ctx->nom_dirty = false;
+    }
+    job.nom = (const DevNom*)ctx->nom_buf.p;
+    job.n_nom = (int32_t)ctx->nom.size();
+  }
+  job.pod_base = ctx->run_pod_base;
 #if KSS_SPREAD_TRACE
   if (spread) {  // every pod and shard, and the list of nonzero counts loaded / written back
     ctx->trace_words = (size_t)n * (size_t)g.W * G_TW;
@@ -3129,8 +3227,11 @@ static int eval_pod_slot(kss_ctx* ctx, const kss_podset* ps, int32_t pod_index, 
   if (rc) return rc;
   const PlanNeeds need = plan_needs(ctx->key_card_h.data(), ctx->key_flags_h.data(), &one.ps, 1);
   rbk.bytes = r.hi > r.lo ? r.hi : 0;  // slot bytes [0, r.hi) ride in the one copy
-  return run_single(ctx, need, ctx->tdp, 1, /*commit=*/false, /*record=*/false, /*keep_norm=*/true, 0, nullptr,
-                    /*staged=*/false, &rbk, &pu);
+  ctx->run_pod_base = pod_index;  // the uploaded pod is pod_index of the caller's podset (nominator identity)
+  rc = run_single(ctx, need, ctx->tdp, 1, /*commit=*/false, /*record=*/false, /*keep_norm=*/true, 0, nullptr,
+                  /*staged=*/false, &rbk, &pu);
+  ctx->run_pod_base = 0;
+  return rc;
 }
 
 int kss_eval_pod(kss_ctx* ctx, const kss_podset* ps, int32_t pod_index, kss_pod_result* out) {
@@ -3177,6 +3278,11 @@ static BoundPod bound_from_pod(const kss_podset* ps, int i) {
   b.id = -1 - (int64_t)i;
   b.start = KSS_START_UNSET;
   for (int r = 0; r < KSS_NRES; r++) b.req[r] = p.commit_req[r];
+  b.nz[0] = p.commit_nz[0];
+  b.nz[1] = p.commit_nz[1];
+  b.ports = p.port_add;
+  b.has_nz = 1;
+  b.has_vols = p.vol_len > 0 ? 1 : 0;
   b.prio = p.priority;
   b.cls = p.cls;
   b.tlen = std::min(p.own_terms_len, 8);
@@ -3189,8 +3295,23 @@ static void stage_bound(kss_ctx* ctx, const kss_podset* ps) {
   for (int i = 0; i < ps->n_pods; i++) ctx->staged_bp[i] = bound_from_pod(ps, i);
 }
 
+// SchedulingQueue.DeleteNominatedPodIfExists for every assumed pod of a batch (the device did the
+// same for its own copy as it went)
+static void drop_committed_nominations(kss_ctx* ctx, int n) {
+  if (ctx->nom.empty()) return;
+  const size_t before = ctx->nom.size();
+  ctx->nom.erase(std::remove_if(ctx->nom.begin(), ctx->nom.end(),
+                                [&](const DevNom& e) {
+                                  const int i = e.pod - ctx->run_pod_base;
+                                  return i >= 0 && i < n && ctx->meta_host[i].chosen >= 0;
+                                }),
+                 ctx->nom.end());
+  if (ctx->nom.size() != before) ctx->nom_dirty = true;
+}
+
 // the batch's AssumePods, as NodeInfo.AddPod appends them
 static void log_batch_commits(kss_ctx* ctx, int n) {
+  drop_committed_nominations(ctx, n);
   for (int i = 0; i < n && i < (int)ctx->staged_bp.size(); i++) {
     const int local = ctx->meta_host[i].chosen - ctx->dc.node_base;
     if (local >= 0 && local < ctx->dc.N) ctx->bound_log.push_back(BoundOp{local, 1, ctx->staged_bp[i]});
@@ -3247,6 +3368,12 @@ static int commit_one(kss_ctx* ctx, const kss_podset* ps, int32_t pod_index, int
   }
   hipLaunchKernelGGL(k_commit, dim3(1), dim3(64), 0, ctx->stream, ctx->dc, a);
   HIP_TRY(hipGetLastError());  // no synchronisation: every later call on the ctx stream is ordered after it
+  if (sign > 0) {  // assume -> SchedulingQueue.DeleteNominatedPodIfExists
+    const size_t before = ctx->nom.size();
+    ctx->nom.erase(std::remove_if(ctx->nom.begin(), ctx->nom.end(), [&](const DevNom& e) { return e.pod == pod_index; }),
+                   ctx->nom.end());
+    if (ctx->nom.size() != before) ctx->nom_dirty = true;
+  }
   ctx->bound_log.push_back(BoundOp{local, sign > 0 ? 1 : 0, bound_from_pod(ps, pod_index)});
   ctx->bound_dirty = true;
   return 0;
@@ -3395,6 +3522,8 @@ static int svc_start_locked(kss_ctx* ctx) {
   if (!ctx->loaded) return fail(KSS_E_INVAL, "no cluster loaded");
   if (ctx->staged_n <= 0) return fail(KSS_E_INVAL, "the service evaluates staged pods: kss_stage_pods first");
   if (ctx->split_n > 1) return fail(KSS_E_UNSUPPORTED, "the service runs the whole cluster on one device");
+  if (!ctx->nom.empty())
+    return fail(KSS_E_UNSUPPORTED, "the service grid does not read the nominator: kss_eval_pod / batches while pods are nominated");
   auto& v = ctx->svc;
   HIP_TRY(hipSetDevice(ctx->cfg.device));
   HIP_TRY(hipStreamSynchronize(ctx->stream));  // every earlier launch / copy on the ctx stream is done
@@ -4185,6 +4314,14 @@ int kss_load_bound(kss_ctx* ctx, const kss_boundset* bs) {
     b.prio = bs->priority[i];
     b.cls = bs->cls[i];
     b.tlen = bs->terms_len[i];
+    if (bs->nonzero) {
+      b.nz[0] = bs->nonzero[i];
+      b.nz[1] = bs->nonzero[(size_t)bs->n + i];
+      b.has_nz = 1;
+    }
+    b.ports = bs->ports ? bs->ports[i] : 0;
+    if (ctx->host.n_ports < KSS_MAX_PORTS && (b.ports >> ctx->host.n_ports))
+      return fail(KSS_E_INVAL, "bound pod port bit outside the port dictionary");
     for (int t = 0; t < b.tlen; t++) {
       b.terms[t] = bs->ints[bs->terms_off[i] + t];
       if (b.terms[t] < 0 || b.terms[t] >= ctx->host.n_terms) return fail(KSS_E_INVAL, "bound pod term row out of range");
@@ -4196,6 +4333,46 @@ int kss_load_bound(kss_ctx* ctx, const kss_boundset* bs) {
   ctx->bound0.swap(rows);
   ctx->bound0_node.swap(nodes);
   ctx->bound_log.clear();
+  ctx->bound_dirty = true;
+  return 0;
+}
+
+int kss_remove_bound(kss_ctx* ctx, const int64_t* ids, int32_t n) {
+  KSS_SVC_QUIESCE(ctx);
+  if (!ctx || !ctx->loaded || n < 0 || (n > 0 && !ids)) return fail(KSS_E_INVAL, "bad arguments");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  // the table as it stands: the loaded rows, then the commits / rollbacks in call order
+  std::vector<std::pair<int32_t, BoundPod>> found((size_t)n, {-1, BoundPod{}});
+  auto see = [&](int32_t node, const BoundPod& b, bool add) {
+    for (int i = 0; i < n; i++)
+      if (ids[i] == b.id) found[i] = add ? std::make_pair(node, b) : std::make_pair(-1, BoundPod{});
+  };
+  for (size_t i = 0; i < ctx->bound0.size(); i++) see(ctx->bound0_node[i], ctx->bound0[i], true);
+  for (const BoundOp& op : ctx->bound_log) see(op.node, op.b, op.add != 0);
+  for (int i = 0; i < n; i++) {
+    if (found[i].first < 0) return fail(KSS_E_INVAL, "id not in the bound-pod table");
+    for (int j = 0; j < i; j++)
+      if (ids[j] == ids[i]) return fail(KSS_E_INVAL, "id listed twice");
+    if (!found[i].second.has_nz) return fail(KSS_E_UNSUPPORTED, "bound pod loaded without nonzero requests");
+    if (found[i].second.has_vols) return fail(KSS_E_UNSUPPORTED, "bound pod with volumes (kss_apply_volume_delta)");
+  }
+  HIP_TRY(hipSetDevice(ctx->cfg.device));
+  for (int i = 0; i < n; i++) {
+    const BoundPod& b = found[i].second;
+    CommitArgs a{};
+    for (int r = 0; r < KSS_NRES; r++) a.req[r] = b.req[r];
+    a.nz[0] = b.nz[0];
+    a.nz[1] = b.nz[1];
+    a.port_add = b.ports;
+    a.cls = b.cls;
+    a.n_own = b.tlen;
+    for (int t = 0; t < b.tlen; t++) a.own[t] = b.terms[t];
+    a.local = found[i].first;
+    a.sign = -1;
+    hipLaunchKernelGGL(k_commit, dim3(1), dim3(64), 0, ctx->stream, ctx->dc, a);
+    HIP_TRY(hipGetLastError());
+    ctx->bound_log.push_back(BoundOp{found[i].first, 0, b});
+  }
   ctx->bound_dirty = true;
   return 0;
 }
@@ -4361,6 +4538,17 @@ int kss_postfilter_pod(kss_ctx* ctx, const kss_podset* ps, int32_t pod_index, ks
     hp.ipa = one.ps.ipa;
     J.plan_ok = make_plan(hc, hp, one.ps.pods[0], J.plan, bins_cap) ? 1 : 0;
   }
+  if (!ctx->nom.empty()) {  // RunFilterPluginsWithNominatedPods in every dry-run filter call
+    if (ctx->nom_dirty) {
+      if ((rc = ctx->nom_buf.ensure(sizeof(DevNom) * ctx->nom.size()))) return rc;
+      HIP_TRY(hipMemcpyAsync(ctx->nom_buf.p, ctx->nom.data(), sizeof(DevNom) * ctx->nom.size(), hipMemcpyHostToDevice,
+                             ctx->stream));
+      ctx->nom_dirty = false;
+    }
+    J.nom = (const DevNom*)ctx->nom_buf.p;
+    J.n_nom = (int32_t)ctx->nom.size();
+  }
+  J.pod_id = pod_index;
   J.key = (int64_t*)(d + o_key);
   J.n_blocks = (int32_t)std::max<size_t>((N + PRE_NODE_THREADS - 1) / PRE_NODE_THREADS, 1);
   J.victims = (int64_t*)(d + o_vic);

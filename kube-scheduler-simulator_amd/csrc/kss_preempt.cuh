@@ -30,7 +30,9 @@
 //      then over the workgroups' tuples;
 //   5. one lane re-runs the nominated node's reprieve loop and writes the victims' ids in
 //      eviction order.
-// No PodDisruptionBudgets (every victim is non-violating) and no nominated pods.
+// No PodDisruptionBudgets (every victim is non-violating).  Every filter call is
+// RunFilterPluginsWithNominatedPods: the nominator's pods of priority >= the preemptor's on the
+// node take part in a first pass (kss_sched.cuh NomView); they are never victims.
 #pragma once
 #include "kss_sched.cuh"
 
@@ -91,9 +93,13 @@ struct PreemptJob {
   PreemptOut* out;
   PreGlobal* G;
   long long* gbins;  // [bins_cap] the PreFilter histograms and presence bins
+  const DevNom* nom; // the nominator (kss_nominate): RunFilterPluginsWithNominatedPods' first pass
+  int32_t n_nom;
+  int32_t pod_id;    // the preemptor's identity (its podset index: it is never its own nominee)
 };
 
 struct PreHdr {
+  NomPts npts;  // nominees: the pairs at each hard owner's minimum and the next count (from m0 / m1)
   long long red[PRE_WAVES];
   kss_pod pod;
   Plan plan;
@@ -190,6 +196,45 @@ __device__ __forceinline__ void apply_pod(const PreemptJob& J, const kss_pod& p,
   }
 }
 
+// AddPod of nominee q on node n (addNominatedPods: NodeInfo.AddPodInfo and the AddPod extensions),
+// the same updates apply_pod makes for a bound pod
+__device__ __forceinline__ void apply_nom(const PreemptJob& J, const kss_pod& p, const Plan& pl, const DevNom& q, int n,
+                                          DryState& s) {
+  const DevCluster& c = J.c;
+  const DevPods& P = J.P;
+  const int nr = 3 + c.n_scalar;
+#pragma unroll
+  for (int r = 0; r < KSS_NRES; r++)
+    if (r < nr) s.req[r] += q.req[r];
+  s.pods += 1;
+  const kss_spread* sp = P.spreads + p.spread_off;
+  for (int j = 0; j < p.n_hard; j++) {
+    if (!in_list(P.ints, sp[j].cls_off, sp[j].cls_len, q.cls)) continue;
+    const int o = pl.hard_own[j];
+#pragma unroll
+    for (int x = 0; x < MAXH; x++) s.M[x] += x == o ? 1 : 0;
+  }
+  const kss_ipa* ip = P.ipa + p.ipa_off;
+  for (int e = 0; e < p.ipa_len; e++) {
+    const kss_ipa& en = ip[e];
+    if (en.kind > KSS_IPA_REQ_ANTI) continue;
+    if (label_of(c, en.key, n) < 0) continue;
+    const int k = slot_of(pl, en.key);
+    int d = 0, h = 0;
+    if (en.kind == KSS_IPA_EXISTING_ANTI) {
+      for (int t = 0; t < q.n_terms; t++) d += in_list(P.ints, en.row_off, en.row_len, q.terms[t]) ? 1 : 0;
+    } else if (in_list(P.ints, en.row_off, en.row_len, q.cls)) {
+      d = 1;
+      h = en.kind == KSS_IPA_REQ_AFFINITY ? 1 : 2;
+      if (en.kind == KSS_IPA_REQ_AFFINITY) s.T += 1;
+    }
+#pragma unroll
+    for (int x = 0; x < MAXK; x++)
+#pragma unroll
+      for (int y = 0; y < 3; y++) s.A[x][y] += (x == k && y == h) ? d : 0;
+  }
+}
+
 // s.M[o] / s.A[k][h] for runtime o, k (selects over the unrolled indices: no scratch)
 __device__ __forceinline__ int64_t dry_m(const DryState& s, int o) {
   int64_t v = 0;
@@ -261,6 +306,18 @@ __device__ __forceinline__ bool dry_fits(const PreemptJob& J, const kss_pod& p, 
   return true;
 }
 
+// RunFilterPluginsWithNominatedPods over the dry-run view: with nominees on the node (here) the
+// first pass runs with them added, the plain pass decides when it passes
+__device__ __forceinline__ bool dry_fits_nom(const PreemptJob& J, const kss_pod& p, const Plan& pl, const PreHdr& H,
+                                             const DryState& s, int n, uint64_t here) {
+  if (here) {
+    DryState s1 = s;
+    for (uint64_t m = here; m; m &= m - 1) apply_nom(J, p, pl, J.nom[__ffsll((unsigned long long)m) - 1], n, s1);
+    if (!dry_fits(J, p, pl, H, s1, n)) return false;
+  }
+  return dry_fits(J, p, pl, H, s, n);
+}
+
 struct DryResult {
   int64_t hp, sum, cnt, start;  // hp = INT64_MAX: not a candidate
 };
@@ -268,7 +325,7 @@ struct DryResult {
 // SelectVictimsOnNode for node n; ids (optional): the victims' ids in eviction order
 __device__ __forceinline__ DryResult select_victims(const PreemptJob& J, const kss_pod& p, const Plan& pl,
                                                     const PreHdr& H, const long long* bins, int n, int64_t* ids,
-                                                    int ids_cap) {
+                                                    int ids_cap, uint64_t here) {
   const DevCluster& c = J.c;
   const DevPods& P = J.P;
   const DevBound& B = J.B;
@@ -315,14 +372,14 @@ __device__ __forceinline__ DryResult select_victims(const PreemptJob& J, const k
   }
   s.T = H.aff_total;
   for (int k = p0; k < e1; k++) apply_pod(J, p, pl, k, n, -1, s);
-  if (!dry_fits(J, p, pl, H, s, n)) return res;
+  if (!dry_fits_nom(J, p, pl, H, s, n, here)) return res;
   // reprieve in importance order (MoreImportantPod, NodeInfo order on ties)
   int victims = 0;
   int64_t hp = 0, sum = 0, st = 0;
   for (int k = p0; k < e1; k++) {
     const int best = k;
     apply_pod(J, p, pl, best, n, 1, s);
-    if (!dry_fits(J, p, pl, H, s, n)) {
+    if (!dry_fits_nom(J, p, pl, H, s, n, here)) {
       apply_pod(J, p, pl, best, n, -1, s);
       if (victims == 0) {
         hp = B.prio[best];
@@ -585,6 +642,10 @@ __device__ void preempt_nodes(const PreemptJob& J, long long* smem) {
     }
     H.aff_total = G.aff_total;
     H.flags = G.flags;
+    for (int i = 0; i < MAXH; i++) {  // criticalPaths' two smallest: another pair at the minimum, or the next count
+      H.npts.cnt[i] = G.m1[i] == G.m0[i] ? 2 : 1;
+      H.npts.gt[i] = G.m1[i];
+    }
   }
   __syncthreads();
   const kss_pod& p = H.pod;
@@ -602,28 +663,39 @@ __device__ void preempt_nodes(const PreemptJob& J, long long* smem) {
     if (p.names_len >= 0 && !in_names(P, p, (int64_t)c.node_base + n)) {
       n_pot = 1;  // no status in the map: potential, but NodeAffinity rejects it in the dry run
     } else {
-      uint16_t detail = 0;
+      // the scheduling cycle's status of the node: RunFilterPluginsWithNominatedPods
+      const NomView nv{J.nom, J.n_nom, J.pod_id, J.n_nom >= 64 ? ~0ull : ((1ull << J.n_nom) - 1ull)};
+      const uint64_t here = J.n_nom ? nom_here(nv, n, p.priority) : 0;
       const NodeRow row = load_row(c, n);
-      int f = filter_local(c, P, p, en, n, row, &detail);
-      if (!f && ((en >> KSS_F_POD_TOPOLOGY_SPREAD) & 1u) && p.n_hard > 0) {
-        const int r = filter_pts(c, P, p, pl, bins, hard_min, n);
-        if (r) {
-          f = KSS_F_POD_TOPOLOGY_SPREAD;
-          detail = (uint16_t)(r - 1);
+      int f = 0;
+      uint16_t detail = 0;
+      for (int pass = here ? 0 : 1; pass < 2; pass++) {  // pass 0: the nominees added
+        const NomView* v = pass == 0 ? &nv : nullptr;
+        uint16_t dd = 0;
+        int ff = filter_local(c, P, p, en, n, row, &dd, v ? J.nom : nullptr, pass == 0 ? here : 0);
+        if (!ff && ((en >> KSS_F_POD_TOPOLOGY_SPREAD) & 1u) && p.n_hard > 0) {
+          const int r = filter_pts(c, P, p, pl, bins, hard_min, n, v, here, &H.npts);
+          if (r) {
+            ff = KSS_F_POD_TOPOLOGY_SPREAD;
+            dd = (uint16_t)(r - 1);
+          }
         }
-      }
-      if (!f && ((en >> KSS_F_INTER_POD_AFFINITY) & 1u) && p.ipa_len > 0) {
-        const int r = filter_ipa(c, P, p, pl, bins, H.flags, n);
-        if (r) {
-          f = KSS_F_INTER_POD_AFFINITY;
-          detail = (uint16_t)(r - 1);
+        if (!ff && ((en >> KSS_F_INTER_POD_AFFINITY) & 1u) && p.ipa_len > 0) {
+          const int r = filter_ipa(c, P, p, pl, bins, H.flags, n, v, here);
+          if (r) {
+            ff = KSS_F_INTER_POD_AFFINITY;
+            dd = (uint16_t)(r - 1);
+          }
         }
+        f = ff;
+        detail = dd;
+        if (ff) break;  // a first-pass failure is the node's status
       }
       if (!f) {
         feasible = 1;
       } else if (resolvable(f, detail)) {
         n_pot = 1;
-        const DryResult d = select_victims(J, p, pl, H, bins, n, J.vscratch + J.B.ptr[n], INT32_MAX);
+        const DryResult d = select_victims(J, p, pl, H, bins, n, J.vscratch + J.B.ptr[n], INT32_MAX, here);
         if (d.hp != INT64_MAX) {
           n_cand = 1;
           best = d;

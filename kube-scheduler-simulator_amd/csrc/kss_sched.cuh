@@ -95,8 +95,16 @@ struct Plan {
   bool need_stats;
 };
 
+// Nominated pods: per hard spread owner, the pairs at the critical-path minimum and the smallest
+// count above it (uniform over the workgroup: kept in LDS, see NomView below)
+struct NomPts {
+  long long cnt[MAXH];  // pairs whose count equals the minimum (only 1 vs more matters)
+  long long gt[MAXH];   // the smallest pair count above the minimum (INT32_MAX: none)
+};
+
 // Dynamic LDS image (Guideline 17: one 16-byte aligned dynamic region, no statics).
 struct SharedHdr {
+  NomPts npts;
   long long red[MAXWAVES][NSCAL];
   kss_pod pod;  // the current pod's record, copied once per pod
   Plan plan;    // computed by lane 0 of the workgroup each pod, read by all
@@ -501,31 +509,132 @@ __device__ __forceinline__ int64_t ipa_value(const DevCluster& c, const DevPods&
   return s;
 }
 
-// PodTopologySpread.Filter (hard constraints) — returns detail+1 on failure, 0 on pass
-__device__ __forceinline__ int filter_pts(const DevCluster& c, const DevPods& P, const kss_pod& p, const Plan& pl,
-                                          const long long* bins, const long long (&hard_min)[MAXH], int n) {
+// ---------------------------------------------------------------------------
+// Nominated pods (the scheduling queue's nominator, kss_nominate).  RunFilterPluginsWithNominatedPods
+// (v1.26 runtime/framework.go) runs a node's filters first with the nominees of equal or higher
+// priority (other than the pod itself) added -- addNominatedPods: NodeInfo.AddPodInfo plus the
+// AddPod PreFilter extensions, which move only the node's own pairs -- and, when that passes, again
+// on the plain node.  NomView is the table and the entries still nominated in this launch (an
+// entry leaves when its pod is assumed: DeleteNominatedPodIfExists); NomPts, per hard spread
+// owner, the pairs at the critical-path minimum and the smallest count above it, so that the
+// minimum after the node's pair grows is min(the other pairs' minimum, the new count) -- what
+// criticalPaths.update keeps when one pair changes.
+// ---------------------------------------------------------------------------
+struct NomView {
+  const DevNom* e;
+  int n;            // entries (0: no nominator, every nominee path compiles away at run time)
+  int pod;          // the pod's identity (podset index)
+  uint64_t active;  // entries still nominated
+};
+
+// the nominees RunFilterPluginsWithNominatedPods adds on node n for a pod of priority prio
+__device__ __forceinline__ uint64_t nom_here(const NomView& nv, int n, int prio) {
+  uint64_t m = 0;
+  for (int j = 0; j < nv.n; j++) {
+    const DevNom& e = nv.e[j];
+    if (((nv.active >> j) & 1u) && e.node == n && e.pod != nv.pod && e.prio >= prio) m |= 1ull << j;
+  }
+  return m;
+}
+
+// podtopologyspread updateWithPod for hard owner o: one per matching constraint of the group, per nominee
+__device__ __forceinline__ int64_t nom_pts_delta(const DevPods& P, const kss_pod& p, const Plan& pl, const NomView& nv,
+                                                 uint64_t here, int o) {
   const kss_spread* sp = P.spreads + p.spread_off;
+  int64_t dl = 0;
+  for (uint64_t m = here; m; m &= m - 1) {
+    const int cls = nv.e[__ffsll((unsigned long long)m) - 1].cls;
+    for (int j = o; j < p.n_hard; j++)
+      if (pl.hard_own[j] == o) {
+        for (int i = 0; i < sp[j].cls_len; i++) dl += P.ints[sp[j].cls_off + i] == cls ? 1 : 0;
+      }
+  }
+  return dl;
+}
+
+// interpodaffinity updateWithPod on histogram (key, kind): the nominees' required anti-affinity terms
+// matching the pod (existing anti), or their class matching the pod's terms (affinity / anti)
+__device__ __forceinline__ int64_t nom_ipa_delta(const DevPods& P, const kss_pod& p, const NomView& nv, uint64_t here,
+                                                 int key, int kind) {
+  const kss_ipa* ip = P.ipa + p.ipa_off;
+  int64_t dl = 0;
+  for (int e = 0; e < p.ipa_len; e++) {
+    if (ip[e].kind != kind || ip[e].key != key) continue;
+    for (uint64_t m = here; m; m &= m - 1) {
+      const DevNom& q = nv.e[__ffsll((unsigned long long)m) - 1];
+      if (kind == KSS_IPA_EXISTING_ANTI) {
+        for (int t = 0; t < q.n_terms; t++)
+          for (int i = 0; i < ip[e].row_len; i++) dl += P.ints[ip[e].row_off + i] == q.terms[t] ? 1 : 0;
+      } else {
+        for (int i = 0; i < ip[e].row_len; i++) dl += P.ints[ip[e].row_off + i] == q.cls ? 1 : 0;
+      }
+    }
+  }
+  return dl;
+}
+
+// PodTopologySpread.Filter (hard constraints) — returns detail+1 on failure, 0 on pass.  With nv /
+// here / np: the first pass of RunFilterPluginsWithNominatedPods (bins: the histograms with the
+// presence bins behind them, at total_bins).
+__device__ __forceinline__ int filter_pts(const DevCluster& c, const DevPods& P, const kss_pod& p, const Plan& pl,
+                                          const long long* bins, const long long (&hard_min)[MAXH], int n,
+                                          const NomView* nv = nullptr, uint64_t here = 0, const NomPts* np = nullptr) {
+  const kss_spread* sp = P.spreads + p.spread_off;
+  // updateWithPod applies only on nodes with every constraint key whose labels match the pod's
+  // required node affinity
+  const bool upd = nv && has_keys(c, sp, p.n_hard, n) && required_affinity(c, P, p, n);
   for (int i = 0; i < p.n_hard; i++) {
     const int d = label_of(c, sp[i].key, n);
     if (d < 0) return 1 + KSS_PTS_MISSING_LABEL;
     const int o = pl.hard_own[i];
     int64_t match = 0;  // TpPairToMatchNum[(key, value)]
+    bool present = false;
     if (pl.hard_off[i] >= 0) {
       match = bins[pl.hard_off[i] + d];
+      if (nv) present = bins[pl.total_bins + pl.hard_poff[o] + d] != 0;
     } else if (has_keys(c, sp, p.n_hard, n)) {  // a node-valued key: the node's own group count
       for (int j = o; j < p.n_hard; j++)
-        if (pl.hard_own[j] == o && spread_policy_ok(c, P, p, sp[j], n)) match = spread_count(c, P, sp[j], n);
+        if (pl.hard_own[j] == o && spread_policy_ok(c, P, p, sp[j], n)) {
+          match = spread_count(c, P, sp[j], n);
+          present = true;
+        }
     }
-    const int64_t skew = match + (int64_t)sp[i].self_match - hard_min[o];
+    int64_t mn = hard_min[o];
+    if (upd) {
+      const int64_t dl = nom_pts_delta(P, p, pl, *nv, here, o);
+      if (dl) {
+        int64_t others = mn;  // the minimum over the key's other pairs
+        if (present && match == mn && np->cnt[o] == 1) others = np->gt[o];
+        match += dl;
+        mn = match < others ? match : others;
+      }
+    }
+    const int64_t skew = match + (int64_t)sp[i].self_match - mn;
     if (skew > (int64_t)sp[i].max_skew) return 1 + KSS_PTS_CONSTRAINTS_NOT_MATCH;
   }
   return 0;
 }
 
 // InterPodAffinity.Filter — returns detail+1 on failure, 0 on pass.  flags: bit0 ex, bit1 aff, bit2 anti
+// (len(counts) > 0).  With nv / here: the first pass of RunFilterPluginsWithNominatedPods (the
+// nominees' contributions to the node's pairs, and the maps they make non-empty).
 __device__ __forceinline__ int filter_ipa(const DevCluster& c, const DevPods& P, const kss_pod& p, const Plan& pl,
-                                          const long long* bins, long long flags, int n) {
+                                          const long long* bins, long long flags, int n, const NomView* nv = nullptr,
+                                          uint64_t here = 0) {
   const kss_ipa* ip = P.ipa + p.ipa_off;
+  auto value = [&](int key, int h, int d) -> int64_t {
+    int64_t v = ipa_value(c, P, p, pl, bins, slot_of(pl, key), h, d, n);
+    if (nv) v += nom_ipa_delta(P, p, *nv, here, key, h == 0 ? KSS_IPA_EXISTING_ANTI : (h == 1 ? KSS_IPA_REQ_AFFINITY : KSS_IPA_REQ_ANTI));
+    return v;
+  };
+  if (nv) {
+    for (int e = 0; e < p.ipa_len; e++) {
+      const int kind = ip[e].kind;
+      if (kind > KSS_IPA_REQ_ANTI || label_of(c, ip[e].key, n) < 0) continue;
+      if (nom_ipa_delta(P, p, *nv, here, ip[e].key, kind) > 0)
+        flags |= kind == KSS_IPA_EXISTING_ANTI ? 1 : (kind == KSS_IPA_REQ_AFFINITY ? 2 : 4);
+    }
+  }
   // satisfyPodAffinity
   bool have = false, exist = true;
   for (int e = 0; e < p.ipa_len; e++) {
@@ -533,8 +642,7 @@ __device__ __forceinline__ int filter_ipa(const DevCluster& c, const DevPods& P,
     have = true;
     const int d = label_of(c, ip[e].key, n);
     if (d < 0) return 1 + KSS_IPA_AFFINITY;
-    const int k = slot_of(pl, ip[e].key);
-    if (ipa_value(c, P, p, pl, bins, k, 1, d, n) <= 0) exist = false;
+    if (value(ip[e].key, 1, d) <= 0) exist = false;
   }
   if (have && !exist && !(!(flags & 2) && (p.flags & KSS_POD_IPA_SELF_MATCH))) return 1 + KSS_IPA_AFFINITY;
   // satisfyPodAntiAffinity
@@ -543,8 +651,7 @@ __device__ __forceinline__ int filter_ipa(const DevCluster& c, const DevPods& P,
       if (ip[e].kind != KSS_IPA_REQ_ANTI) continue;
       const int d = label_of(c, ip[e].key, n);
       if (d < 0) continue;
-      const int k = slot_of(pl, ip[e].key);
-      if (ipa_value(c, P, p, pl, bins, k, 2, d, n) > 0) return 1 + KSS_IPA_ANTI_AFFINITY;
+      if (value(ip[e].key, 2, d) > 0) return 1 + KSS_IPA_ANTI_AFFINITY;
     }
   }
   // satisfyExistingPodsAntiAffinity
@@ -553,8 +660,7 @@ __device__ __forceinline__ int filter_ipa(const DevCluster& c, const DevPods& P,
       if (ip[e].kind != KSS_IPA_EXISTING_ANTI) continue;
       const int d = label_of(c, ip[e].key, n);
       if (d < 0) continue;
-      const int k = slot_of(pl, ip[e].key);
-      if (ipa_value(c, P, p, pl, bins, k, 0, d, n) > 0) return 1 + KSS_IPA_EXISTING_ANTI_AFFINITY;
+      if (value(ip[e].key, 0, d) > 0) return 1 + KSS_IPA_EXISTING_ANTI_AFFINITY;
     }
   }
   return 0;
@@ -623,25 +729,47 @@ __device__ __forceinline__ SlotArrays slot_arrays(long long* smem, int bins_cap,
 template <bool GEN>
 __device__ __forceinline__ int filter_chain(const DevCluster& c, const DevPods& P, const kss_pod& p, const Plan& pl,
                                             const long long* bins, const long long (&hard_min)[MAXH], long long flags,
-                                            uint32_t en, bool has_ipa, int n, NodeRow& row, uint16_t* detail) {
+                                            uint32_t en, bool has_ipa, int n, NodeRow& row, uint16_t* detail,
+                                            const NomView* nv = nullptr, uint64_t here = 0, const NomPts* np = nullptr) {
   row = load_row(c, n);
-  int f = filter_local(c, P, p, en, n, row, detail);
+  int f = filter_local(c, P, p, en, n, row, detail, nv ? nv->e : nullptr, here);
   if (!f) f = filter_volumes(c, P, p, en, n, detail);
   if (GEN && !f && ((en >> KSS_F_POD_TOPOLOGY_SPREAD) & 1u) && p.n_hard > 0) {
-    const int r = filter_pts(c, P, p, pl, bins, hard_min, n);
+    const int r = filter_pts(c, P, p, pl, bins, hard_min, n, nv, here, np);
     if (r) {
       f = KSS_F_POD_TOPOLOGY_SPREAD;
       *detail = (uint16_t)(r - 1);
     }
   }
   if (!f && ((en >> KSS_F_INTER_POD_AFFINITY) & 1u) && has_ipa) {
-    const int r = filter_ipa(c, P, p, pl, bins, flags, n);
+    const int r = filter_ipa(c, P, p, pl, bins, flags, n, nv, here);
     if (r) {
       f = KSS_F_INTER_POD_AFFINITY;
       *detail = (uint16_t)(r - 1);
     }
   }
   return f;
+}
+
+// RunFilterPluginsWithNominatedPods for node n: with nominees on n the first pass (nominees added)
+// decides when it fails, the plain pass otherwise.  A failure of the plain pass after a passing
+// first pass can only be InterPodAffinity's required affinity -- the last filter plugin -- so the
+// plain record is the simulator's (store.go:423 overwrites per plugin) as it stands.
+template <bool GEN>
+__device__ __forceinline__ int filter_nominated(const DevCluster& c, const DevPods& P, const kss_pod& p, const Plan& pl,
+                                                const long long* bins, const long long (&hard_min)[MAXH],
+                                                long long flags, uint32_t en, bool has_ipa, int n, NodeRow& row,
+                                                uint16_t* detail, const NomView& nv, const NomPts& np) {
+  const int f = filter_chain<GEN>(c, P, p, pl, bins, hard_min, flags, en, has_ipa, n, row, detail);
+  if (nv.n == 0) return f;
+  const uint64_t here = nom_here(nv, n, p.priority);
+  if (!here) return f;
+  NodeRow r1;
+  uint16_t d1 = 0;
+  const int f1 = filter_chain<GEN>(c, P, p, pl, bins, hard_min, flags, en, has_ipa, n, r1, &d1, &nv, here, &np);
+  if (f1 == KSS_F_PASS) return f;
+  *detail = d1;
+  return f1;
 }
 
 // Position of global node g in the pod's ascending PreFilterResult list (binary search).
@@ -664,7 +792,8 @@ __device__ __forceinline__ int names_rank(const DevPods& P, const kss_pod& p, in
 // loop stays in the instruction cache.
 template <bool GEN>
 __device__ __forceinline__ bool schedule_pod(const DevCluster& c, const DevPods& P, const kss_profile& prof, int pi, long long* smem,
-                             Shard& S, int bins_cap, int npt, const Slot* out, bool keep_norm, PodMeta& meta) {
+                             Shard& S, int bins_cap, int npt, const Slot* out, bool keep_norm, PodMeta& meta,
+                             const NomView& nv) {
   const int tid = threadIdx.x, nt = blockDim.x;
   SharedHdr& H = shdr(smem);
   {
@@ -717,6 +846,7 @@ __device__ __forceinline__ bool schedule_pod(const DevCluster& c, const DevPods&
   // ---- stats -----------------------------------------------------------
   long long hard_min[MAXH];
   long long flags = 0;
+  NomPts& npts = H.npts;
 #pragma unroll
   for (int i = 0; i < MAXH; i++) hard_min[i] = INT32_MAX;
   if (GEN && pl.need_stats) {
@@ -760,6 +890,101 @@ __device__ __forceinline__ bool schedule_pod(const DevCluster& c, const DevPods&
     // soft presence bins start empty for the filter pass
     for (int b = pl.hard_pbins + tid; b < pl.total_pbins; b += nt) pres[b] = 0;
     __syncthreads();
+    if (nv.n && p.n_hard > 0) {
+      // nominees: per hard owner, the pairs at the minimum and the smallest count above it (one
+      // more exchange; histogram keys are cluster-wide already, so shard 0 alone adds them)
+      long long v2[2 * MAXH];
+      const int op2[2 * MAXH] = {OP_SUM, OP_SUM, OP_SUM, OP_SUM, OP_MIN, OP_MIN, OP_MIN, OP_MIN};
+#pragma unroll
+      for (int i = 0; i < MAXH; i++) {
+        v2[i] = 0;
+        v2[MAXH + i] = INT32_MAX;
+      }
+#pragma unroll
+      for (int i = 0; i < MAXH; i++) {
+        if (i >= p.n_hard || pl.hard_own[i] != i) continue;
+        const long long mn = hard_min[i];
+        if (pl.hard_off[i] >= 0) {
+          if (S.w != 0) continue;
+          const int nb = c.key_card[sp[i].key] + 1;
+          for (int b = tid; b < nb; b += nt) {
+            if (!pres[pl.hard_poff[i] + b]) continue;
+            const long long x = bins[pl.hard_off[i] + b];
+            v2[i] += x == mn ? 1 : 0;
+            if (x > mn && x < v2[MAXH + i]) v2[MAXH + i] = x;
+          }
+        } else {
+          for (int k = 0; k < npt; k++) {
+            const int n = S.lo + k * nt + tid;
+            if (n >= S.hi || !has_keys(c, sp, p.n_hard, n)) continue;
+            long long x = -1;
+            for (int j = i; j < p.n_hard; j++)
+              if (pl.hard_own[j] == i && spread_policy_ok(c, P, p, sp[j], n)) x = spread_count(c, P, sp[j], n);
+            if (x < 0) continue;
+            v2[i] += x == mn ? 1 : 0;
+            if (x > mn && x < v2[MAXH + i]) v2[MAXH + i] = x;
+          }
+        }
+      }
+      if (!cluster_reduce(smem, S, v2, op2)) return false;
+      if (tid == 0)
+#pragma unroll
+        for (int i = 0; i < MAXH; i++) {
+          npts.cnt[i] = v2[i];
+          npts.gt[i] = v2[MAXH + i];
+        }
+      __syncthreads();
+    }
+  }
+
+  // ---- PreferNominatedNode (findNodesThatFitPod -> evaluateNominatedNode) ---------------------
+  // A pod an earlier preemption nominated first runs findNodesThatPassFilters on [its node] alone,
+  // whatever its PreFilterResult; the one-node list resets nextStartNodeIndex to 0.  A feasible
+  // node is chosen without scoring (only its record is written); otherwise its status stands in
+  // the diagnosis and the full search follows (the same verdict if it reaches the node again).
+  int nom_m = -1, nom_f = KSS_F_PASS;
+  uint16_t nom_d = 0;
+  if (nv.n) {
+    for (int j = 0; j < nv.n; j++)
+      if (((nv.active >> j) & 1u) && nv.e[j].pod == nv.pod) nom_m = nv.e[j].node;
+  }
+  if (nom_m >= 0 && nom_m < c.N) {
+    long long v[1] = {0};
+    const bool mine = nom_m >= S.lo && nom_m < S.hi && ((nom_m - S.lo) % nt) == tid;
+    if (mine) {
+      NodeRow row;
+      nom_f = filter_nominated<GEN>(c, P, p, pl, bins, hard_min, flags, prof.filter_enabled, GEN && p.ipa_len > 0,
+                                    nom_m, row, &nom_d, nv, npts);
+      v[0] = nom_f == KSS_F_PASS ? 1 : 0;
+    }
+    const int op[1] = {OP_MAX};
+    if (!cluster_reduce(smem, S, v, op)) return false;
+    S.cursor = 0;
+    if (v[0]) {
+      if (out) {
+        for (int k = 0; k < npt; k++) {
+          const int n = S.lo + k * nt + tid;
+          if (n >= S.hi) continue;
+          out->fail[n] = n == nom_m ? (uint8_t)KSS_F_PASS : (uint8_t)KSS_F_NOT_EVALUATED;
+          out->detail[n] = 0;
+          if (out->canon) {
+#pragma unroll
+            for (int x = 0; x < KSS_NSCORE; x++) out->raw[(size_t)x * NN + n] = 0;
+            if (keep_norm) {
+#pragma unroll
+              for (int x = 0; x < KSS_NSCORE; x++) out->norm[(size_t)x * NN + n] = 0;
+              out->total[n] = 0;
+            }
+          }
+        }
+      }
+      meta.n_feasible = 1;
+      meta.chosen = (int)(c.node_base + nom_m);
+      return true;
+    }
+    if (!mine) nom_m = -1;  // only the owning lane overrides the node's record below
+  } else {
+    nom_m = -1;
   }
 
   // ---- filter + raw scores -------------------------------------------------
@@ -797,7 +1022,7 @@ __device__ __forceinline__ bool schedule_pod(const DevCluster& c, const DevPods&
       if (n < S.hi && (!restrict_names || in_names(P, p, (int64_t)c.node_base + n))) {
         NodeRow row;
         uint16_t d = 0;
-        fe = filter_chain<GEN>(c, P, p, pl, bins, hard_min, flags, en, has_ipa, n, row, &d) == KSS_F_PASS;
+        fe = filter_nominated<GEN>(c, P, p, pl, bins, hard_min, flags, en, has_ipa, n, row, &d, nv, npts) == KSS_F_PASS;
       }
       const unsigned long long b = __ballot(fe);
       sa.fit[k * nt + tid] = (int)__popcll(b & ((1ull << lane) - 1ull));  // feasible lanes before this one, row k
@@ -849,7 +1074,7 @@ __device__ __forceinline__ bool schedule_pod(const DevCluster& c, const DevPods&
     if (restrict_names && !in_names(P, p, (int64_t)c.node_base + n)) {
       f = KSS_F_NOT_EVALUATED;
     } else {
-      f = filter_chain<GEN>(c, P, p, pl, bins, hard_min, flags, en, has_ipa, n, row, &detail);
+      f = filter_nominated<GEN>(c, P, p, pl, bins, hard_min, flags, en, has_ipa, n, row, &detail, nv, npts);
     }
     bool kept = f == KSS_F_PASS;
     if (win && f != KSS_F_NOT_EVALUATED) {
@@ -865,6 +1090,11 @@ __device__ __forceinline__ bool schedule_pod(const DevCluster& c, const DevPods&
         w_proc = restrict_names ? ((long long)names_rank(P, p, (int64_t)c.node_base + n) - spos + m_list) % m_list
                                 : ((long long)n - nstar + m_list) % m_list;
       }
+    }
+    if (n == nom_m) {  // evaluateNominatedNode's status (infeasible, so never kept): it stands
+      f = nom_f;
+      detail = nom_d;
+      kept = false;
     }
     if (out) {
       KSS_DCHECK(n >= 0 && n < c.N, "out n", n, c.N);

@@ -403,7 +403,8 @@ __device__ void service_loop(DevCluster c, const DevJob& job, const kss_profile&
       PodMeta m;
       if (node & 2) S.cursor = cursor_prev;  // the same scheduling cycle again (the full record of a compact one)
       cursor_prev = S.cursor;
-      if (!schedule_pod<GEN>(c, job.P, prof, pi, smem, S, bins_cap, npt, &s, /*keep_norm=*/true, m)) {
+      if (!schedule_pod<GEN>(c, job.P, prof, pi, smem, S, bins_cap, npt, &s, /*keep_norm=*/true, m,
+                             NomView{nullptr, 0, -1, 0})) {  // the host refuses the service while pods are nominated
         if (threadIdx.x == 0) __hip_atomic_store(&box->err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         break;
       }

@@ -227,7 +227,7 @@ class Names(C.Structure):
 class Boundset(C.Structure):
     _fields_ = [("n", i32), ("n_ints", i32), ("id", P(i64)), ("node", P(i32)), ("priority", P(i32)),
                 ("start", P(i64)), ("cls", P(i32)), ("req", P(i64)), ("terms_off", P(i32)), ("terms_len", P(i32)),
-                ("ints", P(i32))]
+                ("ints", P(i32)), ("nonzero", P(i64)), ("ports", P(C.c_uint64))]
 
 
 class PreemptResult(C.Structure):

@@ -453,7 +453,7 @@ class CompiledCluster:
         s.n_ints = int(sum(int(x) for x in b["terms_len"][:s.n]))
         for name, ct in (("id", abi.i64), ("node", abi.i32), ("priority", abi.i32), ("start", abi.i64),
                          ("cls", abi.i32), ("req", abi.i64), ("terms_off", abi.i32), ("terms_len", abi.i32),
-                         ("ints", abi.i32)):
+                         ("ints", abi.i32), ("nonzero", abi.i64), ("ports", abi.u64)):
             setattr(s, name, abi.ptr(b[name], ct))
         return s
 
@@ -697,7 +697,7 @@ class Compiler:
         pod_count = np.zeros(N, dtype=np.int32)
         class_count = np.zeros((len(classes), N), dtype=np.int32)
         term_count = np.zeros((len(terms), N), dtype=np.int32)
-        bt = dict(id=[], node=[], priority=[], start=[], cls=[], req=[], terms_off=[], terms_len=[], ints=[])
+        bt = dict(id=[], node=[], priority=[], start=[], cls=[], req=[], terms_off=[], terms_len=[], ints=[], nz=[])
         bound_names = []
         for p in self.bound:
             nn = spec(p).get("nodeName")
@@ -718,6 +718,7 @@ class Compiler:
             bound_names.append((ns_of(p), name_of(p)))
             requested[:, i] += np.array(req, dtype=np.int64)
             c0, m0 = calculate_nonzero(p)
+            bt["nz"].append((c0, m0))
             nonzero[0, i] += c0
             nonzero[1, i] += m0
             pod_count[i] += 1
@@ -738,11 +739,15 @@ class Compiler:
         self.ports = ports
         self.port_index = {e: i for i, e in enumerate(ports)}
         port_used = np.zeros(N, dtype=np.uint64)
+        bound_ports = []  # per table row (the bound pods on known nodes, in order)
         for p in self.bound:
             nn = spec(p).get("nodeName")
             if nn in self.node_index:
+                bits = np.uint64(0)
                 for e in host_ports(p):
-                    port_used[self.node_index[nn]] |= np.uint64(1) << np.uint64(self.port_index[e])
+                    bits |= np.uint64(1) << np.uint64(self.port_index[e])
+                port_used[self.node_index[nn]] |= bits
+                bound_ports.append(bits)
         # ImageLocality: rows for the normalized container images of pending pods that some
         # node lists; scaledImageScore per (row, node) with totalNumNodes = N
         states = node_image_states(self.nodes_in)
@@ -784,7 +789,9 @@ class Compiler:
                      cls=np.array(bt["cls"], dtype=np.int32),
                      req=np.ascontiguousarray(np.array(bt["req"], dtype=np.int64).reshape(nb, abi.KSS_NRES).T),
                      terms_off=np.array(bt["terms_off"], dtype=np.int32),
-                     terms_len=np.array(bt["terms_len"], dtype=np.int32), ints=np.array(bt["ints"], dtype=np.int32))
+                     terms_len=np.array(bt["terms_len"], dtype=np.int32), ints=np.array(bt["ints"], dtype=np.int32),
+                     nonzero=np.ascontiguousarray(np.array(bt["nz"], dtype=np.int64).reshape(nb, 2).T),
+                     ports=np.array(bound_ports, dtype=np.uint64))
         bound = {k: (np.zeros(1, dtype=v.dtype) if v.size == 0 else np.ascontiguousarray(v)) for k, v in bound.items()}
         self.cc = CompiledCluster(node_names=names, order=order, scalars=scalars, label_keys=label_keys,
                                   key_values=key_values, taints=taints, classes=classes, terms=terms, arrays=arrays,

@@ -8,7 +8,7 @@ from __future__ import annotations
 
 import ctypes as C
 import os
-from typing import Dict, List, Optional, Sequence
+from typing import Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
 
@@ -81,6 +81,9 @@ SIGNATURES = [
     ("kss_plan_reason", C.c_char_p, [C.c_int32]),
     ("kss_next_start_node_index", C.c_int, [C.c_void_p, P(C.c_int32)]),
     ("kss_set_next_start_node_index", C.c_int, [C.c_void_p, C.c_int32]),
+    ("kss_nominate", C.c_int, [C.c_void_p, P(abi.PodSet), C.c_int32, C.c_int32]),
+    ("kss_clear_nomination", C.c_int, [C.c_void_p, C.c_int32]),
+    ("kss_nominations", C.c_int, [C.c_void_p, P(C.c_int32), P(C.c_int32), C.c_int32, P(C.c_int32)]),
     ("kss_fetch_meta", C.c_int, [C.c_void_p, C.c_int32, C.c_int32, P(C.c_int64)]),
     ("kss_set_names", C.c_int, [C.c_void_p, P(abi.Names)]),
     ("kss_format_annotations", C.c_int, [C.c_void_p, P(abi.PodResult), C.c_int32, C.c_char_p, C.c_size_t,
@@ -93,6 +96,7 @@ SIGNATURES = [
                                                 P(abi.PodResult), C.c_int32, C.c_int32, C.c_int32, C.c_char_p,
                                                 C.c_size_t, P(C.c_size_t)]),
     ("kss_load_bound", C.c_int, [C.c_void_p, P(abi.Boundset)]),
+    ("kss_remove_bound", C.c_int, [C.c_void_p, P(C.c_int64), C.c_int32]),
     ("kss_postfilter_pod", C.c_int, [C.c_void_p, P(abi.PodSet), C.c_int32, P(abi.PreemptResult)]),
     ("kss_stage_pods", C.c_int, [C.c_void_p, P(abi.PodSet)]),
     ("kss_run_staged", C.c_int, [C.c_void_p, C.c_int32, C.c_uint32, P(C.c_int32)]),
@@ -122,7 +126,7 @@ def lib() -> C.CDLL:
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args
-        if L.kss_abi_version() != 3:
+        if L.kss_abi_version() != 4:
             raise ImportError("libkss ABI version mismatch")
         _lib = L
     return _lib
@@ -429,6 +433,12 @@ class Context:
         """The bound pods the PostFilter dry run may evict (CompiledCluster.as_boundset())."""
         check(lib().kss_load_bound(self.h, C.byref(boundset_struct)))
 
+    def remove_bound(self, ids):
+        """The informer's RemovePod for bound-table pods (victims deleted after a PostFilter):
+        kss_remove_bound."""
+        arr = np.array(list(ids) or [0], dtype=np.int64)
+        check(lib().kss_remove_bound(self.h, arr.ctypes.data_as(P(C.c_int64)), len(ids)))
+
     def postfilter_pod(self, podset_struct: abi.PodSet, i: int, victims_cap: int = 1024) -> dict:
         """DefaultPreemption PostFilter dry run of pod i on the current snapshot: status
         (KSS_PREEMPT_*), the nominated node (-1), the victims' bound ids in eviction order and
@@ -540,6 +550,22 @@ class Context:
 
     def set_next_start_node_index(self, v: int):
         check(lib().kss_set_next_start_node_index(self.h, int(v)))
+
+    def nominate(self, ps, i: int, node: int):
+        """PodNominator.AddNominatedPod of ps.pods[i] on global node `node` (kss_nominate)."""
+        check(lib().kss_nominate(self.h, C.byref(ps), int(i), int(node)))
+
+    def clear_nomination(self, i: int):
+        """DeleteNominatedPodIfExists (kss_clear_nomination)."""
+        check(lib().kss_clear_nomination(self.h, int(i)))
+
+    def nominations(self) -> List[Tuple[int, int]]:
+        """[(pod index, global node)] in AddNominatedPod order (kss_nominations)."""
+        pods = (C.c_int32 * 64)()
+        nodes = (C.c_int32 * 64)()
+        n = C.c_int32(0)
+        check(lib().kss_nominations(self.h, pods, nodes, 64, C.byref(n)))
+        return [(int(pods[i]), int(nodes[i])) for i in range(min(n.value, 64))]
 
     def last_handoff_status(self) -> Dict[str, int]:
         """{reloads, shadow, final} of the last k_spread run (kss_last_handoff_status): all 0

@@ -201,3 +201,43 @@ def schedule_with_preemption(nodes, bound, pods, **kw):
         out.append((r, pre, o.annotations(r, pre["nominated"] if pre else None)))
     return o, out
 
+
+
+def schedule_with_nominations(nodes, bound, pods, retries=1, **kw):
+    """The sequence as the simulator's scheduler runs it with DefaultPreemption and a nominator.
+    An unschedulable pod's PostFilter result is acted on the way the scheduler does:
+      * nominated: prepareCandidate deletes the victims (the informer's RemovePod follows) and
+        clears the nominations of lower-priority pods nominated to that node
+        (getLowerPriorityNominatedPods -> ClearNominatedNodeName); handleSchedulingFailure records
+        the pod in the nominator (AddNominatedPod) and it is retried after the pods already
+        queued (at most `retries` times);
+      * no candidate: the PostFilterResult's empty NominatedNodeName clears the pod's nomination;
+      * not eligible: the nomination stays (ModeNoop).
+    Returns (oracle, [(pod index, cycle result, PostFilter result or None)]) in cycle order."""
+    o = ko.Oracle(nodes, bound, **kw)
+    queue = list(range(len(pods)))
+    tries = [0] * len(pods)
+    out = []
+    while queue:
+        j = queue.pop(0)
+        p = pods[j]
+        r = o.schedule_one(p)
+        pre = None
+        if r["selected"] is None:
+            pre = preempt(o, p, r)
+            if pre["status"] == "nominated":
+                node = pre["nominated"]
+                for pi in pre["candidates"][node]:
+                    o.infos[node].remove_pod(pi.pod)
+                prio = pod_priority(p)
+                for _, q, n in list(o.nominated):
+                    if n == node and pod_priority(q) < prio:
+                        o.clear_nomination(q)
+                o.nominate(p, node)
+                if tries[j] < retries:
+                    tries[j] += 1
+                    queue.append(j)
+            elif pre["status"] == "no_candidate":
+                o.clear_nomination(p)
+        out.append((j, r, pre))
+    return o, out
