@@ -1380,6 +1380,10 @@ typedef struct {
   int64_t m0[8], m1[8];
   int32_t id0[8];
   int64_t aff_total;
+  int n_nom; /* the nominator: ps pod indices and local nodes (RunFilterPluginsWithNominatedPods) */
+  const int32_t* nom_pod;
+  const int32_t* nom_node;
+  int pi;    /* the preemptor (never its own nominee) */
 } dryctx;
 
 static int in_list32(const int32_t* ints, int off, int len, int v) {
@@ -1470,6 +1474,49 @@ static int dry_fits(const dryctx* D, const drystate* s, int n) {
   return 1;
 }
 
+/* AddPod of nominee ps->pods[q] on node n (addNominatedPods): the same updates as dry_apply */
+static void dry_apply_nominee(const dryctx* D, int q, int n, drystate* s) {
+  const kss_cluster* cl = D->cl;
+  const kss_podset* ps = D->ps;
+  const kss_pod* p = D->p;
+  const kss_pod* a = &ps->pods[q];
+  for (int r = 0; r < 3 + cl->n_scalar; r++) s->req[r] += a->commit_req[r];
+  s->pods += 1;
+  const kss_spread* hard = ps->spreads + p->spread_off;
+  for (int j = 0; j < p->n_hard; j++)
+    if (in_list32(ps->ints, hard[j].cls_off, hard[j].cls_len, a->cls)) s->M[D->st->hard_own[j]] += 1;
+  const kss_ipa* ipa = ps->ipa + p->ipa_off;
+  for (int e = 0; e < p->ipa_len; e++) {
+    const kss_ipa* en = &ipa[e];
+    if (en->kind > KSS_IPA_REQ_ANTI) continue;
+    if (LV(cl, en->key, n) < 0) continue;
+    const int k = key_slot((podstate*)D->st, en->key);
+    if (en->kind == KSS_IPA_EXISTING_ANTI) {
+      for (int t = 0; t < a->own_terms_len; t++)
+        if (in_list32(ps->ints, en->row_off, en->row_len, ps->ints[a->own_terms_off + t])) s->A[k][0] += 1;
+    } else if (in_list32(ps->ints, en->row_off, en->row_len, a->cls)) {
+      s->A[k][en->kind == KSS_IPA_REQ_AFFINITY ? 1 : 2] += 1;
+      if (en->kind == KSS_IPA_REQ_AFFINITY) s->T += 1;
+    }
+  }
+}
+
+/* RunFilterPluginsWithNominatedPods over the dry-run view: the nominees of priority >= the
+   preemptor's on node n added first; the plain view decides when that passes */
+static int dry_fits_nom(const dryctx* D, const drystate* s, int n) {
+  drystate s1;
+  int added = 0;
+  for (int j = 0; j < D->n_nom; j++) {
+    const int q = D->nom_pod[j];
+    if (D->nom_node[j] != n || q == D->pi || D->ps->pods[q].priority < D->p->priority) continue;
+    if (!added) s1 = *s;
+    added = 1;
+    dry_apply_nominee(D, q, n, &s1);
+  }
+  if (added && !dry_fits(D, &s1, n)) return 0;
+  return dry_fits(D, s, n);
+}
+
 typedef struct {
   int64_t hp, sum, cnt, start; /* hp == INT64_MAX: not a candidate */
 } dryres;
@@ -1507,13 +1554,13 @@ static dryres dry_select(const dryctx* D, int n, int64_t* victims, int cap) {
   }
   s.T = D->aff_total;
   for (int k = p0; k < e1; k++) dry_apply(D, D->ord[k], n, -1, &s);
-  if (!dry_fits(D, &s, n)) return res;
+  if (!dry_fits_nom(D, &s, n)) return res;
   int nv = 0;
   int64_t hp = 0, sum = 0, stt = 0;
   for (int k = p0; k < e1; k++) {
     const int e = D->ord[k];
     dry_apply(D, e, n, 1, &s);
-    if (!dry_fits(D, &s, n)) {
+    if (!dry_fits_nom(D, &s, n)) {
       dry_apply(D, e, n, -1, &s);
       if (nv == 0) {
         hp = bs->priority[e];
@@ -1548,11 +1595,24 @@ static int imp_before(const kss_boundset* bs, int a, int b) { /* MoreImportantPo
 
 /* PostFilter dry run of ps->pods[pi] against cl and the bound pods bs (the state its filters
  * saw).  out->victims / victims_cap as kss_postfilter_pod. */
+int kss_oracle_postfilter_n(const kss_profile* prof, const kss_cluster* cl, const kss_podset* ps, int pi,
+                            const kss_boundset* bs, int threads, kss_preempt_result* out, const int32_t* nom_pod,
+                            const int32_t* nom_node, int32_t n_nom);
+
 int kss_oracle_postfilter(const kss_profile* prof, const kss_cluster* cl, const kss_podset* ps, int pi,
                           const kss_boundset* bs, int threads, kss_preempt_result* out) {
+  return kss_oracle_postfilter_n(prof, cl, ps, pi, bs, threads, out, NULL, NULL, 0);
+}
+
+/* kss_oracle_postfilter with the scheduling queue's nominator (ps pod indices nominated to global
+   nodes): every filter call is RunFilterPluginsWithNominatedPods. */
+int kss_oracle_postfilter_n(const kss_profile* prof, const kss_cluster* cl, const kss_podset* ps, int pi,
+                            const kss_boundset* bs, int threads, kss_preempt_result* out, const int32_t* nom_pod,
+                            const int32_t* nom_node, int32_t n_nom) {
   const kss_pod* p = &ps->pods[pi];
   const int N = cl->n_nodes;
   const int th = threads > 0 ? threads : 1;
+  int32_t* nn_local = NULL;
   out->status = KSS_PREEMPT_NO_CANDIDATE;
   out->nominated = -1;
   out->n_potential = out->n_candidates = out->n_victims = 0;
@@ -1621,6 +1681,31 @@ int kss_oracle_postfilter(const kss_profile* prof, const kss_cluster* cl, const 
     fp[n] = (uint8_t)filter_node(prof, cl, ps, p, &st, n, &fd[n]);
     feasible += fp[n] == KSS_F_PASS;
   }
+  if (n_nom > 0) { /* the scheduling cycle's statuses on nodes holding nominees (serial: in place) */
+    ostate os;
+    if (ostate_init(&os, cl)) {
+      rc = KSS_E_NOMEM;
+      goto done;
+    }
+    nn_local = (int32_t*)malloc(sizeof(int32_t) * (size_t)n_nom);
+    os.nom_active = (uint8_t*)malloc((size_t)n_nom);
+    for (int j = 0; j < n_nom; j++) {
+      nn_local[j] = nom_node[j] - cl->node_base;
+      os.nom_active[j] = nom_pod[j] >= 0 && nom_pod[j] < ps->n_pods && nn_local[j] >= 0 && nn_local[j] < N;
+    }
+    os.n_nom = n_nom;
+    os.nom_pod = nom_pod;
+    os.nom_node = nn_local;
+    for (int j = 0; j < n_nom; j++) {
+      const int n = nn_local[j];
+      if (!os.nom_active[j] || (inset && !inset[n])) continue;
+      int added;
+      const int was = fp[n] == KSS_F_PASS;
+      fp[n] = (uint8_t)filter_with_nominated(prof, &os, ps, pi, &st, n, &fd[n], &added);
+      feasible += (fp[n] == KSS_F_PASS) - was;
+    }
+    ostate_free(&os);
+  }
   if (feasible) {
     out->status = KSS_PREEMPT_SCHEDULABLE;
     goto done;
@@ -1635,6 +1720,10 @@ int kss_oracle_postfilter(const kss_profile* prof, const kss_cluster* cl, const 
   D.bs = bs;
   D.ptr = ptr;
   D.ord = ord;
+  D.n_nom = n_nom;
+  D.nom_pod = nom_pod;
+  D.nom_node = nn_local;
+  D.pi = pi;
   /* criticalPaths per hard owner: the smallest pair count, its pair, the next smallest */
   {
     const kss_spread* hard = ps->spreads + p->spread_off;
@@ -1704,6 +1793,7 @@ int kss_oracle_postfilter(const kss_profile* prof, const kss_cluster* cl, const 
   }
 done:
   podstate_free(&st);
+  free(nn_local);
   free(ptr);
   free(ord);
   free(fp);

@@ -39,18 +39,27 @@ def lib():
         _lib.kss_oracle_postfilter.argtypes = [P(abi.Profile), P(abi.Cluster), P(abi.PodSet), C.c_int,
                                                P(abi.Boundset), C.c_int, P(abi.PreemptResult)]
         _lib.kss_oracle_postfilter.restype = C.c_int
+        _lib.kss_oracle_postfilter_n.argtypes = _lib.kss_oracle_postfilter.argtypes + [P(C.c_int32), P(C.c_int32),
+                                                                                        C.c_int32]
+        _lib.kss_oracle_postfilter_n.restype = C.c_int
     return _lib
 
 
-def postfilter(profile, cluster_struct, podset_struct, i, boundset_struct, threads=1, victims_cap=1024):
-    """kss_oracle_postfilter: the C PostFilter dry run of pod i (the same dict as
-    native.Context.postfilter_pod)."""
+def postfilter(profile, cluster_struct, podset_struct, i, boundset_struct, threads=1, victims_cap=1024,
+               nominations=()):
+    """kss_oracle_postfilter(_n): the C PostFilter dry run of pod i (the same dict as
+    native.Context.postfilter_pod); nominations: [(pod index, global node)]."""
     vic = np.zeros(max(victims_cap, 1), np.int64)
     r = abi.PreemptResult()
     r.victims_cap = victims_cap
     r.victims = vic.ctypes.data_as(C.POINTER(C.c_int64))
-    rc = lib().kss_oracle_postfilter(C.byref(profile), C.byref(cluster_struct), C.byref(podset_struct), i,
-                                     C.byref(boundset_struct), threads, C.byref(r))
+    nominations = list(nominations)
+    nom_pod = np.array([a for a, _ in nominations] or [0], dtype=np.int32)
+    nom_node = np.array([b for _, b in nominations] or [0], dtype=np.int32)
+    rc = lib().kss_oracle_postfilter_n(C.byref(profile), C.byref(cluster_struct), C.byref(podset_struct), i,
+                                       C.byref(boundset_struct), threads, C.byref(r),
+                                       nom_pod.ctypes.data_as(C.POINTER(C.c_int32)),
+                                       nom_node.ctypes.data_as(C.POINTER(C.c_int32)), len(nominations))
     if rc:
         raise RuntimeError(f"kss_oracle_postfilter: {rc}")
     return dict(status=r.status, nominated=r.nominated, n_potential=r.n_potential, n_candidates=r.n_candidates,

@@ -78,9 +78,10 @@ STATUS = {abi.KSS_PREEMPT_NOMINATED: "nominated", abi.KSS_PREEMPT_NO_CANDIDATE: 
           abi.KSS_PREEMPT_NOT_ELIGIBLE: "not_eligible", abi.KSS_PREEMPT_SCHEDULABLE: "schedulable"}
 
 
-def _c_dry_runs(nodes, bound, pods, threads):
+def _c_dry_runs(nodes, bound, pods, threads, nominations=()):
     """The C restatement (oracle/kss_oracle.c kss_oracle_postfilter) of every pod against the
-    initial snapshot (nothing committed), as (status, nominated node, victims, criteria)."""
+    initial snapshot (nothing committed), as (status, nominated node, victims, criteria).
+    nominations: [(pod index, node index)] in the nominator."""
     import oracle_c
     cc, cp, _ = compile_cluster(nodes, bound, pods)
     cl, ps, bs = cc.as_struct(), cp.as_struct(), cc.as_boundset()
@@ -90,15 +91,17 @@ def _c_dry_runs(nodes, bound, pods, threads):
 
     out = []
     for j in range(cp.n):
-        r = oracle_c.postfilter(abi.default_profile(), cl, ps, j, bs, threads=threads)
+        r = oracle_c.postfilter(abi.default_profile(), cl, ps, j, bs, threads=threads, nominations=nominations)
         nom = cc.node_names[r["nominated"]] if r["nominated"] >= 0 else None
         out.append((STATUS[r["status"]], nom, [victim(v) for v in r["victims"]],
                     (r["n_potential"], r["n_candidates"])))
     return out
 
 
-def _py_dry_runs(nodes, bound, pods):
+def _py_dry_runs(nodes, bound, pods, nominations=()):
     o = ko.Oracle(nodes, bound)
+    for a, b in nominations:
+        o.nominate(pods[a], b)
     out = []
     for p in pods:
         r = o.schedule_one(p, commit=False)
@@ -135,3 +138,22 @@ def test_c_postfilter_matches_object_oracle(seed, n_nodes, n_pods, threads):
         else:
             assert g == w, j
     assert "nominated" in kinds
+
+
+@pytest.mark.parametrize("seed,n_nodes,n_pods,threads", [(1, 60, 40, 2), (3, 200, 60, 8), (5, 80, 60, 4)])
+def test_c_postfilter_with_nominees_matches_object_oracle(seed, n_nodes, n_pods, threads):
+    """The same dry runs with a nominator of a dozen pods on random nodes: the nominees of equal or
+    higher priority take part in every filter call (the statuses and SelectVictimsOnNode)."""
+    import random
+    nodes, bound, pods = pf.saturated(seed, n_nodes, n_pods)
+    rnd = random.Random(seed)
+    noms = [(j, rnd.randrange(n_nodes)) for j in rnd.sample(range(n_pods), 12)]
+    got = _c_dry_runs(nodes, bound, pods, threads, noms)
+    want = _py_dry_runs(nodes, bound, pods, noms)
+    plain = _py_dry_runs(nodes, bound, pods)
+    for j, (g, w) in enumerate(zip(got, want)):
+        if w[0] == "schedulable":
+            assert g[0] in ("schedulable", "not_eligible"), j
+        else:
+            assert g == w, j
+    assert want != plain  # the nominees changed some dry run
