@@ -348,7 +348,8 @@ typedef struct kss_pod {
   int32_t img_off, img_len;
   int32_t n_containers;
   int32_t vol_off, vol_len;        /* volume program: pool vols (kss_vol), 0 entries for volume-less pods */
-  int32_t pad2;
+  int32_t uid;                     /* the pod's identity for the nominator (kss_nominate): > 0 a stable caller id
+                                      (the Go plugin interns metadata.uid); 0: its index in the podset stands for it */
 } kss_pod;
 
 typedef struct kss_podset {
@@ -572,9 +573,9 @@ int kss_set_next_start_node_index(kss_ctx* ctx, int32_t value);
  * NominatedNodeName the scheduler's handleSchedulingFailure stores).
  *   kss_nominate          AddNominatedPod: ps.pods[pod_index] is nominated to global node `node`
  *                         (an earlier nomination of the same pod is replaced).  The pod's identity
- *                         is its index in the podset the caller schedules from (the staged one
- *                         for batches, the one passed to kss_eval_pod).  At most 64 entries; pods
- *                         with volumes are refused.
+ *                         is kss_pod.uid when > 0, otherwise its index in the podset the caller
+ *                         schedules from (the staged one for batches, the one passed to
+ *                         kss_eval_pod).  At most 64 entries; pods with volumes are refused.
  *   kss_clear_nomination  DeleteNominatedPodIfExists (a PostFilter that found no candidate, a
  *                         lower-priority nomination cleared by prepareCandidate); no-op if absent
  *   kss_nominations       the entries in AddNominatedPod order (*n = count; cap entries copied)
@@ -590,8 +591,9 @@ int kss_set_next_start_node_index(kss_ctx* ctx, int32_t value);
  * grids refuse (KSS_E_UNSUPPORTED).  Replaces the nominator of the scheduler that
  * simulator/scheduler/scheduler.go:155-168 creates (pkg/scheduler/internal/queue, v1.26). */
 int kss_nominate(kss_ctx* ctx, const kss_podset* ps, int32_t pod_index, int32_t node);
-int kss_clear_nomination(kss_ctx* ctx, int32_t pod_index);
-int kss_nominations(kss_ctx* ctx, int32_t* pods, int32_t* nodes, int32_t cap, int32_t* n);
+int kss_clear_nomination(kss_ctx* ctx, const kss_podset* ps, int32_t pod_index);
+/* ids: the pods' identities (kss_pod.uid when > 0, else -1 - podset index) */
+int kss_nominations(kss_ctx* ctx, int32_t* ids, int32_t* nodes, int32_t cap, int32_t* n);
 
 /* many independent clusters (what-if scenarios, KEP-184): clusters[s] with podsets[s];
  * one workgroup per scenario, no inter-scenario communication. chosen_out is [sum n_pods].

@@ -115,8 +115,11 @@ struct DevJob {
   int32_t* cursor;    // k_schedule / the service: the cluster's nextStartNodeIndex word (null: 0, not kept)
   const DevNom* nom;  // k_schedule: the nominator's entries (kss_nominate), all nominated at launch
   int32_t n_nom;      // entries (<= KSS_NOM_MAX; 0: none)
-  int32_t pod_base;   // the identity of pod pi is pod_base + pi (its index in the caller's podset)
+  int32_t pod_base;   // pod pi is pod pod_base + pi of the caller's podset (its identity when its uid is 0)
 };
+
+// The nominator's pod identity: the caller's uid, else -1 - the pod's podset index
+__host__ __device__ inline int32_t pod_identity(const kss_pod& p, int index) { return p.uid > 0 ? p.uid : -1 - index; }
 
 }  // namespace
 
@@ -169,7 +172,7 @@ __global__ __launch_bounds__(KSS_MAX_THREADS) void k_schedule(const DevJob* __re
   for (int pi = 0; pi < job.n_pods; pi++) {
     uint8_t* base = job.slots + (job.record ? (size_t)pi * job.slot_bytes : 0);
     Slot s;
-    nv.pod = job.pod_base + pi;
+    nv.pod = pod_identity(job.P.pods[pi], job.pod_base + pi);
     s.fail = base + L.fail;
     s.detail = (uint16_t*)(base + L.detail);
     s.raw = (int64_t*)(base + L.raw);
@@ -602,6 +605,7 @@ struct kss_ctx {
   // the scheduling queue's nominator (kss_nominate): host mirror in AddNominatedPod order, uploaded
   // before a launch that reads it; run_pod_base = the podset index of the launch's pod 0
   std::vector<DevNom> nom;
+  std::vector<int32_t> staged_uid;  // the staged pods' nominator identities (batch commits leave it)
   DevBuf nom_buf;
   bool nom_dirty = true;
   int32_t run_pod_base = 0;
@@ -1872,7 +1876,7 @@ int kss_nominate(kss_ctx* ctx, const kss_podset* ps, int32_t pod_index, int32_t 
   DevNom e{};
   e.node = local;
   e.prio = p.priority;
-  e.pod = pod_index;
+  e.pod = pod_identity(p, pod_index);
   e.cls = p.cls;
   e.n_terms = p.own_terms_len;
   for (int t = 0; t < p.own_terms_len; t++) {
@@ -1883,7 +1887,7 @@ int kss_nominate(kss_ctx* ctx, const kss_podset* ps, int32_t pod_index, int32_t 
   for (int r = 0; r < KSS_NRES; r++) e.req[r] = p.commit_req[r];
   std::lock_guard<std::mutex> lk(ctx->mu);
   // AddNominatedPod: an earlier nomination of the pod is replaced (it moves to the end)
-  ctx->nom.erase(std::remove_if(ctx->nom.begin(), ctx->nom.end(), [&](const DevNom& x) { return x.pod == pod_index; }),
+  ctx->nom.erase(std::remove_if(ctx->nom.begin(), ctx->nom.end(), [&](const DevNom& x) { return x.pod == e.pod; }),
                  ctx->nom.end());
   if ((int)ctx->nom.size() >= KSS_NOM_MAX) return fail(KSS_E_UNSUPPORTED, "more than 64 nominated pods");
   ctx->nom.push_back(e);
@@ -1891,19 +1895,21 @@ int kss_nominate(kss_ctx* ctx, const kss_podset* ps, int32_t pod_index, int32_t 
   return 0;
 }
 
-int kss_clear_nomination(kss_ctx* ctx, int32_t pod_index) {
+int kss_clear_nomination(kss_ctx* ctx, const kss_podset* ps, int32_t pod_index) {
   KSS_SVC_QUIESCE(ctx);
-  if (!ctx) return fail(KSS_E_INVAL, "bad arguments");
+  if (!ctx || !ps) return fail(KSS_E_INVAL, "bad arguments");
+  if (pod_index < 0 || pod_index >= ps->n_pods) return fail(KSS_E_INVAL, "pod index out of range");
+  const int32_t id = pod_identity(ps->pods[pod_index], pod_index);
   std::lock_guard<std::mutex> lk(ctx->mu);
   const size_t before = ctx->nom.size();
-  ctx->nom.erase(std::remove_if(ctx->nom.begin(), ctx->nom.end(), [&](const DevNom& x) { return x.pod == pod_index; }),
+  ctx->nom.erase(std::remove_if(ctx->nom.begin(), ctx->nom.end(), [&](const DevNom& x) { return x.pod == id; }),
                  ctx->nom.end());
   if (ctx->nom.size() != before) ctx->nom_dirty = true;
   return 0;
 }
 
 int kss_nominations(kss_ctx* ctx, int32_t* pods, int32_t* nodes, int32_t cap, int32_t* n) {
-  if (!ctx || !n || cap < 0 || (cap > 0 && (!pods || !nodes))) return fail(KSS_E_INVAL, "bad arguments");
+  if (!ctx || !n || cap < 0 || (cap > 0 && (!pods || !nodes))) return fail(KSS_E_INVAL, "bad arguments");  // pods: identities
   std::lock_guard<std::mutex> lk(ctx->mu);
   *n = (int32_t)ctx->nom.size();
   for (int i = 0; i < *n && i < cap; i++) {
@@ -3292,7 +3298,11 @@ static BoundPod bound_from_pod(const kss_podset* ps, int i) {
 
 static void stage_bound(kss_ctx* ctx, const kss_podset* ps) {
   ctx->staged_bp.resize(ps->n_pods);
-  for (int i = 0; i < ps->n_pods; i++) ctx->staged_bp[i] = bound_from_pod(ps, i);
+  ctx->staged_uid.resize(ps->n_pods);
+  for (int i = 0; i < ps->n_pods; i++) {
+    ctx->staged_bp[i] = bound_from_pod(ps, i);
+    ctx->staged_uid[i] = pod_identity(ps->pods[i], i);
+  }
 }
 
 // SchedulingQueue.DeleteNominatedPodIfExists for every assumed pod of a batch (the device did the
@@ -3302,8 +3312,9 @@ static void drop_committed_nominations(kss_ctx* ctx, int n) {
   const size_t before = ctx->nom.size();
   ctx->nom.erase(std::remove_if(ctx->nom.begin(), ctx->nom.end(),
                                 [&](const DevNom& e) {
-                                  const int i = e.pod - ctx->run_pod_base;
-                                  return i >= 0 && i < n && ctx->meta_host[i].chosen >= 0;
+                                  for (int i = 0; i < n && i < (int)ctx->staged_uid.size(); i++)
+                                    if (ctx->staged_uid[i] == e.pod && ctx->meta_host[i].chosen >= 0) return true;
+                                  return false;
                                 }),
                  ctx->nom.end());
   if (ctx->nom.size() != before) ctx->nom_dirty = true;
@@ -3370,7 +3381,8 @@ static int commit_one(kss_ctx* ctx, const kss_podset* ps, int32_t pod_index, int
   HIP_TRY(hipGetLastError());  // no synchronisation: every later call on the ctx stream is ordered after it
   if (sign > 0) {  // assume -> SchedulingQueue.DeleteNominatedPodIfExists
     const size_t before = ctx->nom.size();
-    ctx->nom.erase(std::remove_if(ctx->nom.begin(), ctx->nom.end(), [&](const DevNom& e) { return e.pod == pod_index; }),
+    const int32_t id = pod_identity(p, pod_index);
+    ctx->nom.erase(std::remove_if(ctx->nom.begin(), ctx->nom.end(), [&](const DevNom& e) { return e.pod == id; }),
                    ctx->nom.end());
     if (ctx->nom.size() != before) ctx->nom_dirty = true;
   }
@@ -4548,7 +4560,7 @@ int kss_postfilter_pod(kss_ctx* ctx, const kss_podset* ps, int32_t pod_index, ks
     J.nom = (const DevNom*)ctx->nom_buf.p;
     J.n_nom = (int32_t)ctx->nom.size();
   }
-  J.pod_id = pod_index;
+  J.pod_id = pod_identity(ps->pods[pod_index], pod_index);
   J.key = (int64_t*)(d + o_key);
   J.n_blocks = (int32_t)std::max<size_t>((N + PRE_NODE_THREADS - 1) / PRE_NODE_THREADS, 1);
   J.victims = (int64_t*)(d + o_vic);

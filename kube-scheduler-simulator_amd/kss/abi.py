@@ -179,7 +179,7 @@ class Pod(C.Structure):
         ("ipa_off", i32), ("ipa_len", i32), ("cls", i32), ("own_terms_off", i32), ("own_terms_len", i32),
         ("prefilter_status", i32), ("names_off", i32), ("names_len", i32), ("priority", i32), ("prefilter_msg", i32),
         ("port_conflict", u64), ("port_add", u64), ("img_off", i32), ("img_len", i32), ("n_containers", i32),
-        ("vol_off", i32), ("vol_len", i32), ("pad2", i32),
+        ("vol_off", i32), ("vol_len", i32), ("uid", i32),
     ]
 
 

@@ -82,7 +82,7 @@ SIGNATURES = [
     ("kss_next_start_node_index", C.c_int, [C.c_void_p, P(C.c_int32)]),
     ("kss_set_next_start_node_index", C.c_int, [C.c_void_p, C.c_int32]),
     ("kss_nominate", C.c_int, [C.c_void_p, P(abi.PodSet), C.c_int32, C.c_int32]),
-    ("kss_clear_nomination", C.c_int, [C.c_void_p, C.c_int32]),
+    ("kss_clear_nomination", C.c_int, [C.c_void_p, P(abi.PodSet), C.c_int32]),
     ("kss_nominations", C.c_int, [C.c_void_p, P(C.c_int32), P(C.c_int32), C.c_int32, P(C.c_int32)]),
     ("kss_fetch_meta", C.c_int, [C.c_void_p, C.c_int32, C.c_int32, P(C.c_int64)]),
     ("kss_set_names", C.c_int, [C.c_void_p, P(abi.Names)]),
@@ -555,17 +555,18 @@ class Context:
         """PodNominator.AddNominatedPod of ps.pods[i] on global node `node` (kss_nominate)."""
         check(lib().kss_nominate(self.h, C.byref(ps), int(i), int(node)))
 
-    def clear_nomination(self, i: int):
-        """DeleteNominatedPodIfExists (kss_clear_nomination)."""
-        check(lib().kss_clear_nomination(self.h, int(i)))
+    def clear_nomination(self, ps, i: int):
+        """DeleteNominatedPodIfExists of ps.pods[i] (kss_clear_nomination)."""
+        check(lib().kss_clear_nomination(self.h, C.byref(ps), int(i)))
 
     def nominations(self) -> List[Tuple[int, int]]:
-        """[(pod index, global node)] in AddNominatedPod order (kss_nominations)."""
+        """[(pod, global node)] in AddNominatedPod order (kss_nominations): pod = the podset index
+        of a pod without uid (identity -1 - index), else its uid."""
         pods = (C.c_int32 * 64)()
         nodes = (C.c_int32 * 64)()
         n = C.c_int32(0)
         check(lib().kss_nominations(self.h, pods, nodes, 64, C.byref(n)))
-        return [(int(pods[i]), int(nodes[i])) for i in range(min(n.value, 64))]
+        return [(-1 - int(pods[i]) if pods[i] < 0 else int(pods[i]), int(nodes[i])) for i in range(min(n.value, 64))]
 
     def last_handoff_status(self) -> Dict[str, int]:
         """{reloads, shadow, final} of the last k_spread run (kss_last_handoff_status): all 0

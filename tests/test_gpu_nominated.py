@@ -128,14 +128,17 @@ def test_batch_matches_c_oracle(case, flags, pct):
     ctx.close()
 
 
-def test_per_pod_equals_batch():
+@pytest.mark.parametrize("uid", [False, True])
+def test_per_pod_equals_batch(uid):
     """kss_eval_pod + kss_commit per pod gives the batch's choices and nominator (the pod's identity
-    is its podset index on both paths)."""
+    is its podset index on both paths, or the caller's uid)."""
     make, n_nodes, n_run, inside, outside = CASES["spread_ipa"]
     nodes, bound, pods = make()
     pods = _with_priorities(pods, 23)
     noms = _noms(pods, n_nodes, n_run, 23, inside, outside)
     cc, cp, _ = compile_cluster(nodes, bound, pods)
+    if uid:
+        cp.pods["uid"] = 1000 + np.arange(cp.n, dtype=np.int32)
     ps = cp.as_struct()
     a = _ctx(cc)
     for j, n in noms:
@@ -154,6 +157,11 @@ def test_per_pod_equals_batch():
             b.commit(ps, j, r.chosen)
     assert got == list(want)
     assert b.nominations() == left
+    if uid:
+        assert {q for q, _ in left} <= {1000 + j for j, _ in noms}
+        for q, _ in left:
+            b.clear_nomination(ps, q - 1000)
+        assert b.nominations() == []
     b.close()
 
 
@@ -196,13 +204,13 @@ def _device_seq(nodes, bound, pods):
             ctx.remove_bound(pre["victims"])  # prepareCandidate deletes them; the informer removes them
             for q, n in ctx.nominations():
                 if n == node and prio[q] < prio[j]:
-                    ctx.clear_nomination(q)
+                    ctx.clear_nomination(ps, q)
             ctx.nominate(ps, j, node)
             if tries[j] < 1:
                 tries[j] += 1
                 queue.append(j)
         elif st == "no_candidate":
-            ctx.clear_nomination(j)
+            ctx.clear_nomination(ps, j)
     ctx.close()
     return out
 
