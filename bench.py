@@ -703,25 +703,51 @@ def run_per_pod(args):
     assert chosen_svc == chosen, "service choices differ from kss_eval_pod's"
     # one stamped pass (KSS_SERVICE_STAMPS): where shard 0 spends an evaluation
     os.environ["KSS_SERVICE_STAMPS"] = "1"
-    ctx.reset()
-    phases = []
-    for j in range(min(100, n_pods)):
-        native.check(native.lib().kss_service_eval(ctx.h, j, abi.KSS_FIELD_ALL, ctypes.byref(sview)))
-        st = ctx.service_stamps()
-        phases.append([(st[1] - st[0]) / 100.0, (st[2] - st[1]) / 100.0, (st[3] - st[2]) / 100.0,
-                       (st[4] - st[2]) / 100.0, (st[3] - st[4]) / 100.0])
-        if sview.chosen >= 0:
-            native.check(native.lib().kss_service_commit(ctx.h, j, sview.chosen))
-    ctx.service_stop()
-    del os.environ["KSS_SERVICE_STAMPS"]
-    ph = np.median(np.array(phases), axis=0)
-    ctx.reset()
     slim_fields = abi.KSS_FIELD_FAIL | abi.KSS_FIELD_DETAIL | abi.KSS_FIELD_TOTAL
+
+    def stamped(fields):
+        ctx.reset()
+        phases = []
+        for j in range(min(100, n_pods)):
+            native.check(native.lib().kss_service_eval(ctx.h, j, fields, ctypes.byref(sview)))
+            st = ctx.service_stamps()
+            phases.append([(st[1] - st[0]) / 100.0, (st[2] - st[1]) / 100.0, (st[3] - st[2]) / 100.0,
+                           (st[4] - st[2]) / 100.0, (st[3] - st[4]) / 100.0,
+                           (st[5] - st[1]) / 100.0 if st[5] else 0.0, (st[6] - st[5]) / 100.0 if st[6] else 0.0,
+                           (st[7] - st[6]) / 100.0 if st[7] else 0.0, (st[2] - st[7]) / 100.0 if st[7] else 0.0])
+            if sview.chosen >= 0:
+                native.check(native.lib().kss_service_commit(ctx.h, j, sview.chosen))
+        ctx.service_stop()
+        return np.median(np.array(phases), axis=0)
+
+    ph = stamped(abi.KSS_FIELD_ALL)
+    ph_slim = stamped(slim_fields)
+    del os.environ["KSS_SERVICE_STAMPS"]
+    ctx.reset()
     elapsed_svc_slim, ev_svc_slim, _, chosen_svc_slim = svc_loop(slim_fields)
     assert chosen_svc_slim == chosen
     ctx.reset()
     elapsed_svc_c, ev_svc_c, _, chosen_svc_c = svc_loop(abi.KSS_FIELD_ALL, compact=True)
     assert chosen_svc_c == chosen
+    svc_mode = ctx.service_mode()
+    # the same two loops on the general chain (schedule_pod + the record copy), for comparison
+    os.environ["KSS_SERVICE_GENERAL"] = "1"
+    ctx.reset()
+    el_g, ev_g, _, ch_g = svc_loop(abi.KSS_FIELD_ALL)
+    ctx.reset()
+    el_gs, ev_gs, _, ch_gs = svc_loop(slim_fields)
+    del os.environ["KSS_SERVICE_GENERAL"]
+    assert ch_g == chosen and ch_gs == chosen
+    # A/B: the simple evaluation with every lane's system fence (the general chain's record fence),
+    # and with the static words evaluated per call instead of the table k_static fills at the start
+    ab = {}
+    for env in ("KSS_SVC_FULL_FENCE", "KSS_SVC_NO_STATIC"):
+        os.environ[env] = "1"
+        ctx.reset()
+        el_ab, ev_ab, _, ch_ab = svc_loop(slim_fields)
+        del os.environ[env]
+        assert ch_ab == chosen
+        ab[env] = float(np.median(ev_ab))
     out = {
         "metric": "per-pod API: kss_eval_pod + kss_commit latency (pods/sec in value)",
         "value": n_pods / elapsed,
@@ -759,9 +785,25 @@ def run_per_pod(args):
                                 "api": "kss_service_eval_compact (every field; raw / total int32, norm uint8)",
                                 "eval_us": {"median": float(np.median(ev_svc_c)), "mean": float(ev_svc_c.mean()),
                                             "p90": float(np.percentile(ev_svc_c, 90))}},
+                    "mode": {2: "k_simple-shaped evaluation on an XCD-local grid, record stored from registers",
+                             1: "k_simple-shaped evaluation, record stored from registers",
+                             0: "general chain (schedule_pod + record copy)"}.get(svc_mode, "not started"),
+                    "slim_ab_eval_us_median": {"KSS_SVC_FULL_FENCE=1 (every lane's system fence)": ab["KSS_SVC_FULL_FENCE"],
+                                               "KSS_SVC_NO_STATIC=1 (static words per call)": ab["KSS_SVC_NO_STATIC"]},
+                    "general_chain": {"eval_us_median": float(np.median(ev_g)), "slim_eval_us_median": float(np.median(ev_gs)),
+                                      "pods_per_s": n_pods / el_g, "slim_pods_per_s": n_pods / el_gs,
+                                      "note": "KSS_SERVICE_GENERAL=1: the chain every program shape takes"},
                     "shard0_phases_us_median": {"relay": float(ph[0]), "pod": float(ph[1]),
                                                 "record_copy_and_fence": float(ph[2]), "record_stores": float(ph[3]),
-                                                "system_fence": float(ph[4])},
+                                                "system_fence": float(ph[4]),
+                                                "note": "the k_simple-shaped evaluation stores the record from "
+                                                        "registers inside 'pod'; the fence is the rest"},
+                    "shard0_phases_us_median_slim": {"relay": float(ph_slim[0]), "pod": float(ph_slim[1]),
+                                                     "system_fence": float(ph_slim[4]),
+                                                     "pod_node_pass": float(ph_slim[5]),
+                                                     "pod_stats_exchange": float(ph_slim[6]),
+                                                     "pod_normalise_and_record": float(ph_slim[7]),
+                                                     "pod_key_exchange": float(ph_slim[8])},
                     "geometry": ctx.last_geometry()},
         "eval_device_ms_last": ctx.last_timing()[0],
         "geometry": ctx.last_geometry(),

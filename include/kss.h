@@ -533,8 +533,16 @@ int kss_service_commit(kss_ctx* ctx, int32_t pod_index, int32_t node);
 int kss_service_rollback(kss_ctx* ctx, int32_t pod_index, int32_t node);
 /* Diagnostics (KSS_SERVICE_STAMPS set when the grid starts): shard 0's s_memrealtime (100 MHz)
  * in the last evaluation when it took the command, relayed it, finished the pod, had its
- * record visible to the host, and had issued its record stores (before the system fence). */
-int kss_service_stamps(kss_ctx* ctx, uint64_t* out5);
+ * record visible to the host, and had issued its record stores (before the system fence);
+ * the k_simple-shaped evaluation adds its node pass done, its statistics exchange done and its
+ * record stores issued before the key exchange (out8[5..7], 0 otherwise). */
+int kss_service_stamps(kss_ctx* ctx, uint64_t* out8);
+/* Which evaluation the service grid runs (set when it starts): 1 the k_simple-shaped chain
+ * (staged default-profile pods: no spread / inter-pod programs, host ports, node-cached images,
+ * volumes or extended resources, percentageOfNodesToScore 100) with the record stored from
+ * registers, 2 the same on an XCD-local grid (its exchanges in one XCD's L2), 0 the general
+ * chain (schedule_pod + the record copy), -1 not started. */
+int kss_service_mode(kss_ctx* ctx, int32_t* mode);
 /* commit pod ps.pods[pod_index] to node (AssumePod); rollback undoes it (Unreserve/ForgetPod).
  * The deltas travel in the kernel's arguments (no upload). */
 int kss_commit(kss_ctx* ctx, const kss_podset* ps, int32_t pod_index, int32_t node);

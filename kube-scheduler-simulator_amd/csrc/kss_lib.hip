@@ -204,16 +204,17 @@ __global__ __launch_bounds__(KSS_MAX_THREADS) void k_schedule(const DevJob* __re
 
 // The per-pod service grid (kss_service.cuh): W shards of one cluster, commands from the
 // pinned ring starting at command `seq`.
-template <bool GEN>
+template <bool GEN, bool SIMPLE>
 __global__ __launch_bounds__(KSS_MAX_THREADS) void k_service(const DevJob* __restrict__ jobs, kss_profile prof, int W,
                                                              int npt, int bins_cap, int cache_keys,
                                                              unsigned long long* gran, int* err, SvcBox* box,
                                                              unsigned long long* relay, unsigned long long* seen,
-                                                             uint8_t* rec_host, unsigned long long seq, int stamps) {
+                                                             uint8_t* rec_host, unsigned long long seq, int stamps,
+                                                             int xcd) {
   extern __shared__ __attribute__((aligned(16))) long long smem[];
   const DevJob job = jobs[0];
-  service_loop<GEN>(job.c, job, prof, W, npt, bins_cap, cache_keys, gran, err, box, relay, seen, rec_host, seq, 0u, stamps,
-                    smem);
+  service_loop<GEN, SIMPLE>(job.c, job, prof, W, npt, bins_cap, cache_keys, gran, err, box, relay, seen, rec_host, seq, 0u,
+                            stamps, smem, xcd);
 }
 
 #ifndef KSS_SIMPLE_PW
@@ -702,6 +703,9 @@ struct kss_ctx {
     int W = 0, threads = 0, npt = 0, bins_cap = 0, cache_keys = -1;
     size_t shmem = 0;
     bool gen = false;
+    bool simple = false;  // the k_simple-shaped evaluation (svc_simple_eval)
+    DevBuf stat;          // its static words of every staged pod (k_static at the start)
+    bool xcd = false;     // ... on an XCD-local grid (xcd_slot)
   } svc;
   // split grid (kss_split_*): this context runs part split_part of split_n, split_wl shards
   // each; split_inbox is its exchange inbox (uncached device memory, zeroed once), split_peer
@@ -3484,6 +3488,7 @@ static void svc_free(kss_ctx* ctx) {
   svc_free_rec(v);
   if (v.stream) hipStreamDestroy(v.stream);
   v.relay.release();
+  v.stat.release();
   v.gran.release();
   v.err.release();
   v.job.release();
@@ -3504,9 +3509,11 @@ static int svc_launch(kss_ctx* ctx) {
   std::vector<unsigned long long> seen((size_t)v.W, seq0);  // the relay throttle starts from here
   HIP_TRY(hipMemcpyAsync((char*)v.relay.p + relay_bytes, seen.data(), 8 * seen.size(), hipMemcpyHostToDevice, v.stream));
   if (v.W > 1) HIP_TRY(dev_zero(v.gran.p, v.gran.cap, v.stream));  // epochs restart at 0
-  HIP_TRY(dev_zero(v.err.p, 16, v.stream));
+  HIP_TRY(dev_zero(v.err.p, 16, v.stream));  // the error word and xcd_slot's two counters
   v.box->err = 0;
-  const void* fn = v.gen ? (const void*)k_service<true> : (const void*)k_service<false>;
+  v.box->xcd_fail = 0;
+  const void* fn = v.gen ? (const void*)k_service<true, false>
+                          : (v.simple ? (const void*)k_service<false, true> : (const void*)k_service<false, false>);
   HIP_TRY(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)v.shmem));
   const DevJob* jd = (const DevJob*)v.job.p;
   kss_profile pr = ctx->prof;
@@ -3519,12 +3526,16 @@ static int svc_launch(kss_ctx* ctx) {
   uint8_t* rec = v.rec_dev;
   unsigned long long s0 = seq0;
   int stamps = getenv("KSS_SERVICE_STAMPS") ? 1 : 0;
+  if (getenv("KSS_SVC_FULL_FENCE")) stamps |= 4;  // the simple evaluation's record fence as the general chain's
 #ifdef KSS_EXPERIMENTS
   if (getenv("KSS_SERVICE_NO_DIFF")) stamps |= 2;  // every requested row resent (no row diff)
 #endif
+  int xcd = v.xcd ? 1 : 0;
   void* args[] = {(void*)&jd,  (void*)&pr,  (void*)&W,     (void*)&npt,   (void*)&bins, (void*)&ck, (void*)&gran,
-                  (void*)&err, (void*)&box, (void*)&relay, (void*)&seenp, (void*)&rec, (void*)&s0, (void*)&stamps};
-  if (int rc = launch_resident(fn, dim3((unsigned)W), dim3((unsigned)v.threads), args, v.shmem, v.stream)) return rc;
+                  (void*)&err, (void*)&box, (void*)&relay, (void*)&seenp, (void*)&rec, (void*)&s0, (void*)&stamps,
+                  (void*)&xcd};
+  const unsigned grid = (unsigned)(v.xcd ? XCD_GRID_MULT * W : W);
+  if (int rc = launch_resident(fn, dim3(grid), dim3((unsigned)v.threads), args, v.shmem, v.stream)) return rc;
   v.running = true;
   return 0;
 }
@@ -3547,6 +3558,19 @@ static int svc_start_locked(kss_ctx* ctx) {
   const bool window = ctx->prof.pct_nodes_to_score < 100;  // k_schedule's window exchange: W + 1 values
   if (window) W = std::min(W, XW_MAX - NSCAL);
   const PlanNeeds& need = ctx->staged_need;
+  // the k_simple-shaped evaluation (svc_simple_eval): staged default-profile pods (compact records,
+  // no programs), no window, no extended resources, exact f64 arithmetic, W <= 64 (its exchange:
+  // one lane per shard), the node rows cached in LDS (checked below); KSS_SERVICE_GENERAL=1 keeps
+  // the general chain, for comparison.  On an XCD-local grid when its shards fit one XCD's CUs.
+  const bool simple_pre = ctx->spod_ok && !window && !need.general && ctx->dc.n_scalar == 0 && ctx->small_values &&
+                          f64_exact(ctx->f64_cluster, ctx->f64_pods, ctx->staged_n) && !getenv("KSS_SERVICE_GENERAL");
+  const int xcd_cus = ctx->n_cu / XCD_GRID_MULT;
+  // (off by default: the record's stores to host memory from one XCD were slower than the L2
+  // exchange saved -- C2 slim 20.9 -> 29.0 us, r5o_perpod.json; KSS_SVC_XCD=1 turns it on)
+  static const bool svc_xcd = getenv("KSS_SVC_XCD") && atoi(getenv("KSS_SVC_XCD")) != 0;
+  const bool xcd_ok = svc_xcd && simple_pre && ctx->xcd_mode && ctx->n_cu % XCD_GRID_MULT == 0 && ctx->force_w <= 0 &&
+                      N <= (size_t)xcd_cus * KSS_MAX_THREADS * KSS_MAX_NPT;
+  if (xcd_ok) W = std::min(W, xcd_cus);
   if (W > 1 && need.xw > XW_MAX) return fail(KSS_E_UNSUPPORTED, "topology histograms too large for the service grid");
   if (W > SVC_MAX_SHARDS || W > ctx->n_cu) return fail(KSS_E_UNSUPPORTED, "cluster too large for the service grid");
   Geometry g;
@@ -3613,7 +3637,28 @@ static int svc_start_locked(kss_ctx* ctx) {
   job.slot_bytes = SL.bytes;
   job.prof = ctx->prof;
   job.cursor = (int32_t*)ctx->cursor_buf.p;
+  v.simple = simple_pre && cache_keys >= 0 && g.W <= 64;
+  v.xcd = v.simple && xcd_ok && g.W <= xcd_cus && g.W > 1;
+  job.spods = v.simple ? (const SPod*)ctx->spod_buf.p : nullptr;
+  // the static words of every staged pod (4 bytes per pod and node, at most 4 GiB): one load per
+  // evaluation instead of the pod's requirement chains from HBM (KSS_SVC_NO_STATIC=1: inline)
+  const size_t stat_bytes = sizeof(uint32_t) * (size_t)std::max(ctx->staged_n, 1) * std::max<size_t>(N, 1);
+  const bool pre_static = v.simple && stat_bytes <= ((size_t)4 << 30) && !getenv("KSS_SVC_NO_STATIC");
+  if (pre_static && (rc = v.stat.ensure(stat_bytes))) return rc;
+  job.stat = pre_static ? (uint32_t*)v.stat.p : nullptr;
   HIP_TRY(hipMemcpyAsync(v.job.p, &job, sizeof(DevJob), hipMemcpyHostToDevice, v.stream));
+  if (pre_static) {
+    const dim3 sgrid((unsigned)(std::max<size_t>(N, 1) + 1023) / 1024,
+                     (unsigned)((ctx->staged_n + STATIC_PODS - 1) / STATIC_PODS), 1u);
+    const kss_profile pr = ctx->prof;
+    if (same_profile(pr, default_profile_c()))
+      hipLaunchKernelGGL(k_static<true>, sgrid, dim3(256), 0, v.stream, (const DevJob*)v.job.p, pr, 0, ctx->staged_n, 0,
+                         (int)N);
+    else
+      hipLaunchKernelGGL(k_static<false>, sgrid, dim3(256), 0, v.stream, (const DevJob*)v.job.p, pr, 0, ctx->staged_n, 0,
+                         (int)N);
+    HIP_TRY(hipGetLastError());
+  }
   v.W = g.W;
   v.threads = g.threads;
   v.npt = g.npt;
@@ -3693,6 +3738,13 @@ static int svc_stop(kss_ctx* ctx) {
   return 0;
 }
 
+int kss_service_mode(kss_ctx* ctx, int32_t* mode) {
+  if (!ctx || !mode) return fail(KSS_E_INVAL, "bad arguments");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  *mode = ctx->svc.W > 0 ? (ctx->svc.simple ? (ctx->svc.xcd ? 2 : 1) : 0) : -1;
+  return 0;
+}
+
 int kss_service_start(kss_ctx* ctx) {
   if (!ctx) return fail(KSS_E_INVAL, "null ctx");
   KSS_SVC_QUIESCE(ctx);
@@ -3733,6 +3785,7 @@ static int svc_eval_wait(kss_ctx* ctx, int32_t pod_index, uint32_t fields, bool 
       if (!svc_alive(ctx)) {
         if (__atomic_load_n(&v.box->consumed, __ATOMIC_ACQUIRE) <= seq) {  // left idle before taking it
           v.running = false;
+          if (v.box->xcd_fail) v.xcd = false;  // XCD 0 had too few free CUs: relaunch unrestricted
           if (int rc = svc_launch(ctx)) return rc;
         } else {
           v.running = false;
@@ -3837,10 +3890,10 @@ static int svc_commit(kss_ctx* ctx, int32_t pod_index, int32_t node, int sign) {
 }
 
 int kss_service_commit(kss_ctx* ctx, int32_t pod_index, int32_t node) { return svc_commit(ctx, pod_index, node, 1); }
-int kss_service_stamps(kss_ctx* ctx, uint64_t* out5) {
-  if (!ctx || !out5) return fail(KSS_E_INVAL, "bad arguments");
+int kss_service_stamps(kss_ctx* ctx, uint64_t* out8) {
+  if (!ctx || !out8) return fail(KSS_E_INVAL, "bad arguments");
   if (!ctx->svc.box) return fail(KSS_E_INVAL, "no service grid");
-  for (int i = 0; i < 5; i++) out5[i] = __atomic_load_n(&ctx->svc.box->stamp[i], __ATOMIC_ACQUIRE);
+  for (int i = 0; i < 8; i++) out8[i] = __atomic_load_n(&ctx->svc.box->stamp[i], __ATOMIC_ACQUIRE);
   return 0;
 }
 

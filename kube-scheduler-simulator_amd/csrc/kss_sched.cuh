@@ -113,6 +113,8 @@ struct SharedHdr {
   unsigned svc_dirty;  // the service grid: record rows whose shard segment changed (kss_service.cuh)
   unsigned svc_ovf;    // the service grid: a compact record value did not fit its narrow type
   int cmd[4];   // the service grid's current command (kss_service.cuh)
+  int svc_pf;   // the service grid's prefetched pod (its static words and record in LDS), -1 none
+  int pad_[3];
 };
 
 __device__ __forceinline__ SharedHdr& shdr(long long* smem) { return *reinterpret_cast<SharedHdr*>(smem); }

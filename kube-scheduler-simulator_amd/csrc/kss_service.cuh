@@ -14,7 +14,9 @@
 //     EVAL      schedule_pod (kss_sched.cuh) into the HBM record slot, then copies its own
 //               node range of the requested record fields into the pinned host record,
 //               fences at system scope and stores done[w] = k + 1 (| SVC_DONE_OVF when a
-//               compact record value did not fit)
+//               compact record value did not fit); a SIMPLE grid (staged default-profile
+//               pods) runs svc_simple_eval instead: the k_simple chain, record rows stored
+//               from registers
 //     COMMIT / ROLLBACK   the owning shard applies AssumePod / ForgetPod (commit_pod)
 //     STOP      leave (after writing the LDS node cache back)
 //
@@ -58,6 +60,8 @@ struct SvcBox {
   PodMeta meta;                 // outcome of the last EVAL (shard 0)
   int32_t err;                  // an exchange timed out
   int32_t running;              // 1 while the grid runs (shard 0)
+  int32_t xcd_fail;             // an XCD-local launch found fewer workgroups on XCD 0 than shards
+  int32_t pad;
 };
 
 // Every access to the pinned box and to the relay goes through address-space-1 pointers
@@ -271,15 +275,352 @@ __device__ __forceinline__ unsigned svc_changed_rows(const uint8_t* a, const uin
   return word;
 }
 
-template <bool GEN>
+// ---------------------------------------------------------------------------
+// The k_simple-shaped evaluation (SIMPLE grids: staged default-profile pods -- no spread /
+// inter-pod programs, host ports, node-cached images, volumes or extended resources -- at
+// percentageOfNodesToScore 100).  Per node, from the shard's LDS node rows: the static part of
+// the cycle (static_word: NodeUnschedulable, NodeName, TaintToleration, NodeAffinity and their raw
+// scores) and the state-dependent part (dyn_eval: NodeResourcesFit, the Fit and
+// BalancedAllocation scores) as k_simple computes them, one statistics exchange {feasible, max
+// TaintToleration, max NodeAffinity}, NormalizeScore and the weighted total, one key exchange.
+// The record rows asked for go from registers straight into the pinned host record (the HBM
+// slot and its copy are skipped).  Entries equal schedule_pod<false>'s canonical record.
+// ---------------------------------------------------------------------------
+// The SIMPLE grid's exchange (W <= 64 shards): K 64-bit values per shard, ops[k] OP_SUM / OP_MAX.
+// The workgroup folds its waves in LDS, lane 0 of wave 0 publishes 2K granules {epoch, half}
+// (a plain store when every shard runs on one XCD: the line stays in its L2; else agent scope),
+// lane l < W of wave 0 polls shard l's granules (agent-scope loads, bounded) and the wave folds
+// them; every lane gets the result.  One round trip per exchange, no LDS atomics.
+constexpr int SVC_XG = 8;  // granules per shard row (64 bytes)
+
+// Wave 0's part (out of line: the caller's registers stay free): publish xv[0..K) as 2K granules
+// {epoch, half}, poll every shard's row (lane l: shard l), fold with the operators (opbits: 2 bits
+// per value) and leave the result in xv.  False (abort set, error raised) after the wait bound.
+__device__ __noinline__ bool svc_sweep(long long* smem, unsigned long long* gran, int W, int wself, unsigned ep, int* err,
+                                       int K, unsigned opbits, bool plain) {
+  long long* xv = xvec(smem);
+  const int lane = threadIdx.x & 63;
+  const unsigned long long tag = (unsigned long long)ep << 32;
+  unsigned long long* row = gran + ((size_t)(ep & 1) * W) * SVC_XG;
+  if (lane < 2 * K) {  // lane 2k / 2k+1: value k's low / high half
+    const unsigned long long u = (unsigned long long)xv[lane >> 1];
+    const unsigned long long g = tag | ((lane & 1) ? (u >> 32) : (u & 0xFFFFFFFFull));
+    unsigned long long* p = row + (size_t)wself * SVC_XG + lane;
+    if (plain) asm volatile("global_store_dwordx2 %0, %1, off" ::"v"(p), "v"(g) : "memory");
+    else __hip_atomic_store(gp(p), g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  unsigned long long w2[SVC_XG];
+  long long t0 = 0;
+  for (unsigned spins = 0;; ++spins) {
+    bool ok = true;
+    if (lane < W) {
+      KSS_GLOBAL const unsigned long long* g = gp(row) + (size_t)lane * SVC_XG;
+#pragma unroll
+      for (int i = 0; i < SVC_XG; i++)
+        if (i < 2 * K) w2[i] = __hip_atomic_load(g + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+      for (int i = 0; i < SVC_XG; i++)
+        if (i < 2 * K) ok &= (w2[i] >> 32) == ep;
+    }
+    if (__all(ok)) break;
+    if (spin_expired(spins, t0)) {
+      if (lane == 0) err_raise(err, 1);
+      return false;
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < SVC_XG / 2; k++) {
+    if (k >= K) break;
+    const int op = (int)((opbits >> (2 * k)) & 3u);
+    long long v = lane < W ? (long long)((w2[2 * k + 1] << 32) | (w2[2 * k] & 0xFFFFFFFFull)) : op_identity(op);
+    v = wave_reduce(v, op);
+    if (lane == 0) xv[k] = v;
+  }
+  return true;
+}
+
+// The SIMPLE grid's exchange (W <= 64 shards): K 64-bit values per shard, ops[k] OP_SUM / OP_MAX.
+// The workgroup folds its waves in LDS, wave 0 publishes 2K granules {epoch, half} (a plain store
+// when every shard runs on one XCD: the line stays in its L2; else agent scope) and polls shard
+// l's row on lane l (agent-scope loads, bounded); every lane gets the result.  One round trip per
+// exchange, no LDS atomics.
+template <int K>
+__device__ __forceinline__ bool svc_xchg(long long* smem, Shard& S, bool plain, long long (&v)[K], const int (&ops)[K]) {
+  static_assert(2 * K <= SVC_XG, "granule row");
+  SharedHdr& h = shdr(smem);
+  long long* xv = xvec(smem);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+#pragma unroll
+  for (int k = 0; k < K; k++) {
+    const long long r = wave_reduce(v[k], ops[k]);
+    if (lane == 0) h.red[wave][k] = r;
+  }
+  __syncthreads();
+  if (threadIdx.x < K) {
+    const int k = threadIdx.x;
+    int op = OP_SUM;
+#pragma unroll
+    for (int q = 0; q < K; q++)
+      if (q == k) op = ops[q];
+    long long r = h.red[0][k];
+    for (int x = 1; x < nw; x++) r = op_apply(op, r, h.red[x][k]);
+    xv[k] = r;
+  }
+  __syncthreads();
+  if (S.W > 1) {
+    unsigned opbits = 0;
+#pragma unroll
+    for (int k = 0; k < K; k++) opbits |= (unsigned)ops[k] << (2 * k);
+    ++S.epoch;
+    if (wave == 0 && !svc_sweep(smem, S.gran, S.W, S.w, S.epoch, S.err, K, opbits, plain) && lane == 0) h.abort = 1;
+    __syncthreads();
+    if (h.abort) return false;
+  }
+#pragma unroll
+  for (int k = 0; k < K; k++) v[k] = xv[k];
+  __syncthreads();  // xv may be rewritten by the next exchange
+  return true;
+}
+
+template <bool COMPACT>
+__device__ __forceinline__ void svc_put(uint8_t* host, size_t off, size_t e, int es, int64_t v) {
+  KSS_GLOBAL uint8_t* p = gp(host) + off + e * (size_t)es;
+  if (es == 1) *p = (uint8_t)v;
+  else if (es == 2) *reinterpret_cast<KSS_GLOBAL uint16_t*>(p) = (uint16_t)v;
+  else if (es == 4) *reinterpret_cast<KSS_GLOBAL int32_t*>(p) = (int32_t)v;
+  else *reinterpret_cast<KSS_GLOBAL int64_t*>(p) = v;
+}
+
+// Speculative prefetch for the next evaluation (the plugin evaluates the staged pods in order):
+// pod k's static words of this shard's nodes into the slot array the simple evaluation does not
+// use (ipa), its compact record into the header's pod area, tagged svc_pf = k.  Issued after an
+// evaluation's done flag, it completes while the host reads the record and posts the next command;
+// an evaluation of another pod loads from HBM as before.
+static_assert(sizeof(SPod) <= sizeof(kss_pod), "the compact record fits the header's pod area");
+__device__ __forceinline__ void svc_prefetch(const DevJob& job, long long* smem, const Shard& S, int bins_cap, int npt,
+                                             int k) {
+  SharedHdr& H = shdr(smem);
+  const int tid = threadIdx.x, nt = blockDim.x;
+  const size_t N = (size_t)job.c.N;
+  if (!job.stat || k < 0 || k >= job.n_pods) {
+    if (tid == 0) H.svc_pf = -1;
+    __syncthreads();
+    return;
+  }
+  const SlotArrays sa = slot_arrays(smem, bins_cap, npt * nt);
+  for (int j = 0; j < npt; j++) {
+    const int n = S.lo + j * nt + tid;
+    if (n < S.hi) sa.ipa[j * nt + tid] = ld_ag(gp(job.stat) + (size_t)k * N + n);
+  }
+  constexpr int SW = (int)(sizeof(SPod) / 4);
+  const uint32_t* src = reinterpret_cast<const uint32_t*>(job.spods + k);
+  uint32_t* dst = reinterpret_cast<uint32_t*>(&H.pod);
+  for (int i = tid; i < SW; i += nt) dst[i] = src[i];
+  if (tid == 0) H.svc_pf = k;
+  __syncthreads();
+}
+
+template <bool COMPACT>
+__device__ bool svc_simple_eval(const DevCluster& c, const DevJob& job, const kss_profile& prof, int pi, long long* smem,
+                                Shard& S, int bins_cap, int npt, unsigned want, uint8_t* host, PodMeta& meta, bool plain,
+                                unsigned long long* st3) {
+  const int tid = threadIdx.x, nt = blockDim.x;
+  const size_t N = (size_t)c.N;
+  const SlotLayout L(N);
+  const CompactLayout CL(N);
+  const kss_pod& p = job.P.pods[pi];
+  SharedHdr& H = shdr(smem);
+  const bool hit = H.svc_pf == pi;  // the prefetch guessed this pod: words and record already in LDS
+  const SPod& q = hit ? *reinterpret_cast<const SPod*>(&H.pod) : job.spods[pi];
+  const SlotArrays sa = slot_arrays(smem, bins_cap, npt * nt);
+  // every HBM load of the evaluation first, in flight together: the static words of this lane's
+  // nodes (the table k_static filled) -- no branch between them and the command
+  // (staged through the slot array the simple evaluation leaves unused: a register array indexed
+  // in the node loop would live in scratch)
+  if (job.stat && !hit) {
+    uint32_t wpre[KSS_MAX_NPT];
+#pragma unroll
+    for (int k = 0; k < KSS_MAX_NPT; k++) {
+      const int n = S.lo + k * nt + tid;
+      wpre[k] = (k < npt && n < S.hi) ? ld_ag(gp(job.stat) + (size_t)pi * N + n) : 0u;
+    }
+#pragma unroll
+    for (int k = 0; k < KSS_MAX_NPT; k++)
+      if (k < npt) sa.pts[k * nt + tid] = wpre[k];
+  }
+  meta.chosen = -1;
+  meta.n_feasible = 0;
+  meta.scored = 0;
+  meta.status = 0;
+  meta.best_total = 0;
+  // row offsets in the host record: fail, detail, total, raw x, norm x
+  const size_t o_fail = COMPACT ? CL.fail : L.fail, o_det = COMPACT ? CL.detail : L.detail;
+  const size_t o_tot = COMPACT ? CL.total : L.total, o_raw = COMPACT ? CL.raw : L.raw, o_norm = COMPACT ? CL.norm : L.norm;
+  const int es_tot = COMPACT ? 4 : 8, es_raw = COMPACT ? 4 : 8, es_norm = COMPACT ? 1 : 8;
+  const bool w_fail = want & 1u, w_det = (want >> 1) & 1u, w_tot = (want >> 2) & 1u;
+  const bool w_raw = (want >> 3) & 1u, w_norm = (want >> (3 + KSS_NSCORE)) & 1u;  // every raw / norm row or none
+  if (q.status != 0) {  // PreFilter failure (kss_pod.prefilter_status): no node evaluated
+    for (int k = 0; k < npt; k++) {
+      const int n = S.lo + k * nt + tid;
+      if (n >= S.hi) continue;
+      if (w_fail) svc_put<COMPACT>(host, o_fail, (size_t)n, 1, KSS_F_NOT_EVALUATED);
+      if (w_det) svc_put<COMPACT>(host, o_det, (size_t)n, 2, 0);
+      if (w_tot) svc_put<COMPACT>(host, o_tot, (size_t)n, es_tot, 0);
+#pragma unroll
+      for (int x = 0; x < KSS_NSCORE; x++) {
+        if (w_raw) svc_put<COMPACT>(host, o_raw, (size_t)x * N + n, es_raw, 0);
+        if (w_norm) svc_put<COMPACT>(host, o_norm, (size_t)x * N + n, es_norm, 0);
+      }
+    }
+    meta.status = q.status == KSS_PF_ERROR ? 3 : 2;
+    return true;
+  }
+  const uint32_t en = prof.filter_enabled;
+  long long nf = 0, max_tt = 0, max_na = 0;
+  for (int k = 0; k < npt; k++) {
+    const int n = S.lo + k * nt + tid;
+    const int si = k * nt + tid;
+    if (n >= S.hi) {
+      sa.fail[si] = KSS_F_NOT_EVALUATED;
+      continue;
+    }
+    const NodeRow row = load_row(c, n);
+    // the static word: precomputed for every staged pod at the grid's start (k_static into
+    // job.stat, loaded above) or, without that table, evaluated here
+    const uint32_t w = !job.stat ? static_word(c, job.P, p, prof, n, row.flags, row.th, row.ts)
+                                 : (uint32_t)(hit ? sa.ipa[si] : sa.pts[si]);
+    DynRow dr;
+#pragma unroll
+    for (int r = 0; r < 3; r++) {
+      dr.alloc[r] = (double)row.alloc[r];
+      dr.req[r] = (double)row.req[r];
+      dr.inv[r] = row.alloc[r] > 0 ? 1.0 / (double)row.alloc[r] : 0.0;
+    }
+    dr.nz[0] = (double)row.nz[0];
+    dr.nz[1] = (double)row.nz[1];
+    dr.pods = row.pods;
+    dr.allowed = row.allowed;
+    const SVal e = dyn_eval(prof, q, w, dr);
+    uint16_t detail = 0;
+    if (e.f == KSS_F_TAINT_TOLERATION || e.f == KSS_F_NODE_RESOURCES_FIT)
+      (void)filter_local(c, job.P, p, en, n, row, &detail);  // the failure's detail (taint id, fit bits)
+    sa.fail[si] = e.f | ((int)detail << 8);
+    sa.tt[si] = e.tt;
+    sa.na[si] = e.na;
+    sa.fit[si] = e.fit;
+    sa.ba[si] = e.ba;
+    if (e.f == KSS_F_PASS) {
+      nf++;
+      max_tt = e.tt > max_tt ? e.tt : max_tt;
+      max_na = e.na > max_na ? e.na : max_na;
+    }
+  }
+  if (st3) st3[0] = wall_clock64();
+  {
+    long long v[3] = {nf, max_tt, max_na};
+    const int op[3] = {OP_SUM, OP_MAX, OP_MAX};
+    if (!svc_xchg(smem, S, plain, v, op)) return false;
+    if (st3) st3[1] = wall_clock64();
+    nf = v[0];
+    max_tt = v[1];
+    max_na = v[2];
+  }
+  const bool scored = nf > 1;
+  const float rtt = max_tt ? __builtin_amdgcn_rcpf((float)max_tt) : 0.f, rna = max_na ? __builtin_amdgcn_rcpf((float)max_na) : 0.f;
+  // the selectHost key first (its exchange is the chain), then the record rows
+  long long best = 0;
+  for (int k = 0; k < npt; k++) {
+    const int n = S.lo + k * nt + tid;
+    const int si = k * nt + tid;
+    if (n >= S.hi || (sa.fail[si] & 0xFF) != KSS_F_PASS) continue;
+    const SVal e{KSS_F_PASS, sa.tt[si], (int)sa.na[si], sa.fit[si], sa.ba[si]};
+    const long long key = simple_key(prof, e, scored, (int)max_tt, rtt, (int)max_na, rna, (uint32_t)(c.node_base + n));
+    best = key > best ? key : best;
+  }
+  if (st3) st3[2] = wall_clock64();
+  if (nf > 0) {
+    long long v[1] = {best};
+    const int op[1] = {OP_MAX};
+    if (!svc_xchg(smem, S, plain, v, op)) return false;
+    best = v[0];
+  }
+  for (int k = 0; k < npt; k++) {
+    const int n = S.lo + k * nt + tid;
+    const int si = k * nt + tid;
+    if (n >= S.hi) continue;
+    const int fw = sa.fail[si];
+    const int f = fw & 0xFF;
+    SVal e{f, sa.tt[si], (int)sa.na[si], sa.fit[si], sa.ba[si]};
+    const bool pass = f == KSS_F_PASS;
+    // the row values as scalars (a local array indexed in the store loop would go to scratch)
+    const int64_t r_tt = pass ? e.tt : 0, r_na = pass ? e.na : 0, r_fit = pass ? e.fit : 0, r_ba = pass ? e.ba : 0;
+    int64_t n_tt = 0, n_na = 0, n_fit = 0, n_pts = 0, n_ba = 0, total = 0;
+    if (pass && scored) {
+      const long long key = simple_key(prof, e, scored, (int)max_tt, rtt, (int)max_na, rna, (uint32_t)(c.node_base + n));
+      n_tt = max_tt == 0 ? 100 : 100 - small_div(100 * e.tt, (int)max_tt, rtt);
+      n_na = max_na != 0 ? small_div(100 * e.na, (int)max_na, rna) : e.na;
+      n_fit = e.fit;
+      n_pts = 100;
+      n_ba = e.ba;
+      total = (int64_t)(((unsigned long long)key) >> 32);
+    }
+    if (w_fail) svc_put<COMPACT>(host, o_fail, (size_t)n, 1, f);
+    if (w_det) svc_put<COMPACT>(host, o_det, (size_t)n, 2, (uint16_t)(fw >> 8));
+    if (w_tot) svc_put<COMPACT>(host, o_tot, (size_t)n, es_tot, total);
+    if (w_raw) {
+      svc_put<COMPACT>(host, o_raw, (size_t)KSS_S_TAINT_TOLERATION * N + n, es_raw, r_tt);
+      svc_put<COMPACT>(host, o_raw, (size_t)KSS_S_NODE_AFFINITY * N + n, es_raw, r_na);
+      svc_put<COMPACT>(host, o_raw, (size_t)KSS_S_NODE_RESOURCES_FIT * N + n, es_raw, r_fit);
+      svc_put<COMPACT>(host, o_raw, (size_t)KSS_S_VOLUME_BINDING * N + n, es_raw, 0);
+      svc_put<COMPACT>(host, o_raw, (size_t)KSS_S_POD_TOPOLOGY_SPREAD * N + n, es_raw, 0);
+      svc_put<COMPACT>(host, o_raw, (size_t)KSS_S_INTER_POD_AFFINITY * N + n, es_raw, 0);
+      svc_put<COMPACT>(host, o_raw, (size_t)KSS_S_BALANCED_ALLOCATION * N + n, es_raw, r_ba);
+      svc_put<COMPACT>(host, o_raw, (size_t)KSS_S_IMAGE_LOCALITY * N + n, es_raw, 0);
+    }
+    if (w_norm) {
+      svc_put<COMPACT>(host, o_norm, (size_t)KSS_S_TAINT_TOLERATION * N + n, es_norm, n_tt);
+      svc_put<COMPACT>(host, o_norm, (size_t)KSS_S_NODE_AFFINITY * N + n, es_norm, n_na);
+      svc_put<COMPACT>(host, o_norm, (size_t)KSS_S_NODE_RESOURCES_FIT * N + n, es_norm, n_fit);
+      svc_put<COMPACT>(host, o_norm, (size_t)KSS_S_VOLUME_BINDING * N + n, es_norm, 0);
+      svc_put<COMPACT>(host, o_norm, (size_t)KSS_S_POD_TOPOLOGY_SPREAD * N + n, es_norm, n_pts);
+      svc_put<COMPACT>(host, o_norm, (size_t)KSS_S_INTER_POD_AFFINITY * N + n, es_norm, 0);
+      svc_put<COMPACT>(host, o_norm, (size_t)KSS_S_BALANCED_ALLOCATION * N + n, es_norm, n_ba);
+      svc_put<COMPACT>(host, o_norm, (size_t)KSS_S_IMAGE_LOCALITY * N + n, es_norm, 0);
+    }
+  }
+  meta.n_feasible = (int)nf;
+  if (nf == 0) {
+    meta.status = 1;
+    return true;
+  }
+  const unsigned long long ub = (unsigned long long)best;
+  meta.chosen = (int)(0xFFFFFFFFull - (ub & 0xFFFFFFFFull));
+  meta.scored = scored ? 1 : 0;
+  meta.best_total = scored ? (int64_t)(ub >> 32) : 0;
+  return true;
+}
+
+template <bool GEN, bool SIMPLE>
 __device__ void service_loop(DevCluster c, const DevJob& job, const kss_profile& prof, int W, int npt, int bins_cap,
                              int cache_keys, unsigned long long* gran, int* err, SvcBox* box_flat,
                              unsigned long long* relay_flat, unsigned long long* seen_flat, uint8_t* rec_host,
-                             unsigned long long seq, unsigned epoch0, int stamps, long long* smem) {
+                             unsigned long long seq, unsigned epoch0, int stamps, long long* smem, int xcd) {
   KSS_GLOBAL SvcBox* box = gp(box_flat);
   KSS_GLOBAL unsigned long long* relay = gp(relay_flat);
   KSS_GLOBAL unsigned long long* seen = gp(seen_flat);
-  const int w = blockIdx.x;
+  int w = blockIdx.x;
+  if (SIMPLE && xcd) {
+    // XCD-local grid (xcd_slot): the first W workgroups that run on XCD 0 become the shards, the
+    // others leave; the exchanges and the relay then stay in that XCD's L2.  Too few on XCD 0:
+    // every workgroup leaves before taking a command and the host relaunches unrestricted.
+    if (threadIdx.x == 0) shdr(smem).cmd[0] = xcd_slot(err + 2, W, (int)gridDim.x, err);
+    __syncthreads();
+    w = shdr(smem).cmd[0];
+    __syncthreads();
+    if (w == -2 && threadIdx.x == 0) __hip_atomic_store(&box->xcd_fail, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (w < 0) return;
+  }
+  const bool plain = SIMPLE && xcd;  // XCD-local granule and relay stores
   const size_t N = (size_t)c.N;
   const SlotLayout L(N);
   if (threadIdx.x == 0) shdr(smem).abort = 0;
@@ -308,6 +649,9 @@ __device__ void service_loop(DevCluster c, const DevJob& job, const kss_profile&
     cache_fill(c, S.hi, c.ncl ? c.n_keys : 0);
     __syncthreads();
   }
+  if (threadIdx.x == 0) shdr(smem).svc_pf = -1;  // no prefetched pod (LDS holds garbage until written)
+  __syncthreads();
+  if (SIMPLE) svc_prefetch(job, smem, S, bins_cap, npt, 0);
   int* cmd = shdr(smem).cmd;
   if (w == 0 && threadIdx.x == 0) __hip_atomic_store(&box->running, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   unsigned long long st0 = 0, st1 = 0, st2 = 0, st4 = 0;  // diagnostic clocks of shard 0's lane 0 (stamps)
@@ -358,8 +702,15 @@ __device__ void service_loop(DevCluster c, const DevJob& job, const kss_profile&
             __builtin_amdgcn_s_sleep(1);
           }
         }
-        __hip_atomic_store(slot + 1, svc_w1(seq, node), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(slot, svc_w0(seq, op, fields, pod), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (plain) {  // both words in one 16-byte plain store (XCD 0's L2; the shards poll it there)
+          const unsigned long long w0 = svc_w0(seq, op, fields, pod), w1 = svc_w1(seq, node);
+          typedef unsigned int svc_u32x4 __attribute__((ext_vector_type(4)));
+          const svc_u32x4 q = {(unsigned)w0, (unsigned)(w0 >> 32), (unsigned)w1, (unsigned)(w1 >> 32)};
+          asm volatile("global_store_dwordx4 %0, %1, off" ::"v"((unsigned long long*)slot), "v"(q) : "memory");
+        } else {
+          __hip_atomic_store(slot + 1, svc_w1(seq, node), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(slot, svc_w0(seq, op, fields, pod), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
         if (got) __hip_atomic_store(&box->consumed, seq + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         st1 = wall_clock64();
       } else {
@@ -387,7 +738,51 @@ __device__ void service_loop(DevCluster c, const DevJob& job, const kss_profile&
     const int op = cmd[0], pi = cmd[1], node = cmd[2], fields = cmd[3];
     __syncthreads();  // the command words may be rewritten by the next iteration's lane 0
     if (op == SVC_STOP) break;
-    if (op == SVC_EVAL) {
+    if (SIMPLE && op == SVC_EVAL) {
+      PodMeta m;
+      const bool compact = (node & 1) != 0;
+      unsigned want = 0;
+      for (int r = 0; r < SVC_ROWS; r++) want |= (fields & svc_row_field(r)) ? 1u << r : 0u;
+      unsigned long long st3[3] = {0, 0, 0};
+      unsigned long long* sp3 = ((stamps & 1) && w == 0 && threadIdx.x == 0) ? st3 : nullptr;
+      const bool ok = compact ? svc_simple_eval<true>(c, job, prof, pi, smem, S, bins_cap, npt, want, crec_host, m, plain, sp3)
+                              : svc_simple_eval<false>(c, job, prof, pi, smem, S, bins_cap, npt, want, rec_host, m, plain, sp3);
+      if (!ok) {
+        if (threadIdx.x == 0) __hip_atomic_store(&box->err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        break;
+      }
+      if ((stamps & 1) && w == 0 && threadIdx.x == 0) st2 = st4 = wall_clock64();
+      if (w == 0 && threadIdx.x == 0) {
+        KSS_GLOBAL int32_t* mm = reinterpret_cast<KSS_GLOBAL int32_t*>(&box->meta);
+        mm[0] = m.chosen;
+        mm[1] = m.n_feasible;
+        mm[2] = m.scored;
+        mm[3] = m.status;
+        *reinterpret_cast<KSS_GLOBAL int64_t*>(mm + 4) = m.best_total;
+      }
+      if (stamps & 4) {
+        __threadfence_system();  // (KSS_SVC_FULL_FENCE: every lane's fence, as the general chain)
+      } else {
+        // the record went to coherent (uncached) host memory: each wave waits for its own stores'
+        // completion; after the barrier lane 0's system-scope release store of done[w] orders them
+        // all before the flag (one L2 write-back per shard instead of one per wave)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      __syncthreads();
+      if ((stamps & 1) && w == 0 && threadIdx.x == 0) {
+        KSS_GLOBAL long long* sp = reinterpret_cast<KSS_GLOBAL long long*>(&box->stamp[0]);
+        sp[0] = (long long)st0;
+        sp[1] = (long long)st1;
+        sp[2] = (long long)st2;
+        sp[3] = wall_clock64();
+        sp[4] = (long long)st4;
+        sp[5] = (long long)st3[0];  // node pass done
+        sp[6] = (long long)st3[1];  // statistics exchange done
+        sp[7] = (long long)st3[2];  // normalise + record stores issued, before the key exchange
+      }
+      if (threadIdx.x == 0) st_sys(&box->done[w], seq + 1);
+      svc_prefetch(job, smem, S, bins_cap, npt, pi + 1);  // the next staged pod, in LDS before its command
+    } else if (op == SVC_EVAL) {
       // two HBM record slots used in turn: a row segment equal to the previous evaluation's,
       // which the host record already holds, is not sent over PCIe again
       uint8_t* base = job.slots + (size_t)parity * job.slot_bytes;

@@ -54,6 +54,7 @@ SIGNATURES = [
     ("kss_service_eval_compact", C.c_int, [C.c_void_p, C.c_int32, C.c_uint32, P(abi.PodCView)]),
     ("kss_service_commit", C.c_int, [C.c_void_p, C.c_int32, C.c_int32]),
     ("kss_service_rollback", C.c_int, [C.c_void_p, C.c_int32, C.c_int32]),
+    ("kss_service_mode", C.c_int, [C.c_void_p, P(C.c_int32)]),
     ("kss_service_stamps", C.c_int, [C.c_void_p, P(C.c_uint64)]),
     ("kss_commit", C.c_int, [C.c_void_p, P(abi.PodSet), C.c_int32, C.c_int32]),
     ("kss_rollback", C.c_int, [C.c_void_p, P(abi.PodSet), C.c_int32, C.c_int32]),
@@ -398,6 +399,12 @@ class Context:
     def service_start(self):
         check(lib().kss_service_start(self.h))
 
+    def service_mode(self) -> int:
+        """1: the k_simple-shaped service evaluation, 0: the general chain, -1: not started."""
+        v = C.c_int32(-1)
+        check(lib().kss_service_mode(self.h, C.byref(v)))
+        return v.value
+
     def service_stop(self):
         check(lib().kss_service_stop(self.h))
 
@@ -424,8 +431,9 @@ class Context:
 
     def service_stamps(self):
         """Shard 0's clock (100 MHz ticks) at command taken / relayed / pod done / record
-        visible / record stores issued (before the system fence)."""
-        out = (C.c_uint64 * 5)()
+        visible / record stores issued (before the system fence), and for the k_simple-shaped
+        evaluation node pass / statistics exchange / record stores before the key exchange."""
+        out = (C.c_uint64 * 8)()
         check(lib().kss_service_stamps(self.h, out))
         return list(out)
 

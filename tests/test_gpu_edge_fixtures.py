@@ -1,8 +1,9 @@
 """The hand-derived filter-branch fixtures (tests/edge_fixtures.py) on the device: every
 reason string, PreFilterResult, system-defaulted spreading and the nodeTree tie-break through
-the C-ABI -- as a recorded batch, as an unrecorded batch (the fast loop kernels) and through
-the per-pod eval/commit API -- against the hand-derived expectations and the object-level
-oracle's annotations byte for byte."""
+the C-ABI -- as a recorded batch, as an unrecorded batch (the fast loop kernels), through
+the per-pod eval/commit API and through the resident service grid (its k_simple-shaped
+evaluation for default-profile pods) -- against the hand-derived expectations and the
+object-level oracle's annotations byte for byte."""
 import pytest
 
 import edge_fixtures as ef
@@ -72,4 +73,29 @@ def test_per_pod_eval_commit_matches_hand_derived(name):
         _check(ctx, cc, ps, j, r, exp, want[j], (name, j))
         if r.chosen >= 0:
             ctx.commit(ps, j, r.chosen)
+    ctx.close()
+
+
+@pytest.mark.parametrize("name", sorted(ef.FIXTURES))
+def test_service_eval_commit_matches_hand_derived(name):
+    """The same fixtures through kss_service_eval / kss_service_commit: the record the grid leaves
+    in the pinned host buffer formats to the oracle's annotations."""
+    nodes, bound, pods, expect = ef.FIXTURES[name]()
+    want = _oracle(nodes, bound, pods)
+    cc, cp, _ = compile_cluster(nodes, bound, pods)
+    ps = cp.as_struct()
+    ctx = _ctx(cc, 1)
+    ctx.stage(ps)
+    N = cc.n_nodes
+    for j, exp in enumerate(expect):
+        v = ctx.service_eval(j)
+        r = native.PodResult(N)
+        for k in ("fail_plugin", "fail_detail", "raw", "norm", "total"):
+            getattr(r, k)[...] = getattr(v, k)
+        r.s.chosen, r.s.n_feasible, r.s.best_total = v.chosen, v.n_feasible, v.best_total
+        r.s.scored, r.s.status = v.scored, v.status
+        _check(ctx, cc, ps, j, r, exp, want[j], (name, j, ctx.service_mode()))
+        if v.chosen >= 0:
+            ctx.service_commit(j, v.chosen)
+    ctx.service_stop()
     ctx.close()

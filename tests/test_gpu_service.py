@@ -63,6 +63,8 @@ def _compare(cluster, pods, n, rollback_every=0):
     for j in range(n):
         got = svc.service_eval(j)
         _same(got, want[j], N, j)
+        if j == 0:
+            mode = svc.service_mode()
         if want[j].chosen >= 0:
             svc.service_commit(j, want[j].chosen)
             if rollback_every and j % rollback_every == 0:
@@ -72,12 +74,26 @@ def _compare(cluster, pods, n, rollback_every=0):
     for k in ("requested", "nonzero", "pod_count"):
         np.testing.assert_array_equal(st_s[k], st_r[k], err_msg=k)
     svc.close()
+    return mode if n else -1
 
 
 @pytest.mark.parametrize("config,n_nodes,n_pods", [(2, 5000, 120), (1, 100, 200), (3, 2000, 80), (4, 6000, 60)])
 def test_service_matches_per_pod_api(config, n_nodes, n_pods):
+    """Default-profile configs (1, 2) run the k_simple-shaped evaluation, program configs (3, 4)
+    the general chain; both equal the per-pod API record for record."""
     s = native.Synth(config, SEED_BASE + config, n_nodes, n_pods)
-    _compare(s.cluster, s.pods, n_pods, rollback_every=7)
+    mode = _compare(s.cluster, s.pods, n_pods, rollback_every=7)
+    assert (mode in (1, 2)) if config in (1, 2) else mode == 0, mode
+    s.close()
+
+
+@pytest.mark.parametrize("config,n_nodes,n_pods", [(2, 5000, 60), (1, 100, 80)])
+def test_general_service_matches_per_pod_api(config, n_nodes, n_pods, monkeypatch):
+    """KSS_SERVICE_GENERAL=1 keeps default-profile pods on the general chain (the comparison
+    the per-pod bench reports)."""
+    monkeypatch.setenv("KSS_SERVICE_GENERAL", "1")
+    s = native.Synth(config, SEED_BASE + config, n_nodes, n_pods)
+    assert _compare(s.cluster, s.pods, n_pods, rollback_every=5) == 0
     s.close()
 
 
