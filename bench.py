@@ -741,7 +741,7 @@ def run_per_pod(args):
     # A/B: the simple evaluation with every lane's system fence (the general chain's record fence),
     # and with the static words evaluated per call instead of the table k_static fills at the start
     ab = {}
-    for env in ("KSS_SVC_FULL_FENCE", "KSS_SVC_NO_STATIC"):
+    for env in ("KSS_SVC_FULL_FENCE", "KSS_SVC_NO_STATIC", "KSS_SVC_INLINE_SWEEP"):
         os.environ[env] = "1"
         ctx.reset()
         el_ab, ev_ab, _, ch_ab = svc_loop(slim_fields)
@@ -789,7 +789,8 @@ def run_per_pod(args):
                              1: "k_simple-shaped evaluation, record stored from registers",
                              0: "general chain (schedule_pod + record copy)"}.get(svc_mode, "not started"),
                     "slim_ab_eval_us_median": {"KSS_SVC_FULL_FENCE=1 (every lane's system fence)": ab["KSS_SVC_FULL_FENCE"],
-                                               "KSS_SVC_NO_STATIC=1 (static words per call)": ab["KSS_SVC_NO_STATIC"]},
+                                               "KSS_SVC_NO_STATIC=1 (static words per call)": ab["KSS_SVC_NO_STATIC"],
+                                               "KSS_SVC_INLINE_SWEEP=1 (the exchange sweep inlined)": ab["KSS_SVC_INLINE_SWEEP"]},
                     "general_chain": {"eval_us_median": float(np.median(ev_g)), "slim_eval_us_median": float(np.median(ev_gs)),
                                       "pods_per_s": n_pods / el_g, "slim_pods_per_s": n_pods / el_gs,
                                       "note": "KSS_SERVICE_GENERAL=1: the chain every program shape takes"},

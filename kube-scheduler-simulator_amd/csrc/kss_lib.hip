@@ -204,7 +204,7 @@ __global__ __launch_bounds__(KSS_MAX_THREADS) void k_schedule(const DevJob* __re
 
 // The per-pod service grid (kss_service.cuh): W shards of one cluster, commands from the
 // pinned ring starting at command `seq`.
-template <bool GEN, bool SIMPLE>
+template <bool GEN, bool SIMPLE, bool INL = false>
 __global__ __launch_bounds__(KSS_MAX_THREADS) void k_service(const DevJob* __restrict__ jobs, kss_profile prof, int W,
                                                              int npt, int bins_cap, int cache_keys,
                                                              unsigned long long* gran, int* err, SvcBox* box,
@@ -213,8 +213,8 @@ __global__ __launch_bounds__(KSS_MAX_THREADS) void k_service(const DevJob* __res
                                                              int xcd) {
   extern __shared__ __attribute__((aligned(16))) long long smem[];
   const DevJob job = jobs[0];
-  service_loop<GEN, SIMPLE>(job.c, job, prof, W, npt, bins_cap, cache_keys, gran, err, box, relay, seen, rec_host, seq, 0u,
-                            stamps, smem, xcd);
+  service_loop<GEN, SIMPLE, INL>(job.c, job, prof, W, npt, bins_cap, cache_keys, gran, err, box, relay, seen, rec_host,
+                                 seq, 0u, stamps, smem, xcd);
 }
 
 #ifndef KSS_SIMPLE_PW
@@ -226,7 +226,8 @@ __global__ __launch_bounds__(KSS_MAX_THREADS) void k_service(const DevJob* __res
 template <bool DEF>
 __global__ __launch_bounds__(KSS_MAX_THREADS) void k_simple(const DevJob* __restrict__ jobs, kss_profile prof, int W,
                                                             int cap, int k0, int k1, unsigned long long* gran, int* err,
-                                                            unsigned long long* stamps, XPeers X, unsigned epoch0) {
+                                                            unsigned long long* stamps, XPeers X, unsigned epoch0,
+                                                            int stat_row0) {
   extern __shared__ __attribute__((aligned(16))) long long smem[];
   const int Wl = X.n > 1 ? X.wl : W;  // shards of this launch (a split grid runs [w_off, w_off + wl))
   SimpleHdr& H = *reinterpret_cast<SimpleHdr*>(smem);
@@ -251,11 +252,12 @@ __global__ __launch_bounds__(KSS_MAX_THREADS) void k_simple(const DevJob* __rest
   const int per = (job.c.N + W - 1) / W, nwave = (int)(blockDim.x >> 6);
   unsigned long long* g = gran ? gran + (size_t)ji * 2 * W * SX_VALS : nullptr;
   unsigned long long* sp = ji == 0 ? stamps : nullptr;
+  const uint32_t* stat = job.stat + (size_t)stat_row0 * (size_t)job.c.N;  // the chunk's half of a double-buffered table
   if (per <= PW_LANES * nwave && KSS_SIMPLE_PW)
-    simple_schedule<DEF, true>(job.c, job.spods, job.stat, job.P.ints, k0, min(k1, job.n_pods), job.chosen, job.meta, P, W,
+    simple_schedule<DEF, true>(job.c, job.spods, stat, job.P.ints, k0, min(k1, job.n_pods), job.chosen, job.meta, P, W,
                                w, cap, g, X, epoch0, err, sp, smem);
   else
-    simple_schedule<DEF, false>(job.c, job.spods, job.stat, job.P.ints, k0, min(k1, job.n_pods), job.chosen, job.meta, P,
+    simple_schedule<DEF, false>(job.c, job.spods, stat, job.P.ints, k0, min(k1, job.n_pods), job.chosen, job.meta, P,
                                 W, w, cap, g, X, epoch0, err, sp, smem);
 }
 
@@ -328,15 +330,31 @@ typedef unsigned int kss_u32x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ void st_ag16(uint32_t* p, kss_u32x4 v) {
   asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
 }
+// lkeys > 0: the block's 1024 nodes' label values of the first lkeys keys are copied into LDS
+// once ([key][node], 4 bytes each) and every requirement reads them there: the label columns were
+// read from L2 / HBM once per (pod, node, requirement) -- ~14 vector loads per static word, the
+// wait that dominated k_static (profiles/r5v: SQ_WAIT_ANY 70% of wave cycles).
+constexpr int STATIC_LKEYS = 16;  // label keys cached (more: the loads stay global)
 template <bool DEF>
 __global__ __launch_bounds__(256) void k_static(const DevJob* __restrict__ jobs, kss_profile prof_arg, int k0, int k1,
-                                                int n_lo, int n_hi) {
+                                                int n_lo, int n_hi, int lkeys, int row0, int ppb) {
+  extern __shared__ int32_t slab[];  // [lkeys][1024]
   const DevJob& job = jobs[blockIdx.z];
   const int N = job.c.N;
-  const int n = n_lo + 4 * (int)(blockIdx.x * 256 + threadIdx.x);  // rows [n_lo, min(n_hi, N)): a split grid's own rows
+  const int nb = n_lo + 4 * (int)(blockIdx.x * 256);  // the block's first node
+  const int n = nb + 4 * (int)threadIdx.x;  // rows [n_lo, min(n_hi, N)): a split grid's own rows
   const int kend = min(k1, job.n_pods);
-  const int kb = k0 + (int)blockIdx.y * STATIC_PODS;
+  const int kb = k0 + (int)blockIdx.y * ppb;  // the block's pods: [kb, kb + ppb)
   const int lim = min(N, n_hi);
+  const bool lds = lkeys > 0 && job.c.n_keys <= lkeys;
+  if (lds) {  // every lane reaches the barrier (no early exit above it)
+    const int nk = job.c.n_keys;
+    for (int i = (int)threadIdx.x; i < nk * 1024; i += 256) {
+      const int key = i >> 10, j = i & 1023;
+      slab[i] = nb + j < lim ? gp(job.c.label_value)[(size_t)key * N + nb + j] : -1;
+    }
+    __syncthreads();
+  }
   if (kb >= kend || n >= lim) return;
   const int cnt = min(4, lim - n);
   uint32_t* stat = job.stat;
@@ -344,25 +362,32 @@ __global__ __launch_bounds__(256) void k_static(const DevJob* __restrict__ jobs,
   const bool quad = cnt == 4 && ((N | n_lo) & 3) == 0 && (sa & 15) == 0;
   const bool pair = ((N | n_lo) & 1) == 0 && (sa & 7) == 0;  // 8-byte pairs at even offsets
   const DevCluster c = job.c;
-  const DevPods P = job.P;
+  const DevPodsK P = pods_k(job.P);
   const kss_profile prof = DEF ? default_profile_c() : prof_arg;
   uint32_t f[4];
   uint64_t th[4], ts[4];
 #pragma unroll
   for (int i = 0; i < 4; i++) {
     const int ni = n + min(i, cnt - 1);
-    f[i] = c.node_flags[ni];
-    th[i] = c.taint_hard[ni];
-    ts[i] = c.taint_soft[ni];
+    f[i] = gp(c.node_flags)[ni];
+    th[i] = gp(c.taint_hard)[ni];
+    ts[i] = gp(c.taint_soft)[ni];
   }
-  for (int t = 0; t < STATIC_PODS; t++) {
+  for (int t = 0; t < ppb; t++) {
     const int k = kb + t;
     if (k >= kend) break;
-    const kss_pod& pod = P.pods[k];
+    const auto& pod = P.pods[k];
     uint32_t w[4];
-#pragma unroll
-    for (int i = 0; i < 4; i++) w[i] = static_word(c, P, pod, prof, n + min(i, cnt - 1), f[i], th[i], ts[i]);
-    uint32_t* dst = &stat[(size_t)(k - k0) * N + n];
+    if (lds)
+      static_words4(c, P, pod, prof, n, cnt, f, th, ts,
+                    [&](int key, int i) { return slab[(key << 10) + (n + min(i, cnt - 1) - nb)]; }, w);
+    else
+      static_words4(c, P, pod, prof, n, cnt, f, th, ts,
+                    [&](int key, int i) {
+                      const int ni = n + min(i, cnt - 1);
+                      return c.ncl ? label_of(c, key, ni) : gp(c.label_value)[(size_t)key * N + ni];
+                    }, w);
+    uint32_t* dst = &stat[(size_t)(row0 + k - k0) * N + n];  // row0: the half of a double-buffered table
     if (quad) {
       st_ag16(dst, kss_u32x4{w[0], w[1], w[2], w[3]});
     } else if (pair) {
@@ -2418,12 +2443,35 @@ static void static_rows(const Geometry& g, const XPeers& X, int max_nodes, int& 
   n_hi = std::min(max_nodes, (X.w_off + X.wl) * per);
 }
 
+// k_static over pods [k0, k1) x rows [n_lo, n_hi) of n_jobs jobs; max_keys: the jobs' largest label-key count
+// (the LDS label copy when it is at most STATIC_LKEYS)
+static void launch_static(hipStream_t st, bool def, const DevJob* jobs, const kss_profile& pr, int n_jobs, int k0, int k1,
+                          int n_lo, int n_hi, int max_keys, int row0 = 0) {
+  const int lk = max_keys > 0 && max_keys <= STATIC_LKEYS ? max_keys : 0;
+  // pods per block: with the LDS label copy, enough pods to amortise loading it (C5: 32 pods of
+  // 1,000 nodes per block, 16k blocks per 512-scenario chunk)
+  int ppb = lk ? 4 * STATIC_PODS : STATIC_PODS;
+  if (const char* e = getenv("KSS_STATIC_PPB")) ppb = std::max(1, std::min(256, atoi(e)));
+  const dim3 sgrid((unsigned)(std::max(n_hi - n_lo, 1) + 1023) / 1024, (unsigned)((k1 - k0 + ppb - 1) / ppb),
+                   (unsigned)n_jobs);
+  const size_t sh = sizeof(int32_t) * 1024 * (size_t)lk;
+  if (def)
+    hipLaunchKernelGGL(k_static<true>, sgrid, dim3(256), sh, st, jobs, pr, k0, k1, n_lo, n_hi, lk, row0, ppb);
+  else
+    hipLaunchKernelGGL(k_static<false>, sgrid, dim3(256), sh, st, jobs, pr, k0, k1, n_lo, n_hi, lk, row0, ppb);
+}
+
 // xcd: one job on an XCD-local grid (xcd_slot); a chunk whose launch reports the placement
 // failure (err = 3, no state touched) is synchronised on and run again unrestricted.
 static int launch_simple(hipStream_t st, const Geometry& g, int n_jobs, const DevJob* jobs, const kss_profile& prof,
                          int n_pods_max, int max_nodes, int chunk, unsigned long long* gran, size_t gran_bytes, int* err,
                          unsigned long long* stamps = nullptr, hipEvent_t* ev = nullptr, const SplitRun* split = nullptr,
-                         int nsc = 0, bool xcd = false, int* xcd_fallbacks = nullptr) {
+                         int nsc = 0, bool xcd = false, int* xcd_fallbacks = nullptr, int max_keys = 0,
+                         hipStream_t st2 = nullptr, std::vector<hipEvent_t>* pev = nullptr) {
+  // st2 (with pev, two events per chunk): the static words of chunk i+1 are computed on st2 into the
+  // other half of a double-buffered table while k_simple runs chunk i on st (each job's table holds
+  // 2 x chunk rows); k_simple of chunk i waits for its k_static, k_static of chunk i+1 for
+  // k_simple of chunk i-1 (the last reader of that half)
   int cap = simple_cap(g);
   const size_t shmem = simple_lds_bytes(cap, nsc);
   const bool def = same_profile(prof, default_profile_c());
@@ -2437,15 +2485,38 @@ static int launch_simple(hipStream_t st, const Geometry& g, int n_jobs, const De
   kss_profile pr = prof;
   int W = g.W, n_lo = 0, n_hi = 0;
   static_rows(g, X, max_nodes, n_lo, n_hi);
+  const bool pipe = st2 && pev && !sp_grid && !xcd;
+  const int n_chunks = (n_pods_max + chunk - 1) / std::max(chunk, 1);
+  if (pipe) {
+    while ((int)pev->size() < 2 * n_chunks) {
+      hipEvent_t e;
+      HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      pev->push_back(e);
+    }
+    // (*pev)[2i]: k_static of chunk i done (st2), (*pev)[2i+1]: k_simple of chunk i done (st)
+    HIP_TRY(hipEventRecord((*pev)[1], st));  // st's work so far (the reset) before st2 writes the table
+    HIP_TRY(hipStreamWaitEvent(st2, (*pev)[1], 0));
+    launch_static(st2, def, jobs, pr, n_jobs, 0, std::min(n_pods_max, chunk), n_lo, n_hi, max_keys, 0);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord((*pev)[0], st2));
+  }
   for (int k0 = 0; k0 < n_pods_max; k0 += chunk) {
     int k1 = std::min(n_pods_max, k0 + chunk);
-    const dim3 sgrid((unsigned)(std::max(n_hi - n_lo, 1) + 1023) / 1024, (unsigned)((k1 - k0 + STATIC_PODS - 1) / STATIC_PODS),
-                     (unsigned)n_jobs);
-    if (def)
-      hipLaunchKernelGGL(k_static<true>, sgrid, dim3(256), 0, st, jobs, pr, k0, k1, n_lo, n_hi);
-    else
-      hipLaunchKernelGGL(k_static<false>, sgrid, dim3(256), 0, st, jobs, pr, k0, k1, n_lo, n_hi);
-    HIP_TRY(hipGetLastError());
+    const int ci_ = k0 / std::max(chunk, 1);
+    int row0 = pipe ? (ci_ & 1) * chunk : 0;
+    if (pipe) {
+      HIP_TRY(hipStreamWaitEvent(st, (*pev)[2 * ci_], 0));  // this chunk's static words
+      if (k1 < n_pods_max) {  // the next chunk's, into the other half, once chunk ci-1 no longer reads it
+        if (ci_ > 0) HIP_TRY(hipStreamWaitEvent(st2, (*pev)[2 * (ci_ - 1) + 1], 0));
+        launch_static(st2, def, jobs, pr, n_jobs, k1, std::min(n_pods_max, k1 + chunk), n_lo, n_hi, max_keys,
+                      ((ci_ + 1) & 1) * chunk);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipEventRecord((*pev)[2 * (ci_ + 1)], st2));
+      }
+    } else {
+      launch_static(st, def, jobs, pr, n_jobs, k0, k1, n_lo, n_hi, max_keys);
+      HIP_TRY(hipGetLastError());
+    }
     unsigned epoch0 = 0;
     unsigned long long* gc = gran;
     if (sp_grid) {
@@ -2455,8 +2526,8 @@ static int launch_simple(hipStream_t st, const Geometry& g, int n_jobs, const De
       HIP_TRY(dev_zero(gran, gran_bytes, st));
     }
     unsigned long long* sp = k0 == 0 ? stamps : nullptr;
-    void* args[] = {(void*)&jobs, (void*)&pr, (void*)&W,  (void*)&cap, (void*)&k0, (void*)&k1,
-                    (void*)&gc,   (void*)&err, (void*)&sp, (void*)&X,   (void*)&epoch0};
+    void* args[] = {(void*)&jobs, (void*)&pr, (void*)&W,  (void*)&cap, (void*)&k0,     (void*)&k1,
+                    (void*)&gc,   (void*)&err, (void*)&sp, (void*)&X,   (void*)&epoch0, (void*)&row0};
     const int ci = k0 / chunk;
     if (ev) HIP_TRY(hipEventRecord(ev[2 * ci], st));
     if (xcd) {
@@ -2479,6 +2550,7 @@ static int launch_simple(hipStream_t st, const Geometry& g, int n_jobs, const De
       HIP_TRY(hipLaunchKernel(fn, grid, block, args, shmem, st));
     }
     if (ev) HIP_TRY(hipEventRecord(ev[2 * ci + 1], st));
+    if (pipe) HIP_TRY(hipEventRecord((*pev)[2 * ci + 1], st));
   }
   hipLaunchKernelGGL(k_counts, dim3((unsigned)((n_pods_max + 255) / 256), (unsigned)n_jobs), dim3(256), 0, st, jobs, 0,
                      n_pods_max);
@@ -2552,11 +2624,7 @@ static int launch_spread(hipStream_t st, const Geometry& g, const GpodNeeds& q, 
   static_rows(g, X, max_nodes, n_lo, n_hi);
   for (int k0 = 0; k0 < n_pods; k0 += chunk) {
     int k1 = std::min(n_pods, k0 + chunk);
-    const dim3 sgrid((unsigned)(std::max(n_hi - n_lo, 1) + 1023) / 1024, (unsigned)((k1 - k0 + STATIC_PODS - 1) / STATIC_PODS), 1u);
-    if (def)
-      hipLaunchKernelGGL(k_static<true>, sgrid, dim3(256), 0, st, jobs, pr, k0, k1, n_lo, n_hi);
-    else
-      hipLaunchKernelGGL(k_static<false>, sgrid, dim3(256), 0, st, jobs, pr, k0, k1, n_lo, n_hi);
+    launch_static(st, def, jobs, pr, 1, k0, k1, n_lo, n_hi, n_keys);
     HIP_TRY(hipGetLastError());
     unsigned epoch0 = 0;
     unsigned long long* gc = gran;
@@ -2918,7 +2986,7 @@ static int run_single_impl(kss_ctx* ctx, const PlanNeeds& need, const DevPods& d
   if (simple)
     rc = launch_simple(ctx->stream, g, 1, jd, ctx->prof, n, (int)N, chunk, gran, gb,
                        errp, stamps, ctx->loop_ev.data(), split ? &srun : nullptr, ctx->dc.n_scalar, ctx->last_xcd[0] != 0,
-                       &ctx->last_xcd[1]);
+                       &ctx->last_xcd[1], ctx->dc.n_keys);
   else if (spread)
   {
     const HandoffLayout hl(g.W, n_res, (int)N, ctx->dc.n_scalar);
@@ -3512,8 +3580,10 @@ static int svc_launch(kss_ctx* ctx) {
   HIP_TRY(dev_zero(v.err.p, 16, v.stream));  // the error word and xcd_slot's two counters
   v.box->err = 0;
   v.box->xcd_fail = 0;
+  const bool inl = getenv("KSS_SVC_INLINE_SWEEP") && atoi(getenv("KSS_SVC_INLINE_SWEEP")) != 0;
   const void* fn = v.gen ? (const void*)k_service<true, false>
-                          : (v.simple ? (const void*)k_service<false, true> : (const void*)k_service<false, false>);
+                         : (v.simple ? (inl ? (const void*)k_service<false, true, true> : (const void*)k_service<false, true>)
+                                     : (const void*)k_service<false, false>);
   HIP_TRY(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)v.shmem));
   const DevJob* jd = (const DevJob*)v.job.p;
   kss_profile pr = ctx->prof;
@@ -3648,15 +3718,8 @@ static int svc_start_locked(kss_ctx* ctx) {
   job.stat = pre_static ? (uint32_t*)v.stat.p : nullptr;
   HIP_TRY(hipMemcpyAsync(v.job.p, &job, sizeof(DevJob), hipMemcpyHostToDevice, v.stream));
   if (pre_static) {
-    const dim3 sgrid((unsigned)(std::max<size_t>(N, 1) + 1023) / 1024,
-                     (unsigned)((ctx->staged_n + STATIC_PODS - 1) / STATIC_PODS), 1u);
-    const kss_profile pr = ctx->prof;
-    if (same_profile(pr, default_profile_c()))
-      hipLaunchKernelGGL(k_static<true>, sgrid, dim3(256), 0, v.stream, (const DevJob*)v.job.p, pr, 0, ctx->staged_n, 0,
-                         (int)N);
-    else
-      hipLaunchKernelGGL(k_static<false>, sgrid, dim3(256), 0, v.stream, (const DevJob*)v.job.p, pr, 0, ctx->staged_n, 0,
-                         (int)N);
+    launch_static(v.stream, same_profile(ctx->prof, default_profile_c()), (const DevJob*)v.job.p, ctx->prof, 1, 0,
+                  ctx->staged_n, 0, (int)N, ctx->dc.n_keys);
     HIP_TRY(hipGetLastError());
   }
   v.W = g.W;
@@ -4104,8 +4167,9 @@ struct kss_sweep {
   int device = 0;
   kss_profile prof{};
   int n_scen = 0;
-  hipStream_t st = nullptr;
+  hipStream_t st = nullptr, st2 = nullptr;  // st2: k_static of the next chunk (double-buffered table)
   hipEvent_t e0 = nullptr, e1 = nullptr;
+  std::vector<hipEvent_t> pev;
   char* arena = nullptr;
   size_t up_bytes = 0;                   // [0, up_bytes): uploaded once (inputs, pristine state, jobs)
   size_t pristine_off = 0, live_off = 0, mut_bytes = 0;
@@ -4123,6 +4187,8 @@ struct kss_sweep {
     if (arena) hipFree(arena);
     if (e0) hipEventDestroy(e0);
     if (e1) hipEventDestroy(e1);
+    for (hipEvent_t e : pev) hipEventDestroy(e);
+    if (st2) hipStreamSynchronize(st2), hipStreamDestroy(st2);
     if (st) hipStreamDestroy(st);
   }
 };
@@ -4214,14 +4280,22 @@ kss_sweep* kss_sweep_create(int32_t device, const kss_profile* prof, int32_t n_s
   sw->cursor_off = dry.last;
   size_t sum_nodes = 0;
   for (int s = 0; s < n_scen; s++) sum_nodes += (size_t)clusters[s].n_nodes;
+  // KSS_SWEEP_PIPE (more than one chunk): two halves of chunk rows per scenario within the same
+  // budget, the next chunk's static words computed on a second stream while k_simple runs this one.
+  // Off by default: C5 ran 13.5 against 12.6 ms per step (r5y: k_simple slows by more than the
+  // k_static time it hides when both share the CUs)
   sw->chunk = simple ? static_chunk(sum_nodes, sw->max_pods) : 0;
+  const bool dbl = simple && sw->chunk < sw->max_pods && getenv("KSS_SWEEP_PIPE") != nullptr;
+  if (dbl) sw->chunk = static_chunk(2 * sum_nodes, sw->max_pods);
+  const int halves = dbl ? 2 : 1;
   if (simple) {
-    dry.put<uint32_t>(nullptr, (size_t)sw->chunk * sum_nodes + 4 * (size_t)n_scen);  // + 16-byte alignment per scenario
+    dry.put<uint32_t>(nullptr, (size_t)halves * sw->chunk * sum_nodes + 4 * (size_t)n_scen);  // + 16-byte alignment per scenario
     sw->stat_off = dry.last;
   }
   const size_t total = dry.o;
   if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&sw->st, hipStreamNonBlocking) != hipSuccess ||
-      hipEventCreate(&sw->e0) != hipSuccess || hipEventCreate(&sw->e1) != hipSuccess) {
+      hipEventCreate(&sw->e0) != hipSuccess || hipEventCreate(&sw->e1) != hipSuccess ||
+      (dbl && hipStreamCreateWithFlags(&sw->st2, hipStreamNonBlocking) != hipSuccess)) {
     fail(KSS_E_DEVICE, "stream/event creation failed");
     return nullptr;
   }
@@ -4267,7 +4341,7 @@ kss_sweep* kss_sweep_create(int32_t device, const kss_profile* prof, int32_t n_s
     o_chosen += (size_t)podsets[s].n_pods;
     if (simple) {
       jobs[s].stat = reinterpret_cast<uint32_t*>(sw->arena + sw->stat_off) + o_stat;
-      o_stat += ((size_t)sw->chunk * (size_t)clusters[s].n_nodes + 3) / 4 * 4;  // 16-byte aligned per scenario
+      o_stat += ((size_t)halves * sw->chunk * (size_t)clusters[s].n_nodes + 3) / 4 * 4;  // 16-byte aligned per scenario
     }
   }
   memcpy(img.get() + sw->jobs_off, jobs.data(), sizeof(DevJob) * n_scen);
@@ -4303,7 +4377,8 @@ int kss_sweep_run(kss_sweep* sw, int32_t* chosen_out, double* device_ms) {
   const DevJob* jobs = reinterpret_cast<const DevJob*>(sw->arena + sw->jobs_off);
   int rc;
   if (sw->simple)
-    rc = launch_simple(st, sw->g, sw->n_scen, jobs, sw->prof, sw->max_pods, sw->max_nodes, sw->chunk, nullptr, 0, err);
+    rc = launch_simple(st, sw->g, sw->n_scen, jobs, sw->prof, sw->max_pods, sw->max_nodes, sw->chunk, nullptr, 0, err, nullptr,
+                       nullptr, nullptr, 0, false, nullptr, sw->max_keys, sw->st2, &sw->pev);
   else
     rc = launch_schedule(st, sw->g, sw->n_scen, sw->need.bins_cap + (sw->prof.pct_nodes_to_score < 100 ? 1 : 0),
                          sw->need.general, sw->max_keys, jobs, sw->prof, nullptr, err);

@@ -339,12 +339,56 @@ __device__ __noinline__ bool svc_sweep(long long* smem, unsigned long long* gran
   return true;
 }
 
+// the same, inlined (KSS_SVC_INLINE_SWEEP=1 selects the kernel built with it: an A/B of the call)
+__device__ __forceinline__ bool svc_sweep_inl(long long* smem, unsigned long long* gran, int W, int wself, unsigned ep, int* err,
+                                       int K, unsigned opbits, bool plain) {
+  long long* xv = xvec(smem);
+  const int lane = threadIdx.x & 63;
+  const unsigned long long tag = (unsigned long long)ep << 32;
+  unsigned long long* row = gran + ((size_t)(ep & 1) * W) * SVC_XG;
+  if (lane < 2 * K) {  // lane 2k / 2k+1: value k's low / high half
+    const unsigned long long u = (unsigned long long)xv[lane >> 1];
+    const unsigned long long g = tag | ((lane & 1) ? (u >> 32) : (u & 0xFFFFFFFFull));
+    unsigned long long* p = row + (size_t)wself * SVC_XG + lane;
+    if (plain) asm volatile("global_store_dwordx2 %0, %1, off" ::"v"(p), "v"(g) : "memory");
+    else __hip_atomic_store(gp(p), g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  unsigned long long w2[SVC_XG];
+  long long t0 = 0;
+  for (unsigned spins = 0;; ++spins) {
+    bool ok = true;
+    if (lane < W) {
+      KSS_GLOBAL const unsigned long long* g = gp(row) + (size_t)lane * SVC_XG;
+#pragma unroll
+      for (int i = 0; i < SVC_XG; i++)
+        if (i < 2 * K) w2[i] = __hip_atomic_load(g + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+      for (int i = 0; i < SVC_XG; i++)
+        if (i < 2 * K) ok &= (w2[i] >> 32) == ep;
+    }
+    if (__all(ok)) break;
+    if (spin_expired(spins, t0)) {
+      if (lane == 0) err_raise(err, 1);
+      return false;
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < SVC_XG / 2; k++) {
+    if (k >= K) break;
+    const int op = (int)((opbits >> (2 * k)) & 3u);
+    long long v = lane < W ? (long long)((w2[2 * k + 1] << 32) | (w2[2 * k] & 0xFFFFFFFFull)) : op_identity(op);
+    v = wave_reduce(v, op);
+    if (lane == 0) xv[k] = v;
+  }
+  return true;
+}
+
 // The SIMPLE grid's exchange (W <= 64 shards): K 64-bit values per shard, ops[k] OP_SUM / OP_MAX.
 // The workgroup folds its waves in LDS, wave 0 publishes 2K granules {epoch, half} (a plain store
 // when every shard runs on one XCD: the line stays in its L2; else agent scope) and polls shard
 // l's row on lane l (agent-scope loads, bounded); every lane gets the result.  One round trip per
 // exchange, no LDS atomics.
-template <int K>
+template <int K, bool INL = false>
 __device__ __forceinline__ bool svc_xchg(long long* smem, Shard& S, bool plain, long long (&v)[K], const int (&ops)[K]) {
   static_assert(2 * K <= SVC_XG, "granule row");
   SharedHdr& h = shdr(smem);
@@ -372,7 +416,11 @@ __device__ __forceinline__ bool svc_xchg(long long* smem, Shard& S, bool plain, 
 #pragma unroll
     for (int k = 0; k < K; k++) opbits |= (unsigned)ops[k] << (2 * k);
     ++S.epoch;
-    if (wave == 0 && !svc_sweep(smem, S.gran, S.W, S.w, S.epoch, S.err, K, opbits, plain) && lane == 0) h.abort = 1;
+    if (wave == 0) {
+      const bool ok = INL ? svc_sweep_inl(smem, S.gran, S.W, S.w, S.epoch, S.err, K, opbits, plain)
+                          : svc_sweep(smem, S.gran, S.W, S.w, S.epoch, S.err, K, opbits, plain);
+      if (!ok && lane == 0) h.abort = 1;
+    }
     __syncthreads();
     if (h.abort) return false;
   }
@@ -420,7 +468,7 @@ __device__ __forceinline__ void svc_prefetch(const DevJob& job, long long* smem,
   __syncthreads();
 }
 
-template <bool COMPACT>
+template <bool COMPACT, bool INL>
 __device__ bool svc_simple_eval(const DevCluster& c, const DevJob& job, const kss_profile& prof, int pi, long long* smem,
                                 Shard& S, int bins_cap, int npt, unsigned want, uint8_t* host, PodMeta& meta, bool plain,
                                 unsigned long long* st3) {
@@ -519,7 +567,7 @@ __device__ bool svc_simple_eval(const DevCluster& c, const DevJob& job, const ks
   {
     long long v[3] = {nf, max_tt, max_na};
     const int op[3] = {OP_SUM, OP_MAX, OP_MAX};
-    if (!svc_xchg(smem, S, plain, v, op)) return false;
+    if (!svc_xchg<3, INL>(smem, S, plain, v, op)) return false;
     if (st3) st3[1] = wall_clock64();
     nf = v[0];
     max_tt = v[1];
@@ -541,7 +589,7 @@ __device__ bool svc_simple_eval(const DevCluster& c, const DevJob& job, const ks
   if (nf > 0) {
     long long v[1] = {best};
     const int op[1] = {OP_MAX};
-    if (!svc_xchg(smem, S, plain, v, op)) return false;
+    if (!svc_xchg<1, INL>(smem, S, plain, v, op)) return false;
     best = v[0];
   }
   for (int k = 0; k < npt; k++) {
@@ -600,7 +648,7 @@ __device__ bool svc_simple_eval(const DevCluster& c, const DevJob& job, const ks
   return true;
 }
 
-template <bool GEN, bool SIMPLE>
+template <bool GEN, bool SIMPLE, bool INL = false>
 __device__ void service_loop(DevCluster c, const DevJob& job, const kss_profile& prof, int W, int npt, int bins_cap,
                              int cache_keys, unsigned long long* gran, int* err, SvcBox* box_flat,
                              unsigned long long* relay_flat, unsigned long long* seen_flat, uint8_t* rec_host,
@@ -745,8 +793,9 @@ __device__ void service_loop(DevCluster c, const DevJob& job, const kss_profile&
       for (int r = 0; r < SVC_ROWS; r++) want |= (fields & svc_row_field(r)) ? 1u << r : 0u;
       unsigned long long st3[3] = {0, 0, 0};
       unsigned long long* sp3 = ((stamps & 1) && w == 0 && threadIdx.x == 0) ? st3 : nullptr;
-      const bool ok = compact ? svc_simple_eval<true>(c, job, prof, pi, smem, S, bins_cap, npt, want, crec_host, m, plain, sp3)
-                              : svc_simple_eval<false>(c, job, prof, pi, smem, S, bins_cap, npt, want, rec_host, m, plain, sp3);
+      const bool ok = compact
+                          ? svc_simple_eval<true, INL>(c, job, prof, pi, smem, S, bins_cap, npt, want, crec_host, m, plain, sp3)
+                          : svc_simple_eval<false, INL>(c, job, prof, pi, smem, S, bins_cap, npt, want, rec_host, m, plain, sp3);
       if (!ok) {
         if (threadIdx.x == 0) __hip_atomic_store(&box->err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         break;

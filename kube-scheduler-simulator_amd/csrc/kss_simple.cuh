@@ -207,12 +207,13 @@ __device__ __forceinline__ int sw_code(uint32_t w) {
 __device__ __forceinline__ int sw_tt(uint32_t w) { return (int)((w >> 5) & 0x7Fu); }
 __device__ __forceinline__ int sw_na(uint32_t w) { return (int)(w >> 12); }
 
-__device__ __forceinline__ uint32_t static_word(const DevCluster& c, const DevPods& P, const kss_pod& p,
-                                                const kss_profile& prof, int n, uint32_t flags, uint64_t th,
-                                                uint64_t ts) {
+// lab(key): the node's interned label value (label_of by default; k_static reads an LDS copy)
+template <class Lab>
+__device__ __forceinline__ uint32_t static_word_l(const DevCluster& c, const DevPods& P, const kss_pod& p,
+                                                  const kss_profile& prof, int n, uint32_t flags, uint64_t th,
+                                                  uint64_t ts, Lab lab) {
   const int64_t g = (int64_t)c.node_base + n;
   if (p.prefilter_status != 0) return SW_NOT_EVALUATED;
-  auto lab = [&](int key) { return label_of(c, key, n); };
   const bool aff = required_affinity_t(c, P.reqs, P.terms, P.ints, p, g, lab);
   const bool tol = (th & ~p.tol_hard) == 0;
   const uint32_t pol = (aff ? SW_AFF_OK : 0u) | (tol ? SW_TAINT_OK : 0u);
@@ -231,6 +232,164 @@ __device__ __forceinline__ uint32_t static_word(const DevCluster& c, const DevPo
   const uint32_t tt = (uint32_t)__popcll(ts & ~p.tol_soft);                         // TaintToleration.Score
   const uint32_t na = (uint32_t)na_score_t(c, P.reqs, P.terms, P.ints, p, g, lab);  // NodeAffinity.Score
   return pol | (tt << 5) | (na << 12);
+}
+
+__device__ __forceinline__ uint32_t static_word(const DevCluster& c, const DevPods& P, const kss_pod& p,
+                                                const kss_profile& prof, int n, uint32_t flags, uint64_t th,
+                                                uint64_t ts) {
+  return static_word_l(c, P, p, prof, n, flags, th, ts, [&](int key) { return label_of(c, key, n); });
+}
+
+// k_static's form: the words of one pod on a lane's four nodes at once.  Every requirement of
+// the pod is decoded once (scalar loads of the wave-uniform program) and matched against the
+// four nodes' label values into a 4-bit mask, so the pod's program is walked once per lane
+// instead of once per node and no loop diverges between the four nodes.  Word for word equal
+// to static_word_l (req_match_t / required_affinity_t / na_score_t, kss_eval.cuh).
+// lab(key, i): the label value id of node g[i] (-1 absent).
+// The pod program is read through constant-address-space pointers (DevPodsK): a wave-uniform
+// address there becomes a scalar load (the program never changes during a launch); through
+// generic pointers every field was a per-lane flat load (k_static r6a: 557 vector loads per
+// wave, waves waiting 77 % of their cycles).
+#define KSS_CONST __attribute__((address_space(4)))
+struct DevPodsK {
+  const KSS_CONST kss_pod* pods;
+  const KSS_CONST kss_req* reqs;
+  const KSS_CONST kss_term* terms;
+  const KSS_CONST int32_t* ints;
+};
+__device__ __forceinline__ DevPodsK pods_k(const DevPods& P) {
+  return DevPodsK{(const KSS_CONST kss_pod*)P.pods, (const KSS_CONST kss_req*)P.reqs,
+                  (const KSS_CONST kss_term*)P.terms, (const KSS_CONST int32_t*)P.ints};
+}
+template <class Ints, class Req, class Lab4>
+__device__ __forceinline__ uint32_t req_mask4(const DevCluster& c, Ints ints, const Req& r,
+                                              const int64_t (&g)[4], Lab4 lab) {
+  const int op = r.op;
+  if (op == KSS_OP_FALSE) return 0u;
+  if (op == KSS_OP_TRUE) return 15u;
+  uint32_t m = 0;
+  if (op == KSS_OP_NAME_IN || op == KSS_OP_NAME_NOTIN) {
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      const bool hit = r.ival >= 0 && g[i] == r.ival;
+      m |= (uint32_t)(op == KSS_OP_NAME_IN ? hit : !hit) << i;
+    }
+    return m;
+  }
+  int32_t v[4];
+#pragma unroll
+  for (int i = 0; i < 4; i++) v[i] = lab(r.key, i);
+  switch (op) {
+    case KSS_OP_MASK:
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        const uint64_t b = v[i] < 0 ? (r.mask >> 63) : (v[i] < 63 ? (r.mask >> v[i]) : 0ull);
+        m |= (uint32_t)(b & 1ull) << i;
+      }
+      return m;
+    case KSS_OP_IN:
+    case KSS_OP_NOTIN: {
+      uint32_t hit = 0;
+      for (int j = 0; j < r.list_len; j++) {
+        const int32_t x = ints[r.list_off + j];
+#pragma unroll
+        for (int i = 0; i < 4; i++) hit |= (uint32_t)(x == v[i]) << i;
+      }
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        const bool b = ((hit >> i) & 1u) != 0;
+        m |= (uint32_t)(op == KSS_OP_IN ? (v[i] >= 0 && b) : (v[i] < 0 || !b)) << i;
+      }
+      return m;
+    }
+    case KSS_OP_EXISTS:
+    case KSS_OP_DNE:
+#pragma unroll
+      for (int i = 0; i < 4; i++) m |= (uint32_t)((v[i] >= 0) == (op == KSS_OP_EXISTS)) << i;
+      return m;
+    case KSS_OP_GT:
+    case KSS_OP_LT:
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        if (v[i] < 0) continue;
+        const int32_t gi = gp(c.key_base)[r.key] + v[i];
+        if (!gp(c.value_is_int)[gi]) continue;
+        const int64_t x = gp(c.value_int)[gi];
+        m |= (uint32_t)(op == KSS_OP_GT ? x > r.ival : x < r.ival) << i;
+      }
+      return m;
+    default:
+      return 0u;
+  }
+}
+
+template <class PV, class Term, class Lab4>
+__device__ __forceinline__ uint32_t term_mask4(const DevCluster& c, const PV& P, const Term& t,
+                                               const int64_t (&g)[4], Lab4 lab) {
+  uint32_t m = 15u;
+  for (int i = 0; i < t.req_len; i++) m &= req_mask4(c, P.ints, P.reqs[t.req_off + i], g, lab);
+  return m;
+}
+
+// words w[i] of pod p on nodes n + min(i, cnt - 1), i < 4 (flags / th / ts: those nodes' columns)
+template <class PV, class Pod, class Lab4>
+__device__ __forceinline__ void static_words4(const DevCluster& c, const PV& P, const Pod& p,
+                                              const kss_profile& prof, int n, int cnt, const uint32_t (&flags)[4],
+                                              const uint64_t (&th)[4], const uint64_t (&ts)[4], Lab4 lab,
+                                              uint32_t (&w)[4]) {
+  if (p.prefilter_status != 0) {
+#pragma unroll
+    for (int i = 0; i < 4; i++) w[i] = SW_NOT_EVALUATED;
+    return;
+  }
+  int64_t g[4];
+#pragma unroll
+  for (int i = 0; i < 4; i++) g[i] = (int64_t)c.node_base + n + min(i, cnt - 1);
+  // nodeaffinity.RequiredNodeAffinity.Match: nodeSelector AND (OR over terms)
+  uint32_t aff = 15u;
+  for (int i = 0; i < p.sel_len; i++) aff &= req_mask4(c, P.ints, P.reqs[p.sel_off + i], g, lab);
+  if (p.flags & KSS_POD_HAS_REQ_AFFINITY) {
+    uint32_t any = 0;
+    for (int t = 0; t < p.aff_len; t++) any |= term_mask4(c, P, P.terms[p.aff_off + t], g, lab);
+    aff &= any;
+  }
+  uint32_t in = 15u;  // NodeAffinity PreFilterResult
+  if (p.names_len >= 0) {
+    in = 0;
+    for (int j = 0; j < p.names_len; j++) {
+      const int64_t x = (int64_t)P.ints[p.names_off + j];
+#pragma unroll
+      for (int i = 0; i < 4; i++) in |= (uint32_t)(x == g[i]) << i;
+    }
+  }
+  uint32_t na[4] = {0, 0, 0, 0};  // NodeAffinity.Score
+  for (int t = 0; t < p.pref_len; t++) {
+    const auto& term = P.terms[p.pref_off + t];
+    const uint32_t tm = term_mask4(c, P, term, g, lab);
+#pragma unroll
+    for (int i = 0; i < 4; i++)
+      if ((tm >> i) & 1u) na[i] += (uint32_t)term.weight;
+  }
+  const uint32_t en = prof.filter_enabled;
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    const bool a = (aff >> i) & 1u;
+    const bool tol = (th[i] & ~p.tol_hard) == 0;
+    const uint32_t pol = (a ? SW_AFF_OK : 0u) | (tol ? SW_TAINT_OK : 0u);
+    uint32_t r;
+    if (!((in >> i) & 1u)) r = pol | SW_NOT_EVALUATED;
+    else if (((en >> KSS_F_NODE_UNSCHEDULABLE) & 1u) && (flags[i] & KSS_NODE_UNSCHEDULABLE) && !(p.flags & KSS_POD_TOL_UNSCHEDULABLE))
+      r = pol | KSS_F_NODE_UNSCHEDULABLE;
+    else if (((en >> KSS_F_NODE_NAME) & 1u) && p.node_name != -1 && (int64_t)p.node_name != g[i])
+      r = pol | KSS_F_NODE_NAME;
+    else if (((en >> KSS_F_TAINT_TOLERATION) & 1u) && !tol)
+      r = pol | KSS_F_TAINT_TOLERATION;
+    else if (((en >> KSS_F_NODE_AFFINITY) & 1u) && !a)
+      r = pol | KSS_F_NODE_AFFINITY;
+    else
+      r = pol | ((uint32_t)__popcll(ts[i] & ~p.tol_soft) << 5) | (na[i] << 12);
+    w[i] = r;
+  }
 }
 
 // One (pod, node) result of the compact path: filter verdict and raw scores.
