@@ -1242,6 +1242,20 @@ bool build_gpods(const kss_podset* ps, int n_scalar, int n_classes, const int32_
     // exchanges: E1 (scalars + bins), E2 (scalars + soft presence)
     if (MAXH + 1 + off + g.hard_pbins > G_XW || 13 + (poff - g.hard_pbins) > G_XW) return gfail(need, GP_XW, i);
     need.xw = std::max(need.xw, std::max(MAXH + 1 + off + g.hard_pbins, 13 + (poff - g.hard_pbins)));
+    // the statistics exchange folded into the previous pod's argmax (kss_spread.cuh
+    // spread_argmax_fold): histogram-valued DoNotSchedule groups only (a node-valued group's
+    // critical path is a minimum over nodes, which a single node's delta cannot update), and the
+    // fused exchange within the granule stride; the delta bound is checked for the batch below
+    g.fold = 0;
+    if (stats) {
+      bool node_valued = false;
+      for (int c = 0; c < p.n_hard; c++) node_valued |= g.sp[c].off < 0;
+      const int np = p.n_hard + p.n_soft + g.n_ipa + (g.n_ipa > 0 ? 1 : 0), fm = 2 + off + g.hard_pbins + np;
+      if (!node_valued && np <= G_PAY && fm <= G_XW) {
+        g.fold = 1;
+        need.xw = std::max(need.xw, fm);
+      }
+    }
     need.bins_cap = std::max(need.bins_cap, off + poff);
     // AssumePod's count rows: the pod's class, its own term rows
     if (1 + p.own_terms_len > G_CMT) return gfail(need, GP_COMMIT, i);
@@ -1258,6 +1272,10 @@ bool build_gpods(const kss_podset* ps, int n_scalar, int n_classes, const int32_
       need.max_mult = std::max(need.max_mult, m);
     }
   }
+  // a folded delta travels as int16 (payload low half): Σ|coefficient| x commits per row bounds it.
+  // Opt-in (KSS_FOLD=1): measured no faster on C4 and slower on C3
+  if (need.ref_weight * need.max_mult > 32767 || !getenv("KSS_FOLD"))
+    for (int i = 0; i < ps->n_pods; i++) out[(size_t)i].fold = 0;
   // rows first read by a later pod than one committing to them: re-resolve the commits
   size_t rmax = 0;
   int rmax_pod = 0;
@@ -2395,11 +2413,12 @@ static bool scalar_fast_ok(const kss_profile& p, int n_scalar) {
 
 // Static-word scratch bound (KSS_STATIC_BYTES): pods are processed in chunks whose words
 // fit; each chunk is one k_static launch and one k_simple launch (node state stays in HBM
-// between them).  1 GiB covers C2 (5,000 x 10,000 x 4 B = 200 MB) in one chunk.
+// between them).  2 GiB covers C2 (5,000 x 10,000 x 4 B = 200 MB) and the C5 share (512
+// scenarios x 1,000 x 1,000 x 4 B = 2.05 GB) in one chunk.
 static size_t static_budget() {
   const char* e = getenv("KSS_STATIC_BYTES");
   const long long v = e ? atoll(e) : 0;
-  return v > 0 ? (size_t)v : ((size_t)1 << 30);
+  return v > 0 ? (size_t)v : ((size_t)2 << 30);
 }
 
 // Pods per chunk for jobs whose node counts sum to sum_nodes.
@@ -2448,9 +2467,9 @@ static void static_rows(const Geometry& g, const XPeers& X, int max_nodes, int& 
 static void launch_static(hipStream_t st, bool def, const DevJob* jobs, const kss_profile& pr, int n_jobs, int k0, int k1,
                           int n_lo, int n_hi, int max_keys, int row0 = 0) {
   const int lk = max_keys > 0 && max_keys <= STATIC_LKEYS ? max_keys : 0;
-  // pods per block: with the LDS label copy, enough pods to amortise loading it (C5: 32 pods of
-  // 1,000 nodes per block, 16k blocks per 512-scenario chunk)
-  int ppb = lk ? 4 * STATIC_PODS : STATIC_PODS;
+  // pods per block: with the LDS label copy, enough pods to amortise loading it (C5: 64 pods of
+  // 1,000 nodes per block; r6c: 8 / 16 / 32 / 64 within 1 % of each other)
+  int ppb = lk ? 8 * STATIC_PODS : STATIC_PODS;
   if (const char* e = getenv("KSS_STATIC_PPB")) ppb = std::max(1, std::min(256, atoi(e)));
   const dim3 sgrid((unsigned)(std::max(n_hi - n_lo, 1) + 1023) / 1024, (unsigned)((k1 - k0 + ppb - 1) / ppb),
                    (unsigned)n_jobs);

@@ -41,6 +41,7 @@ constexpr int G_XW = 512;    // 32-bit values per shard per exchange (host-check
 // 4 KiB stride (G_XW) every shard's value j shared one page offset, so the whole grid's
 // polls and publishes went to one memory channel.
 constexpr int G_NS = 16;     // scalar slots of an exchange
+constexpr int G_PAY = 32;    // payload values of a fused exchange (spread_argmax_fold)
 constexpr int G_SCORE = 3;   // GIpa.kind of a merged InterPodAffinity score entry (KSS_IPA_SCORE_CLASS)
 constexpr int G_NSTAMP = KSS_NSTAMP_PODS / 2;  // pods with diagnostic phase stamps, 16 per pod
 
@@ -108,7 +109,9 @@ struct alignas(16) GPod {
   SPod dyn;
   int32_t pflags, n_hard, n_soft, n_ipa;
   int32_t n_keys, total_bins, hard_pbins, total_pbins;
-  int32_t need_stats, n_cmt, pad0, pad1;
+  int32_t need_stats, n_cmt;
+  int32_t fold;  // the statistics exchange may ride with the previous pod's argmax (spread_argmax_fold)
+  int32_t pad1;
   int32_t key[MAXK];
   int32_t hoff[MAXK][4];
   int32_t cmt[G_CMT];   // resident row index, or -(1 + class row) / -(1 + n_classes + term row) in HBM
@@ -153,8 +156,12 @@ struct alignas(16) SpreadHdr {
   long long kx[MAXWAVES];  // multi-wave argmax sweep: each wave's maximum
   long long kres;
   kss_profile prof;  // a runtime (non-default) profile, staged word by word (as SimpleHdr)
+  unsigned long long pay[G_PAY];  // fused exchange: {key, payload} of the best shard per payload value
+  int32_t payv[G_PAY];            // ... this shard's payloads, as published
+  int32_t fmin[MAXH];             // ... the next pod's critical-path minima and flags
+  int32_t fflags;
   int32_t abort;
-  int32_t pad[3];
+  int32_t pad[2];
 };
 
 struct SpreadShard {
@@ -323,15 +330,19 @@ __device__ __forceinline__ bool spread_exchange(SpreadHdr& H, int32_t* xs, unsig
                                                 int W, int wself, int gs,
                                                 unsigned epoch, int* err, int K, unsigned opbits, int sum_lo, int ns,
                                                 int or_lo, int no, unsigned long long* sp, int gw = 0, int nsw = 1,
-                                                int phase = 3) {
+                                                int phase = 3, int np = 0) {
   constexpr int XS = G_XS;
   const int lane = threadIdx.x & 63, nw = blockDim.x >> 6;
-  const int M = K + ns + no;
+  // np > 0 (spread_argmax_fold): after the bins, np payload values H.payv[] whose fold keeps
+  // the value of the shard with the largest key (scalar 0, a compressed key with its top bit
+  // flipped so that the signed MAX orders it), into H.pay[] as {key, payload}
+  const int M0 = K + ns + no, M = M0 + np;
   KSS_GLOBAL unsigned long long* gran = gp(gran_);
   auto slot = [&](int j) -> int32_t* {
     if (j < K) return xs + j;
     if (j < K + ns) return xs + G_NS + sum_lo + (j - K);
-    return xs + G_NS + or_lo + (j - K - ns);
+    if (j < M0) return xs + G_NS + or_lo + (j - K - ns);
+    return H.payv + (j - M0);
   };
   auto opof = [&](int j) { return j < K ? (int)((opbits >> (2 * j)) & 3u) : (j < K + ns ? OP_SUM : OP_OR); };
   const unsigned long long tag = (unsigned long long)epoch << 32;
@@ -345,7 +356,8 @@ __device__ __forceinline__ bool spread_exchange(SpreadHdr& H, int32_t* xs, unsig
       for (int x = 1; x < nw; x++) v = op32_lane(op, v, H.red[x][j]);
     }
     xpub(X, gran_, mine + j, tag | (uint32_t)v);
-    *sl = ident32(op);
+    if (j < M0) *sl = ident32(op);
+    else H.pay[j - M0] = 0ull;
   }
   if (sp && lane == 0) sp[2] = wall_clock64();
   if (!(phase & 2)) return true;
@@ -357,8 +369,10 @@ __device__ __forceinline__ bool spread_exchange(SpreadHdr& H, int32_t* xs, unsig
     const int t = gl / mc, j = j0 + (gl - t * mc);
     const bool act = t < T;
     const int op = opof(min(j, M - 1));
+    const bool payl = j >= M0;
     // the operator differs between lanes: fold all four, branch-free, and pick one at the end
     int32_t a_sum = 0, a_max = INT32_MIN, a_min = INT32_MAX, a_or = 0;
+    uint32_t a_key = 0, a_pay = 0;  // payload lanes: the largest key seen and its shard's payload
     // loads per lane sized to the shards this lane polls (4, 8 or 16), every load issued
     // unconditionally from a clamped address (no exec-mask region per load), the lanes and
     // shards past the end masked in the tag test and the fold
@@ -366,7 +380,7 @@ __device__ __forceinline__ bool spread_exchange(SpreadHdr& H, int32_t* xs, unsig
       constexpr int XSN = decltype(xs_c)::value;
       const int jc = min(j, M - 1);
       for (int w0 = 0; w0 < W; w0 += T * XSN) {
-        unsigned long long g[XSN];
+        unsigned long long g[XSN], gk[XSN];
         long long t0_ = 0;
         for (unsigned spins = 0;; ++spins) {
           bool ok = true;
@@ -375,6 +389,14 @@ __device__ __forceinline__ bool spread_exchange(SpreadHdr& H, int32_t* xs, unsig
             const int w = w0 + t + T * b;
             g[b] = __hip_atomic_load(base + (size_t)min(w, W - 1) * gs + jc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             ok &= !(act && w < W) || (g[b] >> 32) == epoch;
+          }
+          if (np && payl) {  // the key granule of the same shards, for the payload lanes
+#pragma unroll
+            for (int b = 0; b < XSN; b++) {
+              const int w = w0 + t + T * b;
+              gk[b] = __hip_atomic_load(base + (size_t)min(w, W - 1) * gs, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              ok &= !(act && payl && w < W) || (gk[b] >> 32) == epoch;
+            }
           }
           if (__all(ok)) break;
           if (spread_spin_over(spins, t0_, err)) {
@@ -395,6 +417,11 @@ __device__ __forceinline__ bool spread_exchange(SpreadHdr& H, int32_t* xs, unsig
           a_max = max(a_max, in ? x : INT32_MIN);
           a_min = min(a_min, in ? x : INT32_MAX);
           a_or |= in ? x : 0;
+          if (np) {
+            const uint32_t kk = in ? ((uint32_t)gk[b] ^ 0x80000000u) : 0u;
+            a_pay = kk > a_key ? (uint32_t)g[b] : a_pay;
+            a_key = kk > a_key ? kk : a_key;
+          }
         }
       }
       return true;
@@ -405,7 +432,9 @@ __device__ __forceinline__ bool spread_exchange(SpreadHdr& H, int32_t* xs, unsig
                                    : sweep(std::integral_constant<int, XS>{});
     if (!swept) return false;
     const int32_t acc = op == OP_SUM ? a_sum : (op == OP_MAX ? a_max : (op == OP_MIN ? a_min : a_or));
-    if (act) {
+    if (act && payl) {
+      if (a_key) atomicMax(&H.pay[j - M0], ((unsigned long long)a_key << 32) | a_pay);
+    } else if (act) {
       int32_t* sl = slot(j);
       switch (op) {
         case OP_SUM: atomicAdd(sl, acc); break;
@@ -625,6 +654,173 @@ __device__ __forceinline__ bool spread_argmax(SpreadHdr& H, int W, int w, int gs
   lds_barrier();
   if (H.abort) return false;
   key = H.kres;
+  return true;
+}
+
+// ---- The statistics exchange of pod k+1 folded into pod k's argmax ----
+// Pod k+1's statistics (its PreFilter / PreScore histograms and InterPodAffinity flags) need the
+// node state after pod k's AssumePod, which only the argmax decides.  Every shard computes them on
+// the state before it (H0) and publishes them with its selectHost key, plus the change its own
+// candidate would make if it won (the candidate node's contribution after pod k's commit minus
+// before: one (bin, delta) per constraint / entry, and the candidate's flags after the commit);
+// the fused sweep sums H0 over the shards and keeps the payloads of the shard with the largest key
+// (the winner), which every shard then applies.  Counts only grow on a commit, so the flags are an
+// OR.  One exchange per pod fewer on the chain; pods whose DoNotSchedule group is node-valued
+// (a critical path over nodes) keep their own exchange (GPod::fold, build_gpods).
+
+// g_sum at slot s as if pod q had been committed there (its resident count rows + 1 each)
+__device__ __forceinline__ int32_t g_sum_post(const SpreadShard& L, const GPod& qn, int off, int len, int s, const GPod& q) {
+  const uint32_t* R = grefs(qn);
+  int32_t v = 0;
+  for (int i = 0; i < len; i++) {
+    const uint32_t r = R[off + i];
+    const int row = (int)(r & 0xFFFFu);
+    int32_t c = (int32_t)L.cnt[row * L.cap + s];
+    for (int m = 0; m < q.n_cmt; m++) c += q.cmt[m] == row ? 1 : 0;
+    v += (int32_t)(int16_t)(r >> 16) * c;
+  }
+  return v;
+}
+__device__ __forceinline__ bool g_any_post(const SpreadShard& L, const GPod& qn, int off, int len, int s, const GPod& q) {
+  const uint32_t* R = grefs(qn);
+  bool a = false;
+  for (int i = 0; i < len; i++) {
+    const int row = (int)(R[off + i] & 0xFFFFu);
+    bool hit = L.cnt[row * L.cap + s] != 0;
+    for (int m = 0; m < q.n_cmt; m++) hit |= q.cmt[m] == row;
+    a |= hit;
+  }
+  return a;
+}
+__device__ __forceinline__ int32_t pay_of(int bin, int32_t delta) {
+  return delta == 0 || bin < 0 ? 0 : (int32_t)(((uint32_t)(bin + 1) << 16) | (uint32_t)(uint16_t)(int16_t)delta);
+}
+
+// Payload j of candidate slot s (static word wd of pod qn): j < n_hard + n_soft the constraint
+// j's histogram delta (stats_node's accumulation), then one per inter-pod entry, the last the
+// candidate's InterPodAffinity flags after the commit (only when the pod has inter-pod entries).
+__device__ __forceinline__ int32_t fold_payload(const SpreadShard& L, const GPod& q, const GPod& qn, int j, int s,
+                                                uint32_t wd) {
+  const int cap = L.cap;
+  const int nc = qn.n_hard + qn.n_soft;
+  if (j < qn.n_hard) {
+    const GSpread& sp = qn.sp[j];
+    if (sp.own != j || sp.off < 0 || !g_has_keys(L, qn.sp, qn.n_hard, s)) return 0;
+    int32_t pre = -1, post = -1;  // the group's last admitting member
+    for (int m = j; m < qn.n_hard; m++) {
+      const GSpread& mm = qn.sp[m];
+      if (mm.own == j && g_policy(mm, wd)) {
+        pre = g_sum(L, qn, mm.ri_off, mm.ri_len, s);
+        post = g_sum_post(L, qn, mm.ri_off, mm.ri_len, s, q);
+      }
+    }
+    if (pre < 0) return 0;
+    return pay_of(sp.off + L.lbl[sp.key * cap + s], post - pre);
+  }
+  if (j < nc) {
+    const GSpread* so = qn.sp + qn.n_hard;
+    const GSpread& sp = qn.sp[j];
+    if (sp.mode != SOFT_HIST || !g_policy(sp, wd)) return 0;
+    if ((qn.pflags & KSS_POD_PTS_REQUIRE_ALL) && !g_has_keys(L, so, qn.n_soft, s)) return 0;
+    int d = L.lbl[sp.key * cap + s];
+    if (d < 0) d = sp.empty;
+    return pay_of(sp.off + d, g_sum_post(L, qn, sp.ri_off, sp.ri_len, s, q) - g_sum(L, qn, sp.ri_off, sp.ri_len, s));
+  }
+  const bool has_labels = (L.r32[2 * cap + s] & KSS_NODE_HAS_LABELS) != 0;
+  if (j < nc + qn.n_ipa) {
+    const GIpa& en = qn.ipa[j - nc];
+    const int d = L.lbl[en.key * cap + s];
+    if (d < 0) return 0;
+    int ho;
+    if (en.kind == G_SCORE) {
+      if (!has_labels) return 0;
+      ho = qn.hoff[en.slot][3];
+    } else {
+      ho = qn.hoff[en.slot][en.kind == KSS_IPA_EXISTING_ANTI ? 0 : (en.kind == KSS_IPA_REQ_AFFINITY ? 1 : 2)];
+    }
+    if (ho < 0) return 0;
+    return pay_of(ho + d, g_sum_post(L, qn, en.ri_off, en.ri_len, s, q) - g_sum(L, qn, en.ri_off, en.ri_len, s));
+  }
+  int32_t f = 0;  // the flags stats_node would give the candidate after the commit
+  for (int e = 0; e < qn.n_ipa; e++) {
+    const GIpa& en = qn.ipa[e];
+    if (L.lbl[en.key * cap + s] < 0) continue;
+    if (en.kind == G_SCORE) {
+      if (has_labels && g_any_post(L, qn, en.ri_off, en.ri_len, s, q)) f |= 8;
+    } else {
+      const int h = en.kind == KSS_IPA_EXISTING_ANTI ? 0 : (en.kind == KSS_IPA_REQ_AFFINITY ? 1 : 2);
+      if (g_sum_post(L, qn, en.ri_off, en.ri_len, s, q) > 0) f |= 1 << h;
+    }
+  }
+  return f;
+}
+
+// spread_argmax for pod q with pod qn's statistics riding along (every wave calls it; bins of
+// qn already accumulated by this shard's statistics pass, flags_local its lanes' flags).  On
+// return: key = the cluster's best key of q, the bins hold qn's cluster statistics after q's
+// AssumePod, H.fmin / H.fflags qn's critical-path minima and flags.  False on abort.
+__device__ __forceinline__ bool spread_argmax_fold(SpreadHdr& H, const SpreadShard& L, int W, int w, int gs,
+                                                   unsigned& epoch, unsigned long long* gran, const XPeers& X, int* err,
+                                                   int parity, long long& key, int kb, int node_base, int lo,
+                                                   const GPod& q, const GPod& qn, int32_t flags_local,
+                                                   const uint32_t* sw1) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  int32_t* xs = L.xs;
+  const long long r = wave_max_key(key, kb, node_base);
+  int32_t fl[1] = {flags_local};
+  const int opo[1] = {OP_OR};
+  wave_red32(fl, opo);
+  if (lane == 0) {
+    H.kred[parity][wave] = r;
+    H.red[wave][0] = (int32_t)(key_compress(r, kb, node_base) ^ 0x80000000u);
+    H.red[wave][1] = fl[0];
+  }
+  lds_barrier();
+  long long best = H.kred[parity][0];
+  for (int x = 1; x < nw; x++) best = H.kred[parity][x] > best ? H.kred[parity][x] : best;
+  const int np = qn.n_hard + qn.n_soft + qn.n_ipa + (qn.n_ipa > 0 ? 1 : 0);  // + the flags slot
+  if (wave == 0) {  // this shard's candidate's payloads (read back by the publishing lanes of this wave)
+    const int cs = best ? (int)(0xFFFFFFFFu - (uint32_t)(unsigned long long)best) - node_base - lo : -1;
+    for (int j = lane; j < np; j += 64) H.payv[j] = cs >= 0 ? fold_payload(L, q, qn, j, cs, sw1[cs]) : 0;
+  }
+  ++epoch;
+  const int K = 2, ns = qn.total_bins, no = qn.hard_pbins;
+  const unsigned opbits = (unsigned)OP_MAX | ((unsigned)OP_OR << 2);
+  const int M = K + ns + no + np;
+  if (nw == 1 || (long long)W * M <= (long long)KSS_SPREAD_MW_MIN) {
+    if (wave == 0) spread_exchange(H, xs, gran, X, W, w, gs, epoch, err, K, opbits, 0, ns, ns, no, nullptr, 0, 1, 3, np);
+  } else {
+    if (wave == 0) spread_exchange(H, xs, gran, X, W, w, gs, epoch, err, K, opbits, 0, ns, ns, no, nullptr, 0, 1, 1, np);
+    lds_barrier();  // identities in the slots before any wave folds into them
+    const int nsw = min(nw, KSS_SPREAD_SWEEP_WAVES);
+    if (wave < nsw) spread_exchange(H, xs, gran, X, W, w, gs, epoch, err, K, opbits, 0, ns, ns, no, nullptr, wave, nsw, 2, np);
+  }
+  lds_barrier();
+  if (H.abort) return false;
+  if (wave == 0) {  // the winner's payloads, then qn's critical paths over the final bins
+    int32_t* bins = xs + G_NS;
+    for (int j = lane; j < np; j += 64) {
+      const unsigned long long P = H.pay[j];
+      const uint32_t p = (uint32_t)P;
+      if (!(P >> 32) || !p) continue;
+      if (qn.n_ipa > 0 && j == np - 1) atomicOr(&xs[1], (int32_t)p);
+      else atomicAdd(&bins[(p >> 16) - 1], (int32_t)(int16_t)(p & 0xFFFFu));
+    }
+    for (int i = 0; i < qn.n_hard; i++) {
+      const GSpread& sp = qn.sp[i];
+      int32_t m[1] = {INT32_MAX};
+      if (sp.off >= 0 && sp.own == i)
+        for (int b = lane; b < sp.nb; b += 64)
+          if (bins[qn.total_bins + sp.poff + b]) m[0] = min(m[0], bins[sp.off + b]);
+      const int op[1] = {OP_MIN};
+      wave_red32(m, op);
+      if (lane == 0) H.fmin[i] = m[0];
+    }
+    if (lane == 0) H.fflags = xs[1];
+  }
+  const uint32_t kc = (uint32_t)xs[0] ^ 0x80000000u;
+  lds_barrier();
+  key = key_expand(kc, kb, node_base);
   return true;
 }
 
@@ -1132,6 +1328,7 @@ __device__ __forceinline__ void spread_schedule(const GTrace& tr, DevCluster c, 
   for (int j = 0; j < G_PF; j++) pfw[j] = 0;
   unsigned epoch = epoch0;  // granule tags above every tag an earlier launch left (split grids)
   int kparity = 0;
+  bool folded = false;  // this pod's statistics came with the previous pod's argmax (spread_argmax_fold)
   for (int k = k0; k < k1; k++) {
 #define GSTAMP(i)                                                                      \
   do {                                                                                 \
@@ -1173,7 +1370,11 @@ __device__ __forceinline__ void spread_schedule(const GTrace& tr, DevCluster c, 
 #endif
     // ---- stats: PodTopologySpread PreFilter, InterPodAffinity PreFilter / PreScore ----
     if (KSS_SPREAD_SAFE) lds_barrier();
-    if (evaluated && q.need_stats) {
+    if (evaluated && folded) {  // the bins already hold the cluster statistics
+#pragma unroll
+      for (int i = 0; i < MAXH; i++) hard_min[i] = i < q.n_hard ? H.fmin[i] : INT32_MAX;
+      flags = H.fflags;
+    } else if (evaluated && q.need_stats) {
 #if KSS_SPREAD_TRACE == 1
       uint32_t th0 = 0;  // a hash of the first hard group's count per node, read before the pass
       for (int s = tid; s < own; s += nt) th0 = th0 * 31u + (uint32_t)trace_eff(L, q, s, sw[s]) + 7u * (uint32_t)s;
@@ -1351,6 +1552,7 @@ __device__ __forceinline__ void spread_schedule(const GTrace& tr, DevCluster c, 
         evaluated = false;
       }
     }
+    bool fold_next = false;
     if (evaluated) {
       const bool scored = nf > 1;  // a single feasible node is selected without scoring
       // ---- PodTopologySpread PreScore sizes + Score ----
@@ -1426,6 +1628,25 @@ __device__ __forceinline__ void spread_schedule(const GTrace& tr, DevCluster c, 
           GSTAMP(6);
         }
       }
+      // ---- pod k+1's statistics, published with this pod's key (spread_argmax_fold) ----
+      // (this pod's passes no longer read the bins: the last reads were behind E2 / E3's barriers)
+      const GPod& qn = *reinterpret_cast<const GPod*>(L.ring + ((k + 1) % 3) * gq);
+      const uint32_t* sw1 = L.st + ((k + 1) & 1) * cap;
+      fold_next = W > 1 && kb > 0 && k + 1 < k1 && qn.dyn.status == 0 && qn.need_stats && qn.fold;
+      int32_t flags_n = 0;
+      if (fold_next) {
+        if (pf_on) {  // pod k+1's static words, prefetched into registers at this pod's start
+#pragma unroll
+          for (int j = 0; j < G_PF; j++)
+            if (j < pf_per) L.st[((k + 1) & 1) * cap + min(j * pf_n + pf_lane, own - 1)] = pfw[j];
+        }
+        for (int b = tid; b < qn.total_bins + qn.total_pbins; b += nt) bins[b] = 0;
+        lds_barrier();
+        int32_t hmin_n[MAXH];
+#pragma unroll
+        for (int i = 0; i < MAXH; i++) hmin_n[i] = INT32_MAX;
+        for (int s = tid; s < own; s += nt) stats_node(L, qn, s, sw1[s], bins, hmin_n, flags_n);
+      }
       // ---- NormalizeScore + weights + selectHost ----
       const bool ipa_norm = (flags & 8) != 0;
       const int64_t ipa_diff = (int64_t)ipa_max - (int64_t)ipa_min;
@@ -1474,7 +1695,10 @@ __device__ __forceinline__ void spread_schedule(const GTrace& tr, DevCluster c, 
         best = key > best ? key : best;
       }
       GSTAMP(7);
-      if (!spread_argmax(H, W, w, gs, epoch, gran, X, err, kparity, best, kb, c.node_base)) return;
+      if (fold_next ? !spread_argmax_fold(H, L, W, w, gs, epoch, gran, X, err, kparity, best, kb, c.node_base, lo, q, qn,
+                                          flags_n, sw1)
+                    : !spread_argmax(H, W, w, gs, epoch, gran, X, err, kparity, best, kb, c.node_base))
+        return;
       GSTAMP(8);
       kparity ^= 1;
 #if KSS_SPREAD_TRACE
@@ -1559,11 +1783,12 @@ __device__ __forceinline__ void spread_schedule(const GTrace& tr, DevCluster c, 
     }
     // the statistics bins of pod k+1, zeroed ahead of the barrier that ends this pod (its
     // passes no longer read them): its stats pass then starts without a barrier of its own
-    if (k + 1 < k1) {
+    if (k + 1 < k1 && !fold_next) {  // (folded: they hold its exchanged statistics)
       const GPod& qn = *reinterpret_cast<const GPod*>(L.ring + ((k + 1) % 3) * gq);
       if (qn.dyn.status == 0 && qn.need_stats)
         for (int b = tid; b < qn.total_bins + qn.total_pbins; b += nt) bins[b] = 0;
     }
+    folded = fold_next;
     lds_barrier();
     GSTAMP(9);
 #undef GSTAMP

@@ -93,6 +93,42 @@ def test_program_fuzz_many_seeds_forced_shards(monkeypatch):
         ctx.close()
 
 
+@pytest.mark.parametrize("fold", [True, False])
+@pytest.mark.parametrize("shards", [2, 9, 40])
+def test_statistics_fold_matches_oracle(fold, shards, monkeypatch):
+    """Pod k+1's statistics exchange folded into pod k's argmax (spread_argmax_fold) and, with
+    without KSS_FOLD (the default), the separate exchange: the fuzz mixes pods that fold (histogram-valued
+    DoNotSchedule groups, inter-pod histograms and flags) with pods that cannot (node-valued
+    DoNotSchedule groups) and unschedulable pods that run no argmax, so both paths alternate."""
+    monkeypatch.setenv("KSS_SHARDS", str(shards))
+    if fold:
+        monkeypatch.setenv("KSS_FOLD", "1")
+    prof = abi.default_profile()
+    on_spread = 0
+    for seed in (20, 21, 22, 51):
+        cc, cp = _fuzz(seed, 211, 150)
+        ncl, nt = len(cc.classes), len(cc.terms)
+        chosen_o, res, st = _oracle(prof, cc.as_struct(), cp.as_struct(), cp.n, cc.n_nodes, ncl, nt)
+        ctx = native.Context(prof)
+        ctx.load(cc.as_struct())
+        chosen = ctx.schedule_batch(cp.as_struct(), cp.n)
+        # a program over k_spread's per-shard tables sends the batch to k_schedule (parity either way)
+        on_spread += ctx.last_kernel() == "k_spread" and ctx.last_geometry()["shards"] == shards
+        _check(ctx, res, st, chosen, chosen_o, cp.n, cc.n_nodes, ncl, nt)
+        ctx.close()
+    assert on_spread >= 3
+    monkeypatch.delenv("KSS_SHARDS")  # the automatic geometry (3,000 nodes do not fit 2 shards' LDS)
+    s = native.Synth(3, 7, 3000, 250)  # the C3 recipe: zone DoNotSchedule, inter-pod entries
+    chosen_o, res, st = _oracle(prof, s.cluster, s.pods, 250, 3000, s.cluster.n_classes, s.cluster.n_terms)
+    ctx = native.Context(prof)
+    ctx.load(s.cluster)
+    ctx.stage(s.pods)
+    chosen = ctx.run_staged(250)
+    assert ctx.last_kernel() == "k_spread"
+    _check(ctx, res, st, chosen, chosen_o, 250, 3000, s.cluster.n_classes, s.cluster.n_terms)
+    ctx.close()
+
+
 def test_k_spread_static_chunks(monkeypatch):
     """KSS_STATIC_BYTES forces one k_static + one k_spread launch per 23 pods: the commits of
     every launch reach HBM (node rows and count rows) before the next one reads them."""
