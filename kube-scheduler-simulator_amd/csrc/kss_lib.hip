@@ -262,8 +262,10 @@ __global__ __launch_bounds__(KSS_MAX_THREADS) void k_simple(const DevJob* __rest
 }
 
 // grid = W (one cluster); each shard's nodes live in LDS (cap slots); bins_cap: histogram +
-// presence values of the exchange vector.  DEF: the v1.26 default profile, folded.
-template <bool DEF>
+// presence values of the exchange vector.  DEF: the v1.26 default profile, folded.  FOLD: the
+// statistics fold compiled in (KSS_FOLD=1; a separate kernel, so the default one keeps the
+// register allocation the fold's code would spill: 36 against 164 B of scratch per lane).
+template <bool DEF, bool FOLD>
 __global__ __launch_bounds__(KSS_MAX_THREADS) void k_spread(const DevJob* __restrict__ jobs, int W, int cap, int bins_cap,
                                                             int n_res, int gq, int gs, int k0, int k1, unsigned long long* gran,
                                                             int* err, unsigned long long* stamps, int nst, XPeers X,
@@ -296,7 +298,7 @@ __global__ __launch_bounds__(KSS_MAX_THREADS) void k_spread(const DevJob* __rest
     __syncthreads();
   }
   const kss_profile& P = DEF ? def_prof : H.prof;
-  spread_schedule<DEF>(job.trace, job.c, job.gpods, job.stat, job.res_rows, n_res, k0, min(k1, job.n_pods), job.chosen, job.meta, P, W, w,
+  spread_schedule<DEF, FOLD>(job.trace, job.c, job.gpods, job.stat, job.res_rows, n_res, k0, min(k1, job.n_pods), job.chosen, job.meta, P, W, w,
                   cap, bins_cap, gq, gs, gran ? gran + (size_t)ji * 2 * W * gs : nullptr, X, epoch0, err, stamps, nst, hc,
                   smem);
 }
@@ -2413,12 +2415,17 @@ static bool scalar_fast_ok(const kss_profile& p, int n_scalar) {
 
 // Static-word scratch bound (KSS_STATIC_BYTES): pods are processed in chunks whose words
 // fit; each chunk is one k_static launch and one k_simple launch (node state stays in HBM
-// between them).  2 GiB covers C2 (5,000 x 10,000 x 4 B = 200 MB) and the C5 share (512
-// scenarios x 1,000 x 1,000 x 4 B = 2.05 GB) in one chunk.
+// between them).  Default: an eighth of the current device's free memory, between 1 and 16 GiB
+// (MI355X: 16 GiB) -- C2 (5,000 x 10,000 x 4 B = 200 MB), C4 (100,000 x 20,000: 8 GB) and the
+// c5_sweep leg (4,096 scenarios x 1,000 x 1,000: 16.4 GB) in one chunk, without per-chunk
+// relaunches of the loop kernel.
 static size_t static_budget() {
   const char* e = getenv("KSS_STATIC_BYTES");
   const long long v = e ? atoll(e) : 0;
-  return v > 0 ? (size_t)v : ((size_t)2 << 30);
+  if (v > 0) return (size_t)v;
+  size_t fr = 0, tot = 0;
+  if (hipMemGetInfo(&fr, &tot) != hipSuccess) fr = 0;
+  return std::min((size_t)16 << 30, std::max((size_t)1 << 30, fr / 8));
 }
 
 // Pods per chunk for jobs whose node counts sum to sum_nodes.
@@ -2631,7 +2638,9 @@ static int launch_spread(hipStream_t st, const Geometry& g, const GpodNeeds& q, 
     shmem = std::max(shmem, std::min((size_t)KSS_LDS_BUDGET, (size_t)std::max(0, atoi(e))));
 #endif
   const bool def = same_profile(prof, default_profile_c());
-  const void* fn = def ? (const void*)k_spread<true> : (const void*)k_spread<false>;
+  const bool fold = getenv("KSS_FOLD") != nullptr;
+  const void* fn = def ? (fold ? (const void*)k_spread<true, true> : (const void*)k_spread<true, false>)
+                       : (fold ? (const void*)k_spread<false, true> : (const void*)k_spread<false, false>);
   HIP_TRY(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shmem));
   XPeers X = split ? split->X : XPeers{};
   const bool sp_grid = X.n > 1;
@@ -4303,6 +4312,7 @@ kss_sweep* kss_sweep_create(int32_t device, const kss_profile* prof, int32_t n_s
   // budget, the next chunk's static words computed on a second stream while k_simple runs this one.
   // Off by default: C5 ran 13.5 against 12.6 ms per step (r5y: k_simple slows by more than the
   // k_static time it hides when both share the CUs)
+  if (simple) hipSetDevice(device);  // the budget follows this device's free memory
   sw->chunk = simple ? static_chunk(sum_nodes, sw->max_pods) : 0;
   const bool dbl = simple && sw->chunk < sw->max_pods && getenv("KSS_SWEEP_PIPE") != nullptr;
   if (dbl) sw->chunk = static_chunk(2 * sum_nodes, sw->max_pods);

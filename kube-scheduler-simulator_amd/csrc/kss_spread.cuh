@@ -1153,8 +1153,8 @@ __device__ __forceinline__ int32_t trace_eff(const SpreadShard& L, const GPod& q
 #endif
 
 // The batch for shard w of one cluster, pods [k0, k1).  res_rows: the resident count rows
-// (class r as r, term r as n_classes + r), n_res of them.
-template <bool DEF>
+// (class r as r, term r as n_classes + r), n_res of them.  FOLD: spread_argmax_fold compiled in.
+template <bool DEF, bool FOLD>
 __device__ __forceinline__ void spread_schedule(const GTrace& tr, DevCluster c, const GPod* __restrict__ gpods,
                                                 const uint32_t* __restrict__ stat, const int32_t* __restrict__ res_rows,
                                                 int n_res, int k0, int k1, int32_t* chosen, PodMeta* meta,
@@ -1370,7 +1370,7 @@ __device__ __forceinline__ void spread_schedule(const GTrace& tr, DevCluster c, 
 #endif
     // ---- stats: PodTopologySpread PreFilter, InterPodAffinity PreFilter / PreScore ----
     if (KSS_SPREAD_SAFE) lds_barrier();
-    if (evaluated && folded) {  // the bins already hold the cluster statistics
+    if (FOLD && evaluated && folded) {  // the bins already hold the cluster statistics
 #pragma unroll
       for (int i = 0; i < MAXH; i++) hard_min[i] = i < q.n_hard ? H.fmin[i] : INT32_MAX;
       flags = H.fflags;
@@ -1632,7 +1632,7 @@ __device__ __forceinline__ void spread_schedule(const GTrace& tr, DevCluster c, 
       // (this pod's passes no longer read the bins: the last reads were behind E2 / E3's barriers)
       const GPod& qn = *reinterpret_cast<const GPod*>(L.ring + ((k + 1) % 3) * gq);
       const uint32_t* sw1 = L.st + ((k + 1) & 1) * cap;
-      fold_next = W > 1 && kb > 0 && k + 1 < k1 && qn.dyn.status == 0 && qn.need_stats && qn.fold;
+      fold_next = FOLD && W > 1 && kb > 0 && k + 1 < k1 && qn.dyn.status == 0 && qn.need_stats && qn.fold;
       int32_t flags_n = 0;
       if (fold_next) {
         if (pf_on) {  // pod k+1's static words, prefetched into registers at this pod's start
