@@ -148,9 +148,9 @@ __device__ __forceinline__ int64_t group_count(const DevCluster& c, const DevPod
 struct DryState {
   int64_t req[KSS_NRES];
   int64_t pods;
-  int64_t M[MAXH];
-  int64_t A[MAXK][3];
-  int64_t T;
+  int32_t M[MAXH];     // pod counts (32 bits: the state stays in registers, k_preempt_nodes
+  int32_t A[MAXK][3];  // spilled 80 B per lane with 64-bit counts)
+  int32_t T;
 };
 
 // RemovePod (sign = -1) / AddPod (+1) of bound pod e on node n, with the RemovePod /
@@ -352,10 +352,10 @@ __device__ __forceinline__ DryResult select_victims(const PreemptJob& J, const k
     if (i >= p.n_hard || pl.hard_own[i] != i) continue;
     if (pl.hard_off[i] >= 0) {
       const int d = label_of(c, sp[i].key, n);
-      s.M[i] = d >= 0 ? bins[pl.hard_off[i] + d] : 0;
+      s.M[i] = d >= 0 ? (int32_t)bins[pl.hard_off[i] + d] : 0;
     } else {
       const int64_t g = group_count(c, P, p, pl, i, n);
-      s.M[i] = g > 0 ? g : 0;
+      s.M[i] = g > 0 ? (int32_t)g : 0;
     }
   }
 #pragma unroll
@@ -368,9 +368,9 @@ __device__ __forceinline__ DryResult select_victims(const PreemptJob& J, const k
     const int d = label_of(c, pl.key[k], n);
     if (d < 0) continue;
 #pragma unroll
-    for (int h = 0; h < 3; h++) s.A[k][h] = ipa_value(c, P, p, pl, bins, k, h, d, n);
+    for (int h = 0; h < 3; h++) s.A[k][h] = (int32_t)ipa_value(c, P, p, pl, bins, k, h, d, n);
   }
-  s.T = H.aff_total;
+  s.T = (int32_t)H.aff_total;
   for (int k = p0; k < e1; k++) apply_pod(J, p, pl, k, n, -1, s);
   if (!dry_fits_nom(J, p, pl, H, s, n, here)) return res;
   // reprieve in importance order (MoreImportantPod, NodeInfo order on ties)
