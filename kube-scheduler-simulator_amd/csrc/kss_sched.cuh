@@ -56,6 +56,14 @@ __device__ __forceinline__ bool spin_expired(unsigned spins, long long& t0) {
 }
 // The launch error word only grows (atomic max): a state-check failure (2) is never
 // overwritten by the exchange timeouts (1) it causes in the shards still waiting for it.
+// The pause between two polls of an exchange granule (experiment builds: -DKSS_SPIN_SLEEP=0 polls
+// back to back, larger values sleep longer; s_sleep n waits about 64 n clocks)
+#ifndef KSS_SPIN_SLEEP
+#define KSS_SPIN_SLEEP 1
+#endif
+__device__ __forceinline__ void spin_pause() {
+  if (KSS_SPIN_SLEEP > 0) __builtin_amdgcn_s_sleep(KSS_SPIN_SLEEP);
+}
 __device__ __forceinline__ void err_raise(int* err, int code) {
   __hip_atomic_fetch_max(err, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }

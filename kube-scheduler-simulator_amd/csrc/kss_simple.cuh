@@ -752,7 +752,7 @@ __device__ __forceinline__ bool simple_exchange(SimpleHdr& H, unsigned long long
         }
         return false;
       }
-      __builtin_amdgcn_s_sleep(1);
+      spin_pause();
     }
     const long long k = (long long)(((unsigned long long)got[ch][1] << 32) | got[ch][0]);
     best = k > best ? k : best;
@@ -1081,6 +1081,7 @@ __device__ __forceinline__ bool simple_sync_pw(SimpleHdr& H, int& parity, long l
   wave_red_stats_pw(u);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
   if (sp && threadIdx.x == 0) sp[7] = wall_clock64();
+  if (sp && (threadIdx.x == 64 || threadIdx.x == 128)) sp[9 + (threadIdx.x >> 6)] = wall_clock64();  // waves 1, 2 reach it
   if (lane == 0) {
     H.red[parity][wave][0] = wbest;
 #pragma unroll
@@ -1252,6 +1253,7 @@ __device__ __forceinline__ void simple_schedule(DevCluster c, const SPod* __rest
                                             ? gstamps + (size_t)w * 8 * KSS_NSTAMP_PODS + (size_t)(k - k0) * 16
                                             : nullptr;
     if (sp && tid == 0) sp[0] = wall_clock64();
+    if (sp && tid == 64) sp[9] = wall_clock64();  // wave 1's start of the pod
     const SPod& pk = L.ring[(k + RING) % RING];
     // pod k+PD: record and static words -> registers now, -> their ring slots at the end
     // Only the prefetch waves (all but wave 0, unless there is one wave) issue these loads:

@@ -406,7 +406,7 @@ __device__ __forceinline__ bool spread_exchange(SpreadHdr& H, int32_t* xs, unsig
             }
             return false;
           }
-          __builtin_amdgcn_s_sleep(1);
+          spin_pause();
         }
         if (sp && lane == 0) sp[3] = wall_clock64();
 #pragma unroll
@@ -586,7 +586,7 @@ __device__ __forceinline__ bool spread_argmax(SpreadHdr& H, int W, int w, int gs
           }
           break;
         }
-        __builtin_amdgcn_s_sleep(1);
+        spin_pause();
       }
 #pragma unroll
       for (int b = 0; b < 4; b++) {
@@ -641,7 +641,7 @@ __device__ __forceinline__ bool spread_argmax(SpreadHdr& H, int W, int w, int gs
           }
           break;
         }
-        __builtin_amdgcn_s_sleep(1);
+        spin_pause();
       }
       const long long k = s >= W ? 0
                           : kb ? key_expand((uint32_t)lo, kb, node_base)
