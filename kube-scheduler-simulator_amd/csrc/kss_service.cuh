@@ -150,6 +150,9 @@ __device__ __forceinline__ void svc_st(uint8_t* dst, const SvcRow& x, size_t e, 
 // round), then converts and stores: one load round trip per batch of 10 rows instead of one
 // per row.  Interior stores are 16-byte (4-byte for compact uint8 rows); the unaligned ends
 // of each row segment go element by element.
+#ifndef KSS_SVC_RB
+#define KSS_SVC_RB 4  // 10 held 2.1 KB of scratch per lane in the general chain's kernel (r6n A/B: general chain 54.7 -> 47.3 us full, 40.9 -> 31.5 slim)
+#endif
 template <bool COMPACT>
 __device__ __forceinline__ void svc_send(const uint8_t* slot, uint8_t* host, const SlotLayout& L,
                                          const CompactLayout& CL, size_t N, unsigned send, int lo, int hi, bool& ovf) {
@@ -157,7 +160,7 @@ __device__ __forceinline__ void svc_send(const uint8_t* slot, uint8_t* host, con
   // lanes: a wave's stores to host memory complete one instruction at a time, so the rows
   // are spread over every wave of the shard rather than the lanes of one
   const int lane = (int)threadIdx.x & 63, wave = (int)threadIdx.x >> 6, nw = (int)blockDim.x >> 6;
-  constexpr int RB = 10;  // rows per batch (registers: RB x 2 x 16 bytes)
+  constexpr int RB = KSS_SVC_RB;  // rows per batch (registers: RB x 2 x 16 bytes)
   // interior chunks of a row: at most (hi - lo) / 2 + 1 (16-byte stores of 8-byte elements)
   const int rounds = ((hi - lo) / 2 + 1 + 63) / 64;
   for (int rb = 0; rb < SVC_ROWS; rb += RB) {
