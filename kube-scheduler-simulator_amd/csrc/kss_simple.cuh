@@ -1055,6 +1055,21 @@ __device__ __forceinline__ void simple_pass_a_pw(const kss_profile& prof, const 
 
 // AssumePod of pk on shard slot s (LDS node rows; the class / term counts follow after the
 // launch, k_counts).
+// KSS_LANE_COMMIT: the winner's AssumePod over the lanes of one wave (simple_commit_lanes)
+#ifndef KSS_LANE_COMMIT
+#define KSS_LANE_COMMIT 1  // r7c A/B: C2 284.7k -> 290.7k pods/s, C4 unchanged; 0 keeps one lane
+#endif
+static_assert(offsetof(SPod, cnz) == offsetof(SPod, creq) + 3 * sizeof(double), "creq, cnz adjacent");
+// The same AssumePod spread over the lanes of one wave: lane r < 5 adds row 3 + r (Requested cpu /
+// memory / ephemeral, then NonZeroRequested cpu / memory: creq and cnz are adjacent), lane 5 the
+// pod count, lanes 8.. the extended resources -- the rows' LDS round trips overlap instead of
+// following each other on one lane.
+__device__ __forceinline__ void simple_commit_lanes(const SimpleShard& L, const SPod& pk, int s, int lane) {
+  const int cap = L.cap;
+  if (lane < 5) L.r64[(3 + lane) * cap + s] += (&pk.creq[0])[lane];
+  if (lane == 5) L.r32[s] += 1;
+  if (lane >= 8 && lane < 8 + L.nsc) L.sc[(size_t)(L.nsc + lane - 8) * cap + s] += pk.sc_req[lane - 8];
+}
 __device__ __forceinline__ void simple_commit_slot(const SimpleShard& L, const SPod& pk, int s) {
   const int cap = L.cap;
 #pragma unroll
@@ -1134,20 +1149,25 @@ __device__ __forceinline__ bool simple_sync_pw(SimpleHdr& H, int& parity, long l
     }
     if (sp && lane == 0) sp[4] = wall_clock64();
     if (W == 1) {  // the winner (if any) is this shard's best
+      const bool h1 = best != 0;
+      const int slot = (int)(0xFFFFFFFFu - (uint32_t)(unsigned long long)best) - node_base - lo;
       if (lane == 0) {
-        const bool h1 = best != 0;
         H.res[0] = best;
         H.res[1] = h1 ? t[3] : t[0];
         H.res[2] = h1 ? t[4] : t[1];
         H.res[3] = h1 ? t[5] : t[2];
-        if (commit && h1) simple_commit_slot(L, pk, (int)(0xFFFFFFFFu - (uint32_t)(unsigned long long)best) - node_base - lo);
+        if (!KSS_LANE_COMMIT && commit && h1) simple_commit_slot(L, pk, slot);
       }
+      if (KSS_LANE_COMMIT && commit && h1) simple_commit_lanes(L, pk, slot, lane);
     } else {
       const long long v[7] = {best, t[0], t[1], t[2], t[3], t[4], t[5]};
-      if (simple_exchange(H, gran, X, W, w, epoch, err, v, per, node_base, kb) && commit && lane == 0) {
-        const long long K = H.res[0];
+      if (simple_exchange(H, gran, X, W, w, epoch, err, v, per, node_base, kb) && commit && (KSS_LANE_COMMIT || lane == 0)) {
+        const long long K = H.res[0];  // (written by lane 0 of this wave: in order)
         const int x = K ? (int)(0xFFFFFFFFu - (uint32_t)(unsigned long long)K) - node_base - lo : -1;
-        if (x >= 0 && x < own) simple_commit_slot(L, pk, x);
+        if (x >= 0 && x < own) {
+          if (KSS_LANE_COMMIT) simple_commit_lanes(L, pk, x, lane);
+          else simple_commit_slot(L, pk, x);
+        }
       }
     }
   }
@@ -1365,7 +1385,10 @@ __device__ __forceinline__ void simple_schedule(DevCluster c, const SPod* __rest
       const bool won = x >= lo && x < hi;
       sub_s = won ? x - lo : -1;
       sub_h = PW ? cap + (won ? (x - lo) / max(pwv, 1) : 0) : cap;
-      if (!PW && won && tid == 0) simple_commit_slot(L, pk, x - lo);
+      if (!PW && won && (KSS_LANE_COMMIT ? tid < 64 : tid == 0)) {
+        if (KSS_LANE_COMMIT) simple_commit_lanes(L, pk, x - lo, tid);
+        else simple_commit_slot(L, pk, x - lo);
+      }
       // the HBM-only class / term counts are applied after the launch (k_counts): nothing in
       // this loop reads them
     }

@@ -1758,7 +1758,17 @@ __device__ __forceinline__ void spread_schedule(const GTrace& tr, DevCluster c, 
       }
     }
 #endif
-    if (won && tid == 0) {
+    if (KSS_LANE_COMMIT && won && tid < 64) {  // the rows over wave 0's lanes (simple_commit_lanes)
+      const int s = x - lo;
+      const SPod& pk = q.dyn;
+      if (tid < 5) L.r64[(3 + tid) * cap + s] += (&pk.creq[0])[tid];
+      if (tid == 5) L.r32[s] += 1;
+      if (tid >= 8 && tid < 8 + nsc) L.sc[(size_t)(nsc + tid - 8) * cap + s] += pk.sc_req[tid - 8];
+      if (tid == 32)
+        for (int i = 0; i < q.n_cmt; i++)
+          if (q.cmt[i] >= 0) L.cnt[q.cmt[i] * cap + s] += 1;
+    }
+    if (!KSS_LANE_COMMIT && won && tid == 0) {
       const int s = x - lo;
       const SPod& pk = q.dyn;
 #pragma unroll
