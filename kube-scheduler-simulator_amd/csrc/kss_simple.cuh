@@ -1056,6 +1056,9 @@ __device__ __forceinline__ void simple_pass_a_pw(const kss_profile& prof, const 
 // AssumePod of pk on shard slot s (LDS node rows; the class / term counts follow after the
 // launch, k_counts).
 // KSS_LANE_COMMIT: the winner's AssumePod over the lanes of one wave (simple_commit_lanes)
+#ifndef KSS_LANE_COMBINE
+#define KSS_LANE_COMBINE 1  // simple_sync_pw: the waves' partials combined lane-parallel (r7d A/B: C2 291.8k -> 301.3k pods/s)
+#endif
 #ifndef KSS_LANE_COMMIT
 #define KSS_LANE_COMMIT 1  // r7c A/B: C2 284.7k -> 290.7k pods/s, C4 unchanged; 0 keeps one lane
 #endif
@@ -1106,6 +1109,33 @@ __device__ __forceinline__ bool simple_sync_pw(SimpleHdr& H, int& parity, long l
   if (sp && threadIdx.x == 0) sp[8] = wall_clock64();
   idle();
   if (wave == 0) {  // wave 0 alone combines (every lane the same few LDS words: broadcasts) and exchanges
+#if KSS_LANE_COMBINE
+    // lane v < nw reads wave v's partials (one LDS round trip for all waves), then three DPP
+    // steps over the (at most 8) lanes: the largest key, and the six statistics with the best
+    // wave contributing its H1
+    const bool in = lane < nw;
+    const long long* hv = H.red[parity][in ? lane : 0];
+    const long long kv = in ? hv[0] : 0;
+    uint32_t xv[6];
+#pragma unroll
+    for (int i = 0; i < 6; i++) xv[i] = in ? (uint32_t)hv[1 + i] : 0u;
+    long long best = kv;
+    best = dpp_step<OP_MAX, 0xB1, 0xF>(best);
+    best = dpp_step<OP_MAX, 0x4E, 0xF>(best);
+    best = dpp_step<OP_MAX, 0x141, 0xF>(best);
+    {
+      const unsigned long long ub = (unsigned long long)best;
+      best = (long long)(((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(ub >> 32), 0) << 32) |
+                         (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)ub, 0));
+    }
+    const bool me = in && best != 0 && kv == best;  // keys carry the node index: one wave at most
+    uint32_t t[6] = {xv[0], xv[1], xv[2], me ? xv[3] : xv[0], me ? xv[4] : xv[1], me ? xv[5] : xv[2]};
+    dpp_stats_step<0xB1, 0xF>(t);
+    dpp_stats_step<0x4E, 0xF>(t);
+    dpp_stats_step<0x141, 0xF>(t);
+#pragma unroll
+    for (int i = 0; i < 6; i++) t[i] = (uint32_t)__builtin_amdgcn_readlane((int)t[i], 0);
+#else
     // waves 0 and 1 (the usual per-wave geometry) read at once, unconditionally; waves 2.. in a loop
     const long long* h0 = H.red[parity][0];
     const long long* h1 = H.red[parity][nw > 1 ? 1 : 0];
@@ -1147,6 +1177,7 @@ __device__ __forceinline__ bool simple_sync_pw(SimpleHdr& H, int& parity, long l
       t[4] = max(t[4], (uint32_t)h[o + 1]);
       t[5] = max(t[5], (uint32_t)h[o + 2]);
     }
+#endif
     if (sp && lane == 0) sp[4] = wall_clock64();
     if (W == 1) {  // the winner (if any) is this shard's best
       const bool h1 = best != 0;
