@@ -316,6 +316,9 @@ __device__ __forceinline__ void wave_red32(int32_t (&v)[K], const int (&ops)[K])
 // also count in lgkmcnt and make every following LDS wait on the HBM stores.
 // phase bit 0: publish (wave 0), bit 1: sweep by wave gw of nsw sweeping waves (lanes of
 // every sweeping wave share the values: T = 64 nsw / M lanes per value).
+#ifndef KSS_LANE_RED
+#define KSS_LANE_RED 0  // spread_reduce: the waves' partials written by K lanes (r7g A/B: C4 -0.5 %, C3 -1.4 %: off)
+#endif
 constexpr int G_XS = 16;  // at most this many shards polled per lane at once (4 / 8 / 16 by need)
 #ifndef KSS_SPREAD_SAFE
 #define KSS_SPREAD_SAFE 0  // experiment builds: extra barriers around the exchanges
@@ -481,7 +484,14 @@ __device__ __forceinline__ bool spread_reduce(SpreadHdr& H, int32_t* xs, int W, 
 #pragma unroll
   for (int k = 0; k < K; k++) r[k] = v[k];
   wave_red32(r, ops);
-  if (lane == 0) {
+  if (KSS_LANE_RED) {  // lane k writes value k: one LDS store instruction instead of K on lane 0
+    if (lane < K) {
+      int32_t x = r[0];
+#pragma unroll
+      for (int k = 1; k < K; k++) x = lane == k ? r[k] : x;
+      H.red[wave][lane] = x;
+    }
+  } else if (lane == 0) {
 #pragma unroll
     for (int k = 0; k < K; k++) H.red[wave][k] = r[k];
   }
