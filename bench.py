@@ -54,7 +54,7 @@ def cpu_threads():
     return max(1, min(t, aff)), {"nproc": os.cpu_count(), "affinity_cpus": aff, "omp_num_threads": env}
 
 
-def cpu_baseline(config, n_nodes, n_pods, seconds, threads, seed=0, curve=True):
+def cpu_baseline(config, n_nodes, n_pods, seconds, threads, seed=0, curve=True, pct=100):
     """The CPU oracle (plain-C restatement, OpenMP over nodes: the reference's
     parallelize.Until over nodes inside each pod) on the same workload: the whole
     sequential batch is scheduled from the initial snapshot, repeated until `seconds` of wall
@@ -64,6 +64,7 @@ def cpu_baseline(config, n_nodes, n_pods, seconds, threads, seed=0, curve=True):
 
     s = native.Synth(config, seed, n_nodes, n_pods)
     prof = abi.default_profile()
+    prof.pct_nodes_to_score = pct
     kw = dict(threads=threads, record=False, n_classes=s.cluster.n_classes, n_terms=s.cluster.n_terms)
     # size the prefix so one batch takes at most ~seconds/3
     n = min(n_pods, 64)
@@ -77,7 +78,7 @@ def cpu_baseline(config, n_nodes, n_pods, seconds, threads, seed=0, curve=True):
         oracle_c.schedule(prof, s.cluster, s.pods, n, n_nodes, **kw)
         t_used += time.perf_counter() - t0
         reps += 1
-    evals = reps * n * n_nodes
+    evals = reps * n * num_feasible_nodes_to_find(n_nodes, pct)
     _, host = cpu_threads()
     out = {"value": evals / t_used, "unit": "pod-node evals/s", "cores": threads, "kind": "port", "host": host,
            "sample": f"{reps} x the first {n} of {n_pods} pods of config C{config} ({n_nodes} nodes), "
@@ -162,6 +163,16 @@ def cpu_baseline_scenarios(n_nodes, n_pods, seconds, threads, seed_of):
             "host": host, "pods_per_s": n_scen * n_pods / dt,
             "sample": f"{n_scen} C5 scenarios ({n_nodes} nodes x {n_pods} pods each, synthesis included), "
                       f"{threads} scenarios in parallel, {dt:.1f} s wall, oracle/kss_oracle.c single-threaded per scenario"}
+
+
+def num_feasible_nodes_to_find(n: int, pct: int) -> int:
+    """v1.26 schedule_one.go numFeasibleNodesToFind (the simulator's scheduler always has pct 0:
+    simulator/scheduler/scheduler.go:163,258-275)."""
+    if n < 100 or pct >= 100:
+        return n
+    if pct <= 0:
+        pct = max(5, 50 - n // 125)
+    return max(100, n * pct // 100)
 
 
 def rank_seed(seed_base, cfg, rank):
@@ -586,7 +597,7 @@ def latency_profile(cfg, n_nodes, n_pods, seed, device):
     import stamps
     from kss import abi, native
     path = os.path.join(tempfile.mkdtemp(prefix="kss_stamps_"), "stamps.bin")
-    os.environ["KSS_STAMPS_FILE"] = path
+    native.set_stamps_file(path)
     try:
         s = native.Synth(cfg, seed, n_nodes, min(n_pods, 1000))
         ctx = native.Context(abi.default_profile(), device=device)
@@ -596,7 +607,7 @@ def latency_profile(cfg, n_nodes, n_pods, seed, device):
         ctx.close()
         s.close()
     finally:
-        del os.environ["KSS_STAMPS_FILE"]
+        native.set_stamps_file(None)
     out = stamps.latency_summary(path)
     if not out.get("pods"):  # the stamp buffer did not fit in the shard's LDS (k_spread at large shards)
         return {"kernel": out.get("kernel"), "shards": out.get("shards"), "pods": 0, "bound_us_per_pod": None,
@@ -702,7 +713,7 @@ def run_per_pod(args):
     elapsed_svc, ev_svc, cm_svc, chosen_svc = svc_loop(abi.KSS_FIELD_ALL)
     assert chosen_svc == chosen, "service choices differ from kss_eval_pod's"
     # one stamped pass (KSS_SERVICE_STAMPS): where shard 0 spends an evaluation
-    os.environ["KSS_SERVICE_STAMPS"] = "1"
+    native.set_option("service_stamps", 1)
     slim_fields = abi.KSS_FIELD_FAIL | abi.KSS_FIELD_DETAIL | abi.KSS_FIELD_TOTAL
 
     def stamped(fields):
@@ -722,7 +733,7 @@ def run_per_pod(args):
 
     ph = stamped(abi.KSS_FIELD_ALL)
     ph_slim = stamped(slim_fields)
-    del os.environ["KSS_SERVICE_STAMPS"]
+    native.set_option("service_stamps", 0)
     ctx.reset()
     elapsed_svc_slim, ev_svc_slim, _, chosen_svc_slim = svc_loop(slim_fields)
     assert chosen_svc_slim == chosen
@@ -731,21 +742,22 @@ def run_per_pod(args):
     assert chosen_svc_c == chosen
     svc_mode = ctx.service_mode()
     # the same two loops on the general chain (schedule_pod + the record copy), for comparison
-    os.environ["KSS_SERVICE_GENERAL"] = "1"
+    native.set_option("service_general", 1)
     ctx.reset()
     el_g, ev_g, _, ch_g = svc_loop(abi.KSS_FIELD_ALL)
     ctx.reset()
     el_gs, ev_gs, _, ch_gs = svc_loop(slim_fields)
-    del os.environ["KSS_SERVICE_GENERAL"]
+    native.set_option("service_general", 0)
     assert ch_g == chosen and ch_gs == chosen
     # A/B: the simple evaluation with every lane's system fence (the general chain's record fence),
     # and with the static words evaluated per call instead of the table k_static fills at the start
     ab = {}
-    for env in ("KSS_SVC_FULL_FENCE", "KSS_SVC_NO_STATIC", "KSS_SVC_INLINE_SWEEP"):
-        os.environ[env] = "1"
+    for env, opt in (("KSS_SVC_FULL_FENCE", "svc_full_fence"), ("KSS_SVC_NO_STATIC", "svc_no_static"),
+                     ("KSS_SVC_INLINE_SWEEP", "svc_inline_sweep")):
+        native.set_option(opt, 1)
         ctx.reset()
         el_ab, ev_ab, _, ch_ab = svc_loop(slim_fields)
-        del os.environ[env]
+        native.set_option(opt, 0)
         assert ch_ab == chosen
         ab[env] = float(np.median(ev_ab))
     out = {
@@ -959,14 +971,35 @@ def c5_sweep_leg(args, world: int, rank: int, local: int, dist) -> dict:
     1,000 nodes x 1,000 pods in all, 4,096 / world per rank in one resident sweep per GPU (no
     data-path collective), so every world size runs the same whole job (strong scaling; at world
     8 it is the 512-per-GPU shape BASELINE names).  Child processes as in the C4 leg."""
-    res = child_leg(args, world, rank, local, dist, ["--scenarios", str(4096 // world), "--no-traffic"], "C5 sweep",
-                    args.c4_timeout, min(args.cpu_seconds, 6.0))
+    res = child_leg(args, world, rank, local, dist, ["--scenarios", str(4096 // world)], "C5 sweep",
+                    args.c4_timeout, min(args.cpu_seconds, 6.0), traffic=True)
     if res and "error" not in res:
         res["scaling"] = "strong"  # 4,096 scenarios in all at every world size
     return res
 
 
-def child_leg(args, world: int, rank: int, local: int, dist, mode, label, timeout, cpu_seconds) -> dict:
+def c3_leg(args, world: int, rank: int, local: int, dist) -> dict:
+    """BASELINE configs[2] beside the main line: C3 (5,000 nodes x 10,000 pods, default profile +
+    PodTopologySpread + InterPodAffinity programs: k_static + k_spread), the same fields as the
+    main line (roofline with PMC traffic, latency and VALU rooflines, CPU baseline) from a child
+    `bench.py --config 3` run.  At world > 1 every rank schedules its own C3 cluster (weak)."""
+    return child_leg(args, world, rank, local, dist, ["--config", "3", "--no-legs"], "C3", args.c4_timeout,
+                     min(args.cpu_seconds, 8.0), traffic=True)
+
+
+def c2_pct0_leg(args, world: int, rank: int, local: int, dist) -> dict:
+    """The simulator's own setting beside the main line: C2 with percentageOfNodesToScore = 0,
+    the adaptive numFeasibleNodesToFind the simulator's scheduler always runs with
+    (simulator/scheduler/scheduler.go:163,258-275): max(5, 50 - 5000/125) = 10 % -> each pod
+    filters nodes from nextStartNodeIndex until 500 feasible ones are found, and scores those.
+    `evals` counts the filter evaluations the window actually made per pod (the line's
+    evals_per_pod), not N."""
+    return child_leg(args, world, rank, local, dist, ["--config", "2", "--pct", "0", "--no-legs", "--no-traffic", "--no-latency"],
+                     "C2 pct=0", args.c4_timeout, min(args.cpu_seconds, 6.0))
+
+
+def child_leg(args, world: int, rank: int, local: int, dist, mode, label, timeout, cpu_seconds,
+              traffic=False) -> dict:
     """Run `bench.py <mode>` as one child process per rank (torchrun's environment passed on, a
     fresh gloo port), after the main timing.  Returns rank 0's JSON line (others: {}), or an
     error record when any rank's child failed."""
@@ -981,6 +1014,8 @@ def child_leg(args, world: int, rank: int, local: int, dist, mode, label, timeou
            "--cpu-seconds", str(cpu_seconds)]
     if args.no_cpu:
         cmd.append("--no-cpu")
+    if traffic and args.no_traffic:
+        cmd.append("--no-traffic")
     t0 = time.perf_counter()
     try:
         r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=timeout)
@@ -1032,10 +1067,18 @@ def main():
     ap.add_argument("--postfilter", action="store_true", help="DefaultPreemption PostFilter dry runs (kss_postfilter_pod)")
     ap.add_argument("--no-c4", action="store_true", help="skip the C4 split-grid leg of the main line")
     ap.add_argument("--no-c5", action="store_true", help="skip the C5 scenario-sweep leg of the main line")
+    ap.add_argument("--no-c3", action="store_true", help="skip the C3 (PTS + IPA, k_spread) leg of the main line")
+    ap.add_argument("--no-pct0", action="store_true", help="skip the C2 percentageOfNodesToScore=0 leg of the main line")
+    ap.add_argument("--no-legs", action="store_true", help="no extra legs (the legs' own child runs)")
+    ap.add_argument("--pct", type=int, default=100,
+                    help="percentageOfNodesToScore of the profile (100: every node, the north_star setting; "
+                         "0: the simulator's adaptive default)")
     ap.add_argument("--c4-timeout", type=float, default=420.0, help="seconds for the C4 split-grid leg")
     args = ap.parse_args()
     if args.inner:
-        args.no_cpu = args.no_traffic = args.no_latency = args.no_c4 = args.no_c5 = True
+        args.no_cpu = args.no_traffic = args.no_latency = args.no_legs = True
+    if args.no_legs:
+        args.no_c3 = args.no_pct0 = args.no_c4 = args.no_c5 = True
     world_env = os.environ.get("WORLD_SIZE")
     if args.gpus > 1 and world_env is None:
         sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
@@ -1075,11 +1118,13 @@ def main():
     seed = rank_seed(SEED_BASE, cfg, rank)
     s = native.Synth(cfg, seed, n_nodes, n_pods)
     prof = abi.default_profile()
+    prof.pct_nodes_to_score = args.pct
     ctx = native.Context(prof, device=local)
     ctx.load(s.cluster)
     ctx.stage(s.pods)
     import numpy as np
     chosen = np.zeros(n_pods, np.int32)
+    xcd_fallbacks = []
 
     loop_ms = []
 
@@ -1087,6 +1132,7 @@ def main():
         ctx.reset()
         ctx.run_staged(n_pods, out=chosen)
         loop_ms.append(ctx.last_loop_ms())
+        xcd_fallbacks.append(ctx.last_xcd_local().get("fallbacks", 0))
         return ctx.last_timing()[0]
 
     for _ in range(args.warmup):
@@ -1104,7 +1150,10 @@ def main():
     scheduled = int((chosen >= 0).sum())
     elapsed, scheduled_total = reduce_over_ranks(elapsed, scheduled, dist)
 
-    evals = world * n_pods * n_nodes * args.steps
+    # filter + score evaluations per pod: every node at pct=100; below, the window's
+    # numFeasibleNodesToFind (a lower bound of the nodes it filters, stated in the line)
+    evals_per_pod = num_feasible_nodes_to_find(n_nodes, args.pct)
+    evals = world * n_pods * evals_per_pod * args.steps
     value = evals / elapsed
     pods_per_s = scheduled_total * args.steps / elapsed
     kern_avg_s = sum(kern_ms) / len(kern_ms) / 1e3
@@ -1118,13 +1167,16 @@ def main():
     print(json.dumps({"rank": rank, "device": local, "world_size": world, "pods_scheduled": scheduled,
                       "elapsed_s": t1 - t0}), file=sys.stderr, flush=True)
     # the node-axis figure (C4 split grid over every rank's GPU) once the main timing is done
-    c4 = None if args.no_c4 or cfg != 2 or args.nodes or args.pods else c4_split_leg(args, world, rank, local, dist)
-    c5 = None if args.no_c5 or cfg != 2 or args.nodes or args.pods else c5_sweep_leg(args, world, rank, local, dist)
+    main_shape = cfg == 2 and not args.nodes and not args.pods and args.pct == 100
+    c4 = None if args.no_c4 or not main_shape else c4_split_leg(args, world, rank, local, dist)
+    c5 = None if args.no_c5 or not main_shape else c5_sweep_leg(args, world, rank, local, dist)
+    c3 = None if args.no_c3 or not main_shape else c3_leg(args, world, rank, local, dist)
+    c2p0 = None if args.no_pct0 or not main_shape else c2_pct0_leg(args, world, rank, local, dist)
     if rank == 0:
         cpu = None
         if not args.no_cpu and world == 1:
             threads, _ = cpu_threads()
-            cpu = cpu_baseline(cfg, n_nodes, n_pods, args.cpu_seconds, threads, seed=seed)
+            cpu = cpu_baseline(cfg, n_nodes, n_pods, args.cpu_seconds, threads, seed=seed, pct=args.pct)
         latency = None
         if not args.no_latency and world == 1:
             latency = latency_profile(cfg, n_nodes, n_pods, seed, local)
@@ -1144,15 +1196,23 @@ def main():
             "vs_baseline": None,
             "dtype": "int64/f64",
             "data": "synthetic (SplitMix64 seed 0x5EED0000+config[+7919*rank])",
-            "config": {"workload": f"C{cfg}: {n_nodes} nodes x {n_pods} pods, {RECIPE[cfg]}, sequential, pct=100"
+            "config": {"workload": f"C{cfg}: {n_nodes} nodes x {n_pods} pods, {RECIPE[cfg]}, sequential, "
+                                   f"pct={args.pct}"
                                    + (f"; one independent cluster per GPU (seed + rank) x{world}" if world > 1 else ""),
-                       "nodes": n_nodes, "pods": n_pods, "parallelism": f"scenario x{world}"},
+                       "nodes": n_nodes, "pods": n_pods, "parallelism": f"scenario x{world}",
+                       "percentage_of_nodes_to_score": args.pct},
+            "evals_per_pod": evals_per_pod,
+            "evals_note": ("every node filtered and scored" if evals_per_pod == n_nodes else
+                           f"numFeasibleNodesToFind = {evals_per_pod} per pod: the window filters at least this many "
+                           "nodes (more when some are infeasible) and scores at most this many"),
             "pods_per_s": pods_per_s,
             "pods_scheduled_per_step": scheduled,
             "kernel_ms_per_step": kern_avg_s * 1e3,
             "loop_kernel_ms_per_step": loop_s * 1e3,
             "us_per_pod": elapsed / args.steps / n_pods * 1e6,
             "geometry": ctx.last_geometry(),
+            "xcd_fallbacks": int(sum(xcd_fallbacks[-args.steps:])),
+            "xcd_local": ctx.last_xcd_local().get("used", 0),
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": ctx.last_kernel(), "bytes_per_eval": B_EVAL[cfg],
@@ -1164,6 +1224,8 @@ def main():
             "gpu_over_cpu": gpu_over_cpu(pods_per_s, cpu),
             "c4_split": c4,
             "c5_sweep": c5,
+            "c3": c3,
+            "c2_pct0": c2p0,
         }
         print(json.dumps(out), flush=True)
     ctx.close()

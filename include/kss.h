@@ -422,6 +422,24 @@ typedef struct kss_config {
 int kss_abi_version(void);
 const char* kss_last_error(void); /* thread-local message of the last failing call */
 
+/* Tuning and diagnosis options, process-wide (no reference counterpart: the reference reads no
+ * such knobs).  The library reads no environment variable: a plugin host's environment changes
+ * nothing, and every option keeps its default until set here.  Names: "shards" (shards per
+ * cluster, 0 automatic), "xcd" (1: XCD-local grids where the shards fit one XCD), "xcd_shards",
+ * "no_simple", "no_spread", "threads", "force_threads", "nodes_per_shard", "static_bytes" (k_static
+ * budget; 0: an eighth of free memory), "static_ppb", "fold" (k_spread statistics fold), "no_cache",
+ * "coop_launch", "service_general", "service_stamps", "svc_xcd", "svc_no_static", "svc_full_fence",
+ * "svc_inline_sweep", "svc_huge", "service_no_diff", "sweep_pipe", "axis_blocks", "axis_no_fold",
+ * "trace_path", "xcd_force_fallback" (XCD-local launches report failed placement, so the
+ * unrestricted rerun runs: tests).  Read when a context is created (shards, xcd, xcd_shards,
+ * no_simple, no_spread, threads, nodes_per_shard, axis_*) or at each launch (the rest).
+ * KSS_E_NOTFOUND for an unknown name.  kss_set_stamps_file: per-phase timestamps of every launch
+ * of contexts created afterwards are appended to `path` (NULL: off). */
+int kss_set_option(const char* name, int64_t value);
+int kss_get_option(const char* name, int64_t* value);
+int kss_reset_options(void);
+int kss_set_stamps_file(const char* path);
+
 kss_ctx* kss_create(const kss_config* cfg, const kss_profile* prof);
 void kss_destroy(kss_ctx* ctx);
 
@@ -501,10 +519,9 @@ int kss_eval_pod_view(kss_ctx* ctx, const kss_podset* ps, int32_t pod_index, uin
  *                       command and is restarted by the next call.  Every other entry point
  *                       that touches the context's device state stops it first.
  * Results equal kss_eval_pod_view / kss_commit / kss_rollback on the same state.
- * The resident grid occupies the hardware queue its stream maps to (GPU_MAX_HW_QUEUES per
- * process): work of OTHER contexts or streams of the process that shares that queue waits for
- * the grid to leave (kss_service_stop, or its idle exit).  Drive one context per process through
- * the service, or stop it before using another. */
+ * The resident grid runs on a stream with a hardware queue of its own (a CU-masked stream: the
+ * runtime's GPU_MAX_HW_QUEUES shared queues are not used), so no other context's or stream's
+ * work waits behind it; the grid's workgroups still occupy CUs until it leaves. */
 int kss_service_start(kss_ctx* ctx);
 int kss_service_stop(kss_ctx* ctx);
 int kss_service_eval(kss_ctx* ctx, int32_t pod_index, uint32_t fields, kss_pod_view* out);
@@ -668,7 +685,9 @@ int kss_axis_commit(kss_ctx* ctx, int32_t pod_index, const int64_t* key_dev, con
  * peer stores) and polled in the local inbox, so a pod costs no launch and no host round
  * trip on any GPU.  Every part ends with the full chosen / outcome vectors; node state is
  * current on each part for its own rows.
- *   kss_split_config  allocates the zeroed inbox (n_parts == 1 clears the split)
+ *   kss_split_config  allocates the zeroed inbox (n_parts == 1 clears the split) and moves the
+ *                     context to a stream with a hardware queue of its own (parts that share one
+ *                     of the runtime's GPU_MAX_HW_QUEUES queues would run one after the other)
  *   kss_split_inbox   the inbox's device pointer / size / IPC handle (KSS_IPC_HANDLE_BYTES)
  *   kss_split_peers   every part's inbox as addressable in this process (in-process parts)
  *   kss_split_open    the same from the parts' IPC handles (one process per GPU)
@@ -829,8 +848,10 @@ int kss_abi_sizes(int32_t* out, int32_t n);
  * (kss_plan_reason).  The launch still checks LDS geometry and value bounds. */
 int kss_plan_podset(const kss_cluster* cl, const kss_podset* ps, int32_t* out3);
 /* The same with the profile the batch runs under (NULL: kss_plan_podset): a profile with
- * percentageOfNodesToScore below 100, or one that scores an extended resource on a cluster that
- * has them, also rules out both loop kernels (out3[1] = 0, out3[2] the reason). */
+ * percentageOfNodesToScore below 100 on a cluster of 100+ nodes (the findNodesThatPassFilters
+ * window) keeps k_simple only when no pod has a NodeAffinity PreFilterResult list, and rules out
+ * k_spread; a profile that scores an extended resource on a cluster that has them rules out both
+ * loop kernels (out3[1] = the pod, out3[2] the reason). */
 int kss_plan_podset_ex(const kss_cluster* cl, const kss_podset* ps, const kss_profile* prof, int32_t* out3);
 const char* kss_plan_reason(int32_t code);
 /* Test support: y[i] = the device restatement of Go math.Log (kss_spread.cuh go_log_dev,

@@ -56,6 +56,85 @@ int fail(int code, const std::string& msg) {
   return code;
 }
 
+// Tuning and diagnosis options (kss_set_option, include/kss.h): process-wide, changed only by an
+// explicit call.  The product library reads no environment variable, so a plugin host's
+// environment changes nothing; experiment builds (make exp, -DKSS_EXPERIMENTS) start each
+// option from KSS_<ENV> for the A/B recipes in tools/.
+enum KssOpt {
+  O_SHARDS, O_XCD, O_XCD_SHARDS, O_NO_SIMPLE, O_NO_SPREAD, O_AXIS_BLOCKS, O_AXIS_NO_FOLD, O_NODES_PER_SHARD,
+  O_THREADS, O_FORCE_THREADS, O_COOP_LAUNCH, O_NO_CACHE, O_STATIC_BYTES, O_STATIC_PPB, O_FOLD, O_TRACE_PATH,
+  O_SVC_INLINE_SWEEP, O_SERVICE_STAMPS, O_SVC_FULL_FENCE, O_SERVICE_GENERAL, O_SVC_XCD, O_SVC_NO_STATIC,
+  O_SWEEP_PIPE, O_SERVICE_NO_DIFF, O_SVC_HUGE, O_XCD_FORCE_FALLBACK, O_N
+};
+struct OptDef {
+  const char* name;
+  const char* env;
+  long long dflt;
+};
+const OptDef kOptDefs[O_N] = {
+    {"shards", "KSS_SHARDS", 0},                    // shards per cluster (0: automatic)
+    {"xcd", "KSS_XCD", 1},                          // XCD-local grids where the shards fit one XCD
+    {"xcd_shards", "KSS_XCD_SHARDS", 0},            // shards of an XCD-local grid (0: CUs per XCD)
+    {"no_simple", "KSS_NO_SIMPLE", 0},              // never k_simple
+    {"no_spread", "KSS_NO_SPREAD", 0},              // never k_spread
+    {"axis_blocks", "KSS_AXIS_BLOCKS", 0},          // cap on the node-axis grid
+    {"axis_no_fold", "KSS_AXIS_NO_FOLD", 0},        // timing experiment only (wrong results)
+    {"nodes_per_shard", "KSS_NODES_PER_SHARD", 128},
+    {"threads", "KSS_THREADS", 0},                  // preferred workgroup size (0: automatic)
+    {"force_threads", "KSS_FORCE_THREADS", 0},      // exact workgroup size (0: automatic)
+    {"coop_launch", "KSS_COOP_LAUNCH", 0},          // hipLaunchCooperativeKernel for sharded grids
+    {"no_cache", "KSS_NO_CACHE", 0},                // k_schedule without its LDS node cache
+    {"static_bytes", "KSS_STATIC_BYTES", 0},        // k_static budget (0: an eighth of free memory)
+    {"static_ppb", "KSS_STATIC_PPB", 0},            // k_static pods per block (0: automatic)
+    {"fold", "KSS_FOLD", 0},                        // k_spread statistics fold
+    {"trace_path", "KSS_TRACE_PATH", 0},            // print the batch routing decision
+    {"svc_inline_sweep", "KSS_SVC_INLINE_SWEEP", 0},
+    {"service_stamps", "KSS_SERVICE_STAMPS", 0},
+    {"svc_full_fence", "KSS_SVC_FULL_FENCE", 0},
+    {"service_general", "KSS_SERVICE_GENERAL", 0},  // the service's general chain for every pod
+    {"svc_xcd", "KSS_SVC_XCD", 0},
+    {"svc_no_static", "KSS_SVC_NO_STATIC", 0},
+    {"sweep_pipe", "KSS_SWEEP_PIPE", 0},
+    {"service_no_diff", "KSS_SERVICE_NO_DIFF", 0},
+    {"svc_huge", "KSS_SVC_HUGE", 0},
+    {"xcd_force_fallback", "KSS_XCD_FORCE_FALLBACK", 0},  // XCD-local launches report failed placement
+};
+std::atomic<long long> g_opt[O_N];
+std::once_flag g_opt_once;
+std::mutex g_stamps_mu;
+std::string g_stamps_path;  // kss_set_stamps_file
+
+void opt_defaults() {
+  for (int i = 0; i < O_N; i++) {
+    long long v = kOptDefs[i].dflt;
+#ifdef KSS_EXPERIMENTS
+    if (const char* e = getenv(kOptDefs[i].env)) v = (*e >= '0' && *e <= '9') || *e == '-' ? atoll(e) : 1;
+#endif
+    g_opt[i].store(v, std::memory_order_relaxed);
+  }
+#ifdef KSS_EXPERIMENTS
+  if (const char* e = getenv("KSS_STAMPS_FILE")) g_stamps_path = e;
+#endif
+}
+long long opt(KssOpt o) {
+  std::call_once(g_opt_once, opt_defaults);
+  return g_opt[o].load(std::memory_order_relaxed);
+}
+
+// A stream on a hardware queue of its own.  The HIP runtime maps a process's plain streams onto
+// at most GPU_MAX_HW_QUEUES queues (4 on the box), and a kernel queued behind another stream's
+// kernel on a shared queue does not start before that one ends: the parts of a split grid, which
+// poll each other's granules, then wait out the exchange bound (tools/queue_share_probe.hip,
+// profiles/r8a_queue_share_probe.txt: 4 queues, 6 streams -> 4 of 6 waits timed out; the r5d
+// split failure).  A CU-masked stream gets a queue of its own whatever the queue
+// count: every CU in the mask, 0 of 6 waits timed out at 4 queues and 0 of 4 at 1 queue.
+hipError_t dedicated_stream(int n_cu, hipStream_t* st) {
+  std::vector<uint32_t> mask((size_t)(std::max(n_cu, 1) + 31) / 32, 0xffffffffu);
+  if (n_cu % 32) mask.back() = (1u << (n_cu % 32)) - 1u;
+  return hipExtStreamCreateWithCUMask(st, (uint32_t)mask.size(), mask.data());
+}
+
+
 #define HIP_TRY(expr)                                                                        \
   do {                                                                                       \
     hipError_t _e = (expr);                                                                  \
@@ -223,17 +302,21 @@ __global__ __launch_bounds__(KSS_MAX_THREADS) void k_service(const DevJob* __res
 // grid = n_jobs * W, as k_schedule; each shard's nodes live in LDS (cap slots).
 // DEF: the profile is the v1.26 default, folded into the code.
 // Pods [k0, min(k1, n_pods)) of every job; the job's stat buffer holds their static words.
-template <bool DEF>
+// WIN: percentageOfNodesToScore < 100 (one job): k_find = numFeasibleNodesToFind, the window of
+// simple_sync_win, nextStartNodeIndex in job.cursor.
+template <bool DEF, bool WIN>
 __global__ __launch_bounds__(KSS_MAX_THREADS) void k_simple(const DevJob* __restrict__ jobs, kss_profile prof, int W,
                                                             int cap, int k0, int k1, unsigned long long* gran, int* err,
                                                             unsigned long long* stamps, XPeers X, unsigned epoch0,
-                                                            int stat_row0) {
+                                                            int stat_row0, int k_find) {
   extern __shared__ __attribute__((aligned(16))) long long smem[];
   const int Wl = X.n > 1 ? X.wl : W;  // shards of this launch (a split grid runs [w_off, w_off + wl))
   SimpleHdr& H = *reinterpret_cast<SimpleHdr*>(smem);
   int xs = 0;
   if (X.xcd_local) {  // one cluster, every shard on XCD 0 (xcd_slot); the other workgroups leave
-    if (threadIdx.x == 0) H.pad[0] = xcd_slot(reinterpret_cast<int*>(gran + 2 * (size_t)W * SX_VALS), W, (int)gridDim.x, err);
+    if (threadIdx.x == 0)  // the counters behind the granules (and the window's cut granules)
+      H.pad[0] = xcd_slot(reinterpret_cast<int*>(gran + (WIN ? 2 * (size_t)W * SXW_VALS + 2 * SXW_E2 : 2 * (size_t)W * SX_VALS)),
+                          W, (int)gridDim.x, err, X.xcd_local == 2);
     __syncthreads();
     xs = H.pad[0];
     if (xs < 0) return;
@@ -250,15 +333,15 @@ __global__ __launch_bounds__(KSS_MAX_THREADS) void k_simple(const DevJob* __rest
   const kss_profile& P = DEF ? def_prof : H.prof;
   // per-wave mode when every shard's nodes fit PW_LANES slots per wave (one node per lane)
   const int per = (job.c.N + W - 1) / W, nwave = (int)(blockDim.x >> 6);
-  unsigned long long* g = gran ? gran + (size_t)ji * 2 * W * SX_VALS : nullptr;
+  unsigned long long* g = gran ? gran + (size_t)ji * 2 * W * SX_VALS : nullptr;  // (WIN: one job)
   unsigned long long* sp = ji == 0 ? stamps : nullptr;
   const uint32_t* stat = job.stat + (size_t)stat_row0 * (size_t)job.c.N;  // the chunk's half of a double-buffered table
   if (per <= PW_LANES * nwave && KSS_SIMPLE_PW)
-    simple_schedule<DEF, true>(job.c, job.spods, stat, job.P.ints, k0, min(k1, job.n_pods), job.chosen, job.meta, P, W,
-                               w, cap, g, X, epoch0, err, sp, smem);
+    simple_schedule<DEF, true, WIN>(job.c, job.spods, stat, job.P.ints, k0, min(k1, job.n_pods), job.chosen, job.meta, P,
+                                    W, w, cap, g, X, epoch0, err, sp, smem, k_find, job.cursor);
   else
-    simple_schedule<DEF, false>(job.c, job.spods, stat, job.P.ints, k0, min(k1, job.n_pods), job.chosen, job.meta, P,
-                                W, w, cap, g, X, epoch0, err, sp, smem);
+    simple_schedule<DEF, false, WIN>(job.c, job.spods, stat, job.P.ints, k0, min(k1, job.n_pods), job.chosen, job.meta,
+                                     P, W, w, cap, g, X, epoch0, err, sp, smem, k_find, job.cursor);
 }
 
 // grid = W (one cluster); each shard's nodes live in LDS (cap slots); bins_cap: histogram +
@@ -275,7 +358,8 @@ __global__ __launch_bounds__(KSS_MAX_THREADS) void k_spread(const DevJob* __rest
   SpreadHdr& H = *reinterpret_cast<SpreadHdr*>(smem);
   int xs = 0;
   if (X.xcd_local) {  // one cluster, every shard on XCD 0 (xcd_slot); the other workgroups leave
-    if (threadIdx.x == 0) H.pad[0] = xcd_slot(reinterpret_cast<int*>(gran + 2 * (size_t)W * gs), W, (int)gridDim.x, err);
+    if (threadIdx.x == 0)
+      H.pad[0] = xcd_slot(reinterpret_cast<int*>(gran + 2 * (size_t)W * gs), W, (int)gridDim.x, err, X.xcd_local == 2);
     __syncthreads();
     xs = H.pad[0];
     if (xs < 0) return;
@@ -657,13 +741,16 @@ struct kss_ctx {
   int pref_threads = 256;     // KSS_THREADS
   PlanNeeds staged_need;
   int last_geom[3] = {0, 0, 0};
-  const char* stamps_file = nullptr;  // KSS_STAMPS_FILE: dump per-phase timestamps of each launch
+  bool stream_dedicated = false;      // `stream` has a hardware queue of its own (split parts: dedicated_stream)
+  const char* stamps_file = nullptr;  // kss_set_stamps_file: dump per-phase timestamps of each launch
+  std::string stamps_path;
   DevBuf stamp_buf;
   // compact records of the staged pods for k_simple (spod_ok false: some pod needs
   // k_schedule) and the static-word scratch of the current chunk
   DevBuf spod_buf, stat_buf;
   std::vector<SPod> spod_host;
   bool spod_ok = false;
+  bool staged_names = false;  // some staged pod has a NodeAffinity PreFilterResult node list
   // host-resolved programs of the staged pods for k_spread (gpod_ok false: k_schedule)
   DevBuf gpod_buf;
   std::vector<uint4> gpod_host;  // records, gneed.gq uint4 each
@@ -1053,7 +1140,8 @@ const char* const kGpReason[GP_NCODES] = {
     "more than 16 inter-pod-affinity entries after merging",
     "the profile scores an extended (scalar) resource: k_simple / k_spread score cpu, memory and ephemeral-storage only",
     "host ports (NodePorts), node-cached images (ImageLocality) or volumes: k_schedule only",
-    "percentageOfNodesToScore below 100 (numFeasibleNodesToFind / nextStartNodeIndex window): k_schedule only",
+    "percentageOfNodesToScore below 100 (numFeasibleNodesToFind / nextStartNodeIndex window): k_simple for pods "
+    "without a NodeAffinity PreFilterResult list, else k_schedule",
     "the profile scores an extended (scalar) resource and the cluster has extended resources: k_schedule only",
 };
 
@@ -1276,7 +1364,7 @@ bool build_gpods(const kss_podset* ps, int n_scalar, int n_classes, const int32_
   }
   // a folded delta travels as int16 (payload low half): Σ|coefficient| x commits per row bounds it.
   // Opt-in (KSS_FOLD=1): measured no faster on C4 and slower on C3
-  if (need.ref_weight * need.max_mult > 32767 || !getenv("KSS_FOLD"))
+  if (need.ref_weight * need.max_mult > 32767 || !opt(O_FOLD))
     for (int i = 0; i < ps->n_pods; i++) out[(size_t)i].fold = 0;
   // rows first read by a later pod than one committing to them: re-resolve the commits
   size_t rmax = 0;
@@ -1528,6 +1616,42 @@ extern "C" {
 int kss_abi_version(void) { return KSS_ABI_VERSION; }
 const char* kss_last_error(void) { return g_err.c_str(); }
 
+int kss_set_option(const char* name, int64_t value) {
+  if (!name) return fail(KSS_E_INVAL, "null option name");
+  std::call_once(g_opt_once, opt_defaults);
+  for (int i = 0; i < O_N; i++)
+    if (!strcmp(name, kOptDefs[i].name)) {
+      g_opt[i].store((long long)value, std::memory_order_relaxed);
+      return 0;
+    }
+  return fail(KSS_E_NOTFOUND, std::string("unknown option ") + name);
+}
+
+int kss_get_option(const char* name, int64_t* value) {
+  if (!name || !value) return fail(KSS_E_INVAL, "bad arguments");
+  for (int i = 0; i < O_N; i++)
+    if (!strcmp(name, kOptDefs[i].name)) {
+      *value = opt((KssOpt)i);
+      return 0;
+    }
+  return fail(KSS_E_NOTFOUND, std::string("unknown option ") + name);
+}
+
+int kss_reset_options(void) {
+  std::call_once(g_opt_once, opt_defaults);
+  for (int i = 0; i < O_N; i++) g_opt[i].store(kOptDefs[i].dflt, std::memory_order_relaxed);
+  std::lock_guard<std::mutex> lk(g_stamps_mu);
+  g_stamps_path.clear();
+  return 0;
+}
+
+int kss_set_stamps_file(const char* path) {
+  std::call_once(g_opt_once, opt_defaults);
+  std::lock_guard<std::mutex> lk(g_stamps_mu);
+  g_stamps_path = path ? path : "";
+  return 0;
+}
+
 #if KSS_SPREAD_TRACE
 // Trace builds only (not in kss.h): the last k_spread run's trace words [n][W][G_TW], its
 // count list (1 + 4 G_TLIST words) and resident rows.  Returns the words copied.
@@ -1577,16 +1701,20 @@ kss_ctx* kss_create(const kss_config* cfg, const kss_profile* prof) {
   hipDeviceProp_t dp{};
   if (hipGetDeviceProperties(&dp, cfg->device) == hipSuccess) ctx->n_cu = dp.multiProcessorCount;
   if (ctx->n_cu <= 0) ctx->n_cu = 1;
-  if (const char* e = getenv("KSS_SHARDS")) ctx->force_w = std::max(0, atoi(e));
-  if (const char* e = getenv("KSS_XCD")) ctx->xcd_mode = atoi(e) != 0;
-  if (const char* e = getenv("KSS_XCD_SHARDS")) ctx->xcd_w = std::max(0, std::min(64, atoi(e)));
-  ctx->stamps_file = getenv("KSS_STAMPS_FILE");
-  ctx->no_simple = getenv("KSS_NO_SIMPLE") != nullptr;
-  ctx->no_spread = getenv("KSS_NO_SPREAD") != nullptr;
-  if (const char* e = getenv("KSS_AXIS_BLOCKS")) ctx->axis_max_blocks = std::max(0, atoi(e));
-  ctx->axis_no_fold = getenv("KSS_AXIS_NO_FOLD") != nullptr;
-  if (const char* e = getenv("KSS_NODES_PER_SHARD")) ctx->nodes_per_shard = std::max(1, atoi(e));
-  if (const char* e = getenv("KSS_THREADS")) ctx->pref_threads = std::min(KSS_MAX_THREADS, std::max(64, atoi(e)));
+  ctx->force_w = (int)std::max(0ll, opt(O_SHARDS));
+  ctx->xcd_mode = opt(O_XCD) != 0;
+  ctx->xcd_w = (int)std::max(0ll, std::min(64ll, opt(O_XCD_SHARDS)));
+  {
+    std::lock_guard<std::mutex> lk(g_stamps_mu);
+    ctx->stamps_path = g_stamps_path;
+  }
+  ctx->stamps_file = ctx->stamps_path.empty() ? nullptr : ctx->stamps_path.c_str();
+  ctx->no_simple = opt(O_NO_SIMPLE) != 0;
+  ctx->no_spread = opt(O_NO_SPREAD) != 0;
+  ctx->axis_max_blocks = (int)std::max(0ll, opt(O_AXIS_BLOCKS));
+  ctx->axis_no_fold = opt(O_AXIS_NO_FOLD) != 0;
+  ctx->nodes_per_shard = (int)std::max(1ll, opt(O_NODES_PER_SHARD));
+  if (opt(O_THREADS) > 0) ctx->pref_threads = (int)std::min<long long>(KSS_MAX_THREADS, std::max(64ll, opt(O_THREADS)));
   if (hipSetDevice(cfg->device) != hipSuccess || hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreate(&ctx->ev0) != hipSuccess || hipEventCreate(&ctx->ev1) != hipSuccess) {
     fail(KSS_E_DEVICE, "stream/event creation failed");
@@ -2105,6 +2233,13 @@ int kss_split_config(kss_ctx* ctx, int32_t n_parts, int32_t part, int32_t shards
   HIP_TRY(hipStreamSynchronize(ctx->stream));
   split_release(ctx);
   if (n_parts == 1) return 0;  // one part: the whole grid on this device, no inbox
+  if (!ctx->stream_dedicated) {  // every part's grid must run beside the others': a queue of its own
+    hipStream_t st = nullptr;
+    HIP_TRY(dedicated_stream(ctx->n_cu, &st));
+    HIP_TRY(hipStreamDestroy(ctx->stream));
+    ctx->stream = st;
+    ctx->stream_dedicated = true;
+  }
   const size_t W = (size_t)n_parts * (size_t)shards_per_part;
   // two halves (chunk parity, split_chunks), each double-buffered by epoch parity
   const size_t bytes = 2 * sizeof(unsigned long long) * 2 * W * (size_t)std::max(2 * XW_MAX, G_XW);
@@ -2310,12 +2445,12 @@ static bool pick_geometry(int maxN, int W, int pref_threads, Geometry& g) {
   int t = std::min(KSS_MAX_THREADS, std::max(pref_threads, 64));
   if (per < t) t = std::max(64, (per + 63) / 64 * 64);
   int npt = (per + t - 1) / t;
-  const char* ft = getenv("KSS_FORCE_THREADS");  // tuning / diagnosis: exact workgroup size
-  if (ft) {
-    t = std::min(KSS_MAX_THREADS, std::max(64, atoi(ft) / 64 * 64));
+  const long long ft = opt(O_FORCE_THREADS);  // tuning / diagnosis: exact workgroup size
+  if (ft > 0) {
+    t = (int)std::min<long long>(KSS_MAX_THREADS, std::max(64ll, ft / 64 * 64));
     npt = (per + t - 1) / t;
   }
-  while (!ft && npt > 4 && t < KSS_MAX_THREADS) {
+  while (ft <= 0 && npt > 4 && t < KSS_MAX_THREADS) {
     t = std::min(KSS_MAX_THREADS, t * 2);
     npt = (per + t - 1) / t;
   }
@@ -2329,8 +2464,7 @@ static bool pick_geometry(int maxN, int W, int pref_threads, Geometry& g) {
 // no more workgroups than CUs) and launches plainly.  KSS_COOP_LAUNCH=1 uses the
 // cooperative launch instead (same residency, runtime-checked).
 static int launch_resident(const void* fn, dim3 grid, dim3 block, void** args, size_t shmem, hipStream_t st) {
-  static const bool coop = getenv("KSS_COOP_LAUNCH") != nullptr;
-  if (coop) {
+  if (opt(O_COOP_LAUNCH)) {
     HIP_TRY(hipLaunchCooperativeKernel(fn, grid, block, args, (unsigned)shmem, st));
     return 0;
   }
@@ -2354,7 +2488,7 @@ static int launch_schedule(hipStream_t st, const Geometry& g, int n_jobs, int bi
   if (base > KSS_LDS_BUDGET) return fail(KSS_E_UNSUPPORTED, "per-workgroup LDS budget exceeded (too many nodes per shard)");
   // node cache with every label key, without labels, or none, whatever fits
   int cache_keys = -1;
-  if (!getenv("KSS_NO_CACHE")) {
+  if (!opt(O_NO_CACHE)) {
     if (base + node_cache_bytes(cap, n_keys) <= KSS_LDS_BUDGET) cache_keys = n_keys;
     else if (base + node_cache_bytes(cap, 0) <= KSS_LDS_BUDGET) cache_keys = 0;
   }
@@ -2420,8 +2554,7 @@ static bool scalar_fast_ok(const kss_profile& p, int n_scalar) {
 // c5_sweep leg (4,096 scenarios x 1,000 x 1,000: 16.4 GB) in one chunk, without per-chunk
 // relaunches of the loop kernel.
 static size_t static_budget() {
-  const char* e = getenv("KSS_STATIC_BYTES");
-  const long long v = e ? atoll(e) : 0;
+  const long long v = opt(O_STATIC_BYTES);
   if (v > 0) return (size_t)v;
   size_t fr = 0, tot = 0;
   if (hipMemGetInfo(&fr, &tot) != hipSuccess) fr = 0;
@@ -2477,7 +2610,7 @@ static void launch_static(hipStream_t st, bool def, const DevJob* jobs, const ks
   // pods per block: with the LDS label copy, enough pods to amortise loading it (C5: 64 pods of
   // 1,000 nodes per block; r6c: 8 / 16 / 32 / 64 within 1 % of each other)
   int ppb = lk ? 8 * STATIC_PODS : STATIC_PODS;
-  if (const char* e = getenv("KSS_STATIC_PPB")) ppb = std::max(1, std::min(256, atoi(e)));
+  if (opt(O_STATIC_PPB) > 0) ppb = (int)std::min(256ll, opt(O_STATIC_PPB));
   const dim3 sgrid((unsigned)(std::max(n_hi - n_lo, 1) + 1023) / 1024, (unsigned)((k1 - k0 + ppb - 1) / ppb),
                    (unsigned)n_jobs);
   const size_t sh = sizeof(int32_t) * 1024 * (size_t)lk;
@@ -2493,7 +2626,7 @@ static int launch_simple(hipStream_t st, const Geometry& g, int n_jobs, const De
                          int n_pods_max, int max_nodes, int chunk, unsigned long long* gran, size_t gran_bytes, int* err,
                          unsigned long long* stamps = nullptr, hipEvent_t* ev = nullptr, const SplitRun* split = nullptr,
                          int nsc = 0, bool xcd = false, int* xcd_fallbacks = nullptr, int max_keys = 0,
-                         hipStream_t st2 = nullptr, std::vector<hipEvent_t>* pev = nullptr) {
+                         hipStream_t st2 = nullptr, std::vector<hipEvent_t>* pev = nullptr, int k_find = 0) {
   // st2 (with pev, two events per chunk): the static words of chunk i+1 are computed on st2 into the
   // other half of a double-buffered table while k_simple runs chunk i on st (each job's table holds
   // 2 x chunk rows); k_simple of chunk i waits for its k_static, k_static of chunk i+1 for
@@ -2501,7 +2634,10 @@ static int launch_simple(hipStream_t st, const Geometry& g, int n_jobs, const De
   int cap = simple_cap(g);
   const size_t shmem = simple_lds_bytes(cap, nsc);
   const bool def = same_profile(prof, default_profile_c());
-  const void* fn = def ? (const void*)k_simple<true> : (const void*)k_simple<false>;
+  // k_find > 0: the percentageOfNodesToScore window (one job, not split)
+  const bool win = k_find > 0;
+  const void* fn = win ? (def ? (const void*)k_simple<true, true> : (const void*)k_simple<false, true>)
+                       : (def ? (const void*)k_simple<true, false> : (const void*)k_simple<false, false>);
   HIP_TRY(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shmem));
   XPeers X = split ? split->X : XPeers{};
   const bool sp_grid = X.n > 1;
@@ -2553,11 +2689,11 @@ static int launch_simple(hipStream_t st, const Geometry& g, int n_jobs, const De
     }
     unsigned long long* sp = k0 == 0 ? stamps : nullptr;
     void* args[] = {(void*)&jobs, (void*)&pr, (void*)&W,  (void*)&cap, (void*)&k0,     (void*)&k1,
-                    (void*)&gc,   (void*)&err, (void*)&sp, (void*)&X,   (void*)&epoch0, (void*)&row0};
+                    (void*)&gc,   (void*)&err, (void*)&sp, (void*)&X,   (void*)&epoch0, (void*)&row0, (void*)&k_find};
     const int ci = k0 / chunk;
     if (ev) HIP_TRY(hipEventRecord(ev[2 * ci], st));
     if (xcd) {
-      X.xcd_local = 1;
+      X.xcd_local = opt(O_XCD_FORCE_FALLBACK) ? 2 : 1;  // 2: placement reported failed (tests)
       if (int rc = launch_resident(fn, xgrid, block, args, shmem, st)) return rc;
       int e = 0;
       HIP_TRY(hipMemcpyAsync(&e, err, sizeof(int), hipMemcpyDeviceToHost, st));
@@ -2638,7 +2774,7 @@ static int launch_spread(hipStream_t st, const Geometry& g, const GpodNeeds& q, 
     shmem = std::max(shmem, std::min((size_t)KSS_LDS_BUDGET, (size_t)std::max(0, atoi(e))));
 #endif
   const bool def = same_profile(prof, default_profile_c());
-  const bool fold = getenv("KSS_FOLD") != nullptr;
+  const bool fold = opt(O_FOLD) != 0;
   const void* fn = def ? (fold ? (const void*)k_spread<true, true> : (const void*)k_spread<true, false>)
                        : (fold ? (const void*)k_spread<false, true> : (const void*)k_spread<false, false>);
   HIP_TRY(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shmem));
@@ -2682,7 +2818,7 @@ static int launch_spread(hipStream_t st, const Geometry& g, const GpodNeeds& q, 
     const int ci = k0 / chunk;
     if (ev) HIP_TRY(hipEventRecord(ev[2 * ci], st));
     if (xcd) {  // as launch_simple: an XCD-local grid, run again unrestricted when placement failed
-      X.xcd_local = 1;
+      X.xcd_local = opt(O_XCD_FORCE_FALLBACK) ? 2 : 1;  // 2: placement reported failed (tests)
       if (int rc = launch_resident(fn, xgrid, block, args, shmem, st)) return rc;
       int e = 0;
       HIP_TRY(hipMemcpyAsync(&e, err, sizeof(int), hipMemcpyDeviceToHost, st));
@@ -2791,12 +2927,16 @@ static int run_single_impl(kss_ctx* ctx, const PlanNeeds& need, const DevPods& d
   // percentageOfNodesToScore below 100: findNodesThatPassFilters' window (numFeasibleNodesToFind,
   // nextStartNodeIndex) runs on k_schedule only; its per-shard count exchange needs W + 1 values
   const bool window = ctx->prof.pct_nodes_to_score < 100;
-  if (window) W = std::min(W, XW_MAX - NSCAL);
+  // k_simple runs the window itself (simple_sync_win) for pods without a PreFilterResult list on an
+  // unsplit grid; k_find = N: the list is too short for a window (every node processed)
+  const int k_find = window ? num_feasible_to_find((int)N, ctx->prof.pct_nodes_to_score) : (int)N;
+  const bool simple_win_ok = !window || k_find >= (int)N || (!split && !ctx->staged_names);
+  if (window) W = std::min(W, XW_MAX - NSCAL);  // k_schedule's window exchange: W + 1 values
   // nominated pods (kss_nominate): RunFilterPluginsWithNominatedPods and PreferNominatedNode run on
   // k_schedule only
   const bool nomq = !ctx->nom.empty();
   if (nomq && split) return fail(KSS_E_UNSUPPORTED, "split grids do not read the nominator");
-  const bool simple_ok = !window && !nomq && staged && ctx->spod_ok && commit && !record && !keep_norm && !need.general &&
+  const bool simple_ok = simple_win_ok && !nomq && staged && ctx->spod_ok && commit && !record && !keep_norm && !need.general &&
                          scalar_fast_ok(ctx->prof, ctx->dc.n_scalar) && ctx->small_values && f64_exact(ctx->f64_cluster, ctx->f64_pods, n) &&
                          !ctx->no_simple && !(flags & KSS_SCHED_GENERAL_KERNEL);
   if (simple_ok && ctx->force_w <= 0 && !split) W = std::min(W, 64 * SX_CHUNKS);
@@ -2815,7 +2955,7 @@ static int run_single_impl(kss_ctx* ctx, const PlanNeeds& need, const DevPods& d
                          scalar_fast_ok(ctx->prof, ctx->dc.n_scalar) && ctx->small_values && f64_exact(ctx->f64_cluster, ctx->f64_pods, n) &&
                          !ctx->no_simple && !ctx->no_spread && !(flags & KSS_SCHED_GENERAL_KERNEL) &&
                          spread_bounds_ok(ctx->gneed, count_total, cell_total, (int)N);
-  if (getenv("KSS_TRACE_PATH"))  // diagnosis: why a batch with programs is (not) on k_spread
+  if (opt(O_TRACE_PATH))  // diagnosis: why a batch with programs is (not) on k_spread
     fprintf(stderr,
             "kss path: staged=%d gpod_ok=%d commit=%d record=%d general=%d scalar=%d small=%d f64=%d bounds=%d "
             "(ref_weight=%lld total=%.0f cell=%.0f) n_res=%zu bins=%d\n",
@@ -2837,7 +2977,7 @@ static int run_single_impl(kss_ctx* ctx, const PlanNeeds& need, const DevPods& d
   const bool simple = simple_ok && simple_fits(g, ctx->dc.n_scalar);
   const int n_res = (int)ctx->gneed.res_rows.size();
   bool spread = spread_ok && spread_fits(g, ctx->gneed, ctx->dc.n_keys, n_res, N, ctx->dc.n_scalar);
-  if (spread && !simple && !getenv("KSS_THREADS") && !getenv("KSS_FORCE_THREADS")) {
+  if (spread && !simple && opt(O_THREADS) <= 0 && opt(O_FORCE_THREADS) <= 0) {
     // k_spread: one node per lane where the workgroup allows it (up to KSS_SPREAD_PREF_THREADS):
     // its per-node passes are the chain between exchanges (C4: 256 -> 512 lanes, stats +
     // filter + normalise 4.4 -> 2.6 us per pod)
@@ -3014,7 +3154,7 @@ static int run_single_impl(kss_ctx* ctx, const PlanNeeds& need, const DevPods& d
   if (simple)
     rc = launch_simple(ctx->stream, g, 1, jd, ctx->prof, n, (int)N, chunk, gran, gb,
                        errp, stamps, ctx->loop_ev.data(), split ? &srun : nullptr, ctx->dc.n_scalar, ctx->last_xcd[0] != 0,
-                       &ctx->last_xcd[1], ctx->dc.n_keys);
+                       &ctx->last_xcd[1], ctx->dc.n_keys, nullptr, nullptr, k_find < (int)N ? k_find : 0);
   else if (spread)
   {
     const HandoffLayout hl(g.W, n_res, (int)N, ctx->dc.n_scalar);
@@ -3127,7 +3267,11 @@ static int stage_spods(kss_ctx* ctx, const kss_podset* ps) {
   ctx->f64_pods = F64Bounds{};
   f64_bounds_pods(ps, ctx->f64_pods);
   ctx->staged_max_own = 0;
-  for (int i = 0; i < ps->n_pods; i++) ctx->staged_max_own = std::max(ctx->staged_max_own, (int)ps->pods[i].own_terms_len);
+  ctx->staged_names = false;
+  for (int i = 0; i < ps->n_pods; i++) {
+    ctx->staged_max_own = std::max(ctx->staged_max_own, (int)ps->pods[i].own_terms_len);
+    ctx->staged_names |= ps->pods[i].names_len >= 0;
+  }
   ctx->spod_ok = build_spods(ps, ctx->dc.n_scalar, ctx->spod_host);
   ctx->gpod_ok = false;
   if (!ctx->spod_ok) {  // programs: the resolved records of k_spread
@@ -3608,7 +3752,7 @@ static int svc_launch(kss_ctx* ctx) {
   HIP_TRY(dev_zero(v.err.p, 16, v.stream));  // the error word and xcd_slot's two counters
   v.box->err = 0;
   v.box->xcd_fail = 0;
-  const bool inl = getenv("KSS_SVC_INLINE_SWEEP") && atoi(getenv("KSS_SVC_INLINE_SWEEP")) != 0;
+  const bool inl = opt(O_SVC_INLINE_SWEEP) != 0;
   const void* fn = v.gen ? (const void*)k_service<true, false>
                          : (v.simple ? (inl ? (const void*)k_service<false, true, true> : (const void*)k_service<false, true>)
                                      : (const void*)k_service<false, false>);
@@ -3623,11 +3767,9 @@ static int svc_launch(kss_ctx* ctx) {
   unsigned long long* seenp = relay + 2 * SVC_DRING;
   uint8_t* rec = v.rec_dev;
   unsigned long long s0 = seq0;
-  int stamps = getenv("KSS_SERVICE_STAMPS") ? 1 : 0;
-  if (getenv("KSS_SVC_FULL_FENCE")) stamps |= 4;  // the simple evaluation's record fence as the general chain's
-#ifdef KSS_EXPERIMENTS
-  if (getenv("KSS_SERVICE_NO_DIFF")) stamps |= 2;  // every requested row resent (no row diff)
-#endif
+  int stamps = opt(O_SERVICE_STAMPS) ? 1 : 0;
+  if (opt(O_SVC_FULL_FENCE)) stamps |= 4;  // the simple evaluation's record fence as the general chain's
+  if (opt(O_SERVICE_NO_DIFF)) stamps |= 2;  // every requested row resent (no row diff)
   int xcd = v.xcd ? 1 : 0;
   void* args[] = {(void*)&jd,  (void*)&pr,  (void*)&W,     (void*)&npt,   (void*)&bins, (void*)&ck, (void*)&gran,
                   (void*)&err, (void*)&box, (void*)&relay, (void*)&seenp, (void*)&rec, (void*)&s0, (void*)&stamps,
@@ -3661,11 +3803,11 @@ static int svc_start_locked(kss_ctx* ctx) {
   // one lane per shard), the node rows cached in LDS (checked below); KSS_SERVICE_GENERAL=1 keeps
   // the general chain, for comparison.  On an XCD-local grid when its shards fit one XCD's CUs.
   const bool simple_pre = ctx->spod_ok && !window && !need.general && ctx->dc.n_scalar == 0 && ctx->small_values &&
-                          f64_exact(ctx->f64_cluster, ctx->f64_pods, ctx->staged_n) && !getenv("KSS_SERVICE_GENERAL");
+                          f64_exact(ctx->f64_cluster, ctx->f64_pods, ctx->staged_n) && !opt(O_SERVICE_GENERAL);
   const int xcd_cus = ctx->n_cu / XCD_GRID_MULT;
   // (off by default: the record's stores to host memory from one XCD were slower than the L2
   // exchange saved -- C2 slim 20.9 -> 29.0 us, r5o_perpod.json; KSS_SVC_XCD=1 turns it on)
-  static const bool svc_xcd = getenv("KSS_SVC_XCD") && atoi(getenv("KSS_SVC_XCD")) != 0;
+  const bool svc_xcd = opt(O_SVC_XCD) != 0;
   const bool xcd_ok = svc_xcd && simple_pre && ctx->xcd_mode && ctx->n_cu % XCD_GRID_MULT == 0 && ctx->force_w <= 0 &&
                       N <= (size_t)xcd_cus * KSS_MAX_THREADS * KSS_MAX_NPT;
   if (xcd_ok) W = std::min(W, xcd_cus);
@@ -3680,7 +3822,8 @@ static int svc_start_locked(kss_ctx* ctx) {
   int cache_keys = -1;
   if (base + node_cache_bytes(cap, ctx->dc.n_keys) <= KSS_LDS_BUDGET) cache_keys = ctx->dc.n_keys;
   else if (base + node_cache_bytes(cap, 0) <= KSS_LDS_BUDGET) cache_keys = 0;
-  if (!v.stream) HIP_TRY(hipStreamCreateWithFlags(&v.stream, hipStreamNonBlocking));
+  // the resident grid on a queue of its own: no other stream's kernel waits behind it
+  if (!v.stream) HIP_TRY(dedicated_stream(ctx->n_cu, &v.stream));
   const SlotLayout SL(N);
   if (!v.box) {
     HIP_TRY(hipHostMalloc((void**)&v.box, sizeof(SvcBox), hipHostMallocCoherent | hipHostMallocMapped));
@@ -3691,11 +3834,7 @@ static int svc_start_locked(kss_ctx* ctx) {
   const size_t rec_bytes = SL.bytes + CompactLayout(N).bytes;  // the full record, then the compact one
   if (v.rec_bytes < rec_bytes) {
     svc_free_rec(v);
-#ifdef KSS_EXPERIMENTS
-    const bool huge = getenv("KSS_SVC_HUGE") != nullptr;
-#else
-    constexpr bool huge = false;
-#endif
+    const bool huge = opt(O_SVC_HUGE) != 0;
     if (huge) {
       // experiment: the record in transparent huge pages (madvise), registered with the device,
       // so that its rows do not each take their own 4 KiB translation
@@ -3741,7 +3880,7 @@ static int svc_start_locked(kss_ctx* ctx) {
   // the static words of every staged pod (4 bytes per pod and node, at most 4 GiB): one load per
   // evaluation instead of the pod's requirement chains from HBM (KSS_SVC_NO_STATIC=1: inline)
   const size_t stat_bytes = sizeof(uint32_t) * (size_t)std::max(ctx->staged_n, 1) * std::max<size_t>(N, 1);
-  const bool pre_static = v.simple && stat_bytes <= ((size_t)4 << 30) && !getenv("KSS_SVC_NO_STATIC");
+  const bool pre_static = v.simple && stat_bytes <= ((size_t)4 << 30) && !opt(O_SVC_NO_STATIC);
   if (pre_static && (rc = v.stat.ensure(stat_bytes))) return rc;
   job.stat = pre_static ? (uint32_t*)v.stat.p : nullptr;
   HIP_TRY(hipMemcpyAsync(v.job.p, &job, sizeof(DevJob), hipMemcpyHostToDevice, v.stream));
@@ -4255,7 +4394,7 @@ kss_sweep* kss_sweep_create(int32_t device, const kss_profile* prof, int32_t n_s
   // one workgroup per scenario: at most two node slots per lane (C5, 1,000 nodes: 512
   // threads ran the 512-scenario sweep in 16.5 ms against 23.7 ms at 256)
   int pref = sw->max_nodes > 512 ? 512 : 256;
-  if (const char* e = getenv("KSS_THREADS")) pref = std::min(KSS_MAX_THREADS, std::max(64, atoi(e)));
+  if (opt(O_THREADS) > 0) pref = (int)std::min<long long>(KSS_MAX_THREADS, std::max(64ll, opt(O_THREADS)));
   if (!pick_geometry(sw->max_nodes, 1, pref, sw->g)) {
     fail(KSS_E_UNSUPPORTED, "scenario cluster too large for one workgroup");
     return nullptr;
@@ -4263,7 +4402,7 @@ kss_sweep* kss_sweep_create(int32_t device, const kss_profile* prof, int32_t n_s
   // k_static + k_simple for the whole sweep when every scenario qualifies (no spread /
   // inter-pod programs, no scalar resources, values inside the exact f64 envelope)
   std::vector<std::vector<SPod>> spods(n_scen);
-  bool simple = getenv("KSS_NO_SIMPLE") == nullptr && !sw->need.general && simple_fits(sw->g, 0) &&
+  bool simple = !opt(O_NO_SIMPLE) && !sw->need.general && simple_fits(sw->g, 0) &&
                 prof->pct_nodes_to_score >= 100;  // the window runs on k_schedule
   for (int i = 0; i < prof->fit_n && simple; i++) simple = prof->fit_weight[i] >= 0 && prof->fit_weight[i] < (1ll << 20);
   for (int s = 0; s < n_scen && simple; s++) {
@@ -4314,7 +4453,7 @@ kss_sweep* kss_sweep_create(int32_t device, const kss_profile* prof, int32_t n_s
   // k_static time it hides when both share the CUs)
   if (simple) hipSetDevice(device);  // the budget follows this device's free memory
   sw->chunk = simple ? static_chunk(sum_nodes, sw->max_pods) : 0;
-  const bool dbl = simple && sw->chunk < sw->max_pods && getenv("KSS_SWEEP_PIPE") != nullptr;
+  const bool dbl = simple && sw->chunk < sw->max_pods && opt(O_SWEEP_PIPE) != 0;
   if (dbl) sw->chunk = static_chunk(2 * sum_nodes, sw->max_pods);
   const int halves = dbl ? 2 : 1;
   if (simple) {
@@ -4832,9 +4971,15 @@ int kss_plan_podset_ex(const kss_cluster* cl, const kss_podset* ps, const kss_pr
   if (int rc = check_profile(prof)) return rc;
   if (int rc = kss_plan_podset(cl, ps, out3)) return rc;
   if (out3[0] == 0) return 0;  // the programs already rule out both loop kernels
-  if (prof->pct_nodes_to_score < 100) {
+  // the window (percentageOfNodesToScore < 100 on a list long enough to stop early) runs on k_simple
+  // for pods without a PreFilterResult node list (simple_sync_win), never on k_spread
+  int names_pod = -1;
+  for (int i = 0; i < ps->n_pods && names_pod < 0; i++)
+    if (ps->pods[i].names_len >= 0) names_pod = i;
+  const bool win = num_feasible_to_find(cl->n_nodes, prof->pct_nodes_to_score) < cl->n_nodes;
+  if (win && (out3[0] == 2 || names_pod >= 0)) {
+    out3[1] = out3[0] == 2 || names_pod < 0 ? (ps->n_pods > 0 ? 0 : -1) : names_pod;
     out3[0] = 0;
-    out3[1] = ps->n_pods > 0 ? 0 : -1;
     out3[2] = GP_PCT;
   } else if (!scalar_fast_ok(*prof, cl->n_scalar)) {
     out3[0] = 0;

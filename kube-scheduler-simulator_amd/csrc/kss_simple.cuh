@@ -113,9 +113,15 @@ constexpr int SX_VALS = 8;    // granules per shard per exchange: key lo/hi, H0 
 // XCD 0 gets fewer than W of them (counted once every workgroup of the grid has started), the
 // launch fails with err = 3 before touching any state and the host runs it again unrestricted.
 // ctr: two zeroed words behind the launch's granules, [0] shards taken, [1] workgroups started.
-// Returns the shard, -1 (leave), -2 (placement failed).
+// Returns the shard, -1 (leave), -2 (placement failed).  force_fail (kss_set_option
+// "xcd_force_fallback", tests): workgroup 0 reports failed placement and every workgroup leaves,
+// so the host's unrestricted rerun is what schedules the batch.
 constexpr int XCD_GRID_MULT = 8;
-__device__ __forceinline__ int xcd_slot(int* ctr, int W, int grid, int* err) {
+__device__ __forceinline__ int xcd_slot(int* ctr, int W, int grid, int* err, bool force_fail = false) {
+  if (force_fail) {
+    if (blockIdx.x == 0) err_raise(err, 3);
+    return blockIdx.x == 0 ? -2 : -1;
+  }
   int slot = -1;
   if (xcc_id() == 0) {
     slot = atomicAdd(&ctr[0], 1);
@@ -672,9 +678,13 @@ __device__ __forceinline__ long long wave_max_key(long long key, int kb, int nod
 }
 
 // LDS image of the loop head: reduction scratch (double-buffered), exchange results.
+constexpr int SX_RED = 16;  // per-wave reduction row: the key and up to 15 statistics (the window's 12)
 struct alignas(16) SimpleHdr {
-  long long red[2][MAXWAVES][SX_VALS];
+  long long red[2][MAXWAVES][SX_RED];
   long long res[4];  // winner key of the previous pod; nf, max TT, max NA of the next pod
+  long long win[10];  // window (simple_sync_win): F, TT / NA of the wholly kept segments, cut shard, part, j; d, TT, NA
+  int cutc[2][MAXWAVES];  // window cut scan: feasible nodes of the part per wave
+  int cutm[MAXWAVES][2];  // ... and the waves' maxima of the kept ones
   kss_profile prof;  // a runtime (non-default) profile: indexed by resource id, so in LDS, not scratch
   int abort;
   int pad[3];
@@ -1210,16 +1220,441 @@ __device__ __forceinline__ bool simple_sync_pw(SimpleHdr& H, int& parity, long l
   return true;
 }
 
+// ---------------------------------------------------------------------------
+// percentageOfNodesToScore < 100: findNodesThatPassFilters' window on k_simple
+// ---------------------------------------------------------------------------
+// v1.26 findNodesThatPassFilters (Parallelism = 1, the deterministic form) checks
+// the nodes from nextStartNodeIndex s in canonical order, wrapping, and stops once K + 1 feasible
+// nodes were found (K = numFeasibleNodesToFind): the first K are kept (scored, selectHost's
+// candidates); the (K+1)-th, d, was filtered but dropped, and nextStartNodeIndex becomes d (the
+// processed count is the d - s nodes before it).  With F <= K feasible nodes every node is
+// visited, every feasible one kept, and s stays.
+// Here the window rides on the pod's statistics exchange.  Each shard splits its slots at the
+// pod's start node into part a (node >= s) and part b (node < s), so the visiting order is the
+// segments a_0 .. a_{W-1}, b_0 .. b_{W-1}, and publishes per part {feasible count, max raw TT,
+// max raw NA} for H0 and H1 (SXW_VALS granules).  After the sweep every shard knows from the
+// segments' counts the segment holding the (K+1)-th feasible node (the cut) and the maxima of
+// the segments wholly before it; the cut segment's shard ranks its feasible nodes (ballots) for
+// d and the maxima of its first j, and publishes them (a second exchange of SXW_E2 granules,
+// polled from that one shard).  Pass B keeps node n iff feasible and (no cut or (n - s) mod N <
+// (d - s) mod N).  Statistics index: (h * 2 + part) * 3 + {0 F, 1 TT, 2 NA}, h = 0 H0, 1 H1.
+constexpr int SXW_VALS = 10;  // granules per shard: key lo / hi, then {F << 16 | TT, NA} of a0, b0, a1, b1
+constexpr int SXW_E2 = 4;     // the cut shard's granules per epoch parity: d, TT, NA (+ pad)
+
+__device__ __forceinline__ void win_acc(uint32_t (&u)[12], bool c0, bool c1, int part, const SVal& e) {
+#pragma unroll
+  for (int v = 0; v < 4; v++) {
+    const bool on = ((v >> 1) ? c1 : c0) && (v & 1) == part;
+    u[v * 3] += on ? 1u : 0u;
+    u[v * 3 + 1] = max(u[v * 3 + 1], on ? (uint32_t)e.tt : 0u);
+    u[v * 3 + 2] = max(u[v * 3 + 2], on ? (uint32_t)e.na : 0u);
+  }
+}
+
+// simple_pass_a with the window's split: part a / b of each slot by its node against `start`
+template <bool DEF>
+__device__ __forceinline__ void simple_pass_a_win(const kss_profile& prof, const SPod& q_lds, const SPod& q0_lds,
+                                                  const SimpleShard& L, int sl, int own, int cand_s, int lo, int start,
+                                                  uint32_t (&u)[12]) {
+  const int tid = threadIdx.x, nt = blockDim.x;
+  const uint32_t* sw = L.st + (size_t)sl * L.cap;
+  const SPod q = q_lds;
+  SPod q0;
+#pragma unroll
+  for (int k = 0; k < 3; k++) q0.creq[k] = q0_lds.creq[k];
+  q0.cnz[0] = q0_lds.cnz[0];
+  q0.cnz[1] = q0_lds.cnz[1];
+  const bool scal = L.nsc > 0 && (DEF || ((prof.filter_enabled >> KSS_F_NODE_RESOURCES_FIT) & 1u));
+#pragma unroll
+  for (int i = 0; i < 12; i++) u[i] = 0;
+  for (int s = tid; s <= L.cap; s += nt) {
+    const bool extra = s == own && cand_s >= 0;
+    if (s >= own && !extra) continue;
+    const int ns = extra ? cand_s : s;
+    const uint32_t wd = sw[ns];
+    DynRow r = shard_row(L, ns);
+    if (extra) add_commit(r, q0);
+    SVal e = DEF ? dyn_eval_def(q, wd, r) : dyn_eval(prof, q, wd, r);
+    if (scal && e.f == 0 && scalar_short(L.sc, L.nsc, L.cap, ns, q_lds, extra, q0_lds)) e.f = KSS_F_NODE_RESOURCES_FIT;
+    cv_put(L, extra ? L.cap : s, e);
+    win_acc(u, e.f == 0 && !extra, e.f == 0 && s != cand_s, lo + ns >= start ? 0 : 1, e);
+  }
+}
+
+// simple_pass_a_pw with the window's split
+template <bool DEF>
+__device__ __forceinline__ void simple_pass_a_pw_win(const kss_profile& prof, const SPod& q_lds, const SPod& q0_lds,
+                                                     const SimpleShard& L, int sl, int own, int pwv, int cand_w, int lo,
+                                                     int start, uint32_t (&u)[12]) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const uint32_t* sw = L.st + (size_t)sl * L.cap;
+  const SPod q = q_lds;
+  SPod q0;
+#pragma unroll
+  for (int k = 0; k < 3; k++) q0.creq[k] = q0_lds.creq[k];
+  q0.cnz[0] = q0_lds.cnz[0];
+  q0.cnz[1] = q0_lds.cnz[1];
+  const bool scal = L.nsc > 0 && (DEF || ((prof.filter_enabled >> KSS_F_NODE_RESOURCES_FIT) & 1u));
+  const int s = wv * pwv + lane;
+  const bool extra = lane == pwv && cand_w >= 0;
+  const bool mine = lane < pwv && s < own;
+#pragma unroll
+  for (int i = 0; i < 12; i++) u[i] = 0;
+  if (mine || extra) {
+    const int ns = extra ? cand_w : s;
+    const uint32_t wd = sw[ns];
+    DynRow r = shard_row(L, ns);
+    if (extra) add_commit(r, q0);
+    SVal e = DEF ? dyn_eval_def(q, wd, r) : dyn_eval(prof, q, wd, r);
+    if (scal && e.f == 0 && scalar_short(L.sc, L.nsc, L.cap, ns, q_lds, extra, q0_lds)) e.f = KSS_F_NODE_RESOURCES_FIT;
+    cv_put(L, extra ? L.cap + wv : s, e);
+    win_acc(u, e.f == 0 && !extra, e.f == 0 && (extra || s != cand_w), lo + ns >= start ? 0 : 1, e);
+  }
+}
+
+// the twelve window statistics over DPP lanes: counts summed, maxima kept
+template <int CTRL, int ROWS>
+__device__ __forceinline__ void dpp_win_step(uint32_t (&v)[12]) {
+  uint32_t t[12];
+#pragma unroll
+  for (int i = 0; i < 12; i++) t[i] = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v[i], CTRL, ROWS, 0xF, false);
+#pragma unroll
+  for (int i = 0; i < 12; i++) v[i] = (i % 3 == 0) ? v[i] + t[i] : max(v[i], t[i]);
+}
+
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t t = (uint32_t)__shfl_up((int)v, o, 64);
+    v += lane >= o ? t : 0u;
+  }
+  return v;
+}
+
+// The cut shard: rank the feasible nodes of `part` (pod k+1's verdicts; the winner's slot takes
+// its H1 verdict) in canonical order; d = the node of rank j, TT / NA = the maxima over ranks < j.
+// Whole workgroup; results uniform.
+template <bool PW>
+__device__ __forceinline__ void win_cut_scan(SimpleHdr& H, const SimpleShard& L, int own, int lo, int start, int part,
+                                             int j, int sub_s, int sub_h, int pwv, int& d, int& ptt, int& pna) {
+  const int tid = threadIdx.x, nt = blockDim.x, lane = tid & 63, wave = tid >> 6, nw = nt >> 6;
+  const int iters = PW ? 1 : (own + nt - 1) / nt;
+  int carry = 0, mt = 0, mn = 0;
+  for (int it = 0; it < iters; it++) {
+    const int s = PW ? wave * pwv + lane : it * nt + tid;
+    const bool valid = PW ? (lane < pwv && s < own) : s < own;
+    bool f = false;
+    SVal e{0, 0, 0, 0, 0};
+    if (valid && (part == 0 ? lo + s >= start : lo + s < start)) {
+      e = cv_get(L, s == sub_s ? sub_h : s);
+      f = e.f == 0;
+    }
+    const unsigned long long b = __ballot(f);
+    if (lane == 0) H.cutc[it & 1][wave] = (int)__popcll(b);
+    lds_barrier();
+    int before = 0, tot = 0;
+    for (int x = 0; x < nw; x++) {
+      const int cx = H.cutc[it & 1][x];
+      before += x < wave ? cx : 0;
+      tot += cx;
+    }
+    const int rank = carry + before + (int)__popcll(b & ((1ull << lane) - 1ull));
+    if (f && rank == j) H.win[6] = lo + s;
+    mt = max(mt, (f && rank < j) ? e.tt : 0);
+    mn = max(mn, (f && rank < j) ? e.na : 0);
+    carry += tot;
+  }
+  mt = (int)wave_red<OP_MAX>(mt);
+  mn = (int)wave_red<OP_MAX>(mn);
+  if (lane == 0) {
+    H.cutm[wave][0] = mt;
+    H.cutm[wave][1] = mn;
+  }
+  lds_barrier();
+  ptt = 0;
+  pna = 0;
+  for (int x = 0; x < nw; x++) {
+    ptt = max(ptt, H.cutm[x][0]);
+    pna = max(pna, H.cutm[x][1]);
+  }
+  d = (int)H.win[6];
+}
+
+// The window's statistics exchange (both per-wave and per-thread modes; PW: the best wave contributes
+// its H1, else every wave's H1 set already accounts for the shard's candidate).  Pod k's AssumePod
+// on the winner's slot is applied here (wave 0, lane-parallel) before the closing barrier.
+// R = {winner key of pod k, kept count, max TT, max NA of pod k+1 over its kept nodes}, d_out = pod
+// k+1's dropped node (-1: no cut).  start: pod k+1's nextStartNodeIndex.  False if the launch aborted.
+template <bool PW, typename Idle>
+__device__ __forceinline__ bool simple_sync_win(SimpleHdr& H, int& parity, long long wkey, uint32_t (&u)[12], int W,
+                                                int w, unsigned epoch, unsigned long long* gran, const XPeers& X,
+                                                int* err, int per, int node_base, int lo, int own, const SPod& pk,
+                                                bool commit, const SimpleShard& L, int kb, int k_find, int start,
+                                                int pwv, long long (&R)[4], int& d_out,
+                                                KSS_GLOBAL unsigned long long* sp, Idle&& idle) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  dpp_win_step<0xB1, 0xF>(u);
+  dpp_win_step<0x4E, 0xF>(u);
+  dpp_win_step<0x141, 0xF>(u);
+  dpp_win_step<0x140, 0xF>(u);
+  dpp_win_step<0x142, 0xA>(u);
+  dpp_win_step<0x143, 0xC>(u);
+  if (lane == 63) {  // the reduced values sit in lane 63
+    H.red[parity][wave][0] = wkey;
+#pragma unroll
+    for (int i = 0; i < 12; i++) H.red[parity][wave][1 + i] = u[i];
+  }
+  lds_barrier();
+  idle();
+  if (wave == 0) {
+    // the shard: lane v < nw reads wave v's row, three DPP steps over the (at most 8) lanes
+    const bool in = lane < nw;
+    const long long* hv = H.red[parity][in ? lane : 0];
+    const long long kv = in ? hv[0] : 0;
+    long long best = kv;
+    best = dpp_step<OP_MAX, 0xB1, 0xF>(best);
+    best = dpp_step<OP_MAX, 0x4E, 0xF>(best);
+    best = dpp_step<OP_MAX, 0x141, 0xF>(best);
+    {
+      const unsigned long long ub = (unsigned long long)best;
+      best = (long long)(((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(ub >> 32), 0) << 32) |
+                         (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)ub, 0));
+    }
+    const bool me = PW ? (in && best != 0 && kv == best) : in;
+    uint32_t t[12];
+#pragma unroll
+    for (int i = 0; i < 6; i++) {
+      t[i] = in ? (uint32_t)hv[1 + i] : 0u;
+      t[6 + i] = in ? (uint32_t)(me ? hv[7 + i] : hv[1 + i]) : 0u;
+    }
+    dpp_win_step<0xB1, 0xF>(t);
+    dpp_win_step<0x4E, 0xF>(t);
+    dpp_win_step<0x141, 0xF>(t);
+#pragma unroll
+    for (int i = 0; i < 12; i++) t[i] = (uint32_t)__builtin_amdgcn_readlane((int)t[i], 0);
+    if (sp && lane == 0) sp[4] = wall_clock64();
+    // every shard's packed values in the lane of that shard (W == 1: this shard in lane 0)
+    uint32_t got[SX_CHUNKS][8];
+    long long gbest = best;
+    bool ok = true;
+    if (W == 1) {
+#pragma unroll
+      for (int v = 0; v < 4; v++) {
+        got[0][2 * v] = lane == 0 ? (t[3 * v] << 16) | t[3 * v + 1] : 0u;
+        got[0][2 * v + 1] = lane == 0 ? t[3 * v + 2] : 0u;
+      }
+#pragma unroll
+      for (int ch = 1; ch < SX_CHUNKS; ch++)
+#pragma unroll
+        for (int i = 0; i < 8; i++) got[ch][i] = 0;
+    } else {
+      const unsigned long long tag = (unsigned long long)epoch << 32;
+      if (lane < SXW_VALS) {
+        uint32_t x = (uint32_t)(unsigned long long)best;
+        x = lane == 1 ? (uint32_t)((unsigned long long)best >> 32) : x;
+#pragma unroll
+        for (int v = 0; v < 4; v++) {
+          x = lane == 2 + 2 * v ? ((t[3 * v] << 16) | t[3 * v + 1]) : x;
+          x = lane == 3 + 2 * v ? t[3 * v + 2] : x;
+        }
+        xpub(X, gran, ((size_t)(epoch & 1) * W + w) * SXW_VALS + lane, tag | x);
+      }
+      const unsigned long long* base = gran + (size_t)(epoch & 1) * W * SXW_VALS;
+      long long kbest = 0;
+#pragma unroll
+      for (int ch = 0; ch < SX_CHUNKS; ch++) {
+#pragma unroll
+        for (int i = 0; i < 8; i++) got[ch][i] = 0;
+        if (ch * 64 >= W || !ok) continue;
+        const int s = ch * 64 + lane;
+        const bool valid = s < W;
+        long long t0_ = 0;
+        uint32_t k2[2] = {0, 0};
+        for (unsigned spins = 0;; ++spins) {
+          bool okp = true;
+          unsigned long long g[SXW_VALS];
+#pragma unroll
+          for (int i = 0; i < SXW_VALS; i++)
+            g[i] = __hip_atomic_load(base + (size_t)(valid ? s : 0) * SXW_VALS + i, __ATOMIC_RELAXED,
+                                     __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+          for (int i = 0; i < SXW_VALS; i++) okp &= !valid || (g[i] >> 32) == epoch;
+          if (__all(okp)) {
+            k2[0] = valid ? (uint32_t)g[0] : 0u;
+            k2[1] = valid ? (uint32_t)g[1] : 0u;
+#pragma unroll
+            for (int i = 0; i < 8; i++) got[ch][i] = valid ? (uint32_t)g[2 + i] : 0u;
+            break;
+          }
+          if (spin_expired(spins, t0_)) {
+            if (lane == 0) {
+              H.abort = 1;
+              err_raise(err, 1);
+            }
+            ok = false;
+            break;
+          }
+          spin_pause();
+        }
+        const long long kk = (long long)(((unsigned long long)k2[1] << 32) | k2[0]);
+        kbest = kk > kbest ? kk : kbest;
+      }
+      gbest = wave_max_key(kbest, kb, node_base);
+    }
+    if (ok) {
+      const int gl = gbest != 0 ? (int)(0xFFFFFFFFu - (uint32_t)(unsigned long long)gbest) - node_base : -1;
+      // each lane's shard: H1 when the winner is one of its nodes
+      uint32_t Fa[SX_CHUNKS], Fb[SX_CHUNKS], ta[SX_CHUNKS], tb[SX_CHUNKS], na_[SX_CHUNKS], nb_[SX_CHUNKS];
+      uint32_t A = 0, B = 0;
+#pragma unroll
+      for (int ch = 0; ch < SX_CHUNKS; ch++) {
+        const int s = ch * 64 + lane;
+        const bool h1 = W > 1 ? (gl >= s * per && gl < s * per + per) : gbest != 0;
+        const int o = h1 ? 4 : 0;
+        Fa[ch] = got[ch][o] >> 16;
+        ta[ch] = got[ch][o] & 0xFFFFu;
+        na_[ch] = got[ch][o + 1];
+        Fb[ch] = got[ch][o + 2] >> 16;
+        tb[ch] = got[ch][o + 2] & 0xFFFFu;
+        nb_[ch] = got[ch][o + 3];
+        A += Fa[ch];
+        B += Fb[ch];
+      }
+      A = (uint32_t)wave_red<OP_SUM>((long long)A);
+      B = (uint32_t)wave_red<OP_SUM>((long long)B);
+      const uint32_t F = A + B, K = (uint32_t)k_find;
+      uint32_t ftt = 0, fna = 0;
+      int cut = -1, part = 0, j = 0;
+      if (F <= K) {
+#pragma unroll
+        for (int ch = 0; ch < SX_CHUNKS; ch++) {
+          ftt = max(ftt, max(ta[ch], tb[ch]));
+          fna = max(fna, max(na_[ch], nb_[ch]));
+        }
+      } else {
+        uint32_t ca = 0, cb = A;  // segments before this chunk
+        unsigned long long hit = 0;
+        int hit_ch = -1;
+        uint32_t pre_hit = 0;
+#pragma unroll
+        for (int ch = 0; ch < SX_CHUNKS; ch++) {
+          const uint32_t ia = wave_incl_scan(Fa[ch]), ib = wave_incl_scan(Fb[ch]);
+          const uint32_t pa = ca + ia - Fa[ch], pb = cb + ib - Fb[ch];
+          ftt = max(ftt, pa + Fa[ch] <= K ? ta[ch] : 0u);
+          fna = max(fna, pa + Fa[ch] <= K ? na_[ch] : 0u);
+          ftt = max(ftt, pb + Fb[ch] <= K ? tb[ch] : 0u);
+          fna = max(fna, pb + Fb[ch] <= K ? nb_[ch] : 0u);
+          const bool cA = pa <= K && K < pa + Fa[ch], cB = pb <= K && K < pb + Fb[ch];
+          const unsigned long long ba = __ballot(cA), bb = __ballot(cB);
+          if (hit_ch < 0 && (ba | bb)) {
+            const int l = __ffsll((long long)(ba ? ba : bb)) - 1;
+            hit_ch = ch;
+            hit = ba ? 0ull : 1ull;
+            cut = ch * 64 + l;
+            pre_hit = (uint32_t)__builtin_amdgcn_readlane((int)(ba ? pa : pb), l);
+          }
+          ca += (uint32_t)__builtin_amdgcn_readlane((int)ia, 63);
+          cb += (uint32_t)__builtin_amdgcn_readlane((int)ib, 63);
+        }
+        part = (int)hit;
+        j = (int)(K - pre_hit);
+      }
+      ftt = (uint32_t)wave_red<OP_MAX>((long long)ftt);
+      fna = (uint32_t)wave_red<OP_MAX>((long long)fna);
+      // pod k's AssumePod on the winner's slot (before the closing barrier: the next pod's pass A
+      // reads that row without a barrier of its own)
+      if (commit && gbest != 0) {
+        const int x = gl - lo;
+        if (x >= 0 && x < own) simple_commit_lanes(L, pk, x, lane);
+      }
+      if (lane == 0) {
+        H.res[0] = gbest;
+        H.win[0] = F;
+        H.win[1] = ftt;
+        H.win[2] = fna;
+        H.win[3] = cut;
+        H.win[4] = part;
+        H.win[5] = j;
+      }
+    }
+  }
+  parity ^= 1;
+  lds_barrier();
+  if (H.abort) return false;
+  const long long F = H.win[0];
+  const int cut = (int)H.win[3];
+  long long mtt = H.win[1], mna = H.win[2], nf = F;
+  int d = -1;
+  if (cut >= 0) {
+    nf = k_find;
+    const long long best = H.res[0];
+    const int gl = best != 0 ? (int)(0xFFFFFFFFu - (uint32_t)(unsigned long long)best) - node_base : -1;
+    const bool won = gl >= lo && gl < lo + own;
+    const int sub_s = won ? gl - lo : -1;
+    const int sub_h = PW ? L.cap + (won ? (gl - lo) / max(pwv, 1) : 0) : L.cap;
+    const size_t e2 = 2 * (size_t)W * SXW_VALS + (size_t)(epoch & 1) * SXW_E2;
+    if (cut == w) {  // uniform over the workgroup
+      int cd = -1, ctt = 0, cna = 0;
+      win_cut_scan<PW>(H, L, own, lo, start, (int)H.win[4], (int)H.win[5], sub_s, sub_h, pwv, cd, ctt, cna);
+      if (W == 1) {
+        d = cd;
+        mtt = max(mtt, (long long)ctt);
+        mna = max(mna, (long long)cna);
+      } else if (threadIdx.x < 3) {
+        const unsigned long long tag = (unsigned long long)epoch << 32;
+        const uint32_t x = threadIdx.x == 0 ? (uint32_t)cd : (threadIdx.x == 1 ? (uint32_t)ctt : (uint32_t)cna);
+        xpub(X, gran, e2 + threadIdx.x, tag | x);
+      }
+    }
+    if (W > 1) {
+      if (wave == 0) {
+        const unsigned long long* b2 = gran + e2;
+        long long t0_ = 0;
+        for (unsigned spins = 0;; ++spins) {
+          const unsigned long long g = __hip_atomic_load(b2 + min(lane, 2), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (__all((g >> 32) == epoch)) {
+            if (lane < 3) H.win[7 + lane] = (long long)(uint32_t)g;
+            break;
+          }
+          if (spin_expired(spins, t0_)) {
+            if (lane == 0) {
+              H.abort = 1;
+              err_raise(err, 1);
+            }
+            break;
+          }
+          spin_pause();
+        }
+      }
+      lds_barrier();
+      if (H.abort) return false;
+      d = (int)H.win[7];
+      mtt = max(mtt, H.win[8]);
+      mna = max(mna, H.win[9]);
+    }
+  }
+  R[0] = H.res[0];
+  R[1] = nf;
+  R[2] = mtt;
+  R[3] = mna;
+  d_out = d;
+  return true;
+}
+
 // Pods [k0, k1) of the batch for shard w of one cluster (every pod commits).  `stat`
 // holds the static words of those pods ([k - k0][N]).  On an exchange timeout the error
 // word is set and the shard leaves without writing node state back.  PW: per-wave mode
-// (simple_sync_pw; the caller checks that every shard's nodes fit it).
-template <bool DEF, bool PW>
+// (simple_sync_pw; the caller checks that every shard's nodes fit it).  WIN: percentageOfNodesToScore
+// < 100 (simple_sync_win): k_find = numFeasibleNodesToFind, cursor = the cluster's nextStartNodeIndex
+// word (read at the start, written back by shard 0 at the end).
+template <bool DEF, bool PW, bool WIN>
 __device__ __forceinline__ void simple_schedule(DevCluster c, const SPod* __restrict__ spods,
                                                 const uint32_t* __restrict__ stat, const int32_t* __restrict__ ints,
                                                 int k0, int k1, int32_t* chosen, PodMeta* meta, const kss_profile& prof,
                                                 int W, int w, int cap, unsigned long long* gran, const XPeers& X,
-                                                unsigned epoch0, int* err, unsigned long long* stamps, long long* smem) {
+                                                unsigned epoch0, int* err, unsigned long long* stamps, long long* smem,
+                                                int k_find = 0, int32_t* cursor = nullptr) {
   const int tid = threadIdx.x, nt = blockDim.x;
   SimpleHdr& H = *reinterpret_cast<SimpleHdr*>(smem);
   const SimpleShard L = shard_view(reinterpret_cast<uint8_t*>(smem) + sizeof(SimpleHdr), cap, c.n_scalar);
@@ -1259,6 +1694,9 @@ __device__ __forceinline__ void simple_schedule(DevCluster c, const SPod* __rest
   }
   if (tid == 0) H.abort = 0;
   __syncthreads();
+  // the window (WIN): pod k's start node and dropped node (pass B), pod k0's start from the cursor
+  int wst = 0, wd = -1;
+  const int cur0 = WIN && cursor && c.N > 0 ? (int)(((long long)ld_ag(cursor) % c.N + c.N) % c.N) : 0;
 
   KSS_GLOBAL const uint32_t* gstat = gp(stat);
   KSS_GLOBAL const uint4* gspod = gp(reinterpret_cast<const uint4*>(spods));
@@ -1358,7 +1796,12 @@ __device__ __forceinline__ void simple_schedule(DevCluster c, const SPod* __rest
       if (keys && lane < pwv && s < own) {
         const SVal e = cv_get(L, s == sub_s ? sub_h : s);
         const long long key = simple_key(prof, e, scored, max_tt, rtt, max_na, rna, (uint32_t)(c.node_base + lo + s));
-        best = e.f == 0 ? key : 0;
+        bool kept = true;
+        if (WIN && wd >= 0) {  // inside the window [wst, wd) in visiting order
+          const int n = lo + s;
+          kept = (n >= wst ? n - wst : n + c.N - wst) < (wd >= wst ? wd - wst : wd + c.N - wst);
+        }
+        best = (e.f == 0 && kept) ? key : 0;
       }
       if (sp && tid == 0) sp[1] = wall_clock64();
       best = wave_max_key(best, kb, c.node_base);
@@ -1369,7 +1812,12 @@ __device__ __forceinline__ void simple_schedule(DevCluster c, const SPod* __rest
           for (int s = tid; s < own; s += nt) {
             const SVal e = cv_get(L, s == sub_s ? sub_h : s);
             const long long key = simple_key(prof, e, scored, max_tt, rtt, max_na, rna, (uint32_t)(c.node_base + lo + s));
-            best = (e.f == 0 && key > best) ? key : best;
+            bool kept = true;
+            if (WIN && wd >= 0) {
+              const int n = lo + s;
+              kept = (n >= wst ? n - wst : n + c.N - wst) < (wd >= wst ? wd - wst : wd + c.N - wst);
+            }
+            best = (e.f == 0 && kept && key > best) ? key : best;
           }
         }
         if (sp && tid == 0) sp[1] = wall_clock64();
@@ -1385,7 +1833,25 @@ __device__ __forceinline__ void simple_schedule(DevCluster c, const SPod* __rest
     // pass A: pod k+1 before pod k's commit, and on the candidate after it
     const SPod& qn = L.ring[(k + 1) % RING];
     const int sln = (k + 1) % RING;
-    if constexpr (PW) {
+    if constexpr (WIN) {
+      // pod k+1 starts where pod k's window stopped (its dropped node), else where pod k started
+      const int wsn = k >= k0 ? (wd >= 0 ? wd : wst) : cur0;
+      uint32_t u[12];
+      if (k + 1 < k1) {
+        if constexpr (PW) simple_pass_a_pw_win<DEF>(prof, qn, pk, L, sln, own, pwv, cand, lo, wsn, u);
+        else simple_pass_a_win<DEF>(prof, qn, pk, L, sln, own, cand, lo, wsn, u);
+      } else {
+#pragma unroll
+        for (int i = 0; i < 12; i++) u[i] = 0;
+      }
+      if (sp && tid == 0) sp[3] = wall_clock64();
+      int dn = -1;
+      if (!simple_sync_win<PW>(H, parity, best, u, W, w, ++epoch, gran, X, err, per, c.node_base, lo, own, pk, k >= k0, L,
+                               kb, k_find, wsn, pwv, R, dn, sp, prefetch_idle))
+        return;
+      wst = wsn;
+      wd = dn;
+    } else if constexpr (PW) {
       uint32_t u[6];
       if (k + 1 < k1) {
         simple_pass_a_pw<DEF>(prof, qn, pk, L, sln, own, pwv, cand, u);
@@ -1416,7 +1882,7 @@ __device__ __forceinline__ void simple_schedule(DevCluster c, const SPod* __rest
       const bool won = x >= lo && x < hi;
       sub_s = won ? x - lo : -1;
       sub_h = PW ? cap + (won ? (x - lo) / max(pwv, 1) : 0) : cap;
-      if (!PW && won && (KSS_LANE_COMMIT ? tid < 64 : tid == 0)) {
+      if (!PW && !WIN && won && (KSS_LANE_COMMIT ? tid < 64 : tid == 0)) {
         if (KSS_LANE_COMMIT) simple_commit_lanes(L, pk, x - lo, tid);
         else simple_commit_slot(L, pk, x - lo);
       }
@@ -1442,6 +1908,8 @@ __device__ __forceinline__ void simple_schedule(DevCluster c, const SPod* __rest
     if (sp && tid == 0) sp[6] = wall_clock64();
   }
   if (tid == out_tid) store_pending();  // the last pod's outcome
+  // nextStartNodeIndex after the last pod (every shard holds it; the first shard writes it)
+  if (WIN && cursor && w == 0 && tid == 0) st_ag(cursor, (int32_t)wst);
   // node state back to HBM
   __syncthreads();
   for (int s = tid; s < own; s += nt) {

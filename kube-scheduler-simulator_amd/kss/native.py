@@ -34,6 +34,10 @@ _lib: Optional[C.CDLL] = None
 SIGNATURES = [
     ("kss_abi_version", C.c_int, []),
     ("kss_last_error", C.c_char_p, []),
+    ("kss_set_option", C.c_int, [C.c_char_p, C.c_int64]),
+    ("kss_get_option", C.c_int, [C.c_char_p, P(C.c_int64)]),
+    ("kss_reset_options", C.c_int, []),
+    ("kss_set_stamps_file", C.c_int, [C.c_char_p]),
     ("kss_abi_sizes", C.c_int, [P(C.c_int32), C.c_int32]),
     ("kss_default_profile", None, [P(abi.Profile)]),
     ("kss_create", C.c_void_p, [P(abi.Config), P(abi.Profile)]),
@@ -136,6 +140,46 @@ def lib() -> C.CDLL:
 def check(rc: int):
     if rc != 0:
         raise KssError(rc, (lib().kss_last_error() or b"").decode())
+
+
+def set_option(name: str, value: int):
+    """kss_set_option: a process-wide tuning / diagnosis option (the library reads no environment)."""
+    check(lib().kss_set_option(name.encode(), int(value)))
+
+
+def get_option(name: str) -> int:
+    v = C.c_int64()
+    check(lib().kss_get_option(name.encode(), C.byref(v)))
+    return v.value
+
+
+def reset_options():
+    """Every option back to its default, stamps off (kss_reset_options)."""
+    check(lib().kss_reset_options())
+
+
+def set_stamps_file(path: Optional[str]):
+    """kss_set_stamps_file: phase stamps of contexts created afterwards go to `path` (None: off)."""
+    check(lib().kss_set_stamps_file(path.encode() if path else None))
+
+
+class options:
+    """with native.options(shards=9, static_bytes=...): set, then restore the previous values."""
+
+    def __init__(self, **kw):
+        self.kw = kw
+        self.old = {}
+
+    def __enter__(self):
+        for k, v in self.kw.items():
+            self.old[k] = get_option(k)
+            set_option(k, v)
+        return self
+
+    def __exit__(self, *exc):
+        for k, v in self.old.items():
+            set_option(k, v)
+        return False
 
 
 class PodView:
@@ -373,9 +417,9 @@ class Context:
     def stage(self, podset_struct: abi.PodSet):
         check(lib().kss_stage_pods(self.h, C.byref(podset_struct)))
 
-    def run_staged(self, n: int, record=False, out: Optional[np.ndarray] = None) -> np.ndarray:
+    def run_staged(self, n: int, record=False, out: Optional[np.ndarray] = None, flags: int = 0) -> np.ndarray:
         chosen = out if out is not None else np.full(max(n, 1), -2, np.int32)
-        fl = abi.KSS_SCHED_RECORD if record else 0
+        fl = (abi.KSS_SCHED_RECORD if record else 0) | flags
         check(lib().kss_run_staged(self.h, n, fl, chosen.ctypes.data_as(P(C.c_int32))))
         return chosen[:n]
 

@@ -182,23 +182,34 @@ def store_profile_from_config(cfg: Optional[dict], scalars: Sequence[str] = ()) 
     return prof
 
 
-def profile_from_config(cfg: Optional[dict], scalars: Sequence[str] = ()) -> abi.Profile:
-    """kss_profile of a KubeSchedulerConfiguration's (first) profile; None -> the default.
+def profile_from_config(cfg: Optional[dict], scalars: Sequence[str] = (),
+                        pct_nodes_to_score: Optional[int] = None) -> abi.Profile:
+    """kss_profile of a KubeSchedulerConfiguration's (first) profile; None -> the default plugins.
     Weights follow the framework (the Score extension point's entry wins over MultiPoint's);
-    the result store's annotation weights are ``store_weights_from_config``."""
+    the result store's annotation weights are ``store_weights_from_config``.
+
+    percentageOfNodesToScore: the simulator's scheduler keeps only Profiles and Extenders of the
+    configuration it is given and resets every other field to the v1 defaults
+    (filterOutNonAllowedChangesOnCfg, simulator/scheduler/scheduler.go:258-275, applied at
+    :163), so it always runs with 0 -- the adaptive numFeasibleNodesToFind -- whatever the
+    configuration (or its absence) says.  The profile follows that: 0, unless the caller opts in
+    to another value with ``pct_nodes_to_score`` (the north_star / bench workloads use 100).  The
+    configuration's own field is still validated (ValidateKubeSchedulerConfiguration: 0..100)."""
+    if pct_nodes_to_score is not None and not 0 <= int(pct_nodes_to_score) <= 100:
+        raise Unsupported("percentageOfNodesToScore must be between 0 and 100")
+    pct = 0 if pct_nodes_to_score is None else int(pct_nodes_to_score)
     prof = abi.default_profile()
+    prof.pct_nodes_to_score = pct
     if not cfg:
         return prof
     profiles = cfg.get("profiles") or [{}]
     if len(profiles) > 1:
         raise Unsupported("one scheduler profile only (plugins.go getScorePluginWeight reads profiles[0])")
     p0 = profiles[0]
-    # v1.26 has the global field only (profiles gained their own in v1.27); unset means the v1
-    # default 0, the adaptive numFeasibleNodesToFind -- what the simulator's built-in scheduler
-    # always runs with (it resets the configuration to its defaults, scheduler.go:258-275)
-    pct = cfg.get("percentageOfNodesToScore")
-    pct = 0 if pct is None else int(pct)
-    if not 0 <= pct <= 100:
+    # v1.26 has the global field only (profiles gained their own in v1.27); validated, then reset
+    # by the simulator (see above)
+    cfg_pct = cfg.get("percentageOfNodesToScore")
+    if cfg_pct is not None and not 0 <= int(cfg_pct) <= 100:
         raise Unsupported("percentageOfNodesToScore must be between 0 and 100 (ValidateKubeSchedulerConfiguration)")
     plugins = p0.get("plugins") or {}
     multi = merge_plugin_set(DEFAULT_MULTIPOINT, plugins.get("multiPoint"))

@@ -3,13 +3,9 @@ import sys
 
 import pytest
 
-# Hardware queues per process (HIP's default is 4, read when the HIP runtime starts).  The
-# in-process split-grid tests run up to 4 contexts whose grids must all be resident at once,
-# each on its own stream; torch's stream (opened first, below) takes a queue too, and two
-# streams sharing a queue run their kernels one after the other -- a split grid's parts would
-# then wait on each other until the exchange bound.  8 queues keep every part on its own.
-if int(os.environ.get("GPU_MAX_HW_QUEUES") or 4) < 8:  # the GPU box exports HIP's default, 4
-    os.environ["GPU_MAX_HW_QUEUES"] = "8"
+# No GPU_MAX_HW_QUEUES here: the box's default (4) holds for the whole session.  The split
+# grid's parts and the service grid each get a hardware queue of their own from the library
+# (kss_split_config / the service's CU-masked stream), whatever the runtime's queue count.
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(ROOT, "kube-scheduler-simulator_amd")
@@ -39,6 +35,18 @@ def pytest_collection_modifyitems(session, config, items):
 
 
 CLEAN_HANDOFF = {"reloads": 0, "shadow": 0, "final": 0}
+
+
+@pytest.fixture(autouse=True)
+def _kss_options_reset(request):
+    """Every -m gpu test starts and ends with the library's default options (kss_set_option)."""
+    if request.node.get_closest_marker("gpu") is None:
+        yield
+        return
+    from kss import native
+    native.reset_options()
+    yield
+    native.reset_options()
 
 
 @pytest.fixture(autouse=True)

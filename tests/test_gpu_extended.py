@@ -21,7 +21,7 @@ def _run(prof, nodes, bound, pods, flags=0, kernel=None, shards=None, monkeypatc
     chosen_o, res, st = oracle_c.schedule(prof, cc.as_struct(), cp.as_struct(), cp.n, cc.n_nodes, record="meta",
                                           threads=8, n_classes=ncl, n_terms=nt)
     if shards and monkeypatch:
-        monkeypatch.setenv("KSS_SHARDS", str(shards))
+        native.set_option("shards", str(shards))
     ctx = native.Context(prof)
     ctx.load(cc.as_struct())
     chosen = ctx.schedule_batch(cp.as_struct(), cp.n, flags=flags)

@@ -137,7 +137,7 @@ def test_k_simple_100k_nodes_two_sweep_chunks():
 @pytest.mark.parametrize("shards", [65, 100])
 def test_k_simple_forced_shards_above_one_chunk(shards, monkeypatch):
     """KSS_SHARDS forces W > 64 on a 20,000-node cluster (second sweep chunk, ragged)."""
-    monkeypatch.setenv("KSS_SHARDS", str(shards))
+    native.set_option("shards", str(shards))
     prof = abi.default_profile()
     n_nodes, n_pods = 20000, 300
     s = native.Synth(2, 0, n_nodes, n_pods)
@@ -161,7 +161,7 @@ def test_c4_recipe_on_one_gpu(kernel, n_pods, monkeypatch):
     reads ~100 count rows, which fit only because the LDS slots are strided by the 391-node
     shard, not by threads x slots per lane."""
     if kernel == "k_schedule":
-        monkeypatch.setenv("KSS_NO_SPREAD", "1")
+        native.set_option("no_spread", "1")
     prof = abi.default_profile()
     n_nodes = 100000
     s = native.Synth(4, 0, n_nodes, n_pods)
@@ -184,7 +184,7 @@ def test_c4_bench_shape_many_chunks(monkeypatch):
     launch boundaries.  Chosen nodes, per-pod outcomes and the final state with the class
     counts against the C oracle."""
     n_nodes, n_pods, per_chunk = 100000, 5000, 1250
-    monkeypatch.setenv("KSS_STATIC_BYTES", str(4 * n_nodes * per_chunk))
+    native.set_option("static_bytes", str(4 * n_nodes * per_chunk))
     prof = abi.default_profile()
     s = native.Synth(4, SEED_BASE + 4, n_nodes, n_pods)
     chosen_o, res, st = _oracle(prof, s, n_pods, record="meta")
@@ -249,7 +249,7 @@ def test_c5_sweep_forced_chunks_three_reruns(monkeypatch):
     k_static chunks of 300 pods: every rerun restores all scenarios' node state with the reset
     kernel (no runtime copy) and the chunks hand node state over in HBM; three runs, each equal
     to the oracle scenario by scenario."""
-    monkeypatch.setenv("KSS_STATIC_BYTES", str(4 * 64 * 1000 * 300))
+    native.set_option("static_bytes", str(4 * 64 * 1000 * 300))
     prof = abi.default_profile()
     syn = [native.Synth(5, SEED_BASE + 5 + 7919 * k, 1000, 1000) for k in range(64)]
     sw = native.Sweep(prof, [x.cluster for x in syn], [x.pods for x in syn])
@@ -269,7 +269,7 @@ def test_sweep_odd_chunk_mixed_node_parity(monkeypatch):
     static words start at a 16-byte boundary, so k_static's paired 8-byte stores stay aligned
     (ADVICE r4); 151 pods, two runs."""
     sizes = [1001, 37, 700, 999, 3, 512, 64]
-    monkeypatch.setenv("KSS_STATIC_BYTES", str(4 * sum(sizes) * 37))
+    native.set_option("static_bytes", str(4 * sum(sizes) * 37))
     prof = abi.default_profile()
     syn = [native.Synth(2, SEED_BASE + 2 + 7919 * k, n, 151) for k, n in enumerate(sizes)]
     sw = native.Sweep(prof, [x.cluster for x in syn], [x.pods for x in syn])
@@ -313,7 +313,7 @@ def test_k_simple_custom_profile_matches_oracle(n_nodes, n_pods):
 def test_k_simple_small_static_chunks(monkeypatch):
     """KSS_STATIC_BYTES forces the static words into many chunks (one k_static + one
     k_simple launch each, node state carried in HBM): same result as one chunk."""
-    monkeypatch.setenv("KSS_STATIC_BYTES", str(4 * 3000 * 37))  # 37 pods per chunk
+    native.set_option("static_bytes", str(4 * 3000 * 37))  # 37 pods per chunk
     prof = abi.default_profile()
     n_nodes, n_pods = 3000, 400
     s = native.Synth(2, 0, n_nodes, n_pods)
@@ -326,3 +326,35 @@ def test_k_simple_small_static_chunks(monkeypatch):
     _meta_equal(ctx.fetch_meta(n_pods), res, n_pods)
     _state_equal(ctx, st, n_nodes, 0, 0)
     ctx.close()
+
+
+@pytest.mark.parametrize("config,kernel", [(2, "k_simple"), (3, "k_spread")])
+@pytest.mark.parametrize("mode", ["forced_fallback", "xcd_off"])
+def test_xcd_local_fallback_and_off(config, kernel, mode):
+    """The XCD-local grid's fallback: when XCD 0 does not get W workgroups the launch
+    fails with err 3 before touching any state and the host runs it again unrestricted.
+    forced_fallback: kss_set_option("xcd_force_fallback") makes every XCD-local launch report
+    failed placement, so the unrestricted rerun schedules the batch (counted in fallbacks);
+    xcd_off: kss_set_option("xcd", 0), no XCD-local launch at all.  Both equal the oracle."""
+    prof = abi.default_profile()
+    n_nodes, n_pods = 5000, 400
+    s = native.Synth(config, SEED_BASE + config, n_nodes, n_pods)
+    chosen_o, res, st = _oracle(prof, s, n_pods, record="meta")
+    native.set_option("xcd_force_fallback" if mode == "forced_fallback" else "xcd", 1 if mode == "forced_fallback" else 0)
+    ctx = native.Context(prof)
+    ctx.load(s.cluster)
+    ctx.stage(s.pods)
+    for rep in range(2):
+        ctx.reset()
+        chosen = ctx.run_staged(n_pods)
+        assert ctx.last_kernel() == kernel
+        xl = ctx.last_xcd_local()
+        if mode == "forced_fallback":
+            assert xl == {"used": 1, "fallbacks": 1}, xl
+        else:
+            assert xl["used"] == 0 and xl["fallbacks"] == 0, xl
+        np.testing.assert_array_equal(chosen, chosen_o, err_msg=f"run {rep}")
+        _meta_equal(ctx.fetch_meta(n_pods), res, n_pods)
+        _state_equal(ctx, st, n_nodes, s.cluster.n_classes, s.cluster.n_terms)
+    ctx.close()
+    s.close()

@@ -91,7 +91,7 @@ def test_service_matches_per_pod_api(config, n_nodes, n_pods):
 def test_general_service_matches_per_pod_api(config, n_nodes, n_pods, monkeypatch):
     """KSS_SERVICE_GENERAL=1 keeps default-profile pods on the general chain (the comparison
     the per-pod bench reports)."""
-    monkeypatch.setenv("KSS_SERVICE_GENERAL", "1")
+    native.set_option("service_general", "1")
     s = native.Synth(config, SEED_BASE + config, n_nodes, n_pods)
     assert _compare(s.cluster, s.pods, n_pods, rollback_every=5) == 0
     s.close()

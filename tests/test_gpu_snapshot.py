@@ -16,8 +16,8 @@ from kss.compile import compile_cluster
 pytestmark = pytest.mark.gpu
 
 
-def _oracle(cc, cp):
-    return oracle_c.schedule(abi.default_profile(), cc.as_struct(), cp.as_struct(), cp.n, cc.n_nodes, record="meta",
+def _oracle(cc, cp, prof=None):
+    return oracle_c.schedule(prof or abi.default_profile(), cc.as_struct(), cp.as_struct(), cp.n, cc.n_nodes, record="meta",
                              n_classes=len(cc.classes), n_terms=len(cc.terms))
 
 
@@ -55,10 +55,13 @@ def test_snapshot_json_schedules_like_objects():
     nodes, bound, pods = synth.make_cluster(3, n_nodes=500, n_pods=300)
     snap = snapshot.read_snapshot(json.dumps(synth.to_resources_for_snap(nodes, bound, pods)))
     cc, cp, _ = compile_cluster(snap.nodes, snap.bound, snap.pending, snap.namespaces)
-    ctx = native.Context(snapshot.profile_from_config(snap.scheduler_config, cc.scalars))
+    # the simulator's profile: percentageOfNodesToScore reset to 0 (adaptive: 230 of 500 nodes)
+    prof = snapshot.profile_from_config(snap.scheduler_config, cc.scalars)
+    assert prof.pct_nodes_to_score == 0
+    ctx = native.Context(prof)
     ctx.load(cc.as_struct())
     ctx.stage(cp.as_struct())
     ch = ctx.run_staged(cp.n)
     cc0, cp0, _ = compile_cluster(nodes, bound, pods)
-    np.testing.assert_array_equal(ch, _oracle(cc0, cp0)[0])
+    np.testing.assert_array_equal(ch, _oracle(cc0, cp0, prof)[0])
     ctx.close()

@@ -29,7 +29,7 @@ def _oracle(s, n_pods):
     (4, 20000, 400, 2, 32, "k_spread"),
     (3, 3000, 300, 2, 12, "k_spread"),
     (4, 100000, 200, 2, 128, "k_spread"),
-    (4, 100000, 300, 4, 64, "k_spread"),   # BASELINE configs[3] split 4 ways (4 contexts: GPU_MAX_HW_QUEUES = 4)
+    (4, 100000, 300, 4, 64, "k_spread"),   # BASELINE configs[3] split 4 ways (4 contexts, each on a queue of its own)
     (2, 100000, 300, 4, 32, "k_simple"),
 ])
 def test_in_process_parts_match_oracle(config, n_nodes, n_pods, n_parts, wl, kernel):
@@ -68,7 +68,7 @@ def test_parts_over_many_chunks(monkeypatch, config, n_nodes, n_pods, per_chunk,
     chunks exchange through the two inbox halves, so a part that starts chunk c + 1 never
     overwrites a granule of chunk c that its peer is still polling.  Three runs back to back
     (the chunk sequence continues across runs)."""
-    monkeypatch.setenv("KSS_STATIC_BYTES", str(4 * n_nodes * per_chunk))
+    native.set_option("static_bytes", str(4 * n_nodes * per_chunk))
     s = native.Synth(config, SEED_BASE + config, n_nodes, n_pods)
     ch_o, res, st = _oracle(s, n_pods)
     sp = split.InProcessSplit(s.cluster, s.pods, 2, wl)
@@ -287,3 +287,45 @@ def test_processes_through_ipc_handles(world, config, n_nodes, n_pods, wl, two_g
         np.testing.assert_array_equal(np.array(chosen), ch_o, err_msg=f"rank {rank}")
         np.testing.assert_array_equal(np.array(req, dtype=np.int64).reshape(abi.KSS_NRES, hi - lo),
                                       st["requested"][:, lo:hi], err_msg=f"rank {rank}")
+
+
+def _few_queues_main(queues, config, n_nodes, n_pods, n_parts, wl, q):
+    os.environ["GPU_MAX_HW_QUEUES"] = str(queues)  # before this child's HIP runtimes start
+    try:
+        import torch
+        torch.zeros(1, device="cuda")
+        s = native.Synth(config, SEED_BASE + config, n_nodes, n_pods)
+        sp = split.InProcessSplit(s.cluster, s.pods, n_parts, wl)
+        outs = []
+        for _ in range(2):
+            sp.reset()
+            outs.append([ch.tolist() for ch in sp.run(n_pods)])
+        st = [c.last_handoff_status() for c in sp.ctxs]
+        sp.close()
+        q.put((outs, st, None))
+    except Exception as e:  # noqa: BLE001 - reported to the parent
+        q.put((None, None, repr(e)))
+
+
+@pytest.mark.parametrize("queues", [1, 4])
+def test_parts_on_few_hardware_queues(queues):
+    """The r5d failure's configuration: 4 in-process parts at or below the runtime's
+    hardware-queue count (4 is the box's default; 1 shares every plain stream).  Plain streams
+    on a shared queue run their kernels one after the other, so the parts would wait out the
+    exchange bound; kss_split_config gives each part a queue of its own, and every part equals
+    the oracle, twice, with clean hand-offs."""
+    import multiprocessing as mp
+    config, n_nodes, n_pods, n_parts, wl = 4, 20000, 200, 4, 16
+    s = native.Synth(config, SEED_BASE + config, n_nodes, n_pods)
+    ch_o, _, _ = _oracle(s, n_pods)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_few_queues_main, args=(queues, config, n_nodes, n_pods, n_parts, wl, q))
+    p.start()
+    outs, st, err = q.get(timeout=100)
+    p.join(timeout=30)
+    assert err is None, err
+    for rep, run in enumerate(outs):
+        for part, ch in enumerate(run):
+            np.testing.assert_array_equal(np.array(ch), ch_o, err_msg=f"part {part} run {rep}")
+    assert all(x == {"reloads": 0, "shadow": 0, "final": 0} for x in st), st

@@ -79,7 +79,7 @@ def test_program_fuzz_matches_oracle(seed, n_nodes, n_pods, mode):
 
 def test_program_fuzz_many_seeds_forced_shards(monkeypatch):
     """Twelve more seeds at 9 shards (ragged last shard)."""
-    monkeypatch.setenv("KSS_SHARDS", "9")
+    native.set_option("shards", "9")
     prof = abi.default_profile()
     for seed in range(20, 32):
         cc, cp = _fuzz(seed, 211, 150)
@@ -100,9 +100,9 @@ def test_statistics_fold_matches_oracle(fold, shards, monkeypatch):
     without KSS_FOLD (the default), the separate exchange: the fuzz mixes pods that fold (histogram-valued
     DoNotSchedule groups, inter-pod histograms and flags) with pods that cannot (node-valued
     DoNotSchedule groups) and unschedulable pods that run no argmax, so both paths alternate."""
-    monkeypatch.setenv("KSS_SHARDS", str(shards))
+    native.set_option("shards", str(shards))
     if fold:
-        monkeypatch.setenv("KSS_FOLD", "1")
+        native.set_option("fold", "1")
     prof = abi.default_profile()
     on_spread = 0
     for seed in (20, 21, 22, 51):
@@ -117,7 +117,7 @@ def test_statistics_fold_matches_oracle(fold, shards, monkeypatch):
         _check(ctx, res, st, chosen, chosen_o, cp.n, cc.n_nodes, ncl, nt)
         ctx.close()
     assert on_spread >= 3
-    monkeypatch.delenv("KSS_SHARDS")  # the automatic geometry (3,000 nodes do not fit 2 shards' LDS)
+    native.set_option("shards", 0)  # the automatic geometry (3,000 nodes do not fit 2 shards' LDS)
     s = native.Synth(3, 7, 3000, 250)  # the C3 recipe: zone DoNotSchedule, inter-pod entries
     chosen_o, res, st = _oracle(prof, s.cluster, s.pods, 250, 3000, s.cluster.n_classes, s.cluster.n_terms)
     ctx = native.Context(prof)
@@ -133,7 +133,7 @@ def test_k_spread_static_chunks(monkeypatch):
     """KSS_STATIC_BYTES forces one k_static + one k_spread launch per 23 pods: the commits of
     every launch reach HBM (node rows and count rows) before the next one reads them."""
     s = native.Synth(3, 0, 2000, 300)
-    monkeypatch.setenv("KSS_STATIC_BYTES", str(4 * 2000 * 23))
+    native.set_option("static_bytes", str(4 * 2000 * 23))
     prof = abi.default_profile()
     chosen_o, res, st = _oracle(prof, s.cluster, s.pods, 300, 2000, s.cluster.n_classes, s.cluster.n_terms)
     ctx = native.Context(prof)

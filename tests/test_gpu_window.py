@@ -4,7 +4,9 @@ C oracle -- chosen nodes, per-pod outcomes, every per-node record (the unvisited
 that ended the search, scores over the kept nodes), the final node state and the cursor --
 through every entry point that runs a scheduling cycle: recorded and unrecorded batches (one
 and several workgroups), staged runs continued across launches, the per-pod API, the service
-grid and scenario sweeps.  (The loop kernels refuse the window: tests/test_plan.py.)"""
+grid and scenario sweeps.  Staged default-profile batches run the window on k_simple
+(simple_sync_win: per-wave and per-thread modes, one and several shards, XCD-local or not,
+several chunk launches handing the cursor on); k_spread refuses it (tests/test_plan.py)."""
 import os
 
 import numpy as np
@@ -82,10 +84,12 @@ def test_c2_window_records(pct, flags):
     ctx.close()
 
 
+@pytest.mark.parametrize("kernel", ["k_simple", "k_schedule"])
 @pytest.mark.parametrize("pct", [0, 30])
-def test_c2_full_batch_window(pct):
-    """The whole C2 batch (5,000 nodes x 10,000 pods) unrecorded and staged: chosen nodes,
-    outcomes, the final node state and nextStartNodeIndex."""
+def test_c2_full_batch_window(pct, kernel):
+    """The whole C2 batch (5,000 nodes x 10,000 pods) unrecorded and staged, on k_simple's window
+    (the default route) and forced onto k_schedule: chosen nodes, outcomes, the final node state
+    and nextStartNodeIndex."""
     n_nodes, n_pods = 5000, 10000
     prof = _prof(pct)
     s = native.Synth(2, SEED_BASE + 2, n_nodes, n_pods)
@@ -93,14 +97,77 @@ def test_c2_full_batch_window(pct):
     ctx = native.Context(prof)
     ctx.load(s.cluster)
     ctx.stage(s.pods)
-    chosen = ctx.run_staged(n_pods)
-    assert ctx.last_kernel() == "k_schedule"
+    chosen = ctx.run_staged(n_pods, flags=abi.KSS_SCHED_GENERAL_KERNEL if kernel == "k_schedule" else 0)
+    assert ctx.last_kernel() == kernel
     np.testing.assert_array_equal(chosen, ch_o)
     _meta_equal(ctx.fetch_meta(n_pods), res, n_pods)
     assert ctx.next_start_node_index() == st["next_start"]
     g = ctx.node_state()
     np.testing.assert_array_equal(g["requested"][:, :n_nodes], st["requested"][:, :n_nodes])
     np.testing.assert_array_equal(g["pod_count"][:n_nodes], st["pod_count"][:n_nodes])
+    ctx.close()
+
+
+@pytest.mark.parametrize("geometry", ["xcd_local", "unrestricted", "one_shard", "three_shards", "chunks"])
+@pytest.mark.parametrize("pct", [0, 12])
+def test_k_simple_window_geometries(pct, geometry):
+    """k_simple's window (simple_sync_win) in each of its shapes against the C oracle: the XCD-local
+    grid (32 shards, per-wave mode), the unrestricted one (40 shards), one shard (no exchange, the
+    cut ranked locally, per-thread mode), three shards of 1,667 nodes (per-thread mode), and several
+    chunk launches (KSS static budget: 7 launches hand nextStartNodeIndex on through the device
+    word).  The batch starts at a set cursor; two runs."""
+    n_nodes, n_pods = 5000, 1500
+    prof = _prof(pct)
+    s = native.Synth(2, SEED_BASE + 2, n_nodes, n_pods)
+    ch_o, res, st = _oracle(prof, s.cluster, s.pods, n_pods, n_nodes, record="meta", cursor=4321)
+    if geometry == "unrestricted":
+        native.set_option("xcd", 0)
+    elif geometry == "one_shard":
+        native.set_option("shards", 1)
+    elif geometry == "three_shards":
+        native.set_option("shards", 3)
+    elif geometry == "chunks":
+        native.set_option("static_bytes", 4 * n_nodes * 220)
+    ctx = native.Context(prof)
+    ctx.load(s.cluster)
+    ctx.stage(s.pods)
+    for rep in range(2):
+        ctx.reset()
+        ctx.set_next_start_node_index(4321)
+        chosen = ctx.run_staged(n_pods)
+        assert ctx.last_kernel() == "k_simple"
+        want_shards = {"xcd_local": 32, "unrestricted": 40, "one_shard": 1, "three_shards": 3}.get(geometry)
+        if want_shards:
+            assert ctx.last_geometry()["shards"] == want_shards, ctx.last_geometry()
+        if geometry == "chunks":
+            assert ctx.last_timing()[1] >= 2 * 7
+        np.testing.assert_array_equal(chosen, ch_o, err_msg=f"run {rep}")
+        _meta_equal(ctx.fetch_meta(n_pods), res, n_pods)
+        assert ctx.next_start_node_index() == st["next_start"]
+        g = ctx.node_state()
+        np.testing.assert_array_equal(g["requested"][:, :n_nodes], st["requested"][:, :n_nodes])
+    ctx.close()
+
+
+@pytest.mark.parametrize("n_nodes", [101, 180, 700])
+def test_k_simple_window_small_and_saturating(n_nodes):
+    """Window edges on k_simple: K = 100 of 101 / 180 nodes, and a cluster the batch saturates (pods
+    become unschedulable, F <= K: every node visited, the cursor stays) -- chosen nodes, outcomes and
+    the cursor against the oracle."""
+    n_pods = 2500 if n_nodes == 700 else 400
+    prof = _prof(0)
+    s = native.Synth(1, SEED_BASE + 1, n_nodes, n_pods)
+    ch_o, res, st = _oracle(prof, s.cluster, s.pods, n_pods, n_nodes, record="meta")
+    ctx = native.Context(prof)
+    ctx.load(s.cluster)
+    ctx.stage(s.pods)
+    chosen = ctx.run_staged(n_pods)
+    assert ctx.last_kernel() == "k_simple"
+    np.testing.assert_array_equal(chosen, ch_o)
+    _meta_equal(ctx.fetch_meta(n_pods), res, n_pods)
+    assert ctx.next_start_node_index() == st["next_start"]
+    if n_nodes == 700:
+        assert (ch_o < 0).any()  # the batch saturates the cluster
     ctx.close()
 
 

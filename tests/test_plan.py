@@ -48,16 +48,34 @@ def test_refusal_names_pod_and_reason():
 
 
 def test_profile_aware_plan():
-    """kss_plan_podset_ex: the profile rules out both loop kernels when percentageOfNodesToScore
-    is below 100 (the window runs on k_schedule), or when it scores an extended resource that
-    the cluster has; otherwise it answers as kss_plan_podset."""
+    """kss_plan_podset_ex: percentageOfNodesToScore below 100 on 100+ nodes (the window) keeps
+    k_simple for pods without a PreFilterResult list (simple_sync_win) and rules out k_spread and
+    name-listed pods; a profile that scores an extended resource the cluster has rules out both
+    loop kernels; otherwise it answers as kss_plan_podset."""
     s = native.Synth(2, 0, 500, 50)
     assert native.plan_podset(s.cluster, s.pods)["kernel"] == "k_simple"
     for pct in (0, 30, 99):
         p = abi.default_profile()
         p.pct_nodes_to_score = pct
-        r = native.plan_podset(s.cluster, s.pods, p)
-        assert r["kernel"] == "k_schedule" and "percentageOfNodesToScore" in r["reason"], r
+        assert native.plan_podset(s.cluster, s.pods, p)["kernel"] == "k_simple"
+    small = native.Synth(2, 0, 99, 20)  # fewer than 100 nodes: no window at all
+    p = abi.default_profile()
+    p.pct_nodes_to_score = 0
+    assert native.plan_podset(small.cluster, small.pods, p)["kernel"] == "k_simple"
+    # programs (k_spread) and PreFilterResult node lists keep the window on k_schedule
+    from kss import synth
+    from test_oracle_crosscheck import with_name_sets
+    nodes, bound, pods = synth.make_cluster(3, 300, 40)
+    cc, cp, _ = compile_cluster(nodes, bound, pods)
+    assert native.plan_podset(cc.as_struct(), cp.as_struct())["kernel"] == "k_spread"
+    r = native.plan_podset(cc.as_struct(), cp.as_struct(), p)
+    assert r["kernel"] == "k_schedule" and "percentageOfNodesToScore" in r["reason"], r
+    nodes, bound, pods = synth.make_cluster(2, 300, 40)
+    pods = with_name_sets(pods, [n["metadata"]["name"] for n in nodes], every=5, size=120)
+    cc, cp, _ = compile_cluster(nodes, bound, pods)
+    assert native.plan_podset(cc.as_struct(), cp.as_struct())["kernel"] == "k_simple"
+    r = native.plan_podset(cc.as_struct(), cp.as_struct(), p)
+    assert r["kernel"] == "k_schedule" and "PreFilterResult" in r["reason"], r
     assert native.plan_podset(s.cluster, s.pods, abi.default_profile())["kernel"] == "k_simple"
     nodes, bound, pods = progfuzz.make(2, 60, 200, n_extended=2, programs=False)
     cc, cp, _ = compile_cluster(nodes, bound, pods)

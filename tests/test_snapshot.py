@@ -40,10 +40,12 @@ def test_priority_class_resolution():
 
 
 def test_default_config_is_the_default_profile():
-    assert _same_profile(snapshot.profile_from_config(None), abi.default_profile())
     d = abi.default_profile()
-    d.pct_nodes_to_score = 0  # a configuration without the field: the v1 default, adaptive
+    d.pct_nodes_to_score = 0  # the simulator's scheduler always runs with the v1 default: adaptive
+    assert _same_profile(snapshot.profile_from_config(None), d)
     assert _same_profile(snapshot.profile_from_config({"profiles": [{"schedulerName": "default-scheduler"}]}), d)
+    # the north_star / bench workloads opt in to scoring every node
+    assert _same_profile(snapshot.profile_from_config(None, pct_nodes_to_score=100), abi.default_profile())
 
 
 def test_config_weights_disables_and_args():
@@ -94,9 +96,15 @@ def test_config_star_disable_and_refusals():
     assert p.filter_enabled == (1 << abi.KSS_F_NODE_RESOURCES_FIT) | (1 << abi.KSS_F_TAINT_TOLERATION)
     assert p.score_enabled == (1 << abi.KSS_S_NODE_RESOURCES_FIT) | (1 << abi.KSS_S_TAINT_TOLERATION)
     assert p.weight[abi.KSS_S_TAINT_TOLERATION] == 7 and p.weight[abi.KSS_S_NODE_RESOURCES_FIT] == 1
-    assert snapshot.profile_from_config({"percentageOfNodesToScore": 50, "profiles": [{}]}).pct_nodes_to_score == 50
-    assert snapshot.profile_from_config({"profiles": [{}]}).pct_nodes_to_score == 0  # the v1 default: adaptive
-    assert snapshot.profile_from_config(None).pct_nodes_to_score == 100  # no configuration: the north_star profile
+    # filterOutNonAllowedChangesOnCfg (simulator/scheduler/scheduler.go:258-275) resets the field
+    # to the v1 default 0 whatever the configuration says; 100 only by an explicit opt-in
+    assert snapshot.profile_from_config({"percentageOfNodesToScore": 50, "profiles": [{}]}).pct_nodes_to_score == 0
+    assert snapshot.profile_from_config({"percentageOfNodesToScore": 100, "profiles": [{}]}).pct_nodes_to_score == 0
+    assert snapshot.profile_from_config({"profiles": [{}]}).pct_nodes_to_score == 0
+    assert snapshot.profile_from_config(None).pct_nodes_to_score == 0
+    assert snapshot.profile_from_config({"profiles": [{}]}, pct_nodes_to_score=30).pct_nodes_to_score == 30
+    with pytest.raises(Unsupported):
+        snapshot.profile_from_config(None, pct_nodes_to_score=-1)
     with pytest.raises(Unsupported):
         snapshot.profile_from_config({"percentageOfNodesToScore": 101, "profiles": [{}]})
     with pytest.raises(Unsupported):

@@ -21,11 +21,8 @@ def main():
     n_nodes = DEFAULT_SIZES[cfg][0]
     for w in [int(x) for x in sys.argv[2:]] or [0]:
         path = os.path.join(tempfile.mkdtemp(prefix="kss_stamps_"), "stamps.bin")
-        os.environ["KSS_STAMPS_FILE"] = path
-        if w:
-            os.environ["KSS_SHARDS"] = str(w)
-        else:
-            os.environ.pop("KSS_SHARDS", None)
+        native.set_stamps_file(path)
+        native.set_option("shards", w)
         s = native.Synth(cfg, SEED_BASE + cfg, n_nodes, 1000)
         ctx = native.Context(abi.default_profile(), device=0)
         ctx.load(s.cluster)
