@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define KSS_ABI_VERSION 4
+#define KSS_ABI_VERSION 5
 
 /* ---- error codes ------------------------------------------------------- */
 #define KSS_OK 0
@@ -108,6 +108,9 @@ enum kss_filter_plugin {
  * NodeVolumeLimits / AzureDiskLimits: "node(s) exceed max volume count" (detail 0) */
 #define KSS_VB_NODE_CONFLICT 0 /* VolumeBinding: "node(s) had volume node affinity conflict" */
 #define KSS_VB_PV_NOT_EXIST 1  /* "node(s) unavailable due to one or more pvc(s) bound to non-existent pv(s)" */
+#define KSS_VB_BIND_CONFLICT 2 /* "node(s) didn't find available persistent volumes to bind" */
+#define KSS_VB_NODE_BIND 3     /* node conflict, then bind conflict (the reasons joined with ", ") */
+#define KSS_VB_BIND_PV_NOT_EXIST 4 /* bind conflict, then PV not exist */
 /* VolumeZone: detail 0 = "node(s) had no available volume zone", 1 + i = kss_names.messages[i] */
 
 /* ---- score plugins, in default MultiPoint order ------------------------- */
@@ -203,6 +206,18 @@ typedef struct kss_cluster {
   const int32_t* vol_limit;      /* [n_vol_keys][n_nodes] */
   const int32_t* vol_row_key;    /* [n_vol_rows] key the row's volume counts under, -1 (disk usage rows) */
   const int32_t* vol_key_plugin; /* [n_vol_keys] KSS_F_EBS_LIMITS / _GCEPD_ / _NODE_VOLUME_ / _AZURE_DISK_LIMITS */
+  /* VolumeBinding for unbound WaitForFirstConsumer claims (binder.go FindPodVolumes): the
+   * binder's assume cache as two mutable columns.  A candidate PV is one some pending pod's
+   * delayed claim may bind (KSS_VOL_BIND_WFFC lists); a delayed claim is an unbound claim of a
+   * WaitForFirstConsumer class some pending pod uses.
+   *   pv_owner[v]   0: available; c + 1: bound to delayed claim c (spec.claimRef in the
+   *                 snapshot, or AssumePodVolumes' static binding)
+   *   claim_node[c] the claim's volume.kubernetes.io/selected-node: -1 none, -2 a node outside
+   *                 the snapshot, else the node's canonical index (AssumePodVolumes' provisioning) */
+  int32_t n_pvs;
+  int32_t n_wclaims;
+  const int32_t* pv_owner;   /* [n_pvs] (mutable) */
+  const int32_t* claim_node; /* [n_wclaims] (mutable) */
 } kss_cluster;
 
 /* ---- pod programs --------------------------------------------------------
@@ -285,8 +300,20 @@ enum kss_vol_kind {
   KSS_VOL_ZONE = 4,           /* VolumeZone on zone-labelled nodes: requirements [a, a + b) (AND) */
   KSS_VOL_ZONE_ERROR = 5,     /* VolumeZone on zone-labelled nodes: the status message kss_names.messages[a] */
   KSS_VOL_OWN = 6,            /* AssumePod: vol_count[row][n] += 1 (0 -> 1 also adds 1 to the row's key) */
-  KSS_VOL_OWN_PRIVATE = 7     /* AssumePod: vol_attached[key][n] += count */
+  KSS_VOL_OWN_PRIVATE = 7,    /* AssumePod: vol_attached[key][n] += count */
+  KSS_VOL_BIND_WFFC = 8       /* VolumeBinding delayed claim `key` (an unbound WaitForFirstConsumer claim), after the
+                                 pod's BIND_AFFINITY / BIND_PV_MISSING entries, in increasing storage request (stable):
+                                 candidate PVs ints[a .. a + 3b) as {pv, term_off, term_len} triplets in increasing
+                                 capacity, then name (term_len -1: no required node affinity; else its terms, OR, over
+                                 the node's labels); count bit 0: its class can provision (a provisioner other than
+                                 kubernetes.io/no-provisioner), count >> 1: the class's allowedTopologies as terms
+                                 [row, row + (count >> 1)) (0: any node).  FindMatchingVolume: a PV with pv_owner ==
+                                 key + 1 is the claim's (its node affinity decides), else the first available one not
+                                 chosen by an earlier claim whose affinity matches; a claim with a selected node, or
+                                 without a match, is provisioned (checkVolumeProvisions).  AssumePod (Reserve's
+                                 AssumePodVolumes) sets pv_owner / claim_node on the chosen node. */
 };
+#define KSS_MAX_WFFC 4 /* delayed claims per pod */
 typedef struct kss_vol {
   int32_t kind;
   int32_t key;
@@ -465,6 +492,11 @@ int kss_read_volume_state(kss_ctx* ctx, int32_t* vol_count /*[n_vol_rows][N] or 
                           int32_t* vol_attached /*[n_vol_keys][N] or NULL*/);
 int kss_apply_volume_delta(kss_ctx* ctx, const int32_t* node, const int32_t* row, const int32_t* value, int32_t n,
                            int32_t mode);
+/* The binder's assume cache (kss_cluster pv_owner / claim_node) read back: what AssumePodVolumes
+ * (batch commits, kss_commit) and RevertAssumedPodVolumes (kss_rollback) left.  Replaces the
+ * volumebinding plugin's pvCache / pvcCache (binder.go AssumePodVolumes, simulator
+ * scheduler's default VolumeBinding, plugin_test.go:28). */
+int kss_read_binding_state(kss_ctx* ctx, int32_t* pv_owner /*[n_pvs] or NULL*/, int32_t* claim_node /*[n_wclaims] or NULL*/);
 /* read back the mutable columns (requested [KSS_NRES][N], nonzero [2][N], pod_count [N]) */
 int kss_read_node_state(kss_ctx* ctx, int64_t* requested, int64_t* nonzero, int32_t* pod_count,
                         int32_t* class_count /*[n_classes][N] or NULL*/, int32_t* term_count /*or NULL*/);

@@ -70,6 +70,13 @@ struct DevCluster {
   const int32_t* vol_limit;
   const int32_t* vol_row_key;
   const int32_t* vol_key_plugin;
+  // the binder's assume cache for WaitForFirstConsumer claims (kss_cluster pv_owner / claim_node):
+  // mutable, with the snapshot's values beside them (ForgetPod restores those)
+  int32_t n_pvs, n_wclaims;
+  int32_t* pv_owner;
+  int32_t* claim_node;
+  const int32_t* pv_owner0;
+  const int32_t* claim_node0;
   // Shard-resident LDS copies of the hot node columns (set inside the kernel; null on
   // the host and in kernels without a cache).  Slot i holds node nc_lo + i.
   int64_t* nc64;    // [8][nc_cap]: alloc cpu/mem/eph, requested cpu/mem/eph, nonzero cpu/mem
@@ -379,6 +386,155 @@ __device__ __forceinline__ int limit_exceeded(const DevCluster& c, int key, int 
   return (int64_t)c.vol_attached[(size_t)key * N + n] + newc > (int64_t)lim ? pl : 0;
 }
 
+__device__ __forceinline__ bool vb_kind(int k) {
+  return k == KSS_VOL_BIND_AFFINITY || k == KSS_VOL_BIND_PV_MISSING || k == KSS_VOL_BIND_WFFC;
+}
+
+// pv_helpers.go FindMatchingVolume for delayed claim entry v on node n (candidates: ints[v.a ..],
+// {pv, term_off, term_len} triplets in increasing capacity, then name): a PV bound to the claim
+// (pv_owner == key + 1: its claimRef, or assumed by AssumePodVolumes) and not chosen by an earlier
+// claim of the pod (chosen[0 .. nch): excludedVolumes; a pod can list one claim twice) is returned
+// -- or nothing, when its node affinity fails -- wherever it comes; else the first available PV not
+// chosen whose node affinity matches.  -1: no match.
+template <class Lab>
+__device__ __forceinline__ int wffc_match(const DevCluster& c, const kss_req* reqs, const kss_term* terms,
+                                          const int32_t* ints, const kss_vol& v, const int (&chosen)[KSS_MAX_WFFC],
+                                          int nch, Lab lab) {
+  auto node_ok = [&](int i) {  // volumeutil.CheckNodeAffinity(pv, node.Labels)
+    const int ta = ints[v.a + 3 * i + 1], tb = ints[v.a + 3 * i + 2];
+    if (tb < 0) return true;
+    bool ok = false;
+    for (int t = 0; t < tb && !ok; t++) ok = term_match_t(c, reqs, ints, terms[ta + t], -1, lab);
+    return ok;
+  };
+  for (int i = 0; i < v.b; i++) {  // excludedVolumes come first: a PV an earlier claim took is skipped
+    const int pv = ints[v.a + 3 * i];
+    bool taken = false;
+    for (int k = 0; k < KSS_MAX_WFFC; k++) taken |= k < nch && chosen[k] == pv;
+    if (!taken && c.pv_owner[pv] == v.key + 1) return node_ok(i) ? pv : -1;
+  }
+  for (int i = 0; i < v.b; i++) {
+    const int pv = ints[v.a + 3 * i];
+    if (c.pv_owner[pv] != 0) continue;
+    bool taken = false;
+    for (int k = 0; k < KSS_MAX_WFFC; k++) taken |= k < nch && chosen[k] == pv;
+    if (taken || !node_ok(i)) continue;
+    return pv;
+  }
+  return -1;
+}
+
+// VolumeBinding.Filter -> binder.go FindPodVolumes on node n over the pod's VolumeBinding
+// entries [e0, e1): checkBoundClaims (BIND_AFFINITY / BIND_PV_MISSING in claim order, the first
+// failure ends it), then the delayed claims (BIND_WFFC): a claim selected for another node fails
+// at once; findMatchingVolumes over the others; checkVolumeProvisions over the selected and the
+// unmatched ones.  Returns -1 when satisfied, else the KSS_VB_* detail (the reasons in
+// FindPodVolumes' order: node conflict, bind conflict, PV not exist).  pick (optional): per
+// BIND_WFFC entry in order, the statically bound PV, or -1 for a provisioned claim
+// (AssumePodVolumes' podVolumes).
+template <class Lab>
+__device__ __forceinline__ int vb_eval(const DevCluster& c, const kss_req* reqs, const kss_term* terms,
+                                       const int32_t* ints, const kss_vol* vols, int e0, int e1, int n, Lab lab,
+                                       int* pick = nullptr) {
+  int bound = 0;  // 1 node conflict, 2 a bound claim's PV does not exist
+  for (int e = e0; e < e1 && bound == 0; e++) {
+    const kss_vol& v = vols[e];
+    if (v.kind == KSS_VOL_BIND_PV_MISSING) {
+      bound = 2;
+    } else if (v.kind == KSS_VOL_BIND_AFFINITY) {
+      bool ok = false;
+      for (int t = 0; t < v.b && !ok; t++) ok = term_match_t(c, reqs, ints, terms[v.a + t], -1, lab);
+      if (!ok) bound = 1;
+    }
+  }
+  bool unbound_ok = true;
+  for (int e = e0; e < e1 && unbound_ok; e++)  // the selected-node fast path
+    if (vols[e].kind == KSS_VOL_BIND_WFFC) {
+      const int sel = c.claim_node[vols[e].key];
+      if (sel != -1 && sel != n) unbound_ok = false;
+    }
+  if (unbound_ok) {
+    int chosen[KSS_MAX_WFFC] = {-1, -1, -1, -1};
+    int nch = 0, wi = 0;
+    unsigned prov = 0;  // the claims to provision: selected for this node, or without a match
+    for (int e = e0; e < e1; e++) {
+      const kss_vol& v = vols[e];
+      if (v.kind != KSS_VOL_BIND_WFFC) continue;
+      int m = -1;
+      if (c.claim_node[v.key] == -1) {
+        m = wffc_match(c, reqs, terms, ints, v, chosen, nch, lab);
+        if (m >= 0 && nch < KSS_MAX_WFFC) chosen[nch++] = m;
+        if (m < 0) unbound_ok = false;  // foundMatches false: the provisioning check decides below
+      }
+      if (m < 0) prov |= 1u << wi;
+      if (pick && wi < KSS_MAX_WFFC) pick[wi] = m;
+      wi++;
+    }
+    if (prov) {  // checkVolumeProvisions: a provisioner, and the class's allowedTopologies admit the node
+      unbound_ok = true;
+      wi = 0;
+      for (int e = e0; e < e1 && unbound_ok; e++) {
+        const kss_vol& v = vols[e];
+        if (v.kind != KSS_VOL_BIND_WFFC) continue;
+        if ((prov >> wi) & 1u) {
+          if (!(v.count & 1)) {
+            unbound_ok = false;
+          } else if ((v.count >> 1) > 0) {
+            bool ok = false;
+            for (int t = 0; t < (v.count >> 1) && !ok; t++) ok = term_match_t(c, reqs, ints, terms[v.row + t], -1, lab);
+            unbound_ok = ok;
+          }
+        }
+        wi++;
+      }
+    }
+  }
+  if (!unbound_ok) return bound == 1 ? KSS_VB_NODE_BIND : (bound == 2 ? KSS_VB_BIND_PV_NOT_EXIST : KSS_VB_BIND_CONFLICT);
+  return bound == 1 ? KSS_VB_NODE_CONFLICT : (bound == 2 ? KSS_VB_PV_NOT_EXIST : -1);
+}
+
+// Reserve's AssumePodVolumes (sign 1) on node `local`: the static bindings' PVs become the claims'
+// (pv_owner), the provisioned claims select the node (claim_node); Unreserve's
+// RevertAssumedPodVolumes (sign -1): the claims' PVs and the claims back to the snapshot's values.
+// Every shard of a grid runs it with the same result (the columns are global, not per node).
+template <class Lab>
+__device__ __forceinline__ void wffc_commit(const DevCluster& c, const kss_req* reqs, const kss_term* terms,
+                                            const int32_t* ints, const kss_vol* vols, const kss_pod& p, int local,
+                                            int sign, Lab lab) {
+  int e0 = -1, e1 = -1;
+  for (int e = 0; e < p.vol_len; e++)
+    if (vb_kind(vols[p.vol_off + e].kind)) {
+      if (e0 < 0) e0 = p.vol_off + e;
+      e1 = p.vol_off + e + 1;
+    }
+  if (e0 < 0) return;
+  bool any = false;
+  for (int e = e0; e < e1; e++) any |= vols[e].kind == KSS_VOL_BIND_WFFC;
+  if (!any) return;
+  if (sign > 0) {
+    int pick[KSS_MAX_WFFC] = {-1, -1, -1, -1};
+    vb_eval(c, reqs, terms, ints, vols, e0, e1, local, lab, pick);
+    int wi = 0;
+    for (int e = e0; e < e1; e++) {
+      const kss_vol& v = vols[e];
+      if (v.kind != KSS_VOL_BIND_WFFC) continue;
+      if (wi < KSS_MAX_WFFC && pick[wi] >= 0) c.pv_owner[pick[wi]] = v.key + 1;
+      else c.claim_node[v.key] = local;
+      wi++;
+    }
+  } else {
+    for (int e = e0; e < e1; e++) {
+      const kss_vol& v = vols[e];
+      if (v.kind != KSS_VOL_BIND_WFFC) continue;
+      for (int i = 0; i < v.b; i++) {
+        const int pv = ints[v.a + 3 * i];
+        if (c.pv_owner[pv] == v.key + 1) c.pv_owner[pv] = c.pv_owner0[pv];
+      }
+      c.claim_node[v.key] = c.claim_node0[v.key];
+    }
+  }
+}
+
 template <class Lab>
 __device__ __forceinline__ int filter_volumes_t(const DevCluster& c, const kss_req* reqs, const kss_term* terms,
                                                 const int32_t* ints, const kss_vol* vols, const kss_pod& p,
@@ -408,21 +564,20 @@ __device__ __forceinline__ int filter_volumes_t(const DevCluster& c, const kss_r
         newc += v.row >= 0 ? (c.vol_count[(size_t)v.row * N + n] == 0 ? 1 : 0) : v.count;
         break;
       case KSS_VOL_BIND_AFFINITY:
+      case KSS_VOL_BIND_PV_MISSING:
+      case KSS_VOL_BIND_WFFC: {  // VolumeBinding: its entries (consecutive) as one FindPodVolumes
+        int e1 = e + 1;
+        while (e1 < p.vol_len && vb_kind(vols[p.vol_off + e1].kind)) e1++;
         if ((enabled >> KSS_F_VOLUME_BINDING) & 1u) {
-          bool ok = false;
-          for (int t = 0; t < v.b && !ok; t++) ok = term_match_t(c, reqs, ints, terms[v.a + t], -1, lab);
-          if (!ok) {
-            *detail = KSS_VB_NODE_CONFLICT;
+          const int d = vb_eval(c, reqs, terms, ints, vols, p.vol_off + e, p.vol_off + e1, n, lab);
+          if (d >= 0) {
+            *detail = (uint16_t)d;
             return KSS_F_VOLUME_BINDING;
           }
         }
+        e = e1 - 1;
         break;
-      case KSS_VOL_BIND_PV_MISSING:
-        if ((enabled >> KSS_F_VOLUME_BINDING) & 1u) {
-          *detail = KSS_VB_PV_NOT_EXIST;
-          return KSS_F_VOLUME_BINDING;
-        }
-        break;
+      }
       case KSS_VOL_ZONE:
         if (((enabled >> KSS_F_VOLUME_ZONE) & 1u) && (node_flags & KSS_NODE_VOLUME_ZONE)) {
           for (int k = 0; k < v.b; k++)

@@ -184,9 +184,23 @@ std::string fail_message(const kss_host_names* nm, int plugin, unsigned detail) 
     case KSS_F_NODE_VOLUME_LIMITS:
     case KSS_F_AZURE_DISK_LIMITS:
       return "node(s) exceed max volume count";
-    case KSS_F_VOLUME_BINDING:
-      return detail == KSS_VB_PV_NOT_EXIST ? "node(s) unavailable due to one or more pvc(s) bound to non-existent pv(s)"
-                                           : "node(s) had volume node affinity conflict";
+    case KSS_F_VOLUME_BINDING: {  // FindPodVolumes' reasons, joined by Status.Message()
+      static const char* const kNode = "node(s) had volume node affinity conflict";
+      static const char* const kBind = "node(s) didn't find available persistent volumes to bind";
+      static const char* const kNoPV = "node(s) unavailable due to one or more pvc(s) bound to non-existent pv(s)";
+      switch (detail) {
+        case KSS_VB_PV_NOT_EXIST:
+          return kNoPV;
+        case KSS_VB_BIND_CONFLICT:
+          return kBind;
+        case KSS_VB_NODE_BIND:
+          return std::string(kNode) + ", " + kBind;
+        case KSS_VB_BIND_PV_NOT_EXIST:
+          return std::string(kBind) + ", " + kNoPV;
+        default:
+          return kNode;
+      }
+    }
     case KSS_F_VOLUME_ZONE:
       if (detail == 0) return "node(s) had no available volume zone";
       return detail - 1 < nm->message.size() ? nm->message[detail - 1] : std::string();

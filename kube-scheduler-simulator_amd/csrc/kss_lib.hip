@@ -273,6 +273,11 @@ __global__ __launch_bounds__(KSS_MAX_THREADS) void k_schedule(const DevJob* __re
       }
       const int local = m.chosen - c.node_base;
       if (job.commit && m.chosen >= 0 && local >= S.lo && local < S.hi) commit_pod(c, job.P, job.P.pods[pi], local, 1);
+      // the binder's assume cache is global: every shard applies AssumePodVolumes (identical
+      // values; every shard finished this pod's filters before the argmax exchange ended)
+      if (job.commit && m.chosen >= 0 && job.P.pods[pi].vol_len > 0)
+        wffc_commit(c, job.P.reqs, job.P.terms, job.P.ints, job.P.vols, job.P.pods[pi], local, 1,
+                    [&](int key) { return c.label_value[(size_t)key * N + local]; });
     }
     __syncthreads();
     KSS_STAMP(S, 6);
@@ -525,6 +530,16 @@ __global__ void k_commit(DevCluster c, CommitArgs a) {
   handoff_drain();
 }
 
+// The binder's AssumePodVolumes / RevertAssumedPodVolumes of pod 0 of P on node `local`
+// (kss_commit / kss_rollback of a pod with WaitForFirstConsumer claims; wffc_commit).
+__global__ void k_wffc_commit(DevCluster c, DevPods P, int local, int sign) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  const size_t N = (size_t)c.N;
+  wffc_commit(c, P.reqs, P.terms, P.ints, P.vols, P.pods[0], local, sign,
+              [&](int key) { return c.label_value[(size_t)key * N + local]; });
+  handoff_drain();
+}
+
 // DefaultPreemption PostFilter dry run of one pod (kss_postfilter_pod): three launches.
 __global__ __launch_bounds__(PRE_THREADS) void k_preempt_stats(const PreemptJob* __restrict__ job) {
   extern __shared__ __attribute__((aligned(16))) long long smem[];
@@ -577,13 +592,14 @@ __global__ void k_count_delta(DevCluster c, const int32_t* node, const int32_t* 
 // kss_reset_node_state: the mutable columns back to their load-time copy, as a kernel (the
 // same hand-off path as every other writer of node state, not a copy engine): up to 8
 // (destination, source, 32-bit words) ranges, grid-stride, agent-scope stores.
+constexpr int KSS_NMUT = 10;  // mutable cluster columns (reset / pristine copies)
 struct ResetArgs {
-  uint32_t* dst[8];
-  const uint32_t* src[8];
-  size_t n4[8];
+  uint32_t* dst[KSS_NMUT];
+  const uint32_t* src[KSS_NMUT];
+  size_t n4[KSS_NMUT];
 };
 __global__ __launch_bounds__(256) void k_reset_state(ResetArgs a) {
-  for (int r = 0; r < 8; r++)
+  for (int r = 0; r < KSS_NMUT; r++)
     for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < a.n4[r]; i += (size_t)gridDim.x * blockDim.x)
       st_ag(a.dst[r] + i, ld_ag(a.src[r] + i));
   handoff_release();
@@ -693,8 +709,8 @@ struct kss_ctx {
   DevCluster dc{};
   DevBuf cluster_buf;
   DevBuf pristine_buf;  // load-time copy of the mutable columns (kss_reset_node_state)
-  size_t mut_bytes[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  size_t pristine_off[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  size_t mut_bytes[KSS_NMUT] = {};
+  size_t pristine_off[KSS_NMUT] = {};
   // pods
   DevBuf pod_buf;      // staged pod programs (kss_stage_pods / kss_schedule_batch)
   DevPods dp{};
@@ -714,6 +730,7 @@ struct kss_ctx {
   std::vector<uint32_t> key_flags_h;
   DevBuf gran_buf, err_buf;
   DevBuf cursor_buf;  // nextStartNodeIndex (one int32), kept on the device across launches
+  DevBuf wffc_pod_buf;  // kss_commit / kss_rollback: the pod's program for k_wffc_commit
   // the scheduling queue's nominator (kss_nominate): host mirror in AddNominatedPod order, uploaded
   // before a launch that reads it; run_pod_base = the podset index of the launch's pod 0
   std::vector<DevNom> nom;
@@ -983,6 +1000,16 @@ int validate(const kss_cluster* cl, const kss_podset* ps, int n) {
         break;
       case KSS_VOL_BIND_PV_MISSING:
         break;
+      case KSS_VOL_BIND_WFFC:
+        if (v.key < 0 || v.key >= cl->n_wclaims || v.b < 0 || !in(v.a, 3 * (int64_t)v.b, ps->n_ints) ||
+            !in(v.row, v.count >> 1, ps->n_terms) || v.count < 0)
+          return fail(KSS_E_INVAL, "WaitForFirstConsumer claim entry out of range");
+        for (int j = 0; j < v.b; j++) {
+          const int32_t pv = ps->ints[v.a + 3 * j], ta = ps->ints[v.a + 3 * j + 1], tb = ps->ints[v.a + 3 * j + 2];
+          if (pv < 0 || pv >= cl->n_pvs || (tb >= 0 && !in(ta, tb, ps->n_terms)) || tb < -1)
+            return fail(KSS_E_INVAL, "WaitForFirstConsumer candidate out of range");
+        }
+        break;
       default:
         return fail(KSS_E_INVAL, "bad volume entry kind");
     }
@@ -992,6 +1019,11 @@ int validate(const kss_cluster* cl, const kss_podset* ps, int n) {
     if (p.prefilter_status < KSS_PF_OK || p.prefilter_status > KSS_PF_VOLUME_BINDING)
       return fail(KSS_E_INVAL, "bad prefilter status");
     if (!in(p.vol_off, p.vol_len, ps->n_vols)) return fail(KSS_E_INVAL, "pod volume program out of range");
+    {
+      int nw = 0;
+      for (int e = 0; e < p.vol_len; e++) nw += ps->vols[p.vol_off + e].kind == KSS_VOL_BIND_WFFC;
+      if (nw > KSS_MAX_WFFC) return fail(KSS_E_UNSUPPORTED, "more than KSS_MAX_WFFC delayed claims in one pod");
+    }
     if (!in(p.sel_off, p.sel_len, ps->n_reqs) || !in(p.aff_off, p.aff_len, ps->n_terms) ||
         !in(p.pref_off, p.pref_len, ps->n_terms) || !in(p.spread_off, (int64_t)p.n_hard + p.n_soft, ps->n_spreads) ||
         !in(p.ipa_off, p.ipa_len, ps->n_ipa) || !in(p.own_terms_off, p.own_terms_len, ps->n_ints))
@@ -1411,7 +1443,7 @@ bool spread_bounds_ok(const GpodNeeds& q, double total, double cell, int N) {
 
 struct ClusterLayout {
   size_t o_alloc, o_req, o_nz, o_allowed, o_podc, o_flags, o_th, o_ts, o_to, o_lv, o_kb, o_kc, o_kf, o_ke, o_vi, o_vii,
-      o_cc, o_tc, o_log, o_pu, o_img, o_vc, o_va, o_vl, o_vrk, o_vkp, total;
+      o_cc, o_tc, o_log, o_pu, o_img, o_vc, o_va, o_vl, o_vrk, o_vkp, o_pvo, o_cln, total;
   ClusterLayout(const kss_cluster* cl, int class_cap, int term_cap) {
     const size_t N = (size_t)cl->n_nodes;
     size_t o = 0;
@@ -1446,6 +1478,8 @@ struct ClusterLayout {
     o_vl = take(4 * (size_t)cl->n_vol_keys * N);
     o_vrk = take(4 * (size_t)cl->n_vol_rows);
     o_vkp = take(4 * (size_t)cl->n_vol_keys);
+    o_pvo = take(4 * (size_t)cl->n_pvs);
+    o_cln = take(4 * (size_t)cl->n_wclaims);
     total = o;
   }
 };
@@ -1486,6 +1520,8 @@ int fill_cluster(hipStream_t st, const kss_cluster* cl, int class_cap, int term_
   rc |= cp(L.o_vl, cl->vol_limit, 4 * (size_t)cl->n_vol_keys * N);
   rc |= cp(L.o_vrk, cl->vol_row_key, 4 * (size_t)cl->n_vol_rows);
   rc |= cp(L.o_vkp, cl->vol_key_plugin, 4 * (size_t)cl->n_vol_keys);
+  rc |= cp(L.o_pvo, cl->pv_owner, 4 * (size_t)cl->n_pvs);
+  rc |= cp(L.o_cln, cl->claim_node, 4 * (size_t)cl->n_wclaims);
   logtab.resize(N + 3);
   for (size_t k = 0; k < N + 3; k++) logtab[k] = kss_go_log((double)(k + 2));
   rc |= cp(L.o_log, logtab.data(), 8 * (N + 3));
@@ -1527,6 +1563,12 @@ int fill_cluster(hipStream_t st, const kss_cluster* cl, int class_cap, int term_
   dc.vol_limit = (const int32_t*)(b + L.o_vl);
   dc.vol_row_key = (const int32_t*)(b + L.o_vrk);
   dc.vol_key_plugin = (const int32_t*)(b + L.o_vkp);
+  dc.n_pvs = cl->n_pvs;
+  dc.n_wclaims = cl->n_wclaims;
+  dc.pv_owner = (int32_t*)(b + L.o_pvo);
+  dc.claim_node = (int32_t*)(b + L.o_cln);
+  dc.pv_owner0 = dc.pv_owner;  // the pristine copies once kss_load_cluster has made them
+  dc.claim_node0 = dc.claim_node;
   return 0;
 }
 
@@ -1566,6 +1608,12 @@ int check_cluster(const kss_cluster* cl) {
   for (int k = 0; k < cl->n_vol_keys; k++)
     if (cl->vol_key_plugin[k] < KSS_F_EBS_LIMITS || cl->vol_key_plugin[k] > KSS_F_AZURE_DISK_LIMITS)
       return fail(KSS_E_INVAL, "volume key plugin out of range");
+  if (cl->n_pvs < 0 || cl->n_wclaims < 0 || (cl->n_pvs > 0 && !cl->pv_owner) || (cl->n_wclaims > 0 && !cl->claim_node))
+    return fail(KSS_E_INVAL, "bad WaitForFirstConsumer columns");
+  for (int v = 0; v < cl->n_pvs; v++)
+    if (cl->pv_owner[v] < 0 || cl->pv_owner[v] > cl->n_wclaims) return fail(KSS_E_INVAL, "pv_owner out of range");
+  for (int c = 0; c < cl->n_wclaims; c++)
+    if (cl->claim_node[c] < -2 || cl->claim_node[c] >= cl->n_nodes) return fail(KSS_E_INVAL, "claim_node out of range");
   return 0;
 }
 
@@ -1736,6 +1784,7 @@ void kss_destroy(kss_ctx* ctx) {
   ctx->pristine_buf.release();
   ctx->pod_buf.release();
   ctx->tmp_pod_buf.release();
+  ctx->wffc_pod_buf.release();
   ctx->slot_buf.release();
   ctx->meta_buf.release();
   ctx->chosen_buf.release();
@@ -1780,22 +1829,33 @@ int kss_load_cluster(kss_ctx* ctx, const kss_cluster* cl) {
   if (rc) return rc;
   // pristine copy of the mutable columns
   const size_t N = (size_t)cl->n_nodes;
-  const size_t mb[8] = {8 * KSS_NRES * N,          8 * 2 * N, 4 * N, 4 * (size_t)class_cap * N, 4 * (size_t)term_cap * N,
-                        8 * N, 4 * (size_t)cl->n_vol_rows * N, 4 * (size_t)cl->n_vol_keys * N};
+  const size_t mb[KSS_NMUT] = {8 * KSS_NRES * N,
+                               8 * 2 * N,
+                               4 * N,
+                               4 * (size_t)class_cap * N,
+                               4 * (size_t)term_cap * N,
+                               8 * N,
+                               4 * (size_t)cl->n_vol_rows * N,
+                               4 * (size_t)cl->n_vol_keys * N,
+                               4 * (size_t)cl->n_pvs,
+                               4 * (size_t)cl->n_wclaims};
   size_t tot = 0;
-  for (int i = 0; i < 8; i++) {
+  for (int i = 0; i < KSS_NMUT; i++) {
     ctx->mut_bytes[i] = mb[i];
     ctx->pristine_off[i] = tot;
     tot = align_up(tot + mb[i], 256);
   }
   rc = ctx->pristine_buf.ensure(tot);
   if (rc) return rc;
-  void* src[8] = {ctx->dc.requested,  ctx->dc.nonzero,   ctx->dc.pod_count, ctx->dc.class_count,
-                  ctx->dc.term_count, ctx->dc.port_used, ctx->dc.vol_count, ctx->dc.vol_attached};
+  void* src[KSS_NMUT] = {ctx->dc.requested,  ctx->dc.nonzero,   ctx->dc.pod_count,    ctx->dc.class_count,
+                         ctx->dc.term_count, ctx->dc.port_used, ctx->dc.vol_count,    ctx->dc.vol_attached,
+                         ctx->dc.pv_owner,   ctx->dc.claim_node};
+  ctx->dc.pv_owner0 = (const int32_t*)((char*)ctx->pristine_buf.p + ctx->pristine_off[8]);
+  ctx->dc.claim_node0 = (const int32_t*)((char*)ctx->pristine_buf.p + ctx->pristine_off[9]);
   {  // the copy by the reset kernel (agent-scope loads and stores), not the runtime's copy path
     ResetArgs a{};
     size_t most = 0;
-    for (int i = 0; i < 8; i++) {
+    for (int i = 0; i < KSS_NMUT; i++) {
       a.dst[i] = (uint32_t*)((char*)ctx->pristine_buf.p + ctx->pristine_off[i]);
       a.src[i] = (const uint32_t*)src[i];
       a.n4[i] = src[i] ? mb[i] / 4 : 0;
@@ -1998,8 +2058,9 @@ int kss_reset_node_state(kss_ctx* ctx) {
   if (!ctx || !ctx->loaded) return fail(KSS_E_INVAL, "no cluster loaded");
   std::lock_guard<std::mutex> lk(ctx->mu);
   HIP_TRY(hipSetDevice(ctx->cfg.device));
-  void* dst[8] = {ctx->dc.requested,  ctx->dc.nonzero,   ctx->dc.pod_count, ctx->dc.class_count,
-                  ctx->dc.term_count, ctx->dc.port_used, ctx->dc.vol_count, ctx->dc.vol_attached};
+  void* dst[KSS_NMUT] = {ctx->dc.requested,  ctx->dc.nonzero,   ctx->dc.pod_count,    ctx->dc.class_count,
+                         ctx->dc.term_count, ctx->dc.port_used, ctx->dc.vol_count,    ctx->dc.vol_attached,
+                         ctx->dc.pv_owner,   ctx->dc.claim_node};
   ctx->count_bound = ctx->count_bound0;
   ctx->cell_bound = ctx->cell_bound0;
   ctx->bound_log.clear();
@@ -2007,7 +2068,7 @@ int kss_reset_node_state(kss_ctx* ctx) {
   ctx->state_unknown = false;
   ResetArgs a{};
   size_t most = 0;
-  for (int i = 0; i < 8; i++) {
+  for (int i = 0; i < KSS_NMUT; i++) {
     a.dst[i] = (uint32_t*)dst[i];
     a.src[i] = (const uint32_t*)((char*)ctx->pristine_buf.p + ctx->pristine_off[i]);
     a.n4[i] = ctx->mut_bytes[i] / 4;
@@ -2343,6 +2404,20 @@ int kss_apply_port_delta(kss_ctx* ctx, const int32_t* idx, int32_t n, const uint
   // rows are few (pods bound elsewhere): one 8-byte copy per row, ordered on the stream
   for (int i = 0; i < n; i++)
     HIP_TRY(hipMemcpyAsync(ctx->dc.port_used + idx[i], port_used + i, 8, hipMemcpyHostToDevice, ctx->stream));
+  HIP_TRY(hipStreamSynchronize(ctx->stream));
+  return 0;
+}
+
+int kss_read_binding_state(kss_ctx* ctx, int32_t* pv_owner, int32_t* claim_node) {
+  KSS_SVC_QUIESCE(ctx);
+  if (!ctx || !ctx->loaded) return fail(KSS_E_INVAL, "no cluster loaded");
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  HIP_TRY(hipSetDevice(ctx->cfg.device));
+  if (pv_owner && ctx->dc.n_pvs)
+    HIP_TRY(hipMemcpyAsync(pv_owner, ctx->dc.pv_owner, 4 * (size_t)ctx->dc.n_pvs, hipMemcpyDeviceToHost, ctx->stream));
+  if (claim_node && ctx->dc.n_wclaims)
+    HIP_TRY(hipMemcpyAsync(claim_node, ctx->dc.claim_node, 4 * (size_t)ctx->dc.n_wclaims, hipMemcpyDeviceToHost,
+                           ctx->stream));
   HIP_TRY(hipStreamSynchronize(ctx->stream));
   return 0;
 }
@@ -3437,6 +3512,24 @@ static int compact_pod(const kss_podset* ps, int i, OnePod& o) {
       const int32_t at = (int32_t)o.reqs.size();
       for (int k = 0; k < v.b; k++) req(ps->reqs[v.a + k]);
       v.a = at;
+    } else if (v.kind == KSS_VOL_BIND_WFFC) {  // candidate triplets and their terms, the class's topology terms
+      if (v.b < 0 || v.count < 0 || !in(v.a, 3 * (int64_t)v.b, ps->n_ints) || !in(v.row, v.count >> 1, ps->n_terms))
+        return fail(KSS_E_INVAL, "WaitForFirstConsumer claim entry out of range");
+      std::vector<int32_t> trip(ps->ints + v.a, ps->ints + v.a + 3 * (size_t)v.b);
+      for (int j = 0; j < v.b; j++) {
+        const int32_t ta = trip[3 * j + 1], tb = trip[3 * j + 2];
+        if (tb < 0) continue;
+        if (!in(ta, tb, ps->n_terms)) return fail(KSS_E_INVAL, "WaitForFirstConsumer candidate out of range");
+        trip[3 * j + 1] = (int32_t)o.terms.size();
+        for (int t = 0; t < tb; t++)
+          if (!term(ps->terms[ta + t])) return fail(KSS_E_INVAL, "term out of range");
+      }
+      const int32_t at = (int32_t)o.terms.size();
+      for (int t = 0; t < (v.count >> 1); t++)
+        if (!term(ps->terms[v.row + t])) return fail(KSS_E_INVAL, "term out of range");
+      v.row = at;
+      v.a = (int32_t)o.ints.size();
+      o.ints.insert(o.ints.end(), trip.begin(), trip.end());
     }
     o.vols.push_back(v);
   }
@@ -3623,6 +3716,17 @@ static int commit_one(kss_ctx* ctx, const kss_podset* ps, int32_t pod_index, int
   }
   hipLaunchKernelGGL(k_commit, dim3(1), dim3(64), 0, ctx->stream, ctx->dc, a);
   HIP_TRY(hipGetLastError());  // no synchronisation: every later call on the ctx stream is ordered after it
+  bool wffc = false;
+  for (int e = 0; e < p.vol_len; e++) wffc |= ps->vols[p.vol_off + e].kind == KSS_VOL_BIND_WFFC;
+  if (wffc) {  // AssumePodVolumes / RevertAssumedPodVolumes on the device (the assume cache lives there)
+    OnePod one;
+    if (int rc = compact_pod(ps, pod_index, one)) return rc;
+    DevPods dpw{};
+    if (int rc = upload_podset(ctx->stream, ctx->wffc_pod_buf, &one.ps, dpw)) return rc;
+    hipLaunchKernelGGL(k_wffc_commit, dim3(1), dim3(64), 0, ctx->stream, ctx->dc, dpw, local, sign);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipStreamSynchronize(ctx->stream));  // `one` (the upload's host source) goes out of scope
+  }
   if (sign > 0) {  // assume -> SchedulingQueue.DeleteNominatedPodIfExists
     const size_t before = ctx->nom.size();
     const int32_t id = pod_identity(p, pod_index);

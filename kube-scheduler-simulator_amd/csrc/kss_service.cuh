@@ -902,6 +902,9 @@ __device__ void service_loop(DevCluster c, const DevJob& job, const kss_profile&
       const int local = node - c.node_base;
       if (threadIdx.x == 0 && local >= S.lo && local < S.hi)
         commit_pod(c, job.P, job.P.pods[pi], local, op == SVC_COMMIT ? 1 : -1);
+      if (threadIdx.x == 0 && job.P.pods[pi].vol_len > 0)  // the assume cache is global: every shard
+        wffc_commit(c, job.P.reqs, job.P.terms, job.P.ints, job.P.vols, job.P.pods[pi], local,
+                    op == SVC_COMMIT ? 1 : -1, [&](int key) { return c.label_value[(size_t)key * (size_t)c.N + local]; });
       __syncthreads();
     }
     if (threadIdx.x == 0) __hip_atomic_store(seen + w, seq + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

@@ -76,6 +76,9 @@ KSS_IPA_ANTI_AFFINITY = 1
 KSS_IPA_EXISTING_ANTI_AFFINITY = 2
 KSS_VB_NODE_CONFLICT = 0
 KSS_VB_PV_NOT_EXIST = 1
+KSS_VB_BIND_CONFLICT = 2
+KSS_VB_NODE_BIND = 3
+KSS_VB_BIND_PV_NOT_EXIST = 4
 
 SCORE_PLUGINS = [
     "TaintToleration",
@@ -104,8 +107,9 @@ KSS_SPREAD_POLICY_TAINTS_HONOR = 1 << 1
 (KSS_IPA_EXISTING_ANTI, KSS_IPA_REQ_AFFINITY, KSS_IPA_REQ_ANTI, KSS_IPA_SCORE_CLASS, KSS_IPA_SCORE_TERM) = range(5)
 
 (KSS_VOL_CONFLICT, KSS_VOL_LIMIT, KSS_VOL_BIND_AFFINITY, KSS_VOL_BIND_PV_MISSING, KSS_VOL_ZONE, KSS_VOL_ZONE_ERROR,
- KSS_VOL_OWN, KSS_VOL_OWN_PRIVATE) = range(8)
+ KSS_VOL_OWN, KSS_VOL_OWN_PRIVATE, KSS_VOL_BIND_WFFC) = range(9)
 KSS_MAX_VOL_KEYS = 64
+KSS_MAX_WFFC = 4
 KSS_PF_OK, KSS_PF_NODE_AFFINITY_CONFLICT, KSS_PF_ERROR, KSS_PF_VOLUME_BINDING = range(4)
 
 KSS_POD_TOL_UNSCHEDULABLE = 1 << 0
@@ -146,6 +150,7 @@ class Cluster(C.Structure):
         ("n_ports", i32), ("n_images", i32), ("port_used", P(u64)), ("image_score", P(i64)),
         ("n_vol_rows", i32), ("n_vol_keys", i32), ("vol_count", P(i32)), ("vol_attached", P(i32)),
         ("vol_limit", P(i32)), ("vol_row_key", P(i32)), ("vol_key_plugin", P(i32)),
+        ("n_pvs", i32), ("n_wclaims", i32), ("pv_owner", P(i32)), ("claim_node", P(i32)),
     ]
 
 

@@ -411,6 +411,8 @@ class CompiledCluster:
     images: List[str] = field(default_factory=list)                   # image_score rows (image names)
     vol_rows: list = field(default_factory=list)                      # vol_count rows (volumes.VolumeCompiler.rows)
     vol_keys: List[str] = field(default_factory=list)                 # attach-limit keys
+    pvs: List[str] = field(default_factory=list)                      # candidate PVs of WaitForFirstConsumer claims (pv_owner)
+    wclaims: List[Tuple[str, str]] = field(default_factory=list)      # those claims (namespace, name) (claim_node)
     _keep: list = field(default_factory=list)
 
     @property
@@ -426,8 +428,10 @@ class CompiledCluster:
         c.image_score = abi.ptr(a["image_score"], abi.i64)
         c.n_vol_rows = len(self.vol_rows)
         c.n_vol_keys = len(self.vol_keys)
-        for name in ("vol_count", "vol_attached", "vol_limit", "vol_row_key", "vol_key_plugin"):
+        for name in ("vol_count", "vol_attached", "vol_limit", "vol_row_key", "vol_key_plugin", "pv_owner", "claim_node"):
             setattr(c, name, abi.ptr(a[name], abi.i32))
+        c.n_pvs = len(self.pvs)
+        c.n_wclaims = len(self.wclaims)
         c.n_nodes = self.n_nodes
         c.n_scalar = len(self.scalars)
         c.n_label_keys = len(self.label_keys)
@@ -780,7 +784,9 @@ class Compiler:
                       vol_attached=vc.vol_attached if vc else np.zeros((0, N), np.int32),
                       vol_limit=vc.vol_limit if vc else np.zeros((0, N), np.int32),
                       vol_row_key=vc.vol_row_key if vc else np.zeros(0, np.int32),
-                      vol_key_plugin=vc.vol_key_plugin if vc else np.zeros(0, np.int32))
+                      vol_key_plugin=vc.vol_key_plugin if vc else np.zeros(0, np.int32),
+                      pv_owner=vc.pv_owner if vc else np.zeros(0, np.int32),
+                      claim_node=vc.claim_node if vc else np.zeros(0, np.int32))
         arrays = {k: (np.zeros(1, dtype=v.dtype) if v.size == 0 else np.ascontiguousarray(v))
                   for k, v in arrays.items()}
         nb = len(bound_names)
@@ -796,7 +802,9 @@ class Compiler:
         self.cc = CompiledCluster(node_names=names, order=order, scalars=scalars, label_keys=label_keys,
                                   key_values=key_values, taints=taints, classes=classes, terms=terms, arrays=arrays,
                                   namespaces=self.namespaces, bound=bound, bound_names=bound_names, ports=ports,
-                                  images=images, vol_rows=list(vc.rows) if vc else [], vol_keys=list(vc.keys) if vc else [])
+                                  images=images, vol_rows=list(vc.rows) if vc else [], vol_keys=list(vc.keys) if vc else [],
+                                  pvs=list(vc.pv_names) if vc else [],
+                                  wclaims=[vc.claim_key(pvc) for pvc in vc.wclaims] if vc else [])
         self.node_labels = node_labels
         self.key_flags = key_flags
         pods = self._compile_pods(self.pending)
@@ -970,7 +978,7 @@ class Compiler:
                 self._reqs.append(self._req(key, "In", tuple(vals)))
             return off, len(self._reqs) - off
 
-        prog = self.vc.program(j, pv_terms, zone_reqs)
+        prog = self.vc.program(j, pv_terms, zone_reqs, self._list)
         self._vols.extend(prog)
         rec["vol_len"] = len(prog)
 

@@ -48,6 +48,7 @@ SIGNATURES = [
     ("kss_read_node_state", C.c_int, [C.c_void_p, P(C.c_int64), P(C.c_int64), P(C.c_int32), P(C.c_int32), P(C.c_int32)]),
     ("kss_read_port_state", C.c_int, [C.c_void_p, P(C.c_uint64)]),
     ("kss_read_volume_state", C.c_int, [C.c_void_p, P(C.c_int32), P(C.c_int32)]),
+    ("kss_read_binding_state", C.c_int, [C.c_void_p, P(C.c_int32), P(C.c_int32)]),
     ("kss_apply_volume_delta", C.c_int, [C.c_void_p, P(C.c_int32), P(C.c_int32), P(C.c_int32), C.c_int32, C.c_int32]),
     ("kss_apply_port_delta", C.c_int, [C.c_void_p, P(C.c_int32), C.c_int32, P(C.c_uint64)]),
     ("kss_eval_pod", C.c_int, [C.c_void_p, P(abi.PodSet), C.c_int32, P(abi.PodResult)]),
@@ -131,7 +132,7 @@ def lib() -> C.CDLL:
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args
-        if L.kss_abi_version() != 4:
+        if L.kss_abi_version() != 5:
             raise ImportError("libkss ABI version mismatch")
         _lib = L
     return _lib
@@ -363,6 +364,8 @@ class Context:
         self.n_scalar = cluster_struct.n_scalar
         self.n_vol_rows = cluster_struct.n_vol_rows
         self.n_vol_keys = cluster_struct.n_vol_keys
+        self.n_pvs = cluster_struct.n_pvs
+        self.n_wclaims = cluster_struct.n_wclaims
         if names is not None:
             st, keep = names
             self._keep = keep
@@ -566,6 +569,13 @@ class Context:
         va = np.zeros((max(self.n_vol_keys, 1), N), np.int32)
         check(lib().kss_read_volume_state(self.h, vc.ctypes.data_as(P(C.c_int32)), va.ctypes.data_as(P(C.c_int32))))
         return vc[:self.n_vol_rows, :self.n_nodes], va[:self.n_vol_keys, :self.n_nodes]
+
+    def binding_state(self):
+        """(pv_owner [n_pvs], claim_node [n_wclaims]): the binder's assume cache (kss_read_binding_state)."""
+        po = np.zeros(max(self.n_pvs, 1), np.int32)
+        cn = np.zeros(max(self.n_wclaims, 1), np.int32)
+        check(lib().kss_read_binding_state(self.h, po.ctypes.data_as(P(C.c_int32)), cn.ctypes.data_as(P(C.c_int32))))
+        return po[:self.n_pvs], cn[:self.n_wclaims]
 
     def apply_volume_delta(self, node, row, value, overwrite=False):
         """vol_count / vol_attached sync (kss_apply_volume_delta): row r < n_vol_rows is a vol_count

@@ -14,8 +14,13 @@ Restates the v1.26.2 volume plugins of the default MultiPoint set
                        getVolumeLimits, volumeutil.GetCSIAttachLimitKey -> a key per CSI driver
   VolumeBinding        volumebinding/volume_binding.go PreFilter (podHasPVCs,
                        GetPodVolumeClaims) -> KSS_PF_VOLUME_BINDING; Filter -> binder.go
-                       checkBoundClaims -> KSS_VOL_BIND_* entries (PV node affinity as
-                       node-selector terms over the node's labels alone)
+                       FindPodVolumes: checkBoundClaims -> KSS_VOL_BIND_AFFINITY / _PV_MISSING
+                       entries (PV node affinity as node-selector terms over the node's labels
+                       alone); unbound WaitForFirstConsumer claims -> KSS_VOL_BIND_WFFC entries
+                       (findMatchingVolumes / FindMatchingVolume's static checks resolved here into
+                       each claim's candidate PVs, smallest first; checkVolumeProvisions' class
+                       provisioner and allowedTopologies) over the binder's assume cache, which
+                       the cluster carries as pv_owner / claim_node
   VolumeZone           volumezone/volume_zone.go Filter -> KSS_VOL_ZONE requirements
 
 The device never sees a volume object.  A volume that a pending pod uses is either
@@ -23,11 +28,14 @@ The device never sees a volume object.  A volume that a pending pod uses is eith
 AssumePod) or *shared*, in which case it gets a vol_count row so the filter can find it
 already attached on a node.  Disk usages a pending pod's volumes conflict with get rows too.
 
-Refused (kss.compile.Unsupported), each naming why: unbound claims of a
-WaitForFirstConsumer class (FindPodVolumes' static binding / provisioning search and the
-binder's assume cache), a StorageClass without volumeBindingMode (a PreFilter Error), in-tree
-volumes of a plugin a CSINode lists as migrated (CSI translation), and nodes whose two
-instance-type labels disagree (getMaxVolumeFunc reads whichever Go map order yields first).
+Refused (kss.compile.Unsupported), each naming why: a StorageClass without volumeBindingMode (a
+PreFilter Error), in-tree volumes of a plugin a CSINode lists as migrated (CSI translation), nodes
+whose two instance-type labels disagree (getMaxVolumeFunc reads whichever Go map order yields
+first), more than KSS_MAX_WFFC delayed claims in one pod, and two PVs pre-bound to one delayed
+claim (which FindMatchingVolume returns depends on pvCache list order).  Determinism decision:
+ListPVs is map-backed, so equally small PVs go by name.  Storage capacity (hasEnoughCapacity) is
+not checked: it applies only to CSIDrivers with storageCapacity set, and the snapshot
+(ResourcesForSnap) carries none.
 """
 from __future__ import annotations
 
@@ -47,6 +55,8 @@ VOLUME_ZONE_LABELS = ("failure-domain.beta.kubernetes.io/zone", "failure-domain.
                       "topology.kubernetes.io/zone", "topology.kubernetes.io/region")
 INSTANCE_TYPE_LABELS = ("beta.kubernetes.io/instance-type", "node.kubernetes.io/instance-type")
 UNBOUND_IMMEDIATE = "pod has unbound immediate PersistentVolumeClaims"
+ANN_SELECTED_NODE = "volume.kubernetes.io/selected-node"
+NOT_SUPPORTED_PROVISIONER = "kubernetes.io/no-provisioner"
 
 # plugin -> (pod / PV volume source, id field, provisioner = in-tree plugin name, limit key, default max)
 NON_CSI = {
@@ -235,7 +245,7 @@ class VolumeCompiler:
                     return err, None
         if not has:
             return None, None
-        bound, immediate = [], False
+        bound, delayed, immediate = [], [], False
         for vol in _spec(pod).get("volumes") or []:
             name, _ = self.claim_name(pod, vol)
             if name is None:
@@ -251,12 +261,14 @@ class VolumeCompiler:
                     raise Unsupported(f'VolumeBindingMode not set for StorageClass "{cls}" (a PreFilter Error)')
                 delay = mode == "WaitForFirstConsumer"
             if delay and not _spec(pvc).get("volumeName"):
-                raise Unsupported("unbound WaitForFirstConsumer claim: VolumeBinding's PV search / provisioning "
-                                  "is not on the device path")
+                delayed.append(pvc)  # unboundClaimsDelayBinding
+                continue
             immediate = True  # "Prebound PVCs are treated as unbound immediate binding"
         if immediate:
             return UNBOUND_IMMEDIATE, None
-        return None, bound
+        if len(delayed) > abi.KSS_MAX_WFFC:
+            raise Unsupported(f"more than {abi.KSS_MAX_WFFC} unbound WaitForFirstConsumer claims in one pod")
+        return None, (bound, delayed)
 
     # ---------------------------------------------------------------- limit plugins
     def _non_csi_ids(self, plugin, pod, new_pod) -> set:
@@ -406,8 +418,16 @@ class VolumeCompiler:
         keys = set()
         for j, pod in enumerate(self.pending):
             msg, claims = self._prefilter[j]
-            for pvc in claims or []:
-                pv = self.pv.get(_spec(pvc).get("volumeName"))
+            bound, delayed = claims or ([], [])
+            pvs = [self.pv.get(_spec(pvc).get("volumeName")) for pvc in bound]
+            for pvc in delayed:
+                c = self.wclaim_index[self.claim_key(pvc)]
+                pvs += [self.pv[self.pv_names[v]] for v in self.wclaim_cands[c]]
+                sc = self.sc.get(self.pvc_class(pvc)) or {}
+                for t in sc.get("allowedTopologies") or []:
+                    for e in t.get("matchLabelExpressions") or []:
+                        keys.add(e.get("key", ""))
+            for pv in pvs:
                 req = ((_spec(pv).get("nodeAffinity") or {}).get("required")) if pv else None
                 for t in (req or {}).get("nodeSelectorTerms") or []:
                     for e in t.get("matchExpressions") or []:
@@ -500,6 +520,7 @@ class VolumeCompiler:
                     vol_limit[k, n] = self._non_csi_limit(plugin, node)
         self.vol_count, self.vol_attached, self.vol_limit = vol_count, vol_attached, vol_limit
         self.vol_row_key, self.vol_key_plugin = vol_row_key, vol_key_plugin
+        self._build_wffc(live)
         # --- per pending pod: conflict rows, limit entries, own rows
         self._conflict, self._limits, self._own, self._private = {}, {}, {}, {}
         for j in live:
@@ -529,6 +550,109 @@ class VolumeCompiler:
             self._own[j] = sorted(own)
             self._private[j] = priv
 
+    # ---------------------------------------------------------------- WaitForFirstConsumer
+    @staticmethod
+    def claim_key(pvc) -> Tuple[str, str]:
+        return _ns(pvc), _meta(pvc).get("name") or ""
+
+    @staticmethod
+    def claim_request(pvc) -> int:
+        return value(((_spec(pvc).get("resources") or {}).get("requests") or {}).get("storage", "0"))
+
+    @staticmethod
+    def pv_class(pv) -> str:
+        """storagehelpers.GetPersistentVolumeClass."""
+        ann = _meta(pv).get("annotations") or {}
+        if ANN_BETA_STORAGE_CLASS in ann:
+            return ann[ANN_BETA_STORAGE_CLASS]
+        return _spec(pv).get("storageClassName") or ""
+
+    @staticmethod
+    def bound_to(pv, pvc) -> bool:
+        """IsVolumeBoundToClaim: claimRef name / namespace, and uid when the ref has one."""
+        ref = _spec(pv).get("claimRef")
+        if not ref:
+            return False
+        return ((ref.get("name") or "") == (_meta(pvc).get("name") or "") and (ref.get("namespace") or "") == _ns(pvc)
+                and (not ref.get("uid") or ref.get("uid") == (_meta(pvc).get("uid") or "")))
+
+    def _candidates(self, pvc) -> Tuple[List[str], Optional[str]]:
+        """FindMatchingVolume's node-independent checks over ListPVs(class): the PVs the claim may
+        bind in increasing capacity, then name, and the PV pre-bound to it (claimRef) if any."""
+        from .compile import Unsupported
+        from .selectors import SelectorError, label_selector_as_selector
+        cls = self.pvc_class(pvc)
+        req = self.claim_request(pvc)
+        mode = _spec(pvc).get("volumeMode") or "Filesystem"
+        modes = set(_spec(pvc).get("accessModes") or [])
+        sel = _spec(pvc).get("selector")
+        try:
+            selector = label_selector_as_selector(sel) if sel is not None else None
+        except SelectorError:
+            raise Unsupported("a WaitForFirstConsumer claim's selector does not parse (a Filter Error)")
+        out, pre = [], []
+        for name in sorted(self.pv):
+            pv = self.pv[name]
+            if self.pv_class(pv) != cls:
+                continue
+            ref = _spec(pv).get("claimRef")
+            if ref and not self.bound_to(pv, pvc):
+                continue
+            cap = value((_spec(pv).get("capacity") or {}).get("storage", "0"))
+            if cap < req or (_spec(pv).get("volumeMode") or "Filesystem") != mode or _meta(pv).get("deletionTimestamp"):
+                continue
+            if ref:
+                pre.append(name)  # returned whenever its node affinity holds (phase / selector / modes unchecked)
+                out.append((cap, name))
+                continue
+            if ((pv.get("status") or {}).get("phase")) != "Available":
+                continue
+            if selector is not None and not selector.matches(_meta(pv).get("labels") or {}):
+                continue
+            if not modes <= set(_spec(pv).get("accessModes") or []):
+                continue
+            out.append((cap, name))
+        if len(pre) > 1:
+            raise Unsupported("two PVs pre-bound (claimRef) to one WaitForFirstConsumer claim: "
+                              "FindMatchingVolume's answer depends on pvCache list order")
+        return [nm for _, nm in sorted(out)], (pre[0] if pre else None)
+
+    def _build_wffc(self, live):
+        """The delayed claims of the live pending pods (ids in first-use order), their candidate
+        PVs (ids in order of first appearance) and the assume cache's initial state."""
+        claims: List[dict] = []
+        self.wclaim_index: Dict[Tuple[str, str], int] = {}
+        for j in live:
+            _, cl = self._prefilter[j]
+            for pvc in (cl or ([], []))[1]:
+                k = self.claim_key(pvc)
+                if k not in self.wclaim_index:
+                    self.wclaim_index[k] = len(claims)
+                    claims.append(pvc)
+        self.pv_names: List[str] = []
+        pv_index: Dict[str, int] = {}
+        self.wclaim_cands: List[List[int]] = []
+        owner: Dict[int, int] = {}
+        for c, pvc in enumerate(claims):
+            names, pre = self._candidates(pvc)
+            ids = []
+            for nm in names:
+                if nm not in pv_index:
+                    pv_index[nm] = len(self.pv_names)
+                    self.pv_names.append(nm)
+                ids.append(pv_index[nm])
+            self.wclaim_cands.append(ids)
+            if pre is not None:
+                owner[pv_index[pre]] = c + 1
+        self.wclaims = claims
+        self.pv_owner = np.array([owner.get(v, 0) for v in range(len(self.pv_names))], np.int32)
+        node_index = {(_meta(n).get("name") or ""): i for i, n in enumerate(self.nodes)}
+        sel = []
+        for pvc in claims:
+            s = (_meta(pvc).get("annotations") or {}).get(ANN_SELECTED_NODE)
+            sel.append(-1 if s is None else node_index.get(s, -2))
+        self.claim_node = np.array(sel, np.int32)
+
     # ---------------------------------------------------------------- results
     def node_zone_flags(self) -> np.ndarray:
         f = np.zeros(self.N, np.uint32)
@@ -541,17 +665,18 @@ class VolumeCompiler:
     def prefilter(self, j: int) -> Tuple[Optional[str], Optional[list]]:
         return self._prefilter[j]
 
-    def program(self, j: int, pv_terms, zone_reqs) -> List[tuple]:
+    def program(self, j: int, pv_terms, zone_reqs, int_list=None) -> List[tuple]:
         """kss_vol rows (kind, key, row, count, a, b) of pending pod j, in filter order.
         pv_terms(required node selector) -> (term_off, term_len); zone_reqs([(key, values)])
-        -> (req_off, req_len): the compiler's pools."""
+        -> (req_off, req_len); int_list(values) -> (off, len): the compiler's pools."""
         msg, claims = self._prefilter[j]
         if msg is not None:
             return []
         pod = self.pending[j]
         out = [(abi.KSS_VOL_CONFLICT, -1, r, 0, 0, 0) for r in self._conflict[j]]
         out += [(abi.KSS_VOL_LIMIT, k, r, c, 0, 0) for k, r, c in self._limits[j]]
-        for pvc in claims or []:  # checkBoundClaims, in claim order
+        bound, delayed = claims or ([], [])
+        for pvc in bound:  # checkBoundClaims, in claim order
             pv = self.pv.get(_spec(pvc).get("volumeName"))
             if pv is None:
                 out.append((abi.KSS_VOL_BIND_PV_MISSING, -1, -1, 0, 0, 0))
@@ -560,6 +685,24 @@ class VolumeCompiler:
             if req is not None:
                 a, b = pv_terms(req.get("nodeSelectorTerms") or [])
                 out.append((abi.KSS_VOL_BIND_AFFINITY, -1, -1, 0, a, b))
+        # unbound WaitForFirstConsumer claims: findMatchingVolumes' order (byPVCSize, stable)
+        for pvc in sorted(delayed, key=self.claim_request):
+            c = self.wclaim_index[self.claim_key(pvc)]
+            trip = []
+            for v in self.wclaim_cands[c]:
+                req = (_spec(self.pv[self.pv_names[v]]).get("nodeAffinity") or {}).get("required")
+                ta, tb = pv_terms(req.get("nodeSelectorTerms") or []) if req is not None else (0, -1)
+                trip += [v, ta, tb]
+            a, _ = int_list(trip)
+            sc = self.sc[self.pvc_class(pvc)]
+            prov = (sc.get("provisioner") or "") not in ("", NOT_SUPPORTED_PROVISIONER)
+            topo = [{"matchExpressions": [{"key": e.get("key", ""), "operator": "In", "values": list(e.get("values") or [])}
+                                          for e in t.get("matchLabelExpressions") or []]}
+                    for t in sc.get("allowedTopologies") or []]
+            ta, tb = pv_terms(topo) if topo else (0, 0)
+            if topo and tb == 0:  # every term empty: "nil or empty term selects no objects"
+                prov = False
+            out.append((abi.KSS_VOL_BIND_WFFC, c, ta, (tb << 1) | (1 if prov else 0), a, len(trip) // 3))
         if _spec(pod).get("volumes") or []:
             cons, err = self.zone_constraints(pod)
             for c in cons:

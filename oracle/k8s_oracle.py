@@ -699,10 +699,22 @@ class Oracle:
         return None
 
     def assume(self, pod, i: int):
-        """Cache.AssumePod -> NodeInfo.AddPod, then SchedulingQueue.DeleteNominatedPodIfExists
-        (schedule_one.go assume)."""
+        """Reserve's VolumeBinding.AssumePodVolumes (the binder's assume cache: WaitForFirstConsumer
+        claims' static bindings and provisioning decisions on node i), Cache.AssumePod ->
+        NodeInfo.AddPod, then SchedulingQueue.DeleteNominatedPodIfExists (schedule_one.go assume)."""
+        if _spec(pod).get("volumes"):
+            _, claims = self.storage.binding_prefilter(pod)
+            self.storage.assume(claims, self.infos[i].node, NodeSelectorTerms)
         self.infos[i].add_pod(pod)
         self.clear_nomination(pod)
+
+    def forget(self, pod, i: int):
+        """Unreserve: VolumeBinding.Unreserve (RevertAssumedPodVolumes) and Cache.ForgetPod ->
+        NodeInfo.RemovePod."""
+        if _spec(pod).get("volumes"):
+            _, claims = self.storage.binding_prefilter(pod)
+            self.storage.revert(claims)
+        self.infos[i].remove_pod(pod)
 
     def filter_with_nominated(self, pod, i: int, ni: "NodeInfo", pts_st, ipa_st, vb_claims=None):
         """framework.RunFilterPluginsWithNominatedPods (v1.26 runtime/framework.go) over NodeInfo ni

@@ -15,14 +15,23 @@ restated from the upstream function it names):
   NodeVolumeLimits    nodevolumelimits/csi.go  CSILimits.Filter / filterAttachableVolumes /
                       getCSIDriverInfo(FromSC) / getVolumeLimits; volumeutil.GetCSIAttachLimitKey
   VolumeBinding       volumebinding/volume_binding.go PreFilter (podHasPVCs,
-                      GetPodVolumeClaims) / Filter -> binder.go FindPodVolumes / checkBoundClaims;
+                      GetPodVolumeClaims) / Filter -> binder.go FindPodVolumes: checkBoundClaims,
+                      findMatchingVolumes (pv_helpers.go FindMatchingVolume) and
+                      checkVolumeProvisions for unbound WaitForFirstConsumer claims; Reserve ->
+                      AssumePodVolumes (the assume cache), Unreserve -> RevertAssumedPodVolumes;
                       Score returns 0 (VolumeCapacityPriority is alpha, off)
   VolumeZone          volumezone/volume_zone.go  Filter
 
-Refused (Unsupported), each with its reason: unbound PVCs of a WaitForFirstConsumer class
-(FindPodVolumes' static-binding / provisioning search and the binder's assume cache), a
-StorageClass without volumeBindingMode (a PreFilter Error), and in-tree volumes of a plugin
-some CSINode lists as migrated (storage.alpha.kubernetes.io/migrated-plugins: CSI translation).
+Determinism decisions (upstream is random here): FindMatchingVolume walks pvCache.ListPVs(class),
+a map-backed list, and keeps the first of equally small PVs -- here the PVs go by name.  Storage
+capacity (hasEnoughCapacity) is not checked: it applies only to CSIDriver objects with
+storageCapacity set, and the simulator's snapshot (ResourcesForSnap) carries no CSIDrivers.
+
+Refused (Unsupported), each with its reason: a StorageClass without volumeBindingMode (a PreFilter
+Error), in-tree volumes of a plugin some CSINode lists as migrated
+(storage.alpha.kubernetes.io/migrated-plugins: CSI translation), an unbound WaitForFirstConsumer
+claim without a class name or whose class is missing at provisioning (Filter Errors), and two PVs
+pre-bound (spec.claimRef) to one claim (which FindMatchingVolume returns depends on list order).
 
 Used only by tests/ (checker), never by the product.
 """
@@ -45,6 +54,9 @@ MSG_NODE_CONFLICT = "node(s) had volume node affinity conflict"
 MSG_PV_NOT_EXIST = "node(s) unavailable due to one or more pvc(s) bound to non-existent pv(s)"
 MSG_ZONE_CONFLICT = "node(s) had no available volume zone"
 MSG_UNBOUND_IMMEDIATE = "pod has unbound immediate PersistentVolumeClaims"
+MSG_BIND_CONFLICT = "node(s) didn't find available persistent volumes to bind"
+ANN_SELECTED_NODE = "volume.kubernetes.io/selected-node"
+NOT_SUPPORTED_PROVISIONER = "kubernetes.io/no-provisioner"
 
 # the in-tree limit plugins: (plugin, inline/PV source field, id field, provisioner, limit key, default max)
 NON_CSI = {
@@ -107,14 +119,46 @@ def label_zones_to_set(v: str):
     return out
 
 
+def storage_bytes(q) -> int:
+    """resource.Quantity of a storage request / capacity, in bytes (0 when absent)."""
+    if q is None:
+        return 0
+    from k8s_oracle import qvalue
+    return qvalue(q)
+
+
+class VBClaims:
+    """GetPodVolumeClaims: the pod's bound claims and its unbound WaitForFirstConsumer claims
+    (pod volume order)."""
+
+    def __init__(self, bound, delayed):
+        self.bound = bound
+        self.delayed = delayed
+
+
 class Storage:
-    """The snapshot's PVs, PVCs, StorageClasses and CSINodes (listers)."""
+    """The snapshot's PVs, PVCs, StorageClasses and CSINodes (listers), plus the binder's assume
+    cache for WaitForFirstConsumer claims: PVs assumed bound to a claim (spec.claimRef) and claims
+    assumed provisioned on a node (the selected-node annotation)."""
 
     def __init__(self, pvs=(), pvcs=(), storage_classes=(), csinodes=()):
         self.pv = {_meta(p)["name"]: p for p in pvs}
         self.pvc = {(_meta(p).get("namespace") or "default", _meta(p)["name"]): p for p in pvcs}
         self.sc = {_meta(s)["name"]: s for s in storage_classes}
         self.csinode = {_meta(c)["name"]: c for c in csinodes}
+        # the assume cache: pv name -> (namespace, claim name, uid) of its claimRef; claim key -> node name
+        self.pv_ref0 = {}
+        for name, pv in self.pv.items():
+            ref = _spec(pv).get("claimRef")
+            if ref:
+                self.pv_ref0[name] = (ref.get("namespace") or "", ref.get("name") or "", ref.get("uid") or "")
+        self.pv_ref = dict(self.pv_ref0)
+        self.selected0 = {}
+        for key, pvc in self.pvc.items():
+            sel = (_meta(pvc).get("annotations") or {}).get(ANN_SELECTED_NODE)
+            if sel is not None:
+                self.selected0[key] = sel
+        self.selected = dict(self.selected0)
 
     # ------------------------------------------------------------ helpers
     @staticmethod
@@ -210,7 +254,7 @@ class Storage:
                     return err, None
         if not has:
             return None, None
-        bound, immediate = [], False
+        bound, delayed, immediate = [], [], False
         for vol in _spec(pod).get("volumes") or []:  # GetPodVolumeClaims
             name, _ = self.claim_name(pod, vol)
             if name is None:
@@ -227,28 +271,193 @@ class Storage:
                     raise Unsupported(f'VolumeBindingMode not set for StorageClass "{cls}" (a PreFilter Error)')
                 delay = mode == "WaitForFirstConsumer"
             if delay and not _spec(pvc).get("volumeName"):
-                raise Unsupported("unbound WaitForFirstConsumer claim: FindPodVolumes' binding search is not restated")
-            immediate = True
+                delayed.append(pvc)  # unboundClaimsDelayBinding
+                continue
+            immediate = True  # "Prebound PVCs are treated as unbound immediate binding"
         if immediate:
             return MSG_UNBOUND_IMMEDIATE, None
-        return None, bound
+        return None, VBClaims(bound, delayed)
 
-    def binding_filter(self, claims, node, node_selector_terms) -> Optional[str]:
-        """VolumeBinding.Filter -> FindPodVolumes -> checkBoundClaims (bound claims in order):
-        a missing PV ends the walk (boundPVsFound false), a PV whose required node affinity does
-        not match the node's labels ends it (boundVolumesSatisfied false)."""
-        if claims is None:
-            return None
+    @staticmethod
+    def _pv_node_ok(pv, node, node_selector_terms) -> bool:
+        """volumeutil.CheckNodeAffinity(pv, node.Labels): the PV's required node selector over a
+        node that carries only the labels."""
+        req = ((_spec(pv).get("nodeAffinity") or {}).get("required"))
+        if req is None:
+            return True
         labels_only = {"metadata": {"labels": dict(_meta(node).get("labels") or {})}}
-        for pvc in claims:
+        return node_selector_terms(req.get("nodeSelectorTerms") or []).match(labels_only)
+
+    @staticmethod
+    def _claim_key(pvc):
+        return (_meta(pvc).get("namespace") or "default", _meta(pvc)["name"])
+
+    def _bound_to(self, pv_name, pvc) -> bool:
+        """IsVolumeBoundToClaim against the assume cache's claimRef."""
+        ref = self.pv_ref.get(pv_name)
+        if ref is None:
+            return False
+        ns, name = self._claim_key(pvc)
+        uid = _meta(pvc).get("uid") or ""
+        return ref[0] == ns and ref[1] == name and (ref[2] == "" or ref[2] == uid)
+
+    def find_matching_volume(self, pvc, node, excluded, node_selector_terms) -> Optional[str]:
+        """pv_helpers.go FindMatchingVolume(claim, pvCache.ListPVs(class), node, chosenPVs,
+        delayBinding=true): a PV bound to the claim is returned (or nothing, if its node
+        affinity fails) wherever it comes; otherwise the smallest available PV that passes every
+        check (ties: the first by name)."""
+        cls = self.pvc_class(pvc)
+        req = storage_bytes(((_spec(pvc).get("resources") or {}).get("requests") or {}).get("storage"))
+        sel = _spec(pvc).get("selector")
+        claim_mode = _spec(pvc).get("volumeMode") or "Filesystem"
+        modes = set(_spec(pvc).get("accessModes") or [])
+        best, best_q = None, None
+        for name in sorted(self.pv):
+            pv = self.pv[name]
+            if self.pv_class(pv) != cls or name in excluded:  # ListPVs(class); excludedVolumes
+                continue
+            if name in self.pv_ref and not self._bound_to(name, pvc):
+                continue
+            q = storage_bytes((_spec(pv).get("capacity") or {}).get("storage"))
+            if q < req:
+                continue
+            if (_spec(pv).get("volumeMode") or "Filesystem") != claim_mode:  # CheckVolumeModeMismatches
+                continue
+            if _meta(pv).get("deletionTimestamp"):
+                continue
+            ok = self._pv_node_ok(pv, node, node_selector_terms)
+            if self._bound_to(name, pvc):
+                return name if ok else None
+            if ((pv.get("status") or {}).get("phase")) != "Available":
+                continue
+            if sel is not None and not self._selector_matches(sel, _meta(pv).get("labels") or {}):
+                continue
+            if not ok:
+                continue
+            if not modes <= set(_spec(pv).get("accessModes") or []):  # CheckAccessModes
+                continue
+            if best is None or q < best_q:
+                best, best_q = name, q
+        return best
+
+    @staticmethod
+    def pv_class(pv) -> str:
+        """storagehelpers.GetPersistentVolumeClass."""
+        ann = _meta(pv).get("annotations") or {}
+        if ANN_BETA_STORAGE_CLASS in ann:
+            return ann[ANN_BETA_STORAGE_CLASS]
+        return _spec(pv).get("storageClassName") or ""
+
+    @staticmethod
+    def _selector_matches(sel, labels) -> bool:
+        """metav1.LabelSelectorAsSelector(...).Matches (a selector that does not parse is a
+        FindMatchingVolume error: a Filter Error status, refused)."""
+        from k8s_oracle import LSel
+        ls = LSel(sel)
+        if getattr(ls, "error", False):
+            raise Unsupported("a claim selector that does not parse (a Filter Error)")
+        return ls.matches(labels)
+
+    def _provisionable(self, pvc, node) -> bool:
+        """checkVolumeProvisions for one claim: a class with a provisioner whose allowedTopologies
+        admit the node (MatchTopologySelectorTerms over the node's labels)."""
+        cls = self.pvc_class(pvc)
+        if not cls or cls not in self.sc:
+            raise Unsupported("an unbound WaitForFirstConsumer claim without a (known) class: a Filter Error")
+        sc = self.sc[cls]
+        prov = sc.get("provisioner") or ""
+        if prov == "" or prov == NOT_SUPPORTED_PROVISIONER:
+            return False
+        terms = sc.get("allowedTopologies") or []
+        if not terms:
+            return True
+        lb = _meta(node).get("labels") or {}
+        return any(all(e.get("key") in lb and lb[e.get("key")] in (e.get("values") or [])
+                       for e in t.get("matchLabelExpressions") or []) for t in terms)
+
+    def find_pod_volumes(self, claims, node, node_selector_terms):
+        """binder.go FindPodVolumes: (reasons, static bindings [(pvc, pv name)], claims to provision)."""
+        bound_ok, pvs_found, unbound_ok = True, True, True
+        bindings, provision = [], []
+        for pvc in claims.bound:  # checkBoundClaims: the first failure ends the walk
             pv = self.pv.get(_spec(pvc).get("volumeName"))
             if pv is None:
-                return MSG_PV_NOT_EXIST
-            req = ((_spec(pv).get("nodeAffinity") or {}).get("required"))
-            if req is not None:  # volumeutil.CheckNodeAffinity(pv, node.Labels)
-                if not node_selector_terms(req.get("nodeSelectorTerms") or []).match(labels_only):
-                    return MSG_NODE_CONFLICT
-        return None
+                pvs_found = False
+                break
+            if not self._pv_node_ok(pv, node, node_selector_terms):
+                bound_ok = False
+                break
+        if claims.delayed:
+            to_match, fast_fail = [], False
+            for pvc in claims.delayed:
+                sel = self.selected.get(self._claim_key(pvc))
+                if sel is not None:
+                    if sel != _meta(node).get("name"):
+                        unbound_ok, fast_fail = False, True
+                        break
+                    provision.append(pvc)
+                else:
+                    to_match.append(pvc)
+            if not fast_fail:
+                if to_match:  # findMatchingVolumes: claims by increasing request (stable)
+                    chosen = set()
+                    for pvc in sorted(to_match, key=lambda c: storage_bytes(
+                            ((_spec(c).get("resources") or {}).get("requests") or {}).get("storage"))):
+                        pv = self.find_matching_volume(pvc, node, chosen, node_selector_terms)
+                        if pv is None:
+                            provision.append(pvc)
+                            unbound_ok = False
+                        else:
+                            chosen.add(pv)
+                            bindings.append((pvc, pv))
+                if provision:  # checkVolumeProvisions: the first claim that cannot be provisioned ends it
+                    unbound_ok = all(self._provisionable(pvc, node) for pvc in provision)
+        reasons = []
+        if not bound_ok:
+            reasons.append(MSG_NODE_CONFLICT)
+        if not unbound_ok:
+            reasons.append(MSG_BIND_CONFLICT)
+        if not pvs_found:
+            reasons.append(MSG_PV_NOT_EXIST)
+        return reasons, bindings, provision
+
+    def binding_filter(self, claims, node, node_selector_terms) -> Optional[str]:
+        """VolumeBinding.Filter -> FindPodVolumes: the status message (the reasons joined with
+        ", "), or None."""
+        if claims is None:
+            return None
+        reasons, _, _ = self.find_pod_volumes(claims, node, node_selector_terms)
+        return ", ".join(reasons) if reasons else None
+
+    def assume(self, claims, node, node_selector_terms):
+        """Reserve -> AssumePodVolumes on the chosen node: the static bindings' PVs get the
+        claim as claimRef, the provisioned claims the node as selected-node."""
+        if claims is None or not claims.delayed:
+            return
+        _, bindings, provision = self.find_pod_volumes(claims, node, node_selector_terms)
+        for pvc, pv in bindings:
+            ns, name = self._claim_key(pvc)
+            self.pv_ref[pv] = (ns, name, _meta(pvc).get("uid") or "")
+        for pvc in provision:
+            self.selected[self._claim_key(pvc)] = _meta(node).get("name")
+
+    def revert(self, claims):
+        """Unreserve -> RevertAssumedPodVolumes: the claims' PVs and the claims back to the
+        informer's (snapshot) objects."""
+        if claims is None:
+            return
+        for pvc in claims.delayed:
+            key = self._claim_key(pvc)
+            for pv, ref in list(self.pv_ref.items()):
+                if (ref[0], ref[1]) == key and self.pv_ref0.get(pv) != ref:
+                    if pv in self.pv_ref0:
+                        self.pv_ref[pv] = self.pv_ref0[pv]
+                    else:
+                        del self.pv_ref[pv]
+            if key in self.selected0:
+                self.selected[key] = self.selected0[key]
+            else:
+                self.selected.pop(key, None)
 
     # ------------------------------------------------------------ VolumeRestrictions
     @staticmethod

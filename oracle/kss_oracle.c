@@ -81,6 +81,8 @@ typedef struct {
   uint64_t* port_used;
   int32_t* vol_count;
   int32_t* vol_attached;
+  int32_t* pv_owner;   /* the binder's assume cache (kss_cluster pv_owner / claim_node) */
+  int32_t* claim_node;
   int32_t cursor; /* the scheduler's nextStartNodeIndex (schedule_one.go findNodesThatPassFilters) */
   /* the scheduling queue's nominator (PodNominator): pods of ps nominated to a node by an earlier
      preemption; a nomination leaves when its pod is assumed (DeleteNominatedPodIfExists) */
@@ -105,9 +107,13 @@ static int ostate_init(ostate* s, const kss_cluster* cl) {
   s->port_used = (uint64_t*)calloc(N ? N : 1, sizeof(uint64_t));
   s->vol_count = (int32_t*)calloc((size_t)cl->n_vol_rows * N + 1, sizeof(int32_t));
   s->vol_attached = (int32_t*)calloc((size_t)cl->n_vol_keys * N + 1, sizeof(int32_t));
+  s->pv_owner = (int32_t*)calloc((size_t)cl->n_pvs + 1, sizeof(int32_t));
+  s->claim_node = (int32_t*)calloc((size_t)cl->n_wclaims + 1, sizeof(int32_t));
   if (!s->requested || !s->nonzero || !s->pod_count || !s->class_count || !s->term_count || !s->port_used ||
-      !s->vol_count || !s->vol_attached)
+      !s->vol_count || !s->vol_attached || !s->pv_owner || !s->claim_node)
     return -1;
+  if (cl->n_pvs) memcpy(s->pv_owner, cl->pv_owner, sizeof(int32_t) * (size_t)cl->n_pvs);
+  if (cl->n_wclaims) memcpy(s->claim_node, cl->claim_node, sizeof(int32_t) * (size_t)cl->n_wclaims);
   if (cl->n_vol_rows) memcpy(s->vol_count, cl->vol_count, sizeof(int32_t) * (size_t)cl->n_vol_rows * N);
   if (cl->n_vol_keys) memcpy(s->vol_attached, cl->vol_attached, sizeof(int32_t) * (size_t)cl->n_vol_keys * N);
   if (cl->port_used) memcpy(s->port_used, cl->port_used, sizeof(uint64_t) * N);
@@ -124,6 +130,8 @@ static int ostate_init(ostate* s, const kss_cluster* cl) {
   s->c.port_used = s->port_used;
   s->c.vol_count = s->vol_count;
   s->c.vol_attached = s->vol_attached;
+  s->c.pv_owner = s->pv_owner;
+  s->c.claim_node = s->claim_node;
   return 0;
 }
 
@@ -136,6 +144,8 @@ static void ostate_free(ostate* s) {
   free(s->port_used);
   free(s->vol_count);
   free(s->vol_attached);
+  free(s->pv_owner);
+  free(s->claim_node);
   free(s->nom_active);
 }
 
@@ -411,6 +421,96 @@ static int limit_check(const kss_cluster* cl, uint32_t en, int key, int n, int64
   return (int64_t)cl->vol_attached[(size_t)key * N + n] + newc > (int64_t)lim ? pl : 0;
 }
 
+static int is_vb(int k) { return k == KSS_VOL_BIND_AFFINITY || k == KSS_VOL_BIND_PV_MISSING || k == KSS_VOL_BIND_WFFC; }
+
+/* pv_helpers.go FindMatchingVolume (delayBinding, scheduler path) for delayed claim entry v on node
+   n over its candidates (ints triplets {pv, term_off, term_len}, smallest capacity first, then
+   name; the host applied every node-independent check): the PV bound to the claim (claimRef or
+   assumed: pv_owner == key + 1) answers wherever it comes -- itself if its node affinity holds,
+   else nothing; otherwise the first available candidate not among chosen[0, nch) whose node
+   affinity holds.  -1: no match. */
+static int pv_affinity_ok(const kss_cluster* cl, const kss_podset* ps, const kss_vol* v, int i, int n) {
+  int ta = ps->ints[v->a + 3 * i + 1], tb = ps->ints[v->a + 3 * i + 2];
+  if (tb < 0) return 1; /* CheckNodeAffinity: no required node affinity */
+  for (int t = 0; t < tb; t++)
+    if (term_matches(cl, ps, &ps->terms[ta + t], n)) return 1;
+  return 0;
+}
+static int find_matching_volume(const kss_cluster* cl, const kss_podset* ps, const kss_vol* v, const int* chosen, int nch,
+                                int n) {
+  for (int i = 0; i < v->b; i++) { /* excludedVolumes come first: a PV an earlier claim took is skipped */
+    int pv = ps->ints[v->a + 3 * i], taken = 0;
+    for (int k = 0; k < nch; k++) taken |= chosen[k] == pv;
+    if (!taken && cl->pv_owner[pv] == v->key + 1) return pv_affinity_ok(cl, ps, v, i, n) ? pv : -1;
+  }
+  for (int i = 0; i < v->b; i++) {
+    int pv = ps->ints[v->a + 3 * i], taken = 0;
+    if (cl->pv_owner[pv] != 0) continue; /* claimRef set to another claim */
+    for (int k = 0; k < nch; k++) taken |= chosen[k] == pv;
+    if (!taken && pv_affinity_ok(cl, ps, v, i, n)) return pv;
+  }
+  return -1;
+}
+
+/* binder.go FindPodVolumes over VolumeBinding entries [e0, e1) of the pod on node n: -1 when
+   satisfied, else the KSS_VB_* detail.  pick (optional, one per BIND_WFFC entry): the static
+   binding's PV, -1 for a claim to provision. */
+static int find_pod_volumes(const kss_cluster* cl, const kss_podset* ps, int e0, int e1, int n, int* pick) {
+  int bound = 0; /* checkBoundClaims: 1 node conflict, 2 PV not found; the first failure ends it */
+  for (int e = e0; e < e1 && !bound; e++) {
+    const kss_vol* v = &ps->vols[e];
+    if (v->kind == KSS_VOL_BIND_PV_MISSING) {
+      bound = 2;
+    } else if (v->kind == KSS_VOL_BIND_AFFINITY) {
+      int ok = 0;
+      for (int t = 0; t < v->b && !ok; t++) ok = term_matches(cl, ps, &ps->terms[v->a + t], n);
+      if (!ok) bound = 1;
+    }
+  }
+  int unbound_ok = 1;
+  for (int e = e0; e < e1 && unbound_ok; e++) /* claims whose selected-node annotation names another node */
+    if (ps->vols[e].kind == KSS_VOL_BIND_WFFC) {
+      int sel = cl->claim_node[ps->vols[e].key];
+      if (sel != -1 && sel != n) unbound_ok = 0;
+    }
+  if (unbound_ok) {
+    int chosen[KSS_MAX_WFFC], nch = 0, wi = 0, to_prov[KSS_MAX_WFFC] = {0, 0, 0, 0}, any = 0;
+    for (int e = e0; e < e1; e++) { /* findMatchingVolumes: entries come by increasing request */
+      const kss_vol* v = &ps->vols[e];
+      if (v->kind != KSS_VOL_BIND_WFFC) continue;
+      int m = -1;
+      if (cl->claim_node[v->key] == -1) {
+        m = find_matching_volume(cl, ps, v, chosen, nch, n);
+        if (m >= 0) chosen[nch++] = m;
+        else unbound_ok = 0;
+      }
+      if (m < 0) to_prov[wi] = any = 1;
+      if (pick) pick[wi] = m;
+      wi++;
+    }
+    if (any) { /* checkVolumeProvisions: a provisioner whose class's allowedTopologies admit the node */
+      unbound_ok = 1;
+      wi = 0;
+      for (int e = e0; e < e1 && unbound_ok; e++) {
+        const kss_vol* v = &ps->vols[e];
+        if (v->kind != KSS_VOL_BIND_WFFC) continue;
+        if (to_prov[wi]) {
+          if (!(v->count & 1)) {
+            unbound_ok = 0;
+          } else if ((v->count >> 1) > 0) {
+            int ok = 0;
+            for (int t = 0; t < (v->count >> 1) && !ok; t++) ok = term_matches(cl, ps, &ps->terms[v->row + t], n);
+            unbound_ok = ok;
+          }
+        }
+        wi++;
+      }
+    }
+  }
+  if (!unbound_ok) return bound == 1 ? KSS_VB_NODE_BIND : (bound == 2 ? KSS_VB_BIND_PV_NOT_EXIST : KSS_VB_BIND_CONFLICT);
+  return bound == 1 ? KSS_VB_NODE_CONFLICT : (bound == 2 ? KSS_VB_PV_NOT_EXIST : -1);
+}
+
 static int volume_filters(const kss_cluster* cl, const kss_podset* ps, const kss_pod* p, uint32_t en, int n,
                           uint16_t* detail) {
   size_t N = (size_t)cl->n_nodes;
@@ -436,20 +536,17 @@ static int volume_filters(const kss_cluster* cl, const kss_podset* ps, const kss
         newc += cl->vol_count[(size_t)v->row * N + n] == 0 ? 1 : 0; /* delete(newVolumes, attached) */
       else
         newc += v->count;
-    } else if (v->kind == KSS_VOL_BIND_AFFINITY) {
+    } else if (is_vb(v->kind)) { /* VolumeBinding: its consecutive entries as one FindPodVolumes */
+      int e1 = e + 1;
+      while (e1 < p->vol_len && is_vb(ps->vols[p->vol_off + e1].kind)) e1++;
       if ((en >> KSS_F_VOLUME_BINDING) & 1u) {
-        int ok = 0;
-        for (int t = 0; t < v->b && !ok; t++) ok = term_matches(cl, ps, &ps->terms[v->a + t], n);
-        if (!ok) {
-          *detail = KSS_VB_NODE_CONFLICT;
+        int d = find_pod_volumes(cl, ps, p->vol_off + e, p->vol_off + e1, n, NULL);
+        if (d >= 0) {
+          *detail = (uint16_t)d;
           return KSS_F_VOLUME_BINDING;
         }
       }
-    } else if (v->kind == KSS_VOL_BIND_PV_MISSING) {
-      if ((en >> KSS_F_VOLUME_BINDING) & 1u) {
-        *detail = KSS_VB_PV_NOT_EXIST;
-        return KSS_F_VOLUME_BINDING;
-      }
+      e = e1 - 1;
     } else if (v->kind == KSS_VOL_ZONE) {
       if (((en >> KSS_F_VOLUME_ZONE) & 1u) && zone_node)
         for (int k = 0; k < v->b; k++)
@@ -1220,6 +1317,24 @@ static void commit(ostate* s, const kss_podset* ps, int pi, int node_local) {
       s->vol_attached[(size_t)v->key * N + node_local] += v->count;
     }
   }
+  /* Reserve's AssumePodVolumes: the delayed claims' static bindings and provisioning on this node */
+  int e0 = -1, e1 = -1;
+  for (int e = 0; e < p->vol_len; e++)
+    if (is_vb(ps->vols[p->vol_off + e].kind)) {
+      if (e0 < 0) e0 = p->vol_off + e;
+      e1 = p->vol_off + e + 1;
+    }
+  if (e0 >= 0) {
+    int pick[KSS_MAX_WFFC] = {-1, -1, -1, -1}, wi = 0;
+    find_pod_volumes(&s->c, ps, e0, e1, node_local, pick);
+    for (int e = e0; e < e1; e++) {
+      const kss_vol* v = &ps->vols[e];
+      if (v->kind != KSS_VOL_BIND_WFFC) continue;
+      if (pick[wi] >= 0) s->pv_owner[pick[wi]] = v->key + 1;
+      else s->claim_node[v->key] = node_local;
+      wi++;
+    }
+  }
 }
 
 /* ---------------------------------------------------------------------------
@@ -1276,12 +1391,34 @@ int kss_oracle_schedule_c(const kss_profile* prof, const kss_cluster* cl, const 
                                NULL, NULL, 0, NULL);
 }
 
+/* kss_oracle_schedule_n with the binder's assume cache after the batch (out_pv_owner [n_pvs],
+   out_claim_node [n_wclaims]; NULL: not wanted). */
+int kss_oracle_schedule_w(const kss_profile* prof, const kss_cluster* cl, const kss_podset* ps, int n,
+                          int32_t* chosen, kss_pod_result* results, int threads, int64_t* out_requested,
+                          int64_t* out_nonzero, int32_t* out_pod_count, int32_t* out_class_count,
+                          int32_t* out_term_count, uint64_t* out_port_used, int32_t* out_vol_count,
+                          int32_t* out_vol_attached, int32_t* cursor, const int32_t* nom_pod,
+                          const int32_t* nom_node, int32_t n_nom, uint8_t* nom_left, int32_t* out_pv_owner,
+                          int32_t* out_claim_node);
+
 int kss_oracle_schedule_n(const kss_profile* prof, const kss_cluster* cl, const kss_podset* ps, int n,
                           int32_t* chosen, kss_pod_result* results, int threads, int64_t* out_requested,
                           int64_t* out_nonzero, int32_t* out_pod_count, int32_t* out_class_count,
                           int32_t* out_term_count, uint64_t* out_port_used, int32_t* out_vol_count,
                           int32_t* out_vol_attached, int32_t* cursor, const int32_t* nom_pod,
                           const int32_t* nom_node, int32_t n_nom, uint8_t* nom_left) {
+  return kss_oracle_schedule_w(prof, cl, ps, n, chosen, results, threads, out_requested, out_nonzero, out_pod_count,
+                               out_class_count, out_term_count, out_port_used, out_vol_count, out_vol_attached, cursor,
+                               nom_pod, nom_node, n_nom, nom_left, NULL, NULL);
+}
+
+int kss_oracle_schedule_w(const kss_profile* prof, const kss_cluster* cl, const kss_podset* ps, int n,
+                          int32_t* chosen, kss_pod_result* results, int threads, int64_t* out_requested,
+                          int64_t* out_nonzero, int32_t* out_pod_count, int32_t* out_class_count,
+                          int32_t* out_term_count, uint64_t* out_port_used, int32_t* out_vol_count,
+                          int32_t* out_vol_attached, int32_t* cursor, const int32_t* nom_pod,
+                          const int32_t* nom_node, int32_t n_nom, uint8_t* nom_left, int32_t* out_pv_owner,
+                          int32_t* out_claim_node) {
   ostate s;
   if (ostate_init(&s, cl)) return KSS_E_NOMEM;
   if (cursor) s.cursor = *cursor;
@@ -1320,6 +1457,8 @@ int kss_oracle_schedule_n(const kss_profile* prof, const kss_cluster* cl, const 
   if (out_vol_attached && cl->n_vol_keys)
     memcpy(out_vol_attached, s.vol_attached, sizeof(int32_t) * (size_t)cl->n_vol_keys * N);
   if (cursor) *cursor = s.cursor;
+  if (out_pv_owner && cl->n_pvs) memcpy(out_pv_owner, s.pv_owner, sizeof(int32_t) * (size_t)cl->n_pvs);
+  if (out_claim_node && cl->n_wclaims) memcpy(out_claim_node, s.claim_node, sizeof(int32_t) * (size_t)cl->n_wclaims);
   if (nom_left)
     for (int j = 0; j < n_nom; j++) nom_left[j] = s.nom_active[j];
   free(nn_local);

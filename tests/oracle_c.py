@@ -30,6 +30,8 @@ def lib():
         _lib.kss_oracle_schedule_n.argtypes = _lib.kss_oracle_schedule_c.argtypes + [
             P(C.c_int32), P(C.c_int32), C.c_int32, P(C.c_uint8)]
         _lib.kss_oracle_schedule_n.restype = C.c_int
+        _lib.kss_oracle_schedule_w.argtypes = _lib.kss_oracle_schedule_n.argtypes + [P(C.c_int32), P(C.c_int32)]
+        _lib.kss_oracle_schedule_w.restype = C.c_int
         _lib.kss_oracle_eval_pod.argtypes = [P(abi.Profile), P(abi.Cluster), P(abi.PodSet), C.c_int,
                                              P(abi.PodResult), C.c_int]
         _lib.kss_oracle_eval_pod.restype = C.c_int
@@ -109,14 +111,16 @@ def schedule(profile, cluster_struct, podset_struct, n_pods, n_nodes, threads=1,
               pod_count=np.zeros(N, np.int32), class_count=np.zeros((max(n_classes, 1), N), np.int32),
               term_count=np.zeros((max(n_terms, 1), N), np.int32), port_used=np.zeros(N, np.uint64),
               vol_count=np.zeros((max(cluster_struct.n_vol_rows, 1), N), np.int32),
-              vol_attached=np.zeros((max(cluster_struct.n_vol_keys, 1), N), np.int32))
+              vol_attached=np.zeros((max(cluster_struct.n_vol_keys, 1), N), np.int32),
+              pv_owner=np.zeros(max(cluster_struct.n_pvs, 1), np.int32),
+              claim_node=np.zeros(max(cluster_struct.n_wclaims, 1), np.int32))
     P = C.POINTER
     cur = C.c_int32(cursor)
     nominations = list(nominations)
     nom_pod = np.array([a for a, _ in nominations] or [0], dtype=np.int32)
     nom_node = np.array([b for _, b in nominations] or [0], dtype=np.int32)
     nom_left = np.zeros(max(len(nominations), 1), dtype=np.uint8)
-    rc = L.kss_oracle_schedule_n(C.byref(profile), C.byref(cluster_struct), C.byref(podset_struct), n_pods,
+    rc = L.kss_oracle_schedule_w(C.byref(profile), C.byref(cluster_struct), C.byref(podset_struct), n_pods,
                                chosen.ctypes.data_as(P(C.c_int32)), res.structs if res else None, threads,
                                st["requested"].ctypes.data_as(P(C.c_int64)), st["nonzero"].ctypes.data_as(P(C.c_int64)),
                                st["pod_count"].ctypes.data_as(P(C.c_int32)),
@@ -126,8 +130,11 @@ def schedule(profile, cluster_struct, podset_struct, n_pods, n_nodes, threads=1,
                                st["vol_count"].ctypes.data_as(P(C.c_int32)),
                                st["vol_attached"].ctypes.data_as(P(C.c_int32)), C.byref(cur),
                                nom_pod.ctypes.data_as(P(C.c_int32)), nom_node.ctypes.data_as(P(C.c_int32)),
-                               len(nominations), nom_left.ctypes.data_as(P(C.c_uint8)))
+                               len(nominations), nom_left.ctypes.data_as(P(C.c_uint8)),
+                               st["pv_owner"].ctypes.data_as(P(C.c_int32)), st["claim_node"].ctypes.data_as(P(C.c_int32)))
     assert rc == 0, f"oracle rc={rc}"
+    st["pv_owner"] = st["pv_owner"][:cluster_struct.n_pvs]
+    st["claim_node"] = st["claim_node"][:cluster_struct.n_wclaims]
     st["next_start"] = cur.value
     st["nominations"] = [e for e, keep in zip(nominations, nom_left) if keep]
     st["vol_count"] = st["vol_count"][:cluster_struct.n_vol_rows, :n_nodes]

@@ -156,3 +156,81 @@ def test_refusals():
     with pytest.raises(native.KssError, match="volumes"):
         ctx.postfilter_pod(ps, j)
     ctx.close()
+
+
+def _binding_equal(ctx, fin):
+    po, cn = ctx.binding_state()
+    np.testing.assert_array_equal(po, fin["pv_owner"])
+    np.testing.assert_array_equal(cn, fin["claim_node"])
+
+
+@pytest.mark.parametrize("seed,n_nodes,flags", [(100, 12, 0), (103, 12, 0), (105, 12, abi.KSS_SCHED_FORCE_MULTI_WG),
+                                                (108, 12, 0), (111, 12, 0), (114, 300, 0)])
+def test_random_wffc_clusters_match_oracle(seed, n_nodes, flags):
+    """Unbound WaitForFirstConsumer claims (binder.go FindPodVolumes / AssumePodVolumes) on random
+    clusters against the C oracle: every verdict and detail (bind conflicts, the joined node + bind
+    reason), choice and total, the vol_count / vol_attached state and the assume cache the batch
+    leaves (pv_owner, claim_node) -- on one shard and on several (every shard applies the assume)."""
+    nodes, bound, pods, st = volume_fuzz.make(seed, n_nodes=n_nodes, n_bound=max(16, n_nodes), wffc=True)
+    cc, cp, _ = compile_cluster(nodes, bound, pods, storage=st)
+    assert cc.wclaims
+    ch_o, res, fin = _oracle(cc, cp)
+    ctx = native.Context(abi.default_profile(), max_pods_record=cp.n)
+    ctx.load(cc.as_struct())
+    chosen = ctx.schedule_batch(cp.as_struct(), cp.n, record=True, flags=flags)
+    if flags:
+        assert ctx.last_geometry()["shards"] > 1
+    np.testing.assert_array_equal(chosen, ch_o)
+    N = cc.n_nodes
+    for j in range(cp.n):
+        r = ctx.fetch_record(j)
+        np.testing.assert_array_equal(r.fail_plugin[:N], res.fail_plugin[j], err_msg=f"pod {j}")
+        np.testing.assert_array_equal(r.fail_detail[:N], res.fail_detail[j], err_msg=f"pod {j}")
+        if r.scored:
+            feas = res.fail_plugin[j] == 0
+            np.testing.assert_array_equal(r.total[feas], res.total[j][feas], err_msg=f"pod {j}")
+    vc, va = ctx.volume_state()
+    np.testing.assert_array_equal(vc, fin["vol_count"])
+    np.testing.assert_array_equal(va, fin["vol_attached"])
+    _binding_equal(ctx, fin)
+    ctx.reset()  # the snapshot's assume cache back
+    po, cn = ctx.binding_state()
+    np.testing.assert_array_equal(po, cc.arrays["pv_owner"][:len(cc.pvs)])
+    np.testing.assert_array_equal(cn, cc.arrays["claim_node"][:len(cc.wclaims)])
+    ctx.close()
+
+
+def test_wffc_per_pod_commit_rollback_and_service():
+    """The drop-in's per-pod shape with WaitForFirstConsumer claims: kss_eval_pod + kss_commit
+    (Reserve's AssumePodVolumes through k_wffc_commit) pod after pod equals the batch oracle and
+    its assume cache; kss_rollback in reverse (RevertAssumedPodVolumes) restores the snapshot's;
+    the resident service grid (eval + queued commits, every shard applying the assume) does the same."""
+    nodes, bound, pods, st = volume_fuzz.make(100, wffc=True)
+    cc, cp, _ = compile_cluster(nodes, bound, pods, storage=st)
+    ps = cp.as_struct()
+    ch_o, _, fin = _oracle(cc, cp, record="meta")
+    ctx = native.Context(abi.default_profile())
+    ctx.load(cc.as_struct())
+    done = []
+    for j in range(cp.n):
+        r = ctx.eval_pod(ps, j)
+        assert r.chosen == ch_o[j], j
+        if r.chosen >= 0:
+            ctx.commit(ps, j, r.chosen)
+            done.append((j, r.chosen))
+    _binding_equal(ctx, fin)
+    for j, n in reversed(done):
+        ctx.rollback(ps, j, n)
+    po, cn = ctx.binding_state()
+    np.testing.assert_array_equal(po, cc.arrays["pv_owner"][:len(cc.pvs)])
+    np.testing.assert_array_equal(cn, cc.arrays["claim_node"][:len(cc.wclaims)])
+    ctx.reset()
+    ctx.stage(ps)
+    for j in range(cp.n):
+        v = ctx.service_eval(j)
+        assert v.chosen == ch_o[j], j
+        if v.chosen >= 0:
+            ctx.service_commit(j, v.chosen)
+    ctx.service_stop()
+    _binding_equal(ctx, fin)
+    ctx.close()

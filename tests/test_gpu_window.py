@@ -115,11 +115,12 @@ def test_k_simple_window_geometries(pct, geometry):
     grid (32 shards, per-wave mode), the unrestricted one (40 shards), one shard (no exchange, the
     cut ranked locally, per-thread mode), three shards of 1,667 nodes (per-thread mode), and several
     chunk launches (KSS static budget: 7 launches hand nextStartNodeIndex on through the device
-    word).  The batch starts at a set cursor; two runs."""
-    n_nodes, n_pods = 5000, 1500
+    word).  The batch starts at a set cursor; two runs.  (One shard: 2,500 nodes, k_simple's largest shard
+    is 3,072.)"""
+    n_nodes, n_pods = (2500 if geometry == "one_shard" else 5000), 1500  # one k_simple shard: <= 3,072 nodes
     prof = _prof(pct)
     s = native.Synth(2, SEED_BASE + 2, n_nodes, n_pods)
-    ch_o, res, st = _oracle(prof, s.cluster, s.pods, n_pods, n_nodes, record="meta", cursor=4321)
+    ch_o, res, st = _oracle(prof, s.cluster, s.pods, n_pods, n_nodes, record="meta", cursor=2321)
     if geometry == "unrestricted":
         native.set_option("xcd", 0)
     elif geometry == "one_shard":
@@ -133,7 +134,7 @@ def test_k_simple_window_geometries(pct, geometry):
     ctx.stage(s.pods)
     for rep in range(2):
         ctx.reset()
-        ctx.set_next_start_node_index(4321)
+        ctx.set_next_start_node_index(2321)
         chosen = ctx.run_staged(n_pods)
         assert ctx.last_kernel() == "k_simple"
         want_shards = {"xcd_local": 32, "unrestricted": 40, "one_shard": 1, "three_shards": 3}.get(geometry)

@@ -50,7 +50,8 @@ def test_every_volume_reason_is_covered():
             st = (exp.get("extra") or {}).get("scheduler-simulator/prefilter-result-status")
             if st:
                 pre.add(st["VolumeBinding"])
-    for msg in (vf.M_DISK, vf.M_MAXVOL, vf.M_VB_CONFLICT, vf.M_VB_NOPV, vf.M_ZONE):
+    for msg in (vf.M_DISK, vf.M_MAXVOL, vf.M_VB_CONFLICT, vf.M_VB_NOPV, vf.M_ZONE, vf.M_VB_BIND,
+                vf.M_VB_CONFLICT + ", " + vf.M_VB_BIND):
         assert msg in seen, msg
     assert vf.M_UNBOUND in pre
     plugins = {f[0] for fx in vf.FIXTURES.values() for exp in fx()[3] for f in exp["filter"].values() if f}
@@ -103,9 +104,16 @@ def test_intree_rbd_provisioner_is_not_a_csi_driver():
 def test_refusals():
     nodes = [ef.node("a")]
     wffc = {"metadata": {"name": "late"}, "provisioner": "x", "volumeBindingMode": "WaitForFirstConsumer"}
-    st = vf.storage(pvcs=[vf.pvc("u", bound=False, sc="late")], scs=[wffc])
-    with pytest.raises(Unsupported, match="WaitForFirstConsumer"):
-        compile_cluster(nodes, [], [vf.vpod("p", vf.claim("u"))], storage=st)
+    claims = [vf.pvc(f"u{i}", bound=False, sc="late") for i in range(abi.KSS_MAX_WFFC + 1)]
+    st = vf.storage(pvcs=claims, scs=[wffc])
+    compile_cluster(nodes, [], [vf.vpod("p", *[vf.claim(f"u{i}") for i in range(abi.KSS_MAX_WFFC)])], storage=st)
+    with pytest.raises(Unsupported, match="WaitForFirstConsumer"):  # one delayed claim too many
+        compile_cluster(nodes, [], [vf.vpod("p", *[vf.claim(f"u{i}") for i in range(abi.KSS_MAX_WFFC + 1)])],
+                        storage=st)
+    twice = vf.storage(pvs=[vf.wpv("x", 1, "late", claim_ref="u0"), vf.wpv("y", 1, "late", claim_ref="u0")],
+                       pvcs=claims, scs=[wffc])
+    with pytest.raises(Unsupported, match="pre-bound"):
+        compile_cluster(nodes, [], [vf.vpod("p", vf.claim("u0"))], storage=twice)
     mig = [{"metadata": {"name": "a", "annotations": {"storage.alpha.kubernetes.io/migrated-plugins":
                                                       "kubernetes.io/aws-ebs"}}, "spec": {"drivers": []}}]
     with pytest.raises(Unsupported, match="migrated"):
@@ -157,3 +165,67 @@ def test_plan_names_volumes():
     cc, cp, _ = compile_cluster(nodes, bound, pods, storage=st)
     plan = native.plan_podset(cc.as_struct(), cp.as_struct())
     assert plan["kernel"] == "k_schedule" and "volumes" in plan["reason"], plan
+
+
+def test_wffc_assume_cache_final_state():
+    """Both oracles end the WaitForFirstConsumer fixture with the hand-derived assume cache: each
+    claim's static binding (pv_owner) and the provisioned claim's selected node (claim_node)."""
+    import oracle_c
+    nodes, bound, pods, _, st = vf.fx_wait_for_first_consumer()
+    cc, cp, _ = compile_cluster(nodes, bound, pods, storage=st)
+    _, _, fs = oracle_c.schedule(abi.default_profile(), cc.as_struct(), cp.as_struct(), cp.n, cc.n_nodes,
+                                 record=False, n_classes=len(cc.classes), n_terms=len(cc.terms))
+    claim_of = {i + 1: name for i, (_, name) in enumerate(cc.wclaims)}
+    got = {claim_of[o]: cc.pvs[v] for v, o in enumerate(fs["pv_owner"]) if o}
+    assert got == vf.WFFC_FINAL_BINDINGS
+    sel = {cc.wclaims[c][1]: cc.node_names[n] for c, n in enumerate(fs["claim_node"]) if n >= 0}
+    assert sel == vf.WFFC_FINAL_SELECTED
+    o = _oracle(nodes, bound, st)
+    for p in pods:
+        o.schedule_one(p)
+    assert {ref[1]: pv for pv, ref in o.storage.pv_ref.items()} == vf.WFFC_FINAL_BINDINGS
+    assert o.storage.selected == {("default", k): v for k, v in vf.WFFC_FINAL_SELECTED.items()}
+
+
+@pytest.mark.parametrize("seed", range(16))
+def test_oracles_agree_on_random_wffc_clusters(seed):
+    """WaitForFirstConsumer claims on random clusters (tests/volume_fuzz.py wffc=True): the object
+    oracle's FindPodVolumes / AssumePodVolumes and the C oracle over the compiled candidate lists
+    agree pod after pod, and on the assume cache they leave."""
+    import oracle_c
+    import volume_fuzz
+    nodes, bound, pods, st = volume_fuzz.make(100 + seed, wffc=True)
+    cc, cp, chosen, res = run_both(nodes, bound, pods, storage=st)
+    assert cc.wclaims and cp.n_vols > 0
+    _, _, fs = oracle_c.schedule(abi.default_profile(), cc.as_struct(), cp.as_struct(), cp.n, cc.n_nodes,
+                                 record=False, n_classes=len(cc.classes), n_terms=len(cc.terms))
+    o = _oracle(nodes, bound, st)
+    for p in pods:
+        o.schedule_one(p)
+    claim_of = {i + 1: name for i, (_, name) in enumerate(cc.wclaims)}
+    got = {cc.pvs[v]: claim_of[int(x)] for v, x in enumerate(fs["pv_owner"]) if x}
+    want = {pv: ref[1] for pv, ref in o.storage.pv_ref.items() if pv in set(cc.pvs)}
+    assert got == want
+    sel = {cc.wclaims[c][1]: int(n) for c, n in enumerate(fs["claim_node"]) if n != -1}
+    want_sel = {k[1]: (cc.node_names.index(v) if v in cc.node_names else -2) for k, v in o.storage.selected.items()
+                if k in set(cc.wclaims)}
+    assert sel == want_sel
+
+
+def test_random_wffc_clusters_reach_every_branch():
+    """Across the seeds the WaitForFirstConsumer fuzz reaches bind conflicts, the combined node +
+    bind conflict reason, static bindings and provisioning (both assume-cache columns move)."""
+    import oracle_c
+    import volume_fuzz
+    details, moved_pv, moved_claim = set(), False, False
+    for seed in range(16):
+        nodes, bound, pods, st = volume_fuzz.make(100 + seed, wffc=True)
+        cc, cp, _ = compile_cluster(nodes, bound, pods, storage=st)
+        ch, res, fs = oracle_c.schedule(abi.default_profile(), cc.as_struct(), cp.as_struct(), cp.n, cc.n_nodes,
+                                        record=True, n_classes=len(cc.classes), n_terms=len(cc.terms))
+        vb = res.fail_plugin == abi.KSS_F_VOLUME_BINDING
+        details |= {int(d) for d in res.fail_detail[vb]}
+        moved_pv |= bool((fs["pv_owner"] != cc.arrays["pv_owner"][:len(cc.pvs)]).any())
+        moved_claim |= bool((fs["claim_node"] != cc.arrays["claim_node"][:len(cc.wclaims)]).any())
+    assert {abi.KSS_VB_BIND_CONFLICT} <= details, details
+    assert moved_pv and moved_claim

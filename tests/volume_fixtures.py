@@ -24,6 +24,7 @@ M_VB_CONFLICT = "node(s) had volume node affinity conflict"       # volumebindin
 M_VB_NOPV = "node(s) unavailable due to one or more pvc(s) bound to non-existent pv(s)"  # ErrReasonPVNotExist
 M_ZONE = "node(s) had no available volume zone"                   # volume_zone.go ErrReasonConflict
 M_UNBOUND = "pod has unbound immediate PersistentVolumeClaims"
+M_VB_BIND = "node(s) didn't find available persistent volumes to bind"  # volumebinding ErrReasonBindConflict
 
 
 def vpod(name, *volumes, node_name=None):
@@ -244,10 +245,96 @@ def fx_volume_zone():
     return nodes, [], pods, expect, st
 
 
+# --------------------------------------------------------------------------------------
+# VolumeBinding for unbound WaitForFirstConsumer claims (binder.go FindPodVolumes, v1.26):
+# claims selected for another node (volume.kubernetes.io/selected-node) fail at once; the others
+# go by increasing request (findMatchingVolumes) to FindMatchingVolume -- a PV pre-bound to the
+# claim (claimRef) answers by its node affinity alone, else the smallest Available PV of the class
+# with enough capacity, the claim's access modes, a matching node affinity, and not chosen by an
+# earlier claim of the pod or bound (assumed) to another claim; claims left over must be
+# provisionable (checkVolumeProvisions: a provisioner other than kubernetes.io/no-provisioner whose
+# class's allowedTopologies admit the node).  Reserve's AssumePodVolumes then binds the chosen PVs
+# to the claims and marks provisioned claims selected for the node, which later pods see.
+# Reasons: node conflict (bound claims) before bind conflict, joined with ", ".
+GI = 1 << 30
+
+
+def wpv(name, gib, sc, zone=None, claim_ref=None):
+    spec = {"capacity": {"storage": f"{gib}Gi"}, "storageClassName": sc, "accessModes": ["ReadWriteOnce"],
+            "local": {"path": "/mnt/" + name}}
+    if zone is not None:
+        spec["nodeAffinity"] = {"required": {"nodeSelectorTerms": [
+            {"matchExpressions": [{"key": ZONE, "operator": "In", "values": [zone]}]}]}}
+    if claim_ref is not None:
+        spec["claimRef"] = {"namespace": "default", "name": claim_ref}
+    return {"metadata": {"name": name}, "spec": spec, "status": {"phase": "Available"}}
+
+
+def wpvc(name, gib, sc):
+    return {"metadata": {"name": name, "namespace": "default"},
+            "spec": {"storageClassName": sc, "accessModes": ["ReadWriteOnce"],
+                     "resources": {"requests": {"storage": f"{gib}Gi"}}}}
+
+
+def wsc(name, provisioner, zones=None):
+    sc = {"metadata": {"name": name}, "provisioner": provisioner, "volumeBindingMode": "WaitForFirstConsumer"}
+    if zones is not None:
+        sc["allowedTopologies"] = [{"matchLabelExpressions": [{"key": ZONE, "values": list(zones)}]}]
+    return sc
+
+
+def fx_wait_for_first_consumer():
+    nodes = [node("a", zone="zone-a"), node("b", zone="zone-b"), node("c", zone="zone-c")]
+    za = [{"matchExpressions": [{"key": ZONE, "operator": "In", "values": ["zone-a"]}]}]
+    st = storage(
+        pvs=[wpv("pv-a-5", 5, "local", "zone-a"), wpv("pv-a-10", 10, "local", "zone-a"),
+             wpv("pv-b-20", 20, "local", "zone-b"), wpv("pv-c-8", 8, "local", "zone-c"),
+             wpv("pv-pre", 1, "local", "zone-a", claim_ref="l-pre"), wpv("pv-w-3", 3, "wffc", "zone-c"),
+             wpv("pv2-a-6", 6, "local2", "zone-a"), wpv("pv2-a-7", 7, "local2", "zone-a"),
+             wpv("pv2-b-7", 7, "local2", "zone-b"), pv("pv-za", affinity_terms=za)],
+        pvcs=[wpvc("l-4", 4, "local"), wpvc("l-4b", 4, "local"), wpvc("l-9", 9, "local"), wpvc("l-15", 15, "local"),
+              wpvc("d-1", 1, "wffc-b"), wpvc("w-2", 2, "wffc"), wpvc("l-pre", 1, "local"), wpvc("x-7", 7, "local2"),
+              wpvc("x-6", 6, "local2"), pvc("c-za", "pv-za")],
+        scs=[wsc("local", "kubernetes.io/no-provisioner"), wsc("local2", "kubernetes.io/no-provisioner"),
+             wsc("wffc", "csi.example.com"), wsc("wffc-b", "csi.example.com", zones=["zone-b"])])
+    pods = [vpod("p1", claim("l-4")),     # every node has a PV (a: pv-a-5, the smallest); a (ties)
+            vpod("p2", claim("l-4b")),    # a: pv-a-5 taken, pv-a-10; b: pv-b-20; c: pv-c-8; b (a has p1)
+            vpod("p3", claim("l-9")),     # 9Gi: pv-a-10 on a; b's pv-b-20 is p2's: no PV, no provisioner
+            vpod("p4", claim("l-15")),    # only pv-b-20 is large enough, and it is taken: nowhere
+            vpod("p5", claim("d-1")),     # no PV: provisioned where wffc-b's topology allows, b
+            vpod("p6", claim("d-1")),     # d-1 is now selected for b: the other nodes fail at once
+            vpod("p7", claim("w-2")),     # pv-w-3 on c, provisioning elsewhere (no topology); c (no pods)
+            vpod("p8", claim("l-pre")),   # pv-pre is pre-bound: only its zone-a node, though pv-c-8 is free
+            vpod("p9", claim("c-za"), claim("l-15")),  # bound pv-za (zone-a) and an impossible claim
+            vpod("p10", claim("x-7"), claim("x-6"))]   # x-6 first: a gets pv2-a-6 + pv2-a-7; b's pv2-b-7 once
+    B = ("VolumeBinding", M_VB_BIND)
+    NB = ("VolumeBinding", M_VB_CONFLICT + ", " + M_VB_BIND)
+    expect = [
+        {"filter": _all("abc"), "selected": "a"},
+        {"filter": _all("abc"), "selected": "b"},
+        {"filter": {"a": None, "b": B, "c": B}, "selected": "a"},
+        {"filter": _all("abc", B), "selected": ""},
+        {"filter": {"a": B, "b": None, "c": B}, "selected": "b"},
+        {"filter": {"a": B, "b": None, "c": B}, "selected": "b"},
+        {"filter": _all("abc"), "selected": "c"},           # pods: a 2, b 3, c 0
+        {"filter": {"a": None, "b": B, "c": B}, "selected": "a"},
+        {"filter": {"a": B, "b": NB, "c": NB}, "selected": ""},
+        {"filter": {"a": None, "b": B, "c": B}, "selected": "a"},
+    ]
+    return nodes, [], pods, expect, st
+
+
+# the assume cache after the fixture's pods (claim -> its PV; claims selected for a node)
+WFFC_FINAL_BINDINGS = {"l-4": "pv-a-5", "l-4b": "pv-b-20", "l-9": "pv-a-10", "w-2": "pv-w-3", "l-pre": "pv-pre",
+                       "x-6": "pv2-a-6", "x-7": "pv2-a-7"}
+WFFC_FINAL_SELECTED = {"d-1": "b"}
+
+
 FIXTURES = {
     "disk_conflict": fx_disk_conflict,
     "non_csi_limits": fx_non_csi_limits,
     "csi_limits": fx_csi_limits,
     "volume_binding": fx_volume_binding,
     "volume_zone": fx_volume_zone,
+    "wait_for_first_consumer": fx_wait_for_first_consumer,
 }

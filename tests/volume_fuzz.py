@@ -3,7 +3,10 @@ labels and attach limits (allocatable and CSINode counts), PVs of CSI drivers, E
 with zone labels and node affinity, claims bound / bound to a missing PV / unbound, and pods
 mixing inline disks (GCE PD, EBS, RBD, iSCSI; read-only or not) with claims, shared between
 pods.  Every shape the volume plugins distinguish shows up at these sizes; nothing the
-device path refuses (WaitForFirstConsumer, CSI migration) is generated."""
+device path refuses (CSI migration) is generated.  wffc=True adds unbound WaitForFirstConsumer
+claims (a no-provisioner class with local PVs, a CSI class with allowedTopologies or none), PVs
+of several sizes with zone affinity, pre-bound (claimRef) PVs and claims already selected for a
+node (or for a node outside the snapshot), shared between pods."""
 import random
 
 import volume_fixtures as vf
@@ -13,7 +16,7 @@ ZONES = ["zone-a", "zone-b", "zone-c"]
 DRIVERS = ["ebs.csi.aws.com", "pd.csi.storage.gke.io"]
 
 
-def make(seed: int, n_nodes: int = 12, n_bound: int = 16, n_pods: int = 40):
+def make(seed: int, n_nodes: int = 12, n_bound: int = 16, n_pods: int = 40, wffc: bool = False):
     rng = random.Random(seed)
     nodes, csinodes = [], []
     for i in range(n_nodes):
@@ -63,6 +66,32 @@ def make(seed: int, n_nodes: int = 12, n_bound: int = 16, n_pods: int = 40):
     scs = [{"metadata": {"name": "fast"}, "provisioner": DRIVERS[0], "volumeBindingMode": "Immediate"},
            {"metadata": {"name": "gp"}, "provisioner": "kubernetes.io/aws-ebs", "volumeBindingMode": "Immediate"}]
     pvcs.append(vf.pvc("c-gp", bound=False, sc="gp"))
+    n_w = 0
+    if wffc:  # WaitForFirstConsumer: classes, candidate PVs, delayed claims
+        scs.append(vf.wsc("lw", "kubernetes.io/no-provisioner"))
+        scs.append(vf.wsc("cw", DRIVERS[1], zones=rng.sample(ZONES, rng.randint(1, 2)) if rng.random() < 0.7 else None))
+        n_w = 12
+        for k in range(16):
+            cls = "lw" if k < 11 else "cw"
+            zone = rng.choice(ZONES) if rng.random() < 0.8 else None
+            ref = "w-%d" % rng.randrange(n_w) if rng.random() < 0.12 else None
+            pv = vf.wpv("wpv-%d" % k, rng.randint(1, 16), cls, zone=zone, claim_ref=ref)
+            if rng.random() < 0.1:
+                pv["status"]["phase"] = "Released"
+            pvs.append(pv)
+        for k in range(n_w):
+            c = vf.wpvc("w-%d" % k, rng.randint(1, 12), "lw" if rng.random() < 0.7 else "cw")
+            if rng.random() < 0.15:
+                c["metadata"]["annotations"] = {"volume.kubernetes.io/selected-node":
+                                                rng.choice(["n%02d" % rng.randrange(n_nodes), "gone"])}
+            pvcs.append(c)
+        seen_ref = set()
+        for pv in pvs:  # at most one PV pre-bound to a claim (the device path refuses two)
+            ref = pv["spec"].get("claimRef")
+            if ref:
+                if ref["name"] in seen_ref:
+                    del pv["spec"]["claimRef"]
+                seen_ref.add(ref["name"])
 
     def volumes(pending):
         out = []
@@ -80,6 +109,8 @@ def make(seed: int, n_nodes: int = 12, n_bound: int = 16, n_pods: int = 40):
                                       "readOnly": rng.random() < 0.5}})
             elif r < 0.36:
                 out.append(vf.azure("az-%d" % rng.randrange(3)))
+            elif n_w and pending and r < 0.70:
+                out.append(vf.claim("w-%d" % rng.randrange(n_w)))
             elif r < 0.94 or not pending:
                 out.append(vf.claim("c-%d" % rng.randrange(24)))
             else:
