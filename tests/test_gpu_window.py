@@ -113,14 +113,15 @@ def test_c2_full_batch_window(pct, kernel):
 def test_k_simple_window_geometries(pct, geometry):
     """k_simple's window (simple_sync_win) in each of its shapes against the C oracle: the XCD-local
     grid (32 shards, per-wave mode), the unrestricted one (40 shards), one shard (no exchange, the
-    cut ranked locally, per-thread mode), three shards of 1,667 nodes (per-thread mode), and several
+    cut ranked locally, per-thread mode), three shards of 1,000 nodes (per-thread mode), and several
     chunk launches (KSS static budget: 7 launches hand nextStartNodeIndex on through the device
-    word).  The batch starts at a set cursor; two runs.  (One shard: 2,500 nodes, k_simple's largest shard
-    is 3,072.)"""
-    n_nodes, n_pods = (2500 if geometry == "one_shard" else 5000), 1500  # one k_simple shard: <= 3,072 nodes
+    word).  The batch starts at a set cursor; two runs.  (A k_simple shard holds at most ~1,200
+    nodes: 132 B of LDS per node slot, simple_lds_bytes.)"""
+    n_nodes = {"one_shard": 1000, "three_shards": 3000}.get(geometry, 5000)
+    n_pods, cursor = 1500, (777 if geometry == "one_shard" else 2321)
     prof = _prof(pct)
     s = native.Synth(2, SEED_BASE + 2, n_nodes, n_pods)
-    ch_o, res, st = _oracle(prof, s.cluster, s.pods, n_pods, n_nodes, record="meta", cursor=2321)
+    ch_o, res, st = _oracle(prof, s.cluster, s.pods, n_pods, n_nodes, record="meta", cursor=cursor)
     if geometry == "unrestricted":
         native.set_option("xcd", 0)
     elif geometry == "one_shard":
@@ -134,7 +135,7 @@ def test_k_simple_window_geometries(pct, geometry):
     ctx.stage(s.pods)
     for rep in range(2):
         ctx.reset()
-        ctx.set_next_start_node_index(2321)
+        ctx.set_next_start_node_index(cursor)
         chosen = ctx.run_staged(n_pods)
         assert ctx.last_kernel() == "k_simple"
         want_shards = {"xcd_local": 32, "unrestricted": 40, "one_shard": 1, "three_shards": 3}.get(geometry)
@@ -150,12 +151,12 @@ def test_k_simple_window_geometries(pct, geometry):
     ctx.close()
 
 
-@pytest.mark.parametrize("n_nodes", [101, 180, 700])
+@pytest.mark.parametrize("n_nodes", [101, 180, 150])
 def test_k_simple_window_small_and_saturating(n_nodes):
     """Window edges on k_simple: K = 100 of 101 / 180 nodes, and a cluster the batch saturates (pods
     become unschedulable, F <= K: every node visited, the cursor stays) -- chosen nodes, outcomes and
     the cursor against the oracle."""
-    n_pods = 2500 if n_nodes == 700 else 400
+    n_pods = 6000 if n_nodes == 150 else 400  # 150 nodes / 6,000 pods: 1,542 unschedulable
     prof = _prof(0)
     s = native.Synth(1, SEED_BASE + 1, n_nodes, n_pods)
     ch_o, res, st = _oracle(prof, s.cluster, s.pods, n_pods, n_nodes, record="meta")
@@ -167,7 +168,7 @@ def test_k_simple_window_small_and_saturating(n_nodes):
     np.testing.assert_array_equal(chosen, ch_o)
     _meta_equal(ctx.fetch_meta(n_pods), res, n_pods)
     assert ctx.next_start_node_index() == st["next_start"]
-    if n_nodes == 700:
+    if n_nodes == 150:
         assert (ch_o < 0).any()  # the batch saturates the cluster
     ctx.close()
 
