@@ -31,6 +31,7 @@
 #include <thread>
 #include <cstdio>
 #include <cstring>
+#include <unordered_map>
 #include <mutex>
 #include <atomic>
 #include <string>
@@ -734,6 +735,7 @@ struct kss_ctx {
   // the scheduling queue's nominator (kss_nominate): host mirror in AddNominatedPod order, uploaded
   // before a launch that reads it; run_pod_base = the podset index of the launch's pod 0
   std::vector<DevNom> nom;
+  std::unordered_map<int32_t, const kss_podset*> nom_src;  // index-keyed entries: the podset they index
   std::vector<int32_t> staged_uid;  // the staged pods' nominator identities (batch commits leave it)
   DevBuf nom_buf;
   bool nom_dirty = true;
@@ -2096,13 +2098,8 @@ int kss_next_start_node_index(kss_ctx* ctx, int32_t* out) {
   return 0;
 }
 
-int kss_nominate(kss_ctx* ctx, const kss_podset* ps, int32_t pod_index, int32_t node) {
-  KSS_SVC_QUIESCE(ctx);
-  if (!ctx || !ctx->loaded || !ps) return fail(KSS_E_INVAL, "bad arguments");
-  if (pod_index < 0 || pod_index >= ps->n_pods) return fail(KSS_E_INVAL, "pod index out of range");
-  const int local = node - ctx->dc.node_base;
-  if (local < 0 || local >= ctx->dc.N) return fail(KSS_E_INVAL, "node out of range");
-  if (ctx->split_n > 1) return fail(KSS_E_UNSUPPORTED, "split grids do not read the nominator");
+// The nominator entry of ps.pods[pod_index] on local row `local` (AddNominatedPod's NominatedPod)
+static int nom_entry(const kss_ctx* ctx, const kss_podset* ps, int32_t pod_index, int32_t local, DevNom& e) {
   const kss_pod& p = ps->pods[pod_index];
   if (p.vol_len > 0) return fail(KSS_E_UNSUPPORTED, "a nominated pod with volumes (the volume filters do not add nominees)");
   if (p.cls < 0 || p.cls >= ctx->host.n_classes) return fail(KSS_E_INVAL, "pod class out of range");
@@ -2111,7 +2108,7 @@ int kss_nominate(kss_ctx* ctx, const kss_podset* ps, int32_t pod_index, int32_t 
   if (p.own_terms_len > 8) return fail(KSS_E_UNSUPPORTED, "a nominated pod with more than 8 own term rows");
   if (ctx->host.n_ports < KSS_MAX_PORTS && (p.port_add >> ctx->host.n_ports))
     return fail(KSS_E_INVAL, "pod port bit outside the port dictionary");
-  DevNom e{};
+  e = DevNom{};
   e.node = local;
   e.prio = p.priority;
   e.pod = pod_identity(p, pod_index);
@@ -2123,12 +2120,50 @@ int kss_nominate(kss_ctx* ctx, const kss_podset* ps, int32_t pod_index, int32_t 
   }
   e.ports = p.port_add;
   for (int r = 0; r < KSS_NRES; r++) e.req[r] = p.commit_req[r];
+  return 0;
+}
+
+// An index-keyed identity (-1 - index: a pod without uid) names a pod of one pod list.  Every
+// entry point that takes a podset first drops the index-keyed entries that belong to another
+// podset, or whose index now holds a different pod (restaged or edited list), so no pod
+// inherits another's nomination: PreferNominatedNode and RunFilterPluginsWithNominatedPods'
+// self-exclusion follow the pod, not the slot.  uid-keyed entries are left alone.  Call with
+// ctx->mu held.
+static void nom_check_podset(kss_ctx* ctx, const kss_podset* ps) {
+  if (ctx->nom.empty()) return;
+  const size_t before = ctx->nom.size();
+  ctx->nom.erase(std::remove_if(ctx->nom.begin(), ctx->nom.end(),
+                                [&](const DevNom& e) {
+                                  if (e.pod >= 0) return false;
+                                  auto it = ctx->nom_src.find(e.pod);
+                                  if (it == ctx->nom_src.end() || it->second != ps) return true;
+                                  const int idx = -1 - e.pod;
+                                  if (idx >= ps->n_pods || ps->pods[idx].uid > 0) return true;
+                                  DevNom now;
+                                  if (nom_entry(ctx, ps, idx, e.node, now)) return true;
+                                  return std::memcmp(&now, &e, sizeof(DevNom)) != 0;
+                                }),
+                 ctx->nom.end());
+  if (ctx->nom.size() != before) ctx->nom_dirty = true;
+}
+
+int kss_nominate(kss_ctx* ctx, const kss_podset* ps, int32_t pod_index, int32_t node) {
+  KSS_SVC_QUIESCE(ctx);
+  if (!ctx || !ctx->loaded || !ps) return fail(KSS_E_INVAL, "bad arguments");
+  if (pod_index < 0 || pod_index >= ps->n_pods) return fail(KSS_E_INVAL, "pod index out of range");
+  const int local = node - ctx->dc.node_base;
+  if (local < 0 || local >= ctx->dc.N) return fail(KSS_E_INVAL, "node out of range");
+  if (ctx->split_n > 1) return fail(KSS_E_UNSUPPORTED, "split grids do not read the nominator");
+  DevNom e;
+  if (int rc = nom_entry(ctx, ps, pod_index, local, e)) return rc;
   std::lock_guard<std::mutex> lk(ctx->mu);
+  nom_check_podset(ctx, ps);
   // AddNominatedPod: an earlier nomination of the pod is replaced (it moves to the end)
   ctx->nom.erase(std::remove_if(ctx->nom.begin(), ctx->nom.end(), [&](const DevNom& x) { return x.pod == e.pod; }),
                  ctx->nom.end());
   if ((int)ctx->nom.size() >= KSS_NOM_MAX) return fail(KSS_E_UNSUPPORTED, "more than 64 nominated pods");
   ctx->nom.push_back(e);
+  if (e.pod < 0) ctx->nom_src[e.pod] = ps;
   ctx->nom_dirty = true;
   return 0;
 }
@@ -2139,6 +2174,7 @@ int kss_clear_nomination(kss_ctx* ctx, const kss_podset* ps, int32_t pod_index) 
   if (pod_index < 0 || pod_index >= ps->n_pods) return fail(KSS_E_INVAL, "pod index out of range");
   const int32_t id = pod_identity(ps->pods[pod_index], pod_index);
   std::lock_guard<std::mutex> lk(ctx->mu);
+  nom_check_podset(ctx, ps);
   const size_t before = ctx->nom.size();
   ctx->nom.erase(std::remove_if(ctx->nom.begin(), ctx->nom.end(), [&](const DevNom& x) { return x.pod == id; }),
                  ctx->nom.end());
@@ -3556,6 +3592,7 @@ static int compact_pod(const kss_podset* ps, int i, OnePod& o) {
 static int eval_pod_slot(kss_ctx* ctx, const kss_podset* ps, int32_t pod_index, const SlotRange& r, ReadBack& rbk) {
   if (!ctx || !ctx->loaded || !ps) return fail(KSS_E_INVAL, "bad arguments");
   if (pod_index < 0 || pod_index >= ps->n_pods) return fail(KSS_E_INVAL, "pod index out of range");
+  nom_check_podset(ctx, ps);
   OnePod one;
   int rc = compact_pod(ps, pod_index, one);
   if (rc) return rc;
@@ -3709,6 +3746,7 @@ static int commit_one(kss_ctx* ctx, const kss_podset* ps, int32_t pod_index, int
   a.local = local;
   a.sign = sign;
   std::lock_guard<std::mutex> lk(ctx->mu);
+  nom_check_podset(ctx, ps);
   HIP_TRY(hipSetDevice(ctx->cfg.device));
   if (sign > 0) {
     ctx->count_bound += 1.0 + (double)p.own_terms_len;
@@ -3760,6 +3798,7 @@ int kss_schedule_batch(kss_ctx* ctx, const kss_podset* ps, int32_t n, uint32_t f
   const bool record = (flags & KSS_SCHED_RECORD) != 0;
   if (record && n > ctx->cfg.max_pods_record) return fail(KSS_E_INVAL, "record capacity (max_pods_record) exceeded");
   std::lock_guard<std::mutex> lk(ctx->mu);
+  nom_check_podset(ctx, ps);
   HIP_TRY(hipSetDevice(ctx->cfg.device));
   rc = upload_podset(ctx->stream, ctx->pod_buf, ps, ctx->dp);
   if (rc) return rc;
@@ -3782,6 +3821,7 @@ int kss_stage_pods(kss_ctx* ctx, const kss_podset* ps) {
   int rc = validate(&ctx->host, ps, ps->n_pods);
   if (rc) return rc;
   std::lock_guard<std::mutex> lk(ctx->mu);
+  nom_check_podset(ctx, ps);
   HIP_TRY(hipSetDevice(ctx->cfg.device));
   rc = upload_podset(ctx->stream, ctx->pod_buf, ps, ctx->dp);
   if (rc) return rc;
@@ -4911,6 +4951,7 @@ int kss_postfilter_pod(kss_ctx* ctx, const kss_podset* ps, int32_t pod_index, ks
   if (rc) return rc;
   if ((rc = validate(&ctx->host, &one.ps, 1))) return rc;
   std::lock_guard<std::mutex> lk(ctx->mu);
+  nom_check_podset(ctx, ps);
   HIP_TRY(hipSetDevice(ctx->cfg.device));
   rc = upload_podset(ctx->stream, ctx->tmp_pod_buf, &one.ps, ctx->tdp);
   if (rc) return rc;

@@ -954,6 +954,7 @@ __device__ __forceinline__ bool schedule_pod(const DevCluster& c, const DevPods&
   // the diagnosis and the full search follows (the same verdict if it reaches the node again).
   int nom_m = -1, nom_f = KSS_F_PASS;
   uint16_t nom_d = 0;
+  bool nom_failed = false;  // uniform: evaluateNominatedNode's failure is in the diagnosis map
   if (nv.n) {
     for (int j = 0; j < nv.n; j++)
       if (((nv.active >> j) & 1u) && nv.e[j].pod == nv.pod) nom_m = nv.e[j].node;
@@ -992,6 +993,7 @@ __device__ __forceinline__ bool schedule_pod(const DevCluster& c, const DevPods&
       meta.chosen = (int)(c.node_base + nom_m);
       return true;
     }
+    nom_failed = true;
     if (!mine) nom_m = -1;  // only the owning lane overrides the node's record below
   } else {
     nom_m = -1;
@@ -1065,6 +1067,9 @@ __device__ __forceinline__ bool schedule_pod(const DevCluster& c, const DevPods&
     if (w_total <= k_find) S.cursor = (int)(((long long)S.cursor + m_list) % m_list);  // no stop: all processed
   }
   long long w_proc = 0;  // nodes processed before the stopping node (its lane only)
+  // the nominated node's map entry counts once more unless the search reaches that node again
+  // (it is outside the list, or after the stopping node): its lane only
+  long long nom_x = 0;
 
   long long nf = 0, max_tt = 0, max_na = 0;
   long long nign = 0, ipa_min = INT64_MAX, ipa_max = INT64_MIN, smissing = 0;
@@ -1102,6 +1107,7 @@ __device__ __forceinline__ bool schedule_pod(const DevCluster& c, const DevPods&
       }
     }
     if (n == nom_m) {  // evaluateNominatedNode's status (infeasible, so never kept): it stands
+      nom_x = f == KSS_F_NOT_EVALUATED ? 1 : 0;
       f = nom_f;
       detail = nom_d;
       kept = false;
@@ -1196,6 +1202,12 @@ __device__ __forceinline__ bool schedule_pod(const DevCluster& c, const DevPods&
   KSS_STAMP(S, 3);
   meta.n_feasible = (int)nf;
   if (nf == 0) {
+    if (nom_failed && m_list > 0) {  // no window stop: only the nominated node's count is left
+      long long v[1] = {nom_x};
+      const int op[1] = {OP_SUM};
+      if (!cluster_reduce(smem, S, v, op)) return false;
+      S.cursor = (int)(((long long)S.cursor + v[0]) % m_list);
+    }
     meta.status = 1;
     return true;
   }
@@ -1333,8 +1345,8 @@ __device__ __forceinline__ bool schedule_pod(const DevCluster& c, const DevPods&
     best = key > best ? key : best;
   }
   KSS_STAMP(S, 4);
-  if (win && w_total > k_find) {  // with the stopping node's processed count
-    long long v[2] = {best, w_proc};
+  if ((win && w_total > k_find) || (nom_failed && m_list > 0)) {  // with the processed count still to add
+    long long v[2] = {best, w_proc + nom_x};
     const int op[2] = {OP_MAX, OP_SUM};
     if (!cluster_reduce(smem, S, v, op)) return false;
     best = v[0];

@@ -1203,7 +1203,9 @@ class Oracle:
         node_list = [i for i, ni in enumerate(self.infos) if node_subset is None or _name(ni.node) in node_subset]
         m = len(node_list)
         num_to_find = num_feasible_nodes_to_find(m, self.pct)
-        feasible_len, statuses = 0, 0
+        # diagnosis.NodeToStatusMap, keyed by node: it already holds evaluateNominatedNode's failure,
+        # which the full search overwrites (one entry) only if it visits that node again
+        feasible_len, statuses = 0, ({nom} if nom is not None else set())
         res["dropped"] = None
         for j in range(m):
             i = node_list[(self.next_start + j) % m]
@@ -1219,9 +1221,9 @@ class Oracle:
                     break
                 feasible.append(i)
             else:
-                statuses += 1  # diagnosis.NodeToStatusMap
+                statuses.add(i)
         if m:
-            self.next_start = (self.next_start + feasible_len + statuses) % m
+            self.next_start = (self.next_start + feasible_len + len(statuses)) % m
         feasible.sort()  # selectHost's deterministic tie-break is the canonical index, not the visit order
         res["n_feasible"] = len(feasible)
         if not feasible:

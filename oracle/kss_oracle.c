@@ -1075,6 +1075,9 @@ static int schedule_one(const kss_profile* prof, ostate* s, const kss_podset* ps
         fp[n] = KSS_F_NOT_EVALUATED;
         fd[n] = 0;
       }
+      /* the diagnosis map already holds evaluateNominatedNode's failure: one node more unless
+         the search visited that node again (outside the list, or after the stopping node) */
+      if (nom_m >= 0 && ((inset && !inset[nom_m]) || fp[nom_m] == KSS_F_NOT_EVALUATED)) processed++;
       s->cursor = (int32_t)(((int64_t)s->cursor + processed) % m);
     }
     free(list);

@@ -60,3 +60,28 @@ def fixture():
         (5, {"selected": None, "fail": {"n1": NRF, "n2": NRF, "n3": NRF}, "nominated_left": ["big"]}),
     ]
     return nodes, bound, pods, noms, expect
+
+
+def window_fixture():
+    """nextStartNodeIndex after a failed evaluateNominatedNode (hand-derived from v1.26
+    findNodesThatPassFilters: processedNodes = feasibleNodesLen + len(diagnosis.NodeToStatusMap),
+    the map keyed by node and already holding the nominated node's status).
+
+    120 empty nodes w000..w119 of 4 CPUs, except w119 which a 4-CPU pod fills; percentageOfNodesToScore
+    50 -> numFeasibleNodesToFind = max(60, 100) = 100.  Both pods are nominated to w119.
+
+      0 p (1 CPU)  evaluateNominatedNode: w119 fails NodeResourcesFit, the one-node list sets the
+                   cursor to 0.  The full search visits w000..w100 and stops at w100 (the 101st
+                   feasible node: filtered, dropped); w101..w119 are not reached, so w119's entry is
+                   the map's 101st -> processed 100 + 1, cursor 101.
+      1 q (1 CPU, matchFields metadata.name In w000 | ... | w009: a 10-node PreFilterResult list, no
+                   window)  w119 fails (NodeAffinity first), cursor 0; the search visits the 10 listed nodes (all
+                   feasible) and the map holds w119 alone -> processed 10 + 1, cursor 11 % 10 = 1.
+    Returns nodes, bound, pods, nominations [(pod, node name)], pct, expected cursor after each pod."""
+    nodes = [_node("w%03d" % i) for i in range(120)]
+    bound = [_pod("fill", "4", 0, node="w119")]
+    # one term per name (a field selector's In takes exactly one value); the terms' union is the list
+    names = {"nodeAffinity": {"requiredDuringSchedulingIgnoredDuringExecution": {"nodeSelectorTerms": [
+        {"matchFields": [{"key": "metadata.name", "operator": "In", "values": ["w%03d" % i]}]} for i in range(10)]}}}
+    pods = [_pod("p", "1", 0, {"app": "p"}), _pod("q", "1", 0, {"app": "q"}, affinity=names)]
+    return nodes, bound, pods, [(0, "w119"), (1, "w119")], 50, [101, 1]

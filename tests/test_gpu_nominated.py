@@ -241,3 +241,72 @@ def test_remove_bound_restores_node_state():
     with pytest.raises(native.KssError):
         ctx.remove_bound(node0[:1])  # no longer in the table
     ctx.close()
+
+
+def test_window_fixture_cursor():
+    """nominated_fixtures.window_fixture on k_schedule: nextStartNodeIndex counts the nominated
+    node's status when the search does not reach that node again (the window stops first: 101;
+    the node is outside the PreFilterResult list: 1), equal to the C oracle's records."""
+    nodes, bound, pods, noms, pct, cursors = nf.window_fixture()
+    cc, cp, _ = compile_cluster(nodes, bound, pods)
+    idx = {n: i for i, n in enumerate(cc.node_names)}
+    prof = abi.default_profile()
+    prof.pct_nodes_to_score = pct
+    ps = cp.as_struct()
+    for n_run, want in ((1, cursors[0]), (2, cursors[1])):
+        ch_o, res, st = oracle_c.schedule(prof, cc.as_struct(), ps, n_run, cc.n_nodes, n_classes=len(cc.classes),
+                                          n_terms=len(cc.terms), nominations=[(j, idx[n]) for j, n in noms])
+        assert st["next_start"] == want
+        ctx = _ctx(cc, prof, record=n_run)
+        for j, n in noms:
+            ctx.nominate(ps, j, idx[n])
+        chosen = ctx.schedule_batch(ps, n_run, record=True)
+        assert ctx.last_kernel() == "k_schedule"
+        np.testing.assert_array_equal(chosen, ch_o)
+        assert ctx.next_start_node_index() == want
+        for j in range(n_run):
+            r = ctx.fetch_record(j)
+            np.testing.assert_array_equal(r.fail_plugin[:cc.n_nodes], res.fail_plugin[j, :cc.n_nodes], err_msg=str(j))
+            np.testing.assert_array_equal(r.fail_detail[:cc.n_nodes], res.fail_detail[j, :cc.n_nodes], err_msg=str(j))
+        ctx.close()
+
+
+def test_index_keyed_nominations_follow_the_pod():
+    """A pod without uid is nominated by its podset index.  The entry belongs to that podset and
+    that pod: a call with another podset, or after the pod at that index changed, drops it, so no
+    other pod inherits PreferNominatedNode or the nominee self-exclusion; an unchanged podset
+    keeps it, and uid-keyed entries survive any podset."""
+    nodes, bound, pods, noms, expect = nf.fixture()
+    cc, cp, _ = compile_cluster(nodes, bound, pods)
+    idx = {n: i for i, n in enumerate(cc.node_names)}
+    ps = cp.as_struct()
+    ctx = _ctx(cc)
+    ctx.nominate(ps, 5, idx["n2"])
+    ctx.eval_pod(ps, 0)  # same podset, pod 5 unchanged: kept
+    assert ctx.nominations() == [(5, idx["n2"])]
+    # another pod list (the pods reversed): "low" now sits at index 5 and must not inherit n2
+    cc2, cp2, _ = compile_cluster(nodes, bound, pods[::-1])
+    ps2 = cp2.as_struct()
+    r = ctx.eval_pod(ps2, 5)
+    assert ctx.nominations() == []
+    ref = _ctx(cc)
+    want = ref.eval_pod(ps2, 5)  # no nominator at all
+    assert r.chosen == want.chosen
+    np.testing.assert_array_equal(r.fail_plugin[:cc.n_nodes], want.fail_plugin[:cc.n_nodes])
+    ref.close()
+    # the same podset with the nominated pod edited in place (its priority): dropped
+    ctx.nominate(ps, 5, idx["n2"])
+    cp.pods["priority"][5] = 7
+    ctx.eval_pod(ps, 0)
+    assert ctx.nominations() == []
+    cp.pods["priority"][5] = 100
+    # restaging another list drops it too
+    ctx.nominate(ps, 4, idx["n3"])
+    ctx.stage(ps2)
+    assert ctx.nominations() == []
+    # uid-keyed: survives a different podset
+    cp.pods["uid"] = 500 + np.arange(cp.n, dtype=np.int32)
+    ctx.nominate(ps, 5, idx["n2"])
+    ctx.eval_pod(ps2, 0)
+    assert ctx.nominations() == [(505, idx["n2"])]
+    ctx.close()

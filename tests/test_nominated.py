@@ -112,3 +112,35 @@ def test_fixture_c_oracle():
         assert got == want["selected"], (j, got, want)
     left = sorted(cp.names[j][1] for j, _ in st["nominations"])
     assert left == expect[-1][1]["nominated_left"]
+
+
+def test_window_fixture_cursor_counts_the_nominated_status():
+    """nominated_fixtures.window_fixture: the nominated node's failure counts in processedNodes when
+    the search does not reach that node again (window stop; outside the PreFilterResult list), in
+    both oracles."""
+    nodes, bound, pods, noms, pct, cursors = nf.window_fixture()
+    o = ko.Oracle(nodes, bound, percentage_of_nodes_to_score=pct)
+    for j, n in noms:
+        o.nominate(pods[j], o.by_name[n])
+    for j, want in enumerate(cursors):
+        r = o.schedule_one(pods[j])
+        assert r["selected"] is not None and r["fail"][o.by_name["w119"]] == ("NodeResourcesFit", "NodeAffinity")[j], j
+        assert o.next_start == want, (j, o.next_start)
+    r0 = None
+    from kss.compile import compile_cluster
+    from kss import abi
+    import oracle_c
+    cc, cp, _ = compile_cluster(nodes, bound, pods)
+    idx = {n: i for i, n in enumerate(cc.node_names)}
+    prof = abi.default_profile()
+    prof.pct_nodes_to_score = pct
+    for n_run, want in ((1, cursors[0]), (2, cursors[1])):
+        ch, res, st = oracle_c.schedule(prof, cc.as_struct(), cp.as_struct(), n_run, cc.n_nodes,
+                                        n_classes=len(cc.classes), n_terms=len(cc.terms),
+                                        nominations=[(j, idx[n]) for j, n in noms])
+        assert st["next_start"] == want, (n_run, st["next_start"])
+        if n_run == 1:
+            r0 = res
+    # pod 0's record: w100 ended the search (passed, dropped), w101..w118 never visited
+    assert int(r0.fail_plugin[0, idx["w100"]]) == 0 and int(r0.fail_detail[0, idx["w100"]]) == abi.KSS_PASS_NOT_KEPT
+    assert all(int(r0.fail_plugin[0, idx["w%03d" % i]]) == abi.KSS_F_NOT_EVALUATED for i in range(101, 119))
