@@ -586,7 +586,7 @@ def run_split(args):
         dist.destroy_process_group()
 
 
-def latency_profile(cfg, n_nodes, n_pods, seed, device):
+def latency_profile(cfg, n_nodes, n_pods, seed, device, pct=100):
     """roofline.latency: the per-pod chain is latency-bound, so beside the HBM fraction the line
     carries the phase breakdown of one stamped run (KSS_STAMPS_FILE: s_memrealtime per phase,
     the first 128 pods, outside the timed region) and the measured exchange floor (per
@@ -600,7 +600,9 @@ def latency_profile(cfg, n_nodes, n_pods, seed, device):
     native.set_stamps_file(path)
     try:
         s = native.Synth(cfg, seed, n_nodes, min(n_pods, 1000))
-        ctx = native.Context(abi.default_profile(), device=device)
+        prof = abi.default_profile()
+        prof.pct_nodes_to_score = pct
+        ctx = native.Context(prof, device=device)
         ctx.load(s.cluster)
         ctx.stage(s.pods)
         ctx.run_staged(s.n_pods)
@@ -994,7 +996,7 @@ def c2_pct0_leg(args, world: int, rank: int, local: int, dist) -> dict:
     filters nodes from nextStartNodeIndex until 500 feasible ones are found, and scores those.
     `evals` counts the filter evaluations the window actually made per pod (the line's
     evals_per_pod), not N."""
-    return child_leg(args, world, rank, local, dist, ["--config", "2", "--pct", "0", "--no-legs", "--no-traffic", "--no-latency"],
+    return child_leg(args, world, rank, local, dist, ["--config", "2", "--pct", "0", "--no-legs", "--no-traffic"],
                      "C2 pct=0", args.c4_timeout, min(args.cpu_seconds, 6.0))
 
 
@@ -1179,7 +1181,7 @@ def main():
             cpu = cpu_baseline(cfg, n_nodes, n_pods, args.cpu_seconds, threads, seed=seed, pct=args.pct)
         latency = None
         if not args.no_latency and world == 1:
-            latency = latency_profile(cfg, n_nodes, n_pods, seed, local)
+            latency = latency_profile(cfg, n_nodes, n_pods, seed, local, pct=args.pct)
             latency["us_per_pod"] = elapsed / args.steps / n_pods * 1e6
             if latency.get("bound_us_per_pod"):
                 latency["frac"] = latency["bound_us_per_pod"] / latency["us_per_pod"]

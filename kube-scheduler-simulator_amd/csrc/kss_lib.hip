@@ -65,7 +65,7 @@ enum KssOpt {
   O_SHARDS, O_XCD, O_XCD_SHARDS, O_NO_SIMPLE, O_NO_SPREAD, O_AXIS_BLOCKS, O_AXIS_NO_FOLD, O_NODES_PER_SHARD,
   O_THREADS, O_FORCE_THREADS, O_COOP_LAUNCH, O_NO_CACHE, O_STATIC_BYTES, O_STATIC_PPB, O_FOLD, O_TRACE_PATH,
   O_SVC_INLINE_SWEEP, O_SERVICE_STAMPS, O_SVC_FULL_FENCE, O_SERVICE_GENERAL, O_SVC_XCD, O_SVC_NO_STATIC,
-  O_SWEEP_PIPE, O_SERVICE_NO_DIFF, O_SVC_HUGE, O_XCD_FORCE_FALLBACK, O_N
+  O_SWEEP_PIPE, O_SERVICE_NO_DIFF, O_SVC_HUGE, O_XCD_FORCE_FALLBACK, O_SPREAD_TWO_LEVEL, O_N
 };
 struct OptDef {
   const char* name;
@@ -99,6 +99,7 @@ const OptDef kOptDefs[O_N] = {
     {"service_no_diff", "KSS_SERVICE_NO_DIFF", 0},
     {"svc_huge", "KSS_SVC_HUGE", 0},
     {"xcd_force_fallback", "KSS_XCD_FORCE_FALLBACK", 0},  // XCD-local launches report failed placement
+    {"spread_two_level", "KSS_SPREAD_TWO_LEVEL", 1},      // k_spread's two-level selectHost exchange (W > 64)
 };
 std::atomic<long long> g_opt[O_N];
 std::once_flag g_opt_once;
@@ -371,6 +372,10 @@ __global__ __launch_bounds__(KSS_MAX_THREADS) void k_spread(const DevJob* __rest
     if (xs < 0) return;
   }
   const int ji = X.xcd_local ? 0 : blockIdx.x / Wl, w = X.xcd_local ? xs : X.w_off + (int)(blockIdx.x % Wl);
+  if (X.tl) {  // the two-level selectHost exchange: the shard's XCD and rank there (tl_register)
+    if (threadIdx.x == 0) tl_register(H, X.tl, W, err);
+    __syncthreads();
+  }
   const DevJob job = jobs[ji];
   constexpr kss_profile def_prof = default_profile_c();
 #ifdef KSS_LDS_POISON  // experiment builds: the shard's LDS image filled with a pattern first
@@ -2903,6 +2908,12 @@ static int launch_spread(hipStream_t st, const Geometry& g, const GpodNeeds& q, 
   xcd = xcd && !sp_grid && gran && g.W > 1;
   const dim3 grid((unsigned)(sp_grid ? X.wl : g.W)), block((unsigned)g.threads);
   const dim3 xgrid((unsigned)(XCD_GRID_MULT * g.W));
+  // many shards on one part: the two-level selectHost exchange, its area at the end of the
+  // granule buffer (run_single reserves tl_words)
+  const size_t tlw = tl_words(g.W);
+  if (!sp_grid && !xcd && gran && g.W > 64 && opt(O_SPREAD_TWO_LEVEL) &&
+      gran_bytes / 8 >= tlw + 2 * (size_t)g.W * (size_t)gs + 16)
+    X.tl = gran + gran_bytes / 8 - tlw;
   kss_profile pr = prof;
   int W = g.W, n_lo = 0, n_hi = 0;
   static_rows(g, X, max_nodes, n_lo, n_hi);
@@ -2910,10 +2921,12 @@ static int launch_spread(hipStream_t st, const Geometry& g, const GpodNeeds& q, 
     int k1 = std::min(n_pods, k0 + chunk);
     launch_static(st, def, jobs, pr, 1, k0, k1, n_lo, n_hi, n_keys);
     HIP_TRY(hipGetLastError());
-    unsigned epoch0 = 0;
+    // every chunk's tags above the previous chunk's (a line an earlier chunk left in an XCD's
+    // L2 never carries a current tag), the buffer zeroed as well
+    unsigned epoch0 = (unsigned)(k0 / std::max(chunk, 1)) * chunk_span(chunk);
     unsigned long long* gc = gran;
     if (sp_grid) {
-      epoch0 = split->epoch0 + (unsigned)(k0 / std::max(chunk, 1)) * chunk_span(chunk);
+      epoch0 += split->epoch0;
       split_chunk_view(*split, k0 / std::max(chunk, 1), gran, gc, X);
     } else if (gran && k0 > 0) {
       HIP_TRY(dev_zero(gran, gran_bytes, st));
@@ -3205,7 +3218,7 @@ static int run_single_impl(kss_ctx* ctx, const PlanNeeds& need, const DevPods& d
   rc = ctx->err_buf.ensure(16);
   if (rc) return rc;
   unsigned long long* gran = nullptr;
-  const size_t gb = sizeof(unsigned long long) * 2 * (size_t)g.W * std::max(2 * XW_MAX, G_XW);
+  const size_t gb = sizeof(unsigned long long) * (2 * (size_t)g.W * std::max(2 * XW_MAX, G_XW) + (spread ? tl_words(g.W) : 0));
   unsigned epoch0 = 0;
   SplitRun srun;
   if (split) {  // the local inbox, never cleared: this run's epochs start above every earlier tag

@@ -682,7 +682,7 @@ constexpr int SX_RED = 16;  // per-wave reduction row: the key and up to 15 stat
 struct alignas(16) SimpleHdr {
   long long red[2][MAXWAVES][SX_RED];
   long long res[4];  // winner key of the previous pod; nf, max TT, max NA of the next pod
-  long long win[10];  // window (simple_sync_win): F, TT / NA of the wholly kept segments, cut shard, part, j; d, TT, NA
+  long long win[12];  // window (simple_sync_win): F, TT / NA of the wholly kept segments, cut shard, part, j; d, TT, NA; E2 needed
   int cutc[2][MAXWAVES];  // window cut scan: feasible nodes of the part per wave
   int cutm[MAXWAVES][2];  // ... and the waves' maxima of the kept ones
   kss_profile prof;  // a runtime (non-default) profile: indexed by resource id, so in LDS, not scratch
@@ -1234,10 +1234,15 @@ __device__ __forceinline__ bool simple_sync_pw(SimpleHdr& H, int& parity, long l
 // segments a_0 .. a_{W-1}, b_0 .. b_{W-1}, and publishes per part {feasible count, max raw TT,
 // max raw NA} for H0 and H1 (SXW_VALS granules).  After the sweep every shard knows from the
 // segments' counts the segment holding the (K+1)-th feasible node (the cut) and the maxima of
-// the segments wholly before it; the cut segment's shard ranks its feasible nodes (ballots) for
-// d and the maxima of its first j, and publishes them (a second exchange of SXW_E2 granules,
-// polled from that one shard).  Pass B keeps node n iff feasible and (no cut or (n - s) mod N <
-// (d - s) mod N).  Statistics index: (h * 2 + part) * 3 + {0 F, 1 TT, 2 NA}, h = 0 H0, 1 H1.
+// the segments wholly before it.  Only the cut segment's shard needs d: every other shard's
+// segments lie wholly before or after the cut, so pass B keeps node n iff feasible and (no cut,
+// or seg(n) < cut segment, or seg(n) == cut segment and n < d), and the next pod's split needs
+// only the start SHARD elsewhere (shards before it: every node in part b; after it: part a).
+// The cut shard ranks its feasible nodes (ballots) for d and the maxima over its first j; a
+// second exchange (SXW_E2 granules, polled from that one shard) carries those maxima only when
+// the cut segment's maxima over ALL its feasible nodes exceed the wholly kept segments' (known
+// to every shard from the first exchange): otherwise they cannot change the result.
+// Statistics index: (h * 2 + part) * 3 + {0 F, 1 TT, 2 NA}, h = 0 H0, 1 H1.
 constexpr int SXW_VALS = 10;  // granules per shard: key lo / hi, then {F << 16 | TT, NA} of a0, b0, a1, b1
 constexpr int SXW_E2 = 4;     // the cut shard's granules per epoch parity: d, TT, NA (+ pad)
 
@@ -1384,14 +1389,16 @@ __device__ __forceinline__ void win_cut_scan(SimpleHdr& H, const SimpleShard& L,
 // The window's statistics exchange (both per-wave and per-thread modes; PW: the best wave contributes
 // its H1, else every wave's H1 set already accounts for the shard's candidate).  Pod k's AssumePod
 // on the winner's slot is applied here (wave 0, lane-parallel) before the closing barrier.
-// R = {winner key of pod k, kept count, max TT, max NA of pod k+1 over its kept nodes}, d_out = pod
-// k+1's dropped node (-1: no cut).  start: pod k+1's nextStartNodeIndex.  False if the launch aborted.
+// R = {winner key of pod k, kept count, max TT, max NA of pod k+1 over its kept nodes}; cs_out = pod
+// k+1's cut segment (part * W + shard, -1: no cut), d_out = its dropped node (on the cut shard;
+// -1 elsewhere).  start: this shard's split of pod k+1's node list (win_start).  False if the
+// launch aborted.
 template <bool PW, typename Idle>
 __device__ __forceinline__ bool simple_sync_win(SimpleHdr& H, int& parity, long long wkey, uint32_t (&u)[12], int W,
                                                 int w, unsigned epoch, unsigned long long* gran, const XPeers& X,
                                                 int* err, int per, int node_base, int lo, int own, const SPod& pk,
                                                 bool commit, const SimpleShard& L, int kb, int k_find, int start,
-                                                int pwv, long long (&R)[4], int& d_out,
+                                                int pwv, long long (&R)[4], int& d_out, int& cs_out,
                                                 KSS_GLOBAL unsigned long long* sp, Idle&& idle) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
   dpp_win_step<0xB1, 0xF>(u);
@@ -1524,7 +1531,7 @@ __device__ __forceinline__ bool simple_sync_win(SimpleHdr& H, int& parity, long 
       A = (uint32_t)wave_red<OP_SUM>((long long)A);
       B = (uint32_t)wave_red<OP_SUM>((long long)B);
       const uint32_t F = A + B, K = (uint32_t)k_find;
-      uint32_t ftt = 0, fna = 0;
+      uint32_t ftt = 0, fna = 0, cut_tt = 0, cut_na = 0;  // cut_*: the cut segment's maxima over all its feasible nodes
       int cut = -1, part = 0, j = 0;
       if (F <= K) {
 #pragma unroll
@@ -1553,6 +1560,8 @@ __device__ __forceinline__ bool simple_sync_win(SimpleHdr& H, int& parity, long 
             hit = ba ? 0ull : 1ull;
             cut = ch * 64 + l;
             pre_hit = (uint32_t)__builtin_amdgcn_readlane((int)(ba ? pa : pb), l);
+            cut_tt = (uint32_t)__builtin_amdgcn_readlane((int)(ba ? ta[ch] : tb[ch]), l);
+            cut_na = (uint32_t)__builtin_amdgcn_readlane((int)(ba ? na_[ch] : nb_[ch]), l);
           }
           ca += (uint32_t)__builtin_amdgcn_readlane((int)ia, 63);
           cb += (uint32_t)__builtin_amdgcn_readlane((int)ib, 63);
@@ -1576,6 +1585,7 @@ __device__ __forceinline__ bool simple_sync_win(SimpleHdr& H, int& parity, long 
         H.win[3] = cut;
         H.win[4] = part;
         H.win[5] = j;
+        H.win[10] = cut >= 0 && (cut_tt > ftt || cut_na > fna);  // the cut shard's partial maxima can matter
       }
     }
   }
@@ -1586,8 +1596,10 @@ __device__ __forceinline__ bool simple_sync_win(SimpleHdr& H, int& parity, long 
   const int cut = (int)H.win[3];
   long long mtt = H.win[1], mna = H.win[2], nf = F;
   int d = -1;
+  cs_out = cut >= 0 ? (int)H.win[4] * W + cut : -1;
   if (cut >= 0) {
     nf = k_find;
+    const bool need = H.win[10] != 0;
     const long long best = H.res[0];
     const int gl = best != 0 ? (int)(0xFFFFFFFFu - (uint32_t)(unsigned long long)best) - node_base : -1;
     const bool won = gl >= lo && gl < lo + own;
@@ -1597,17 +1609,17 @@ __device__ __forceinline__ bool simple_sync_win(SimpleHdr& H, int& parity, long 
     if (cut == w) {  // uniform over the workgroup
       int cd = -1, ctt = 0, cna = 0;
       win_cut_scan<PW>(H, L, own, lo, start, (int)H.win[4], (int)H.win[5], sub_s, sub_h, pwv, cd, ctt, cna);
+      d = cd;
       if (W == 1) {
-        d = cd;
         mtt = max(mtt, (long long)ctt);
         mna = max(mna, (long long)cna);
-      } else if (threadIdx.x < 3) {
+      } else if (need && threadIdx.x < 3) {
         const unsigned long long tag = (unsigned long long)epoch << 32;
         const uint32_t x = threadIdx.x == 0 ? (uint32_t)cd : (threadIdx.x == 1 ? (uint32_t)ctt : (uint32_t)cna);
         xpub(X, gran, e2 + threadIdx.x, tag | x);
       }
     }
-    if (W > 1) {
+    if (W > 1 && need) {
       if (wave == 0) {
         const unsigned long long* b2 = gran + e2;
         long long t0_ = 0;
@@ -1629,7 +1641,6 @@ __device__ __forceinline__ bool simple_sync_win(SimpleHdr& H, int& parity, long 
       }
       lds_barrier();
       if (H.abort) return false;
-      d = (int)H.win[7];
       mtt = max(mtt, H.win[8]);
       mna = max(mna, H.win[9]);
     }
@@ -1694,9 +1705,15 @@ __device__ __forceinline__ void simple_schedule(DevCluster c, const SPod* __rest
   }
   if (tid == 0) H.abort = 0;
   __syncthreads();
-  // the window (WIN): pod k's start node and dropped node (pass B), pod k0's start from the cursor
-  int wst = 0, wd = -1;
+  // the window (WIN).  A shard splits its slots at a pod's start node s into part a (node >= s) and
+  // part b by `wsl`: s itself on the shard holding s (the start shard, wss), past its last node on
+  // shards before it (every node in part b), its first node on shards after it (every node in part
+  // a).  wsx: s, on the start shard.  wcs: pod k's cut segment (-1 none), wd: its dropped node, on
+  // the cut shard (pass B).  Pod k0 starts at the cursor word.
   const int cur0 = WIN && cursor && c.N > 0 ? (int)(((long long)ld_ag(cursor) % c.N + c.N) % c.N) : 0;
+  auto win_start = [&](int sh, int x) { return w < sh ? lo + own : (w > sh ? lo : x); };
+  int wss = WIN ? min(cur0 / max(per, 1), W - 1) : 0, wsx = cur0;
+  int wsl = win_start(wss, cur0), wcs = -1, wd = -1;
 
   KSS_GLOBAL const uint32_t* gstat = gp(stat);
   KSS_GLOBAL const uint4* gspod = gp(reinterpret_cast<const uint4*>(spods));
@@ -1797,9 +1814,9 @@ __device__ __forceinline__ void simple_schedule(DevCluster c, const SPod* __rest
         const SVal e = cv_get(L, s == sub_s ? sub_h : s);
         const long long key = simple_key(prof, e, scored, max_tt, rtt, max_na, rna, (uint32_t)(c.node_base + lo + s));
         bool kept = true;
-        if (WIN && wd >= 0) {  // inside the window [wst, wd) in visiting order
-          const int n = lo + s;
-          kept = (n >= wst ? n - wst : n + c.N - wst) < (wd >= wst ? wd - wst : wd + c.N - wst);
+        if (WIN && wcs >= 0) {  // the node's segment before the cut segment, or before d inside it
+          const int n = lo + s, seg = (n >= wsl ? 0 : W) + w;
+          kept = seg < wcs || (seg == wcs && n < wd);
         }
         best = (e.f == 0 && kept) ? key : 0;
       }
@@ -1813,9 +1830,9 @@ __device__ __forceinline__ void simple_schedule(DevCluster c, const SPod* __rest
             const SVal e = cv_get(L, s == sub_s ? sub_h : s);
             const long long key = simple_key(prof, e, scored, max_tt, rtt, max_na, rna, (uint32_t)(c.node_base + lo + s));
             bool kept = true;
-            if (WIN && wd >= 0) {
-              const int n = lo + s;
-              kept = (n >= wst ? n - wst : n + c.N - wst) < (wd >= wst ? wd - wst : wd + c.N - wst);
+            if (WIN && wcs >= 0) {
+              const int n = lo + s, seg = (n >= wsl ? 0 : W) + w;
+              kept = seg < wcs || (seg == wcs && n < wd);
             }
             best = (e.f == 0 && kept && key > best) ? key : best;
           }
@@ -1834,23 +1851,25 @@ __device__ __forceinline__ void simple_schedule(DevCluster c, const SPod* __rest
     const SPod& qn = L.ring[(k + 1) % RING];
     const int sln = (k + 1) % RING;
     if constexpr (WIN) {
-      // pod k+1 starts where pod k's window stopped (its dropped node), else where pod k started
-      const int wsn = k >= k0 ? (wd >= 0 ? wd : wst) : cur0;
+      // pod k+1 starts where pod k's window stopped (its dropped node, on the cut shard), else
+      // where pod k started
+      if (k >= k0 && wcs >= 0) {
+        wss = wcs % W;
+        if (w == wss) wsx = wd;
+        wsl = win_start(wss, wd);
+      }
       uint32_t u[12];
       if (k + 1 < k1) {
-        if constexpr (PW) simple_pass_a_pw_win<DEF>(prof, qn, pk, L, sln, own, pwv, cand, lo, wsn, u);
-        else simple_pass_a_win<DEF>(prof, qn, pk, L, sln, own, cand, lo, wsn, u);
+        if constexpr (PW) simple_pass_a_pw_win<DEF>(prof, qn, pk, L, sln, own, pwv, cand, lo, wsl, u);
+        else simple_pass_a_win<DEF>(prof, qn, pk, L, sln, own, cand, lo, wsl, u);
       } else {
 #pragma unroll
         for (int i = 0; i < 12; i++) u[i] = 0;
       }
       if (sp && tid == 0) sp[3] = wall_clock64();
-      int dn = -1;
       if (!simple_sync_win<PW>(H, parity, best, u, W, w, ++epoch, gran, X, err, per, c.node_base, lo, own, pk, k >= k0, L,
-                               kb, k_find, wsn, pwv, R, dn, sp, prefetch_idle))
+                               kb, k_find, wsl, pwv, R, wd, wcs, sp, prefetch_idle))
         return;
-      wst = wsn;
-      wd = dn;
     } else if constexpr (PW) {
       uint32_t u[6];
       if (k + 1 < k1) {
@@ -1908,8 +1927,9 @@ __device__ __forceinline__ void simple_schedule(DevCluster c, const SPod* __rest
     if (sp && tid == 0) sp[6] = wall_clock64();
   }
   if (tid == out_tid) store_pending();  // the last pod's outcome
-  // nextStartNodeIndex after the last pod (every shard holds it; the first shard writes it)
-  if (WIN && cursor && w == 0 && tid == 0) st_ag(cursor, (int32_t)wst);
+  // nextStartNodeIndex after the last pod: the start shard of the pod after it writes it (the last
+  // iteration's pass A, for no pod, already moved the start past the last pod's cut)
+  if (WIN && cursor && w == wss && tid == 0) st_ag(cursor, (int32_t)wsx);
   // node state back to HBM
   __syncthreads();
   for (int s = tid; s < own; s += nt) {

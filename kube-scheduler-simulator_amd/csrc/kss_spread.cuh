@@ -162,6 +162,8 @@ struct alignas(16) SpreadHdr {
   int32_t fflags;
   int32_t abort;
   int32_t pad[2];
+  int32_t tl_x, tl_s, tl_n;  // two-level exchange (X.tl): the shard's XCD, its rank there, the XCD's shards
+  uint32_t tl_mask;          // ... the XCDs holding shards
 };
 
 struct SpreadShard {
@@ -545,6 +547,111 @@ __device__ __forceinline__ bool spread_reduce(SpreadHdr& H, int32_t* xs, int W, 
   return true;
 }
 
+// ---- Two-level selectHost exchange (one part, W > 64 shards over the chip's XCDs) -------------
+// The flat exchange has every shard poll every shard's granule across XCDs: at C4's 256 shards
+// a 3.2 us step (four waves sweep, then an LDS combine).  Two levels instead: each shard stores
+// its key with a PLAIN store into its XCD's area (the line stays in that XCD's L2, which the
+// polls read: tools/xcd_exchange_probe.hip, 0.41 against 1.23 us a round); the XCD's rank-0
+// shard polls its XCD's <= 64 keys with one load per lane, stores their maximum write-through
+// (agent scope) into one line per XCD, and every shard polls the <= 16 XCD maxima.  Which XCD
+// a shard runs on is read from XCC_ID at the start of the launch (tl_register), never assumed.
+// Area (8-byte words, X.tl): [0, 16) counters (shards per XCD, [8] all), then per parity
+// TL_G x tl_ls(W) XCD slots, then per parity TL_G lines of 16 words (one XCD maximum each).
+constexpr int TL_G = 16;  // XCC ids 0..15
+__host__ __device__ inline int tl_ls(int W) { return (W + 15) / 16 * 16; }
+__host__ __device__ inline size_t tl_words(int W) { return 16 + 2 * (size_t)TL_G * tl_ls(W) + 2 * (size_t)TL_G * 16; }
+
+// Thread 0: the shard's XCD and rank there; every shard of the launch registered (bounded wait).
+__device__ __forceinline__ void tl_register(SpreadHdr& H, unsigned long long* tl, int W, int* err) {
+  int* cnt = reinterpret_cast<int*>(tl);  // [0, TL_G) per XCD, [TL_G] all
+  const int x = xcc_id() & (TL_G - 1);
+  const int s = atomicAdd(&cnt[x], 1);
+  atomicAdd(&cnt[TL_G], 1);
+  long long t0 = 0;
+  bool ok = false;
+  for (unsigned spins = 0;; ++spins) {
+    if (__hip_atomic_load(&cnt[TL_G], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= W) {
+      ok = true;
+      break;
+    }
+    if (spin_expired(spins, t0)) break;
+    __builtin_amdgcn_s_sleep(1);
+  }
+  uint32_t mask = 0;
+  for (int g = 0; g < TL_G; g++)
+    mask |= (ok && __hip_atomic_load(&cnt[g], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) > 0) ? 1u << g : 0u;
+  H.tl_x = x;
+  H.tl_s = s;
+  H.tl_n = ok ? __hip_atomic_load(&cnt[x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+  H.tl_mask = mask;
+  if (!ok) err_raise(err, 1);
+}
+
+// Wave 0: the cluster maximum of the shards' 32-bit compressed keys (kc) through the two levels.
+// False on a timed-out wait (H.abort set).
+__device__ __forceinline__ bool tl_argmax(SpreadHdr& H, const XPeers& X, int W, unsigned epoch, uint32_t kc, int* err,
+                                          uint32_t& out) {
+  const int lane = threadIdx.x & 63;
+  const int ls = tl_ls(W);
+  const unsigned long long tag = (unsigned long long)epoch << 32;
+  unsigned long long* loc = X.tl + 16 + ((size_t)(epoch & 1) * TL_G + H.tl_x) * ls;
+  unsigned long long* glob = X.tl + 16 + 2 * (size_t)TL_G * ls + (size_t)(epoch & 1) * TL_G * 16;
+  if (lane == 0) asm volatile("global_store_dwordx2 %0, %1, off" ::"v"(loc + H.tl_s), "v"(tag | kc) : "memory");
+  if (H.tl_s == 0) {  // the XCD's maximum: its shards' keys from this XCD's L2
+    uint32_t m = 0;
+    const int n = H.tl_n;
+    for (int c0 = 0; c0 < n; c0 += 64) {
+      const int s = c0 + lane;
+      unsigned long long v = tag;
+      long long t0 = 0;
+      for (unsigned spins = 0;; ++spins) {
+        if (s < n) v = __hip_atomic_load(gp(loc) + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (__all((v >> 32) == epoch)) break;
+        if (spread_spin_over(spins, t0, err)) {
+          if (lane == 0) {
+            H.abort = 1;
+            err_raise(err, 1);
+          }
+          return false;
+        }
+        spin_pause();
+      }
+      m = max(m, s < n ? (uint32_t)v : 0u);
+    }
+    m = max(m, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)m, 0xB1, 0xF, 0xF, false));
+    m = max(m, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)m, 0x4E, 0xF, 0xF, false));
+    m = max(m, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)m, 0x141, 0xF, 0xF, false));
+    m = max(m, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)m, 0x140, 0xF, 0xF, false));
+    m = max(m, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)m, 0x142, 0xA, 0xF, false));
+    m = max(m, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)m, 0x143, 0xC, 0xF, false));
+    m = (uint32_t)__builtin_amdgcn_readlane((int)m, 63);
+    if (lane == 0) __hip_atomic_store(gp(glob) + 16 * (size_t)H.tl_x, tag | m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  // the XCDs' maxima: lane g polls XCD g's line
+  const bool in = lane < TL_G && ((H.tl_mask >> lane) & 1u);
+  unsigned long long v = tag;
+  long long t0 = 0;
+  for (unsigned spins = 0;; ++spins) {
+    if (in) v = __hip_atomic_load(gp(glob) + 16 * (size_t)lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (__all((v >> 32) == epoch)) break;
+    if (spread_spin_over(spins, t0, err)) {
+      if (lane == 0) {
+        H.abort = 1;
+        err_raise(err, 1);
+      }
+      return false;
+    }
+    spin_pause();
+  }
+  uint32_t m = in ? (uint32_t)v : 0u;
+  m = max(m, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)m, 0xB1, 0xF, 0xF, false));
+  m = max(m, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)m, 0x4E, 0xF, 0xF, false));
+  m = max(m, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)m, 0x141, 0xF, 0xF, false));
+  m = max(m, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)m, 0x140, 0xF, 0xF, false));
+  out = (uint32_t)__builtin_amdgcn_readlane((int)m, 15);
+  return true;
+}
+
 // Cluster MAX of the packed selectHost key: one granule {epoch, 32-bit key} per shard when the
 // key fits 32 bits (kb > 0, key_bits), else two (lo, hi).
 __device__ __forceinline__ bool spread_argmax(SpreadHdr& H, int W, int w, int gs, unsigned& epoch, unsigned long long* gran,
@@ -563,6 +670,16 @@ __device__ __forceinline__ bool spread_argmax(SpreadHdr& H, int W, int w, int gs
   ++epoch;
   const int ng = kb ? 1 : 2;  // granules per shard
   const uint32_t kc = kb ? key_compress(best, kb, node_base) : 0u;
+  if (X.tl && kb) {  // two levels (tl_argmax): wave 0, the other waves wait at the barrier
+    if (wave == 0) {
+      uint32_t m = 0;
+      if (tl_argmax(H, X, W, epoch, kc, err, m) && lane == 0) H.kres = m ? key_expand(m, kb, node_base) : 0;
+    }
+    lds_barrier();
+    if (H.abort) return false;
+    key = H.kres;
+    return true;
+  }
   if (nw > 1 && W > 64) {  // every wave polls a share of the shards, 4 per lane in flight
     const unsigned long long tag = (unsigned long long)epoch << 32;
     if (wave == 0 && lane < ng)

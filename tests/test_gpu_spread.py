@@ -253,3 +253,38 @@ def test_program_fuzz_records_on_k_schedule(seed):
                                           err_msg=f"pod {j}")
             np.testing.assert_array_equal(r.total[:cc.n_nodes][feas], res.total[j, :cc.n_nodes][feas])
     ctx.close()
+
+
+@pytest.mark.parametrize("two_level", [1, 0])
+@pytest.mark.parametrize("shards", [65, 130])
+def test_two_level_argmax_many_shards(two_level, shards):
+    """k_spread's selectHost exchange at more than 64 shards: two levels (XCD-local plain
+    stores to the XCD's rank-0 shard, then one line per XCD; tl_argmax) and the flat sweep
+    (option spread_two_level 0), on fuzzed programs with ragged shards and over three chunk
+    launches, against the C oracle."""
+    native.set_option("shards", str(shards))
+    native.set_option("spread_two_level", str(two_level))
+    prof = abi.default_profile()
+    on_spread = 0
+    for seed in (20, 21, 51):
+        cc, cp = _fuzz(seed, 1000, 150)
+        ncl, nt = len(cc.classes), len(cc.terms)
+        chosen_o, res, st = _oracle(prof, cc.as_struct(), cp.as_struct(), cp.n, cc.n_nodes, ncl, nt)
+        ctx = native.Context(prof)
+        ctx.load(cc.as_struct())
+        chosen = ctx.schedule_batch(cp.as_struct(), cp.n)
+        on_spread += ctx.last_kernel() == "k_spread" and ctx.last_geometry()["shards"] == shards
+        _check(ctx, res, st, chosen, chosen_o, cp.n, cc.n_nodes, ncl, nt)
+        ctx.close()
+    assert on_spread >= 2
+    s = native.Synth(4, 3, 20000, 300)  # C4's recipe, three k_static chunks
+    native.set_option("static_bytes", str(4 * 20000 * 100))
+    chosen_o, res, st = _oracle(prof, s.cluster, s.pods, 300, 20000, s.cluster.n_classes, s.cluster.n_terms)
+    ctx = native.Context(prof)
+    ctx.load(s.cluster)
+    ctx.stage(s.pods)
+    chosen = ctx.run_staged(300)
+    assert ctx.last_kernel() == "k_spread" and ctx.last_geometry()["shards"] == shards
+    assert ctx.last_timing()[1] == 6
+    _check(ctx, res, st, chosen, chosen_o, 300, 20000, s.cluster.n_classes, s.cluster.n_terms)
+    ctx.close()
