@@ -170,6 +170,7 @@ struct XPeers {
   int32_t xcd_local;  // k_simple, one part: every shard on one XCD (xcd_slot), granules published with plain stores
   unsigned long long* inbox[KSS_MAX_PARTS];
   unsigned long long* tl;  // k_spread, one part, many shards: the two-level selectHost exchange's area (null: off)
+  int32_t tl_red;          // ... the statistics / filter exchanges in two levels too (spread_exchange_tl)
 };
 
 

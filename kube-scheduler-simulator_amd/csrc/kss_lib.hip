@@ -99,7 +99,7 @@ const OptDef kOptDefs[O_N] = {
     {"service_no_diff", "KSS_SERVICE_NO_DIFF", 0},
     {"svc_huge", "KSS_SVC_HUGE", 0},
     {"xcd_force_fallback", "KSS_XCD_FORCE_FALLBACK", 0},  // XCD-local launches report failed placement
-    {"spread_two_level", "KSS_SPREAD_TWO_LEVEL", 1},      // k_spread's two-level selectHost exchange (W > 64)
+    {"spread_two_level", "KSS_SPREAD_TWO_LEVEL", 1},      // k_spread at W > 64: 1 two-level selectHost exchange, 2 + reductions
 };
 std::atomic<long long> g_opt[O_N];
 std::once_flag g_opt_once;
@@ -2913,7 +2913,7 @@ static int launch_spread(hipStream_t st, const Geometry& g, const GpodNeeds& q, 
   const size_t tlw = tl_words(g.W);
   if (!sp_grid && !xcd && gran && g.W > 64 && opt(O_SPREAD_TWO_LEVEL) &&
       gran_bytes / 8 >= tlw + 2 * (size_t)g.W * (size_t)gs + 16)
-    X.tl = gran + gran_bytes / 8 - tlw;
+    X.tl = gran + gran_bytes / 8 - tlw, X.tl_red = opt(O_SPREAD_TWO_LEVEL) >= 2;
   kss_profile pr = prof;
   int W = g.W, n_lo = 0, n_hi = 0;
   static_rows(g, X, max_nodes, n_lo, n_hi);
@@ -3218,7 +3218,10 @@ static int run_single_impl(kss_ctx* ctx, const PlanNeeds& need, const DevPods& d
   rc = ctx->err_buf.ensure(16);
   if (rc) return rc;
   unsigned long long* gran = nullptr;
-  const size_t gb = sizeof(unsigned long long) * (2 * (size_t)g.W * std::max(2 * XW_MAX, G_XW) + (spread ? tl_words(g.W) : 0));
+  // k_spread on one part: the two-level exchanges' area behind the granules (launch_spread); a
+  // split grid's inbox holds the granules alone
+  const size_t gb = sizeof(unsigned long long) *
+                    (2 * (size_t)g.W * std::max(2 * XW_MAX, G_XW) + (spread && !split ? tl_words(g.W) : 0));
   unsigned epoch0 = 0;
   SplitRun srun;
   if (split) {  // the local inbox, never cleared: this run's epochs start above every earlier tag

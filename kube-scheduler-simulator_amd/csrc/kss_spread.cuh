@@ -469,84 +469,6 @@ __device__ __forceinline__ void hard_minima(const GPod& q, int32_t* xs) {
   }
 }
 
-// Cluster reduction of K int32 scalars v[] (ops[]), plus (W > 1) the cross-shard SUM of
-// bins [sum_lo, sum_lo + ns) and OR of [or_lo, or_lo + no) of xs.  local: workgroup only.
-// minima_q: the exchange wave then folds pod minima_q's critical-path minima into v (the
-// statistics exchange).  LDS-only barriers (the prefetch waves' HBM loads stay in flight).
-// False on abort.
-template <int K>
-__device__ __forceinline__ bool spread_reduce(SpreadHdr& H, int32_t* xs, int W, int w, int gs, unsigned& epoch,
-                                              unsigned long long* gran, const XPeers& X, int* err, int32_t (&v)[K],
-                                              const int (&ops)[K], int sum_lo = 0, int ns = 0, int or_lo = 0,
-                                              int no = 0, bool local = false, unsigned long long* sp = nullptr,
-                                              const GPod* minima_q = nullptr) {
-  static_assert(K <= G_NS, "too many values");
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
-  int32_t r[K];
-#pragma unroll
-  for (int k = 0; k < K; k++) r[k] = v[k];
-  wave_red32(r, ops);
-  if (KSS_LANE_RED) {  // lane k writes value k: one LDS store instruction instead of K on lane 0
-    if (lane < K) {
-      int32_t x = r[0];
-#pragma unroll
-      for (int k = 1; k < K; k++) x = lane == k ? r[k] : x;
-      H.red[wave][lane] = x;
-    }
-  } else if (lane == 0) {
-#pragma unroll
-    for (int k = 0; k < K; k++) H.red[wave][k] = r[k];
-  }
-  lds_barrier();
-  if (sp && threadIdx.x == 0) sp[0] = wall_clock64();
-  const bool xchg = W > 1 && !local;
-  if (!xchg) {
-    if (threadIdx.x < K) {
-      const int k = threadIdx.x;
-      int op = OP_SUM;
-#pragma unroll
-      for (int q = 0; q < K; q++)
-        if (q == k) op = ops[q];
-      int32_t r = H.red[0][k];
-      for (int x = 1; x < nw; x++) r = op32(op, r, H.red[x][k]);
-      xs[k] = r;
-    }
-    if (minima_q && wave == 0) hard_minima(*minima_q, xs);
-    lds_barrier();
-  } else {
-    unsigned opbits = 0;
-#pragma unroll
-    for (int k = 0; k < K; k++) opbits |= (unsigned)ops[k] << (2 * k);
-    ++epoch;
-    if (sp && threadIdx.x == 0) sp[1] = wall_clock64();
-    const int M = K + ns + no;
-    if (nw == 1 || (long long)W * M <= (long long)KSS_SPREAD_MW_MIN) {  // one polling round for one wave: wave 0 alone
-      if (wave == 0 && spread_exchange(H, xs, gran, X, W, w, gs, epoch, err, K, opbits, sum_lo, ns, or_lo, no, sp) &&
-          minima_q)
-        hard_minima(*minima_q, xs);
-      if (sp && threadIdx.x == 0) sp[4] = wall_clock64();
-      lds_barrier();
-      if (H.abort) return false;
-    } else {  // many shards: wave 0 publishes, every wave sweeps a share (fewer polling rounds)
-      if (wave == 0) spread_exchange(H, xs, gran, X, W, w, gs, epoch, err, K, opbits, sum_lo, ns, or_lo, no, sp, 0, 1, 1);
-      lds_barrier();  // the slots hold the operators' identities before any wave folds into them
-      const int nsw = min(nw, KSS_SPREAD_SWEEP_WAVES);  // the sweeping waves (the rest wait)
-      if (wave < nsw) spread_exchange(H, xs, gran, X, W, w, gs, epoch, err, K, opbits, sum_lo, ns, or_lo, no, nullptr, wave, nsw, 2);
-      lds_barrier();
-      if (H.abort) return false;
-      if (minima_q && wave == 0) hard_minima(*minima_q, xs);
-      if (sp && threadIdx.x == 0) sp[4] = wall_clock64();
-      lds_barrier();
-    }
-  }
-#pragma unroll
-  for (int k = 0; k < K; k++) v[k] = xs[k];
-  // no barrier here: the next reduction rewrites xs[0..K) (publish resets, or the local
-  // path's stores) only behind its own first barrier, which every wave reaches after reading
-  if (KSS_SPREAD_SAFE) lds_barrier();  // experiment: a trailing barrier after every exchange
-  return true;
-}
-
 // ---- Two-level selectHost exchange (one part, W > 64 shards over the chip's XCDs) -------------
 // The flat exchange has every shard poll every shard's granule across XCDs: at C4's 256 shards
 // a 3.2 us step (four waves sweep, then an LDS combine).  Two levels instead: each shard stores
@@ -555,11 +477,21 @@ __device__ __forceinline__ bool spread_reduce(SpreadHdr& H, int32_t* xs, int W, 
 // shard polls its XCD's <= 64 keys with one load per lane, stores their maximum write-through
 // (agent scope) into one line per XCD, and every shard polls the <= 16 XCD maxima.  Which XCD
 // a shard runs on is read from XCC_ID at the start of the launch (tl_register), never assumed.
-// Area (8-byte words, X.tl): [0, 16) counters (shards per XCD, [8] all), then per parity
-// TL_G x tl_ls(W) XCD slots, then per parity TL_G lines of 16 words (one XCD maximum each).
+// The statistics and filter exchanges (spread_reduce) can take the same two levels when they carry
+// at most TL_M values (spread_exchange_tl, option spread_two_level = 2).  Measured slower at C4
+// (x_stats 2.17 -> 2.36, x_filter 2.79 -> 3.01 us, 95.7k -> 90.8k pods/s, profiles/r8j_c4_bench.json):
+// the flat sweep spreads those values over four waves, the two levels put two dependent hops on
+// one wave; off by default.
+// Area (8-byte words, X.tl): [0, 16) counters (shards per XCD, [TL_G] all); the argmax: per parity
+// TL_G x tl_ls(W) XCD slots, then per parity TL_G lines of 16 words (one XCD maximum each); the
+// reductions: per parity TL_G x tl_ls(W) lines of TL_M values (one line per shard), then per
+// parity TL_G lines of TL_M values.
 constexpr int TL_G = 16;  // XCC ids 0..15
+constexpr int TL_M = 16;  // values of a two-level reduction (one 128-byte line)
 __host__ __device__ inline int tl_ls(int W) { return (W + 15) / 16 * 16; }
-__host__ __device__ inline size_t tl_words(int W) { return 16 + 2 * (size_t)TL_G * tl_ls(W) + 2 * (size_t)TL_G * 16; }
+__host__ __device__ inline size_t tl_o_rloc(int W) { return 16 + 2 * (size_t)TL_G * tl_ls(W) + 2 * (size_t)TL_G * 16; }
+__host__ __device__ inline size_t tl_o_rglob(int W) { return tl_o_rloc(W) + 2 * (size_t)TL_G * tl_ls(W) * TL_M; }
+__host__ __device__ inline size_t tl_words(int W) { return tl_o_rglob(W) + 2 * (size_t)TL_G * TL_M; }
 
 // Thread 0: the shard's XCD and rank there; every shard of the launch registered (bounded wait).
 __device__ __forceinline__ void tl_register(SpreadHdr& H, unsigned long long* tl, int W, int* err) {
@@ -649,6 +581,189 @@ __device__ __forceinline__ bool tl_argmax(SpreadHdr& H, const XPeers& X, int W, 
   m = max(m, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)m, 0x141, 0xF, 0xF, false));
   m = max(m, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)m, 0x140, 0xF, 0xF, false));
   out = (uint32_t)__builtin_amdgcn_readlane((int)m, 15);
+  return true;
+}
+
+// spread_exchange's two-level form (X.tl, M = K + ns + no <= TL_M values, no payload): wave 0.
+// Every shard stores its M values as one line into its XCD's area (plain stores: that XCD's L2);
+// the XCD's rank-0 shard folds its shards' lines (MP = M rounded up to a power of two lanes per
+// shard, 64 / MP shards per load round) and stores the XCD's M values write-through into one
+// line; every shard folds the XCDs' lines into xs.  False on a timed-out wait (H.abort set).
+__device__ __forceinline__ bool spread_exchange_tl(SpreadHdr& H, int32_t* xs, const XPeers& X, int W, unsigned epoch,
+                                                   int* err, int K, unsigned opbits, int sum_lo, int ns, int or_lo,
+                                                   int no) {
+  const int lane = threadIdx.x & 63, nw = blockDim.x >> 6;
+  const int M = K + ns + no;
+  const int MP = M <= 4 ? 4 : (M <= 8 ? 8 : 16);
+  auto slot = [&](int j) -> int32_t* {
+    if (j < K) return xs + j;
+    if (j < K + ns) return xs + G_NS + sum_lo + (j - K);
+    return xs + G_NS + or_lo + (j - K - ns);
+  };
+  auto opof = [&](int j) { return j < K ? (int)((opbits >> (2 * j)) & 3u) : (j < K + ns ? OP_SUM : OP_OR); };
+  const int ls = tl_ls(W);
+  const unsigned long long tag = (unsigned long long)epoch << 32;
+  unsigned long long* loc = X.tl + tl_o_rloc(W) + ((size_t)(epoch & 1) * TL_G + H.tl_x) * ls * TL_M;
+  unsigned long long* glob = X.tl + tl_o_rglob(W) + (size_t)(epoch & 1) * TL_G * TL_M;
+  const int j = lane & (MP - 1), t = lane / MP, T = 64 / MP;
+  const bool jv = j < M;
+  const int op = opof(jv ? j : 0);
+  if (lane < M) {  // this shard's values (scalars: its waves' partials)
+    int32_t v = *slot(lane);
+    if (lane < K) {
+      v = H.red[0][lane];
+      for (int x = 1; x < nw; x++) v = op32_lane(op, v, H.red[x][lane]);
+    }
+    asm volatile("global_store_dwordx2 %0, %1, off" ::"v"(loc + (size_t)H.tl_s * TL_M + lane), "v"(tag | (uint32_t)v)
+                 : "memory");
+  }
+  auto wait_all = [&](auto&& load, unsigned long long (&g)[4], bool (&in)[4]) -> bool {
+    long long t0 = 0;
+    for (unsigned spins = 0;; ++spins) {
+      bool ok = true;
+#pragma unroll
+      for (int b = 0; b < 4; b++) {
+        g[b] = in[b] ? load(b) : tag;
+        ok &= (g[b] >> 32) == epoch;
+      }
+      if (__all(ok)) return true;
+      if (spread_spin_over(spins, t0, err)) {
+        if (lane == 0) {
+          H.abort = 1;
+          err_raise(err, 1);
+        }
+        return false;
+      }
+      spin_pause();
+    }
+  };
+  if (H.tl_s == 0) {  // the XCD's values: its shards' lines from this XCD's L2
+    int32_t acc = ident32(op);
+    const int n = H.tl_n;
+    for (int s0 = 0; s0 < n; s0 += 4 * T) {
+      unsigned long long g[4];
+      bool in[4];
+#pragma unroll
+      for (int b = 0; b < 4; b++) in[b] = jv && s0 + t + T * b < n;
+      if (!wait_all([&](int b) { return __hip_atomic_load(gp(loc) + (size_t)(s0 + t + T * b) * TL_M + j, __ATOMIC_RELAXED,
+                                                          __HIP_MEMORY_SCOPE_AGENT); },
+                    g, in))
+        return false;
+#pragma unroll
+      for (int b = 0; b < 4; b++)
+        if (in[b]) acc = op32_lane(op, acc, (int32_t)(uint32_t)g[b]);
+    }
+    for (int o = MP; o < 64; o <<= 1) acc = op32_lane(op, acc, __shfl_xor(acc, o, 64));
+    if (t == 0 && jv)
+      __hip_atomic_store(gp(glob) + (size_t)H.tl_x * TL_M + j, tag | (uint32_t)acc, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+  }
+  // every shard: the XCDs' lines, 4 * T of them per load round
+  int32_t acc = ident32(op);
+  for (int g0 = 0; g0 < TL_G; g0 += 4 * T) {
+    const uint32_t span = (4 * T >= 32) ? 0xFFFFFFFFu : ((1u << (4 * T)) - 1u);
+    if (((H.tl_mask >> g0) & span) == 0) continue;
+    unsigned long long g[4];
+    bool in[4];
+#pragma unroll
+    for (int b = 0; b < 4; b++) {
+      const int x = g0 + t + T * b;
+      in[b] = jv && x < TL_G && ((H.tl_mask >> x) & 1u);
+    }
+    if (!wait_all([&](int b) { return __hip_atomic_load(gp(glob) + (size_t)(g0 + t + T * b) * TL_M + j, __ATOMIC_RELAXED,
+                                                        __HIP_MEMORY_SCOPE_AGENT); },
+                  g, in))
+      return false;
+#pragma unroll
+    for (int b = 0; b < 4; b++)
+      if (in[b]) acc = op32_lane(op, acc, (int32_t)(uint32_t)g[b]);
+  }
+  for (int o = MP; o < 64; o <<= 1) acc = op32_lane(op, acc, __shfl_xor(acc, o, 64));
+  if (t == 0 && jv) *slot(j) = acc;
+  return true;
+}
+
+// Cluster reduction of K int32 scalars v[] (ops[]), plus (W > 1) the cross-shard SUM of
+// bins [sum_lo, sum_lo + ns) and OR of [or_lo, or_lo + no) of xs.  local: workgroup only.
+// minima_q: the exchange wave then folds pod minima_q's critical-path minima into v (the
+// statistics exchange).  LDS-only barriers (the prefetch waves' HBM loads stay in flight).
+// False on abort.
+template <int K>
+__device__ __forceinline__ bool spread_reduce(SpreadHdr& H, int32_t* xs, int W, int w, int gs, unsigned& epoch,
+                                              unsigned long long* gran, const XPeers& X, int* err, int32_t (&v)[K],
+                                              const int (&ops)[K], int sum_lo = 0, int ns = 0, int or_lo = 0,
+                                              int no = 0, bool local = false, unsigned long long* sp = nullptr,
+                                              const GPod* minima_q = nullptr) {
+  static_assert(K <= G_NS, "too many values");
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  int32_t r[K];
+#pragma unroll
+  for (int k = 0; k < K; k++) r[k] = v[k];
+  wave_red32(r, ops);
+  if (KSS_LANE_RED) {  // lane k writes value k: one LDS store instruction instead of K on lane 0
+    if (lane < K) {
+      int32_t x = r[0];
+#pragma unroll
+      for (int k = 1; k < K; k++) x = lane == k ? r[k] : x;
+      H.red[wave][lane] = x;
+    }
+  } else if (lane == 0) {
+#pragma unroll
+    for (int k = 0; k < K; k++) H.red[wave][k] = r[k];
+  }
+  lds_barrier();
+  if (sp && threadIdx.x == 0) sp[0] = wall_clock64();
+  const bool xchg = W > 1 && !local;
+  if (!xchg) {
+    if (threadIdx.x < K) {
+      const int k = threadIdx.x;
+      int op = OP_SUM;
+#pragma unroll
+      for (int q = 0; q < K; q++)
+        if (q == k) op = ops[q];
+      int32_t r = H.red[0][k];
+      for (int x = 1; x < nw; x++) r = op32(op, r, H.red[x][k]);
+      xs[k] = r;
+    }
+    if (minima_q && wave == 0) hard_minima(*minima_q, xs);
+    lds_barrier();
+  } else {
+    unsigned opbits = 0;
+#pragma unroll
+    for (int k = 0; k < K; k++) opbits |= (unsigned)ops[k] << (2 * k);
+    ++epoch;
+    if (sp && threadIdx.x == 0) sp[1] = wall_clock64();
+    const int M = K + ns + no;
+    if (X.tl_red && M <= TL_M) {  // two levels (spread_exchange_tl; option spread_two_level = 2), wave 0
+      if (wave == 0 && spread_exchange_tl(H, xs, X, W, epoch, err, K, opbits, sum_lo, ns, or_lo, no) && minima_q)
+        hard_minima(*minima_q, xs);
+      if (sp && threadIdx.x == 0) sp[4] = wall_clock64();
+      lds_barrier();
+      if (H.abort) return false;
+    } else if (nw == 1 || (long long)W * M <= (long long)KSS_SPREAD_MW_MIN) {  // one polling round for one wave: wave 0 alone
+      if (wave == 0 && spread_exchange(H, xs, gran, X, W, w, gs, epoch, err, K, opbits, sum_lo, ns, or_lo, no, sp) &&
+          minima_q)
+        hard_minima(*minima_q, xs);
+      if (sp && threadIdx.x == 0) sp[4] = wall_clock64();
+      lds_barrier();
+      if (H.abort) return false;
+    } else {  // many shards: wave 0 publishes, every wave sweeps a share (fewer polling rounds)
+      if (wave == 0) spread_exchange(H, xs, gran, X, W, w, gs, epoch, err, K, opbits, sum_lo, ns, or_lo, no, sp, 0, 1, 1);
+      lds_barrier();  // the slots hold the operators' identities before any wave folds into them
+      const int nsw = min(nw, KSS_SPREAD_SWEEP_WAVES);  // the sweeping waves (the rest wait)
+      if (wave < nsw) spread_exchange(H, xs, gran, X, W, w, gs, epoch, err, K, opbits, sum_lo, ns, or_lo, no, nullptr, wave, nsw, 2);
+      lds_barrier();
+      if (H.abort) return false;
+      if (minima_q && wave == 0) hard_minima(*minima_q, xs);
+      if (sp && threadIdx.x == 0) sp[4] = wall_clock64();
+      lds_barrier();
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < K; k++) v[k] = xs[k];
+  // no barrier here: the next reduction rewrites xs[0..K) (publish resets, or the local
+  // path's stores) only behind its own first barrier, which every wave reaches after reading
+  if (KSS_SPREAD_SAFE) lds_barrier();  // experiment: a trailing barrier after every exchange
   return true;
 }
 

@@ -255,12 +255,13 @@ def test_program_fuzz_records_on_k_schedule(seed):
     ctx.close()
 
 
-@pytest.mark.parametrize("two_level", [1, 0])
+@pytest.mark.parametrize("two_level", [1, 0, 2])
 @pytest.mark.parametrize("shards", [65, 130])
 def test_two_level_argmax_many_shards(two_level, shards):
-    """k_spread's selectHost exchange at more than 64 shards: two levels (XCD-local plain
-    stores to the XCD's rank-0 shard, then one line per XCD; tl_argmax) and the flat sweep
-    (option spread_two_level 0), on fuzzed programs with ragged shards and over three chunk
+    """k_spread's exchanges at more than 64 shards: the selectHost key in two levels (XCD-local
+    plain stores to the XCD's rank-0 shard, then one line per XCD; tl_argmax; the default), the
+    flat sweep (option spread_two_level 0), and the statistics / filter exchanges in two levels
+    too (2, spread_exchange_tl), on fuzzed programs with ragged shards and over three chunk
     launches, against the C oracle."""
     native.set_option("shards", str(shards))
     native.set_option("spread_two_level", str(two_level))
