@@ -631,7 +631,9 @@ def run_per_pod(args):
     n_nodes = args.nodes or 5000
     n_pods = args.pods or 500
     s = native.Synth(2, SEED_BASE + 2, n_nodes, n_pods)
-    ctx = native.Context(abi.default_profile())
+    prof = abi.default_profile()
+    prof.pct_nodes_to_score = args.pct  # --pct 0: the simulator's own setting (adaptive window)
+    ctx = native.Context(prof)
     ctx.load(s.cluster)
     for j in range(min(args.warmup * 20, n_pods)):  # warm the kernels, then restore the snapshot
         r = ctx.eval_pod(s.pods, j)
@@ -775,8 +777,9 @@ def run_per_pod(args):
         "vs_baseline": None,
         "dtype": "int64/f64",
         "data": "synthetic (SplitMix64 seed 0x5EED0002)",
-        "config": {"workload": f"C2 cluster, per-pod API: {n_nodes} nodes, {n_pods} pods one call pair each",
-                   "nodes": n_nodes, "pods": n_pods, "parallelism": "none"},
+        "config": {"workload": f"C2 cluster, per-pod API: {n_nodes} nodes, {n_pods} pods one call pair each, "
+                               f"pct={args.pct}",
+                   "nodes": n_nodes, "pods": n_pods, "parallelism": "none", "percentage_of_nodes_to_score": args.pct},
         "eval_us": {"median": float(np.median(ev)), "mean": float(ev.mean()), "p90": float(np.percentile(ev, 90))},
         "eval_slim_us": {"median": float(np.median(ev_slim)), "mean": float(ev_slim.mean()),
                          "p90": float(np.percentile(ev_slim, 90)), "fields": "fail_plugin, fail_detail, total",

@@ -1415,6 +1415,17 @@ int kss_oracle_schedule_n(const kss_profile* prof, const kss_cluster* cl, const 
                                nom_pod, nom_node, n_nom, nom_left, NULL, NULL);
 }
 
+/* kss_oracle_schedule_w where pods with skip_commit[i] != 0 are evaluated but not assumed: the
+   per-pod API's commit followed by a rollback of the same pod (Reserve then Unreserve leave the
+   node state as it was; tests/test_gpu_service.py replays a service sequence with it). */
+int kss_oracle_schedule_wm(const kss_profile* prof, const kss_cluster* cl, const kss_podset* ps, int n,
+                           int32_t* chosen, kss_pod_result* results, int threads, int64_t* out_requested,
+                           int64_t* out_nonzero, int32_t* out_pod_count, int32_t* out_class_count,
+                           int32_t* out_term_count, uint64_t* out_port_used, int32_t* out_vol_count,
+                           int32_t* out_vol_attached, int32_t* cursor, const int32_t* nom_pod,
+                           const int32_t* nom_node, int32_t n_nom, uint8_t* nom_left, int32_t* out_pv_owner,
+                           int32_t* out_claim_node, const uint8_t* skip_commit);
+
 int kss_oracle_schedule_w(const kss_profile* prof, const kss_cluster* cl, const kss_podset* ps, int n,
                           int32_t* chosen, kss_pod_result* results, int threads, int64_t* out_requested,
                           int64_t* out_nonzero, int32_t* out_pod_count, int32_t* out_class_count,
@@ -1422,6 +1433,18 @@ int kss_oracle_schedule_w(const kss_profile* prof, const kss_cluster* cl, const 
                           int32_t* out_vol_attached, int32_t* cursor, const int32_t* nom_pod,
                           const int32_t* nom_node, int32_t n_nom, uint8_t* nom_left, int32_t* out_pv_owner,
                           int32_t* out_claim_node) {
+  return kss_oracle_schedule_wm(prof, cl, ps, n, chosen, results, threads, out_requested, out_nonzero, out_pod_count,
+                                out_class_count, out_term_count, out_port_used, out_vol_count, out_vol_attached,
+                                cursor, nom_pod, nom_node, n_nom, nom_left, out_pv_owner, out_claim_node, NULL);
+}
+
+int kss_oracle_schedule_wm(const kss_profile* prof, const kss_cluster* cl, const kss_podset* ps, int n,
+                           int32_t* chosen, kss_pod_result* results, int threads, int64_t* out_requested,
+                           int64_t* out_nonzero, int32_t* out_pod_count, int32_t* out_class_count,
+                           int32_t* out_term_count, uint64_t* out_port_used, int32_t* out_vol_count,
+                           int32_t* out_vol_attached, int32_t* cursor, const int32_t* nom_pod,
+                           const int32_t* nom_node, int32_t n_nom, uint8_t* nom_left, int32_t* out_pv_owner,
+                           int32_t* out_claim_node, const uint8_t* skip_commit) {
   ostate s;
   if (ostate_init(&s, cl)) return KSS_E_NOMEM;
   if (cursor) s.cursor = *cursor;
@@ -1446,7 +1469,7 @@ int kss_oracle_schedule_w(const kss_profile* prof, const kss_cluster* cl, const 
     rc = schedule_one(prof, &s, ps, i, out, th);
     if (rc) break;
     chosen[i] = out->chosen;
-    if (out->chosen >= 0) commit(&s, ps, i, out->chosen - cl->node_base);
+    if (out->chosen >= 0 && !(skip_commit && skip_commit[i])) commit(&s, ps, i, out->chosen - cl->node_base);
   }
   size_t N = (size_t)cl->n_nodes;
   if (out_requested) memcpy(out_requested, s.requested, sizeof(int64_t) * KSS_NRES * N);

@@ -32,6 +32,8 @@ def lib():
         _lib.kss_oracle_schedule_n.restype = C.c_int
         _lib.kss_oracle_schedule_w.argtypes = _lib.kss_oracle_schedule_n.argtypes + [P(C.c_int32), P(C.c_int32)]
         _lib.kss_oracle_schedule_w.restype = C.c_int
+        _lib.kss_oracle_schedule_wm.argtypes = _lib.kss_oracle_schedule_w.argtypes + [P(C.c_uint8)]
+        _lib.kss_oracle_schedule_wm.restype = C.c_int
         _lib.kss_oracle_eval_pod.argtypes = [P(abi.Profile), P(abi.Cluster), P(abi.PodSet), C.c_int,
                                              P(abi.PodResult), C.c_int]
         _lib.kss_oracle_eval_pod.restype = C.c_int
@@ -97,12 +99,13 @@ class Results:
 
 
 def schedule(profile, cluster_struct, podset_struct, n_pods, n_nodes, threads=1, record=True, n_classes=0,
-             n_terms=0, cursor=0, nominations=()):
+             n_terms=0, cursor=0, nominations=(), skip_commit=None):
     """Run the C oracle sequentially; returns (chosen, Results|None, final_state dict).
     record=True keeps every per-node array, record="meta" only the per-pod outcomes.
     cursor: the scheduler's nextStartNodeIndex at the first pod; the final value is
     final_state["next_start"].  nominations: [(pod index, global node)] in the nominator's
-    order; final_state["nominations"] lists those still active afterwards."""
+    order; final_state["nominations"] lists those still active afterwards.  skip_commit: per pod,
+    evaluated but not assumed (a commit the caller rolled back)."""
     L = lib()
     chosen = np.full(max(n_pods, 1), -2, dtype=np.int32)
     res = Results(n_pods, n_nodes, arrays=record is True) if record else None
@@ -120,7 +123,10 @@ def schedule(profile, cluster_struct, podset_struct, n_pods, n_nodes, threads=1,
     nom_pod = np.array([a for a, _ in nominations] or [0], dtype=np.int32)
     nom_node = np.array([b for _, b in nominations] or [0], dtype=np.int32)
     nom_left = np.zeros(max(len(nominations), 1), dtype=np.uint8)
-    rc = L.kss_oracle_schedule_w(C.byref(profile), C.byref(cluster_struct), C.byref(podset_struct), n_pods,
+    skip = np.zeros(max(n_pods, 1), np.uint8)
+    if skip_commit is not None:
+        skip[:n_pods] = np.asarray(skip_commit, np.uint8)[:n_pods]
+    rc = L.kss_oracle_schedule_wm(C.byref(profile), C.byref(cluster_struct), C.byref(podset_struct), n_pods,
                                chosen.ctypes.data_as(P(C.c_int32)), res.structs if res else None, threads,
                                st["requested"].ctypes.data_as(P(C.c_int64)), st["nonzero"].ctypes.data_as(P(C.c_int64)),
                                st["pod_count"].ctypes.data_as(P(C.c_int32)),
@@ -131,7 +137,8 @@ def schedule(profile, cluster_struct, podset_struct, n_pods, n_nodes, threads=1,
                                st["vol_attached"].ctypes.data_as(P(C.c_int32)), C.byref(cur),
                                nom_pod.ctypes.data_as(P(C.c_int32)), nom_node.ctypes.data_as(P(C.c_int32)),
                                len(nominations), nom_left.ctypes.data_as(P(C.c_uint8)),
-                               st["pv_owner"].ctypes.data_as(P(C.c_int32)), st["claim_node"].ctypes.data_as(P(C.c_int32)))
+                               st["pv_owner"].ctypes.data_as(P(C.c_int32)), st["claim_node"].ctypes.data_as(P(C.c_int32)),
+                               skip.ctypes.data_as(P(C.c_uint8)))
     assert rc == 0, f"oracle rc={rc}"
     st["pv_owner"] = st["pv_owner"][:cluster_struct.n_pvs]
     st["claim_node"] = st["claim_node"][:cluster_struct.n_wclaims]
