@@ -3968,10 +3968,11 @@ static int svc_start_locked(kss_ctx* ctx) {
   if (window) W = std::min(W, XW_MAX - NSCAL);
   const PlanNeeds& need = ctx->staged_need;
   // the k_simple-shaped evaluation (svc_simple_eval): staged default-profile pods (compact records,
-  // no programs), no window, no extended resources, exact f64 arithmetic, W <= 64 (its exchange:
+  // no programs; under percentageOfNodesToScore < 100 no PreFilterResult node lists: svc_window),
+  // no extended resources, exact f64 arithmetic, W <= 64 (its exchange:
   // one lane per shard), the node rows cached in LDS (checked below); KSS_SERVICE_GENERAL=1 keeps
   // the general chain, for comparison.  On an XCD-local grid when its shards fit one XCD's CUs.
-  const bool simple_pre = ctx->spod_ok && !window && !need.general && ctx->dc.n_scalar == 0 && ctx->small_values &&
+  const bool simple_pre = ctx->spod_ok && (!window || !ctx->staged_names) && !need.general && ctx->dc.n_scalar == 0 && ctx->small_values &&
                           f64_exact(ctx->f64_cluster, ctx->f64_pods, ctx->staged_n) && !opt(O_SERVICE_GENERAL);
   const int xcd_cus = ctx->n_cu / XCD_GRID_MULT;
   // (off by default: the record's stores to host memory from one XCD were slower than the L2

@@ -471,6 +471,194 @@ __device__ __forceinline__ void svc_prefetch(const DevJob& job, long long* smem,
   __syncthreads();
 }
 
+// The findNodesThatPassFilters window on the SIMPLE evaluation (percentageOfNodesToScore < 100,
+// no PreFilterResult node lists): k_simple's simple_sync_win for one pod, without
+// the speculative halves.  The node list is visited from the cursor s0 in canonical order,
+// wrapping: segments a_0 .. a_{W-1} (each shard's nodes >= s0), then b_0 .. b_{W-1} (< s0).  One
+// exchange gathers every shard's {feasible count, max raw TaintToleration, max raw NodeAffinity}
+// per part (lane l of wave 0 <- shard l: W <= 64); every shard finds the segment holding the
+// (K+1)-th feasible node and the maxima of the segments wholly before it; the cut segment's
+// shard ranks its feasible nodes for the stopping node d and the maxima over the first j, and a
+// second exchange hands {d, TT, NA} to every shard (the cursor moves to d everywhere).
+// u = this lane's {Fa, TTa, NAa, Fb, TTb, NAb}.  Out: nf (kept feasible nodes), the maxima over
+// them, wd (d, -1 when fewer than K + 1 nodes are feasible).  False on abort.
+__device__ bool svc_window(long long* smem, Shard& S, bool plain, int K, int s0, const SlotArrays& sa, int npt,
+                           const uint32_t (&u)[6], long long& nf, long long& mtt, long long& mna, int& wd) {
+  SharedHdr& h = shdr(smem);
+  long long* xv = xvec(smem);
+  const int tid = threadIdx.x, nt = blockDim.x, lane = tid & 63, wave = tid >> 6, nw = nt >> 6;
+#pragma unroll
+  for (int i = 0; i < 6; i++) {
+    const long long r = wave_reduce((long long)u[i], i % 3 == 0 ? OP_SUM : OP_MAX);
+    if (lane == 0) h.red[wave][i] = r;
+  }
+  __syncthreads();
+  const unsigned ep = S.W > 1 ? ++S.epoch : S.epoch;
+  if (wave == 0) {
+    long long v[6];
+#pragma unroll
+    for (int i = 0; i < 6; i++) {
+      v[i] = h.red[0][i];
+      for (int x = 1; x < nw; x++) v[i] = op_apply(i % 3 == 0 ? OP_SUM : OP_MAX, v[i], h.red[x][i]);
+    }
+    // every shard's row in the lane of that shard: {Fa << 16 | TTa, NAa, Fb << 16 | TTb, NAb}
+    const uint32_t mine[4] = {(uint32_t)((v[0] << 16) | v[1]), (uint32_t)v[2], (uint32_t)((v[3] << 16) | v[4]),
+                              (uint32_t)v[5]};
+    uint32_t g4[4] = {0, 0, 0, 0};
+    bool ok = true;
+    if (S.W == 1) {
+#pragma unroll
+      for (int i = 0; i < 4; i++) g4[i] = lane == 0 ? mine[i] : 0u;
+    } else {
+      const unsigned long long tag = (unsigned long long)ep << 32;
+      unsigned long long* row = S.gran + (size_t)(ep & 1) * S.W * SVC_XG;
+      if (lane < 4) {
+        uint32_t x = mine[0];
+        x = lane == 1 ? mine[1] : x;
+        x = lane == 2 ? mine[2] : x;
+        x = lane == 3 ? mine[3] : x;
+        unsigned long long* q = row + (size_t)S.w * SVC_XG + lane;
+        if (plain) asm volatile("global_store_dwordx2 %0, %1, off" ::"v"(q), "v"(tag | x) : "memory");
+        else __hip_atomic_store(gp(q), tag | x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      long long t0 = 0;
+      for (unsigned spins = 0;; ++spins) {
+        bool got = true;
+        unsigned long long w4[4] = {tag, tag, tag, tag};
+        if (lane < S.W) {
+          KSS_GLOBAL const unsigned long long* g = gp(row) + (size_t)lane * SVC_XG;
+#pragma unroll
+          for (int i = 0; i < 4; i++) w4[i] = __hip_atomic_load(g + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; i++) got &= (w4[i] >> 32) == ep;
+        if (__all(got)) {
+#pragma unroll
+          for (int i = 0; i < 4; i++) g4[i] = lane < S.W ? (uint32_t)w4[i] : 0u;
+          break;
+        }
+        if (spin_expired(spins, t0)) {
+          if (lane == 0) err_raise(S.err, 1);
+          ok = false;
+          break;
+        }
+      }
+    }
+    const uint32_t Fa = g4[0] >> 16, ta = g4[0] & 0xFFFFu, na = g4[1], Fb = g4[2] >> 16, tb = g4[2] & 0xFFFFu, nb = g4[3];
+    const uint32_t A = (uint32_t)wave_reduce((long long)Fa, OP_SUM), B = (uint32_t)wave_reduce((long long)Fb, OP_SUM);
+    const uint32_t F = A + B;
+    long long ftt, fna;
+    int cut = -1, part = 0, j = 0;
+    if (F <= (uint32_t)K) {
+      ftt = wave_reduce((long long)max(ta, tb), OP_MAX);
+      fna = wave_reduce((long long)max(na, nb), OP_MAX);
+    } else {
+      const uint32_t pa = wave_incl_scan(Fa) - Fa, pb = A + wave_incl_scan(Fb) - Fb, Ku = (uint32_t)K;
+      ftt = wave_reduce((long long)max(pa + Fa <= Ku ? ta : 0u, pb + Fb <= Ku ? tb : 0u), OP_MAX);
+      fna = wave_reduce((long long)max(pa + Fa <= Ku ? na : 0u, pb + Fb <= Ku ? nb : 0u), OP_MAX);
+      const unsigned long long ba = __ballot(pa <= Ku && Ku < pa + Fa), bb = __ballot(pb <= Ku && Ku < pb + Fb);
+      const int l = __ffsll((long long)(ba ? ba : bb)) - 1;
+      cut = l;
+      part = ba ? 0 : 1;
+      j = (int)(Ku - (uint32_t)__builtin_amdgcn_readlane((int)(ba ? pa : pb), l));
+    }
+    if (lane == 0) {
+      xv[0] = F;
+      xv[1] = ftt;
+      xv[2] = fna;
+      xv[3] = cut;
+      xv[4] = part;
+      xv[5] = j;
+      xv[6] = -1;  // d, written by the cut shard's scan
+      if (!ok) h.abort = 1;
+    }
+  }
+  __syncthreads();
+  if (h.abort) return false;
+  nf = xv[0];
+  mtt = xv[1];
+  mna = xv[2];
+  wd = -1;
+  const int cut = (int)xv[3], part = (int)xv[4], j = (int)xv[5];
+  if (cut < 0) return true;
+  nf = K;
+  int ctt = 0, cna = 0;
+  if (cut == S.w) {  // rank the part's feasible nodes in canonical order (slot k-major): d = rank j
+    int carry = 0;
+    for (int k = 0; k < npt; k++) {
+      const int n = S.lo + k * nt + tid, si = k * nt + tid;
+      const bool f = n < S.hi && (sa.fail[si] & 0xFF) == KSS_F_PASS && (part == 0 ? n >= s0 : n < s0);
+      const unsigned long long b = __ballot(f);
+      if (lane == 0) h.red[wave][8 + (k & 1)] = (long long)__popcll(b);
+      __syncthreads();
+      int before = 0, tot = 0;
+      for (int x = 0; x < nw; x++) {
+        const int cx = (int)h.red[x][8 + (k & 1)];
+        before += x < wave ? cx : 0;
+        tot += cx;
+      }
+      const int rank = carry + before + (int)__popcll(b & ((1ull << lane) - 1ull));
+      if (f && rank == j) xv[6] = n;
+      ctt = max(ctt, (f && rank < j) ? sa.tt[si] : 0);
+      cna = max(cna, (f && rank < j) ? (int)sa.na[si] : 0);
+      carry += tot;
+    }
+    ctt = (int)wave_reduce((long long)ctt, OP_MAX);
+    cna = (int)wave_reduce((long long)cna, OP_MAX);
+    if (lane == 0) {
+      h.red[wave][10] = ctt;
+      h.red[wave][11] = cna;
+    }
+    __syncthreads();
+    for (int x = 0; x < nw; x++) {
+      ctt = max(ctt, (int)h.red[x][10]);
+      cna = max(cna, (int)h.red[x][11]);
+    }
+  }
+  if (S.W == 1) {
+    wd = (int)xv[6];
+    mtt = max(mtt, (long long)ctt);
+    mna = max(mna, (long long)cna);
+    __syncthreads();  // xv is rewritten by the next exchange
+    return true;
+  }
+  // the second exchange keeps the first one's epoch, in an area of its own (parity ep & 1): the
+  // next exchange's tag is ep + 1, so no shard can overwrite a row another still polls
+  const unsigned ep2 = ep;
+  unsigned long long* e2 = S.gran + 2 * (size_t)S.W * SVC_XG + (size_t)(ep2 & 1) * 4;
+  const unsigned long long tag2 = (unsigned long long)ep2 << 32;
+  if (cut == S.w && tid < 3) {
+    const uint32_t x = tid == 0 ? (uint32_t)xv[6] : (tid == 1 ? (uint32_t)ctt : (uint32_t)cna);
+    if (plain) asm volatile("global_store_dwordx2 %0, %1, off" ::"v"(e2 + tid), "v"(tag2 | x) : "memory");
+    else __hip_atomic_store(gp(e2) + tid, tag2 | x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();  // the cut shard's xv[6] read before any lane rewrites it below
+  if (wave == 0) {
+    long long t0 = 0;
+    for (unsigned spins = 0;; ++spins) {
+      const unsigned long long g = __hip_atomic_load(gp(e2) + min(lane, 2), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (__all((g >> 32) == ep2)) {
+        if (lane < 3) xv[8 + lane] = (long long)(uint32_t)g;
+        break;
+      }
+      if (spin_expired(spins, t0)) {
+        if (lane == 0) {
+          err_raise(S.err, 1);
+          h.abort = 1;
+        }
+        break;
+      }
+    }
+  }
+  __syncthreads();
+  if (h.abort) return false;
+  wd = (int)xv[8];
+  mtt = max(mtt, xv[9]);
+  mna = max(mna, xv[10]);
+  __syncthreads();  // xv is rewritten by the next exchange
+  return true;
+}
+
 template <bool COMPACT, bool INL>
 __device__ bool svc_simple_eval(const DevCluster& c, const DevJob& job, const kss_profile& prof, int pi, long long* smem,
                                 Shard& S, int bins_cap, int npt, unsigned want, uint8_t* host, PodMeta& meta, bool plain,
@@ -527,6 +715,11 @@ __device__ bool svc_simple_eval(const DevCluster& c, const DevJob& job, const ks
     return true;
   }
   const uint32_t en = prof.filter_enabled;
+  // percentageOfNodesToScore < 100: the window from the cursor (svc_window)
+  const int k_find = num_feasible_to_find(c.N, prof.pct_nodes_to_score);
+  const bool win = k_find < c.N;
+  const int s0 = win ? (int)(((long long)S.cursor % c.N + c.N) % c.N) : 0;
+  uint32_t wu[6] = {0, 0, 0, 0, 0, 0};  // this lane's {Fa, TTa, NAa, Fb, TTb, NAb}
   long long nf = 0, max_tt = 0, max_na = 0;
   for (int k = 0; k < npt; k++) {
     const int n = S.lo + k * nt + tid;
@@ -564,10 +757,18 @@ __device__ bool svc_simple_eval(const DevCluster& c, const DevJob& job, const ks
       nf++;
       max_tt = e.tt > max_tt ? e.tt : max_tt;
       max_na = e.na > max_na ? e.na : max_na;
+      const int o = n >= s0 ? 0 : 3;
+      wu[o] += 1;
+      wu[o + 1] = max(wu[o + 1], (uint32_t)e.tt);
+      wu[o + 2] = max(wu[o + 2], (uint32_t)e.na);
     }
   }
   if (st3) st3[0] = wall_clock64();
-  {
+  int wd = -1;  // the window's stopping node (-1: every node visited)
+  if (win) {
+    if (!svc_window(smem, S, plain, k_find, s0, sa, npt, wu, nf, max_tt, max_na, wd)) return false;
+    if (st3) st3[1] = wall_clock64();
+  } else {
     long long v[3] = {nf, max_tt, max_na};
     const int op[3] = {OP_SUM, OP_MAX, OP_MAX};
     if (!svc_xchg<3, INL>(smem, S, plain, v, op)) return false;
@@ -576,6 +777,9 @@ __device__ bool svc_simple_eval(const DevCluster& c, const DevJob& job, const ks
     max_tt = v[1];
     max_na = v[2];
   }
+  // visiting position from the cursor: n was filtered iff pos(n) <= pos(d), kept iff also feasible
+  // and pos(n) < pos(d) (d passed every filter but the framework dropped it)
+  const int pd = wd >= 0 ? (wd - s0 + c.N) % c.N : c.N;
   const bool scored = nf > 1;
   const float rtt = max_tt ? __builtin_amdgcn_rcpf((float)max_tt) : 0.f, rna = max_na ? __builtin_amdgcn_rcpf((float)max_na) : 0.f;
   // the selectHost key first (its exchange is the chain), then the record rows
@@ -583,7 +787,7 @@ __device__ bool svc_simple_eval(const DevCluster& c, const DevJob& job, const ks
   for (int k = 0; k < npt; k++) {
     const int n = S.lo + k * nt + tid;
     const int si = k * nt + tid;
-    if (n >= S.hi || (sa.fail[si] & 0xFF) != KSS_F_PASS) continue;
+    if (n >= S.hi || (sa.fail[si] & 0xFF) != KSS_F_PASS || (n - s0 + c.N) % c.N >= pd) continue;
     const SVal e{KSS_F_PASS, sa.tt[si], (int)sa.na[si], sa.fit[si], sa.ba[si]};
     const long long key = simple_key(prof, e, scored, (int)max_tt, rtt, (int)max_na, rna, (uint32_t)(c.node_base + n));
     best = key > best ? key : best;
@@ -599,10 +803,13 @@ __device__ bool svc_simple_eval(const DevCluster& c, const DevJob& job, const ks
     const int n = S.lo + k * nt + tid;
     const int si = k * nt + tid;
     if (n >= S.hi) continue;
-    const int fw = sa.fail[si];
+    int fw = sa.fail[si];
+    const int pos = (n - s0 + c.N) % c.N;
+    if (pos > pd) fw = KSS_F_NOT_EVALUATED;  // the search stopped before this node
+    else if (pos == pd) fw = KSS_F_PASS | (KSS_PASS_NOT_KEPT << 8);  // the stopping node: filtered, dropped
     const int f = fw & 0xFF;
     SVal e{f, sa.tt[si], (int)sa.na[si], sa.fit[si], sa.ba[si]};
-    const bool pass = f == KSS_F_PASS;
+    const bool pass = f == KSS_F_PASS && pos < pd;
     // the row values as scalars (a local array indexed in the store loop would go to scratch)
     const int64_t r_tt = pass ? e.tt : 0, r_na = pass ? e.na : 0, r_fit = pass ? e.fit : 0, r_ba = pass ? e.ba : 0;
     int64_t n_tt = 0, n_na = 0, n_fit = 0, n_pts = 0, n_ba = 0, total = 0;
@@ -639,6 +846,7 @@ __device__ bool svc_simple_eval(const DevCluster& c, const DevJob& job, const ks
       svc_put<COMPACT>(host, o_norm, (size_t)KSS_S_IMAGE_LOCALITY * N + n, es_norm, 0);
     }
   }
+  if (wd >= 0) S.cursor = wd;  // nextStartNodeIndex: the stopping node (every shard knows it)
   meta.n_feasible = (int)nf;
   if (nf == 0) {
     meta.status = 1;
@@ -796,6 +1004,8 @@ __device__ void service_loop(DevCluster c, const DevJob& job, const kss_profile&
       for (int r = 0; r < SVC_ROWS; r++) want |= (fields & svc_row_field(r)) ? 1u << r : 0u;
       unsigned long long st3[3] = {0, 0, 0};
       unsigned long long* sp3 = ((stamps & 1) && w == 0 && threadIdx.x == 0) ? st3 : nullptr;
+      if (node & 2) S.cursor = cursor_prev;  // the same scheduling cycle again
+      cursor_prev = S.cursor;
       const bool ok = compact
                           ? svc_simple_eval<true, INL>(c, job, prof, pi, smem, S, bins_cap, npt, want, crec_host, m, plain, sp3)
                           : svc_simple_eval<false, INL>(c, job, prof, pi, smem, S, bins_cap, npt, want, rec_host, m, plain, sp3);
@@ -805,6 +1015,7 @@ __device__ void service_loop(DevCluster c, const DevJob& job, const kss_profile&
       }
       if ((stamps & 1) && w == 0 && threadIdx.x == 0) st2 = st4 = wall_clock64();
       if (w == 0 && threadIdx.x == 0) {
+        if (job.cursor) *job.cursor = S.cursor;  // read by the next launch on this context
         KSS_GLOBAL int32_t* mm = reinterpret_cast<KSS_GLOBAL int32_t*>(&box->meta);
         mm[0] = m.chosen;
         mm[1] = m.n_feasible;

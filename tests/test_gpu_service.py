@@ -187,28 +187,34 @@ def test_service_compact_record_equals_full(config, n_nodes, n_pods):
     svc.close()
 
 
-def _oracle_records(cluster, pods, n, rollback_every, n_classes=0, n_terms=0):
+def _oracle_records(cluster, pods, n, rollback_every, n_classes=0, n_terms=0, prof=None):
     """The C oracle's records for the service sequence: pod j evaluated on the state every earlier
     commit left; a commit the sequence rolled back is not assumed (skip_commit)."""
     import oracle_c
     skip = np.zeros(n, np.uint8)
     if rollback_every:
         skip[::rollback_every] = 1
-    return oracle_c.schedule(abi.default_profile(), cluster, pods, n, cluster.n_nodes, threads=8, record=True,
+    return oracle_c.schedule(prof or abi.default_profile(), cluster, pods, n, cluster.n_nodes, threads=8, record=True,
                              n_classes=n_classes, n_terms=n_terms, skip_commit=skip)
 
 
-@pytest.mark.parametrize("config,n_nodes,n_pods", [(2, 5000, 100), (1, 100, 150), (3, 2000, 70), (4, 6000, 50)])
-def test_service_records_match_c_oracle(config, n_nodes, n_pods):
+@pytest.mark.parametrize("config,n_nodes,n_pods,pct", [(2, 5000, 100, 100), (1, 100, 150, 100), (3, 2000, 70, 100),
+                                                       (4, 6000, 50, 100), (2, 5000, 150, 0), (2, 2000, 120, 30),
+                                                       (1, 180, 200, 0), (3, 2000, 60, 0)])
+def test_service_records_match_c_oracle(config, n_nodes, n_pods, pct):
     """The service's full records straight against the C oracle: every pod's
     chosen node, outcome, per-node verdicts and details, raw and normalised scores and weighted
-    totals over the feasible nodes, with the commit / rollback sequence replayed in the oracle
-    (rolled-back pods evaluated, not assumed), and the final node state -- on the k_simple-shaped
-    evaluation (configs 1, 2) and the general chain (3, 4: spread and inter-pod programs)."""
+    totals over the kept nodes, with the commit / rollback sequence replayed in the oracle
+    (rolled-back pods evaluated, not assumed), the cursor and the final node state -- on the
+    k_simple-shaped evaluation (configs 1, 2; at pct < 100 with the window, svc_window: the
+    stopping node recorded as passed and dropped, the nodes after it unevaluated) and the general
+    chain (3, 4: spread and inter-pod programs)."""
     s = native.Synth(config, SEED_BASE + config, n_nodes, n_pods)
     rb = 7
-    ch_o, res, st = _oracle_records(s.cluster, s.pods, n_pods, rb, s.cluster.n_classes, s.cluster.n_terms)
-    svc = native.Context(abi.default_profile())
+    prof = abi.default_profile()
+    prof.pct_nodes_to_score = pct
+    ch_o, res, st = _oracle_records(s.cluster, s.pods, n_pods, rb, s.cluster.n_classes, s.cluster.n_terms, prof)
+    svc = native.Context(prof)
     svc.load(s.cluster)
     svc.stage(s.pods)
     N = svc.n_nodes
@@ -219,9 +225,11 @@ def test_service_records_match_c_oracle(config, n_nodes, n_pods):
                (m["chosen"], m["n_feasible"], m["scored"], m["status"]), (j, m)
         np.testing.assert_array_equal(got.fail_plugin[:N], res.fail_plugin[j, :N], err_msg=f"pod {j} verdicts")
         np.testing.assert_array_equal(got.fail_detail[:N], res.fail_detail[j, :N], err_msg=f"pod {j} details")
+        if j == 0:
+            mode = svc.service_mode()
         if m["scored"]:
             assert got.best_total == m["best_total"], j
-            feas = res.fail_plugin[j, :N] == 0
+            feas = (res.fail_plugin[j, :N] == 0) & (res.fail_detail[j, :N] != abi.KSS_PASS_NOT_KEPT)
             np.testing.assert_array_equal(got.raw[:, :N][:, feas], res.raw[j][:, :N][:, feas], err_msg=f"pod {j} raw")
             np.testing.assert_array_equal(got.norm[:, :N][:, feas], res.norm[j][:, :N][:, feas], err_msg=f"pod {j} norm")
             np.testing.assert_array_equal(got.total[:N][feas], res.total[j, :N][feas], err_msg=f"pod {j} total")
@@ -230,6 +238,8 @@ def test_service_records_match_c_oracle(config, n_nodes, n_pods):
             if j % rb == 0:
                 svc.service_rollback(j, got.chosen)
     svc.service_stop()
+    assert svc.next_start_node_index() == st["next_start"]
+    assert (mode in (1, 2)) if config in (1, 2) else mode == 0, mode
     g = svc.node_state()
     for k in ("requested", "nonzero", "pod_count"):
         np.testing.assert_array_equal(g[k][..., :N], st[k][..., :N], err_msg=k)
