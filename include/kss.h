@@ -588,7 +588,8 @@ int kss_service_rollback(kss_ctx* ctx, int32_t pod_index, int32_t node);
 int kss_service_stamps(kss_ctx* ctx, uint64_t* out8);
 /* Which evaluation the service grid runs (set when it starts): 1 the k_simple-shaped chain
  * (staged default-profile pods: no spread / inter-pod programs, host ports, node-cached images,
- * volumes or extended resources, percentageOfNodesToScore 100) with the record stored from
+ * volumes or extended resources; below percentageOfNodesToScore 100 no PreFilterResult node
+ * lists, the window running on the same chain) with the record stored from
  * registers, 2 the same on an XCD-local grid (its exchanges in one XCD's L2), 0 the general
  * chain (schedule_pod + the record copy), -1 not started. */
 int kss_service_mode(kss_ctx* ctx, int32_t* mode);
