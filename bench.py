@@ -628,9 +628,10 @@ def run_per_pod(args):
     import numpy as np
     from kss import abi, native
     from kss.synth import SEED_BASE
-    n_nodes = args.nodes or 5000
+    n_nodes = args.nodes or (100 if args.config == 1 else 5000)
     n_pods = args.pods or 500
-    s = native.Synth(2, SEED_BASE + 2, n_nodes, n_pods)
+    cfg = args.config if args.config in (1, 2, 3) else 2  # C3: spread + inter-pod programs (the general chain)
+    s = native.Synth(cfg, SEED_BASE + cfg, n_nodes, n_pods)
     prof = abi.default_profile()
     prof.pct_nodes_to_score = args.pct  # --pct 0: the simulator's own setting (adaptive window)
     ctx = native.Context(prof)
@@ -776,8 +777,8 @@ def run_per_pod(args):
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "int64/f64",
-        "data": "synthetic (SplitMix64 seed 0x5EED0002)",
-        "config": {"workload": f"C2 cluster, per-pod API: {n_nodes} nodes, {n_pods} pods one call pair each, "
+        "data": f"synthetic (SplitMix64 seed 0x5EED000{cfg})",
+        "config": {"workload": f"C{cfg} cluster, per-pod API: {n_nodes} nodes, {n_pods} pods one call pair each, "
                                f"pct={args.pct}",
                    "nodes": n_nodes, "pods": n_pods, "parallelism": "none", "percentage_of_nodes_to_score": args.pct},
         "eval_us": {"median": float(np.median(ev)), "mean": float(ev.mean()), "p90": float(np.percentile(ev, 90))},
@@ -830,6 +831,66 @@ def run_per_pod(args):
     print(json.dumps(out), flush=True)
     ctx.close()
     s.close()
+
+
+def run_snapshot(args):
+    """The snapshot path the plugin takes: a C<config> cluster written as the simulator's
+    ResourcesForSnap JSON, read back (kss/snapshot.py read_snapshot), compiled (kss/compile.py) and
+    scheduled as one sequential batch with the profile the simulator's configuration yields --
+    percentageOfNodesToScore 0, the adaptive window (profile_from_config) -- every step from the
+    snapshot's state (a device reset).  Reports the kernel the batch took, pods/s and the window's
+    evaluations per pod; the JSON read and the compile are timed beside it, once."""
+    import json as _json
+    from kss import native, snapshot, synth
+    from kss.compile import compile_cluster
+    cfg = args.config if args.config in (1, 2, 3) else 2
+    n_nodes = args.nodes or 1000
+    n_pods = args.pods or 2000
+    nodes, bound, pods = synth.make_cluster(cfg, n_nodes=n_nodes, n_pods=n_pods)
+    t0 = time.perf_counter()
+    snap = snapshot.read_snapshot(_json.dumps(synth.to_resources_for_snap(nodes, bound, pods)))
+    cc, cp, _ = compile_cluster(snap.nodes, snap.bound, snap.pending, snap.namespaces)
+    prof = snapshot.profile_from_config(snap.scheduler_config, cc.scalars)
+    compile_s = time.perf_counter() - t0
+    ctx = native.Context(prof)
+    ctx.load(cc.as_struct(), names=native.make_names(cc.node_names, cc.taints, cc.scalars))
+    ps = cp.as_struct()
+    ctx.stage(ps)
+    for _ in range(args.warmup):
+        ctx.reset()
+        ctx.run_staged(cp.n)
+    ts = []
+    for _ in range(args.steps):
+        ctx.reset()
+        a = time.perf_counter()
+        chosen = ctx.run_staged(cp.n)
+        ts.append(time.perf_counter() - a)
+    el = sum(ts)
+    k = num_feasible_nodes_to_find(cc.n_nodes, prof.pct_nodes_to_score)
+    out = {
+        "metric": "pods scheduled/sec, simulator snapshot path (ResourcesForSnap -> compile -> batch)",
+        "value": cp.n * args.steps / el,
+        "unit": "pods/s",
+        "n_gpus": 1,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": el / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "int64/f64",
+        "data": f"synthetic (kss.synth config {cfg} objects as ResourcesForSnap JSON)",
+        "config": {"workload": f"C{cfg} recipe snapshot: {cc.n_nodes} nodes, {cp.n} pending pods, pct="
+                               f"{prof.pct_nodes_to_score} (the simulator's reset config)",
+                   "nodes": cc.n_nodes, "pods": cp.n, "percentage_of_nodes_to_score": prof.pct_nodes_to_score},
+        "kernel": ctx.last_kernel(),
+        "geometry": ctx.last_geometry(),
+        "evals_per_pod": k,
+        "scheduled": int((chosen >= 0).sum()),
+        "read_and_compile_s_once": compile_s,
+    }
+    print(json.dumps(out), flush=True)
+    ctx.close()
 
 
 def run_postfilter(args):
@@ -1079,6 +1140,9 @@ def main():
                     help="percentageOfNodesToScore of the profile (100: every node, the north_star setting; "
                          "0: the simulator's adaptive default)")
     ap.add_argument("--c4-timeout", type=float, default=420.0, help="seconds for the C4 split-grid leg")
+    ap.add_argument("--snapshot", action="store_true",
+                    help="the simulator's snapshot path: a ResourcesForSnap JSON read back, compiled, scheduled "
+                         "with the profile the simulator's config gives (percentageOfNodesToScore 0)")
     args = ap.parse_args()
     if args.inner:
         args.no_cpu = args.no_traffic = args.no_latency = args.no_legs = True
@@ -1093,6 +1157,8 @@ def main():
         sys.exit(f"bench.py: LOCAL_RANK {os.environ.get('LOCAL_RANK')} but {visible_gpus()} GPU(s) visible")
     if args.per_pod:
         return run_per_pod(args)
+    if args.snapshot:
+        return run_snapshot(args)
     if args.postfilter:
         return run_postfilter(args)
     if args.split:

@@ -3,7 +3,9 @@
     python tools/c2_stamps.py CONFIG [SHARDS ...]     (SHARDS 0 = the library's own choice)
 
 CONFIG is a BASELINE config index (2 = C2, 3 = C3, 4 = C4); 1000 pods of it are scheduled
-per shard count and tools/stamps.py summarises shard 0's phases."""
+per shard count and tools/stamps.py summarises shard 0's phases.  STAMP_OPTS="name=v,..." sets
+library options first (e.g. no_spread=1: the general kernel k_schedule, the per-pod service's
+chain)."""
 import os
 import sys
 import tempfile
@@ -22,6 +24,9 @@ def main():
     for w in [int(x) for x in sys.argv[2:]] or [0]:
         path = os.path.join(tempfile.mkdtemp(prefix="kss_stamps_"), "stamps.bin")
         native.set_stamps_file(path)
+        for kv in filter(None, os.environ.get("STAMP_OPTS", "").split(",")):
+            k, v = kv.split("=")
+            native.set_option(k, int(v))
         native.set_option("shards", w)
         s = native.Synth(cfg, SEED_BASE + cfg, n_nodes, 1000)
         ctx = native.Context(abi.default_profile(), device=0)
