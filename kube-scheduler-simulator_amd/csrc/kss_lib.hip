@@ -1767,7 +1767,7 @@ kss_ctx* kss_create(const kss_config* cfg, const kss_profile* prof) {
   if (ctx->n_cu <= 0) ctx->n_cu = 1;
   ctx->force_w = (int)std::max(0ll, opt(O_SHARDS));
   ctx->xcd_mode = opt(O_XCD) != 0;
-  ctx->xcd_w = (int)std::max(0ll, std::min(64ll, opt(O_XCD_SHARDS)));
+  ctx->xcd_w = (int)std::max(0ll, std::min((long long)(64 * SX_CHUNKS), opt(O_XCD_SHARDS)));
   {
     std::lock_guard<std::mutex> lk(g_stamps_mu);
     ctx->stamps_path = g_stamps_path;

@@ -947,6 +947,7 @@ __device__ __forceinline__ bool schedule_pod(const DevCluster& c, const DevPods&
     }
   }
 
+  KSS_STAMP(S, 7);  // the PodTopologySpread / InterPodAffinity statistics and their exchange done
   // ---- PreferNominatedNode (findNodesThatFitPod -> evaluateNominatedNode) ---------------------
   // A pod an earlier preemption nominated first runs findNodesThatPassFilters on [its node] alone,
   // whatever its PreFilterResult; the one-node list resets nextStartNodeIndex to 0.  A feasible

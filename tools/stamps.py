@@ -2,7 +2,8 @@
 {kernel, shards} then the stamps).
 
 k_schedule (shard 0, 8 stamps per pod): 0 pod start, 1 plan, 2 filter pass done, 3 filter
-exchange done, 4 normalize pass done, 5 argmax exchange done, 6 commit + barrier done.
+exchange done, 4 normalize pass done, 5 argmax exchange done, 6 commit + barrier done, 7 the
+spread / inter-pod statistics and their exchange done (inside the filter phase).
 k_simple (every shard, 16 per pod): 0 start, 1 pass B, 2 best-key reduction, 3 pass A,
 4 statistics reduction (= publish), 5 exchange + barrier, 6 commit + ring store.  For
 k_simple the arrival skew of the exchange is reported: per pod, the spread of the
@@ -41,8 +42,12 @@ def summarise(path):
             a = a[(a[:, 0] > 0) & (a[:, 6] > 0)]
             d = np.diff(a[:, :7], axis=1) / 100.0
             tot = (a[:, 6] - a[:, 0]) / 100.0
-            lines.append("k_schedule " + " ".join(f"{n}={m:.2f}" for n, m in zip(NAMES, np.median(d, axis=0)))
-                         + f" | pod={np.median(tot):.2f} us (n={len(a)})")
+            line = ("k_schedule " + " ".join(f"{n}={m:.2f}" for n, m in zip(NAMES, np.median(d, axis=0)))
+                    + f" | pod={np.median(tot):.2f} us (n={len(a)})")
+            if (a[:, 7] > 0).any():  # stamp 7: the statistics (+ their exchange) done inside `filter`
+                st = (a[:, 7] - a[:, 1]) / 100.0
+                line += f"\n  filter = statistics + exchange {np.median(st):.2f} + filter pass {np.median(d[:, 1] - st):.2f} us"
+            lines.append(line)
             continue
         a = a.reshape(w, NSTAMP_PODS // 2, 16)
         if kind == 2:
