@@ -791,6 +791,68 @@ __device__ __forceinline__ bool simple_exchange(SimpleHdr& H, unsigned long long
   return true;
 }
 
+// The poll half of simple_exchange for any wave (KSS_PW_ALLPOLL): every shard's row of the
+// exchange at `epoch` (this shard's own row included, published by its wave 0), the winner key
+// and the statistics (the winner's shard contributing its H1), into R of every lane of the
+// calling wave.  False after the wait bound (H.abort set).
+__device__ __forceinline__ bool simple_exchange_poll(SimpleHdr& H, unsigned long long* gran, int W, unsigned epoch,
+                                                     int* err, int per, int node_base, int kb, long long (&R)[4]) {
+  const int lane = threadIdx.x & 63;
+  const unsigned long long* base = gran + (size_t)(epoch & 1) * W * SX_VALS;
+  uint32_t got[SX_CHUNKS][SX_VALS];
+  long long best = 0;
+#pragma unroll
+  for (int ch = 0; ch < SX_CHUNKS; ch++) {
+#pragma unroll
+    for (int i = 0; i < SX_VALS; i++) got[ch][i] = 0;
+    if (ch * 64 >= W) continue;
+    const int s = ch * 64 + lane;
+    const bool valid = s < W;
+    long long t0_ = 0;
+    for (unsigned spins = 0;; ++spins) {
+      bool ok = true;
+      unsigned long long g[SX_VALS];
+#pragma unroll
+      for (int i = 0; i < SX_VALS; i++)
+        g[i] = __hip_atomic_load(base + (size_t)(valid ? s : 0) * SX_VALS + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+      for (int i = 0; i < SX_VALS; i++) {
+        ok &= !valid || (g[i] >> 32) == epoch;
+        got[ch][i] = valid ? (uint32_t)g[i] : 0u;
+      }
+      if (__all(ok)) break;
+      if (spin_expired(spins, t0_)) {
+        if (lane == 0) {
+          H.abort = 1;
+          err_raise(err, 1);
+        }
+        return false;
+      }
+      spin_pause();
+    }
+    const long long k = (long long)(((unsigned long long)got[ch][1] << 32) | got[ch][0]);
+    best = k > best ? k : best;
+  }
+  best = wave_max_key(best, kb, node_base);
+  const int gl = best != 0 ? (int)(0xFFFFFFFFu - (uint32_t)(unsigned long long)best) - node_base : -1;
+  uint32_t u[6] = {0, 0, 0, 0, 0, 0};
+#pragma unroll
+  for (int ch = 0; ch < SX_CHUNKS; ch++) {
+    const int s = ch * 64 + lane;
+    if (s >= W) continue;
+    const bool h1 = gl >= s * per && gl < s * per + per;
+    u[0] += h1 ? got[ch][5] : got[ch][2];
+    u[1] = max(u[1], h1 ? got[ch][6] : got[ch][3]);
+    u[2] = max(u[2], h1 ? got[ch][7] : got[ch][4]);
+  }
+  wave_red_stats(u);
+  R[0] = best;
+  R[1] = u[0];
+  R[2] = u[1];
+  R[3] = u[2];
+  return true;
+}
+
 // Block-reduce the six partial statistics of the next pod, exchange them with the
 // current pod's shard-best key, and leave {winner key, nf, max TT, max NA} in R[] of
 // every lane.  False if the launch aborted (exchange timeout).
@@ -1069,6 +1131,12 @@ __device__ __forceinline__ void simple_pass_a_pw(const kss_profile& prof, const 
 #ifndef KSS_LANE_COMBINE
 #define KSS_LANE_COMBINE 1  // simple_sync_pw: the waves' partials combined lane-parallel (r7d A/B: C2 291.8k -> 301.3k pods/s)
 #endif
+#ifndef KSS_PW_ALLPOLL
+// simple_sync_pw: every wave polls the exchange itself, no closing barrier.  r8t A/B: C2 261k
+// against 304k pods/s -- the prefetch waves' polls queue behind their own HBM prefetch loads
+// (vmcnt is in order), so the pod waits for them: off
+#define KSS_PW_ALLPOLL 0
+#endif
 #ifndef KSS_LANE_COMMIT
 #define KSS_LANE_COMMIT 1  // r7c A/B: C2 284.7k -> 290.7k pods/s, C4 unchanged; 0 keeps one lane
 #endif
@@ -1200,6 +1268,15 @@ __device__ __forceinline__ bool simple_sync_pw(SimpleHdr& H, int& parity, long l
         if (!KSS_LANE_COMMIT && commit && h1) simple_commit_slot(L, pk, slot);
       }
       if (KSS_LANE_COMMIT && commit && h1) simple_commit_lanes(L, pk, slot, lane);
+    } else if (KSS_PW_ALLPOLL) {  // publish only: every wave polls below
+      if (lane < SX_VALS) {
+        const unsigned long long key = (unsigned long long)best, tag = (unsigned long long)epoch << 32;
+        uint32_t x = (uint32_t)key;
+        x = lane == 1 ? (uint32_t)(key >> 32) : x;
+#pragma unroll
+        for (int i = 0; i < 6; i++) x = lane == i + 2 ? t[i] : x;
+        xpub(X, gran, ((size_t)(epoch & 1) * W + w) * SX_VALS + lane, tag | x);
+      }
     } else {
       const long long v[7] = {best, t[0], t[1], t[2], t[3], t[4], t[5]};
       if (simple_exchange(H, gran, X, W, w, epoch, err, v, per, node_base, kb) && commit && (KSS_LANE_COMMIT || lane == 0)) {
@@ -1211,6 +1288,19 @@ __device__ __forceinline__ bool simple_sync_pw(SimpleHdr& H, int& parity, long l
         }
       }
     }
+  }
+  if (KSS_PW_ALLPOLL && W > 1) {
+    // every wave polls the shards' rows itself and commits pod k on the winner's slot if that slot
+    // is one of its own: no closing barrier.  Each wave's next reads (pass B / pass A) touch only
+    // its own slots, and a wave reaching the next statistics barrier has finished this pod's poll,
+    // so the reduction rows (parity-alternated) are never overwritten while read.
+    parity ^= 1;
+    if (!simple_exchange_poll(H, gran, W, epoch, err, per, node_base, kb, R)) return false;
+    const long long K = R[0];
+    const int x = K ? (int)(0xFFFFFFFFu - (uint32_t)(unsigned long long)K) - node_base - lo : -1;
+    const int pwv = (own + nw - 1) / nw;  // the wave's slots (simple_schedule's per-wave split)
+    if (commit && x >= 0 && x < own && x / max(pwv, 1) == wave) simple_commit_lanes(L, pk, x, lane);
+    return true;
   }
   parity ^= 1;
   lds_barrier();
