@@ -1131,6 +1131,12 @@ __device__ __forceinline__ void simple_pass_a_pw(const kss_profile& prof, const 
 #ifndef KSS_LANE_COMBINE
 #define KSS_LANE_COMBINE 1  // simple_sync_pw: the waves' partials combined lane-parallel (r7d A/B: C2 291.8k -> 301.3k pods/s)
 #endif
+#ifndef KSS_PF_LAST_WAVE
+// per-wave mode with 3+ waves: the last wave (fewest slots) alone prefetches the next records and
+// static words, so the first prefetch wave reaches the statistics barrier with the others (r8u
+// A/B, C2: 303.3 / 303.6 k against 301.6 / 301.5 k pods/s)
+#define KSS_PF_LAST_WAVE 1
+#endif
 #ifndef KSS_PW_ALLPOLL
 // simple_sync_pw: every wave polls the exchange itself, no closing barrier.  r8t A/B: C2 261k
 // against 304k pods/s -- the prefetch waves' polls queue behind their own HBM prefetch loads
@@ -1835,12 +1841,14 @@ __device__ __forceinline__ void simple_schedule(DevCluster c, const SPod* __rest
   const int pwv = (own + nwave - 1) / nwave;  // per-wave mode: the wave's node slots (<= PW_LANES)
   const int kb = key_bits(prof, c.N);  // 32-bit key reductions when the keys fit (0: 64-bit)
   // prefetch lanes: every wave but wave 0 (readfirstlane: a wave-uniform, scalar branch)
-  const bool pf_wave = nwave == 1 || __builtin_amdgcn_readfirstlane(tid >> 6) >= 1;
+  // (KSS_PF_LAST_WAVE, per-wave mode with 3+ waves: the last wave alone prefetches -- A/B)
+  const int pf_w0 = (PW && KSS_PF_LAST_WAVE && nwave >= 3) ? nwave - 1 : 1;
+  const bool pf_wave = nwave == 1 || __builtin_amdgcn_readfirstlane(tid >> 6) >= pf_w0;
   uint4 pfq = make_uint4(0, 0, 0, 0);  // prefetched record / static words of pod k+PD, live across the loop
   uint32_t pfw[PF_MAX];
 #pragma unroll
   for (int j = 0; j < PF_MAX; j++) pfw[j] = 0;
-  const int pf_lane = nwave == 1 ? tid : tid - 64, pf_n = nwave == 1 ? nt : nt - 64;
+  const int pf_lane = nwave == 1 ? tid : tid - 64 * pf_w0, pf_n = nwave == 1 ? nt : nt - 64 * pf_w0;
   const int pf_per = (own + pf_n - 1) / pf_n;  // static words per prefetch lane (<= PF_MAX)
   // k = k0 - 1 is the prologue: pass A of pod k0 and the exchange of its statistics
   for (int k = k0 - 1; k < k1; k++) {
