@@ -20,8 +20,36 @@ from kss.synth import SEED_BASE  # noqa: E402
 SIZES = {1: (100, 1000), 2: (5000, 10000), 3: (5000, 10000), 4: (100000, 20000)}
 
 
+def sweep_ab(settings):
+    """C5 shape: 512 scenarios x 1,000 nodes x 1,000 pods in one resident sweep, per setting."""
+    n_scen = int(os.environ.get("AB_SCEN", "512"))
+    syn = [native.Synth(5, SEED_BASE + 5 + 7919 * k, 1000, 1000) for k in range(n_scen)]
+    ref = None
+    for setting in settings or [""]:
+        native.reset_options()
+        for kv in filter(None, setting.split(",")):
+            k, v = kv.split("=")
+            native.set_option(k, int(v))
+        sw = native.Sweep(abi.default_profile(), [x.cluster for x in syn], [x.pods for x in syn])
+        sw.run()
+        best = None
+        for _ in range(3):
+            t0 = time.perf_counter()
+            chosen, ms = sw.run()
+            wall = time.perf_counter() - t0
+            best = wall if best is None else min(best, wall)
+        same = ref is None or bool(np.array_equal(chosen, ref))
+        ref = chosen if ref is None else ref
+        print(f"C5 x{n_scen} [{setting or 'default'}] {sw.info()['kernel']} {n_scen * 1e6 / best / 1e9:.2f} G evals/s "
+              f"({best * 1e3:.2f} ms) same_as_first={same}", flush=True)
+        sw.close()
+    native.reset_options()
+
+
 def main():
     cfg = int(sys.argv[1])
+    if cfg == 5:
+        return sweep_ab(sys.argv[2:])
     n_nodes, n_pods = SIZES[cfg]
     pct = int(os.environ.get("AB_PCT", "100"))
     s = native.Synth(cfg, SEED_BASE + cfg, n_nodes, n_pods)
