@@ -1438,7 +1438,8 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
 // Whole workgroup; results uniform.
 template <bool PW>
 __device__ __forceinline__ void win_cut_scan(SimpleHdr& H, const SimpleShard& L, int own, int lo, int start, int part,
-                                             int j, int sub_s, int sub_h, int pwv, int& d, int& ptt, int& pna) {
+                                             int j, int sub_s, int sub_h, int pwv, int& d, int& ptt, int& pna,
+                                             bool maxima = true) {
   const int tid = threadIdx.x, nt = blockDim.x, lane = tid & 63, wave = tid >> 6, nw = nt >> 6;
   const int iters = PW ? 1 : (own + nt - 1) / nt;
   int carry = 0, mt = 0, mn = 0;
@@ -1466,6 +1467,13 @@ __device__ __forceinline__ void win_cut_scan(SimpleHdr& H, const SimpleShard& L,
     mn = max(mn, (f && rank < j) ? e.na : 0);
     carry += tot;
   }
+  ptt = 0;
+  pna = 0;
+  if (!maxima) {  // the cut segment's maxima cannot exceed the kept ones: only d is needed
+    lds_barrier();  // H.win[6] written by its lane
+    d = (int)H.win[6];
+    return;
+  }
   mt = (int)wave_red<OP_MAX>(mt);
   mn = (int)wave_red<OP_MAX>(mn);
   if (lane == 0) {
@@ -1473,8 +1481,6 @@ __device__ __forceinline__ void win_cut_scan(SimpleHdr& H, const SimpleShard& L,
     H.cutm[wave][1] = mn;
   }
   lds_barrier();
-  ptt = 0;
-  pna = 0;
   for (int x = 0; x < nw; x++) {
     ptt = max(ptt, H.cutm[x][0]);
     pna = max(pna, H.cutm[x][1]);
@@ -1497,12 +1503,43 @@ __device__ __forceinline__ bool simple_sync_win(SimpleHdr& H, int& parity, long 
                                                 int pwv, long long (&R)[4], int& d_out, int& cs_out,
                                                 KSS_GLOBAL unsigned long long* sp, Idle&& idle) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
-  dpp_win_step<0xB1, 0xF>(u);
-  dpp_win_step<0x4E, 0xF>(u);
-  dpp_win_step<0x141, 0xF>(u);
-  dpp_win_step<0x140, 0xF>(u);
-  dpp_win_step<0x142, 0xA>(u);
-  dpp_win_step<0x143, 0xC>(u);
+  if (PW) {
+    // one node (or the H1 re-evaluation) per lane: the four counts are ballot popcounts, the four
+    // TaintToleration maxima (<= 64) ride as two packed 16-bit pairs, the NodeAffinity maxima alone:
+    // six DPP chains instead of twelve
+    uint32_t c4[4];
+#pragma unroll
+    for (int v = 0; v < 4; v++) c4[v] = (uint32_t)__popcll(__ballot(u[3 * v] != 0));
+    uint32_t tp0 = u[1] | (u[4] << 16), tp1 = u[7] | (u[10] << 16), n0 = u[2], n1 = u[5], n2 = u[8], n3 = u[11];
+    auto step = [&](auto ctrl, auto rows) {
+      constexpr int C = decltype(ctrl)::value, R = decltype(rows)::value;
+      dpp_pw_step<C, R>(tp0, n0, n1);
+      dpp_pw_step<C, R>(tp1, n2, n3);
+    };
+    step(std::integral_constant<int, 0xB1>{}, std::integral_constant<int, 0xF>{});
+    step(std::integral_constant<int, 0x4E>{}, std::integral_constant<int, 0xF>{});
+    step(std::integral_constant<int, 0x141>{}, std::integral_constant<int, 0xF>{});
+    step(std::integral_constant<int, 0x140>{}, std::integral_constant<int, 0xF>{});
+    step(std::integral_constant<int, 0x142>{}, std::integral_constant<int, 0xA>{});
+    step(std::integral_constant<int, 0x143>{}, std::integral_constant<int, 0xC>{});
+#pragma unroll
+    for (int v = 0; v < 4; v++) u[3 * v] = c4[v];
+    u[1] = tp0 & 0xFFFFu;
+    u[4] = tp0 >> 16;
+    u[7] = tp1 & 0xFFFFu;
+    u[10] = tp1 >> 16;
+    u[2] = n0;
+    u[5] = n1;
+    u[8] = n2;
+    u[11] = n3;
+  } else {
+    dpp_win_step<0xB1, 0xF>(u);
+    dpp_win_step<0x4E, 0xF>(u);
+    dpp_win_step<0x141, 0xF>(u);
+    dpp_win_step<0x140, 0xF>(u);
+    dpp_win_step<0x142, 0xA>(u);
+    dpp_win_step<0x143, 0xC>(u);
+  }
   if (lane == 63) {  // the reduced values sit in lane 63
     H.red[parity][wave][0] = wkey;
 #pragma unroll
@@ -1642,6 +1679,7 @@ __device__ __forceinline__ bool simple_sync_win(SimpleHdr& H, int& parity, long 
         uint32_t pre_hit = 0;
 #pragma unroll
         for (int ch = 0; ch < SX_CHUNKS; ch++) {
+          if (ch * 64 >= W) break;  // (uniform) no shard in this chunk
           const uint32_t ia = wave_incl_scan(Fa[ch]), ib = wave_incl_scan(Fb[ch]);
           const uint32_t pa = ca + ia - Fa[ch], pb = cb + ib - Fb[ch];
           ftt = max(ftt, pa + Fa[ch] <= K ? ta[ch] : 0u);
@@ -1704,7 +1742,7 @@ __device__ __forceinline__ bool simple_sync_win(SimpleHdr& H, int& parity, long 
     const size_t e2 = 2 * (size_t)W * SXW_VALS + (size_t)(epoch & 1) * SXW_E2;
     if (cut == w) {  // uniform over the workgroup
       int cd = -1, ctt = 0, cna = 0;
-      win_cut_scan<PW>(H, L, own, lo, start, (int)H.win[4], (int)H.win[5], sub_s, sub_h, pwv, cd, ctt, cna);
+      win_cut_scan<PW>(H, L, own, lo, start, (int)H.win[4], (int)H.win[5], sub_s, sub_h, pwv, cd, ctt, cna, need);
       d = cd;
       if (W == 1) {
         mtt = max(mtt, (long long)ctt);
