@@ -1423,14 +1423,47 @@ __device__ __forceinline__ void dpp_win_step(uint32_t (&v)[12]) {
   for (int i = 0; i < 12; i++) v[i] = (i % 3 == 0) ? v[i] + t[i] : max(v[i], t[i]);
 }
 
+// inclusive prefix sum over the wave in DPP: row_shr 1, 2, 4, 8 scan each row of 16 lanes (lanes
+// whose source falls outside the row add 0), row_bcast:15 adds row 0's total to row 1 and row 2's to
+// row 3, row_bcast:31 adds rows 0-1's total to rows 2 and 3
+template <int CTRL, int ROWS>
+__device__ __forceinline__ void dpp_add2(uint32_t& a, uint32_t& b) {
+  const uint32_t ta = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)a, CTRL, ROWS, 0xF, false);
+  const uint32_t tb = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)b, CTRL, ROWS, 0xF, false);
+  a += ta;
+  b += tb;
+}
+__device__ __forceinline__ void wave_incl_scan2(uint32_t& a, uint32_t& b) {
+  dpp_add2<0x111, 0xF>(a, b);
+  dpp_add2<0x112, 0xF>(a, b);
+  dpp_add2<0x114, 0xF>(a, b);
+  dpp_add2<0x118, 0xF>(a, b);
+  dpp_add2<0x142, 0xA>(a, b);
+  dpp_add2<0x143, 0xC>(a, b);
+}
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
-  const int lane = threadIdx.x & 63;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const uint32_t t = (uint32_t)__shfl_up((int)v, o, 64);
-    v += lane >= o ? t : 0u;
-  }
+  uint32_t z = 0;
+  wave_incl_scan2(v, z);
   return v;
+}
+// the maxima of two non-negative 32-bit values over the wave (uniform results)
+__device__ __forceinline__ void wave_max2(uint32_t& a, uint32_t& b) {
+  uint32_t t[2] = {a, b};
+  auto step = [&](auto ctrl, auto rows) {
+    constexpr int C = decltype(ctrl)::value, R = decltype(rows)::value;
+    const uint32_t x = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)t[0], C, R, 0xF, false);
+    const uint32_t y = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)t[1], C, R, 0xF, false);
+    t[0] = max(t[0], x);
+    t[1] = max(t[1], y);
+  };
+  step(std::integral_constant<int, 0xB1>{}, std::integral_constant<int, 0xF>{});
+  step(std::integral_constant<int, 0x4E>{}, std::integral_constant<int, 0xF>{});
+  step(std::integral_constant<int, 0x141>{}, std::integral_constant<int, 0xF>{});
+  step(std::integral_constant<int, 0x140>{}, std::integral_constant<int, 0xF>{});
+  step(std::integral_constant<int, 0x142>{}, std::integral_constant<int, 0xA>{});
+  step(std::integral_constant<int, 0x143>{}, std::integral_constant<int, 0xC>{});
+  a = (uint32_t)__builtin_amdgcn_readlane((int)t[0], 63);
+  b = (uint32_t)__builtin_amdgcn_readlane((int)t[1], 63);
 }
 
 // The cut shard: rank the feasible nodes of `part` (pod k+1's verdicts; the winner's slot takes
@@ -1540,12 +1573,14 @@ __device__ __forceinline__ bool simple_sync_win(SimpleHdr& H, int& parity, long 
     dpp_win_step<0x142, 0xA>(u);
     dpp_win_step<0x143, 0xC>(u);
   }
+  if (sp && threadIdx.x == 0) sp[7] = wall_clock64();
   if (lane == 63) {  // the reduced values sit in lane 63
     H.red[parity][wave][0] = wkey;
 #pragma unroll
     for (int i = 0; i < 12; i++) H.red[parity][wave][1 + i] = u[i];
   }
   lds_barrier();
+  if (sp && threadIdx.x == 0) sp[8] = wall_clock64();
   idle();
   if (wave == 0) {
     // the shard: lane v < nw reads wave v's row, three DPP steps over the (at most 8) lanes
@@ -1562,17 +1597,52 @@ __device__ __forceinline__ bool simple_sync_win(SimpleHdr& H, int& parity, long 
                          (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)ub, 0));
     }
     const bool me = PW ? (in && best != 0 && kv == best) : in;
+    // per set (0: every wave's H0 values, 1: the best wave's H1 in place of its H0) the part a / b
+    // counts and TaintToleration maxima as packed 16-bit pairs (both below 2^16: the exchange packs
+    // them the same way), the NodeAffinity maxima alone: 8 words over three DPP steps
+    kss_u16x2 pc[2], pt[2];
+    uint32_t pn[4];
+#pragma unroll
+    for (int st = 0; st < 2; st++) {
+      const int b = st == 0 ? 1 : (me ? 7 : 1);
+      pc[st] = __builtin_bit_cast(kss_u16x2, in ? (uint32_t)hv[b] | ((uint32_t)hv[b + 3] << 16) : 0u);
+      pt[st] = __builtin_bit_cast(kss_u16x2, in ? (uint32_t)hv[b + 1] | ((uint32_t)hv[b + 4] << 16) : 0u);
+      pn[2 * st] = in ? (uint32_t)hv[b + 2] : 0u;
+      pn[2 * st + 1] = in ? (uint32_t)hv[b + 5] : 0u;
+    }
+    auto cstep = [&](auto ctrl) {
+      constexpr int C = decltype(ctrl)::value;
+      uint32_t m[8];
+#pragma unroll
+      for (int st = 0; st < 2; st++) {
+        m[st] = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)__builtin_bit_cast(uint32_t, pc[st]), C, 0xF, 0xF, false);
+        m[2 + st] = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)__builtin_bit_cast(uint32_t, pt[st]), C, 0xF, 0xF, false);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; i++) m[4 + i] = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)pn[i], C, 0xF, 0xF, false);
+#pragma unroll
+      for (int st = 0; st < 2; st++) {
+        pc[st] = pc[st] + __builtin_bit_cast(kss_u16x2, m[st]);
+        pt[st] = __builtin_elementwise_max(pt[st], __builtin_bit_cast(kss_u16x2, m[2 + st]));
+      }
+#pragma unroll
+      for (int i = 0; i < 4; i++) pn[i] = max(pn[i], m[4 + i]);
+    };
+    cstep(std::integral_constant<int, 0xB1>{});
+    cstep(std::integral_constant<int, 0x4E>{});
+    cstep(std::integral_constant<int, 0x141>{});
     uint32_t t[12];
 #pragma unroll
-    for (int i = 0; i < 6; i++) {
-      t[i] = in ? (uint32_t)hv[1 + i] : 0u;
-      t[6 + i] = in ? (uint32_t)(me ? hv[7 + i] : hv[1 + i]) : 0u;
+    for (int st = 0; st < 2; st++) {
+      const uint32_t c = (uint32_t)__builtin_amdgcn_readlane((int)__builtin_bit_cast(uint32_t, pc[st]), 0);
+      const uint32_t x = (uint32_t)__builtin_amdgcn_readlane((int)__builtin_bit_cast(uint32_t, pt[st]), 0);
+      t[6 * st + 0] = c & 0xFFFFu;
+      t[6 * st + 1] = x & 0xFFFFu;
+      t[6 * st + 2] = (uint32_t)__builtin_amdgcn_readlane((int)pn[2 * st], 0);
+      t[6 * st + 3] = c >> 16;
+      t[6 * st + 4] = x >> 16;
+      t[6 * st + 5] = (uint32_t)__builtin_amdgcn_readlane((int)pn[2 * st + 1], 0);
     }
-    dpp_win_step<0xB1, 0xF>(t);
-    dpp_win_step<0x4E, 0xF>(t);
-    dpp_win_step<0x141, 0xF>(t);
-#pragma unroll
-    for (int i = 0; i < 12; i++) t[i] = (uint32_t)__builtin_amdgcn_readlane((int)t[i], 0);
     if (sp && lane == 0) sp[4] = wall_clock64();
     // every shard's packed values in the lane of that shard (W == 1: this shard in lane 0)
     uint32_t got[SX_CHUNKS][8];
@@ -1642,11 +1712,12 @@ __device__ __forceinline__ bool simple_sync_win(SimpleHdr& H, int& parity, long 
       }
       gbest = wave_max_key(kbest, kb, node_base);
     }
+    if (sp && lane == 0) sp[10] = wall_clock64();
     if (ok) {
       const int gl = gbest != 0 ? (int)(0xFFFFFFFFu - (uint32_t)(unsigned long long)gbest) - node_base : -1;
       // each lane's shard: H1 when the winner is one of its nodes
       uint32_t Fa[SX_CHUNKS], Fb[SX_CHUNKS], ta[SX_CHUNKS], tb[SX_CHUNKS], na_[SX_CHUNKS], nb_[SX_CHUNKS];
-      uint32_t A = 0, B = 0;
+      uint32_t A = 0, B = 0, sa[SX_CHUNKS], sb[SX_CHUNKS], TA[SX_CHUNKS], TB[SX_CHUNKS];
 #pragma unroll
       for (int ch = 0; ch < SX_CHUNKS; ch++) {
         const int s = ch * 64 + lane;
@@ -1658,11 +1729,18 @@ __device__ __forceinline__ bool simple_sync_win(SimpleHdr& H, int& parity, long 
         Fb[ch] = got[ch][o + 2] >> 16;
         tb[ch] = got[ch][o + 2] & 0xFFFFu;
         nb_[ch] = got[ch][o + 3];
-        A += Fa[ch];
-        B += Fb[ch];
+        // per chunk: the inclusive scans of the part a / b counts and their totals
+        sa[ch] = Fa[ch];
+        sb[ch] = Fb[ch];
+        TA[ch] = TB[ch] = 0;
+        if (ch * 64 < W) {  // (uniform)
+          wave_incl_scan2(sa[ch], sb[ch]);
+          TA[ch] = (uint32_t)__builtin_amdgcn_readlane((int)sa[ch], 63);
+          TB[ch] = (uint32_t)__builtin_amdgcn_readlane((int)sb[ch], 63);
+        }
+        A += TA[ch];
+        B += TB[ch];
       }
-      A = (uint32_t)wave_red<OP_SUM>((long long)A);
-      B = (uint32_t)wave_red<OP_SUM>((long long)B);
       const uint32_t F = A + B, K = (uint32_t)k_find;
       uint32_t ftt = 0, fna = 0, cut_tt = 0, cut_na = 0;  // cut_*: the cut segment's maxima over all its feasible nodes
       int cut = -1, part = 0, j = 0;
@@ -1680,8 +1758,7 @@ __device__ __forceinline__ bool simple_sync_win(SimpleHdr& H, int& parity, long 
 #pragma unroll
         for (int ch = 0; ch < SX_CHUNKS; ch++) {
           if (ch * 64 >= W) break;  // (uniform) no shard in this chunk
-          const uint32_t ia = wave_incl_scan(Fa[ch]), ib = wave_incl_scan(Fb[ch]);
-          const uint32_t pa = ca + ia - Fa[ch], pb = cb + ib - Fb[ch];
+          const uint32_t pa = ca + sa[ch] - Fa[ch], pb = cb + sb[ch] - Fb[ch];
           ftt = max(ftt, pa + Fa[ch] <= K ? ta[ch] : 0u);
           fna = max(fna, pa + Fa[ch] <= K ? na_[ch] : 0u);
           ftt = max(ftt, pb + Fb[ch] <= K ? tb[ch] : 0u);
@@ -1697,14 +1774,13 @@ __device__ __forceinline__ bool simple_sync_win(SimpleHdr& H, int& parity, long 
             cut_tt = (uint32_t)__builtin_amdgcn_readlane((int)(ba ? ta[ch] : tb[ch]), l);
             cut_na = (uint32_t)__builtin_amdgcn_readlane((int)(ba ? na_[ch] : nb_[ch]), l);
           }
-          ca += (uint32_t)__builtin_amdgcn_readlane((int)ia, 63);
-          cb += (uint32_t)__builtin_amdgcn_readlane((int)ib, 63);
+          ca += TA[ch];
+          cb += TB[ch];
         }
         part = (int)hit;
         j = (int)(K - pre_hit);
       }
-      ftt = (uint32_t)wave_red<OP_MAX>((long long)ftt);
-      fna = (uint32_t)wave_red<OP_MAX>((long long)fna);
+      wave_max2(ftt, fna);
       // pod k's AssumePod on the winner's slot (before the closing barrier: the next pod's pass A
       // reads that row without a barrier of its own)
       if (commit && gbest != 0) {
@@ -1720,6 +1796,10 @@ __device__ __forceinline__ bool simple_sync_win(SimpleHdr& H, int& parity, long 
         H.win[4] = part;
         H.win[5] = j;
         H.win[10] = cut >= 0 && (cut_tt > ftt || cut_na > fna);  // the cut shard's partial maxima can matter
+        if (sp) {
+          sp[11] = wall_clock64();
+          sp[14] = 1 + (cut == w ? 2 : 0) + (H.win[10] ? 4 : 0);
+        }
       }
     }
   }
@@ -1752,6 +1832,7 @@ __device__ __forceinline__ bool simple_sync_win(SimpleHdr& H, int& parity, long 
         const uint32_t x = threadIdx.x == 0 ? (uint32_t)cd : (threadIdx.x == 1 ? (uint32_t)ctt : (uint32_t)cna);
         xpub(X, gran, e2 + threadIdx.x, tag | x);
       }
+      if (sp && threadIdx.x == 0) sp[12] = wall_clock64();
     }
     if (W > 1 && need) {
       if (wave == 0) {

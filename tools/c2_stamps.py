@@ -5,7 +5,7 @@
 CONFIG is a BASELINE config index (2 = C2, 3 = C3, 4 = C4); 1000 pods of it are scheduled
 per shard count and tools/stamps.py summarises shard 0's phases.  STAMP_OPTS="name=v,..." sets
 library options first (e.g. no_spread=1: the general kernel k_schedule, the per-pod service's
-chain)."""
+chain); STAMP_PCT sets percentageOfNodesToScore (default 100; 0 = the adaptive window)."""
 import os
 import sys
 import tempfile
@@ -29,7 +29,9 @@ def main():
             native.set_option(k, int(v))
         native.set_option("shards", w)
         s = native.Synth(cfg, SEED_BASE + cfg, n_nodes, 1000)
-        ctx = native.Context(abi.default_profile(), device=0)
+        prof = abi.default_profile()
+        prof.pct_nodes_to_score = int(os.environ.get("STAMP_PCT", "100"))
+        ctx = native.Context(prof, device=0)
         ctx.load(s.cluster)
         ctx.stage(s.pods)
         ctx.run_staged(s.n_pods)

@@ -80,8 +80,26 @@ def summarise(path):
             dd = np.median(np.diff(seq, axis=1) / 100.0, axis=0)
             line += (f"\n  red_stats detail (shard 0): wave_red={dd[0]:.2f} write+barrier={dd[1]:.2f}"
                      f" combine={dd[2]:.2f} us")
+        if (s0[ok, 14] > 0).any():  # window mode: exchange detail (slots 10-14)
+            line += window_detail(s0[ok])
         lines.append(line)
     return "\n".join(lines)
+
+
+def window_detail(s):
+    """k_simple window exchange of shard 0: combine done (4) -> poll done (10) -> cut computed (11)
+    -> [cut shard: rank scan done (12)] -> done (5); slot 14 = 1 + 2 (shard 0 holds the cut) + 4
+    (the second exchange E2 was needed)."""
+    f = s[:, 14]
+    d1 = np.median((s[:, 10] - s[:, 4]) / 100.0)
+    d2 = np.median((s[:, 11] - s[:, 10]) / 100.0)
+    d3 = np.median((s[:, 5] - s[:, 11]) / 100.0)
+    line = (f"\n  window (shard 0): publish+poll={d1:.2f} cut={d2:.2f} rest={d3:.2f} us;"
+            f" shard 0 cut in {int(((f & 2) > 0).sum())}/{len(f)} pods, E2 needed in {int(((f & 4) > 0).sum())}")
+    c = (f & 2) > 0
+    if c.any():
+        line += f"; as cut shard: rank scan {np.median((s[c, 12] - s[c, 11]) / 100.0):.2f} us"
+    return line
 
 
 def spread_summary(w, a):
