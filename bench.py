@@ -1064,6 +1064,15 @@ def c2_pct0_leg(args, world: int, rank: int, local: int, dist) -> dict:
                      "C2 pct=0", args.c4_timeout, min(args.cpu_seconds, 6.0))
 
 
+def c3_pct0_leg(args, world: int, rank: int, local: int, dist) -> dict:
+    """C3 at the simulator's adaptive default (percentageOfNodesToScore = 0: K = 500 of 5,000
+    nodes), on k_spread's window (kss_spread.cuh spread_schedule WIN): the PreFilter statistics
+    over every node, the filter until the 501st feasible node from nextStartNodeIndex, the score
+    over the 500 kept ones."""
+    return child_leg(args, world, rank, local, dist, ["--config", "3", "--pct", "0", "--no-legs", "--no-traffic"],
+                     "C3 pct=0", args.c4_timeout, min(args.cpu_seconds, 6.0))
+
+
 def child_leg(args, world: int, rank: int, local: int, dist, mode, label, timeout, cpu_seconds,
               traffic=False) -> dict:
     """Run `bench.py <mode>` as one child process per rank (torchrun's environment passed on, a
@@ -1134,7 +1143,7 @@ def main():
     ap.add_argument("--no-c4", action="store_true", help="skip the C4 split-grid leg of the main line")
     ap.add_argument("--no-c5", action="store_true", help="skip the C5 scenario-sweep leg of the main line")
     ap.add_argument("--no-c3", action="store_true", help="skip the C3 (PTS + IPA, k_spread) leg of the main line")
-    ap.add_argument("--no-pct0", action="store_true", help="skip the C2 percentageOfNodesToScore=0 leg of the main line")
+    ap.add_argument("--no-pct0", action="store_true", help="skip the C2 / C3 percentageOfNodesToScore=0 legs of the main line")
     ap.add_argument("--no-legs", action="store_true", help="no extra legs (the legs' own child runs)")
     ap.add_argument("--pct", type=int, default=100,
                     help="percentageOfNodesToScore of the profile (100: every node, the north_star setting; "
@@ -1243,6 +1252,7 @@ def main():
     c5 = None if args.no_c5 or not main_shape else c5_sweep_leg(args, world, rank, local, dist)
     c3 = None if args.no_c3 or not main_shape else c3_leg(args, world, rank, local, dist)
     c2p0 = None if args.no_pct0 or not main_shape else c2_pct0_leg(args, world, rank, local, dist)
+    c3p0 = None if args.no_pct0 or not main_shape else c3_pct0_leg(args, world, rank, local, dist)
     if rank == 0:
         cpu = None
         if not args.no_cpu and world == 1:
@@ -1297,6 +1307,7 @@ def main():
             "c5_sweep": c5,
             "c3": c3,
             "c2_pct0": c2p0,
+            "c3_pct0": c3p0,
         }
         print(json.dumps(out), flush=True)
     ctx.close()

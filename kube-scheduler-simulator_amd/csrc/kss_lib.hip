@@ -65,7 +65,7 @@ enum KssOpt {
   O_SHARDS, O_XCD, O_XCD_SHARDS, O_NO_SIMPLE, O_NO_SPREAD, O_AXIS_BLOCKS, O_AXIS_NO_FOLD, O_NODES_PER_SHARD,
   O_THREADS, O_FORCE_THREADS, O_COOP_LAUNCH, O_NO_CACHE, O_STATIC_BYTES, O_STATIC_PPB, O_FOLD, O_TRACE_PATH,
   O_SVC_INLINE_SWEEP, O_SERVICE_STAMPS, O_SVC_FULL_FENCE, O_SERVICE_GENERAL, O_SVC_XCD, O_SVC_NO_STATIC,
-  O_SWEEP_PIPE, O_SERVICE_NO_DIFF, O_SVC_HUGE, O_XCD_FORCE_FALLBACK, O_SPREAD_TWO_LEVEL, O_N
+  O_SWEEP_PIPE, O_SERVICE_NO_DIFF, O_SVC_HUGE, O_XCD_FORCE_FALLBACK, O_SPREAD_TWO_LEVEL, O_SPREAD_LB256, O_N
 };
 struct OptDef {
   const char* name;
@@ -100,6 +100,7 @@ const OptDef kOptDefs[O_N] = {
     {"svc_huge", "KSS_SVC_HUGE", 0},
     {"xcd_force_fallback", "KSS_XCD_FORCE_FALLBACK", 0},  // XCD-local launches report failed placement
     {"spread_two_level", "KSS_SPREAD_TWO_LEVEL", 1},      // k_spread at W > 64: 1 two-level selectHost exchange, 2 + reductions
+    {"spread_lb256", "KSS_SPREAD_LB256", 1},              // k_spread compiled for <= 256 lanes when the shard fits
 };
 std::atomic<long long> g_opt[O_N];
 std::once_flag g_opt_once;
@@ -355,11 +356,16 @@ __global__ __launch_bounds__(KSS_MAX_THREADS) void k_simple(const DevJob* __rest
 // presence values of the exchange vector.  DEF: the v1.26 default profile, folded.  FOLD: the
 // statistics fold compiled in (KSS_FOLD=1; a separate kernel, so the default one keeps the
 // register allocation the fold's code would spill: 36 against 164 B of scratch per lane).
-template <bool DEF, bool FOLD>
-__global__ __launch_bounds__(KSS_MAX_THREADS) void k_spread(const DevJob* __restrict__ jobs, int W, int cap, int bins_cap,
+// LB: the workgroup-size bound the register allocation is made for.  At <= 256 lanes (C3's
+// 192-lane shards) one wave per SIMD: 512 registers per lane (256 VGPRs + 256 AGPRs), so the
+// allocator keeps in registers what the 512-lane bound spills to scratch.
+// WIN: percentageOfNodesToScore < 100 (one job): k_find = numFeasibleNodesToFind, the window's
+// nextStartNodeIndex in job.cursor (kss_spread.cuh spread_schedule)
+template <bool DEF, bool FOLD, int LB, bool WIN>
+__global__ __launch_bounds__(LB) void k_spread(const DevJob* __restrict__ jobs, int W, int cap, int bins_cap,
                                                             int n_res, int gq, int gs, int k0, int k1, unsigned long long* gran,
                                                             int* err, unsigned long long* stamps, int nst, XPeers X,
-                                                            unsigned epoch0, HandoffCheck hc) {
+                                                            unsigned epoch0, HandoffCheck hc, int k_find) {
   extern __shared__ __attribute__((aligned(16))) long long smem[];
   const int Wl = X.n > 1 ? X.wl : W;
   SpreadHdr& H = *reinterpret_cast<SpreadHdr*>(smem);
@@ -380,7 +386,7 @@ __global__ __launch_bounds__(KSS_MAX_THREADS) void k_spread(const DevJob* __rest
   constexpr kss_profile def_prof = default_profile_c();
 #ifdef KSS_LDS_POISON  // experiment builds: the shard's LDS image filled with a pattern first
   {
-    const size_t words = spread_lds_bytes(cap, bins_cap, job.c.n_keys, n_res, gq, job.c.n_scalar) / 4;
+    const size_t words = spread_lds_bytes(cap, bins_cap, job.c.n_keys, n_res, gq, job.c.n_scalar, FOLD) / 4;
     uint32_t* p = reinterpret_cast<uint32_t*>(smem);
     for (size_t i = threadIdx.x; i < words; i += blockDim.x) p[i] = 0x5A5A5A5Au;
     __syncthreads();
@@ -393,9 +399,9 @@ __global__ __launch_bounds__(KSS_MAX_THREADS) void k_spread(const DevJob* __rest
     __syncthreads();
   }
   const kss_profile& P = DEF ? def_prof : H.prof;
-  spread_schedule<DEF, FOLD>(job.trace, job.c, job.gpods, job.stat, job.res_rows, n_res, k0, min(k1, job.n_pods), job.chosen, job.meta, P, W, w,
+  spread_schedule<DEF, FOLD, WIN>(job.trace, job.c, job.gpods, job.stat, job.res_rows, n_res, k0, min(k1, job.n_pods), job.chosen, job.meta, P, W, w,
                   cap, bins_cap, gq, gs, gran ? gran + (size_t)ji * 2 * W * gs : nullptr, X, epoch0, err, stamps, nst, hc,
-                  smem);
+                  smem, k_find, job.cursor);
 }
 
 // Class / term counts of the chosen nodes of pods [k0, min(k1, n_pods)) of every job
@@ -681,6 +687,8 @@ struct GpodNeeds {
   std::vector<int32_t> res_rows;  // the resident count rows: class r as r, term r as n_classes + r
   int gq = 0;             // record stride (uint4) of the batch
   int xw = 2;             // longest exchange of the batch (values per shard; the argmax's 2 at least)
+  int fold_xw = 0;        // fold: max bins + hard presence of a folding pod (carried by the previous pod's E2)
+  int soft_xw = 0;        // max soft presence bins of a pod (its own E2)
   int gs() const { return (xw + 15) / 16 * 16; }  // granule stride per shard: whole 128-byte lines
   int fail_code = 0, fail_pod = -1;  // why / where build_gpods refused (GP_*)
 };
@@ -1188,8 +1196,8 @@ const char* const kGpReason[GP_NCODES] = {
     "more than 16 inter-pod-affinity entries after merging",
     "the profile scores an extended (scalar) resource: k_simple / k_spread score cpu, memory and ephemeral-storage only",
     "host ports (NodePorts), node-cached images (ImageLocality) or volumes: k_schedule only",
-    "percentageOfNodesToScore below 100 (numFeasibleNodesToFind / nextStartNodeIndex window): k_simple for pods "
-    "without a NodeAffinity PreFilterResult list, else k_schedule",
+    "percentageOfNodesToScore below 100 (numFeasibleNodesToFind / nextStartNodeIndex window): k_simple, and k_spread "
+    "under the default profile, for pods without a NodeAffinity PreFilterResult list, else k_schedule",
     "the profile scores an extended (scalar) resource and the cluster has extended resources: k_schedule only",
 };
 
@@ -1380,20 +1388,24 @@ bool build_gpods(const kss_podset* ps, int n_scalar, int n_classes, const int32_
     // exchanges: E1 (scalars + bins), E2 (scalars + soft presence)
     if (MAXH + 1 + off + g.hard_pbins > G_XW || 13 + (poff - g.hard_pbins) > G_XW) return gfail(need, GP_XW, i);
     need.xw = std::max(need.xw, std::max(MAXH + 1 + off + g.hard_pbins, 13 + (poff - g.hard_pbins)));
-    // the statistics exchange folded into the previous pod's argmax (kss_spread.cuh
-    // spread_argmax_fold): histogram-valued DoNotSchedule groups only (a node-valued group's
-    // critical path is a minimum over nodes, which a single node's delta cannot update), and the
-    // fused exchange within the granule stride; the delta bound is checked for the batch below
+    // the statistics exchange folded into the previous pod's filter exchange and argmax
+    // (kss_spread.cuh spread_argmax_pay): histogram-valued DoNotSchedule groups only (a
+    // node-valued group's critical path is a minimum over nodes, which a single node's delta
+    // cannot update); the previous pod's filter exchange (at most 14 scalars and its soft
+    // presence) carries this pod's bins and hard presence, its argmax one payload per
+    // constraint / entry.  need.fold_xw / soft_xw bound the widest such pair (checked below).
     g.fold = 0;
     if (stats) {
       bool node_valued = false;
       for (int c = 0; c < p.n_hard; c++) node_valued |= g.sp[c].off < 0;
-      const int np = p.n_hard + p.n_soft + g.n_ipa + (g.n_ipa > 0 ? 1 : 0), fm = 2 + off + g.hard_pbins + np;
-      if (!node_valued && np <= G_PAY && fm <= G_XW) {
+      const int np = p.n_hard + p.n_soft + g.n_ipa + (g.n_ipa > 0 ? 1 : 0);
+      if (!node_valued && np <= G_PAY && 1 + np <= G_XW && off + g.hard_pbins <= G_XW) {
         g.fold = 1;
-        need.xw = std::max(need.xw, fm);
+        need.fold_xw = std::max(need.fold_xw, off + g.hard_pbins);
+        need.xw = std::max(need.xw, 1 + np);
       }
     }
+    need.soft_xw = std::max(need.soft_xw, poff - g.hard_pbins);
     need.bins_cap = std::max(need.bins_cap, off + poff);
     // AssumePod's count rows: the pod's class, its own term rows
     if (1 + p.own_terms_len > G_CMT) return gfail(need, GP_COMMIT, i);
@@ -1412,8 +1424,10 @@ bool build_gpods(const kss_podset* ps, int n_scalar, int n_classes, const int32_
   }
   // a folded delta travels as int16 (payload low half): Σ|coefficient| x commits per row bounds it.
   // Opt-in (KSS_FOLD=1): measured no faster on C4 and slower on C3
-  if (need.ref_weight * need.max_mult > 32767 || !opt(O_FOLD))
+  if (need.ref_weight * need.max_mult > 32767 || !opt(O_FOLD) || 14 + need.soft_xw + need.fold_xw > G_XW)
     for (int i = 0; i < ps->n_pods; i++) out[(size_t)i].fold = 0;
+  else
+    need.xw = std::max(need.xw, 14 + need.soft_xw + need.fold_xw);
   // rows first read by a later pod than one committing to them: re-resolve the commits
   size_t rmax = 0;
   int rmax_pod = 0;
@@ -2858,7 +2872,7 @@ static int spread_cap(const Geometry& g, size_t N) {
 }
 
 static size_t spread_lds(const Geometry& g, const GpodNeeds& q, int n_keys, int n_res, size_t N, int nsc) {
-  return spread_lds_bytes(spread_cap(g, N), q.bins_cap, n_keys, n_res, q.gq, nsc);
+  return spread_lds_bytes(spread_cap(g, N), q.bins_cap, n_keys, n_res, q.gq, nsc, opt(O_FOLD) != 0);
 }
 
 static bool spread_fits(const Geometry& g, const GpodNeeds& q, int n_keys, int n_res, size_t N, int nsc) {
@@ -2886,7 +2900,8 @@ static int launch_spread(hipStream_t st, const Geometry& g, const GpodNeeds& q, 
                          const DevJob* jobs, const kss_profile& prof, int n_pods, int max_nodes, int chunk,
                          unsigned long long* gran, size_t gran_bytes, int* err, unsigned long long* stamps = nullptr,
                          hipEvent_t* ev = nullptr, const SplitRun* split = nullptr, unsigned long long* ck = nullptr,
-                         unsigned long long* ck_seq = nullptr, int nsc = 0, bool xcd = false, int* xcd_fallbacks = nullptr) {
+                         unsigned long long* ck_seq = nullptr, int nsc = 0, bool xcd = false, int* xcd_fallbacks = nullptr,
+                         int k_find = 0) {
   int cap = spread_cap(g, (size_t)max_nodes), bins_cap = q.bins_cap, nr = n_res, gq = q.gq, gs = q.gs();
   size_t shmem = spread_lds(g, q, n_keys, n_res, (size_t)max_nodes, nsc);
   // diagnostic stamps in LDS: as many pods (<= G_NSTAMP, >= 8) as fit beside the shard state
@@ -2900,8 +2915,18 @@ static int launch_spread(hipStream_t st, const Geometry& g, const GpodNeeds& q, 
 #endif
   const bool def = same_profile(prof, default_profile_c());
   const bool fold = opt(O_FOLD) != 0;
-  const void* fn = def ? (fold ? (const void*)k_spread<true, true> : (const void*)k_spread<true, false>)
-                       : (fold ? (const void*)k_spread<false, true> : (const void*)k_spread<false, false>);
+  const bool lb = g.threads <= 256 && opt(O_SPREAD_LB256);
+  const void* fn = lb ? (def ? (fold ? (const void*)k_spread<true, true, 256, false> : (const void*)k_spread<true, false, 256, false>)
+                             : (fold ? (const void*)k_spread<false, true, 256, false> : (const void*)k_spread<false, false, 256, false>))
+                      : (def ? (fold ? (const void*)k_spread<true, true, KSS_MAX_THREADS, false>
+                                     : (const void*)k_spread<true, false, KSS_MAX_THREADS, false>)
+                             : (fold ? (const void*)k_spread<false, true, KSS_MAX_THREADS, false>
+                                     : (const void*)k_spread<false, false, KSS_MAX_THREADS, false>));
+  // the window (default profile, no fold): its own instantiations
+  if (k_find > 0) {
+    if (!def || fold) return fail(KSS_E_INVAL, "k_spread window: default profile, no statistics fold");
+    fn = lb ? (const void*)k_spread<true, false, 256, true> : (const void*)k_spread<true, false, KSS_MAX_THREADS, true>;
+  }
   HIP_TRY(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shmem));
   XPeers X = split ? split->X : XPeers{};
   const bool sp_grid = X.n > 1;
@@ -2947,7 +2972,7 @@ static int launch_spread(hipStream_t st, const Geometry& g, const GpodNeeds& q, 
     }
     void* args[] = {(void*)&jobs, (void*)&W,  (void*)&cap, (void*)&bins_cap, (void*)&nr,  (void*)&gq, (void*)&gs, (void*)&k0,
                     (void*)&k1,   (void*)&gc, (void*)&err, (void*)&sp,       (void*)&nst, (void*)&X,  (void*)&epoch0,
-                    (void*)&hc};
+                    (void*)&hc,   (void*)&k_find};
     const int ci = k0 / chunk;
     if (ev) HIP_TRY(hipEventRecord(ev[2 * ci], st));
     if (xcd) {  // as launch_simple: an XCD-local grid, run again unrestricted when placement failed
@@ -3084,7 +3109,12 @@ static int run_single_impl(kss_ctx* ctx, const PlanNeeds& need, const DevPods& d
   // a batch with programs on k_spread: 32-bit counts and scores (spread_bounds_ok)
   const double count_total = ctx->count_bound + (commit ? (double)n * (1.0 + ctx->staged_max_own) : 0.0);
   const double cell_total = ctx->cell_bound + (commit ? (double)n * ctx->gneed.max_mult : 0.0);
-  const bool spread_ok = !window && !nomq && staged && ctx->gpod_ok && commit && !record && !keep_norm && need.general &&
+  // k_spread runs the window itself (spread_schedule WIN) for default-profile pods without a
+  // PreFilterResult list on an unsplit grid, the statistics fold off
+  const bool spread_win = window && k_find < (int)N;
+  const bool spread_win_ok = !spread_win || (!split && !ctx->staged_names && !opt(O_FOLD) &&
+                                             same_profile(ctx->prof, default_profile_c()));
+  const bool spread_ok = spread_win_ok && !nomq && staged && ctx->gpod_ok && commit && !record && !keep_norm && need.general &&
                          scalar_fast_ok(ctx->prof, ctx->dc.n_scalar) && ctx->small_values && f64_exact(ctx->f64_cluster, ctx->f64_pods, n) &&
                          !ctx->no_simple && !ctx->no_spread && !(flags & KSS_SCHED_GENERAL_KERNEL) &&
                          spread_bounds_ok(ctx->gneed, count_total, cell_total, (int)N);
@@ -3297,9 +3327,16 @@ static int run_single_impl(kss_ctx* ctx, const PlanNeeds& need, const DevPods& d
     if ((rc = ctx->ck_buf.ensure(sizeof(unsigned long long) * hl.words))) return rc;
     HIP_TRY(dev_zero((unsigned long long*)ctx->ck_buf.p + hl.o_diag, sizeof(unsigned long long), ctx->stream));
     ctx->ck_diag_off = hl.o_diag;
-    rc = launch_spread(ctx->stream, g, ctx->gneed, ctx->dc.n_keys, n_res, jd, ctx->prof, n,
+    // the window's count exchange: W SUM values behind the pod's bins, one scalar
+    GpodNeeds qw = ctx->gneed;
+    if (spread_win) {
+      qw.bins_cap += g.W;
+      qw.xw = std::max(qw.xw, g.W + 1);
+    }
+    rc = launch_spread(ctx->stream, g, qw, ctx->dc.n_keys, n_res, jd, ctx->prof, n,
                        (int)N, chunk, gran, gb, errp, stamps, ctx->loop_ev.data(), split ? &srun : nullptr,
-                       (unsigned long long*)ctx->ck_buf.p, &ctx->ck_seq, ctx->dc.n_scalar, xcd_spread, &ctx->last_xcd[1]);
+                       (unsigned long long*)ctx->ck_buf.p, &ctx->ck_seq, ctx->dc.n_scalar, xcd_spread, &ctx->last_xcd[1],
+                       spread_win ? k_find : 0);
   }
   else  // window: the per-shard feasible counts sit behind the plan's bins
     rc = launch_schedule(ctx->stream, g, 1, std::max(need.bins_cap, 0) + (window ? g.W : 0), need.general, ctx->dc.n_keys,
@@ -5144,13 +5181,15 @@ int kss_plan_podset_ex(const kss_cluster* cl, const kss_podset* ps, const kss_pr
   if (int rc = kss_plan_podset(cl, ps, out3)) return rc;
   if (out3[0] == 0) return 0;  // the programs already rule out both loop kernels
   // the window (percentageOfNodesToScore < 100 on a list long enough to stop early) runs on k_simple
-  // for pods without a PreFilterResult node list (simple_sync_win), never on k_spread
+  // (simple_sync_win) and, under the default profile, on k_spread (spread_schedule WIN) for pods
+  // without a PreFilterResult node list
   int names_pod = -1;
   for (int i = 0; i < ps->n_pods && names_pod < 0; i++)
     if (ps->pods[i].names_len >= 0) names_pod = i;
   const bool win = num_feasible_to_find(cl->n_nodes, prof->pct_nodes_to_score) < cl->n_nodes;
-  if (win && (out3[0] == 2 || names_pod >= 0)) {
-    out3[1] = out3[0] == 2 || names_pod < 0 ? (ps->n_pods > 0 ? 0 : -1) : names_pod;
+  const bool spread_def = out3[0] == 2 && same_profile(*prof, default_profile_c()) && !opt(O_FOLD);
+  if (win && ((out3[0] == 2 && !spread_def) || names_pod >= 0)) {
+    out3[1] = names_pod >= 0 ? names_pod : (ps->n_pods > 0 ? 0 : -1);
     out3[0] = 0;
     out3[2] = GP_PCT;
   } else if (!scalar_fast_ok(*prof, cl->n_scalar)) {

@@ -41,7 +41,7 @@ constexpr int G_XW = 512;    // 32-bit values per shard per exchange (host-check
 // 4 KiB stride (G_XW) every shard's value j shared one page offset, so the whole grid's
 // polls and publishes went to one memory channel.
 constexpr int G_NS = 16;     // scalar slots of an exchange
-constexpr int G_PAY = 32;    // payload values of a fused exchange (spread_argmax_fold)
+constexpr int G_PAY = 32;    // payload values of the argmax exchange (spread_argmax_pay)
 constexpr int G_SCORE = 3;   // GIpa.kind of a merged InterPodAffinity score entry (KSS_IPA_SCORE_CLASS)
 constexpr int G_NSTAMP = KSS_NSTAMP_PODS / 2;  // pods with diagnostic phase stamps, 16 per pod
 
@@ -71,6 +71,8 @@ enum : int {
   GT_CMT = 80,       // [8] the winner shard's commit: n_cmt, then (resident row, count before) pairs
   GT_PRO = 88,       // nonzero bins of the first pod's range right after the prologue zeroed them
   GT_XCC = 89,       // (first pod of a launch) the XCD the shard's workgroup runs on
+  GT_WIN = 90,       // [9] window: shard count, before-start count, exchanged before count, parts a before,
+                     // all parts a, parts b before, stopping node + 1, kept nodes, start node
 };
 constexpr int G_TLIST = 1 << 20;  // entries of the count list: {tag, row, node, value}; tag = k0 (load) or -1 - k1 (store)
 struct GTrace {
@@ -110,7 +112,7 @@ struct alignas(16) GPod {
   int32_t pflags, n_hard, n_soft, n_ipa;
   int32_t n_keys, total_bins, hard_pbins, total_pbins;
   int32_t need_stats, n_cmt;
-  int32_t fold;  // the statistics exchange may ride with the previous pod's argmax (spread_argmax_fold)
+  int32_t fold;  // the statistics may ride with the previous pod's exchanges (spread_argmax_pay)
   int32_t pad1;
   int32_t key[MAXK];
   int32_t hoff[MAXK][4];
@@ -164,6 +166,9 @@ struct alignas(16) SpreadHdr {
   int32_t pad[2];
   int32_t tl_x, tl_s, tl_n;  // two-level exchange (X.tl): the shard's XCD, its rank there, the XCD's shards
   uint32_t tl_mask;          // ... the XCDs holding shards
+  int32_t wc[G_PF][MAXWAVES];  // window: feasible slots per (loop iteration, wave)
+  int32_t wb[G_PF][MAXWAVES];  // ... of them, nodes before the start node
+  int32_t wsum[4];             // ... parts a before this shard, all parts a, parts b before this shard
 };
 
 struct SpreadShard {
@@ -187,28 +192,32 @@ struct SpreadShard {
   int cap, nsc;
 };
 
-__host__ __device__ inline size_t spread_lds_bytes(int cap, int bins_cap, int n_keys, int n_res, int gq, int nsc = 0) {
+// fold (k_spread<., true>): two bins areas (pod k and pod k + 1, by parity) and three static-word
+// slots (pods k .. k + 2: the early statistics pass of pod k + 1 reads its words during pod k)
+__host__ __device__ inline size_t spread_lds_bytes(int cap, int bins_cap, int n_keys, int n_res, int gq, int nsc = 0,
+                                                   bool fold = false) {
   const size_t C = (size_t)cap;
-  size_t b = (sizeof(SpreadHdr) + 4 * ((size_t)G_NS + (size_t)bins_cap) + 15) / 16 * 16;
-  b += 3 * 16 * (size_t)gq + 4 * 2 * C + ((size_t)n_res * C * 2 + 15) / 16 * 16;
+  const size_t nb = (size_t)bins_cap * (fold ? 2 : 1), nst = fold ? 3 : 2;
+  size_t b = (sizeof(SpreadHdr) + 4 * ((size_t)G_NS + nb) + 15) / 16 * 16;
+  b += 3 * 16 * (size_t)gq + 4 * nst * C + ((size_t)n_res * C * 2 + 15) / 16 * 16;
   b += 8 * 8 * C + 8 * 3 * C + 8 * 2 * C + 4 * 3 * C + 4 * (size_t)n_keys * C + 4 * 6 * C;
   b += 16 * (size_t)nsc * C;
   return b;
 }
 
 __device__ __forceinline__ SpreadShard spread_view(long long* smem, int cap, int bins_cap, int n_keys, int n_res,
-                                                   int gq, int nsc) {
+                                                   int gq, int nsc, bool fold = false) {
   SpreadShard L;
   const size_t C = (size_t)cap;
   L.nsc = nsc;
   uint8_t* b = reinterpret_cast<uint8_t*>(smem);
   size_t o = sizeof(SpreadHdr);
   L.xs = reinterpret_cast<int32_t*>(b + o);
-  o = (o + 4 * ((size_t)G_NS + (size_t)bins_cap) + 15) / 16 * 16;
+  o = (o + 4 * ((size_t)G_NS + (size_t)bins_cap * (fold ? 2 : 1)) + 15) / 16 * 16;
   L.ring = reinterpret_cast<uint4*>(b + o);
   o += 3 * 16 * (size_t)gq;
   L.st = reinterpret_cast<uint32_t*>(b + o);
-  o += 4 * 2 * C;
+  o += 4 * (fold ? 3 : 2) * C;
   L.cnt = reinterpret_cast<uint16_t*>(b + o);
   o += ((size_t)n_res * C * 2 + 15) / 16 * 16;
   L.r64 = reinterpret_cast<double*>(b + o);
@@ -335,18 +344,21 @@ __device__ __forceinline__ bool spread_exchange(SpreadHdr& H, int32_t* xs, unsig
                                                 int W, int wself, int gs,
                                                 unsigned epoch, int* err, int K, unsigned opbits, int sum_lo, int ns,
                                                 int or_lo, int no, unsigned long long* sp, int gw = 0, int nsw = 1,
-                                                int phase = 3, int np = 0) {
+                                                int phase = 3, int np = 0, int or2_lo = 0, int no2 = 0) {
   constexpr int XS = G_XS;
   const int lane = threadIdx.x & 63, nw = blockDim.x >> 6;
-  // np > 0 (spread_argmax_fold): after the bins, np payload values H.payv[] whose fold keeps
+  // np > 0 (spread_argmax_pay): after the bins, np payload values H.payv[] whose fold keeps
   // the value of the shard with the largest key (scalar 0, a compressed key with its top bit
-  // flipped so that the signed MAX orders it), into H.pay[] as {key, payload}
-  const int M0 = K + ns + no, M = M0 + np;
+  // flipped so that the signed MAX orders it), into H.pay[] as {key, payload}.
+  // no2: a second OR range [or2_lo, + no2) after the first (the fold's early statistics of the
+  // next pod ride with this pod's filter exchange: its hard presence in the other bins area)
+  const int M0 = K + ns + no + no2, M = M0 + np;
   KSS_GLOBAL unsigned long long* gran = gp(gran_);
   auto slot = [&](int j) -> int32_t* {
     if (j < K) return xs + j;
     if (j < K + ns) return xs + G_NS + sum_lo + (j - K);
-    if (j < M0) return xs + G_NS + or_lo + (j - K - ns);
+    if (j < K + ns + no) return xs + G_NS + or_lo + (j - K - ns);
+    if (j < M0) return xs + G_NS + or2_lo + (j - K - ns - no);
     return H.payv + (j - M0);
   };
   auto opof = [&](int j) { return j < K ? (int)((opbits >> (2 * j)) & 3u) : (j < K + ns ? OP_SUM : OP_OR); };
@@ -454,9 +466,8 @@ __device__ __forceinline__ bool spread_exchange(SpreadHdr& H, int32_t* xs, unsig
 
 // Wave 0, once the cluster bins are final: criticalPaths[0] of pod q's histogram-valued
 // DoNotSchedule groups — the minimum over the present domains, into the scalar xs[i].
-__device__ __forceinline__ void hard_minima(const GPod& q, int32_t* xs) {
+__device__ __forceinline__ void hard_minima(const GPod& q, int32_t* xs, const int32_t* bins) {
   const int lane = threadIdx.x & 63;
-  const int32_t* bins = xs + G_NS;
   for (int i = 0; i < q.n_hard; i++) {
     const GSpread& sp = q.sp[i];
     if (sp.off < 0 || sp.own != i) continue;
@@ -584,6 +595,88 @@ __device__ __forceinline__ bool tl_argmax(SpreadHdr& H, const XPeers& X, int W, 
   return true;
 }
 
+// tl_argmax with payloads (spread_argmax_pay at W > 64, X.tl): wave 0.  Each shard stores one
+// line into its XCD's reduction area: word 0 its compressed key kc (0: no candidate), words
+// 1..np its payloads H.payv[]; the XCD's rank-0 shard keeps, per word, the value of its shards'
+// largest key and stores that line write-through; every shard does the same over the XCDs'
+// lines.  Out: the cluster's largest key, H.pay[j] = {key, payload j} of its shard.  The line
+// area is the two-level reductions' (tl_o_rloc / tl_o_rglob), on the same epoch sequence.
+__device__ __forceinline__ bool tl_argmax_pay(SpreadHdr& H, const XPeers& X, int W, unsigned epoch, uint32_t kc,
+                                              int np, int* err, uint32_t& out) {
+  const int lane = threadIdx.x & 63;
+  const int M = 1 + np;
+  const int MP = M <= 4 ? 4 : (M <= 8 ? 8 : 16);
+  const int ls = tl_ls(W);
+  const unsigned long long tag = (unsigned long long)epoch << 32;
+  unsigned long long* loc = X.tl + tl_o_rloc(W) + ((size_t)(epoch & 1) * TL_G + H.tl_x) * ls * TL_M;
+  unsigned long long* glob = X.tl + tl_o_rglob(W) + (size_t)(epoch & 1) * TL_G * TL_M;
+  const int j = lane & (MP - 1), t = lane / MP, T = 64 / MP;
+  const bool jv = j < M;
+  if (lane < M) {
+    const uint32_t v = lane == 0 ? kc : (uint32_t)H.payv[lane - 1];
+    asm volatile("global_store_dwordx2 %0, %1, off" ::"v"(loc + (size_t)H.tl_s * TL_M + lane), "v"(tag | v) : "memory");
+  }
+  // (key, value) pairs of up to 4 lines per lane, the value of the largest key kept
+  auto fold_lines = [&](auto&& addr, auto&& in_of, int n0, int n, uint32_t& a_key, uint32_t& a_val) -> bool {
+    for (int s0 = n0; s0 < n; s0 += 4 * T) {
+      unsigned long long g[4], gk[4];
+      bool in[4];
+#pragma unroll
+      for (int b = 0; b < 4; b++) in[b] = jv && in_of(s0 + t + T * b);
+      long long t0 = 0;
+      for (unsigned spins = 0;; ++spins) {
+        bool ok = true;
+#pragma unroll
+        for (int b = 0; b < 4; b++) {
+          g[b] = gk[b] = tag;
+          if (in[b]) {
+            g[b] = __hip_atomic_load(addr(s0 + t + T * b) + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            gk[b] = __hip_atomic_load(addr(s0 + t + T * b), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          }
+          ok &= ((g[b] >> 32) == epoch) & ((gk[b] >> 32) == epoch);
+        }
+        if (__all(ok)) break;
+        if (spread_spin_over(spins, t0, err)) {
+          if (lane == 0) {
+            H.abort = 1;
+            err_raise(err, 1);
+          }
+          return false;
+        }
+        spin_pause();
+      }
+#pragma unroll
+      for (int b = 0; b < 4; b++) {
+        const uint32_t k = in[b] ? (uint32_t)gk[b] : 0u;
+        a_val = k > a_key ? (uint32_t)g[b] : a_val;
+        a_key = k > a_key ? k : a_key;
+      }
+    }
+    for (int o = MP; o < 64; o <<= 1) {
+      const uint32_t ok_ = (uint32_t)__shfl_xor((int)a_key, o, 64), ov = (uint32_t)__shfl_xor((int)a_val, o, 64);
+      a_val = ok_ > a_key ? ov : a_val;
+      a_key = ok_ > a_key ? ok_ : a_key;
+    }
+    return true;
+  };
+  if (H.tl_s == 0) {  // the XCD's line: its shards' lines from this XCD's L2
+    uint32_t a_key = 0, a_val = 0;
+    const int n = H.tl_n;
+    if (!fold_lines([&](int s) { return gp(loc) + (size_t)s * TL_M; }, [&](int s) { return s < n; }, 0, n, a_key, a_val))
+      return false;
+    if (t == 0 && jv)
+      __hip_atomic_store(gp(glob) + (size_t)H.tl_x * TL_M + j, tag | (j == 0 ? a_key : a_val), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+  }
+  uint32_t a_key = 0, a_val = 0;  // every shard: the XCDs' lines
+  if (!fold_lines([&](int x) { return gp(glob) + (size_t)x * TL_M; },
+                  [&](int x) { return x < TL_G && ((H.tl_mask >> x) & 1u); }, 0, TL_G, a_key, a_val))
+    return false;
+  if (t == 0 && j >= 1 && jv) H.pay[j - 1] = ((unsigned long long)a_key << 32) | a_val;
+  out = (uint32_t)__builtin_amdgcn_readfirstlane((int)a_key);
+  return true;
+}
+
 // spread_exchange's two-level form (X.tl, M = K + ns + no <= TL_M values, no payload): wave 0.
 // Every shard stores its M values as one line into its XCD's area (plain stores: that XCD's L2);
 // the XCD's rank-0 shard folds its shards' lines (MP = M rounded up to a power of two lanes per
@@ -693,7 +786,7 @@ __device__ __forceinline__ bool spread_reduce(SpreadHdr& H, int32_t* xs, int W, 
                                               unsigned long long* gran, const XPeers& X, int* err, int32_t (&v)[K],
                                               const int (&ops)[K], int sum_lo = 0, int ns = 0, int or_lo = 0,
                                               int no = 0, bool local = false, unsigned long long* sp = nullptr,
-                                              const GPod* minima_q = nullptr) {
+                                              const GPod* minima_q = nullptr, int or2_lo = 0, int no2 = 0) {
   static_assert(K <= G_NS, "too many values");
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
   int32_t r[K];
@@ -725,7 +818,7 @@ __device__ __forceinline__ bool spread_reduce(SpreadHdr& H, int32_t* xs, int W, 
       for (int x = 1; x < nw; x++) r = op32(op, r, H.red[x][k]);
       xs[k] = r;
     }
-    if (minima_q && wave == 0) hard_minima(*minima_q, xs);
+    if (minima_q && wave == 0) hard_minima(*minima_q, xs, xs + G_NS + sum_lo);
     lds_barrier();
   } else {
     unsigned opbits = 0;
@@ -733,28 +826,32 @@ __device__ __forceinline__ bool spread_reduce(SpreadHdr& H, int32_t* xs, int W, 
     for (int k = 0; k < K; k++) opbits |= (unsigned)ops[k] << (2 * k);
     ++epoch;
     if (sp && threadIdx.x == 0) sp[1] = wall_clock64();
-    const int M = K + ns + no;
-    if (X.tl_red && M <= TL_M) {  // two levels (spread_exchange_tl; option spread_two_level = 2), wave 0
+    const int M = K + ns + no + no2;
+    if (X.tl_red && M <= TL_M && no2 == 0) {  // two levels (spread_exchange_tl; option spread_two_level = 2), wave 0
       if (wave == 0 && spread_exchange_tl(H, xs, X, W, epoch, err, K, opbits, sum_lo, ns, or_lo, no) && minima_q)
-        hard_minima(*minima_q, xs);
+        hard_minima(*minima_q, xs, xs + G_NS + sum_lo);
       if (sp && threadIdx.x == 0) sp[4] = wall_clock64();
       lds_barrier();
       if (H.abort) return false;
     } else if (nw == 1 || (long long)W * M <= (long long)KSS_SPREAD_MW_MIN) {  // one polling round for one wave: wave 0 alone
-      if (wave == 0 && spread_exchange(H, xs, gran, X, W, w, gs, epoch, err, K, opbits, sum_lo, ns, or_lo, no, sp) &&
+      if (wave == 0 && spread_exchange(H, xs, gran, X, W, w, gs, epoch, err, K, opbits, sum_lo, ns, or_lo, no, sp, 0, 1, 3,
+                                       0, or2_lo, no2) &&
           minima_q)
-        hard_minima(*minima_q, xs);
+        hard_minima(*minima_q, xs, xs + G_NS + sum_lo);
       if (sp && threadIdx.x == 0) sp[4] = wall_clock64();
       lds_barrier();
       if (H.abort) return false;
     } else {  // many shards: wave 0 publishes, every wave sweeps a share (fewer polling rounds)
-      if (wave == 0) spread_exchange(H, xs, gran, X, W, w, gs, epoch, err, K, opbits, sum_lo, ns, or_lo, no, sp, 0, 1, 1);
+      if (wave == 0)
+        spread_exchange(H, xs, gran, X, W, w, gs, epoch, err, K, opbits, sum_lo, ns, or_lo, no, sp, 0, 1, 1, 0, or2_lo, no2);
       lds_barrier();  // the slots hold the operators' identities before any wave folds into them
       const int nsw = min(nw, KSS_SPREAD_SWEEP_WAVES);  // the sweeping waves (the rest wait)
-      if (wave < nsw) spread_exchange(H, xs, gran, X, W, w, gs, epoch, err, K, opbits, sum_lo, ns, or_lo, no, nullptr, wave, nsw, 2);
+      if (wave < nsw)
+        spread_exchange(H, xs, gran, X, W, w, gs, epoch, err, K, opbits, sum_lo, ns, or_lo, no, nullptr, wave, nsw, 2, 0,
+                        or2_lo, no2);
       lds_barrier();
       if (H.abort) return false;
-      if (minima_q && wave == 0) hard_minima(*minima_q, xs);
+      if (minima_q && wave == 0) hard_minima(*minima_q, xs, xs + G_NS + sum_lo);
       if (sp && threadIdx.x == 0) sp[4] = wall_clock64();
       lds_barrier();
     }
@@ -997,25 +1094,42 @@ __device__ __forceinline__ int32_t fold_payload(const SpreadShard& L, const GPod
   return f;
 }
 
-// spread_argmax for pod q with pod qn's statistics riding along (every wave calls it; bins of
-// qn already accumulated by this shard's statistics pass, flags_local its lanes' flags).  On
-// return: key = the cluster's best key of q, the bins hold qn's cluster statistics after q's
-// AssumePod, H.fmin / H.fflags qn's critical-path minima and flags.  False on abort.
-__device__ __forceinline__ bool spread_argmax_fold(SpreadHdr& H, const SpreadShard& L, int W, int w, int gs,
-                                                   unsigned& epoch, unsigned long long* gran, const XPeers& X, int* err,
-                                                   int parity, long long& key, int kb, int node_base, int lo,
-                                                   const GPod& q, const GPod& qn, int32_t flags_local,
-                                                   const uint32_t* sw1) {
+// Wave 0, pod qn's statistics final in bins (its cluster histograms after pod q's AssumePod):
+// its critical-path minima into H.fmin, its flags into H.fflags (read after the next barrier).
+__device__ __forceinline__ void fold_minima(SpreadHdr& H, const GPod& qn, const int32_t* bins, int32_t flags) {
+  const int lane = threadIdx.x & 63;
+  for (int i = 0; i < qn.n_hard; i++) {
+    const GSpread& sp = qn.sp[i];
+    int32_t m[1] = {INT32_MAX};
+    if (sp.off >= 0 && sp.own == i)
+      for (int b = lane; b < sp.nb; b += 64)
+        if (bins[qn.total_bins + sp.poff + b]) m[0] = min(m[0], bins[sp.off + b]);
+    const int op[1] = {OP_MIN};
+    wave_red32(m, op);
+    if (lane == 0) H.fmin[i] = m[0];
+  }
+  if (lane == 0) H.fflags = flags;
+}
+
+// spread_argmax for pod q, with the change its winner makes to pod qn's statistics riding along
+// (every wave calls it).  qn's statistics on the state before q's AssumePod (H0) were exchanged
+// with q's filter exchange into bins_n (flags_n their flags); each shard publishes, beside its
+// key, the payloads its candidate would add to them if it won (fold_payload: one (bin, delta) per
+// constraint / entry, then the candidate's InterPodAffinity flags after the commit); the sweep
+// keeps, per payload value, the value of the shard with the largest key.  On return: key = the
+// cluster's best key of q, bins_n hold qn's cluster statistics after q's AssumePod, H.fmin /
+// H.fflags qn's critical-path minima and flags.  False on abort.
+__device__ __forceinline__ bool spread_argmax_pay(SpreadHdr& H, const SpreadShard& L, int W, int w, int gs,
+                                                  unsigned& epoch, unsigned long long* gran, const XPeers& X, int* err,
+                                                  int parity, long long& key, int kb, int node_base, int lo,
+                                                  const GPod& q, const GPod& qn, int32_t* bins_n, int32_t flags_n,
+                                                  const uint32_t* sw1) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
   int32_t* xs = L.xs;
   const long long r = wave_max_key(key, kb, node_base);
-  int32_t fl[1] = {flags_local};
-  const int opo[1] = {OP_OR};
-  wave_red32(fl, opo);
   if (lane == 0) {
     H.kred[parity][wave] = r;
     H.red[wave][0] = (int32_t)(key_compress(r, kb, node_base) ^ 0x80000000u);
-    H.red[wave][1] = fl[0];
   }
   lds_barrier();
   long long best = H.kred[parity][0];
@@ -1026,41 +1140,40 @@ __device__ __forceinline__ bool spread_argmax_fold(SpreadHdr& H, const SpreadSha
     for (int j = lane; j < np; j += 64) H.payv[j] = cs >= 0 ? fold_payload(L, q, qn, j, cs, sw1[cs]) : 0;
   }
   ++epoch;
-  const int K = 2, ns = qn.total_bins, no = qn.hard_pbins;
-  const unsigned opbits = (unsigned)OP_MAX | ((unsigned)OP_OR << 2);
-  const int M = K + ns + no + np;
-  if (nw == 1 || (long long)W * M <= (long long)KSS_SPREAD_MW_MIN) {
-    if (wave == 0) spread_exchange(H, xs, gran, X, W, w, gs, epoch, err, K, opbits, 0, ns, ns, no, nullptr, 0, 1, 3, np);
+  const int K = 1;
+  const unsigned opbits = (unsigned)OP_MAX;
+  const int M = K + np;
+  if (X.tl && M <= TL_M) {  // two levels (tl_argmax_pay): wave 0, the other waves wait at the barrier
+    if (wave == 0) {
+      uint32_t m = 0;
+      if (tl_argmax_pay(H, X, W, epoch, key_compress(best, kb, node_base), np, err, m) && lane == 0)
+        xs[0] = (int32_t)(m ^ 0x80000000u);
+    }
+  } else if (nw == 1 || (long long)W * M <= (long long)KSS_SPREAD_MW_MIN) {
+    if (wave == 0) spread_exchange(H, xs, gran, X, W, w, gs, epoch, err, K, opbits, 0, 0, 0, 0, nullptr, 0, 1, 3, np);
   } else {
-    if (wave == 0) spread_exchange(H, xs, gran, X, W, w, gs, epoch, err, K, opbits, 0, ns, ns, no, nullptr, 0, 1, 1, np);
+    if (wave == 0) spread_exchange(H, xs, gran, X, W, w, gs, epoch, err, K, opbits, 0, 0, 0, 0, nullptr, 0, 1, 1, np);
     lds_barrier();  // identities in the slots before any wave folds into them
     const int nsw = min(nw, KSS_SPREAD_SWEEP_WAVES);
-    if (wave < nsw) spread_exchange(H, xs, gran, X, W, w, gs, epoch, err, K, opbits, 0, ns, ns, no, nullptr, wave, nsw, 2, np);
+    if (wave < nsw) spread_exchange(H, xs, gran, X, W, w, gs, epoch, err, K, opbits, 0, 0, 0, 0, nullptr, wave, nsw, 2, np);
   }
   lds_barrier();
   if (H.abort) return false;
+  const uint32_t kc = (uint32_t)xs[0] ^ 0x80000000u;
   if (wave == 0) {  // the winner's payloads, then qn's critical paths over the final bins
-    int32_t* bins = xs + G_NS;
+    int32_t fl = 0;
     for (int j = lane; j < np; j += 64) {
       const unsigned long long P = H.pay[j];
       const uint32_t p = (uint32_t)P;
       if (!(P >> 32) || !p) continue;
-      if (qn.n_ipa > 0 && j == np - 1) atomicOr(&xs[1], (int32_t)p);
-      else atomicAdd(&bins[(p >> 16) - 1], (int32_t)(int16_t)(p & 0xFFFFu));
+      if (qn.n_ipa > 0 && j == np - 1) fl |= (int32_t)p;
+      else atomicAdd(&bins_n[(p >> 16) - 1], (int32_t)(int16_t)(p & 0xFFFFu));
     }
-    for (int i = 0; i < qn.n_hard; i++) {
-      const GSpread& sp = qn.sp[i];
-      int32_t m[1] = {INT32_MAX};
-      if (sp.off >= 0 && sp.own == i)
-        for (int b = lane; b < sp.nb; b += 64)
-          if (bins[qn.total_bins + sp.poff + b]) m[0] = min(m[0], bins[sp.off + b]);
-      const int op[1] = {OP_MIN};
-      wave_red32(m, op);
-      if (lane == 0) H.fmin[i] = m[0];
-    }
-    if (lane == 0) H.fflags = xs[1];
+    int32_t f[1] = {fl};
+    const int op[1] = {OP_OR};
+    wave_red32(f, op);
+    fold_minima(H, qn, bins_n, flags_n | f[0]);
   }
-  const uint32_t kc = (uint32_t)xs[0] ^ 0x80000000u;
   lds_barrier();
   key = key_expand(kc, kb, node_base);
   return true;
@@ -1395,30 +1508,36 @@ __device__ __forceinline__ int32_t trace_eff(const SpreadShard& L, const GPod& q
 #endif
 
 // The batch for shard w of one cluster, pods [k0, k1).  res_rows: the resident count rows
-// (class r as r, term r as n_classes + r), n_res of them.  FOLD: spread_argmax_fold compiled in.
-template <bool DEF, bool FOLD>
+// (class r as r, term r as n_classes + r), n_res of them.  FOLD: the next pod's statistics ride with
+// this pod's filter exchange and argmax (spread_argmax_pay).
+template <bool DEF, bool FOLD, bool WIN>
 __device__ __forceinline__ void spread_schedule(const GTrace& tr, DevCluster c, const GPod* __restrict__ gpods,
                                                 const uint32_t* __restrict__ stat, const int32_t* __restrict__ res_rows,
                                                 int n_res, int k0, int k1, int32_t* chosen, PodMeta* meta,
                                                 const kss_profile& prof, int W, int w, int cap, int bins_cap, int gq, int gs,
                                                 unsigned long long* gran, const XPeers& X, unsigned epoch0, int* err,
                                                 unsigned long long* stamps, int nst, const HandoffCheck& hc,
-                                                long long* smem) {
-  const int tid = threadIdx.x, nt = blockDim.x;
+                                                long long* smem, int k_find = 0, int32_t* cursor = nullptr) {
+  const int tid = threadIdx.x, nt = blockDim.x, lane = tid & 63, wave = tid >> 6;
+  // WIN: nextStartNodeIndex for the launch (every shard holds the same value; shard 0 writes it back)
+  int wstart = WIN && cursor && c.N > 0 ? (int)(((long long)ld_ag(cursor) % c.N + c.N) % c.N) : 0;
   SpreadHdr& H = *reinterpret_cast<SpreadHdr*>(smem);
-  const SpreadShard L = spread_view(smem, cap, bins_cap, c.n_keys, n_res, gq, c.n_scalar);
+  const SpreadShard L = spread_view(smem, cap, bins_cap, c.n_keys, n_res, gq, c.n_scalar, FOLD);
   const int nsc = c.n_scalar;
+  // FOLD: pod j's static words in slot j % 3 (its early statistics pass reads pod k + 1's during
+  // pod k) and its bins in area j & 1; otherwise slot j & 1 and one area
+  auto st_slot = [](int j) { return FOLD ? j % 3 : j & 1; };
+  const int bstride = FOLD ? bins_cap : 0;
   const int kb = key_bits(prof, c.N);  // 32-bit selectHost keys when they fit (0: 64-bit, two granules)
   const size_t N = (size_t)c.N;
   const int per = (c.N + W - 1) / W;
   const int lo = min(c.N, w * per), hi = min(c.N, lo + per), own = hi - lo;
   if (k1 <= k0) return;
-  int32_t* bins = L.xs + G_NS;
   // diagnostic phase stamps (KSS_STAMPS_FILE): s_memrealtime into LDS, copied out at the end
   // (no HBM store on the exchange wave while the loop runs)
   unsigned long long* stl =
       stamps ? reinterpret_cast<unsigned long long*>(reinterpret_cast<uint8_t*>(smem) +
-                                                     spread_lds_bytes(cap, bins_cap, c.n_keys, n_res, gq, c.n_scalar))
+                                                     spread_lds_bytes(cap, bins_cap, c.n_keys, n_res, gq, c.n_scalar, FOLD))
              : nullptr;
   if (stl)
     for (int i = tid; i < 16 * nst; i += nt) stl[i] = 0;
@@ -1437,7 +1556,8 @@ __device__ __forceinline__ void spread_schedule(const GTrace& tr, DevCluster c, 
     L.r32[2 * cap + s] = (int32_t)c.node_flags[n];
     for (int k = 0; k < c.n_keys; k++) L.lbl[k * cap + s] = c.label_value[(size_t)k * N + n];
     for (int i = 0; i < nsc; i++) L.sc[(size_t)i * cap + s] = c.alloc[(size_t)(3 + i) * N + n];
-    L.st[(k0 & 1) * cap + s] = ld_ag(&stat[(size_t)lo + s]);
+    L.st[st_slot(k0) * cap + s] = ld_ag(&stat[(size_t)lo + s]);
+    if (FOLD && k0 + 1 < k1) L.st[st_slot(k0 + 1) * cap + s] = ld_ag(&stat[N + (size_t)lo + s]);
   }
   // node state handed over by the previous chunk: loaded, then checked against the sum its
   // epilogue stored (HandoffCheck); loaded again until they agree, a bounded number of times,
@@ -1532,7 +1652,9 @@ __device__ __forceinline__ void spread_schedule(const GTrace& tr, DevCluster c, 
   }
   if (tid == 0) H.abort = 0;
   __syncthreads();  // the first record is in the ring: zero its statistics bins
-  {
+  if (FOLD) {  // both areas (pods k0 and k0 + 1)
+    for (int b = tid; b < 2 * bins_cap; b += nt) L.xs[G_NS + b] = 0;
+  } else {
     const GPod& q0 = *reinterpret_cast<const GPod*>(L.ring + (k0 % 3) * gq);
     if (q0.dyn.status == 0 && q0.need_stats)
       for (int b = tid; b < q0.total_bins + q0.total_pbins; b += nt) L.xs[G_NS + b] = 0;
@@ -1548,7 +1670,7 @@ __device__ __forceinline__ void spread_schedule(const GTrace& tr, DevCluster c, 
     const GPod& q0 = *reinterpret_cast<const GPod*>(L.ring + (k0 % 3) * gq);
     int nz = 0;
     if (q0.dyn.status == 0 && q0.need_stats)
-      for (int b = tid; b < q0.total_bins + q0.total_pbins; b += nt) nz += bins[b] != 0 ? 1 : 0;
+      for (int b = tid; b < q0.total_bins + q0.total_pbins; b += nt) nz += L.xs[G_NS + (k0 & 1) * bstride + b] != 0 ? 1 : 0;
     if (nz) atomicAdd(&tr.words[((size_t)k0 * W + w) * G_TW + GT_PRO], nz);
   }
 #endif
@@ -1570,7 +1692,7 @@ __device__ __forceinline__ void spread_schedule(const GTrace& tr, DevCluster c, 
   for (int j = 0; j < G_PF; j++) pfw[j] = 0;
   unsigned epoch = epoch0;  // granule tags above every tag an earlier launch left (split grids)
   int kparity = 0;
-  bool folded = false;  // this pod's statistics came with the previous pod's argmax (spread_argmax_fold)
+  bool folded = false;  // this pod's statistics came with the previous pod's exchanges (spread_argmax_pay)
   for (int k = k0; k < k1; k++) {
 #define GSTAMP(i)                                                                      \
   do {                                                                                 \
@@ -1578,11 +1700,15 @@ __device__ __forceinline__ void spread_schedule(const GTrace& tr, DevCluster c, 
   } while (0)
     GSTAMP(0);
     const GPod& q = *reinterpret_cast<const GPod*>(L.ring + (k % 3) * gq);
-    const uint32_t* sw = L.st + (k & 1) * cap;
-    // prefetch (every wave but wave 0): record of pod k+2, static words of pod k+1.  The
-    // branch is wave-uniform and the loads inside it unconditional (clamped indices).  A
+    const uint32_t* sw = L.st + st_slot(k) * cap;
+    int32_t* bins = L.xs + G_NS + (k & 1) * bstride;  // this pod's histogram / presence bins
+    const int boff = (k & 1) * bstride;                // ... as spread_reduce's offsets
+    // prefetch (every wave but wave 0): record of pod k+2, static words of pod k+1 (FOLD: k+2).
+    // The branch is wave-uniform and the loads inside it unconditional (clamped indices).  A
     // shard without nodes still takes every record: its exchanges follow the programs.
+    const int pfs = FOLD ? k + 2 : k + 1;  // the pod whose static words this pod prefetches
     const bool pf_on = pf_wave && k + 1 < k1;
+    const bool pfs_on = pf_wave && pfs < k1;
     if (pf_on) {
       if (k + 2 < k1) {
         KSS_GLOBAL const uint4* src = ggq + (size_t)(k + 2) * gq;
@@ -1591,9 +1717,11 @@ __device__ __forceinline__ void spread_schedule(const GTrace& tr, DevCluster c, 
         pfq0 = make_uint4(a.x, a.y, a.z, a.w);
         pfq1 = make_uint4(b.x, b.y, b.z, b.w);
       }
+    }
+    if (pfs_on) {
 #pragma unroll
       for (int j = 0; j < G_PF; j++)
-        if (j < pf_per) pfw[j] = ld_ag(&gstat[(size_t)(k + 1 - k0) * N + lo + min(j * pf_n + pf_lane, own - 1)]);
+        if (j < pf_per) pfw[j] = ld_ag(&gstat[(size_t)(pfs - k0) * N + lo + min(j * pf_n + pf_lane, own - 1)]);
     }
     PodMeta m;
     m.chosen = -1;
@@ -1652,8 +1780,8 @@ __device__ __forceinline__ void spread_schedule(const GTrace& tr, DevCluster c, 
       v[MAXH] = flags;
       // histogram SUM over every bin, hard-pair presence OR (soft presence, still zero, is
       // filled by the filter pass), then the critical-path minima
-      if (!spread_reduce(H, L.xs, W, w, gs, epoch, gran, X, err, v, op, 0, q.total_bins, q.total_bins, q.hard_pbins, false,
-                         nullptr, &q))
+      if (!spread_reduce(H, L.xs, W, w, gs, epoch, gran, X, err, v, op, boff, q.total_bins, boff + q.total_bins, q.hard_pbins,
+                         false, nullptr, &q))
         return;
 #pragma unroll
       for (int i = 0; i < MAXH; i++) hard_min[i] = v[i];
@@ -1668,6 +1796,13 @@ __device__ __forceinline__ void spread_schedule(const GTrace& tr, DevCluster c, 
 #endif
       GSTAMP(2);
     }
+    // pod k+1: its record, static words and bins area (FOLD: its statistics ride with this pod)
+    const GPod& qn = *reinterpret_cast<const GPod*>(L.ring + ((k + 1) % 3) * gq);
+    const uint32_t* sw1 = L.st + st_slot(k + 1) * cap;
+    int32_t* bins_n = L.xs + G_NS + ((k + 1) & 1) * bstride;
+    const int boffn = ((k + 1) & 1) * bstride;
+    bool fold_next = false;
+    int32_t flags_n = 0;
     // ---- filter + raw scores ----
     const bool has_soft = q.n_soft > 0, has_ipa = q.n_ipa > 0;
     const bool one_soft = q.n_soft == 1;
@@ -1676,6 +1811,58 @@ __device__ __forceinline__ void spread_schedule(const GTrace& tr, DevCluster c, 
     int32_t nf = 0, nign = 0, max_tt = 0, max_na = 0, ipa_min = INT32_MAX, ipa_max = INT32_MIN, smissing = 0;
     int32_t sdirect[MAXS] = {0, 0, 0, 0};
     int32_t cmin = INT32_MAX, cmax = INT32_MIN, lacks = 0;
+    // a kept feasible node's part of the filter exchange's statistics (every feasible node; under
+    // the window the nodes the search keeps, after the count exchange); returns the node's
+    // "ignored" bit (PodTopologySpread PreScore IgnoredNodes)
+    auto keep = [&](int s, uint32_t wd, int32_t tt, int32_t na, int64_t ipa) -> int {
+      nf++;
+      max_tt = tt > max_tt ? tt : max_tt;
+      max_na = na > max_na ? na : max_na;
+      if (has_ipa) {
+        ipa_min = (int32_t)min((int64_t)ipa_min, ipa);
+        ipa_max = (int32_t)max((int64_t)ipa_max, ipa);
+      }
+      if (!has_soft) return 0;
+      if ((q.pflags & KSS_POD_PTS_REQUIRE_ALL) && !g_has_keys(L, soft, q.n_soft, s)) {
+        nign++;
+        return 1;
+      }
+      for (int i = 0; i < q.n_soft; i++) {
+        const GSpread& sp = soft[i];
+        int d = L.lbl[sp.key * cap + s];
+        if (sp.mode == SOFT_DIRECT) {
+          if (d >= 0) sdirect[i]++;
+          else smissing |= 1 << i;
+        } else if (sp.mode == SOFT_HIST) {
+          if (d < 0) d = sp.empty;
+          bins[q.total_bins + sp.poff + d] = 1;
+        }
+      }
+      if (one_soft) {  // the count the node's PodTopologySpread raw score is monotone in
+        const GSpread& sp = soft[0];
+        const int d = L.lbl[sp.key * cap + s];
+        int32_t cnt = -1;
+        if (d >= 0) {
+          if (sp.mode == SOFT_HOST) cnt = g_sum(L, q, sp.ri_off, sp.ri_len, s);
+          else if (sp.mode == SOFT_DIRECT) cnt = g_policy(sp, wd) ? g_sum(L, q, sp.ri_off, sp.ri_len, s) : 0;
+          else cnt = bins[sp.off + d];
+        }
+        L.scnt[s] = cnt;
+        if (cnt < 0) {
+          lacks = 1;
+        } else {
+          cmin = min(cmin, cnt);
+          cmax = max(cmax, cnt);
+        }
+      }
+      return 0;
+    };
+    // WIN: percentageOfNodesToScore < 100 (findNodesThatPassFilters' window, Parallelism = 1 order
+    // from nextStartNodeIndex wstart): the statistics cover the first k_find feasible nodes only
+    const bool win = WIN && evaluated && k_find < c.N;
+    int it = 0, wstop = -1;  // window: loop iteration; the stopping node (the (k_find + 1)-th feasible)
+    if (WIN && win && lane == 0)
+      for (int i = 0; i < G_PF; i++) H.wc[i][wave] = H.wb[i][wave] = 0;
     if (evaluated) {
       const SPod qd = q.dyn;  // in registers: the loop's LDS stores would make every field a reload
       for (int s = tid; s < own; s += nt) {
@@ -1701,78 +1888,161 @@ __device__ __forceinline__ void spread_schedule(const GTrace& tr, DevCluster c, 
           e.f = KSS_F_INTER_POD_AFFINITY;
         int ign = 0;
         if (e.f == 0) {
-          nf++;
-          max_tt = e.tt > max_tt ? e.tt : max_tt;
-          max_na = e.na > max_na ? e.na : max_na;
-          int64_t ipa = 0;
-          if (has_ipa) {
-            ipa = g_ipa_score(L, q, bins, s);
-            ipa_min = (int32_t)min((int64_t)ipa_min, ipa);
-            ipa_max = (int32_t)max((int64_t)ipa_max, ipa);
-          }
+          const int64_t ipa = has_ipa ? g_ipa_score(L, q, bins, s) : 0;
           L.stt[s] = e.tt;
           L.sna[s] = e.na;
           L.sfit[s] = e.fit;
           L.sba[s] = e.ba;
           L.sipa[s] = ipa;
-          if (has_soft) {
-            if ((q.pflags & KSS_POD_PTS_REQUIRE_ALL) && !g_has_keys(L, soft, q.n_soft, s)) {
-              nign++;
-              ign = 1;
-            } else {
-              for (int i = 0; i < q.n_soft; i++) {
-                const GSpread& sp = soft[i];
-                int d = L.lbl[sp.key * cap + s];
-                if (sp.mode == SOFT_DIRECT) {
-                  if (d >= 0) sdirect[i]++;
-                  else smissing |= 1 << i;
-                } else if (sp.mode == SOFT_HIST) {
-                  if (d < 0) d = sp.empty;
-                  bins[q.total_bins + sp.poff + d] = 1;
-                }
-              }
-              if (one_soft) {  // the count the node's PodTopologySpread raw score is monotone in
-                const GSpread& sp = soft[0];
-                const int d = L.lbl[sp.key * cap + s];
-                int32_t cnt = -1;
-                if (d >= 0) {
-                  if (sp.mode == SOFT_HOST) cnt = g_sum(L, q, sp.ri_off, sp.ri_len, s);
-                  else if (sp.mode == SOFT_DIRECT) cnt = g_policy(sp, wd) ? g_sum(L, q, sp.ri_off, sp.ri_len, s) : 0;
-                  else cnt = bins[sp.off + d];
-                }
-                L.scnt[s] = cnt;
-                if (cnt < 0) {
-                  lacks = 1;
-                } else {
-                  cmin = min(cmin, cnt);
-                  cmax = max(cmax, cnt);
-                }
-              }
-            }
-          }
+          if (!win) ign = keep(s, wd, e.tt, e.na, ipa);
         }
         L.sf[s] = e.f | (ign << 16);
+        if (WIN && win) {  // the window's shard-local prefix: feasible slots per (iteration, wave)
+          const unsigned long long bf = __ballot(e.f == 0), bb = __ballot(e.f == 0 && lo + s < wstart);
+          if (lane == 0) {
+            H.wc[it][wave] = __popcll(bf);
+            H.wb[it][wave] = __popcll(bb);
+          }
+          ++it;
+        }
       }
       GSTAMP(3);
+      if (WIN && win) {
+        // the count exchange: every shard's feasible count (W SUM values behind the pod's bins:
+        // this shard's at index w) and the feasible nodes of the start shard before the start node
+        lds_barrier();  // the (iteration, wave) counts
+        const int nwv = nt >> 6, nit = (own + nt - 1) / nt;
+        int32_t cw = 0, cb = 0;
+        for (int i = 0; i < nit; i++)
+          for (int x = 0; x < nwv; x++) {
+            cw += H.wc[i][x];
+            cb += H.wb[i][x];
+          }
+        const int wo = boff + q.total_bins + q.total_pbins;
+        for (int x = tid; x < W; x += nt) L.xs[G_NS + wo + x] = x == w ? cw : 0;
+        // (only the start shard's: the shards wholly before the start node are parts b entirely)
+        int32_t vb[1] = {tid == 0 && w == min(wstart / max(per, 1), W - 1) ? cb : 0};
+        const int opb[1] = {OP_SUM};
+        if (!spread_reduce(H, L.xs, W, w, gs, epoch, gran, X, err, vb, opb, wo, W, 0, 0, false, nullptr)) return;
+        // visiting order: the shards' parts a (nodes >= wstart) in shard order, then their parts b
+        if (tid < 64) {
+          const int per_ = max(per, 1), ws = min(wstart / per_, W - 1);
+          int32_t acc[3] = {0, 0, 0};  // parts a before this shard, all parts a, parts b before this shard
+          for (int v = lane; v < W; v += 64) {
+            const int32_t cv = L.xs[G_NS + wo + v];
+            const int32_t av = v < ws ? 0 : (v == ws ? cv - vb[0] : cv), bv = v < ws ? cv : (v == ws ? vb[0] : 0);
+            acc[0] += v < w ? av : 0;
+            acc[1] += av;
+            acc[2] += v < w ? bv : 0;
+          }
+          const int op3[3] = {OP_SUM, OP_SUM, OP_SUM};
+          wave_red32(acc, op3);
+          if (lane == 0) {
+            H.wsum[0] = acc[0];
+            H.wsum[1] = acc[1];
+            H.wsum[2] = acc[2];
+          }
+        }
+        lds_barrier();
+        const int32_t a_before = H.wsum[0], a_tot = H.wsum[1], b_before = H.wsum[2];
+        // kept pass: Fb(n) = the feasible nodes before n in visiting order; kept iff Fb < k_find,
+        // the feasible node with Fb = k_find stops the search (filtered, not kept)
+        int pre_w = 0;  // feasible slots of this shard before iteration i's wave
+        for (int i = 0; i < nit; i++) {
+          int before_i = 0;
+          for (int x = 0; x < nwv; x++) before_i += (x < wave ? H.wc[i][x] : 0);
+          const int s = tid + i * nt;
+          const bool f = s < own && (L.sf[s] & 0xFFFF) == KSS_F_PASS;
+          const unsigned long long bf = __ballot(f);
+          const int g = pre_w + before_i + __popcll(bf & ((1ull << lane) - 1ull));
+          if (f) {
+            const int n = lo + s;
+            const int fb = n < wstart ? a_tot + b_before + g : a_before + g - cb;
+            if (fb < k_find) {
+              if (keep(s, sw[s], L.stt[s], L.sna[s], L.sipa[s])) L.sf[s] |= 1 << 16;
+            } else {
+              L.sf[s] = 0xFFFF;  // filtered and passed, but not in the feasible list
+              if (fb == k_find) wstop = n;
+            }
+          }
+          for (int x = 0; x < nwv; x++) pre_w += H.wc[i][x];
+        }
+#if KSS_SPREAD_TRACE
+        if (tid == 0) {
+          tw[GT_WIN] = cw;
+          tw[GT_WIN + 1] = cb;
+          tw[GT_WIN + 2] = vb[0];
+          tw[GT_WIN + 3] = a_before;
+          tw[GT_WIN + 4] = a_tot;
+          tw[GT_WIN + 5] = b_before;
+          tw[GT_WIN + 8] = wstart;
+        }
+        if (wstop >= 0) atomicMax(&tw[GT_WIN + 6], wstop + 1);
+        atomicAdd(&tw[GT_WIN + 7], nf);
+#endif
+      }
+      // FOLD: pod k+1's statistics pass on the state before this pod's AssumePod (H0), into its
+      // own bins area; they ride with this pod's filter exchange, and the winner's change to them
+      // with the argmax (spread_argmax_pay).  Pods whose DoNotSchedule group is node-valued keep
+      // their own statistics exchange (GPod::fold, build_gpods).
+      if (FOLD) {
+        fold_next = W > 1 && kb > 0 && k + 1 < k1 && qn.dyn.status == 0 && qn.need_stats && qn.fold;
+        if (fold_next) {
+          int32_t hmin_n[MAXH];
+#pragma unroll
+          for (int i = 0; i < MAXH; i++) hmin_n[i] = INT32_MAX;
+          for (int s = tid; s < own; s += nt) stats_node(L, qn, s, sw1[s], bins_n, hmin_n, flags_n);
+        }
+      }
       // one exchange: feasible count, normalisation maxima, IPA extrema, PTS sizes / extrema.
       // A pod without ScheduleAnyway constraints and inter-pod terms (C4's zone spread) needs
       // only the first three: the other ten stay at their identities on every shard, so they
       // are not exchanged (a quarter of the granules each shard sweeps).
       unsigned long long* est = stl && k - k0 < nst ? stl + (k - k0) * 16 + 10 : nullptr;
-      if (!has_soft && !has_ipa) {
-        int32_t v[3] = {nf, max_tt, max_na};
-        const int op[3] = {OP_SUM, OP_MAX, OP_MAX};
+      const int nsn = fold_next ? qn.total_bins : 0, non = fold_next ? qn.hard_pbins : 0;  // pod k+1's H0
+      if (WIN && !has_soft && !has_ipa) {
+        int32_t v[4] = {nf, max_tt, max_na, wstop};
+        const int op[4] = {OP_SUM, OP_MAX, OP_MAX, OP_MAX};
         if (!spread_reduce(H, L.xs, W, w, gs, epoch, gran, X, err, v, op, 0, 0, 0, 0, false, est)) return;
         nf = v[0];
         max_tt = v[1];
         max_na = v[2];
+        wstop = v[3];
+      } else if (!has_soft && !has_ipa) {
+        if constexpr (FOLD) {
+          int32_t v[4] = {nf, max_tt, max_na, flags_n};
+          const int op[4] = {OP_SUM, OP_MAX, OP_MAX, OP_OR};
+          if (!spread_reduce(H, L.xs, W, w, gs, epoch, gran, X, err, v, op, boffn, nsn, boffn + qn.total_bins, non, false,
+                             est))
+            return;
+          nf = v[0];
+          max_tt = v[1];
+          max_na = v[2];
+          flags_n = v[3];
+        } else {
+          int32_t v[3] = {nf, max_tt, max_na};
+          const int op[3] = {OP_SUM, OP_MAX, OP_MAX};
+          if (!spread_reduce(H, L.xs, W, w, gs, epoch, gran, X, err, v, op, 0, 0, 0, 0, false, est)) return;
+          nf = v[0];
+          max_tt = v[1];
+          max_na = v[2];
+        }
       } else {
-        int32_t v[13] = {nf, nign, max_tt, max_na, ipa_min, ipa_max, smissing | (lacks << 30), sdirect[0], sdirect[1],
+        constexpr int KV = FOLD || WIN ? 14 : 13;
+        int32_t v[KV] = {nf, nign, max_tt, max_na, ipa_min, ipa_max, smissing | (lacks << 30), sdirect[0], sdirect[1],
                          sdirect[2], sdirect[3], cmin, cmax};
-        const int op[13] = {OP_SUM, OP_SUM, OP_MAX, OP_MAX, OP_MIN, OP_MAX, OP_OR, OP_SUM, OP_SUM, OP_SUM, OP_SUM,
-                            OP_MIN, OP_MAX};
-        if (!spread_reduce(H, L.xs, W, w, gs, epoch, gran, X, err, v, op, 0, 0, q.total_bins + q.hard_pbins,
-                           q.total_pbins - q.hard_pbins, false, est))
+        int op[KV] = {OP_SUM, OP_SUM, OP_MAX, OP_MAX, OP_MIN, OP_MAX, OP_OR, OP_SUM, OP_SUM, OP_SUM, OP_SUM,
+                      OP_MIN, OP_MAX};
+        if (FOLD) {
+          v[KV - 1] = flags_n;
+          op[KV - 1] = OP_OR;
+        }
+        if (WIN) {  // (never together with FOLD)
+          v[KV - 1] = wstop;
+          op[KV - 1] = OP_MAX;
+        }
+        if (!spread_reduce(H, L.xs, W, w, gs, epoch, gran, X, err, v, op, boffn, nsn, boff + q.total_bins + q.hard_pbins,
+                           q.total_pbins - q.hard_pbins, false, est, nullptr, boffn + qn.total_bins, non))
           return;
         nf = v[0];
         nign = v[1];
@@ -1786,15 +2056,20 @@ __device__ __forceinline__ void spread_schedule(const GTrace& tr, DevCluster c, 
         for (int i = 0; i < MAXS; i++) sdirect[i] = v[7 + i];
         cmin = v[11];
         cmax = v[12];
+        if (FOLD) flags_n = v[KV - 1];
+        if (WIN) wstop = v[KV - 1];
       }
+      // nextStartNodeIndex: the stopping node, or unchanged when every node was processed
+      if (WIN && win && wstop >= 0) wstart = wstop;
       GSTAMP(4);
       m.n_feasible = nf;
       if (nf == 0) {
         m.status = 1;
         evaluated = false;
+        // no AssumePod: pod k+1's exchanged statistics are final
+        if (FOLD && fold_next && tid < 64) fold_minima(H, qn, bins_n, flags_n);
       }
     }
-    bool fold_next = false;
     if (evaluated) {
       const bool scored = nf > 1;  // a single feasible node is selected without scoring
       // ---- PodTopologySpread PreScore sizes + Score ----
@@ -1870,25 +2145,6 @@ __device__ __forceinline__ void spread_schedule(const GTrace& tr, DevCluster c, 
           GSTAMP(6);
         }
       }
-      // ---- pod k+1's statistics, published with this pod's key (spread_argmax_fold) ----
-      // (this pod's passes no longer read the bins: the last reads were behind E2 / E3's barriers)
-      const GPod& qn = *reinterpret_cast<const GPod*>(L.ring + ((k + 1) % 3) * gq);
-      const uint32_t* sw1 = L.st + ((k + 1) & 1) * cap;
-      fold_next = FOLD && W > 1 && kb > 0 && k + 1 < k1 && qn.dyn.status == 0 && qn.need_stats && qn.fold;
-      int32_t flags_n = 0;
-      if (fold_next) {
-        if (pf_on) {  // pod k+1's static words, prefetched into registers at this pod's start
-#pragma unroll
-          for (int j = 0; j < G_PF; j++)
-            if (j < pf_per) L.st[((k + 1) & 1) * cap + min(j * pf_n + pf_lane, own - 1)] = pfw[j];
-        }
-        for (int b = tid; b < qn.total_bins + qn.total_pbins; b += nt) bins[b] = 0;
-        lds_barrier();
-        int32_t hmin_n[MAXH];
-#pragma unroll
-        for (int i = 0; i < MAXH; i++) hmin_n[i] = INT32_MAX;
-        for (int s = tid; s < own; s += nt) stats_node(L, qn, s, sw1[s], bins, hmin_n, flags_n);
-      }
       // ---- NormalizeScore + weights + selectHost ----
       const bool ipa_norm = (flags & 8) != 0;
       const int64_t ipa_diff = (int64_t)ipa_max - (int64_t)ipa_min;
@@ -1937,8 +2193,8 @@ __device__ __forceinline__ void spread_schedule(const GTrace& tr, DevCluster c, 
         best = key > best ? key : best;
       }
       GSTAMP(7);
-      if (fold_next ? !spread_argmax_fold(H, L, W, w, gs, epoch, gran, X, err, kparity, best, kb, c.node_base, lo, q, qn,
-                                          flags_n, sw1)
+      if (fold_next ? !spread_argmax_pay(H, L, W, w, gs, epoch, gran, X, err, kparity, best, kb, c.node_base, lo, q, qn,
+                                         bins_n, flags_n, sw1)
                     : !spread_argmax(H, W, w, gs, epoch, gran, X, err, kparity, best, kb, c.node_base))
         return;
       GSTAMP(8);
@@ -2023,22 +2279,24 @@ __device__ __forceinline__ void spread_schedule(const GTrace& tr, DevCluster c, 
         if (q.cmt[i] >= 0) L.cnt[q.cmt[i] * cap + s] += 1;
     }
     // ---- prefetched data of pods k+1 / k+2 -> their LDS slots ----
-    if (pf_on) {
-      if (k + 2 < k1) {  // lanes past the end rewrite the last uint4 with its own value
-        uint4* dst = L.ring + ((k + 2) % 3) * gq;
-        dst[min(pf_lane, gq - 1)] = pfq0;
-        dst[min(pf_lane + pf_n, gq - 1)] = pfq1;
-      }
+    if (pf_on && k + 2 < k1) {  // lanes past the end rewrite the last uint4 with its own value
+      uint4* dst = L.ring + ((k + 2) % 3) * gq;
+      dst[min(pf_lane, gq - 1)] = pfq0;
+      dst[min(pf_lane + pf_n, gq - 1)] = pfq1;
+    }
+    if (pfs_on) {
 #pragma unroll
       for (int j = 0; j < G_PF; j++)
-        if (j < pf_per) L.st[((k + 1) & 1) * cap + min(j * pf_n + pf_lane, own - 1)] = pfw[j];
+        if (j < pf_per) L.st[st_slot(pfs) * cap + min(j * pf_n + pf_lane, own - 1)] = pfw[j];
     }
     // the statistics bins of pod k+1, zeroed ahead of the barrier that ends this pod (its
     // passes no longer read them): its stats pass then starts without a barrier of its own
-    if (k + 1 < k1 && !fold_next) {  // (folded: they hold its exchanged statistics)
-      const GPod& qn = *reinterpret_cast<const GPod*>(L.ring + ((k + 1) % 3) * gq);
-      if (qn.dyn.status == 0 && qn.need_stats)
-        for (int b = tid; b < qn.total_bins + qn.total_pbins; b += nt) bins[b] = 0;
+    // (FOLD: this pod's own area, for pod k+2; pod k+1's area holds its statistics when folded,
+    // and was zeroed at the end of pod k-1 when not)
+    if (FOLD) {
+      for (int b = tid; b < bins_cap; b += nt) bins[b] = 0;
+    } else if (k + 1 < k1 && qn.dyn.status == 0 && qn.need_stats) {
+      for (int b = tid; b < qn.total_bins + qn.total_pbins; b += nt) bins[b] = 0;
     }
     folded = fold_next;
     lds_barrier();
@@ -2046,6 +2304,7 @@ __device__ __forceinline__ void spread_schedule(const GTrace& tr, DevCluster c, 
 #undef GSTAMP
   }
   // node state and the resident count rows back to HBM
+  if (WIN && cursor && w == 0 && tid == 0) *cursor = wstart;  // stream order: the next launch reads it
   __syncthreads();
   if (stl)
     for (int i = tid; i < 16 * nst; i += nt) stamps[(size_t)w * 8 * KSS_NSTAMP_PODS + i] = stl[i];

@@ -49,8 +49,9 @@ def test_refusal_names_pod_and_reason():
 
 def test_profile_aware_plan():
     """kss_plan_podset_ex: percentageOfNodesToScore below 100 on 100+ nodes (the window) keeps
-    k_simple for pods without a PreFilterResult list (simple_sync_win) and rules out k_spread and
-    name-listed pods; a profile that scores an extended resource the cluster has rules out both
+    k_simple for pods without a PreFilterResult list (simple_sync_win) and k_spread under the
+    default profile (spread_schedule WIN), and rules out name-listed pods and k_spread under a
+    custom profile; a profile that scores an extended resource the cluster has rules out both
     loop kernels; otherwise it answers as kss_plan_podset."""
     s = native.Synth(2, 0, 500, 50)
     assert native.plan_podset(s.cluster, s.pods)["kernel"] == "k_simple"
@@ -62,13 +63,18 @@ def test_profile_aware_plan():
     p = abi.default_profile()
     p.pct_nodes_to_score = 0
     assert native.plan_podset(small.cluster, small.pods, p)["kernel"] == "k_simple"
-    # programs (k_spread) and PreFilterResult node lists keep the window on k_schedule
+    # programs keep k_spread under the default profile; a custom profile and PreFilterResult node
+    # lists keep the window on k_schedule
     from kss import synth
     from test_oracle_crosscheck import with_name_sets
     nodes, bound, pods = synth.make_cluster(3, 300, 40)
     cc, cp, _ = compile_cluster(nodes, bound, pods)
     assert native.plan_podset(cc.as_struct(), cp.as_struct())["kernel"] == "k_spread"
-    r = native.plan_podset(cc.as_struct(), cp.as_struct(), p)
+    assert native.plan_podset(cc.as_struct(), cp.as_struct(), p)["kernel"] == "k_spread"
+    pc = abi.default_profile()
+    pc.pct_nodes_to_score = 0
+    pc.weight[abi.KSS_S_TAINT_TOLERATION] = 5
+    r = native.plan_podset(cc.as_struct(), cp.as_struct(), pc)
     assert r["kernel"] == "k_schedule" and "percentageOfNodesToScore" in r["reason"], r
     nodes, bound, pods = synth.make_cluster(2, 300, 40)
     pods = with_name_sets(pods, [n["metadata"]["name"] for n in nodes], every=5, size=120)
