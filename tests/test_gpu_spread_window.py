@@ -5,7 +5,7 @@ afterwards, kss_oracle.c).  Chosen nodes, per-pod outcomes (n_feasible = the kep
 final node and count state, and nextStartNodeIndex.
 
   * the C3 recipe at 5,000 nodes (K = 500 adaptive, 1,500 at 30 %) on the XCD-local grid (32
-    shards), unrestricted, on nine shards, and across chunk launches (the cursor handed on through
+    shards), unrestricted, on 24 shards, and across chunk launches (the cursor handed on through
     the device word), from a set cursor, two runs each;
   * C4's recipe at 20,000 nodes (448-lane shards, the 512-lane kernel; more than 64 shards: the
     two-level selectHost exchange);
@@ -66,7 +66,7 @@ def test_c3_window_geometries(pct, geometry):
     if geometry == "unrestricted":
         native.set_option("xcd", 0)
     elif geometry == "few_shards":
-        native.set_option("shards", 9)
+        native.set_option("shards", 24)
     elif geometry == "chunks":
         native.set_option("static_bytes", 4 * n_nodes * 150)
     ctx = native.Context(prof)
@@ -78,7 +78,7 @@ def test_c3_window_geometries(pct, geometry):
         chosen = ctx.run_staged(n_pods)
         assert ctx.last_kernel() == "k_spread", rep
         if geometry == "few_shards":
-            assert ctx.last_geometry()["shards"] == 9
+            assert ctx.last_geometry()["shards"] == 24
         if geometry == "chunks":
             assert ctx.last_timing()[1] >= 2 * 5
         _check(ctx, chosen, ch_o, res, st, n_pods, n_nodes, ncl, nt)
@@ -104,6 +104,18 @@ def test_c4_recipe_window():
     ctx.close()
 
 
+def _no_name_lists(pods):
+    """matchFields metadata.name In (a PreFilterResult node list: the window then takes k_schedule)
+    turned into NotIn, so the fuzz batch stays on k_spread."""
+    for p in pods:
+        na = p.get("spec", {}).get("affinity", {}).get("nodeAffinity", {})
+        for t in na.get("requiredDuringSchedulingIgnoredDuringExecution", {}).get("nodeSelectorTerms", []):
+            for f in t.get("matchFields", []):
+                if f.get("key") == "metadata.name" and f.get("operator") == "In":
+                    f["operator"] = "NotIn"
+    return pods
+
+
 @pytest.mark.parametrize("shards", [2, 9])
 @pytest.mark.parametrize("pct", [0, 40])
 def test_program_fuzz_window(shards, pct):
@@ -111,6 +123,7 @@ def test_program_fuzz_window(shards, pct):
     on_spread = 0
     for seed in (20, 21, 22, 51):
         nodes, bound, pods = progfuzz.make(seed, 211, 150)
+        pods = _no_name_lists(pods)
         cc, cp, _ = compile_cluster(nodes, bound, pods)
         ncl, nt = len(cc.classes), len(cc.terms)
         ch_o, res, st = oracle_c.schedule(prof, cc.as_struct(), cp.as_struct(), cp.n, cc.n_nodes, record="meta",
