@@ -1887,14 +1887,62 @@ __device__ __forceinline__ void spread_schedule(const GTrace& tr, DevCluster c, 
         if (e.f == 0 && ((en >> KSS_F_INTER_POD_AFFINITY) & 1u) && has_ipa && g_filter_ipa(L, q, bins, flags, s))
           e.f = KSS_F_INTER_POD_AFFINITY;
         int ign = 0;
-        if (e.f == 0) {
-          const int64_t ipa = has_ipa ? g_ipa_score(L, q, bins, s) : 0;
+        if (WIN && win && e.f == 0) {  // the window: stored, accumulated by the kept pass
+          L.stt[s] = e.tt;
+          L.sna[s] = e.na;
+          L.sfit[s] = e.fit;
+          L.sba[s] = e.ba;
+          L.sipa[s] = has_ipa ? g_ipa_score(L, q, bins, s) : 0;
+        } else if (e.f == 0) {  // (keep()'s accumulation, written out: the default kernel's registers)
+          nf++;
+          max_tt = e.tt > max_tt ? e.tt : max_tt;
+          max_na = e.na > max_na ? e.na : max_na;
+          int64_t ipa = 0;
+          if (has_ipa) {
+            ipa = g_ipa_score(L, q, bins, s);
+            ipa_min = (int32_t)min((int64_t)ipa_min, ipa);
+            ipa_max = (int32_t)max((int64_t)ipa_max, ipa);
+          }
           L.stt[s] = e.tt;
           L.sna[s] = e.na;
           L.sfit[s] = e.fit;
           L.sba[s] = e.ba;
           L.sipa[s] = ipa;
-          if (!win) ign = keep(s, wd, e.tt, e.na, ipa);
+          if (has_soft) {
+            if ((q.pflags & KSS_POD_PTS_REQUIRE_ALL) && !g_has_keys(L, soft, q.n_soft, s)) {
+              nign++;
+              ign = 1;
+            } else {
+              for (int i = 0; i < q.n_soft; i++) {
+                const GSpread& sp = soft[i];
+                int d = L.lbl[sp.key * cap + s];
+                if (sp.mode == SOFT_DIRECT) {
+                  if (d >= 0) sdirect[i]++;
+                  else smissing |= 1 << i;
+                } else if (sp.mode == SOFT_HIST) {
+                  if (d < 0) d = sp.empty;
+                  bins[q.total_bins + sp.poff + d] = 1;
+                }
+              }
+              if (one_soft) {  // the count the node's PodTopologySpread raw score is monotone in
+                const GSpread& sp = soft[0];
+                const int d = L.lbl[sp.key * cap + s];
+                int32_t cnt = -1;
+                if (d >= 0) {
+                  if (sp.mode == SOFT_HOST) cnt = g_sum(L, q, sp.ri_off, sp.ri_len, s);
+                  else if (sp.mode == SOFT_DIRECT) cnt = g_policy(sp, wd) ? g_sum(L, q, sp.ri_off, sp.ri_len, s) : 0;
+                  else cnt = bins[sp.off + d];
+                }
+                L.scnt[s] = cnt;
+                if (cnt < 0) {
+                  lacks = 1;
+                } else {
+                  cmin = min(cmin, cnt);
+                  cmax = max(cmax, cnt);
+                }
+              }
+            }
+          }
         }
         L.sf[s] = e.f | (ign << 16);
         if (WIN && win) {  // the window's shard-local prefix: feasible slots per (iteration, wave)
@@ -2031,16 +2079,13 @@ __device__ __forceinline__ void spread_schedule(const GTrace& tr, DevCluster c, 
         constexpr int KV = FOLD || WIN ? 14 : 13;
         int32_t v[KV] = {nf, nign, max_tt, max_na, ipa_min, ipa_max, smissing | (lacks << 30), sdirect[0], sdirect[1],
                          sdirect[2], sdirect[3], cmin, cmax};
-        int op[KV] = {OP_SUM, OP_SUM, OP_MAX, OP_MAX, OP_MIN, OP_MAX, OP_OR, OP_SUM, OP_SUM, OP_SUM, OP_SUM,
-                      OP_MIN, OP_MAX};
-        if (FOLD) {
-          v[KV - 1] = flags_n;
-          op[KV - 1] = OP_OR;
-        }
-        if (WIN) {  // (never together with FOLD)
-          v[KV - 1] = wstop;
-          op[KV - 1] = OP_MAX;
-        }
+        // the 14th scalar: pod k+1's flags (FOLD) or the window's stopping node (WIN; never both);
+        // the operators stay a constant array (a written one is a private array in scratch)
+        const int op14[14] = {OP_SUM, OP_SUM, OP_MAX, OP_MAX, OP_MIN, OP_MAX, OP_OR, OP_SUM, OP_SUM, OP_SUM, OP_SUM,
+                              OP_MIN, OP_MAX, FOLD ? OP_OR : OP_MAX};
+        const int(&op)[KV] = *reinterpret_cast<const int(*)[KV]>(op14);
+        if (FOLD) v[KV - 1] = flags_n;
+        if (WIN) v[KV - 1] = wstop;
         if (!spread_reduce(H, L.xs, W, w, gs, epoch, gran, X, err, v, op, boffn, nsn, boff + q.total_bins + q.hard_pbins,
                            q.total_pbins - q.hard_pbins, false, est, nullptr, boffn + qn.total_bins, non))
           return;
@@ -2295,8 +2340,10 @@ __device__ __forceinline__ void spread_schedule(const GTrace& tr, DevCluster c, 
     // and was zeroed at the end of pod k-1 when not)
     if (FOLD) {
       for (int b = tid; b < bins_cap; b += nt) bins[b] = 0;
-    } else if (k + 1 < k1 && qn.dyn.status == 0 && qn.need_stats) {
-      for (int b = tid; b < qn.total_bins + qn.total_pbins; b += nt) bins[b] = 0;
+    } else if (k + 1 < k1) {  // (the record again, not qn: a pointer live across the pod costs registers)
+      const GPod& qz = *reinterpret_cast<const GPod*>(L.ring + ((k + 1) % 3) * gq);
+      if (qz.dyn.status == 0 && qz.need_stats)
+        for (int b = tid; b < qz.total_bins + qz.total_pbins; b += nt) bins[b] = 0;
     }
     folded = fold_next;
     lds_barrier();
