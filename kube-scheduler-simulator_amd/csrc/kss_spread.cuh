@@ -786,7 +786,9 @@ __device__ __forceinline__ bool spread_reduce(SpreadHdr& H, int32_t* xs, int W, 
                                               unsigned long long* gran, const XPeers& X, int* err, int32_t (&v)[K],
                                               const int (&ops)[K], int sum_lo = 0, int ns = 0, int or_lo = 0,
                                               int no = 0, bool local = false, unsigned long long* sp = nullptr,
-                                              const GPod* minima_q = nullptr, int or2_lo = 0, int no2 = 0) {
+                                              const GPod* minima_q = nullptr, int or2_lo = 0, int no2 = 0, int kx = K) {
+  // kx <= K: the scalars exchanged across shards (the pod needs only its first kx; the others hold
+  // their operators' identities, which hard_minima then folds into)
   static_assert(K <= G_NS, "too many values");
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
   int32_t r[K];
@@ -803,6 +805,13 @@ __device__ __forceinline__ bool spread_reduce(SpreadHdr& H, int32_t* xs, int W, 
   } else if (lane == 0) {
 #pragma unroll
     for (int k = 0; k < K; k++) H.red[wave][k] = r[k];
+  }
+  if (kx < K && threadIdx.x >= kx && threadIdx.x < K) {
+    int op = OP_SUM;
+#pragma unroll
+    for (int q = 0; q < K; q++)
+      if (q == (int)threadIdx.x) op = ops[q];
+    xs[threadIdx.x] = ident32(op);
   }
   lds_barrier();
   if (sp && threadIdx.x == 0) sp[0] = wall_clock64();
@@ -826,15 +835,16 @@ __device__ __forceinline__ bool spread_reduce(SpreadHdr& H, int32_t* xs, int W, 
     for (int k = 0; k < K; k++) opbits |= (unsigned)ops[k] << (2 * k);
     ++epoch;
     if (sp && threadIdx.x == 0) sp[1] = wall_clock64();
-    const int M = K + ns + no + no2;
+    const int KX = W > 1 && !local ? kx : K;
+    const int M = KX + ns + no + no2;
     if (X.tl_red && M <= TL_M && no2 == 0) {  // two levels (spread_exchange_tl; option spread_two_level = 2), wave 0
-      if (wave == 0 && spread_exchange_tl(H, xs, X, W, epoch, err, K, opbits, sum_lo, ns, or_lo, no) && minima_q)
+      if (wave == 0 && spread_exchange_tl(H, xs, X, W, epoch, err, KX, opbits, sum_lo, ns, or_lo, no) && minima_q)
         hard_minima(*minima_q, xs, xs + G_NS + sum_lo);
       if (sp && threadIdx.x == 0) sp[4] = wall_clock64();
       lds_barrier();
       if (H.abort) return false;
     } else if (nw == 1 || (long long)W * M <= (long long)KSS_SPREAD_MW_MIN) {  // one polling round for one wave: wave 0 alone
-      if (wave == 0 && spread_exchange(H, xs, gran, X, W, w, gs, epoch, err, K, opbits, sum_lo, ns, or_lo, no, sp, 0, 1, 3,
+      if (wave == 0 && spread_exchange(H, xs, gran, X, W, w, gs, epoch, err, KX, opbits, sum_lo, ns, or_lo, no, sp, 0, 1, 3,
                                        0, or2_lo, no2) &&
           minima_q)
         hard_minima(*minima_q, xs, xs + G_NS + sum_lo);
@@ -843,11 +853,11 @@ __device__ __forceinline__ bool spread_reduce(SpreadHdr& H, int32_t* xs, int W, 
       if (H.abort) return false;
     } else {  // many shards: wave 0 publishes, every wave sweeps a share (fewer polling rounds)
       if (wave == 0)
-        spread_exchange(H, xs, gran, X, W, w, gs, epoch, err, K, opbits, sum_lo, ns, or_lo, no, sp, 0, 1, 1, 0, or2_lo, no2);
+        spread_exchange(H, xs, gran, X, W, w, gs, epoch, err, KX, opbits, sum_lo, ns, or_lo, no, sp, 0, 1, 1, 0, or2_lo, no2);
       lds_barrier();  // the slots hold the operators' identities before any wave folds into them
       const int nsw = min(nw, KSS_SPREAD_SWEEP_WAVES);  // the sweeping waves (the rest wait)
       if (wave < nsw)
-        spread_exchange(H, xs, gran, X, W, w, gs, epoch, err, K, opbits, sum_lo, ns, or_lo, no, nullptr, wave, nsw, 2, 0,
+        spread_exchange(H, xs, gran, X, W, w, gs, epoch, err, KX, opbits, sum_lo, ns, or_lo, no, nullptr, wave, nsw, 2, 0,
                         or2_lo, no2);
       lds_barrier();
       if (H.abort) return false;
@@ -857,7 +867,7 @@ __device__ __forceinline__ bool spread_reduce(SpreadHdr& H, int32_t* xs, int W, 
     }
   }
 #pragma unroll
-  for (int k = 0; k < K; k++) v[k] = xs[k];
+  for (int k = 0; k < K; k++) v[k] = xs[k];  // (k >= kx: the identity, or the folded minimum)
   // no barrier here: the next reduction rewrites xs[0..K) (publish resets, or the local
   // path's stores) only behind its own first barrier, which every wave reaches after reading
   if (KSS_SPREAD_SAFE) lds_barrier();  // experiment: a trailing barrier after every exchange
@@ -1780,8 +1790,15 @@ __device__ __forceinline__ void spread_schedule(const GTrace& tr, DevCluster c, 
       v[MAXH] = flags;
       // histogram SUM over every bin, hard-pair presence OR (soft presence, still zero, is
       // filled by the filter pass), then the critical-path minima
+      // at more than 64 shards the scalars cross shards only for node-valued DoNotSchedule groups
+      // (their minimum over nodes) or inter-pod entries (the flags); histogram groups' minima come
+      // from the bins.  C4 (256 shards, zone spread): 8 granules per shard instead of 13, 93.4-94.2k
+      // -> 98.4-98.9k pods/s; C3 (32 shards) keeps all five (67.3k against 68.4k in the same A/B,
+      // profiles/r9l_stats_scalars_ab.txt)
+      bool node_valued = false;
+      for (int i = 0; i < q.n_hard; i++) node_valued |= q.sp[i].off < 0;
       if (!spread_reduce(H, L.xs, W, w, gs, epoch, gran, X, err, v, op, boff, q.total_bins, boff + q.total_bins, q.hard_pbins,
-                         false, nullptr, &q))
+                         false, nullptr, &q, 0, 0, W <= 64 || node_valued || q.n_ipa > 0 ? MAXH + 1 : 0))
         return;
 #pragma unroll
       for (int i = 0; i < MAXH; i++) hard_min[i] = v[i];
